@@ -1,0 +1,186 @@
+/*
+ * trivy_amd C-ABI: the drop-in boundary of the MI355X vulnerability-matching engine.
+ *
+ * This is the surface a cgo shim binds (INTEGRATION.md shows the Go side).  Plain
+ * pointers and sizes only; no Go pointers are retained past a call (cgo rule); every
+ * string/array returned is owned by the library and freed by the matching *_free call.
+ *
+ * Reference surfaces each entry point replaces (fwereade/trivy @ 2025-01-14):
+ *   tvm_db_*                   trivy-db db.Init (pkg/commands/artifact/run.go:311) and the
+ *                              per-call bucket reads behind <os>.VulnSrc.Get /
+ *                              db.Config.GetAdvisories (used at pkg/detector/library/driver.go:114)
+ *   tvm_engine_open/close      (new) device-resident tables, replaces the bbolt mmap
+ *   tvm_engine_swap            server DB hot update (pkg/rpc/server/listen.go:154-190)
+ *   tvm_ospkg_detect           ospkg.Detect            pkg/detector/ospkg/detect.go:63-82
+ *   tvm_ospkg_driver_detect    ospkg.Driver.Detect     pkg/detector/ospkg/detect.go:57-60
+ *   tvm_ospkg_is_supported     ospkg.Driver.IsSupportedVersion  detect.go:59
+ *   tvm_batch_* / tvm_match_*  (new) many-target batching behind concurrent Detect calls
+ *                              (pkg/k8s/scanner/scanner.go:141, pkg/rpc/server/server.go:45)
+ *
+ * Error convention: functions return 0 on success and a non-zero TVM_E* code on failure,
+ * with a NUL-terminated message written to (err, errlen).  Messages carry the same text
+ * the reference's errors do (e.g. "failed to get debian advisories: failed to unmarshal
+ * advisory JSON: ...", wrapped "failed detection: ..." by tvm_ospkg_detect).
+ */
+#ifndef TRIVY_AMD_H
+#define TRIVY_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TVM_ABI_VERSION 1
+
+enum {
+  TVM_OK = 0,
+  TVM_EDETECT = 1,          /* detection failed (message in err) */
+  TVM_EUNSUPPORTED_OS = 2,  /* ospkg.ErrUnsupportedOS (detect.go:30) */
+  TVM_EINVAL = 3,
+  TVM_EDEVICE = 4,          /* HIP / device failure; no CPU fallback exists */
+};
+
+typedef struct tvm_db tvm_db;
+typedef struct tvm_engine tvm_engine;
+typedef struct tvm_batch tvm_batch;
+
+typedef struct {
+  const char* p;
+  size_t n;
+} tvm_str;
+
+/* ftypes.Package fields read by the detectors (pkg/fanal/types/artifact.go:68-105). */
+typedef struct {
+  tvm_str id, name, version, release, arch;
+  int64_t epoch;
+  tvm_str src_name, src_version, src_release;
+  int64_t src_epoch;
+  tvm_str modularitylabel;
+  int32_t has_build_info;           /* BuildInfo != nil */
+  const tvm_str* content_sets;      /* BuildInfo.ContentSets */
+  size_t n_content_sets;
+  tvm_str nvr, build_arch;          /* BuildInfo.Nvr, BuildInfo.Arch */
+  tvm_str file_path;
+} tvm_package;
+
+/* ftypes.Repository (artifact.go:57-60); pass NULL for a nil *Repository. */
+typedef struct {
+  tvm_str family, release;
+} tvm_repository;
+
+/* copy_flags: which fields of input package pkg_index the driver copies verbatim. */
+enum {
+  TVM_COPY_PKG_ID = 1,
+  TVM_COPY_PKG_NAME = 2,
+  TVM_COPY_IDENTIFIER = 4, /* PkgIdentifier */
+  TVM_COPY_LAYER = 8,      /* Layer */
+};
+
+/* types.DetectedVulnerability (pkg/types/vulnerability.go:9-31). Empty string = unset. */
+typedef struct {
+  uint32_t pkg_index;
+  uint32_t copy_flags;
+  const char* vulnerability_id;
+  const char* const* vendor_ids;    /* NULL when nil */
+  size_t n_vendor_ids;
+  const char* pkg_id;
+  const char* pkg_name;
+  const char* pkg_path;
+  const char* installed_version;
+  const char* fixed_version;
+  int32_t status;                   /* dbTypes.Status */
+  const char* severity_source;      /* SeveritySource */
+  const char* severity;             /* Vulnerability.Severity */
+  int32_t has_data_source;          /* DataSource != nil */
+  const char* data_source_id;
+  const char* data_source_name;
+  const char* data_source_url;
+  const char* custom_json;          /* Custom as JSON text; NULL when nil */
+} tvm_vuln;
+
+typedef struct {
+  tvm_vuln* vulns;
+  size_t n;
+  int32_t eosl;                     /* ospkg.Detect's second return value */
+  void* priv;
+} tvm_result;
+
+/* ---- library ------------------------------------------------------------------------ */
+const char* tvm_version(void);
+int tvm_abi_version(void);
+
+/* ---- advisory DB (host side) -------------------------------------------------------- */
+tvm_db* tvm_db_new(void);
+void tvm_db_free(tvm_db* db);
+/* One bbolt record: bucket path (root bucket, nested buckets...) + key -> JSON value.
+ * path has `depth` elements, the last being the key. */
+int tvm_db_put(tvm_db* db, const tvm_str* path, size_t depth, const char* value, size_t vlen);
+/* n records at once: paths is n*depth elements (row-major), values has n elements. */
+int tvm_db_put_many(tvm_db* db, size_t n, const tvm_str* paths, size_t depth, const tvm_str* values);
+/* n records from one byte arena: record r's path items and value are the (depth + 1)
+ * slices off[r*(depth+1) + j], len[...] (j = depth is the value). */
+int tvm_db_put_arena(tvm_db* db, size_t n, size_t depth, const char* arena, const uint64_t* off,
+                     const uint32_t* len);
+/* Decode + flatten into device images. Must be called once, before tvm_engine_open. */
+int tvm_db_finalize(tvm_db* db, char* err, size_t errlen);
+/* Statistics: [0] platforms [1] keys [2] advisories [3] interval rows [4] key-arena bytes */
+void tvm_db_stats(const tvm_db* db, uint64_t out[5]);
+
+/* ---- device engine -------------------------------------------------------------------- */
+/* Uploads the finalized tables to HIP device `device`.  `db` must outlive the engine. */
+tvm_engine* tvm_engine_open(tvm_db* db, int device, char* err, size_t errlen);
+void tvm_engine_close(tvm_engine* e);
+/* Atomically replaces the engine's tables (waits for in-flight calls; server hot update). */
+int tvm_engine_swap(tvm_engine* e, tvm_db* db, char* err, size_t errlen);
+uint64_t tvm_engine_table_bytes(const tvm_engine* e);
+
+/* ---- ospkg ------------------------------------------------------------------------------ */
+/* ospkg.Detect: family = ftypes.OSType ("debian", "ubuntu", ...); now_unix = clock.Now(ctx).
+ * Returns TVM_EUNSUPPORTED_OS for an unknown family. */
+int tvm_ospkg_detect(tvm_engine* e, const char* os_family, const char* os_name, const tvm_repository* repo,
+                     const tvm_package* pkgs, size_t n, int64_t now_unix, tvm_result* out, char* err,
+                     size_t errlen);
+/* Driver.Detect of drivers[os_family] (no gpg-pubkey filter, no EOSL, no wrapping). */
+int tvm_ospkg_driver_detect(tvm_engine* e, const char* os_family, const char* os_ver, const tvm_repository* repo,
+                            const tvm_package* pkgs, size_t n, int64_t now_unix, tvm_result* out, char* err,
+                            size_t errlen);
+/* Driver.IsSupportedVersion: 1 / 0, or -1 for an unsupported family. */
+int tvm_ospkg_is_supported(const char* os_family, const char* os_ver, int64_t now_unix);
+void tvm_result_free(tvm_result* r);
+
+/* ---- many-target batches (device-resident; bench + request coalescing) ---------------- */
+tvm_batch* tvm_batch_new(void);
+void tvm_batch_free(tvm_batch* b);
+/* Adds one package under an explicit root bucket (e.g. "debian 12"), lookup name and the
+ * formatted version the driver compares.  Returns the package's batch index. */
+int64_t tvm_batch_add(tvm_batch* b, tvm_engine* e, const char* bucket, tvm_str name, tvm_str version);
+/* n packages of one bucket from a byte arena; returns the batch index of the first. */
+int64_t tvm_batch_add_many(tvm_batch* b, tvm_engine* e, const char* bucket, size_t n, const char* arena,
+                           const uint64_t* name_off, const uint32_t* name_len, const uint64_t* ver_off,
+                           const uint32_t* ver_len);
+int64_t tvm_batch_size(const tvm_batch* b);
+/* Copies the batch to the device and sizes the match buffer. */
+int tvm_batch_upload(tvm_engine* e, tvm_batch* b, uint64_t match_cap, char* err, size_t errlen);
+/* Enqueues one match pass on the engine stream (async). */
+int tvm_match_launch(tvm_engine* e, tvm_batch* b, char* err, size_t errlen);
+int tvm_engine_sync(tvm_engine* e, char* err, size_t errlen);
+/* After sync: total matches, first poisoned package (-1 none), internal error bits. */
+int tvm_match_status(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* err_pkg, uint64_t* err_bits);
+/* Copies up to cap pairs {pkg_index, advisory_index} (uint32 x2) to host. */
+int tvm_match_fetch(tvm_engine* e, tvm_batch* b, uint32_t* pairs, uint64_t cap, uint64_t* n_out);
+/* Times `steps` back-to-back launches with HIP events on the engine stream (ms total). */
+int tvm_match_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err, size_t errlen);
+/* Algorithmic bytes of one pass (DESIGN.md "roofline"), computed on the host from the batch. */
+uint64_t tvm_match_algorithmic_bytes(tvm_engine* e, tvm_batch* b);
+/* Host-side sort key of a version string (diagnostics/tests): grammar 1 = dpkg.
+ * Returns the key length (<= cap bytes written) or -1 when the version does not parse. */
+int tvm_version_key(int grammar, const char* s, size_t n, uint8_t* out, size_t cap);
+/* Advisory fields for host-side inspection of batch results. */
+const char* tvm_db_advisory_vuln_id(const tvm_db* db, uint32_t adv);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TRIVY_AMD_H */

@@ -1,0 +1,63 @@
+import datetime
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+
+
+def load_case_file(driver):
+    with open(os.path.join(GOLDEN, "cases", driver + ".json"), encoding="utf-8") as f:
+        return json.load(f)
+
+
+def fixture_paths(rel_list):
+    return [os.path.join(GOLDEN, "fixtures", r) for r in rel_list]
+
+
+def parse_now(s):
+    return int(datetime.datetime.strptime(s, "%Y-%m-%dT%H:%M:%SZ").replace(tzinfo=datetime.timezone.utc).timestamp())
+
+
+def _drop_zero(v):
+    """Go zero values are indistinguishable from absent fields in the reference's structs."""
+    return {k: x for k, x in v.items() if x not in ("", 0, None, {}, [])}
+
+
+def canon(vulns):
+    """Canonical multiset order (SURVEY.md §8c parity definition)."""
+    vulns = [_drop_zero(v) for v in vulns]
+    key = lambda v: (v.get("PkgID", ""), v.get("PkgName", ""), v.get("InstalledVersion", ""),
+                     v.get("VulnerabilityID", ""), v.get("FixedVersion", ""), v.get("PkgPath", ""))
+    return sorted(vulns, key=lambda v: (key(v), json.dumps(v, sort_keys=True)))
+
+
+@pytest.fixture(scope="session")
+def oracle_built():
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    return True
+
+
+@pytest.fixture(scope="session")
+def engine_factory():
+    """Builds engines from fixture record files (GPU tests only)."""
+    import trivy_amd
+    cache = {}
+
+    def make(rel_list):
+        key = tuple(rel_list)
+        if key not in cache:
+            db = trivy_amd.load_fixture_files(fixture_paths(rel_list))
+            cache[key] = trivy_amd.Engine(db, 0)
+        return cache[key]
+
+    return make

@@ -1,0 +1,185 @@
+"""Seeded synthetic trivy-db + package batches (bench and large parity tests).
+
+The pinned trivy-db (ghcr.io/aquasecurity/trivy-db:2) cannot be fetched offline
+(SURVEY.md §7 hard part 6), so throughput is measured on a generated DB with the
+distributions of SURVEY.md §8d, and parity at scale is checked against the oracle
+on the same generated data.
+
+Everything is emitted pre-sorted in bbolt byte order (platform buckets, package
+buckets, vulnerability IDs), so the engine's global advisory index equals the CSR
+index here - tests can compare (package, advisory) pairs directly.
+"""
+import numpy as np
+
+SEED_DB = 0x7157DB
+
+DEBIAN_DS = b'{"ID":"debian","Name":"Debian Security Tracker","URL":"https://salsa.debian.org/security-tracker-team/security-tracker"}'
+UBUNTU_DS = b'{"ID":"ubuntu","Name":"Ubuntu CVE Tracker","URL":"https://git.launchpad.net/ubuntu-cve-tracker"}'
+AMAZON_DS = b'{"ID":"amazon","Name":"Amazon Linux Security Center","URL":"https://alas.aws.amazon.com/"}'
+
+_SYL = [b"lib", b"py", b"gnu", b"x", b"ssl", b"core", b"util", b"net", b"font", b"perl", b"gtk", b"qt", b"db",
+        b"cups", b"krb", b"sql", b"z", b"bz", b"xml", b"curl", b"dev", b"data", b"doc", b"common", b"bin"]
+
+
+def _counts(rng, n, mean, cap):
+    """Heavy-tailed advisories-per-key with the requested mean (Pareto tail, >= 1)."""
+    c = 1 + np.floor(rng.pareto(1.6, n) * (mean - 1) * 0.6)
+    c = np.minimum(c, cap).astype(np.int64)
+    c = np.maximum(c, 1)
+    return c
+
+
+class SynthDB:
+    """platforms: list of root bucket names (sorted).  CSR: key -> advisories."""
+
+    def __init__(self, platforms, key_plat, key_names, adv_begin, adv_vid, adv_fixed, key_base):
+        self.platforms = platforms
+        self.key_plat = key_plat
+        self.key_names = key_names
+        self.adv_begin = adv_begin
+        self.adv_vid = adv_vid
+        self.adv_fixed = adv_fixed
+        self.key_base = key_base
+        self.plat_keys = [np.nonzero(key_plat == p)[0] for p in range(len(platforms))]
+
+    @property
+    def n_adv(self):
+        return int(self.adv_begin[-1])
+
+    def records_arena(self, poison_keys=()):
+        """(n, depth=3, arena, off, len) for tvm_db_put_arena, plus data-source records."""
+        items = []
+        poison = set(int(k) for k in poison_keys)
+        for k in range(len(self.key_names)):
+            root = self.platforms[self.key_plat[k]].encode()
+            name = self.key_names[k]
+            for a in range(self.adv_begin[k], self.adv_begin[k + 1]):
+                val = b'{"FixedVersion":"' + self.adv_fixed[a] + b'"}'
+                if k in poison and a == self.adv_begin[k]:
+                    val = b'{"FixedVersion":["bad"]}'
+                items += [root, name, self.adv_vid[a], val]
+        return _arena(items, 3)
+
+    def source_arena(self):
+        items = []
+        for p in self.platforms:
+            ds = DEBIAN_DS if p.startswith("debian") else UBUNTU_DS if p.startswith("ubuntu") else AMAZON_DS
+            items += [b"data-source", p.encode(), ds]
+        return _arena(items, 2)
+
+
+def _arena(items, depth):
+    lens = np.fromiter((len(x) for x in items), dtype=np.uint32, count=len(items))
+    off = np.zeros(len(items), dtype=np.uint64)
+    if len(items):
+        off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    return len(items) // (depth + 1), depth, b"".join(items), off, lens
+
+
+def _deb_version(epoch, major, minor, patch, rev, ubuntu, tilde, dfsg):
+    v = b"%d.%d.%d" % (major, minor, patch)
+    if tilde:
+        v += b"~rc%d" % tilde
+    if dfsg:
+        v += b"+dfsg"
+    v += (b"-%dubuntu0.%d" % (rev, rev % 7)) if ubuntu else (b"-%d+deb12u%d" % (rev, rev % 5) if rev % 3 == 0 else b"-%d" % rev)
+    if epoch:
+        v = b"%d:" % epoch + v
+    return v
+
+
+def make_db(platforms, keys_per_plat, seed=SEED_DB, mean_adv=12, max_adv=5000, unfixed=0.15):
+    """dpkg-family DB (debian/ubuntu/amazon buckets)."""
+    rng = np.random.default_rng(seed)
+    platforms = sorted(platforms)
+    key_plat, key_names, counts, bases = [], [], [], []
+    for p, root in enumerate(platforms):
+        n = keys_per_plat
+        syl = rng.integers(0, len(_SYL), size=(n, 2))
+        names = sorted({_SYL[a] + _SYL[b] + b"%d" % i for i, (a, b) in enumerate(syl)} | {b"linux"})
+        c = _counts(rng, len(names), mean_adv, max_adv)
+        c[names.index(b"linux")] = max_adv  # the heavy key of every real distro
+        key_plat += [p] * len(names)
+        key_names += names
+        counts.append(c)
+        for _ in names:
+            bases.append((int(rng.random() < 0.05) * int(rng.integers(1, 4)), int(rng.integers(0, 20)),
+                          int(rng.integers(0, 30)), int(rng.random() < 0.1), root.startswith("ubuntu")))
+    counts = np.concatenate(counts)
+    adv_begin = np.zeros(len(key_names) + 1, dtype=np.int64)
+    adv_begin[1:] = np.cumsum(counts)
+    n_adv = int(adv_begin[-1])
+    patch = rng.integers(0, 40, n_adv)
+    rev = rng.integers(1, 9, n_adv)
+    tilde = (rng.random(n_adv) < 0.03) * rng.integers(1, 4, n_adv)
+    is_unfixed = rng.random(n_adv) < unfixed
+    adv_vid, adv_fixed = [], []
+    for k in range(len(key_names)):
+        b, e = int(adv_begin[k]), int(adv_begin[k + 1])
+        ep, ma, mi, dfsg, ubu = bases[k]
+        ids = sorted(b"CVE-%d-%d" % (2000 + (j * 7919 + k) % 25, 1000 + j) for j in range(e - b))
+        adv_vid += ids
+        for a in range(b, e):
+            adv_fixed.append(b"" if is_unfixed[a] else
+                             _deb_version(ep, ma, mi, int(patch[a]), int(rev[a]), ubu, int(tilde[a]), dfsg))
+    return SynthDB(platforms, np.array(key_plat, dtype=np.int32), key_names, adv_begin, adv_vid, adv_fixed, bases)
+
+
+class SynthBatch:
+    def __init__(self, plat, names, versions, target_bounds):
+        self.plat = plat            # np.int32 per package (-1 absent bucket)
+        self.names = names          # list[bytes]
+        self.versions = versions    # list[bytes]
+        self.targets = target_bounds  # [(plat, begin, end)] one entry per SBOM/target
+
+    def __len__(self):
+        return len(self.names)
+
+    def arena(self):
+        """arena bytes + name/version offsets and lengths (interleaved name, version)."""
+        items = [x for pair in zip(self.names, self.versions) for x in pair]
+        lens = np.fromiter((len(x) for x in items), dtype=np.uint32, count=len(items))
+        off = np.zeros(len(items), dtype=np.uint64)
+        if len(items):
+            off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        return b"".join(items), off[0::2].copy(), lens[0::2].copy(), off[1::2].copy(), lens[1::2].copy()
+
+
+def make_batch(db, n_targets, pkgs_per_target, plat_weights, seed, miss=0.25, zipf=2.5, invalid=0.002,
+               long_versions=0.0):
+    """SBOM-like batch: each target draws one platform, then packages over its keys."""
+    rng = np.random.default_rng(seed)
+    w = np.asarray(plat_weights, dtype=np.float64)
+    w = w / w.sum()
+    t_plat = rng.choice(len(db.platforms), size=n_targets, p=w)
+    plat, names, versions, targets = [], [], [], []
+    for t in range(n_targets):
+        p = int(t_plat[t])
+        keys = db.plat_keys[p]
+        n = pkgs_per_target
+        # popularity skew without a single dominant key: P(rank < r) = (r / K) ** (1 / zipf)
+        rank = np.minimum((len(keys) * rng.random(n) ** zipf).astype(np.int64), len(keys) - 1)
+        perm_seed = (p * 1000003) % len(keys)
+        kidx = keys[(rank * 7919 + perm_seed) % len(keys)]
+        missing = rng.random(n) < miss
+        patch = rng.integers(0, 40, n)
+        rev = rng.integers(1, 9, n)
+        bad = rng.random(n) < invalid
+        longv = rng.random(n) < long_versions
+        b0 = len(names)
+        for i in range(n):
+            k = int(kidx[i])
+            ep, ma, mi, dfsg, ubu = db.key_base[k]
+            if missing[i]:
+                names.append(b"absent-%d-%d" % (t, i))
+            else:
+                names.append(db.key_names[k])
+            v = _deb_version(ep, ma, mi, int(patch[i]), int(rev[i]), ubu, 0, dfsg)
+            if bad[i]:
+                v = b"x" + v  # upstream must start with a digit: parse error
+            if longv[i]:
+                v = v + b"+" + b".".join(b"%d" % j for j in range(30))
+            versions.append(v)
+        plat += [p] * n
+        targets.append((p, b0, len(names)))
+    return SynthBatch(np.array(plat, dtype=np.int32), names, versions, targets)

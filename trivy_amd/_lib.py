@@ -1,0 +1,135 @@
+"""ctypes binding of the trivy_amd C-ABI (include/trivy_amd.h).
+
+The native library is the product: there is no Python or CPU fallback for any
+matching step.  Loading fails loudly when libtrivy_amd.so has not been built.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtrivy_amd.so")
+
+TVM_OK, TVM_EDETECT, TVM_EUNSUPPORTED_OS, TVM_EINVAL, TVM_EDEVICE = 0, 1, 2, 3, 4
+COPY_PKG_ID, COPY_PKG_NAME, COPY_IDENTIFIER, COPY_LAYER = 1, 2, 4, 8
+
+
+class Str(ctypes.Structure):
+    _fields_ = [("p", ctypes.c_char_p), ("n", ctypes.c_size_t)]
+
+
+class Package(ctypes.Structure):
+    _fields_ = [
+        ("id", Str), ("name", Str), ("version", Str), ("release", Str), ("arch", Str),
+        ("epoch", ctypes.c_int64),
+        ("src_name", Str), ("src_version", Str), ("src_release", Str),
+        ("src_epoch", ctypes.c_int64),
+        ("modularitylabel", Str),
+        ("has_build_info", ctypes.c_int32),
+        ("content_sets", ctypes.POINTER(Str)), ("n_content_sets", ctypes.c_size_t),
+        ("nvr", Str), ("build_arch", Str),
+        ("file_path", Str),
+    ]
+
+
+class Repository(ctypes.Structure):
+    _fields_ = [("family", Str), ("release", Str)]
+
+
+class Vuln(ctypes.Structure):
+    _fields_ = [
+        ("pkg_index", ctypes.c_uint32), ("copy_flags", ctypes.c_uint32),
+        ("vulnerability_id", ctypes.c_char_p),
+        ("vendor_ids", ctypes.POINTER(ctypes.c_char_p)), ("n_vendor_ids", ctypes.c_size_t),
+        ("pkg_id", ctypes.c_char_p), ("pkg_name", ctypes.c_char_p), ("pkg_path", ctypes.c_char_p),
+        ("installed_version", ctypes.c_char_p), ("fixed_version", ctypes.c_char_p),
+        ("status", ctypes.c_int32),
+        ("severity_source", ctypes.c_char_p), ("severity", ctypes.c_char_p),
+        ("has_data_source", ctypes.c_int32),
+        ("data_source_id", ctypes.c_char_p), ("data_source_name", ctypes.c_char_p),
+        ("data_source_url", ctypes.c_char_p),
+        ("custom_json", ctypes.c_char_p),
+    ]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("vulns", ctypes.POINTER(Vuln)), ("n", ctypes.c_size_t), ("eosl", ctypes.c_int32),
+                ("priv", ctypes.c_void_p)]
+
+
+# (name, restype, argtypes) for every exported symbol of include/trivy_amd.h
+_P = ctypes.c_void_p
+_SIG = [
+    ("tvm_version", ctypes.c_char_p, []),
+    ("tvm_abi_version", ctypes.c_int, []),
+    ("tvm_db_new", _P, []),
+    ("tvm_db_free", None, [_P]),
+    ("tvm_db_put", ctypes.c_int, [_P, ctypes.POINTER(Str), ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_db_put_many", ctypes.c_int, [_P, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    ("tvm_db_put_arena", ctypes.c_int, [_P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p]),
+    ("tvm_db_finalize", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_db_stats", None, [_P, ctypes.POINTER(ctypes.c_uint64)]),
+    ("tvm_engine_open", _P, [_P, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_engine_close", None, [_P]),
+    ("tvm_engine_swap", ctypes.c_int, [_P, _P, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_engine_table_bytes", ctypes.c_uint64, [_P]),
+    ("tvm_ospkg_detect", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(Repository),
+                                        ctypes.POINTER(Package), ctypes.c_size_t, ctypes.c_int64,
+                                        ctypes.POINTER(Result), ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_ospkg_driver_detect", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(Repository),
+                                               ctypes.POINTER(Package), ctypes.c_size_t, ctypes.c_int64,
+                                               ctypes.POINTER(Result), ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_ospkg_is_supported", ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int64]),
+    ("tvm_result_free", None, [ctypes.POINTER(Result)]),
+    ("tvm_batch_new", _P, []),
+    ("tvm_batch_free", None, [_P]),
+    ("tvm_batch_add", ctypes.c_int64, [_P, _P, ctypes.c_char_p, Str, Str]),
+    ("tvm_batch_add_many", ctypes.c_int64, [_P, _P, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("tvm_batch_size", ctypes.c_int64, [_P]),
+    ("tvm_batch_upload", ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_match_launch", ctypes.c_int, [_P, _P, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_engine_sync", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_match_status", ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64),
+                                        ctypes.POINTER(ctypes.c_uint64)]),
+    ("tvm_match_fetch", ctypes.c_int, [_P, _P, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
+    ("tvm_match_time", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_char_p,
+                                      ctypes.c_size_t]),
+    ("tvm_match_algorithmic_bytes", ctypes.c_uint64, [_P, _P]),
+    ("tvm_version_key", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p,
+                                       ctypes.c_size_t]),
+    ("tvm_db_advisory_vuln_id", ctypes.c_char_p, [_P, ctypes.c_uint32]),
+]
+
+EXPORTED = [s[0] for s in _SIG]
+
+_lib = None
+
+
+def lib():
+    """The loaded native library (raises if it is missing: no fallback exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"trivy_amd native library not built: {LIB_PATH} (run __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in _SIG:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def s(x):
+    """Python str/bytes -> tvm_str (keeps the bytes object alive on the struct)."""
+    if x is None:
+        return Str(None, 0)
+    b = x.encode() if isinstance(x, str) else bytes(x)
+    st = Str(b, len(b))
+    st._keep = b
+    return st
+
+
+def errbuf():
+    return ctypes.create_string_buffer(4096)

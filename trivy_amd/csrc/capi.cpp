@@ -1,0 +1,452 @@
+// C-ABI implementation (include/trivy_amd.h).
+#include "../../include/trivy_amd.h"
+
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <vector>
+
+#include "db.h"
+#include "drivers.h"
+#include "engine.h"
+#include "verkey.h"
+
+using namespace tvm;
+
+struct tvm_db {
+  DB db;
+  bool finalized = false;
+};
+
+struct tvm_engine {
+  std::shared_mutex mu;  // calls share; swap is exclusive (listen.go:154-190 quiesce)
+  std::unique_ptr<Engine> eng;
+  tvm_db* db = nullptr;
+  int device = 0;
+};
+
+struct tvm_batch {
+  HostBatch hb;
+  DevBatch dev;
+  DevMatches m;
+  bool uploaded = false;
+  int device = 0;
+};
+
+namespace {
+
+void set_err(char* err, size_t errlen, const std::string& msg) {
+  if (!err || errlen == 0) return;
+  size_t n = std::min(errlen - 1, msg.size());
+  memcpy(err, msg.data(), n);
+  err[n] = 0;
+}
+
+std::string_view sv(const tvm_str& s) { return s.p ? std::string_view(s.p, s.n) : std::string_view(); }
+
+std::vector<Pkg> to_pkgs(const tvm_package* pkgs, size_t n) {
+  std::vector<Pkg> out(n);
+  for (size_t i = 0; i < n; i++) {
+    const tvm_package& p = pkgs[i];
+    Pkg& q = out[i];
+    q.id = sv(p.id);
+    q.name = sv(p.name);
+    q.version = sv(p.version);
+    q.release = sv(p.release);
+    q.arch = sv(p.arch);
+    q.epoch = p.epoch;
+    q.src_name = sv(p.src_name);
+    q.src_version = sv(p.src_version);
+    q.src_release = sv(p.src_release);
+    q.src_epoch = p.src_epoch;
+    q.modularitylabel = sv(p.modularitylabel);
+    q.has_build_info = p.has_build_info != 0;
+    for (size_t k = 0; k < p.n_content_sets; k++) q.content_sets.push_back(sv(p.content_sets[k]));
+    q.nvr = sv(p.nvr);
+    q.build_arch = sv(p.build_arch);
+    q.file_path = sv(p.file_path);
+  }
+  return out;
+}
+
+struct ResultStore {
+  std::vector<Vuln> v;
+  std::vector<tvm_vuln> c;
+  std::vector<std::vector<const char*>> vendor_ptrs;
+};
+
+void export_result(const DB& db, std::vector<Vuln>&& vulns, bool eosl, tvm_result* out) {
+  auto* rs = new ResultStore();
+  rs->v = std::move(vulns);
+  rs->c.resize(rs->v.size());
+  rs->vendor_ptrs.resize(rs->v.size());
+  for (size_t i = 0; i < rs->v.size(); i++) {
+    const Vuln& v = rs->v[i];
+    tvm_vuln& c = rs->c[i];
+    memset(&c, 0, sizeof(c));
+    c.pkg_index = v.pkg;
+    c.copy_flags = v.copy;
+    c.vulnerability_id = v.vuln_id.c_str();
+    if (!v.vendor_ids.empty()) {
+      for (const std::string& s : v.vendor_ids) rs->vendor_ptrs[i].push_back(s.c_str());
+      c.vendor_ids = rs->vendor_ptrs[i].data();
+      c.n_vendor_ids = v.vendor_ids.size();
+    }
+    c.pkg_id = v.pkg_id.c_str();
+    c.pkg_name = v.pkg_name.c_str();
+    c.pkg_path = v.pkg_path.c_str();
+    c.installed_version = v.installed.c_str();
+    c.fixed_version = v.fixed.c_str();
+    c.status = v.status;
+    c.severity_source = v.severity_source.c_str();
+    c.severity = v.severity.c_str();
+    if (v.data_source >= 0) {
+      const DataSource& ds = db.sources[size_t(v.data_source)];
+      c.has_data_source = 1;
+      c.data_source_id = ds.id.c_str();
+      c.data_source_name = ds.name.c_str();
+      c.data_source_url = ds.url.c_str();
+    } else {
+      c.data_source_id = c.data_source_name = c.data_source_url = "";
+    }
+    c.custom_json = v.has_custom ? v.custom.c_str() : nullptr;
+  }
+  out->vulns = rs->c.data();
+  out->n = rs->c.size();
+  out->eosl = eosl ? 1 : 0;
+  out->priv = rs;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* tvm_version(void) { return "trivy_amd 0.1.0 (gfx950)"; }
+int tvm_abi_version(void) { return TVM_ABI_VERSION; }
+
+tvm_db* tvm_db_new(void) { return new tvm_db(); }
+void tvm_db_free(tvm_db* db) { delete db; }
+
+int tvm_db_put(tvm_db* db, const tvm_str* path, size_t depth, const char* value, size_t vlen) {
+  if (!db || db->finalized || !path || depth == 0) return TVM_EINVAL;
+  std::vector<std::string> p(depth);
+  for (size_t i = 0; i < depth; i++) p[i] = std::string(sv(path[i]));
+  db->db.put(p, std::string_view(value ? value : "", value ? vlen : 0));
+  return TVM_OK;
+}
+
+int tvm_db_put_many(tvm_db* db, size_t n, const tvm_str* paths, size_t depth, const tvm_str* values) {
+  if (!db || db->finalized || (n && (!paths || !values)) || depth == 0) return TVM_EINVAL;
+  std::vector<std::string> p(depth);
+  for (size_t r = 0; r < n; r++) {
+    for (size_t i = 0; i < depth; i++) p[i] = std::string(sv(paths[r * depth + i]));
+    db->db.put(p, sv(values[r]));
+  }
+  return TVM_OK;
+}
+
+int tvm_db_put_arena(tvm_db* db, size_t n, size_t depth, const char* arena, const uint64_t* off,
+                     const uint32_t* len) {
+  if (!db || db->finalized || depth == 0 || (n && (!arena || !off || !len))) return TVM_EINVAL;
+  std::vector<std::string> p(depth);
+  for (size_t r = 0; r < n; r++) {
+    const size_t b = r * (depth + 1);
+    for (size_t i = 0; i < depth; i++) p[i].assign(arena + off[b + i], len[b + i]);
+    db->db.put(p, std::string_view(arena + off[b + depth], len[b + depth]));
+  }
+  return TVM_OK;
+}
+
+int tvm_db_finalize(tvm_db* db, char* err, size_t errlen) {
+  if (!db || db->finalized) return TVM_EINVAL;
+  std::string e;
+  if (!db->db.finalize(e)) {
+    set_err(err, errlen, e);
+    return TVM_EINVAL;
+  }
+  db->finalized = true;
+  return TVM_OK;
+}
+
+void tvm_db_stats(const tvm_db* db, uint64_t out[5]) {
+  out[0] = db->db.plats.size();
+  out[1] = db->db.keys.size();
+  out[2] = db->db.advs.size();
+  out[3] = db->db.rows.size();
+  out[4] = db->db.key_words.size() * 8;
+}
+
+const char* tvm_db_advisory_vuln_id(const tvm_db* db, uint32_t adv) {
+  return adv < db->db.advs.size() ? db->db.advs[adv].vuln_id.c_str() : nullptr;
+}
+
+tvm_engine* tvm_engine_open(tvm_db* db, int device, char* err, size_t errlen) {
+  if (!db || !db->finalized) {
+    set_err(err, errlen, "tvm_engine_open: DB not finalized");
+    return nullptr;
+  }
+  std::string e;
+  Engine* eng = Engine::open(db->db, device, e);
+  if (!eng) {
+    set_err(err, errlen, e);
+    return nullptr;
+  }
+  auto* t = new tvm_engine();
+  t->eng.reset(eng);
+  t->db = db;
+  t->device = device;
+  return t;
+}
+
+void tvm_engine_close(tvm_engine* e) { delete e; }
+
+int tvm_engine_swap(tvm_engine* e, tvm_db* db, char* err, size_t errlen) {
+  if (!e || !db || !db->finalized) return TVM_EINVAL;
+  std::string msg;
+  Engine* fresh = Engine::open(db->db, e->device, msg);  // build before quiescing
+  if (!fresh) {
+    set_err(err, errlen, msg);
+    return TVM_EDEVICE;
+  }
+  std::unique_lock<std::shared_mutex> lk(e->mu);
+  e->eng.reset(fresh);
+  e->db = db;
+  return TVM_OK;
+}
+
+uint64_t tvm_engine_table_bytes(const tvm_engine* e) { return e ? e->eng->table_bytes() : 0; }
+
+static int detect_common(tvm_engine* e, bool full, const char* fam, const char* ver, const tvm_repository* repo,
+                         const tvm_package* pkgs, size_t n, int64_t now, tvm_result* out, char* err,
+                         size_t errlen) {
+  if (!e || !fam || !ver || !out || (n && !pkgs)) return TVM_EINVAL;
+  memset(out, 0, sizeof(*out));
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  std::vector<Pkg> p = to_pkgs(pkgs, n);
+  Repo r;
+  if (repo) {
+    r.family = sv(repo->family);
+    r.release = sv(repo->release);
+  }
+  std::vector<Vuln> vulns;
+  std::string msg;
+  bool eosl = false;
+  if (full) {
+    DetectStatus st = ospkg_detect(*e->eng, fam, ver, repo ? &r : nullptr, p, now, vulns, eosl, msg);
+    if (st != DETECT_OK) {
+      set_err(err, errlen, msg);
+      return st == DETECT_UNSUPPORTED_OS ? TVM_EUNSUPPORTED_OS : TVM_EDETECT;
+    }
+  } else {
+    const OsDriver* d = find_os_driver(fam);
+    if (!d) {
+      set_err(err, errlen, "unsupported os");
+      return TVM_EUNSUPPORTED_OS;
+    }
+    if (!d->detect(*e->eng, ver, repo ? &r : nullptr, p, now, vulns, msg)) {
+      set_err(err, errlen, msg);
+      return TVM_EDETECT;
+    }
+  }
+  export_result(e->eng->db(), std::move(vulns), eosl, out);
+  return TVM_OK;
+}
+
+int tvm_ospkg_detect(tvm_engine* e, const char* f, const char* v, const tvm_repository* repo, const tvm_package* pkgs,
+                     size_t n, int64_t now, tvm_result* out, char* err, size_t errlen) {
+  return detect_common(e, true, f, v, repo, pkgs, n, now, out, err, errlen);
+}
+
+int tvm_ospkg_driver_detect(tvm_engine* e, const char* f, const char* v, const tvm_repository* repo,
+                            const tvm_package* pkgs, size_t n, int64_t now, tvm_result* out, char* err,
+                            size_t errlen) {
+  return detect_common(e, false, f, v, repo, pkgs, n, now, out, err, errlen);
+}
+
+int tvm_ospkg_is_supported(const char* fam, const char* ver, int64_t now) {
+  const OsDriver* d = fam ? find_os_driver(fam) : nullptr;
+  if (!d || !ver) return -1;
+  return d->is_supported(fam, ver, now) ? 1 : 0;
+}
+
+void tvm_result_free(tvm_result* r) {
+  if (!r) return;
+  delete static_cast<ResultStore*>(r->priv);
+  memset(r, 0, sizeof(*r));
+}
+
+// ---- batches ------------------------------------------------------------------------------
+
+tvm_batch* tvm_batch_new(void) { return new tvm_batch(); }
+
+void tvm_batch_free(tvm_batch* b) {
+  if (!b) return;
+  if (b->uploaded) {
+    hipSetDevice(b->device);
+    hipFree(b->dev.desc);
+    hipFree(b->dev.arena);
+    hipFree(b->m.pairs);
+    hipFree(b->m.ctl);
+  }
+  delete b;
+}
+
+int64_t tvm_batch_add(tvm_batch* b, tvm_engine* e, const char* bucket, tvm_str name, tvm_str version) {
+  if (!b || !e || !bucket || b->uploaded) return -1;
+  int32_t plat = e->eng->db().find_plat(bucket);
+  b->hb.add(plat < 0 ? 0xFFFFFFFFu : uint32_t(plat), sv(name), sv(version));
+  return int64_t(b->hb.desc.size() - 1);
+}
+
+int64_t tvm_batch_add_many(tvm_batch* b, tvm_engine* e, const char* bucket, size_t n, const char* arena,
+                           const uint64_t* name_off, const uint32_t* name_len, const uint64_t* ver_off,
+                           const uint32_t* ver_len) {
+  if (!b || !e || !bucket || b->uploaded || (n && (!arena || !name_off || !name_len || !ver_off || !ver_len)))
+    return -1;
+  int32_t plat = e->eng->db().find_plat(bucket);
+  const uint32_t pid = plat < 0 ? 0xFFFFFFFFu : uint32_t(plat);
+  const int64_t first = int64_t(b->hb.desc.size());
+  b->hb.desc.reserve(b->hb.desc.size() + n);
+  for (size_t i = 0; i < n; i++)
+    b->hb.add(pid, std::string_view(arena + name_off[i], name_len[i]), std::string_view(arena + ver_off[i], ver_len[i]));
+  return first;
+}
+
+int64_t tvm_batch_size(const tvm_batch* b) { return b ? int64_t(b->hb.desc.size()) : 0; }
+
+int tvm_batch_upload(tvm_engine* e, tvm_batch* b, uint64_t cap, char* err, size_t errlen) {
+  if (!e || !b) return TVM_EINVAL;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  std::string msg;
+  if (b->uploaded) {
+    e->eng->free_batch(b->dev);
+    e->eng->free_matches(b->m);
+    b->uploaded = false;
+  }
+  if (!e->eng->upload(b->hb, b->dev, msg) || !e->eng->alloc_matches(cap, b->m, msg)) {
+    set_err(err, errlen, msg);
+    return TVM_EDEVICE;
+  }
+  b->uploaded = true;
+  b->device = e->device;
+  return TVM_OK;
+}
+
+int tvm_match_launch(tvm_engine* e, tvm_batch* b, char* err, size_t errlen) {
+  if (!e || !b || !b->uploaded) return TVM_EINVAL;
+  std::string msg;
+  if (!e->eng->launch(b->dev, b->m, e->eng->stream(), msg)) {
+    set_err(err, errlen, msg);
+    return TVM_EDEVICE;
+  }
+  return TVM_OK;
+}
+
+int tvm_engine_sync(tvm_engine* e, char* err, size_t errlen) {
+  if (!e) return TVM_EINVAL;
+  hipError_t st = hipStreamSynchronize(e->eng->stream());
+  if (st != hipSuccess) {
+    set_err(err, errlen, std::string("hipStreamSynchronize: ") + hipGetErrorString(st));
+    return TVM_EDEVICE;
+  }
+  return TVM_OK;
+}
+
+int tvm_match_status(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* err_pkg, uint64_t* err_bits) {
+  if (!e || !b || !b->uploaded) return TVM_EINVAL;
+  unsigned long long ctl[8];
+  hipSetDevice(e->device);
+  if (hipMemcpy(ctl, b->m.ctl, sizeof(ctl), hipMemcpyDeviceToHost) != hipSuccess) return TVM_EDEVICE;
+  if (n_matches) *n_matches = ctl[0];
+  if (err_pkg) *err_pkg = ctl[1] ? int64_t(b->dev.n - ctl[1]) : -1;
+  if (err_bits) *err_bits = ctl[3];
+  return TVM_OK;
+}
+
+int tvm_match_fetch(tvm_engine* e, tvm_batch* b, uint32_t* pairs, uint64_t cap, uint64_t* n_out) {
+  uint64_t n = 0;
+  int rc = tvm_match_status(e, b, &n, nullptr, nullptr);
+  if (rc) return rc;
+  n = std::min<uint64_t>(std::min<uint64_t>(n, cap), b->m.cap);
+  if (n && hipMemcpy(pairs, b->m.pairs, n * sizeof(uint2), hipMemcpyDeviceToHost) != hipSuccess) return TVM_EDEVICE;
+  if (n_out) *n_out = n;
+  return TVM_OK;
+}
+
+int tvm_match_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err, size_t errlen) {
+  if (!e || !b || !b->uploaded || steps <= 0) return TVM_EINVAL;
+  hipSetDevice(e->device);
+  hipEvent_t t0, t1;
+  hipEventCreate(&t0);
+  hipEventCreate(&t1);
+  hipStream_t st = e->eng->stream();
+  hipEventRecord(t0, st);
+  std::string msg;
+  for (int i = 0; i < steps; i++) {
+    if (!e->eng->launch(b->dev, b->m, st, msg)) {
+      set_err(err, errlen, msg);
+      return TVM_EDEVICE;
+    }
+  }
+  hipEventRecord(t1, st);
+  hipEventSynchronize(t1);
+  float f = 0;
+  hipEventElapsedTime(&f, t0, t1);
+  hipEventDestroy(t0);
+  hipEventDestroy(t1);
+  *ms = f;
+  return TVM_OK;
+}
+
+uint64_t tvm_match_algorithmic_bytes(tvm_engine* e, tvm_batch* b) {
+  // DESIGN.md "Roofline": per package 16 B descriptor + name + version bytes, per probed
+  // package 8 B slot hash + 16 B slot value + name verify, per (package, row) 16 B row +
+  // bound-key bytes, per match 8 B output.  Computed exactly from the batch + tables.
+  if (!e || !b) return 0;
+  const DB& db = e->eng->db();
+  uint64_t bytes = 0;
+  for (const uint4& d : b->hb.desc) {
+    uint32_t nlen = d.w & 0xFFFF, vlen = d.w >> 16;
+    bytes += 16 + nlen + vlen;
+    if (d.x >= db.plats.size()) continue;
+    bytes += 24;
+    std::string_view name(reinterpret_cast<const char*>(b->hb.arena.data()) + d.y, nlen);
+    int32_t k = db.find_key(d.x, name);
+    if (k < 0) continue;
+    bytes += nlen;
+    const std::string ks = db.keys[size_t(k)].name;
+    uint64_t h = key_hash(d.x, reinterpret_cast<const uint8_t*>(ks.data()), uint32_t(ks.size()));
+    for (uint64_t i = h & db.slot_mask; db.slot_hash[i]; i = (i + 1) & db.slot_mask) {
+      if (db.slot_key[i] != uint32_t(k)) continue;
+      const SlotVal& v = db.slot_val[i];
+      for (uint32_t r = 0; r < v.row_count; r++) {
+        const Row& row = db.rows[v.row_begin + r];
+        bytes += 16;
+        if (!(row.hi_len & KEY_INF)) bytes += row.hi_len & KEY_LEN_MASK;
+        if (!(row.lo_len & KEY_INF)) bytes += row.lo_len & KEY_LEN_MASK;
+      }
+      break;
+    }
+  }
+  uint64_t m = 0;
+  if (b->uploaded) tvm_match_status(e, b, &m, nullptr, nullptr);
+  return bytes + 8 * m;
+}
+
+int tvm_version_key(int grammar, const char* s, size_t n, uint8_t* out, size_t cap) {
+  struct Sink {
+    uint8_t* o;
+    size_t cap, n = 0;
+    void put(uint8_t b) {
+      if (n < cap) o[n] = b;
+      n++;
+    }
+  } sink{out, cap};
+  if (grammar <= 0 || grammar > 255 || !s) return -1;
+  if (!encode_version(uint8_t(grammar), reinterpret_cast<const uint8_t*>(s), uint32_t(n), sink)) return -1;
+  return int(sink.n);
+}
+
+}  // extern "C"

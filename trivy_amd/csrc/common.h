@@ -1,0 +1,112 @@
+// Shared host/device definitions for the trivy_amd matching engine.
+//
+// Everything here is compiled twice by hipcc: once for the host flattener
+// (advisory side, at DB load time) and once for gfx950 (installed-package side,
+// inside the kernels), so both sides agree bit for bit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TVM_HD __host__ __device__ __forceinline__
+
+namespace tvm {
+
+// Version grammar of a platform (which third-party comparator the reference uses).
+enum Cmp : uint8_t {
+  CMP_NONE = 0,
+  CMP_DEB = 1,   // knqyf263/go-deb-version (debian, ubuntu, amazon)
+};
+
+// Driver families (reference pkg/detector/ospkg/detect.go:32-48 and library/driver.go:25-93).
+enum Drv : uint8_t {
+  DRV_NONE = 0,
+  DRV_DEBIAN = 1,
+  DRV_UBUNTU = 2,
+  DRV_AMAZON = 3,
+};
+
+// Per-platform flags (device-visible).
+enum : uint32_t {
+  PLAT_LOOKUP_FIRST = 1u << 0,  // DB lookup (and its decode error) precedes the installed parse
+};
+
+// One interval row: the advisory matches installed version v iff
+//   ALWAYS, or v parsed and lo <=/< v and v </<= hi.
+// Keys live in the key arena (8-byte aligned, little-endian words holding the
+// sort-key bytes in memory order).  lo/hi lengths carry flags in their top bits.
+struct alignas(16) Row {
+  uint32_t lo_off;   // word offset into key arena
+  uint32_t hi_off;
+  uint32_t adv;      // global advisory index (host-side record)
+  uint16_t lo_len;   // bytes | flags
+  uint16_t hi_len;
+};
+enum : uint16_t {
+  KEY_LEN_MASK = 0x3FFF,
+  KEY_INF = 0x8000,      // lo = -inf / hi = +inf
+  KEY_INCL = 0x4000,     // bound is inclusive (lo default inclusive: set for lo; hi default exclusive)
+};
+enum : uint32_t {
+  ROW_ALWAYS = 1u << 31, // in Row::adv: matches even when the installed version fails to parse
+  ROW_ADV_MASK = 0x7FFFFFFFu,
+};
+
+// Platform descriptor (device-visible).
+struct alignas(8) PlatInfo {
+  uint8_t cmp;
+  uint8_t drv;
+  uint16_t pad;
+  uint32_t flags;
+};
+
+// Hash-index slot values.
+struct alignas(16) SlotVal {
+  uint32_t name_off;   // into the DB name arena
+  uint32_t name_len;   // bytes | SLOT_POISONED
+  uint32_t row_begin;
+  uint32_t row_count;
+};
+enum : uint32_t { SLOT_POISONED = 1u << 31, SLOT_LEN_MASK = 0x7FFFFFFFu };
+
+// 64-bit key hash of (platform, name): FNV-1a over the bytes seeded by the platform,
+// finished with the murmur3 fmix64 avalanche.  Never 0 (0 marks an empty slot).
+TVM_HD uint64_t key_hash(uint32_t plat, const uint8_t* s, uint32_t n) {
+  uint64_t h = 0xcbf29ce484222325ULL ^ (uint64_t(plat) * 0x9E3779B97F4A7C15ULL);
+  for (uint32_t i = 0; i < n; i++) {
+    h ^= s[i];
+    h *= 0x100000001b3ULL;
+  }
+  h ^= h >> 33;
+  h *= 0xff51afd7ed558ccdULL;
+  h ^= h >> 33;
+  h *= 0xc4ceb9fe1a85ec53ULL;
+  h ^= h >> 33;
+  return h ? h : 1;
+}
+
+// Lexicographic compare of two sort keys held in 8-byte words (memory-order bytes,
+// zero padded): memcmp over the common length, then shorter-first.
+TVM_HD int key_cmp(const uint64_t* a, uint32_t na, const uint64_t* b, uint32_t nb) {
+  uint32_t m = na < nb ? na : nb;
+  uint32_t full = m >> 3, rem = m & 7;
+  for (uint32_t w = 0; w < full; w++) {
+    uint64_t x = a[w], y = b[w];
+    if (x != y) {
+      x = __builtin_bswap64(x);
+      y = __builtin_bswap64(y);
+      return x < y ? -1 : 1;
+    }
+  }
+  if (rem) {
+    uint64_t mask = (1ULL << (8 * rem)) - 1;  // low `rem` bytes in memory order
+    uint64_t x = a[full] & mask, y = b[full] & mask;
+    if (x != y) {
+      x = __builtin_bswap64(x);
+      y = __builtin_bswap64(y);
+      return x < y ? -1 : 1;
+    }
+  }
+  return (na > nb) - (na < nb);
+}
+
+}  // namespace tvm

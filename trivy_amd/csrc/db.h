@@ -1,0 +1,106 @@
+// Load-time flattener: trivy-db bucket tree -> columnar tables for HBM.
+//
+// Replaces the per-call trivy-db lookups of the reference (db.Config.GetAdvisories /
+// <os>.VulnSrc.Get, called from pkg/detector/ospkg/*/ *.go and
+// pkg/detector/library/driver.go:114) with one pass at load time, at the point where
+// the reference opens the DB (pkg/commands/artifact/run.go:311 db.Init).
+//
+// Input: the bucket tree as (path..., key) -> JSON value records, exactly what a bbolt
+// walk (or bolt-fixtures YAML) produces.  Output: the device images in DeviceImage.
+#pragma once
+#include <cstdint>
+#include <map>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+#include "common.h"
+
+namespace tvm {
+
+struct DataSource {
+  std::string id, name, url;
+  bool empty() const { return id.empty() && name.empty() && url.empty(); }
+};
+
+// trivy-db pkg/types.Advisory as decoded by json.Unmarshal (fields the detectors read).
+struct Advisory {
+  std::string vuln_id;                 // from the bucket key
+  std::vector<std::string> vendor_ids;
+  std::vector<std::string> arches;
+  int64_t status = 0;
+  int64_t severity = 0;
+  std::string fixed, affected;
+  std::vector<std::string> vulnerable, patched, unaffected;
+  int32_t data_source = -1;            // index into DB::sources, -1 = nil
+  std::string custom;                  // raw JSON text of Custom, "" = nil
+  bool has_inline_source = false;      // DataSource present in the value JSON itself
+  DataSource inline_source;
+};
+
+// Decodes one advisory value (Go json.Unmarshal into types.Advisory).
+bool decode_advisory(std::string_view json, Advisory& a, std::string& err);
+
+struct Bucket {
+  std::map<std::string, Bucket> sub;        // nested buckets (byte order = bbolt order)
+  std::map<std::string, std::string> kv;    // key -> JSON value
+};
+
+struct Platform {
+  std::string name;   // root bucket name
+  uint8_t drv = DRV_NONE;
+  uint8_t cmp = CMP_NONE;
+  uint32_t flags = 0;
+};
+
+struct Key {
+  uint32_t plat;
+  std::string name;
+  std::vector<uint32_t> advs;  // advisory indices, bbolt key (vulnID) order
+  bool poisoned = false;
+  std::string err;
+};
+
+class DB {
+ public:
+  // ---- intake (before finalize) ----
+  void put(const std::vector<std::string>& path, std::string_view value);
+  // Decode + flatten; false on a structural error.
+  bool finalize(std::string& err);
+
+  // ---- flattened host view ----
+  std::vector<Platform> plats;
+  std::vector<Key> keys;
+  std::vector<Advisory> advs;
+  std::vector<DataSource> sources;
+  int32_t find_plat(std::string_view root) const;
+  // Host-side lookup of a key index (used by drivers for error text); -1 if absent.
+  int32_t find_key(uint32_t plat, std::string_view name) const;
+
+  // ---- device images ----
+  std::vector<uint64_t> slot_hash;
+  std::vector<SlotVal> slot_val;
+  std::vector<uint32_t> slot_key;   // host only: slot -> Key index
+  std::vector<uint8_t> name_arena;
+  std::vector<Row> rows;
+  std::vector<uint64_t> key_words;
+  std::vector<PlatInfo> plat_info;
+  uint64_t slot_mask = 0;
+  uint64_t n_rows_total = 0;
+
+  const Bucket& tree() const { return root_; }
+
+ private:
+  Bucket root_;
+  std::unordered_map<std::string, uint32_t> plat_by_name_;
+  std::unordered_map<std::string, uint32_t> key_dedup_;  // encoded key bytes -> word offset
+  uint32_t intern_key(const std::vector<uint8_t>& k);
+  void flatten_os(uint32_t plat, const Bucket& b, int32_t ds);
+  void build_index();
+};
+
+// Classifies a root bucket name into a driver family (OS buckets only).
+bool classify_os_bucket(std::string_view root, uint8_t& drv, uint8_t& cmp, uint32_t& flags);
+
+}  // namespace tvm

@@ -1,0 +1,96 @@
+// Device engine: HBM-resident advisory tables + the match kernel (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+namespace tvm {
+
+class DB;
+
+// Device view of the flattened tables (db.h device images).
+struct DevDB {
+  const uint64_t* slot_hash = nullptr;
+  const SlotVal* slot_val = nullptr;
+  uint64_t slot_mask = 0;
+  const uint8_t* name_arena = nullptr;
+  const Row* rows = nullptr;
+  const uint64_t* key_words = nullptr;
+  const PlatInfo* plats = nullptr;
+  uint32_t n_plats = 0;
+};
+
+// A package batch in SoA-of-descriptors form.  desc[i] = {plat, name_off, ver_off,
+// name_len | ver_len << 16} into `arena`; plat = 0xFFFFFFFF when the bucket is absent.
+struct HostBatch {
+  std::vector<uint4> desc;
+  std::vector<uint8_t> arena;
+  void add(uint32_t plat, std::string_view name, std::string_view ver);
+};
+
+struct DevBatch {
+  uint4* desc = nullptr;
+  uint8_t* arena = nullptr;
+  uint32_t n = 0;
+  uint64_t arena_bytes = 0;
+  uint64_t spill_words = 0;  // scratch needed for installed keys longer than the LDS slot
+};
+
+// Device-side results of one match launch.
+struct DevMatches {
+  uint2* pairs = nullptr;          // {pkg index, advisory index}, (pkg, advisory) order
+  uint64_t cap = 0;                // capacity in pairs
+  // control block (device): [0] total matches, [1] first poisoned pkg (~0 = none),
+  // [2] spill words used, [3] error bits
+  unsigned long long* ctl = nullptr;
+};
+enum : uint32_t { ERR_SPILL = 1, ERR_LOOKBACK = 2 };
+
+class Engine {
+ public:
+  ~Engine();
+  static Engine* open(const DB& db, int device, std::string& err);
+  int device() const { return dev_; }
+  hipStream_t stream() const { return stream_; }
+  uint64_t table_bytes() const { return table_bytes_; }
+
+  // Device-resident batch management.
+  bool upload(const HostBatch& hb, DevBatch& db, std::string& err);
+  void free_batch(DevBatch& db);
+  bool alloc_matches(uint64_t cap, DevMatches& m, std::string& err);
+  void free_matches(DevMatches& m);
+
+  // Enqueues one match pass on `stream` (no host synchronisation).
+  bool launch(const DevBatch& b, const DevMatches& m, hipStream_t stream, std::string& err);
+
+  // Convenience: upload, match, download. out = pairs; err_pkg = first poisoned package or -1.
+  bool match_host(const HostBatch& hb, std::vector<uint2>& out, int64_t& err_pkg, std::string& err);
+
+  // Algorithmic bytes of one pass over `hb` (roofline numerator).
+  const DB& db() const { return *db_; }
+
+ private:
+  int dev_ = 0;
+  hipStream_t stream_ = nullptr;
+  const DB* db_ = nullptr;
+  DevDB d_;
+  std::vector<void*> allocs_;
+  uint64_t table_bytes_ = 0;
+  // per-launch scratch
+  unsigned long long* tile_words_ = nullptr;
+  uint64_t tile_cap_ = 0;
+  uint64_t* spill_ = nullptr;
+  uint64_t spill_cap_ = 0;
+  std::mutex call_mu_;  // serialises host-synchronous calls sharing the scratch buffers
+  bool ensure_scratch(uint32_t n_tiles, uint64_t spill_words, std::string& err);
+};
+
+constexpr int kTile = 256;         // packages per workgroup (one per lane)
+constexpr int kKeySlotWords = 8;   // LDS bytes per installed key = 64
+
+}  // namespace tvm

@@ -1,0 +1,479 @@
+// Device engine and the fused match kernel (gfx950 / CDNA4).
+//
+// Replaces the per-package loops of the reference drivers (e.g.
+// pkg/detector/ospkg/debian/debian.go:65-117, ubuntu/ubuntu.go:86-126,
+// library/driver.go:111-137) with one launch over a whole batch of packages from
+// many targets.  One workgroup (4 waves) owns a tile of 256 consecutive packages:
+//
+//   1. probe+encode (lane per package): hash (platform, name), linear-probe the
+//      open-addressing index, verify the name bytes, and encode the installed
+//      version into its sort key in LDS (verkey.h, the same code the flattener ran
+//      on the advisory side at load time);
+//   2. block exclusive scan of the per-package row counts (wave shuffles + LDS);
+//   3. pair loop: the tile's (package, row) pairs are dealt 256 at a time to the
+//      lanes (binary search of the LDS scan maps pair -> package), each pair is one
+//      interval test = one or two word-wise key compares; a Zipf-heavy key simply
+//      makes its tile loop longer, never a single lane;
+//   4. ballot/popcount compaction into an LDS match buffer, then a decoupled
+//      look-back across tiles (dynamic tile tickets, one 64-bit {status, value}
+//      word per tile, agent-scope relaxed atomics) gives the tile's global output
+//      offset, so the match list comes out in (package, row) order with no second
+//      pass and no host round trip.
+//
+// All arithmetic is integer/byte; the kernel is bound by HBM/L2 traffic (rows,
+// keys, descriptors and strings), never by ALU.
+#include "engine.h"
+
+#include <algorithm>
+#include <cstring>
+
+#include "db.h"
+#include "verkey.h"
+
+namespace tvm {
+
+namespace {
+
+constexpr int kWaves = kTile / 64;
+constexpr int kMBuf = 2048;  // LDS match buffer (uint2 entries) per tile
+
+struct MatchArgs {
+  DevDB db;
+  const uint4* desc;
+  const uint8_t* arena;
+  uint32_t n;
+  uint32_t n_tiles;
+  uint2* out;
+  uint64_t out_cap;
+  unsigned long long* tile_words;
+  unsigned long long* ctl;  // [0] total, [1] n - first poisoned, [2] spill used, [3] err bits, [4] ticket
+  uint64_t* spill;
+  uint64_t spill_cap;
+};
+
+enum : uint32_t { KI_VALID = 1u << 31, KI_SPILL = 1u << 30, KI_LEN = 0x3FFFu };
+enum : unsigned long long { LB_AGG = 1ull << 62, LB_PFX = 2ull << 62, LB_VAL = (1ull << 62) - 1 };
+
+struct TileShared {
+  uint64_t key[kTile * kKeySlotWords];  // installed keys (16 KiB)
+  uint2 mbuf[kMBuf];                    // compacted matches (16 KiB)
+  uint32_t scan[kTile + 1];             // exclusive scan of row counts
+  uint32_t rbeg[kTile];                 // first row per package
+  uint32_t kinfo[kTile];                // key length | flags
+  uint32_t koff[kTile];                 // spill word offset when KI_SPILL
+  uint32_t wsum[kWaves];
+  uint32_t tile;
+  unsigned long long base;
+};
+
+__device__ __forceinline__ bool name_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+
+// Block-wide exclusive scan of v over kTile lanes; returns the block total.
+__device__ __forceinline__ uint32_t block_scan(TileShared& s, uint32_t v, uint32_t tid) {
+  const uint32_t lane = tid & 63, wave = tid >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= uint32_t(d)) x += y;
+  }
+  if (lane == 63) s.wsum[wave] = x;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kWaves; w++) {
+    uint32_t t = s.wsum[w];
+    off += (uint32_t(w) < wave) ? t : 0;
+    tot += t;
+  }
+  s.scan[tid] = off + x - v;
+  if (tid == 0) s.scan[kTile] = tot;
+  __syncthreads();
+  return tot;
+}
+
+// Evaluates pair j of the tile; returns true and fills rec when it matches.
+__device__ __forceinline__ bool eval_pair(const MatchArgs& a, TileShared& s, uint32_t j, uint2& rec) {
+  // q = last package with scan[q] <= j (its count is > 0 because j < scan[q + 1])
+  uint32_t lo = 0, hi = kTile;  // invariant: scan[lo] <= j < scan[hi]
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (s.scan[mid] <= j) lo = mid;
+    else hi = mid;
+  }
+  const uint32_t q = lo;
+  const Row row = a.db.rows[s.rbeg[q] + (j - s.scan[q])];
+  const uint32_t ki = s.kinfo[q];
+  bool m;
+  if (row.adv & ROW_ALWAYS) {
+    m = true;
+  } else if (!(ki & KI_VALID)) {
+    m = false;
+  } else {
+    const uint64_t* k = (ki & KI_SPILL) ? a.spill + s.koff[q] : &s.key[q * kKeySlotWords];
+    const uint32_t kl = ki & KI_LEN;
+    m = true;
+    if (!(row.hi_len & KEY_INF)) {
+      int c = key_cmp(k, kl, a.db.key_words + row.hi_off, row.hi_len & KEY_LEN_MASK);
+      m = (row.hi_len & KEY_INCL) ? c <= 0 : c < 0;
+    }
+    if (m && !(row.lo_len & KEY_INF)) {
+      int c = key_cmp(k, kl, a.db.key_words + row.lo_off, row.lo_len & KEY_LEN_MASK);
+      m = (row.lo_len & KEY_INCL) ? c >= 0 : c > 0;
+    }
+  }
+  rec = make_uint2(s.tile * kTile + q, row.adv & ROW_ADV_MASK);
+  return m;
+}
+
+// One sweep over the tile's pairs.  DIRECT=false: compact into LDS (count all, store
+// the first kMBuf).  DIRECT=true: store straight to out[base + position].
+template <bool DIRECT>
+__device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared& s, uint32_t total_pairs,
+                                          uint32_t tid, unsigned long long base) {
+  const uint32_t lane = tid & 63, wave = tid >> 6;
+  uint32_t nm = 0;
+  for (uint32_t b0 = 0; b0 < total_pairs; b0 += kTile) {
+    const uint32_t j = b0 + tid;
+    uint2 rec = make_uint2(0, 0);
+    const bool m = (j < total_pairs) && eval_pair(a, s, j, rec);
+    const unsigned long long bal = __ballot(m);
+    const uint32_t lane_off = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) s.wsum[wave] = uint32_t(__popcll(bal));
+    __syncthreads();
+    uint32_t woff = 0, ctot = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) {
+      uint32_t t = s.wsum[w];
+      woff += (uint32_t(w) < wave) ? t : 0;
+      ctot += t;
+    }
+    const uint32_t pos = nm + woff + lane_off;
+    if (m) {
+      if (DIRECT) {
+        if (base + pos < a.out_cap) a.out[base + pos] = rec;
+      } else if (pos < uint32_t(kMBuf)) {
+        s.mbuf[pos] = rec;
+      }
+    }
+    nm += ctot;
+    __syncthreads();
+  }
+  return nm;
+}
+
+__global__ __launch_bounds__(kTile) void match_kernel(MatchArgs a) {
+  __shared__ TileShared s;
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) s.tile = atomicAdd(reinterpret_cast<unsigned int*>(&a.ctl[4]), 1u);
+  __syncthreads();
+  const uint32_t tile = s.tile;
+  const uint32_t p = tile * kTile + tid;
+
+  // ---- 1. probe + encode -------------------------------------------------------------
+  uint32_t cnt = 0, rbeg = 0, kinfo = 0, koff = 0;
+  if (p < a.n) {
+    const uint4 d = a.desc[p];
+    if (d.x < a.db.n_plats) {
+      const PlatInfo pi = a.db.plats[d.x];
+      const uint8_t* name = a.arena + d.y;
+      const uint8_t* ver = a.arena + d.z;
+      const uint32_t nlen = d.w & 0xFFFFu, vlen = d.w >> 16;
+      // installed version -> sort key (LDS slot, or spill for long versions)
+      uint64_t* dst = &s.key[tid * kKeySlotWords];
+      uint32_t need = 0;
+      if ((key_bound(vlen) + 7) / 8 > uint32_t(kKeySlotWords)) {  // might not fit: size it exactly
+        CountSink cs;
+        need = encode_version(pi.cmp, ver, vlen, cs) ? (cs.n + 7) / 8 : 0;
+      }
+      bool spill_ok = true;
+      if (need > uint32_t(kKeySlotWords)) {
+        unsigned long long o = atomicAdd(&a.ctl[2], (unsigned long long)need);
+        if (o + need > a.spill_cap) {
+          atomicOr(&a.ctl[3], (unsigned long long)ERR_SPILL);
+          spill_ok = false;
+        } else {
+          dst = a.spill + o;
+          koff = uint32_t(o);
+          kinfo |= KI_SPILL;
+        }
+      }
+      bool valid = false;
+      if (spill_ok) {
+        WordSink ws(dst);
+        valid = encode_version(pi.cmp, ver, vlen, ws);
+        ws.flush();
+        kinfo |= (ws.n & KI_LEN) | (valid ? KI_VALID : 0u);
+      }
+      // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup
+      if (valid || (pi.flags & PLAT_LOOKUP_FIRST)) {
+        const uint64_t h = key_hash(d.x, name, nlen);
+        for (uint64_t i = h & a.db.slot_mask;; i = (i + 1) & a.db.slot_mask) {
+          const uint64_t sh = a.db.slot_hash[i];
+          if (sh == 0) break;
+          if (sh != h) continue;
+          const SlotVal sv = a.db.slot_val[i];
+          if ((sv.name_len & SLOT_LEN_MASK) != nlen || !name_eq(name, a.db.name_arena + sv.name_off, nlen)) continue;
+          if (sv.name_len & SLOT_POISONED) {
+            atomicMax(&a.ctl[1], (unsigned long long)(a.n - p));
+          } else if (valid) {
+            cnt = sv.row_count;
+            rbeg = sv.row_begin;
+          }
+          break;
+        }
+      }
+    }
+  }
+  s.rbeg[tid] = rbeg;
+  s.kinfo[tid] = kinfo;
+  s.koff[tid] = koff;
+
+  // ---- 2. scan of row counts ------------------------------------------------------------
+  const uint32_t total_pairs = block_scan(s, cnt, tid);
+
+  // ---- 3+4. pair loop with LDS compaction ------------------------------------------------
+  const uint32_t nm = sweep<false>(a, s, total_pairs, tid, 0);
+
+  // ---- decoupled look-back for the tile's output offset ----------------------------------
+  if (tid == 0) {
+    unsigned long long excl = 0;
+    if (tile == 0) {
+      __hip_atomic_store(&a.tile_words[0], LB_PFX | nm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(&a.tile_words[tile], LB_AGG | nm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t j = int64_t(tile) - 1;
+      uint32_t spins = 0;
+      while (j >= 0) {
+        const unsigned long long w = __hip_atomic_load(&a.tile_words[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long st = w & ~LB_VAL;
+        if (st == 0) {
+          if (++spins > (1u << 24)) {  // predecessors hold earlier tickets and are running; bound anyway
+            atomicOr(&a.ctl[3], (unsigned long long)ERR_LOOKBACK);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        excl += w & LB_VAL;
+        if (st == LB_PFX) break;
+        j--;
+      }
+      __hip_atomic_store(&a.tile_words[tile], LB_PFX | (excl + nm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tile == a.n_tiles - 1) a.ctl[0] = excl + nm;
+    s.base = excl;
+  }
+  __syncthreads();
+  const unsigned long long base = s.base;
+
+  // ---- 5. store the tile's matches -------------------------------------------------------
+  if (nm <= uint32_t(kMBuf)) {
+    for (uint32_t i = tid; i < nm; i += kTile)
+      if (base + i < a.out_cap) a.out[base + i] = s.mbuf[i];
+  } else {
+    sweep<true>(a, s, total_pairs, tid, base);  // rare: more matches than the LDS buffer
+  }
+}
+
+bool hip_ok(hipError_t e, const char* what, std::string& err) {
+  if (e == hipSuccess) return true;
+  err = std::string(what) + ": " + hipGetErrorString(e);
+  return false;
+}
+
+template <class T>
+bool upload_vec(const std::vector<T>& v, T** dst, std::vector<void*>& allocs, uint64_t& bytes, std::string& err) {
+  size_t n = std::max<size_t>(v.size(), 1) * sizeof(T);
+  void* p = nullptr;
+  if (!hip_ok(hipMalloc(&p, n), "hipMalloc(tables)", err)) return false;
+  allocs.push_back(p);
+  if (!v.empty() && !hip_ok(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy(tables)", err))
+    return false;
+  bytes += n;
+  *dst = static_cast<T*>(p);
+  return true;
+}
+
+}  // namespace
+
+void HostBatch::add(uint32_t plat, std::string_view name, std::string_view ver) {
+  uint4 d;
+  d.x = plat;
+  d.y = uint32_t(arena.size());
+  arena.insert(arena.end(), name.begin(), name.end());
+  d.z = uint32_t(arena.size());
+  arena.insert(arena.end(), ver.begin(), ver.end());
+  d.w = uint32_t(std::min<size_t>(name.size(), 0xFFFF)) | (uint32_t(std::min<size_t>(ver.size(), 0xFFFF)) << 16);
+  desc.push_back(d);
+}
+
+Engine::~Engine() {
+  if (dev_ >= 0) hipSetDevice(dev_);
+  for (void* p : allocs_) hipFree(p);
+  if (tile_words_) hipFree(tile_words_);
+  if (spill_) hipFree(spill_);
+  if (stream_) hipStreamDestroy(stream_);
+}
+
+Engine* Engine::open(const DB& db, int device, std::string& err) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    err = "no HIP device available (trivy_amd requires an MI355X / gfx950 GPU)";
+    return nullptr;
+  }
+  if (device < 0 || device >= ndev) {
+    err = "invalid HIP device index";
+    return nullptr;
+  }
+  Engine* e = new Engine();
+  e->dev_ = device;
+  e->db_ = &db;
+  if (!hip_ok(hipSetDevice(device), "hipSetDevice", err) ||
+      !hip_ok(hipStreamCreateWithFlags(&e->stream_, hipStreamNonBlocking), "hipStreamCreate", err)) {
+    delete e;
+    return nullptr;
+  }
+  uint64_t* sh; SlotVal* sv; uint8_t* na; Row* rows; uint64_t* kw; PlatInfo* pl;
+  bool ok = upload_vec(db.slot_hash, &sh, e->allocs_, e->table_bytes_, err) &&
+            upload_vec(db.slot_val, &sv, e->allocs_, e->table_bytes_, err) &&
+            upload_vec(db.name_arena, &na, e->allocs_, e->table_bytes_, err) &&
+            upload_vec(db.rows, &rows, e->allocs_, e->table_bytes_, err) &&
+            upload_vec(db.key_words, &kw, e->allocs_, e->table_bytes_, err) &&
+            upload_vec(db.plat_info, &pl, e->allocs_, e->table_bytes_, err);
+  if (!ok) {
+    delete e;
+    return nullptr;
+  }
+  e->d_.slot_hash = sh;
+  e->d_.slot_val = sv;
+  e->d_.slot_mask = db.slot_mask;
+  e->d_.name_arena = na;
+  e->d_.rows = rows;
+  e->d_.key_words = kw;
+  e->d_.plats = pl;
+  e->d_.n_plats = uint32_t(db.plats.size());
+  return e;
+}
+
+bool Engine::ensure_scratch(uint32_t n_tiles, uint64_t spill_words, std::string& err) {
+  if (n_tiles > tile_cap_) {
+    if (tile_words_) hipFree(tile_words_);
+    tile_words_ = nullptr;
+    uint64_t cap = std::max<uint64_t>(n_tiles, 1024);
+    if (!hip_ok(hipMalloc(&tile_words_, cap * 8), "hipMalloc(tile words)", err)) return false;
+    tile_cap_ = cap;
+  }
+  if (spill_words > spill_cap_) {
+    if (spill_) hipFree(spill_);
+    spill_ = nullptr;
+    uint64_t cap = std::max<uint64_t>(spill_words, 4096);
+    if (!hip_ok(hipMalloc(&spill_, cap * 8), "hipMalloc(spill)", err)) return false;
+    spill_cap_ = cap;
+  }
+  return true;
+}
+
+bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
+  hipSetDevice(dev_);
+  b.n = uint32_t(hb.desc.size());
+  b.arena_bytes = hb.arena.size();
+  b.spill_words = 0;
+  for (const uint4& d : hb.desc) {
+    uint32_t need = (key_bound(d.w >> 16) + 7) / 8;
+    if (need > uint32_t(kKeySlotWords)) b.spill_words += need;
+  }
+  if (!hip_ok(hipMalloc(&b.desc, std::max<size_t>(hb.desc.size(), 1) * sizeof(uint4)), "hipMalloc(batch)", err)) return false;
+  if (!hip_ok(hipMalloc(&b.arena, std::max<size_t>(hb.arena.size(), 1)), "hipMalloc(batch arena)", err)) return false;
+  if (!hb.desc.empty() &&
+      !hip_ok(hipMemcpy(b.desc, hb.desc.data(), hb.desc.size() * sizeof(uint4), hipMemcpyHostToDevice), "H2D batch", err))
+    return false;
+  if (!hb.arena.empty() &&
+      !hip_ok(hipMemcpy(b.arena, hb.arena.data(), hb.arena.size(), hipMemcpyHostToDevice), "H2D arena", err))
+    return false;
+  return true;
+}
+
+void Engine::free_batch(DevBatch& b) {
+  hipSetDevice(dev_);
+  if (b.desc) hipFree(b.desc);
+  if (b.arena) hipFree(b.arena);
+  b = DevBatch{};
+}
+
+bool Engine::alloc_matches(uint64_t cap, DevMatches& m, std::string& err) {
+  hipSetDevice(dev_);
+  m.cap = std::max<uint64_t>(cap, 1);
+  if (!hip_ok(hipMalloc(&m.pairs, m.cap * sizeof(uint2)), "hipMalloc(matches)", err)) return false;
+  if (!hip_ok(hipMalloc(&m.ctl, 8 * sizeof(unsigned long long)), "hipMalloc(ctl)", err)) return false;
+  return true;
+}
+
+void Engine::free_matches(DevMatches& m) {
+  hipSetDevice(dev_);
+  if (m.pairs) hipFree(m.pairs);
+  if (m.ctl) hipFree(m.ctl);
+  m = DevMatches{};
+}
+
+bool Engine::launch(const DevBatch& b, const DevMatches& m, hipStream_t st, std::string& err) {
+  hipSetDevice(dev_);
+  const uint32_t n_tiles = (b.n + kTile - 1) / kTile;
+  if (!ensure_scratch(n_tiles, b.spill_words, err)) return false;
+  if (!hip_ok(hipMemsetAsync(m.ctl, 0, 8 * sizeof(unsigned long long), st), "memset(ctl)", err)) return false;
+  if (n_tiles == 0) return true;
+  if (!hip_ok(hipMemsetAsync(tile_words_, 0, uint64_t(n_tiles) * 8, st), "memset(tiles)", err)) return false;
+  MatchArgs a;
+  a.db = d_;
+  a.desc = b.desc;
+  a.arena = b.arena;
+  a.n = b.n;
+  a.n_tiles = n_tiles;
+  a.out = m.pairs;
+  a.out_cap = m.cap;
+  a.tile_words = tile_words_;
+  a.ctl = m.ctl;
+  a.spill = spill_;
+  a.spill_cap = spill_cap_;
+  hipLaunchKernelGGL(match_kernel, dim3(n_tiles), dim3(kTile), 0, st, a);
+  return hip_ok(hipGetLastError(), "match_kernel launch", err);
+}
+
+bool Engine::match_host(const HostBatch& hb, std::vector<uint2>& out, int64_t& err_pkg, std::string& err) {
+  out.clear();
+  err_pkg = -1;
+  if (hb.desc.empty()) return true;
+  std::lock_guard<std::mutex> lk(call_mu_);
+  DevBatch b;
+  if (!upload(hb, b, err)) { free_batch(b); return false; }
+  uint64_t cap = std::max<uint64_t>(hb.desc.size() * 4, 1024);
+  bool ok = true;
+  for (int attempt = 0; attempt < 2 && ok; attempt++) {
+    DevMatches m;
+    ok = alloc_matches(cap, m, err) && launch(b, m, stream_, err) &&
+         hip_ok(hipStreamSynchronize(stream_), "match_kernel", err);
+    unsigned long long ctl[8] = {0};
+    if (ok) ok = hip_ok(hipMemcpy(ctl, m.ctl, sizeof(ctl), hipMemcpyDeviceToHost), "D2H ctl", err);
+    if (ok && ctl[3]) { err = "match kernel internal error bits " + std::to_string(ctl[3]); ok = false; }
+    if (ok && ctl[0] > cap) {  // output buffer too small: rerun with the exact size
+      cap = ctl[0];
+      free_matches(m);
+      continue;
+    }
+    if (ok) {
+      err_pkg = ctl[1] ? int64_t(b.n - ctl[1]) : -1;
+      out.resize(ctl[0]);
+      if (!out.empty()) ok = hip_ok(hipMemcpy(out.data(), m.pairs, out.size() * sizeof(uint2), hipMemcpyDeviceToHost), "D2H matches", err);
+    }
+    free_matches(m);
+    break;
+  }
+  free_batch(b);
+  return ok;
+}
+
+}  // namespace tvm

@@ -1,0 +1,253 @@
+// Version sort-key encoders (host + device).
+//
+// Every supported version grammar is mapped to a byte string whose plain
+// lexicographic order (common.h key_cmp) IS the reference comparator's order.
+// The flattener encodes advisory bounds (FixedVersion, AffectedVersion, ...) once
+// at load time with these functions; the probe kernel encodes each installed
+// version on the GPU with the very same code, so a (package, advisory) test is
+// one short word-wise compare instead of a parse + compare per pair.
+//
+// ---- dpkg: github.com/knqyf263/go-deb-version (reference go.mod:62) ---------------------
+// Call sites: pkg/detector/ospkg/debian/debian.go:66,107,113, ubuntu/ubuntu.go:92,116,122,
+// amazon/amazon.go:67,74,80.  go-deb-version compares epoch (int), then upstream, then
+// revision; each part is cut into pairs (non-digit run, digit run) - the first run is
+// "" when the part starts with a digit, missing entries are ("", 0) - and a pair
+// compares its runs byte by byte with weights '~' < end-of-run < letters < others
+// (letter = unicode.IsLetter of the byte read as a Latin-1 rune), then its digit runs
+// as integers (strconv.Atoi, which clamps at MaxInt64 on overflow).
+//
+// Key layout:  EPOCH  PART(upstream)  PART(revision)
+//   EPOCH        = nbytes(1) + big-endian minimal bytes
+//   PART("")     = TERM0 END            (the empty part equals one ("", 0) pair)
+//   PART(s)      = { code(c) for c in run ; TERM_k ; k big-endian bytes of the number }* END
+//   codes: '~'=0x01 < END=0x02 < TERM_k=0x03+k (k=0..8) < letters 0x0C..0x80 < others 0x81..0xFF
+// TERM_k both ends the run (end-of-run weight 0 sits between '~' and letters) and
+// orders numbers by byte length before value.  A missing pair at index >= 1 is
+// represented by END, which sorts exactly like the ("", 0) padding against any real
+// pair (whose run is non-empty there).  Bound: len(key) <= 2*len(version) + 12.
+#pragma once
+#include "common.h"
+#include "unicode_tab.h"
+
+namespace tvm {
+
+// ------------------------------------------------------------------ Unicode categories ----
+static __constant__ uint32_t d_uni_letter[TVM_UNI_NLETTER][2] = {TVM_UNI_LETTER_RANGES};
+static __constant__ uint32_t d_uni_digit[TVM_UNI_NDIGIT][2] = {TVM_UNI_DIGIT_RANGES};
+static const uint32_t h_uni_letter[TVM_UNI_NLETTER][2] = {TVM_UNI_LETTER_RANGES};
+static const uint32_t h_uni_digit[TVM_UNI_NDIGIT][2] = {TVM_UNI_DIGIT_RANGES};
+
+TVM_HD bool uni_in(const uint32_t (*t)[2], int n, uint32_t cp) {
+  int lo = 0, hi = n - 1;
+  while (lo <= hi) {
+    int mid = (lo + hi) >> 1;
+    if (cp < t[mid][0]) hi = mid - 1;
+    else if (cp > t[mid][1]) lo = mid + 1;
+    else return true;
+  }
+  return false;
+}
+// unicode.IsLetter
+TVM_HD bool rune_letter(uint32_t cp) {
+  if (cp < 0x80) return ((cp | 0x20) >= 'a' && (cp | 0x20) <= 'z');
+#ifdef __HIP_DEVICE_COMPILE__
+  return uni_in(d_uni_letter, TVM_UNI_NLETTER, cp);
+#else
+  return uni_in(h_uni_letter, TVM_UNI_NLETTER, cp);
+#endif
+}
+// unicode.IsDigit
+TVM_HD bool rune_digit(uint32_t cp) {
+  if (cp < 0x80) return cp >= '0' && cp <= '9';
+#ifdef __HIP_DEVICE_COMPILE__
+  return uni_in(d_uni_digit, TVM_UNI_NDIGIT, cp);
+#else
+  return uni_in(h_uni_digit, TVM_UNI_NDIGIT, cp);
+#endif
+}
+// utf8.DecodeRuneInString: invalid -> U+FFFD with width 1.
+TVM_HD uint32_t decode_rune(const uint8_t* s, uint32_t n, uint32_t* w) {
+  uint32_t c = s[0];
+  *w = 1;
+  if (c < 0x80) return c;
+  uint32_t lo = 0x80, hi = 0xBF, need, cp;
+  if (c >= 0xC2 && c <= 0xDF) { need = 1; cp = c & 0x1F; }
+  else if (c >= 0xE0 && c <= 0xEF) { need = 2; cp = c & 0x0F; if (c == 0xE0) lo = 0xA0; if (c == 0xED) hi = 0x9F; }
+  else if (c >= 0xF0 && c <= 0xF4) { need = 3; cp = c & 0x07; if (c == 0xF0) lo = 0x90; if (c == 0xF4) hi = 0x8F; }
+  else return 0xFFFD;
+  if (need >= n) return 0xFFFD;
+  for (uint32_t k = 1; k <= need; k++) {
+    uint32_t d = s[k];
+    if (k == 1 ? (d < lo || d > hi) : (d < 0x80 || d > 0xBF)) return 0xFFFD;
+    cp = (cp << 6) | (d & 0x3F);
+  }
+  *w = need + 1;
+  return cp;
+}
+
+TVM_HD bool is_adigit(uint8_t c) { return c >= '0' && c <= '9'; }
+
+// ------------------------------------------------------------------------------ dpkg -----
+enum : uint8_t { DEB_TILDE = 0x01, DEB_END = 0x02, DEB_TERM0 = 0x03 };
+
+struct DebCodes { uint8_t v[256]; };
+constexpr bool latin1_letter(int b) {
+  return (b >= 'A' && b <= 'Z') || (b >= 'a' && b <= 'z') || b == 0xAA || b == 0xB5 || b == 0xBA ||
+         (b >= 0xC0 && b <= 0xFF && b != 0xD7 && b != 0xF7);
+}
+constexpr DebCodes make_deb_codes() {
+  DebCodes t{};
+  int code = 0x0C;
+  for (int b = 0; b < 256; b++)
+    if (latin1_letter(b)) t.v[b] = uint8_t(code++);
+  for (int b = 1; b < 256; b++)
+    if (!latin1_letter(b) && !(b >= '0' && b <= '9') && b != '~') t.v[b] = uint8_t(code++);
+  t.v['~'] = DEB_TILDE;
+  return t;
+}
+static_assert(make_deb_codes().v[0xFF] == 0x80 && make_deb_codes().v[0xF7] == 0xFF &&
+                  make_deb_codes().v['A'] == 0x0C && make_deb_codes().v['.'] > 0x80,
+              "dpkg code table must fill 0x0C..0xFF exactly");
+static __constant__ DebCodes d_deb_codes = make_deb_codes();
+static constexpr DebCodes h_deb_codes = make_deb_codes();
+
+TVM_HD uint8_t deb_code(uint8_t b) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return d_deb_codes.v[b];
+#else
+  return h_deb_codes.v[b];
+#endif
+}
+
+// verifyUpstreamVersion / verifyDebianRevision rune checks.
+TVM_HD bool deb_valid_runes(const uint8_t* s, uint32_t n, bool upstream) {
+  uint32_t i = 0;
+  while (i < n) {
+    uint8_t c = s[i];
+    if (c < 0x80) {
+      bool ok = is_adigit(c) || ((c | 0x20) >= 'a' && (c | 0x20) <= 'z') || c == '.' || c == '+' ||
+                c == '~' || c == '_' || (upstream && (c == '-' || c == ':'));
+      if (!ok) return false;
+      i++;
+    } else {
+      uint32_t w;
+      uint32_t r = decode_rune(s + i, n - i, &w);
+      if (!rune_letter(r) && !rune_digit(r)) return false;
+      i += w;
+    }
+  }
+  return true;
+}
+
+template <class Sink>
+TVM_HD void deb_part(const uint8_t* s, uint32_t n, Sink& o) {
+  if (n == 0) {
+    o.put(DEB_TERM0);
+    o.put(DEB_END);
+    return;
+  }
+  uint32_t i = 0;
+  while (i < n) {
+    while (i < n && !is_adigit(s[i])) o.put(deb_code(s[i++]));
+    uint64_t v = 0;
+    bool over = false;
+    while (i < n && is_adigit(s[i])) {
+      uint64_t d = uint64_t(s[i++] - '0');
+      if (!over) {
+        if (v > (uint64_t(INT64_MAX) - d) / 10) over = true;
+        else v = v * 10 + d;
+      }
+    }
+    if (over) v = uint64_t(INT64_MAX);
+    uint32_t k = 0;
+    for (uint64_t t = v; t; t >>= 8) k++;
+    o.put(uint8_t(DEB_TERM0 + k));
+    for (int b = int(k) - 1; b >= 0; b--) o.put(uint8_t(v >> (8 * b)));
+  }
+  o.put(DEB_END);
+}
+
+// go-deb-version NewVersion + key emission.  Returns false (emitting nothing) on a
+// parse error; the caller's sink receives the key otherwise.
+template <class Sink>
+TVM_HD bool deb_encode(const uint8_t* s, uint32_t n, Sink& o) {
+  // epoch: strconv.Atoi of the text before the first ':'; negative -> error
+  uint32_t colon = n;
+  for (uint32_t i = 0; i < n; i++)
+    if (s[i] == ':') { colon = i; break; }
+  uint64_t epoch = 0;
+  const uint8_t* r = s;
+  uint32_t rn = n;
+  if (colon < n) {
+    uint32_t i = 0;
+    bool neg = false;
+    if (colon > 0 && (s[0] == '+' || s[0] == '-')) { neg = s[0] == '-'; i = 1; }
+    if (i == colon) return false;
+    for (; i < colon; i++) {
+      if (!is_adigit(s[i])) return false;
+      uint64_t d = uint64_t(s[i] - '0');
+      if (epoch > (~0ULL - d) / 10) return false;
+      epoch = epoch * 10 + d;
+      if (epoch > uint64_t(INT64_MAX) + (neg ? 1 : 0)) return false;
+    }
+    if (neg && epoch != 0) return false;  // epoch is negative
+    r = s + colon + 1;
+    rn = n - colon - 1;
+  }
+  // split at the last '-'
+  uint32_t dash = rn;
+  for (uint32_t i = rn; i-- > 0;)
+    if (r[i] == '-') { dash = i; break; }
+  const uint8_t* up = r;
+  uint32_t nup = dash;
+  const uint8_t* rev = r + (dash < rn ? dash + 1 : rn);
+  uint32_t nrev = dash < rn ? rn - dash - 1 : 0;
+  if (nup == 0 || !is_adigit(up[0])) return false;
+  if (!deb_valid_runes(up, nup, true) || !deb_valid_runes(rev, nrev, false)) return false;
+  uint32_t k = 0;
+  for (uint64_t t = epoch; t; t >>= 8) k++;
+  o.put(uint8_t(k));
+  for (int b = int(k) - 1; b >= 0; b--) o.put(uint8_t(epoch >> (8 * b)));
+  deb_part(up, nup, o);
+  deb_part(rev, nrev, o);
+  return true;
+}
+
+// Upper bound on the key length of a version string of n bytes (all grammars).
+TVM_HD uint32_t key_bound(uint32_t n) { return 2 * n + 16; }
+
+// ---------------------------------------------------------------------------- sinks -----
+// Device sink: packs bytes into little-endian 64-bit words and stores whole words.
+struct WordSink {
+  uint64_t* dst;
+  uint64_t acc = 0;
+  uint32_t n = 0;
+  TVM_HD explicit WordSink(uint64_t* d) : dst(d) {}
+  TVM_HD void put(uint8_t b) {
+    acc |= uint64_t(b) << (8 * (n & 7));
+    if ((++n & 7) == 0) {
+      dst[(n >> 3) - 1] = acc;
+      acc = 0;
+    }
+  }
+  TVM_HD void flush() {
+    if (n & 7) dst[n >> 3] = acc;
+  }
+};
+
+// Counting sink (length only).
+struct CountSink {
+  uint32_t n = 0;
+  TVM_HD void put(uint8_t) { n++; }
+};
+
+// Dispatch by grammar.
+template <class Sink>
+TVM_HD bool encode_version(uint8_t cmp, const uint8_t* s, uint32_t n, Sink& o) {
+  switch (cmp) {
+    case CMP_DEB: return deb_encode(s, n, o);
+    default: return false;
+  }
+}
+
+}  // namespace tvm

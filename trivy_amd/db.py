@@ -1,0 +1,107 @@
+"""Advisory DB intake and device engine (wrappers of tvm_db_* / tvm_engine_*).
+
+Replaces trivy-db's db.Init (reference pkg/commands/artifact/run.go:311): the
+bucket tree is handed over record by record - (bucket path..., key) -> JSON
+value, what a bbolt walk or bolt-fixtures (pkg/dbtest/db.go:17-36) produces -
+then flattened once and uploaded to HBM.
+"""
+import ctypes
+import json
+
+from . import _lib
+from ._lib import lib, s, errbuf, Str
+
+
+class DB:
+    def __init__(self):
+        self.h = lib().tvm_db_new()
+        self._finalized = False
+
+    def put(self, path, value):
+        arr = (Str * len(path))(*[s(p) for p in path])
+        v = value.encode() if isinstance(value, str) else value
+        rc = lib().tvm_db_put(self.h, arr, len(path), v, len(v))
+        if rc:
+            raise ValueError(f"tvm_db_put failed ({rc})")
+
+    def put_records(self, records):
+        """records: iterable of {"path": [...], "value": "<json>"} (tests/golden/fixtures format)."""
+        by_depth = {}
+        for r in records:
+            by_depth.setdefault(len(r["path"]), []).append(r)
+        for depth, recs in by_depth.items():
+            keep = []
+            paths = (Str * (len(recs) * depth))()
+            vals = (Str * len(recs))()
+            for i, r in enumerate(recs):
+                for j, p in enumerate(r["path"]):
+                    b = p.encode()
+                    keep.append(b)
+                    paths[i * depth + j] = Str(b, len(b))
+                v = r["value"].encode()
+                keep.append(v)
+                vals[i] = Str(v, len(v))
+            rc = lib().tvm_db_put_many(self.h, len(recs), ctypes.cast(paths, ctypes.c_void_p), depth,
+                                       ctypes.cast(vals, ctypes.c_void_p))
+            if rc:
+                raise ValueError(f"tvm_db_put_many failed ({rc})")
+
+    def finalize(self):
+        e = errbuf()
+        rc = lib().tvm_db_finalize(self.h, e, len(e))
+        if rc:
+            raise ValueError(e.value.decode())
+        self._finalized = True
+        return self
+
+    def stats(self):
+        out = (ctypes.c_uint64 * 5)()
+        lib().tvm_db_stats(self.h, out)
+        return dict(zip(["platforms", "keys", "advisories", "rows", "key_bytes"], list(out)))
+
+    def __del__(self):
+        h, self.h = getattr(self, "h", None), None
+        if h and _lib._lib is not None:
+            _lib._lib.tvm_db_free(h)
+
+
+def load_fixture_files(paths):
+    """Build + finalize a DB from tests/golden/fixtures JSON files (dbtest.InitDB analogue)."""
+    db = DB()
+    for p in paths:
+        with open(p, encoding="utf-8") as f:
+            db.put_records(json.load(f))
+    return db.finalize()
+
+
+class Engine:
+    """Device-resident tables on one HIP device (fails loudly without a GPU)."""
+
+    def __init__(self, db, device=0):
+        if not db._finalized:
+            db.finalize()
+        e = errbuf()
+        self.db = db  # the engine references the DB's host tables
+        self.h = lib().tvm_engine_open(db.h, device, e, len(e))
+        if not self.h:
+            raise RuntimeError(f"tvm_engine_open: {e.value.decode()}")
+
+    def swap(self, db):
+        if not db._finalized:
+            db.finalize()
+        e = errbuf()
+        rc = lib().tvm_engine_swap(self.h, db.h, e, len(e))
+        if rc:
+            raise RuntimeError(e.value.decode())
+        self.db = db
+
+    def table_bytes(self):
+        return lib().tvm_engine_table_bytes(self.h)
+
+    def close(self):
+        h, self.h = getattr(self, "h", None), None
+        if h and _lib._lib is not None:
+            _lib._lib.tvm_engine_close(h)
+
+    def __del__(self):
+        self.close()
