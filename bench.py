@@ -161,7 +161,8 @@ def main():
         from trivy_amd._lib import lib
         out = np.zeros(2 * total, dtype=np.uint32)
         got = ctypes.c_uint64()
-        lib().tvm_match_fetch(eng.h, b, out.ctypes.data, total, ctypes.byref(got))
+        if lib().tvm_match_fetch(eng.h, b, out.ctypes.data, total, ctypes.byref(got)):
+            raise RuntimeError("tvm_match_fetch failed")
         opk, oad = om.match(om.Prepared(sdb, batch), n_threads=args.cpu_threads)
         pr = out.reshape(-1, 2)
         ok = np.array_equal(pr[:, 0], opk) and np.array_equal(pr[:, 1], oad)

@@ -168,7 +168,9 @@ int tvm_match_launch(tvm_engine* e, tvm_batch* b, char* err, size_t errlen);
 int tvm_engine_sync(tvm_engine* e, char* err, size_t errlen);
 /* After sync: total matches, first poisoned package (-1 none), internal error bits. */
 int tvm_match_status(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* err_pkg, uint64_t* err_bits);
-/* Copies up to cap pairs {pkg_index, advisory_index} (uint32 x2) to host. */
+/* Copies up to cap pairs {pkg_index, advisory_index} (uint32 x2) to host in (package,
+ * advisory) order.  TVM_EINVAL when the device match buffer overflowed (n_matches > the
+ * upload's match_cap): re-upload with match_cap >= n_matches. */
 int tvm_match_fetch(tvm_engine* e, tvm_batch* b, uint32_t* pairs, uint64_t cap, uint64_t* n_out);
 /* Times `steps` back-to-back launches with HIP events on the engine stream (ms total). */
 int tvm_match_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err, size_t errlen);

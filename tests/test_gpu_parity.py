@@ -42,7 +42,11 @@ def run_batch(eng, sdb, batch, cap=None):
         assert bits.value == 0
         out = np.zeros(2 * max(n.value, 1), dtype=np.uint32)
         got = ctypes.c_uint64()
-        assert L.tvm_match_fetch(eng.h, b, out.ctypes.data, n.value, ctypes.byref(got)) == 0
+        rc = L.tvm_match_fetch(eng.h, b, out.ctypes.data, n.value, ctypes.byref(got))
+        if cap is not None and n.value > cap:
+            assert rc != 0 and got.value == 0  # overflow is reported, never silently truncated
+            return None, None, errp.value, n.value
+        assert rc == 0
         pairs = out[:2 * got.value].reshape(-1, 2)
         return pairs[:, 0].astype(np.int64), pairs[:, 1].astype(np.int64), errp.value, n.value
     finally:
@@ -74,7 +78,7 @@ def test_output_buffer_too_small_reports_total(world):
     sdb, eng = world
     batch = make_batch(sdb, 20, 200, [1, 1, 1, 1], seed=5)
     pk, ad, errp, total = run_batch(eng, sdb, batch, cap=10)
-    assert total > 10 and len(pk) == 10
+    assert total > 10 and pk is None
 
 
 def test_heavy_key_overflows_lds_buffer(oracle_built):

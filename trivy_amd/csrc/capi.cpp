@@ -287,8 +287,9 @@ void tvm_batch_free(tvm_batch* b) {
     hipSetDevice(b->device);
     hipFree(b->dev.desc);
     hipFree(b->dev.arena);
-    hipFree(b->m.pairs);
-    hipFree(b->m.ctl);
+    (void)hipFree(b->m.pairs);
+    (void)hipFree(b->m.dir);
+    (void)hipFree(b->m.ctl);
   }
   delete b;
 }
@@ -325,7 +326,7 @@ int tvm_batch_upload(tvm_engine* e, tvm_batch* b, uint64_t cap, char* err, size_
     e->eng->free_matches(b->m);
     b->uploaded = false;
   }
-  if (!e->eng->upload(b->hb, b->dev, msg) || !e->eng->alloc_matches(cap, b->m, msg)) {
+  if (!e->eng->upload(b->hb, b->dev, msg) || !e->eng->alloc_matches(cap, b->dev.n, b->m, msg)) {
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
   }
@@ -369,8 +370,14 @@ int tvm_match_fetch(tvm_engine* e, tvm_batch* b, uint32_t* pairs, uint64_t cap, 
   uint64_t n = 0;
   int rc = tvm_match_status(e, b, &n, nullptr, nullptr);
   if (rc) return rc;
-  n = std::min<uint64_t>(std::min<uint64_t>(n, cap), b->m.cap);
-  if (n && hipMemcpy(pairs, b->m.pairs, n * sizeof(uint2), hipMemcpyDeviceToHost) != hipSuccess) return TVM_EDEVICE;
+  if (n_out) *n_out = 0;
+  if (n > b->m.cap) return TVM_EINVAL;  // device buffer overflowed: re-upload with a larger cap
+  std::vector<uint2> ordered;
+  std::string msg;
+  (void)hipSetDevice(e->device);
+  if (!Engine::fetch_ordered(b->m, b->dev.n, n, ordered, msg)) return TVM_EDEVICE;
+  n = std::min<uint64_t>(n, cap);
+  if (n) memcpy(pairs, ordered.data(), n * sizeof(uint2));
   if (n_out) *n_out = n;
   return TVM_OK;
 }
@@ -423,8 +430,8 @@ uint64_t tvm_match_algorithmic_bytes(tvm_engine* e, tvm_batch* b) {
       const SlotVal& v = db.slot_val[i];
       for (uint32_t r = 0; r < v.row_count; r++) {
         const Row& row = db.rows[v.row_begin + r];
-        bytes += 16;
-        if (!(row.hi_len & KEY_INF)) bytes += row.hi_len & KEY_LEN_MASK;
+        bytes += sizeof(Row);  // 16 B header + 16 B inline hi-key prefix
+        if (!(row.hi_len & KEY_INF) && (row.hi_len & KEY_LEN_MASK) > 16) bytes += (row.hi_len & KEY_LEN_MASK) - 16;
         if (!(row.lo_len & KEY_INF)) bytes += row.lo_len & KEY_LEN_MASK;
       }
       break;

@@ -40,6 +40,8 @@ struct alignas(16) Row {
   uint32_t adv;      // global advisory index (host-side record)
   uint16_t lo_len;   // bytes | flags
   uint16_t hi_len;
+  uint64_t hi_pre0;  // first 16 bytes of the hi key inline (memory-order words, zero padded):
+  uint64_t hi_pre1;  // most compares finish here without touching the key arena
 };
 enum : uint16_t {
   KEY_LEN_MASK = 0x3FFF,
@@ -107,6 +109,32 @@ TVM_HD int key_cmp(const uint64_t* a, uint32_t na, const uint64_t* b, uint32_t n
     }
   }
   return (na > nb) - (na < nb);
+}
+
+// key_cmp(a, b) where the first two words of b are given inline (b0, b1) and the full b
+// lives at b_full (read only when the first 16 bytes tie and both keys are longer).
+TVM_HD int key_cmp_pre(const uint64_t* a, uint32_t na, uint64_t b0, uint64_t b1, const uint64_t* b_full,
+                       uint32_t nb) {
+  const uint32_t m = na < nb ? na : nb;
+  const uint64_t w[2] = {b0, b1};
+#pragma unroll
+  for (uint32_t i = 0; i < 2; i++) {
+    if (8 * i >= m) return (na > nb) - (na < nb);
+    uint64_t x = a[i], y = w[i];
+    const uint32_t left = m - 8 * i;
+    if (left < 8) {
+      const uint64_t mask = (1ULL << (8 * left)) - 1;
+      x &= mask;
+      y &= mask;
+    }
+    if (x != y) {
+      x = __builtin_bswap64(x);
+      y = __builtin_bswap64(y);
+      return x < y ? -1 : 1;
+    }
+  }
+  if (m <= 16) return (na > nb) - (na < nb);
+  return key_cmp(a + 2, na - 16, b_full + 2, nb - 16);
 }
 
 }  // namespace tvm

@@ -218,6 +218,8 @@ void DB::build_index() {
           if (!deb_encode(reinterpret_cast<const uint8_t*>(a.fixed.data()), uint32_t(a.fixed.size()), s)) continue;
           r.hi_off = intern_key(kb);
           r.hi_len = uint16_t(kb.size());
+          for (size_t i = 0; i < kb.size() && i < 16; i++)
+            (i < 8 ? r.hi_pre0 : r.hi_pre1) |= uint64_t(kb[i]) << (8 * (i % 8));
         }
       } else {
         continue;

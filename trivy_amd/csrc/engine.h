@@ -41,15 +41,25 @@ struct DevBatch {
   uint64_t spill_words = 0;  // scratch needed for installed keys longer than the LDS slot
 };
 
-// Device-side results of one match launch.
+// Device-side results of one match launch: the per-package advisory lists.
+// Tile t (packages [256t, 256t+256)) owns the segment pairs[dir[t].base .. + dir[t].count),
+// ordered by (package, advisory); segments are placed by one atomic reservation per
+// tile, so the global (package, advisory) order is read through the directory.
+struct TileDir {
+  unsigned long long base;
+  uint32_t count;
+  uint32_t pad;
+};
 struct DevMatches {
-  uint2* pairs = nullptr;          // {pkg index, advisory index}, (pkg, advisory) order
+  uint2* pairs = nullptr;          // {pkg index, advisory index}
   uint64_t cap = 0;                // capacity in pairs
-  // control block (device): [0] total matches, [1] first poisoned pkg (~0 = none),
-  // [2] spill words used, [3] error bits
+  TileDir* dir = nullptr;          // one entry per tile
+  uint32_t dir_cap = 0;
+  // control block (device): [0] total matches (reservation counter), [1] n - first
+  // poisoned pkg (0 = none), [2] spill words used, [3] error bits, [4] tile ticket
   unsigned long long* ctl = nullptr;
 };
-enum : uint32_t { ERR_SPILL = 1, ERR_LOOKBACK = 2 };
+enum : uint32_t { ERR_SPILL = 1, ERR_TILES = 2 };
 
 class Engine {
  public:
@@ -62,11 +72,16 @@ class Engine {
   // Device-resident batch management.
   bool upload(const HostBatch& hb, DevBatch& db, std::string& err);
   void free_batch(DevBatch& db);
-  bool alloc_matches(uint64_t cap, DevMatches& m, std::string& err);
+  bool alloc_matches(uint64_t cap, uint32_t n_pkgs, DevMatches& m, std::string& err);
   void free_matches(DevMatches& m);
 
   // Enqueues one match pass on `stream` (no host synchronisation).
   bool launch(const DevBatch& b, const DevMatches& m, hipStream_t stream, std::string& err);
+
+  // After the pass: copies the match lists to host in (package, advisory) order.
+  // Returns false when the device buffer was too small (total > m.cap).
+  static bool fetch_ordered(const DevMatches& m, uint32_t n_pkgs, uint64_t total, std::vector<uint2>& out,
+                            std::string& err);
 
   // Convenience: upload, match, download. out = pairs; err_pkg = first poisoned package or -1.
   bool match_host(const HostBatch& hb, std::vector<uint2>& out, int64_t& err_pkg, std::string& err);
@@ -82,12 +97,10 @@ class Engine {
   std::vector<void*> allocs_;
   uint64_t table_bytes_ = 0;
   // per-launch scratch
-  unsigned long long* tile_words_ = nullptr;
-  uint64_t tile_cap_ = 0;
   uint64_t* spill_ = nullptr;
   uint64_t spill_cap_ = 0;
   std::mutex call_mu_;  // serialises host-synchronous calls sharing the scratch buffers
-  bool ensure_scratch(uint32_t n_tiles, uint64_t spill_words, std::string& err);
+  bool ensure_scratch(uint64_t spill_words, std::string& err);
 };
 
 constexpr int kTile = 256;         // packages per workgroup (one per lane)

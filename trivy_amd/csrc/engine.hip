@@ -45,26 +45,30 @@ struct MatchArgs {
   uint32_t n_tiles;
   uint2* out;
   uint64_t out_cap;
-  unsigned long long* tile_words;
+  TileDir* dir;
   unsigned long long* ctl;  // [0] total, [1] n - first poisoned, [2] spill used, [3] err bits, [4] ticket
   uint64_t* spill;
   uint64_t spill_cap;
 };
 
 enum : uint32_t { KI_VALID = 1u << 31, KI_SPILL = 1u << 30, KI_LEN = 0x3FFFu };
-enum : unsigned long long { LB_AGG = 1ull << 62, LB_PFX = 2ull << 62, LB_VAL = (1ull << 62) - 1 };
 
 struct TileShared {
   uint64_t key[kTile * kKeySlotWords];  // installed keys (16 KiB)
-  uint2 mbuf[kMBuf];                    // compacted matches (16 KiB)
+  union {
+    uint2 mbuf[kMBuf];                  // phase 3: compacted matches (16 KiB)
+    uint4 stage[kMBuf / 2];             // phase 1: the tile's name/version bytes
+  };
   uint32_t scan[kTile + 1];             // exclusive scan of row counts
   uint32_t rbeg[kTile];                 // first row per package
   uint32_t kinfo[kTile];                // key length | flags
   uint32_t koff[kTile];                 // spill word offset when KI_SPILL
   uint32_t wsum[kWaves];
   uint32_t tile;
+  uint32_t span_lo, span_hi;            // arena window of the tile's strings
   unsigned long long base;
 };
+constexpr uint32_t kStageBytes = kMBuf * 8;
 
 __device__ __forceinline__ bool name_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
   for (uint32_t i = 0; i < n; i++)
@@ -118,7 +122,7 @@ __device__ __forceinline__ bool eval_pair(const MatchArgs& a, TileShared& s, uin
     const uint32_t kl = ki & KI_LEN;
     m = true;
     if (!(row.hi_len & KEY_INF)) {
-      int c = key_cmp(k, kl, a.db.key_words + row.hi_off, row.hi_len & KEY_LEN_MASK);
+      int c = key_cmp_pre(k, kl, row.hi_pre0, row.hi_pre1, a.db.key_words + row.hi_off, row.hi_len & KEY_LEN_MASK);
       m = (row.hi_len & KEY_INCL) ? c <= 0 : c < 0;
     }
     if (m && !(row.lo_len & KEY_INF)) {
@@ -169,19 +173,54 @@ __device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared& s, uin
 __global__ __launch_bounds__(kTile) void match_kernel(MatchArgs a) {
   __shared__ TileShared s;
   const uint32_t tid = threadIdx.x;
-  if (tid == 0) s.tile = atomicAdd(reinterpret_cast<unsigned int*>(&a.ctl[4]), 1u);
+  if (tid == 0) {
+    s.tile = atomicAdd(reinterpret_cast<unsigned int*>(&a.ctl[4]), 1u);
+    s.span_lo = 0xFFFFFFFFu;
+    s.span_hi = 0;
+  }
   __syncthreads();
   const uint32_t tile = s.tile;
   const uint32_t p = tile * kTile + tid;
 
+  // ---- 0. stage the tile's name/version bytes in LDS (coalesced 16-byte loads) ------------
+  uint4 d = make_uint4(0xFFFFFFFFu, 0, 0, 0);
+  if (p < a.n) d = a.desc[p];
+  {
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+    if (p < a.n) {
+      lo = d.y < d.z ? d.y : d.z;
+      const uint32_t e1 = d.y + (d.w & 0xFFFFu), e2 = d.z + (d.w >> 16);
+      hi = e1 > e2 ? e1 : e2;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint32_t l2 = __shfl_xor(lo, o, 64), h2 = __shfl_xor(hi, o, 64);
+      lo = l2 < lo ? l2 : lo;
+      hi = h2 > hi ? h2 : hi;
+    }
+    if ((tid & 63) == 0) {
+      atomicMin(&s.span_lo, lo);
+      atomicMax(&s.span_hi, hi);
+    }
+  }
+  __syncthreads();
+  const uint32_t base16 = s.span_lo & ~15u;
+  const bool staged = s.span_hi > base16 && s.span_hi - base16 <= kStageBytes;
+  if (staged) {
+    const uint32_t nv = (s.span_hi - base16 + 15) / 16;
+    const uint4* src = reinterpret_cast<const uint4*>(a.arena + base16);
+    for (uint32_t i = tid; i < nv; i += kTile) s.stage[i] = src[i];
+  }
+  __syncthreads();
+  const uint8_t* strings = staged ? reinterpret_cast<const uint8_t*>(s.stage) - base16 : a.arena;
+
   // ---- 1. probe + encode -------------------------------------------------------------
   uint32_t cnt = 0, rbeg = 0, kinfo = 0, koff = 0;
   if (p < a.n) {
-    const uint4 d = a.desc[p];
     if (d.x < a.db.n_plats) {
       const PlatInfo pi = a.db.plats[d.x];
-      const uint8_t* name = a.arena + d.y;
-      const uint8_t* ver = a.arena + d.z;
+      const uint8_t* name = strings + d.y;
+      const uint8_t* ver = strings + d.z;
       const uint32_t nlen = d.w & 0xFFFFu, vlen = d.w >> 16;
       // installed version -> sort key (LDS slot, or spill for long versions)
       uint64_t* dst = &s.key[tid * kKeySlotWords];
@@ -214,9 +253,9 @@ __global__ __launch_bounds__(kTile) void match_kernel(MatchArgs a) {
         const uint64_t h = key_hash(d.x, name, nlen);
         for (uint64_t i = h & a.db.slot_mask;; i = (i + 1) & a.db.slot_mask) {
           const uint64_t sh = a.db.slot_hash[i];
+          const SlotVal sv = a.db.slot_val[i];  // issued with the hash: no dependent round trip
           if (sh == 0) break;
           if (sh != h) continue;
-          const SlotVal sv = a.db.slot_val[i];
           if ((sv.name_len & SLOT_LEN_MASK) != nlen || !name_eq(name, a.db.name_arena + sv.name_off, nlen)) continue;
           if (sv.name_len & SLOT_POISONED) {
             atomicMax(&a.ctl[1], (unsigned long long)(a.n - p));
@@ -239,34 +278,15 @@ __global__ __launch_bounds__(kTile) void match_kernel(MatchArgs a) {
   // ---- 3+4. pair loop with LDS compaction ------------------------------------------------
   const uint32_t nm = sweep<false>(a, s, total_pairs, tid, 0);
 
-  // ---- decoupled look-back for the tile's output offset ----------------------------------
+  // ---- reserve the tile's output segment (one atomic per tile, no inter-tile waiting) -----
   if (tid == 0) {
-    unsigned long long excl = 0;
-    if (tile == 0) {
-      __hip_atomic_store(&a.tile_words[0], LB_PFX | nm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(&a.tile_words[tile], LB_AGG | nm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int64_t j = int64_t(tile) - 1;
-      uint32_t spins = 0;
-      while (j >= 0) {
-        const unsigned long long w = __hip_atomic_load(&a.tile_words[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long st = w & ~LB_VAL;
-        if (st == 0) {
-          if (++spins > (1u << 24)) {  // predecessors hold earlier tickets and are running; bound anyway
-            atomicOr(&a.ctl[3], (unsigned long long)ERR_LOOKBACK);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        excl += w & LB_VAL;
-        if (st == LB_PFX) break;
-        j--;
-      }
-      __hip_atomic_store(&a.tile_words[tile], LB_PFX | (excl + nm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (tile == a.n_tiles - 1) a.ctl[0] = excl + nm;
-    s.base = excl;
+    const unsigned long long base = nm ? atomicAdd(&a.ctl[0], (unsigned long long)nm) : 0ull;
+    TileDir d;
+    d.base = base;
+    d.count = nm;
+    d.pad = 0;
+    a.dir[tile] = d;
+    s.base = base;
   }
   __syncthreads();
   const unsigned long long base = s.base;
@@ -314,9 +334,8 @@ void HostBatch::add(uint32_t plat, std::string_view name, std::string_view ver) 
 
 Engine::~Engine() {
   if (dev_ >= 0) hipSetDevice(dev_);
-  for (void* p : allocs_) hipFree(p);
-  if (tile_words_) hipFree(tile_words_);
-  if (spill_) hipFree(spill_);
+  for (void* p : allocs_) (void)hipFree(p);
+  if (spill_) (void)hipFree(spill_);
   if (stream_) hipStreamDestroy(stream_);
 }
 
@@ -360,14 +379,7 @@ Engine* Engine::open(const DB& db, int device, std::string& err) {
   return e;
 }
 
-bool Engine::ensure_scratch(uint32_t n_tiles, uint64_t spill_words, std::string& err) {
-  if (n_tiles > tile_cap_) {
-    if (tile_words_) hipFree(tile_words_);
-    tile_words_ = nullptr;
-    uint64_t cap = std::max<uint64_t>(n_tiles, 1024);
-    if (!hip_ok(hipMalloc(&tile_words_, cap * 8), "hipMalloc(tile words)", err)) return false;
-    tile_cap_ = cap;
-  }
+bool Engine::ensure_scratch(uint64_t spill_words, std::string& err) {
   if (spill_words > spill_cap_) {
     if (spill_) hipFree(spill_);
     spill_ = nullptr;
@@ -388,7 +400,8 @@ bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
     if (need > uint32_t(kKeySlotWords)) b.spill_words += need;
   }
   if (!hip_ok(hipMalloc(&b.desc, std::max<size_t>(hb.desc.size(), 1) * sizeof(uint4)), "hipMalloc(batch)", err)) return false;
-  if (!hip_ok(hipMalloc(&b.arena, std::max<size_t>(hb.arena.size(), 1)), "hipMalloc(batch arena)", err)) return false;
+  // +32 B tail: the kernel stages whole 16-byte lines of the arena into LDS
+  if (!hip_ok(hipMalloc(&b.arena, (hb.arena.size() + 32 + 15) & ~size_t(15)), "hipMalloc(batch arena)", err)) return false;
   if (!hb.desc.empty() &&
       !hip_ok(hipMemcpy(b.desc, hb.desc.data(), hb.desc.size() * sizeof(uint4), hipMemcpyHostToDevice), "H2D batch", err))
     return false;
@@ -405,28 +418,53 @@ void Engine::free_batch(DevBatch& b) {
   b = DevBatch{};
 }
 
-bool Engine::alloc_matches(uint64_t cap, DevMatches& m, std::string& err) {
-  hipSetDevice(dev_);
+bool Engine::alloc_matches(uint64_t cap, uint32_t n_pkgs, DevMatches& m, std::string& err) {
+  (void)hipSetDevice(dev_);
   m.cap = std::max<uint64_t>(cap, 1);
+  m.dir_cap = std::max<uint32_t>((n_pkgs + kTile - 1) / kTile, 1);
   if (!hip_ok(hipMalloc(&m.pairs, m.cap * sizeof(uint2)), "hipMalloc(matches)", err)) return false;
+  if (!hip_ok(hipMalloc(&m.dir, m.dir_cap * sizeof(TileDir)), "hipMalloc(tile dir)", err)) return false;
   if (!hip_ok(hipMalloc(&m.ctl, 8 * sizeof(unsigned long long)), "hipMalloc(ctl)", err)) return false;
   return true;
 }
 
 void Engine::free_matches(DevMatches& m) {
-  hipSetDevice(dev_);
-  if (m.pairs) hipFree(m.pairs);
-  if (m.ctl) hipFree(m.ctl);
+  (void)hipSetDevice(dev_);
+  if (m.pairs) (void)hipFree(m.pairs);
+  if (m.dir) (void)hipFree(m.dir);
+  if (m.ctl) (void)hipFree(m.ctl);
   m = DevMatches{};
 }
 
+bool Engine::fetch_ordered(const DevMatches& m, uint32_t n_pkgs, uint64_t total, std::vector<uint2>& out,
+                           std::string& err) {
+  out.clear();
+  if (total > m.cap) {
+    err = "match buffer too small";
+    return false;
+  }
+  const uint32_t n_tiles = (n_pkgs + kTile - 1) / kTile;
+  std::vector<TileDir> dir(n_tiles);
+  std::vector<uint2> raw(total);
+  if (n_tiles && !hip_ok(hipMemcpy(dir.data(), m.dir, n_tiles * sizeof(TileDir), hipMemcpyDeviceToHost), "D2H dir", err))
+    return false;
+  if (total && !hip_ok(hipMemcpy(raw.data(), m.pairs, total * sizeof(uint2), hipMemcpyDeviceToHost), "D2H matches", err))
+    return false;
+  out.reserve(total);
+  for (const TileDir& d : dir) out.insert(out.end(), raw.begin() + d.base, raw.begin() + d.base + d.count);
+  return true;
+}
+
 bool Engine::launch(const DevBatch& b, const DevMatches& m, hipStream_t st, std::string& err) {
-  hipSetDevice(dev_);
+  (void)hipSetDevice(dev_);
   const uint32_t n_tiles = (b.n + kTile - 1) / kTile;
-  if (!ensure_scratch(n_tiles, b.spill_words, err)) return false;
+  if (n_tiles > m.dir_cap) {
+    err = "tile directory smaller than the batch";
+    return false;
+  }
+  if (!ensure_scratch(b.spill_words, err)) return false;
   if (!hip_ok(hipMemsetAsync(m.ctl, 0, 8 * sizeof(unsigned long long), st), "memset(ctl)", err)) return false;
   if (n_tiles == 0) return true;
-  if (!hip_ok(hipMemsetAsync(tile_words_, 0, uint64_t(n_tiles) * 8, st), "memset(tiles)", err)) return false;
   MatchArgs a;
   a.db = d_;
   a.desc = b.desc;
@@ -435,7 +473,7 @@ bool Engine::launch(const DevBatch& b, const DevMatches& m, hipStream_t st, std:
   a.n_tiles = n_tiles;
   a.out = m.pairs;
   a.out_cap = m.cap;
-  a.tile_words = tile_words_;
+  a.dir = m.dir;
   a.ctl = m.ctl;
   a.spill = spill_;
   a.spill_cap = spill_cap_;
@@ -454,7 +492,7 @@ bool Engine::match_host(const HostBatch& hb, std::vector<uint2>& out, int64_t& e
   bool ok = true;
   for (int attempt = 0; attempt < 2 && ok; attempt++) {
     DevMatches m;
-    ok = alloc_matches(cap, m, err) && launch(b, m, stream_, err) &&
+    ok = alloc_matches(cap, b.n, m, err) && launch(b, m, stream_, err) &&
          hip_ok(hipStreamSynchronize(stream_), "match_kernel", err);
     unsigned long long ctl[8] = {0};
     if (ok) ok = hip_ok(hipMemcpy(ctl, m.ctl, sizeof(ctl), hipMemcpyDeviceToHost), "D2H ctl", err);
@@ -466,8 +504,7 @@ bool Engine::match_host(const HostBatch& hb, std::vector<uint2>& out, int64_t& e
     }
     if (ok) {
       err_pkg = ctl[1] ? int64_t(b.n - ctl[1]) : -1;
-      out.resize(ctl[0]);
-      if (!out.empty()) ok = hip_ok(hipMemcpy(out.data(), m.pairs, out.size() * sizeof(uint2), hipMemcpyDeviceToHost), "D2H matches", err);
+      ok = fetch_ordered(m, b.n, ctl[0], out, err);
     }
     free_matches(m);
     break;
