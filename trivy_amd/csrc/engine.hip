@@ -212,15 +212,17 @@ __global__ __launch_bounds__(kTile) void match_kernel(MatchArgs a) {
     for (uint32_t i = tid; i < nv; i += kTile) s.stage[i] = src[i];
   }
   __syncthreads();
-  const uint8_t* strings = staged ? reinterpret_cast<const uint8_t*>(s.stage) - base16 : a.arena;
+  // Rebase offsets as integers: an LDS pointer minus a large arena offset would wrap the
+  // 32-bit LDS address before its conversion to a flat pointer.
+  const uint8_t* stage_bytes = reinterpret_cast<const uint8_t*>(s.stage);
 
   // ---- 1. probe + encode -------------------------------------------------------------
   uint32_t cnt = 0, rbeg = 0, kinfo = 0, koff = 0;
   if (p < a.n) {
     if (d.x < a.db.n_plats) {
       const PlatInfo pi = a.db.plats[d.x];
-      const uint8_t* name = strings + d.y;
-      const uint8_t* ver = strings + d.z;
+      const uint8_t* name = staged ? stage_bytes + (d.y - base16) : a.arena + d.y;
+      const uint8_t* ver = staged ? stage_bytes + (d.z - base16) : a.arena + d.z;
       const uint32_t nlen = d.w & 0xFFFFu, vlen = d.w >> 16;
       // installed version -> sort key (LDS slot, or spill for long versions)
       uint64_t* dst = &s.key[tid * kKeySlotWords];
