@@ -23,6 +23,16 @@ def build_engine(sdb, poison=()):
 
 
 def run_batch(eng, sdb, batch, cap=None):
+    """Runs one match pass; with cap=None the match buffer is re-sized to the exact total."""
+    if cap is None:
+        r = _run_batch(eng, sdb, batch, max(1024, 8 * len(batch)))
+        if r[0] is not None:
+            return r
+        cap = r[3]
+    return _run_batch(eng, sdb, batch, cap, strict=True)
+
+
+def _run_batch(eng, sdb, batch, cap, strict=False):
     from trivy_amd._lib import lib, errbuf
     L = lib()
     b = L.tvm_batch_new()
@@ -34,7 +44,7 @@ def run_batch(eng, sdb, batch, cap=None):
                                          voff[b0:].ctypes.data, vlen[b0:].ctypes.data)
             assert first == b0
         e = errbuf()
-        assert L.tvm_batch_upload(eng.h, b, cap or max(1024, 8 * len(batch)), e, len(e)) == 0, e.value
+        assert L.tvm_batch_upload(eng.h, b, cap, e, len(e)) == 0, e.value
         assert L.tvm_match_launch(eng.h, b, e, len(e)) == 0, e.value
         assert L.tvm_engine_sync(eng.h, e, len(e)) == 0, e.value
         n, errp, bits = ctypes.c_uint64(), ctypes.c_int64(), ctypes.c_uint64()
@@ -43,7 +53,7 @@ def run_batch(eng, sdb, batch, cap=None):
         out = np.zeros(2 * max(n.value, 1), dtype=np.uint32)
         got = ctypes.c_uint64()
         rc = L.tvm_match_fetch(eng.h, b, out.ctypes.data, n.value, ctypes.byref(got))
-        if cap is not None and n.value > cap:
+        if n.value > cap:
             assert rc != 0 and got.value == 0  # overflow is reported, never silently truncated
             return None, None, errp.value, n.value
         assert rc == 0
