@@ -121,6 +121,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify the bench batch against the oracle")
+    ap.add_argument("--variant", type=int, default=None, help="match-kernel variant (tvm_engine_set_variant)")
+    ap.add_argument("--sweep", type=int, default=0,
+                    help="time every kernel variant over N interleaved rounds (stderr table) before the bench")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -172,6 +175,27 @@ def main():
 
     # ---- warmup + timed region -------------------------------------------------------------
     from trivy_amd._lib import lib, errbuf
+    if args.sweep and rank == 0:
+        names, v = [], 0
+        while lib().tvm_variant_name(v):
+            names.append(lib().tvm_variant_name(v).decode())
+            v += 1
+        times = {n: [] for n in names}
+        for _ in range(args.sweep):
+            for v, n in enumerate(names):
+                lib().tvm_engine_set_variant(eng.h, v)
+                launch(eng, b, 2)
+                ms = ctypes.c_double()
+                e = errbuf()
+                lib().tvm_match_time(eng.h, b, 10, ctypes.byref(ms), e, len(e))
+                times[n].append(ms.value / 10)
+                if status(eng, b) != (total, -1, 0):
+                    raise RuntimeError(f"variant {n} disagrees on the match count")
+        for n in names:
+            t = sorted(times[n])
+            log(rank, f"[sweep] {n:>16}: median {t[len(t)//2]:.4f} ms  min {t[0]:.4f} ms per pass")
+    if args.variant is not None:
+        lib().tvm_engine_set_variant(eng.h, args.variant)
     launch(eng, b, args.warmup)
 
     def barrier():
@@ -229,6 +253,7 @@ def main():
             "dtype": "u8",
             "data": "synthetic (seeded trivy-db + SBOM batch, tools/synth.py)",
             "config": {"workload": cfg_name, "packages_per_gpu": n_pkgs, "matches_per_gpu": total,
+                       "kernel_variant": lib().tvm_variant_name(lib().tvm_engine_set_variant(eng.h, -1)).decode(),
                        "db_keys": len(sdb.key_names), "db_advisories": sdb.n_adv,
                        "platforms": PLATS, "parallelism": f"replicated tables, batch sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -135,6 +135,10 @@ void tvm_engine_close(tvm_engine* e);
 /* Atomically replaces the engine's tables (waits for in-flight calls; server hot update). */
 int tvm_engine_swap(tvm_engine* e, tvm_db* db, char* err, size_t errlen);
 uint64_t tvm_engine_table_bytes(const tvm_engine* e);
+/* Tuning knob: selects the match-kernel variant (tile size / LDS budget); returns the
+ * previous one.  v < 0 only queries.  Names via tvm_variant_name (NULL past the last). */
+int tvm_engine_set_variant(tvm_engine* e, int v);
+const char* tvm_variant_name(int v);
 
 /* ---- ospkg ------------------------------------------------------------------------------ */
 /* ospkg.Detect: family = ftypes.OSType ("debian", "ubuntu", ...); now_unix = clock.Now(ctx).

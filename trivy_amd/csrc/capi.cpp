@@ -218,6 +218,14 @@ int tvm_engine_swap(tvm_engine* e, tvm_db* db, char* err, size_t errlen) {
 
 uint64_t tvm_engine_table_bytes(const tvm_engine* e) { return e ? e->eng->table_bytes() : 0; }
 
+int tvm_engine_set_variant(tvm_engine* e, int v) {
+  if (!e) return -1;
+  std::unique_lock<std::shared_mutex> lk(e->mu);
+  return v < 0 ? e->eng->variant() : e->eng->set_variant(v);
+}
+
+const char* tvm_variant_name(int v) { return variant_name(v); }
+
 static int detect_common(tvm_engine* e, bool full, const char* fam, const char* ver, const tvm_repository* repo,
                          const tvm_package* pkgs, size_t n, int64_t now, tvm_result* out, char* err,
                          size_t errlen) {

@@ -86,11 +86,16 @@ class Engine {
   // Convenience: upload, match, download. out = pairs; err_pkg = first poisoned package or -1.
   bool match_host(const HostBatch& hb, std::vector<uint2>& out, int64_t& err_pkg, std::string& err);
 
-  // Algorithmic bytes of one pass over `hb` (roofline numerator).
   const DB& db() const { return *db_; }
+
+  // Kernel variant (tile size / LDS budget); returns the previous one.  Default 0,
+  // overridable with the TVM_VARIANT environment variable at open().
+  int set_variant(int v);
+  int variant() const { return variant_; }
 
  private:
   int dev_ = 0;
+  int variant_ = 0;
   hipStream_t stream_ = nullptr;
   const DB* db_ = nullptr;
   DevDB d_;
@@ -103,7 +108,8 @@ class Engine {
   bool ensure_scratch(uint64_t spill_words, std::string& err);
 };
 
-constexpr int kTile = 256;         // packages per workgroup (one per lane)
-constexpr int kKeySlotWords = 8;   // LDS bytes per installed key = 64
+// Kernel variants: count and names (engine.hip kVariants).
+int num_variants();
+const char* variant_name(int v);
 
 }  // namespace tvm

@@ -3,28 +3,32 @@
 // Replaces the per-package loops of the reference drivers (e.g.
 // pkg/detector/ospkg/debian/debian.go:65-117, ubuntu/ubuntu.go:86-126,
 // library/driver.go:111-137) with one launch over a whole batch of packages from
-// many targets.  One workgroup (4 waves) owns a tile of 256 consecutive packages:
+// many targets.  One workgroup owns a tile of T consecutive packages (one per lane):
 //
+//   0. stage: the tile's name/version bytes (one contiguous arena window) are copied
+//      into LDS with coalesced 16-byte loads, so the byte-serial hashing/parsing below
+//      runs on LDS latency instead of global latency;
 //   1. probe+encode (lane per package): hash (platform, name), linear-probe the
-//      open-addressing index, verify the name bytes, and encode the installed
-//      version into its sort key in LDS (verkey.h, the same code the flattener ran
-//      on the advisory side at load time);
+//      open-addressing index (slot hash and value loaded together), verify the name
+//      bytes, and encode the installed version into its sort key in LDS (verkey.h, the
+//      same code the flattener ran on the advisory side at load time);
 //   2. block exclusive scan of the per-package row counts (wave shuffles + LDS);
-//   3. pair loop: the tile's (package, row) pairs are dealt 256 at a time to the
-//      lanes (binary search of the LDS scan maps pair -> package), each pair is one
-//      interval test = one or two word-wise key compares; a Zipf-heavy key simply
-//      makes its tile loop longer, never a single lane;
-//   4. ballot/popcount compaction into an LDS match buffer, then a decoupled
-//      look-back across tiles (dynamic tile tickets, one 64-bit {status, value}
-//      word per tile, agent-scope relaxed atomics) gives the tile's global output
-//      offset, so the match list comes out in (package, row) order with no second
-//      pass and no host round trip.
+//   3. pair sweep: the tile's (package, row) pairs are dealt T at a time to the lanes
+//      (binary search of the LDS scan maps pair -> package); each pair is one interval
+//      test against a 32-byte row whose first 16 key bytes are inline, so most pairs
+//      cost one row load; the next chunk's row is loaded before the current one is
+//      tested (software pipelining); a Zipf-heavy key makes its tile loop longer, never
+//      a single lane;
+//   4. ballot/popcount compaction into an LDS match buffer, then one atomic reservation
+//      per tile and a tile directory entry: the per-package advisory lists come out in
+//      (package, row) order within each tile segment with no inter-tile waiting.
 //
-// All arithmetic is integer/byte; the kernel is bound by HBM/L2 traffic (rows,
-// keys, descriptors and strings), never by ALU.
+// All arithmetic is integer/byte; the kernel is bound by memory latency/traffic
+// (rows, keys, descriptors, strings), never by ALU.
 #include "engine.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "db.h"
@@ -33,9 +37,6 @@
 namespace tvm {
 
 namespace {
-
-constexpr int kWaves = kTile / 64;
-constexpr int kMBuf = 2048;  // LDS match buffer (uint2 entries) per tile
 
 struct MatchArgs {
   DevDB db;
@@ -46,29 +47,29 @@ struct MatchArgs {
   uint2* out;
   uint64_t out_cap;
   TileDir* dir;
-  unsigned long long* ctl;  // [0] total, [1] n - first poisoned, [2] spill used, [3] err bits, [4] ticket
+  unsigned long long* ctl;  // [0] total, [1] n - first poisoned, [2] spill used, [3] err bits, [4] ticket, [5] tile size
   uint64_t* spill;
   uint64_t spill_cap;
 };
 
 enum : uint32_t { KI_VALID = 1u << 31, KI_SPILL = 1u << 30, KI_LEN = 0x3FFFu };
 
+template <int T, int KW, int MB>
 struct TileShared {
-  uint64_t key[kTile * kKeySlotWords];  // installed keys (16 KiB)
+  uint64_t key[T * KW];       // installed keys
   union {
-    uint2 mbuf[kMBuf];                  // phase 3: compacted matches (16 KiB)
-    uint4 stage[kMBuf / 2];             // phase 1: the tile's name/version bytes
+    uint2 mbuf[MB];           // phase 3: compacted matches
+    uint4 stage[MB / 2];      // phase 0/1: the tile's name/version bytes
   };
-  uint32_t scan[kTile + 1];             // exclusive scan of row counts
-  uint32_t rbeg[kTile];                 // first row per package
-  uint32_t kinfo[kTile];                // key length | flags
-  uint32_t koff[kTile];                 // spill word offset when KI_SPILL
-  uint32_t wsum[kWaves];
+  uint32_t scan[T + 1];       // exclusive scan of row counts
+  uint32_t rbeg[T];           // first row per package
+  uint32_t kinfo[T];          // key length | flags
+  uint32_t koff[T];           // spill word offset when KI_SPILL
+  uint32_t wsum[T / 64];
   uint32_t tile;
-  uint32_t span_lo, span_hi;            // arena window of the tile's strings
+  uint32_t span_lo, span_hi;  // arena window of the tile's strings
   unsigned long long base;
 };
-constexpr uint32_t kStageBytes = kMBuf * 8;
 
 __device__ __forceinline__ bool name_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
   for (uint32_t i = 0; i < n; i++)
@@ -76,8 +77,10 @@ __device__ __forceinline__ bool name_eq(const uint8_t* a, const uint8_t* b, uint
   return true;
 }
 
-// Block-wide exclusive scan of v over kTile lanes; returns the block total.
-__device__ __forceinline__ uint32_t block_scan(TileShared& s, uint32_t v, uint32_t tid) {
+// Block-wide exclusive scan of v over T lanes; returns the block total.
+template <int T, class S>
+__device__ __forceinline__ uint32_t block_scan(S& s, uint32_t v, uint32_t tid) {
+  constexpr int W = T / 64;
   const uint32_t lane = tid & 63, wave = tid >> 6;
   uint32_t x = v;
 #pragma unroll
@@ -89,100 +92,118 @@ __device__ __forceinline__ uint32_t block_scan(TileShared& s, uint32_t v, uint32
   __syncthreads();
   uint32_t off = 0, tot = 0;
 #pragma unroll
-  for (int w = 0; w < kWaves; w++) {
+  for (int w = 0; w < W; w++) {
     uint32_t t = s.wsum[w];
     off += (uint32_t(w) < wave) ? t : 0;
     tot += t;
   }
   s.scan[tid] = off + x - v;
-  if (tid == 0) s.scan[kTile] = tot;
+  if (tid == 0) s.scan[T] = tot;
   __syncthreads();
   return tot;
 }
 
-// Evaluates pair j of the tile; returns true and fills rec when it matches.
-__device__ __forceinline__ bool eval_pair(const MatchArgs& a, TileShared& s, uint32_t j, uint2& rec) {
-  // q = last package with scan[q] <= j (its count is > 0 because j < scan[q + 1])
-  uint32_t lo = 0, hi = kTile;  // invariant: scan[lo] <= j < scan[hi]
+// Package of pair j: the last q with scan[q] <= j (its count is > 0 since j < scan[q + 1]).
+template <int T, class S>
+__device__ __forceinline__ uint32_t pair_pkg(const S& s, uint32_t j) {
+  uint32_t lo = 0, hi = T;  // invariant: scan[lo] <= j < scan[hi]
   while (hi - lo > 1) {
-    uint32_t mid = (lo + hi) >> 1;
+    const uint32_t mid = (lo + hi) >> 1;
     if (s.scan[mid] <= j) lo = mid;
     else hi = mid;
   }
-  const uint32_t q = lo;
-  const Row row = a.db.rows[s.rbeg[q] + (j - s.scan[q])];
+  return lo;
+}
+
+// Interval test of package q's installed key against one row.
+template <int KW, class S>
+__device__ __forceinline__ bool eval_row(const MatchArgs& a, const S& s, uint32_t q, const Row& row) {
+  if (row.adv & ROW_ALWAYS) return true;
   const uint32_t ki = s.kinfo[q];
-  bool m;
-  if (row.adv & ROW_ALWAYS) {
-    m = true;
-  } else if (!(ki & KI_VALID)) {
-    m = false;
-  } else {
-    const uint64_t* k = (ki & KI_SPILL) ? a.spill + s.koff[q] : &s.key[q * kKeySlotWords];
-    const uint32_t kl = ki & KI_LEN;
-    m = true;
-    if (!(row.hi_len & KEY_INF)) {
-      int c = key_cmp_pre(k, kl, row.hi_pre0, row.hi_pre1, a.db.key_words + row.hi_off, row.hi_len & KEY_LEN_MASK);
-      m = (row.hi_len & KEY_INCL) ? c <= 0 : c < 0;
-    }
-    if (m && !(row.lo_len & KEY_INF)) {
-      int c = key_cmp(k, kl, a.db.key_words + row.lo_off, row.lo_len & KEY_LEN_MASK);
-      m = (row.lo_len & KEY_INCL) ? c >= 0 : c > 0;
-    }
+  if (!(ki & KI_VALID)) return false;
+  const uint64_t* k = (ki & KI_SPILL) ? a.spill + s.koff[q] : &s.key[q * KW];
+  const uint32_t kl = ki & KI_LEN;
+  bool m = true;
+  if (!(row.hi_len & KEY_INF)) {
+    const int c = key_cmp_pre(k, kl, row.hi_pre0, row.hi_pre1, a.db.key_words + row.hi_off, row.hi_len & KEY_LEN_MASK);
+    m = (row.hi_len & KEY_INCL) ? c <= 0 : c < 0;
   }
-  rec = make_uint2(s.tile * kTile + q, row.adv & ROW_ADV_MASK);
+  if (m && !(row.lo_len & KEY_INF)) {
+    const int c = key_cmp(k, kl, a.db.key_words + row.lo_off, row.lo_len & KEY_LEN_MASK);
+    m = (row.lo_len & KEY_INCL) ? c >= 0 : c > 0;
+  }
   return m;
 }
 
-// One sweep over the tile's pairs.  DIRECT=false: compact into LDS (count all, store
-// the first kMBuf).  DIRECT=true: store straight to out[base + position].
-template <bool DIRECT>
-__device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared& s, uint32_t total_pairs,
+// One sweep over the tile's pairs.  DIRECT=false: compact into LDS (count all, store the
+// first MB).  DIRECT=true: store straight to out[base + position].
+template <int T, int KW, int MB, bool DIRECT>
+__device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared<T, KW, MB>& s, uint32_t total_pairs,
                                           uint32_t tid, unsigned long long base) {
+  constexpr int W = T / 64;
   const uint32_t lane = tid & 63, wave = tid >> 6;
   uint32_t nm = 0;
-  for (uint32_t b0 = 0; b0 < total_pairs; b0 += kTile) {
-    const uint32_t j = b0 + tid;
-    uint2 rec = make_uint2(0, 0);
-    const bool m = (j < total_pairs) && eval_pair(a, s, j, rec);
+  uint32_t j = tid, q = 0;
+  Row row{};
+  if (j < total_pairs) {
+    q = pair_pkg<T>(s, j);
+    row = a.db.rows[s.rbeg[q] + (j - s.scan[q])];
+  }
+  for (uint32_t b0 = 0; b0 < total_pairs; b0 += T) {
+    // issue the next chunk's row load before testing this chunk's pair
+    const uint32_t jn = j + T;
+    uint32_t qn = 0;
+    Row rown{};
+    if (jn < total_pairs) {
+      qn = pair_pkg<T>(s, jn);
+      rown = a.db.rows[s.rbeg[qn] + (jn - s.scan[qn])];
+    }
+    const bool m = (j < total_pairs) && eval_row<KW>(a, s, q, row);
     const unsigned long long bal = __ballot(m);
     const uint32_t lane_off = __popcll(bal & ((1ull << lane) - 1ull));
     if (lane == 0) s.wsum[wave] = uint32_t(__popcll(bal));
     __syncthreads();
     uint32_t woff = 0, ctot = 0;
 #pragma unroll
-    for (int w = 0; w < kWaves; w++) {
-      uint32_t t = s.wsum[w];
+    for (int w = 0; w < W; w++) {
+      const uint32_t t = s.wsum[w];
       woff += (uint32_t(w) < wave) ? t : 0;
       ctot += t;
     }
     const uint32_t pos = nm + woff + lane_off;
     if (m) {
+      const uint2 rec = make_uint2(s.tile * T + q, row.adv & ROW_ADV_MASK);
       if (DIRECT) {
         if (base + pos < a.out_cap) a.out[base + pos] = rec;
-      } else if (pos < uint32_t(kMBuf)) {
+      } else if (pos < uint32_t(MB)) {
         s.mbuf[pos] = rec;
       }
     }
     nm += ctot;
     __syncthreads();
+    j = jn;
+    q = qn;
+    row = rown;
   }
   return nm;
 }
 
-__global__ __launch_bounds__(kTile) void match_kernel(MatchArgs a) {
-  __shared__ TileShared s;
+template <int T, int KW, int MB>
+__global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
+  __shared__ TileShared<T, KW, MB> s;
+  constexpr uint32_t kStageBytes = MB * 8;
   const uint32_t tid = threadIdx.x;
   if (tid == 0) {
     s.tile = atomicAdd(reinterpret_cast<unsigned int*>(&a.ctl[4]), 1u);
     s.span_lo = 0xFFFFFFFFu;
     s.span_hi = 0;
+    if (blockIdx.x == 0) a.ctl[5] = T;
   }
   __syncthreads();
   const uint32_t tile = s.tile;
-  const uint32_t p = tile * kTile + tid;
+  const uint32_t p = tile * T + tid;
 
-  // ---- 0. stage the tile's name/version bytes in LDS (coalesced 16-byte loads) ------------
+  // ---- 0. stage the tile's name/version bytes in LDS (coalesced 16-byte loads) ---------
   uint4 d = make_uint4(0xFFFFFFFFu, 0, 0, 0);
   if (p < a.n) d = a.desc[p];
   {
@@ -209,7 +230,7 @@ __global__ __launch_bounds__(kTile) void match_kernel(MatchArgs a) {
   if (staged) {
     const uint32_t nv = (s.span_hi - base16 + 15) / 16;
     const uint4* src = reinterpret_cast<const uint4*>(a.arena + base16);
-    for (uint32_t i = tid; i < nv; i += kTile) s.stage[i] = src[i];
+    for (uint32_t i = tid; i < nv; i += T) s.stage[i] = src[i];
   }
   __syncthreads();
   // Rebase offsets as integers: an LDS pointer minus a large arena offset would wrap the
@@ -218,55 +239,53 @@ __global__ __launch_bounds__(kTile) void match_kernel(MatchArgs a) {
 
   // ---- 1. probe + encode -------------------------------------------------------------
   uint32_t cnt = 0, rbeg = 0, kinfo = 0, koff = 0;
-  if (p < a.n) {
-    if (d.x < a.db.n_plats) {
-      const PlatInfo pi = a.db.plats[d.x];
-      const uint8_t* name = staged ? stage_bytes + (d.y - base16) : a.arena + d.y;
-      const uint8_t* ver = staged ? stage_bytes + (d.z - base16) : a.arena + d.z;
-      const uint32_t nlen = d.w & 0xFFFFu, vlen = d.w >> 16;
-      // installed version -> sort key (LDS slot, or spill for long versions)
-      uint64_t* dst = &s.key[tid * kKeySlotWords];
-      uint32_t need = 0;
-      if ((key_bound(vlen) + 7) / 8 > uint32_t(kKeySlotWords)) {  // might not fit: size it exactly
-        CountSink cs;
-        need = encode_version(pi.cmp, ver, vlen, cs) ? (cs.n + 7) / 8 : 0;
+  if (p < a.n && d.x < a.db.n_plats) {
+    const PlatInfo pi = a.db.plats[d.x];
+    const uint8_t* name = staged ? stage_bytes + (d.y - base16) : a.arena + d.y;
+    const uint8_t* ver = staged ? stage_bytes + (d.z - base16) : a.arena + d.z;
+    const uint32_t nlen = d.w & 0xFFFFu, vlen = d.w >> 16;
+    // installed version -> sort key (LDS slot, or global spill for long versions)
+    uint64_t* dst = &s.key[tid * KW];
+    uint32_t need = 0;
+    if ((key_bound(vlen) + 7) / 8 > uint32_t(KW)) {  // might not fit: size it exactly
+      CountSink cs;
+      need = encode_version(pi.cmp, ver, vlen, cs) ? (cs.n + 7) / 8 : 0;
+    }
+    bool spill_ok = true;
+    if (need > uint32_t(KW)) {
+      const unsigned long long o = atomicAdd(&a.ctl[2], (unsigned long long)need);
+      if (o + need > a.spill_cap) {
+        atomicOr(&a.ctl[3], (unsigned long long)ERR_SPILL);
+        spill_ok = false;
+      } else {
+        dst = a.spill + o;
+        koff = uint32_t(o);
+        kinfo |= KI_SPILL;
       }
-      bool spill_ok = true;
-      if (need > uint32_t(kKeySlotWords)) {
-        unsigned long long o = atomicAdd(&a.ctl[2], (unsigned long long)need);
-        if (o + need > a.spill_cap) {
-          atomicOr(&a.ctl[3], (unsigned long long)ERR_SPILL);
-          spill_ok = false;
-        } else {
-          dst = a.spill + o;
-          koff = uint32_t(o);
-          kinfo |= KI_SPILL;
+    }
+    bool valid = false;
+    if (spill_ok) {
+      WordSink ws(dst);
+      valid = encode_version(pi.cmp, ver, vlen, ws);
+      ws.flush();
+      kinfo |= (ws.n & KI_LEN) | (valid ? KI_VALID : 0u);
+    }
+    // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup
+    if (valid || (pi.flags & PLAT_LOOKUP_FIRST)) {
+      const uint64_t h = key_hash(d.x, name, nlen);
+      for (uint64_t i = h & a.db.slot_mask;; i = (i + 1) & a.db.slot_mask) {
+        const uint64_t sh = a.db.slot_hash[i];
+        const SlotVal sv = a.db.slot_val[i];  // issued with the hash: no dependent round trip
+        if (sh == 0) break;
+        if (sh != h) continue;
+        if ((sv.name_len & SLOT_LEN_MASK) != nlen || !name_eq(name, a.db.name_arena + sv.name_off, nlen)) continue;
+        if (sv.name_len & SLOT_POISONED) {
+          atomicMax(&a.ctl[1], (unsigned long long)(a.n - p));
+        } else if (valid) {
+          cnt = sv.row_count;
+          rbeg = sv.row_begin;
         }
-      }
-      bool valid = false;
-      if (spill_ok) {
-        WordSink ws(dst);
-        valid = encode_version(pi.cmp, ver, vlen, ws);
-        ws.flush();
-        kinfo |= (ws.n & KI_LEN) | (valid ? KI_VALID : 0u);
-      }
-      // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup
-      if (valid || (pi.flags & PLAT_LOOKUP_FIRST)) {
-        const uint64_t h = key_hash(d.x, name, nlen);
-        for (uint64_t i = h & a.db.slot_mask;; i = (i + 1) & a.db.slot_mask) {
-          const uint64_t sh = a.db.slot_hash[i];
-          const SlotVal sv = a.db.slot_val[i];  // issued with the hash: no dependent round trip
-          if (sh == 0) break;
-          if (sh != h) continue;
-          if ((sv.name_len & SLOT_LEN_MASK) != nlen || !name_eq(name, a.db.name_arena + sv.name_off, nlen)) continue;
-          if (sv.name_len & SLOT_POISONED) {
-            atomicMax(&a.ctl[1], (unsigned long long)(a.n - p));
-          } else if (valid) {
-            cnt = sv.row_count;
-            rbeg = sv.row_begin;
-          }
-          break;
-        }
+        break;
       }
     }
   }
@@ -275,32 +294,55 @@ __global__ __launch_bounds__(kTile) void match_kernel(MatchArgs a) {
   s.koff[tid] = koff;
 
   // ---- 2. scan of row counts ------------------------------------------------------------
-  const uint32_t total_pairs = block_scan(s, cnt, tid);
+  const uint32_t total_pairs = block_scan<T>(s, cnt, tid);
 
-  // ---- 3+4. pair loop with LDS compaction ------------------------------------------------
-  const uint32_t nm = sweep<false>(a, s, total_pairs, tid, 0);
+  // ---- 3+4. pair sweep with LDS compaction -----------------------------------------------
+  const uint32_t nm = sweep<T, KW, MB, false>(a, s, total_pairs, tid, 0);
 
   // ---- reserve the tile's output segment (one atomic per tile, no inter-tile waiting) -----
   if (tid == 0) {
     const unsigned long long base = nm ? atomicAdd(&a.ctl[0], (unsigned long long)nm) : 0ull;
-    TileDir d;
-    d.base = base;
-    d.count = nm;
-    d.pad = 0;
-    a.dir[tile] = d;
+    TileDir e;
+    e.base = base;
+    e.count = nm;
+    e.pad = 0;
+    a.dir[tile] = e;
     s.base = base;
   }
   __syncthreads();
   const unsigned long long base = s.base;
 
   // ---- 5. store the tile's matches -------------------------------------------------------
-  if (nm <= uint32_t(kMBuf)) {
-    for (uint32_t i = tid; i < nm; i += kTile)
+  if (nm <= uint32_t(MB)) {
+    for (uint32_t i = tid; i < nm; i += T)
       if (base + i < a.out_cap) a.out[base + i] = s.mbuf[i];
   } else {
-    sweep<true>(a, s, total_pairs, tid, base);  // rare: more matches than the LDS buffer
+    sweep<T, KW, MB, true>(a, s, total_pairs, tid, base);  // rare: more matches than the LDS buffer
   }
 }
+
+// Kernel variants (tile packages T, LDS key words KW, LDS match entries MB).
+struct VariantInfo {
+  int tile;
+  void (*launch)(uint32_t n_tiles, hipStream_t st, const MatchArgs& a);
+  const char* name;
+};
+
+template <int T, int KW, int MB>
+void launch_variant(uint32_t n_tiles, hipStream_t st, const MatchArgs& a) {
+  hipLaunchKernelGGL((match_kernel<T, KW, MB>), dim3(n_tiles), dim3(T), 0, st, a);
+}
+
+const VariantInfo kVariants[] = {
+    {256, launch_variant<256, 8, 2048>, "t256_k64_m2048"},
+    {256, launch_variant<256, 4, 2048>, "t256_k32_m2048"},
+    {128, launch_variant<128, 4, 1024>, "t128_k32_m1024"},
+    {64, launch_variant<64, 4, 512>, "t64_k32_m512"},
+    {128, launch_variant<128, 4, 2048>, "t128_k32_m2048"},
+};
+constexpr int kNumVariants = int(sizeof(kVariants) / sizeof(kVariants[0]));
+constexpr int kMinTile = 64;
+constexpr int kMinKeyWords = 4;
 
 bool hip_ok(hipError_t e, const char* what, std::string& err) {
   if (e == hipSuccess) return true;
@@ -323,6 +365,9 @@ bool upload_vec(const std::vector<T>& v, T** dst, std::vector<void*>& allocs, ui
 
 }  // namespace
 
+int num_variants() { return kNumVariants; }
+const char* variant_name(int v) { return v >= 0 && v < kNumVariants ? kVariants[v].name : nullptr; }
+
 void HostBatch::add(uint32_t plat, std::string_view name, std::string_view ver) {
   uint4 d;
   d.x = plat;
@@ -335,10 +380,10 @@ void HostBatch::add(uint32_t plat, std::string_view name, std::string_view ver) 
 }
 
 Engine::~Engine() {
-  if (dev_ >= 0) hipSetDevice(dev_);
+  if (dev_ >= 0) (void)hipSetDevice(dev_);
   for (void* p : allocs_) (void)hipFree(p);
   if (spill_) (void)hipFree(spill_);
-  if (stream_) hipStreamDestroy(stream_);
+  if (stream_) (void)hipStreamDestroy(stream_);
 }
 
 Engine* Engine::open(const DB& db, int device, std::string& err) {
@@ -354,6 +399,7 @@ Engine* Engine::open(const DB& db, int device, std::string& err) {
   Engine* e = new Engine();
   e->dev_ = device;
   e->db_ = &db;
+  if (const char* v = std::getenv("TVM_VARIANT")) e->set_variant(std::atoi(v));
   if (!hip_ok(hipSetDevice(device), "hipSetDevice", err) ||
       !hip_ok(hipStreamCreateWithFlags(&e->stream_, hipStreamNonBlocking), "hipStreamCreate", err)) {
     delete e;
@@ -381,11 +427,17 @@ Engine* Engine::open(const DB& db, int device, std::string& err) {
   return e;
 }
 
+int Engine::set_variant(int v) {
+  const int old = variant_;
+  if (v >= 0 && v < kNumVariants) variant_ = v;
+  return old;
+}
+
 bool Engine::ensure_scratch(uint64_t spill_words, std::string& err) {
   if (spill_words > spill_cap_) {
-    if (spill_) hipFree(spill_);
+    if (spill_) (void)hipFree(spill_);
     spill_ = nullptr;
-    uint64_t cap = std::max<uint64_t>(spill_words, 4096);
+    const uint64_t cap = std::max<uint64_t>(spill_words, 4096);
     if (!hip_ok(hipMalloc(&spill_, cap * 8), "hipMalloc(spill)", err)) return false;
     spill_cap_ = cap;
   }
@@ -393,13 +445,13 @@ bool Engine::ensure_scratch(uint64_t spill_words, std::string& err) {
 }
 
 bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
-  hipSetDevice(dev_);
+  (void)hipSetDevice(dev_);
   b.n = uint32_t(hb.desc.size());
   b.arena_bytes = hb.arena.size();
   b.spill_words = 0;
   for (const uint4& d : hb.desc) {
-    uint32_t need = (key_bound(d.w >> 16) + 7) / 8;
-    if (need > uint32_t(kKeySlotWords)) b.spill_words += need;
+    const uint32_t need = (key_bound(d.w >> 16) + 7) / 8;
+    if (need > uint32_t(kMinKeyWords)) b.spill_words += need;  // bound for every variant
   }
   if (!hip_ok(hipMalloc(&b.desc, std::max<size_t>(hb.desc.size(), 1) * sizeof(uint4)), "hipMalloc(batch)", err)) return false;
   // +32 B tail: the kernel stages whole 16-byte lines of the arena into LDS
@@ -414,16 +466,16 @@ bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
 }
 
 void Engine::free_batch(DevBatch& b) {
-  hipSetDevice(dev_);
-  if (b.desc) hipFree(b.desc);
-  if (b.arena) hipFree(b.arena);
+  (void)hipSetDevice(dev_);
+  if (b.desc) (void)hipFree(b.desc);
+  if (b.arena) (void)hipFree(b.arena);
   b = DevBatch{};
 }
 
 bool Engine::alloc_matches(uint64_t cap, uint32_t n_pkgs, DevMatches& m, std::string& err) {
   (void)hipSetDevice(dev_);
   m.cap = std::max<uint64_t>(cap, 1);
-  m.dir_cap = std::max<uint32_t>((n_pkgs + kTile - 1) / kTile, 1);
+  m.dir_cap = std::max<uint32_t>((n_pkgs + kMinTile - 1) / kMinTile, 1);
   if (!hip_ok(hipMalloc(&m.pairs, m.cap * sizeof(uint2)), "hipMalloc(matches)", err)) return false;
   if (!hip_ok(hipMalloc(&m.dir, m.dir_cap * sizeof(TileDir)), "hipMalloc(tile dir)", err)) return false;
   if (!hip_ok(hipMalloc(&m.ctl, 8 * sizeof(unsigned long long)), "hipMalloc(ctl)", err)) return false;
@@ -445,7 +497,10 @@ bool Engine::fetch_ordered(const DevMatches& m, uint32_t n_pkgs, uint64_t total,
     err = "match buffer too small";
     return false;
   }
-  const uint32_t n_tiles = (n_pkgs + kTile - 1) / kTile;
+  unsigned long long ctl[8];
+  if (!hip_ok(hipMemcpy(ctl, m.ctl, sizeof(ctl), hipMemcpyDeviceToHost), "D2H ctl", err)) return false;
+  const uint32_t tile = ctl[5] ? uint32_t(ctl[5]) : 256;
+  const uint32_t n_tiles = (n_pkgs + tile - 1) / tile;
   std::vector<TileDir> dir(n_tiles);
   std::vector<uint2> raw(total);
   if (n_tiles && !hip_ok(hipMemcpy(dir.data(), m.dir, n_tiles * sizeof(TileDir), hipMemcpyDeviceToHost), "D2H dir", err))
@@ -459,7 +514,8 @@ bool Engine::fetch_ordered(const DevMatches& m, uint32_t n_pkgs, uint64_t total,
 
 bool Engine::launch(const DevBatch& b, const DevMatches& m, hipStream_t st, std::string& err) {
   (void)hipSetDevice(dev_);
-  const uint32_t n_tiles = (b.n + kTile - 1) / kTile;
+  const VariantInfo& v = kVariants[variant_];
+  const uint32_t n_tiles = (b.n + v.tile - 1) / v.tile;
   if (n_tiles > m.dir_cap) {
     err = "tile directory smaller than the batch";
     return false;
@@ -479,7 +535,7 @@ bool Engine::launch(const DevBatch& b, const DevMatches& m, hipStream_t st, std:
   a.ctl = m.ctl;
   a.spill = spill_;
   a.spill_cap = spill_cap_;
-  hipLaunchKernelGGL(match_kernel, dim3(n_tiles), dim3(kTile), 0, st, a);
+  v.launch(n_tiles, st, a);
   return hip_ok(hipGetLastError(), "match_kernel launch", err);
 }
 
@@ -489,7 +545,10 @@ bool Engine::match_host(const HostBatch& hb, std::vector<uint2>& out, int64_t& e
   if (hb.desc.empty()) return true;
   std::lock_guard<std::mutex> lk(call_mu_);
   DevBatch b;
-  if (!upload(hb, b, err)) { free_batch(b); return false; }
+  if (!upload(hb, b, err)) {
+    free_batch(b);
+    return false;
+  }
   uint64_t cap = std::max<uint64_t>(hb.desc.size() * 4, 1024);
   bool ok = true;
   for (int attempt = 0; attempt < 2 && ok; attempt++) {
@@ -498,7 +557,10 @@ bool Engine::match_host(const HostBatch& hb, std::vector<uint2>& out, int64_t& e
          hip_ok(hipStreamSynchronize(stream_), "match_kernel", err);
     unsigned long long ctl[8] = {0};
     if (ok) ok = hip_ok(hipMemcpy(ctl, m.ctl, sizeof(ctl), hipMemcpyDeviceToHost), "D2H ctl", err);
-    if (ok && ctl[3]) { err = "match kernel internal error bits " + std::to_string(ctl[3]); ok = false; }
+    if (ok && ctl[3]) {
+      err = "match kernel internal error bits " + std::to_string(ctl[3]);
+      ok = false;
+    }
     if (ok && ctl[0] > cap) {  // output buffer too small: rerun with the exact size
       cap = ctl[0];
       free_matches(m);
