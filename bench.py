@@ -189,13 +189,12 @@ def main():
                 e = errbuf()
                 lib().tvm_match_time(eng.h, b, 10, ctypes.byref(ms), e, len(e))
                 times[n].append(ms.value / 10)
-                if status(eng, b) != (total, -1, 0):
+                if not n.startswith("ablate") and status(eng, b) != (total, -1, 0):
                     raise RuntimeError(f"variant {n} disagrees on the match count")
         for n in names:
             t = sorted(times[n])
             log(rank, f"[sweep] {n:>16}: median {t[len(t)//2]:.4f} ms  min {t[0]:.4f} ms per pass")
-    if args.variant is not None:
-        lib().tvm_engine_set_variant(eng.h, args.variant)
+    lib().tvm_engine_set_variant(eng.h, args.variant if args.variant is not None else 0)
     launch(eng, b, args.warmup)
 
     def barrier():

@@ -147,39 +147,39 @@ class SynthBatch:
 
 def make_batch(db, n_targets, pkgs_per_target, plat_weights, seed, miss=0.25, zipf=2.5, invalid=0.002,
                long_versions=0.0):
-    """SBOM-like batch: each target draws one platform, then packages over its keys."""
+    """SBOM-like batch: each target draws one platform, then packages over its keys (numpy-vectorised)."""
     rng = np.random.default_rng(seed)
     w = np.asarray(plat_weights, dtype=np.float64)
     w = w / w.sum()
     t_plat = rng.choice(len(db.platforms), size=n_targets, p=w)
-    plat, names, versions, targets = [], [], [], []
-    for t in range(n_targets):
-        p = int(t_plat[t])
-        keys = db.plat_keys[p]
-        n = pkgs_per_target
-        # popularity skew without a single dominant key: P(rank < r) = (r / K) ** (1 / zipf)
-        rank = np.minimum((len(keys) * rng.random(n) ** zipf).astype(np.int64), len(keys) - 1)
-        perm_seed = (p * 1000003) % len(keys)
-        kidx = keys[(rank * 7919 + perm_seed) % len(keys)]
-        missing = rng.random(n) < miss
-        patch = rng.integers(0, 40, n)
-        rev = rng.integers(1, 9, n)
-        bad = rng.random(n) < invalid
-        longv = rng.random(n) < long_versions
-        b0 = len(names)
-        for i in range(n):
-            k = int(kidx[i])
-            ep, ma, mi, dfsg, ubu = db.key_base[k]
-            if missing[i]:
-                names.append(b"absent-%d-%d" % (t, i))
-            else:
-                names.append(db.key_names[k])
-            v = _deb_version(ep, ma, mi, int(patch[i]), int(rev[i]), ubu, 0, dfsg)
-            if bad[i]:
-                v = b"x" + v  # upstream must start with a digit: parse error
-            if longv[i]:
-                v = v + b"+" + b".".join(b"%d" % j for j in range(30))
-            versions.append(v)
-        plat += [p] * n
-        targets.append((p, b0, len(names)))
-    return SynthBatch(np.array(plat, dtype=np.int32), names, versions, targets)
+    n = n_targets * pkgs_per_target
+    plat = np.repeat(t_plat, pkgs_per_target).astype(np.int32)
+    start = np.array([int(k[0]) if len(k) else 0 for k in db.plat_keys], dtype=np.int64)
+    K = np.array([len(k) for k in db.plat_keys], dtype=np.int64)[plat]
+    # popularity skew without a single dominant key: P(rank < r) = (r / K) ** (1 / zipf)
+    rank = np.minimum((K * rng.random(n) ** zipf).astype(np.int64), K - 1)
+    local = (rank * 7919 + (plat.astype(np.int64) * 1000003) % K) % K
+    kidx = start[plat] + local  # keys of one platform are contiguous (make_db emits them per platform)
+    missing = rng.random(n) < miss
+    patch = rng.integers(0, 40, n)
+    rev = rng.integers(1, 9, n)
+    bad = rng.random(n) < invalid
+    longv = rng.random(n) < long_versions
+    base = np.array(db.key_base, dtype=np.int64)  # (ep, major, minor, dfsg, ubuntu) per key
+    kb = base[kidx]
+    prefix = np.array([(b"%d:" % e if e else b"") + b"%d.%d." % (ma, mi) for e, ma, mi, _, _ in db.key_base],
+                      dtype=object)[kidx].astype("S")
+    v = np.char.add(prefix, patch.astype("S"))
+    v = np.char.add(v, np.where(kb[:, 3] == 1, b"+dfsg", b"").astype("S"))
+    v = np.char.add(np.char.add(v, b"-"), rev.astype("S"))
+    deb_tail = np.where(rev % 3 == 0, np.char.add(b"+deb12u", (rev % 5).astype("S")), b"")
+    ubu_tail = np.char.add(b"ubuntu0.", (rev % 7).astype("S"))
+    v = np.char.add(v, np.where(kb[:, 4] == 1, ubu_tail, deb_tail).astype("S"))
+    v = np.where(bad, np.char.add(b"x", v), v)  # upstream must start with a digit: parse error
+    if long_versions:
+        v = np.where(longv, np.char.add(v, b"+" + b".".join(b"%d" % j for j in range(30))), v)
+    names = np.array(db.key_names, dtype=object)[kidx]
+    miss_idx = np.nonzero(missing)[0]
+    names[miss_idx] = [b"absent-%d" % i for i in miss_idx]
+    targets = [(int(t_plat[t]), t * pkgs_per_target, (t + 1) * pkgs_per_target) for t in range(n_targets)]
+    return SynthBatch(plat, names.tolist(), v.tolist(), targets)

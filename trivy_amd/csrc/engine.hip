@@ -137,7 +137,8 @@ __device__ __forceinline__ bool eval_row(const MatchArgs& a, const S& s, uint32_
 
 // One sweep over the tile's pairs.  DIRECT=false: compact into LDS (count all, store the
 // first MB).  DIRECT=true: store straight to out[base + position].
-template <int T, int KW, int MB, bool DIRECT>
+// AB (ablation, diagnostics only): 2 = load rows but skip the key compare.
+template <int T, int KW, int MB, bool DIRECT, int AB = 0>
 __device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared<T, KW, MB>& s, uint32_t total_pairs,
                                           uint32_t tid, unsigned long long base) {
   constexpr int W = T / 64;
@@ -158,7 +159,7 @@ __device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared<T, KW, 
       qn = pair_pkg<T>(s, jn);
       rown = a.db.rows[s.rbeg[qn] + (jn - s.scan[qn])];
     }
-    const bool m = (j < total_pairs) && eval_row<KW>(a, s, q, row);
+    const bool m = (j < total_pairs) && (AB == 2 ? (row.adv & 7u) == 0 : eval_row<KW>(a, s, q, row));
     const unsigned long long bal = __ballot(m);
     const uint32_t lane_off = __popcll(bal & ((1ull << lane) - 1ull));
     if (lane == 0) s.wsum[wave] = uint32_t(__popcll(bal));
@@ -188,7 +189,9 @@ __device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared<T, KW, 
   return nm;
 }
 
-template <int T, int KW, int MB>
+// AB (ablation, diagnostics only): 0 = full kernel, 1 = stage+probe+encode+scan only,
+// 2 = no key compare.  Ablation variants produce wrong match lists by construction.
+template <int T, int KW, int MB, int AB = 0>
 __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
   __shared__ TileShared<T, KW, MB> s;
   constexpr uint32_t kStageBytes = MB * 8;
@@ -297,7 +300,7 @@ __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
   const uint32_t total_pairs = block_scan<T>(s, cnt, tid);
 
   // ---- 3+4. pair sweep with LDS compaction -----------------------------------------------
-  const uint32_t nm = sweep<T, KW, MB, false>(a, s, total_pairs, tid, 0);
+  const uint32_t nm = AB == 1 ? (total_pairs & 1u) : sweep<T, KW, MB, false, AB>(a, s, total_pairs, tid, 0);
 
   // ---- reserve the tile's output segment (one atomic per tile, no inter-tile waiting) -----
   if (tid == 0) {
@@ -317,7 +320,7 @@ __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
     for (uint32_t i = tid; i < nm; i += T)
       if (base + i < a.out_cap) a.out[base + i] = s.mbuf[i];
   } else {
-    sweep<T, KW, MB, true>(a, s, total_pairs, tid, base);  // rare: more matches than the LDS buffer
+    sweep<T, KW, MB, true, AB>(a, s, total_pairs, tid, base);  // rare: more matches than the LDS buffer
   }
 }
 
@@ -328,9 +331,9 @@ struct VariantInfo {
   const char* name;
 };
 
-template <int T, int KW, int MB>
+template <int T, int KW, int MB, int AB = 0>
 void launch_variant(uint32_t n_tiles, hipStream_t st, const MatchArgs& a) {
-  hipLaunchKernelGGL((match_kernel<T, KW, MB>), dim3(n_tiles), dim3(T), 0, st, a);
+  hipLaunchKernelGGL((match_kernel<T, KW, MB, AB>), dim3(n_tiles), dim3(T), 0, st, a);
 }
 
 const VariantInfo kVariants[] = {
@@ -339,6 +342,8 @@ const VariantInfo kVariants[] = {
     {128, launch_variant<128, 4, 1024>, "t128_k32_m1024"},
     {64, launch_variant<64, 4, 512>, "t64_k32_m512"},
     {128, launch_variant<128, 4, 2048>, "t128_k32_m2048"},
+    {256, launch_variant<256, 8, 2048, 1>, "ablate_probe_only"},
+    {256, launch_variant<256, 8, 2048, 2>, "ablate_no_cmp"},
 };
 constexpr int kNumVariants = int(sizeof(kVariants) / sizeof(kVariants[0]));
 constexpr int kMinTile = 64;
