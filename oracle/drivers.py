@@ -7,13 +7,16 @@ imports this.  Small cases only (dict lookups, per-call JSON decode - like the
 reference, which decodes every advisory on every Get).
 
 Restated from (fwereade/trivy @ 2025-01-14):
-  pkg/detector/ospkg/detect.go:63-82           Detect (gpg-pubkey filter, EOSL)
-  pkg/detector/ospkg/debian/debian.go:57-119   Debian Scanner.Detect
-  pkg/detector/ospkg/ubuntu/ubuntu.go:79-151   Ubuntu Scanner.Detect + versionFromEolDates
-  pkg/detector/ospkg/amazon/amazon.go:43-97    Amazon Scanner.Detect
+  pkg/detector/ospkg/detect.go:32-82           drivers map, Detect (gpg-pubkey filter, EOSL)
+  pkg/detector/ospkg/version/version.go:15-38  Major / Minor / Supported
   pkg/scanner/utils/utils.go:10-29             FormatVersion / FormatSrcVersion
-  trivy-db db.Config.GetAdvisories (third party, go.mod:25) as described in SURVEY.md §8a a28
+  pkg/detector/ospkg/<os>/<os>.go              every driver's Detect + IsSupportedVersion
+and the third-party trivy-db (go.mod:25, absent here) as described in SURVEY.md §8a
+a28-a30: GetAdvisories / ForEachAdvisory (data-source join), redhat-oval Get (CPE
+resolution through the "Red Hat CPE" bucket, one advisory per (entry, CVE)), rocky Get
+(per-arch Entries).
 """
+import calendar
 import ctypes
 import json
 import os
@@ -30,21 +33,63 @@ def lib():
         path = os.path.join(_HERE, "liboracle.so")
         if not os.path.exists(path):
             raise RuntimeError("oracle not built: run `make -C oracle`")
-        _LIB = ctypes.CDLL(path)
-        _LIB.orc_deb_cmp_str.restype = ctypes.c_int
-        _LIB.orc_deb_cmp_str.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
+        L = ctypes.CDLL(path)
+        for fn in ("orc_deb_cmp_str", "orc_apk_cmp_str", "orc_rpm_cmp_str"):
+            f = getattr(L, fn)
+            f.restype = ctypes.c_int
+            f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
+        _LIB = L
     return _LIB
+
+
+def _b(x):
+    return x.encode() if isinstance(x, str) else x
 
 
 def deb_cmp(a, b):
     """go-deb-version: 2 = a fails to parse, 3 = b fails, else sign(Compare)."""
-    a = a.encode() if isinstance(a, str) else a
-    b = b.encode() if isinstance(b, str) else b
+    a, b = _b(a), _b(b)
     return lib().orc_deb_cmp_str(a, len(a), b, len(b))
 
 
 def deb_valid(v):
     return deb_cmp(v, "0") != 2
+
+
+def apk_cmp(a, b):
+    """go-apk-version: 2 = a fails to parse, 3 = b fails, else sign(Compare)."""
+    a, b = _b(a), _b(b)
+    return lib().orc_apk_cmp_str(a, len(a), b, len(b))
+
+
+def apk_valid(v):
+    return apk_cmp(v, "0") != 2
+
+
+def rpm_cmp(a, b):
+    """go-rpm-version Compare (never fails)."""
+    a, b = _b(a), _b(b)
+    return lib().orc_rpm_cmp_str(a, len(a), b, len(b))
+
+
+def rpm_string(v):
+    """go-rpm-version Version.String(): the epoch is dropped when it is not positive."""
+    epoch, rest = 0, v
+    if ":" in v:
+        e, rest = v.split(":", 1)
+        try:
+            epoch = int(e) if e.lstrip("+-").isdigit() and e.strip() == e else 0
+        except ValueError:
+            epoch = 0
+        if abs(epoch) > 2 ** 63 - 1:
+            epoch = 0
+    i = rest.find("-")
+    ver, rel = (rest[:i], rest[i + 1:]) if i >= 0 else (rest, "")
+    out = f"{epoch}:" if epoch > 0 else ""
+    out += ver
+    if rel:
+        out += "-" + rel
+    return out
 
 
 class DecodeError(Exception):
@@ -56,15 +101,10 @@ _FIELDS = {"vulnerabilityid": ("VulnerabilityID", str), "vendorids": ("VendorIDs
            "fixedversion": ("FixedVersion", str), "affectedversion": ("AffectedVersion", str),
            "vulnerableversions": ("VulnerableVersions", list), "patchedversions": ("PatchedVersions", list),
            "unaffectedversions": ("UnaffectedVersions", list), "datasource": ("DataSource", dict),
-           "custom": ("Custom", object)}
+           "custom": ("Custom", object), "entries": ("Entries", "entries")}
 
 
-def decode_advisory(text):
-    """json.Unmarshal into trivy-db types.Advisory (type errors -> DecodeError)."""
-    try:
-        v = json.loads(text)
-    except ValueError as e:
-        raise DecodeError(str(e))
+def _decode_obj(v):
     out = {}
     if v is None:
         return out
@@ -91,9 +131,95 @@ def decode_advisory(text):
             x = ["" if e is None else e for e in x]
         elif typ is dict and not isinstance(x, dict):
             raise DecodeError(f"{name}: not an object")
+        elif typ == "entries":
+            if not isinstance(x, list):
+                raise DecodeError("Entries: not an array")
+            x = [_decode_obj(e) for e in x]
         if name == "Custom":
             x = json.dumps(x, separators=(",", ":"))
         out[name] = x
+    return out
+
+
+def decode_advisory(text):
+    """json.Unmarshal into trivy-db types.Advisory (type errors -> DecodeError)."""
+    try:
+        v = json.loads(text)
+    except ValueError as e:
+        raise DecodeError(str(e))
+    return _decode_obj(v)
+
+
+def decode_redhat(text):
+    """json.Unmarshal into trivy-db redhat-oval Advisory {Entries: [{FixedVersion, Affected,
+    Arches, Status, Cves: [{ID, Severity}]}]}."""
+    try:
+        v = json.loads(text)
+    except ValueError as e:
+        raise DecodeError(str(e))
+    if v is None:
+        return []
+    if not isinstance(v, dict):
+        raise DecodeError("not an object")
+    ents = None
+    for k, x in v.items():
+        if k.lower() == "entries":
+            ents = x
+    if ents is None:
+        return []
+    if not isinstance(ents, list):
+        raise DecodeError("Entries: not an array")
+    out = []
+    for e in ents:
+        if e is None:
+            out.append({"FixedVersion": "", "Affected": [], "Arches": [], "Status": 0, "Cves": []})
+            continue
+        if not isinstance(e, dict):
+            raise DecodeError("entry: not an object")
+        d = {"FixedVersion": "", "Affected": [], "Arches": [], "Status": 0, "Cves": []}
+        for k, x in e.items():
+            kl = k.lower()
+            if x is None:
+                continue
+            if kl == "fixedversion":
+                if not isinstance(x, str):
+                    raise DecodeError("FixedVersion")
+                d["FixedVersion"] = x
+            elif kl == "affected":
+                if not isinstance(x, list) or any(isinstance(i, bool) or not isinstance(i, int) for i in x):
+                    raise DecodeError("Affected")
+                d["Affected"] = x
+            elif kl == "arches":
+                if not isinstance(x, list) or any(i is not None and not isinstance(i, str) for i in x):
+                    raise DecodeError("Arches")
+                d["Arches"] = ["" if i is None else i for i in x]
+            elif kl == "status":
+                if isinstance(x, bool) or not isinstance(x, int):
+                    raise DecodeError("Status")
+                d["Status"] = x
+            elif kl == "cves":
+                if not isinstance(x, list):
+                    raise DecodeError("Cves")
+                cves = []
+                for c in x:
+                    cd = {"ID": "", "Severity": 0}
+                    if c is not None:
+                        if not isinstance(c, dict):
+                            raise DecodeError("cve")
+                        for ck, cx in c.items():
+                            if cx is None:
+                                continue
+                            if ck.lower() == "id":
+                                if not isinstance(cx, str):
+                                    raise DecodeError("cve ID")
+                                cd["ID"] = cx
+                            elif ck.lower() == "severity":
+                                if isinstance(cx, bool) or not isinstance(cx, int):
+                                    raise DecodeError("cve Severity")
+                                cd["Severity"] = cx
+                    cves.append(cd)
+                d["Cves"] = cves
+        out.append(d)
     return out
 
 
@@ -124,16 +250,19 @@ class Records:
         out = {k: d[k] for k in ("ID", "Name", "URL") if d.get(k)}
         return out or None
 
-    def get(self, root, name):
-        """GetAdvisories(root, name): list of advisories sorted by vulnID, or raises DecodeError."""
+    def raw(self, root, name):
+        """(vulnID, value) pairs of bucket root/name in bbolt key order."""
         b = self.tree.get(("b", root), {}).get(("b", name))
         if not b:
             return []
+        return [(vid, val) for (kind, vid), val in sorted(b.items(), key=lambda kv: kv[0][1].encode())
+                if kind == "k"]
+
+    def get(self, root, name):
+        """GetAdvisories(root, name): list of advisories sorted by vulnID, or raises DecodeError."""
         src = self.data_source(root)
         out = []
-        for (kind, vid), val in sorted(b.items(), key=lambda kv: kv[0][1].encode()):
-            if kind != "k":
-                continue
+        for vid, val in self.raw(root, name):
             a = decode_advisory(val)
             a["VulnerabilityID"] = vid
             if src:
@@ -141,6 +270,63 @@ class Records:
             elif "DataSource" in a:
                 a["DataSource"] = {k: a["DataSource"][k] for k in ("ID", "Name", "URL") if a["DataSource"].get(k)}
             out.append(a)
+        return out
+
+    def get_rocky(self, root, name, arch):
+        """trivy-db rocky Get(release, name, arch): per advisory, the Entries whose Arches
+        contain arch (FixedVersion/VendorIDs of the entry); an advisory without Entries is
+        returned as is."""
+        out = []
+        for a in self.get(root, name):
+            ents = a.pop("Entries", None)
+            if not ents:
+                out.append(a)
+                continue
+            for e in ents:
+                if arch in (e.get("Arches") or []):
+                    b = {k: v for k, v in a.items() if k not in ("FixedVersion", "VendorIDs", "Arches")}
+                    for k in ("FixedVersion", "VendorIDs", "Arches"):
+                        if e.get(k):
+                            b[k] = e[k]
+                    out.append(b)
+        return out
+
+    def redhat_cpes(self, content_sets, nvrs):
+        """trivy-db RedHatRepoToCPEs / RedHatNVRToCPEs, uniq'ed."""
+        cpe = self.tree.get(("b", "Red Hat CPE"), {})
+        out = []
+        for sub, keys in (("repository", content_sets), ("nvr", nvrs)):
+            b = cpe.get(("b", sub), {})
+            for k in keys:
+                v = b.get(("k", k))
+                if v is None:
+                    continue
+                for i in json.loads(v) or []:
+                    if i not in out:
+                        out.append(i)
+        return out
+
+    def get_redhat(self, name, content_sets, nvrs):
+        """trivy-db redhat-oval Get(pkgName, repositories, nvrs)."""
+        cpes = set(self.redhat_cpes(content_sets, nvrs))
+        out = []
+        for vid, val in self.raw("Red Hat", name):
+            try:
+                entries = decode_redhat(val)
+            except DecodeError as e:
+                raise DecodeError(f"failed to unmarshal advisory JSON: {e}")
+            for e in entries:
+                if not any(i in cpes for i in e["Affected"]):
+                    continue
+                for c in e["Cves"]:
+                    a = {"Severity": c["Severity"], "FixedVersion": e["FixedVersion"], "Arches": e["Arches"],
+                         "Status": e["Status"]}
+                    if vid.startswith("CVE-"):
+                        a["VulnerabilityID"] = vid
+                    else:
+                        a["VulnerabilityID"] = c["ID"]
+                        a["VendorIDs"] = [vid]
+                    out.append(a)
         return out
 
 
@@ -165,28 +351,101 @@ def major(v):
     return v.split(".", 1)[0]
 
 
-def _base(p, a, installed):
+def minor(v):
+    parts = v.split(".", 2)
+    return v if len(parts) == 1 else parts[0] + "." + parts[1]
+
+
+def _eol(y, m, d):
+    return calendar.timegm((y, m, d, 23, 59, 59, 0, 0, 0))
+
+
+def _tab(d):
+    return {k: _eol(*v) for k, v in d.items()}
+
+
+# eolDates of each driver (transcribed data, <os>.go top of file)
+UBUNTU_EOL = _tab({
+    "4.10": (2006, 4, 30), "5.04": (2006, 10, 31), "5.10": (2007, 4, 13), "6.06": (2011, 6, 1),
+    "6.10": (2008, 4, 25), "7.04": (2008, 10, 19), "7.10": (2009, 4, 18), "8.04": (2013, 5, 9),
+    "8.10": (2010, 4, 30), "9.04": (2010, 10, 23), "9.10": (2011, 4, 29), "10.04": (2015, 4, 29),
+    "10.10": (2012, 4, 10), "11.04": (2012, 10, 28), "11.10": (2013, 5, 9), "12.04": (2019, 4, 26),
+    "12.04-ESM": (2019, 4, 28), "12.10": (2014, 5, 16), "13.04": (2014, 1, 27), "13.10": (2014, 7, 17),
+    "14.04": (2022, 4, 25), "14.04-ESM": (2024, 4, 25), "14.10": (2015, 7, 23), "15.04": (2016, 1, 23),
+    "15.10": (2016, 7, 22), "16.04": (2021, 4, 21), "16.04-ESM": (2026, 4, 29), "16.10": (2017, 7, 20),
+    "17.04": (2018, 1, 13), "17.10": (2018, 7, 19), "18.04": (2023, 5, 31), "18.04-ESM": (2028, 3, 31),
+    "18.10": (2019, 7, 18), "19.04": (2020, 1, 18), "19.10": (2020, 7, 17), "20.04": (2025, 4, 23),
+    "20.10": (2021, 7, 22), "21.04": (2022, 1, 20), "21.10": (2022, 7, 14), "22.04": (2027, 4, 23),
+    "22.10": (2023, 7, 20), "23.04": (2024, 1, 20)})
+DEBIAN_EOL = _tab({
+    "1.1": (1997, 6, 5), "1.2": (1998, 6, 5), "1.3": (1999, 3, 9), "2.0": (2000, 3, 9), "2.1": (2000, 10, 30),
+    "2.2": (2003, 7, 30), "3.0": (2006, 6, 30), "3.1": (2008, 3, 30), "4.0": (2010, 2, 15), "5.0": (2012, 2, 6),
+    "6.0": (2016, 2, 29), "7": (2018, 5, 31), "8": (2020, 6, 30), "9": (2022, 6, 30), "10": (2024, 6, 30),
+    "11": (2026, 8, 14), "12": (2028, 6, 10), "13": (3000, 1, 1)})
+ALPINE_EOL = _tab({
+    "2.0": (2012, 4, 1), "2.1": (2012, 11, 1), "2.2": (2013, 5, 1), "2.3": (2013, 11, 1), "2.4": (2014, 5, 1),
+    "2.5": (2014, 11, 1), "2.6": (2015, 5, 1), "2.7": (2015, 11, 1), "3.0": (2016, 5, 1), "3.1": (2016, 11, 1),
+    "3.2": (2017, 5, 1), "3.3": (2017, 11, 1), "3.4": (2018, 5, 1), "3.5": (2018, 11, 1), "3.6": (2019, 5, 1),
+    "3.7": (2019, 11, 1), "3.8": (2020, 5, 1), "3.9": (2020, 11, 1), "3.10": (2021, 5, 1), "3.11": (2021, 11, 1),
+    "3.12": (2022, 5, 1), "3.13": (2022, 11, 1), "3.14": (2023, 5, 1), "3.15": (2023, 11, 1),
+    "3.16": (2024, 5, 23), "3.17": (2024, 11, 22), "3.18": (2025, 5, 9), "3.19": (2025, 11, 1)})
+ALPINE_EOL["edge"] = calendar.timegm((9999, 1, 1, 0, 0, 0, 0, 0, 0))
+AMAZON_EOL = _tab({"1": (2023, 12, 31), "2": (2025, 6, 30), "2023": (2028, 3, 15)})
+REDHAT_EOL = _tab({"4": (2017, 5, 31), "5": (2020, 11, 30), "6": (2024, 6, 30), "7": (3000, 1, 1),
+                   "8": (3000, 1, 1), "9": (3000, 1, 1)})
+CENTOS_EOL = _tab({"3": (2010, 10, 31), "4": (2012, 2, 29), "5": (2017, 3, 31), "6": (2020, 11, 30),
+                   "7": (2024, 6, 30), "8": (2021, 12, 31)})
+ALMA_EOL = _tab({"8": (2029, 3, 1), "9": (2032, 5, 31)})
+ROCKY_EOL = _tab({"8": (2029, 5, 31), "9": (2032, 5, 31)})
+ORACLE_EOL = _tab({"3": (2011, 12, 31), "4": (2013, 12, 31), "5": (2017, 12, 31), "6": (2021, 3, 21),
+                   "7": (2024, 7, 23), "8": (2029, 7, 18), "9": (2032, 7, 18)})
+PHOTON_EOL = _tab({"1.0": (2022, 2, 28), "2.0": (2022, 12, 31), "3.0": (2024, 6, 30), "4.0": (2025, 12, 31)})
+SLES_EOL = _tab({
+    "10": (2007, 12, 31), "10.1": (2008, 11, 30), "10.2": (2010, 4, 11), "10.3": (2011, 10, 11),
+    "10.4": (2013, 7, 31), "11": (2010, 12, 31), "11.1": (2012, 8, 31), "11.2": (2014, 1, 31),
+    "11.3": (2016, 1, 31), "11.4": (2019, 3, 31), "12": (2016, 6, 30), "12.1": (2017, 5, 31),
+    "12.2": (2018, 3, 31), "12.3": (2019, 1, 30), "12.4": (2020, 6, 30), "12.5": (2024, 10, 31),
+    "15": (2019, 12, 31), "15.1": (2021, 1, 31), "15.2": (2021, 12, 31), "15.3": (2022, 12, 31),
+    "15.4": (2023, 12, 31), "15.5": (2028, 12, 31)})
+OPENSUSE_EOL = _tab({
+    "42.1": (2017, 5, 17), "42.2": (2018, 1, 26), "42.3": (2019, 6, 30), "15.0": (2019, 12, 3),
+    "15.1": (2020, 11, 30), "15.2": (2021, 11, 30), "15.3": (2022, 11, 30), "15.4": (2023, 11, 30),
+    "15.5": (2024, 12, 31)})
+
+
+def supported(eol, ver, now):
+    """osver.Supported (version.go:31-38)."""
+    return ver not in eol or now < eol[ver]
+
+
+def _base(p, a, installed, fixed=None, pkg_id=True, custom=True):
     d = {"VulnerabilityID": a["VulnerabilityID"]}
-    for k_out, val in [("PkgID", p.get("ID")), ("PkgName", p.get("Name")), ("PkgIdentifier", p.get("Identifier")),
-                       ("InstalledVersion", installed), ("FixedVersion", a.get("FixedVersion")),
-                       ("Layer", p.get("Layer")), ("DataSource", a.get("DataSource")), ("Custom", a.get("Custom"))]:
+    fixed = a.get("FixedVersion") if fixed is None else fixed
+    for k_out, val in [("PkgID", p.get("ID") if pkg_id else None), ("PkgName", p.get("Name")),
+                       ("PkgIdentifier", p.get("Identifier")), ("InstalledVersion", installed),
+                       ("FixedVersion", fixed), ("Layer", p.get("Layer")), ("DataSource", a.get("DataSource")),
+                       ("Custom", a.get("Custom") if custom else None)]:
         if val:
             d[k_out] = val
     return d
 
 
-def debian_detect(db, os_ver, pkgs):
+def _get(db, err, root, name):
+    try:
+        return db.get(root, name)
+    except DecodeError as e:
+        raise DecodeError(f"{err}: failed to unmarshal advisory JSON: {e}")
+
+
+# --------------------------------------------------------------------- dpkg drivers ----
+def debian_detect(db, os_ver, repo, pkgs, now=None):
     root = "debian " + major(os_ver)
     out = []
     for p in pkgs:
         src = fmt_src(p)
         if not deb_valid(src):
             continue
-        try:
-            advs = db.get(root, p.get("SrcName", ""))
-        except DecodeError as e:
-            raise DecodeError(f"failed to get debian advisories: failed to unmarshal advisory JSON: {e}")
-        for a in advs:
+        for a in _get(db, "failed to get debian advisories", root, p.get("SrcName", "")):
             v = _base(p, a, fmt(p))
             if a.get("VendorIDs"):
                 v["VendorIDs"] = a["VendorIDs"]
@@ -207,38 +466,6 @@ def debian_detect(db, os_ver, pkgs):
     return out
 
 
-def _eol(y, m, d):
-    import calendar
-    return calendar.timegm((y, m, d, 23, 59, 59, 0, 0, 0))
-
-
-# ubuntu.go:19-64 eolDates (transcribed data)
-UBUNTU_EOL = {k: _eol(*v) for k, v in {
-    "4.10": (2006, 4, 30), "5.04": (2006, 10, 31), "5.10": (2007, 4, 13), "6.06": (2011, 6, 1),
-    "6.10": (2008, 4, 25), "7.04": (2008, 10, 19), "7.10": (2009, 4, 18), "8.04": (2013, 5, 9),
-    "8.10": (2010, 4, 30), "9.04": (2010, 10, 23), "9.10": (2011, 4, 29), "10.04": (2015, 4, 29),
-    "10.10": (2012, 4, 10), "11.04": (2012, 10, 28), "11.10": (2013, 5, 9), "12.04": (2019, 4, 26),
-    "12.04-ESM": (2019, 4, 28), "12.10": (2014, 5, 16), "13.04": (2014, 1, 27), "13.10": (2014, 7, 17),
-    "14.04": (2022, 4, 25), "14.04-ESM": (2024, 4, 25), "14.10": (2015, 7, 23), "15.04": (2016, 1, 23),
-    "15.10": (2016, 7, 22), "16.04": (2021, 4, 21), "16.04-ESM": (2026, 4, 29), "16.10": (2017, 7, 20),
-    "17.04": (2018, 1, 13), "17.10": (2018, 7, 19), "18.04": (2023, 5, 31), "18.04-ESM": (2028, 3, 31),
-    "18.10": (2019, 7, 18), "19.04": (2020, 1, 18), "19.10": (2020, 7, 17), "20.04": (2025, 4, 23),
-    "20.10": (2021, 7, 22), "21.04": (2022, 1, 20), "21.10": (2022, 7, 14), "22.04": (2027, 4, 23),
-    "22.10": (2023, 7, 20), "23.04": (2024, 1, 20)}.items()}
-
-# debian.go:20-40 eolDates
-DEBIAN_EOL = {k: _eol(*v) for k, v in {
-    "1.1": (1997, 6, 5), "1.2": (1998, 6, 5), "1.3": (1999, 3, 9), "2.0": (2000, 3, 9), "2.1": (2000, 10, 30),
-    "2.2": (2003, 7, 30), "3.0": (2006, 6, 30), "3.1": (2008, 3, 30), "4.0": (2010, 2, 15), "5.0": (2012, 2, 6),
-    "6.0": (2016, 2, 29), "7": (2018, 5, 31), "8": (2020, 6, 30), "9": (2022, 6, 30), "10": (2024, 6, 30),
-    "11": (2026, 8, 14), "12": (2028, 6, 10), "13": (3000, 1, 1)}.items()}
-
-
-def supported(eol, ver, now):
-    """osver.Supported (version.go:31-38)."""
-    return ver not in eol or now < eol[ver]
-
-
 def ubuntu_version_from_eol(os_ver, now, eol):
     if os_ver in eol:
         return os_ver
@@ -248,15 +475,11 @@ def ubuntu_version_from_eol(os_ver, now, eol):
     return os_ver
 
 
-def ubuntu_detect(db, os_ver, pkgs, now, eol=None):
-    eol = UBUNTU_EOL if eol is None else eol
+def ubuntu_detect(db, os_ver, repo, pkgs, now):
     out = []
     for p in pkgs:
-        os_ver = ubuntu_version_from_eol(os_ver, now, eol)
-        try:
-            advs = db.get("ubuntu " + os_ver, p.get("SrcName", ""))
-        except DecodeError as e:
-            raise DecodeError(f"failed to get Ubuntu advisories: {e}")
+        os_ver = ubuntu_version_from_eol(os_ver, now, UBUNTU_EOL)
+        advs = _get(db, "failed to get Ubuntu advisories", "ubuntu " + os_ver, p.get("SrcName", ""))
         src = fmt_src(p)
         if not deb_valid(src):
             continue
@@ -274,17 +497,17 @@ def ubuntu_detect(db, os_ver, pkgs, now, eol=None):
     return out
 
 
-def amazon_detect(db, os_ver, pkgs):
+def amazon_release(os_ver):
     f = os_ver.split()
     v = major(f[0] if f else "")
-    if v not in ("2", "2022", "2023"):
-        v = "1"
+    return v if v in ("2", "2022", "2023") else "1"
+
+
+def amazon_detect(db, os_ver, repo, pkgs, now=None):
+    v = amazon_release(os_ver)
     out = []
     for p in pkgs:
-        try:
-            advs = db.get("amazon linux " + v, p.get("Name", ""))
-        except DecodeError as e:
-            raise DecodeError(f"failed to get amazon advisories: {e}")
+        advs = _get(db, "failed to get amazon advisories", "amazon linux " + v, p.get("Name", ""))
         inst = fmt(p)
         if inst == "" or not deb_valid(inst):
             continue
@@ -295,3 +518,242 @@ def amazon_detect(db, os_ver, pkgs):
             if r < 0:
                 out.append(_base(p, a, inst))
     return out
+
+
+# ---------------------------------------------------------------------- apk drivers ----
+def alpine_repo_release(repo):
+    if not repo:
+        return ""
+    rel = repo.get("Release", "")
+    if rel.count(".") > 1:
+        rel = rel[:rel.rfind(".")]
+    return rel
+
+
+def alpine_stream(os_ver, repo):
+    v = minor(os_ver)
+    rr = alpine_repo_release(repo)
+    return rr if rr != "" and v != rr else v
+
+
+def alpine_vulnerable(inst, a):
+    aff = a.get("AffectedVersion", "")
+    if aff != "":
+        if not apk_valid(aff):
+            return False
+        if apk_cmp(aff, inst) > 0:
+            return False
+    fixed = a.get("FixedVersion", "")
+    if fixed == "":
+        return True
+    if not apk_valid(fixed):
+        return False
+    return apk_cmp(inst, fixed) < 0
+
+
+def alpine_detect(db, os_ver, repo, pkgs, now=None):
+    root = "alpine " + alpine_stream(os_ver, repo)
+    out = []
+    for p in pkgs:
+        name = p.get("SrcName") or p.get("Name", "")
+        advs = _get(db, "failed to get alpine advisories", root, name)
+        src = fmt_src(p)
+        if not apk_valid(src):
+            continue
+        for a in advs:
+            if alpine_vulnerable(src, a):
+                out.append(_base(p, a, fmt(p)))
+    return out
+
+
+def _apk_stream_detect(root, err):
+    def detect(db, os_ver, repo, pkgs, now=None):
+        out = []
+        for p in pkgs:
+            name = p.get("SrcName") or p.get("Name", "")
+            advs = _get(db, err, root, name)
+            inst = fmt(p)
+            if not apk_valid(inst):
+                continue
+            for a in advs:
+                fixed = a.get("FixedVersion", "")
+                if apk_valid(fixed) and apk_cmp(inst, fixed) < 0:
+                    out.append(_base(p, a, inst))
+        return out
+    return detect
+
+
+wolfi_detect = _apk_stream_detect("wolfi", "failed to get Wolfi advisories")
+chainguard_detect = _apk_stream_detect("chainguard", "failed to get Chainguard advisories")
+
+
+# ---------------------------------------------------------------------- rpm drivers ----
+REDHAT_DEFAULT_CONTENT_SETS = {
+    "6": ["rhel-6-server-rpms", "rhel-6-server-extras-rpms"],
+    "7": ["rhel-7-server-rpms", "rhel-7-server-extras-rpms"],
+    "8": ["rhel-8-for-x86_64-baseos-rpms", "rhel-8-for-x86_64-appstream-rpms"],
+    "9": ["rhel-9-for-x86_64-baseos-rpms", "rhel-9-for-x86_64-appstream-rpms"],
+}
+
+
+def add_modular_namespace(name, label):
+    """redhat.go:207-220 / alma.go: label[:2nd ':'] + '::' + name."""
+    count = 0
+    for i, ch in enumerate(label):
+        if ch == ":":
+            count += 1
+        if count == 2:
+            return label[:i] + "::" + name
+    return name
+
+
+def redhat_detect(db, os_ver, repo, pkgs, now=None):
+    os_ver = major(os_ver)
+    out = []
+    for p in pkgs:
+        if p.get("Release", "").endswith(".remi"):
+            continue
+        name = add_modular_namespace(p.get("Name", ""), p.get("Modularitylabel", ""))
+        bi = p.get("BuildInfo")
+        if bi is None:
+            cs, nvr = REDHAT_DEFAULT_CONTENT_SETS.get(os_ver, []), ""
+        else:
+            cs, nvr = bi.get("ContentSets") or [], f"{bi.get('Nvr', '')}-{bi.get('Arch', '')}"
+        try:
+            advs = db.get_redhat(name, cs, [nvr])
+        except DecodeError as e:
+            raise DecodeError(f"redhat vulnerability detection error: failed to get Red Hat advisories: {e}")
+        inst = fmt(p)
+        uniq = {}
+        for a in advs:
+            if a["Arches"] and p.get("Arch", "") != "noarch" and p.get("Arch", "") not in a["Arches"]:
+                continue
+            vid = a["VulnerabilityID"]
+            v = {"VulnerabilityID": vid, "PkgID": p.get("ID"), "PkgName": p.get("Name"), "InstalledVersion": inst,
+                 "PkgIdentifier": p.get("Identifier"), "Status": a["Status"], "Layer": p.get("Layer"),
+                 "SeveritySource": "redhat",
+                 "Severity": SEVERITY[a["Severity"]] if 0 <= a["Severity"] < 5 else SEVERITY[0]}
+            if a["FixedVersion"] == "":
+                if vid not in uniq:
+                    uniq[vid] = v
+                continue
+            if rpm_cmp(inst, a["FixedVersion"]) < 0:
+                v["VendorIDs"] = a.get("VendorIDs")
+                v["FixedVersion"] = rpm_string(a["FixedVersion"])
+                if vid in uniq:
+                    u = uniq[vid]
+                    u["VendorIDs"] = sorted(set((u.get("VendorIDs") or []) + (v["VendorIDs"] or [])))
+                    if rpm_cmp(u.get("FixedVersion") or "", a["FixedVersion"]) < 0:
+                        u["FixedVersion"] = v["FixedVersion"]
+                else:
+                    uniq[vid] = v
+        out += [{k: x for k, x in v.items() if x not in (None, "", [], 0) or k == "VulnerabilityID"}
+                for _, v in sorted(uniq.items())]
+    return out
+
+
+def _rpm_simple(root_fn, err, name_fn=lambda p: p.get("Name", ""), inst_fn=fmt, fixed_out="raw",
+                skip=lambda p: False, unfixed=False, pkg_id=True, custom=True, getter="get"):
+    def detect(db, os_ver, repo, pkgs, now=None):
+        root = root_fn(os_ver)
+        out = []
+        for p in pkgs:
+            if skip(p):
+                continue
+            try:
+                if getter == "rocky":
+                    advs = db.get_rocky(root, name_fn(p), p.get("Arch", ""))
+                else:
+                    advs = db.get(root, name_fn(p))
+            except DecodeError as e:
+                raise DecodeError(f"{err}: failed to unmarshal advisory JSON: {e}")
+            cmp_ver = inst_fn(p)
+            for a in advs:
+                fixed = a.get("FixedVersion", "")
+                if unfixed and fixed == "":
+                    out.append(_base(p, a, fmt(p), fixed="", pkg_id=pkg_id, custom=custom))
+                    continue
+                if getter == "oracle" and extract_ksplice(fixed) != extract_ksplice(p.get("Release", "")):
+                    continue
+                if rpm_cmp(cmp_ver, fixed) < 0:
+                    f = rpm_string(fixed) if fixed_out == "string" else fixed
+                    out.append(_base(p, a, fmt(p), fixed=f, pkg_id=pkg_id, custom=custom))
+        return out
+    return detect
+
+
+def extract_ksplice(v):
+    for s in v.lower().split("."):
+        if s.startswith("ksplice"):
+            return s
+    return ""
+
+
+alma_detect = _rpm_simple(lambda v: "alma " + major(v), "failed to get AlmaLinux advisories",
+                          name_fn=lambda p: add_modular_namespace(p.get("Name", ""), p.get("Modularitylabel", "")),
+                          fixed_out="string",
+                          skip=lambda p: ".module_el" in p.get("Release", "") and not p.get("Modularitylabel"))
+rocky_detect = _rpm_simple(lambda v: "rocky " + major(v), "failed to get Rocky Linux advisories", fixed_out="string",
+                           skip=lambda p: bool(p.get("Modularitylabel")), getter="rocky")
+oracle_detect = _rpm_simple(lambda v: "Oracle Linux " + major(v), "failed to get Oracle Linux advisory",
+                            getter="oracle")
+photon_detect = _rpm_simple(lambda v: "Photon OS " + v,
+                            "failed to get Photon Linux advisory: failed to get Photon advisories",
+                            name_fn=lambda p: p.get("SrcName", ""))
+mariner_detect = _rpm_simple(lambda v: "CBL-Mariner " + minor(v), "failed to get CBL-Mariner advisories",
+                             name_fn=lambda p: p.get("SrcName", ""), inst_fn=fmt_src, fixed_out="string",
+                             unfixed=True, pkg_id=False, custom=False)
+sles_detect = _rpm_simple(lambda v: "SUSE Linux Enterprise " + v,
+                          "failed to get SUSE advisory: failed to get SUSE advisories")
+opensuse_detect = _rpm_simple(lambda v: "openSUSE Leap " + v,
+                              "failed to get SUSE advisory: failed to get SUSE advisories")
+
+
+# --------------------------------------------------------------------- dispatcher ----
+def _always(ver, now):
+    return True
+
+
+# family (ftypes.OSType) -> (detect, is_supported(os_ver, now))
+DRIVERS = {
+    "alpine": (alpine_detect, lambda v, now: supported(ALPINE_EOL, minor(v), now)),
+    "alma": (alma_detect, lambda v, now: supported(ALMA_EOL, major(v), now)),
+    "amazon": (amazon_detect, lambda v, now: supported(AMAZON_EOL, amazon_release(v), now)),
+    "cbl-mariner": (mariner_detect, _always),
+    "debian": (debian_detect, lambda v, now: supported(DEBIAN_EOL, major(v), now)),
+    "ubuntu": (ubuntu_detect, lambda v, now: supported(UBUNTU_EOL, v, now)),
+    "redhat": (redhat_detect, lambda v, now: supported(REDHAT_EOL, major(v), now)),
+    "centos": (redhat_detect, lambda v, now: supported(CENTOS_EOL, major(v), now)),
+    "rocky": (rocky_detect, lambda v, now: supported(ROCKY_EOL, major(v), now)),
+    "oracle": (oracle_detect, lambda v, now: supported(ORACLE_EOL, major(v), now)),
+    "opensuse.leap": (opensuse_detect, lambda v, now: supported(OPENSUSE_EOL, v, now)),
+    "suse linux enterprise server": (sles_detect, lambda v, now: supported(SLES_EOL, v, now)),
+    "photon": (photon_detect, lambda v, now: supported(PHOTON_EOL, v, now)),
+    "wolfi": (wolfi_detect, _always),
+    "chainguard": (chainguard_detect, _always),
+}
+
+
+class UnsupportedOS(Exception):
+    pass
+
+
+def driver_detect(family, os_ver, repo, pkgs, db, now):
+    return DRIVERS[family][0](db, os_ver, repo, pkgs, now)
+
+
+def is_supported(family, os_ver, now):
+    return DRIVERS[family][1](os_ver, now)
+
+
+def detect(db, family, os_name, repo, pkgs, now):
+    """ospkg.Detect (detect.go:63-82)."""
+    if family not in DRIVERS:
+        raise UnsupportedOS("unsupported os")
+    eosl = not is_supported(family, os_name, now)
+    kept = [p for p in pkgs if p.get("Name") != "gpg-pubkey"]
+    try:
+        vulns = driver_detect(family, os_name, repo, kept, db, now)
+    except DecodeError as e:
+        raise DecodeError(f"failed detection: {e}")
+    return vulns, eosl

@@ -36,6 +36,25 @@ int orc_deb_cmp(const orc_deb* a, const orc_deb* b);
  * else the sign of Compare (-1/0/1). */
 int orc_deb_cmp_str(const char* a, size_t na, const char* b, size_t nb);
 
+/* ---- go-apk-version v0.0.0-20200609155635-041fdbb8563f (go.mod:61) ----------------------- */
+int orc_apk_valid(const char* s, size_t n);
+int orc_apk_cmp(const char* a, size_t na, const char* b, size_t nb);
+/* 2 if a fails to parse, 3 if b fails, else -1/0/1 */
+int orc_apk_cmp_str(const char* a, size_t na, const char* b, size_t nb);
+
+/* ---- go-rpm-version v0.0.0-20220614171824-631e686d1075 (go.mod:63) ------------------------ */
+typedef struct {
+  int64_t epoch;
+  const char* ver;
+  size_t nver;
+  const char* rel;
+  size_t nrel;
+} orc_rpm;
+void orc_rpm_parse(const char* s, size_t n, orc_rpm* out);  /* never fails */
+int orc_rpmvercmp(const char* a, size_t na, const char* b, size_t nb);
+int orc_rpm_cmp(const orc_rpm* a, const orc_rpm* b);
+int orc_rpm_cmp_str(const char* a, size_t na, const char* b, size_t nb);
+
 /* ---- driver-level batch matcher ----------------------------------------------------------
  * One OS bucket per package (platform id), advisories keyed by (platform, name).
  * Matches follow the per-driver semantics of SURVEY.md §8a' (the "unfixed" and

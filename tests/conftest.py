@@ -28,7 +28,14 @@ def parse_now(s):
 
 
 def _drop_zero(v):
-    """Go zero values are indistinguishable from absent fields in the reference's structs."""
+    """Go zero values are indistinguishable from absent fields in the reference's structs.
+    The embedded types.Vulnerability (vulnerability.go:30) is flattened: detectors only set
+    its Severity."""
+    v = dict(v)
+    emb = v.pop("Vulnerability", None)
+    if isinstance(emb, dict):
+        for k, x in emb.items():
+            v.setdefault(k, x)
     return {k: x for k, x in v.items() if x not in ("", 0, None, {}, [])}
 
 

@@ -11,28 +11,29 @@ from conftest import load_case_file, fixture_paths, parse_now, canon
 import oracle.drivers as od
 
 
-@pytest.mark.parametrize("driver", ["debian", "ubuntu"])
-def test_oracle_driver_cases(oracle_built, driver):
-    cf = load_case_file(driver)
-    for case in cf["detect"]:
-        db = od.Records.from_files(fixture_paths(case["fixtures"]))
-        args = (db, case["os_ver"], case["pkgs"])
-        fn = {"debian": lambda: od.debian_detect(*args),
-              "ubuntu": lambda: od.ubuntu_detect(*args, parse_now(case["now"]))}[driver]
-        if case.get("want_err"):
-            with pytest.raises(od.DecodeError) as ei:
-                fn()
-            assert case["want_err"] in str(ei.value), case["name"]
-        else:
-            assert canon(fn()) == canon(case["want"]), case["name"]
+import golden_tables as gt
+
+_DETECT = [c for d in gt.OS_DRIVERS for c in gt.os_detect_cases(d)]
+_SUPPORTED = [c for d in gt.OS_DRIVERS for c in gt.os_supported_cases(d)]
 
 
-@pytest.mark.parametrize("driver,eol", [("debian", "DEBIAN_EOL"), ("ubuntu", "UBUNTU_EOL")])
-def test_oracle_supported(driver, eol):
-    table = getattr(od, eol)
-    for case in load_case_file(driver)["supported"]:
-        ver = od.major(case["os_ver"]) if driver == "debian" else case["os_ver"]
-        assert od.supported(table, ver, parse_now(case["now"])) == case["want"], case["name"]
+@pytest.mark.parametrize("case", _DETECT, ids=[c[0] for c in _DETECT])
+def test_oracle_driver_cases(oracle_built, case):
+    """Every TestScanner_Detect case of pkg/detector/ospkg/*/*_test.go against the oracle."""
+    cid, fixtures, family, os_ver, repo, pkgs, want, want_err, now = case
+    db = od.Records.from_files(fixtures)
+    if want_err is not None:
+        with pytest.raises(od.DecodeError) as ei:
+            od.driver_detect(family, os_ver, repo, pkgs, db, now)
+        assert want_err in str(ei.value), cid
+    else:
+        assert canon(od.driver_detect(family, os_ver, repo, pkgs, db, now)) == canon(want), cid
+
+
+@pytest.mark.parametrize("case", _SUPPORTED, ids=[c[0] for c in _SUPPORTED])
+def test_oracle_supported(case):
+    cid, family, os_ver, now, want = case
+    assert od.is_supported(family, os_ver, now) == want, cid
 
 
 # dpkg orderings the reference fixtures/tests pin (debian_test.go, ubuntu_test.go,
