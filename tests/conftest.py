@@ -14,15 +14,6 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
 
 
-def load_case_file(driver):
-    with open(os.path.join(GOLDEN, "cases", driver + ".json"), encoding="utf-8") as f:
-        return json.load(f)
-
-
-def fixture_paths(rel_list):
-    return [os.path.join(GOLDEN, "fixtures", r) for r in rel_list]
-
-
 def parse_now(s):
     return int(datetime.datetime.strptime(s, "%Y-%m-%dT%H:%M:%SZ").replace(tzinfo=datetime.timezone.utc).timestamp())
 
@@ -52,19 +43,3 @@ def oracle_built():
     import subprocess
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
     return True
-
-
-@pytest.fixture(scope="session")
-def engine_factory():
-    """Builds engines from fixture record files (GPU tests only)."""
-    import trivy_amd
-    cache = {}
-
-    def make(rel_list):
-        key = tuple(rel_list)
-        if key not in cache:
-            db = trivy_amd.load_fixture_files(fixture_paths(rel_list))
-            cache[key] = trivy_amd.Engine(db, 0)
-        return cache[key]
-
-    return make

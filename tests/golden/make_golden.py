@@ -18,9 +18,8 @@ Output format: one JSON file per fixture, a list of records
     {"path": ["debian 9", "apache2", "CVE-2012-3499"], "value": "<json text>"}
 where `path` is the bucket chain plus the final key.
 
-The hand-transcribed driver test tables live in tests/golden/cases/*.json; they
-are inputs/expected outputs copied as data from the reference's Go test tables
-(file:line cited in each case's "ref" field), not generated by this script.
+The driver test tables (inputs / expected outputs of the reference's *_test.go) are
+transcribed as data by tests/golden/extract_go_tables.py into tests/golden/tables/.
 
 Usage:  python tests/golden/make_golden.py [/root/reference]
 """

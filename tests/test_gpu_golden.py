@@ -1,67 +1,87 @@
-"""GPU: the reference's own driver test tables, through the C-ABI (HIP path only)."""
+"""GPU: the reference's own driver test tables (all 13 OS drivers), through the C-ABI.
+
+Every TestScanner_Detect / TestScanner_IsSupportedVersion case of
+pkg/detector/ospkg/*/*_test.go (transcribed by tests/golden/extract_go_tables.py) runs
+through libtrivy_amd.so's HIP path and must equal the reference's expected output
+(canonical multiset) - and the oracle's.
+"""
 import pytest
 
-from conftest import load_case_file, parse_now, canon
+import golden_tables as gt
+from conftest import canon
 
 pytestmark = pytest.mark.gpu
 
+_DETECT = [c for d in gt.OS_DRIVERS for c in gt.os_detect_cases(d)]
+_ENGINES = {}
 
-@pytest.mark.parametrize("driver", ["debian", "ubuntu"])
-def test_driver_cases(engine_factory, driver):
+
+def _engine(paths):
+    import trivy_amd
+    key = tuple(paths)
+    if key not in _ENGINES:
+        _ENGINES[key] = trivy_amd.Engine(trivy_amd.load_fixture_files(paths), 0)
+    return _ENGINES[key]
+
+
+@pytest.mark.parametrize("case", _DETECT, ids=[c[0] for c in _DETECT])
+def test_driver_cases(case):
     from trivy_amd.detector.ospkg import Scanner, DetectError
-    cf = load_case_file(driver)
-    for case in cf["detect"]:
-        eng = engine_factory(case["fixtures"])
-        sc = Scanner(eng, driver)
-        now = parse_now(case["now"]) if "now" in case else None
-        if case.get("want_err"):
-            with pytest.raises(DetectError) as ei:
-                sc.detect(case["os_ver"], case.get("repo"), case["pkgs"], now=now)
-            assert case["want_err"] in str(ei.value), case["name"]
-        else:
-            got = sc.detect(case["os_ver"], case.get("repo"), case["pkgs"], now=now)
-            assert canon(got) == canon(case["want"]), case["name"]
+    cid, fixtures, family, os_ver, repo, pkgs, want, want_err, now = case
+    sc = Scanner(_engine(fixtures), family)
+    if want_err is not None:
+        with pytest.raises(DetectError) as ei:
+            sc.detect(os_ver, repo, pkgs, now=now)
+        assert want_err in str(ei.value), cid
+    else:
+        assert canon(sc.detect(os_ver, repo, pkgs, now=now)) == canon(want), cid
 
 
-def test_ospkg_detect_wraps_and_filters(engine_factory):
+def test_ospkg_detect_wraps_and_filters():
     """detect.go:63-82: gpg-pubkey filtered, errors wrapped, unsupported OS."""
     from trivy_amd.detector.ospkg import detect, DetectError, UnsupportedOSError
-    eng = engine_factory(["ospkg/debian/debian.json", "ospkg/debian/data-source.json"])
+    fx = gt.fixture_files("debian", ["debian.yaml", "data-source.yaml"])
+    eng = _engine(fx)
     pkgs = [{"Name": "gpg-pubkey", "Version": "1", "SrcName": "apache2", "SrcVersion": "1.0"},
             {"Name": "htpasswd", "Version": "2.4.24", "SrcName": "apache2", "SrcVersion": "2.4.24"}]
-    vulns, eosl = detect(eng, "debian", "9.1", None, pkgs, now=parse_now("2020-01-01T00:00:00Z"))
+    vulns, eosl = detect(eng, "debian", "9.1", None, pkgs, now=gt.parse_now("2020-01-01T00:00:00Z"))
     assert {v["PkgName"] for v in vulns} == {"htpasswd"}
     assert sorted(v["VulnerabilityID"] for v in vulns) == ["CVE-2020-11985", "CVE-2021-31618"]
     assert eosl is False
-    _, eosl = detect(eng, "debian", "9.1", None, pkgs, now=parse_now("2023-01-01T00:00:00Z"))
+    _, eosl = detect(eng, "debian", "9.1", None, pkgs, now=gt.parse_now("2023-01-01T00:00:00Z"))
     assert eosl is True
     with pytest.raises(UnsupportedOSError):
         detect(eng, "plan9", "1", None, pkgs)
-    bad = engine_factory(["ospkg/debian/invalid.json", "ospkg/debian/data-source.json"])
+    bad = _engine(gt.fixture_files("debian", ["invalid.yaml", "data-source.yaml"]))
     with pytest.raises(DetectError, match="failed detection: failed to get debian advisories: failed to unmarshal"):
         detect(bad, "debian", "9.1", None, pkgs[1:])
 
 
-def test_debian_parse_error_skips_before_lookup(engine_factory):
+def test_debian_parse_error_skips_before_lookup():
     """debian.go:66-70: an unparsable installed version never reaches the (poisoned) bucket."""
     from trivy_amd.detector.ospkg import Scanner
-    eng = engine_factory(["ospkg/debian/invalid.json", "ospkg/debian/data-source.json"])
+    eng = _engine(gt.fixture_files("debian", ["invalid.yaml", "data-source.yaml"]))
     pkgs = [{"Name": "htpasswd", "Version": "x", "SrcName": "apache2", "SrcVersion": "not-a-version"}]
     assert Scanner(eng, "debian").detect("9.1", None, pkgs) == []
 
 
-def test_oracle_agrees_on_golden_cases(engine_factory, oracle_built):
+def test_lookup_first_drivers_raise_for_unparsable_packages():
+    """alpine.go:88-97: the lookup (and its decode error) precedes the installed parse."""
+    from trivy_amd.detector.ospkg import Scanner, DetectError
+    eng = _engine(gt.fixture_files("alpine", ["invalid.yaml", "data-source.yaml"]))
+    pkgs = [{"Name": "jq", "Version": "invalid", "SrcName": "jq", "SrcVersion": "invalid"}]
+    with pytest.raises(DetectError, match="failed to get alpine advisories"):
+        Scanner(eng, "alpine").detect("3.10.2", None, pkgs)
+
+
+def test_oracle_agrees_on_golden_cases(oracle_built):
     """The Python oracle drivers and the GPU path agree on every golden case."""
     import oracle.drivers as od
     from trivy_amd.detector.ospkg import Scanner
-    from conftest import fixture_paths
-    for driver in ["debian", "ubuntu"]:
-        for case in load_case_file(driver)["detect"]:
-            if case.get("want_err"):
-                continue
-            rec = od.Records.from_files(fixture_paths(case["fixtures"]))
-            now = parse_now(case["now"]) if "now" in case else None
-            want = (od.debian_detect(rec, case["os_ver"], case["pkgs"]) if driver == "debian"
-                    else od.ubuntu_detect(rec, case["os_ver"], case["pkgs"], now))
-            got = Scanner(engine_factory(case["fixtures"]), driver).detect(case["os_ver"], None, case["pkgs"], now=now)
-            assert canon(got) == canon(want)
+    for cid, fixtures, family, os_ver, repo, pkgs, want, want_err, now in _DETECT:
+        if want_err is not None:
+            continue
+        rec = od.Records.from_files(fixtures)
+        ref = od.driver_detect(family, os_ver, repo, pkgs, rec, now)
+        got = Scanner(_engine(fixtures), family).detect(os_ver, repo, pkgs, now=now)
+        assert canon(got) == canon(ref), cid

@@ -6,7 +6,7 @@ driver test tables (tests/golden/) and require the exact expected results.
 """
 import pytest
 
-from conftest import load_case_file, fixture_paths, parse_now, canon
+from conftest import canon
 
 import oracle.drivers as od
 

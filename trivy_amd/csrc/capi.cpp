@@ -292,12 +292,11 @@ tvm_batch* tvm_batch_new(void) { return new tvm_batch(); }
 void tvm_batch_free(tvm_batch* b) {
   if (!b) return;
   if (b->uploaded) {
-    hipSetDevice(b->device);
-    hipFree(b->dev.desc);
-    hipFree(b->dev.arena);
-    (void)hipFree(b->m.pairs);
-    (void)hipFree(b->m.dir);
-    (void)hipFree(b->m.ctl);
+    (void)hipSetDevice(b->device);
+    for (void* p : {static_cast<void*>(b->dev.desc), static_cast<void*>(b->dev.arena), static_cast<void*>(b->dev.attr),
+                    static_cast<void*>(b->dev.cpe_bits), static_cast<void*>(b->m.pairs), static_cast<void*>(b->m.dir),
+                    static_cast<void*>(b->m.ctl)})
+      if (p) (void)hipFree(p);
   }
   delete b;
 }
@@ -366,7 +365,7 @@ int tvm_engine_sync(tvm_engine* e, char* err, size_t errlen) {
 int tvm_match_status(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* err_pkg, uint64_t* err_bits) {
   if (!e || !b || !b->uploaded) return TVM_EINVAL;
   unsigned long long ctl[8];
-  hipSetDevice(e->device);
+  (void)hipSetDevice(e->device);
   if (hipMemcpy(ctl, b->m.ctl, sizeof(ctl), hipMemcpyDeviceToHost) != hipSuccess) return TVM_EDEVICE;
   if (n_matches) *n_matches = ctl[0];
   if (err_pkg) *err_pkg = ctl[1] ? int64_t(b->dev.n - ctl[1]) : -1;
@@ -391,26 +390,30 @@ int tvm_match_fetch(tvm_engine* e, tvm_batch* b, uint32_t* pairs, uint64_t cap, 
 }
 
 int tvm_match_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err, size_t errlen) {
-  if (!e || !b || !b->uploaded || steps <= 0) return TVM_EINVAL;
-  hipSetDevice(e->device);
-  hipEvent_t t0, t1;
-  hipEventCreate(&t0);
-  hipEventCreate(&t1);
+  if (!e || !b || !b->uploaded || steps <= 0 || !ms) return TVM_EINVAL;
+  (void)hipSetDevice(e->device);
+  hipEvent_t t0 = nullptr, t1 = nullptr;
   hipStream_t st = e->eng->stream();
-  hipEventRecord(t0, st);
   std::string msg;
-  for (int i = 0; i < steps; i++) {
-    if (!e->eng->launch(b->dev, b->m, st, msg)) {
-      set_err(err, errlen, msg);
-      return TVM_EDEVICE;
-    }
+  int rc = TVM_OK;
+  if (hipEventCreate(&t0) != hipSuccess || hipEventCreate(&t1) != hipSuccess || hipEventRecord(t0, st) != hipSuccess) {
+    msg = "hipEvent setup failed";
+    rc = TVM_EDEVICE;
   }
-  hipEventRecord(t1, st);
-  hipEventSynchronize(t1);
+  for (int i = 0; rc == TVM_OK && i < steps; i++)
+    if (!e->eng->launch(b->dev, b->m, st, msg)) rc = TVM_EDEVICE;
   float f = 0;
-  hipEventElapsedTime(&f, t0, t1);
-  hipEventDestroy(t0);
-  hipEventDestroy(t1);
+  if (rc == TVM_OK && (hipEventRecord(t1, st) != hipSuccess || hipEventSynchronize(t1) != hipSuccess ||
+                       hipEventElapsedTime(&f, t0, t1) != hipSuccess)) {
+    msg = "hipEvent timing failed";
+    rc = TVM_EDEVICE;
+  }
+  if (t0) (void)hipEventDestroy(t0);
+  if (t1) (void)hipEventDestroy(t1);
+  if (rc != TVM_OK) {
+    set_err(err, errlen, msg);
+    return rc;
+  }
   *ms = f;
   return TVM_OK;
 }

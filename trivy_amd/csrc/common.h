@@ -15,6 +15,8 @@ namespace tvm {
 enum Cmp : uint8_t {
   CMP_NONE = 0,
   CMP_DEB = 1,   // knqyf263/go-deb-version (debian, ubuntu, amazon)
+  CMP_APK = 2,   // knqyf263/go-apk-version (alpine, wolfi, chainguard)
+  CMP_RPM = 3,   // knqyf263/go-rpm-version (redhat/centos, alma, rocky, oracle, suse, photon, mariner)
 };
 
 // Driver families (reference pkg/detector/ospkg/detect.go:32-48 and library/driver.go:25-93).
@@ -23,6 +25,16 @@ enum Drv : uint8_t {
   DRV_DEBIAN = 1,
   DRV_UBUNTU = 2,
   DRV_AMAZON = 3,
+  DRV_ALPINE = 4,
+  DRV_WOLFI = 5,
+  DRV_CHAINGUARD = 6,
+  DRV_REDHAT = 7,
+  DRV_ALMA = 8,
+  DRV_ROCKY = 9,
+  DRV_ORACLE = 10,
+  DRV_SUSE = 11,
+  DRV_PHOTON = 12,
+  DRV_MARINER = 13,
 };
 
 // Per-platform flags (device-visible).
@@ -50,8 +62,30 @@ enum : uint16_t {
 };
 enum : uint32_t {
   ROW_ALWAYS = 1u << 31, // in Row::adv: matches even when the installed version fails to parse
-  ROW_ADV_MASK = 0x7FFFFFFFu,
+  ROW_FILTER = 1u << 30, // in Row::adv: also test the package against RowAux (arch / CPE / tag)
+  ROW_ADV_MASK = 0x3FFFFFFFu,
 };
+
+// Per-(package, advisory) predicates beyond the version interval, read only for rows
+// flagged ROW_FILTER (rows[] and aux[] are parallel arrays):
+//   AUX_ARCH_RH   redhat.go:129-135: pass if no arches, or the package is noarch, or its
+//                 arch is listed;
+//   AUX_ARCH_IN   trivy-db rocky Get: pass only if the package arch is listed;
+//   AUX_CPE       trivy-db redhat-oval Get: pass if one of the entry's affected CPE indices
+//                 is in the package's CPE set (content sets + NVR, resolved on the host);
+//   AUX_TAG       oracle.go:65-69: the advisory's ksplice tag equals the package's.
+struct alignas(16) RowAux {
+  uint32_t kind;
+  uint32_t tag;
+  uint32_t list_off;  // into aux_ids: n_arch arch ids, then n_cpe CPE indices
+  uint16_t n_arch;
+  uint16_t n_cpe;
+};
+enum : uint32_t { AUX_ARCH_RH = 1, AUX_ARCH_IN = 2, AUX_CPE = 4, AUX_TAG = 8 };
+
+// Package attributes (uint2 per package, only for batches that carry filtered rows):
+// x = arch id | PA_NOARCH, y = ksplice tag (oracle) or CPE-set id (redhat).
+enum : uint32_t { PA_NOARCH = 1u << 31, PA_ARCH_MASK = 0x7FFFFFFFu, PA_ARCH_NONE = 0x7FFFFFFFu };
 
 // Platform descriptor (device-visible).
 struct alignas(8) PlatInfo {

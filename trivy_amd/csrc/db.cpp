@@ -14,11 +14,22 @@ struct VecSink {
   void put(uint8_t b) { v->push_back(b); }
 };
 
+const char* kind_name(const JVal& v) {
+  switch (v.kind) {
+    case JVal::Arr: return "array";
+    case JVal::Obj: return "object";
+    case JVal::Num: return "number";
+    case JVal::Bool: return "bool";
+    case JVal::Str: return "string";
+    default: return "null";
+  }
+}
+
 bool dec_string(const JVal& v, std::string& out, const char* field, std::string& err) {
   if (v.kind == JVal::Null) return true;
   if (v.kind != JVal::Str) {
-    err = std::string("json: cannot unmarshal ") + (v.kind == JVal::Arr ? "array" : v.kind == JVal::Obj ? "object" : v.kind == JVal::Num ? "number" : "bool") +
-          " into Go struct field Advisory." + field + " of type string";
+    err = std::string("json: cannot unmarshal ") + kind_name(v) + " into Go struct field Advisory." + field +
+          " of type string";
     return false;
   }
   out = v.s;
@@ -28,14 +39,16 @@ bool dec_string(const JVal& v, std::string& out, const char* field, std::string&
 bool dec_strings(const JVal& v, std::vector<std::string>& out, const char* field, std::string& err) {
   if (v.kind == JVal::Null) { out.clear(); return true; }
   if (v.kind != JVal::Arr) {
-    err = std::string("json: cannot unmarshal into Go struct field Advisory.") + field + " of type []string";
+    err = std::string("json: cannot unmarshal ") + kind_name(v) + " into Go struct field Advisory." + field +
+          " of type []string";
     return false;
   }
   out.clear();
   for (const JVal& e : v.arr) {
     if (e.kind == JVal::Null) { out.emplace_back(); continue; }
     if (e.kind != JVal::Str) {
-      err = std::string("json: cannot unmarshal into Go struct field Advisory.") + field + " of type string";
+      err = std::string("json: cannot unmarshal ") + kind_name(e) + " into Go struct field Advisory." + field +
+            " of type string";
       return false;
     }
     out.push_back(e.s);
@@ -46,9 +59,24 @@ bool dec_strings(const JVal& v, std::vector<std::string>& out, const char* field
 bool dec_int(const JVal& v, int64_t& out, const char* field, std::string& err) {
   if (v.kind == JVal::Null) return true;
   if (!json_int(v, out)) {
-    err = std::string("json: cannot unmarshal ") + (v.kind == JVal::Num ? "number " + v.s : std::string("value")) +
+    err = std::string("json: cannot unmarshal ") + (v.kind == JVal::Num ? "number " + v.s : std::string(kind_name(v))) +
           " into Go struct field Advisory." + field + " of type int";
     return false;
+  }
+  return true;
+}
+
+bool dec_ints(const JVal& v, std::vector<int64_t>& out, const char* field, std::string& err) {
+  out.clear();
+  if (v.kind == JVal::Null) return true;
+  if (v.kind != JVal::Arr) {
+    err = std::string("json: cannot unmarshal ") + kind_name(v) + " into Go struct field " + field + " of type []int";
+    return false;
+  }
+  for (const JVal& e : v.arr) {
+    int64_t x = 0;
+    if (e.kind != JVal::Null && !dec_int(e, x, field, err)) return false;
+    out.push_back(x);
   }
   return true;
 }
@@ -74,14 +102,12 @@ bool dec_source(const JVal& v, DataSource& ds, std::string& err) {
   return true;
 }
 
-}  // namespace
+bool decode_adv_value(const JVal& v, Advisory& a, std::string& err);
 
-bool decode_advisory(std::string_view json, Advisory& a, std::string& err) {
-  JVal v;
-  if (!json_parse(json, v, err)) return false;
+bool decode_adv_value(const JVal& v, Advisory& a, std::string& err) {
   if (v.kind == JVal::Null) return true;
   if (v.kind != JVal::Obj) {
-    err = "json: cannot unmarshal into Go value of type types.Advisory";
+    err = std::string("json: cannot unmarshal ") + kind_name(v) + " into Go value of type types.Advisory";
     return false;
   }
   for (const auto& [k, x] : v.obj) {
@@ -109,9 +135,128 @@ bool decode_advisory(std::string_view json, Advisory& a, std::string& err) {
       if (x.kind != JVal::Null) ok = a.has_inline_source = dec_source(x, a.inline_source, err);
     }
     else if (json_key_eq(k, "Custom")) a.custom = x.kind == JVal::Null ? std::string() : std::string(x.raw);
+    else if (json_key_eq(k, "Entries")) {
+      a.entries.clear();
+      if (x.kind == JVal::Null) continue;
+      if (x.kind != JVal::Arr) {
+        err = std::string("json: cannot unmarshal ") + kind_name(x) + " into Go struct field Advisory.Entries";
+        return false;
+      }
+      for (const JVal& e : x.arr) {
+        Advisory sub;
+        if (!decode_adv_value(e, sub, err)) return false;
+        a.entries.push_back(std::move(sub));
+      }
+    }
     if (!ok) return false;
   }
   return true;
+}
+
+// trivy-db redhat-oval value: {Entries: [{FixedVersion, Affected: [int], Arches, Status,
+// Cves: [{ID, Severity}]}]} (fixture pkg/detector/ospkg/redhat/testdata/fixtures/redhat.yaml).
+struct RhCve {
+  std::string id;
+  int64_t severity = 0;
+};
+struct RhEntry {
+  std::string fixed;
+  std::vector<int64_t> affected;
+  std::vector<std::string> arches;
+  int64_t status = 0;
+  std::vector<RhCve> cves;
+};
+
+bool decode_redhat(std::string_view text, std::vector<RhEntry>& out, std::string& err) {
+  JVal v;
+  if (!json_parse(text, v, err)) return false;
+  out.clear();
+  if (v.kind == JVal::Null) return true;
+  if (v.kind != JVal::Obj) {
+    err = std::string("json: cannot unmarshal ") + kind_name(v) + " into Go value of type redhatoval.Advisory";
+    return false;
+  }
+  for (const auto& [k, ents] : v.obj) {
+    if (!json_key_eq(k, "Entries")) continue;
+    out.clear();
+    if (ents.kind == JVal::Null) continue;
+    if (ents.kind != JVal::Arr) {
+      err = std::string("json: cannot unmarshal ") + kind_name(ents) +
+            " into Go struct field Advisory.Entries of type []redhatoval.Entry";
+      return false;
+    }
+    for (const JVal& e : ents.arr) {
+      RhEntry re;
+      if (e.kind != JVal::Null) {
+        if (e.kind != JVal::Obj) {
+          err = std::string("json: cannot unmarshal ") + kind_name(e) + " into Go value of type redhatoval.Entry";
+          return false;
+        }
+        for (const auto& [ek, x] : e.obj) {
+          bool ok = true;
+          if (json_key_eq(ek, "FixedVersion")) ok = dec_string(x, re.fixed, "FixedVersion", err);
+          else if (json_key_eq(ek, "Affected")) ok = dec_ints(x, re.affected, "Entry.Affected", err);
+          else if (json_key_eq(ek, "Arches")) ok = dec_strings(x, re.arches, "Arches", err);
+          else if (json_key_eq(ek, "Status")) ok = dec_int(x, re.status, "Status", err);
+          else if (json_key_eq(ek, "Cves")) {
+            re.cves.clear();
+            if (x.kind == JVal::Null) continue;
+            if (x.kind != JVal::Arr) {
+              err = std::string("json: cannot unmarshal ") + kind_name(x) + " into Go struct field Entry.Cves";
+              return false;
+            }
+            for (const JVal& c : x.arr) {
+              RhCve rc;
+              if (c.kind != JVal::Null) {
+                if (c.kind != JVal::Obj) {
+                  err = std::string("json: cannot unmarshal ") + kind_name(c) + " into Go value of type redhatoval.CveEntry";
+                  return false;
+                }
+                for (const auto& [ck, cx] : c.obj) {
+                  if (json_key_eq(ck, "ID")) ok = dec_string(cx, rc.id, "ID", err);
+                  else if (json_key_eq(ck, "Severity")) ok = dec_int(cx, rc.severity, "Severity", err);
+                  if (!ok) return false;
+                }
+              }
+              re.cves.push_back(std::move(rc));
+            }
+          }
+          if (!ok) return false;
+        }
+      }
+      out.push_back(std::move(re));
+    }
+  }
+  return true;
+}
+
+bool decode_int_list(std::string_view text, std::vector<int64_t>& out) {
+  JVal v;
+  std::string err;
+  if (!json_parse(text, v, err)) return false;
+  return dec_ints(v, out, "[]int", err);
+}
+
+}  // namespace
+
+bool decode_advisory(std::string_view json, Advisory& a, std::string& err) {
+  JVal v;
+  if (!json_parse(json, v, err)) return false;
+  return decode_adv_value(v, a, err);
+}
+
+std::string extract_ksplice(std::string_view v) {
+  std::string low(v);
+  for (char& c : low)
+    if (c >= 'A' && c <= 'Z') c = char(c - 'A' + 'a');
+  size_t b = 0;
+  for (;;) {
+    size_t e = low.find('.', b);
+    std::string_view seg = std::string_view(low).substr(b, e == std::string::npos ? std::string::npos : e - b);
+    if (seg.rfind("ksplice", 0) == 0) return std::string(seg);
+    if (e == std::string::npos) return "";
+    b = e + 1;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -125,10 +270,23 @@ void DB::put(const std::vector<std::string>& path, std::string_view value) {
 
 bool classify_os_bucket(std::string_view root, uint8_t& drv, uint8_t& cmp, uint32_t& flags) {
   auto starts = [&](const char* p) { return root.rfind(p, 0) == 0; };
-  flags = 0;
-  if (starts("debian ")) { drv = DRV_DEBIAN; cmp = CMP_DEB; return true; }
-  if (starts("ubuntu ")) { drv = DRV_UBUNTU; cmp = CMP_DEB; flags = PLAT_LOOKUP_FIRST; return true; }
-  if (starts("amazon linux ")) { drv = DRV_AMAZON; cmp = CMP_DEB; flags = PLAT_LOOKUP_FIRST; return true; }
+  // Lookup-first drivers run vs.Get before parsing the installed version, so a poisoned
+  // key fails the call even for an unparsable package (ubuntu.go:86-96, amazon.go:57-71,
+  // alpine.go:88-97, wolfi.go:37-49); rpm versions never fail to parse.
+  flags = PLAT_LOOKUP_FIRST;
+  if (starts("debian ")) { drv = DRV_DEBIAN; cmp = CMP_DEB; flags = 0; return true; }
+  if (starts("ubuntu ")) { drv = DRV_UBUNTU; cmp = CMP_DEB; return true; }
+  if (starts("amazon linux ")) { drv = DRV_AMAZON; cmp = CMP_DEB; return true; }
+  if (starts("alpine ")) { drv = DRV_ALPINE; cmp = CMP_APK; return true; }
+  if (root == "wolfi") { drv = DRV_WOLFI; cmp = CMP_APK; return true; }
+  if (root == "chainguard") { drv = DRV_CHAINGUARD; cmp = CMP_APK; return true; }
+  if (root == "Red Hat") { drv = DRV_REDHAT; cmp = CMP_RPM; return true; }
+  if (starts("alma ")) { drv = DRV_ALMA; cmp = CMP_RPM; return true; }
+  if (starts("rocky ")) { drv = DRV_ROCKY; cmp = CMP_RPM; return true; }
+  if (starts("Oracle Linux ")) { drv = DRV_ORACLE; cmp = CMP_RPM; return true; }
+  if (starts("SUSE Linux Enterprise ") || starts("openSUSE Leap ")) { drv = DRV_SUSE; cmp = CMP_RPM; return true; }
+  if (starts("Photon OS ")) { drv = DRV_PHOTON; cmp = CMP_RPM; return true; }
+  if (starts("CBL-Mariner ")) { drv = DRV_MARINER; cmp = CMP_RPM; return true; }
   return false;
 }
 
@@ -150,6 +308,39 @@ int32_t DB::find_key(uint32_t plat, std::string_view name) const {
   return -1;
 }
 
+std::vector<int64_t> DB::redhat_cpes(const std::vector<std::string_view>& repos,
+                                     const std::vector<std::string_view>& nvrs) const {
+  std::vector<int64_t> out;
+  auto add = [&](const std::unordered_map<std::string, std::vector<int64_t>>& m, std::string_view k) {
+    auto it = m.find(std::string(k));
+    if (it == m.end()) return;
+    for (int64_t c : it->second)
+      if (std::find(out.begin(), out.end(), c) == out.end()) out.push_back(c);
+  };
+  for (std::string_view r : repos) add(rh_repo_, r);
+  for (std::string_view n : nvrs) add(rh_nvr_, n);
+  return out;
+}
+
+uint32_t DB::arch_id(std::string_view arch) const {
+  auto it = arch_ids_.find(std::string(arch));
+  return it == arch_ids_.end() ? PA_ARCH_NONE : it->second;
+}
+
+uint32_t DB::ksplice_id(std::string_view tag) const {
+  if (tag.empty()) return 0;
+  auto it = ksplice_ids_.find(std::string(tag));
+  return it == ksplice_ids_.end() ? 0xFFFFFFFFu : it->second;
+}
+
+uint32_t DB::intern_arch(const std::string& a) {
+  auto it = arch_ids_.find(a);
+  if (it != arch_ids_.end()) return it->second;
+  const uint32_t id = uint32_t(arch_ids_.size());
+  arch_ids_.emplace(a, id);
+  return id;
+}
+
 uint32_t DB::intern_key(const std::vector<uint8_t>& k) {
   std::string s(k.begin(), k.end());
   auto it = key_dedup_.find(s);
@@ -163,18 +354,43 @@ uint32_t DB::intern_key(const std::vector<uint8_t>& k) {
 }
 
 void DB::flatten_os(uint32_t plat, const Bucket& root, int32_t ds) {
+  const Platform& P = plats[plat];
   for (const auto& [pkg, bkt] : root.sub) {
     Key key;
     key.plat = plat;
     key.name = pkg;
+    auto poison = [&](const std::string& e) {
+      if (!key.poisoned) key.err = "failed to unmarshal advisory JSON: " + e;
+      key.poisoned = true;
+    };
     for (const auto& [vid, val] : bkt.kv) {
-      Advisory a;
       std::string err;
-      if (!decode_advisory(val, a, err)) {
-        if (!key.poisoned) key.err = "failed to unmarshal advisory JSON: " + err;
-        key.poisoned = true;
+      if (P.drv == DRV_REDHAT) {
+        // trivy-db redhat-oval Get: one advisory per (entry, CVE); CPE filtering per package
+        std::vector<RhEntry> ents;
+        if (!decode_redhat(val, ents, err)) { poison(err); continue; }
+        for (const RhEntry& e : ents) {
+          for (const RhCve& c : e.cves) {
+            Advisory a;
+            a.severity = c.severity;
+            a.fixed = e.fixed;
+            a.arches = e.arches;
+            a.status = e.status;
+            a.cpes = e.affected;
+            if (vid.rfind("CVE-", 0) == 0) {
+              a.vuln_id = vid;
+            } else {
+              a.vuln_id = c.id;
+              a.vendor_ids = {vid};
+            }
+            key.advs.push_back(uint32_t(advs.size()));
+            advs.push_back(std::move(a));
+          }
+        }
         continue;
       }
+      Advisory a;
+      if (!decode_advisory(val, a, err)) { poison(err); continue; }
       a.vuln_id = vid;
       // trivy-db GetAdvisories: the data-source bucket entry wins when non-empty,
       // otherwise the value's own DataSource (if any) stays.
@@ -184,6 +400,21 @@ void DB::flatten_os(uint32_t plat, const Bucket& root, int32_t ds) {
         sources.push_back(a.inline_source);
         a.data_source = int32_t(sources.size() - 1);
       }
+      if (P.drv == DRV_ROCKY && !a.entries.empty()) {
+        // trivy-db rocky Get(release, name, arch): one advisory per arch entry
+        for (const Advisory& e : a.entries) {
+          Advisory b = a;
+          b.entries.clear();
+          b.fixed = e.fixed;
+          b.vendor_ids = e.vendor_ids;
+          b.arches = e.arches;
+          b.arch_entry = true;
+          key.advs.push_back(uint32_t(advs.size()));
+          advs.push_back(std::move(b));
+        }
+        continue;
+      }
+      a.entries.clear();
       key.advs.push_back(uint32_t(advs.size()));
       advs.push_back(std::move(a));
     }
@@ -192,44 +423,126 @@ void DB::flatten_os(uint32_t plat, const Bucket& root, int32_t ds) {
   }
 }
 
+// Advisory -> interval row(s) of its driver (SURVEY.md §8a' "unfixed" and parse-error
+// columns).  Returns false when the advisory can never be reported (no row).
+bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::vector<uint8_t>& kb) {
+  Row r{};
+  r.adv = ai;
+  r.lo_len = KEY_INF;
+  r.hi_len = KEY_INF;
+  auto encode = [&](const std::string& v, uint32_t& off, uint16_t& len) {
+    kb.clear();
+    VecSink s{&kb};
+    if (!encode_version(P.cmp, reinterpret_cast<const uint8_t*>(v.data()), uint32_t(v.size()), s)) return false;
+    off = intern_key(kb);
+    len = uint16_t(kb.size());
+    return true;
+  };
+  auto set_hi = [&](const std::string& v) {
+    if (!encode(v, r.hi_off, r.hi_len)) return false;
+    for (size_t i = 0; i < kb.size() && i < 16; i++) (i < 8 ? r.hi_pre0 : r.hi_pre1) |= uint64_t(kb[i]) << (8 * (i % 8));
+    return true;
+  };
+  RowAux x{};
+  switch (P.drv) {
+    case DRV_DEBIAN:
+    case DRV_UBUNTU:
+    case DRV_MARINER:
+      // debian.go:99-102, ubuntu.go:110-113, mariner.go:62-66: unfixed is reported;
+      // an unparsable fixed version skips the advisory
+      if (!a.fixed.empty() && !set_hi(a.fixed)) return false;
+      break;
+    case DRV_AMAZON:
+    case DRV_WOLFI:
+    case DRV_CHAINGUARD:
+      // amazon.go:73-77, wolfi.go:66-71: the fixed version must parse ("" does not for dpkg)
+      if (!set_hi(a.fixed)) return false;
+      break;
+    case DRV_ALPINE:
+      // alpine.go:122-153: installed >= AffectedVersion when set; unfixed reported
+      if (!a.affected.empty()) {
+        uint16_t l = 0;
+        if (!encode(a.affected, r.lo_off, l)) return false;
+        r.lo_len = uint16_t(l | KEY_INCL);
+      }
+      if (!a.fixed.empty() && !set_hi(a.fixed)) return false;
+      break;
+    case DRV_REDHAT:
+      // redhat.go:146-180: unfixed (first one wins, merged on the host) or installed < fixed
+      if (!a.fixed.empty()) set_hi(a.fixed);
+      if (!a.arches.empty()) x.kind |= AUX_ARCH_RH;
+      x.kind |= AUX_CPE;
+      break;
+    case DRV_ROCKY:
+      set_hi(a.fixed);
+      if (a.arch_entry) x.kind |= AUX_ARCH_IN;
+      break;
+    case DRV_ORACLE: {
+      // oracle.go:65-69: skip unless the ksplice tags agree
+      set_hi(a.fixed);
+      x.kind |= AUX_TAG;
+      const std::string t = extract_ksplice(a.fixed);
+      if (t.empty()) {
+        x.tag = 0;
+      } else {
+        auto it = ksplice_ids_.find(t);
+        if (it == ksplice_ids_.end()) it = ksplice_ids_.emplace(t, uint32_t(ksplice_ids_.size() + 1)).first;
+        x.tag = it->second;
+      }
+      break;
+    }
+    case DRV_ALMA:
+    case DRV_SUSE:
+    case DRV_PHOTON:
+      set_hi(a.fixed);  // rpm never fails; "" parses to the smallest version
+      break;
+    default:
+      return false;
+  }
+  if (r.hi_len != KEY_INF) r.hi_len = uint16_t(r.hi_len & KEY_LEN_MASK);
+  if (x.kind) {
+    r.adv |= ROW_FILTER;
+    x.list_off = uint32_t(aux_ids.size());
+    if (x.kind & (AUX_ARCH_RH | AUX_ARCH_IN)) {
+      for (const std::string& s : a.arches) aux_ids.push_back(intern_arch(s));
+      x.n_arch = uint16_t(a.arches.size());
+    }
+    if (x.kind & AUX_CPE) {
+      for (int64_t c : a.cpes) {
+        aux_ids.push_back(c < 0 || c >= int64_t(0xFFFFFFFF) ? 0xFFFFFFFFu : uint32_t(c));
+        if (c >= 0 && c < int64_t(1) << 24) n_cpe = std::max<uint32_t>(n_cpe, uint32_t(c) + 1);
+      }
+      x.n_cpe = uint16_t(a.cpes.size());
+    }
+    has_filters = true;
+  }
+  rows.push_back(r);
+  aux.push_back(x);
+  return true;
+}
+
 void DB::build_index() {
   // rows + key arena
   rows.clear();
+  aux.clear();
+  aux_ids.clear();
   std::vector<uint8_t> kb;
   std::vector<uint32_t> row_begin(keys.size()), row_count(keys.size());
   for (size_t k = 0; k < keys.size(); k++) {
     const Key& key = keys[k];
     const Platform& P = plats[key.plat];
     row_begin[k] = uint32_t(rows.size());
-    for (uint32_t ai : key.advs) {
-      const Advisory& a = advs[ai];
-      Row r{};
-      r.adv = ai;
-      r.lo_len = KEY_INF;
-      if (P.cmp == CMP_DEB) {
-        if (a.fixed.empty()) {
-          // debian.go:99-102 / ubuntu.go:110-113: unfixed is always reported;
-          // amazon.go:73-77 parses "" and skips the advisory.
-          if (P.drv == DRV_AMAZON) continue;
-          r.hi_len = KEY_INF;
-        } else {
-          kb.clear();
-          VecSink s{&kb};
-          if (!deb_encode(reinterpret_cast<const uint8_t*>(a.fixed.data()), uint32_t(a.fixed.size()), s)) continue;
-          r.hi_off = intern_key(kb);
-          r.hi_len = uint16_t(kb.size());
-          for (size_t i = 0; i < kb.size() && i < 16; i++)
-            (i < 8 ? r.hi_pre0 : r.hi_pre1) |= uint64_t(kb[i]) << (8 * (i % 8));
-        }
-      } else {
-        continue;
-      }
-      rows.push_back(r);
-    }
+    for (uint32_t ai : key.advs) compile_rows(P, advs[ai], ai, kb);
     row_count[k] = uint32_t(rows.size()) - row_begin[k];
   }
   n_rows_total = rows.size();
   if (key_words.empty()) key_words.push_back(0);
+  if (aux_ids.empty()) aux_ids.push_back(0);
+  // CPE indices present only in the repository / nvr maps widen the bitset too
+  for (const auto* m : {&rh_repo_, &rh_nvr_})
+    for (const auto& [k, v] : *m)
+      for (int64_t c : v)
+        if (c >= 0 && c < int64_t(1) << 24) n_cpe = std::max<uint32_t>(n_cpe, uint32_t(c) + 1);
 
   // hash index, load factor <= 0.5
   uint64_t cap = 16;
@@ -282,6 +595,19 @@ bool DB::finalize(std::string& err) {
       }
       sources.push_back(ds);
       ds_of_root[root] = int32_t(sources.size() - 1);
+    }
+  }
+  // Red Hat CPE maps: "Red Hat CPE" -> "repository" | "nvr" -> key -> JSON []int
+  auto cpe = root_.sub.find("Red Hat CPE");
+  if (cpe != root_.sub.end()) {
+    for (const auto& [sub, dst] : {std::pair<const char*, decltype(&rh_repo_)>{"repository", &rh_repo_},
+                                   std::pair<const char*, decltype(&rh_repo_)>{"nvr", &rh_nvr_}}) {
+      auto b = cpe->second.sub.find(sub);
+      if (b == cpe->second.sub.end()) continue;
+      for (const auto& [k, v] : b->second.kv) {
+        std::vector<int64_t> ids;
+        if (decode_int_list(v, ids)) (*dst)[k] = std::move(ids);
+      }
     }
   }
   for (const auto& [name, b] : root_.sub) {

@@ -6,7 +6,7 @@
 // the reference opens the DB (pkg/commands/artifact/run.go:311 db.Init).
 //
 // Input: the bucket tree as (path..., key) -> JSON value records, exactly what a bbolt
-// walk (or bolt-fixtures YAML) produces.  Output: the device images in DeviceImage.
+// walk (or bolt-fixtures YAML) produces.  Output: the device images below.
 #pragma once
 #include <cstdint>
 #include <map>
@@ -24,9 +24,11 @@ struct DataSource {
   bool empty() const { return id.empty() && name.empty() && url.empty(); }
 };
 
-// trivy-db pkg/types.Advisory as decoded by json.Unmarshal (fields the detectors read).
+// One advisory as the reference driver sees it after trivy-db's Get: trivy-db
+// pkg/types.Advisory for most sources; for Red Hat one record per (entry, CVE) of the
+// redhat-oval value, for Rocky one per arch entry.
 struct Advisory {
-  std::string vuln_id;                 // from the bucket key
+  std::string vuln_id;                 // from the bucket key (or the CVE of a Red Hat entry)
   std::vector<std::string> vendor_ids;
   std::vector<std::string> arches;
   int64_t status = 0;
@@ -37,6 +39,9 @@ struct Advisory {
   std::string custom;                  // raw JSON text of Custom, "" = nil
   bool has_inline_source = false;      // DataSource present in the value JSON itself
   DataSource inline_source;
+  std::vector<Advisory> entries;       // Rocky: per-arch entries (types.Advisory.Entries)
+  std::vector<int64_t> cpes;           // Red Hat: the entry's affected CPE indices
+  bool arch_entry = false;             // Rocky: expanded from an arch entry (arch must be listed)
 };
 
 // Decodes one advisory value (Go json.Unmarshal into types.Advisory).
@@ -78,16 +83,28 @@ class DB {
   // Host-side lookup of a key index (used by drivers for error text); -1 if absent.
   int32_t find_key(uint32_t plat, std::string_view name) const;
 
+  // Red Hat CPE resolution (trivy-db RedHatRepoToCPEs / RedHatNVRToCPEs): the unique CPE
+  // indices of content sets + NVRs, in first-seen order.
+  std::vector<int64_t> redhat_cpes(const std::vector<std::string_view>& repos,
+                                   const std::vector<std::string_view>& nvrs) const;
+  uint32_t n_cpe = 0;  // 1 + the largest CPE index anywhere (bitset width)
+  // Arch / ksplice dictionaries for package attributes (PA_* in common.h).
+  uint32_t arch_id(std::string_view arch) const;    // PA_ARCH_NONE when no advisory lists it
+  uint32_t ksplice_id(std::string_view tag) const;  // 0 for "", 0xFFFFFFFF when unknown
+
   // ---- device images ----
   std::vector<uint64_t> slot_hash;
   std::vector<SlotVal> slot_val;
   std::vector<uint32_t> slot_key;   // host only: slot -> Key index
   std::vector<uint8_t> name_arena;
   std::vector<Row> rows;
+  std::vector<RowAux> aux;          // parallel to rows (read only for ROW_FILTER rows)
+  std::vector<uint32_t> aux_ids;
   std::vector<uint64_t> key_words;
   std::vector<PlatInfo> plat_info;
   uint64_t slot_mask = 0;
   uint64_t n_rows_total = 0;
+  bool has_filters = false;
 
   const Bucket& tree() const { return root_; }
 
@@ -95,12 +112,19 @@ class DB {
   Bucket root_;
   std::unordered_map<std::string, uint32_t> plat_by_name_;
   std::unordered_map<std::string, uint32_t> key_dedup_;  // encoded key bytes -> word offset
+  std::unordered_map<std::string, std::vector<int64_t>> rh_repo_, rh_nvr_;
+  std::unordered_map<std::string, uint32_t> arch_ids_, ksplice_ids_;
   uint32_t intern_key(const std::vector<uint8_t>& k);
+  uint32_t intern_arch(const std::string& a);
   void flatten_os(uint32_t plat, const Bucket& b, int32_t ds);
+  bool compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::vector<uint8_t>& kb);
   void build_index();
 };
 
 // Classifies a root bucket name into a driver family (OS buckets only).
 bool classify_os_bucket(std::string_view root, uint8_t& drv, uint8_t& cmp, uint32_t& flags);
+
+// oracle.go:101-109 extractKsplice: the lower-cased dot-segment starting "ksplice", or "".
+std::string extract_ksplice(std::string_view v);
 
 }  // namespace tvm

@@ -1,11 +1,18 @@
 // OS drivers (see drivers.h).  Field population per driver follows SURVEY.md §8a'.
+//
+// Each driver keeps the reference's per-target prologue (which root bucket, which name,
+// which formatted version, which packages are skipped before the lookup) and epilogue
+// (which DetectedVulnerability fields are set, Red Hat's per-CVE merge).  The
+// per-(package, advisory) loop runs in one GPU launch per call (Engine::match_host).
 #include "drivers.h"
 
 #include <algorithm>
 #include <cstdio>
+#include <functional>
 #include <map>
 
 #include "db.h"
+#include "verkey.h"
 
 namespace tvm {
 
@@ -42,6 +49,7 @@ int64_t eol_unix(int y, int m, int d) {
 namespace {
 
 const char* const kSeverity[] = {"UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"};
+const char* severity_name(int64_t s) { return (s >= 0 && s < 5) ? kSeverity[s] : kSeverity[0]; }
 
 struct Eol {
   const char* ver;
@@ -63,12 +71,194 @@ bool supported(const EolMap& eol, std::string_view ver, int64_t now) {
   return now < it->second;
 }
 
-// Runs the GPU match for one target: per package (name, version) or skipped.
+// ---- eolDates of each driver (<os>/<os>.go; transcribed data) ----------------------------
+const EolMap& debian_eol() {
+  static const EolMap m = make_eol(
+      {{"1.1", 1997, 6, 5}, {"1.2", 1998, 6, 5}, {"1.3", 1999, 3, 9}, {"2.0", 2000, 3, 9}, {"2.1", 2000, 10, 30},
+       {"2.2", 2003, 7, 30}, {"3.0", 2006, 6, 30}, {"3.1", 2008, 3, 30}, {"4.0", 2010, 2, 15}, {"5.0", 2012, 2, 6},
+       {"6.0", 2016, 2, 29}, {"7", 2018, 5, 31}, {"8", 2020, 6, 30}, {"9", 2022, 6, 30}, {"10", 2024, 6, 30},
+       {"11", 2026, 8, 14}, {"12", 2028, 6, 10}, {"13", 3000, 1, 1}});
+  return m;
+}
+const EolMap& ubuntu_eol() {
+  static const EolMap m = make_eol(
+      {{"4.10", 2006, 4, 30}, {"5.04", 2006, 10, 31}, {"5.10", 2007, 4, 13}, {"6.06", 2011, 6, 1},
+       {"6.10", 2008, 4, 25}, {"7.04", 2008, 10, 19}, {"7.10", 2009, 4, 18}, {"8.04", 2013, 5, 9},
+       {"8.10", 2010, 4, 30}, {"9.04", 2010, 10, 23}, {"9.10", 2011, 4, 29}, {"10.04", 2015, 4, 29},
+       {"10.10", 2012, 4, 10}, {"11.04", 2012, 10, 28}, {"11.10", 2013, 5, 9}, {"12.04", 2019, 4, 26},
+       {"12.04-ESM", 2019, 4, 28}, {"12.10", 2014, 5, 16}, {"13.04", 2014, 1, 27}, {"13.10", 2014, 7, 17},
+       {"14.04", 2022, 4, 25}, {"14.04-ESM", 2024, 4, 25}, {"14.10", 2015, 7, 23}, {"15.04", 2016, 1, 23},
+       {"15.10", 2016, 7, 22}, {"16.04", 2021, 4, 21}, {"16.04-ESM", 2026, 4, 29}, {"16.10", 2017, 7, 20},
+       {"17.04", 2018, 1, 13}, {"17.10", 2018, 7, 19}, {"18.04", 2023, 5, 31}, {"18.04-ESM", 2028, 3, 31},
+       {"18.10", 2019, 7, 18}, {"19.04", 2020, 1, 18}, {"19.10", 2020, 7, 17}, {"20.04", 2025, 4, 23},
+       {"20.10", 2021, 7, 22}, {"21.04", 2022, 1, 20}, {"21.10", 2022, 7, 14}, {"22.04", 2027, 4, 23},
+       {"22.10", 2023, 7, 20}, {"23.04", 2024, 1, 20}});
+  return m;
+}
+const EolMap& alpine_eol() {
+  static const EolMap m = [] {
+    EolMap t = make_eol(
+        {{"2.0", 2012, 4, 1}, {"2.1", 2012, 11, 1}, {"2.2", 2013, 5, 1}, {"2.3", 2013, 11, 1}, {"2.4", 2014, 5, 1},
+         {"2.5", 2014, 11, 1}, {"2.6", 2015, 5, 1}, {"2.7", 2015, 11, 1}, {"3.0", 2016, 5, 1}, {"3.1", 2016, 11, 1},
+         {"3.2", 2017, 5, 1}, {"3.3", 2017, 11, 1}, {"3.4", 2018, 5, 1}, {"3.5", 2018, 11, 1}, {"3.6", 2019, 5, 1},
+         {"3.7", 2019, 11, 1}, {"3.8", 2020, 5, 1}, {"3.9", 2020, 11, 1}, {"3.10", 2021, 5, 1},
+         {"3.11", 2021, 11, 1}, {"3.12", 2022, 5, 1}, {"3.13", 2022, 11, 1}, {"3.14", 2023, 5, 1},
+         {"3.15", 2023, 11, 1}, {"3.16", 2024, 5, 23}, {"3.17", 2024, 11, 22}, {"3.18", 2025, 5, 9},
+         {"3.19", 2025, 11, 1}});
+    t["edge"] = eol_unix(9999, 1, 1) - (23 * 3600 + 59 * 60 + 59);  // time.Date(9999,1,1,0,0,0)
+    return t;
+  }();
+  return m;
+}
+const EolMap& amazon_eol() {
+  static const EolMap m = make_eol({{"1", 2023, 12, 31}, {"2", 2025, 6, 30}, {"2023", 2028, 3, 15}});
+  return m;
+}
+const EolMap& redhat_eol() {
+  static const EolMap m = make_eol({{"4", 2017, 5, 31}, {"5", 2020, 11, 30}, {"6", 2024, 6, 30},
+                                    {"7", 3000, 1, 1}, {"8", 3000, 1, 1}, {"9", 3000, 1, 1}});
+  return m;
+}
+const EolMap& centos_eol() {
+  static const EolMap m = make_eol({{"3", 2010, 10, 31}, {"4", 2012, 2, 29}, {"5", 2017, 3, 31},
+                                    {"6", 2020, 11, 30}, {"7", 2024, 6, 30}, {"8", 2021, 12, 31}});
+  return m;
+}
+const EolMap& alma_eol() {
+  static const EolMap m = make_eol({{"8", 2029, 3, 1}, {"9", 2032, 5, 31}});
+  return m;
+}
+const EolMap& rocky_eol() {
+  static const EolMap m = make_eol({{"8", 2029, 5, 31}, {"9", 2032, 5, 31}});
+  return m;
+}
+const EolMap& oracle_eol() {
+  static const EolMap m = make_eol({{"3", 2011, 12, 31}, {"4", 2013, 12, 31}, {"5", 2017, 12, 31},
+                                    {"6", 2021, 3, 21}, {"7", 2024, 7, 23}, {"8", 2029, 7, 18}, {"9", 2032, 7, 18}});
+  return m;
+}
+const EolMap& photon_eol() {
+  static const EolMap m =
+      make_eol({{"1.0", 2022, 2, 28}, {"2.0", 2022, 12, 31}, {"3.0", 2024, 6, 30}, {"4.0", 2025, 12, 31}});
+  return m;
+}
+const EolMap& sles_eol() {
+  static const EolMap m = make_eol(
+      {{"10", 2007, 12, 31}, {"10.1", 2008, 11, 30}, {"10.2", 2010, 4, 11}, {"10.3", 2011, 10, 11},
+       {"10.4", 2013, 7, 31}, {"11", 2010, 12, 31}, {"11.1", 2012, 8, 31}, {"11.2", 2014, 1, 31},
+       {"11.3", 2016, 1, 31}, {"11.4", 2019, 3, 31}, {"12", 2016, 6, 30}, {"12.1", 2017, 5, 31},
+       {"12.2", 2018, 3, 31}, {"12.3", 2019, 1, 30}, {"12.4", 2020, 6, 30}, {"12.5", 2024, 10, 31},
+       {"15", 2019, 12, 31}, {"15.1", 2021, 1, 31}, {"15.2", 2021, 12, 31}, {"15.3", 2022, 12, 31},
+       {"15.4", 2023, 12, 31}, {"15.5", 2028, 12, 31}});
+  return m;
+}
+const EolMap& opensuse_eol() {
+  static const EolMap m = make_eol(
+      {{"42.1", 2017, 5, 17}, {"42.2", 2018, 1, 26}, {"42.3", 2019, 6, 30}, {"15.0", 2019, 12, 3},
+       {"15.1", 2020, 11, 30}, {"15.2", 2021, 11, 30}, {"15.3", 2022, 11, 30}, {"15.4", 2023, 11, 30},
+       {"15.5", 2024, 12, 31}});
+  return m;
+}
+
+// amazon.go:46-52: first field, major, anything but 2/2022/2023 is "1"
+std::string amazon_release(std::string_view os_ver) {
+  size_t b = os_ver.find_first_not_of(" \t\n\v\f\r");
+  std::string_view f = b == std::string_view::npos ? std::string_view() : os_ver.substr(b);
+  f = f.substr(0, f.find_first_of(" \t\n\v\f\r"));
+  std::string v = os_major(f);
+  if (v != "2" && v != "2022" && v != "2023") v = "1";
+  return v;
+}
+
+// ubuntu.go:136-151 versionFromEolDates (the reference reads time.Now(); we use `now`)
+std::string ubuntu_release(std::string_view os_ver, int64_t now) {
+  const EolMap& eol = ubuntu_eol();
+  if (eol.count(os_ver)) return std::string(os_ver);
+  std::string ver(os_ver);
+  while (!ver.empty() && std::string_view("-ESM").find(ver.back()) != std::string_view::npos) ver.pop_back();
+  auto it = eol.find(ver);
+  if (it != eol.end() && now < it->second) return ver;
+  return std::string(os_ver);
+}
+
+// alpine.go:155-169 repoRelease + the stream choice of Detect (alpine.go:67-83)
+std::string alpine_stream(std::string_view os_ver, const Repo* repo) {
+  std::string v = os_minor(os_ver);
+  std::string rr;
+  if (repo) {
+    rr = std::string(repo->release);
+    if (std::count(rr.begin(), rr.end(), '.') > 1) rr = rr.substr(0, rr.rfind('.'));
+  }
+  return (!rr.empty() && v != rr) ? rr : v;
+}
+
+// redhat.go:207-220 addModularNamespace
+std::string modular_name(std::string_view name, std::string_view label) {
+  int count = 0;
+  for (size_t i = 0; i < label.size(); i++) {
+    if (label[i] == ':') count++;
+    if (count == 2) return std::string(label.substr(0, i)) + "::" + std::string(name);
+  }
+  return std::string(name);
+}
+
+// go-rpm-version Version.String(): epoch dropped unless positive
+std::string rpm_string(std::string_view v) {
+  int64_t epoch = 0;
+  std::string_view rest = v;
+  size_t c = v.find(':');
+  if (c != std::string_view::npos) {
+    std::string_view e = v.substr(0, c);
+    size_t i = 0;
+    bool neg = false, ok = !e.empty();
+    if (!e.empty() && (e[0] == '+' || e[0] == '-')) {
+      neg = e[0] == '-';
+      i = 1;
+      ok = e.size() > 1;
+    }
+    uint64_t x = 0;
+    for (; ok && i < e.size(); i++) {
+      if (e[i] < '0' || e[i] > '9') { ok = false; break; }
+      const uint64_t d = uint64_t(e[i] - '0');
+      if (x > (uint64_t(INT64_MAX) - d) / 10) { ok = false; break; }
+      x = x * 10 + d;
+    }
+    epoch = ok ? (neg ? -int64_t(x) : int64_t(x)) : 0;
+    rest = v.substr(c + 1);
+  }
+  std::string out = epoch > 0 ? std::to_string(epoch) + ":" : std::string();
+  size_t d = rest.find('-');
+  out += std::string(rest.substr(0, d));
+  if (d != std::string_view::npos && d + 1 < rest.size()) {
+    out += '-';
+    out += std::string(rest.substr(d + 1));
+  }
+  return out;
+}
+
+struct VecSink {
+  std::vector<uint8_t>* v;
+  void put(uint8_t b) { v->push_back(b); }
+};
+
+// go-rpm-version a.LessThan(b), host side (sort keys, verkey.h)
+bool rpm_less(std::string_view a, std::string_view b) {
+  std::vector<uint8_t> ka, kb;
+  VecSink sa{&ka}, sb{&kb};
+  rpm_encode(reinterpret_cast<const uint8_t*>(a.data()), uint32_t(a.size()), sa);
+  rpm_encode(reinterpret_cast<const uint8_t*>(b.data()), uint32_t(b.size()), sb);
+  return std::lexicographical_compare(ka.begin(), ka.end(), kb.begin(), kb.end());
+}
+
+// ---- one GPU pass per Detect call ---------------------------------------------------------
 struct Plan {
   int32_t plat = -1;
   HostBatch batch;
   void add(bool skip, std::string_view name, std::string_view ver) {
     batch.add(skip || plat < 0 ? 0xFFFFFFFFu : uint32_t(plat), name, ver);
+  }
+  void add(bool skip, std::string_view name, std::string_view ver, uint2 a) {
+    batch.add(skip || plat < 0 ? 0xFFFFFFFFu : uint32_t(plat), name, ver, a);
   }
 };
 
@@ -86,38 +276,65 @@ bool run_plan(Engine& eng, const Plan& plan, std::vector<uint2>& pairs, std::str
   return true;
 }
 
-void fill_common(Vuln& v, const Advisory& a) {
-  v.vuln_id = a.vuln_id;
-  v.fixed = a.fixed;
-  v.data_source = a.data_source;
-  v.has_custom = !a.custom.empty();
-  v.custom = a.custom;
-}
+// ---- table-driven drivers ------------------------------------------------------------------
+enum NameSel { NAME_BIN, NAME_SRC, NAME_SRC_OR_BIN, NAME_MODULAR };
+enum VerSel { VER_BIN, VER_SRC };
+enum : uint32_t {
+  F_PKGID = 1,        // PkgID copied
+  F_CUSTOM = 2,       // Custom copied
+  F_DEBIAN = 4,       // VendorIDs, Status, package-specific severity (debian.go:84-98)
+  F_RPM_STRING = 8,   // FixedVersion = rpm Version.String()
+  F_KSPLICE = 16,     // package ksplice tag attribute (oracle)
+  F_ARCH = 32,        // package arch attribute (rocky)
+};
 
-// ---------------------------------------------------------------- debian.go ----------
-class Debian : public OsDriver {
-  EolMap eol_ = make_eol({{"1.1", 1997, 6, 5}, {"1.2", 1998, 6, 5}, {"1.3", 1999, 3, 9}, {"2.0", 2000, 3, 9},
-                          {"2.1", 2000, 10, 30}, {"2.2", 2003, 7, 30}, {"3.0", 2006, 6, 30}, {"3.1", 2008, 3, 30},
-                          {"4.0", 2010, 2, 15}, {"5.0", 2012, 2, 6}, {"6.0", 2016, 2, 29}, {"7", 2018, 5, 31},
-                          {"8", 2020, 6, 30}, {"9", 2022, 6, 30}, {"10", 2024, 6, 30}, {"11", 2026, 8, 14},
-                          {"12", 2028, 6, 10}, {"13", 3000, 1, 1}});
+struct Spec {
+  std::function<std::string(std::string_view os_ver, const Repo* repo, int64_t now)> bucket;
+  NameSel name;
+  VerSel ver;
+  uint32_t flags;
+  const char* err_prefix;
+  std::function<bool(const Pkg&)> skip;  // skipped before the lookup (no error possible)
+  std::function<bool(std::string_view family, std::string_view os_ver, int64_t now)> supported;
+};
+
+class TableDriver : public OsDriver {
+  Spec s_;
 
  public:
-  bool detect(Engine& eng, std::string_view os_ver, const Repo*, const std::vector<Pkg>& pkgs, int64_t,
+  explicit TableDriver(Spec s) : s_(std::move(s)) {}
+
+  bool detect(Engine& eng, std::string_view os_ver, const Repo* repo, const std::vector<Pkg>& pkgs, int64_t now,
               std::vector<Vuln>& out, std::string& err) const override {
     const DB& db = eng.db();
     Plan plan;
-    plan.plat = db.find_plat("debian " + os_major(os_ver));  // debian.go:60,72
-    std::vector<std::string> src(pkgs.size());
+    plan.plat = db.find_plat(s_.bucket(os_ver, repo, now));
+    std::vector<std::string> cmpv(pkgs.size()), names(pkgs.size());
     for (size_t i = 0; i < pkgs.size(); i++) {
-      src[i] = format_version(pkgs[i].src_epoch, pkgs[i].src_version, pkgs[i].src_release);
-      plan.add(false, pkgs[i].src_name, src[i]);
+      const Pkg& p = pkgs[i];
+      cmpv[i] = s_.ver == VER_SRC ? format_version(p.src_epoch, p.src_version, p.src_release)
+                                  : format_version(p.epoch, p.version, p.release);
+      switch (s_.name) {
+        case NAME_BIN: names[i] = std::string(p.name); break;
+        case NAME_SRC: names[i] = std::string(p.src_name); break;
+        case NAME_SRC_OR_BIN: names[i] = std::string(p.src_name.empty() ? p.name : p.src_name); break;
+        case NAME_MODULAR: names[i] = modular_name(p.name, p.modularitylabel); break;
+      }
+      const bool skip = s_.skip && s_.skip(p);
+      if (s_.flags & (F_KSPLICE | F_ARCH)) {
+        uint2 a = make_uint2(PA_ARCH_NONE, 0xFFFFFFFFu);
+        if (s_.flags & F_ARCH) a.x = db.arch_id(p.arch);
+        if (s_.flags & F_KSPLICE) a.y = db.ksplice_id(extract_ksplice(p.release));
+        plan.add(skip, names[i], cmpv[i], a);
+      } else {
+        plan.add(skip, names[i], cmpv[i]);
+      }
     }
     std::vector<uint2> pairs;
     std::string key_err;
     if (!run_plan(eng, plan, pairs, key_err, err)) return false;
     if (!key_err.empty()) {
-      err = "failed to get debian advisories: " + key_err;  // debian.go:73-75
+      err = std::string(s_.err_prefix) + key_err;
       return false;
     }
     for (const uint2& m : pairs) {
@@ -125,150 +342,213 @@ class Debian : public OsDriver {
       const Advisory& a = db.advs[m.y];
       Vuln v;
       v.pkg = m.x;
-      v.copy = COPY_PKG_ID | COPY_PKG_NAME | COPY_IDENTIFIER | COPY_LAYER;
-      fill_common(v, a);
-      v.vendor_ids = a.vendor_ids;
-      v.pkg_id = std::string(p.id);
+      v.copy = COPY_PKG_NAME | COPY_IDENTIFIER | COPY_LAYER | ((s_.flags & F_PKGID) ? COPY_PKG_ID : 0);
+      v.vuln_id = a.vuln_id;
+      v.data_source = a.data_source;
+      if (s_.flags & F_CUSTOM) {
+        v.has_custom = !a.custom.empty();
+        v.custom = a.custom;
+      }
+      if (s_.flags & F_PKGID) v.pkg_id = std::string(p.id);
       v.pkg_name = std::string(p.name);
       v.installed = format_version(p.epoch, p.version, p.release);
-      v.status = int32_t(a.status);
-      if (a.severity != 0) {  // debian.go:92-98 package-specific severity
-        v.severity_source = "debian";
-        v.severity = (a.severity > 0 && a.severity < 5) ? kSeverity[a.severity] : kSeverity[0];
+      v.fixed = (s_.flags & F_RPM_STRING) && !a.fixed.empty() ? rpm_string(a.fixed) : a.fixed;
+      if (s_.flags & F_DEBIAN) {
+        v.vendor_ids = a.vendor_ids;
+        v.status = int32_t(a.status);
+        if (a.severity != 0) {  // debian.go:92-98 package-specific severity
+          v.severity_source = "debian";
+          v.severity = severity_name(a.severity);
+        }
       }
       out.push_back(std::move(v));
     }
     return true;
   }
-  bool is_supported(std::string_view, std::string_view os_ver, int64_t now) const override {
-    return supported(eol_, os_major(os_ver), now);
+
+  bool is_supported(std::string_view family, std::string_view os_ver, int64_t now) const override {
+    return s_.supported(family, os_ver, now);
   }
 };
 
-// ---------------------------------------------------------------- ubuntu.go ----------
-class Ubuntu : public OsDriver {
-  EolMap eol_ = make_eol({{"4.10", 2006, 4, 30}, {"5.04", 2006, 10, 31}, {"5.10", 2007, 4, 13},
-                          {"6.06", 2011, 6, 1}, {"6.10", 2008, 4, 25}, {"7.04", 2008, 10, 19},
-                          {"7.10", 2009, 4, 18}, {"8.04", 2013, 5, 9}, {"8.10", 2010, 4, 30},
-                          {"9.04", 2010, 10, 23}, {"9.10", 2011, 4, 29}, {"10.04", 2015, 4, 29},
-                          {"10.10", 2012, 4, 10}, {"11.04", 2012, 10, 28}, {"11.10", 2013, 5, 9},
-                          {"12.04", 2019, 4, 26}, {"12.04-ESM", 2019, 4, 28}, {"12.10", 2014, 5, 16},
-                          {"13.04", 2014, 1, 27}, {"13.10", 2014, 7, 17}, {"14.04", 2022, 4, 25},
-                          {"14.04-ESM", 2024, 4, 25}, {"14.10", 2015, 7, 23}, {"15.04", 2016, 1, 23},
-                          {"15.10", 2016, 7, 22}, {"16.04", 2021, 4, 21}, {"16.04-ESM", 2026, 4, 29},
-                          {"16.10", 2017, 7, 20}, {"17.04", 2018, 1, 13}, {"17.10", 2018, 7, 19},
-                          {"18.04", 2023, 5, 31}, {"18.04-ESM", 2028, 3, 31}, {"18.10", 2019, 7, 18},
-                          {"19.04", 2020, 1, 18}, {"19.10", 2020, 7, 17}, {"20.04", 2025, 4, 23},
-                          {"20.10", 2021, 7, 22}, {"21.04", 2022, 1, 20}, {"21.10", 2022, 7, 14},
-                          {"22.04", 2027, 4, 23}, {"22.10", 2023, 7, 20}, {"23.04", 2024, 1, 20}});
+// ---- redhat.go ---------------------------------------------------------------------------
+const std::map<std::string, std::vector<std::string>, std::less<>>& redhat_default_content_sets() {
+  static const std::map<std::string, std::vector<std::string>, std::less<>> m = {
+      {"6", {"rhel-6-server-rpms", "rhel-6-server-extras-rpms"}},
+      {"7", {"rhel-7-server-rpms", "rhel-7-server-extras-rpms"}},
+      {"8", {"rhel-8-for-x86_64-baseos-rpms", "rhel-8-for-x86_64-appstream-rpms"}},
+      {"9", {"rhel-9-for-x86_64-baseos-rpms", "rhel-9-for-x86_64-appstream-rpms"}},
+  };
+  return m;
+}
 
-  // versionFromEolDates (ubuntu.go:136-151); the reference reads time.Now() here, we use `now`.
-  std::string version_from_eol(std::string_view os_ver, int64_t now) const {
-    if (eol_.count(os_ver)) return std::string(os_ver);
-    std::string ver(os_ver);
-    while (!ver.empty() && std::string_view("-ESM").find(ver.back()) != std::string_view::npos) ver.pop_back();  // TrimRight cutset
-    auto it = eol_.find(ver);
-    if (it != eol_.end() && now < it->second) return ver;
-    return std::string(os_ver);
-  }
-
+class RedHat : public OsDriver {
  public:
-  bool detect(Engine& eng, std::string_view os_ver, const Repo*, const std::vector<Pkg>& pkgs, int64_t now,
+  bool detect(Engine& eng, std::string_view os_ver_in, const Repo*, const std::vector<Pkg>& pkgs, int64_t,
               std::vector<Vuln>& out, std::string& err) const override {
     const DB& db = eng.db();
+    const std::string os_ver = os_major(os_ver_in);
     Plan plan;
-    plan.plat = pkgs.empty() ? -1 : db.find_plat("ubuntu " + version_from_eol(os_ver, now));
-    std::vector<std::string> src(pkgs.size());
+    plan.plat = db.find_plat("Red Hat");
+    // CPE sets: one per distinct (content sets, NVR) among the packages (redhat.go:112-120)
+    const uint32_t words = std::max<uint32_t>((db.n_cpe + 31) / 32, 1);
+    std::map<std::vector<std::string>, uint32_t> set_ids;
+    plan.batch.cpe_words = words;
+    std::vector<std::string> inst(pkgs.size()), names(pkgs.size());
     for (size_t i = 0; i < pkgs.size(); i++) {
-      src[i] = format_version(pkgs[i].src_epoch, pkgs[i].src_version, pkgs[i].src_release);
-      plan.add(false, pkgs[i].src_name, src[i]);
+      const Pkg& p = pkgs[i];
+      const bool remi = p.release.size() >= 5 && p.release.substr(p.release.size() - 5) == ".remi";
+      names[i] = modular_name(p.name, p.modularitylabel);
+      inst[i] = format_version(p.epoch, p.version, p.release);
+      std::vector<std::string> key;  // content sets..., "\x01" + nvr
+      std::vector<std::string_view> repos, nvrs;
+      std::string nvr;
+      if (!p.has_build_info) {
+        auto it = redhat_default_content_sets().find(os_ver);
+        if (it != redhat_default_content_sets().end())
+          for (const std::string& c : it->second) repos.push_back(c);
+      } else {
+        repos = p.content_sets;
+        nvr = std::string(p.nvr) + "-" + std::string(p.build_arch);
+      }
+      nvrs.push_back(nvr);
+      for (std::string_view r : repos) key.emplace_back(r);
+      key.push_back("\x01" + nvr);
+      auto it = set_ids.find(key);
+      if (it == set_ids.end()) {
+        it = set_ids.emplace(key, uint32_t(set_ids.size())).first;
+        plan.batch.cpe_bits.resize(plan.batch.cpe_bits.size() + words, 0u);
+        uint32_t* bits = plan.batch.cpe_bits.data() + size_t(it->second) * words;
+        for (int64_t c : db.redhat_cpes(repos, nvrs))
+          if (c >= 0 && uint64_t(c) < uint64_t(words) * 32) bits[c >> 5] |= 1u << (c & 31);
+      }
+      uint2 a;
+      a.x = db.arch_id(p.arch) | (p.arch == "noarch" ? PA_NOARCH : 0u);
+      a.y = it->second;
+      plan.add(remi, names[i], inst[i], a);  // isFromSupportedVendor (redhat.go:197-205)
     }
     std::vector<uint2> pairs;
     std::string key_err;
     if (!run_plan(eng, plan, pairs, key_err, err)) return false;
     if (!key_err.empty()) {
-      err = "failed to get Ubuntu advisories: " + key_err;  // ubuntu.go:87-90
+      err = "redhat vulnerability detection error: failed to get Red Hat advisories: " + key_err;
       return false;
     }
-    for (const uint2& m : pairs) {
-      const Pkg& p = pkgs[m.x];
-      const Advisory& a = db.advs[m.y];
-      Vuln v;
-      v.pkg = m.x;
-      v.copy = COPY_PKG_ID | COPY_PKG_NAME | COPY_IDENTIFIER | COPY_LAYER;
-      fill_common(v, a);
-      v.pkg_id = std::string(p.id);
-      v.pkg_name = std::string(p.name);
-      v.installed = format_version(p.epoch, p.version, p.release);
-      out.push_back(std::move(v));
+    // per package: uniqVulns merge (redhat.go:146-180), then sorted by VulnerabilityID
+    size_t i = 0;
+    while (i < pairs.size()) {
+      const uint32_t pk = pairs[i].x;
+      const Pkg& p = pkgs[pk];
+      std::map<std::string, Vuln> uniq;
+      for (; i < pairs.size() && pairs[i].x == pk; i++) {
+        const Advisory& a = db.advs[pairs[i].y];
+        Vuln v;
+        v.pkg = pk;
+        v.copy = COPY_PKG_ID | COPY_PKG_NAME | COPY_IDENTIFIER | COPY_LAYER;
+        v.vuln_id = a.vuln_id;
+        v.pkg_id = std::string(p.id);
+        v.pkg_name = std::string(p.name);
+        v.installed = inst[pk];
+        v.status = int32_t(a.status);
+        v.severity_source = "redhat";
+        v.severity = severity_name(a.severity);
+        auto it = uniq.find(a.vuln_id);
+        if (a.fixed.empty()) {
+          if (it == uniq.end()) uniq.emplace(a.vuln_id, std::move(v));
+          continue;
+        }
+        v.vendor_ids = a.vendor_ids;
+        v.fixed = rpm_string(a.fixed);
+        if (it == uniq.end()) {
+          uniq.emplace(a.vuln_id, std::move(v));
+          continue;
+        }
+        Vuln& u = it->second;  // ustrings.Unique: sorted, de-duplicated union
+        std::vector<std::string> ids = u.vendor_ids;
+        ids.insert(ids.end(), v.vendor_ids.begin(), v.vendor_ids.end());
+        std::sort(ids.begin(), ids.end());
+        ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+        u.vendor_ids = std::move(ids);
+        if (rpm_less(u.fixed, a.fixed)) u.fixed = v.fixed;
+      }
+      for (auto& [id, v] : uniq) out.push_back(std::move(v));
     }
     return true;
   }
-  bool is_supported(std::string_view, std::string_view os_ver, int64_t now) const override {
-    return supported(eol_, os_ver, now);
+  bool is_supported(std::string_view family, std::string_view os_ver, int64_t now) const override {
+    return supported(family == "centos" ? centos_eol() : redhat_eol(), os_major(os_ver), now);
   }
 };
 
-// ---------------------------------------------------------------- amazon.go ----------
-class Amazon : public OsDriver {
-  EolMap eol_ = make_eol({{"1", 2023, 12, 31}, {"2", 2025, 6, 30}, {"2023", 2028, 3, 15}});
+bool always(std::string_view, std::string_view, int64_t) { return true; }
 
-  static std::string norm(std::string_view os_ver) {  // amazon.go:46-52
-    size_t b = os_ver.find_first_not_of(" \t\n\v\f\r");
-    std::string_view f = b == std::string_view::npos ? std::string_view() : os_ver.substr(b);
-    f = f.substr(0, f.find_first_of(" \t\n\v\f\r"));
-    std::string v = os_major(f);
-    if (v != "2" && v != "2022" && v != "2023") v = "1";
-    return v;
-  }
+std::function<bool(std::string_view, std::string_view, int64_t)> eol_of(const EolMap& (*tab)(),
+                                                                           std::string (*norm)(std::string_view)) {
+  return [tab, norm](std::string_view, std::string_view v, int64_t now) {
+    return supported(tab(), norm ? norm(v) : std::string(v), now);
+  };
+}
 
- public:
-  bool detect(Engine& eng, std::string_view os_ver, const Repo*, const std::vector<Pkg>& pkgs, int64_t,
-              std::vector<Vuln>& out, std::string& err) const override {
-    const DB& db = eng.db();
-    Plan plan;
-    plan.plat = db.find_plat("amazon linux " + norm(os_ver));
-    std::vector<std::string> inst(pkgs.size());
-    for (size_t i = 0; i < pkgs.size(); i++) {
-      inst[i] = format_version(pkgs[i].epoch, pkgs[i].version, pkgs[i].release);
-      plan.add(false, pkgs[i].name, inst[i]);
-    }
-    std::vector<uint2> pairs;
-    std::string key_err;
-    if (!run_plan(eng, plan, pairs, key_err, err)) return false;
-    if (!key_err.empty()) {
-      err = "failed to get amazon advisories: " + key_err;  // amazon.go:59-61
-      return false;
-    }
-    for (const uint2& m : pairs) {
-      const Pkg& p = pkgs[m.x];
-      const Advisory& a = db.advs[m.y];
-      Vuln v;
-      v.pkg = m.x;
-      v.copy = COPY_PKG_ID | COPY_PKG_NAME | COPY_IDENTIFIER | COPY_LAYER;
-      fill_common(v, a);
-      v.pkg_id = std::string(p.id);
-      v.pkg_name = std::string(p.name);
-      v.installed = inst[m.x];
-      out.push_back(std::move(v));
-    }
-    return true;
-  }
-  bool is_supported(std::string_view, std::string_view os_ver, int64_t now) const override {
-    return supported(eol_, norm(os_ver), now);
-  }
-};
+std::string os_minor_s(std::string_view v) { return os_minor(v); }
+std::string os_major_s(std::string_view v) { return os_major(v); }
+std::string amazon_release_s(std::string_view v) { return amazon_release(v); }
 
 }  // namespace
 
 const OsDriver* find_os_driver(std::string_view family) {
-  static const Debian debian;
-  static const Ubuntu ubuntu;
-  static const Amazon amazon;
-  if (family == "debian") return &debian;
-  if (family == "ubuntu") return &ubuntu;
-  if (family == "amazon") return &amazon;
-  return nullptr;
+  static const std::map<std::string, std::unique_ptr<OsDriver>, std::less<>> drivers = [] {
+    std::map<std::string, std::unique_ptr<OsDriver>, std::less<>> m;
+    auto add = [&](const char* fam, Spec s) { m[fam] = std::make_unique<TableDriver>(std::move(s)); };
+    add("debian", {[](std::string_view v, const Repo*, int64_t) { return "debian " + os_major(v); }, NAME_SRC, VER_SRC,
+                   F_PKGID | F_CUSTOM | F_DEBIAN, "failed to get debian advisories: ", nullptr,
+                   eol_of(debian_eol, os_major_s)});
+    add("ubuntu", {[](std::string_view v, const Repo*, int64_t now) { return "ubuntu " + ubuntu_release(v, now); },
+                   NAME_SRC, VER_SRC, F_PKGID | F_CUSTOM, "failed to get Ubuntu advisories: ", nullptr,
+                   eol_of(ubuntu_eol, nullptr)});
+    add("amazon", {[](std::string_view v, const Repo*, int64_t) { return "amazon linux " + amazon_release(v); },
+                   NAME_BIN, VER_BIN, F_PKGID | F_CUSTOM, "failed to get amazon advisories: ", nullptr,
+                   eol_of(amazon_eol, amazon_release_s)});
+    add("alpine", {[](std::string_view v, const Repo* r, int64_t) { return "alpine " + alpine_stream(v, r); },
+                   NAME_SRC_OR_BIN, VER_SRC, F_PKGID | F_CUSTOM, "failed to get alpine advisories: ", nullptr,
+                   eol_of(alpine_eol, os_minor_s)});
+    add("wolfi", {[](std::string_view, const Repo*, int64_t) { return std::string("wolfi"); }, NAME_SRC_OR_BIN,
+                  VER_BIN, F_PKGID | F_CUSTOM, "failed to get Wolfi advisories: ", nullptr, always});
+    add("chainguard", {[](std::string_view, const Repo*, int64_t) { return std::string("chainguard"); },
+                       NAME_SRC_OR_BIN, VER_BIN, F_PKGID | F_CUSTOM, "failed to get Chainguard advisories: ", nullptr,
+                       always});
+    add("alma", {[](std::string_view v, const Repo*, int64_t) { return "alma " + os_major(v); }, NAME_MODULAR, VER_BIN,
+                 F_PKGID | F_CUSTOM | F_RPM_STRING, "failed to get AlmaLinux advisories: ",
+                 [](const Pkg& p) {  // alma.go:53-57
+                   return p.release.find(".module_el") != std::string_view::npos && p.modularitylabel.empty();
+                 },
+                 eol_of(alma_eol, os_major_s)});
+    add("rocky", {[](std::string_view v, const Repo*, int64_t) { return "rocky " + os_major(v); }, NAME_MODULAR,
+                  VER_BIN, F_PKGID | F_CUSTOM | F_RPM_STRING | F_ARCH, "failed to get Rocky Linux advisories: ",
+                  [](const Pkg& p) { return !p.modularitylabel.empty(); },  // rocky.go:52-56
+                  eol_of(rocky_eol, os_major_s)});
+    add("oracle", {[](std::string_view v, const Repo*, int64_t) { return "Oracle Linux " + os_major(v); }, NAME_BIN,
+                   VER_BIN, F_PKGID | F_CUSTOM | F_KSPLICE, "failed to get Oracle Linux advisory: ", nullptr,
+                   eol_of(oracle_eol, os_major_s)});
+    add("opensuse.leap", {[](std::string_view v, const Repo*, int64_t) { return "openSUSE Leap " + std::string(v); },
+                          NAME_BIN, VER_BIN, F_PKGID | F_CUSTOM,
+                          "failed to get SUSE advisory: failed to get SUSE advisories: ", nullptr,
+                          eol_of(opensuse_eol, nullptr)});
+    add("suse linux enterprise server",
+        {[](std::string_view v, const Repo*, int64_t) { return "SUSE Linux Enterprise " + std::string(v); }, NAME_BIN,
+         VER_BIN, F_PKGID | F_CUSTOM, "failed to get SUSE advisory: failed to get SUSE advisories: ", nullptr,
+         eol_of(sles_eol, nullptr)});
+    add("photon", {[](std::string_view v, const Repo*, int64_t) { return "Photon OS " + std::string(v); }, NAME_SRC,
+                   VER_BIN, F_PKGID | F_CUSTOM,
+                   "failed to get Photon Linux advisory: failed to get Photon advisories: ", nullptr,
+                   eol_of(photon_eol, nullptr)});
+    add("cbl-mariner", {[](std::string_view v, const Repo*, int64_t) { return "CBL-Mariner " + os_minor(v); },
+                        NAME_SRC, VER_SRC, F_RPM_STRING, "failed to get CBL-Mariner advisories: ", nullptr, always});
+    m["redhat"] = std::make_unique<RedHat>();
+    m["centos"] = std::make_unique<RedHat>();
+    return m;
+  }();
+  auto it = drivers.find(family);
+  return it == drivers.end() ? nullptr : it->second.get();
 }
 
 DetectStatus ospkg_detect(Engine& eng, std::string_view family, std::string_view os_name, const Repo* repo,

@@ -23,19 +23,32 @@ struct DevDB {
   const uint64_t* key_words = nullptr;
   const PlatInfo* plats = nullptr;
   uint32_t n_plats = 0;
+  const RowAux* aux = nullptr;
+  const uint32_t* aux_ids = nullptr;
 };
 
 // A package batch in SoA-of-descriptors form.  desc[i] = {plat, name_off, ver_off,
 // name_len | ver_len << 16} into `arena`; plat = 0xFFFFFFFF when the bucket is absent.
+// Optional per-package attributes (common.h PA_*), present when the batch touches rows
+// with filters: attr[i] = {arch id | PA_NOARCH, ksplice tag or CPE-set id}; CPE set s is
+// the bitset cpe_bits[s * cpe_words .. +cpe_words) over CPE indices.
 struct HostBatch {
   std::vector<uint4> desc;
   std::vector<uint8_t> arena;
+  std::vector<uint2> attr;
+  std::vector<uint32_t> cpe_bits;
+  uint32_t cpe_words = 0;
   void add(uint32_t plat, std::string_view name, std::string_view ver);
+  void add(uint32_t plat, std::string_view name, std::string_view ver, uint2 a);
 };
 
 struct DevBatch {
   uint4* desc = nullptr;
   uint8_t* arena = nullptr;
+  uint2* attr = nullptr;
+  uint32_t* cpe_bits = nullptr;
+  uint32_t cpe_words = 0;
+  uint32_t n_cpe_sets = 0;
   uint32_t n = 0;
   uint64_t arena_bytes = 0;
   uint64_t spill_words = 0;  // scratch needed for installed keys longer than the LDS slot

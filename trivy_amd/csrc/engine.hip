@@ -42,6 +42,10 @@ struct MatchArgs {
   DevDB db;
   const uint4* desc;
   const uint8_t* arena;
+  const uint2* attr;       // per-package attributes, nullptr when no row of the DB filters
+  const uint32_t* cpe_bits;
+  uint32_t cpe_words;
+  uint32_t n_cpe_sets;
   uint32_t n;
   uint32_t n_tiles;
   uint2* out;
@@ -65,6 +69,7 @@ struct TileShared {
   uint32_t rbeg[T];           // first row per package
   uint32_t kinfo[T];          // key length | flags
   uint32_t koff[T];           // spill word offset when KI_SPILL
+  uint2 pattr[T];             // package attributes (filtered rows only)
   uint32_t wsum[T / 64];
   uint32_t tile;
   uint32_t span_lo, span_hi;  // arena window of the tile's strings
@@ -115,9 +120,34 @@ __device__ __forceinline__ uint32_t pair_pkg(const S& s, uint32_t j) {
   return lo;
 }
 
-// Interval test of package q's installed key against one row.
+// Per-package predicates of a ROW_FILTER row (common.h RowAux).
+__device__ __attribute__((noinline)) bool aux_pass(const MatchArgs& a, uint32_t ridx, uint2 pa) {
+  const RowAux x = a.db.aux[ridx];
+  const uint32_t* ids = a.db.aux_ids + x.list_off;
+  if (x.kind & (AUX_ARCH_RH | AUX_ARCH_IN)) {
+    bool ok = (x.kind & AUX_ARCH_RH) && (x.n_arch == 0 || (pa.x & PA_NOARCH));
+    const uint32_t arch = pa.x & PA_ARCH_MASK;
+    for (uint32_t i = 0; i < x.n_arch && !ok; i++) ok = ids[i] == arch;
+    if (!ok) return false;
+  }
+  if (x.kind & AUX_CPE) {
+    if (pa.y >= a.n_cpe_sets) return false;
+    const uint32_t* set = a.cpe_bits + size_t(pa.y) * a.cpe_words;
+    bool ok = false;
+    for (uint32_t i = 0; i < x.n_cpe && !ok; i++) {
+      const uint32_t c = ids[x.n_arch + i];
+      ok = (c >> 5) < a.cpe_words && ((set[c >> 5] >> (c & 31)) & 1u);
+    }
+    if (!ok) return false;
+  }
+  if ((x.kind & AUX_TAG) && x.tag != pa.y) return false;
+  return true;
+}
+
+// Interval test of package q's installed key against one row (global index ridx).
 template <int KW, class S>
-__device__ __forceinline__ bool eval_row(const MatchArgs& a, const S& s, uint32_t q, const Row& row) {
+__device__ __forceinline__ bool eval_row(const MatchArgs& a, const S& s, uint32_t q, const Row& row, uint32_t ridx) {
+  if ((row.adv & ROW_FILTER) && !aux_pass(a, ridx, s.pattr[q])) return false;
   if (row.adv & ROW_ALWAYS) return true;
   const uint32_t ki = s.kinfo[q];
   if (!(ki & KI_VALID)) return false;
@@ -144,22 +174,24 @@ __device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared<T, KW, 
   constexpr int W = T / 64;
   const uint32_t lane = tid & 63, wave = tid >> 6;
   uint32_t nm = 0;
-  uint32_t j = tid, q = 0;
+  uint32_t j = tid, q = 0, ridx = 0;
   Row row{};
   if (j < total_pairs) {
     q = pair_pkg<T>(s, j);
-    row = a.db.rows[s.rbeg[q] + (j - s.scan[q])];
+    ridx = s.rbeg[q] + (j - s.scan[q]);
+    row = a.db.rows[ridx];
   }
   for (uint32_t b0 = 0; b0 < total_pairs; b0 += T) {
     // issue the next chunk's row load before testing this chunk's pair
     const uint32_t jn = j + T;
-    uint32_t qn = 0;
+    uint32_t qn = 0, ridxn = 0;
     Row rown{};
     if (jn < total_pairs) {
       qn = pair_pkg<T>(s, jn);
-      rown = a.db.rows[s.rbeg[qn] + (jn - s.scan[qn])];
+      ridxn = s.rbeg[qn] + (jn - s.scan[qn]);
+      rown = a.db.rows[ridxn];
     }
-    const bool m = (j < total_pairs) && (AB == 2 ? (row.adv & 7u) == 0 : eval_row<KW>(a, s, q, row));
+    const bool m = (j < total_pairs) && (AB == 2 ? (row.adv & 7u) == 0 : eval_row<KW>(a, s, q, row, ridx));
     const unsigned long long bal = __ballot(m);
     const uint32_t lane_off = __popcll(bal & ((1ull << lane) - 1ull));
     if (lane == 0) s.wsum[wave] = uint32_t(__popcll(bal));
@@ -184,6 +216,7 @@ __device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared<T, KW, 
     __syncthreads();
     j = jn;
     q = qn;
+    ridx = ridxn;
     row = rown;
   }
   return nm;
@@ -250,7 +283,7 @@ __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
     // installed version -> sort key (LDS slot, or global spill for long versions)
     uint64_t* dst = &s.key[tid * KW];
     uint32_t need = 0;
-    if ((key_bound(vlen) + 7) / 8 > uint32_t(KW)) {  // might not fit: size it exactly
+    if ((key_bound(pi.cmp, vlen) + 7) / 8 > uint32_t(KW)) {  // might not fit: size it exactly
       CountSink cs;
       need = encode_version(pi.cmp, ver, vlen, cs) ? (cs.n + 7) / 8 : 0;
     }
@@ -295,6 +328,7 @@ __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
   s.rbeg[tid] = rbeg;
   s.kinfo[tid] = kinfo;
   s.koff[tid] = koff;
+  s.pattr[tid] = (a.attr && p < a.n) ? a.attr[p] : make_uint2(PA_ARCH_NONE, 0xFFFFFFFFu);
 
   // ---- 2. scan of row counts ------------------------------------------------------------
   const uint32_t total_pairs = block_scan<T>(s, cnt, tid);
@@ -382,6 +416,14 @@ void HostBatch::add(uint32_t plat, std::string_view name, std::string_view ver) 
   arena.insert(arena.end(), ver.begin(), ver.end());
   d.w = uint32_t(std::min<size_t>(name.size(), 0xFFFF)) | (uint32_t(std::min<size_t>(ver.size(), 0xFFFF)) << 16);
   desc.push_back(d);
+  if (!attr.empty()) attr.push_back(make_uint2(PA_ARCH_NONE, 0xFFFFFFFFu));
+}
+
+void HostBatch::add(uint32_t plat, std::string_view name, std::string_view ver, uint2 a) {
+  if (attr.size() < desc.size()) attr.resize(desc.size(), make_uint2(PA_ARCH_NONE, 0xFFFFFFFFu));
+  add(plat, name, ver);
+  if (attr.size() < desc.size()) attr.push_back(a);
+  else attr.back() = a;
 }
 
 Engine::~Engine() {
@@ -410,8 +452,10 @@ Engine* Engine::open(const DB& db, int device, std::string& err) {
     delete e;
     return nullptr;
   }
-  uint64_t* sh; SlotVal* sv; uint8_t* na; Row* rows; uint64_t* kw; PlatInfo* pl;
-  bool ok = upload_vec(db.slot_hash, &sh, e->allocs_, e->table_bytes_, err) &&
+  uint64_t* sh; SlotVal* sv; uint8_t* na; Row* rows; uint64_t* kw; PlatInfo* pl; RowAux* ax; uint32_t* ai;
+  bool ok = upload_vec(db.aux, &ax, e->allocs_, e->table_bytes_, err) &&
+            upload_vec(db.aux_ids, &ai, e->allocs_, e->table_bytes_, err) &&
+            upload_vec(db.slot_hash, &sh, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.slot_val, &sv, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.name_arena, &na, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.rows, &rows, e->allocs_, e->table_bytes_, err) &&
@@ -428,6 +472,8 @@ Engine* Engine::open(const DB& db, int device, std::string& err) {
   e->d_.rows = rows;
   e->d_.key_words = kw;
   e->d_.plats = pl;
+  e->d_.aux = ax;
+  e->d_.aux_ids = ai;
   e->d_.n_plats = uint32_t(db.plats.size());
   return e;
 }
@@ -455,7 +501,7 @@ bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
   b.arena_bytes = hb.arena.size();
   b.spill_words = 0;
   for (const uint4& d : hb.desc) {
-    const uint32_t need = (key_bound(d.w >> 16) + 7) / 8;
+    const uint32_t need = (key_bound(CMP_APK, d.w >> 16) + 7) / 8;  // the widest grammar bound
     if (need > uint32_t(kMinKeyWords)) b.spill_words += need;  // bound for every variant
   }
   if (!hip_ok(hipMalloc(&b.desc, std::max<size_t>(hb.desc.size(), 1) * sizeof(uint4)), "hipMalloc(batch)", err)) return false;
@@ -467,6 +513,22 @@ bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
   if (!hb.arena.empty() &&
       !hip_ok(hipMemcpy(b.arena, hb.arena.data(), hb.arena.size(), hipMemcpyHostToDevice), "H2D arena", err))
     return false;
+  if (!hb.attr.empty()) {
+    if (hb.attr.size() != hb.desc.size()) {
+      err = "batch attributes do not cover every package";
+      return false;
+    }
+    if (!hip_ok(hipMalloc(&b.attr, hb.attr.size() * sizeof(uint2)), "hipMalloc(batch attr)", err) ||
+        !hip_ok(hipMemcpy(b.attr, hb.attr.data(), hb.attr.size() * sizeof(uint2), hipMemcpyHostToDevice), "H2D attr", err))
+      return false;
+  }
+  if (!hb.cpe_bits.empty() && hb.cpe_words) {
+    if (!hip_ok(hipMalloc(&b.cpe_bits, hb.cpe_bits.size() * 4), "hipMalloc(cpe sets)", err) ||
+        !hip_ok(hipMemcpy(b.cpe_bits, hb.cpe_bits.data(), hb.cpe_bits.size() * 4, hipMemcpyHostToDevice), "H2D cpe", err))
+      return false;
+    b.cpe_words = hb.cpe_words;
+    b.n_cpe_sets = uint32_t(hb.cpe_bits.size() / hb.cpe_words);
+  }
   return true;
 }
 
@@ -474,6 +536,8 @@ void Engine::free_batch(DevBatch& b) {
   (void)hipSetDevice(dev_);
   if (b.desc) (void)hipFree(b.desc);
   if (b.arena) (void)hipFree(b.arena);
+  if (b.attr) (void)hipFree(b.attr);
+  if (b.cpe_bits) (void)hipFree(b.cpe_bits);
   b = DevBatch{};
 }
 
@@ -532,6 +596,10 @@ bool Engine::launch(const DevBatch& b, const DevMatches& m, hipStream_t st, std:
   a.db = d_;
   a.desc = b.desc;
   a.arena = b.arena;
+  a.attr = b.attr;
+  a.cpe_bits = b.cpe_bits;
+  a.cpe_words = b.cpe_words;
+  a.n_cpe_sets = b.n_cpe_sets;
   a.n = b.n;
   a.n_tiles = n_tiles;
   a.out = m.pairs;

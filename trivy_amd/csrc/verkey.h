@@ -213,8 +213,249 @@ TVM_HD bool deb_encode(const uint8_t* s, uint32_t n, Sink& o) {
   return true;
 }
 
-// Upper bound on the key length of a version string of n bytes (all grammars).
-TVM_HD uint32_t key_bound(uint32_t n) { return 2 * n + 16; }
+
+// ------------------------------------------------------------------- signed integers -----
+// Order-preserving variable-length code of a signed 64-bit value: v >= 0 as 0x80+k then
+// k big-endian bytes (k minimal, 0 for v = 0); v < 0 as 0x7F-k then the k bytes of
+// ~(-(v+1)) (more negative -> smaller).  Self-delimiting, so a following token starts at
+// the same offset in two keys whose values are equal.
+template <class Sink>
+TVM_HD void put_sint(int64_t v, Sink& o) {
+  if (v >= 0) {
+    const uint64_t u = uint64_t(v);
+    uint32_t k = 0;
+    for (uint64_t t = u; t; t >>= 8) k++;
+    o.put(uint8_t(0x80 + k));
+    for (int b = int(k) - 1; b >= 0; b--) o.put(uint8_t(u >> (8 * b)));
+  } else {
+    const uint64_t m = ~uint64_t(v);  // -(v+1) >= 0
+    uint32_t k = 0;
+    for (uint64_t t = m; t; t >>= 8) k++;
+    o.put(uint8_t(0x7F - k));
+    for (int b = int(k) - 1; b >= 0; b--) o.put(uint8_t(~(m >> (8 * b))));
+  }
+}
+
+// ------------------------------------------------------------------------------- apk -----
+// github.com/knqyf263/go-apk-version (reference go.mod:61), the Go port of apk-tools'
+// version.c.  Call sites: alpine/alpine.go:93,126,141, wolfi/wolfi.go:48,68,
+// chainguard/chainguard.go:48,68.  A version is a stream of tokens whose kind is decided
+// before each read (first kind: DIGIT); two versions compare value by value while the
+// kinds agree; when the kinds differ, a pre-release suffix (_alpha/_beta/_pre/_rc) is
+// smaller than anything, otherwise the LATER kind in the list DOZ, DIGIT, LETTER, SUFFIX,
+// SUFFIX_NO, REVISION_NO, END is the smaller version.  Key = one class byte per token
+// (that order inverted, pre-suffixes first) followed by put_sint(value); END ends it.
+enum : int { APK_INVALID = -1, APK_DOZ = 0, APK_DIGIT, APK_LETTER, APK_SUFFIX, APK_SUFFIX_NO, APK_REV, APK_END };
+enum : uint8_t {
+  APKC_SUFPRE = 0x01, APKC_END = 0x02, APKC_REV = 0x03, APKC_SUFNO = 0x04, APKC_SUFPOST = 0x05,
+  APKC_LETTER = 0x06, APKC_DIGIT = 0x07, APKC_DOZ = 0x08,
+};
+
+TVM_HD bool apk_lower(uint8_t c) { return c >= 'a' && c <= 'z'; }
+
+// next_token of version.c: the kind of the token that starts at s[i] (consumes separators).
+TVM_HD int apk_next_kind(int kind, const uint8_t* s, uint32_t n, uint32_t& i) {
+  int k = APK_INVALID;
+  if (i >= n || s[i] == 0) {
+    k = APK_END;
+  } else if ((kind == APK_DIGIT || kind == APK_DOZ) && apk_lower(s[i])) {
+    k = APK_LETTER;
+  } else if (kind == APK_LETTER && is_adigit(s[i])) {
+    k = APK_DIGIT;
+  } else if (kind == APK_SUFFIX && is_adigit(s[i])) {
+    k = APK_SUFFIX_NO;
+  } else {
+    if (s[i] == '.') k = APK_DOZ;
+    else if (s[i] == '_') k = APK_SUFFIX;
+    else if (s[i] == '-') {
+      if (i + 1 < n && s[i + 1] == 'r') {
+        k = APK_REV;
+        i++;
+      }
+    }
+    i++;
+  }
+  if (k < kind && !((k == APK_DOZ && kind == APK_DIGIT) || (k == APK_SUFFIX && kind == APK_SUFFIX_NO) ||
+                    (k == APK_DIGIT && kind == APK_LETTER)))
+    k = APK_INVALID;
+  return k;
+}
+
+TVM_HD bool apk_prefix(const uint8_t* s, uint32_t n, uint32_t i, const char* w, uint32_t wl) {
+  if (i + wl > n) return false;
+  for (uint32_t j = 0; j < wl; j++)
+    if (s[i + j] != uint8_t(w[j])) return false;
+  return true;
+}
+
+template <class Sink>
+TVM_HD bool apk_encode(const uint8_t* s, uint32_t n, Sink& o) {
+  int kind = APK_DIGIT;
+  uint32_t i = 0;
+  for (;;) {
+    if (i >= n) {
+      // get_token on an empty rest ("" or a trailing separator) still yields a token of
+      // the pending kind with value 0, then END ("1_" == "1_cvs", "" == "0")
+      static constexpr uint8_t kCls[] = {APKC_DOZ, APKC_DIGIT, APKC_LETTER, APKC_SUFPOST, APKC_SUFNO, APKC_REV};
+      if (kind >= APK_DOZ && kind <= APK_REV) {
+        o.put(kCls[kind]);
+        put_sint(0, o);
+      }
+      o.put(APKC_END);
+      return true;
+    }
+    int64_t v = 0;
+    int nt = APK_INVALID;
+    uint8_t cls;
+    switch (kind) {
+      case APK_DOZ:
+        if (s[i] == '0') {
+          uint32_t z = 0;
+          while (i < n && s[i] == '0') i++, z++;
+          v = -int64_t(z);
+          nt = APK_DIGIT;
+          cls = APKC_DOZ;
+          break;
+        }
+        [[fallthrough]];
+      case APK_DIGIT:
+      case APK_SUFFIX_NO:
+      case APK_REV: {
+        uint64_t u = 0;  // Go int arithmetic: wraps like the reference on overflow
+        while (i < n && is_adigit(s[i])) u = u * 10 + uint64_t(s[i++] - '0');
+        v = int64_t(u);
+        cls = kind == APK_DOZ ? APKC_DOZ : kind == APK_DIGIT ? APKC_DIGIT : kind == APK_REV ? APKC_REV : APKC_SUFNO;
+        break;
+      }
+      case APK_LETTER:
+        v = s[i++];
+        cls = APKC_LETTER;
+        break;
+      case APK_SUFFIX: {
+        // pre: alpha beta pre rc -> -4..-1 ; post: cvs svn git hg p -> 0..4
+        if (apk_prefix(s, n, i, "alpha", 5)) { v = -4; i += 5; }
+        else if (apk_prefix(s, n, i, "beta", 4)) { v = -3; i += 4; }
+        else if (apk_prefix(s, n, i, "pre", 3)) { v = -2; i += 3; }
+        else if (apk_prefix(s, n, i, "rc", 2)) { v = -1; i += 2; }
+        else if (apk_prefix(s, n, i, "cvs", 3)) { v = 0; i += 3; }
+        else if (apk_prefix(s, n, i, "svn", 3)) { v = 1; i += 3; }
+        else if (apk_prefix(s, n, i, "git", 3)) { v = 2; i += 3; }
+        else if (apk_prefix(s, n, i, "hg", 2)) { v = 3; i += 2; }
+        else if (apk_prefix(s, n, i, "p", 1)) { v = 4; i += 1; }
+        else return false;
+        cls = v < 0 ? APKC_SUFPRE : APKC_SUFPOST;
+        break;
+      }
+      default:
+        return false;
+    }
+    o.put(cls);
+    put_sint(v, o);
+    if (i >= n) kind = APK_END;
+    else if (nt != APK_INVALID) kind = nt;
+    else kind = apk_next_kind(kind, s, n, i);
+    if (kind == APK_INVALID) return false;
+    if (kind == APK_END) {
+      o.put(APKC_END);
+      return true;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------- rpm -----
+// github.com/knqyf263/go-rpm-version (reference go.mod:63).  Never fails.  Epoch =
+// strconv.Atoi before the first ':' (0 when absent or unparsable); release after the
+// FIRST '-' (pinned by redhat_test.go "advisories have different arches").  rpmvercmp
+// segments ([a-zA-Z]+ | [0-9]+ | ~; other bytes separate): '~' < end-of-string < letters <
+// numbers; letters bytewise, numbers by value.  Key = put_sint(epoch) PART(version)
+// PART(release), PART = segments then END:
+//   '~' = 0x01, END = 0x02, letters = 0x03 + the letters (0x41..0x7A, above every class
+//   byte, so a shorter run sorts first), number = 0x04 + digit count (leading zeros
+//   dropped; 1 byte < 0xFA, else 0xFA + 2 bytes) + digits packed two per byte.
+enum : uint8_t { RPM_TILDE = 0x01, RPM_END = 0x02, RPM_ALPHA = 0x03, RPM_NUM = 0x04 };
+
+TVM_HD bool rpm_alpha(uint8_t c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); }
+
+template <class Sink>
+TVM_HD void rpm_part(const uint8_t* s, uint32_t n, Sink& o) {
+  uint32_t i = 0;
+  while (i < n) {
+    const uint8_t c = s[i];
+    if (c == '~') {
+      o.put(RPM_TILDE);
+      i++;
+    } else if (rpm_alpha(c)) {
+      o.put(RPM_ALPHA);
+      while (i < n && rpm_alpha(s[i])) o.put(s[i++]);
+    } else if (is_adigit(c)) {
+      while (i < n && s[i] == '0') i++;
+      uint32_t b = i;
+      while (i < n && is_adigit(s[i])) i++;
+      const uint32_t len = i - b;
+      o.put(RPM_NUM);
+      if (len < 0xFA) {
+        o.put(uint8_t(len));
+      } else {
+        o.put(0xFA);
+        o.put(uint8_t(len >> 8));
+        o.put(uint8_t(len));
+      }
+      for (uint32_t j = b; j < i; j += 2) {
+        const uint8_t hi = uint8_t(s[j] - '0'), lo = j + 1 < i ? uint8_t(s[j + 1] - '0') : 0;
+        o.put(uint8_t((hi << 4) | lo));
+      }
+    } else {
+      i++;
+    }
+  }
+  o.put(RPM_END);
+}
+
+template <class Sink>
+TVM_HD bool rpm_encode(const uint8_t* s, uint32_t n, Sink& o) {
+  int64_t epoch = 0;
+  uint32_t colon = n;
+  for (uint32_t i = 0; i < n; i++)
+    if (s[i] == ':') { colon = i; break; }
+  const uint8_t* r = s;
+  uint32_t rn = n;
+  if (colon < n) {
+    uint32_t i = 0;
+    bool neg = false, ok = colon > 0;
+    if (colon > 0 && (s[0] == '+' || s[0] == '-')) {
+      neg = s[0] == '-';
+      i = 1;
+      ok = colon > 1;
+    }
+    uint64_t e = 0;
+    for (; ok && i < colon; i++) {
+      if (!is_adigit(s[i])) { ok = false; break; }
+      const uint64_t d = uint64_t(s[i] - '0');
+      if (e > (uint64_t(INT64_MAX) - d) / 10) { ok = false; break; }
+      e = e * 10 + d;
+    }
+    epoch = ok ? (neg ? -int64_t(e) : int64_t(e)) : 0;
+    r = s + colon + 1;
+    rn = n - colon - 1;
+  }
+  uint32_t dash = rn;
+  for (uint32_t i = 0; i < rn; i++)
+    if (r[i] == '-') { dash = i; break; }
+  put_sint(epoch, o);
+  rpm_part(r, dash, o);
+  if (dash < rn) rpm_part(r + dash + 1, rn - dash - 1, o);
+  else rpm_part(r, 0, o);
+  return true;
+}
+
+// Upper bound on the key length of a version string of n bytes.
+TVM_HD uint32_t key_bound(uint8_t cmp, uint32_t n) {
+  switch (cmp) {
+    case CMP_APK: return 4 * n + 16;
+    case CMP_RPM: return 3 * n + 16;
+    default: return 2 * n + 16;
+  }
+}
 
 // ---------------------------------------------------------------------------- sinks -----
 // Device sink: packs bytes into little-endian 64-bit words and stores whole words.
@@ -246,6 +487,8 @@ template <class Sink>
 TVM_HD bool encode_version(uint8_t cmp, const uint8_t* s, uint32_t n, Sink& o) {
   switch (cmp) {
     case CMP_DEB: return deb_encode(s, n, o);
+    case CMP_APK: return apk_encode(s, n, o);
+    case CMP_RPM: return rpm_encode(s, n, o);
     default: return false;
   }
 }
