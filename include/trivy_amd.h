@@ -40,6 +40,7 @@ enum {
   TVM_EUNSUPPORTED_OS = 2,  /* ospkg.ErrUnsupportedOS (detect.go:30) */
   TVM_EINVAL = 3,
   TVM_EDEVICE = 4,          /* HIP / device failure; no CPU fallback exists */
+  TVM_EUNSUPPORTED_TYPE = 5,/* library.NewDriver returned false (detect.go:12-15: nil, nil) */
 };
 
 typedef struct tvm_db tvm_db;
@@ -135,6 +136,8 @@ void tvm_engine_close(tvm_engine* e);
 /* Atomically replaces the engine's tables (waits for in-flight calls; server hot update). */
 int tvm_engine_swap(tvm_engine* e, tvm_db* db, char* err, size_t errlen);
 uint64_t tvm_engine_table_bytes(const tvm_engine* e);
+/* Integrity check: re-reads every device table and compares it with the host image. */
+int tvm_engine_verify(tvm_engine* e, char* err, size_t errlen);
 /* Tuning knob: selects the match-kernel variant (tile size / LDS budget); returns the
  * previous one.  v < 0 only queries.  Names via tvm_variant_name (NULL past the last). */
 int tvm_engine_set_variant(tvm_engine* e, int v);
@@ -153,6 +156,20 @@ int tvm_ospkg_driver_detect(tvm_engine* e, const char* os_family, const char* os
 /* Driver.IsSupportedVersion: 1 / 0, or -1 for an unsupported family. */
 int tvm_ospkg_is_supported(const char* os_family, const char* os_ver, int64_t now_unix);
 void tvm_result_free(tvm_result* r);
+
+/* ---- library (language packages) ---------------------------------------------------------
+ * pkg/detector/library: NewDriver (driver.go:25-93), (*Driver).DetectVulnerabilities
+ * (driver.go:111-137) and Detect (detect.go:11-42).  lib_type is an ftypes.LangType
+ * ("npm", "pip", "gomod", "jar", ...).  Unsupported types return TVM_EUNSUPPORTED_TYPE. */
+/* Driver.Type(): the trivy-db ecosystem of lib_type, or NULL when NewDriver fails. */
+const char* tvm_library_type(const char* lib_type);
+/* library.Detect: packages use id, name, version, file_path (-> PkgPath); results carry
+ * COPY_LAYER | COPY_IDENTIFIER.  Errors: "failed to scan <eco> vulnerabilities: ...". */
+int tvm_library_detect(tvm_engine* e, const char* lib_type, const tvm_package* pkgs, size_t n, tvm_result* out,
+                       char* err, size_t errlen);
+/* Driver.DetectVulnerabilities(pkgID, pkgName, pkgVer): errors "failed to get <eco> advisories: ...". */
+int tvm_library_detect_vulnerabilities(tvm_engine* e, const char* lib_type, tvm_str pkg_id, tvm_str pkg_name,
+                                       tvm_str pkg_ver, tvm_result* out, char* err, size_t errlen);
 
 /* ---- many-target batches (device-resident; bench + request coalescing) ---------------- */
 tvm_batch* tvm_batch_new(void);
@@ -180,9 +197,16 @@ int tvm_match_fetch(tvm_engine* e, tvm_batch* b, uint32_t* pairs, uint64_t cap, 
 int tvm_match_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err, size_t errlen);
 /* Algorithmic bytes of one pass (DESIGN.md "roofline"), computed on the host from the batch. */
 uint64_t tvm_match_algorithmic_bytes(tvm_engine* e, tvm_batch* b);
-/* Host-side sort key of a version string (diagnostics/tests): grammar 1 = dpkg.
+/* Host-side sort key of a version string (diagnostics/tests).  Grammars: 1 dpkg, 2 apk,
+ * 3 rpm, 4 go-version, 5 npm, 6 PEP 440, 7 Maven, 8 RubyGems, 9 Bitnami.
  * Returns the key length (<= cap bytes written) or -1 when the version does not parse. */
 int tvm_version_key(int grammar, const char* s, size_t n, uint8_t* out, size_t cap);
+/* Version class of a library grammar (npm: 1 pre-release; PEP 440: bits local/pre/post), -1 on error. */
+int tvm_version_class(int grammar, const char* s, size_t n);
+/* Host-side compare.IsVulnerable through the load-time interval compiler (tests): 1/0, -1
+ * when the advisory JSON does not decode. */
+int tvm_lib_is_vulnerable_host(int grammar, const char* ver, size_t ver_len, const char* advisory_json,
+                               size_t json_len);
 /* Advisory fields for host-side inspection of batch results. */
 const char* tvm_db_advisory_vuln_id(const tvm_db* db, uint32_t adv);
 

@@ -197,6 +197,8 @@ class NpmVer:
         if not m:
             raise VersionError(f"invalid semantic version: {s}")
         self.t = (int(m.group(1)), int(m.group(2)), int(m.group(3)))
+        if max(self.t) > U64:  # UNPINNED: numeric fields are 64-bit
+            raise VersionError(f"invalid semantic version: {s}")
         self.pre = m.group(4).split(".") if m.group(4) else []
 
     @staticmethod
@@ -325,8 +327,8 @@ def _npm_test(op, v, c):
 
 def npm_match(ver, constraint):
     v = NpmVer(ver)
-    for alt in constraint.split("||"):
-        cs = _npm_set(alt)
+    sets = [_npm_set(alt) for alt in constraint.split("||")]  # NewConstraints parses every set first
+    for cs in sets:
         if not all(_npm_test(op, v, c) for op, c in cs):
             continue
         if v.pre and not any(c.pre and c.t == v.t for _, c in cs):
@@ -358,6 +360,9 @@ class PepVer:
         else:
             self.post = None
         self.dev = int(m.group("dev_n") or 0) if m.group("dev_l") else None
+        nums = [self.epoch] + self.release + [x for x in (self.pre and self.pre[1], self.post, self.dev) if x]
+        if max(nums) > U64:  # UNPINNED: numeric fields are 64-bit
+            raise VersionError(f"malformed version: {s}")
         loc = m.group("local")
         self.local = tuple(int(x) if x.isdigit() else x.lower() for x in re.split(r"[-_\.]", loc)) if loc else None
 
@@ -477,9 +482,12 @@ def pep_match(ver, constraint):
                 if not m:
                     raise ConstraintError(f"improper constraint: {alt}")
                 sv = m.group(2)
-                if not sv.endswith(".*"):
-                    PepVer(sv)  # validates
-                cs.append((m.group(1) or "==", sv))
+                op = m.group(1) or "=="
+                # NewSpecifiers validates every specifier up front
+                pv = PepVer(sv[:-2] if sv.endswith(".*") else sv)
+                if op == "~=" and len(pv.release) < 2:
+                    raise ConstraintError(f"~= needs two release segments: {sv}")
+                cs.append((op, sv))
                 pos = m.end()
         if not cs:
             raise ConstraintError(f"improper constraint: {alt}")

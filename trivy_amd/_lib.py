@@ -9,7 +9,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtrivy_amd.so")
 
-TVM_OK, TVM_EDETECT, TVM_EUNSUPPORTED_OS, TVM_EINVAL, TVM_EDEVICE = 0, 1, 2, 3, 4
+TVM_OK, TVM_EDETECT, TVM_EUNSUPPORTED_OS, TVM_EINVAL, TVM_EDEVICE, TVM_EUNSUPPORTED_TYPE = 0, 1, 2, 3, 4, 5
 COPY_PKG_ID, COPY_PKG_NAME, COPY_IDENTIFIER, COPY_LAYER = 1, 2, 4, 8
 
 
@@ -73,6 +73,7 @@ _SIG = [
     ("tvm_engine_close", None, [_P]),
     ("tvm_engine_swap", ctypes.c_int, [_P, _P, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_engine_table_bytes", ctypes.c_uint64, [_P]),
+    ("tvm_engine_verify", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_engine_set_variant", ctypes.c_int, [_P, ctypes.c_int]),
     ("tvm_variant_name", ctypes.c_char_p, [ctypes.c_int]),
     ("tvm_ospkg_detect", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(Repository),
@@ -101,6 +102,14 @@ _SIG = [
     ("tvm_version_key", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p,
                                        ctypes.c_size_t]),
     ("tvm_db_advisory_vuln_id", ctypes.c_char_p, [_P, ctypes.c_uint32]),
+    ("tvm_version_class", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_lib_is_vulnerable_host", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                                  ctypes.c_size_t]),
+    ("tvm_library_type", ctypes.c_char_p, [ctypes.c_char_p]),
+    ("tvm_library_detect", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.POINTER(Package), ctypes.c_size_t,
+                                          ctypes.POINTER(Result), ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_library_detect_vulnerabilities", ctypes.c_int, [_P, ctypes.c_char_p, Str, Str, Str, ctypes.POINTER(Result),
+                                                          ctypes.c_char_p, ctypes.c_size_t]),
 ]
 
 EXPORTED = [s[0] for s in _SIG]

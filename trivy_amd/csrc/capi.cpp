@@ -11,7 +11,8 @@
 #include "db.h"
 #include "drivers.h"
 #include "engine.h"
-#include "verkey.h"
+#include "libdb.h"
+#include "libver.h"
 
 using namespace tvm;
 
@@ -217,6 +218,17 @@ int tvm_engine_swap(tvm_engine* e, tvm_db* db, char* err, size_t errlen) {
 }
 
 uint64_t tvm_engine_table_bytes(const tvm_engine* e) { return e ? e->eng->table_bytes() : 0; }
+
+int tvm_engine_verify(tvm_engine* e, char* err, size_t errlen) {
+  if (!e) return TVM_EINVAL;
+  std::unique_lock<std::shared_mutex> lk(e->mu);
+  std::string msg;
+  if (!e->eng->verify(msg)) {
+    set_err(err, errlen, msg);
+    return TVM_EDEVICE;
+  }
+  return TVM_OK;
+}
 
 int tvm_engine_set_variant(tvm_engine* e, int v) {
   if (!e) return -1;
@@ -463,8 +475,69 @@ int tvm_version_key(int grammar, const char* s, size_t n, uint8_t* out, size_t c
     }
   } sink{out, cap};
   if (grammar <= 0 || grammar > 255 || !s) return -1;
-  if (!encode_version(uint8_t(grammar), reinterpret_cast<const uint8_t*>(s), uint32_t(n), sink)) return -1;
+  uint32_t cls = 0;
+  if (!encode_version_cls(uint8_t(grammar), reinterpret_cast<const uint8_t*>(s), uint32_t(n), sink, cls)) return -1;
   return int(sink.n);
 }
+
+int tvm_version_class(int grammar, const char* s, size_t n) {
+  struct Sink {
+    void put(uint8_t) {}
+  } sink;
+  uint32_t cls = 0;
+  if (grammar <= 0 || grammar > 255 || !s) return -1;
+  if (!encode_version_cls(uint8_t(grammar), reinterpret_cast<const uint8_t*>(s), uint32_t(n), sink, cls)) return -1;
+  return int(cls);
+}
+
+int tvm_lib_is_vulnerable_host(int grammar, const char* ver, size_t ver_len, const char* advisory_json,
+                               size_t json_len) {
+  Advisory a;
+  std::string e;
+  if (!ver || !advisory_json || !decode_advisory(std::string_view(advisory_json, json_len), a, e)) return -1;
+  const LibRows r = lib_compile_advisory(uint8_t(grammar), a.vulnerable, a.patched, a.unaffected);
+  return lib_rows_contain(uint8_t(grammar), r, std::string(ver, ver_len)) ? 1 : 0;
+}
+
+int tvm_library_detect(tvm_engine* e, const char* lib_type, const tvm_package* pkgs, size_t n, tvm_result* out,
+                       char* err, size_t errlen) {
+  if (!e || !lib_type || !out || (n && !pkgs)) return TVM_EINVAL;
+  memset(out, 0, sizeof(*out));
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  std::vector<Pkg> p = to_pkgs(pkgs, n);
+  std::vector<Vuln> vulns;
+  std::string msg;
+  const DetectStatus st = library_detect(*e->eng, lib_type, p, vulns, msg);
+  if (st == DETECT_UNSUPPORTED_OS) return TVM_EUNSUPPORTED_TYPE;
+  if (st != DETECT_OK) {
+    set_err(err, errlen, msg);
+    return TVM_EDETECT;
+  }
+  export_result(e->eng->db(), std::move(vulns), false, out);
+  return TVM_OK;
+}
+
+int tvm_library_detect_vulnerabilities(tvm_engine* e, const char* lib_type, tvm_str pkg_id, tvm_str pkg_name,
+                                       tvm_str pkg_ver, tvm_result* out, char* err, size_t errlen) {
+  if (!e || !lib_type || !out) return TVM_EINVAL;
+  memset(out, 0, sizeof(*out));
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  std::vector<Pkg> p(1);
+  p[0].id = sv(pkg_id);
+  p[0].name = sv(pkg_name);
+  p[0].version = sv(pkg_ver);
+  std::vector<Vuln> vulns;
+  std::string msg;
+  const DetectStatus st = library_detect_vulnerabilities(*e->eng, lib_type, p, vulns, msg);
+  if (st == DETECT_UNSUPPORTED_OS) return TVM_EUNSUPPORTED_TYPE;
+  if (st != DETECT_OK) {
+    set_err(err, errlen, msg);
+    return TVM_EDETECT;
+  }
+  export_result(e->eng->db(), std::move(vulns), false, out);
+  return TVM_OK;
+}
+
+const char* tvm_library_type(const char* lib_type) { return lib_type ? library_ecosystem(lib_type) : nullptr; }
 
 }  // extern "C"

@@ -17,6 +17,13 @@ enum Cmp : uint8_t {
   CMP_DEB = 1,   // knqyf263/go-deb-version (debian, ubuntu, amazon)
   CMP_APK = 2,   // knqyf263/go-apk-version (alpine, wolfi, chainguard)
   CMP_RPM = 3,   // knqyf263/go-rpm-version (redhat/centos, alma, rocky, oracle, suse, photon, mariner)
+  // library grammars (libver.h; pkg/detector/library/driver.go:25-93)
+  CMP_GENERIC = 4,  // aquasecurity/go-version (cargo, composer, go, nuget, pub, erlang, conan, swift, k8s)
+  CMP_NPM = 5,      // aquasecurity/go-npm-version
+  CMP_PEP440 = 6,   // aquasecurity/go-pep440-version
+  CMP_MAVEN = 7,    // masahiro331/go-mvn-version
+  CMP_GEM = 8,      // aquasecurity/go-gem-version (rubygems, cocoapods)
+  CMP_BITNAMI = 9,  // bitnami/go-version
 };
 
 // Driver families (reference pkg/detector/ospkg/detect.go:32-48 and library/driver.go:25-93).
@@ -35,6 +42,7 @@ enum Drv : uint8_t {
   DRV_SUSE = 11,
   DRV_PHOTON = 12,
   DRV_MARINER = 13,
+  DRV_LIBRARY = 14,  // pkg/detector/library (one platform per ecosystem prefix "eco::")
 };
 
 // Per-platform flags (device-visible).
@@ -81,7 +89,9 @@ struct alignas(16) RowAux {
   uint16_t n_arch;
   uint16_t n_cpe;
 };
-enum : uint32_t { AUX_ARCH_RH = 1, AUX_ARCH_IN = 2, AUX_CPE = 4, AUX_TAG = 8 };
+//   AUX_CLASS     library rows: pass if bit <installed version class> of `tag` is set
+//                 (libver.h classes: npm pre-release, PEP 440 local/pre/post).
+enum : uint32_t { AUX_ARCH_RH = 1, AUX_ARCH_IN = 2, AUX_CPE = 4, AUX_TAG = 8, AUX_CLASS = 16 };
 
 // Package attributes (uint2 per package, only for batches that carry filtered rows):
 // x = arch id | PA_NOARCH, y = ksplice tag (oracle) or CPE-set id (redhat).

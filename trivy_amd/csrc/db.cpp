@@ -4,7 +4,8 @@
 #include <algorithm>
 
 #include "json.h"
-#include "verkey.h"
+#include "libdb.h"
+#include "libver.h"
 
 namespace tvm {
 namespace {
@@ -353,6 +354,93 @@ uint32_t DB::intern_key(const std::vector<uint8_t>& k) {
   return off;
 }
 
+uint8_t ecosystem_grammar(std::string_view eco) {
+  if (eco == "rubygems" || eco == "cocoapods") return CMP_GEM;
+  if (eco == "maven") return CMP_MAVEN;
+  if (eco == "npm") return CMP_NPM;
+  if (eco == "pip") return CMP_PEP440;
+  if (eco == "bitnami") return CMP_BITNAMI;
+  if (eco == "cargo" || eco == "composer" || eco == "go" || eco == "nuget" || eco == "pub" || eco == "erlang" ||
+      eco == "conan" || eco == "swift" || eco == "k8s")
+    return CMP_GENERIC;
+  return CMP_NONE;
+}
+
+std::string create_fixed_versions(const Advisory& a) {
+  std::vector<std::string> out;
+  auto add = [&](std::string v) {
+    if (std::find(out.begin(), out.end(), v) == out.end()) out.push_back(std::move(v));
+  };
+  auto trim = [](std::string_view v) {
+    const char* ws = " \t\n\v\f\r";
+    const size_t b = v.find_first_not_of(ws);
+    if (b == std::string_view::npos) return std::string();
+    return std::string(v.substr(b, v.find_last_not_of(ws) - b + 1));
+  };
+  if (!a.patched.empty()) {
+    for (const std::string& v : a.patched) add(v);
+  } else {
+    for (const std::string& v : a.vulnerable) {
+      size_t b = 0;
+      for (;;) {
+        const size_t e = v.find(',', b);
+        std::string s = trim(std::string_view(v).substr(b, e == std::string::npos ? std::string::npos : e - b));
+        if (s.rfind("<=", 0) != 0 && s.rfind("<", 0) == 0) add(trim(std::string_view(s).substr(1)));
+        if (e == std::string::npos) break;
+        b = e + 1;
+      }
+    }
+  }
+  std::string j;
+  for (size_t i = 0; i < out.size(); i++) j += (i ? ", " : "") + out[i];
+  return j;
+}
+
+// trivy-db GetAdvisories("<eco>::", name): every root bucket with the prefix, in bbolt
+// key order; a later root overwrites an earlier one's value for the same vulnID; then
+// each value is decoded (a failure poisons the key: the reference fails the call only
+// when a package looks it up, driver_test.go "malformed JSON").
+void DB::flatten_library(uint32_t plat, const std::vector<std::pair<const Bucket*, int32_t>>& roots) {
+  std::map<std::string, std::map<std::string, std::pair<const std::string*, int32_t>>> merged;
+  for (const auto& [root, ds] : roots)
+    for (const auto& [pkg, bkt] : root->sub)
+      for (const auto& [vid, val] : bkt.kv)
+        if (!val.empty()) merged[pkg][vid] = {&val, ds};
+  for (const auto& [pkg, vals] : merged) {
+    Key key;
+    key.plat = plat;
+    key.name = pkg;
+    for (const auto& [vid, v] : vals) {
+      const auto& [val, ds] = v;
+      if (ds == -2) {  // the root's data-source entry does not decode
+        if (!key.poisoned) key.err = "failed to get data source";
+        key.poisoned = true;
+        continue;
+      }
+      Advisory a;
+      std::string err;
+      if (!decode_advisory(*val, a, err)) {
+        if (!key.poisoned) key.err = "failed to unmarshal advisory JSON: " + err;
+        key.poisoned = true;
+        continue;
+      }
+      a.vuln_id = vid;
+      if (ds >= 0) {
+        a.data_source = ds;
+      } else if (a.has_inline_source) {
+        sources.push_back(a.inline_source);
+        a.data_source = int32_t(sources.size() - 1);
+      }
+      a.entries.clear();
+      a.lib_fixed = create_fixed_versions(a);
+      key.advs.push_back(uint32_t(advs.size()));
+      advs.push_back(std::move(a));
+    }
+    if (key.poisoned) key.advs.clear();
+    keys.push_back(std::move(key));
+  }
+}
+
 void DB::flatten_os(uint32_t plat, const Bucket& root, int32_t ds) {
   const Platform& P = plats[plat];
   for (const auto& [pkg, bkt] : root.sub) {
@@ -365,6 +453,7 @@ void DB::flatten_os(uint32_t plat, const Bucket& root, int32_t ds) {
     };
     for (const auto& [vid, val] : bkt.kv) {
       std::string err;
+      if (val.empty()) continue;  // trivy-db forEach skips empty values
       if (P.drv == DRV_REDHAT) {
         // trivy-db redhat-oval Get: one advisory per (entry, CVE); CPE filtering per package
         std::vector<RhEntry> ents;
@@ -426,6 +515,60 @@ void DB::flatten_os(uint32_t plat, const Bucket& root, int32_t ds) {
 // Advisory -> interval row(s) of its driver (SURVEY.md §8a' "unfixed" and parse-error
 // columns).  Returns false when the advisory can never be reported (no row).
 bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::vector<uint8_t>& kb) {
+  if (P.drv == DRV_LIBRARY) {
+    // compare.IsVulnerable as disjoint intervals per version class (libdb.h); classes
+    // sharing an interval share its row; a row that holds for a subset of the classes
+    // carries an AUX_CLASS filter.
+    const LibRows lr = lib_compile_advisory(P.cmp, a.vulnerable, a.patched, a.unaffected);
+    if (lr.always) {
+      Row r{};
+      r.adv = ai | ROW_ALWAYS;
+      r.lo_len = r.hi_len = KEY_INF;
+      rows.push_back(r);
+      aux.push_back(RowAux{});
+      return true;
+    }
+    std::vector<std::pair<KInterval, uint32_t>> ivs;  // interval -> class mask
+    auto same = [](const KBound& x, const KBound& y) {
+      return x.inf == y.inf && (x.inf || (x.k == y.k && x.incl == y.incl));
+    };
+    for (int c = 0; c < lr.ncls; c++)
+      for (const KInterval& v : lr.cls[size_t(c)]) {
+        bool found = false;
+        for (auto& [w, mask] : ivs)
+          if (same(w.lo, v.lo) && same(w.hi, v.hi)) {
+            mask |= 1u << c;
+            found = true;
+          }
+        if (!found) ivs.push_back({v, 1u << c});
+      }
+    const uint32_t all = (1u << lr.ncls) - 1;
+    for (const auto& [v, mask] : ivs) {
+      Row r{};
+      r.adv = ai;
+      r.lo_len = r.hi_len = KEY_INF;
+      auto put = [&](const KBound& b, uint32_t& off, uint16_t& len, bool hi) {
+        if (b.inf) return;
+        kb.assign(b.k.begin(), b.k.end());
+        off = intern_key(kb);
+        len = uint16_t(std::min<size_t>(kb.size(), KEY_LEN_MASK) | (b.incl ? KEY_INCL : 0));
+        if (hi)
+          for (size_t i = 0; i < kb.size() && i < 16; i++) (i < 8 ? r.hi_pre0 : r.hi_pre1) |= uint64_t(kb[i]) << (8 * (i % 8));
+      };
+      put(v.lo, r.lo_off, r.lo_len, false);
+      put(v.hi, r.hi_off, r.hi_len, true);
+      RowAux x{};
+      if (mask != all) {
+        r.adv |= ROW_FILTER;
+        x.kind = AUX_CLASS;
+        x.tag = mask;
+        has_filters = true;
+      }
+      rows.push_back(r);
+      aux.push_back(x);
+    }
+    return !ivs.empty();
+  }
   Row r{};
   r.adv = ai;
   r.lo_len = KEY_INF;
@@ -609,6 +752,26 @@ bool DB::finalize(std::string& err) {
         if (decode_int_list(v, ids)) (*dst)[k] = std::move(ids);
       }
     }
+  }
+  // library ecosystems: root buckets "<eco>::<source>" grouped by prefix
+  std::map<std::string, std::vector<std::pair<const Bucket*, int32_t>>> eco_roots;
+  for (const auto& [name, b] : root_.sub) {
+    const size_t sep = name.find("::");
+    if (sep == std::string::npos) continue;
+    const std::string eco = name.substr(0, sep);
+    if (ecosystem_grammar(eco) == CMP_NONE) continue;
+    int32_t ds = -1;
+    auto d = ds_of_root.find(name);
+    if (d != ds_of_root.end() && !sources[size_t(d->second)].empty()) ds = d->second;
+    if (ds_err.count(name)) ds = -2;
+    eco_roots[eco + "::"].push_back({&b, ds});
+  }
+  for (const auto& [prefix, roots] : eco_roots) {
+    const uint32_t pid = uint32_t(plats.size());
+    plats.push_back(Platform{prefix, DRV_LIBRARY, ecosystem_grammar(prefix.substr(0, prefix.size() - 2)),
+                             PLAT_LOOKUP_FIRST});
+    plat_by_name_[prefix] = pid;
+    flatten_library(pid, roots);
   }
   for (const auto& [name, b] : root_.sub) {
     uint8_t drv, cmp;

@@ -42,7 +42,14 @@ struct Advisory {
   std::vector<Advisory> entries;       // Rocky: per-arch entries (types.Advisory.Entries)
   std::vector<int64_t> cpes;           // Red Hat: the entry's affected CPE indices
   bool arch_entry = false;             // Rocky: expanded from an arch entry (arch must be listed)
+  std::string lib_fixed;               // library: createFixedVersions (driver.go:139-159)
 };
+
+// Library ecosystems: trivy-db bucket prefix (ecosystem) and the grammar its comparer
+// uses (driver.go:25-93); CMP_NONE when no LangType maps to it.
+uint8_t ecosystem_grammar(std::string_view eco);
+// createFixedVersions (driver.go:139-159).
+std::string create_fixed_versions(const Advisory& a);
 
 // Decodes one advisory value (Go json.Unmarshal into types.Advisory).
 bool decode_advisory(std::string_view json, Advisory& a, std::string& err);
@@ -117,6 +124,7 @@ class DB {
   uint32_t intern_key(const std::vector<uint8_t>& k);
   uint32_t intern_arch(const std::string& a);
   void flatten_os(uint32_t plat, const Bucket& b, int32_t ds);
+  void flatten_library(uint32_t plat, const std::vector<std::pair<const Bucket*, int32_t>>& roots);
   bool compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::vector<uint8_t>& kb);
   void build_index();
 };

@@ -579,4 +579,85 @@ DetectStatus ospkg_detect(Engine& eng, std::string_view family, std::string_view
   return DETECT_OK;
 }
 
+// ---------------------------------------------------------------- library ------------------
+const char* library_ecosystem(std::string_view t) {
+  // NewDriver (driver.go:25-93): LangType -> ecosystem
+  static const std::map<std::string, const char*, std::less<>> m = {
+      {"bundler", "rubygems"}, {"gemspec", "rubygems"}, {"rustbinary", "cargo"}, {"cargo", "cargo"},
+      {"composer", "composer"}, {"gobinary", "go"}, {"gomod", "go"}, {"jar", "maven"}, {"pom", "maven"},
+      {"gradle", "maven"}, {"npm", "npm"}, {"yarn", "npm"}, {"pnpm", "npm"}, {"node-pkg", "npm"},
+      {"javascript", "npm"}, {"nuget", "nuget"}, {"dotnet-core", "nuget"}, {"packages-props", "nuget"},
+      {"pipenv", "pip"}, {"poetry", "pip"}, {"pip", "pip"}, {"python-pkg", "pip"}, {"pub", "pub"},
+      {"hex", "erlang"}, {"conan", "conan"}, {"swift", "swift"}, {"cocoapods", "cocoapods"},
+      {"bitnami", "bitnami"}, {"kubernetes", "k8s"},
+  };
+  auto it = m.find(t);
+  return it == m.end() ? nullptr : it->second;
+}
+
+std::string normalize_pkg_name(std::string_view eco, std::string_view name) {
+  std::string n(name);
+  if (eco == "pip") {
+    for (char& c : n) {
+      if (c >= 'A' && c <= 'Z') c = char(c - 'A' + 'a');
+      else if (c == '_') c = '-';
+    }
+  }
+  return n;
+}
+
+namespace {
+
+DetectStatus library_run(Engine& eng, std::string_view lib_type, const std::vector<Pkg>& pkgs, bool wrap,
+                         std::vector<Vuln>& out, std::string& err) {
+  const char* eco = library_ecosystem(lib_type);
+  if (!eco) return DETECT_UNSUPPORTED_OS;
+  const DB& db = eng.db();
+  Plan plan;
+  plan.plat = db.find_plat(std::string(eco) + "::");
+  std::vector<std::string> names(pkgs.size());
+  for (size_t i = 0; i < pkgs.size(); i++) {
+    names[i] = normalize_pkg_name(eco, pkgs[i].name);
+    plan.add(false, names[i], pkgs[i].version);
+  }
+  std::vector<uint2> pairs;
+  std::string key_err;
+  if (!run_plan(eng, plan, pairs, key_err, err)) return DETECT_ERROR;
+  if (!key_err.empty()) {
+    const std::string e(eco);
+    err = "failed to get " + e + " advisories: " + key_err;  // driver.go:115-117
+    if (wrap)  // detect.go:30-32, 18-20
+      err = "failed to scan " + e + " vulnerabilities: failed to detect " + e + " vulnerabilities: " + err;
+    return DETECT_ERROR;
+  }
+  for (const uint2& m : pairs) {
+    const Pkg& p = pkgs[m.x];
+    const Advisory& a = db.advs[m.y];
+    Vuln v;
+    v.pkg = m.x;
+    v.copy = COPY_PKG_ID | COPY_PKG_NAME | (wrap ? COPY_IDENTIFIER | COPY_LAYER : 0);
+    v.vuln_id = a.vuln_id;
+    v.pkg_id = std::string(p.id);
+    v.pkg_name = std::string(p.name);
+    v.installed = std::string(p.version);
+    v.fixed = a.lib_fixed;
+    v.data_source = a.data_source;
+    if (wrap) v.pkg_path = std::string(p.file_path);  // detect.go:33-37
+    out.push_back(std::move(v));
+  }
+  return DETECT_OK;
+}
+
+}  // namespace
+
+DetectStatus library_detect(Engine& eng, std::string_view lib_type, const std::vector<Pkg>& pkgs,
+                            std::vector<Vuln>& out, std::string& err) {
+  return library_run(eng, lib_type, pkgs, true, out, err);
+}
+
+DetectStatus library_detect_vulnerabilities(Engine& eng, std::string_view lib_type, const std::vector<Pkg>& pkgs,
+                                            std::vector<Vuln>& out, std::string& err) {
+  return library_run(eng, lib_type, pkgs, false, out, err);
+}
+
 }  // namespace tvm

@@ -74,4 +74,17 @@ DetectStatus ospkg_detect(Engine& eng, std::string_view family, std::string_view
 // Unix time of time.Date(y, m, d, 23, 59, 59, 0, UTC).
 int64_t eol_unix(int y, int m, int d);
 
+// ---- library (pkg/detector/library) ------------------------------------------------
+// NewDriver(libType) -> Driver.Type(): the ecosystem, or nullptr when unsupported.
+const char* library_ecosystem(std::string_view lib_type);
+// library.Detect (detect.go:11-42): DETECT_UNSUPPORTED_OS means NewDriver returned false
+// (the reference returns nil, nil).  Vuln.pkg indexes pkgs (Name, Version, ID, FilePath).
+DetectStatus library_detect(Engine& eng, std::string_view lib_type, const std::vector<Pkg>& pkgs,
+                            std::vector<Vuln>& out, std::string& err);
+// (*Driver).DetectVulnerabilities (driver.go:111-137) for each package, errors unwrapped.
+DetectStatus library_detect_vulnerabilities(Engine& eng, std::string_view lib_type, const std::vector<Pkg>& pkgs,
+                                            std::vector<Vuln>& out, std::string& err);
+// vulnerability.NormalizePkgName (trivy-db): pip names lower-cased, "_" -> "-".
+std::string normalize_pkg_name(std::string_view eco, std::string_view name);
+
 }  // namespace tvm

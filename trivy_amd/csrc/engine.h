@@ -104,6 +104,8 @@ class Engine {
   // Kernel variant (tile size / LDS budget); returns the previous one.  Default 0,
   // overridable with the TVM_VARIANT environment variable at open().
   int set_variant(int v);
+  // Integrity check: the device tables still equal the host images (bytes compared).
+  bool verify(std::string& err);
   int variant() const { return variant_; }
 
  private:

@@ -32,7 +32,7 @@
 #include <cstring>
 
 #include "db.h"
-#include "verkey.h"
+#include "libver.h"
 
 namespace tvm {
 
@@ -56,7 +56,7 @@ struct MatchArgs {
   uint64_t spill_cap;
 };
 
-enum : uint32_t { KI_VALID = 1u << 31, KI_SPILL = 1u << 30, KI_LEN = 0x3FFFu };
+enum : uint32_t { KI_VALID = 1u << 31, KI_SPILL = 1u << 30, KI_LEN = 0x3FFFu, KI_CLS_SHIFT = 26, KI_CLS_MASK = 7u };
 
 template <int T, int KW, int MB>
 struct TileShared {
@@ -121,7 +121,7 @@ __device__ __forceinline__ uint32_t pair_pkg(const S& s, uint32_t j) {
 }
 
 // Per-package predicates of a ROW_FILTER row (common.h RowAux).
-__device__ __attribute__((noinline)) bool aux_pass(const MatchArgs& a, uint32_t ridx, uint2 pa) {
+__device__ __attribute__((noinline)) bool aux_pass(const MatchArgs& a, uint32_t ridx, uint2 pa, uint32_t ki) {
   const RowAux x = a.db.aux[ridx];
   const uint32_t* ids = a.db.aux_ids + x.list_off;
   if (x.kind & (AUX_ARCH_RH | AUX_ARCH_IN)) {
@@ -141,13 +141,14 @@ __device__ __attribute__((noinline)) bool aux_pass(const MatchArgs& a, uint32_t 
     if (!ok) return false;
   }
   if ((x.kind & AUX_TAG) && x.tag != pa.y) return false;
+  if ((x.kind & AUX_CLASS) && !((x.tag >> ((ki >> KI_CLS_SHIFT) & KI_CLS_MASK)) & 1u)) return false;
   return true;
 }
 
 // Interval test of package q's installed key against one row (global index ridx).
 template <int KW, class S>
 __device__ __forceinline__ bool eval_row(const MatchArgs& a, const S& s, uint32_t q, const Row& row, uint32_t ridx) {
-  if ((row.adv & ROW_FILTER) && !aux_pass(a, ridx, s.pattr[q])) return false;
+  if ((row.adv & ROW_FILTER) && !aux_pass(a, ridx, s.pattr[q], s.kinfo[q])) return false;
   if (row.adv & ROW_ALWAYS) return true;
   const uint32_t ki = s.kinfo[q];
   if (!(ki & KI_VALID)) return false;
@@ -285,7 +286,8 @@ __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
     uint32_t need = 0;
     if ((key_bound(pi.cmp, vlen) + 7) / 8 > uint32_t(KW)) {  // might not fit: size it exactly
       CountSink cs;
-      need = encode_version(pi.cmp, ver, vlen, cs) ? (cs.n + 7) / 8 : 0;
+      uint32_t cls_unused;
+      need = encode_version_cls(pi.cmp, ver, vlen, cs, cls_unused) ? (cs.n + 7) / 8 : 0;
     }
     bool spill_ok = true;
     if (need > uint32_t(KW)) {
@@ -302,9 +304,10 @@ __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
     bool valid = false;
     if (spill_ok) {
       WordSink ws(dst);
-      valid = encode_version(pi.cmp, ver, vlen, ws);
+      uint32_t cls = 0;
+      valid = encode_version_cls(pi.cmp, ver, vlen, ws, cls);
       ws.flush();
-      kinfo |= (ws.n & KI_LEN) | (valid ? KI_VALID : 0u);
+      kinfo |= (ws.n & KI_LEN) | (valid ? KI_VALID : 0u) | ((cls & KI_CLS_MASK) << KI_CLS_SHIFT);
     }
     // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup
     if (valid || (pi.flags & PLAT_LOOKUP_FIRST)) {
@@ -501,7 +504,7 @@ bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
   b.arena_bytes = hb.arena.size();
   b.spill_words = 0;
   for (const uint4& d : hb.desc) {
-    const uint32_t need = (key_bound(CMP_APK, d.w >> 16) + 7) / 8;  // the widest grammar bound
+    const uint32_t need = (key_bound_any(d.w >> 16) + 7) / 8;  // the widest grammar bound
     if (need > uint32_t(kMinKeyWords)) b.spill_words += need;  // bound for every variant
   }
   if (!hip_ok(hipMalloc(&b.desc, std::max<size_t>(hb.desc.size(), 1) * sizeof(uint4)), "hipMalloc(batch)", err)) return false;
@@ -648,6 +651,33 @@ bool Engine::match_host(const HostBatch& hb, std::vector<uint2>& out, int64_t& e
   }
   free_batch(b);
   return ok;
+}
+
+}  // namespace tvm
+
+namespace tvm {
+
+bool Engine::verify(std::string& err) {
+  (void)hipSetDevice(dev_);
+  auto check = [&](const void* dev, const void* host, size_t bytes, const char* what) {
+    if (!bytes) return true;
+    std::vector<uint8_t> tmp(bytes);
+    if (!hip_ok(hipMemcpy(tmp.data(), dev, bytes, hipMemcpyDeviceToHost), "D2H verify", err)) return false;
+    if (std::memcmp(tmp.data(), host, bytes) != 0) {
+      err = std::string("device table differs from the host image: ") + what;
+      return false;
+    }
+    return true;
+  };
+  const DB& db = *db_;
+  return check(d_.slot_hash, db.slot_hash.data(), db.slot_hash.size() * 8, "slot_hash") &&
+         check(d_.slot_val, db.slot_val.data(), db.slot_val.size() * sizeof(SlotVal), "slot_val") &&
+         check(d_.name_arena, db.name_arena.data(), db.name_arena.size(), "name_arena") &&
+         check(d_.rows, db.rows.data(), db.rows.size() * sizeof(Row), "rows") &&
+         check(d_.key_words, db.key_words.data(), db.key_words.size() * 8, "key_words") &&
+         check(d_.plats, db.plat_info.data(), db.plat_info.size() * sizeof(PlatInfo), "plats") &&
+         check(d_.aux, db.aux.data(), db.aux.size() * sizeof(RowAux), "aux") &&
+         check(d_.aux_ids, db.aux_ids.data(), db.aux_ids.size() * 4, "aux_ids");
 }
 
 }  // namespace tvm

@@ -1,0 +1,825 @@
+// Sort-key encoders of the library (language-package) version grammars (host + device).
+//
+// Same contract as verkey.h: each grammar maps a version string to a byte string whose
+// plain lexicographic order (common.h key_cmp) is the grammar's version order, plus a
+// small "class" (npm: pre-release; PEP 440: local / pre-release / post-release) that the
+// constraint compiler needs where a grammar's constraint semantics are not interval-shaped
+// over the order alone (node-semver's pre-release rule, PEP 440's exclusive comparisons).
+// Reference call sites: pkg/detector/library/compare/compare.go:58-78 and
+// compare/{npm,pep440,maven,rubygems,bitnami}/compare.go:20-32.  The six third-party
+// modules (reference go.mod:16-19,37,73) are absent; their published algorithms are
+// restated (oracle/library.py is the independent pairwise restatement the keys are fuzzed
+// against).  Parsing mirrors each module's regular expression.
+#pragma once
+#include "verkey.h"
+
+namespace tvm {
+
+// ---------------------------------------------------------------------------- helpers ---
+TVM_HD bool lv_alpha(uint8_t c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); }
+TVM_HD bool lv_alnum(uint8_t c) { return lv_alpha(c) || is_adigit(c); }
+TVM_HD uint8_t lv_lower(uint8_t c) { return (c >= 'A' && c <= 'Z') ? uint8_t(c + 32) : c; }
+TVM_HD bool lv_space(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\f' || c == '\v'; }
+
+// Decimal digits [b, e) as a uint64; false on overflow.
+TVM_HD bool lv_u64(const uint8_t* s, uint32_t b, uint32_t e, uint64_t& v) {
+  v = 0;
+  for (uint32_t i = b; i < e; i++) {
+    const uint64_t d = uint64_t(s[i] - '0');
+    if (v > (~0ULL - d) / 10) return false;
+    v = v * 10 + d;
+  }
+  return true;
+}
+
+// Unsigned 64-bit values: 0x80+k then k big-endian bytes (put_sint's code for v >= 0).
+template <class Sink>
+TVM_HD void put_uvar(uint64_t u, Sink& o) {
+  uint32_t k = 0;
+  for (uint64_t t = u; t; t >>= 8) k++;
+  o.put(uint8_t(0x80 + k));
+  for (int b = int(k) - 1; b >= 0; b--) o.put(uint8_t(u >> (8 * b)));
+}
+
+// Arbitrary-precision decimal: leading zeros dropped, digit count, digits two per byte.
+template <class Sink>
+TVM_HD void put_digits(const uint8_t* s, uint32_t b, uint32_t e, Sink& o) {
+  while (b < e && s[b] == '0') b++;
+  const uint32_t len = e - b;
+  if (len < 0xFA) {
+    o.put(uint8_t(len));
+  } else {
+    o.put(0xFA);
+    o.put(uint8_t(len >> 8));
+    o.put(uint8_t(len));
+  }
+  for (uint32_t j = b; j < e; j += 2) {
+    const uint8_t hi = uint8_t(s[j] - '0'), lo = j + 1 < e ? uint8_t(s[j + 1] - '0') : 0;
+    o.put(uint8_t((hi << 4) | lo));
+  }
+}
+
+// semver-style identifier list "a.b.c" over [b, e) with identifier bytes allowed by `ok`.
+template <class F>
+TVM_HD bool lv_idents(const uint8_t* s, uint32_t b, uint32_t e, F ok) {
+  if (b >= e) return false;
+  uint32_t run = 0;
+  for (uint32_t i = b; i < e; i++) {
+    if (s[i] == '.') {
+      if (!run) return false;
+      run = 0;
+    } else if (ok(s[i])) {
+      run++;
+    } else {
+      return false;
+    }
+  }
+  return run > 0;
+}
+
+// Pre-release identifiers: numeric (all digits) = 0x01 + digits, else 0x02 + bytes + 0x00;
+// list end 0x00 (a shorter list sorts first; numeric < alphanumeric).
+template <class Sink>
+TVM_HD void put_idents(const uint8_t* s, uint32_t b, uint32_t e, Sink& o) {
+  uint32_t i = b;
+  while (i < e) {
+    uint32_t j = i;
+    bool num = true;
+    while (j < e && s[j] != '.') num &= is_adigit(s[j++]);
+    if (num) {
+      o.put(0x01);
+      put_digits(s, i, j, o);
+    } else {
+      o.put(0x02);
+      for (uint32_t k = i; k < j; k++) o.put(s[k]);
+      o.put(0x00);
+    }
+    i = j + 1;
+  }
+  o.put(0x00);
+}
+
+TVM_HD bool gen_ident_char(uint8_t c) { return lv_alnum(c) || c == '-' || c == '~'; }
+TVM_HD bool npm_ident_char(uint8_t c) { return lv_alnum(c) || c == '-'; }
+
+// =========================================================================== GENERIC ====
+// github.com/aquasecurity/go-version (go.mod:19), hashicorp-style:
+//   v?N(.N)*  ( -IDENTS | [A-Za-z-~]IDENTS )?  (+IDENTS)?      IDENT = [0-9A-Za-z-~]+
+// Order: zero-padded numeric segments, then pre-release (none > some; semver identifier
+// precedence); build metadata ignored.  Bitnami (github.com/bitnami/go-version, go.mod:37)
+// reads an all-digit "-N" as a package revision compared after everything else.
+// Key: segments (trailing zeros dropped) as put_sint, 0x01, then 0x03 (release) or
+// 0x02 + identifiers, then (bitnami) the revision digits.
+struct GenParts {
+  uint32_t rel_b, rel_e;   // release span (after the optional 'v')
+  uint32_t pre_b, pre_e;   // pre-release identifiers (empty: none)
+  uint32_t rev_b, rev_e;   // bitnami revision digits (empty: 0)
+  uint32_t n_segs_key;     // segments up to the last non-zero one
+};
+
+TVM_HD bool gen_parse(const uint8_t* s, uint32_t n, bool bitnami, GenParts& g) {
+  uint32_t i = 0;
+  if (i < n && s[i] == 'v') i++;
+  g.rel_b = i;
+  uint32_t segs = 0, last_nz = 0;
+  for (;;) {
+    const uint32_t b = i;
+    while (i < n && is_adigit(s[i])) i++;
+    if (i == b) return false;
+    uint64_t v;
+    if (!lv_u64(s, b, i, v)) return false;  // part.NewUint64 overflow
+    segs++;
+    if (v) last_nz = segs;
+    if (i + 1 < n && s[i] == '.' && is_adigit(s[i + 1])) {
+      i++;
+      continue;
+    }
+    break;
+  }
+  g.rel_e = i;
+  g.n_segs_key = last_nz;
+  uint32_t plus = n;
+  for (uint32_t k = i; k < n; k++)
+    if (s[k] == '+') { plus = k; break; }
+  if (plus < n && !lv_idents(s, plus + 1, n, gen_ident_char)) return false;
+  g.pre_b = g.pre_e = i;
+  g.rev_b = g.rev_e = 0;
+  if (i < plus) {
+    if (s[i] == '-' && lv_idents(s, i + 1, plus, gen_ident_char)) {
+      g.pre_b = i + 1;
+      g.pre_e = plus;
+      bool digits = true;
+      for (uint32_t k = i + 1; k < plus; k++) digits &= is_adigit(s[k]);
+      if (bitnami && digits) {
+        g.rev_b = i + 1;
+        g.rev_e = plus;
+        g.pre_b = g.pre_e = i;
+      }
+    } else if ((lv_alpha(s[i]) || s[i] == '-' || s[i] == '~') && lv_idents(s, i, plus, gen_ident_char)) {
+      g.pre_b = i;
+      g.pre_e = plus;
+    } else {
+      return false;
+    }
+  }
+  return true;
+}
+
+template <class Sink>
+TVM_HD void gen_emit_release(const uint8_t* s, const GenParts& g, Sink& o) {
+  uint32_t i = g.rel_b;
+  for (uint32_t k = 0; k < g.n_segs_key; k++) {
+    const uint32_t b = i;
+    while (i < g.rel_e && is_adigit(s[i])) i++;  // bounded: the bytes after a version are arbitrary
+    uint64_t v;
+    lv_u64(s, b, i, v);
+    put_uvar(v, o);
+    i++;
+  }
+}
+
+template <class Sink>
+TVM_HD void gen_emit(const uint8_t* s, const GenParts& g, bool bitnami, Sink& o) {
+  gen_emit_release(s, g, o);
+  o.put(0x01);
+  if (g.pre_e > g.pre_b) {
+    o.put(0x02);
+    put_idents(s, g.pre_b, g.pre_e, o);
+  } else {
+    o.put(0x03);
+  }
+  if (bitnami) put_digits(s, g.rev_b, g.rev_e, o);
+}
+
+template <class Sink>
+TVM_HD bool gen_encode(const uint8_t* s, uint32_t n, bool bitnami, Sink& o) {
+  GenParts g;
+  if (!gen_parse(s, n, bitnami, g)) return false;
+  gen_emit(s, g, bitnami, o);
+  return true;
+}
+
+// =============================================================================== NPM ====
+// github.com/aquasecurity/go-npm-version (go.mod:17), node-semver:
+//   \s*[v=]*\s*N.N.N (-?IDENTS)? (+IDENTS)? \s*          IDENT = [0-9A-Za-z-]+
+// Key: put_sint(major) put_sint(minor) put_sint(patch), then 0x03 (release) or 0x02 +
+// identifiers.  Class 1 = has a pre-release (node-semver's pre-release gating).
+struct NpmParts {
+  uint32_t num_b[3], num_e[3];
+  uint32_t pre_b, pre_e;
+};
+
+TVM_HD bool npm_parse(const uint8_t* s, uint32_t n, NpmParts& p) {
+  uint32_t i = 0;
+  while (i < n && lv_space(s[i])) i++;
+  while (i < n && (s[i] == 'v' || s[i] == '=')) i++;
+  while (i < n && lv_space(s[i])) i++;
+  for (int k = 0; k < 3; k++) {
+    if (k) {
+      if (i >= n || s[i] != '.') return false;
+      i++;
+    }
+    p.num_b[k] = i;
+    while (i < n && is_adigit(s[i])) i++;
+    p.num_e[k] = i;
+    uint64_t v;
+    if (p.num_e[k] == p.num_b[k] || !lv_u64(s, p.num_b[k], i, v)) return false;
+  }
+  uint32_t end = n;
+  while (end > i && lv_space(s[end - 1])) end--;
+  uint32_t plus = end;
+  for (uint32_t k = i; k < end; k++)
+    if (s[k] == '+') { plus = k; break; }
+  if (plus < end && !lv_idents(s, plus + 1, end, npm_ident_char)) return false;
+  p.pre_b = p.pre_e = i;
+  if (i < plus) {
+    if (s[i] == '-' && lv_idents(s, i + 1, plus, npm_ident_char)) {
+      p.pre_b = i + 1;
+    } else if (lv_idents(s, i, plus, npm_ident_char)) {
+      p.pre_b = i;
+    } else {
+      return false;
+    }
+    p.pre_e = plus;
+  }
+  return true;
+}
+
+template <class Sink>
+TVM_HD void npm_emit(const uint8_t* s, const NpmParts& p, Sink& o) {
+  for (int k = 0; k < 3; k++) {
+    uint64_t v;
+    lv_u64(s, p.num_b[k], p.num_e[k], v);
+    put_uvar(v, o);
+  }
+  if (p.pre_e > p.pre_b) {
+    o.put(0x02);
+    put_idents(s, p.pre_b, p.pre_e, o);
+  } else {
+    o.put(0x03);
+  }
+}
+
+template <class Sink>
+TVM_HD bool npm_encode(const uint8_t* s, uint32_t n, Sink& o, uint32_t& cls) {
+  NpmParts p;
+  if (!npm_parse(s, n, p)) return false;
+  npm_emit(s, p, o);
+  cls = p.pre_e > p.pre_b ? 1u : 0u;
+  return true;
+}
+
+// ============================================================================ PEP 440 ====
+// github.com/aquasecurity/go-pep440-version (go.mod:18), the PEP 440 / packaging
+// VERSION_PATTERN (case-insensitive):
+//   v? (N!)? N(.N)* ([-_.]?(alpha|a|beta|b|preview|pre|c|rc)[-_.]?N?)?
+//   (-N | [-_.]?(post|rev|r)[-_.]?N?)? ([-_.]?dev[-_.]?N?)? (+L([-_.]L)*)?     L = [a-z0-9]+
+// Key (packaging's _cmpkey): put_sint(epoch), release without trailing zeros, 0x01, then
+// PRE (0x01 dev-only / 0x02 letter n / 0x03 none), POST (0x01 none / 0x02 n), DEV
+// (0x01 n / 0x02 none), LOCAL (0x01 none / 0x02 segments 0x00; numeric segments above
+// alphanumeric ones).  Class bits: 1 local, 2 pre-release (pre or dev), 4 post-release.
+struct PepParts {
+  uint64_t epoch;
+  uint32_t rel_b, rel_e, rel_key_segs;
+  int pre_l;                 // -1 none, 0 a, 1 b, 2 rc
+  uint64_t pre_n, post_n, dev_n;
+  bool post, dev;
+  uint32_t loc_b, loc_e;     // local span (empty: none)
+};
+
+TVM_HD bool pep_sep(uint8_t c) { return c == '-' || c == '_' || c == '.'; }
+
+// Case-insensitive keyword at i; returns its length or 0.
+TVM_HD uint32_t pep_kw(const uint8_t* s, uint32_t n, uint32_t i, const char* w) {
+  uint32_t k = 0;
+  while (w[k]) {
+    if (i + k >= n || lv_lower(s[i + k]) != uint8_t(w[k])) return 0;
+    k++;
+  }
+  return k;
+}
+
+TVM_HD bool pep_num(const uint8_t* s, uint32_t n, uint32_t& i, uint64_t& v) {
+  const uint32_t b = i;
+  while (i < n && is_adigit(s[i])) i++;
+  return lv_u64(s, b, i, v);
+}
+
+TVM_HD bool pep_parse(const uint8_t* s, uint32_t n, PepParts& p) {
+  uint32_t i = 0;
+  while (i < n && lv_space(s[i])) i++;
+  while (n > i && lv_space(s[n - 1])) n--;
+  if (i < n && (s[i] == 'v' || s[i] == 'V')) i++;
+  p.epoch = 0;
+  {  // (N!)?
+    uint32_t j = i;
+    while (j < n && is_adigit(s[j])) j++;
+    if (j > i && j < n && s[j] == '!') {
+      if (!lv_u64(s, i, j, p.epoch)) return false;
+      i = j + 1;
+    }
+  }
+  p.rel_b = i;
+  uint32_t segs = 0, last_nz = 0;
+  for (;;) {
+    const uint32_t b = i;
+    uint64_t v;
+    if (!pep_num(s, n, i, v) || i == b) return false;
+    segs++;
+    if (v) last_nz = segs;
+    if (i + 1 < n && s[i] == '.' && is_adigit(s[i + 1])) {
+      i++;
+      continue;
+    }
+    break;
+  }
+  p.rel_e = i;
+  p.rel_key_segs = last_nz;
+  // pre
+  p.pre_l = -1;
+  p.pre_n = 0;
+  {
+    uint32_t j = i;
+    if (j < n && pep_sep(s[j])) j++;
+    static constexpr const char* kPre[] = {"alpha", "a", "beta", "b", "preview", "pre", "c", "rc"};
+    static constexpr int kPreL[] = {0, 0, 1, 1, 2, 2, 2, 2};
+    for (int k = 0; k < 8; k++) {
+      const uint32_t l = pep_kw(s, n, j, kPre[k]);
+      if (!l) continue;
+      p.pre_l = kPreL[k];
+      j += l;
+      if (j < n && pep_sep(s[j]) && !(j + 1 < n && is_adigit(s[j + 1])) && !(j + 1 < n && lv_alpha(s[j + 1]))) {
+        j++;  // trailing optional separator, no number ([-_.]? with N? empty)
+      } else if (j < n && pep_sep(s[j]) && j + 1 < n && is_adigit(s[j + 1])) {
+        j++;
+      }
+      if (!pep_num(s, n, j, p.pre_n)) return false;
+      i = j;
+      break;
+    }
+  }
+  // post: -N | [-_.]?(post|rev|r)[-_.]?N?
+  p.post = false;
+  p.post_n = 0;
+  if (i + 1 < n && s[i] == '-' && is_adigit(s[i + 1])) {
+    i++;
+    if (!pep_num(s, n, i, p.post_n)) return false;
+    p.post = true;
+  } else {
+    uint32_t j = i;
+    if (j < n && pep_sep(s[j])) j++;
+    uint32_t l = pep_kw(s, n, j, "post");
+    if (!l) l = pep_kw(s, n, j, "rev");
+    if (!l) l = pep_kw(s, n, j, "r");
+    if (l) {
+      j += l;
+      if (j < n && pep_sep(s[j]) && !(j + 1 < n && lv_alpha(s[j + 1]))) j++;
+      if (!pep_num(s, n, j, p.post_n)) return false;
+      p.post = true;
+      i = j;
+    }
+  }
+  // dev
+  p.dev = false;
+  p.dev_n = 0;
+  {
+    uint32_t j = i;
+    if (j < n && pep_sep(s[j])) j++;
+    const uint32_t l = pep_kw(s, n, j, "dev");
+    if (l) {
+      j += l;
+      if (j < n && pep_sep(s[j])) j++;
+      if (!pep_num(s, n, j, p.dev_n)) return false;
+      p.dev = true;
+      i = j;
+    }
+  }
+  // local
+  p.loc_b = p.loc_e = i;
+  if (i < n && s[i] == '+') {
+    uint32_t j = i + 1, run = 0;
+    for (; j < n; j++) {
+      if (lv_alnum(s[j])) run++;
+      else if (pep_sep(s[j]) && run) run = 0;
+      else return false;
+    }
+    if (!run) return false;
+    p.loc_b = i + 1;
+    p.loc_e = n;
+    i = n;
+  }
+  return i == n;
+}
+
+enum : uint32_t { PEP_CLS_LOCAL = 1, PEP_CLS_PRE = 2, PEP_CLS_POST = 4 };
+
+TVM_HD uint32_t pep_class(const PepParts& p) {
+  return (p.loc_e > p.loc_b ? PEP_CLS_LOCAL : 0) | ((p.pre_l >= 0 || p.dev) ? PEP_CLS_PRE : 0) |
+         (p.post ? PEP_CLS_POST : 0);
+}
+
+// Emission stops after `upto`: 0 epoch+release+0x01 (the "base" prefix), 1 through DEV
+// (the public version), 2 everything.
+template <class Sink>
+TVM_HD void pep_emit(const uint8_t* s, const PepParts& p, int upto, Sink& o) {
+  put_uvar(p.epoch, o);
+  uint32_t i = p.rel_b;
+  for (uint32_t k = 0; k < p.rel_key_segs; k++) {
+    uint64_t v;
+    pep_num(s, p.rel_e, i, v);
+    put_uvar(v, o);
+    i++;
+  }
+  o.put(0x01);
+  if (upto == 0) return;
+  if (p.pre_l < 0 && !p.post && p.dev) {
+    o.put(0x01);
+  } else if (p.pre_l >= 0) {
+    o.put(0x02);
+    o.put(uint8_t(p.pre_l));
+    put_uvar(p.pre_n, o);
+  } else {
+    o.put(0x03);
+  }
+  if (p.post) {
+    o.put(0x02);
+    put_uvar(p.post_n, o);
+  } else {
+    o.put(0x01);
+  }
+  if (p.dev) {
+    o.put(0x01);
+    put_uvar(p.dev_n, o);
+  } else {
+    o.put(0x02);
+  }
+  if (upto == 1) return;
+  if (p.loc_e > p.loc_b) {
+    o.put(0x02);
+    uint32_t j = p.loc_b;
+    while (j < p.loc_e) {
+      uint32_t e = j;
+      bool num = true;
+      while (e < p.loc_e && !pep_sep(s[e])) num &= is_adigit(s[e++]);
+      if (num) {
+        o.put(0x02);
+        put_digits(s, j, e, o);
+      } else {
+        o.put(0x01);
+        for (uint32_t k = j; k < e; k++) o.put(lv_lower(s[k]));
+        o.put(0x00);
+      }
+      j = e + 1;
+    }
+    o.put(0x00);
+  } else {
+    o.put(0x01);
+  }
+}
+
+template <class Sink>
+TVM_HD bool pep_encode(const uint8_t* s, uint32_t n, Sink& o, uint32_t& cls) {
+  PepParts p;
+  if (!pep_parse(s, n, p)) return false;
+  pep_emit(s, p, 2, o);
+  cls = pep_class(p);
+  return true;
+}
+
+// ============================================================================== MAVEN ====
+// github.com/masahiro331/go-mvn-version (go.mod:73), Maven's ComparableVersion: lower-cased;
+// '.' separates items, '-' and digit<->letter transitions open a sub-list (always the last
+// item of its parent); one-letter a/b/m before a digit read alpha/beta/milestone; ga,
+// final, release -> "" and cr -> rc; each list drops trailing nulls (0, "", empty lists),
+// looking through non-null sub-lists; lists compare item by item padded with null.
+// Key per item (ComparableVersion is a total order for everything but exotic mixes of
+// "0"/"" items with qualifiers at one position):
+//   0x10+q  alpha/beta/milestone/rc/snapshot      0x20  sub-list below null (first item < null)
+//   0x28    0 followed by something below null    0x30  end of list, and the "" qualifier
+//   0x40    sp                                     0x50  other qualifier: bytes, 0x00
+//   0x60    sub-list above null                    0x68  0 followed by something above null
+//   0x70    integer > 0 (digits)
+// Versions must match ^[0-9A-Za-z][0-9A-Za-z._+-]*$ (go-mvn-version rejects other bytes).
+enum : uint8_t { MV_INT = 1, MV_STR = 2, MV_OPEN = 3 };
+struct MvnTok {
+  uint8_t kind;
+  uint8_t q;          // MV_STR: 0..4 pre, 5 "", 6 sp, 7 other
+  uint8_t removed;
+  uint8_t zero;       // MV_INT: value is 0
+  uint32_t b, e;      // source span (MV_INT digits, MV_STR raw letters)
+};
+constexpr int kMvnMaxTok = 48;
+
+TVM_HD int mvn_qual(const uint8_t* s, uint32_t b, uint32_t e, bool followed_by_digit) {
+  auto eq = [&](const char* w) {
+    uint32_t k = 0;
+    for (; w[k]; k++)
+      if (b + k >= e || lv_lower(s[b + k]) != uint8_t(w[k])) return false;
+    return b + k == e;
+  };
+  if (followed_by_digit && e - b == 1) {
+    const uint8_t c = lv_lower(s[b]);
+    if (c == 'a') return 0;
+    if (c == 'b') return 1;
+    if (c == 'm') return 2;
+  }
+  if (eq("alpha")) return 0;
+  if (eq("beta")) return 1;
+  if (eq("milestone")) return 2;
+  if (eq("rc") || eq("cr")) return 3;
+  if (eq("snapshot")) return 4;
+  if (e == b || eq("ga") || eq("final") || eq("release")) return 5;
+  if (eq("sp")) return 6;
+  return 7;
+}
+
+struct MvnParse {
+  MvnTok t[kMvnMaxTok];
+  int n = 0;
+};
+
+TVM_HD bool mvn_push(MvnParse& P, uint8_t kind, uint32_t b, uint32_t e, const uint8_t* s, bool fbd) {
+  if (P.n >= kMvnMaxTok) return false;
+  MvnTok& k = P.t[P.n++];
+  k.kind = kind;
+  k.b = b;
+  k.e = e;
+  k.removed = 0;
+  k.zero = 0;
+  k.q = 0;
+  if (kind == MV_INT) {
+    uint32_t i = b;
+    while (i < e && s[i] == '0') i++;
+    k.zero = i == e;
+  } else if (kind == MV_STR) {
+    k.q = uint8_t(mvn_qual(s, b, e, fbd));
+  }
+  return true;
+}
+
+TVM_HD bool mvn_null(const MvnTok& k) {
+  return (k.kind == MV_INT && k.zero) || (k.kind == MV_STR && k.q == 5);
+}
+
+TVM_HD bool mvn_parse(const uint8_t* s, uint32_t n, MvnParse& P) {
+  uint32_t b0 = 0;
+  while (b0 < n && lv_space(s[b0])) b0++;
+  while (n > b0 && lv_space(s[n - 1])) n--;
+  if (b0 >= n || !lv_alnum(s[b0])) return false;
+  for (uint32_t i = b0; i < n; i++)
+    if (!(lv_alnum(s[i]) || s[i] == '.' || s[i] == '-' || s[i] == '_' || s[i] == '+')) return false;
+  P.n = 0;
+  bool digit = false;
+  uint32_t start = b0;
+  for (uint32_t i = b0; i < n; i++) {
+    const uint8_t c = s[i];
+    if (c == '.' || c == '-') {
+      if (i == start) {
+        if (!mvn_push(P, MV_INT, i, i, s, false)) return false;
+      } else if (!mvn_push(P, digit ? MV_INT : MV_STR, start, i, s, false)) {
+        return false;
+      }
+      start = i + 1;
+      if (c == '-' && !mvn_push(P, MV_OPEN, i, i, s, false)) return false;
+    } else if (is_adigit(c)) {
+      if (!digit && i > start) {
+        if (!mvn_push(P, MV_STR, start, i, s, true) || !mvn_push(P, MV_OPEN, i, i, s, false)) return false;
+        start = i;
+      }
+      digit = true;
+    } else {
+      if (digit && i > start) {
+        if (!mvn_push(P, MV_INT, start, i, s, false) || !mvn_push(P, MV_OPEN, i, i, s, false)) return false;
+        start = i;
+      }
+      digit = false;
+    }
+  }
+  if (n > start && !mvn_push(P, digit ? MV_INT : MV_STR, start, n, s, false)) return false;
+  // normalize, innermost list first: list l is the spine [starts[l], starts[l+1]) whose
+  // last token (the OPEN of list l+1) is its sub-list item
+  int list_end = P.n;
+  // find list starts
+  int starts[kMvnMaxTok + 1];
+  int ns = 0;
+  starts[ns++] = 0;
+  for (int k = 0; k < P.n; k++)
+    if (P.t[k].kind == MV_OPEN) starts[ns++] = k + 1;
+  bool inner_null = true;  // the list after the current one is empty (null)
+  for (int l = ns - 1; l >= 0; l--) {
+    const int b = starts[l];
+    const int e = list_end;  // items of list l: [b, e) minus the OPEN at e-1 if any
+    bool stop = false;
+    for (int k = e - 1; k >= b && !stop; k--) {
+      MvnTok& t = P.t[k];
+      if (t.removed) continue;
+      if (t.kind == MV_OPEN) {
+        if (inner_null) t.removed = 1;  // empty sub-list: null -> removed, keep looking
+        continue;                       // non-null sub-list: look through it
+      }
+      if (mvn_null(t)) t.removed = 1;
+      else stop = true;
+    }
+    inner_null = true;
+    for (int k = b; k < e; k++)
+      if (!P.t[k].removed) inner_null = false;
+    list_end = b;  // the parent's range ends with this list's OPEN token
+  }
+  return true;
+}
+
+// Relation of the item starting at token k (skipping removed ones) to null:
+// -1 below, 0 equal, +1 above.  For a sub-list: its first item's relation.
+TVM_HD int mvn_rel(const MvnParse& P, int k) {
+  for (; k < P.n; k++) {
+    const MvnTok& t = P.t[k];
+    if (t.removed) continue;
+    if (t.kind == MV_OPEN) continue;  // first item of the sub-list decides
+    if (t.kind == MV_INT) return t.zero ? 0 : 1;
+    return t.q < 5 ? -1 : (t.q == 5 ? 0 : 1);
+  }
+  return 0;
+}
+
+template <class Sink>
+TVM_HD void mvn_emit(const uint8_t* s, const MvnParse& P, Sink& o) {
+  int depth = 0;
+  for (int k = 0; k < P.n; k++) {
+    const MvnTok& t = P.t[k];
+    if (t.removed) continue;
+    if (t.kind == MV_OPEN) {
+      o.put(mvn_rel(P, k + 1) < 0 ? 0x20 : 0x60);
+      depth++;
+      continue;
+    }
+    if (t.kind == MV_INT) {
+      if (!t.zero) {
+        o.put(0x70);
+        put_digits(s, t.b, t.e, o);
+      } else {
+        // lookahead: the next item of this list that is not a zero (a sub-list counts)
+        int r = 0;
+        for (int j = k + 1; j < P.n; j++) {
+          const MvnTok& u = P.t[j];
+          if (u.removed) continue;
+          if (u.kind == MV_INT && u.zero) continue;
+          r = u.kind == MV_OPEN ? mvn_rel(P, j + 1) : mvn_rel(P, j);
+          break;
+        }
+        o.put(r < 0 ? 0x28 : 0x68);
+      }
+      continue;
+    }
+    if (t.q < 5) o.put(uint8_t(0x10 + t.q));
+    else if (t.q == 5) o.put(0x30);
+    else if (t.q == 6) o.put(0x40);
+    else {
+      o.put(0x50);
+      for (uint32_t i = t.b; i < t.e; i++) o.put(lv_lower(s[i]));
+      o.put(0x00);
+    }
+  }
+  for (int d = 0; d <= depth; d++) o.put(0x30);
+}
+
+template <class Sink>
+TVM_HD bool mvn_encode(const uint8_t* s, uint32_t n, Sink& o) {
+  MvnParse P;
+  if (!mvn_parse(s, n, P)) return false;
+  mvn_emit(s, P, o);
+  return true;
+}
+
+// =========================================================================== RUBYGEMS ====
+// github.com/aquasecurity/go-gem-version (go.mod:16), Gem::Version:
+//   \s*( N(.[0-9a-zA-Z]+)* (-[0-9A-Za-z-]+(.[0-9A-Za-z-]+)*)? )?\s*     ("" reads "0")
+// '-' reads ".pre."; segments = digit runs (integers) and letter runs (strings); canonical
+// segments drop trailing zeros of the numeric prefix and of the string part; comparison
+// pads with 0, strings sort below integers.
+// Key: string 0x01 bytes 0x00 | zero followed by a string 0x02 | end 0x03 | zero followed
+// by an integer 0x04 | integer > 0: 0x05 digits.
+struct GemSeg {
+  uint8_t str;    // 1 letters, 0 digits
+  uint8_t zero;
+  uint32_t b, e;  // span; b == e for the synthetic "pre" of a '-'
+};
+constexpr int kGemMaxSeg = 48;
+
+TVM_HD bool gem_parse(const uint8_t* s, uint32_t n, GemSeg* seg, int& ns) {
+  uint32_t i = 0;
+  while (i < n && lv_space(s[i])) i++;
+  while (n > i && lv_space(s[n - 1])) n--;
+  ns = 0;
+  if (i == n) {  // "" is "0"
+    seg[0] = GemSeg{0, 1, 0, 0};
+    ns = 1;
+    return true;
+  }
+  // validate: digits, then (.[0-9a-zA-Z]+)*, then optional -[0-9A-Za-z-]+(.[0-9A-Za-z-]+)*
+  uint32_t j = i;
+  while (j < n && is_adigit(s[j])) j++;
+  if (j == i) return false;
+  while (j < n && s[j] == '.') {
+    const uint32_t b = ++j;
+    while (j < n && lv_alnum(s[j])) j++;
+    if (j == b) return false;
+  }
+  if (j < n) {
+    if (s[j] != '-') return false;
+    j++;
+    uint32_t run = 0;
+    for (; j < n; j++) {
+      if (lv_alnum(s[j]) || s[j] == '-') run++;
+      else if (s[j] == '.' && run) run = 0;
+      else return false;
+    }
+    if (!run) return false;
+  }
+  for (uint32_t k = i; k < n;) {
+    if (s[k] == '-') {  // ".pre."
+      if (ns >= kGemMaxSeg) return false;
+      seg[ns++] = GemSeg{1, 0, k, k};
+      k++;
+    } else if (is_adigit(s[k]) || lv_alpha(s[k])) {
+      const bool d = is_adigit(s[k]);
+      const uint32_t b = k;
+      while (k < n && (d ? is_adigit(s[k]) : lv_alpha(s[k]))) k++;
+      if (ns >= kGemMaxSeg) return false;
+      bool zero = false;
+      if (d) {
+        uint32_t z = b;
+        while (z < k && s[z] == '0') z++;
+        zero = z == k;
+      }
+      seg[ns++] = GemSeg{uint8_t(d ? 0 : 1), uint8_t(zero), b, k};
+    } else {
+      k++;
+    }
+  }
+  return true;
+}
+
+// Canonical segments: marks dropped ones with e = b = ~0u.
+TVM_HD void gem_canonical(GemSeg* seg, int ns) {
+  int first_str = ns;
+  for (int k = 0; k < ns; k++)
+    if (seg[k].str) { first_str = k; break; }
+  for (int k = first_str - 1; k >= 0 && !seg[k].str && seg[k].zero; k--) seg[k].b = seg[k].e = ~0u;
+  for (int k = ns - 1; k >= first_str && !seg[k].str && seg[k].zero; k--) seg[k].b = seg[k].e = ~0u;
+}
+
+template <class Sink>
+TVM_HD void gem_emit(const uint8_t* s, const GemSeg* seg, int ns, Sink& o) {
+  for (int k = 0; k < ns; k++) {
+    const GemSeg& g = seg[k];
+    if (g.b == ~0u) continue;
+    if (g.str) {
+      o.put(0x01);
+      if (g.b == g.e) {
+        o.put('p'); o.put('r'); o.put('e');
+      } else {
+        for (uint32_t i = g.b; i < g.e; i++) o.put(s[i]);
+      }
+      o.put(0x00);
+    } else if (!g.zero) {
+      o.put(0x05);
+      put_digits(s, g.b, g.e, o);
+    } else {
+      int nxt = 0;  // 1 integer, -1 string
+      for (int j = k + 1; j < ns; j++) {
+        if (seg[j].b == ~0u || (!seg[j].str && seg[j].zero)) continue;
+        nxt = seg[j].str ? -1 : 1;
+        break;
+      }
+      o.put(nxt < 0 ? 0x02 : 0x04);
+    }
+  }
+  o.put(0x03);
+}
+
+template <class Sink>
+TVM_HD bool gem_encode(const uint8_t* s, uint32_t n, Sink& o) {
+  GemSeg seg[kGemMaxSeg];
+  int ns;
+  if (!gem_parse(s, n, seg, ns)) return false;
+  gem_canonical(seg, ns);
+  gem_emit(s, seg, ns, o);
+  return true;
+}
+
+// ------------------------------------------------------------------ grammar dispatch ----
+template <class Sink>
+TVM_HD bool encode_version_cls(uint8_t cmp, const uint8_t* s, uint32_t n, Sink& o, uint32_t& cls) {
+  cls = 0;
+  switch (cmp) {
+    case CMP_GENERIC: return gen_encode(s, n, false, o);
+    case CMP_BITNAMI: return gen_encode(s, n, true, o);
+    case CMP_NPM: return npm_encode(s, n, o, cls);
+    case CMP_PEP440: return pep_encode(s, n, o, cls);
+    case CMP_MAVEN: return mvn_encode(s, n, o);
+    case CMP_GEM: return gem_encode(s, n, o);
+    default: return encode_version(cmp, s, n, o);
+  }
+}
+
+}  // namespace tvm

@@ -448,14 +448,19 @@ TVM_HD bool rpm_encode(const uint8_t* s, uint32_t n, Sink& o) {
   return true;
 }
 
-// Upper bound on the key length of a version string of n bytes.
+// Upper bound on the key length of a version string of n bytes (every grammar fits in
+// key_bound_any).
 TVM_HD uint32_t key_bound(uint8_t cmp, uint32_t n) {
   switch (cmp) {
     case CMP_APK: return 4 * n + 16;
     case CMP_RPM: return 3 * n + 16;
-    default: return 2 * n + 16;
+    case CMP_DEB: return 2 * n + 16;
+    case CMP_GEM: return 5 * n + 16;
+    default: return 3 * n + 24;  // library grammars (libver.h)
   }
 }
+
+TVM_HD uint32_t key_bound_any(uint32_t n) { return 5 * n + 24; }
 
 // ---------------------------------------------------------------------------- sinks -----
 // Device sink: packs bytes into little-endian 64-bit words and stores whole words.

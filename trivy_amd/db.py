@@ -95,6 +95,12 @@ class Engine:
             raise RuntimeError(e.value.decode())
         self.db = db
 
+    def verify(self):
+        """Raises when a device table no longer equals its host image."""
+        e = errbuf()
+        if lib().tvm_engine_verify(self.h, e, len(e)):
+            raise RuntimeError(e.value.decode())
+
     def table_bytes(self):
         return lib().tvm_engine_table_bytes(self.h)
 
