@@ -121,6 +121,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--check", action="store_true", help="verify the bench batch against the oracle")
+    ap.add_argument("--gather", action="store_true",
+                    help="after the timed region, gather all match lists to rank 0 (RCCL), reported apart")
     ap.add_argument("--variant", type=int, default=None, help="match-kernel variant (tvm_engine_set_variant)")
     ap.add_argument("--sweep", type=int, default=0,
                     help="time every kernel variant over N interleaved rounds (stderr table) before the bench")
@@ -197,31 +199,33 @@ def main():
     lib().tvm_engine_set_variant(eng.h, args.variant if args.variant is not None else 0)
     launch(eng, b, args.warmup)
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
-    def sync():
-        if torch.cuda.is_available():
-            torch.cuda.synchronize()
-
-    barrier()
-    sync()
-    t_start = time.perf_counter()
+    from trivy_amd import dist as td
     ms = ctypes.c_double()
     e = errbuf()
-    if lib().tvm_match_time(eng.h, b, args.steps, ctypes.byref(ms), e, len(e)):
-        raise RuntimeError(e.value.decode())
-    sync()
-    barrier()
-    wall = time.perf_counter() - t_start
-    if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
+
+    def timed_region():
+        if lib().tvm_match_time(eng.h, b, args.steps, ctypes.byref(ms), e, len(e)):
+            raise RuntimeError(e.value.decode())
+
+    sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
+    dev = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
+    wall = td.timed(timed_region, steps=1, warmup=0, sync=sync, device=dev)
     total2, errp2, bits2 = status(eng, b)
     if (total2, errp2, bits2) != (total, -1, 0):
         raise RuntimeError("timed launches disagree with the first pass")
+
+    gather = None
+    if args.gather:  # optional RCCL gather of every rank's match list to rank 0, timed apart
+        pairs = torch.empty((total, 2), dtype=torch.int32, device=dev)
+        got = ctypes.c_uint64()
+        if lib().tvm_match_copy_device(eng.h, b, pairs.data_ptr(), total, ctypes.byref(got)) or got.value != total:
+            raise RuntimeError("tvm_match_copy_device failed")
+        g0 = time.perf_counter()
+        merged = td.gather_pairs(pairs, rank * n_pkgs)
+        sync()
+        g_wall = td.max_over_ranks(time.perf_counter() - g0, dev)
+        gather = {"ms": g_wall * 1e3, "pairs_on_root": None if merged is None else int(merged.shape[0]),
+                  "bytes_per_rank": total * 16}
 
     value = world * n_pkgs * args.steps / wall
     launch_s = ms.value / 1e3 / args.steps
@@ -261,6 +265,8 @@ def main():
                          "kernel_ms": launch_s * 1e3},
             "cpu_baseline": cpu,
         }
+        if gather is not None:
+            line["gather"] = gather
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -193,6 +193,10 @@ int tvm_match_status(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* 
  * advisory) order.  TVM_EINVAL when the device match buffer overflowed (n_matches > the
  * upload's match_cap): re-upload with match_cap >= n_matches. */
 int tvm_match_fetch(tvm_engine* e, tvm_batch* b, uint32_t* pairs, uint64_t cap, uint64_t* n_out);
+/* Copies up to cap raw pairs device-to-device into dst (device memory on the engine's GPU):
+ * package order within a tile, tiles in completion order (sort by (pkg, adv) to canonicalise).
+ * For multi-GPU gathers that keep the match list off the host. */
+int tvm_match_copy_device(tvm_engine* e, tvm_batch* b, void* dst, uint64_t cap, uint64_t* n_out);
 /* Times `steps` back-to-back launches with HIP events on the engine stream (ms total). */
 int tvm_match_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err, size_t errlen);
 /* Algorithmic bytes of one pass (DESIGN.md "roofline"), computed on the host from the batch. */

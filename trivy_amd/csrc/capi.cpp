@@ -401,6 +401,22 @@ int tvm_match_fetch(tvm_engine* e, tvm_batch* b, uint32_t* pairs, uint64_t cap, 
   return TVM_OK;
 }
 
+int tvm_match_copy_device(tvm_engine* e, tvm_batch* b, void* dst, uint64_t cap, uint64_t* n_out) {
+  uint64_t n = 0;
+  int rc = tvm_match_status(e, b, &n, nullptr, nullptr);
+  if (rc) return rc;
+  if (n_out) *n_out = 0;
+  if (n > b->m.cap) return TVM_EINVAL;
+  n = std::min<uint64_t>(n, cap);
+  (void)hipSetDevice(e->device);
+  hipStream_t st = e->eng->stream();
+  if (n && (!dst || hipMemcpyAsync(dst, b->m.pairs, n * sizeof(uint2), hipMemcpyDeviceToDevice, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess))
+    return TVM_EDEVICE;
+  if (n_out) *n_out = n;
+  return TVM_OK;
+}
+
 int tvm_match_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err, size_t errlen) {
   if (!e || !b || !b->uploaded || steps <= 0 || !ms) return TVM_EINVAL;
   (void)hipSetDevice(e->device);
