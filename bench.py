@@ -2,22 +2,25 @@
 """Benchmark: packages matched/sec on BASELINE.json config C2 (dpkg, ~4M packages).
 
 BASELINE.json metric: "packages matched/sec (node) at 1/2/4/8 GPUs; probe HBM GB/s vs peak".
-Workload (config[1]): 10k synthetic Debian/Ubuntu image SBOMs x 400 packages = 4M packages,
-Debian:Ubuntu 60:40 (debian 11/12, ubuntu 20.04/22.04/24.04), against a seeded synthetic
-trivy-db of 5 x 30k package keys (~1.7M advisories, heavy-tailed, 15% unfixed).  The pinned
-trivy-db cannot be fetched offline, hence synthetic data (tools/synth.py).
+Workload (config[1], the default): 10k synthetic Debian/Ubuntu image SBOMs x 400 packages =
+4M packages, Debian:Ubuntu 60:40 (debian 11/12, ubuntu 20.04/22.04/24.04), against a seeded
+synthetic trivy-db of 5 x 30k package keys (~1.7M advisories, heavy-tailed, 15% unfixed).
+The pinned trivy-db cannot be fetched offline, hence synthetic data (tools/synth.py).
+--config c3 / c5 run the language-package (1M npm/pip/maven/go) and RHEL-family/Alpine
+(rpm + apk) mixes of tools/synth_mix.py instead - extra measurements, not the headline.
 
 One step = one pass of the match kernel over the whole device-resident batch: packages
 (descriptors + name/version bytes) in HBM -> (package, advisory) match list in HBM.
-Weak scaling: every rank matches its own 4M-package batch against its own replica of the
-tables; no collective on the data path.  value = all ranks' packages x steps / max wall.
+Weak scaling: every rank matches its own batch against its own replica of the tables; no
+collective on the data path.  value = all ranks' packages x steps / max-over-ranks wall.
+--gather additionally gathers every rank's match list to rank 0 over RCCL after the timed
+region and reports that time apart.
 
 Also reported: roofline (algorithmic bytes per launch / HIP-event launch time, vs the
 8 TB/s HBM peak), the oracle CPU baseline on a bounded sample (rank 0, N=1 only), and
 traffic from the committed rocprofv3 PMC summary when one matches this config.
 """
 import argparse
-import ctypes
 import json
 import os
 import sys
@@ -38,63 +41,103 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def build_engine(sdb, device):
-    import trivy_amd
-    from trivy_amd._lib import lib
-    db = trivy_amd.DB()
-    for n, depth, arena, off, lens in (sdb.records_arena(), sdb.source_arena()):
-        if lib().tvm_db_put_arena(db.h, n, depth, arena, off.ctypes.data, lens.ctypes.data):
-            raise RuntimeError("tvm_db_put_arena failed")
-    db.finalize()
-    return trivy_amd.Engine(db, device)
+# ---- workloads ----------------------------------------------------------------------------
+class C2:
+    """dpkg fleet (tools/synth.py); the oracle C port (oracle/match.c) is the CPU baseline."""
+
+    def __init__(self, args, rank):
+        from tools.synth import make_db, make_batch
+        self.sdb = make_db(PLATS, args.keys_per_plat)
+        self.batch = make_batch(self.sdb, args.targets, args.pkgs_per_target, WEIGHTS, seed=2 + 1000 * rank)
+        self.name = f"c2-dpkg-{args.targets}x{args.pkgs_per_target}"
+        self.n_adv = self.sdb.n_adv
+        self.n_keys = len(self.sdb.key_names)
+        self.plats = PLATS
+
+    def load(self, db):
+        for n, depth, arena, off, lens in (self.sdb.records_arena(), self.sdb.source_arena()):
+            db.put_arena(n, depth, arena, off, lens)
+
+    def fill(self, mb):
+        arena, noff, nlen, voff, vlen = self.batch.arena()
+        for p, b0, b1 in self.batch.targets:
+            mb.add_arena(self.sdb.platforms[p], b1 - b0, arena, noff[b0:], nlen[b0:], voff[b0:], vlen[b0:])
+
+    def check(self, pairs, threads):
+        from oracle import match as om
+        opk, oad = om.match(om.Prepared(self.sdb, self.batch), n_threads=threads)
+        return bool(np.array_equal(pairs[:, 0], opk) and np.array_equal(pairs[:, 1], oad))
+
+    def cpu_baseline(self, budget_s, threads):
+        from oracle import match as om
+        from tools.synth import SynthBatch
+        batch = self.batch
+        n_total = len(batch)
+        n = min(n_total, 200_000)
+        while True:
+            sub = SynthBatch(batch.plat[:n], batch.names[:n], batch.versions[:n], [])
+            prep = om.Prepared(self.sdb, sub)
+            t = time.perf_counter()
+            om.match(prep, n_threads=threads)
+            dt = time.perf_counter() - t
+            if dt >= budget_s * 0.5 or n == n_total:
+                return {"value": n / dt, "unit": "packages/s", "cores": threads, "kind": "port",
+                        "sample": f"first {n} packages of the same batch, oracle/match.c orc_match with "
+                                  f"{threads} threads, {dt:.1f}s"}
+            n = min(n_total, int(n * max(2.0, budget_s / max(dt, 1e-3))))
 
 
-def upload_batch(eng, sdb, batch, cap):
-    from trivy_amd._lib import lib, errbuf
-    L = lib()
-    b = L.tvm_batch_new()
-    arena, noff, nlen, voff, vlen = batch.arena()
-    for p, b0, b1 in batch.targets:
-        L.tvm_batch_add_many(b, eng.h, sdb.platforms[p].encode(), b1 - b0, arena, noff[b0:].ctypes.data,
-                             nlen[b0:].ctypes.data, voff[b0:].ctypes.data, vlen[b0:].ctypes.data)
-    e = errbuf()
-    if L.tvm_batch_upload(eng.h, b, cap, e, len(e)):
-        raise RuntimeError(e.value.decode())
-    return b
+class Mix:
+    """C3 (language packages) / C5 (rpm + apk) mixes of tools/synth_mix.py; the CPU baseline
+    is the Python oracle drivers on a bounded sample (1 core)."""
 
+    def __init__(self, args, rank, which):
+        from tools import synth_mix as sm
+        self.sm = sm
+        plats, self.weights, kpp, n = {
+            "c3": (sm.C3_PLATS, sm.C3_WEIGHTS, 25_000, 1_000_000),
+            "c5": (sm.C5_PLATS, sm.C5_WEIGHTS, 12_000, 20_000_000)}[which]
+        n = args.packages or n
+        self.sdb = sm.make_mix_db(plats, kpp)
+        self.batch = sm.make_mix_batch(self.sdb, n, self.weights, seed=2 + 1000 * rank)
+        self.name = f"{which}-{'lang' if which == 'c3' else 'rpm-apk'}-{n}"
+        self.n_adv = self.sdb.n_adv
+        self.n_keys = len(self.sdb.keys)
+        self.plats = [b for b, _ in plats]
 
-def status(eng, b):
-    from trivy_amd._lib import lib
-    n, errp, bits = ctypes.c_uint64(), ctypes.c_int64(), ctypes.c_uint64()
-    lib().tvm_match_status(eng.h, b, ctypes.byref(n), ctypes.byref(errp), ctypes.byref(bits))
-    return n.value, errp.value, bits.value
+    def load(self, db):
+        self.sdb.put(db)
 
+    def fill(self, mb):
+        self.sm.add_to(mb, self.sdb, self.batch)
 
-def launch(eng, b, k=1):
-    from trivy_amd._lib import lib, errbuf
-    e = errbuf()
-    for _ in range(k):
-        if lib().tvm_match_launch(eng.h, b, e, len(e)):
-            raise RuntimeError(e.value.decode())
-    if lib().tvm_engine_sync(eng.h, e, len(e)):
-        raise RuntimeError(e.value.decode())
+    def check(self, pairs, threads):
+        return None  # tests/test_gpu_mix.py holds the parity check for these mixes
 
-
-def cpu_baseline(sdb, batch, budget_s, threads):
-    """Oracle (C restatement of the reference loops, 'port') on a bounded sample."""
-    from oracle import match as om
-    from tools.synth import SynthBatch
-    n_total = len(batch)
-    n = min(n_total, 200_000)
-    while True:
-        sub = SynthBatch(batch.plat[:n], batch.names[:n], batch.versions[:n], [])
-        prep = om.Prepared(sdb, sub)
-        t = time.perf_counter()
-        om.match(prep, n_threads=threads)
-        dt = time.perf_counter() - t
-        if dt >= budget_s * 0.5 or n == n_total:
-            return n / dt, n, dt
-        n = min(n_total, int(n * max(2.0, budget_s / max(dt, 1e-3))))
+    def cpu_baseline(self, budget_s, threads):
+        import oracle.drivers as od
+        import oracle.library as ol
+        sm = self.sm
+        per, n_done, dt = 200, 0, 0.0
+        while dt < budget_s:
+            for p, g in self.batch.groups:
+                bucket, kind = self.sdb.plats[p]
+                idx = np.arange(min(per, len(g["key"])))
+                pkgs = sm.driver_packages(self.sdb, p, g, idx)
+                roots = sm.C3_ROOTS.get(kind, [bucket])
+                recs = od.Records(self.sdb.records_for({r: {x["Name"] for x in pkgs} for r in roots}))
+                t = time.perf_counter()
+                if kind in sm.LANG_OF:
+                    ol.detect(recs, sm.LANG_OF[kind], pkgs)
+                else:
+                    fam, fmt = sm.DRIVER_OF[kind]
+                    od.driver_detect(fam, fmt.format(bucket.split(" ")[-1]), None, pkgs, recs, None)
+                dt += time.perf_counter() - t
+                n_done += len(idx)
+            per *= 2
+        return {"value": n_done / dt, "unit": "packages/s", "cores": 1, "kind": "port",
+                "sample": f"{n_done} packages (first rows of every platform group), oracle/drivers.py + "
+                          f"oracle/library.py per-driver Detect, 1 thread, {dt:.1f}s (Python)"}
 
 
 def pmc_traffic(cfg_name):
@@ -114,13 +157,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", choices=["c2", "c3", "c5"], default="c2")
     ap.add_argument("--keys-per-plat", type=int, default=30000)
     ap.add_argument("--targets", type=int, default=10000)
     ap.add_argument("--pkgs-per-target", type=int, default=400)
+    ap.add_argument("--packages", type=int, default=0, help="c3/c5: packages per GPU (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--check", action="store_true", help="verify the bench batch against the oracle")
+    ap.add_argument("--check", action="store_true", help="verify the bench batch against the oracle (c2)")
     ap.add_argument("--gather", action="store_true",
                     help="after the timed region, gather all match lists to rank 0 (RCCL), reported apart")
     ap.add_argument("--variant", type=int, default=None, help="match-kernel variant (tvm_engine_set_variant)")
@@ -139,44 +184,33 @@ def main():
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
 
-    from tools.synth import make_db, make_batch
+    import trivy_amd
+    from trivy_amd import dist as td
+    from trivy_amd._lib import lib
+    from trivy_amd.batch import MatchBatch
     t0 = time.perf_counter()
-    sdb = make_db(PLATS, args.keys_per_plat)
-    eng = build_engine(sdb, local)
-    log(rank, f"[bench] db: {len(sdb.key_names)} keys, {sdb.n_adv} advisories, tables {eng.table_bytes()/1e6:.1f} MB "
-              f"({time.perf_counter()-t0:.1f}s)")
+    wl = C2(args, rank) if args.config == "c2" else Mix(args, rank, args.config)
+    db = trivy_amd.DB()
+    wl.load(db)
+    eng = trivy_amd.Engine(db.finalize(), local)
+    log(rank, f"[bench] {wl.name}: db {wl.n_keys} keys, {wl.n_adv} advisories, tables "
+              f"{eng.table_bytes()/1e6:.1f} MB ({time.perf_counter()-t0:.1f}s)")
     t0 = time.perf_counter()
-    batch = make_batch(sdb, args.targets, args.pkgs_per_target, WEIGHTS, seed=2 + 1000 * rank)
-    n_pkgs = len(batch)
-    b = upload_batch(eng, sdb, batch, cap=8 * n_pkgs)
-    launch(eng, b)
-    total, errp, bits = status(eng, b)
-    if total > 8 * n_pkgs:  # size the match buffer exactly, once
-        from trivy_amd._lib import lib
-        lib().tvm_batch_free(b)
-        b = upload_batch(eng, sdb, batch, cap=total)
-        launch(eng, b)
-        total, errp, bits = status(eng, b)
+    mb = MatchBatch(eng)
+    wl.fill(mb)
+    n_pkgs = len(mb)
+    total, errp, bits = mb.run()
     if bits or errp != -1:
         raise RuntimeError(f"engine error bits={bits} poisoned_pkg={errp}")
     log(rank, f"[bench] batch: {n_pkgs} packages, {total} matches ({time.perf_counter()-t0:.1f}s)")
 
     if args.check and rank == 0:
-        from oracle import match as om
-        from trivy_amd._lib import lib
-        out = np.zeros(2 * total, dtype=np.uint32)
-        got = ctypes.c_uint64()
-        if lib().tvm_match_fetch(eng.h, b, out.ctypes.data, total, ctypes.byref(got)):
-            raise RuntimeError("tvm_match_fetch failed")
-        opk, oad = om.match(om.Prepared(sdb, batch), n_threads=args.cpu_threads)
-        pr = out.reshape(-1, 2)
-        ok = np.array_equal(pr[:, 0], opk) and np.array_equal(pr[:, 1], oad)
-        log(rank, f"[bench] check vs oracle: {'OK' if ok else 'MISMATCH'}")
-        if not ok:
+        ok = wl.check(mb.pairs(), args.cpu_threads)
+        log(rank, f"[bench] check vs oracle: {'OK' if ok else 'MISMATCH' if ok is False else 'n/a'}")
+        if ok is False:
             raise SystemExit(1)
 
     # ---- warmup + timed region -------------------------------------------------------------
-    from trivy_amd._lib import lib, errbuf
     if args.sweep and rank == 0:
         names, v = [], 0
         while lib().tvm_variant_name(v):
@@ -186,39 +220,29 @@ def main():
         for _ in range(args.sweep):
             for v, n in enumerate(names):
                 lib().tvm_engine_set_variant(eng.h, v)
-                launch(eng, b, 2)
-                ms = ctypes.c_double()
-                e = errbuf()
-                lib().tvm_match_time(eng.h, b, 10, ctypes.byref(ms), e, len(e))
-                times[n].append(ms.value / 10)
-                if not n.startswith("ablate") and status(eng, b) != (total, -1, 0):
+                mb.launch(2)
+                times[n].append(mb.time(10))
+                if not n.startswith("ablate") and mb.status() != (total, -1, 0):
                     raise RuntimeError(f"variant {n} disagrees on the match count")
         for n in names:
             t = sorted(times[n])
             log(rank, f"[sweep] {n:>16}: median {t[len(t)//2]:.4f} ms  min {t[0]:.4f} ms per pass")
     lib().tvm_engine_set_variant(eng.h, args.variant if args.variant is not None else 0)
-    launch(eng, b, args.warmup)
-
-    from trivy_amd import dist as td
-    ms = ctypes.c_double()
-    e = errbuf()
-
-    def timed_region():
-        if lib().tvm_match_time(eng.h, b, args.steps, ctypes.byref(ms), e, len(e)):
-            raise RuntimeError(e.value.decode())
+    mb.launch(args.warmup)
 
     sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
     dev = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
-    wall = td.timed(timed_region, steps=1, warmup=0, sync=sync, device=dev)
-    total2, errp2, bits2 = status(eng, b)
-    if (total2, errp2, bits2) != (total, -1, 0):
+    launch_ms = []
+    wall = td.timed(lambda: launch_ms.append(mb.time(args.steps)), steps=1, warmup=0, sync=sync, device=dev)
+    if mb.status() != (total, -1, 0):
         raise RuntimeError("timed launches disagree with the first pass")
 
     gather = None
     if args.gather:  # optional RCCL gather of every rank's match list to rank 0, timed apart
+        import ctypes
         pairs = torch.empty((total, 2), dtype=torch.int32, device=dev)
         got = ctypes.c_uint64()
-        if lib().tvm_match_copy_device(eng.h, b, pairs.data_ptr(), total, ctypes.byref(got)) or got.value != total:
+        if lib().tvm_match_copy_device(eng.h, mb.h, pairs.data_ptr(), total, ctypes.byref(got)) or got.value != total:
             raise RuntimeError("tvm_match_copy_device failed")
         g0 = time.perf_counter()
         merged = td.gather_pairs(pairs, rank * n_pkgs)
@@ -228,19 +252,15 @@ def main():
                   "bytes_per_rank": total * 16}
 
     value = world * n_pkgs * args.steps / wall
-    launch_s = ms.value / 1e3 / args.steps
-    alg_bytes = lib().tvm_match_algorithmic_bytes(eng.h, b)
+    launch_s = launch_ms[0] / 1e3
+    alg_bytes = mb.algorithmic_bytes()
     achieved = alg_bytes / launch_s / 1e9
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        rate, n_sample, dt = cpu_baseline(sdb, batch, args.cpu_seconds, args.cpu_threads)
-        cpu = {"value": rate, "unit": "packages/s", "cores": args.cpu_threads, "kind": "port",
-               "sample": f"first {n_sample} packages of the same batch, oracle/match.c orc_match with "
-                         f"{args.cpu_threads} threads, {dt:.1f}s"}
+        cpu = wl.cpu_baseline(args.cpu_seconds, args.cpu_threads)
 
-    cfg_name = f"c2-dpkg-{args.targets}x{args.pkgs_per_target}"
-    traffic = pmc_traffic(cfg_name)
+    traffic = pmc_traffic(wl.name)
     if rank == 0:
         line = {
             "metric": "packages matched/sec (node)",
@@ -254,11 +274,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (seeded trivy-db + SBOM batch, tools/synth.py)",
-            "config": {"workload": cfg_name, "packages_per_gpu": n_pkgs, "matches_per_gpu": total,
+            "data": "synthetic (seeded trivy-db + SBOM batch, tools/synth.py / tools/synth_mix.py)",
+            "config": {"workload": wl.name, "packages_per_gpu": n_pkgs, "matches_per_gpu": total,
                        "kernel_variant": lib().tvm_variant_name(lib().tvm_engine_set_variant(eng.h, -1)).decode(),
-                       "db_keys": len(sdb.key_names), "db_advisories": sdb.n_adv,
-                       "platforms": PLATS, "parallelism": f"replicated tables, batch sharded x{world}"},
+                       "db_keys": wl.n_keys, "db_advisories": wl.n_adv,
+                       "platforms": wl.plats, "parallelism": f"replicated tables, batch sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "algorithmic_bytes_per_launch": alg_bytes,

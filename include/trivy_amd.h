@@ -177,6 +177,15 @@ void tvm_batch_free(tvm_batch* b);
 /* Adds one package under an explicit root bucket (e.g. "debian 12"), lookup name and the
  * formatted version the driver compares.  Returns the package's batch index. */
 int64_t tvm_batch_add(tvm_batch* b, tvm_engine* e, const char* bucket, tvm_str name, tvm_str version);
+/* tvm_batch_add_many plus the per-package attributes the rpm drivers filter on (the batch
+ * form of what tvm_ospkg_detect derives from tvm_package): TVM_ATTR_ARCH takes one arch
+ * string per package (rocky.go arch entries, redhat.go arch filter), TVM_ATTR_KSPLICE tags
+ * each package with the ksplice token of its release (oracle.go:46-53, 77). */
+enum { TVM_ATTR_ARCH = 1, TVM_ATTR_KSPLICE = 2 };
+int64_t tvm_batch_add_many_ex(tvm_batch* b, tvm_engine* e, const char* bucket, size_t n, const char* arena,
+                              const uint64_t* name_off, const uint32_t* name_len, const uint64_t* ver_off,
+                              const uint32_t* ver_len, const uint64_t* arch_off, const uint32_t* arch_len,
+                              uint32_t flags);
 /* n packages of one bucket from a byte arena; returns the batch index of the first. */
 int64_t tvm_batch_add_many(tvm_batch* b, tvm_engine* e, const char* bucket, size_t n, const char* arena,
                            const uint64_t* name_off, const uint32_t* name_len, const uint64_t* ver_off,

@@ -1,0 +1,64 @@
+"""GPU: the rpm/apk (BASELINE.json C5) and language-package (C3) workloads through the batch
+API - 400k packages per run over a generated DB of each config's platform mix - checked
+per platform on a random sample against (1) the per-driver C-ABI entry points
+(tvm_ospkg_driver_detect / tvm_library_detect, one launch per sample) and (2) the oracle's
+drivers (oracle/drivers.py, oracle/library.py).  (2) pins the semantics, (1) vs the batch
+pairs checks that a package's result does not depend on the rest of the batch."""
+import collections
+
+import numpy as np
+import pytest
+
+from conftest import canon
+from tools import synth_mix as sm
+
+pytestmark = pytest.mark.gpu
+
+CFGS = {"c5": (sm.C5_PLATS, sm.C5_WEIGHTS, 3000), "c3": (sm.C3_PLATS, sm.C3_WEIGHTS, 5000)}
+
+
+@pytest.mark.parametrize("cfg", list(CFGS))
+def test_mix_batch_parity(cfg):
+    import oracle.drivers as od
+    import oracle.library as ol
+    import trivy_amd
+    from trivy_amd.batch import MatchBatch, advisory_vuln_id
+    from trivy_amd.detector import library, ospkg
+    plats, weights, kpp = CFGS[cfg]
+    sdb = sm.make_mix_db(plats, kpp, seed=0x5EED + len(cfg))
+    db = sdb.put(trivy_amd.DB()).finalize()
+    eng = trivy_amd.Engine(db, 0)
+    batch = sm.make_mix_batch(sdb, 400_000, weights, seed=17)
+    mb = MatchBatch(eng)
+    firsts = sm.add_to(mb, sdb, batch)
+    total, errp, bits = mb.run()
+    assert errp == -1 and bits == 0 and total > 200_000
+    pairs = mb.pairs().astype(np.int64)
+    assert np.all(np.diff(pairs[:, 0] * (1 << 32) + pairs[:, 1]) > 0)  # (package, advisory) order
+    rng = np.random.default_rng(5)
+    checked = 0
+    for (p, g), (_, first) in zip(batch.groups, firsts):
+        bucket, kind = sdb.plats[p]
+        idx = np.sort(rng.choice(len(g["key"]), 250, replace=False))
+        pkgs = sm.driver_packages(sdb, p, g, idx)
+        roots = sm.C3_ROOTS.get(kind, [bucket])
+        recs = sdb.records_for({r: {x["Name"] for x in pkgs} for r in roots})
+        if kind in sm.LANG_OF:
+            want = ol.detect(od.Records(recs), sm.LANG_OF[kind], pkgs)
+            got = library.detect(eng, sm.LANG_OF[kind], pkgs)
+        else:
+            fam, fmt = sm.DRIVER_OF[kind]
+            os_ver = fmt.format(bucket.split(" ")[-1])
+            want = od.driver_detect(fam, os_ver, None, pkgs, od.Records(recs), None)
+            got = ospkg.Scanner(eng, fam).detect(os_ver, None, pkgs)
+        assert canon(got) == canon(want), bucket
+        # the batch pairs of the sampled packages name the same (package, vulnerability) multiset
+        rows = {int(first + i): int(i) for i in idx}
+        lo, hi = np.searchsorted(pairs[:, 0], [first, first + len(g["key"])])
+        seg = pairs[lo:hi]
+        seg = seg[np.isin(seg[:, 0], list(rows))]
+        from_batch = collections.Counter((rows[int(a)], advisory_vuln_id(db, int(b))) for a, b in seg)
+        from_oracle = collections.Counter((int(v["PkgID"][1:]), v["VulnerabilityID"]) for v in want)
+        assert from_batch == from_oracle, bucket
+        checked += len(want)
+    assert checked > 1000

@@ -1,0 +1,267 @@
+"""Seeded synthetic DBs + batches for the rpm/apk (BASELINE.json C5) and language-package
+(C3) workloads.
+
+Like tools/synth.py (the dpkg C2 workload), the pinned trivy-db cannot be fetched offline,
+so the advisory tables are generated with the value formats the drivers read (plain
+FixedVersion for alma/oracle/alpine, arch Entries for rocky, Vulnerable/Patched constraint
+lists for GHSA-style language buckets) and heavy-tailed advisories per package.  Every
+generated package keeps its structured fields, so the same package can be handed to the
+batch API (bucket + formatted version + attributes) and, for a sample, to the per-driver
+APIs and to the oracle (tests/test_gpu_mix.py).
+"""
+import json
+
+import numpy as np
+
+from tools.synth import _SYL, _counts
+
+# (batch bucket, kind, DB roots) - OS buckets are their own root; language buckets scan
+# every root with the "eco::" prefix (pkg/detector/library/driver.go:124-131)
+C5_PLATS = [("Oracle Linux 8", "oracle"), ("Oracle Linux 9", "oracle"), ("alma 8", "alma"), ("alma 9", "alma"),
+            ("alpine 3.19", "alpine"), ("alpine 3.20", "alpine"), ("rocky 8", "rocky"), ("rocky 9", "rocky")]
+C5_WEIGHTS = [8, 8, 18, 18, 12, 12, 12, 12]
+C3_PLATS = [("go::", "go"), ("maven::", "maven"), ("npm::", "npm"), ("pip::", "pip")]
+C3_WEIGHTS = [15, 20, 40, 25]
+C3_ROOTS = {"go": ["go::GitHub Security Advisory Go", "go::The Go Vulnerability Database"],
+            "maven": ["maven::GitHub Security Advisory Maven"], "npm": ["npm::GitHub Security Advisory npm"],
+            "pip": ["pip::GitHub Security Advisory pip"]}
+DRIVER_OF = {"alma": ("alma", "{}"), "rocky": ("rocky", "{}"), "oracle": ("oracle", "{}"),
+             "alpine": ("alpine", "{}.1")}
+LANG_OF = {"go": "gomod", "maven": "jar", "npm": "npm", "pip": "pip"}
+ARCHES = [b"x86_64", b"aarch64", b"noarch", b"i686"]
+
+
+def _os_ver(bucket):
+    return bucket.split(" ")[-1]
+
+
+class MixDB:
+    """records: list of (path tuple of str, value str) in bbolt byte order per root."""
+
+    def __init__(self, plats, keys, key_plat, key_base, records, sources):
+        self.plats = plats          # [(bucket, kind)]
+        self.keys = keys            # [bytes] package names, contiguous per platform
+        self.key_plat = key_plat    # np.int32
+        self.key_base = key_base    # np.int64 [n_keys, 3]: major, minor, flag (epoch / ksplice / scope)
+        self.records = records
+        self.sources = sources
+        self.plat_keys = [np.nonzero(key_plat == p)[0] for p in range(len(plats))]
+        self.n_adv = len(records)
+
+    def put(self, db):
+        """Loads the records into a trivy_amd.DB through tvm_db_put_arena."""
+        from trivy_amd.batch import arena_of
+        for depth, recs in ((3, self.records), (2, self.sources)):
+            cols = list(zip(*[tuple(p.encode() for p in path) + (v.encode(),) for path, v in recs]))
+            arena, c = arena_of(*cols)
+            # tvm_db_put_arena wants the items of one record adjacent: interleave the columns
+            off = np.stack([o for o, _ in c], axis=1).reshape(-1)
+            lens = np.stack([n for _, n in c], axis=1).reshape(-1)
+            db.put_arena(len(recs), depth, arena, np.ascontiguousarray(off), np.ascontiguousarray(lens))
+        return db
+
+    def records_for(self, names_by_root):
+        """Fixture-format records of the given (root -> names) buckets + data sources."""
+        out = [{"path": list(p), "value": v} for p, v in self.sources]
+        for path, v in self.records:
+            if path[1] in names_by_root.get(path[0], ()):
+                out.append({"path": list(path), "value": v})
+        return out
+
+
+def _names(rng, kind, n):
+    syl = rng.integers(0, len(_SYL), size=(n, 3))
+    out = []
+    for i, (a, b, c) in enumerate(syl):
+        s = (_SYL[a] + _SYL[b]).decode()
+        if kind == "npm":
+            out.append(f"@{_SYL[c].decode()}/{s}{i}" if i % 5 == 0 else f"{s}-{i}")
+        elif kind == "pip":
+            out.append(f"{s}-{_SYL[c].decode()}{i}")
+        elif kind == "maven":
+            out.append(f"org.{_SYL[c].decode()}:{s}{i}")
+        elif kind == "go":
+            out.append(f"github.com/{_SYL[c].decode()}/{s}{i}")
+        else:
+            out.append(f"{s}{_SYL[c].decode()}{i}")
+    return sorted(set(out), key=str.encode)
+
+
+def _rpm(ep, ma, mi, p, r, el, ksplice):
+    v = f"{ma}.{mi}.{p}-{r}.el{el}" if not ksplice else f"{ma}.{mi}.{p}-{r}.0.1.ksplice{ksplice}.el{el}"
+    return f"{ep}:{v}" if ep else v
+
+
+def _lib_adv(rng, kind, ma, mi, f):
+    lo = f"{ma}.{mi}.0" if rng.random() < 0.6 else f"{ma}.0.0"
+    hi = f"{ma}.{mi}.{f}"
+    sep = " " if kind == "npm" else ", "
+    x = rng.random()
+    if x < 0.55:
+        vul = [f">={lo}{sep}<{hi}"]
+    elif x < 0.85:
+        vul = [f"<{hi}"]
+    else:
+        vul = [f">={lo}{sep}<{hi}", f">={ma + 1}.0.0{sep}<{ma + 1}.{mi}.{f}"]
+    adv = {"VulnerableVersions": vul}
+    if rng.random() < 0.6:
+        adv["PatchedVersions"] = [f">={hi}" if kind != "pip" or rng.random() < 0.5 else hi]
+    if rng.random() < 0.1:
+        adv = {"PatchedVersions": [f">={hi}"]}
+    return adv
+
+
+def make_mix_db(plats, keys_per_plat, seed=0x5EED, mean_adv=6, max_adv=400):
+    rng = np.random.default_rng(seed)
+    keys, key_plat, key_base, records, sources = [], [], [], [], []
+    for p, (bucket, kind) in enumerate(plats):
+        names = _names(rng, kind, keys_per_plat)
+        cnt = _counts(rng, len(names), mean_adv, max_adv)
+        roots = C3_ROOTS.get(kind, [bucket])
+        for r in roots:
+            sources.append((("data-source", r), json.dumps({"ID": kind, "Name": f"{r} source", "URL": f"https://{kind}"})))
+        el = _os_ver(bucket).split(".")[0]
+        by_root = {r: [] for r in roots}
+        for i, name in enumerate(names):
+            ma, mi = int(rng.integers(0, 12)), int(rng.integers(0, 20))
+            flag = int(rng.random() < 0.05) * int(rng.integers(1, 3))  # rpm epoch / oracle ksplice
+            keys.append(name.encode())
+            key_plat.append(p)
+            key_base.append((ma, mi, flag))
+            for j in range(int(cnt[i])):
+                vid = f"CVE-{2010 + (j * 31 + i) % 15}-{10000 + j}"
+                f = int(rng.integers(0, 40))
+                r = int(rng.integers(1, 9))
+                if kind == "alpine":
+                    val = {"FixedVersion": f"{ma}.{mi}.{f}-r{r}" if rng.random() > 0.01 else "0"}
+                elif kind == "alma":
+                    val = {"FixedVersion": _rpm(flag, ma, mi, f, r, el, 0)}
+                elif kind == "oracle":
+                    ks = flag if rng.random() < 0.5 else 0
+                    val = {"FixedVersion": _rpm(0, ma, mi, f, r, el, ks)}
+                elif kind == "rocky":
+                    ents = [{"FixedVersion": _rpm(flag, ma, mi, f, r, el, 0), "Arches": ["aarch64", "x86_64"]}]
+                    if rng.random() < 0.3:
+                        ents.append({"FixedVersion": _rpm(flag, ma, mi, f + 1, r, el, 0), "Arches": ["noarch"]})
+                    val = {"Entries": ents}
+                else:
+                    val = _lib_adv(rng, kind, ma, mi, f)
+                root = roots[0] if len(roots) == 1 or rng.random() < 0.7 else roots[1]
+                by_root[root].append(((root, name, vid), json.dumps(val)))
+                if len(roots) > 1 and rng.random() < 0.1:  # the same ID in the other source too
+                    other = roots[1] if root == roots[0] else roots[0]
+                    by_root[other].append(((other, name, vid), json.dumps(_lib_adv(rng, kind, ma, mi, f))))
+        for r in roots:
+            seen = {}
+            for path, v in by_root[r]:
+                seen[path] = v
+            records += sorted(seen.items(), key=lambda kv: tuple(x.encode() for x in kv[0]))
+    sources.sort(key=lambda kv: kv[0][1].encode())
+    return MixDB(plats, keys, np.array(key_plat, dtype=np.int32), np.array(key_base, dtype=np.int64),
+                 records, sources)
+
+
+def _cat(*parts):
+    out = parts[0]
+    for p in parts[1:]:
+        out = np.char.add(out, p)
+    return out
+
+
+def _s(a):
+    return np.asarray(a).astype("S")
+
+
+class MixBatch:
+    """Per platform: key index, structured version fields, and the batch-API columns."""
+
+    def __init__(self, groups):
+        self.groups = groups  # [(plat, dict of columns)]
+
+    def __len__(self):
+        return sum(len(g["key"]) for _, g in self.groups)
+
+
+def make_mix_batch(db, n, weights, seed, miss=0.25, zipf=2.5):
+    rng = np.random.default_rng(seed)
+    w = np.asarray(weights, dtype=np.float64)
+    counts = rng.multinomial(n, w / w.sum())
+    groups = []
+    for p, (bucket, kind) in enumerate(db.plats):
+        m = int(counts[p])
+        ks = db.plat_keys[p]
+        if m == 0 or len(ks) == 0:
+            continue
+        K = len(ks)
+        rank = np.minimum((K * rng.random(m) ** zipf).astype(np.int64), K - 1)
+        key = ks[(rank * 7919 + p * 1000003) % K]
+        base = db.key_base[key]
+        ma, mi, flag = base[:, 0], base[:, 1], base[:, 2]
+        patch = rng.integers(0, 40, m)
+        rel = rng.integers(1, 9, m)
+        names = np.array(db.keys, dtype=object)[key].astype("S")
+        missing = rng.random(m) < miss
+        names = np.where(missing, _cat(b"absent-", _s(np.arange(m))), names)
+        mmp = _cat(_s(ma), b".", _s(mi), b".", _s(patch))
+        g = {"key": np.where(missing, -1, key), "name": names}
+        el = _os_ver(bucket).split(".")[0].encode()
+        if kind == "alpine":
+            g["ver"] = _cat(mmp, b"-r", _s(rel))
+            g["rel"] = np.full(m, b"", dtype="S1")
+            g["epoch"] = np.zeros(m, dtype=np.int64)
+            g["version"] = g["ver"]
+        else:
+            if kind == "oracle":
+                ks = np.where((flag > 0) & (rng.random(m) < 0.5), flag, 0)
+                relv = np.where(ks > 0, _cat(_s(rel), b".0.1.ksplice", _s(ks), b".el", el), _cat(_s(rel), b".el", el))
+                epoch = np.zeros(m, dtype=np.int64)
+            else:
+                relv = _cat(_s(rel), b".el", el)
+                epoch = np.where(rng.random(m) < 0.9, flag, 0)
+            g["version"], g["rel"], g["epoch"] = mmp, relv, epoch
+            full = _cat(mmp, b"-", relv)
+            g["ver"] = np.where(epoch > 0, _cat(_s(epoch), b":", full), full)
+            if kind == "rocky":
+                g["arch"] = np.array(ARCHES, dtype="S")[rng.choice(4, m, p=[0.6, 0.25, 0.1, 0.05])]
+        if kind in LANG_OF:
+            v = mmp
+            pre = rng.random(m)
+            if kind == "npm":
+                v = np.where(pre < 0.03, _cat(v, b"-beta.", _s(rel)), v)
+            elif kind == "pip":
+                v = np.where(pre < 0.03, _cat(v, b"rc", _s(rel)), np.where(pre < 0.05, _cat(v, b".post1"), v))
+            elif kind == "maven":
+                v = np.where(pre < 0.03, _cat(v, b"-rc", _s(rel)), v)
+            elif kind == "go":
+                v = np.where(pre < 0.5, _cat(b"v", v), v)
+            g["ver"] = g["version"] = v
+        groups.append((p, g))
+    return MixBatch(groups)
+
+
+def add_to(mb, db, batch):
+    """Adds every group to a trivy_amd.batch.MatchBatch; returns [(plat, first index)]."""
+    out = []
+    for p, g in batch.groups:
+        bucket, kind = db.plats[p]
+        first = mb.add_many(bucket, g["name"], g["ver"], arches=g.get("arch"), ksplice=(kind == "oracle"))
+        out.append((p, first))
+    return out
+
+
+def driver_packages(db, p, g, idx):
+    """The packages at rows idx of group g as the drivers' package dicts (ftypes.Package)."""
+    bucket, kind = db.plats[p]
+    pk = []
+    for i in idx:
+        name = g["name"][i].decode()
+        if kind in LANG_OF:
+            pk.append({"Name": name, "Version": g["ver"][i].decode(), "ID": f"p{i}"})
+            continue
+        d = {"ID": f"p{i}", "Name": name, "Version": g["version"][i].decode(), "Release": g["rel"][i].decode(),
+             "Epoch": int(g["epoch"][i]), "SrcName": name, "SrcVersion": g["version"][i].decode(),
+             "SrcRelease": g["rel"][i].decode(), "SrcEpoch": int(g["epoch"][i])}
+        if "arch" in g:
+            d["Arch"] = g["arch"][i].decode()
+        pk.append(d)
+    return pk

@@ -89,6 +89,9 @@ _SIG = [
     ("tvm_batch_add", ctypes.c_int64, [_P, _P, ctypes.c_char_p, Str, Str]),
     ("tvm_batch_add_many", ctypes.c_int64, [_P, _P, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    ("tvm_batch_add_many_ex", ctypes.c_int64, [_P, _P, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_uint32]),
     ("tvm_batch_size", ctypes.c_int64, [_P]),
     ("tvm_batch_upload", ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_match_launch", ctypes.c_int, [_P, _P, ctypes.c_char_p, ctypes.c_size_t]),

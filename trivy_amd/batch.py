@@ -1,0 +1,152 @@
+"""Batch matching: many targets' packages in one device pass (wrappers of tvm_batch_* /
+tvm_match_*).
+
+The reference matches package by package inside each driver's Detect loop
+(pkg/detector/ospkg/*/*.go, pkg/detector/library/detect.go:29-60); a scan server sees
+thousands of targets at once, so this layer coalesces them: every package is added with
+its platform bucket (the string a driver would pass to Get: "debian 12", "alma 9",
+"npm::", ...), an already-formatted version and, for the rpm drivers that filter on them,
+its arch / ksplice attributes; one launch returns every (package, advisory) pair.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import lib, errbuf
+
+ATTR_ARCH, ATTR_KSPLICE = 1, 2
+
+
+def _packed(col):
+    """(bytes, lens u32) of a byte-string column (list or numpy 'S' array, no NUL bytes)."""
+    a = col if isinstance(col, np.ndarray) and col.dtype.kind == "S" else np.array(list(col), dtype="S")
+    n, w = len(a), a.dtype.itemsize
+    if n == 0 or w == 0:
+        return b"", np.zeros(n, dtype=np.uint32)
+    lens = np.char.str_len(a).astype(np.uint32)
+    mat = np.ascontiguousarray(a).view(np.uint8).reshape(n, w)
+    return mat[np.arange(w, dtype=np.uint32)[None, :] < lens[:, None]].tobytes(), lens
+
+
+def arena_of(*columns):
+    """Packs byte-string columns into one arena, column after column:
+    (arena, [(off u64, len u32) per column])."""
+    parts, cols, base = [], [], 0
+    for c in columns:
+        data, lens = _packed(c)
+        off = np.zeros(len(lens), dtype=np.uint64)
+        if len(lens):
+            off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        cols.append((off + np.uint64(base), lens))
+        parts.append(data)
+        base += len(data)
+    return b"".join(parts), cols
+
+
+class MatchBatch:
+    """One device batch on `engine`; fail-loud (RuntimeError) on every C-ABI error."""
+
+    def __init__(self, engine):
+        self.engine = engine
+        self.h = lib().tvm_batch_new()
+        self.total = None
+
+    def add_many(self, bucket, names, versions, arches=None, ksplice=False):
+        """Adds len(names) packages of one platform bucket; returns the first index."""
+        if not len(names):
+            return len(self)
+        cols = [names, versions] + ([arches] if arches is not None else [])
+        arena, c = arena_of(*cols)
+        flags = (ATTR_ARCH if arches is not None else 0) | (ATTR_KSPLICE if ksplice else 0)
+        ao, al = c[2] if arches is not None else (None, None)
+        first = lib().tvm_batch_add_many_ex(
+            self.h, self.engine.h, bucket.encode(), len(names), arena, c[0][0].ctypes.data, c[0][1].ctypes.data,
+            c[1][0].ctypes.data, c[1][1].ctypes.data, ao.ctypes.data if ao is not None else None,
+            al.ctypes.data if al is not None else None, flags)
+        if first < 0:
+            raise RuntimeError("tvm_batch_add_many_ex rejected the packages")
+        return first
+
+    def add_arena(self, bucket, n, arena, name_off, name_len, ver_off, ver_len):
+        """Adds n packages whose name/version bytes already sit in one arena (u64 offsets,
+        u32 lengths as numpy arrays); returns the first index."""
+        first = lib().tvm_batch_add_many(self.h, self.engine.h, bucket.encode(), n, arena, name_off.ctypes.data,
+                                         name_len.ctypes.data, ver_off.ctypes.data, ver_len.ctypes.data)
+        if first < 0:
+            raise RuntimeError("tvm_batch_add_many rejected the packages")
+        return first
+
+    def __len__(self):
+        return lib().tvm_batch_size(self.h)
+
+    def _check(self, rc, e, what):
+        if rc:
+            raise RuntimeError(f"{what}: {e.value.decode()}")
+
+    def upload(self, match_cap=None):
+        e = errbuf()
+        cap = match_cap if match_cap is not None else max(1024, 8 * len(self))
+        self._check(lib().tvm_batch_upload(self.engine.h, self.h, cap, e, len(e)), e, "tvm_batch_upload")
+        self.cap = cap
+        return self
+
+    def launch(self, k=1, sync=True):
+        e = errbuf()
+        for _ in range(k):
+            self._check(lib().tvm_match_launch(self.engine.h, self.h, e, len(e)), e, "tvm_match_launch")
+        if sync:
+            self._check(lib().tvm_engine_sync(self.engine.h, e, len(e)), e, "tvm_engine_sync")
+        return self
+
+    def status(self):
+        """(n_matches, first poisoned package or -1, error bits)."""
+        n, errp, bits = ctypes.c_uint64(), ctypes.c_int64(), ctypes.c_uint64()
+        rc = lib().tvm_match_status(self.engine.h, self.h, ctypes.byref(n), ctypes.byref(errp), ctypes.byref(bits))
+        if rc:
+            raise RuntimeError(f"tvm_match_status failed ({rc})")
+        return n.value, errp.value, bits.value
+
+    def run(self):
+        """Upload (sizing the match buffer exactly after a first pass if needed) + one pass."""
+        self.upload().launch()
+        total, errp, bits = self.status()
+        if total > self.cap:
+            self.upload(total).launch()
+            total, errp, bits = self.status()
+        self.total = total
+        return total, errp, bits
+
+    def pairs(self):
+        """All (package, advisory) pairs as uint32 [n, 2], in (package, advisory) order."""
+        total = self.status()[0]
+        out = np.zeros((total, 2), dtype=np.uint32)
+        got = ctypes.c_uint64()
+        if lib().tvm_match_fetch(self.engine.h, self.h, out.ctypes.data, total, ctypes.byref(got)):
+            raise RuntimeError("tvm_match_fetch failed (match buffer overflow?)")
+        return out[:got.value]
+
+    def time(self, steps):
+        """ms per pass over `steps` back-to-back launches (HIP events on the engine stream)."""
+        ms = ctypes.c_double()
+        e = errbuf()
+        self._check(lib().tvm_match_time(self.engine.h, self.h, steps, ctypes.byref(ms), e, len(e)), e,
+                    "tvm_match_time")
+        return ms.value / steps
+
+    def algorithmic_bytes(self):
+        return lib().tvm_match_algorithmic_bytes(self.engine.h, self.h)
+
+    def close(self):
+        h, self.h = getattr(self, "h", None), None
+        if h:
+            from . import _lib
+            if _lib._lib is not None:
+                _lib._lib.tvm_batch_free(h)
+
+    def __del__(self):
+        self.close()
+
+
+def advisory_vuln_id(db, adv):
+    p = lib().tvm_db_advisory_vuln_id(db.h, adv)
+    return p.decode() if p else None

@@ -334,6 +334,32 @@ int64_t tvm_batch_add_many(tvm_batch* b, tvm_engine* e, const char* bucket, size
   return first;
 }
 
+int64_t tvm_batch_add_many_ex(tvm_batch* b, tvm_engine* e, const char* bucket, size_t n, const char* arena,
+                              const uint64_t* name_off, const uint32_t* name_len, const uint64_t* ver_off,
+                              const uint32_t* ver_len, const uint64_t* arch_off, const uint32_t* arch_len,
+                              uint32_t flags) {
+  if (!b || !e || !bucket || b->uploaded || (flags & ~uint32_t(TVM_ATTR_ARCH | TVM_ATTR_KSPLICE)) ||
+      (n && (!arena || !name_off || !name_len || !ver_off || !ver_len)) ||
+      (n && (flags & TVM_ATTR_ARCH) && (!arch_off || !arch_len)))
+    return -1;
+  const DB& db = e->eng->db();
+  int32_t plat = db.find_plat(bucket);
+  const uint32_t pid = plat < 0 ? 0xFFFFFFFFu : uint32_t(plat);
+  const int64_t first = int64_t(b->hb.desc.size());
+  b->hb.desc.reserve(b->hb.desc.size() + n);
+  for (size_t i = 0; i < n; i++) {
+    const std::string_view ver(arena + ver_off[i], ver_len[i]);
+    uint2 a = make_uint2(PA_ARCH_NONE, 0xFFFFFFFFu);
+    if (flags & TVM_ATTR_ARCH) a.x = db.arch_id(std::string_view(arena + arch_off[i], arch_len[i]));
+    if (flags & TVM_ATTR_KSPLICE) {
+      const size_t dash = ver.find('-');  // release = text after the first '-' (rpm split, rpm.c)
+      a.y = db.ksplice_id(extract_ksplice(dash == std::string_view::npos ? std::string_view() : ver.substr(dash + 1)));
+    }
+    b->hb.add(pid, std::string_view(arena + name_off[i], name_len[i]), ver, a);
+  }
+  return first;
+}
+
 int64_t tvm_batch_size(const tvm_batch* b) { return b ? int64_t(b->hb.desc.size()) : 0; }
 
 int tvm_batch_upload(tvm_engine* e, tvm_batch* b, uint64_t cap, char* err, size_t errlen) {

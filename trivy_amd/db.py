@@ -46,6 +46,13 @@ class DB:
             if rc:
                 raise ValueError(f"tvm_db_put_many failed ({rc})")
 
+    def put_arena(self, n, depth, arena, off, lens):
+        """n records of `depth` path components + value, packed in one arena (record r's
+        strings are items r*(depth+1) .. r*(depth+1)+depth; off u64 / lens u32 per item)."""
+        rc = lib().tvm_db_put_arena(self.h, n, depth, arena, off.ctypes.data, lens.ctypes.data)
+        if rc:
+            raise ValueError(f"tvm_db_put_arena failed ({rc})")
+
     def finalize(self):
         e = errbuf()
         rc = lib().tvm_db_finalize(self.h, e, len(e))
