@@ -313,6 +313,13 @@ void tvm_batch_free(tvm_batch* b) {
   delete b;
 }
 
+// Geometric growth: many small add_many calls (one per target) must not re-allocate the
+// descriptor array to its exact size every time (quadratic copying).
+static void reserve_more(HostBatch& hb, size_t n) {
+  const size_t want = hb.desc.size() + n;
+  if (want > hb.desc.capacity()) hb.desc.reserve(std::max(want, 2 * hb.desc.capacity()));
+}
+
 int64_t tvm_batch_add(tvm_batch* b, tvm_engine* e, const char* bucket, tvm_str name, tvm_str version) {
   if (!b || !e || !bucket || b->uploaded) return -1;
   int32_t plat = e->eng->db().find_plat(bucket);
@@ -328,7 +335,7 @@ int64_t tvm_batch_add_many(tvm_batch* b, tvm_engine* e, const char* bucket, size
   int32_t plat = e->eng->db().find_plat(bucket);
   const uint32_t pid = plat < 0 ? 0xFFFFFFFFu : uint32_t(plat);
   const int64_t first = int64_t(b->hb.desc.size());
-  b->hb.desc.reserve(b->hb.desc.size() + n);
+  reserve_more(b->hb, n);
   for (size_t i = 0; i < n; i++)
     b->hb.add(pid, std::string_view(arena + name_off[i], name_len[i]), std::string_view(arena + ver_off[i], ver_len[i]));
   return first;
@@ -346,7 +353,7 @@ int64_t tvm_batch_add_many_ex(tvm_batch* b, tvm_engine* e, const char* bucket, s
   int32_t plat = db.find_plat(bucket);
   const uint32_t pid = plat < 0 ? 0xFFFFFFFFu : uint32_t(plat);
   const int64_t first = int64_t(b->hb.desc.size());
-  b->hb.desc.reserve(b->hb.desc.size() + n);
+  reserve_more(b->hb, n);
   for (size_t i = 0; i < n; i++) {
     const std::string_view ver(arena + ver_off[i], ver_len[i]);
     uint2 a = make_uint2(PA_ARCH_NONE, 0xFFFFFFFFu);

@@ -52,6 +52,7 @@ struct DevBatch {
   uint32_t n = 0;
   uint64_t arena_bytes = 0;
   uint64_t spill_words = 0;  // scratch needed for installed keys longer than the LDS slot
+  uint32_t gm = 0;           // grammar bits (1 << Cmp) of the batch's platforms (libver.h GM_*)
 };
 
 // Device-side results of one match launch: the per-package advisory lists.
@@ -84,6 +85,7 @@ class Engine {
 
   // Device-resident batch management.
   bool upload(const HostBatch& hb, DevBatch& db, std::string& err);
+  uint32_t grammar_set(const HostBatch& hb) const;
   void free_batch(DevBatch& db);
   bool alloc_matches(uint64_t cap, uint32_t n_pkgs, DevMatches& m, std::string& err);
   void free_matches(DevMatches& m);

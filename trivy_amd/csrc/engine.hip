@@ -121,7 +121,7 @@ __device__ __forceinline__ uint32_t pair_pkg(const S& s, uint32_t j) {
 }
 
 // Per-package predicates of a ROW_FILTER row (common.h RowAux).
-__device__ __attribute__((noinline)) bool aux_pass(const MatchArgs& a, uint32_t ridx, uint2 pa, uint32_t ki) {
+__device__ __forceinline__ bool aux_pass(const MatchArgs& a, uint32_t ridx, uint2 pa, uint32_t ki) {
   const RowAux x = a.db.aux[ridx];
   const uint32_t* ids = a.db.aux_ids + x.list_off;
   if (x.kind & (AUX_ARCH_RH | AUX_ARCH_IN)) {
@@ -224,8 +224,8 @@ __device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared<T, KW, 
 }
 
 // AB (ablation, diagnostics only): 0 = full kernel, 1 = stage+probe+encode+scan only,
-// 2 = no key compare.  Ablation variants produce wrong match lists by construction.
-template <int T, int KW, int MB, int AB = 0>
+// 2 = no key compare, 3 = stage+encode+scan (no probe), 4 = stage+probe+scan (no encode).  Ablation variants produce wrong match lists by construction.
+template <int T, int KW, int MB, uint32_t GM, int AB = 0>
 __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
   __shared__ TileShared<T, KW, MB> s;
   constexpr uint32_t kStageBytes = MB * 8;
@@ -284,13 +284,13 @@ __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
     // installed version -> sort key (LDS slot, or global spill for long versions)
     uint64_t* dst = &s.key[tid * KW];
     uint32_t need = 0;
-    if ((key_bound(pi.cmp, vlen) + 7) / 8 > uint32_t(KW)) {  // might not fit: size it exactly
+    if (AB != 4 && (key_bound(pi.cmp, vlen) + 7) / 8 > uint32_t(KW)) {  // might not fit: size it exactly
       CountSink cs;
       uint32_t cls_unused;
-      need = encode_version_cls(pi.cmp, ver, vlen, cs, cls_unused) ? (cs.n + 7) / 8 : 0;
+      need = encode_version_gm<GM>(pi.cmp, ver, vlen, cs, cls_unused) ? (cs.n + 7) / 8 : 0;
     }
-    bool spill_ok = true;
-    if (need > uint32_t(KW)) {
+    bool spill_ok = AB != 4;
+    if (AB != 4 && need > uint32_t(KW)) {
       const unsigned long long o = atomicAdd(&a.ctl[2], (unsigned long long)need);
       if (o + need > a.spill_cap) {
         atomicOr(&a.ctl[3], (unsigned long long)ERR_SPILL);
@@ -302,15 +302,16 @@ __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
       }
     }
     bool valid = false;
+    if (AB == 4) valid = true;
     if (spill_ok) {
       WordSink ws(dst);
       uint32_t cls = 0;
-      valid = encode_version_cls(pi.cmp, ver, vlen, ws, cls);
+      valid = encode_version_gm<GM>(pi.cmp, ver, vlen, ws, cls);
       ws.flush();
       kinfo |= (ws.n & KI_LEN) | (valid ? KI_VALID : 0u) | ((cls & KI_CLS_MASK) << KI_CLS_SHIFT);
     }
     // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup
-    if (valid || (pi.flags & PLAT_LOOKUP_FIRST)) {
+    if (AB != 3 && (valid || (pi.flags & PLAT_LOOKUP_FIRST))) {
       const uint64_t h = key_hash(d.x, name, nlen);
       for (uint64_t i = h & a.db.slot_mask;; i = (i + 1) & a.db.slot_mask) {
         const uint64_t sh = a.db.slot_hash[i];
@@ -337,7 +338,7 @@ __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
   const uint32_t total_pairs = block_scan<T>(s, cnt, tid);
 
   // ---- 3+4. pair sweep with LDS compaction -----------------------------------------------
-  const uint32_t nm = AB == 1 ? (total_pairs & 1u) : sweep<T, KW, MB, false, AB>(a, s, total_pairs, tid, 0);
+  const uint32_t nm = (AB == 1 || AB >= 3) ? (total_pairs & 1u) : sweep<T, KW, MB, false, AB>(a, s, total_pairs, tid, 0);
 
   // ---- reserve the tile's output segment (one atomic per tile, no inter-tile waiting) -----
   if (tid == 0) {
@@ -361,27 +362,36 @@ __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
   }
 }
 
-// Kernel variants (tile packages T, LDS key words KW, LDS match entries MB).
+// Kernel variants (tile packages T, LDS key words KW, LDS match entries MB), each
+// instantiated for the three grammar sets (libver.h GM_*): the host launches the smallest
+// set that covers the batch's platforms, so a dpkg-only batch runs a kernel with only the
+// dpkg encoder in it (no library-grammar register/scratch footprint).
+using LaunchFn = void (*)(uint32_t n_tiles, hipStream_t st, const MatchArgs& a);
 struct VariantInfo {
   int tile;
-  void (*launch)(uint32_t n_tiles, hipStream_t st, const MatchArgs& a);
+  LaunchFn launch[3];  // GM_DEB, GM_OS, GM_ALL
   const char* name;
 };
 
-template <int T, int KW, int MB, int AB = 0>
-void launch_variant(uint32_t n_tiles, hipStream_t st, const MatchArgs& a) {
-  hipLaunchKernelGGL((match_kernel<T, KW, MB, AB>), dim3(n_tiles), dim3(T), 0, st, a);
+template <int T, int KW, int MB, uint32_t GM, int AB>
+void launch_one(uint32_t n_tiles, hipStream_t st, const MatchArgs& a) {
+  hipLaunchKernelGGL((match_kernel<T, KW, MB, GM, AB>), dim3(n_tiles), dim3(T), 0, st, a);
 }
+#define TVM_VARIANT(T, KW, MB, AB, NAME) \
+  { T, {launch_one<T, KW, MB, GM_DEB, AB>, launch_one<T, KW, MB, GM_OS, AB>, launch_one<T, KW, MB, GM_ALL, AB>}, NAME }
 
 const VariantInfo kVariants[] = {
-    {256, launch_variant<256, 8, 2048>, "t256_k64_m2048"},
-    {256, launch_variant<256, 4, 2048>, "t256_k32_m2048"},
-    {128, launch_variant<128, 4, 1024>, "t128_k32_m1024"},
-    {64, launch_variant<64, 4, 512>, "t64_k32_m512"},
-    {128, launch_variant<128, 4, 2048>, "t128_k32_m2048"},
-    {256, launch_variant<256, 8, 2048, 1>, "ablate_probe_only"},
-    {256, launch_variant<256, 8, 2048, 2>, "ablate_no_cmp"},
+    TVM_VARIANT(256, 8, 2048, 0, "t256_k64_m2048"),
+    TVM_VARIANT(256, 4, 2048, 0, "t256_k32_m2048"),
+    TVM_VARIANT(128, 4, 1024, 0, "t128_k32_m1024"),
+    TVM_VARIANT(64, 4, 512, 0, "t64_k32_m512"),
+    TVM_VARIANT(128, 4, 2048, 0, "t128_k32_m2048"),
+    TVM_VARIANT(256, 8, 2048, 1, "ablate_probe_only"),
+    TVM_VARIANT(256, 8, 2048, 2, "ablate_no_cmp"),
+    TVM_VARIANT(256, 8, 2048, 3, "ablate_encode_only"),
+    TVM_VARIANT(256, 8, 2048, 4, "ablate_probe_no_encode"),
 };
+#undef TVM_VARIANT
 constexpr int kNumVariants = int(sizeof(kVariants) / sizeof(kVariants[0]));
 constexpr int kMinTile = 64;
 constexpr int kMinKeyWords = 4;
@@ -498,11 +508,25 @@ bool Engine::ensure_scratch(uint64_t spill_words, std::string& err) {
   return true;
 }
 
+// Grammar bits (1 << Cmp) of the platforms a batch touches.
+uint32_t Engine::grammar_set(const HostBatch& hb) const {
+  const auto& pi = db_->plat_info;
+  std::vector<uint8_t> seen(pi.size(), 0);
+  uint32_t gm = 0;
+  for (const uint4& d : hb.desc)
+    if (d.x < pi.size() && !seen[d.x]) {
+      seen[d.x] = 1;
+      gm |= 1u << pi[d.x].cmp;
+    }
+  return gm & GM_ALL;
+}
+
 bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
   (void)hipSetDevice(dev_);
   b.n = uint32_t(hb.desc.size());
   b.arena_bytes = hb.arena.size();
   b.spill_words = 0;
+  b.gm = grammar_set(hb);
   for (const uint4& d : hb.desc) {
     const uint32_t need = (key_bound_any(d.w >> 16) + 7) / 8;  // the widest grammar bound
     if (need > uint32_t(kMinKeyWords)) b.spill_words += need;  // bound for every variant
@@ -611,7 +635,8 @@ bool Engine::launch(const DevBatch& b, const DevMatches& m, hipStream_t st, std:
   a.ctl = m.ctl;
   a.spill = spill_;
   a.spill_cap = spill_cap_;
-  v.launch(n_tiles, st, a);
+  const int gi = (b.gm & ~GM_DEB) == 0 ? 0 : (b.gm & ~GM_OS) == 0 ? 1 : 2;
+  v.launch[gi](n_tiles, st, a);
   return hip_ok(hipGetLastError(), "match_kernel launch", err);
 }
 

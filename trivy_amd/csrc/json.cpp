@@ -211,7 +211,7 @@ struct Parser {
 }  // namespace
 
 bool json_parse(std::string_view text, JVal& out, std::string& err) {
-  Parser p{text};
+  Parser p{text, 0, {}, 0};
   if (!p.val(out)) { err = p.err; return false; }
   p.ws();
   if (p.i != text.size()) { err = "invalid character after top-level value"; return false; }

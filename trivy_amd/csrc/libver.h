@@ -822,4 +822,26 @@ TVM_HD bool encode_version_cls(uint8_t cmp, const uint8_t* s, uint32_t n, Sink& 
   }
 }
 
+// Grammar sets a match kernel is specialised for (bit c = Cmp c): a batch whose platforms
+// only use the dpkg grammar runs a kernel with no other encoder in it, so the register and
+// scratch footprint is the dpkg one.  The host picks the smallest set covering the batch.
+enum : uint32_t {
+  GM_DEB = 1u << CMP_DEB,
+  GM_OS = GM_DEB | (1u << CMP_APK) | (1u << CMP_RPM),
+  GM_ALL = 0x3FEu,
+};
+
+template <uint32_t GM, class Sink>
+TVM_HD bool encode_version_gm(uint8_t cmp, const uint8_t* s, uint32_t n, Sink& o, uint32_t& cls) {
+  cls = 0;
+  if (!((GM >> cmp) & 1u)) return false;
+  if constexpr (GM == GM_DEB) {
+    return deb_encode(s, n, o);
+  } else if constexpr ((GM & ~GM_OS) == 0) {
+    return encode_version(cmp, s, n, o);
+  } else {
+    return encode_version_cls(cmp, s, n, o, cls);
+  }
+}
+
 }  // namespace tvm
