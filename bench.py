@@ -234,7 +234,8 @@ def main():
     dev = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
     launch_ms = []
     wall = td.timed(lambda: launch_ms.append(mb.time(args.steps)), steps=1, warmup=0, sync=sync, device=dev)
-    if mb.status() != (total, -1, 0):
+    vname = lib().tvm_variant_name(lib().tvm_engine_set_variant(eng.h, -1)).decode()
+    if mb.status() != (total, -1, 0) and not vname.startswith("ablate"):  # ablations are wrong by design
         raise RuntimeError("timed launches disagree with the first pass")
 
     gather = None

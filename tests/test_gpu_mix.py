@@ -62,3 +62,31 @@ def test_mix_batch_parity(cfg):
         assert from_batch == from_oracle, bucket
         checked += len(want)
     assert checked > 1000
+
+
+@pytest.mark.parametrize("cfg", list(CFGS))
+def test_mix_variants_agree(cfg):
+    """rpm/apk/library grammars and row filters: every kernel variant yields variant 0's pairs."""
+    import trivy_amd
+    from trivy_amd._lib import lib
+    from trivy_amd.batch import MatchBatch
+    from test_gpu_parity import variants
+    plats, weights, kpp = CFGS[cfg]
+    sdb = sm.make_mix_db(plats, kpp // 3, seed=0x77 + len(cfg))
+    eng = trivy_amd.Engine(sdb.put(trivy_amd.DB()).finalize(), 0)
+    batch = sm.make_mix_batch(sdb, 60_000, weights, seed=23)
+    ref = None
+    try:
+        for v in variants():
+            lib().tvm_engine_set_variant(eng.h, v)
+            mb = MatchBatch(eng)
+            sm.add_to(mb, sdb, batch)
+            total, errp, bits = mb.run()
+            assert errp == -1 and bits == 0
+            pairs = mb.pairs()
+            if ref is None:
+                ref = pairs
+                assert total > 10_000
+            assert np.array_equal(pairs, ref), lib().tvm_variant_name(v)
+    finally:
+        lib().tvm_engine_set_variant(eng.h, 0)

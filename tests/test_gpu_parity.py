@@ -121,3 +121,32 @@ def test_empty_batch(world):
     from tools.synth import SynthBatch
     pk, ad, errp, total = run_batch(eng, sdb, SynthBatch(np.zeros(0, dtype=np.int32), [], [], []))
     assert total == 0 and errp == -1
+
+
+def variants():
+    """Indices of the non-ablation match-kernel variants (engine.hip kVariants)."""
+    from trivy_amd._lib import lib
+    out, v = [], 0
+    while lib().tvm_variant_name(v):
+        if not lib().tvm_variant_name(v).decode().startswith("ablate"):
+            out.append(v)
+        v += 1
+    return out
+
+
+def test_every_variant_matches_oracle(world, oracle_built):
+    """Every tile/LDS-budget variant (10% long versions: keys spill past the LDS slot)."""
+    from trivy_amd._lib import lib
+    sdb, eng = world
+    batch = make_batch(sdb, 40, 500, [3, 3, 2, 2], seed=21, long_versions=0.1, invalid=0.01)
+    opk, oad = om.match(om.Prepared(sdb, batch), n_threads=8)
+    vs = variants()
+    assert len(vs) >= 5
+    try:
+        for v in vs:
+            lib().tvm_engine_set_variant(eng.h, v)
+            pk, ad, errp, total = run_batch(eng, sdb, batch)
+            assert errp == -1 and total == len(opk), lib().tvm_variant_name(v)
+            assert np.array_equal(pk, opk) and np.array_equal(ad, oad), lib().tvm_variant_name(v)
+    finally:
+        lib().tvm_engine_set_variant(eng.h, 0)

@@ -113,21 +113,27 @@ struct alignas(16) SlotVal {
   uint32_t row_count;
 };
 enum : uint32_t { SLOT_POISONED = 1u << 31, SLOT_LEN_MASK = 0x7FFFFFFFu };
+// Names in the DB name arena start 8-byte aligned, zero padded to a word boundary, and
+// the arena ends with kNameWords zero words: the probe verifies a name with kNameWords
+// independent word loads (one memory round trip) instead of a byte loop.
+constexpr uint32_t kNameWords = 4;
 
 // 64-bit key hash of (platform, name): FNV-1a over the bytes seeded by the platform,
 // finished with the murmur3 fmix64 avalanche.  Never 0 (0 marks an empty slot).
-TVM_HD uint64_t key_hash(uint32_t plat, const uint8_t* s, uint32_t n) {
-  uint64_t h = 0xcbf29ce484222325ULL ^ (uint64_t(plat) * 0x9E3779B97F4A7C15ULL);
-  for (uint32_t i = 0; i < n; i++) {
-    h ^= s[i];
-    h *= 0x100000001b3ULL;
-  }
+TVM_HD uint64_t key_hash_seed(uint32_t plat) { return 0xcbf29ce484222325ULL ^ (uint64_t(plat) * 0x9E3779B97F4A7C15ULL); }
+TVM_HD uint64_t key_hash_step(uint64_t h, uint8_t c) { return (h ^ c) * 0x100000001b3ULL; }
+TVM_HD uint64_t key_hash_fin(uint64_t h) {
   h ^= h >> 33;
   h *= 0xff51afd7ed558ccdULL;
   h ^= h >> 33;
   h *= 0xc4ceb9fe1a85ec53ULL;
   h ^= h >> 33;
   return h ? h : 1;
+}
+TVM_HD uint64_t key_hash(uint32_t plat, const uint8_t* s, uint32_t n) {
+  uint64_t h = key_hash_seed(plat);
+  for (uint32_t i = 0; i < n; i++) h = key_hash_step(h, s[i]);
+  return key_hash_fin(h);
 }
 
 // Lexicographic compare of two sort keys held in 8-byte words (memory-order bytes,
@@ -155,16 +161,18 @@ TVM_HD int key_cmp(const uint64_t* a, uint32_t na, const uint64_t* b, uint32_t n
   return (na > nb) - (na < nb);
 }
 
-// key_cmp(a, b) where the first two words of b are given inline (b0, b1) and the full b
-// lives at b_full (read only when the first 16 bytes tie and both keys are longer).
-TVM_HD int key_cmp_pre(const uint64_t* a, uint32_t na, uint64_t b0, uint64_t b1, const uint64_t* b_full,
-                       uint32_t nb) {
+// key_cmp(a, b) where the first two words of both keys are given inline (a0, a1, b0, b1)
+// and the full keys live at a_full / b_full (read only when the first 16 bytes tie and
+// both keys are longer).
+TVM_HD int key_cmp_pre2(uint64_t a0, uint64_t a1, const uint64_t* a_full, uint32_t na, uint64_t b0, uint64_t b1,
+                        const uint64_t* b_full, uint32_t nb) {
   const uint32_t m = na < nb ? na : nb;
+  const uint64_t v[2] = {a0, a1};
   const uint64_t w[2] = {b0, b1};
 #pragma unroll
   for (uint32_t i = 0; i < 2; i++) {
     if (8 * i >= m) return (na > nb) - (na < nb);
-    uint64_t x = a[i], y = w[i];
+    uint64_t x = v[i], y = w[i];
     const uint32_t left = m - 8 * i;
     if (left < 8) {
       const uint64_t mask = (1ULL << (8 * left)) - 1;
@@ -178,7 +186,11 @@ TVM_HD int key_cmp_pre(const uint64_t* a, uint32_t na, uint64_t b0, uint64_t b1,
     }
   }
   if (m <= 16) return (na > nb) - (na < nb);
-  return key_cmp(a + 2, na - 16, b_full + 2, nb - 16);
+  return key_cmp(a_full + 2, na - 16, b_full + 2, nb - 16);
+}
+TVM_HD int key_cmp_pre(const uint64_t* a, uint32_t na, uint64_t b0, uint64_t b1, const uint64_t* b_full,
+                       uint32_t nb) {
+  return key_cmp_pre2(a[0], a[1], a, na, b0, b1, b_full, nb);
 }
 
 }  // namespace tvm

@@ -709,8 +709,10 @@ void DB::build_index() {
     slot_val[i] = v;
     slot_key[i] = uint32_t(k);
     name_arena.insert(name_arena.end(), key.name.begin(), key.name.end());
+    name_arena.resize((name_arena.size() + 7) & ~size_t(7), 0);  // 8-B aligned names, zero padded
   }
-  if (name_arena.empty()) name_arena.push_back(0);
+  // tail: the probe kernel loads kNameWords whole words from any name's start
+  name_arena.resize(name_arena.size() + 8 * kNameWords, 0);
 
   plat_info.resize(plats.size());
   for (size_t p = 0; p < plats.size(); p++) {

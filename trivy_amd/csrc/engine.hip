@@ -54,13 +54,14 @@ struct MatchArgs {
   unsigned long long* ctl;  // [0] total, [1] n - first poisoned, [2] spill used, [3] err bits, [4] ticket, [5] tile size
   uint64_t* spill;
   uint64_t spill_cap;
+  uint64_t* kbuf;  // KG variants: installed-key slots in global memory, KW words per package
 };
 
 enum : uint32_t { KI_VALID = 1u << 31, KI_SPILL = 1u << 30, KI_LEN = 0x3FFFu, KI_CLS_SHIFT = 26, KI_CLS_MASK = 7u };
 
-template <int T, int KW, int MB>
+template <int T, int KW, int MB, bool KG>
 struct TileShared {
-  uint64_t key[T * KW];       // installed keys
+  uint64_t key[KG ? 1 : T * KW];  // installed keys (KG: in global memory instead)
   union {
     uint2 mbuf[MB];           // phase 3: compacted matches
     uint4 stage[MB / 2];      // phase 0/1: the tile's name/version bytes
@@ -80,6 +81,42 @@ __device__ __forceinline__ bool name_eq(const uint8_t* a, const uint8_t* b, uint
   for (uint32_t i = 0; i < n; i++)
     if (a[i] != b[i]) return false;
   return true;
+}
+
+// key_hash (common.h) fused with packing the name's first kNameWords*8 bytes into words
+// (memory order, zero padded), so the slot's name is verified with word compares.
+__device__ __forceinline__ uint64_t hash_pack(uint32_t plat, const uint8_t* s, uint32_t n, uint64_t (&w)[kNameWords]) {
+  static_assert(kNameWords == 4, "hash_pack fills exactly four words");
+  uint64_t h = key_hash_seed(plat), cur = 0;
+  w[0] = w[1] = w[2] = w[3] = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint8_t c = s[i];
+    h = key_hash_step(h, c);
+    cur |= uint64_t(c) << (8 * (i & 7));
+    if ((i & 7) == 7 || i + 1 == n) {  // a word is complete (or the name ends)
+      const uint32_t k = i >> 3;
+      if (k == 0) w[0] = cur;
+      else if (k == 1) w[1] = cur;
+      else if (k == 2) w[2] = cur;
+      else if (k == 3) w[3] = cur;
+      cur = 0;
+    }
+  }
+  return key_hash_fin(h);
+}
+
+// Name check against the DB arena (8-B aligned, zero padded, kNameWords-word tail): the
+// four word loads are issued together; names longer than 32 bytes finish bytewise.
+__device__ __forceinline__ bool name_eq_w(const uint64_t (&w)[kNameWords], const uint8_t* name, const uint8_t* arena,
+                                          uint32_t off, uint32_t n) {
+  const uint64_t* y = reinterpret_cast<const uint64_t*>(arena + off);
+  const uint64_t y0 = y[0], y1 = y[1], y2 = y[2], y3 = y[3];
+  bool eq = n == 0 || w[0] == y0;
+  if (n > 8) eq &= w[1] == y1;
+  if (n > 16) eq &= w[2] == y2;
+  if (n > 24) eq &= w[3] == y3;
+  if (eq && n > 32) eq = name_eq(name + 32, arena + off + 32, n - 32);
+  return eq;
 }
 
 // Block-wide exclusive scan of v over T lanes; returns the block total.
@@ -145,18 +182,29 @@ __device__ __forceinline__ bool aux_pass(const MatchArgs& a, uint32_t ridx, uint
   return true;
 }
 
-// Interval test of package q's installed key against one row (global index ridx).
-template <int KW, class S>
-__device__ __forceinline__ bool eval_row(const MatchArgs& a, const S& s, uint32_t q, const Row& row, uint32_t ridx) {
+// Installed key of tile package q: the global spill area for long keys, else its slot
+// (LDS, or global memory for KG variants).
+template <int T, int KW, bool KG, class S>
+__device__ __forceinline__ const uint64_t* key_ptr(const MatchArgs& a, const S& s, uint32_t q) {
+  if (s.kinfo[q] & KI_SPILL) return a.spill + s.koff[q];
+  if constexpr (KG) return a.kbuf + size_t(s.tile * T + q) * KW;
+  else return &s.key[q * KW];
+}
+
+// Interval test of package q's installed key (k; first two words k0, k1 already loaded)
+// against one row (global index ridx).
+template <class S>
+__device__ __forceinline__ bool eval_row(const MatchArgs& a, const S& s, uint32_t q, const Row& row, uint32_t ridx,
+                                         const uint64_t* k, uint64_t k0, uint64_t k1) {
   if ((row.adv & ROW_FILTER) && !aux_pass(a, ridx, s.pattr[q], s.kinfo[q])) return false;
   if (row.adv & ROW_ALWAYS) return true;
   const uint32_t ki = s.kinfo[q];
   if (!(ki & KI_VALID)) return false;
-  const uint64_t* k = (ki & KI_SPILL) ? a.spill + s.koff[q] : &s.key[q * KW];
   const uint32_t kl = ki & KI_LEN;
   bool m = true;
   if (!(row.hi_len & KEY_INF)) {
-    const int c = key_cmp_pre(k, kl, row.hi_pre0, row.hi_pre1, a.db.key_words + row.hi_off, row.hi_len & KEY_LEN_MASK);
+    const int c = key_cmp_pre2(k0, k1, k, kl, row.hi_pre0, row.hi_pre1, a.db.key_words + row.hi_off,
+                               row.hi_len & KEY_LEN_MASK);
     m = (row.hi_len & KEY_INCL) ? c <= 0 : c < 0;
   }
   if (m && !(row.lo_len & KEY_INF)) {
@@ -169,30 +217,42 @@ __device__ __forceinline__ bool eval_row(const MatchArgs& a, const S& s, uint32_
 // One sweep over the tile's pairs.  DIRECT=false: compact into LDS (count all, store the
 // first MB).  DIRECT=true: store straight to out[base + position].
 // AB (ablation, diagnostics only): 2 = load rows but skip the key compare.
-template <int T, int KW, int MB, bool DIRECT, int AB = 0>
-__device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared<T, KW, MB>& s, uint32_t total_pairs,
+template <int T, int KW, int MB, bool KG, bool DIRECT, int AB = 0>
+__device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared<T, KW, MB, KG>& s, uint32_t total_pairs,
                                           uint32_t tid, unsigned long long base) {
   constexpr int W = T / 64;
   const uint32_t lane = tid & 63, wave = tid >> 6;
   uint32_t nm = 0;
   uint32_t j = tid, q = 0, ridx = 0;
   Row row{};
+  const uint64_t* kp = nullptr;
+  uint64_t k0 = 0, k1 = 0;  // KG: the key's first words travel with the row load
   if (j < total_pairs) {
     q = pair_pkg<T>(s, j);
     ridx = s.rbeg[q] + (j - s.scan[q]);
     row = a.db.rows[ridx];
+    kp = key_ptr<T, KW, KG>(a, s, q);
+    if (KG) k0 = kp[0], k1 = kp[1];
   }
   for (uint32_t b0 = 0; b0 < total_pairs; b0 += T) {
     // issue the next chunk's row load before testing this chunk's pair
     const uint32_t jn = j + T;
     uint32_t qn = 0, ridxn = 0;
     Row rown{};
+    const uint64_t* kpn = nullptr;
+    uint64_t k0n = 0, k1n = 0;
     if (jn < total_pairs) {
       qn = pair_pkg<T>(s, jn);
       ridxn = s.rbeg[qn] + (jn - s.scan[qn]);
       rown = a.db.rows[ridxn];
+      kpn = key_ptr<T, KW, KG>(a, s, qn);
+      if (KG) k0n = kpn[0], k1n = kpn[1];
     }
-    const bool m = (j < total_pairs) && (AB == 2 ? (row.adv & 7u) == 0 : eval_row<KW>(a, s, q, row, ridx));
+    if (!KG && j < total_pairs) {
+      if (s.kinfo[q] & KI_SPILL) k0 = kp[0], k1 = kp[1];
+      else k0 = s.key[q * KW], k1 = s.key[q * KW + 1];  // LDS loads, not flat ones
+    }
+    const bool m = (j < total_pairs) && (AB == 2 ? (row.adv & 7u) == 0 : eval_row(a, s, q, row, ridx, kp, k0, k1));
     const unsigned long long bal = __ballot(m);
     const uint32_t lane_off = __popcll(bal & ((1ull << lane) - 1ull));
     if (lane == 0) s.wsum[wave] = uint32_t(__popcll(bal));
@@ -219,19 +279,80 @@ __device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared<T, KW, 
     q = qn;
     ridx = ridxn;
     row = rown;
+    kp = kpn;
+    k0 = k0n;
+    k1 = k1n;
   }
   return nm;
 }
 
+// Phase 1 for one package: encode the installed version into its key slot and probe the
+// index.  Instantiated separately for LDS-staged and global string pointers so the staged
+// case compiles to LDS loads rather than generic (flat) ones.
+template <int T, int KW, int MB, bool KG, uint32_t GM, int AB>
+__device__ __forceinline__ void probe_encode(const MatchArgs& a, TileShared<T, KW, MB, KG>& s, uint32_t tid,
+                                             uint32_t p, const uint4 d, const uint8_t* name, const uint8_t* ver,
+                                             uint32_t& cnt, uint32_t& rbeg, uint32_t& kinfo, uint32_t& koff) {
+  const PlatInfo pi = a.db.plats[d.x];
+  const uint32_t nlen = d.w & 0xFFFFu, vlen = d.w >> 16;
+  // installed version -> sort key: one optimistic pass into the LDS slot; a key longer
+  // than the slot is re-encoded into the global spill area
+  bool valid = AB == 4;
+  if (AB != 4) {
+    uint64_t* slot;
+    if constexpr (KG) slot = a.kbuf + size_t(p) * KW;
+    else slot = &s.key[tid * KW];
+    CapWordSink cs(slot, KW * 8);
+    uint32_t cls = 0;
+    valid = encode_version_gm<GM>(pi.cmp, ver, vlen, cs, cls);
+    cs.flush();
+    if (valid && cs.n > uint32_t(KW * 8)) {
+      const uint32_t need = (cs.n + 7) / 8;
+      const unsigned long long o = atomicAdd(&a.ctl[2], (unsigned long long)need);
+      if (o + need > a.spill_cap) {
+        atomicOr(&a.ctl[3], (unsigned long long)ERR_SPILL);
+        valid = false;
+      } else {
+        WordSink ws(a.spill + o);
+        uint32_t cls2 = 0;
+        encode_version_gm<GM>(pi.cmp, ver, vlen, ws, cls2);
+        ws.flush();
+        koff = uint32_t(o);
+        kinfo |= KI_SPILL;
+      }
+    }
+    kinfo |= (cs.n & KI_LEN) | (valid ? KI_VALID : 0u) | ((cls & KI_CLS_MASK) << KI_CLS_SHIFT);
+  }
+  // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup
+  if (AB != 3 && (valid || (pi.flags & PLAT_LOOKUP_FIRST))) {
+    uint64_t nw[kNameWords];
+    const uint64_t h = hash_pack(d.x, name, nlen, nw);
+    for (uint64_t i = h & a.db.slot_mask;; i = (i + 1) & a.db.slot_mask) {
+      const uint64_t sh = a.db.slot_hash[i];
+      const SlotVal sv = a.db.slot_val[i];  // issued with the hash: no dependent round trip
+      if (sh == 0) break;
+      if (sh != h) continue;
+      if ((sv.name_len & SLOT_LEN_MASK) != nlen || !name_eq_w(nw, name, a.db.name_arena, sv.name_off, nlen)) continue;
+      if (sv.name_len & SLOT_POISONED) {
+        atomicMax(&a.ctl[1], (unsigned long long)(a.n - p));
+      } else if (valid) {
+        cnt = sv.row_count;
+        rbeg = sv.row_begin;
+      }
+      break;
+    }
+  }
+}
+
 // AB (ablation, diagnostics only): 0 = full kernel, 1 = stage+probe+encode+scan only,
 // 2 = no key compare, 3 = stage+encode+scan (no probe), 4 = stage+probe+scan (no encode).  Ablation variants produce wrong match lists by construction.
-template <int T, int KW, int MB, uint32_t GM, int AB = 0>
+template <int T, int KW, int MB, bool KG, uint32_t GM, int AB = 0>
 __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
-  __shared__ TileShared<T, KW, MB> s;
+  __shared__ TileShared<T, KW, MB, KG> s;
   constexpr uint32_t kStageBytes = MB * 8;
   const uint32_t tid = threadIdx.x;
   if (tid == 0) {
-    s.tile = atomicAdd(reinterpret_cast<unsigned int*>(&a.ctl[4]), 1u);
+    s.tile = blockIdx.x;  // segments are placed through the tile directory: any order works
     s.span_lo = 0xFFFFFFFFu;
     s.span_hi = 0;
     if (blockIdx.x == 0) a.ctl[5] = T;
@@ -277,57 +398,11 @@ __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
   // ---- 1. probe + encode -------------------------------------------------------------
   uint32_t cnt = 0, rbeg = 0, kinfo = 0, koff = 0;
   if (p < a.n && d.x < a.db.n_plats) {
-    const PlatInfo pi = a.db.plats[d.x];
-    const uint8_t* name = staged ? stage_bytes + (d.y - base16) : a.arena + d.y;
-    const uint8_t* ver = staged ? stage_bytes + (d.z - base16) : a.arena + d.z;
-    const uint32_t nlen = d.w & 0xFFFFu, vlen = d.w >> 16;
-    // installed version -> sort key (LDS slot, or global spill for long versions)
-    uint64_t* dst = &s.key[tid * KW];
-    uint32_t need = 0;
-    if (AB != 4 && (key_bound(pi.cmp, vlen) + 7) / 8 > uint32_t(KW)) {  // might not fit: size it exactly
-      CountSink cs;
-      uint32_t cls_unused;
-      need = encode_version_gm<GM>(pi.cmp, ver, vlen, cs, cls_unused) ? (cs.n + 7) / 8 : 0;
-    }
-    bool spill_ok = AB != 4;
-    if (AB != 4 && need > uint32_t(KW)) {
-      const unsigned long long o = atomicAdd(&a.ctl[2], (unsigned long long)need);
-      if (o + need > a.spill_cap) {
-        atomicOr(&a.ctl[3], (unsigned long long)ERR_SPILL);
-        spill_ok = false;
-      } else {
-        dst = a.spill + o;
-        koff = uint32_t(o);
-        kinfo |= KI_SPILL;
-      }
-    }
-    bool valid = false;
-    if (AB == 4) valid = true;
-    if (spill_ok) {
-      WordSink ws(dst);
-      uint32_t cls = 0;
-      valid = encode_version_gm<GM>(pi.cmp, ver, vlen, ws, cls);
-      ws.flush();
-      kinfo |= (ws.n & KI_LEN) | (valid ? KI_VALID : 0u) | ((cls & KI_CLS_MASK) << KI_CLS_SHIFT);
-    }
-    // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup
-    if (AB != 3 && (valid || (pi.flags & PLAT_LOOKUP_FIRST))) {
-      const uint64_t h = key_hash(d.x, name, nlen);
-      for (uint64_t i = h & a.db.slot_mask;; i = (i + 1) & a.db.slot_mask) {
-        const uint64_t sh = a.db.slot_hash[i];
-        const SlotVal sv = a.db.slot_val[i];  // issued with the hash: no dependent round trip
-        if (sh == 0) break;
-        if (sh != h) continue;
-        if ((sv.name_len & SLOT_LEN_MASK) != nlen || !name_eq(name, a.db.name_arena + sv.name_off, nlen)) continue;
-        if (sv.name_len & SLOT_POISONED) {
-          atomicMax(&a.ctl[1], (unsigned long long)(a.n - p));
-        } else if (valid) {
-          cnt = sv.row_count;
-          rbeg = sv.row_begin;
-        }
-        break;
-      }
-    }
+    if (staged)
+      probe_encode<T, KW, MB, KG, GM, AB>(a, s, tid, p, d, stage_bytes + (d.y - base16), stage_bytes + (d.z - base16),
+                                          cnt, rbeg, kinfo, koff);
+    else
+      probe_encode<T, KW, MB, KG, GM, AB>(a, s, tid, p, d, a.arena + d.y, a.arena + d.z, cnt, rbeg, kinfo, koff);
   }
   s.rbeg[tid] = rbeg;
   s.kinfo[tid] = kinfo;
@@ -338,7 +413,7 @@ __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
   const uint32_t total_pairs = block_scan<T>(s, cnt, tid);
 
   // ---- 3+4. pair sweep with LDS compaction -----------------------------------------------
-  const uint32_t nm = (AB == 1 || AB >= 3) ? (total_pairs & 1u) : sweep<T, KW, MB, false, AB>(a, s, total_pairs, tid, 0);
+  const uint32_t nm = (AB == 1 || AB >= 3) ? (total_pairs & 1u) : sweep<T, KW, MB, KG, false, AB>(a, s, total_pairs, tid, 0);
 
   // ---- reserve the tile's output segment (one atomic per tile, no inter-tile waiting) -----
   if (tid == 0) {
@@ -358,7 +433,7 @@ __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
     for (uint32_t i = tid; i < nm; i += T)
       if (base + i < a.out_cap) a.out[base + i] = s.mbuf[i];
   } else {
-    sweep<T, KW, MB, true, AB>(a, s, total_pairs, tid, base);  // rare: more matches than the LDS buffer
+    sweep<T, KW, MB, KG, true, AB>(a, s, total_pairs, tid, base);  // rare: more matches than the LDS buffer
   }
 }
 
@@ -369,16 +444,24 @@ __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
 using LaunchFn = void (*)(uint32_t n_tiles, hipStream_t st, const MatchArgs& a);
 struct VariantInfo {
   int tile;
+  int kw;
+  bool kg;             // installed keys in global memory (KW words per package)
   LaunchFn launch[3];  // GM_DEB, GM_OS, GM_ALL
   const char* name;
 };
 
-template <int T, int KW, int MB, uint32_t GM, int AB>
+template <int T, int KW, int MB, bool KG, uint32_t GM, int AB>
 void launch_one(uint32_t n_tiles, hipStream_t st, const MatchArgs& a) {
-  hipLaunchKernelGGL((match_kernel<T, KW, MB, GM, AB>), dim3(n_tiles), dim3(T), 0, st, a);
+  hipLaunchKernelGGL((match_kernel<T, KW, MB, KG, GM, AB>), dim3(n_tiles), dim3(T), 0, st, a);
 }
-#define TVM_VARIANT(T, KW, MB, AB, NAME) \
-  { T, {launch_one<T, KW, MB, GM_DEB, AB>, launch_one<T, KW, MB, GM_OS, AB>, launch_one<T, KW, MB, GM_ALL, AB>}, NAME }
+#define TVM_VARIANT_G(T, KW, MB, KG, AB, NAME)                                                   \
+  {                                                                                             \
+    T, KW, KG,                                                                                  \
+        {launch_one<T, KW, MB, KG, GM_DEB, AB>, launch_one<T, KW, MB, KG, GM_OS, AB>,           \
+         launch_one<T, KW, MB, KG, GM_ALL, AB>},                                                \
+        NAME                                                                                    \
+  }
+#define TVM_VARIANT(T, KW, MB, AB, NAME) TVM_VARIANT_G(T, KW, MB, false, AB, NAME)
 
 const VariantInfo kVariants[] = {
     TVM_VARIANT(256, 8, 2048, 0, "t256_k64_m2048"),
@@ -386,12 +469,19 @@ const VariantInfo kVariants[] = {
     TVM_VARIANT(128, 4, 1024, 0, "t128_k32_m1024"),
     TVM_VARIANT(64, 4, 512, 0, "t64_k32_m512"),
     TVM_VARIANT(128, 4, 2048, 0, "t128_k32_m2048"),
+    TVM_VARIANT(256, 6, 1536, 0, "t256_k48_m1536"),
+    TVM_VARIANT(256, 4, 1536, 0, "t256_k32_m1536"),
+    TVM_VARIANT_G(256, 8, 1536, true, 0, "t256_g64_m1536"),
+    TVM_VARIANT_G(256, 8, 2048, true, 0, "t256_g64_m2048"),
+    TVM_VARIANT_G(256, 4, 1536, true, 0, "t256_g32_m1536"),
+    TVM_VARIANT_G(128, 8, 1024, true, 0, "t128_g64_m1024"),
     TVM_VARIANT(256, 8, 2048, 1, "ablate_probe_only"),
     TVM_VARIANT(256, 8, 2048, 2, "ablate_no_cmp"),
     TVM_VARIANT(256, 8, 2048, 3, "ablate_encode_only"),
     TVM_VARIANT(256, 8, 2048, 4, "ablate_probe_no_encode"),
 };
 #undef TVM_VARIANT
+#undef TVM_VARIANT_G
 constexpr int kNumVariants = int(sizeof(kVariants) / sizeof(kVariants[0]));
 constexpr int kMinTile = 64;
 constexpr int kMinKeyWords = 4;
@@ -616,7 +706,8 @@ bool Engine::launch(const DevBatch& b, const DevMatches& m, hipStream_t st, std:
     err = "tile directory smaller than the batch";
     return false;
   }
-  if (!ensure_scratch(b.spill_words, err)) return false;
+  const uint64_t kslots = v.kg ? uint64_t(n_tiles) * v.tile * v.kw : 0;  // KG: per-package key slots
+  if (!ensure_scratch(b.spill_words + kslots, err)) return false;
   if (!hip_ok(hipMemsetAsync(m.ctl, 0, 8 * sizeof(unsigned long long), st), "memset(ctl)", err)) return false;
   if (n_tiles == 0) return true;
   MatchArgs a;
@@ -633,8 +724,9 @@ bool Engine::launch(const DevBatch& b, const DevMatches& m, hipStream_t st, std:
   a.out_cap = m.cap;
   a.dir = m.dir;
   a.ctl = m.ctl;
-  a.spill = spill_;
-  a.spill_cap = spill_cap_;
+  a.kbuf = spill_;
+  a.spill = spill_ + kslots;
+  a.spill_cap = spill_cap_ - kslots;
   const int gi = (b.gm & ~GM_DEB) == 0 ? 0 : (b.gm & ~GM_OS) == 0 ? 1 : 2;
   v.launch[gi](n_tiles, st, a);
   return hip_ok(hipGetLastError(), "match_kernel launch", err);

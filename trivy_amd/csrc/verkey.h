@@ -111,7 +111,27 @@ static_assert(make_deb_codes().v[0xFF] == 0x80 && make_deb_codes().v[0xF7] == 0x
 static __constant__ DebCodes d_deb_codes = make_deb_codes();
 static constexpr DebCodes h_deb_codes = make_deb_codes();
 
+// ASCII bytes by arithmetic (no table load in the per-lane parse loop): letters take
+// 0x0C.. in byte order, the other non-digit bytes 0x81.. in byte order ('~' aside).
+TVM_HD constexpr uint8_t deb_code_ascii(uint8_t b) {
+  return b >= 'a' && b <= 'z'   ? uint8_t(b - 'a' + 0x26)
+         : b >= 'A' && b <= 'Z' ? uint8_t(b - 'A' + 0x0C)
+         : b == '~'             ? uint8_t(DEB_TILDE)
+         : b < 0x30             ? uint8_t(b + 0x80)
+         : b < 0x41             ? uint8_t(b + 0x76)
+         : b < 0x61             ? uint8_t(b + 0x5C)
+         : b < 0x7F             ? uint8_t(b + 0x42)
+                                : uint8_t(0xC0);
+}
+constexpr bool deb_code_ascii_ok() {
+  for (int b = 1; b < 0x80; b++)
+    if (!(b >= '0' && b <= '9') && deb_code_ascii(uint8_t(b)) != make_deb_codes().v[b]) return false;
+  return true;
+}
+static_assert(deb_code_ascii_ok(), "dpkg ASCII codes must equal the table");
+
 TVM_HD uint8_t deb_code(uint8_t b) {
+  if (b < 0x80) return deb_code_ascii(b);
 #ifdef __HIP_DEVICE_COMPILE__
   return d_deb_codes.v[b];
 #else
@@ -139,6 +159,34 @@ TVM_HD bool deb_valid_runes(const uint8_t* s, uint32_t n, bool upstream) {
   return true;
 }
 
+// One digit run [i, e) as TERM_k + k big-endian bytes; strconv.Atoi clamps at MaxInt64.
+// Runs of <= 9 significant digits (nearly all) accumulate in 32 bits.
+template <class Sink>
+TVM_HD void deb_number(const uint8_t* s, uint32_t i, uint32_t e, Sink& o) {
+  while (i < e && s[i] == '0') i++;
+  uint64_t v;
+  if (e - i <= 9) {
+    uint32_t v32 = 0;
+    for (; i < e; i++) v32 = v32 * 10u + uint32_t(s[i] - '0');
+    v = v32;
+  } else if (e - i > 19) {
+    v = uint64_t(INT64_MAX);
+  } else {
+    v = 0;
+    bool over = false;
+    for (; i < e && !over; i++) {
+      const uint64_t d = uint64_t(s[i] - '0');
+      if (v > (uint64_t(INT64_MAX) - d) / 10) over = true;
+      else v = v * 10 + d;
+    }
+    if (over) v = uint64_t(INT64_MAX);
+  }
+  const uint32_t k = v ? uint32_t(8 - (__builtin_clzll(v) >> 3)) : 0u;
+  o.put(uint8_t(DEB_TERM0 + k));
+  for (int b = int(k) - 1; b >= 0; b--) o.put(uint8_t(v >> (8 * b)));
+}
+
+// PART(s) of the key layout above (s already validated).
 template <class Sink>
 TVM_HD void deb_part(const uint8_t* s, uint32_t n, Sink& o) {
   if (n == 0) {
@@ -149,35 +197,42 @@ TVM_HD void deb_part(const uint8_t* s, uint32_t n, Sink& o) {
   uint32_t i = 0;
   while (i < n) {
     while (i < n && !is_adigit(s[i])) o.put(deb_code(s[i++]));
-    uint64_t v = 0;
-    bool over = false;
-    while (i < n && is_adigit(s[i])) {
-      uint64_t d = uint64_t(s[i++] - '0');
-      if (!over) {
-        if (v > (uint64_t(INT64_MAX) - d) / 10) over = true;
-        else v = v * 10 + d;
-      }
-    }
-    if (over) v = uint64_t(INT64_MAX);
-    uint32_t k = 0;
-    for (uint64_t t = v; t; t >>= 8) k++;
-    o.put(uint8_t(DEB_TERM0 + k));
-    for (int b = int(k) - 1; b >= 0; b--) o.put(uint8_t(v >> (8 * b)));
+    uint32_t e = i;
+    while (e < n && is_adigit(s[e])) e++;
+    deb_number(s, i, e, o);
+    i = e;
   }
   o.put(DEB_END);
 }
 
-// go-deb-version NewVersion + key emission.  Returns false (emitting nothing) on a
-// parse error; the caller's sink receives the key otherwise.
+// ASCII bytes go-deb-version accepts in an upstream version (digits, letters, . + ~ _ - :);
+// the revision accepts the same set minus '-' and ':'.
+constexpr uint64_t kDebOk0 = (1ull << '.') | (1ull << '+') | (1ull << '-') | (1ull << ':') | (0x3FFull << '0');
+constexpr uint64_t kDebOk1 = (1ull << ('_' - 64)) | (1ull << ('~' - 64)) | (0x3FFFFFFull << ('A' - 64)) |
+                             (0x3FFFFFFull << ('a' - 64));
+
+// go-deb-version NewVersion + key emission.  Returns false on a parse error (the sink
+// may have received a partial key, which the caller discards).  One pre-pass finds the
+// first ':' (epoch), the last '-' (revision) and checks the ASCII character sets; only a
+// string with non-ASCII bytes takes the rune-decoding validity check.
 template <class Sink>
 TVM_HD bool deb_encode(const uint8_t* s, uint32_t n, Sink& o) {
+  uint32_t colon = n, dash = n, last_colon = n;
+  bool bad = false, high = false;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint8_t c = s[i];
+    if (c == ':') {
+      if (colon == n) colon = i;
+      last_colon = i;
+    } else if (c == '-') {
+      dash = i;
+    }
+    if (c >= 0x80) high = true;
+    else bad |= !(((c < 64 ? kDebOk0 >> c : kDebOk1 >> (c - 64)) & 1u));
+  }
   // epoch: strconv.Atoi of the text before the first ':'; negative -> error
-  uint32_t colon = n;
-  for (uint32_t i = 0; i < n; i++)
-    if (s[i] == ':') { colon = i; break; }
   uint64_t epoch = 0;
-  const uint8_t* r = s;
-  uint32_t rn = n;
+  uint32_t r0 = 0;
   if (colon < n) {
     uint32_t i = 0;
     bool neg = false;
@@ -191,28 +246,32 @@ TVM_HD bool deb_encode(const uint8_t* s, uint32_t n, Sink& o) {
       if (epoch > uint64_t(INT64_MAX) + (neg ? 1 : 0)) return false;
     }
     if (neg && epoch != 0) return false;  // epoch is negative
-    r = s + colon + 1;
-    rn = n - colon - 1;
+    r0 = colon + 1;
   }
-  // split at the last '-'
-  uint32_t dash = rn;
-  for (uint32_t i = rn; i-- > 0;)
-    if (r[i] == '-') { dash = i; break; }
-  const uint8_t* up = r;
-  uint32_t nup = dash;
-  const uint8_t* rev = r + (dash < rn ? dash + 1 : rn);
-  uint32_t nrev = dash < rn ? rn - dash - 1 : 0;
+  // split the rest at its last '-'
+  const bool has_rev = dash < n && dash >= r0;
+  const uint8_t* up = s + r0;
+  const uint32_t nup = (has_rev ? dash : n) - r0;
+  const uint8_t* rev = has_rev ? s + dash + 1 : s + n;
+  const uint32_t nrev = has_rev ? n - dash - 1 : 0;
   if (nup == 0 || !is_adigit(up[0])) return false;
-  if (!deb_valid_runes(up, nup, true) || !deb_valid_runes(rev, nrev, false)) return false;
-  uint32_t k = 0;
-  for (uint64_t t = epoch; t; t >>= 8) k++;
+  if (high) {
+    if (!deb_valid_runes(up, nup, true) || !deb_valid_runes(rev, nrev, false)) return false;
+  } else {
+    // the epoch text was checked above; the rest must be in the ASCII sets, and the
+    // revision (after the last '-') may not hold a ':'
+    if (bad) {
+      if (!deb_valid_runes(up, nup, true) || !deb_valid_runes(rev, nrev, false)) return false;
+    }
+    if (has_rev && last_colon < n && last_colon > dash) return false;
+  }
+  const uint32_t k = epoch ? uint32_t(8 - (__builtin_clzll(epoch) >> 3)) : 0u;
   o.put(uint8_t(k));
   for (int b = int(k) - 1; b >= 0; b--) o.put(uint8_t(epoch >> (8 * b)));
   deb_part(up, nup, o);
   deb_part(rev, nrev, o);
   return true;
 }
-
 
 // ------------------------------------------------------------------- signed integers -----
 // Order-preserving variable-length code of a signed 64-bit value: v >= 0 as 0x80+k then
@@ -478,6 +537,29 @@ struct WordSink {
   }
   TVM_HD void flush() {
     if (n & 7) dst[n >> 3] = acc;
+  }
+};
+
+// Device sink with a capacity: stores the key while it fits in cap_bytes (whole words)
+// and counts every byte, so one pass both encodes a typical key and sizes a long one.
+struct CapWordSink {
+  uint64_t* dst;
+  uint32_t cap;
+  uint64_t acc = 0;
+  uint32_t n = 0;
+  TVM_HD CapWordSink(uint64_t* d, uint32_t cap_bytes) : dst(d), cap(cap_bytes) {}
+  TVM_HD void put(uint8_t b) {
+    if (n < cap) {
+      acc |= uint64_t(b) << (8 * (n & 7));
+      if ((n & 7) == 7) {
+        dst[n >> 3] = acc;
+        acc = 0;
+      }
+    }
+    n++;
+  }
+  TVM_HD void flush() {
+    if (n < cap && (n & 7)) dst[n >> 3] = acc;
   }
 };
 
