@@ -139,9 +139,12 @@ uint64_t tvm_engine_table_bytes(const tvm_engine* e);
 /* Integrity check: re-reads every device table and compares it with the host image. */
 int tvm_engine_verify(tvm_engine* e, char* err, size_t errlen);
 /* Tuning knob: selects the match-kernel variant (tile size / LDS budget); returns the
- * previous one.  v < 0 only queries.  Names via tvm_variant_name (NULL past the last). */
+ * previous one.  v < 0 only queries.  Names via tvm_variant_name (NULL past the last);
+ * variant 0 = "auto" (default): the tuned variant for the batch's grammar set. */
 int tvm_engine_set_variant(tvm_engine* e, int v);
 const char* tvm_variant_name(int v);
+/* Variant index the engine's most recent launch ran (auto resolved); -1 before any. */
+int tvm_engine_last_variant(tvm_engine* e);
 
 /* ---- ospkg ------------------------------------------------------------------------------ */
 /* ospkg.Detect: family = ftypes.OSType ("debian", "ubuntu", ...); now_unix = clock.Now(ctx).

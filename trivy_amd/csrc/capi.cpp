@@ -238,6 +238,12 @@ int tvm_engine_set_variant(tvm_engine* e, int v) {
 
 const char* tvm_variant_name(int v) { return variant_name(v); }
 
+int tvm_engine_last_variant(tvm_engine* e) {
+  if (!e) return -1;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  return e->eng->last_launched();
+}
+
 static int detect_common(tvm_engine* e, bool full, const char* fam, const char* ver, const tvm_repository* repo,
                          const tvm_package* pkgs, size_t n, int64_t now, tvm_result* out, char* err,
                          size_t errlen) {

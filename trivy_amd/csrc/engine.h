@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -103,9 +104,12 @@ class Engine {
 
   const DB& db() const { return *db_; }
 
-  // Kernel variant (tile size / LDS budget); returns the previous one.  Default 0,
-  // overridable with the TVM_VARIANT environment variable at open().
+  // Kernel variant (tile size / LDS budget); returns the previous one.  Default 0 =
+  // "auto" (the tuned variant for the batch's grammar set), overridable with the
+  // TVM_VARIANT environment variable at open().
   int set_variant(int v);
+  // Variant index of the most recent launch (auto resolved), -1 before the first.
+  int last_launched() const { return last_launched_; }
   // Integrity check: the device tables still equal the host images (bytes compared).
   bool verify(std::string& err);
   int variant() const { return variant_; }
@@ -113,6 +117,7 @@ class Engine {
  private:
   int dev_ = 0;
   int variant_ = 0;
+  std::atomic<int> last_launched_{-1};
   hipStream_t stream_ = nullptr;
   const DB* db_ = nullptr;
   DevDB d_;
@@ -125,8 +130,10 @@ class Engine {
   bool ensure_scratch(uint64_t spill_words, std::string& err);
 };
 
-// Kernel variants: count and names (engine.hip kVariants).
+// Kernel variants: count and names (engine.hip; 0 = "auto").
 int num_variants();
 const char* variant_name(int v);
+// The variant "auto" (0) resolves to for a batch of grammar bits gm; other v unchanged.
+int resolve_variant(int v, uint32_t gm);
 
 }  // namespace tvm
