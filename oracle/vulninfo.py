@@ -1,0 +1,176 @@
+"""ORACLE - TEST INFRASTRUCTURE ONLY.
+
+Pure-Python restatement of the reference's vulnerability-detail join, the step right
+after the detectors.  Used only by tests/, smoke() and bench.py's
+checker; the product (trivy_amd/csrc/vulninfo.cpp + fill.hip) never imports it.
+
+Restated from (fwereade/trivy @ 2025-01-14):
+  pkg/vulnerability/vulnerability.go:15-39    primaryURLPrefixes
+  pkg/vulnerability/vulnerability.go:60-109   Client.FillInfo
+  pkg/vulnerability/vulnerability.go:111-134  getVendorSeverity
+  pkg/vulnerability/vulnerability.go:136-157  getPrimaryURL
+and the third-party trivy-db (github.com/aquasecurity/trivy-db v0.0.0-20231005141211-
+4fc651f7ac8d, reference go.mod:25, absent here): db.Config.GetVulnerability reads bucket
+"vulnerability"[vulnID] and json.Unmarshals it into types.Vulnerability (Title,
+Description, Severity string, CweIDs, VendorSeverity map[SourceID]Severity(int), CVSS,
+References, PublishedDate, LastModifiedDate); a missing key or a decode error is an
+error, which FillInfo logs and skips (vulnerability.go:72-76).  Severity.String() is
+SeverityNames[s]; NewSeverity(name) returns the index of name or UNKNOWN.
+
+Pinned by the reference's own table (pkg/vulnerability/vulnerability_test.go:17-283,
+transcribed to tests/golden/tables/vulnerability__vulnerability_test.json) and by the
+integration goldens (integration/testdata/*.json.golden: Severity, SeveritySource,
+PrimaryURL, Status of every reported vulnerability).
+"""
+import json
+
+SEVERITY = ["UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"]
+STATUS_AFFECTED, STATUS_FIXED = 2, 3
+GHSA, NVD = "ghsa", "nvd"
+
+# vulnerability.go:15-39 (source IDs: trivy-db pkg/vulnsrc/vulnerability constants)
+PRIMARY_URL_PREFIXES = {
+    "debian": ["http://www.debian.org", "https://www.debian.org"],
+    "ubuntu": ["http://www.ubuntu.com", "https://usn.ubuntu.com"],
+    "redhat": ["https://access.redhat.com"],
+    "suse-cvrf": ["http://lists.opensuse.org", "https://lists.opensuse.org"],
+    "oracle-oval": ["http://linux.oracle.com/errata", "https://linux.oracle.com/errata"],
+    "nodejs-security-wg": ["https://www.npmjs.com", "https://hackerone.com"],
+    "ruby-advisory-db": ["https://groups.google.com"],
+}
+
+_STR, _STRS, _VSEV, _CVSS, _TIME = "str", "strs", "vsev", "cvss", "time"
+_VULN_FIELDS = {"title": ("Title", _STR), "description": ("Description", _STR), "severity": ("Severity", _STR),
+                "cweids": ("CweIDs", _STRS), "vendorseverity": ("VendorSeverity", _VSEV),
+                "cvss": ("CVSS", _CVSS), "references": ("References", _STRS),
+                "publisheddate": ("PublishedDate", _TIME), "lastmodifieddate": ("LastModifiedDate", _TIME)}
+
+
+class DecodeError(Exception):
+    pass
+
+
+def _is_int(x):
+    return isinstance(x, int) and not isinstance(x, bool)
+
+
+def decode_vulnerability(text):
+    """json.Unmarshal(value, &types.Vulnerability); raises DecodeError on a type mismatch."""
+    try:
+        v = json.loads(text)
+    except ValueError as e:
+        raise DecodeError(str(e))
+    out = {}
+    if v is None:
+        return out
+    if not isinstance(v, dict):
+        raise DecodeError("cannot unmarshal into types.Vulnerability")
+    for k, x in v.items():
+        f = _VULN_FIELDS.get(k.lower())
+        if f is None:
+            continue
+        name, kind = f
+        if x is None:
+            out.pop(name, None)
+            continue
+        if kind in (_STR, _TIME):
+            if not isinstance(x, str):
+                raise DecodeError(f"field {name}")
+        elif kind == _STRS:
+            if not isinstance(x, list) or any(e is not None and not isinstance(e, str) for e in x):
+                raise DecodeError(f"field {name}")
+            x = [e or "" for e in x]
+        elif kind == _VSEV:
+            if not isinstance(x, dict) or any(e is not None and not _is_int(e) for e in x.values()):
+                raise DecodeError(f"field {name}")
+            x = {s: (e or 0) for s, e in x.items()}
+        elif kind == _CVSS:
+            if not isinstance(x, dict) or any(e is not None and not isinstance(e, dict) for e in x.values()):
+                raise DecodeError(f"field {name}")
+        out[name] = x
+    return out
+
+
+def severity_string(s):
+    return SEVERITY[s] if 0 <= s < len(SEVERITY) else SEVERITY[0]  # out of range: unpinned (Go panics)
+
+
+def get_vendor_severity(vuln_id, vuln, source):
+    """vulnerability.go:111-134."""
+    vs = vuln.get("VendorSeverity") or {}
+    if source in vs:
+        return severity_string(vs[source]), source
+    if vuln_id.startswith("GHSA-") and GHSA in vs:
+        return severity_string(vs[GHSA]), GHSA
+    if NVD in vs:
+        return severity_string(vs[NVD]), NVD
+    if not vuln.get("Severity"):
+        return SEVERITY[0], ""
+    return vuln["Severity"], ""
+
+
+def get_primary_url(vuln_id, refs, source):
+    """vulnerability.go:136-157."""
+    if vuln_id.startswith("CVE-"):
+        return "https://avd.aquasec.com/nvd/" + vuln_id.lower()
+    if vuln_id.startswith("RUSTSEC-"):
+        return "https://osv.dev/vulnerability/" + vuln_id
+    if vuln_id.startswith("GHSA-"):
+        return "https://github.com/advisories/" + vuln_id
+    if vuln_id.startswith("TEMP-"):
+        return "https://security-tracker.debian.org/tracker/" + vuln_id
+    for pre in PRIMARY_URL_PREFIXES.get(source, []):
+        for ref in refs or []:
+            if ref.startswith(pre):
+                return ref
+    return ""
+
+
+def vulnerability_bucket(records):
+    """vulnID -> raw JSON text of bucket "vulnerability" (fixture record lists)."""
+    out = {}
+    for r in records:
+        if len(r["path"]) == 2 and r["path"][0] == "vulnerability":
+            out[r["path"][1]] = r["value"]
+    return out
+
+
+def fill_info(bucket, vulns):
+    """Client.FillInfo (vulnerability.go:60-109) over DetectedVulnerability dicts (Go field
+    names; absent = zero value).  Returns new dicts; the inputs are not modified."""
+    out = []
+    for v in vulns:
+        v = json.loads(json.dumps(v))
+        if v.get("FixedVersion"):
+            v["Status"] = STATUS_FIXED
+        elif not v.get("Status"):
+            v["Status"] = STATUS_AFFECTED
+        vid = v.get("VulnerabilityID", "")
+        raw = bucket.get(vid)
+        if raw is None:
+            out.append(v)
+            continue
+        try:
+            vuln = decode_vulnerability(raw)
+        except DecodeError:
+            out.append(v)
+            continue
+        source = (v.get("DataSource") or {}).get("ID", "")
+        severity, sev_source = get_vendor_severity(vid, vuln, source)
+        if v.get("SeveritySource"):
+            severity = (v.get("Vulnerability") or {}).get("Severity", "")
+            sev_source = v["SeveritySource"]
+            vs = dict(vuln.get("VendorSeverity") or {})
+            vs[sev_source] = SEVERITY.index(severity) if severity in SEVERITY else 0
+            vuln["VendorSeverity"] = vs
+        vuln["Severity"] = severity
+        v["Vulnerability"] = vuln
+        v["SeveritySource"] = sev_source
+        v["PrimaryURL"] = get_primary_url(vid, vuln.get("References"), source)
+        for k in ("SeveritySource", "PrimaryURL"):
+            if not v[k]:
+                del v[k]
+        if not vuln["Severity"]:
+            del vuln["Severity"]
+        out.append(v)
+    return out

@@ -42,6 +42,7 @@ FILES = [
     "pkg/detector/library/compare/pep440/compare_test.go",
     "pkg/detector/library/compare/rubygems/compare_test.go",
     "pkg/scanner/utils/utils_test.go",
+    "pkg/vulnerability/vulnerability_test.go",
 ]
 
 # trivy-db / trivy constants used in the tables (values from trivy-db pkg/types and
