@@ -54,8 +54,13 @@ class C2:
         self.n_keys = len(self.sdb.key_names)
         self.plats = PLATS
 
-    def load(self, db):
-        for n, depth, arena, off, lens in (self.sdb.records_arena(), self.sdb.source_arena()):
+    def load(self, db, vulns=True):
+        from tools.synth_vuln import vuln_arena
+        parts = [self.sdb.records_arena(detail=vulns), self.sdb.source_arena()]
+        if vulns:  # bucket "vulnerability" for the FillInfo leg (tools/synth_vuln.py)
+            parts.append(vuln_arena(self.sdb.vuln_ids()))
+        self.has_vulns = vulns
+        for n, depth, arena, off, lens in parts:
             db.put_arena(n, depth, arena, off, lens)
 
     def fill(self, mb):
@@ -165,6 +170,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-fill", action="store_true", help="c2: skip the FillInfo leg (no vulnerability bucket)")
     ap.add_argument("--check", action="store_true", help="verify the bench batch against the oracle (c2)")
     ap.add_argument("--gather", action="store_true",
                     help="after the timed region, gather all match lists to rank 0 (RCCL), reported apart")
@@ -191,7 +197,10 @@ def main():
     t0 = time.perf_counter()
     wl = C2(args, rank) if args.config == "c2" else Mix(args, rank, args.config)
     db = trivy_amd.DB()
-    wl.load(db)
+    if args.config == "c2":
+        wl.load(db, vulns=not args.no_fill)
+    else:
+        wl.load(db)
     eng = trivy_amd.Engine(db.finalize(), local)
     log(rank, f"[bench] {wl.name}: db {wl.n_keys} keys, {wl.n_adv} advisories, tables "
               f"{eng.table_bytes()/1e6:.1f} MB ({time.perf_counter()-t0:.1f}s)")
@@ -257,6 +266,18 @@ def main():
     alg_bytes = mb.algorithmic_bytes()
     achieved = alg_bytes / launch_s / 1e9
 
+    fill = None
+    if getattr(wl, "has_vulns", False):
+        # FillInfo (vulnerability.go:60-157) fused behind the match list: timed apart, on the
+        # same stream, over the same device-resident pairs (DESIGN.md "FillInfo")
+        mb.launch(1)
+        fill_ms = mb.fill_time(args.steps)
+        fill_bytes = mb.fill_algorithmic_bytes()
+        fill_gbs = fill_bytes / (fill_ms / 1e3) / 1e9
+        fill = {"kernel_ms": fill_ms, "matches_per_s": total / (fill_ms / 1e3),
+                "algorithmic_bytes_per_launch": fill_bytes, "achieved_GBs": fill_gbs,
+                "frac": fill_gbs / HBM_PEAK_GBS, "db_vulnerabilities": len(wl.sdb.vuln_ids())}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = wl.cpu_baseline(args.cpu_seconds, args.cpu_threads)
@@ -288,6 +309,8 @@ def main():
         }
         if gather is not None:
             line["gather"] = gather
+        if fill is not None:
+            line["fill_info"] = fill
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -16,6 +16,9 @@
  *   tvm_ospkg_is_supported     ospkg.Driver.IsSupportedVersion  detect.go:59
  *   tvm_batch_* / tvm_match_*  (new) many-target batching behind concurrent Detect calls
  *                              (pkg/k8s/scanner/scanner.go:141, pkg/rpc/server/server.go:45)
+ *   tvm_fill_info              vulnerability.Client.FillInfo  pkg/vulnerability/vulnerability.go:60-109
+ *                              (with getVendorSeverity :111-134 and getPrimaryURL :136-157)
+ *   tvm_match_fill*            (new) FillInfo fused behind a batch's device-resident match list
  *
  * Error convention: functions return 0 on success and a non-zero TVM_E* code on failure,
  * with a NUL-terminated message written to (err, errlen).  Messages carry the same text
@@ -225,6 +228,54 @@ int tvm_lib_is_vulnerable_host(int grammar, const char* ver, size_t ver_len, con
                                size_t json_len);
 /* Advisory fields for host-side inspection of batch results. */
 const char* tvm_db_advisory_vuln_id(const tvm_db* db, uint32_t adv);
+
+/* ---- vulnerability detail: FillInfo ------------------------------------------------ */
+/* One detected vulnerability as FillInfo reads it (vulnerability.go:60-109). */
+typedef struct {
+  tvm_str vulnerability_id;
+  tvm_str data_source_id;       /* DataSource.ID; empty when DataSource is nil */
+  tvm_str severity_source;      /* SeveritySource the detector set; empty = none */
+  tvm_str severity;             /* Vulnerability.Severity the detector set (read with severity_source) */
+  int32_t status;               /* Status the detector set (dbTypes.Status) */
+  int32_t has_fixed_version;    /* FixedVersion != "" */
+} tvm_fill_in;
+/* What FillInfo writes back.  When !found (trivy-db GetVulnerability failed: unknown ID or
+ * undecodable record; the reference logs and skips, :72-76) only status changed and the
+ * other fields are "" / NULL. */
+typedef struct {
+  int32_t found;
+  int32_t status;                    /* Status */
+  const char* severity;              /* Vulnerability.Severity */
+  const char* severity_source;       /* SeveritySource */
+  const char* primary_url;           /* PrimaryURL */
+  const char* vulnerability_json;    /* the Vulnerability as JSON (trivy-db types.Vulnerability
+                                        fields, omitempty; VendorSeverity includes the detector's
+                                        package-specific entry, :95-101); NULL when !found */
+} tvm_fill_out;
+typedef struct {
+  tvm_fill_out* items;
+  size_t n;
+  void* priv;
+} tvm_fill_result;
+/* Client.FillInfo over n detected vulnerabilities: decisions on the GPU (one launch), the
+ * strings rebuilt on the host.  Thread-safe. */
+int tvm_fill_info(tvm_engine* e, const tvm_fill_in* in, size_t n, tvm_fill_result* out, char* err, size_t errlen);
+void tvm_fill_result_free(tvm_fill_result* r);
+/* Batch path: enqueue FillInfo over the batch's device match list right behind
+ * tvm_match_launch (same stream, no host round trip); each (package, advisory) pair is
+ * filled as its driver's Detect would have populated it (no Red Hat per-CVE merge). */
+int tvm_match_fill(tvm_engine* e, tvm_batch* b, char* err, size_t errlen);
+/* After sync: per pair, in tvm_match_fetch order, 4 uint32: {vulnerability record
+ * (0xFFFFFFFF = not found), status, severity code
+ * (0..4 SeverityNames; 0xFFFD detector's; 0xFFFE DB string; 0xFFFF out of range) |
+ * severity-source id << 16 (0xFFFF = none), primary URL kind << 28 | reference index}. */
+int tvm_match_fill_fetch(tvm_engine* e, tvm_batch* b, uint32_t* out4, uint64_t cap, uint64_t* n_out);
+/* Times `steps` back-to-back tvm_match_fill launches (ms total); needs a completed match. */
+int tvm_match_fill_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err, size_t errlen);
+/* Algorithmic bytes of one tvm_match_fill pass over the batch's current match list. */
+uint64_t tvm_match_fill_algorithmic_bytes(tvm_engine* e, tvm_batch* b);
+/* Name of a severity-source id from tvm_match_fill_fetch ("" for 0xFFFF / unknown). */
+const char* tvm_fill_source_name(tvm_engine* e, uint32_t id);
 
 #ifdef __cplusplus
 }

@@ -87,8 +87,29 @@ def decode_vulnerability(text):
         elif kind == _CVSS:
             if not isinstance(x, dict) or any(e is not None and not isinstance(e, dict) for e in x.values()):
                 raise DecodeError(f"field {name}")
+            x = {src: _cvss(e or {}) for src, e in x.items()}
         out[name] = x
     return out
+
+
+_CVSS_FIELDS = {"v2vector": ("V2Vector", str), "v3vector": ("V3Vector", str), "v2score": ("V2Score", float),
+                "v3score": ("V3Score", float)}
+
+
+def _cvss(e):
+    """types.CVSS {V2Vector, V3Vector string; V2Score, V3Score float64}, zero values dropped
+    (the struct's omitempty form)."""
+    out = {}
+    for k, v in e.items():
+        f = _CVSS_FIELDS.get(k.lower())
+        if f is None or v is None:
+            continue
+        name, typ = f
+        if typ is str and not isinstance(v, str) or typ is float and (isinstance(v, bool) or
+                                                                      not isinstance(v, (int, float))):
+            raise DecodeError(f"field CVSS.{name}")
+        out[name] = v
+    return {k: v for k, v in out.items() if v}
 
 
 def severity_string(s):

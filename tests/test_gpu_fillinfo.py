@@ -1,0 +1,163 @@
+"""GPU: FillInfo (vulnerability.go:60-157) through the C-ABI, bit-exact against the
+reference's own vectors and against the oracle (oracle/vulninfo.py):
+
+* every TestClient_FillInfo case (vulnerability_test.go:17-283);
+* the FillInfo fields of every vulnerability of the integration goldens, in one launch;
+* seeded random DBs/inputs covering every branch (unknown IDs, undecodable records,
+  vendor/GHSA/NVD/DB severity, package-specific severities, all URL rules, long IDs);
+* the batch path: FillInfo fused behind a device-resident match list, per pair against
+  the oracle applied to the driver's DetectedVulnerability for that pair.
+"""
+import json
+
+import numpy as np
+import pytest
+
+import fillinfo_golden as fg
+import oracle.vulninfo as vi
+
+pytestmark = pytest.mark.gpu
+
+_TABLE = fg.table_cases()
+
+
+def _engine(records):
+    import trivy_amd
+    db = trivy_amd.DB()
+    db.put_records(records)
+    return trivy_amd.Engine(db, 0)
+
+
+@pytest.mark.parametrize("case", _TABLE, ids=[c[0] for c in _TABLE])
+def test_fillinfo_table(case):
+    from trivy_amd.vulnerability import Client
+    name, fixtures, vulns, want = case
+    got = Client(_engine(fg.load_records(fixtures))).fill_info(vulns)
+    assert [fg.norm(v) for v in got] == [fg.norm(v) for v in want], name
+
+
+def test_fillinfo_integration_goldens():
+    from trivy_amd.vulnerability import Client
+    cases = fg.integration_cases()
+    got = Client(_engine(fg.load_records(fg.integration_fixtures()))).fill_info([c[1] for c in cases])
+    assert len(got) == len(cases) >= 100
+    for (cid, _inp, want), g in zip(cases, got):
+        assert fg.got_form(g) == fg.want_form(want), cid
+
+
+def _random_case(seed, n_vulns=400, n_items=3000):
+    from tools.synth_vuln import SOURCES, vuln_values
+    rng = np.random.default_rng(seed)
+    prefixes = ["CVE-2021-", "GHSA-", "RUSTSEC-2020-", "TEMP-000", "ALAS-2023-", "DSA-", "USN-", "SUSE-SU-", "ELSA-",
+                "NSWG-ECO-", "OSVDB-", "cve-"]
+    ids = []
+    for i in range(n_vulns):
+        p = prefixes[int(rng.integers(0, len(prefixes)))]
+        ids.append((p + str(i) + ("-" + "x" * int(rng.integers(20, 40)) if i % 37 == 0 else "")).encode())
+    ids = sorted(set(ids))
+    recs = [{"path": ["vulnerability", k.decode()], "value": v.decode()} for k, v in vuln_values(ids, seed)]
+    unknown = [b"CVE-1999-%d" % i for i in range(20)] + [b"", b"GHSA-unknown"]
+    pool = ids + unknown
+    items = []
+    for _ in range(n_items):
+        v = {"VulnerabilityID": pool[int(rng.integers(0, len(pool)))].decode()}
+        r = rng.random()
+        if r < 0.8:
+            v["DataSource"] = {"ID": SOURCES[int(rng.integers(0, len(SOURCES)))] if r < 0.75 else "other",
+                               "Name": "n"}
+        if rng.random() < 0.5:
+            v["FixedVersion"] = "1.2.%d" % int(rng.integers(0, 9))
+        if rng.random() < 0.3:
+            v["Status"] = int(rng.integers(0, 8))
+        if rng.random() < 0.15:
+            v["SeveritySource"] = ["debian", "redhat", "nvd"][int(rng.integers(0, 3))]
+            v["Vulnerability"] = {"Severity": ["LOW", "HIGH", "CRITICAL", "bogus", ""][int(rng.integers(0, 5))]}
+        items.append(v)
+    return recs, items
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_fillinfo_random_vs_oracle(seed):
+    from trivy_amd.vulnerability import Client
+    recs, items = _random_case(seed)
+    got = Client(_engine(recs)).fill_info(items)
+    want = vi.fill_info(vi.vulnerability_bucket(recs), items)
+    assert len(got) == len(want)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert fg.norm(g) == fg.norm(w), (i, items[i])
+
+
+def test_fillinfo_empty_and_no_bucket():
+    from trivy_amd.vulnerability import Client
+    c = Client(_engine([{"path": ["data-source", "x"], "value": "{}"}]))
+    assert c.fill_info([]) == []
+    got = c.fill_info([{"VulnerabilityID": "CVE-1-1", "FixedVersion": "1"}, {"VulnerabilityID": "X", "Status": 5}])
+    assert got == [{"VulnerabilityID": "CVE-1-1", "FixedVersion": "1", "Status": 3},
+                   {"VulnerabilityID": "X", "Status": 5}]
+
+
+def test_match_fill_batch_vs_oracle():
+    """Batch path: match kernel -> fill kernel on the same stream; every pair's decision
+    equals the oracle's FillInfo of that pair's debian/ubuntu DetectedVulnerability."""
+    import trivy_amd
+    from trivy_amd._lib import lib
+    from trivy_amd.batch import MatchBatch
+    from tools.synth import DEBIAN_DS, UBUNTU_DS, make_batch, make_db
+    from tools.synth_vuln import vuln_arena, vuln_values
+
+    sdb = make_db(["debian 12", "ubuntu 22.04"], 1500, seed=5)
+    ids = sdb.vuln_ids()
+    db = trivy_amd.DB()
+    for n, depth, arena, off, lens in (sdb.records_arena(detail=True), sdb.source_arena(), vuln_arena(ids, 5)):
+        assert lib().tvm_db_put_arena(db.h, n, depth, arena, off.ctypes.data, lens.ctypes.data) == 0
+    eng = trivy_amd.Engine(db, 0)
+    batch = make_batch(sdb, 12, 300, [1, 1], seed=5)
+    mb = MatchBatch(eng)
+    arena, noff, nlen, voff, vlen = batch.arena()
+    for p, b0, b1 in batch.targets:
+        mb.add_arena(sdb.platforms[p], b1 - b0, arena, noff[b0:], nlen[b0:], voff[b0:], vlen[b0:])
+    total, errp, _ = mb.run()
+    assert errp == -1 and total > 1000
+    pairs = mb.pairs()
+    dec = mb.fill().fill_decisions()
+    assert dec.shape == (len(pairs), 4)
+
+    bucket = {k.decode(): v.decode() for k, v in vuln_values(ids, 5)}
+    rec_of = {k.decode(): i for i, k in enumerate(ids)}
+    ds_of = {p: json.loads((DEBIAN_DS if p.startswith("debian") else UBUNTU_DS).decode()) for p in sdb.platforms}
+    pkg_plat = np.zeros(len(batch), dtype=np.int64)
+    for p, b0, b1 in batch.targets:
+        pkg_plat[b0:b1] = p
+    names = ["UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"]
+    for (pk, adv), d in zip(pairs.tolist(), dec.tolist()):
+        plat = sdb.platforms[pkg_plat[pk]]
+        vid = sdb.adv_vid[adv].decode()
+        v = {"VulnerabilityID": vid, "DataSource": ds_of[plat]}
+        if sdb.adv_fixed[adv]:
+            v["FixedVersion"] = sdb.adv_fixed[adv].decode()
+        if plat.startswith("debian"):  # debian.go:89-98
+            st, sev = sdb.adv_detail(adv)
+            if st:
+                v["Status"] = st
+            if sev:
+                v["SeveritySource"] = "debian"
+                v["Vulnerability"] = {"Severity": names[sev]}
+        w = vi.fill_info(bucket, [v])[0]
+        assert d[1] == w["Status"], (pk, adv)
+        try:
+            found = vid in bucket and vi.decode_vulnerability(bucket[vid]) is not None
+        except vi.DecodeError:
+            found = False
+        if not found:
+            assert d[0] == 0xFFFFFFFF, (pk, adv)  # GetVulnerability error: skipped
+            continue
+        assert d[0] == rec_of[vid]
+        code, src = d[2] & 0xFFFF, d[2] >> 16
+        sev = (v["Vulnerability"]["Severity"] if code == 0xFFFD else
+               json.loads(bucket[vid]).get("Severity", "") if code == 0xFFFE else
+               names[code] if code < 5 else "UNKNOWN")
+        assert sev == w["Vulnerability"].get("Severity", ""), (pk, adv, d)
+        ssrc = v.get("SeveritySource", "") if code == 0xFFFD else lib().tvm_fill_source_name(eng.h, src).decode()
+        assert ssrc == w.get("SeveritySource", ""), (pk, adv, d)
+        assert d[3] >> 28 == 1 and w["PrimaryURL"] == "https://avd.aquasec.com/nvd/" + vid.lower()
+    mb.close()

@@ -46,8 +46,14 @@ class SynthDB:
     def n_adv(self):
         return int(self.adv_begin[-1])
 
-    def records_arena(self, poison_keys=()):
-        """(n, depth=3, arena, off, len) for tvm_db_put_arena, plus data-source records."""
+    @staticmethod
+    def adv_detail(a):
+        """(Status, Severity) of advisory a when records carry detail (deterministic)."""
+        return (a % 8 if a % 3 == 0 else 0), (a % 5 if a % 4 == 0 else 0)
+
+    def records_arena(self, poison_keys=(), detail=False):
+        """(n, depth=3, arena, off, len) for tvm_db_put_arena, plus data-source records.
+        detail=True adds adv_detail()'s Status/Severity to the advisory values."""
         items = []
         poison = set(int(k) for k in poison_keys)
         for k in range(len(self.key_names)):
@@ -55,6 +61,9 @@ class SynthDB:
             name = self.key_names[k]
             for a in range(self.adv_begin[k], self.adv_begin[k + 1]):
                 val = b'{"FixedVersion":"' + self.adv_fixed[a] + b'"}'
+                if detail:
+                    st, sev = self.adv_detail(a)
+                    val = val[:-1] + b',"Status":%d,"Severity":%d}' % (st, sev)
                 if k in poison and a == self.adv_begin[k]:
                     val = b'{"FixedVersion":["bad"]}'
                 items += [root, name, self.adv_vid[a], val]
@@ -66,6 +75,10 @@ class SynthDB:
             ds = DEBIAN_DS if p.startswith("debian") else UBUNTU_DS if p.startswith("ubuntu") else AMAZON_DS
             items += [b"data-source", p.encode(), ds]
         return _arena(items, 2)
+
+    def vuln_ids(self):
+        """Distinct vulnerability IDs of the DB, in bbolt byte order."""
+        return sorted(set(self.adv_vid))
 
 
 def _arena(items, depth):

@@ -56,6 +56,21 @@ class Result(ctypes.Structure):
                 ("priv", ctypes.c_void_p)]
 
 
+class FillIn(ctypes.Structure):
+    _fields_ = [("vulnerability_id", Str), ("data_source_id", Str), ("severity_source", Str), ("severity", Str),
+                ("status", ctypes.c_int32), ("has_fixed_version", ctypes.c_int32)]
+
+
+class FillOut(ctypes.Structure):
+    _fields_ = [("found", ctypes.c_int32), ("status", ctypes.c_int32), ("severity", ctypes.c_char_p),
+                ("severity_source", ctypes.c_char_p), ("primary_url", ctypes.c_char_p),
+                ("vulnerability_json", ctypes.c_char_p)]
+
+
+class FillResult(ctypes.Structure):
+    _fields_ = [("items", ctypes.POINTER(FillOut)), ("n", ctypes.c_size_t), ("priv", ctypes.c_void_p)]
+
+
 # (name, restype, argtypes) for every exported symbol of include/trivy_amd.h
 _P = ctypes.c_void_p
 _SIG = [
@@ -115,6 +130,15 @@ _SIG = [
                                           ctypes.POINTER(Result), ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_library_detect_vulnerabilities", ctypes.c_int, [_P, ctypes.c_char_p, Str, Str, Str, ctypes.POINTER(Result),
                                                           ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_fill_info", ctypes.c_int, [_P, ctypes.POINTER(FillIn), ctypes.c_size_t, ctypes.POINTER(FillResult),
+                                     ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_fill_result_free", None, [ctypes.POINTER(FillResult)]),
+    ("tvm_match_fill", ctypes.c_int, [_P, _P, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_match_fill_fetch", ctypes.c_int, [_P, _P, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
+    ("tvm_match_fill_time", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_char_p,
+                                           ctypes.c_size_t]),
+    ("tvm_match_fill_algorithmic_bytes", ctypes.c_uint64, [_P, _P]),
+    ("tvm_fill_source_name", ctypes.c_char_p, [_P, ctypes.c_uint32]),
 ]
 
 EXPORTED = [s[0] for s in _SIG]

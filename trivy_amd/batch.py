@@ -136,6 +136,35 @@ class MatchBatch:
     def algorithmic_bytes(self):
         return lib().tvm_match_algorithmic_bytes(self.engine.h, self.h)
 
+    # ---- FillInfo fused behind the match list (tvm_match_fill*) ----
+    def fill(self, sync=True):
+        """Enqueue FillInfo over the device match list (after launch())."""
+        e = errbuf()
+        self._check(lib().tvm_match_fill(self.engine.h, self.h, e, len(e)), e, "tvm_match_fill")
+        if sync:
+            self._check(lib().tvm_engine_sync(self.engine.h, e, len(e)), e, "tvm_engine_sync")
+        return self
+
+    def fill_decisions(self):
+        """uint32 [n, 4] per pair in pairs() order: {record or 0xFFFFFFFF, status,
+        severity code | source id << 16, URL kind << 28 | reference index}."""
+        total = self.status()[0]
+        out = np.zeros((total, 4), dtype=np.uint32)
+        got = ctypes.c_uint64()
+        if lib().tvm_match_fill_fetch(self.engine.h, self.h, out.ctypes.data, total, ctypes.byref(got)):
+            raise RuntimeError("tvm_match_fill_fetch failed")
+        return out[:got.value]
+
+    def fill_time(self, steps):
+        ms = ctypes.c_double()
+        e = errbuf()
+        self._check(lib().tvm_match_fill_time(self.engine.h, self.h, steps, ctypes.byref(ms), e, len(e)), e,
+                    "tvm_match_fill_time")
+        return ms.value / steps
+
+    def fill_algorithmic_bytes(self):
+        return lib().tvm_match_fill_algorithmic_bytes(self.engine.h, self.h)
+
     def close(self):
         h, self.h = getattr(self, "h", None), None
         if h:

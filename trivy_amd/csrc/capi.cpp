@@ -2,6 +2,7 @@
 #include "../../include/trivy_amd.h"
 
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <shared_mutex>
@@ -13,17 +14,20 @@
 #include "engine.h"
 #include "libdb.h"
 #include "libver.h"
+#include "vulninfo.h"
 
 using namespace tvm;
 
 struct tvm_db {
   DB db;
+  VulnTable vt;  // bucket "vulnerability" (FillInfo tables)
   bool finalized = false;
 };
 
 struct tvm_engine {
   std::shared_mutex mu;  // calls share; swap is exclusive (listen.go:154-190 quiesce)
   std::unique_ptr<Engine> eng;
+  std::unique_ptr<FillEngine> fill;
   tvm_db* db = nullptr;
   int device = 0;
 };
@@ -32,6 +36,8 @@ struct tvm_batch {
   HostBatch hb;
   DevBatch dev;
   DevMatches m;
+  uint4* fill_out = nullptr;  // tvm_match_fill decisions, parallel to m.pairs
+  uint64_t fill_cap = 0;
   bool uploaded = false;
   int device = 0;
 };
@@ -167,6 +173,7 @@ int tvm_db_finalize(tvm_db* db, char* err, size_t errlen) {
     set_err(err, errlen, e);
     return TVM_EINVAL;
   }
+  db->vt.build(db->db);
   db->finalized = true;
   return TVM_OK;
 }
@@ -194,8 +201,15 @@ tvm_engine* tvm_engine_open(tvm_db* db, int device, char* err, size_t errlen) {
     set_err(err, errlen, e);
     return nullptr;
   }
+  FillEngine* fill = FillEngine::open(db->vt, device, e);
+  if (!fill) {
+    delete eng;
+    set_err(err, errlen, e);
+    return nullptr;
+  }
   auto* t = new tvm_engine();
   t->eng.reset(eng);
+  t->fill.reset(fill);
   t->db = db;
   t->device = device;
   return t;
@@ -207,12 +221,15 @@ int tvm_engine_swap(tvm_engine* e, tvm_db* db, char* err, size_t errlen) {
   if (!e || !db || !db->finalized) return TVM_EINVAL;
   std::string msg;
   Engine* fresh = Engine::open(db->db, e->device, msg);  // build before quiescing
-  if (!fresh) {
+  FillEngine* fresh_fill = fresh ? FillEngine::open(db->vt, e->device, msg) : nullptr;
+  if (!fresh || !fresh_fill) {
+    delete fresh;
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
   }
   std::unique_lock<std::shared_mutex> lk(e->mu);
   e->eng.reset(fresh);
+  e->fill.reset(fresh_fill);
   e->db = db;
   return TVM_OK;
 }
@@ -313,7 +330,7 @@ void tvm_batch_free(tvm_batch* b) {
     (void)hipSetDevice(b->device);
     for (void* p : {static_cast<void*>(b->dev.desc), static_cast<void*>(b->dev.arena), static_cast<void*>(b->dev.attr),
                     static_cast<void*>(b->dev.cpe_bits), static_cast<void*>(b->m.pairs), static_cast<void*>(b->m.dir),
-                    static_cast<void*>(b->m.ctl)})
+                    static_cast<void*>(b->m.ctl), static_cast<void*>(b->fill_out)})
       if (p) (void)hipFree(p);
   }
   delete b;
@@ -596,3 +613,169 @@ int tvm_library_detect_vulnerabilities(tvm_engine* e, const char* lib_type, tvm_
 const char* tvm_library_type(const char* lib_type) { return lib_type ? library_ecosystem(lib_type) : nullptr; }
 
 }  // extern "C"
+
+// ---- FillInfo (vulnerability.go:60-157) ----------------------------------------------
+
+namespace {
+
+struct FillPriv {
+  std::vector<tvm_fill_out> items;
+  std::deque<std::string> strs;  // owned strings; items point into them (deque: stable addresses)
+};
+
+}  // namespace
+
+int tvm_fill_info(tvm_engine* e, const tvm_fill_in* in, size_t n, tvm_fill_result* out, char* err, size_t errlen) {
+  if (!e || !out || (n && !in)) return TVM_EINVAL;
+  *out = tvm_fill_result{nullptr, 0, nullptr};
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  const VulnTable& vt = e->fill->table();
+  std::vector<uint4> items(n);
+  std::vector<uint8_t> arena;
+  for (size_t i = 0; i < n; i++) {
+    const tvm_fill_in& x = in[i];
+    const size_t len = std::min<size_t>(x.vulnerability_id.n, 0xFFFF);  // longer IDs: no record has one
+    const uint32_t src = vt.source_id(std::string_view(x.data_source_id.p ? x.data_source_id.p : "", x.data_source_id.n));
+    uint4 it;
+    it.x = uint32_t(arena.size());
+    it.y = uint32_t(len) | (src << 16);
+    it.z = uint32_t(x.status & 0xFF) | (x.has_fixed_version ? FI_FIXED : 0u) | (x.severity_source.n ? FI_SEV_SRC : 0u);
+    it.w = FILL_NOT_FOUND;
+    if (len) arena.insert(arena.end(), x.vulnerability_id.p, x.vulnerability_id.p + len);
+    items[i] = it;
+  }
+  std::vector<uint4> dec;
+  std::string msg;
+  if (!e->fill->run_host(items, arena, dec, msg)) {
+    set_err(err, errlen, msg);
+    return TVM_EDEVICE;
+  }
+  auto* priv = new FillPriv();
+  priv->items.resize(n);
+  auto keep = [&](std::string s) -> const char* {
+    priv->strs.push_back(std::move(s));
+    return priv->strs.back().c_str();
+  };
+  for (size_t i = 0; i < n; i++) {
+    const tvm_fill_in& x = in[i];
+    const uint4 d = dec[i];
+    tvm_fill_out& o = priv->items[i];
+    o.status = int32_t(d.y);
+    if (!x.has_fixed_version && x.status != 0 && (x.status & ~0xFF)) o.status = x.status;  // beyond the 8-bit item field
+    o.severity = o.severity_source = o.primary_url = "";
+    o.vulnerability_json = nullptr;
+    o.found = d.x != FILL_NOT_FOUND && x.vulnerability_id.n <= 0xFFFF;
+    if (!o.found) continue;
+    const uint32_t code = d.z & 0xFFFFu, ssrc = d.z >> 16;
+    std::string_view extra_src;
+    int64_t extra_val = 0;
+    if (code == SEV_KEEP) {  // the detector's package-specific severity (vulnerability.go:90-101)
+      const std::string_view sev(x.severity.p ? x.severity.p : "", x.severity.n);
+      extra_src = std::string_view(x.severity_source.p, x.severity_source.n);
+      extra_val = fill_new_severity(sev);
+      o.severity = keep(std::string(sev));
+      o.severity_source = keep(std::string(extra_src));
+    } else {
+      o.severity = vt.severity_string(d.x, code).c_str();
+      o.severity_source = ssrc == SRC_NONE ? "" : vt.source_name(ssrc).c_str();
+    }
+    o.primary_url = keep(vt.primary_url(d.x, d.w));
+    o.vulnerability_json = keep(vt.vulnerability_json(d.x, o.severity, extra_src, extra_val));
+  }
+  out->items = priv->items.data();
+  out->n = n;
+  out->priv = priv;
+  return TVM_OK;
+}
+
+void tvm_fill_result_free(tvm_fill_result* r) {
+  if (!r) return;
+  delete static_cast<FillPriv*>(r->priv);
+  *r = tvm_fill_result{nullptr, 0, nullptr};
+}
+
+int tvm_match_fill(tvm_engine* e, tvm_batch* b, char* err, size_t errlen) {
+  if (!e || !b || !b->uploaded) return TVM_EINVAL;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  (void)hipSetDevice(e->device);
+  if (b->fill_cap < b->m.cap) {
+    if (b->fill_out) (void)hipFree(b->fill_out);
+    b->fill_out = nullptr;
+    b->fill_cap = 0;
+    if (hipMalloc(&b->fill_out, std::max<uint64_t>(b->m.cap, 1) * sizeof(uint4)) != hipSuccess) {
+      set_err(err, errlen, "hipMalloc(fill decisions) failed");
+      return TVM_EDEVICE;
+    }
+    b->fill_cap = b->m.cap;
+  }
+  std::string msg;
+  if (!e->fill->launch_pairs(b->m.pairs, b->m.ctl, b->m.cap, b->fill_out, e->eng->stream(), msg)) {
+    set_err(err, errlen, msg);
+    return TVM_EDEVICE;
+  }
+  return TVM_OK;
+}
+
+int tvm_match_fill_fetch(tvm_engine* e, tvm_batch* b, uint32_t* out4, uint64_t cap, uint64_t* n_out) {
+  if (!e || !b || !b->uploaded) return TVM_EINVAL;
+  (void)hipSetDevice(e->device);
+  if (hipStreamSynchronize(e->eng->stream()) != hipSuccess) return TVM_EDEVICE;
+  uint64_t n = 0;
+  int rc = tvm_match_status(e, b, &n, nullptr, nullptr);
+  if (rc) return rc;
+  if (n_out) *n_out = 0;
+  if (n > b->m.cap || n > b->fill_cap) return TVM_EINVAL;
+  unsigned long long ctl[8];
+  if (hipMemcpy(ctl, b->m.ctl, sizeof(ctl), hipMemcpyDeviceToHost) != hipSuccess) return TVM_EDEVICE;
+  const uint32_t tile = ctl[5] ? uint32_t(ctl[5]) : 256;
+  const uint32_t n_tiles = (b->dev.n + tile - 1) / tile;
+  std::vector<TileDir> dir(n_tiles);
+  std::vector<uint4> raw(n);
+  if ((n_tiles && hipMemcpy(dir.data(), b->m.dir, n_tiles * sizeof(TileDir), hipMemcpyDeviceToHost) != hipSuccess) ||
+      (n && hipMemcpy(raw.data(), b->fill_out, n * sizeof(uint4), hipMemcpyDeviceToHost) != hipSuccess))
+    return TVM_EDEVICE;
+  uint64_t k = 0;
+  for (const TileDir& d : dir)  // tile order = tvm_match_fetch's (package, advisory) order
+    for (uint64_t i = d.base; i < d.base + d.count && k < cap; i++, k++)
+      memcpy(out4 + 4 * k, &raw[i], sizeof(uint4));
+  if (n_out) *n_out = k;
+  return TVM_OK;
+}
+
+int tvm_match_fill_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err, size_t errlen) {
+  if (!e || !b || !b->uploaded || steps <= 0 || !ms) return TVM_EINVAL;
+  int rc = tvm_match_fill(e, b, err, errlen);  // sizes the decision buffer
+  if (rc) return rc;
+  (void)hipSetDevice(e->device);
+  hipStream_t st = e->eng->stream();
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+  std::string msg;
+  float f = 0;
+  bool ok = hipEventCreate(&t0) == hipSuccess && hipEventCreate(&t1) == hipSuccess && hipEventRecord(t0, st) == hipSuccess;
+  for (int i = 0; ok && i < steps; i++) ok = e->fill->launch_pairs(b->m.pairs, b->m.ctl, b->m.cap, b->fill_out, st, msg);
+  ok = ok && hipEventRecord(t1, st) == hipSuccess && hipEventSynchronize(t1) == hipSuccess &&
+       hipEventElapsedTime(&f, t0, t1) == hipSuccess;
+  if (t0) (void)hipEventDestroy(t0);
+  if (t1) (void)hipEventDestroy(t1);
+  if (!ok) {
+    set_err(err, errlen, msg.empty() ? "hipEvent timing failed" : msg);
+    return TVM_EDEVICE;
+  }
+  *ms = f;
+  return TVM_OK;
+}
+
+uint64_t tvm_match_fill_algorithmic_bytes(tvm_engine* e, tvm_batch* b) {
+  uint64_t n = 0;
+  if (!e || !b || tvm_match_status(e, b, &n, nullptr, nullptr) || n > b->m.cap) return 0;
+  std::vector<uint2> raw(n);
+  (void)hipSetDevice(e->device);
+  if (n && hipMemcpy(raw.data(), b->m.pairs, n * sizeof(uint2), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  return e->fill->pair_bytes(raw);
+}
+
+const char* tvm_fill_source_name(tvm_engine* e, uint32_t id) {
+  if (!e || id == SRC_NONE) return "";
+  const VulnTable& vt = e->fill->table();
+  return id < 0x7FFF ? vt.source_name(id).c_str() : "";
+}

@@ -5,6 +5,7 @@
 // (which DetectedVulnerability fields are set, Red Hat's per-CVE merge).  The
 // per-(package, advisory) loop runs in one GPU launch per call (Engine::match_host).
 #include "drivers.h"
+#include "vulninfo.h"
 
 #include <algorithm>
 #include <cstdio>
@@ -658,6 +659,42 @@ DetectStatus library_detect(Engine& eng, std::string_view lib_type, const std::v
 DetectStatus library_detect_vulnerabilities(Engine& eng, std::string_view lib_type, const std::vector<Pkg>& pkgs,
                                             std::vector<Vuln>& out, std::string& err) {
   return library_run(eng, lib_type, pkgs, false, out, err);
+}
+
+// FillInfo inputs of one detector output (vulninfo.h): the fields the epilogues above
+// copy from advisory a for a driver of family drv (Status/SeveritySource for debian
+// (debian.go:89-98) and Red Hat (redhat.go:160-161); no DataSource for Red Hat; rpm
+// String() FixedVersion for Red Hat, Alma, Rocky and CBL-Mariner; createFixedVersions
+// for library drivers).  The batch path uses it per (package, advisory) pair.
+void detector_fill_fields(uint8_t drv, const Advisory& a, DetFill& f) {
+  f = DetFill();
+  f.data_source = drv == DRV_REDHAT ? -1 : a.data_source;
+  switch (drv) {
+    case DRV_DEBIAN:
+      f.status = a.status;
+      f.fixed = !a.fixed.empty();
+      if (a.severity != 0) {
+        f.severity_source = "debian";
+        f.severity = severity_name(a.severity);
+      }
+      break;
+    case DRV_REDHAT:
+      f.status = a.status;
+      f.fixed = !a.fixed.empty() && !rpm_string(a.fixed).empty();
+      f.severity_source = "redhat";
+      f.severity = severity_name(a.severity);
+      break;
+    case DRV_ALMA:
+    case DRV_ROCKY:
+    case DRV_MARINER:
+      f.fixed = !a.fixed.empty() && !rpm_string(a.fixed).empty();
+      break;
+    case DRV_LIBRARY:
+      f.fixed = !a.lib_fixed.empty();
+      break;
+    default:
+      f.fixed = !a.fixed.empty();
+  }
 }
 
 }  // namespace tvm

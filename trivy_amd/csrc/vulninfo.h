@@ -1,0 +1,161 @@
+// Vulnerability-detail join (FillInfo) on the GPU: load-time tables + kernel interface.
+//
+// Replaces the per-match work of the reference's pkg/vulnerability/vulnerability.go:
+//   :60-109   Client.FillInfo   - status rule, trivy-db GetVulnerability(vulnID) (a bbolt
+//                                 lookup + JSON decode per detected vulnerability), the
+//                                 detector's package-specific severity override
+//   :111-134  getVendorSeverity - data source -> GHSA (for GHSA- IDs) -> NVD -> DB severity
+//   :136-157  getPrimaryURL     - ID-prefix URLs, else the first reference matching the
+//                                 data source's prefixes (:15-39)
+//
+// At load time bucket "vulnerability" is decoded once (json.Unmarshal into trivy-db
+// types.Vulnerability semantics) into a hash index on the vulnerability ID, one 16-B
+// record per vulnerability and a small entry list per vulnerability holding its
+// VendorSeverity pairs and, for IDs without a URL prefix rule, the reference index the
+// primary-URL rule picks for each data source that has prefixes.  The kernel then does,
+// per detected vulnerability, one hash probe + record + entry scan and writes a 16-B
+// decision; strings (detail JSON, URLs) are rebuilt on the host from the decision.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+namespace tvm {
+
+class DB;
+struct Advisory;
+
+// Decision codes written by the kernel.
+enum : uint32_t {
+  FILL_NOT_FOUND = 0xFFFFFFFFu,  // out.x: GetVulnerability failed (missing key or decode error)
+  SEV_KEEP = 0xFFFDu,            // severity = the detector's (package-specific) severity
+  SEV_RAW = 0xFFFEu,             // severity = the DB's Vulnerability.Severity string verbatim
+  SEV_OOR = 0xFFFFu,             // a VendorSeverity value outside SeverityNames (reported as UNKNOWN)
+  SRC_NONE = 0xFFFFu,            // severity source ""
+  URL_NONE = 0, URL_CVE = 1, URL_RUSTSEC = 2, URL_GHSA = 3, URL_TEMP = 4, URL_REF = 5,
+  URL_KIND_SHIFT = 28, URL_REF_MASK = 0x0FFFFFFFu,
+  // item flags (FillItem.z bits 8..15)
+  FI_FIXED = 1u << 8,            // FixedVersion != ""
+  FI_SEV_SRC = 1u << 9,          // the detector set SeveritySource
+  // entry word: kind (bit 31) | source id (bits 16..30) | value (bits 0..15)
+  ENT_URL = 1u << 31,
+};
+
+// Per-item input (16 B): x = vuln-ID offset into the item arena, y = ID length | source
+// id << 16, z = status | FI_* flags, w = resolved vulnerability record or FILL_NOT_FOUND
+// (batch path; the drop-in path probes and ignores w).
+// Per-item output (16 B): x = record index or FILL_NOT_FOUND, y = status,
+// z = severity code (0..4 = SeverityNames, SEV_*) | severity source id << 16,
+// w = URL kind << 28 | reference index.
+// Record (16 B): x = first entry, y = entry count, z = DB severity code (0..4 or
+// SEV_RAW), w = REC_BAD | ID-prefix URL kind << REC_URL_SHIFT.
+enum : uint32_t { REC_BAD = 1, REC_URL_SHIFT = 4 };
+
+// Host view of one decoded vulnerability (trivy-db types.Vulnerability).
+struct VulnDetail {
+  std::string id;
+  std::string severity;                                  // Vulnerability.Severity
+  std::vector<std::pair<std::string, int64_t>> vendor;   // VendorSeverity, key order
+  std::vector<std::string> refs;                         // References
+  std::string detail_json;                               // canonical JSON of the whole record
+  bool bad = false;                                      // GetVulnerability would fail
+};
+
+class VulnTable {
+ public:
+  // Decodes bucket "vulnerability" of the DB's tree and builds the device images.
+  void build(const DB& db);
+  bool built() const { return built_; }
+
+  // Source-ID dictionary (VendorSeverity keys, primary-URL sources, data sources).
+  uint32_t source_id(std::string_view s) const;  // SRC_NONE when unknown
+  const std::string& source_name(uint32_t id) const {
+    static const std::string none;
+    return id < src_names_.size() ? src_names_[id] : none;
+  }
+  uint32_t ghsa_id() const { return ghsa_; }
+  uint32_t nvd_id() const { return nvd_; }
+  int32_t find(std::string_view vuln_id) const;  // host lookup, -1 when absent
+
+  // Host rebuild of the strings behind a kernel decision (record rec):
+  //   the Vulnerability JSON with Severity = severity and VendorSeverity plus, when
+  //   extra_src is non-empty, VendorSeverity[extra_src] = extra_val (vulnerability.go:95-101);
+  std::string vulnerability_json(uint32_t rec, std::string_view severity, std::string_view extra_src,
+                                 int64_t extra_val) const;
+  //   PrimaryURL from the URL word (kind << 28 | reference index) and the vulnerability ID.
+  std::string primary_url(uint32_t rec, uint32_t url_word) const;
+  //   Severity string of a severity code (0..4, SEV_RAW, SEV_OOR; SEV_KEEP is the caller's).
+  const std::string& severity_string(uint32_t rec, uint32_t code) const;
+
+  std::vector<VulnDetail> vulns;
+
+  // ---- device images ----
+  std::vector<uint64_t> slot_hash;   // 0 = empty; key_hash(kVulnSeed, id)
+  std::vector<uint4> slot_val;       // {id_off, id_len, record, 0}
+  std::vector<uint8_t> id_arena;     // 8-B aligned IDs, zero padded (+4 zero words)
+  std::vector<uint4> recs;           // {entry_off, entry_n, db severity code, REC_BAD | url kind}
+  std::vector<uint32_t> ents;        // ENT_* words
+  uint64_t slot_mask = 0;
+
+  // Batch path: per advisory of the DB, the FillInfo input its detector output carries
+  // (uint4 as the item layout, x/y unused: record in w, source in y >> 16).
+  std::vector<uint4> adv_items;
+
+ private:
+  bool built_ = false;
+  std::unordered_map<std::string, uint32_t> src_ids_;
+  std::vector<std::string> src_names_;
+  std::unordered_map<std::string_view, int32_t> by_id_;
+  uint32_t ghsa_ = SRC_NONE, nvd_ = SRC_NONE;
+  uint32_t intern_source(const std::string& s);
+};
+
+constexpr uint32_t kVulnSeed = 0x7F11A0u;  // key_hash seed of the vulnerability-ID index
+
+// The FillInfo inputs a detector's output for (package, advisory a of a platform of
+// driver family drv) carries (drivers.cpp; the fields each driver's Detect copies).
+struct DetFill {
+  int32_t data_source = -1;       // index into DB::sources, -1 = nil
+  int64_t status = 0;
+  bool fixed = false;             // FixedVersion != ""
+  const char* severity_source = nullptr;
+  const char* severity = nullptr;
+};
+void detector_fill_fields(uint8_t drv, const Advisory& a, DetFill& f);
+
+// Severity names (trivy-db SeverityNames) and NewSeverity.
+const char* fill_severity_name(int64_t s);
+int64_t fill_new_severity(std::string_view s);
+
+// Device side (fill.hip).
+struct FillDev;
+class FillEngine {
+ public:
+  ~FillEngine();
+  static FillEngine* open(const VulnTable& t, int device, std::string& err);
+  // Drop-in path: items (vuln IDs in `arena`) -> decisions, host in / host out.
+  bool run_host(const std::vector<uint4>& items, const std::vector<uint8_t>& arena, std::vector<uint4>& out,
+                std::string& err);
+  // Batch path: decisions for the device match pairs {pkg, adv} (resolved records), on
+  // `stream`; the pair count is read from n_dev on the device (at most cap pairs).
+  bool launch_pairs(const uint2* pairs, const unsigned long long* n_dev, uint64_t cap, uint4* out, hipStream_t stream,
+                    std::string& err);
+  uint64_t table_bytes() const { return table_bytes_; }
+  const VulnTable& table() const { return *t_; }
+  // Algorithmic HBM bytes of one batch-path launch over these pairs (host copy).
+  uint64_t pair_bytes(const std::vector<uint2>& pairs) const;
+
+ private:
+  int dev_ = 0;
+  const VulnTable* t_ = nullptr;
+  FillDev* d_ = nullptr;
+  std::vector<void*> allocs_;
+  uint64_t table_bytes_ = 0;
+  hipStream_t stream_ = nullptr;
+};
+
+}  // namespace tvm
