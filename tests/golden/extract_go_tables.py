@@ -43,6 +43,7 @@ FILES = [
     "pkg/detector/library/compare/rubygems/compare_test.go",
     "pkg/scanner/utils/utils_test.go",
     "pkg/vulnerability/vulnerability_test.go",
+    "pkg/result/filter_test.go",
 ]
 
 # trivy-db / trivy constants used in the tables (values from trivy-db pkg/types and
@@ -81,6 +82,20 @@ FTYPES = {
 }
 for k, v in FTYPES.items():
     CONST["ftypes." + k] = v
+# github.com/package-url/packageurl-go type constants
+for k in ("Golang", "Npm", "Maven", "PyPi", "Apk", "Rpm", "Deb", "Gem", "Cargo", "Composer", "Nuget", "Conan",
+          "Cocoapods", "Hex", "Pub", "Swift", "Bitnami", "Conda", "Docker", "OCI", "Generic"):
+    CONST["packageurl.Type" + k] = k.lower()
+CONST["types.ClassLangPkg"] = "lang-pkgs"
+CONST["types.ClassOSPkg"] = "os-pkgs"
+CONST["types.ClassConfig"] = "config"
+CONST["types.ClassSecret"] = "secret"
+CONST["types.ClassLicense"] = "license"
+CONST["types.ClassLicenseFile"] = "license-file"
+CONST["types.FindingStatusIgnored"] = "ignored"
+CONST["types.FindingStatusNotAffected"] = "not_affected"
+CONST["types.FindingStatusFixed"] = "fixed"
+CONST["types.FindingStatusUnderInvestigation"] = "under_investigation"
 CONST["suse.OpenSUSE"] = "opensuse"                 # suse.go Type enum (iota)
 CONST["suse.SUSEEnterpriseLinux"] = "sles"
 
@@ -356,6 +371,31 @@ def call(name, args):
     return {"__call__": name, "args": args}
 
 
+def _subst(v, env):
+    """Replaces {"__ident__": name} references to the test's local `var (...)` values."""
+    if isinstance(v, dict):
+        if set(v) == {"__ident__"} and v["__ident__"] in env:
+            return env[v["__ident__"]]
+        return {k: _subst(x, env) for k, x in v.items()}
+    if isinstance(v, list):
+        return [_subst(x, env) for x in v]
+    return v
+
+
+def _local_vars(toks, start, end):
+    """name -> value of every `var ( name = value ... )` block in toks[start:end]."""
+    env = {}
+    for k in range(start, end):
+        if toks[k].v == "var" and toks[k + 1].v == "(":
+            p = Parser(toks)
+            p.i = k + 2
+            while p.peek().v != ")":
+                name = p.next().v
+                p.expect("=")
+                env[name] = _subst(p.value(), env)
+    return env
+
+
 def extract(path):
     src = open(path, encoding="utf-8").read()
     toks = tokenize(src)
@@ -365,15 +405,16 @@ def extract(path):
     while i < len(toks):
         t = toks[i]
         if t.k == "id" and t.v == "tests" and i + 1 < len(toks) and toks[i + 1].v == ":=":
-            fn = None
+            fn, fstart = None, 0
             for j in range(i, 0, -1):
                 if toks[j].v == "func" and toks[j + 1].k == "id" and toks[j + 1].v.startswith("Test"):
-                    fn = toks[j + 1].v
+                    fn, fstart = toks[j + 1].v, j
                     break
+            env = _local_vars(toks, fstart, i)
             p = Parser(toks)
             p.i = i + 2
             typ = p.parse_type()
-            body = p.composite(typ)
+            body = _subst(p.composite(typ), env)
             if isinstance(body, dict):  # map[string]struct: name -> case
                 body = [dict(v, name=k) if isinstance(v, dict) else {"name": k, "value": v} for k, v in body.items()]
             tables.append({"func": fn, "cases": body})
