@@ -60,8 +60,8 @@ struct alignas(16) Row {
   uint32_t adv;      // global advisory index (host-side record)
   uint16_t lo_len;   // bytes | flags
   uint16_t hi_len;
-  uint64_t hi_pre0;  // first 16 bytes of the hi key inline (memory-order words, zero padded):
-  uint64_t hi_pre1;  // most compares finish here without touching the key arena
+  uint64_t hi_pre0;  // first 16 bytes of the hi key inline as BIG-ENDIAN words, zero padded, so a
+  uint64_t hi_pre1;  // compare is two u64 compares; most finish here without the key arena
 };
 enum : uint16_t {
   KEY_LEN_MASK = 0x3FFF,

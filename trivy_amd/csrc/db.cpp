@@ -553,7 +553,7 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
         off = intern_key(kb);
         len = uint16_t(std::min<size_t>(kb.size(), KEY_LEN_MASK) | (b.incl ? KEY_INCL : 0));
         if (hi)
-          for (size_t i = 0; i < kb.size() && i < 16; i++) (i < 8 ? r.hi_pre0 : r.hi_pre1) |= uint64_t(kb[i]) << (8 * (i % 8));
+          for (size_t i = 0; i < kb.size() && i < 16; i++) (i < 8 ? r.hi_pre0 : r.hi_pre1) |= uint64_t(kb[i]) << (8 * (7 - i % 8));  // big-endian
       };
       put(v.lo, r.lo_off, r.lo_len, false);
       put(v.hi, r.hi_off, r.hi_len, true);
@@ -583,7 +583,7 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
   };
   auto set_hi = [&](const std::string& v) {
     if (!encode(v, r.hi_off, r.hi_len)) return false;
-    for (size_t i = 0; i < kb.size() && i < 16; i++) (i < 8 ? r.hi_pre0 : r.hi_pre1) |= uint64_t(kb[i]) << (8 * (i % 8));
+    for (size_t i = 0; i < kb.size() && i < 16; i++) (i < 8 ? r.hi_pre0 : r.hi_pre1) |= uint64_t(kb[i]) << (8 * (7 - i % 8));  // big-endian
     return true;
   };
   RowAux x{};

@@ -60,7 +60,10 @@ namespace {
 
 enum : uint32_t { KI_VALID = 1u << 31, KI_SPILL = 1u << 30, KI_LEN = 0x3FFFu, KI_CLS_SHIFT = 26, KI_CLS_MASK = 7u };
 
-template <int T, int KW, int MB, bool KG>
+// FILT: the batch's grammar set has rows with per-package predicates (RowAux); dpkg-only
+// batches (GM_DEB) never do, so their tiles carry no package attributes (2 KB less LDS per
+// block = one more resident workgroup per CU).
+template <int T, int KW, int MB, bool KG, bool FILT>
 struct TileShared {
   uint64_t key[KG ? 1 : T * KW];  // installed keys (KG: in global memory instead)
   union {
@@ -71,7 +74,7 @@ struct TileShared {
   uint32_t rbeg[T];           // first row per package
   uint32_t kinfo[T];          // key length | flags
   uint32_t koff[T];           // spill word offset when KI_SPILL
-  uint2 pattr[T];             // package attributes (filtered rows only)
+  uint2 pattr[FILT ? T : 1];  // package attributes (filtered rows only)
   uint32_t wsum[T / 64];
   uint32_t tile;
   uint32_t span_lo, span_hi;  // arena window of the tile's strings
@@ -183,6 +186,29 @@ __device__ __forceinline__ bool aux_pass(const MatchArgs& a, uint32_t ridx, uint
   return true;
 }
 
+// The installed key's first two words are kept big-endian and zero-masked beyond the key
+// length (be_head, applied once per package in phase 1), like Row::hi_pre*, so an interval
+// bound test is two u64 compares; only 16-byte ties with both keys longer read the tails
+// (memory-order words from word 2 on).
+__device__ __forceinline__ uint64_t be_word(uint64_t w, uint32_t bytes) {  // bytes in [1, 8]
+  if (bytes < 8) w &= (1ull << (8 * bytes)) - 1ull;
+  return __builtin_bswap64(w);
+}
+__device__ __forceinline__ void be_head(uint64_t* k, uint32_t n) {
+  const uint64_t w0 = n ? be_word(k[0], n < 8 ? n : 8) : 0ull;
+  const uint64_t w1 = n > 8 ? be_word(k[1], n < 16 ? n - 8 : 8) : 0ull;
+  k[0] = w0;
+  k[1] = w1;
+}
+// sign(installed key - bound): a0/a1 the installed BE head, b0/b1 the bound's BE head.
+__device__ __forceinline__ int cmp_be(uint64_t a0, uint64_t a1, const uint64_t* a, uint32_t na, uint64_t b0,
+                                      uint64_t b1, const uint64_t* b, uint32_t nb) {
+  if (a0 != b0) return a0 < b0 ? -1 : 1;
+  if (a1 != b1) return a1 < b1 ? -1 : 1;
+  if (na <= 16 || nb <= 16) return (na > nb) - (na < nb);
+  return key_cmp(a + 2, na - 16, b + 2, nb - 16);
+}
+
 // Installed key of tile package q: the global spill area for long keys, else its slot
 // (LDS, or global memory for KG variants).
 template <int T, int KW, bool KG, class S>
@@ -194,22 +220,28 @@ __device__ __forceinline__ const uint64_t* key_ptr(const MatchArgs& a, const S& 
 
 // Interval test of package q's installed key (k; first two words k0, k1 already loaded)
 // against one row (global index ridx).
-template <class S>
+template <bool FILT, class S>
 __device__ __forceinline__ bool eval_row(const MatchArgs& a, const S& s, uint32_t q, const Row& row, uint32_t ridx,
                                          const uint64_t* k, uint64_t k0, uint64_t k1) {
-  if ((row.adv & ROW_FILTER) && !aux_pass(a, ridx, s.pattr[q], s.kinfo[q])) return false;
+  if constexpr (FILT) {
+    if ((row.adv & ROW_FILTER) && !aux_pass(a, ridx, s.pattr[q], s.kinfo[q])) return false;
+  }
   if (row.adv & ROW_ALWAYS) return true;
   const uint32_t ki = s.kinfo[q];
   if (!(ki & KI_VALID)) return false;
   const uint32_t kl = ki & KI_LEN;
   bool m = true;
   if (!(row.hi_len & KEY_INF)) {
-    const int c = key_cmp_pre2(k0, k1, k, kl, row.hi_pre0, row.hi_pre1, a.db.key_words + row.hi_off,
-                               row.hi_len & KEY_LEN_MASK);
+    const int c = cmp_be(k0, k1, k, kl, row.hi_pre0, row.hi_pre1, a.db.key_words + row.hi_off,
+                         row.hi_len & KEY_LEN_MASK);
     m = (row.hi_len & KEY_INCL) ? c <= 0 : c < 0;
   }
-  if (m && !(row.lo_len & KEY_INF)) {
-    const int c = key_cmp(k, kl, a.db.key_words + row.lo_off, row.lo_len & KEY_LEN_MASK);
+  if (m && !(row.lo_len & KEY_INF)) {  // rare (library / rpm ranges): the bound's head from the arena
+    const uint64_t* lw = a.db.key_words + row.lo_off;
+    const uint32_t nl = row.lo_len & KEY_LEN_MASK;
+    const uint64_t l0 = nl ? be_word(lw[0], nl < 8 ? nl : 8) : 0ull;
+    const uint64_t l1 = nl > 8 ? be_word(lw[1], nl < 16 ? nl - 8 : 8) : 0ull;
+    const int c = cmp_be(k0, k1, k, kl, l0, l1, lw, nl);
     m = (row.lo_len & KEY_INCL) ? c >= 0 : c > 0;
   }
   return m;
@@ -218,8 +250,8 @@ __device__ __forceinline__ bool eval_row(const MatchArgs& a, const S& s, uint32_
 // One sweep over the tile's pairs.  DIRECT=false: compact into LDS (count all, store the
 // first MB).  DIRECT=true: store straight to out[base + position].
 // AB (ablation, diagnostics only): 2 = load rows but skip the key compare.
-template <int T, int KW, int MB, bool KG, bool DIRECT, int AB = 0>
-__device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared<T, KW, MB, KG>& s, uint32_t total_pairs,
+template <int T, int KW, int MB, bool KG, bool FILT, bool DIRECT, int AB = 0>
+__device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared<T, KW, MB, KG, FILT>& s, uint32_t total_pairs,
                                           uint32_t tid, unsigned long long base) {
   constexpr int W = T / 64;
   const uint32_t lane = tid & 63, wave = tid >> 6;
@@ -253,7 +285,7 @@ __device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared<T, KW, 
       if (s.kinfo[q] & KI_SPILL) k0 = kp[0], k1 = kp[1];
       else k0 = s.key[q * KW], k1 = s.key[q * KW + 1];  // LDS loads, not flat ones
     }
-    const bool m = (j < total_pairs) && (AB == 2 ? (row.adv & 7u) == 0 : eval_row(a, s, q, row, ridx, kp, k0, k1));
+    const bool m = (j < total_pairs) && (AB == 2 ? (row.adv & 7u) == 0 : eval_row<FILT>(a, s, q, row, ridx, kp, k0, k1));
     const unsigned long long bal = __ballot(m);
     const uint32_t lane_off = __popcll(bal & ((1ull << lane) - 1ull));
     if (lane == 0) s.wsum[wave] = uint32_t(__popcll(bal));
@@ -290,8 +322,8 @@ __device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared<T, KW, 
 // Phase 1 for one package: encode the installed version into its key slot and probe the
 // index.  Instantiated separately for LDS-staged and global string pointers so the staged
 // case compiles to LDS loads rather than generic (flat) ones.
-template <int T, int KW, int MB, bool KG, uint32_t GM, int AB>
-__device__ __forceinline__ void probe_encode(const MatchArgs& a, TileShared<T, KW, MB, KG>& s, uint32_t tid,
+template <int T, int KW, int MB, bool KG, bool FILT, uint32_t GM, int AB>
+__device__ __forceinline__ void probe_encode(const MatchArgs& a, TileShared<T, KW, MB, KG, FILT>& s, uint32_t tid,
                                              uint32_t p, const uint4 d, const uint8_t* name, const uint8_t* ver,
                                              uint32_t& cnt, uint32_t& rbeg, uint32_t& kinfo, uint32_t& koff) {
   const PlatInfo pi = a.db.plats[d.x];
@@ -323,6 +355,7 @@ __device__ __forceinline__ void probe_encode(const MatchArgs& a, TileShared<T, K
       }
     }
     kinfo |= (cs.n & KI_LEN) | (valid ? KI_VALID : 0u) | ((cls & KI_CLS_MASK) << KI_CLS_SHIFT);
+    if (valid) be_head((kinfo & KI_SPILL) ? a.spill + koff : slot, cs.n);
   }
   // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup
   if (AB != 3 && (valid || (pi.flags & PLAT_LOOKUP_FIRST))) {
@@ -349,7 +382,8 @@ __device__ __forceinline__ void probe_encode(const MatchArgs& a, TileShared<T, K
 // 2 = no key compare, 3 = stage+encode+scan (no probe), 4 = stage+probe+scan (no encode).  Ablation variants produce wrong match lists by construction.
 template <int T, int KW, int MB, bool KG, uint32_t GM, int AB = 0>
 __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
-  __shared__ TileShared<T, KW, MB, KG> s;
+  constexpr bool FILT = GM != GM_DEB;
+  __shared__ TileShared<T, KW, MB, KG, FILT> s;
   constexpr uint32_t kStageBytes = MB * 8;
   const uint32_t tid = threadIdx.x;
   if (tid == 0) {
@@ -400,21 +434,21 @@ __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
   uint32_t cnt = 0, rbeg = 0, kinfo = 0, koff = 0;
   if (p < a.n && d.x < a.db.n_plats) {
     if (staged)
-      probe_encode<T, KW, MB, KG, GM, AB>(a, s, tid, p, d, stage_bytes + (d.y - base16), stage_bytes + (d.z - base16),
+      probe_encode<T, KW, MB, KG, FILT, GM, AB>(a, s, tid, p, d, stage_bytes + (d.y - base16), stage_bytes + (d.z - base16),
                                           cnt, rbeg, kinfo, koff);
     else
-      probe_encode<T, KW, MB, KG, GM, AB>(a, s, tid, p, d, a.arena + d.y, a.arena + d.z, cnt, rbeg, kinfo, koff);
+      probe_encode<T, KW, MB, KG, FILT, GM, AB>(a, s, tid, p, d, a.arena + d.y, a.arena + d.z, cnt, rbeg, kinfo, koff);
   }
   s.rbeg[tid] = rbeg;
   s.kinfo[tid] = kinfo;
   s.koff[tid] = koff;
-  s.pattr[tid] = (a.attr && p < a.n) ? a.attr[p] : make_uint2(PA_ARCH_NONE, 0xFFFFFFFFu);
+  if constexpr (FILT) s.pattr[tid] = (a.attr && p < a.n) ? a.attr[p] : make_uint2(PA_ARCH_NONE, 0xFFFFFFFFu);
 
   // ---- 2. scan of row counts ------------------------------------------------------------
   const uint32_t total_pairs = block_scan<T>(s, cnt, tid);
 
   // ---- 3+4. pair sweep with LDS compaction -----------------------------------------------
-  const uint32_t nm = (AB == 1 || AB >= 3) ? (total_pairs & 1u) : sweep<T, KW, MB, KG, false, AB>(a, s, total_pairs, tid, 0);
+  const uint32_t nm = (AB == 1 || AB >= 3) ? (total_pairs & 1u) : sweep<T, KW, MB, KG, FILT, false, AB>(a, s, total_pairs, tid, 0);
 
   // ---- reserve the tile's output segment (one atomic per tile, no inter-tile waiting) -----
   if (tid == 0) {
@@ -434,7 +468,7 @@ __global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
     for (uint32_t i = tid; i < nm; i += T)
       if (base + i < a.out_cap) a.out[base + i] = s.mbuf[i];
   } else {
-    sweep<T, KW, MB, KG, true, AB>(a, s, total_pairs, tid, base);  // rare: more matches than the LDS buffer
+    sweep<T, KW, MB, KG, FILT, true, AB>(a, s, total_pairs, tid, base);  // rare: more matches than the LDS buffer
   }
 }
 
