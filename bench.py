@@ -277,6 +277,13 @@ def main():
         fill = {"kernel_ms": fill_ms, "matches_per_s": total / (fill_ms / 1e3),
                 "algorithmic_bytes_per_launch": fill_bytes, "achieved_GBs": fill_gbs,
                 "frac": fill_gbs / HBM_PEAK_GBS, "db_vulnerabilities": len(wl.sdb.vuln_ids())}
+        # result.Filter (filter.go:60-139) behind FillInfo: default options (every severity),
+        # per result dedup + BySeverity order; wall time per call incl. its one sync
+        mb.fill()
+        fopts = mb.filter_opts()
+        kept = mb.filter(fopts)
+        filt_ms = mb.filter_time(fopts, max(3, args.steps // 4))
+        fill["result_filter"] = {"ms": filt_ms, "kept": kept, "matches_per_s": total / (filt_ms / 1e3)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -19,6 +19,9 @@
  *   tvm_fill_info              vulnerability.Client.FillInfo  pkg/vulnerability/vulnerability.go:60-109
  *                              (with getVendorSeverity :111-134 and getPrimaryURL :136-157)
  *   tvm_match_fill*            (new) FillInfo fused behind a batch's device-resident match list
+ *   tvm_match_filter*          result.FilterResult's vulnerability part (pkg/result/filter.go:60-139:
+ *                              severity / status / ignore-file IDs, dedup, BySeverity order) per
+ *                              result of a batch
  *
  * Error convention: functions return 0 on success and a non-zero TVM_E* code on failure,
  * with a NUL-terminated message written to (err, errlen).  Messages carry the same text
@@ -276,6 +279,25 @@ int tvm_match_fill_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char
 uint64_t tvm_match_fill_algorithmic_bytes(tvm_engine* e, tvm_batch* b);
 /* Name of a severity-source id from tvm_match_fill_fetch ("" for 0xFFFF / unknown). */
 const char* tvm_fill_source_name(tvm_engine* e, uint32_t id);
+
+/* ---- result.Filter over a batch -------------------------------------------------------- */
+/* One tvm_batch_add* call = one Result; its packages' (name, version) are the
+ * DetectedVulnerability PkgName / InstalledVersion, PkgPath is empty. */
+typedef struct {
+  uint32_t severity_mask;        /* bit i: SeverityNames[i] is in FilterOption.Severities */
+  uint32_t ignore_status_mask;   /* bit s: dbTypes.Status s is in FilterOption.IgnoreStatuses */
+  const tvm_str* ignore_ids;     /* IDs of the ignore file's unexpired findings without paths/PURLs */
+  size_t n_ignore_ids;
+} tvm_filter_opts;
+/* filterVulnerabilities + sort.Sort(BySeverity) for every result of the batch, on the GPU,
+ * after tvm_match_launch + tvm_match_fill.  n_kept = surviving vulnerabilities. */
+int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint64_t* n_kept, char* err, size_t errlen);
+/* The surviving {package, advisory} pairs (uint32 x2) in report order: results in add
+ * order, each in BySeverity order. */
+int tvm_match_filter_fetch(tvm_engine* e, tvm_batch* b, uint32_t* pairs, uint64_t cap, uint64_t* n_out);
+/* Wall time of `steps` tvm_match_filter calls (ms total; each call synchronises once). */
+int tvm_match_filter_time(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, int steps, double* ms, char* err,
+                          size_t errlen);
 
 #ifdef __cplusplus
 }

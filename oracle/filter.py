@@ -25,7 +25,7 @@ and third-party semantics (absent here; pinned versions from reference go.mod):
 Pinned by TestFilter (pkg/result/filter_test.go:19-1040, transcribed to
 tests/golden/tables/result__filter_test.json) - the vulnerability parts of its cases -
 with the reference's own ignore files (pkg/result/testdata/.trivyignore{,.yaml}, copied as
-data to tests/golden/fixtures/result/).
+data to tests/golden/result_files/).
 """
 import datetime
 import re

@@ -161,3 +161,96 @@ def test_match_fill_batch_vs_oracle():
         assert ssrc == w.get("SeveritySource", ""), (pk, adv, d)
         assert d[3] >> 28 == 1 and w["PrimaryURL"] == "https://avd.aquasec.com/nvd/" + vid.lower()
     mb.close()
+
+
+def _filter_fixture(seed=9):
+    """A multi-result batch with repeated (name, version) packages inside results, FillInfo
+    run, plus the oracle's view of every result's DetectedVulnerability list."""
+    import trivy_amd
+    from trivy_amd._lib import lib
+    from trivy_amd.batch import MatchBatch
+    from tools.synth import DEBIAN_DS, UBUNTU_DS, SynthBatch, make_batch, make_db
+    from tools.synth_vuln import vuln_arena, vuln_values
+
+    sdb = make_db(["debian 12", "ubuntu 22.04"], 800, seed=seed)
+    ids = sdb.vuln_ids()
+    db = trivy_amd.DB()
+    for n, depth, arena, off, lens in (sdb.records_arena(detail=True), sdb.source_arena(), vuln_arena(ids, seed)):
+        assert lib().tvm_db_put_arena(db.h, n, depth, arena, off.ctypes.data, lens.ctypes.data) == 0
+    eng = trivy_amd.Engine(db, 0)
+    b0 = make_batch(sdb, 30, 120, [1, 1], seed=seed)
+    # duplicate a quarter of every result's packages (same name and version) at its end
+    plat, names, vers, targets = [], [], [], []
+    for p, s, e in b0.targets:
+        idx = list(range(s, e)) + list(range(s, e, 4))
+        start = len(names)
+        for i in idx:
+            plat.append(p)
+            names.append(b0.names[i])
+            vers.append(b0.versions[i])
+        targets.append((p, start, len(names)))
+    batch = SynthBatch(np.array(plat, dtype=np.int32), names, vers, targets)
+    mb = MatchBatch(eng)
+    arena, noff, nlen, voff, vlen = batch.arena()
+    for p, s, e in batch.targets:
+        mb.add_arena(sdb.platforms[p], e - s, arena, noff[s:], nlen[s:], voff[s:], vlen[s:])
+    total, errp, _ = mb.run()
+    assert errp == -1 and total > 1000
+    pairs = mb.pairs()
+    mb.fill()
+    bucket = {k.decode(): v.decode() for k, v in vuln_values(ids, seed)}
+    names5 = ["UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"]
+    ds_of = {p: json.loads((DEBIAN_DS if p.startswith("debian") else UBUNTU_DS).decode()) for p in sdb.platforms}
+    by_target = [[] for _ in batch.targets]
+    tgt_of = np.zeros(len(batch), dtype=np.int64)
+    for t, (_, s, e) in enumerate(batch.targets):
+        tgt_of[s:e] = t
+    for pk, adv in pairs.tolist():  # detection order: package, then advisory
+        t = tgt_of[pk]
+        plat = sdb.platforms[batch.targets[t][0]]
+        v = {"VulnerabilityID": sdb.adv_vid[adv].decode(), "PkgName": batch.names[pk].decode(),
+             "InstalledVersion": batch.versions[pk].decode(), "DataSource": ds_of[plat], "_pair": (pk, adv)}
+        if sdb.adv_fixed[adv]:
+            v["FixedVersion"] = sdb.adv_fixed[adv].decode()
+        if plat.startswith("debian"):
+            st, sev = sdb.adv_detail(adv)
+            if st:
+                v["Status"] = st
+            if sev:
+                v["SeveritySource"] = "debian"
+                v["Vulnerability"] = {"Severity": names5[sev]}
+        by_target[t].append(v)
+    return mb, bucket, by_target, sdb
+
+
+@pytest.mark.parametrize("opts", [
+    dict(severities=("UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL")),
+    dict(severities=("HIGH", "CRITICAL"), ignore_statuses=(5, 7)),
+    dict(severities=("LOW", "MEDIUM", "HIGH"), ignore_statuses=(2,), ignore_ids=("__first3__",)),
+])
+def test_match_filter_batch_vs_oracle(opts):
+    """Batch result.Filter on the GPU (severity, status, ignore IDs, dedup keeping the
+    greater FixedVersion, BySeverity order) equals oracle/filter.py per result, in order."""
+    import oracle.filter as of
+    mb, bucket, by_target, sdb = _filter_fixture()
+    opts = dict(opts)
+    if opts.get("ignore_ids") == ("__first3__",):
+        opts["ignore_ids"] = tuple(v["VulnerabilityID"] for v in by_target[0][:3]) + ("CVE-0000-none",)
+    n = mb.filter(mb.filter_opts(**opts))
+    got = mb.filtered_pairs(n).tolist()
+    findings = [{"ID": i, "Paths": [], "PURLs": [], "ExpiredAt": None, "Statement": ""}
+                for i in opts.get("ignore_ids", ())]
+    want = []
+    for vulns in by_target:
+        filled = vi.fill_info(bucket, [{k: x for k, x in v.items() if k != "_pair"} for v in vulns])
+        for f, v in zip(filled, vulns):
+            f["_pair"] = v["_pair"]
+        kept, _ = of.filter_vulnerabilities("", filled, list(opts["severities"]), opts.get("ignore_statuses", ()),
+                                            findings)
+        want += kept or []
+    assert len(got) == len(want), (len(got), len(want))
+    for (pk, adv), w in zip(got, want):
+        wp, wa = w["_pair"]
+        # a duplicate package's copy is interchangeable: same advisory, same (name, version)
+        assert adv == wa and sdb.adv_vid[adv].decode() == w["VulnerabilityID"], (pk, adv, w)
+    mb.close()

@@ -27,7 +27,7 @@ def findings_for(args):
     name = args.get("ignoreFile")
     if not name:
         return []
-    with open(os.path.join(GOLDEN, "fixtures", "result", IGNORE_FILES[name]), encoding="utf-8") as f:
+    with open(os.path.join(GOLDEN, "result_files", IGNORE_FILES[name]), encoding="utf-8") as f:
         text = f.read()
     return of.parse_ignore_yaml(text, NOW) if name.endswith(".yaml") else of.parse_ignore_text(text, NOW)
 

@@ -71,6 +71,11 @@ class FillResult(ctypes.Structure):
     _fields_ = [("items", ctypes.POINTER(FillOut)), ("n", ctypes.c_size_t), ("priv", ctypes.c_void_p)]
 
 
+class FilterOpts(ctypes.Structure):
+    _fields_ = [("severity_mask", ctypes.c_uint32), ("ignore_status_mask", ctypes.c_uint32),
+                ("ignore_ids", ctypes.POINTER(Str)), ("n_ignore_ids", ctypes.c_size_t)]
+
+
 # (name, restype, argtypes) for every exported symbol of include/trivy_amd.h
 _P = ctypes.c_void_p
 _SIG = [
@@ -139,6 +144,12 @@ _SIG = [
                                            ctypes.c_size_t]),
     ("tvm_match_fill_algorithmic_bytes", ctypes.c_uint64, [_P, _P]),
     ("tvm_fill_source_name", ctypes.c_char_p, [_P, ctypes.c_uint32]),
+    ("tvm_match_filter", ctypes.c_int, [_P, _P, ctypes.POINTER(FilterOpts), ctypes.POINTER(ctypes.c_uint64),
+                                        ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_match_filter_fetch", ctypes.c_int, [_P, _P, ctypes.c_void_p, ctypes.c_uint64,
+                                              ctypes.POINTER(ctypes.c_uint64)]),
+    ("tvm_match_filter_time", ctypes.c_int, [_P, _P, ctypes.POINTER(FilterOpts), ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, ctypes.c_size_t]),
 ]
 
 EXPORTED = [s[0] for s in _SIG]

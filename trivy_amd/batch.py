@@ -165,6 +165,41 @@ class MatchBatch:
     def fill_algorithmic_bytes(self):
         return lib().tvm_match_fill_algorithmic_bytes(self.engine.h, self.h)
 
+    # ---- result.Filter per result (tvm_match_filter*) ----
+    @staticmethod
+    def filter_opts(severities=("UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"), ignore_statuses=(), ignore_ids=()):
+        from ._lib import FilterOpts, Str
+        names = ["UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"]
+        ids = [i.encode() if isinstance(i, str) else bytes(i) for i in ignore_ids]
+        arr = (Str * max(len(ids), 1))(*[Str(b, len(b)) for b in ids])
+        o = FilterOpts(sum(1 << names.index(x) for x in severities), sum(1 << s for s in ignore_statuses), arr,
+                       len(ids))
+        o._keep = (ids, arr)
+        return o
+
+    def filter(self, opts):
+        """filterVulnerabilities + BySeverity for every result (after launch() + fill());
+        returns the number of surviving vulnerabilities."""
+        e = errbuf()
+        n = ctypes.c_uint64()
+        self._check(lib().tvm_match_filter(self.engine.h, self.h, ctypes.byref(opts), ctypes.byref(n), e, len(e)), e,
+                    "tvm_match_filter")
+        return n.value
+
+    def filtered_pairs(self, n):
+        out = np.zeros((n, 2), dtype=np.uint32)
+        got = ctypes.c_uint64()
+        if lib().tvm_match_filter_fetch(self.engine.h, self.h, out.ctypes.data, n, ctypes.byref(got)):
+            raise RuntimeError("tvm_match_filter_fetch failed")
+        return out[:got.value]
+
+    def filter_time(self, opts, steps):
+        ms = ctypes.c_double()
+        e = errbuf()
+        self._check(lib().tvm_match_filter_time(self.engine.h, self.h, ctypes.byref(opts), steps, ctypes.byref(ms), e,
+                                                len(e)), e, "tvm_match_filter_time")
+        return ms.value / steps
+
     def close(self):
         h, self.h = getattr(self, "h", None), None
         if h:

@@ -1,6 +1,8 @@
 // C-ABI implementation (include/trivy_amd.h).
 #include "../../include/trivy_amd.h"
 
+#include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -38,6 +40,8 @@ struct tvm_batch {
   DevMatches m;
   uint4* fill_out = nullptr;  // tvm_match_fill decisions, parallel to m.pairs
   uint64_t fill_cap = 0;
+  std::vector<uint32_t> target_begin;  // first package of every result (one per add call)
+  BatchFilter filter;                  // tvm_match_filter state
   bool uploaded = false;
   int device = 0;
 };
@@ -345,6 +349,7 @@ static void reserve_more(HostBatch& hb, size_t n) {
 
 int64_t tvm_batch_add(tvm_batch* b, tvm_engine* e, const char* bucket, tvm_str name, tvm_str version) {
   if (!b || !e || !bucket || b->uploaded) return -1;
+  b->target_begin.push_back(uint32_t(b->hb.desc.size()));
   int32_t plat = e->eng->db().find_plat(bucket);
   b->hb.add(plat < 0 ? 0xFFFFFFFFu : uint32_t(plat), sv(name), sv(version));
   return int64_t(b->hb.desc.size() - 1);
@@ -358,6 +363,7 @@ int64_t tvm_batch_add_many(tvm_batch* b, tvm_engine* e, const char* bucket, size
   int32_t plat = e->eng->db().find_plat(bucket);
   const uint32_t pid = plat < 0 ? 0xFFFFFFFFu : uint32_t(plat);
   const int64_t first = int64_t(b->hb.desc.size());
+  b->target_begin.push_back(uint32_t(first));
   reserve_more(b->hb, n);
   for (size_t i = 0; i < n; i++)
     b->hb.add(pid, std::string_view(arena + name_off[i], name_len[i]), std::string_view(arena + ver_off[i], ver_len[i]));
@@ -376,6 +382,7 @@ int64_t tvm_batch_add_many_ex(tvm_batch* b, tvm_engine* e, const char* bucket, s
   int32_t plat = db.find_plat(bucket);
   const uint32_t pid = plat < 0 ? 0xFFFFFFFFu : uint32_t(plat);
   const int64_t first = int64_t(b->hb.desc.size());
+  b->target_begin.push_back(uint32_t(first));
   reserve_more(b->hb, n);
   for (size_t i = 0; i < n; i++) {
     const std::string_view ver(arena + ver_off[i], ver_len[i]);
@@ -778,4 +785,112 @@ const char* tvm_fill_source_name(tvm_engine* e, uint32_t id) {
   if (!e || id == SRC_NONE) return "";
   const VulnTable& vt = e->fill->table();
   return id < 0x7FFF ? vt.source_name(id).c_str() : "";
+}
+
+// ---- result.Filter over a batch (filter.go:60-139, filter.hip) --------------------------
+
+namespace {
+
+// Per package: rank of (result, name, version) in result-major byte order, and whether
+// the triple repeats within its result (types.BySeverity's PkgName/InstalledVersion order
+// and filterVulnerabilities' dedup key; batch packages carry no PkgPath).
+void package_ranks(const tvm_batch* b, std::vector<uint32_t>& rank, std::vector<uint8_t>& dup) {
+  const size_t n = b->hb.desc.size();
+  rank.assign(n, 0);
+  dup.assign(n, 0);
+  std::vector<uint32_t> bounds(b->target_begin);
+  bounds.push_back(uint32_t(n));
+  auto name = [&](uint32_t i) {
+    const uint4 d = b->hb.desc[i];
+    return std::string_view(reinterpret_cast<const char*>(b->hb.arena.data()) + d.y, d.w & 0xFFFFu);
+  };
+  auto ver = [&](uint32_t i) {
+    const uint4 d = b->hb.desc[i];
+    return std::string_view(reinterpret_cast<const char*>(b->hb.arena.data()) + d.z, d.w >> 16);
+  };
+  uint32_t next = 0;
+  std::vector<uint32_t> idx;
+  for (size_t t = 0; t + 1 < bounds.size(); t++) {
+    idx.clear();
+    for (uint32_t i = bounds[t]; i < bounds[t + 1]; i++) idx.push_back(i);
+    std::sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) {
+      const int c = name(x).compare(name(y));
+      return c != 0 ? c < 0 : ver(x) < ver(y);
+    });
+    for (size_t k = 0; k < idx.size(); k++) {
+      const bool same = k && name(idx[k]) == name(idx[k - 1]) && ver(idx[k]) == ver(idx[k - 1]);
+      if (k && !same) next++;
+      rank[idx[k]] = next;
+      if (same) dup[idx[k]] = dup[idx[k - 1]] = 1;
+    }
+    if (!idx.empty()) next++;
+  }
+}
+
+}  // namespace
+
+int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint64_t* n_kept, char* err,
+                     size_t errlen) {
+  if (!e || !b || !o || !b->uploaded || (o->n_ignore_ids && !o->ignore_ids)) return TVM_EINVAL;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  (void)hipSetDevice(e->device);
+  hipStream_t st = e->eng->stream();
+  if (hipStreamSynchronize(st) != hipSuccess) return TVM_EDEVICE;
+  uint64_t n = 0;
+  int64_t errp = -1;
+  int rc = tvm_match_status(e, b, &n, &errp, nullptr);
+  if (rc) return rc;
+  if (n > b->m.cap || n > b->fill_cap) {
+    set_err(err, errlen, "tvm_match_filter: run tvm_match_launch + tvm_match_fill with a large enough match buffer first");
+    return TVM_EINVAL;
+  }
+  std::string msg;
+  if (!b->filter.has_packages()) {
+    std::vector<uint32_t> rank;
+    std::vector<uint8_t> dup;
+    package_ranks(b, rank, dup);
+    if (!b->filter.set_packages(rank, dup, msg)) {
+      set_err(err, errlen, msg);
+      return TVM_EDEVICE;
+    }
+  }
+  const VulnTable& vt = e->fill->table();
+  std::vector<uint32_t> ignore;
+  for (size_t i = 0; i < o->n_ignore_ids; i++) {
+    const uint32_t r = vt.vuln_rank(std::string_view(o->ignore_ids[i].p ? o->ignore_ids[i].p : "", o->ignore_ids[i].n));
+    if (r != 0xFFFFFFFFu) ignore.push_back(r);
+  }
+  std::sort(ignore.begin(), ignore.end());
+  ignore.erase(std::unique(ignore.begin(), ignore.end()), ignore.end());
+  if (!b->filter.run(e->fill->dev(), b->m.pairs, b->fill_out, n, ignore, o->severity_mask, o->ignore_status_mask, st,
+                     msg)) {
+    set_err(err, errlen, msg);
+    return TVM_EDEVICE;
+  }
+  if (n_kept) *n_kept = b->filter.survivors();
+  return TVM_OK;
+}
+
+int tvm_match_filter_fetch(tvm_engine* e, tvm_batch* b, uint32_t* pairs, uint64_t cap, uint64_t* n_out) {
+  if (!e || !b || (cap && !pairs)) return TVM_EINVAL;
+  (void)hipSetDevice(e->device);
+  std::vector<uint2> out;
+  std::string msg;
+  if (!b->filter.fetch(out, e->eng->stream(), msg)) return TVM_EDEVICE;
+  const uint64_t k = std::min<uint64_t>(cap, out.size());
+  if (k) memcpy(pairs, out.data(), k * sizeof(uint2));
+  if (n_out) *n_out = k;
+  return TVM_OK;
+}
+
+int tvm_match_filter_time(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, int steps, double* ms, char* err,
+                          size_t errlen) {
+  if (!ms || steps <= 0) return TVM_EINVAL;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < steps; i++) {
+    const int rc = tvm_match_filter(e, b, o, nullptr, err, errlen);
+    if (rc) return rc;
+  }
+  *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return TVM_OK;
 }

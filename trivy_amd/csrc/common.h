@@ -113,6 +113,20 @@ struct alignas(16) SlotVal {
   uint32_t row_count;
 };
 enum : uint32_t { SLOT_POISONED = 1u << 31, SLOT_LEN_MASK = 0x7FFFFFFFu };
+// Device hash slot: one 64-B cache line holding the hash, the row range and the first
+// kSlotNameWords*8 bytes of the name (memory order, zero padded), so a probe verifies the
+// name from the same line it read the hash from; longer names finish against the name
+// arena from byte 40 on.  (The host keeps slot_hash/slot_val for its own lookups.)
+constexpr uint32_t kSlotNameWords = 5;
+struct alignas(64) Slot {
+  uint64_t hash;       // 0 = empty
+  uint32_t row_begin;
+  uint32_t row_count;
+  uint32_t name_len;   // bytes | SLOT_POISONED
+  uint32_t name_off;   // full name in the name arena
+  uint64_t name[kSlotNameWords];
+};
+static_assert(sizeof(Slot) == 64, "one cache line per slot");
 // Names in the DB name arena start 8-byte aligned, zero padded to a word boundary, and
 // the arena ends with kNameWords zero words: the probe verifies a name with kNameWords
 // independent word loads (one memory round trip) instead of a byte loop.

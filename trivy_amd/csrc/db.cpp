@@ -694,6 +694,7 @@ void DB::build_index() {
   slot_hash.assign(cap, 0);
   slot_val.assign(cap, SlotVal{});
   slot_key.assign(cap, 0);
+  slots.assign(cap, Slot{});
   name_arena.clear();
   for (size_t k = 0; k < keys.size(); k++) {
     const Key& key = keys[k];
@@ -708,6 +709,14 @@ void DB::build_index() {
     v.row_count = row_count[k];
     slot_val[i] = v;
     slot_key[i] = uint32_t(k);
+    Slot& sl = slots[i];
+    sl.hash = h;
+    sl.row_begin = v.row_begin;
+    sl.row_count = v.row_count;
+    sl.name_len = v.name_len;
+    sl.name_off = v.name_off;
+    for (size_t b = 0; b < key.name.size() && b < 8 * kSlotNameWords; b++)
+      sl.name[b / 8] |= uint64_t(uint8_t(key.name[b])) << (8 * (b % 8));
     name_arena.insert(name_arena.end(), key.name.begin(), key.name.end());
     name_arena.resize((name_arena.size() + 7) & ~size_t(7), 0);  // 8-B aligned names, zero padded
   }

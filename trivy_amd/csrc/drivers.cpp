@@ -669,6 +669,8 @@ DetectStatus library_detect_vulnerabilities(Engine& eng, std::string_view lib_ty
 void detector_fill_fields(uint8_t drv, const Advisory& a, DetFill& f) {
   f = DetFill();
   f.data_source = drv == DRV_REDHAT ? -1 : a.data_source;
+  const bool rpm_out = drv == DRV_REDHAT || drv == DRV_ALMA || drv == DRV_ROCKY || drv == DRV_MARINER;
+  f.fixed_version = drv == DRV_LIBRARY ? a.lib_fixed : rpm_out && !a.fixed.empty() ? rpm_string(a.fixed) : a.fixed;
   switch (drv) {
     case DRV_DEBIAN:
       f.status = a.status;

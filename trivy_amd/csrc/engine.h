@@ -16,8 +16,7 @@ class DB;
 
 // Device view of the flattened tables (db.h device images).
 struct DevDB {
-  const uint64_t* slot_hash = nullptr;
-  const SlotVal* slot_val = nullptr;
+  const Slot* slots = nullptr;
   uint64_t slot_mask = 0;
   const uint8_t* name_arena = nullptr;
   const Row* rows = nullptr;

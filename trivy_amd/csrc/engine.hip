@@ -130,11 +130,10 @@ Engine* Engine::open(const DB& db, int device, std::string& err) {
     delete e;
     return nullptr;
   }
-  uint64_t* sh; SlotVal* sv; uint8_t* na; Row* rows; uint64_t* kw; PlatInfo* pl; RowAux* ax; uint32_t* ai;
+  Slot* sl; uint8_t* na; Row* rows; uint64_t* kw; PlatInfo* pl; RowAux* ax; uint32_t* ai;
   bool ok = upload_vec(db.aux, &ax, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.aux_ids, &ai, e->allocs_, e->table_bytes_, err) &&
-            upload_vec(db.slot_hash, &sh, e->allocs_, e->table_bytes_, err) &&
-            upload_vec(db.slot_val, &sv, e->allocs_, e->table_bytes_, err) &&
+            upload_vec(db.slots, &sl, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.name_arena, &na, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.rows, &rows, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.key_words, &kw, e->allocs_, e->table_bytes_, err) &&
@@ -143,8 +142,7 @@ Engine* Engine::open(const DB& db, int device, std::string& err) {
     delete e;
     return nullptr;
   }
-  e->d_.slot_hash = sh;
-  e->d_.slot_val = sv;
+  e->d_.slots = sl;
   e->d_.slot_mask = db.slot_mask;
   e->d_.name_arena = na;
   e->d_.rows = rows;
@@ -363,8 +361,7 @@ bool Engine::verify(std::string& err) {
     return true;
   };
   const DB& db = *db_;
-  return check(d_.slot_hash, db.slot_hash.data(), db.slot_hash.size() * 8, "slot_hash") &&
-         check(d_.slot_val, db.slot_val.data(), db.slot_val.size() * sizeof(SlotVal), "slot_val") &&
+  return check(d_.slots, db.slots.data(), db.slots.size() * sizeof(Slot), "slots") &&
          check(d_.name_arena, db.name_arena.data(), db.name_arena.size(), "name_arena") &&
          check(d_.rows, db.rows.data(), db.rows.size() * sizeof(Row), "rows") &&
          check(d_.key_words, db.key_words.data(), db.key_words.size() * 8, "key_words") &&

@@ -20,18 +20,6 @@
 
 namespace tvm {
 
-struct FillDev {
-  const uint64_t* slot_hash;
-  const uint4* slot_val;
-  uint64_t slot_mask;
-  const uint8_t* id_arena;
-  const uint4* recs;
-  const uint32_t* ents;
-  const uint4* adv_items;
-  uint32_t n_advs;
-  uint32_t ghsa, nvd;
-};
-
 namespace {
 
 constexpr int kFillTile = 256;
@@ -186,7 +174,8 @@ FillEngine* FillEngine::open(const VulnTable& t, int device, std::string& err) {
             upload(t.id_arena, &d.id_arena, f->allocs_, f->table_bytes_, err) &&
             upload(t.recs, &d.recs, f->allocs_, f->table_bytes_, err) &&
             upload(t.ents, &d.ents, f->allocs_, f->table_bytes_, err) &&
-            upload(t.adv_items, &d.adv_items, f->allocs_, f->table_bytes_, err);
+            upload(t.adv_items, &d.adv_items, f->allocs_, f->table_bytes_, err) &&
+            upload(t.adv_rank, &d.adv_rank, f->allocs_, f->table_bytes_, err);
   if (!ok) {
     delete f;
     return nullptr;

@@ -87,12 +87,14 @@ __device__ __forceinline__ bool name_eq(const uint8_t* a, const uint8_t* b, uint
   return true;
 }
 
-// key_hash (common.h) fused with packing the name's first kNameWords*8 bytes into words
-// (memory order, zero padded), so the slot's name is verified with word compares.
-__device__ __forceinline__ uint64_t hash_pack(uint32_t plat, const uint8_t* s, uint32_t n, uint64_t (&w)[kNameWords]) {
-  static_assert(kNameWords == 4, "hash_pack fills exactly four words");
+// key_hash (common.h) fused with packing the name's first kSlotNameWords*8 bytes into
+// words (memory order, zero padded), so the slot's inline name is verified with word
+// compares.  Registers only (an if-chain, no dynamically indexed array).
+__device__ __forceinline__ uint64_t hash_pack(uint32_t plat, const uint8_t* s, uint32_t n,
+                                              uint64_t (&w)[kSlotNameWords]) {
+  static_assert(kSlotNameWords == 5, "hash_pack fills exactly five words");
   uint64_t h = key_hash_seed(plat), cur = 0;
-  w[0] = w[1] = w[2] = w[3] = 0;
+  w[0] = w[1] = w[2] = w[3] = w[4] = 0;
   for (uint32_t i = 0; i < n; i++) {
     const uint8_t c = s[i];
     h = key_hash_step(h, c);
@@ -103,23 +105,29 @@ __device__ __forceinline__ uint64_t hash_pack(uint32_t plat, const uint8_t* s, u
       else if (k == 1) w[1] = cur;
       else if (k == 2) w[2] = cur;
       else if (k == 3) w[3] = cur;
+      else if (k == 4) w[4] = cur;
       cur = 0;
     }
   }
   return key_hash_fin(h);
 }
 
-// Name check against the DB arena (8-B aligned, zero padded, kNameWords-word tail): the
-// four word loads are issued together; names longer than 32 bytes finish bytewise.
-__device__ __forceinline__ bool name_eq_w(const uint64_t (&w)[kNameWords], const uint8_t* name, const uint8_t* arena,
-                                          uint32_t off, uint32_t n) {
-  const uint64_t* y = reinterpret_cast<const uint64_t*>(arena + off);
-  const uint64_t y0 = y[0], y1 = y[1], y2 = y[2], y3 = y[3];
-  bool eq = n == 0 || w[0] == y0;
-  if (n > 8) eq &= w[1] == y1;
-  if (n > 16) eq &= w[2] == y2;
-  if (n > 24) eq &= w[3] == y3;
-  if (eq && n > 32) eq = name_eq(name + 32, arena + off + 32, n - 32);
+// Name check against a slot (its first 40 bytes inline, loaded with the hash); names
+// longer than 40 bytes finish bytewise against the name arena.
+__device__ __forceinline__ bool name_eq_slot(const uint64_t (&w)[kSlotNameWords], const uint4 q1, const uint4 q2,
+                                             const uint4 q3, const uint8_t* name, const uint8_t* arena, uint32_t n) {
+  const uint64_t y0 = q1.z | (uint64_t(q1.w) << 32), y1 = q2.x | (uint64_t(q2.y) << 32),
+                 y2 = q2.z | (uint64_t(q2.w) << 32), y3 = q3.x | (uint64_t(q3.y) << 32),
+                 y4 = q3.z | (uint64_t(q3.w) << 32);
+  bool eq = w[0] == y0;  // zero padded on both sides, so a short name compares whole words
+  eq &= w[1] == y1;
+  eq &= w[2] == y2;
+  eq &= w[3] == y3;
+  eq &= w[4] == y4;
+  if (eq && n > 8 * kSlotNameWords) {
+    const uint8_t* full = arena + q1.y;
+    for (uint32_t i = 8 * kSlotNameWords; eq && i < n; i++) eq = full[i] == name[i];
+  }
   return eq;
 }
 
@@ -359,19 +367,21 @@ __device__ __forceinline__ void probe_encode(const MatchArgs& a, TileShared<T, K
   }
   // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup
   if (AB != 3 && (valid || (pi.flags & PLAT_LOOKUP_FIRST))) {
-    uint64_t nw[kNameWords];
+    uint64_t nw[kSlotNameWords];
     const uint64_t h = hash_pack(d.x, name, nlen, nw);
     for (uint64_t i = h & a.db.slot_mask;; i = (i + 1) & a.db.slot_mask) {
-      const uint64_t sh = a.db.slot_hash[i];
-      const SlotVal sv = a.db.slot_val[i];  // issued with the hash: no dependent round trip
+      // the whole 64-B slot in one round trip: hash, rows, inline name
+      const uint4* sp = reinterpret_cast<const uint4*>(a.db.slots + i);
+      const uint4 q0 = sp[0], q1 = sp[1], q2 = sp[2], q3 = sp[3];
+      const uint64_t sh = q0.x | (uint64_t(q0.y) << 32);
       if (sh == 0) break;
       if (sh != h) continue;
-      if ((sv.name_len & SLOT_LEN_MASK) != nlen || !name_eq_w(nw, name, a.db.name_arena, sv.name_off, nlen)) continue;
-      if (sv.name_len & SLOT_POISONED) {
+      if ((q1.x & SLOT_LEN_MASK) != nlen || !name_eq_slot(nw, q1, q2, q3, name, a.db.name_arena, nlen)) continue;
+      if (q1.x & SLOT_POISONED) {
         atomicMax(&a.ctl[1], (unsigned long long)(a.n - p));
       } else if (valid) {
-        cnt = sv.row_count;
-        rbeg = sv.row_begin;
+        cnt = q0.w;
+        rbeg = q0.z;
       }
       break;
     }

@@ -288,6 +288,11 @@ uint32_t VulnTable::source_id(std::string_view s) const {
   return it == src_ids_.end() ? SRC_NONE : it->second;
 }
 
+uint32_t VulnTable::vuln_rank(std::string_view id) const {
+  auto it = vuln_rank_.find(std::string(id));
+  return it == vuln_rank_.end() ? 0xFFFFFFFFu : it->second;
+}
+
 int32_t VulnTable::find(std::string_view id) const {
   auto it = by_id_.find(id);
   return it == by_id_.end() ? -1 : it->second;
@@ -378,7 +383,8 @@ void VulnTable::build(const DB& db) {
   id_arena.resize(id_arena.size() + 8 * kNameWords, 0);
 
   // batch path: the FillInfo input of every advisory's detector output
-  adv_items.assign(db.advs.size(), make_uint4(0, SRC_NONE << 16, 0, FILL_NOT_FOUND));
+  adv_items.assign(db.advs.size(), make_uint4(0, (SRC_NONE << 16) | 0xFFu, 0, FILL_NOT_FOUND));
+  std::vector<std::string> fixed_out(db.advs.size());
   for (const Key& k : db.keys) {
     const uint8_t drv = db.plats[k.plat].drv;
     for (uint32_t ai : k.advs) {
@@ -391,10 +397,31 @@ void VulnTable::build(const DB& db) {
       const int32_t rec = find(a.vuln_id);
       uint4 it;
       it.x = 0;
-      it.y = src << 16;
+      it.y = (src << 16) | (f.severity ? uint32_t(fill_new_severity(f.severity)) : 0xFFu);
       it.z = uint32_t(f.status & 0xFF) | (f.fixed ? FI_FIXED : 0u) | (f.severity_source ? FI_SEV_SRC : 0u);
       it.w = (rec >= 0 && !vulns[size_t(rec)].bad) ? uint32_t(rec) : FILL_NOT_FOUND;
       adv_items[ai] = it;
+      fixed_out[ai] = std::move(f.fixed_version);
+    }
+  }
+  // ranks for the batch filter: vulnerability IDs and output FixedVersions in byte order
+  {
+    std::vector<std::string_view> ids, fx;
+    ids.reserve(db.advs.size());
+    for (const Advisory& a : db.advs) ids.push_back(a.vuln_id);
+    for (const std::string& f : fixed_out) fx.push_back(f);
+    auto rank_of = [](std::vector<std::string_view> v) {
+      std::sort(v.begin(), v.end());
+      v.erase(std::unique(v.begin(), v.end()), v.end());
+      return v;
+    };
+    const auto uid = rank_of(ids), ufx = rank_of(fx);
+    vuln_rank_.clear();
+    for (size_t i = 0; i < uid.size(); i++) vuln_rank_.emplace(std::string(uid[i]), uint32_t(i));
+    adv_rank.assign(db.advs.size(), make_uint2(0, 0));
+    for (size_t i = 0; i < db.advs.size(); i++) {
+      adv_rank[i].x = uint32_t(std::lower_bound(uid.begin(), uid.end(), ids[i]) - uid.begin());
+      adv_rank[i].y = uint32_t(std::lower_bound(ufx.begin(), ufx.end(), std::string_view(fixed_out[i])) - ufx.begin());
     }
   }
   built_ = true;

@@ -102,14 +102,21 @@ class VulnTable {
   uint64_t slot_mask = 0;
 
   // Batch path: per advisory of the DB, the FillInfo input its detector output carries
-  // (uint4 as the item layout, x/y unused: record in w, source in y >> 16).
+  // (uint4 as the item layout: record in w, source in y >> 16, the detector's
+  // package-specific severity index in y & 0xFF (0xFF = none)).
   std::vector<uint4> adv_items;
+  // Batch filter (result.Filter): per advisory {rank of its vulnerability ID among all
+  // advisory IDs, rank of its output FixedVersion among all output FixedVersions}, both
+  // in byte order (Go string order), and the ID -> rank map for ignore files.
+  std::vector<uint2> adv_rank;
+  uint32_t vuln_rank(std::string_view id) const;  // 0xFFFFFFFF when no advisory has it
 
  private:
   bool built_ = false;
   std::unordered_map<std::string, uint32_t> src_ids_;
   std::vector<std::string> src_names_;
   std::unordered_map<std::string_view, int32_t> by_id_;
+  std::unordered_map<std::string, uint32_t> vuln_rank_;
   uint32_t ghsa_ = SRC_NONE, nvd_ = SRC_NONE;
   uint32_t intern_source(const std::string& s);
 };
@@ -124,6 +131,7 @@ struct DetFill {
   bool fixed = false;             // FixedVersion != ""
   const char* severity_source = nullptr;
   const char* severity = nullptr;
+  std::string fixed_version;      // the output FixedVersion
 };
 void detector_fill_fields(uint8_t drv, const Advisory& a, DetFill& f);
 
@@ -132,7 +140,18 @@ const char* fill_severity_name(int64_t s);
 int64_t fill_new_severity(std::string_view s);
 
 // Device side (fill.hip).
-struct FillDev;
+struct FillDev {
+  const uint64_t* slot_hash;
+  const uint4* slot_val;
+  uint64_t slot_mask;
+  const uint8_t* id_arena;
+  const uint4* recs;
+  const uint32_t* ents;
+  const uint4* adv_items;
+  const uint2* adv_rank;
+  uint32_t n_advs;
+  uint32_t ghsa, nvd;
+};
 class FillEngine {
  public:
   ~FillEngine();
@@ -148,6 +167,8 @@ class FillEngine {
   const VulnTable& table() const { return *t_; }
   // Algorithmic HBM bytes of one batch-path launch over these pairs (host copy).
   uint64_t pair_bytes(const std::vector<uint2>& pairs) const;
+  const FillDev& dev() const { return *d_; }
+  int device() const { return dev_; }
 
  private:
   int dev_ = 0;
@@ -156,6 +177,30 @@ class FillEngine {
   std::vector<void*> allocs_;
   uint64_t table_bytes_ = 0;
   hipStream_t stream_ = nullptr;
+};
+
+// result.Filter over a batch's device match list (filter.hip).
+class BatchFilter {
+ public:
+  ~BatchFilter();
+  // Per package: rank of (result, name, version) in result-major byte order (packages
+  // sharing all three share a rank) and whether that triple repeats.
+  bool set_packages(const std::vector<uint32_t>& pkg_rank, const std::vector<uint8_t>& pkg_dup, std::string& err);
+  bool has_packages() const { return n_pkgs_ != 0; }
+  // Filters the n device pairs (with their FillInfo decisions) on `st`; synchronises once
+  // to learn the survivor count.  ignore: sorted vulnerability ranks (VulnTable::vuln_rank).
+  bool run(const FillDev& t, const uint2* pairs, const uint4* fill, uint64_t n, const std::vector<uint32_t>& ignore,
+           uint32_t sev_mask, uint32_t status_mask, hipStream_t st, std::string& err);
+  uint64_t survivors() const { return survivors_; }
+  // The surviving {package, advisory} pairs in report order.
+  bool fetch(std::vector<uint2>& out, hipStream_t st, std::string& err);
+
+ private:
+  void* bufs_[12] = {};
+  uint64_t caps_[12] = {};
+  uint64_t n_ = 0, survivors_ = 0, n_pkgs_ = 0;
+  bool any_dup_ = false;
+  bool grow(void*& p, uint64_t& cap, uint64_t need, std::string& err);
 };
 
 }  // namespace tvm
