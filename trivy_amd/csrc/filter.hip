@@ -108,7 +108,9 @@ __global__ __launch_bounds__(kFilterBlock) void filter_mark(FilterArgs a) {
 }
 
 __global__ __launch_bounds__(kFilterBlock) void filter_select(FilterArgs a) {
+  __shared__ uint32_t wsum[kFilterBlock / 64];
   const uint64_t stride = uint64_t(gridDim.x) * kFilterBlock;
+  uint32_t live_n = 0;  // survivors seen by this lane; one counter atomic per block at the end
   for (uint64_t i = uint64_t(blockIdx.x) * kFilterBlock + threadIdx.x; i < a.n; i += stride) {
     bool live = a.sort_key[i] != kEmpty;
     const uint2 p = a.pairs[i];
@@ -121,8 +123,16 @@ __global__ __launch_bounds__(kFilterBlock) void filter_select(FilterArgs a) {
         live = false;
       }
     }
-    const unsigned long long bal = __ballot(live);
-    if ((threadIdx.x & 63) == 0 && bal) atomicAdd(a.count, (unsigned long long)__popcll(bal));
+    live_n += live ? 1u : 0u;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) live_n += __shfl_xor(live_n, o, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = live_n;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < kFilterBlock / 64; w++) t += wsum[w];
+    if (t) atomicAdd(a.count, (unsigned long long)t);
   }
 }
 
@@ -181,10 +191,14 @@ bool BatchFilter::run(const FillDev& t, const uint2* pairs, const uint4* fill, u
     tcap = 16;
     while (tcap < 2 * n) tcap <<= 1;
   }
+  // sort only the key bits in use: package rank (< 2^pkg_bits) << 32 | severity | ID rank;
+  // a dropped pair's all-ones key stays the largest within any bit range
+  int end_bit = 33;
+  while (end_bit < 64 && (uint64_t(1) << (end_bit - 32)) <= n_pkgs_) end_bit++;
   size_t sort_bytes = 0;
   if (!ok(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, static_cast<unsigned long long*>(nullptr),
                                              static_cast<unsigned long long*>(nullptr), static_cast<uint32_t*>(nullptr),
-                                             static_cast<uint32_t*>(nullptr), int(n), 0, 64, st),
+                                             static_cast<uint32_t*>(nullptr), int(n), 0, end_bit, st),
           "hipcub sort sizing", err))
     return false;
   // 2 ignore, 3 table, 4 sort keys in, 5 sort keys out, 6 mine, 7 idx in, 8 idx out, 9 temp, 10 count, 11 out pairs
@@ -223,7 +237,7 @@ bool BatchFilter::run(const FillDev& t, const uint2* pairs, const uint4* fill, u
   if (!ok(hipGetLastError(), "filter launch", err)) return false;
   if (!ok(hipcub::DeviceRadixSort::SortPairs(bufs_[9], sort_bytes, a.sort_key,
                                              static_cast<unsigned long long*>(bufs_[5]), a.idx,
-                                             static_cast<uint32_t*>(bufs_[8]), int(n), 0, 64, st),
+                                             static_cast<uint32_t*>(bufs_[8]), int(n), 0, end_bit, st),
           "hipcub sort", err))
     return false;
   unsigned long long cnt = 0;
