@@ -288,9 +288,18 @@ typedef struct {
   uint32_t ignore_status_mask;   /* bit s: dbTypes.Status s is in FilterOption.IgnoreStatuses */
   const tvm_str* ignore_ids;     /* IDs of the ignore file's unexpired findings without paths/PURLs */
   size_t n_ignore_ids;
+  /* VEX suppressions (pkg/vex, applied after dedup as filter.go:51-53 filterByVEX does):
+   * pair k drops package vex_pkgs[k]'s finding of vulnerability vex_ids[k].  The host
+   * compiles a VEX document against the batch's package PURLs into these pairs
+   * (trivy_amd/vex.py: OpenVEX openvex.go:21-54, CycloneDX cyclonedx.go:48-84, CSAF
+   * csaf.go:27-83); the per-finding test runs on the GPU.  n_vex = 0: no VEX document. */
+  const uint32_t* vex_pkgs;
+  const tvm_str* vex_ids;
+  size_t n_vex;
 } tvm_filter_opts;
-/* filterVulnerabilities + sort.Sort(BySeverity) for every result of the batch, on the GPU,
- * after tvm_match_launch + tvm_match_fill.  n_kept = surviving vulnerabilities. */
+/* filterVulnerabilities + sort.Sort(BySeverity) (+ the VEX filter) for every result of the
+ * batch, on the GPU, after tvm_match_launch + tvm_match_fill.  n_kept = surviving
+ * vulnerabilities. */
 int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint64_t* n_kept, char* err, size_t errlen);
 /* The surviving {package, advisory} pairs (uint32 x2) in report order: results in add
  * order, each in BySeverity order. */

@@ -254,3 +254,56 @@ def test_match_filter_batch_vs_oracle(opts):
         # a duplicate package's copy is interchangeable: same advisory, same (name, version)
         assert adv == wa and sdb.adv_vid[adv].decode() == w["VulnerabilityID"], (pk, adv, w)
     mb.close()
+
+
+@pytest.mark.parametrize("kind", ["openvex", "cyclonedx", "csaf"])
+def test_match_filter_batch_vex_vs_oracle(kind):
+    """Batch result.Filter + the VEX filter (pkg/result/filter.go:38-104 filterByVEX after
+    FilterResult): the document is compiled on the host (trivy_amd/vex.py) into (package,
+    vulnerability) suppressions, the survivors are tested on the GPU (filter_select), and the
+    result equals oracle/filter.py then oracle/vex.py per result, in order."""
+    import oracle.filter as of
+    import oracle.vex as ov
+    from tools import synth_vex as sv
+    from trivy_amd.vex import VEX
+    mb, bucket, by_target, sdb = _filter_fixture()
+    # package identities: the OS PURL of (platform, name, version); one root image per result
+    n_pkgs = len(mb)
+    purls, refs, result_of = [None] * n_pkgs, [""] * n_pkgs, np.zeros(n_pkgs, dtype=np.int64)
+    roots = [sv.root_of(t) if t % 4 else None for t in range(len(by_target))]
+    findings = []
+    for t, vulns in enumerate(by_target):
+        plat = "debian 12" if vulns and vulns[0]["DataSource"]["ID"] == "debian" else "ubuntu 22.04"
+        for v in vulns:
+            pk = v["_pair"][0]
+            purls[pk] = sv.purl_of(plat, v["PkgName"], v["InstalledVersion"], "amd64" if len(v["PkgName"]) % 3 else None)
+            refs[pk] = "ref-%d-%s-%s" % (t, v["PkgName"], v["InstalledVersion"])
+            result_of[pk] = t
+            findings.append((pk, v["VulnerabilityID"]))
+    rng = np.random.default_rng(11)
+    text = {"openvex": lambda: sv.openvex(rng, findings, purls, len(roots), n_stmts=400),
+            "cyclonedx": lambda: sv.cyclonedx(rng, findings, purls, refs, n_vulns=300),
+            "csaf": lambda: sv.csaf(rng, findings, purls, n_vulns=300)}[kind]()
+    at = "cyclonedx" if kind == "cyclonedx" else ""
+    sup = VEX.new(text, at, sv.SERIAL, 1).suppressions(purls, refs, result_of, roots)
+    opts = dict(severities=("UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"))
+    n = mb.filter(mb.filter_opts(vex=sup, **opts))
+    got = mb.filtered_pairs(n).tolist()
+    oracle_vex = ov.VEX.new(text, at, sv.SERIAL, 1)
+    want, dropped = [], 0
+    for t, vulns in enumerate(by_target):
+        filled = vi.fill_info(bucket, [{k: x for k, x in v.items() if k != "_pair"} for v in vulns])
+        for f, v in zip(filled, vulns):
+            f["_pair"] = v["_pair"]
+            pk = v["_pair"][0]
+            f["PkgIdentifier"] = {"PURL": ov.purl_from_string(purls[pk]), "BOMRef": refs[pk]}
+        kept, _ = of.filter_vulnerabilities("", filled, list(opts["severities"]))
+        after = oracle_vex.filter(kept or [], ov.purl_from_string(roots[t]) if roots[t] else None)
+        dropped += len(kept or []) - len(after)
+        want += after
+    assert dropped > 0
+    assert len(got) == len(want), (len(got), len(want))
+    for (pk, adv), w in zip(got, want):
+        assert adv == w["_pair"][1] and sdb.adv_vid[adv].decode() == w["VulnerabilityID"], (pk, adv, w)
+        assert purls[pk] == purls[w["_pair"][0]]
+    mb.close()

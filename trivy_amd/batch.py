@@ -167,14 +167,23 @@ class MatchBatch:
 
     # ---- result.Filter per result (tvm_match_filter*) ----
     @staticmethod
-    def filter_opts(severities=("UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"), ignore_statuses=(), ignore_ids=()):
+    def filter_opts(severities=("UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"), ignore_statuses=(), ignore_ids=(),
+                    vex=None):
+        """FilterOption's vulnerability part; vex: (package indices, vulnerability IDs) from
+        trivy_amd.vex.VEX.suppressions (None: no VEX document)."""
         from ._lib import FilterOpts, Str
         names = ["UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"]
         ids = [i.encode() if isinstance(i, str) else bytes(i) for i in ignore_ids]
         arr = (Str * max(len(ids), 1))(*[Str(b, len(b)) for b in ids])
+        vpk, vids = vex if vex is not None else (np.zeros(0, dtype=np.uint32), [])
+        vpk = np.ascontiguousarray(vpk, dtype=np.uint32)
+        vids = [i.encode() if isinstance(i, str) else bytes(i) for i in vids]
+        if len(vpk) != len(vids):
+            raise ValueError("vex: one vulnerability ID per package index")
+        varr = (Str * max(len(vids), 1))(*[Str(b, len(b)) for b in vids])
         o = FilterOpts(sum(1 << names.index(x) for x in severities), sum(1 << s for s in ignore_statuses), arr,
-                       len(ids))
-        o._keep = (ids, arr)
+                       len(ids), vpk.ctypes.data if len(vpk) else None, varr, len(vids))
+        o._keep = (ids, arr, vpk, vids, varr)
         return o
 
     def filter(self, opts):

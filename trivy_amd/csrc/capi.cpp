@@ -831,7 +831,9 @@ void package_ranks(const tvm_batch* b, std::vector<uint32_t>& rank, std::vector<
 
 int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint64_t* n_kept, char* err,
                      size_t errlen) {
-  if (!e || !b || !o || !b->uploaded || (o->n_ignore_ids && !o->ignore_ids)) return TVM_EINVAL;
+  if (!e || !b || !o || !b->uploaded || (o->n_ignore_ids && !o->ignore_ids) ||
+      (o->n_vex && (!o->vex_pkgs || !o->vex_ids)))
+    return TVM_EINVAL;
   std::shared_lock<std::shared_mutex> lk(e->mu);
   (void)hipSetDevice(e->device);
   hipStream_t st = e->eng->stream();
@@ -862,8 +864,22 @@ int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint
   }
   std::sort(ignore.begin(), ignore.end());
   ignore.erase(std::unique(ignore.begin(), ignore.end()), ignore.end());
-  if (!b->filter.run(e->fill->dev(), b->m.pairs, b->fill_out, n, ignore, o->severity_mask, o->ignore_status_mask, st,
-                     msg)) {
+  // VEX suppressions as sorted (package << 32 | vulnerability rank) keys; IDs unknown to
+  // the DB cannot name a detected vulnerability and drop out here
+  std::vector<uint64_t> vex;
+  const uint64_t n_pkgs = uint64_t(tvm_batch_size(b));
+  for (size_t i = 0; i < o->n_vex; i++) {
+    if (o->vex_pkgs[i] >= n_pkgs) {
+      set_err(err, errlen, "tvm_match_filter: VEX package index out of range");
+      return TVM_EINVAL;
+    }
+    const uint32_t r = vt.vuln_rank(std::string_view(o->vex_ids[i].p ? o->vex_ids[i].p : "", o->vex_ids[i].n));
+    if (r != 0xFFFFFFFFu) vex.push_back((uint64_t(o->vex_pkgs[i]) << 32) | r);
+  }
+  std::sort(vex.begin(), vex.end());
+  vex.erase(std::unique(vex.begin(), vex.end()), vex.end());
+  if (!b->filter.run(e->fill->dev(), b->m.pairs, b->fill_out, n, ignore, vex, o->severity_mask,
+                     o->ignore_status_mask, st, msg)) {
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
   }

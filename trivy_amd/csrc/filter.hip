@@ -16,7 +16,10 @@
 //   filter_mark    per pair: severity/status/ignore test; duplicates (packages whose
 //                  (result, name, version) repeats) race into an open-addressing table
 //                  with one 64-bit atomicMax of (FixedVersion rank, -package) per key;
-//   filter_select  losers drop out; survivors get the BySeverity sort key
+//   filter_select  losers drop out; then the VEX filter (filter.go:51-53, after dedup):
+//                  a survivor whose (package, vulnerability rank) the host-compiled VEX
+//                  suppression list holds (binary search) drops out too; survivors keep
+//                  the BySeverity sort key
 //                  (package rank << 32 | (4 - severity) << 29 | vulnerability rank);
 //   radix sort     hipcub DeviceRadixSort over (key, pair index), dropped pairs last;
 //   filter_gather  the surviving {package, advisory} pairs in report order.
@@ -43,6 +46,8 @@ struct FilterArgs {
   const uint8_t* pkg_dup;       // per package: its (result, name, version) repeats
   const uint32_t* ignore;       // sorted vulnerability ranks of the ignore file
   uint32_t n_ignore;
+  const unsigned long long* vex;  // sorted (package << 32 | vulnerability rank) VEX suppressions
+  uint32_t n_vex;
   uint32_t sev_mask, status_mask;
   unsigned long long* table;    // {key, value} pairs, 2^k entries (dup pairs only)
   uint64_t table_mask;
@@ -123,6 +128,19 @@ __global__ __launch_bounds__(kFilterBlock) void filter_select(FilterArgs a) {
         live = false;
       }
     }
+    if (live && a.n_vex) {  // VEX: openvex.go:35-40 / cyclonedx.go:56-60 / csaf.go:36-40 drop it
+      const unsigned long long key = (uint64_t(p.x) << 32) | a.t.adv_rank[p.y].x;
+      uint32_t lo = 0, hi = a.n_vex;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.vex[mid] < key) lo = mid + 1;
+        else hi = mid;
+      }
+      if (lo < a.n_vex && a.vex[lo] == key) {
+        a.sort_key[i] = kEmpty;
+        live = false;
+      }
+    }
     live_n += live ? 1u : 0u;
   }
 #pragma unroll
@@ -177,12 +195,12 @@ bool BatchFilter::set_packages(const std::vector<uint32_t>& pkg_rank, const std:
 }
 
 bool BatchFilter::run(const FillDev& t, const uint2* pairs, const uint4* fill, uint64_t n,
-                      const std::vector<uint32_t>& ignore, uint32_t sev_mask, uint32_t status_mask, hipStream_t st,
-                      std::string& err) {
+                      const std::vector<uint32_t>& ignore, const std::vector<uint64_t>& vex, uint32_t sev_mask,
+                      uint32_t status_mask, hipStream_t st, std::string& err) {
   n_ = n;
   survivors_ = 0;
   if (n == 0) return true;
-  if (n > 0xFFFFFFFFull) {
+  if (n > 0xFFFFFFFFull || vex.size() > 0xFFFFFFFFull) {
     err = "filter: too many pairs";
     return false;
   }
@@ -201,13 +219,17 @@ bool BatchFilter::run(const FillDev& t, const uint2* pairs, const uint4* fill, u
                                              static_cast<uint32_t*>(nullptr), int(n), 0, end_bit, st),
           "hipcub sort sizing", err))
     return false;
-  // 2 ignore, 3 table, 4 sort keys in, 5 sort keys out, 6 mine, 7 idx in, 8 idx out, 9 temp, 10 count, 11 out pairs
+  // 2 ignore, 3 table, 4 sort keys in, 5 sort keys out, 6 mine, 7 idx in, 8 idx out, 9 temp, 10 count,
+  // 11 out pairs, 12 VEX suppressions
   if (!grow(bufs_[2], caps_[2], std::max<size_t>(ignore.size(), 1) * 4, err) ||
       !grow(bufs_[3], caps_[3], std::max<uint64_t>(tcap, 1) * 16, err) || !grow(bufs_[4], caps_[4], n * 8, err) ||
       !grow(bufs_[5], caps_[5], n * 8, err) || !grow(bufs_[6], caps_[6], n * 8, err) ||
       !grow(bufs_[7], caps_[7], n * 4, err) || !grow(bufs_[8], caps_[8], n * 4, err) ||
       !grow(bufs_[9], caps_[9], sort_bytes, err) || !grow(bufs_[10], caps_[10], 8, err) ||
-      !grow(bufs_[11], caps_[11], n * 8, err))
+      !grow(bufs_[11], caps_[11], n * 8, err) || !grow(bufs_[12], caps_[12], std::max<size_t>(vex.size(), 1) * 8, err))
+    return false;
+  if (!vex.empty() &&
+      !ok(hipMemcpyAsync(bufs_[12], vex.data(), vex.size() * 8, hipMemcpyHostToDevice, st), "H2D vex", err))
     return false;
   if (!ignore.empty() &&
       !ok(hipMemcpyAsync(bufs_[2], ignore.data(), ignore.size() * 4, hipMemcpyHostToDevice, st), "H2D ignore", err))
@@ -223,6 +245,8 @@ bool BatchFilter::run(const FillDev& t, const uint2* pairs, const uint4* fill, u
   a.pkg_dup = static_cast<const uint8_t*>(bufs_[1]);
   a.ignore = static_cast<const uint32_t*>(bufs_[2]);
   a.n_ignore = uint32_t(ignore.size());
+  a.vex = static_cast<const unsigned long long*>(bufs_[12]);
+  a.n_vex = uint32_t(vex.size());
   a.sev_mask = sev_mask;
   a.status_mask = status_mask;
   a.table = static_cast<unsigned long long*>(bufs_[3]);

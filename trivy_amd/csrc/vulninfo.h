@@ -188,16 +188,18 @@ class BatchFilter {
   bool set_packages(const std::vector<uint32_t>& pkg_rank, const std::vector<uint8_t>& pkg_dup, std::string& err);
   bool has_packages() const { return n_pkgs_ != 0; }
   // Filters the n device pairs (with their FillInfo decisions) on `st`; synchronises once
-  // to learn the survivor count.  ignore: sorted vulnerability ranks (VulnTable::vuln_rank).
+  // to learn the survivor count.  ignore: sorted vulnerability ranks (VulnTable::vuln_rank);
+  // vex: sorted (package << 32 | vulnerability rank) findings a VEX document drops.
   bool run(const FillDev& t, const uint2* pairs, const uint4* fill, uint64_t n, const std::vector<uint32_t>& ignore,
-           uint32_t sev_mask, uint32_t status_mask, hipStream_t st, std::string& err);
+           const std::vector<uint64_t>& vex, uint32_t sev_mask, uint32_t status_mask, hipStream_t st,
+           std::string& err);
   uint64_t survivors() const { return survivors_; }
   // The surviving {package, advisory} pairs in report order.
   bool fetch(std::vector<uint2>& out, hipStream_t st, std::string& err);
 
  private:
-  void* bufs_[12] = {};
-  uint64_t caps_[12] = {};
+  void* bufs_[13] = {};
+  uint64_t caps_[13] = {};
   uint64_t n_ = 0, survivors_ = 0, n_pkgs_ = 0;
   bool any_dup_ = false;
   bool grow(void*& p, uint64_t& cap, uint64_t need, std::string& err);
