@@ -284,6 +284,16 @@ def main():
         kept = mb.filter(fopts)
         filt_ms = mb.filter_time(fopts, max(3, args.steps // 4))
         fill["result_filter"] = {"ms": filt_ms, "kept": kept, "matches_per_s": total / (filt_ms / 1e3)}
+        # + a VEX document's suppressions (filterByVEX, filter.go:38-104): 1% of the findings,
+        # sampled from the match list, as the host compile (trivy_amd/vex.py) would emit them
+        pr = mb.pairs()
+        pick = np.random.default_rng(5).choice(len(pr), size=max(1, len(pr) // 100), replace=False)
+        vex = (pr[pick, 0], [wl.sdb.adv_vid[a] for a in pr[pick, 1].tolist()])
+        vopts = mb.filter_opts(vex=vex)
+        vkept = mb.filter(vopts)
+        vex_ms = mb.filter_time(vopts, max(3, args.steps // 4))
+        fill["result_filter"]["vex"] = {"suppressions": len(pick), "ms": vex_ms, "kept": vkept,
+                                        "matches_per_s": total / (vex_ms / 1e3)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -289,13 +289,16 @@ typedef struct {
   const tvm_str* ignore_ids;     /* IDs of the ignore file's unexpired findings without paths/PURLs */
   size_t n_ignore_ids;
   /* VEX suppressions (pkg/vex, applied after dedup as filter.go:51-53 filterByVEX does):
-   * pair k drops package vex_pkgs[k]'s finding of vulnerability vex_ids[k].  The host
-   * compiles a VEX document against the batch's package PURLs into these pairs
+   * entry k drops package vex_pkgs[k]'s finding of vulnerability vex_ids[vex_id_index[k]].
+   * The host compiles a VEX document against the batch's package PURLs into these entries
    * (trivy_amd/vex.py: OpenVEX openvex.go:21-54, CycloneDX cyclonedx.go:48-84, CSAF
-   * csaf.go:27-83); the per-finding test runs on the GPU.  n_vex = 0: no VEX document. */
+   * csaf.go:27-83); the per-finding test runs on the GPU.  vex_ids holds each distinct ID
+   * once.  n_vex = 0: no VEX document. */
   const uint32_t* vex_pkgs;
-  const tvm_str* vex_ids;
+  const uint32_t* vex_id_index;
   size_t n_vex;
+  const tvm_str* vex_ids;
+  size_t n_vex_ids;
 } tvm_filter_opts;
 /* filterVulnerabilities + sort.Sort(BySeverity) (+ the VEX filter) for every result of the
  * batch, on the GPU, after tvm_match_launch + tvm_match_fill.  n_kept = surviving

@@ -74,7 +74,8 @@ class FillResult(ctypes.Structure):
 class FilterOpts(ctypes.Structure):
     _fields_ = [("severity_mask", ctypes.c_uint32), ("ignore_status_mask", ctypes.c_uint32),
                 ("ignore_ids", ctypes.POINTER(Str)), ("n_ignore_ids", ctypes.c_size_t),
-                ("vex_pkgs", ctypes.c_void_p), ("vex_ids", ctypes.POINTER(Str)), ("n_vex", ctypes.c_size_t)]
+                ("vex_pkgs", ctypes.c_void_p), ("vex_id_index", ctypes.c_void_p), ("n_vex", ctypes.c_size_t),
+                ("vex_ids", ctypes.POINTER(Str)), ("n_vex_ids", ctypes.c_size_t)]
 
 
 # (name, restype, argtypes) for every exported symbol of include/trivy_amd.h

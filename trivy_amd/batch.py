@@ -177,13 +177,16 @@ class MatchBatch:
         arr = (Str * max(len(ids), 1))(*[Str(b, len(b)) for b in ids])
         vpk, vids = vex if vex is not None else (np.zeros(0, dtype=np.uint32), [])
         vpk = np.ascontiguousarray(vpk, dtype=np.uint32)
-        vids = [i.encode() if isinstance(i, str) else bytes(i) for i in vids]
         if len(vpk) != len(vids):
             raise ValueError("vex: one vulnerability ID per package index")
-        varr = (Str * max(len(vids), 1))(*[Str(b, len(b)) for b in vids])
+        uniq = {}
+        vidx = np.array([uniq.setdefault(i, len(uniq)) for i in vids], dtype=np.uint32)
+        ublobs = [i.encode() if isinstance(i, str) else bytes(i) for i in uniq]
+        varr = (Str * max(len(ublobs), 1))(*[Str(b, len(b)) for b in ublobs])
         o = FilterOpts(sum(1 << names.index(x) for x in severities), sum(1 << s for s in ignore_statuses), arr,
-                       len(ids), vpk.ctypes.data if len(vpk) else None, varr, len(vids))
-        o._keep = (ids, arr, vpk, vids, varr)
+                       len(ids), vpk.ctypes.data if len(vpk) else None, vidx.ctypes.data if len(vidx) else None,
+                       len(vpk), varr, len(ublobs))
+        o._keep = (ids, arr, vpk, vidx, ublobs, varr)
         return o
 
     def filter(self, opts):

@@ -832,7 +832,7 @@ void package_ranks(const tvm_batch* b, std::vector<uint32_t>& rank, std::vector<
 int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint64_t* n_kept, char* err,
                      size_t errlen) {
   if (!e || !b || !o || !b->uploaded || (o->n_ignore_ids && !o->ignore_ids) ||
-      (o->n_vex && (!o->vex_pkgs || !o->vex_ids)))
+      (o->n_vex && (!o->vex_pkgs || !o->vex_id_index)) || (o->n_vex_ids && !o->vex_ids))
     return TVM_EINVAL;
   std::shared_lock<std::shared_mutex> lk(e->mu);
   (void)hipSetDevice(e->device);
@@ -864,20 +864,23 @@ int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint
   }
   std::sort(ignore.begin(), ignore.end());
   ignore.erase(std::unique(ignore.begin(), ignore.end()), ignore.end());
-  // VEX suppressions as sorted (package << 32 | vulnerability rank) keys; IDs unknown to
-  // the DB cannot name a detected vulnerability and drop out here
+  // VEX suppressions as (package << 32 | vulnerability rank) keys, sorted on the GPU; each
+  // distinct ID is ranked once; IDs unknown to the DB cannot name a detected vulnerability
+  // and drop out here
+  std::vector<uint32_t> id_rank(o->n_vex_ids);
+  for (size_t i = 0; i < o->n_vex_ids; i++)
+    id_rank[i] = vt.vuln_rank(std::string_view(o->vex_ids[i].p ? o->vex_ids[i].p : "", o->vex_ids[i].n));
   std::vector<uint64_t> vex;
+  vex.reserve(o->n_vex);
   const uint64_t n_pkgs = uint64_t(tvm_batch_size(b));
   for (size_t i = 0; i < o->n_vex; i++) {
-    if (o->vex_pkgs[i] >= n_pkgs) {
-      set_err(err, errlen, "tvm_match_filter: VEX package index out of range");
+    if (o->vex_pkgs[i] >= n_pkgs || o->vex_id_index[i] >= o->n_vex_ids) {
+      set_err(err, errlen, "tvm_match_filter: VEX package or ID index out of range");
       return TVM_EINVAL;
     }
-    const uint32_t r = vt.vuln_rank(std::string_view(o->vex_ids[i].p ? o->vex_ids[i].p : "", o->vex_ids[i].n));
+    const uint32_t r = id_rank[o->vex_id_index[i]];
     if (r != 0xFFFFFFFFu) vex.push_back((uint64_t(o->vex_pkgs[i]) << 32) | r);
   }
-  std::sort(vex.begin(), vex.end());
-  vex.erase(std::unique(vex.begin(), vex.end()), vex.end());
   if (!b->filter.run(e->fill->dev(), b->m.pairs, b->fill_out, n, ignore, vex, o->severity_mask,
                      o->ignore_status_mask, st, msg)) {
     set_err(err, errlen, msg);

@@ -228,9 +228,19 @@ bool BatchFilter::run(const FillDev& t, const uint2* pairs, const uint4* fill, u
       !grow(bufs_[9], caps_[9], sort_bytes, err) || !grow(bufs_[10], caps_[10], 8, err) ||
       !grow(bufs_[11], caps_[11], n * 8, err) || !grow(bufs_[12], caps_[12], std::max<size_t>(vex.size(), 1) * 8, err))
     return false;
-  if (!vex.empty() &&
-      !ok(hipMemcpyAsync(bufs_[12], vex.data(), vex.size() * 8, hipMemcpyHostToDevice, st), "H2D vex", err))
-    return false;
+  if (!vex.empty()) {  // unsorted keys in (bufs_[5], free until the main sort) -> sorted in bufs_[12]
+    size_t vb = 0;
+    if (!ok(hipcub::DeviceRadixSort::SortKeys(nullptr, vb, static_cast<unsigned long long*>(nullptr),
+                                              static_cast<unsigned long long*>(nullptr), int(vex.size()), 0, 64, st),
+            "hipcub vex sort sizing", err) ||
+        !grow(bufs_[9], caps_[9], std::max(sort_bytes, vb), err) ||
+        !grow(bufs_[5], caps_[5], std::max<uint64_t>(n, vex.size()) * 8, err) ||
+        !ok(hipMemcpyAsync(bufs_[5], vex.data(), vex.size() * 8, hipMemcpyHostToDevice, st), "H2D vex", err) ||
+        !ok(hipcub::DeviceRadixSort::SortKeys(bufs_[9], vb, static_cast<unsigned long long*>(bufs_[5]),
+                                              static_cast<unsigned long long*>(bufs_[12]), int(vex.size()), 0, 64, st),
+            "hipcub vex sort", err))
+      return false;
+  }
   if (!ignore.empty() &&
       !ok(hipMemcpyAsync(bufs_[2], ignore.data(), ignore.size() * 4, hipMemcpyHostToDevice, st), "H2D ignore", err))
     return false;

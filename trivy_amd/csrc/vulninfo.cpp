@@ -289,7 +289,7 @@ uint32_t VulnTable::source_id(std::string_view s) const {
 }
 
 uint32_t VulnTable::vuln_rank(std::string_view id) const {
-  auto it = vuln_rank_.find(std::string(id));
+  auto it = vuln_rank_.find(id);
   return it == vuln_rank_.end() ? 0xFFFFFFFFu : it->second;
 }
 
@@ -417,7 +417,12 @@ void VulnTable::build(const DB& db) {
     };
     const auto uid = rank_of(ids), ufx = rank_of(fx);
     vuln_rank_.clear();
-    for (size_t i = 0; i < uid.size(); i++) vuln_rank_.emplace(std::string(uid[i]), uint32_t(i));
+    rank_names_.clear();
+    rank_names_.reserve(uid.size());  // no reallocation below: the map's views stay valid
+    for (size_t i = 0; i < uid.size(); i++) {
+      rank_names_.emplace_back(uid[i]);
+      vuln_rank_.emplace(std::string_view(rank_names_.back()), uint32_t(i));
+    }
     adv_rank.assign(db.advs.size(), make_uint2(0, 0));
     for (size_t i = 0; i < db.advs.size(); i++) {
       adv_rank[i].x = uint32_t(std::lower_bound(uid.begin(), uid.end(), ids[i]) - uid.begin());

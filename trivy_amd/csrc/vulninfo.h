@@ -116,7 +116,8 @@ class VulnTable {
   std::unordered_map<std::string, uint32_t> src_ids_;
   std::vector<std::string> src_names_;
   std::unordered_map<std::string_view, int32_t> by_id_;
-  std::unordered_map<std::string, uint32_t> vuln_rank_;
+  std::vector<std::string> rank_names_;                      // owns the keys of vuln_rank_
+  std::unordered_map<std::string_view, uint32_t> vuln_rank_;  // no allocation per lookup
   uint32_t ghsa_ = SRC_NONE, nvd_ = SRC_NONE;
   uint32_t intern_source(const std::string& s);
 };
