@@ -1,0 +1,270 @@
+"""CycloneDX SBOM -> detector input (mirror of pkg/sbom).
+
+The step before the hot path for SBOM scans (`trivy sbom`, C1): the document's components
+become the OS package list and the language applications the detectors consume, then
+`scan` runs them through the GPU detectors (ospkg.Detect / library.Detect over the
+C-ABI).  Host-side JSON work, O(components); it follows:
+
+  pkg/sbom/cyclonedx/unmarshal.go:63-230  parseBOM / parseComponent (supported component
+      types, PURL, "aquasecurity:trivy:" properties, metadata component = root,
+      dependencies -> relationships between known bom-refs)
+  pkg/sbom/io/decode.go:47-380            Decoder.Decode: one OS component at most, apps by
+      their Type property (aggregating types carry no FilePath), libraries from their PURL
+      (decodeLibrary: class must be OS or language; pkgName: component group/name; PkgID,
+      FilePath, Src*, Modularitylabel, layer properties), fillSrcPkg for OS packages,
+      the OS's dependencies -> OS packages, each app's dependencies -> its libraries,
+      the rest: OS packages (one PURL type only, only when an OS is known) and one
+      application per language type; applications sorted by (Type, FilePath)
+  pkg/purl/purl.go:130-243                LangType / Class / Package (name from namespace,
+      arch / epoch / modularitylabel qualifiers, rpm version-release split)
+  pkg/fanal/types/artifact.go:203-211     Packages.Less (Name, Version, FilePath)
+"""
+import json
+import urllib.parse
+
+NAMESPACE = "aquasecurity:trivy:"
+AGGREGATING = {"python-pkg", "conda-pkg", "gemspec", "node-pkg", "jar"}
+LANG_OF_PURL = {"composer": "composer", "maven": "jar", "gem": "gemspec", "conda": "conda-pkg",
+                "pypi": "python-pkg", "golang": "gobinary", "npm": "node-pkg", "cargo": "cargo", "nuget": "nuget",
+                "swift": "swift", "cocoapods": "cocoapods", "hex": "hex", "conan": "conan", "pub": "pub",
+                "bitnami": "bitnami"}
+K8S_LANG = {"eks": "eks", "gke": "gke", "aks": "aks", "ocp": "ocp", "": "kubernetes"}
+OS_PURL_TYPES = {"apk", "deb", "rpm"}
+CDX_TYPES = {"container", "application", "library", "operating-system", "platform"}
+
+
+class SBOMError(Exception):
+    pass
+
+
+def parse_purl(s):
+    """packageurl-go FromString: {type, namespace, name, version, qualifiers (ordered), subpath};
+    raises SBOMError on a malformed PURL."""
+    if not s.startswith("pkg:"):
+        raise SBOMError("failed to parse PURL: scheme is not \"pkg\"")
+    rest = s[4:].lstrip("/")
+    subpath = ""
+    if "#" in rest:
+        rest, sp = rest.split("#", 1)
+        subpath = "/".join(urllib.parse.unquote(x) for x in sp.strip("/").split("/") if x not in ("", ".", ".."))
+    quals = []
+    if "?" in rest:
+        rest, q = rest.split("?", 1)
+        for kv in q.split("&"):
+            k, _, v = kv.partition("=")
+            if kv and v:
+                quals.append((k.lower(), urllib.parse.unquote(v)))
+    typ, _, rest = rest.partition("/")
+    if not typ or not rest:
+        raise SBOMError("failed to parse PURL: missing type or name")
+    version = ""
+    if "@" in rest:
+        rest, version = rest.rsplit("@", 1)
+        version = urllib.parse.unquote(version)
+    segs = [urllib.parse.unquote(x) for x in rest.strip("/").split("/")]
+    return {"type": typ.lower(), "namespace": "/".join(x for x in segs[:-1] if x), "name": segs[-1],
+            "version": version, "qualifiers": quals, "subpath": subpath}
+
+
+def lang_type(p):
+    """purl.go:130-179."""
+    if p["type"] == "k8s":
+        return K8S_LANG.get(p["namespace"], "")
+    return LANG_OF_PURL.get(p["type"], "")
+
+
+def purl_class(p):
+    """purl.go:181-193."""
+    if p["type"] in OS_PURL_TYPES:
+        return "os-pkgs"
+    return "lang-pkgs" if lang_type(p) else ""
+
+
+def _rpm_split(v):
+    """go-rpm-version NewVersion: [epoch:]version[-release] (the release after the last '-')."""
+    if ":" in v:
+        v = v.split(":", 1)[1]
+    ver, sep, rel = v.rpartition("-")
+    return (ver, rel) if sep else (v, "")
+
+
+def package_of(p):
+    """purl.go:195-243 PackageURL.Package."""
+    name = p["name"]
+    cls = purl_class(p)
+    if p["namespace"] and cls != "os-pkgs":
+        name = p["namespace"] + (":" if p["type"] in ("maven", "gradle") else "/") + p["name"]
+    if p["subpath"] and p["type"] == "cocoapods":
+        name = p["name"] + "/" + p["subpath"]
+    pkg = {"Name": name, "Version": p["version"]}
+    for k, v in p["qualifiers"]:
+        if k == "arch":
+            pkg["Arch"] = v
+        elif k == "modularitylabel":
+            pkg["Modularitylabel"] = v
+        elif k == "epoch" and v.lstrip("+-").isdigit():
+            pkg["Epoch"] = int(v)
+    if p["type"] == "rpm":
+        pkg["Version"], pkg["Release"] = _rpm_split(p["version"])
+    return pkg
+
+
+def dependency_id(lang, name, version):
+    """pkg/dependency/id.go:9-27: name + "@" + version; "/" for conan, ":" for
+    jar/pom/gradle, Go versions get a "v" prefix; an empty version gives the name."""
+    if not version:
+        return name
+    sep = "@"
+    if lang == "conan":
+        sep = "/"
+    elif lang in ("gomod", "gobinary") and not version.startswith("v"):
+        version = "v" + version
+    elif lang in ("jar", "pom", "gradle"):
+        sep = ":"
+    return name + sep + version
+
+
+def _component(c):
+    """unmarshal.go parseComponent; None for an unsupported component type."""
+    if c.get("type") not in CDX_TYPES:
+        return None
+    purl = parse_purl(c["purl"]) if c.get("purl") else None
+    return {"type": c["type"], "name": c.get("name", ""), "group": c.get("group", ""),
+            "version": c.get("version", ""), "bom_ref": c.get("bom-ref", ""), "purl": purl,
+            "purl_str": c.get("purl", ""),
+            "props": [(pr.get("name", "")[len(NAMESPACE):] if pr.get("name", "").startswith(NAMESPACE)
+                       else pr.get("name", ""), pr.get("value", "")) for pr in c.get("properties") or []]}
+
+
+def _library(c):
+    """decode.go decodeLibrary (None: no PURL or an unsupported PURL type)."""
+    p = c["purl"]
+    if p is None or not purl_class(p):
+        return None
+    pkg = package_of(p)
+    if p["type"] != "cocoapods":
+        pkg["Name"] = (c["group"] + (":" if p["type"] in ("maven", "gradle") else "/") + c["name"]
+                       if c["group"] else c["name"])
+    pkg["ID"] = dependency_id(lang_type(p), pkg["Name"], p["version"])
+    for k, v in c["props"]:
+        if k == "PkgID":
+            pkg["ID"] = v
+        elif k == "FilePath":
+            pkg["FilePath"] = v
+        elif k in ("SrcName", "SrcVersion", "SrcRelease", "Modularitylabel"):
+            pkg[k] = v
+        elif k == "SrcEpoch":
+            try:
+                pkg["SrcEpoch"] = int(v)
+            except ValueError:
+                raise SBOMError("failed to decode components: failed to decode library: invalid src epoch")
+        elif k == "LayerDigest":
+            pkg.setdefault("Layer", {})["Digest"] = v
+        elif k == "LayerDiffID":
+            pkg.setdefault("Layer", {})["DiffID"] = v
+    pkg["Identifier"] = {"PURL": c["purl_str"], "BOMRef": c["bom_ref"]}
+    pkg["_purl"] = p
+    if purl_class(p) == "os-pkgs":  # fillSrcPkg (the component carries no SrcVersion of its own)
+        if not pkg.get("SrcName"):
+            pkg["SrcName"] = pkg["Name"]
+        if not pkg.get("SrcVersion"):
+            pkg["SrcVersion"] = pkg["Version"]
+        if not pkg.get("SrcRelease"):
+            pkg["SrcRelease"] = pkg.get("Release", "")
+        if not pkg.get("SrcEpoch"):
+            pkg["SrcEpoch"] = pkg.get("Epoch", 0)
+    return pkg
+
+
+def _sort_pkgs(pkgs):
+    return sorted(pkgs, key=lambda p: (p["Name"].encode(), p["Version"].encode(), p.get("FilePath", "").encode()))
+
+
+def decode_cyclonedx(text):
+    """CycloneDX JSON -> {"OS": {Family, Name} | None, "Packages": [...], "Applications":
+    [{Type, FilePath, Libraries}], "Root": root component or None, "SerialNumber", "Version"}."""
+    try:
+        bom = json.loads(text)
+    except ValueError as e:
+        raise SBOMError("failed to decode CycloneDX JSON: %s" % e)
+    comps, order = {}, []
+    for c in bom.get("components") or []:
+        try:
+            pc = _component(c)
+        except SBOMError:
+            continue  # parseComponents logs and skips a component it cannot parse
+        if pc is not None:
+            comps[pc["bom_ref"]] = pc
+            order.append(pc)
+    root = None
+    mc = (bom.get("metadata") or {}).get("component")
+    if mc:
+        root = _component(mc)
+        if root is None:
+            raise SBOMError("failed to parse root component: unsupported component type")
+        comps[root["bom_ref"]] = root
+        order.append(root)
+    rels = {}
+    for d in bom.get("dependencies") or []:
+        if d.get("ref") in comps:
+            rels[id(comps[d["ref"]])] = [comps[x] for x in d.get("dependsOn") or [] if x in comps]
+
+    os_c, apps, pkgs = None, {}, {}
+    out = {"OS": None, "Packages": [], "Applications": [], "Root": root,
+           "SerialNumber": bom.get("serialNumber", ""), "Version": bom.get("version", 0)}
+    for c in order:
+        if c["type"] == "operating-system":
+            if os_c is not None:
+                raise SBOMError("failed to decode components: multiple OS components are not supported")
+            os_c = c
+            out["OS"] = {"Family": c["name"], "Name": c["version"]}
+            continue
+        if c["type"] == "application":
+            t = next((v for k, v in c["props"] if k == "Type"), "")
+            if t:
+                apps[id(c)] = {"Type": t, "FilePath": "" if t in AGGREGATING else c["name"], "Libraries": []}
+                continue
+        pkg = _library(c)
+        if pkg is not None:
+            pkgs[id(c)] = pkg
+    if os_c is not None:
+        os_pkgs = [pkgs.pop(id(d)) for d in rels.get(id(os_c), []) if id(d) in pkgs]
+        if os_pkgs:
+            out["Packages"] = os_pkgs
+    for cid, app in apps.items():
+        app["Libraries"] = [pkgs.pop(id(d)) for d in rels.get(cid, []) if id(d) in pkgs]
+        out["Applications"].append(app)
+    os_rest, lang_rest = {}, {}
+    for pkg in pkgs.values():
+        p = pkg["_purl"]
+        if purl_class(p) == "os-pkgs":
+            os_rest.setdefault(p["type"], []).append(pkg)
+        else:
+            lang_rest.setdefault(lang_type(p), []).append(pkg)
+    if len(os_rest) > 1:
+        raise SBOMError("failed to aggregate packages: multiple types of OS packages in SBOM are not supported")
+    if os_rest and out["OS"] is not None and out["OS"]["Family"]:
+        out["Packages"] = out["Packages"] + _sort_pkgs(next(iter(os_rest.values())))
+    for t, libs in lang_rest.items():
+        out["Applications"].append({"Type": t, "FilePath": "", "Libraries": _sort_pkgs(libs)})
+    out["Applications"].sort(key=lambda a: (a["Type"].encode(), a["FilePath"].encode()))
+    for p in out["Packages"] + [lib for a in out["Applications"] for lib in a["Libraries"]]:
+        p.pop("_purl", None)
+    return out
+
+
+def scan(engine, sbom, artifact_name="", now=None):
+    """The detector part of scanning a decoded SBOM: ospkg.Detect over the OS packages and
+    library.Detect per application, on the GPU.  Returns [(class, type, target, vulns)];
+    the OS target is "<artifact> (<family> <name>)" as pkg/scanner/local names it."""
+    from .detector import library, ospkg
+    results = []
+    if sbom["OS"] is not None and sbom["OS"]["Family"]:
+        fam, name = sbom["OS"]["Family"], sbom["OS"]["Name"]
+        vulns, _eosl = ospkg.detect(engine, fam, name, None, sbom["Packages"], now=now)
+        results.append(("os-pkgs", fam, "%s (%s %s)" % (artifact_name, fam, name), vulns))
+    for app in sbom["Applications"]:
+        vulns = library.detect(engine, app["Type"], app["Libraries"])
+        if vulns is not None:
+            results.append(("lang-pkgs", app["Type"], app["FilePath"], vulns))
+    return results
