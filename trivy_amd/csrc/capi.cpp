@@ -881,7 +881,7 @@ int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint
     const uint32_t r = id_rank[o->vex_id_index[i]];
     if (r != 0xFFFFFFFFu) vex.push_back((uint64_t(o->vex_pkgs[i]) << 32) | r);
   }
-  if (!b->filter.run(e->fill->dev(), b->m.pairs, b->fill_out, n, ignore, vex, o->severity_mask,
+  if (!b->filter.run(e->fill->dev(), b->m.pairs, b->fill_out, n, ignore, vex, vt.n_vuln_ranks(), o->severity_mask,
                      o->ignore_status_mask, st, msg)) {
     set_err(err, errlen, msg);
     return TVM_EDEVICE;

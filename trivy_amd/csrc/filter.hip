@@ -20,7 +20,8 @@
 //                  a survivor whose (package, vulnerability rank) the host-compiled VEX
 //                  suppression list holds (binary search) drops out too; survivors keep
 //                  the BySeverity sort key
-//                  (package rank << 32 | (4 - severity) << 29 | vulnerability rank);
+//                  (package rank << (b + 3) | (4 - severity) << b | vulnerability rank,
+//                  b = bits of the DB's vulnerability-rank count);
 //   radix sort     hipcub DeviceRadixSort over (key, pair index), dropped pairs last;
 //   filter_gather  the surviving {package, advisory} pairs in report order.
 // Integer work bound by HBM traffic (pairs, decisions, ranks); no MFMA.
@@ -49,6 +50,7 @@ struct FilterArgs {
   const unsigned long long* vex;  // sorted (package << 32 | vulnerability rank) VEX suppressions
   uint32_t n_vex;
   uint32_t sev_mask, status_mask;
+  uint32_t id_bits;             // sort key: package rank << (id_bits + 3) | (4 - severity) << id_bits | ID rank
   unsigned long long* table;    // {key, value} pairs, 2^k entries (dup pairs only)
   uint64_t table_mask;
   unsigned long long* sort_key;
@@ -99,7 +101,8 @@ __global__ __launch_bounds__(kFilterBlock) void filter_mark(FilterArgs a) {
     const unsigned long long val = (uint64_t(rk.y) << 32) | (0xFFFFFFFFu - p.x);
     a.mine[i] = val;
     a.idx[i] = uint32_t(i);
-    a.sort_key[i] = keep ? (uint64_t(a.pkg_rank[p.x]) << 32) | (uint64_t(4u - sev) << 29) | (rk.x & 0x1FFFFFFFu) : kEmpty;
+    a.sort_key[i] = keep ? (uint64_t(a.pkg_rank[p.x]) << (a.id_bits + 3)) | (uint64_t(4u - sev) << a.id_bits) | rk.x
+                         : kEmpty;
     if (keep && a.pkg_dup[p.x]) {  // table entries: {key + 1 (0 = empty), max value}, zeroed
       for (uint64_t s = mix64(key) & a.table_mask;; s = (s + 1) & a.table_mask) {
         const unsigned long long prev = atomicCAS(&a.table[2 * s], 0ull, key + 1);
@@ -195,8 +198,8 @@ bool BatchFilter::set_packages(const std::vector<uint32_t>& pkg_rank, const std:
 }
 
 bool BatchFilter::run(const FillDev& t, const uint2* pairs, const uint4* fill, uint64_t n,
-                      const std::vector<uint32_t>& ignore, const std::vector<uint64_t>& vex, uint32_t sev_mask,
-                      uint32_t status_mask, hipStream_t st, std::string& err) {
+                      const std::vector<uint32_t>& ignore, const std::vector<uint64_t>& vex, uint32_t n_ranks,
+                      uint32_t sev_mask, uint32_t status_mask, hipStream_t st, std::string& err) {
   n_ = n;
   survivors_ = 0;
   if (n == 0) return true;
@@ -209,10 +212,17 @@ bool BatchFilter::run(const FillDev& t, const uint2* pairs, const uint4* fill, u
     tcap = 16;
     while (tcap < 2 * n) tcap <<= 1;
   }
-  // sort only the key bits in use: package rank (< 2^pkg_bits) << 32 | severity | ID rank;
-  // a dropped pair's all-ones key stays the largest within any bit range
-  int end_bit = 33;
-  while (end_bit < 64 && (uint64_t(1) << (end_bit - 32)) <= n_pkgs_) end_bit++;
+  // sort only the key bits in use: package rank (< 2^pkg_bits, never all ones) << (id_bits
+  // + 3) | severity | ID rank (< 2^id_bits); a dropped pair's all-ones key stays the largest
+  uint32_t id_bits = 1;
+  while (id_bits < 32 && (uint64_t(1) << id_bits) < n_ranks) id_bits++;
+  int pkg_bits = 1;
+  while (pkg_bits < 32 && (uint64_t(1) << pkg_bits) <= n_pkgs_) pkg_bits++;
+  const int end_bit = int(id_bits) + 3 + pkg_bits;
+  if (end_bit > 64) {
+    err = "filter: sort key wider than 64 bits";
+    return false;
+  }
   size_t sort_bytes = 0;
   if (!ok(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, static_cast<unsigned long long*>(nullptr),
                                              static_cast<unsigned long long*>(nullptr), static_cast<uint32_t*>(nullptr),
@@ -258,6 +268,7 @@ bool BatchFilter::run(const FillDev& t, const uint2* pairs, const uint4* fill, u
   a.vex = static_cast<const unsigned long long*>(bufs_[12]);
   a.n_vex = uint32_t(vex.size());
   a.sev_mask = sev_mask;
+  a.id_bits = id_bits;
   a.status_mask = status_mask;
   a.table = static_cast<unsigned long long*>(bufs_[3]);
   a.table_mask = tcap ? tcap - 1 : 0;

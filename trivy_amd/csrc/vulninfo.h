@@ -110,6 +110,7 @@ class VulnTable {
   // in byte order (Go string order), and the ID -> rank map for ignore files.
   std::vector<uint2> adv_rank;
   uint32_t vuln_rank(std::string_view id) const;  // 0xFFFFFFFF when no advisory has it
+  uint32_t n_vuln_ranks() const { return uint32_t(rank_names_.size()); }
 
  private:
   bool built_ = false;
@@ -192,8 +193,8 @@ class BatchFilter {
   // to learn the survivor count.  ignore: sorted vulnerability ranks (VulnTable::vuln_rank);
   // vex: sorted (package << 32 | vulnerability rank) findings a VEX document drops.
   bool run(const FillDev& t, const uint2* pairs, const uint4* fill, uint64_t n, const std::vector<uint32_t>& ignore,
-           const std::vector<uint64_t>& vex, uint32_t sev_mask, uint32_t status_mask, hipStream_t st,
-           std::string& err);
+           const std::vector<uint64_t>& vex, uint32_t n_ranks, uint32_t sev_mask, uint32_t status_mask,
+           hipStream_t st, std::string& err);
   uint64_t survivors() const { return survivors_; }
   // The surviving {package, advisory} pairs in report order.
   bool fetch(std::vector<uint2>& out, hipStream_t st, std::string& err);
