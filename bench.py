@@ -184,10 +184,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", 0))
     import torch
     import torch.distributed as dist
+    # TVM_BENCH_BACKEND=gloo rehearses the N>1 path on a box with fewer GPUs than ranks
+    # (ranks then share devices round-robin); the scaling runs use RCCL, one rank per GPU
+    backend = os.environ.get("TVM_BENCH_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group(backend)
     if torch.cuda.is_available():
+        local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
 
     import trivy_amd
@@ -240,7 +244,7 @@ def main():
     mb.launch(args.warmup)
 
     sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
-    dev = f"cuda:{local}" if torch.cuda.is_available() else "cpu"
+    dev = f"cuda:{local}" if torch.cuda.is_available() and backend == "nccl" else "cpu"  # where max-over-ranks reduces
     launch_ms = []
     wall = td.timed(lambda: launch_ms.append(mb.time(args.steps)), steps=1, warmup=0, sync=sync, device=dev)
     vname = lib().tvm_variant_name(lib().tvm_engine_last_variant(eng.h)).decode()
@@ -250,7 +254,7 @@ def main():
     gather = None
     if args.gather:  # optional RCCL gather of every rank's match list to rank 0, timed apart
         import ctypes
-        pairs = torch.empty((total, 2), dtype=torch.int32, device=dev)
+        pairs = torch.empty((total, 2), dtype=torch.int32, device=f"cuda:{local}")
         got = ctypes.c_uint64()
         if lib().tvm_match_copy_device(eng.h, mb.h, pairs.data_ptr(), total, ctypes.byref(got)) or got.value != total:
             raise RuntimeError("tvm_match_copy_device failed")
