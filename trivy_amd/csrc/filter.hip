@@ -13,6 +13,8 @@
 // All strings are replaced by ranks fixed before the launch: the vulnerability ID and
 // output FixedVersion of every advisory (load time, vulninfo.cpp) and the (name, version)
 // of every package within its result (host, once per batch).  Then:
+//   filter_count_dup  pairs of packages whose (result, name, version) repeats (sizes the
+//                  dedup table for them alone; one host synchronisation);
 //   filter_mark    per pair: severity/status/ignore test; duplicates (packages whose
 //                  (result, name, version) repeats) race into an open-addressing table
 //                  with one 64-bit atomicMax of (FixedVersion rank, -package) per key;
@@ -157,6 +159,25 @@ __global__ __launch_bounds__(kFilterBlock) void filter_select(FilterArgs a) {
   }
 }
 
+// Pairs whose package's (result, name, version) repeats: the only ones that enter the dedup
+// table, so the table is sized (and cleared) for them alone.
+__global__ __launch_bounds__(kFilterBlock) void filter_count_dup(const uint2* pairs, const uint8_t* pkg_dup,
+                                                                 uint64_t n, unsigned long long* count) {
+  __shared__ uint32_t wsum[kFilterBlock / 64];
+  const uint64_t stride = uint64_t(gridDim.x) * kFilterBlock;
+  uint32_t c = 0;
+  for (uint64_t i = uint64_t(blockIdx.x) * kFilterBlock + threadIdx.x; i < n; i += stride) c += pkg_dup[pairs[i].x];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < kFilterBlock / 64; w++) t += wsum[w];
+    if (t) atomicAdd(count, (unsigned long long)t);
+  }
+}
+
 __global__ __launch_bounds__(kFilterBlock) void filter_gather(const uint2* pairs, const uint32_t* idx, uint64_t n,
                                                               uint2* out) {
   const uint64_t i = uint64_t(blockIdx.x) * kFilterBlock + threadIdx.x;
@@ -207,10 +228,22 @@ bool BatchFilter::run(const FillDev& t, const uint2* pairs, const uint4* fill, u
     err = "filter: too many pairs";
     return false;
   }
-  uint64_t tcap = 0;
+  const uint32_t blocks = uint32_t(std::min<uint64_t>((n + kFilterBlock - 1) / kFilterBlock, 256ull * 64));
+  uint64_t tcap = 0;  // dedup table: 2^k >= 2 x the pairs that can enter it (load <= 0.5, probes end)
   if (any_dup_) {
-    tcap = 16;
-    while (tcap < 2 * n) tcap <<= 1;
+    unsigned long long dup_n = 0;
+    if (!grow(bufs_[10], caps_[10], 8, err) || !ok(hipMemsetAsync(bufs_[10], 0, 8, st), "memset(dup count)", err))
+      return false;
+    hipLaunchKernelGGL(filter_count_dup, dim3(blocks), dim3(kFilterBlock), 0, st, pairs,
+                       static_cast<const uint8_t*>(bufs_[1]), n, static_cast<unsigned long long*>(bufs_[10]));
+    if (!ok(hipGetLastError(), "filter_count_dup", err) ||
+        !ok(hipMemcpyAsync(&dup_n, bufs_[10], 8, hipMemcpyDeviceToHost, st), "D2H dup count", err) ||
+        !ok(hipStreamSynchronize(st), "filter sync", err))
+      return false;
+    if (dup_n) {
+      tcap = 16;
+      while (tcap < 2 * dup_n) tcap <<= 1;
+    }
   }
   // sort only the key bits in use: package rank (< 2^pkg_bits, never all ones) << (id_bits
   // + 3) | severity | ID rank (< 2^id_bits); a dropped pair's all-ones key stays the largest
@@ -276,7 +309,6 @@ bool BatchFilter::run(const FillDev& t, const uint2* pairs, const uint4* fill, u
   a.mine = static_cast<unsigned long long*>(bufs_[6]);
   a.idx = static_cast<uint32_t*>(bufs_[7]);
   a.count = static_cast<unsigned long long*>(bufs_[10]);
-  const uint32_t blocks = uint32_t(std::min<uint64_t>((n + kFilterBlock - 1) / kFilterBlock, 256ull * 64));
   hipLaunchKernelGGL(filter_mark, dim3(blocks), dim3(kFilterBlock), 0, st, a);
   hipLaunchKernelGGL(filter_select, dim3(blocks), dim3(kFilterBlock), 0, st, a);
   if (!ok(hipGetLastError(), "filter launch", err)) return false;
