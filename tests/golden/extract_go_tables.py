@@ -44,6 +44,7 @@ FILES = [
     "pkg/scanner/utils/utils_test.go",
     "pkg/vulnerability/vulnerability_test.go",
     "pkg/result/filter_test.go",
+    "pkg/fanal/analyzer/pkg/dpkg/dpkg_test.go",
 ]
 
 # trivy-db / trivy constants used in the tables (values from trivy-db pkg/types and
