@@ -45,6 +45,7 @@ FILES = [
     "pkg/vulnerability/vulnerability_test.go",
     "pkg/result/filter_test.go",
     "pkg/fanal/analyzer/pkg/dpkg/dpkg_test.go",
+    "pkg/fanal/analyzer/pkg/apk/apk_test.go",
 ]
 
 # trivy-db / trivy constants used in the tables (values from trivy-db pkg/types and
@@ -397,21 +398,38 @@ def _local_vars(toks, start, end):
     return env
 
 
+def _toplevel_vars(toks):
+    """name -> value of every single `var name = value` declaration (package level)."""
+    env = {}
+    for k in range(len(toks) - 2):
+        if toks[k].v == "var" and toks[k + 1].k == "id" and toks[k + 2].v == "=" and toks[k + 1].v != "tests":
+            p = Parser(toks)
+            p.i = k + 3
+            try:
+                env[toks[k + 1].v] = _subst(p.value(), env)
+            except Exception:  # not a literal: not data
+                pass
+    return env
+
+
 def extract(path):
     src = open(path, encoding="utf-8").read()
     toks = tokenize(src)
     tables = []
+    top = _toplevel_vars(toks)
     i = 0
     # the enclosing test function of each table
     while i < len(toks):
         t = toks[i]
-        if t.k == "id" and t.v == "tests" and i + 1 < len(toks) and toks[i + 1].v == ":=":
+        is_var = i > 0 and toks[i - 1].v == "var" and i + 1 < len(toks) and toks[i + 1].v == "="
+        if t.k == "id" and t.v == "tests" and i + 1 < len(toks) and (toks[i + 1].v == ":=" or is_var):
             fn, fstart = None, 0
             for j in range(i, 0, -1):
                 if toks[j].v == "func" and toks[j + 1].k == "id" and toks[j + 1].v.startswith("Test"):
                     fn, fstart = toks[j + 1].v, j
                     break
-            env = _local_vars(toks, fstart, i)
+            env = dict(top)
+            env.update(_local_vars(toks, fstart, i))
             p = Parser(toks)
             p.i = i + 2
             typ = p.parse_type()
