@@ -299,6 +299,27 @@ def main():
         fill["result_filter"]["vex"] = {"suppressions": len(pick), "ms": vex_ms, "kept": vkept,
                                         "matches_per_s": total / (vex_ms / 1e3)}
 
+    dropin = None
+    if args.config == "c2" and rank == 0:
+        # C1-shaped request through the drop-in per-target path (debian Scanner.Detect,
+        # debian.go:57-119): 100 packages of one Debian 12 image, host prologue + one launch +
+        # sync + host epilogue per call - the latency a single `trivy image` scan sees
+        from trivy_amd.detector.ospkg import Scanner
+        p12 = wl.plats.index("debian 12")
+        b0, b1 = next((b0, b1) for p, b0, b1 in wl.batch.targets if p == p12 and b1 - b0 >= 100)
+        pk = [{"Name": wl.batch.names[i].decode(), "SrcName": wl.batch.names[i].decode(),
+               "Version": wl.batch.versions[i].decode(), "SrcVersion": wl.batch.versions[i].decode()}
+              for i in range(b0, b0 + 100)]
+        sc = Scanner(eng, "debian")
+        found = sc.detect("12", None, pk)
+        t_d = time.perf_counter()
+        n_calls = 200
+        for _ in range(n_calls):
+            sc.detect("12", None, pk)
+        d_ms = (time.perf_counter() - t_d) * 1e3 / n_calls
+        dropin = {"workload": "c1-shaped: 100 debian-12 packages per call", "ms_per_call": d_ms,
+                  "vulnerabilities_per_call": len(found), "packages_per_s": 100 / (d_ms / 1e3)}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = wl.cpu_baseline(args.cpu_seconds, args.cpu_threads)
@@ -332,6 +353,8 @@ def main():
             line["gather"] = gather
         if fill is not None:
             line["fill_info"] = fill
+        if dropin is not None:
+            line["dropin_latency"] = dropin
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
