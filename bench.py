@@ -317,8 +317,22 @@ def main():
         for _ in range(n_calls):
             sc.detect("12", None, pk)
         d_ms = (time.perf_counter() - t_d) * 1e3 / n_calls
+        # the same call at the C-ABI alone (what a cgo caller pays): no Python result objects
+        import ctypes
+        from trivy_amd import _lib as L
+        from trivy_amd.detector import ospkg as osp
+        arr, _keep = osp._pkg_array(pk)
+        res, ebuf, now = L.Result(), L.errbuf(), osp._now(None)
+        t_c = time.perf_counter()
+        for _ in range(n_calls):
+            if lib().tvm_ospkg_driver_detect(eng.h, b"debian", b"12", None, arr, len(pk), now, ctypes.byref(res), ebuf,
+                                             len(ebuf)):
+                raise RuntimeError(ebuf.value.decode())
+            lib().tvm_result_free(ctypes.byref(res))
+        c_ms = (time.perf_counter() - t_c) * 1e3 / n_calls
         dropin = {"workload": "c1-shaped: 100 debian-12 packages per call", "ms_per_call": d_ms,
-                  "vulnerabilities_per_call": len(found), "packages_per_s": 100 / (d_ms / 1e3)}
+                  "c_abi_ms_per_call": c_ms, "vulnerabilities_per_call": len(found),
+                  "packages_per_s": 100 / (d_ms / 1e3)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
