@@ -56,7 +56,7 @@ struct FilterArgs {
   unsigned long long* table;    // {key, value} pairs, 2^k entries (dup pairs only)
   uint64_t table_mask;
   unsigned long long* sort_key;
-  unsigned long long* mine;     // the pair's own (FixedVersion rank, -package) value
+  unsigned long long* mine;     // dup pairs: the table slot filter_mark put the pair's key in
   uint32_t* idx;
   unsigned long long* count;
 };
@@ -101,7 +101,6 @@ __global__ __launch_bounds__(kFilterBlock) void filter_mark(FilterArgs a) {
     }
     const unsigned long long key = (uint64_t(a.pkg_rank[p.x]) << 32) | rk.x;
     const unsigned long long val = (uint64_t(rk.y) << 32) | (0xFFFFFFFFu - p.x);
-    a.mine[i] = val;
     a.idx[i] = uint32_t(i);
     a.sort_key[i] = keep ? (uint64_t(a.pkg_rank[p.x]) << (a.id_bits + 3)) | (uint64_t(4u - sev) << a.id_bits) | rk.x
                          : kEmpty;
@@ -110,6 +109,7 @@ __global__ __launch_bounds__(kFilterBlock) void filter_mark(FilterArgs a) {
         const unsigned long long prev = atomicCAS(&a.table[2 * s], 0ull, key + 1);
         if (prev == 0ull || prev == key + 1) {
           atomicMax(&a.table[2 * s + 1], val);
+          a.mine[i] = s;  // filter_select reads the winner straight from this slot
           break;
         }
       }
@@ -124,11 +124,9 @@ __global__ __launch_bounds__(kFilterBlock) void filter_select(FilterArgs a) {
   for (uint64_t i = uint64_t(blockIdx.x) * kFilterBlock + threadIdx.x; i < a.n; i += stride) {
     bool live = a.sort_key[i] != kEmpty;
     const uint2 p = a.pairs[i];
-    if (live && a.pkg_dup[p.x]) {
-      const unsigned long long key = (uint64_t(a.pkg_rank[p.x]) << 32) | a.t.adv_rank[p.y].x;
-      uint64_t s = mix64(key) & a.table_mask;
-      while (a.table[2 * s] != key + 1) s = (s + 1) & a.table_mask;  // inserted by filter_mark
-      if (a.table[2 * s + 1] != a.mine[i]) {
+    if (live && a.pkg_dup[p.x]) {  // the slot filter_mark inserted this pair's key into
+      const unsigned long long own = (uint64_t(a.t.adv_rank[p.y].y) << 32) | (0xFFFFFFFFu - p.x);
+      if (a.table[2 * a.mine[i] + 1] != own) {
         a.sort_key[i] = kEmpty;  // another duplicate won (greater FixedVersion, or first seen)
         live = false;
       }
