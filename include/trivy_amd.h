@@ -292,13 +292,19 @@ typedef struct {
    * entry k drops package vex_pkgs[k]'s finding of vulnerability vex_ids[vex_id_index[k]].
    * The host compiles a VEX document against the batch's package PURLs into these entries
    * (trivy_amd/vex.py: OpenVEX openvex.go:21-54, CycloneDX cyclonedx.go:48-84, CSAF
-   * csaf.go:27-83); the per-finding test runs on the GPU.  vex_ids holds each distinct ID
-   * once.  n_vex = 0: no VEX document. */
+   * csaf.go:27-83); the per-finding test runs on the GPU.  n_vex = 0: no VEX document. */
   const uint32_t* vex_pkgs;
   const uint32_t* vex_id_index;
   size_t n_vex;
-  const tvm_str* vex_ids;
-  size_t n_vex_ids;
+  /* Ignore-file findings scoped by PURL (ignore.go MatchVulnerability, applied before the
+   * dedup as filter.go:117-122 does): entry k drops package ignore_pair_pkgs[k]'s finding of
+   * pair_ids[ignore_pair_id_index[k]] (trivy_amd/ignore.py compiles them). */
+  const uint32_t* ignore_pair_pkgs;
+  const uint32_t* ignore_pair_id_index;
+  size_t n_ignore_pairs;
+  /* The distinct vulnerability IDs the two pair lists index, each once. */
+  const tvm_str* pair_ids;
+  size_t n_pair_ids;
 } tvm_filter_opts;
 /* filterVulnerabilities + sort.Sort(BySeverity) (+ the VEX filter) for every result of the
  * batch, on the GPU, after tvm_match_launch + tvm_match_fill.  n_kept = surviving

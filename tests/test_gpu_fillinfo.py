@@ -307,3 +307,48 @@ def test_match_filter_batch_vex_vs_oracle(kind):
         assert adv == w["_pair"][1] and sdb.adv_vid[adv].decode() == w["VulnerabilityID"], (pk, adv, w)
         assert purls[pk] == purls[w["_pair"][0]]
     mb.close()
+
+
+def test_match_filter_batch_ignore_purls_vs_oracle():
+    """Ignore-file findings scoped by PURL (ignore.go MatchVulnerability, before the dedup,
+    filter.go:117-122) on the GPU batch filter: plain IDs + PURL-scoped findings (versioned,
+    versionless, qualifier-scoped) equal oracle/filter.py per result."""
+    import oracle.filter as of
+    from tools import synth_vex as sv
+    from trivy_amd.ignore import split_findings
+    mb, bucket, by_target, sdb = _filter_fixture()
+    purls = [None] * len(mb)
+    for vulns in by_target:
+        plat = "debian 12" if vulns and vulns[0]["DataSource"]["ID"] == "debian" else "ubuntu 22.04"
+        for v in vulns:
+            purls[v["_pair"][0]] = sv.purl_of(plat, v["PkgName"], v["InstalledVersion"],
+                                              "amd64" if len(v["PkgName"]) % 3 else None)
+    rng = np.random.default_rng(21)
+    flat = [v for vulns in by_target for v in vulns]
+    findings = []
+    for k in range(120):
+        v = flat[rng.integers(len(flat))]
+        pu = purls[v["_pair"][0]]
+        base, _, q = pu.partition("?")
+        pat = [pu, base, base.rpartition("@")[0], base.rpartition("@")[0] + "?arch=amd64"][k % 4]
+        findings.append({"ID": v["VulnerabilityID"], "Paths": [], "PURLs": [pat], "ExpiredAt": None, "Statement": ""})
+    findings.append({"ID": flat[0]["VulnerabilityID"], "Paths": [], "PURLs": [], "ExpiredAt": None, "Statement": ""})
+    plain, pairs = split_findings(findings, purls)
+    opts = dict(severities=("UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"))
+    n = mb.filter(mb.filter_opts(ignore_ids=plain, ignore_pairs=pairs, **opts))
+    got = mb.filtered_pairs(n).tolist()
+    ofind = [dict(f, PURLs=[of.purl_from_string(x) for x in f["PURLs"]]) for f in findings]
+    want, ignored = [], 0
+    for vulns in by_target:
+        filled = vi.fill_info(bucket, [{k: x for k, x in v.items() if k != "_pair"} for v in vulns])
+        for f, v in zip(filled, vulns):
+            f["_pair"] = v["_pair"]
+            f["PkgIdentifier"] = {"PURL": of.purl_from_string(purls[v["_pair"][0]])}
+        kept, ig = of.filter_vulnerabilities("", filled, list(opts["severities"]), (), ofind)
+        ignored += len(ig)
+        want += kept or []
+    assert ignored > 0
+    assert len(got) == len(want), (len(got), len(want))
+    for (pk, adv), w in zip(got, want):
+        assert adv == w["_pair"][1] and purls[pk] == purls[w["_pair"][0]], (pk, adv, w)
+    mb.close()

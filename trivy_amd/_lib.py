@@ -75,7 +75,8 @@ class FilterOpts(ctypes.Structure):
     _fields_ = [("severity_mask", ctypes.c_uint32), ("ignore_status_mask", ctypes.c_uint32),
                 ("ignore_ids", ctypes.POINTER(Str)), ("n_ignore_ids", ctypes.c_size_t),
                 ("vex_pkgs", ctypes.c_void_p), ("vex_id_index", ctypes.c_void_p), ("n_vex", ctypes.c_size_t),
-                ("vex_ids", ctypes.POINTER(Str)), ("n_vex_ids", ctypes.c_size_t)]
+                ("ignore_pair_pkgs", ctypes.c_void_p), ("ignore_pair_id_index", ctypes.c_void_p),
+                ("n_ignore_pairs", ctypes.c_size_t), ("pair_ids", ctypes.POINTER(Str)), ("n_pair_ids", ctypes.c_size_t)]
 
 
 # (name, restype, argtypes) for every exported symbol of include/trivy_amd.h

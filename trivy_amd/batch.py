@@ -168,25 +168,29 @@ class MatchBatch:
     # ---- result.Filter per result (tvm_match_filter*) ----
     @staticmethod
     def filter_opts(severities=("UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"), ignore_statuses=(), ignore_ids=(),
-                    vex=None):
-        """FilterOption's vulnerability part; vex: (package indices, vulnerability IDs) from
+                    vex=None, ignore_pairs=None):
+        """FilterOption's vulnerability part.  ignore_ids: the ignore file's plain IDs;
+        ignore_pairs: (package indices, IDs) of its PURL-scoped findings
+        (trivy_amd.ignore.pair_suppressions); vex: (package indices, IDs) from
         trivy_amd.vex.VEX.suppressions (None: no VEX document)."""
         from ._lib import FilterOpts, Str
         names = ["UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"]
         ids = [i.encode() if isinstance(i, str) else bytes(i) for i in ignore_ids]
         arr = (Str * max(len(ids), 1))(*[Str(b, len(b)) for b in ids])
-        vpk, vids = vex if vex is not None else (np.zeros(0, dtype=np.uint32), [])
-        vpk = np.ascontiguousarray(vpk, dtype=np.uint32)
-        if len(vpk) != len(vids):
-            raise ValueError("vex: one vulnerability ID per package index")
-        uniq = {}
-        vidx = np.array([uniq.setdefault(i, len(uniq)) for i in vids], dtype=np.uint32)
+        uniq, lists = {}, []
+        for pairs in (vex, ignore_pairs):
+            ppk, pids = pairs if pairs is not None else (np.zeros(0, dtype=np.uint32), [])
+            ppk = np.ascontiguousarray(ppk, dtype=np.uint32)
+            if len(ppk) != len(pids):
+                raise ValueError("one vulnerability ID per package index")
+            lists.append((ppk, np.array([uniq.setdefault(i, len(uniq)) for i in pids], dtype=np.uint32)))
         ublobs = [i.encode() if isinstance(i, str) else bytes(i) for i in uniq]
-        varr = (Str * max(len(ublobs), 1))(*[Str(b, len(b)) for b in ublobs])
+        uarr = (Str * max(len(ublobs), 1))(*[Str(b, len(b)) for b in ublobs])
+        (vpk, vidx), (ipk, iidx) = lists
+        ptr = lambda a: a.ctypes.data if len(a) else None  # noqa: E731
         o = FilterOpts(sum(1 << names.index(x) for x in severities), sum(1 << s for s in ignore_statuses), arr,
-                       len(ids), vpk.ctypes.data if len(vpk) else None, vidx.ctypes.data if len(vidx) else None,
-                       len(vpk), varr, len(ublobs))
-        o._keep = (ids, arr, vpk, vidx, ublobs, varr)
+                       len(ids), ptr(vpk), ptr(vidx), len(vpk), ptr(ipk), ptr(iidx), len(ipk), uarr, len(ublobs))
+        o._keep = (ids, arr, lists, ublobs, uarr)
         return o
 
     def filter(self, opts):

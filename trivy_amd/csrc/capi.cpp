@@ -832,7 +832,8 @@ void package_ranks(const tvm_batch* b, std::vector<uint32_t>& rank, std::vector<
 int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint64_t* n_kept, char* err,
                      size_t errlen) {
   if (!e || !b || !o || !b->uploaded || (o->n_ignore_ids && !o->ignore_ids) ||
-      (o->n_vex && (!o->vex_pkgs || !o->vex_id_index)) || (o->n_vex_ids && !o->vex_ids))
+      (o->n_vex && (!o->vex_pkgs || !o->vex_id_index)) ||
+      (o->n_ignore_pairs && (!o->ignore_pair_pkgs || !o->ignore_pair_id_index)) || (o->n_pair_ids && !o->pair_ids))
     return TVM_EINVAL;
   std::shared_lock<std::shared_mutex> lk(e->mu);
   (void)hipSetDevice(e->device);
@@ -867,19 +868,26 @@ int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint
   // VEX suppressions as (package << 32 | vulnerability rank) keys, sorted on the GPU; each
   // distinct ID is ranked once; IDs unknown to the DB cannot name a detected vulnerability
   // and drop out here
-  std::vector<uint32_t> id_rank(o->n_vex_ids);
-  for (size_t i = 0; i < o->n_vex_ids; i++)
-    id_rank[i] = vt.vuln_rank(std::string_view(o->vex_ids[i].p ? o->vex_ids[i].p : "", o->vex_ids[i].n));
+  // Ignore-file pairs share the array, tagged with bit 31 of the rank word (ranks use < 31
+  // bits): filter_mark looks up the tagged key (before the dedup), filter_select the plain one.
+  std::vector<uint32_t> id_rank(o->n_pair_ids);
+  for (size_t i = 0; i < o->n_pair_ids; i++)
+    id_rank[i] = vt.vuln_rank(std::string_view(o->pair_ids[i].p ? o->pair_ids[i].p : "", o->pair_ids[i].n));
   std::vector<uint64_t> vex;
-  vex.reserve(o->n_vex);
+  vex.reserve(o->n_vex + o->n_ignore_pairs);
   const uint64_t n_pkgs = uint64_t(tvm_batch_size(b));
-  for (size_t i = 0; i < o->n_vex; i++) {
-    if (o->vex_pkgs[i] >= n_pkgs || o->vex_id_index[i] >= o->n_vex_ids) {
-      set_err(err, errlen, "tvm_match_filter: VEX package or ID index out of range");
-      return TVM_EINVAL;
+  for (int list = 0; list < 2; list++) {
+    const uint32_t* pk = list ? o->ignore_pair_pkgs : o->vex_pkgs;
+    const uint32_t* ix = list ? o->ignore_pair_id_index : o->vex_id_index;
+    const size_t cnt = list ? o->n_ignore_pairs : o->n_vex;
+    for (size_t i = 0; i < cnt; i++) {
+      if (pk[i] >= n_pkgs || ix[i] >= o->n_pair_ids) {
+        set_err(err, errlen, "tvm_match_filter: VEX / ignore pair package or ID index out of range");
+        return TVM_EINVAL;
+      }
+      const uint32_t r = id_rank[ix[i]];
+      if (r < 0x80000000u) vex.push_back((uint64_t(pk[i]) << 32) | r | (list ? 0x80000000ull : 0ull));
     }
-    const uint32_t r = id_rank[o->vex_id_index[i]];
-    if (r != 0xFFFFFFFFu) vex.push_back((uint64_t(o->vex_pkgs[i]) << 32) | r);
   }
   if (!b->filter.run(e->fill->dev(), b->m.pairs, b->fill_out, n, ignore, vex, vt.n_vuln_ranks(), o->severity_mask,
                      o->ignore_status_mask, st, msg)) {

@@ -49,7 +49,8 @@ struct FilterArgs {
   const uint8_t* pkg_dup;       // per package: its (result, name, version) repeats
   const uint32_t* ignore;       // sorted vulnerability ranks of the ignore file
   uint32_t n_ignore;
-  const unsigned long long* vex;  // sorted (package << 32 | vulnerability rank) VEX suppressions
+  const unsigned long long* vex;  // sorted (package << 32 | tag << 31 | vulnerability rank):
+                                  // tag 0 VEX suppression, tag 1 ignore-file pair
   uint32_t n_vex;
   uint32_t sev_mask, status_mask;
   uint32_t id_bits;             // sort key: package rank << (id_bits + 3) | (4 - severity) << id_bits | ID rank
@@ -98,6 +99,16 @@ __global__ __launch_bounds__(kFilterBlock) void filter_mark(FilterArgs a) {
         else hi = mid;
       }
       keep = !(lo < a.n_ignore && a.ignore[lo] == rk.x);
+    }
+    if (keep && a.n_vex) {  // ignore findings scoped by PURL: tagged keys, before the dedup
+      const unsigned long long key = (uint64_t(p.x) << 32) | 0x80000000ull | rk.x;
+      uint32_t lo = 0, hi = a.n_vex;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.vex[mid] < key) lo = mid + 1;
+        else hi = mid;
+      }
+      keep = !(lo < a.n_vex && a.vex[lo] == key);
     }
     const unsigned long long key = (uint64_t(a.pkg_rank[p.x]) << 32) | rk.x;
     const unsigned long long val = (uint64_t(rk.y) << 32) | (0xFFFFFFFFu - p.x);
