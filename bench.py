@@ -68,11 +68,6 @@ class C2:
         for p, b0, b1 in self.batch.targets:
             mb.add_arena(self.sdb.platforms[p], b1 - b0, arena, noff[b0:], nlen[b0:], voff[b0:], vlen[b0:])
 
-    def check(self, pairs, threads):
-        from oracle import match as om
-        opk, oad = om.match(om.Prepared(self.sdb, self.batch), n_threads=threads)
-        return bool(np.array_equal(pairs[:, 0], opk) and np.array_equal(pairs[:, 1], oad))
-
     def cpu_baseline(self, budget_s, threads):
         from oracle import match as om
         from tools.synth import SynthBatch
@@ -115,9 +110,6 @@ class Mix:
 
     def fill(self, mb):
         self.sm.add_to(mb, self.sdb, self.batch)
-
-    def check(self, pairs, threads):
-        return None  # tests/test_gpu_mix.py holds the parity check for these mixes
 
     def cpu_baseline(self, budget_s, threads):
         import oracle.drivers as od
@@ -171,7 +163,6 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-fill", action="store_true", help="c2: skip the FillInfo leg (no vulnerability bucket)")
-    ap.add_argument("--check", action="store_true", help="verify the bench batch against the oracle (c2)")
     ap.add_argument("--gather", action="store_true",
                     help="after the timed region, gather all match lists to rank 0 (RCCL), reported apart")
     ap.add_argument("--variant", type=int, default=None, help="match-kernel variant (tvm_engine_set_variant)")
@@ -216,12 +207,6 @@ def main():
     if bits or errp != -1:
         raise RuntimeError(f"engine error bits={bits} poisoned_pkg={errp}")
     log(rank, f"[bench] batch: {n_pkgs} packages, {total} matches ({time.perf_counter()-t0:.1f}s)")
-
-    if args.check and rank == 0:
-        ok = wl.check(mb.pairs(), args.cpu_threads)
-        log(rank, f"[bench] check vs oracle: {'OK' if ok else 'MISMATCH' if ok is False else 'n/a'}")
-        if ok is False:
-            raise SystemExit(1)
 
     # ---- warmup + timed region -------------------------------------------------------------
     if args.sweep and rank == 0:
