@@ -163,6 +163,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-fill", action="store_true", help="c2: skip the FillInfo leg (no vulnerability bucket)")
+    ap.add_argument("--dropin", action="store_true",
+                    help="c2: also time 100-package requests through the per-target driver path (off by default: "
+                         "its many tiny match launches would mix into a kernel-trace average of this command)")
     ap.add_argument("--gather", action="store_true",
                     help="after the timed region, gather all match lists to rank 0 (RCCL), reported apart")
     ap.add_argument("--variant", type=int, default=None, help="match-kernel variant (tvm_engine_set_variant)")
@@ -285,7 +288,7 @@ def main():
                                         "matches_per_s": total / (vex_ms / 1e3)}
 
     dropin = None
-    if args.config == "c2" and rank == 0:
+    if args.dropin and args.config == "c2" and rank == 0:
         # C1-shaped request through the drop-in per-target path (debian Scanner.Detect,
         # debian.go:57-119): 100 packages of one Debian 12 image, host prologue + one launch +
         # sync + host epilogue per call - the latency a single `trivy image` scan sees
