@@ -232,6 +232,40 @@ int tvm_lib_is_vulnerable_host(int grammar, const char* ver, size_t ver_len, con
 /* Advisory fields for host-side inspection of batch results. */
 const char* tvm_db_advisory_vuln_id(const tvm_db* db, uint32_t adv);
 
+/* ---- multi-GPU sharding support ----------------------------------------------------------
+ * Row counts (advisory intervals) of n packages of one bucket from the host index - the
+ * pre-probe that balances a batch's shards by predicted work rather than by package count. */
+int tvm_db_rows_many(const tvm_db* db, const char* bucket, size_t n, const char* arena, const uint64_t* name_off,
+                     const uint32_t* name_len, uint32_t* out);
+/* Adds `base` to the package index of every match the batch reports (a shard of a global
+ * batch reports global indices); default 0. */
+int tvm_batch_set_package_base(tvm_batch* b, uint32_t base);
+/* tvm_batch_upload, but the match columns (package, advisory; uint32 each, cap entries) are
+ * written into caller-owned device buffers on the engine's GPU (e.g. tensors a collective
+ * then gathers); the batch never frees them. */
+int tvm_batch_upload_into(tvm_engine* e, tvm_batch* b, void* pkg_dev, void* adv_dev, uint64_t cap, char* err,
+                          size_t errlen);
+
+/* ---- end-to-end pipelined pass ---------------------------------------------------------
+ * The whole detector path for a host-side batch in one call: the batch goes to the GPU in
+ * chunks (DMA from the batch's own host arrays, pinned in place by prepare), each chunk is
+ * matched as soon as it lands, and its per-package advisory lists come back (CSR) while
+ * the next chunk is matched.  This is what a cgo caller pays per batch of targets
+ * (detect.go:63 / library/detect.go:11 called for every target of a scan). */
+/* Pins the batch (no more adds afterwards) and sizes every device / pinned buffer. */
+int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32_t chunk_packages, char* err,
+                         size_t errlen);
+/* One pass; ms = wall time of the call.  TVM_EINVAL with *n_matches set when the matches do
+ * not fit match_cap (prepare again with a larger one). */
+int tvm_pipeline_run(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* err_pkg, double* ms, char* err,
+                     size_t errlen);
+/* The last pass's result (library-owned pinned memory, valid until the next pass or
+ * tvm_batch_free): package p's advisory indices are adv[row_end[p-1] .. row_end[p])
+ * (row_end[-1] = 0), in (package, advisory) order. */
+int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row_end, uint64_t* n_matches);
+/* Bytes the last pass copied: [0] host to device, [1] device to host, [2] chunks. */
+int tvm_pipeline_stats(tvm_batch* b, uint64_t out[3]);
+
 /* ---- vulnerability detail: FillInfo ------------------------------------------------ */
 /* One detected vulnerability as FillInfo reads it (vulnerability.go:60-109). */
 typedef struct {

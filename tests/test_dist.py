@@ -1,6 +1,8 @@
 """CPU: the multi-GPU layer (trivy_amd/dist.py) with world_size 2 over gloo.
 
-The GPU runs use the same code with the RCCL ("nccl") backend, one process per GPU."""
+The GPU runs use the same code with the RCCL ("nccl") backend, one process per GPU; here
+each rank's match step is the oracle (oracle/match.c) on its shard of ONE global batch, and
+the gathered lists must equal the single-process match of the whole batch."""
 import os
 import socket
 
@@ -31,6 +33,15 @@ def test_balanced_shards_follow_weights():
     assert td.balanced_shards([], 3) == [0, 0, 0, 0]
 
 
+def test_target_shards_keep_targets_whole():
+    tb = [0, 3, 10, 11, 40]
+    w = np.ones(50)
+    w[12] = 100.0
+    b = td.target_shards(tb, 50, w, 3)
+    assert b[0] == 0 and b[-1] == 50 and all(x in tb + [50] for x in b) and b == sorted(b)
+    assert td.target_shards([], 0, [], 2) == [0, 0, 0]
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -39,35 +50,61 @@ def _free_port():
     return p
 
 
+def _global_batch():
+    from tools.synth import make_db, make_batch
+    sdb = make_db(["debian 12", "ubuntu 22.04"], 800, seed=21)
+    batch = make_batch(sdb, 23, 97, [1, 1], seed=22)
+    return sdb, batch
+
+
+def _rows(sdb, batch):
+    """Predicted work per package: advisories of its key (the host pre-probe) + 1."""
+    cnt = {}
+    for k, name in enumerate(sdb.key_names):
+        cnt[(int(sdb.key_plat[k]), name)] = int(sdb.adv_begin[k + 1] - sdb.adv_begin[k])
+    return np.array([cnt.get((int(p), n), 0) + 1 for p, n in zip(batch.plat, batch.names)], dtype=np.float64)
+
+
 def _worker(rank, ws, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     try:
-        b, e = td.shard(10, rank, ws)
-        # rank r matches packages [b, e); rank 1 has one more match than rank 0
-        local = torch.tensor([[i - b, 100 + i] for i in range(b, e)] + ([[0, 7]] if rank == 1 else []),
-                             dtype=torch.int64)
-        merged = td.gather_pairs(local, b)
+        from oracle import match as om
+        from tools.synth import SynthBatch
+        sdb, batch = _global_batch()
+        bounds = td.target_shards([b0 for _, b0, _ in batch.targets], len(batch), _rows(sdb, batch), ws)
+        b, e = bounds[rank], bounds[rank + 1]
+        sub = SynthBatch(batch.plat[b:e], batch.names[b:e], batch.versions[b:e], [])
+        pk, ad = om.match(om.Prepared(sdb, sub), n_threads=2)
+        pkg = torch.tensor(np.asarray(pk, dtype=np.int64) + b, dtype=torch.int32)
+        adv = torch.tensor(np.asarray(ad, dtype=np.int64), dtype=torch.int32)
+        parts = td.MatchGather("cpu")(pkg, adv, len(pk))
         wall = td.timed(lambda: None, steps=3, warmup=1)
         m = td.max_over_ranks(float(rank + 1))
-        q.put((rank, None if merged is None else merged.tolist(), wall >= 0, m))
+        merged = None
+        if parts is not None:
+            merged = (torch.cat([p for p, _ in parts]).tolist(), torch.cat([a for _, a in parts]).tolist())
+        q.put((rank, merged, wall >= 0, m, (b, e)))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(120)
-def test_gather_and_max_over_two_ranks():
+def test_sharded_match_gathers_to_single_rank_result(oracle_built):
+    from oracle import match as om
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    out = dict((r, (m, ok, mx)) for r, m, ok, mx in (q.get(timeout=100) for _ in ps))
+    out = {r: (m, ok, mx, span) for r, m, ok, mx, span in (q.get(timeout=100) for _ in ps)}
     for p in ps:
         p.join(timeout=30)
         assert p.exitcode == 0
-    merged, ok, mx = out[0]
-    assert ok and mx == 2.0 and out[1][2] == 2.0
-    assert out[1][0] is None
-    assert merged == [[i, 100 + i] for i in range(5)] + [[i, 100 + i] for i in range(5, 10)] + [[5, 7]]
+    merged, ok, mx, span0 = out[0]
+    assert ok and mx == 2.0 and out[1][2] == 2.0 and out[1][0] is None
+    assert span0[0] == 0 and span0[1] == out[1][3][0] and 0 < span0[1]  # both ranks got work
+    sdb, batch = _global_batch()
+    opk, oad = om.match(om.Prepared(sdb, batch), n_threads=2)
+    assert merged[0] == [int(x) for x in opk] and merged[1] == [int(x) for x in oad]

@@ -16,7 +16,7 @@ def test_bench_c2_batch_matches_oracle():
     from oracle import match as om
     from trivy_amd.batch import MatchBatch
     args = argparse.Namespace(keys_per_plat=30000, targets=10000, pkgs_per_target=400)
-    wl = bench.C2(args, 0)
+    wl = bench.C2(args)
     db = trivy_amd.DB()
     wl.load(db, vulns=False)
     eng = trivy_amd.Engine(db.finalize(), 0)
@@ -28,3 +28,14 @@ def test_bench_c2_batch_matches_oracle():
     opk, oad = om.match(om.Prepared(wl.sdb, wl.batch), n_threads=16)
     assert np.array_equal(pairs[:, 0], opk) and np.array_equal(pairs[:, 1], oad)
     mb.close()
+    # the end-to-end pipelined pass (bench.py end_to_end) on the same 4M batch: CSR == oracle
+    mp = MatchBatch(eng)
+    wl.fill(mp)
+    mp.pipeline_prepare(match_cap=total, chunk_packages=1 << 19)
+    got, ep, _ = mp.pipeline_run()
+    adv, rend = mp.pipeline_csr()
+    counts = np.diff(np.concatenate([[0], rend.astype(np.int64)]))
+    assert got == total and ep == -1
+    assert np.array_equal(np.repeat(np.arange(len(rend), dtype=np.uint32), counts), opk)
+    assert np.array_equal(adv, oad)
+    mp.close()

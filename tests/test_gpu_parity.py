@@ -128,7 +128,7 @@ def variants():
     from trivy_amd._lib import lib
     out, v = [], 0
     while lib().tvm_variant_name(v):
-        if not lib().tvm_variant_name(v).decode().startswith("ablate"):
+        if not lib().tvm_variant_name(v).decode().startswith(("ablate", "diag")):
             out.append(v)
         v += 1
     return out

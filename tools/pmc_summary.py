@@ -1,12 +1,12 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 outputs of tools/profile_round.sh for the match kernel.
+"""Summarise rocprofv3 outputs (tools/profile_round.sh, tools/pmc_sq.sh) per match kernel.
 
-Prints per-launch averages of every collected counter for match_kernel dispatches and the
-kernel-trace average duration; writes profiles/pmc_summary.json-style JSON to stdout's
-last line.  FETCH_SIZE/WRITE_SIZE are in KiB (rocprofv3); per MI355X_MICROARCH.md §HBM,
-FETCH_SIZE under-reports wide coalesced streaming reads by 2x on gfx950, so both the raw
-and the doubled read figure are given (the kernel's reads are mostly 16-32 B random
-accesses, i.e. not the calibrated wide-stream case).
+For every kernel of the match path (probe_kernel, sweep_kernel) prints the kernel-trace
+average duration and the per-dispatch median of every collected counter, plus per-wave
+instruction counts when SQ_WAVES was collected.  FETCH_SIZE / WRITE_SIZE are KiB
+(rocprofv3); per MI355X_MICROARCH.md §HBM, FETCH_SIZE reports half the bytes of wide
+coalesced streaming reads on gfx950 (only the staging loads here are that shape), so the
+raw figure is given.  The last line is JSON (profiles/pmc_summary.json form).
 """
 import csv
 import glob
@@ -15,36 +15,50 @@ import os
 import statistics
 import sys
 
+KERNELS = ("probe_kernel", "sweep_kernel", "match_kernel", "fill_pairs_kernel")
+
+
+def kname(name):
+    for k in KERNELS:
+        if k in name:
+            return k
+    return None
+
 
 def main(out):
-    res = {"counters": {}}
-    stats = os.path.join(out, "prof_trace", "run_kernel_stats.csv")
-    if os.path.exists(stats):
+    res = {"kernels": {}}
+    for stats in glob.glob(os.path.join(out, "**", "run_kernel_stats.csv"), recursive=True):
         for r in csv.DictReader(open(stats)):
-            if "match_kernel" in r["Name"]:
-                res["kernel"] = r["Name"]
-                res["kernel_avg_ns"] = float(r["AverageNs"])
-                res["kernel_calls"] = int(r["Calls"])
-    for f in sorted(glob.glob(os.path.join(out, "prof_*", "run_counter_collection.csv"))):
+            k = kname(r["Name"])
+            if k:
+                d = res["kernels"].setdefault(k, {"counters": {}})
+                d["name"] = r["Name"]
+                d["avg_ns"] = float(r["AverageNs"])
+                d["calls"] = int(r["Calls"])
+    for f in sorted(glob.glob(os.path.join(out, "**", "run_counter_collection.csv"), recursive=True)):
         vals = {}
         for r in csv.DictReader(open(f)):
-            if "match_kernel" not in r["Kernel_Name"] or "ablate" in r["Kernel_Name"]:
+            k = kname(r["Kernel_Name"])
+            if not k or "diag" in r["Kernel_Name"]:
                 continue
-            vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-        for k, v in vals.items():
-            res["counters"][k] = statistics.median(v)
-    c = res["counters"]
-    if "FETCH_SIZE" in c:
-        res["fetch_bytes_per_launch"] = c["FETCH_SIZE"] * 1024
-    if "WRITE_SIZE" in c:
-        res["write_bytes_per_launch"] = c["WRITE_SIZE"] * 1024
-    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-        res["hbm_bytes_per_launch"] = (c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
-    for k, v in sorted(c.items()):
-        print(f"{k:>28}: {v:,.1f}")
-    for k in ("kernel_avg_ns", "fetch_bytes_per_launch", "write_bytes_per_launch", "hbm_bytes_per_launch"):
-        if k in res:
-            print(f"{k:>28}: {res[k]:,.1f}")
+            vals.setdefault((k, r["Counter_Name"]), []).append(float(r["Counter_Value"]))
+        for (k, c), v in vals.items():
+            res["kernels"].setdefault(k, {"counters": {}})["counters"][c] = statistics.median(v)
+    for k, d in res["kernels"].items():
+        c = d["counters"]
+        if "FETCH_SIZE" in c:
+            d["fetch_bytes_per_launch"] = c["FETCH_SIZE"] * 1024
+        if "WRITE_SIZE" in c:
+            d["write_bytes_per_launch"] = c["WRITE_SIZE"] * 1024
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            d["hbm_bytes_per_launch"] = (c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+        print(f"== {k}  avg {d.get('avg_ns', 0) / 1e3:.1f} us over {d.get('calls', 0)} calls")
+        for n, v in sorted(c.items()):
+            per = f"   ({v / c['SQ_WAVES']:,.1f} per wave)" if "SQ_WAVES" in c and n.startswith("SQ_INSTS") else ""
+            print(f"{n:>28}: {v:,.1f}{per}")
+        for n in ("fetch_bytes_per_launch", "write_bytes_per_launch", "hbm_bytes_per_launch"):
+            if n in d:
+                print(f"{n:>28}: {d[n]:,.1f}")
     print(json.dumps(res))
 
 

@@ -22,6 +22,9 @@ C5_PLATS = [("Oracle Linux 8", "oracle"), ("Oracle Linux 9", "oracle"), ("alma 8
 C5_WEIGHTS = [8, 8, 18, 18, 12, 12, 12, 12]
 C3_PLATS = [("go::", "go"), ("maven::", "maven"), ("npm::", "npm"), ("pip::", "pip")]
 C3_WEIGHTS = [15, 20, 40, 25]
+# C4 (BASELINE config 4): one mixed batch, OS packages 60 % / language packages 40 %
+C4_PLATS = [("Oracle Linux 9", "oracle"), ("alma 9", "alma"), ("alpine 3.20", "alpine"), ("rocky 9", "rocky")] + C3_PLATS
+C4_WEIGHTS = [12, 18, 15, 15] + [6, 8, 16, 10]
 C3_ROOTS = {"go": ["go::GitHub Security Advisory Go", "go::The Go Vulnerability Database"],
             "maven": ["maven::GitHub Security Advisory Maven"], "npm": ["npm::GitHub Security Advisory npm"],
             "pip": ["pip::GitHub Security Advisory pip"]}

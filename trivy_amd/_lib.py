@@ -127,6 +127,17 @@ _SIG = [
     ("tvm_match_time", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_char_p,
                                       ctypes.c_size_t]),
     ("tvm_match_algorithmic_bytes", ctypes.c_uint64, [_P, _P]),
+    ("tvm_db_rows_many", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p]),
+    ("tvm_batch_set_package_base", ctypes.c_int, [_P, ctypes.c_uint32]),
+    ("tvm_batch_upload_into", ctypes.c_int, [_P, _P, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                             ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_pipeline_prepare", ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_pipeline_run", ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64),
+                                        ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_pipeline_result", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
+                                           ctypes.POINTER(ctypes.c_uint64)]),
+    ("tvm_pipeline_stats", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     ("tvm_version_key", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p,
                                        ctypes.c_size_t]),
     ("tvm_db_advisory_vuln_id", ctypes.c_char_p, [_P, ctypes.c_uint32]),

@@ -90,6 +90,25 @@ class MatchBatch:
         self.cap = cap
         return self
 
+    def set_package_base(self, base):
+        """Every match reports package index base + i (a shard of a global batch)."""
+        if lib().tvm_batch_set_package_base(self.h, base):
+            raise RuntimeError("tvm_batch_set_package_base")
+        return self
+
+    def upload_into(self, pkg, adv):
+        """Upload, with the match columns written into caller device buffers (torch int32
+        tensors on the engine's GPU, same length = the match capacity)."""
+        e = errbuf()
+        cap = pkg.numel()
+        if adv.numel() != cap or pkg.dtype.itemsize != 4 or adv.dtype.itemsize != 4:
+            raise ValueError("two 4-byte columns of equal length")
+        self._check(lib().tvm_batch_upload_into(self.engine.h, self.h, pkg.data_ptr(), adv.data_ptr(), cap, e, len(e)),
+                    e, "tvm_batch_upload_into")
+        self.cap = cap
+        self._cols = (pkg, adv)
+        return self
+
     def launch(self, k=1, sync=True):
         e = errbuf()
         for _ in range(k):
@@ -135,6 +154,45 @@ class MatchBatch:
 
     def algorithmic_bytes(self):
         return lib().tvm_match_algorithmic_bytes(self.engine.h, self.h)
+
+    # ---- end-to-end pipelined pass (tvm_pipeline_*) ----
+    def pipeline_prepare(self, match_cap=None, chunk_packages=1 << 19):
+        """Pins the batch and sizes the pipeline (host batch -> GPU -> host CSR)."""
+        e = errbuf()
+        cap = match_cap if match_cap is not None else max(1024, 8 * len(self))
+        self._check(lib().tvm_pipeline_prepare(self.engine.h, self.h, cap, chunk_packages, e, len(e)), e,
+                    "tvm_pipeline_prepare")
+        self.pipe_cap = cap
+        return self
+
+    def pipeline_run(self):
+        """One end-to-end pass: (matches, first poisoned package or -1, wall ms)."""
+        e = errbuf()
+        n, errp, ms = ctypes.c_uint64(), ctypes.c_int64(), ctypes.c_double()
+        rc = lib().tvm_pipeline_run(self.engine.h, self.h, ctypes.byref(n), ctypes.byref(errp), ctypes.byref(ms), e,
+                                    len(e))
+        if rc and n.value > self.pipe_cap:
+            raise OverflowError(n.value)
+        self._check(rc, e, "tvm_pipeline_run")
+        return n.value, errp.value, ms.value
+
+    def pipeline_csr(self):
+        """(adv uint32[matches], row_end uint32[packages]) of the last pass (copies)."""
+        adv, rend, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+        if lib().tvm_pipeline_result(self.h, ctypes.byref(adv), ctypes.byref(rend), ctypes.byref(n)):
+            raise RuntimeError("tvm_pipeline_result: no valid pass")
+        m = len(self)
+        a = np.ctypeslib.as_array((ctypes.c_uint32 * max(n.value, 1)).from_address(adv.value))[:n.value].copy() \
+            if n.value else np.zeros(0, np.uint32)
+        r = np.ctypeslib.as_array((ctypes.c_uint32 * max(m, 1)).from_address(rend.value))[:m].copy() \
+            if m else np.zeros(0, np.uint32)
+        return a, r
+
+    def pipeline_stats(self):
+        out = (ctypes.c_uint64 * 3)()
+        if lib().tvm_pipeline_stats(self.h, out):
+            raise RuntimeError("tvm_pipeline_stats")
+        return {"h2d_bytes": out[0], "d2h_bytes": out[1], "chunks": out[2]}
 
     # ---- FillInfo fused behind the match list (tvm_match_fill*) ----
     def fill(self, sync=True):

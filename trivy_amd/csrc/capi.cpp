@@ -16,6 +16,7 @@
 #include "engine.h"
 #include "libdb.h"
 #include "libver.h"
+#include "pipeline.h"
 #include "vulninfo.h"
 
 using namespace tvm;
@@ -38,10 +39,14 @@ struct tvm_batch {
   HostBatch hb;
   DevBatch dev;
   DevMatches m;
-  uint4* fill_out = nullptr;  // tvm_match_fill decisions, parallel to m.pairs
+  uint4* fill_out = nullptr;  // tvm_match_fill decisions, parallel to the match columns
   uint64_t fill_cap = 0;
   std::vector<uint32_t> target_begin;  // first package of every result (one per add call)
   BatchFilter filter;                  // tvm_match_filter state
+  std::unique_ptr<Pipeline> pipe;      // tvm_pipeline_* state
+  uint32_t pkg_base = 0;               // tvm_batch_set_package_base
+  uint64_t pipe_total = 0;
+  bool external_out = false;  // m.pkg / m.adv belong to the caller (tvm_batch_upload_into)
   bool uploaded = false;
   int device = 0;
 };
@@ -330,11 +335,15 @@ tvm_batch* tvm_batch_new(void) { return new tvm_batch(); }
 
 void tvm_batch_free(tvm_batch* b) {
   if (!b) return;
+  b->pipe.reset();
   if (b->uploaded) {
     (void)hipSetDevice(b->device);
-    for (void* p : {static_cast<void*>(b->dev.desc), static_cast<void*>(b->dev.arena), static_cast<void*>(b->dev.attr),
-                    static_cast<void*>(b->dev.cpe_bits), static_cast<void*>(b->m.pairs), static_cast<void*>(b->m.dir),
-                    static_cast<void*>(b->m.ctl), static_cast<void*>(b->fill_out)})
+    for (void* p : {static_cast<void*>(b->dev.pk), static_cast<void*>(b->dev.tile_off), static_cast<void*>(b->dev.arena),
+                    static_cast<void*>(b->dev.attr), static_cast<void*>(b->dev.cpe_bits), static_cast<void*>(b->dev.rec),
+                    static_cast<void*>(b->dev.tail), static_cast<void*>(b->external_out ? nullptr : b->m.pkg),
+                    static_cast<void*>(b->external_out ? nullptr : b->m.adv), static_cast<void*>(b->m.dir),
+                    static_cast<void*>(b->m.ctl),
+                    static_cast<void*>(b->fill_out)})
       if (p) (void)hipFree(p);
   }
   delete b;
@@ -343,16 +352,16 @@ void tvm_batch_free(tvm_batch* b) {
 // Geometric growth: many small add_many calls (one per target) must not re-allocate the
 // descriptor array to its exact size every time (quadratic copying).
 static void reserve_more(HostBatch& hb, size_t n) {
-  const size_t want = hb.desc.size() + n;
-  if (want > hb.desc.capacity()) hb.desc.reserve(std::max(want, 2 * hb.desc.capacity()));
+  const size_t want = hb.pk.size() + n;
+  if (want > hb.pk.capacity()) hb.pk.reserve(std::max(want, 2 * hb.pk.capacity()));
 }
 
 int64_t tvm_batch_add(tvm_batch* b, tvm_engine* e, const char* bucket, tvm_str name, tvm_str version) {
   if (!b || !e || !bucket || b->uploaded) return -1;
-  b->target_begin.push_back(uint32_t(b->hb.desc.size()));
+  b->target_begin.push_back(uint32_t(b->hb.pk.size()));
   int32_t plat = e->eng->db().find_plat(bucket);
   b->hb.add(plat < 0 ? 0xFFFFFFFFu : uint32_t(plat), sv(name), sv(version));
-  return int64_t(b->hb.desc.size() - 1);
+  return int64_t(b->hb.pk.size() - 1);
 }
 
 int64_t tvm_batch_add_many(tvm_batch* b, tvm_engine* e, const char* bucket, size_t n, const char* arena,
@@ -362,7 +371,7 @@ int64_t tvm_batch_add_many(tvm_batch* b, tvm_engine* e, const char* bucket, size
     return -1;
   int32_t plat = e->eng->db().find_plat(bucket);
   const uint32_t pid = plat < 0 ? 0xFFFFFFFFu : uint32_t(plat);
-  const int64_t first = int64_t(b->hb.desc.size());
+  const int64_t first = int64_t(b->hb.pk.size());
   b->target_begin.push_back(uint32_t(first));
   reserve_more(b->hb, n);
   for (size_t i = 0; i < n; i++)
@@ -381,7 +390,7 @@ int64_t tvm_batch_add_many_ex(tvm_batch* b, tvm_engine* e, const char* bucket, s
   const DB& db = e->eng->db();
   int32_t plat = db.find_plat(bucket);
   const uint32_t pid = plat < 0 ? 0xFFFFFFFFu : uint32_t(plat);
-  const int64_t first = int64_t(b->hb.desc.size());
+  const int64_t first = int64_t(b->hb.pk.size());
   b->target_begin.push_back(uint32_t(first));
   reserve_more(b->hb, n);
   for (size_t i = 0; i < n; i++) {
@@ -397,7 +406,7 @@ int64_t tvm_batch_add_many_ex(tvm_batch* b, tvm_engine* e, const char* bucket, s
   return first;
 }
 
-int64_t tvm_batch_size(const tvm_batch* b) { return b ? int64_t(b->hb.desc.size()) : 0; }
+int64_t tvm_batch_size(const tvm_batch* b) { return b ? int64_t(b->hb.pk.size()) : 0; }
 
 int tvm_batch_upload(tvm_engine* e, tvm_batch* b, uint64_t cap, char* err, size_t errlen) {
   if (!e || !b) return TVM_EINVAL;
@@ -405,15 +414,25 @@ int tvm_batch_upload(tvm_engine* e, tvm_batch* b, uint64_t cap, char* err, size_
   std::string msg;
   if (b->uploaded) {
     e->eng->free_batch(b->dev);
+    if (b->external_out) b->m.pkg = b->m.adv = nullptr;
     e->eng->free_matches(b->m);
+    b->external_out = false;
     b->uploaded = false;
   }
   if (!e->eng->upload(b->hb, b->dev, msg) || !e->eng->alloc_matches(cap, b->dev.n, b->m, msg)) {
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
   }
+  b->dev.pkg_base = b->pkg_base;
   b->uploaded = true;
   b->device = e->device;
+  return TVM_OK;
+}
+
+int tvm_batch_set_package_base(tvm_batch* b, uint32_t base) {
+  if (!b) return TVM_EINVAL;
+  b->pkg_base = base;
+  b->dev.pkg_base = base;
   return TVM_OK;
 }
 
@@ -457,7 +476,7 @@ int tvm_match_fetch(tvm_engine* e, tvm_batch* b, uint32_t* pairs, uint64_t cap, 
   std::vector<uint2> ordered;
   std::string msg;
   (void)hipSetDevice(e->device);
-  if (!Engine::fetch_ordered(b->m, b->dev.n, n, ordered, msg)) return TVM_EDEVICE;
+  if (!Engine::fetch_ordered(b->m, b->dev.n, n, ordered, e->eng->stream(), msg)) return TVM_EDEVICE;
   n = std::min<uint64_t>(n, cap);
   if (n) memcpy(pairs, ordered.data(), n * sizeof(uint2));
   if (n_out) *n_out = n;
@@ -473,7 +492,10 @@ int tvm_match_copy_device(tvm_engine* e, tvm_batch* b, void* dst, uint64_t cap, 
   n = std::min<uint64_t>(n, cap);
   (void)hipSetDevice(e->device);
   hipStream_t st = e->eng->stream();
-  if (n && (!dst || hipMemcpyAsync(dst, b->m.pairs, n * sizeof(uint2), hipMemcpyDeviceToDevice, st) != hipSuccess ||
+  // {pkg, adv} pairs interleaved from the two ordered arrays: two strided device copies
+  if (n && (!dst ||
+            hipMemcpy2DAsync(dst, 8, b->m.pkg, 4, 4, n, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+            hipMemcpy2DAsync(static_cast<char*>(dst) + 4, 8, b->m.adv, 4, 4, n, hipMemcpyDeviceToDevice, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess))
     return TVM_EDEVICE;
   if (n_out) *n_out = n;
@@ -510,23 +532,24 @@ int tvm_match_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err
 }
 
 uint64_t tvm_match_algorithmic_bytes(tvm_engine* e, tvm_batch* b) {
-  // DESIGN.md "Roofline": per package 16 B descriptor + name + version bytes, per probed
+  // DESIGN.md "Roofline": per package 8 B package word + name + version bytes, per probed
   // package 8 B slot hash + 16 B slot value + name verify, per (package, row) 16 B row +
   // bound-key bytes, per match 8 B output.  Computed exactly from the batch + tables.
   if (!e || !b) return 0;
   const DB& db = e->eng->db();
-  uint64_t bytes = 0;
-  for (const uint4& d : b->hb.desc) {
-    uint32_t nlen = d.w & 0xFFFF, vlen = d.w >> 16;
-    bytes += 16 + nlen + vlen;
+  uint64_t bytes = 0, off = 0;
+  for (const uint2& d : b->hb.pk) {
+    const uint32_t nlen = d.y & 0xFFFF, vlen = d.y >> 16;
+    const std::string_view name(reinterpret_cast<const char*>(b->hb.arena.data()) + off, nlen);
+    off += nlen + vlen;
+    bytes += 8 + nlen + vlen;  // package word, strings
     if (d.x >= db.plats.size()) continue;
     bytes += 24;
-    std::string_view name(reinterpret_cast<const char*>(b->hb.arena.data()) + d.y, nlen);
     int32_t k = db.find_key(d.x, name);
     if (k < 0) continue;
     bytes += nlen;
     const std::string ks = db.keys[size_t(k)].name;
-    uint64_t h = key_hash(d.x, reinterpret_cast<const uint8_t*>(ks.data()), uint32_t(ks.size()));
+    uint64_t h = pkg_key_hash(d.x, reinterpret_cast<const uint8_t*>(ks.data()), uint32_t(ks.size()));
     for (uint64_t i = h & db.slot_mask; db.slot_hash[i]; i = (i + 1) & db.slot_mask) {
       if (db.slot_key[i] != uint32_t(k)) continue;
       const SlotVal& v = db.slot_val[i];
@@ -716,7 +739,7 @@ int tvm_match_fill(tvm_engine* e, tvm_batch* b, char* err, size_t errlen) {
     b->fill_cap = b->m.cap;
   }
   std::string msg;
-  if (!e->fill->launch_pairs(b->m.pairs, b->m.ctl, b->m.cap, b->fill_out, e->eng->stream(), msg)) {
+  if (!e->fill->launch_pairs(b->m.adv, b->m.ctl, b->m.cap, b->fill_out, e->eng->stream(), msg)) {
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
   }
@@ -732,10 +755,7 @@ int tvm_match_fill_fetch(tvm_engine* e, tvm_batch* b, uint32_t* out4, uint64_t c
   if (rc) return rc;
   if (n_out) *n_out = 0;
   if (n > b->m.cap || n > b->fill_cap) return TVM_EINVAL;
-  unsigned long long ctl[8];
-  if (hipMemcpy(ctl, b->m.ctl, sizeof(ctl), hipMemcpyDeviceToHost) != hipSuccess) return TVM_EDEVICE;
-  const uint32_t tile = ctl[5] ? uint32_t(ctl[5]) : 256;
-  const uint32_t n_tiles = (b->dev.n + tile - 1) / tile;
+  const uint32_t n_tiles = (b->dev.n + kTile - 1) / kTile;
   std::vector<TileDir> dir(n_tiles);
   std::vector<uint4> raw(n);
   if ((n_tiles && hipMemcpy(dir.data(), b->m.dir, n_tiles * sizeof(TileDir), hipMemcpyDeviceToHost) != hipSuccess) ||
@@ -759,7 +779,7 @@ int tvm_match_fill_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char
   std::string msg;
   float f = 0;
   bool ok = hipEventCreate(&t0) == hipSuccess && hipEventCreate(&t1) == hipSuccess && hipEventRecord(t0, st) == hipSuccess;
-  for (int i = 0; ok && i < steps; i++) ok = e->fill->launch_pairs(b->m.pairs, b->m.ctl, b->m.cap, b->fill_out, st, msg);
+  for (int i = 0; ok && i < steps; i++) ok = e->fill->launch_pairs(b->m.adv, b->m.ctl, b->m.cap, b->fill_out, st, msg);
   ok = ok && hipEventRecord(t1, st) == hipSuccess && hipEventSynchronize(t1) == hipSuccess &&
        hipEventElapsedTime(&f, t0, t1) == hipSuccess;
   if (t0) (void)hipEventDestroy(t0);
@@ -775,10 +795,10 @@ int tvm_match_fill_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char
 uint64_t tvm_match_fill_algorithmic_bytes(tvm_engine* e, tvm_batch* b) {
   uint64_t n = 0;
   if (!e || !b || tvm_match_status(e, b, &n, nullptr, nullptr) || n > b->m.cap) return 0;
-  std::vector<uint2> raw(n);
+  std::vector<uint32_t> adv(n);
   (void)hipSetDevice(e->device);
-  if (n && hipMemcpy(raw.data(), b->m.pairs, n * sizeof(uint2), hipMemcpyDeviceToHost) != hipSuccess) return 0;
-  return e->fill->pair_bytes(raw);
+  if (n && hipMemcpy(adv.data(), b->m.adv, n * 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  return e->fill->pair_bytes(adv);
 }
 
 const char* tvm_fill_source_name(tvm_engine* e, uint32_t id) {
@@ -795,18 +815,19 @@ namespace {
 // the triple repeats within its result (types.BySeverity's PkgName/InstalledVersion order
 // and filterVulnerabilities' dedup key; batch packages carry no PkgPath).
 void package_ranks(const tvm_batch* b, std::vector<uint32_t>& rank, std::vector<uint8_t>& dup) {
-  const size_t n = b->hb.desc.size();
+  const size_t n = b->hb.pk.size();
   rank.assign(n, 0);
   dup.assign(n, 0);
   std::vector<uint32_t> bounds(b->target_begin);
   bounds.push_back(uint32_t(n));
+  std::vector<uint64_t> off;
+  b->hb.name_offsets(off);
   auto name = [&](uint32_t i) {
-    const uint4 d = b->hb.desc[i];
-    return std::string_view(reinterpret_cast<const char*>(b->hb.arena.data()) + d.y, d.w & 0xFFFFu);
+    return std::string_view(reinterpret_cast<const char*>(b->hb.arena.data()) + off[i], b->hb.pk[i].y & 0xFFFFu);
   };
   auto ver = [&](uint32_t i) {
-    const uint4 d = b->hb.desc[i];
-    return std::string_view(reinterpret_cast<const char*>(b->hb.arena.data()) + d.z, d.w >> 16);
+    return std::string_view(reinterpret_cast<const char*>(b->hb.arena.data()) + off[i] + (b->hb.pk[i].y & 0xFFFFu),
+                            b->hb.pk[i].y >> 16);
   };
   uint32_t next = 0;
   std::vector<uint32_t> idx;
@@ -889,7 +910,7 @@ int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint
       if (r < 0x80000000u) vex.push_back((uint64_t(pk[i]) << 32) | r | (list ? 0x80000000ull : 0ull));
     }
   }
-  if (!b->filter.run(e->fill->dev(), b->m.pairs, b->fill_out, n, ignore, vex, vt.n_vuln_ranks(), o->severity_mask,
+  if (!b->filter.run(e->fill->dev(), b->m.pkg, b->m.adv, b->fill_out, n, ignore, vex, vt.n_vuln_ranks(), o->severity_mask,
                      o->ignore_status_mask, st, msg)) {
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
@@ -919,5 +940,106 @@ int tvm_match_filter_time(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o,
     if (rc) return rc;
   }
   *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return TVM_OK;
+}
+
+// ---- end-to-end pipelined pass (pipeline.hip) -------------------------------------------
+
+int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32_t chunk_packages, char* err,
+                         size_t errlen) {
+  if (!e || !b || chunk_packages == 0) return TVM_EINVAL;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  b->pipe.reset(new Pipeline());
+  std::string msg;
+  if (!b->pipe->prepare(*e->eng, b->hb, match_cap, chunk_packages, msg)) {
+    b->pipe.reset();
+    set_err(err, errlen, msg);
+    return TVM_EDEVICE;
+  }
+  b->uploaded = true;  // the batch is pinned in place: no more adds
+  return TVM_OK;
+}
+
+int tvm_pipeline_run(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* err_pkg, double* ms, char* err,
+                     size_t errlen) {
+  if (!e || !b || !b->pipe) return TVM_EINVAL;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  std::string msg;
+  uint64_t total = 0, bits = 0;
+  int64_t ep = -1;
+  const auto t0 = std::chrono::steady_clock::now();
+  const bool ok = b->pipe->run(*e->eng, b->hb, total, ep, bits, msg);
+  const double dt = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (!ok) {
+    set_err(err, errlen, msg);
+    return TVM_EDEVICE;
+  }
+  if (bits) {
+    set_err(err, errlen, "match kernel internal error bits " + std::to_string(bits));
+    return TVM_EDEVICE;
+  }
+  b->pipe_total = total;
+  if (n_matches) *n_matches = total;
+  if (err_pkg) *err_pkg = ep;
+  if (ms) *ms = dt;
+  if (total > b->pipe->cap()) {
+    set_err(err, errlen, "tvm_pipeline_run: match buffer too small (prepare with match_cap >= n_matches)");
+    return TVM_EINVAL;
+  }
+  return TVM_OK;
+}
+
+int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row_end, uint64_t* n_matches) {
+  if (!b || !b->pipe || b->pipe_total > b->pipe->cap()) return TVM_EINVAL;
+  if (adv) *adv = b->pipe->adv();
+  if (row_end) *row_end = b->pipe->row_end();
+  if (n_matches) *n_matches = b->pipe_total;
+  return TVM_OK;
+}
+
+int tvm_pipeline_stats(tvm_batch* b, uint64_t out[3]) {
+  if (!b || !b->pipe || !out) return TVM_EINVAL;
+  out[0] = b->pipe->h2d_bytes();
+  out[1] = b->pipe->d2h_bytes();
+  out[2] = b->pipe->chunks();
+  return TVM_OK;
+}
+
+// ---- sharding support ------------------------------------------------------------------
+
+int tvm_db_rows_many(const tvm_db* db, const char* bucket, size_t n, const char* arena, const uint64_t* name_off,
+                     const uint32_t* name_len, uint32_t* out) {
+  if (!db || !db->finalized || !bucket || (n && (!arena || !name_off || !name_len || !out))) return TVM_EINVAL;
+  const DB& d = db->db;
+  const int32_t plat = d.find_plat(bucket);
+  for (size_t i = 0; i < n; i++) {
+    out[i] = 0;
+    if (plat < 0 || d.slot_hash.empty()) continue;
+    const std::string_view name(arena + name_off[i], name_len[i]);
+    const uint64_t h = pkg_key_hash(uint32_t(plat), reinterpret_cast<const uint8_t*>(name.data()), uint32_t(name.size()));
+    for (uint64_t s = h & d.slot_mask; d.slot_hash[s]; s = (s + 1) & d.slot_mask) {
+      const SlotVal& v = d.slot_val[s];
+      if (d.slot_hash[s] == h && (v.name_len & SLOT_LEN_MASK) == name.size() &&
+          std::equal(name.begin(), name.end(), d.name_arena.begin() + v.name_off)) {
+        out[i] = v.row_count;
+        break;
+      }
+    }
+  }
+  return TVM_OK;
+}
+
+int tvm_batch_upload_into(tvm_engine* e, tvm_batch* b, void* pkg_dev, void* adv_dev, uint64_t cap, char* err,
+                          size_t errlen) {
+  if (!e || !b || !pkg_dev || !adv_dev || cap == 0) return TVM_EINVAL;
+  const int rc = tvm_batch_upload(e, b, 1, err, errlen);
+  if (rc) return rc;
+  (void)hipSetDevice(e->device);
+  (void)hipFree(b->m.pkg);
+  (void)hipFree(b->m.adv);
+  b->m.pkg = static_cast<uint32_t*>(pkg_dev);
+  b->m.adv = static_cast<uint32_t*>(adv_dev);
+  b->m.cap = cap;
+  b->external_out = true;
   return TVM_OK;
 }

@@ -150,6 +150,27 @@ TVM_HD uint64_t key_hash(uint32_t plat, const uint8_t* s, uint32_t n) {
   return key_hash_fin(h);
 }
 
+// Package-index hash of (platform, name): word at a time, so the probe kernel hashes a
+// name with one multiply per 8 bytes (the words it also compares against the slot's
+// inline name).  Seeded by the platform and the length; words are little-endian, the
+// last one zero padded; finished with fmix64.  Never 0.
+TVM_HD uint64_t key_hash_seed2(uint32_t plat, uint32_t n) {
+  return 0xcbf29ce484222325ULL ^ (uint64_t(plat) * 0x9E3779B97F4A7C15ULL) ^ (uint64_t(n) * 0xC2B2AE3D27D4EB4FULL);
+}
+TVM_HD uint64_t key_hash_word(uint64_t h, uint64_t w) {
+  h = (h ^ w) * 0x9FB21C651E98DF25ULL;
+  return h ^ (h >> 29);
+}
+TVM_HD uint64_t pkg_key_hash(uint32_t plat, const uint8_t* s, uint32_t n) {
+  uint64_t h = key_hash_seed2(plat, n);
+  for (uint32_t i = 0; i < n; i += 8) {
+    uint64_t w = 0;
+    for (uint32_t b = 0; b < 8 && i + b < n; b++) w |= uint64_t(s[i + b]) << (8 * b);
+    h = key_hash_word(h, w);
+  }
+  return key_hash_fin(h);
+}
+
 // Lexicographic compare of two sort keys held in 8-byte words (memory-order bytes,
 // zero padded): memcmp over the common length, then shorter-first.
 TVM_HD int key_cmp(const uint64_t* a, uint32_t na, const uint64_t* b, uint32_t nb) {

@@ -297,7 +297,7 @@ int32_t DB::find_plat(std::string_view root) const {
 }
 
 int32_t DB::find_key(uint32_t plat, std::string_view name) const {
-  uint64_t h = key_hash(plat, reinterpret_cast<const uint8_t*>(name.data()), uint32_t(name.size()));
+  uint64_t h = pkg_key_hash(plat, reinterpret_cast<const uint8_t*>(name.data()), uint32_t(name.size()));
   if (slot_hash.empty()) return -1;
   for (uint64_t i = h & slot_mask; slot_hash[i]; i = (i + 1) & slot_mask) {
     if (slot_hash[i] != h) continue;
@@ -698,7 +698,7 @@ void DB::build_index() {
   name_arena.clear();
   for (size_t k = 0; k < keys.size(); k++) {
     const Key& key = keys[k];
-    uint64_t h = key_hash(key.plat, reinterpret_cast<const uint8_t*>(key.name.data()), uint32_t(key.name.size()));
+    uint64_t h = pkg_key_hash(key.plat, reinterpret_cast<const uint8_t*>(key.name.data()), uint32_t(key.name.size()));
     uint64_t i = h & slot_mask;
     while (slot_hash[i]) i = (i + 1) & slot_mask;
     slot_hash[i] = h;

@@ -268,9 +268,8 @@ bool run_plan(Engine& eng, const Plan& plan, std::vector<uint2>& pairs, std::str
   if (!eng.match_host(plan.batch, pairs, err_pkg, err)) return false;
   key_err.clear();
   if (err_pkg >= 0) {
-    const uint4& d = plan.batch.desc[size_t(err_pkg)];
-    std::string_view name(reinterpret_cast<const char*>(plan.batch.arena.data()) + d.y, d.w & 0xFFFF);
-    int32_t k = eng.db().find_key(d.x, name);
+    const std::string_view name = plan.batch.name(size_t(err_pkg));
+    int32_t k = eng.db().find_key(plan.batch.pk[size_t(err_pkg)].x, name);
     key_err = k >= 0 ? eng.db().keys[size_t(k)].err : "advisory decode error";
     if (key_err.empty()) key_err = "advisory decode error";
   }

@@ -1,11 +1,12 @@
-// Device engine: HBM-resident advisory tables + the match kernel (gfx950).
+// Device engine: HBM-resident advisory tables + the match path (gfx950).
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include <cstdint>
 #include <atomic>
+#include <cstdint>
 #include <mutex>
 #include <string>
+#include <string_view>
 #include <vector>
 
 #include "common.h"
@@ -13,6 +14,8 @@
 namespace tvm {
 
 class DB;
+
+constexpr int kTile = 256;  // packages per tile (workgroup) of both match kernels
 
 // Device view of the flattened tables (db.h device images).
 struct DevDB {
@@ -27,50 +30,78 @@ struct DevDB {
   const uint32_t* aux_ids = nullptr;
 };
 
-// A package batch in SoA-of-descriptors form.  desc[i] = {plat, name_off, ver_off,
-// name_len | ver_len << 16} into `arena`; plat = 0xFFFFFFFF when the bucket is absent.
-// Optional per-package attributes (common.h PA_*), present when the batch touches rows
-// with filters: attr[i] = {arch id | PA_NOARCH, ksplice tag or CPE-set id}; CPE set s is
-// the bitset cpe_bits[s * cpe_words .. +cpe_words) over CPE indices.
+// A package batch.  pk[i] = {plat, name_len | ver_len << 16}; the name and version bytes
+// of every package sit back to back in `arena`, package after package, so offsets are
+// implicit: tile_off[t] is the arena offset of package t * kTile (the kernels scan the
+// lengths within a tile).  plat = 0xFFFFFFFF when the bucket is absent.  Lengths
+// saturate at 0xFFFF (the stored bytes are cut to match).  Optional per-package attributes
+// (common.h PA_*), present when the batch touches rows with filters: attr[i] = {arch id |
+// PA_NOARCH, ksplice tag or CPE-set id}; CPE set s is the bitset cpe_bits[s * cpe_words ..
+// +cpe_words) over CPE indices.
 struct HostBatch {
-  std::vector<uint4> desc;
+  std::vector<uint2> pk;
   std::vector<uint8_t> arena;
+  std::vector<uint64_t> tile_off;
   std::vector<uint2> attr;
   std::vector<uint32_t> cpe_bits;
   uint32_t cpe_words = 0;
   void add(uint32_t plat, std::string_view name, std::string_view ver);
   void add(uint32_t plat, std::string_view name, std::string_view ver, uint2 a);
+  size_t size() const { return pk.size(); }
+  uint32_t n_tiles() const { return uint32_t((pk.size() + kTile - 1) / kTile); }
+  // arena offset of package i's name (O(kTile) per call); all of them at once
+  uint64_t name_off(size_t i) const;
+  void name_offsets(std::vector<uint64_t>& off) const;
+  std::string_view name(size_t i) const;
+  std::string_view version(size_t i) const;
+  void clear();
+};
+
+// Per-package record handed from probe_kernel to sweep_kernel (match_kernel.h):
+// meta = {row_begin, row_count, key info, spill word offset}; k0/k1 = the installed key's
+// first 16 bytes as big-endian words.
+struct PkgRec {
+  uint4 meta;
+  uint64_t k0, k1;
 };
 
 struct DevBatch {
-  uint4* desc = nullptr;
+  uint2* pk = nullptr;
+  uint64_t* tile_off = nullptr;
   uint8_t* arena = nullptr;
   uint2* attr = nullptr;
   uint32_t* cpe_bits = nullptr;
   uint32_t cpe_words = 0;
   uint32_t n_cpe_sets = 0;
   uint32_t n = 0;
+  uint32_t n_tiles = 0;
   uint64_t arena_bytes = 0;
-  uint64_t spill_words = 0;  // scratch needed for installed keys longer than the LDS slot
+  uint64_t spill_words = 0;  // scratch for installed keys longer than 32 bytes
   uint32_t gm = 0;           // grammar bits (1 << Cmp) of the batch's platforms (libver.h GM_*)
+  uint32_t pkg_base = 0;     // added to the package index of every match (multi-GPU shards)
+  // probe -> sweep hand-off (device only)
+  PkgRec* rec = nullptr;
+  uint4* tail = nullptr;  // key bytes 16..31 per package
 };
 
-// Device-side results of one match launch: the per-package advisory lists.
-// Tile t (packages [256t, 256t+256)) owns the segment pairs[dir[t].base .. + dir[t].count),
-// ordered by (package, advisory); segments are placed by one atomic reservation per
-// tile, so the global (package, advisory) order is read through the directory.
+// Device-side results of one match pass: the per-package advisory lists as two columns
+// (pkg[i], adv[i]).  Tile t (packages [256t, 256t+256)) owns the segment
+// [dir[t].base, dir[t].base + dir[t].count), in (package, advisory) order; segments are
+// placed by one atomic reservation per tile, so the global order is read through the
+// directory.
 struct TileDir {
   unsigned long long base;
   uint32_t count;
   uint32_t pad;
 };
 struct DevMatches {
-  uint2* pairs = nullptr;          // {pkg index, advisory index}
-  uint64_t cap = 0;                // capacity in pairs
-  TileDir* dir = nullptr;          // one entry per tile
+  uint32_t* pkg = nullptr;
+  uint32_t* adv = nullptr;
+  uint64_t cap = 0;  // capacity in matches
+  TileDir* dir = nullptr;
   uint32_t dir_cap = 0;
   // control block (device): [0] total matches (reservation counter), [1] n - first
-  // poisoned pkg (0 = none), [2] spill words used, [3] error bits, [4] tile ticket
+  // poisoned pkg (0 = none), [2] spill words used, [3] error bits
   unsigned long long* ctl = nullptr;
 };
 enum : uint32_t { ERR_SPILL = 1, ERR_TILES = 2 };
@@ -83,33 +114,35 @@ class Engine {
   hipStream_t stream() const { return stream_; }
   uint64_t table_bytes() const { return table_bytes_; }
 
-  // Device-resident batch management.
-  bool upload(const HostBatch& hb, DevBatch& db, std::string& err);
+  // Device-resident batch management.  alloc_batch sizes the device buffers without
+  // copying (the pipelined path copies chunk by chunk); upload = alloc + copy.
+  bool alloc_batch(const HostBatch& hb, DevBatch& b, std::string& err);
+  bool upload(const HostBatch& hb, DevBatch& b, std::string& err);
   uint32_t grammar_set(const HostBatch& hb) const;
-  void free_batch(DevBatch& db);
+  void free_batch(DevBatch& b);
   bool alloc_matches(uint64_t cap, uint32_t n_pkgs, DevMatches& m, std::string& err);
   void free_matches(DevMatches& m);
 
-  // Enqueues one match pass on `stream` (no host synchronisation).
+  // Enqueues one match pass (probe + sweep over every tile) on `stream`; no host sync.
   bool launch(const DevBatch& b, const DevMatches& m, hipStream_t stream, std::string& err);
+  // The pass over tiles [t_begin, t_end) only: probe on `probe_st`, sweep on `sweep_st`
+  // behind event `ev` (the caller zeroes m.ctl once before the first chunk).
+  bool launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_begin, uint32_t t_end, hipStream_t probe_st,
+                    hipStream_t sweep_st, hipEvent_t ev, std::string& err);
 
-  // After the pass: copies the match lists to host in (package, advisory) order.
-  // Returns false when the device buffer was too small (total > m.cap).
+  // After the pass: the match list as {package, advisory} pairs in (package, advisory) order.
   static bool fetch_ordered(const DevMatches& m, uint32_t n_pkgs, uint64_t total, std::vector<uint2>& out,
-                            std::string& err);
+                            hipStream_t st, std::string& err);
 
   // Convenience: upload, match, download. out = pairs; err_pkg = first poisoned package or -1.
   bool match_host(const HostBatch& hb, std::vector<uint2>& out, int64_t& err_pkg, std::string& err);
 
   const DB& db() const { return *db_; }
 
-  // Kernel variant (tile size / LDS budget); returns the previous one.  Default 0 =
-  // "auto" (the tuned variant for the batch's grammar set), overridable with the
-  // TVM_VARIANT environment variable at open().
+  // Sweep-kernel variant (pairs per lane / LDS buffer); returns the previous one.  Default
+  // 0 = "auto", overridable with the TVM_VARIANT environment variable at open().
   int set_variant(int v);
-  // Variant index of the most recent launch (auto resolved), -1 before the first.
   int last_launched() const { return last_launched_; }
-  // Integrity check: the device tables still equal the host images (bytes compared).
   bool verify(std::string& err);
   int variant() const { return variant_; }
 
@@ -118,6 +151,9 @@ class Engine {
   int variant_ = 0;
   std::atomic<int> last_launched_{-1};
   hipStream_t stream_ = nullptr;
+  hipStream_t stream2_ = nullptr;           // sweep chunks (overlap the next chunk's probe)
+  std::vector<hipEvent_t> ev_;              // probe-done events, one per chunk in flight
+  hipEvent_t ev_done_ = nullptr;
   const DB* db_ = nullptr;
   DevDB d_;
   std::vector<void*> allocs_;
@@ -132,7 +168,6 @@ class Engine {
 // Kernel variants: count and names (engine.hip; 0 = "auto").
 int num_variants();
 const char* variant_name(int v);
-// The variant "auto" (0) resolves to for a batch of grammar bits gm; other v unchanged.
 int resolve_variant(int v, uint32_t gm);
 
 }  // namespace tvm

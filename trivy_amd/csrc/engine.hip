@@ -1,6 +1,6 @@
 // Device engine (host side of the match path): HBM-resident advisory tables, batch
-// upload, variant selection and launch of the match kernel (match_kernel.h, instantiated
-// in kern_*.hip), and ordered read-back of the per-package advisory lists.
+// upload, variant selection and launch of the two match kernels (match_kernel.h,
+// instantiated in kern_*.hip), and read-back of the ordered match list.
 #include "engine.h"
 
 #include <algorithm>
@@ -14,47 +14,52 @@
 namespace tvm {
 
 // kern_*.hip
-const LaunchFn* launch_table_DEB_TUNED();
-const LaunchFn* launch_table_OS_TUNED();
-const LaunchFn* launch_table_ALL_TUNED();
-const LaunchFn* launch_table_DEB_ABLATION();
-const LaunchFn* launch_table_OS_ABLATION();
-const LaunchFn* launch_table_ALL_ABLATION();
+ProbeFn probe_fn_DEB();
+ProbeFn probe_fn_DEB_diag(int d);
+ProbeFn probe_fn_OS();
+ProbeFn probe_fn_ALL();
+const SweepFn* sweep_table(bool filt);
+const FusedFn* fused_table_DEB();
+const FusedFn* fused_table_OS();
+const FusedFn* fused_table_ALL();
 
 namespace {
 
-// Variant table: index 0 = "auto" (kAutoVariant per grammar set), then the tuned list,
-// then the ablations (match_variants.h).  The launch functions live in the kern_*.hip
-// tables, indexed by (grammar set, list, position); the host launches the smallest
-// grammar set that covers the batch's platforms, so a dpkg-only batch runs a kernel with
-// only the dpkg encoder in it (no library-grammar register/scratch footprint).
-struct VariantInfo {
-  int tile;
-  int kw;
-  bool kg;       // installed keys in global memory (KW words per package)
-  const char* name;
+constexpr const char* kVariantNames[] = {
+#define TVM_NAME_(F, K, MB, NAME) NAME,
+    TVM_MATCH_VARIANTS(TVM_NAME_)
+#undef TVM_NAME_
 };
-#define TVM_INFO_(T, KW, MB, KG, AB, NAME) {T, KW, KG, NAME},
-constexpr VariantInfo kTunedInfo[] = {TVM_TUNED_VARIANTS(TVM_INFO_)};
-constexpr VariantInfo kAblInfo[] = {TVM_ABLATION_VARIANTS(TVM_INFO_)};
-#undef TVM_INFO_
-static_assert(sizeof(kTunedInfo) / sizeof(VariantInfo) == kNumTuned, "tuned list");
-static_assert(sizeof(kAblInfo) / sizeof(VariantInfo) == kNumAblations, "ablation list");
-constexpr int kNumVariants = 1 + kNumTuned + kNumAblations;
-constexpr int kMinTile = 64;
-constexpr int kMinKeyWords = 4;
-
-// Variant v (>= 1) of the table above.
-const VariantInfo& variant_info(int v) { return v <= kNumTuned ? kTunedInfo[v - 1] : kAblInfo[v - 1 - kNumTuned]; }
-
 // Grammar-set index of a batch: 0 = dpkg only, 1 = OS grammars, 2 = any.
 int grammar_index(uint32_t gm) { return (gm & ~GM_DEB) == 0 ? 0 : (gm & ~GM_OS) == 0 ? 1 : 2; }
+constexpr int kNumVariants = 1 + kNumTuned;
+// A pass is cut into up to kMaxChunks chunks of at least kMinChunkTiles tiles: chunk c's
+// probe (main stream) overlaps chunk c-1's sweep (second stream) on the same CUs.
+constexpr int kMaxChunks = 8;
+constexpr uint32_t kMinChunkTiles = 512;
+constexpr bool kFusedVariant[] = {
+#define TVM_F_(F, K, MB, NAME) F != 0,
+    TVM_MATCH_VARIANTS(TVM_F_)
+#undef TVM_F_
+};
 
-LaunchFn launch_fn(int gi, int v) {
-  static const LaunchFn* const tuned[3] = {launch_table_DEB_TUNED(), launch_table_OS_TUNED(), launch_table_ALL_TUNED()};
-  static const LaunchFn* const abl[3] = {launch_table_DEB_ABLATION(), launch_table_OS_ABLATION(),
-                                         launch_table_ALL_ABLATION()};
-  return v <= kNumTuned ? tuned[gi][v - 1] : abl[gi][v - 1 - kNumTuned];
+FusedFn fused_fn(uint32_t gm, int vi) {
+  switch (grammar_index(gm)) {
+    case 0: return fused_table_DEB()[vi - 1];
+    case 1: return fused_table_OS()[vi - 1];
+    default: return fused_table_ALL()[vi - 1];
+  }
+}
+
+
+ProbeFn probe_fn(uint32_t gm) {
+  static const int diag = std::getenv("TVM_PROBE_DIAG") ? std::atoi(std::getenv("TVM_PROBE_DIAG")) : 0;
+  if (diag && grammar_index(gm) == 0) return probe_fn_DEB_diag(diag);
+  switch (grammar_index(gm)) {
+    case 0: return probe_fn_DEB();
+    case 1: return probe_fn_OS();
+    default: return probe_fn_ALL();
+  }
 }
 
 bool hip_ok(hipError_t e, const char* what, std::string& err) {
@@ -76,38 +81,84 @@ bool upload_vec(const std::vector<T>& v, T** dst, std::vector<void*>& allocs, ui
   return true;
 }
 
+template <class T>
+bool dmalloc(T** p, size_t count, const char* what, std::string& err) {
+  void* q = nullptr;
+  if (!hip_ok(hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T)), what, err)) return false;
+  *p = static_cast<T*>(q);
+  return true;
+}
+
 }  // namespace
 
 int num_variants() { return kNumVariants; }
 const char* variant_name(int v) {
   if (v == 0) return "auto";
-  return v > 0 && v < kNumVariants ? variant_info(v).name : nullptr;
+  return v > 0 && v < kNumVariants ? kVariantNames[v - 1] : nullptr;
 }
-int resolve_variant(int v, uint32_t gm) { return v == 0 ? 1 + kAutoVariant[grammar_index(gm)] : v; }
+int resolve_variant(int v, uint32_t) { return v == 0 ? 1 + kAutoVariant : v; }
+
+// ---- HostBatch ------------------------------------------------------------------------------
 
 void HostBatch::add(uint32_t plat, std::string_view name, std::string_view ver) {
-  uint4 d;
-  d.x = plat;
-  d.y = uint32_t(arena.size());
-  arena.insert(arena.end(), name.begin(), name.end());
-  d.z = uint32_t(arena.size());
-  arena.insert(arena.end(), ver.begin(), ver.end());
-  d.w = uint32_t(std::min<size_t>(name.size(), 0xFFFF)) | (uint32_t(std::min<size_t>(ver.size(), 0xFFFF)) << 16);
-  desc.push_back(d);
+  if (pk.size() % kTile == 0) tile_off.push_back(arena.size());
+  const size_t nl = std::min<size_t>(name.size(), 0xFFFF), vl = std::min<size_t>(ver.size(), 0xFFFF);
+  pk.push_back(make_uint2(plat, uint32_t(nl) | (uint32_t(vl) << 16)));
+  arena.insert(arena.end(), name.begin(), name.begin() + nl);
+  arena.insert(arena.end(), ver.begin(), ver.begin() + vl);
   if (!attr.empty()) attr.push_back(make_uint2(PA_ARCH_NONE, 0xFFFFFFFFu));
 }
 
 void HostBatch::add(uint32_t plat, std::string_view name, std::string_view ver, uint2 a) {
-  if (attr.size() < desc.size()) attr.resize(desc.size(), make_uint2(PA_ARCH_NONE, 0xFFFFFFFFu));
+  if (attr.size() < pk.size()) attr.resize(pk.size(), make_uint2(PA_ARCH_NONE, 0xFFFFFFFFu));
   add(plat, name, ver);
-  if (attr.size() < desc.size()) attr.push_back(a);
+  if (attr.size() < pk.size()) attr.push_back(a);
   else attr.back() = a;
 }
+
+uint64_t HostBatch::name_off(size_t i) const {
+  const size_t t = i / kTile;
+  uint64_t o = tile_off[t];
+  for (size_t j = t * kTile; j < i; j++) o += (pk[j].y & 0xFFFFu) + (pk[j].y >> 16);
+  return o;
+}
+
+void HostBatch::name_offsets(std::vector<uint64_t>& off) const {
+  off.resize(pk.size());
+  uint64_t o = 0;
+  for (size_t j = 0; j < pk.size(); j++) {
+    off[j] = o;
+    o += (pk[j].y & 0xFFFFu) + (pk[j].y >> 16);
+  }
+}
+
+std::string_view HostBatch::name(size_t i) const {
+  return std::string_view(reinterpret_cast<const char*>(arena.data()) + name_off(i), pk[i].y & 0xFFFFu);
+}
+
+std::string_view HostBatch::version(size_t i) const {
+  return std::string_view(reinterpret_cast<const char*>(arena.data()) + name_off(i) + (pk[i].y & 0xFFFFu),
+                          pk[i].y >> 16);
+}
+
+void HostBatch::clear() {
+  pk.clear();
+  arena.clear();
+  tile_off.clear();
+  attr.clear();
+  cpe_bits.clear();
+  cpe_words = 0;
+}
+
+// ---- Engine -----------------------------------------------------------------------------------
 
 Engine::~Engine() {
   if (dev_ >= 0) (void)hipSetDevice(dev_);
   for (void* p : allocs_) (void)hipFree(p);
   if (spill_) (void)hipFree(spill_);
+  for (hipEvent_t e : ev_) (void)hipEventDestroy(e);
+  if (ev_done_) (void)hipEventDestroy(ev_done_);
+  if (stream2_) (void)hipStreamDestroy(stream2_);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -126,10 +177,18 @@ Engine* Engine::open(const DB& db, int device, std::string& err) {
   e->db_ = &db;
   if (const char* v = std::getenv("TVM_VARIANT")) e->set_variant(std::atoi(v));
   if (!hip_ok(hipSetDevice(device), "hipSetDevice", err) ||
-      !hip_ok(hipStreamCreateWithFlags(&e->stream_, hipStreamNonBlocking), "hipStreamCreate", err)) {
+      !hip_ok(hipStreamCreateWithFlags(&e->stream_, hipStreamNonBlocking), "hipStreamCreate", err) ||
+      !hip_ok(hipStreamCreateWithFlags(&e->stream2_, hipStreamNonBlocking), "hipStreamCreate", err) ||
+      !hip_ok(hipEventCreateWithFlags(&e->ev_done_, hipEventDisableTiming), "hipEventCreate", err)) {
     delete e;
     return nullptr;
   }
+  e->ev_.resize(kMaxChunks);
+  for (hipEvent_t& ev : e->ev_)
+    if (!hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate", err)) {
+      delete e;
+      return nullptr;
+    }
   Slot* sl; uint8_t* na; Row* rows; uint64_t* kw; PlatInfo* pl; RowAux* ax; uint32_t* ai;
   bool ok = upload_vec(db.aux, &ax, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.aux_ids, &ai, e->allocs_, e->table_bytes_, err) &&
@@ -176,7 +235,7 @@ uint32_t Engine::grammar_set(const HostBatch& hb) const {
   const auto& pi = db_->plat_info;
   std::vector<uint8_t> seen(pi.size(), 0);
   uint32_t gm = 0;
-  for (const uint4& d : hb.desc)
+  for (const uint2& d : hb.pk)
     if (d.x < pi.size() && !seen[d.x]) {
       seen[d.x] = 1;
       gm |= 1u << pi[d.x].cmp;
@@ -184,36 +243,47 @@ uint32_t Engine::grammar_set(const HostBatch& hb) const {
   return gm & GM_ALL;
 }
 
-bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
+bool Engine::alloc_batch(const HostBatch& hb, DevBatch& b, std::string& err) {
   (void)hipSetDevice(dev_);
-  b.n = uint32_t(hb.desc.size());
+  b.n = uint32_t(hb.pk.size());
+  b.n_tiles = hb.n_tiles();
   b.arena_bytes = hb.arena.size();
   b.spill_words = 0;
   b.gm = grammar_set(hb);
-  for (const uint4& d : hb.desc) {
-    const uint32_t need = (key_bound_any(d.w >> 16) + 7) / 8;  // the widest grammar bound
-    if (need > uint32_t(kMinKeyWords)) b.spill_words += need;  // bound for every variant
+  for (const uint2& d : hb.pk) {
+    const uint32_t need = (key_bound_any(d.y >> 16) + 7) / 8;  // the widest grammar bound
+    if (need > kKeyWords) b.spill_words += need;
   }
-  if (!hip_ok(hipMalloc(&b.desc, std::max<size_t>(hb.desc.size(), 1) * sizeof(uint4)), "hipMalloc(batch)", err)) return false;
-  // +32 B tail: the kernel stages whole 16-byte lines of the arena into LDS
-  if (!hip_ok(hipMalloc(&b.arena, (hb.arena.size() + 32 + 15) & ~size_t(15)), "hipMalloc(batch arena)", err)) return false;
-  if (!hb.desc.empty() &&
-      !hip_ok(hipMemcpy(b.desc, hb.desc.data(), hb.desc.size() * sizeof(uint4), hipMemcpyHostToDevice), "H2D batch", err))
+  if (!hb.attr.empty() && hb.attr.size() != hb.pk.size()) {
+    err = "batch attributes do not cover every package";
+    return false;
+  }
+  // +32 B tail: the kernels stage whole 16-byte lines and read names as dword triples
+  return dmalloc(&b.pk, hb.pk.size(), "hipMalloc(batch)", err) &&
+         dmalloc(&b.tile_off, size_t(b.n_tiles) + 1, "hipMalloc(tile offsets)", err) &&
+         dmalloc(&b.arena, (hb.arena.size() + 32 + 15) & ~size_t(15), "hipMalloc(batch arena)", err) &&
+         (hb.attr.empty() || dmalloc(&b.attr, hb.attr.size(), "hipMalloc(batch attr)", err)) &&
+         dmalloc(&b.rec, hb.pk.size(), "hipMalloc(package records)", err) &&
+         dmalloc(&b.tail, hb.pk.size(), "hipMalloc(key tails)", err) && ensure_scratch(b.spill_words, err);
+}
+
+bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
+  if (!alloc_batch(hb, b, err)) return false;
+  std::vector<uint64_t> toff(hb.tile_off);
+  toff.push_back(hb.arena.size());
+  if (!hb.pk.empty() && !hip_ok(hipMemcpy(b.pk, hb.pk.data(), hb.pk.size() * sizeof(uint2), hipMemcpyHostToDevice),
+                                "H2D batch", err))
+    return false;
+  if (!hip_ok(hipMemcpy(b.tile_off, toff.data(), toff.size() * 8, hipMemcpyHostToDevice), "H2D tile offsets", err))
     return false;
   if (!hb.arena.empty() &&
       !hip_ok(hipMemcpy(b.arena, hb.arena.data(), hb.arena.size(), hipMemcpyHostToDevice), "H2D arena", err))
     return false;
-  if (!hb.attr.empty()) {
-    if (hb.attr.size() != hb.desc.size()) {
-      err = "batch attributes do not cover every package";
-      return false;
-    }
-    if (!hip_ok(hipMalloc(&b.attr, hb.attr.size() * sizeof(uint2)), "hipMalloc(batch attr)", err) ||
-        !hip_ok(hipMemcpy(b.attr, hb.attr.data(), hb.attr.size() * sizeof(uint2), hipMemcpyHostToDevice), "H2D attr", err))
-      return false;
-  }
+  if (!hb.attr.empty() &&
+      !hip_ok(hipMemcpy(b.attr, hb.attr.data(), hb.attr.size() * sizeof(uint2), hipMemcpyHostToDevice), "H2D attr", err))
+    return false;
   if (!hb.cpe_bits.empty() && hb.cpe_words) {
-    if (!hip_ok(hipMalloc(&b.cpe_bits, hb.cpe_bits.size() * 4), "hipMalloc(cpe sets)", err) ||
+    if (!dmalloc(&b.cpe_bits, hb.cpe_bits.size(), "hipMalloc(cpe sets)", err) ||
         !hip_ok(hipMemcpy(b.cpe_bits, hb.cpe_bits.data(), hb.cpe_bits.size() * 4, hipMemcpyHostToDevice), "H2D cpe", err))
       return false;
     b.cpe_words = hb.cpe_words;
@@ -224,106 +294,157 @@ bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
 
 void Engine::free_batch(DevBatch& b) {
   (void)hipSetDevice(dev_);
-  if (b.desc) (void)hipFree(b.desc);
-  if (b.arena) (void)hipFree(b.arena);
-  if (b.attr) (void)hipFree(b.attr);
-  if (b.cpe_bits) (void)hipFree(b.cpe_bits);
+  for (void* p : {static_cast<void*>(b.pk), static_cast<void*>(b.tile_off), static_cast<void*>(b.arena),
+                  static_cast<void*>(b.attr), static_cast<void*>(b.cpe_bits), static_cast<void*>(b.rec),
+                  static_cast<void*>(b.tail)})
+    if (p) (void)hipFree(p);
   b = DevBatch{};
 }
 
 bool Engine::alloc_matches(uint64_t cap, uint32_t n_pkgs, DevMatches& m, std::string& err) {
   (void)hipSetDevice(dev_);
   m.cap = std::max<uint64_t>(cap, 1);
-  m.dir_cap = std::max<uint32_t>((n_pkgs + kMinTile - 1) / kMinTile, 1);
-  if (!hip_ok(hipMalloc(&m.pairs, m.cap * sizeof(uint2)), "hipMalloc(matches)", err)) return false;
-  if (!hip_ok(hipMalloc(&m.dir, m.dir_cap * sizeof(TileDir)), "hipMalloc(tile dir)", err)) return false;
-  if (!hip_ok(hipMalloc(&m.ctl, 8 * sizeof(unsigned long long)), "hipMalloc(ctl)", err)) return false;
-  return true;
+  m.dir_cap = std::max<uint32_t>((n_pkgs + kTile - 1) / kTile, 1);
+  return dmalloc(&m.pkg, m.cap, "hipMalloc(matches)", err) && dmalloc(&m.adv, m.cap, "hipMalloc(matches)", err) &&
+         dmalloc(&m.dir, m.dir_cap, "hipMalloc(tile dir)", err) && dmalloc(&m.ctl, 8, "hipMalloc(ctl)", err);
 }
 
 void Engine::free_matches(DevMatches& m) {
   (void)hipSetDevice(dev_);
-  if (m.pairs) (void)hipFree(m.pairs);
-  if (m.dir) (void)hipFree(m.dir);
-  if (m.ctl) (void)hipFree(m.ctl);
+  for (void* p : {static_cast<void*>(m.pkg), static_cast<void*>(m.adv), static_cast<void*>(m.dir),
+                  static_cast<void*>(m.ctl)})
+    if (p) (void)hipFree(p);
   m = DevMatches{};
 }
 
 bool Engine::fetch_ordered(const DevMatches& m, uint32_t n_pkgs, uint64_t total, std::vector<uint2>& out,
-                           std::string& err) {
+                           hipStream_t st, std::string& err) {
   out.clear();
   if (total > m.cap) {
     err = "match buffer too small";
     return false;
   }
-  unsigned long long ctl[8];
-  if (!hip_ok(hipMemcpy(ctl, m.ctl, sizeof(ctl), hipMemcpyDeviceToHost), "D2H ctl", err)) return false;
-  const uint32_t tile = ctl[5] ? uint32_t(ctl[5]) : 256;
-  const uint32_t n_tiles = (n_pkgs + tile - 1) / tile;
+  const uint32_t n_tiles = (n_pkgs + kTile - 1) / kTile;
   std::vector<TileDir> dir(n_tiles);
-  std::vector<uint2> raw(total);
-  if (n_tiles && !hip_ok(hipMemcpy(dir.data(), m.dir, n_tiles * sizeof(TileDir), hipMemcpyDeviceToHost), "D2H dir", err))
-    return false;
-  if (total && !hip_ok(hipMemcpy(raw.data(), m.pairs, total * sizeof(uint2), hipMemcpyDeviceToHost), "D2H matches", err))
+  std::vector<uint32_t> pk(total), ad(total);
+  if ((n_tiles && !hip_ok(hipMemcpyAsync(dir.data(), m.dir, n_tiles * sizeof(TileDir), hipMemcpyDeviceToHost, st),
+                          "D2H dir", err)) ||
+      (total && (!hip_ok(hipMemcpyAsync(pk.data(), m.pkg, total * 4, hipMemcpyDeviceToHost, st), "D2H matches", err) ||
+                 !hip_ok(hipMemcpyAsync(ad.data(), m.adv, total * 4, hipMemcpyDeviceToHost, st), "D2H matches", err))) ||
+      !hip_ok(hipStreamSynchronize(st), "D2H matches", err))
     return false;
   out.reserve(total);
-  for (const TileDir& d : dir) out.insert(out.end(), raw.begin() + d.base, raw.begin() + d.base + d.count);
+  for (const TileDir& d : dir)
+    for (uint64_t i = d.base; i < d.base + d.count; i++) out.push_back(make_uint2(pk[i], ad[i]));
   return true;
+}
+
+bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_begin, uint32_t t_end, hipStream_t pst,
+                          hipStream_t sst, hipEvent_t ev, std::string& err) {
+  (void)hipSetDevice(dev_);
+  if (t_end > b.n_tiles) t_end = b.n_tiles;
+  if (t_begin >= t_end) return true;
+  if (t_end > m.dir_cap) {
+    err = "tile directory smaller than the batch";
+    return false;
+  }
+  const int vi = resolve_variant(variant_, b.gm);
+  last_launched_ = vi;
+  const uint32_t nt = t_end - t_begin;
+  const uint32_t p0 = t_begin * kTile;
+  const uint32_t n = std::min<uint32_t>(b.n, t_end * kTile) - p0;
+  ProbeArgs pa;
+  pa.db = d_;
+  pa.pk = b.pk + p0;
+  pa.tile_off = b.tile_off + t_begin;
+  pa.arena = b.arena;
+  pa.n = n;
+  pa.p0 = p0;
+  pa.n_total = b.n;
+  pa.rec = b.rec + p0;
+  pa.tail = b.tail + p0;
+  pa.ctl = m.ctl;
+  pa.spill = spill_;
+  pa.spill_cap = spill_cap_;
+  const bool fused = kFusedVariant[vi - 1];
+  if (!fused) {
+    probe_fn(b.gm)(nt, pst, pa);
+    if (!hip_ok(hipGetLastError(), "probe kernel launch", err)) return false;
+    if (sst != pst && (!hip_ok(hipEventRecord(ev, pst), "hipEventRecord", err) ||
+                       !hip_ok(hipStreamWaitEvent(sst, ev, 0), "hipStreamWaitEvent", err)))
+      return false;
+  }
+  SweepArgs sa;
+  sa.db = d_;
+  sa.rec = b.rec + p0;
+  sa.tail = b.tail + p0;
+  sa.spill = spill_;
+  sa.attr = b.attr ? b.attr + p0 : nullptr;
+  sa.cpe_bits = b.cpe_bits;
+  sa.cpe_words = b.cpe_words;
+  sa.n_cpe_sets = b.n_cpe_sets;
+  sa.n = n;
+  sa.p0 = p0;
+  sa.out_base = b.pkg_base;
+  sa.n_tiles = nt;
+  sa.t0 = t_begin;
+  sa.dir = m.dir;
+  sa.out_pkg = m.pkg;
+  sa.out_adv = m.adv;
+  sa.out_cap = m.cap;
+  sa.ctl = m.ctl;
+  if (fused) {
+    FusedArgs fa;
+    fa.pa = pa;
+    fa.sa = sa;
+    fused_fn(b.gm, vi)(nt, pst, fa);
+    return hip_ok(hipGetLastError(), "match kernel launch", err);
+  }
+  const bool filt = (b.gm & ~GM_DEB) != 0;
+  sweep_table(filt)[vi - 1](nt, sst, sa);
+  return hip_ok(hipGetLastError(), "sweep kernel launch", err);
 }
 
 bool Engine::launch(const DevBatch& b, const DevMatches& m, hipStream_t st, std::string& err) {
   (void)hipSetDevice(dev_);
-  const int vi = resolve_variant(variant_, b.gm);
-  const VariantInfo& v = variant_info(vi);
-  last_launched_ = vi;
-  const uint32_t n_tiles = (b.n + v.tile - 1) / v.tile;
-  if (n_tiles > m.dir_cap) {
-    err = "tile directory smaller than the batch";
-    return false;
-  }
-  const uint64_t kslots = v.kg ? uint64_t(n_tiles) * v.tile * v.kw : 0;  // KG: per-package key slots
-  if (!ensure_scratch(b.spill_words + kslots, err)) return false;
+  if (!ensure_scratch(b.spill_words, err)) return false;
   if (!hip_ok(hipMemsetAsync(m.ctl, 0, 8 * sizeof(unsigned long long), st), "memset(ctl)", err)) return false;
-  if (n_tiles == 0) return true;
-  MatchArgs a;
-  a.db = d_;
-  a.desc = b.desc;
-  a.arena = b.arena;
-  a.attr = b.attr;
-  a.cpe_bits = b.cpe_bits;
-  a.cpe_words = b.cpe_words;
-  a.n_cpe_sets = b.n_cpe_sets;
-  a.n = b.n;
-  a.n_tiles = n_tiles;
-  a.out = m.pairs;
-  a.out_cap = m.cap;
-  a.dir = m.dir;
-  a.ctl = m.ctl;
-  a.kbuf = spill_;
-  a.spill = spill_ + kslots;
-  a.spill_cap = spill_cap_ - kslots;
-  launch_fn(grammar_index(b.gm), vi)(n_tiles, st, a);
-  return hip_ok(hipGetLastError(), "match_kernel launch", err);
+  if (b.n_tiles == 0) return true;
+  // chunk overlap on two streams (TVM_OVERLAP=1): measured slower than one launch
+  static const bool overlap = std::getenv("TVM_OVERLAP") != nullptr;
+  const uint32_t chunks =
+      overlap ? std::max<uint32_t>(1, std::min<uint32_t>(kMaxChunks, b.n_tiles / kMinChunkTiles)) : 1u;
+  if (chunks == 1) return launch_tiles(b, m, 0, b.n_tiles, st, st, nullptr, err);
+  // chunk c: probe on st, sweep on stream2_ behind the probe's event; st then waits for the
+  // last sweep, so a caller synchronising st sees the whole pass
+  const uint32_t per = (b.n_tiles + chunks - 1) / chunks;
+  if (!hip_ok(hipEventRecord(ev_done_, st), "hipEventRecord", err) ||
+      !hip_ok(hipStreamWaitEvent(stream2_, ev_done_, 0), "hipStreamWaitEvent", err))  // ctl zeroed first
+    return false;
+  for (uint32_t c = 0; c < chunks; c++)
+    if (!launch_tiles(b, m, c * per, std::min(b.n_tiles, (c + 1) * per), st, stream2_, ev_[c], err)) return false;
+  return hip_ok(hipEventRecord(ev_done_, stream2_), "hipEventRecord", err) &&
+         hip_ok(hipStreamWaitEvent(st, ev_done_, 0), "hipStreamWaitEvent", err);
 }
 
 bool Engine::match_host(const HostBatch& hb, std::vector<uint2>& out, int64_t& err_pkg, std::string& err) {
   out.clear();
   err_pkg = -1;
-  if (hb.desc.empty()) return true;
+  if (hb.pk.empty()) return true;
   std::lock_guard<std::mutex> lk(call_mu_);
   DevBatch b;
   if (!upload(hb, b, err)) {
     free_batch(b);
     return false;
   }
-  uint64_t cap = std::max<uint64_t>(hb.desc.size() * 4, 1024);
+  uint64_t cap = std::max<uint64_t>(hb.pk.size() * 4, 1024);
   bool ok = true;
   for (int attempt = 0; attempt < 2 && ok; attempt++) {
     DevMatches m;
-    ok = alloc_matches(cap, b.n, m, err) && launch(b, m, stream_, err) &&
-         hip_ok(hipStreamSynchronize(stream_), "match_kernel", err);
+    ok = alloc_matches(cap, b.n, m, err) && launch(b, m, stream_, err);
     unsigned long long ctl[8] = {0};
-    if (ok) ok = hip_ok(hipMemcpy(ctl, m.ctl, sizeof(ctl), hipMemcpyDeviceToHost), "D2H ctl", err);
+    if (ok) ok = hip_ok(hipMemcpyAsync(ctl, m.ctl, sizeof(ctl), hipMemcpyDeviceToHost, stream_), "D2H ctl", err) &&
+                 hip_ok(hipStreamSynchronize(stream_), "match kernels", err);
     if (ok && ctl[3]) {
       err = "match kernel internal error bits " + std::to_string(ctl[3]);
       ok = false;
@@ -335,7 +456,7 @@ bool Engine::match_host(const HostBatch& hb, std::vector<uint2>& out, int64_t& e
     }
     if (ok) {
       err_pkg = ctl[1] ? int64_t(b.n - ctl[1]) : -1;
-      ok = fetch_ordered(m, b.n, ctl[0], out, err);
+      ok = fetch_ordered(m, b.n, ctl[0], out, stream_, err);
     }
     free_matches(m);
     break;
@@ -343,10 +464,6 @@ bool Engine::match_host(const HostBatch& hb, std::vector<uint2>& out, int64_t& e
   free_batch(b);
   return ok;
 }
-
-}  // namespace tvm
-
-namespace tvm {
 
 bool Engine::verify(std::string& err) {
   (void)hipSetDevice(dev_);

@@ -28,7 +28,7 @@ struct FillArgs {
   FillDev t;
   const uint4* items;    // ITEMS
   const uint8_t* arena;  // ITEMS: vulnerability-ID bytes
-  const uint2* pairs;    // PAIRS
+  const uint32_t* adv;   // PAIRS: the ordered match list's advisory column
   const unsigned long long* n_dev;  // PAIRS: match count written by the match kernel
   uint64_t n;            // ITEMS: item count; PAIRS: pair-buffer capacity
   uint4* out;
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(kFillTile) void fill_pairs_kernel(FillArgs a) {
   const uint64_t n = *a.n_dev < a.n ? *a.n_dev : a.n;
   const uint64_t stride = uint64_t(gridDim.x) * kFillTile;
   for (uint64_t i = uint64_t(blockIdx.x) * kFillTile + threadIdx.x; i < n; i += stride) {
-    const uint32_t adv = a.pairs[i].y;
+    const uint32_t adv = a.adv[i];
     const uint4 item = adv < a.t.n_advs ? a.t.adv_items[adv] : make_uint4(0, SRC_NONE << 16, 0, FILL_NOT_FOUND);
     a.out[i] = decide(a.t, item, item.w);
   }
@@ -218,12 +218,12 @@ bool FillEngine::run_host(const std::vector<uint4>& items, const std::vector<uin
   return hip_ok(hipStreamSynchronize(stream_), "fill sync", err) && ok;
 }
 
-bool FillEngine::launch_pairs(const uint2* pairs, const unsigned long long* n_dev, uint64_t cap, uint4* out,
+bool FillEngine::launch_pairs(const uint32_t* adv, const unsigned long long* n_dev, uint64_t cap, uint4* out,
                               hipStream_t stream, std::string& err) {
   if (cap == 0) return true;
   FillArgs a{};
   a.t = *d_;
-  a.pairs = pairs;
+  a.adv = adv;
   a.n_dev = n_dev;
   a.n = cap;
   a.out = out;
@@ -233,14 +233,14 @@ bool FillEngine::launch_pairs(const uint2* pairs, const unsigned long long* n_de
   return hip_ok(hipGetLastError(), "fill_kernel launch", err);
 }
 
-uint64_t FillEngine::pair_bytes(const std::vector<uint2>& pairs) const {
-  // per pair: the pair (8) + its advisory's item (16) + the record (16) + its entry words
-  // (4 each) + the decision (16); no cache-reuse credit
+uint64_t FillEngine::pair_bytes(const std::vector<uint32_t>& adv) const {
+  // per pair: its advisory index (4) + the advisory's item (16) + the record (16) + its
+  // entry words (4 each) + the decision (16); no cache-reuse credit
   uint64_t b = 0;
-  for (const uint2& p : pairs) {
-    b += 8 + 16 + 16;
-    if (p.y < t_->adv_items.size()) {
-      const uint32_t rec = t_->adv_items[p.y].w;
+  for (const uint32_t a : adv) {
+    b += 4 + 16 + 16;
+    if (a < t_->adv_items.size()) {
+      const uint32_t rec = t_->adv_items[a].w;
       if (rec != FILL_NOT_FOUND) b += 16 + 4ull * t_->recs[rec].y;
     }
   }

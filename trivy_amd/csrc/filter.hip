@@ -42,7 +42,8 @@ constexpr unsigned long long kEmpty = ~0ull;  // sort key of a dropped pair
 
 struct FilterArgs {
   FillDev t;
-  const uint2* pairs;
+  const uint32_t* pkg;  // the ordered match list (package, advisory columns)
+  const uint32_t* adv;
   const uint4* fill;
   uint64_t n;
   const uint32_t* pkg_rank;     // per package: rank of (result, name, version) in the batch
@@ -85,7 +86,7 @@ __device__ __forceinline__ uint32_t pair_severity(const FillDev& t, uint4 d, uin
 __global__ __launch_bounds__(kFilterBlock) void filter_mark(FilterArgs a) {
   const uint64_t stride = uint64_t(gridDim.x) * kFilterBlock;
   for (uint64_t i = uint64_t(blockIdx.x) * kFilterBlock + threadIdx.x; i < a.n; i += stride) {
-    const uint2 p = a.pairs[i];
+    const uint2 p = make_uint2(a.pkg[i], a.adv[i]);
     const uint4 d = a.fill[i];
     const uint4 it = a.t.adv_items[p.y];
     const uint2 rk = a.t.adv_rank[p.y];
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(kFilterBlock) void filter_select(FilterArgs a) {
   uint32_t live_n = 0;  // survivors seen by this lane; one counter atomic per block at the end
   for (uint64_t i = uint64_t(blockIdx.x) * kFilterBlock + threadIdx.x; i < a.n; i += stride) {
     bool live = a.sort_key[i] != kEmpty;
-    const uint2 p = a.pairs[i];
+    const uint2 p = make_uint2(a.pkg[i], a.adv[i]);
     if (live && a.pkg_dup[p.x]) {  // the slot filter_mark inserted this pair's key into
       const unsigned long long own = (uint64_t(a.t.adv_rank[p.y].y) << 32) | (0xFFFFFFFFu - p.x);
       if (a.table[2 * a.mine[i] + 1] != own) {
@@ -170,12 +171,12 @@ __global__ __launch_bounds__(kFilterBlock) void filter_select(FilterArgs a) {
 
 // Pairs whose package's (result, name, version) repeats: the only ones that enter the dedup
 // table, so the table is sized (and cleared) for them alone.
-__global__ __launch_bounds__(kFilterBlock) void filter_count_dup(const uint2* pairs, const uint8_t* pkg_dup,
+__global__ __launch_bounds__(kFilterBlock) void filter_count_dup(const uint32_t* pkg, const uint8_t* pkg_dup,
                                                                  uint64_t n, unsigned long long* count) {
   __shared__ uint32_t wsum[kFilterBlock / 64];
   const uint64_t stride = uint64_t(gridDim.x) * kFilterBlock;
   uint32_t c = 0;
-  for (uint64_t i = uint64_t(blockIdx.x) * kFilterBlock + threadIdx.x; i < n; i += stride) c += pkg_dup[pairs[i].x];
+  for (uint64_t i = uint64_t(blockIdx.x) * kFilterBlock + threadIdx.x; i < n; i += stride) c += pkg_dup[pkg[i]];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
@@ -187,10 +188,10 @@ __global__ __launch_bounds__(kFilterBlock) void filter_count_dup(const uint2* pa
   }
 }
 
-__global__ __launch_bounds__(kFilterBlock) void filter_gather(const uint2* pairs, const uint32_t* idx, uint64_t n,
-                                                              uint2* out) {
+__global__ __launch_bounds__(kFilterBlock) void filter_gather(const uint32_t* pkg, const uint32_t* adv,
+                                                              const uint32_t* idx, uint64_t n, uint2* out) {
   const uint64_t i = uint64_t(blockIdx.x) * kFilterBlock + threadIdx.x;
-  if (i < n) out[i] = pairs[idx[i]];
+  if (i < n) out[i] = make_uint2(pkg[idx[i]], adv[idx[i]]);
 }
 
 bool ok(hipError_t e, const char* what, std::string& err) {
@@ -227,7 +228,7 @@ bool BatchFilter::set_packages(const std::vector<uint32_t>& pkg_rank, const std:
           ok(hipMemcpy(bufs_[1], pkg_dup.data(), pkg_dup.size(), hipMemcpyHostToDevice), "hipMemcpy(pkg dup)", err));
 }
 
-bool BatchFilter::run(const FillDev& t, const uint2* pairs, const uint4* fill, uint64_t n,
+bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv, const uint4* fill, uint64_t n,
                       const std::vector<uint32_t>& ignore, const std::vector<uint64_t>& vex, uint32_t n_ranks,
                       uint32_t sev_mask, uint32_t status_mask, hipStream_t st, std::string& err) {
   n_ = n;
@@ -243,7 +244,7 @@ bool BatchFilter::run(const FillDev& t, const uint2* pairs, const uint4* fill, u
     unsigned long long dup_n = 0;
     if (!grow(bufs_[10], caps_[10], 8, err) || !ok(hipMemsetAsync(bufs_[10], 0, 8, st), "memset(dup count)", err))
       return false;
-    hipLaunchKernelGGL(filter_count_dup, dim3(blocks), dim3(kFilterBlock), 0, st, pairs,
+    hipLaunchKernelGGL(filter_count_dup, dim3(blocks), dim3(kFilterBlock), 0, st, pkg,
                        static_cast<const uint8_t*>(bufs_[1]), n, static_cast<unsigned long long*>(bufs_[10]));
     if (!ok(hipGetLastError(), "filter_count_dup", err) ||
         !ok(hipMemcpyAsync(&dup_n, bufs_[10], 8, hipMemcpyDeviceToHost, st), "D2H dup count", err) ||
@@ -300,7 +301,8 @@ bool BatchFilter::run(const FillDev& t, const uint2* pairs, const uint4* fill, u
   if (!ok(hipMemsetAsync(bufs_[10], 0, 8, st), "memset(count)", err)) return false;
   FilterArgs a{};
   a.t = t;
-  a.pairs = pairs;
+  a.pkg = pkg;
+  a.adv = adv;
   a.fill = fill;
   a.n = n;
   a.pkg_rank = static_cast<const uint32_t*>(bufs_[0]);
@@ -333,7 +335,7 @@ bool BatchFilter::run(const FillDev& t, const uint2* pairs, const uint4* fill, u
   survivors_ = cnt;
   if (cnt) {
     hipLaunchKernelGGL(filter_gather, dim3(uint32_t((cnt + kFilterBlock - 1) / kFilterBlock)), dim3(kFilterBlock), 0,
-                       st, pairs, static_cast<const uint32_t*>(bufs_[8]), uint64_t(cnt),
+                       st, pkg, adv, static_cast<const uint32_t*>(bufs_[8]), uint64_t(cnt),
                        static_cast<uint2*>(bufs_[11]));
     if (!ok(hipGetLastError(), "filter gather", err)) return false;
   }

@@ -1,176 +1,320 @@
-// The fused match kernel (gfx950 / CDNA4), as templates.
+// The match path on gfx950 (CDNA4): two kernels per batch (or per pipeline chunk).
 //
 // Replaces the per-package loops of the reference drivers (e.g.
 // pkg/detector/ospkg/debian/debian.go:65-117, ubuntu/ubuntu.go:86-126,
-// library/driver.go:111-137) with one launch over a whole batch of packages from
-// many targets.  One workgroup owns a tile of T consecutive packages (one per lane):
+// library/driver.go:111-137) with two launches over a whole batch of packages from many
+// targets.  Both kernels tile the batch into T = 256 consecutive packages per workgroup.
 //
-//   0. stage: the tile's name/version bytes (one contiguous arena window) are copied
-//      into LDS with coalesced 16-byte loads, so the byte-serial hashing/parsing below
-//      runs on LDS latency instead of global latency;
-//   1. probe+encode (lane per package): hash (platform, name), linear-probe the
-//      open-addressing index (slot hash and value loaded together), verify the name
-//      bytes, and encode the installed version into its sort key in LDS (verkey.h, the
-//      same code the flattener ran on the advisory side at load time);
-//   2. block exclusive scan of the per-package row counts (wave shuffles + LDS);
-//   3. pair sweep: the tile's (package, row) pairs are dealt T at a time to the lanes
-//      (binary search of the LDS scan maps pair -> package); each pair is one interval
-//      test against a 32-byte row whose first 16 key bytes are inline, so most pairs
-//      cost one row load; the next chunk's row is loaded before the current one is
-//      tested (software pipelining); a Zipf-heavy key makes its tile loop longer, never
-//      a single lane;
-//   4. ballot/popcount compaction into an LDS match buffer, then one atomic reservation
-//      per tile and a tile directory entry: the per-package advisory lists come out in
-//      (package, row) order within each tile segment with no inter-tile waiting.
+//   probe_kernel  (lane per package; no barrier after the staging step)
+//     0. the tile's packages are {plat, name_len | ver_len << 16} with their name and
+//        version bytes back to back in the arena from tile_off[t]: a block scan of the
+//        lengths gives every lane its string offsets, and the tile's byte window is staged
+//        into LDS with coalesced 16-byte loads;
+//     1. the installed version is encoded into its sort key (verkey.h / libver.h: the same
+//        code the flattener ran over the advisory bounds at load time); the first 16 key
+//        bytes stay in registers (big-endian, ready for two u64 compares), bytes 16..31 go
+//        to a per-package tail slot, longer keys to the spill area;
+//     2. the name is read as words (aligned LDS dwords + v_alignbyte), hashed word by word
+//        and probed in the open-addressing index (one 64-B slot = hash, rows, first 40 name
+//        bytes), so a probe is one memory round trip;
+//     3. out: per package {k0, k1} and {row_begin, row_count, key info, spill offset}.
+//   sweep_kernel
+//     0. the tile's package records are read (coalesced) into LDS; a block scan of the
+//        row counts over the packages that have rows (ballot-compacted) spans the tile's
+//        (package, row) pair space, and a byte map pair -> package is filled in LDS;
+//     1. rounds of K x 256 pairs: pair j = b0 + k * 256 + lane, so a wave's lanes read
+//        consecutive 32-B rows (coalesced) and every lane has K row loads in flight before
+//        it tests any;
+//     2. per pair one interval test (two u64 compares on the inline 16-byte bound head,
+//        the key tails only on a 16-byte tie); compaction in pair order by one wave ballot
+//        per sub-round and one barrier per round, into an LDS buffer;
+//     3. one atomic reservation per tile places its segment; the tile directory (base,
+//        count) gives the global (package, advisory) order without inter-tile waiting.
+//   The two kernels of consecutive chunks of a pass run on two streams (engine.hip), so one
+//   chunk's probe overlaps the previous chunk's sweep on the same CUs: both are latency-bound.
 //
-// All arithmetic is integer/byte; the kernel is bound by memory latency/traffic
-// (rows, keys, descriptors, strings), never by ALU.
-//
-// The templates are instantiated in kern_*.hip, one translation unit per grammar set
-// (libver.h GM_*) and variant list (match_variants.h), so the build compiles them in
-// parallel; engine.hip only holds the launch tables.
+// All arithmetic is integer/byte work bound by memory traffic and latency: no MFMA.
+// Templates are instantiated per grammar set (libver.h GM_*) in kern_*.hip.
 #pragma once
 #include "engine.h"
 #include "libver.h"
 
 namespace tvm {
 
-struct MatchArgs {
+constexpr uint32_t kStage = 12288;  // LDS bytes for a tile's strings (larger windows read global memory)
+constexpr uint32_t kKeyWords = 4;   // key bytes kept per package (head 16 in registers, tail 16 in a slot)
+constexpr uint32_t kMapCap = 4096;  // tiles with at most this many pairs map pair -> package by an LDS byte map
+
+struct ProbeArgs {
   DevDB db;
-  const uint4* desc;
+  const uint2* pk;           // chunk-relative: {plat, name_len | ver_len << 16}
+  const uint64_t* tile_off;  // chunk-relative: arena offset of each tile's first package (+1)
   const uint8_t* arena;
-  const uint2* attr;       // per-package attributes, nullptr when no row of the DB filters
+  uint32_t n;                // packages in this launch
+  uint32_t p0;               // batch index of the launch's first package
+  uint32_t n_total;          // packages in the whole batch (poisoned-package encoding)
+  PkgRec* rec;               // chunk-relative
+  uint4* tail;               // chunk-relative
+  unsigned long long* ctl;   // [1] n_total - first poisoned, [2] spill words used, [3] error bits
+  uint64_t* spill;
+  uint64_t spill_cap;
+};
+
+struct SweepArgs {
+  DevDB db;
+  const PkgRec* rec;         // chunk-relative
+  const uint4* tail;
+  const uint64_t* spill;
+  const uint2* attr;         // per-package attributes (chunk-relative), nullptr when no row filters
   const uint32_t* cpe_bits;
   uint32_t cpe_words;
   uint32_t n_cpe_sets;
   uint32_t n;
-  uint32_t n_tiles;
-  uint2* out;
+  uint32_t p0;
+  uint32_t out_base;         // added to every output package index (a shard's first global package)
+  uint32_t n_tiles;          // tiles in this launch
+  uint32_t t0;               // batch index of the launch's first tile
+  TileDir* dir;              // batch-indexed tile directory (tile t0 + i)
+  uint32_t* out_pkg;
+  uint32_t* out_adv;
   uint64_t out_cap;
-  TileDir* dir;
-  unsigned long long* ctl;  // [0] total, [1] n - first poisoned, [2] spill used, [3] err bits, [4] ticket, [5] tile size
-  uint64_t* spill;
-  uint64_t spill_cap;
-  uint64_t* kbuf;  // KG variants: installed-key slots in global memory, KW words per package
+  unsigned long long* ctl;   // [0] total matches (reservation counter)
 };
 
-using LaunchFn = void (*)(uint32_t n_tiles, hipStream_t st, const MatchArgs& a);
+struct FusedArgs {
+  ProbeArgs pa;
+  SweepArgs sa;
+};
+
+using ProbeFn = void (*)(uint32_t n_tiles, hipStream_t st, const ProbeArgs& a);
+using SweepFn = void (*)(uint32_t n_tiles, hipStream_t st, const SweepArgs& a);
+using FusedFn = void (*)(uint32_t n_tiles, hipStream_t st, const FusedArgs& a);
 
 namespace {
 
 enum : uint32_t { KI_VALID = 1u << 31, KI_SPILL = 1u << 30, KI_LEN = 0x3FFFu, KI_CLS_SHIFT = 26, KI_CLS_MASK = 7u };
 
-// FILT: the batch's grammar set has rows with per-package predicates (RowAux); dpkg-only
-// batches (GM_DEB) never do, so their tiles carry no package attributes (2 KB less LDS per
-// block = one more resident workgroup per CU).
-template <int T, int KW, int MB, bool KG, bool FILT>
-struct TileShared {
-  uint64_t key[KG ? 1 : T * KW];  // installed keys (KG: in global memory instead)
-  union {
-    uint2 mbuf[MB];           // phase 3: compacted matches
-    uint4 stage[MB / 2];      // phase 0/1: the tile's name/version bytes
-  };
-  uint32_t scan[T + 1];       // exclusive scan of row counts
-  uint32_t rbeg[T];           // first row per package
-  uint32_t kinfo[T];          // key length | flags
-  uint32_t koff[T];           // spill word offset when KI_SPILL
-  uint2 pattr[FILT ? T : 1];  // package attributes (filtered rows only)
-  uint32_t wsum[T / 64];
-  uint32_t tile;
-  uint32_t span_lo, span_hi;  // arena window of the tile's strings
-  unsigned long long base;
-};
-
-__device__ __forceinline__ bool name_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
-  for (uint32_t i = 0; i < n; i++)
-    if (a[i] != b[i]) return false;
-  return true;
-}
-
-// key_hash (common.h) fused with packing the name's first kSlotNameWords*8 bytes into
-// words (memory order, zero padded), so the slot's inline name is verified with word
-// compares.  Registers only (an if-chain, no dynamically indexed array).
-__device__ __forceinline__ uint64_t hash_pack(uint32_t plat, const uint8_t* s, uint32_t n,
-                                              uint64_t (&w)[kSlotNameWords]) {
-  static_assert(kSlotNameWords == 5, "hash_pack fills exactly five words");
-  uint64_t h = key_hash_seed(plat), cur = 0;
-  w[0] = w[1] = w[2] = w[3] = w[4] = 0;
-  for (uint32_t i = 0; i < n; i++) {
-    const uint8_t c = s[i];
-    h = key_hash_step(h, c);
-    cur |= uint64_t(c) << (8 * (i & 7));
-    if ((i & 7) == 7 || i + 1 == n) {  // a word is complete (or the name ends)
-      const uint32_t k = i >> 3;
-      if (k == 0) w[0] = cur;
-      else if (k == 1) w[1] = cur;
-      else if (k == 2) w[2] = cur;
-      else if (k == 3) w[3] = cur;
-      else if (k == 4) w[4] = cur;
-      cur = 0;
-    }
-  }
-  return key_hash_fin(h);
-}
-
-// Name check against a slot (its first 40 bytes inline, loaded with the hash); names
-// longer than 40 bytes finish bytewise against the name arena.
-__device__ __forceinline__ bool name_eq_slot(const uint64_t (&w)[kSlotNameWords], const uint4 q1, const uint4 q2,
-                                             const uint4 q3, const uint8_t* name, const uint8_t* arena, uint32_t n) {
-  const uint64_t y0 = q1.z | (uint64_t(q1.w) << 32), y1 = q2.x | (uint64_t(q2.y) << 32),
-                 y2 = q2.z | (uint64_t(q2.w) << 32), y3 = q3.x | (uint64_t(q3.y) << 32),
-                 y4 = q3.z | (uint64_t(q3.w) << 32);
-  bool eq = w[0] == y0;  // zero padded on both sides, so a short name compares whole words
-  eq &= w[1] == y1;
-  eq &= w[2] == y2;
-  eq &= w[3] == y3;
-  eq &= w[4] == y4;
-  if (eq && n > 8 * kSlotNameWords) {
-    const uint8_t* full = arena + q1.y;
-    for (uint32_t i = 8 * kSlotNameWords; eq && i < n; i++) eq = full[i] == name[i];
-  }
-  return eq;
-}
-
-// Block-wide exclusive scan of v over T lanes; returns the block total.
-template <int T, class S>
-__device__ __forceinline__ uint32_t block_scan(S& s, uint32_t v, uint32_t tid) {
+// Block-wide exclusive scan of v over T lanes (wave shuffles + one LDS exchange); returns
+// the block total.  `wsum` holds T/64 words; two barriers.
+template <int T>
+__device__ __forceinline__ uint32_t block_exscan(uint32_t* wsum, uint32_t v, uint32_t tid, uint32_t& excl) {
   constexpr int W = T / 64;
   const uint32_t lane = tid & 63, wave = tid >> 6;
   uint32_t x = v;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    uint32_t y = __shfl_up(x, d, 64);
+    const uint32_t y = __shfl_up(x, d, 64);
     if (lane >= uint32_t(d)) x += y;
   }
-  if (lane == 63) s.wsum[wave] = x;
+  if (lane == 63) wsum[wave] = x;
   __syncthreads();
   uint32_t off = 0, tot = 0;
 #pragma unroll
   for (int w = 0; w < W; w++) {
-    uint32_t t = s.wsum[w];
+    const uint32_t t = wsum[w];
     off += (uint32_t(w) < wave) ? t : 0;
     tot += t;
   }
-  s.scan[tid] = off + x - v;
-  if (tid == 0) s.scan[T] = tot;
+  excl = off + x - v;
   __syncthreads();
   return tot;
 }
 
-// Package of pair j: the last q with scan[q] <= j (its count is > 0 since j < scan[q + 1]).
-template <int T, class S>
-__device__ __forceinline__ uint32_t pair_pkg(const S& s, uint32_t j) {
-  uint32_t lo = 0, hi = T;  // invariant: scan[lo] <= j < scan[hi]
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (s.scan[mid] <= j) lo = mid;
-    else hi = mid;
+// ---- probe_kernel helpers ---------------------------------------------------------------
+
+// Sort-key sink: key bytes 0..15 accumulate in two registers, bytes 16..31 go to the
+// package's tail slot; every byte is counted, so one pass both encodes a typical key and
+// sizes a long one (which is then re-encoded into the spill area).
+struct HeadSink {
+  uint64_t* tail;
+  uint64_t acc = 0, w0 = 0, w1 = 0;
+  uint32_t n = 0;
+  __device__ explicit HeadSink(uint64_t* t) : tail(t) {}
+  __device__ __forceinline__ void word(uint32_t w) {
+    if (w == 0) w0 = acc;
+    else if (w == 1) w1 = acc;
+    else if (w < kKeyWords) tail[w - 2] = acc;
   }
-  return lo;
+  __device__ __forceinline__ void put(uint8_t b) {
+    acc |= uint64_t(b) << (8 * (n & 7));
+    if ((n & 7) == 7) {
+      word(n >> 3);
+      acc = 0;
+    }
+    n++;
+  }
+  __device__ __forceinline__ void flush() {
+    if (n & 7) word(n >> 3);
+  }
+};
+
+__device__ __forceinline__ uint64_t be_word(uint64_t w, uint32_t bytes) {  // bytes in [1, 8]
+  if (bytes < 8) w &= (1ull << (8 * bytes)) - 1ull;
+  return __builtin_bswap64(w);
 }
 
+// Name bytes -> words.  `s` may sit at any byte offset; the bytes are read as aligned
+// dwords and funnel-shifted (v_alignbyte), so an 8-byte word costs three dword loads
+// instead of eight byte loads.  Word i is zero past the name's end.
+template <class P>
+__device__ __forceinline__ uint64_t name_word(const P* base, uint32_t sh, uint32_t i, uint32_t n) {
+  const uint32_t d0 = base[2 * i], d1 = base[2 * i + 1], d2 = base[2 * i + 2];
+  const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh), hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
+  uint64_t w = uint64_t(lo) | (uint64_t(hi) << 32);
+  const uint32_t left = n - 8 * i;  // > 0
+  if (left < 8) w &= (1ull << (8 * left)) - 1ull;
+  return w;
+}
+
+// Hash of (plat, name) from the name's bytes, word by word.
+template <class P>
+__device__ __forceinline__ uint64_t name_hash(uint32_t plat, const uint8_t* s, uint32_t n) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(s);
+  const P* base = reinterpret_cast<const P*>(a & ~uintptr_t(3));
+  const uint32_t sh = uint32_t(a & 3);
+  uint64_t h = key_hash_seed2(plat, n);
+  for (uint32_t i = 0; 8 * i < n; i++) h = key_hash_word(h, name_word(base, sh, i, n));
+  return key_hash_fin(h);
+}
+
+// Name check against a slot (first 40 bytes inline, loaded with the hash; the name's words
+// are re-read, which is cheaper than keeping five words live across the probe); longer
+// names finish bytewise against the name arena.
+template <class P>
+__device__ __forceinline__ bool name_eq_slot(const uint8_t* s, uint32_t n, const uint4 q1, const uint4 q2,
+                                             const uint4 q3, const uint8_t* arena) {
+  static_assert(kSlotNameWords == 5, "five inline name words");
+  const uintptr_t a = reinterpret_cast<uintptr_t>(s);
+  const P* base = reinterpret_cast<const P*>(a & ~uintptr_t(3));
+  const uint32_t sh = uint32_t(a & 3);
+  const uint64_t y[kSlotNameWords] = {q1.z | (uint64_t(q1.w) << 32), q2.x | (uint64_t(q2.y) << 32),
+                                      q2.z | (uint64_t(q2.w) << 32), q3.x | (uint64_t(q3.y) << 32),
+                                      q3.z | (uint64_t(q3.w) << 32)};
+  bool eq = true;
+#pragma unroll
+  for (uint32_t i = 0; i < kSlotNameWords; i++) eq &= (8 * i < n ? name_word(base, sh, i, n) : 0ull) == y[i];
+  if (eq && n > 8 * kSlotNameWords) {
+    const uint8_t* full = arena + q1.y;
+    for (uint32_t i = 8 * kSlotNameWords; eq && i < n; i++) eq = full[i] == s[i];
+  }
+  return eq;
+}
+
+// One package: encode, hash, probe.  P = uint32_t in the LDS or global address space of s.
+template <uint32_t GM, class P, int DIAG = 0>
+__device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32_t plat, uint32_t nlen, uint32_t vlen,
+                                          const uint8_t* name, const uint8_t* ver, PkgRec& r) {
+  const PlatInfo pi = a.db.plats[plat];
+  uint64_t* tslot = reinterpret_cast<uint64_t*>(a.tail + p);
+  HeadSink hs(tslot);
+  uint32_t cls = 0;
+  bool valid = true;
+  if (DIAG & 1) {
+    hs.n = vlen;
+    hs.w0 = vlen;
+  } else {
+    valid = encode_version_gm<GM>(pi.cmp, ver, vlen, hs, cls);
+  }
+  hs.flush();
+  uint32_t kinfo = 0, koff = 0;
+  if (valid && hs.n > kKeyWords * 8) {  // long key: the whole key again into the spill area
+    const uint32_t need = (hs.n + 7) / 8;
+    const unsigned long long o = atomicAdd(&a.ctl[2], (unsigned long long)need);
+    if (o + need > a.spill_cap) {
+      atomicOr(&a.ctl[3], (unsigned long long)ERR_SPILL);
+      valid = false;
+    } else {
+      WordSink ws(a.spill + o);
+      uint32_t cls2 = 0;
+      encode_version_gm<GM>(pi.cmp, ver, vlen, ws, cls2);
+      ws.flush();
+      koff = uint32_t(o);
+      kinfo |= KI_SPILL;
+    }
+  }
+  const uint32_t kl = hs.n;
+  kinfo |= (kl & KI_LEN) | (valid ? KI_VALID : 0u) | ((cls & KI_CLS_MASK) << KI_CLS_SHIFT);
+  r.k0 = valid && kl ? be_word(hs.w0, kl < 8 ? kl : 8) : 0ull;
+  r.k1 = valid && kl > 8 ? be_word(hs.w1, kl < 16 ? kl - 8 : 8) : 0ull;
+  uint32_t cnt = 0, rbeg = 0;
+  // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup;
+  // lookup-first drivers (ubuntu.go:86-92) probe first, so a poisoned key still raises
+  if (!(DIAG & 2) && (valid || (pi.flags & PLAT_LOOKUP_FIRST))) {
+    const uint64_t h = name_hash<P>(plat, name, nlen);
+    for (uint64_t i = h & a.db.slot_mask;; i = (i + 1) & a.db.slot_mask) {
+      const uint4* sp = reinterpret_cast<const uint4*>(a.db.slots + i);
+      const uint4 q0 = sp[0], q1 = sp[1], q2 = sp[2], q3 = sp[3];  // the whole 64-B slot
+      const uint64_t sh = q0.x | (uint64_t(q0.y) << 32);
+      if (sh == 0) break;
+      if (sh != h) continue;
+      if ((q1.x & SLOT_LEN_MASK) != nlen || !name_eq_slot<P>(name, nlen, q1, q2, q3, a.db.name_arena)) continue;
+      if (q1.x & SLOT_POISONED) {
+        atomicMax(&a.ctl[1], (unsigned long long)(a.n_total - (a.p0 + p)));
+      } else if (valid) {
+        cnt = q0.w;
+        rbeg = q0.z;
+      }
+      break;
+    }
+  }
+  r.meta = make_uint4(rbeg, cnt, kinfo, koff);
+}
+
+template <uint32_t GM, int DIAG = 0>
+__global__ __launch_bounds__(kTile) void probe_kernel(ProbeArgs a) {
+  __shared__ uint4 stage[kStage / 16 + 2];  // +2: the dword reads of a name's last word run past its end
+  __shared__ uint32_t wsum[kTile / 64];
+  const uint32_t tid = threadIdx.x, t = blockIdx.x;
+  const uint32_t p = t * kTile + tid;
+  uint2 d = make_uint2(0xFFFFFFFFu, 0);
+  if (p < a.n) d = a.pk[p];
+  const uint32_t nlen = d.y & 0xFFFFu, vlen = d.y >> 16;
+  uint32_t off = 0;
+  block_exscan<kTile>(wsum, nlen + vlen, tid, off);
+  const uint64_t w0 = a.tile_off[t], w1 = a.tile_off[t + 1];
+  const uint64_t base16 = w0 & ~uint64_t(15);
+  const bool staged = w1 - base16 <= kStage;
+  if (staged) {
+    const uint32_t nv = uint32_t((w1 - base16 + 15) / 16);
+    const uint4* src = reinterpret_cast<const uint4*>(a.arena + base16);
+    for (uint32_t i = tid; i < nv; i += kTile) stage[i] = src[i];
+    if (tid < 2) stage[nv + tid] = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  PkgRec r;
+  r.meta = make_uint4(0, 0, 0, 0);
+  r.k0 = r.k1 = 0;
+  if (p < a.n && d.x < a.db.n_plats) {
+    if (staged) {
+      const uint8_t* sb = reinterpret_cast<const uint8_t*>(stage) + uint32_t(w0 - base16) + off;
+      probe_one<GM, uint32_t, DIAG>(a, p, d.x, nlen, vlen, sb, sb + nlen, r);
+    } else {
+      const uint8_t* gb = a.arena + w0 + off;
+      probe_one<GM, uint32_t, DIAG>(a, p, d.x, nlen, vlen, gb, gb + nlen, r);
+    }
+  }
+  if (p < a.n) a.rec[p] = r;
+}
+
+// ---- sweep_kernel helpers ---------------------------------------------------------------
+
+template <bool FILT>
+struct SweepShared {
+  uint64_t k0[kTile], k1[kTile];  // key heads by tile package
+  uint32_t kinfo[kTile];
+  uint32_t koff[kTile];           // spill word offset of a long key (KI_SPILL)
+  uint2 pattr[FILT ? kTile : 1];
+  uint32_t nz_scan[kTile + 1];    // pair offset of the r-th package that has rows (+ total)
+  uint32_t nz_rd[kTile];          // its row_begin - pair offset
+  uint32_t nz_q[kTile];           // its tile package index
+  uint32_t wsum[2][kTile / 64];
+  uint32_t wsum2[2][8 * (kTile / 64)];  // per round: K sub-rounds x wave match counts
+  uint32_t tile;
+  unsigned long long base;
+};
+
 // Per-package predicates of a ROW_FILTER row (common.h RowAux).
-__device__ __forceinline__ bool aux_pass(const MatchArgs& a, uint32_t ridx, uint2 pa, uint32_t ki) {
+__device__ __forceinline__ bool aux_pass(const SweepArgs& a, uint32_t ridx, uint2 pa, uint32_t ki) {
   const RowAux x = a.db.aux[ridx];
   const uint32_t* ids = a.db.aux_ids + x.list_off;
   if (x.kind & (AUX_ARCH_RH | AUX_ARCH_IN)) {
@@ -194,54 +338,33 @@ __device__ __forceinline__ bool aux_pass(const MatchArgs& a, uint32_t ridx, uint
   return true;
 }
 
-// The installed key's first two words are kept big-endian and zero-masked beyond the key
-// length (be_head, applied once per package in phase 1), like Row::hi_pre*, so an interval
-// bound test is two u64 compares; only 16-byte ties with both keys longer read the tails
-// (memory-order words from word 2 on).
-__device__ __forceinline__ uint64_t be_word(uint64_t w, uint32_t bytes) {  // bytes in [1, 8]
-  if (bytes < 8) w &= (1ull << (8 * bytes)) - 1ull;
-  return __builtin_bswap64(w);
-}
-__device__ __forceinline__ void be_head(uint64_t* k, uint32_t n) {
-  const uint64_t w0 = n ? be_word(k[0], n < 8 ? n : 8) : 0ull;
-  const uint64_t w1 = n > 8 ? be_word(k[1], n < 16 ? n - 8 : 8) : 0ull;
-  k[0] = w0;
-  k[1] = w1;
-}
-// sign(installed key - bound): a0/a1 the installed BE head, b0/b1 the bound's BE head.
-__device__ __forceinline__ int cmp_be(uint64_t a0, uint64_t a1, const uint64_t* a, uint32_t na, uint64_t b0,
-                                      uint64_t b1, const uint64_t* b, uint32_t nb) {
+// sign(installed key - bound) on the big-endian heads; the tails (memory-order words from
+// byte 16 on) only on a 16-byte tie with both keys longer.
+__device__ __forceinline__ int cmp_be(uint64_t a0, uint64_t a1, const uint64_t* atail, uint32_t na, uint64_t b0,
+                                      uint64_t b1, const uint64_t* btail, uint32_t nb) {
   if (a0 != b0) return a0 < b0 ? -1 : 1;
   if (a1 != b1) return a1 < b1 ? -1 : 1;
   if (na <= 16 || nb <= 16) return (na > nb) - (na < nb);
-  return key_cmp(a + 2, na - 16, b + 2, nb - 16);
+  return key_cmp(atail, na - 16, btail, nb - 16);
 }
 
-// Installed key of tile package q: the global spill area for long keys, else its slot
-// (LDS, or global memory for KG variants).
-template <int T, int KW, bool KG, class S>
-__device__ __forceinline__ const uint64_t* key_ptr(const MatchArgs& a, const S& s, uint32_t q) {
-  if (s.kinfo[q] & KI_SPILL) return a.spill + s.koff[q];
-  if constexpr (KG) return a.kbuf + size_t(s.tile * T + q) * KW;
-  else return &s.key[q * KW];
-}
-
-// Interval test of package q's installed key (k; first two words k0, k1 already loaded)
-// against one row (global index ridx).
-template <bool FILT, class S>
-__device__ __forceinline__ bool eval_row(const MatchArgs& a, const S& s, uint32_t q, const Row& row, uint32_t ridx,
-                                         const uint64_t* k, uint64_t k0, uint64_t k1) {
+// Interval test of tile package q's installed key against one row (global index ridx).
+template <bool FILT>
+__device__ __forceinline__ bool eval_row(const SweepArgs& a, const SweepShared<FILT>& s, uint32_t q, uint32_t p,
+                                         const Row& row, uint32_t ridx) {
+  const uint32_t ki = s.kinfo[q];
   if constexpr (FILT) {
-    if ((row.adv & ROW_FILTER) && !aux_pass(a, ridx, s.pattr[q], s.kinfo[q])) return false;
+    if ((row.adv & ROW_FILTER) && !aux_pass(a, ridx, s.pattr[q], ki)) return false;
   }
   if (row.adv & ROW_ALWAYS) return true;
-  const uint32_t ki = s.kinfo[q];
   if (!(ki & KI_VALID)) return false;
   const uint32_t kl = ki & KI_LEN;
+  const uint64_t k0 = s.k0[q], k1 = s.k1[q];
+  const uint64_t* ktail = (ki & KI_SPILL) ? a.spill + s.koff[q] + 2 : reinterpret_cast<const uint64_t*>(a.tail + p);
   bool m = true;
   if (!(row.hi_len & KEY_INF)) {
-    const int c = cmp_be(k0, k1, k, kl, row.hi_pre0, row.hi_pre1, a.db.key_words + row.hi_off,
-                         row.hi_len & KEY_LEN_MASK);
+    const uint64_t* hw = a.db.key_words + row.hi_off;
+    const int c = cmp_be(k0, k1, ktail, kl, row.hi_pre0, row.hi_pre1, hw + 2, row.hi_len & KEY_LEN_MASK);
     m = (row.hi_len & KEY_INCL) ? c <= 0 : c < 0;
   }
   if (m && !(row.lo_len & KEY_INF)) {  // rare (library / rpm ranges): the bound's head from the arena
@@ -249,242 +372,246 @@ __device__ __forceinline__ bool eval_row(const MatchArgs& a, const S& s, uint32_
     const uint32_t nl = row.lo_len & KEY_LEN_MASK;
     const uint64_t l0 = nl ? be_word(lw[0], nl < 8 ? nl : 8) : 0ull;
     const uint64_t l1 = nl > 8 ? be_word(lw[1], nl < 16 ? nl - 8 : 8) : 0ull;
-    const int c = cmp_be(k0, k1, k, kl, l0, l1, lw, nl);
+    const int c = cmp_be(k0, k1, ktail, kl, l0, l1, lw + 2, nl);
     m = (row.lo_len & KEY_INCL) ? c >= 0 : c > 0;
   }
   return m;
 }
 
-// One sweep over the tile's pairs.  DIRECT=false: compact into LDS (count all, store the
-// first MB).  DIRECT=true: store straight to out[base + position].
-// AB (ablation, diagnostics only): 2 = load rows but skip the key compare.
-template <int T, int KW, int MB, bool KG, bool FILT, bool DIRECT, int AB = 0>
-__device__ __forceinline__ uint32_t sweep(const MatchArgs& a, TileShared<T, KW, MB, KG, FILT>& s, uint32_t total_pairs,
-                                          uint32_t tid, unsigned long long base) {
-  constexpr int W = T / 64;
-  const uint32_t lane = tid & 63, wave = tid >> 6;
-  uint32_t nm = 0;
-  uint32_t j = tid, q = 0, ridx = 0;
-  Row row{};
-  const uint64_t* kp = nullptr;
-  uint64_t k0 = 0, k1 = 0;  // KG: the key's first words travel with the row load
-  if (j < total_pairs) {
-    q = pair_pkg<T>(s, j);
-    ridx = s.rbeg[q] + (j - s.scan[q]);
-    row = a.db.rows[ridx];
-    kp = key_ptr<T, KW, KG>(a, s, q);
-    if (KG) k0 = kp[0], k1 = kp[1];
+// Tile package (nz rank) of pair j by binary search of the nz scan (tiles too large for the map).
+template <bool FILT>
+__device__ __forceinline__ uint32_t pair_rank(const SweepShared<FILT>& s, uint32_t nnz, uint32_t j) {
+  uint32_t lo = 0, hi = nnz;  // last r with nz_scan[r] <= j
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (s.nz_scan[mid] <= j) lo = mid;
+    else hi = mid;
   }
-  for (uint32_t b0 = 0; b0 < total_pairs; b0 += T) {
-    // issue the next chunk's row load before testing this chunk's pair
-    const uint32_t jn = j + T;
-    uint32_t qn = 0, ridxn = 0;
-    Row rown{};
-    const uint64_t* kpn = nullptr;
-    uint64_t k0n = 0, k1n = 0;
-    if (jn < total_pairs) {
-      qn = pair_pkg<T>(s, jn);
-      ridxn = s.rbeg[qn] + (jn - s.scan[qn]);
-      rown = a.db.rows[ridxn];
-      kpn = key_ptr<T, KW, KG>(a, s, qn);
-      if (KG) k0n = kpn[0], k1n = kpn[1];
-    }
-    if (!KG && j < total_pairs) {
-      if (s.kinfo[q] & KI_SPILL) k0 = kp[0], k1 = kp[1];
-      else k0 = s.key[q * KW], k1 = s.key[q * KW + 1];  // LDS loads, not flat ones
-    }
-    const bool m = (j < total_pairs) && (AB == 2 ? (row.adv & 7u) == 0 : eval_row<FILT>(a, s, q, row, ridx, kp, k0, k1));
-    const unsigned long long bal = __ballot(m);
-    const uint32_t lane_off = __popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) s.wsum[wave] = uint32_t(__popcll(bal));
-    __syncthreads();
-    uint32_t woff = 0, ctot = 0;
+  return lo;
+}
+
+// One sweep over the tile's pairs in rounds of K x T: pair j = b0 + k * T + tid, so the 64
+// lanes of a wave read consecutive rows (coalesced) and every lane has K row loads in
+// flight before it tests any.  Pair -> package comes from the LDS byte map (one read).
+// Matches are placed in pair order - sub-round by sub-round, a wave ballot per sub-round and
+// one barrier per round for the wave totals - into the LDS buffer while it has room
+// (pass 1, which also counts matches per package), or straight to the output at base +
+// position (DIRECT: pass 2, for a tile with more matches than the buffer).
+template <int K, int MB, bool FILT, bool DIRECT>
+__device__ __forceinline__ uint32_t sweep(const SweepArgs& a, SweepShared<FILT>& s, uint32_t* madv, uint8_t* mq,
+                                          const uint8_t* map, uint32_t nnz, uint32_t total, uint32_t tid,
+                                          unsigned long long base) {
+  constexpr int W = kTile / 64;
+  const uint32_t lane = tid & 63, wave = tid >> 6;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  const uint32_t pbase = s.tile * kTile;
+  const bool use_map = total <= kMapCap;
+  uint32_t nm = 0, round = 0;
+  for (uint32_t b0 = 0; b0 < total; b0 += kTile * K, round++) {
+    Row row[K];
+    uint32_t qq[K], rid[K];
 #pragma unroll
-    for (int w = 0; w < W; w++) {
-      const uint32_t t = s.wsum[w];
-      woff += (uint32_t(w) < wave) ? t : 0;
-      ctot += t;
-    }
-    const uint32_t pos = nm + woff + lane_off;
-    if (m) {
-      const uint2 rec = make_uint2(s.tile * T + q, row.adv & ROW_ADV_MASK);
-      if (DIRECT) {
-        if (base + pos < a.out_cap) a.out[base + pos] = rec;
-      } else if (pos < uint32_t(MB)) {
-        s.mbuf[pos] = rec;
+    for (int k = 0; k < K; k++) {
+      const uint32_t j = b0 + k * kTile + tid;
+      qq[k] = 0;
+      rid[k] = 0;
+      if (j < total) {
+        const uint32_t r = use_map ? uint32_t(map[j]) : pair_rank(s, nnz, j);
+        qq[k] = s.nz_q[r];
+        rid[k] = j + s.nz_rd[r];
+        row[k] = a.db.rows[rid[k]];
       }
     }
-    nm += ctot;
+    uint32_t mask = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++)
+      if (b0 + k * kTile + tid < total && eval_row<FILT>(a, s, qq[k], pbase + qq[k], row[k], rid[k])) mask |= 1u << k;
+    uint32_t* ws = s.wsum2[round & 1];
+    unsigned long long bal[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      bal[k] = __ballot((mask >> k) & 1u);
+      if (lane == 0) ws[k * W + wave] = uint32_t(__popcll(bal[k]));
+    }
     __syncthreads();
-    j = jn;
-    q = qn;
-    ridx = ridxn;
-    row = rown;
-    kp = kpn;
-    k0 = k0n;
-    k1 = k1n;
+    uint32_t acc = nm;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      uint32_t woff = 0, tk = 0;
+#pragma unroll
+      for (int w = 0; w < W; w++) {
+        const uint32_t t = ws[k * W + w];
+        woff += (uint32_t(w) < wave) ? t : 0;
+        tk += t;
+      }
+      if ((mask >> k) & 1u) {
+        const uint32_t pos = acc + woff + uint32_t(__popcll(bal[k] & lt));
+        const uint32_t adv = row[k].adv & ROW_ADV_MASK;
+        if (DIRECT) {
+          if (base + pos < a.out_cap) {
+            a.out_pkg[base + pos] = a.out_base + a.p0 + pbase + qq[k];
+            a.out_adv[base + pos] = adv;
+          }
+        } else {
+          if (pos < uint32_t(MB)) {
+            madv[pos] = adv;
+            mq[pos] = uint8_t(qq[k]);
+          }
+        }
+      }
+      acc += tk;
+    }
+    nm = acc;
   }
   return nm;
 }
 
-// Phase 1 for one package: encode the installed version into its key slot and probe the
-// index.  Instantiated separately for LDS-staged and global string pointers so the staged
-// case compiles to LDS loads rather than generic (flat) ones.
-template <int T, int KW, int MB, bool KG, bool FILT, uint32_t GM, int AB>
-__device__ __forceinline__ void probe_encode(const MatchArgs& a, TileShared<T, KW, MB, KG, FILT>& s, uint32_t tid,
-                                             uint32_t p, const uint4 d, const uint8_t* name, const uint8_t* ver,
-                                             uint32_t& cnt, uint32_t& rbeg, uint32_t& kinfo, uint32_t& koff) {
-  const PlatInfo pi = a.db.plats[d.x];
-  const uint32_t nlen = d.w & 0xFFFFu, vlen = d.w >> 16;
-  // installed version -> sort key: one optimistic pass into the LDS slot; a key longer
-  // than the slot is re-encoded into the global spill area
-  bool valid = AB == 4;
-  if (AB != 4) {
-    uint64_t* slot;
-    if constexpr (KG) slot = a.kbuf + size_t(p) * KW;
-    else slot = &s.key[tid * KW];
-    CapWordSink cs(slot, KW * 8);
-    uint32_t cls = 0;
-    valid = encode_version_gm<GM>(pi.cmp, ver, vlen, cs, cls);
-    cs.flush();
-    if (valid && cs.n > uint32_t(KW * 8)) {
-      const uint32_t need = (cs.n + 7) / 8;
-      const unsigned long long o = atomicAdd(&a.ctl[2], (unsigned long long)need);
-      if (o + need > a.spill_cap) {
-        atomicOr(&a.ctl[3], (unsigned long long)ERR_SPILL);
-        valid = false;
-      } else {
-        WordSink ws(a.spill + o);
-        uint32_t cls2 = 0;
-        encode_version_gm<GM>(pi.cmp, ver, vlen, ws, cls2);
-        ws.flush();
-        koff = uint32_t(o);
-        kinfo |= KI_SPILL;
-      }
-    }
-    kinfo |= (cs.n & KI_LEN) | (valid ? KI_VALID : 0u) | ((cls & KI_CLS_MASK) << KI_CLS_SHIFT);
-    if (valid) be_head((kinfo & KI_SPILL) ? a.spill + koff : slot, cs.n);
-  }
-  // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup
-  if (AB != 3 && (valid || (pi.flags & PLAT_LOOKUP_FIRST))) {
-    uint64_t nw[kSlotNameWords];
-    const uint64_t h = hash_pack(d.x, name, nlen, nw);
-    for (uint64_t i = h & a.db.slot_mask;; i = (i + 1) & a.db.slot_mask) {
-      // the whole 64-B slot in one round trip: hash, rows, inline name
-      const uint4* sp = reinterpret_cast<const uint4*>(a.db.slots + i);
-      const uint4 q0 = sp[0], q1 = sp[1], q2 = sp[2], q3 = sp[3];
-      const uint64_t sh = q0.x | (uint64_t(q0.y) << 32);
-      if (sh == 0) break;
-      if (sh != h) continue;
-      if ((q1.x & SLOT_LEN_MASK) != nlen || !name_eq_slot(nw, q1, q2, q3, name, a.db.name_arena, nlen)) continue;
-      if (q1.x & SLOT_POISONED) {
-        atomicMax(&a.ctl[1], (unsigned long long)(a.n - p));
-      } else if (valid) {
-        cnt = q0.w;
-        rbeg = q0.z;
-      }
-      break;
-    }
-  }
-}
-
-// AB (ablation, diagnostics only): 0 = full kernel, 1 = stage+probe+encode+scan only,
-// 2 = no key compare, 3 = stage+encode+scan (no probe), 4 = stage+probe+scan (no encode).  Ablation variants produce wrong match lists by construction.
-template <int T, int KW, int MB, bool KG, uint32_t GM, int AB = 0>
-__global__ __launch_bounds__(T) void match_kernel(MatchArgs a) {
-  constexpr bool FILT = GM != GM_DEB;
-  __shared__ TileShared<T, KW, MB, KG, FILT> s;
-  constexpr uint32_t kStageBytes = MB * 8;
-  const uint32_t tid = threadIdx.x;
-  if (tid == 0) {
-    s.tile = blockIdx.x;  // segments are placed through the tile directory: any order works
-    s.span_lo = 0xFFFFFFFFu;
-    s.span_hi = 0;
-    if (blockIdx.x == 0) a.ctl[5] = T;
-  }
-  __syncthreads();
-  const uint32_t tile = s.tile;
-  const uint32_t p = tile * T + tid;
-
-  // ---- 0. stage the tile's name/version bytes in LDS (coalesced 16-byte loads) ---------
-  uint4 d = make_uint4(0xFFFFFFFFu, 0, 0, 0);
-  if (p < a.n) d = a.desc[p];
-  {
-    uint32_t lo = 0xFFFFFFFFu, hi = 0;
-    if (p < a.n) {
-      lo = d.y < d.z ? d.y : d.z;
-      const uint32_t e1 = d.y + (d.w & 0xFFFFu), e2 = d.z + (d.w >> 16);
-      hi = e1 > e2 ? e1 : e2;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const uint32_t l2 = __shfl_xor(lo, o, 64), h2 = __shfl_xor(hi, o, 64);
-      lo = l2 < lo ? l2 : lo;
-      hi = h2 > hi ? h2 : hi;
-    }
-    if ((tid & 63) == 0) {
-      atomicMin(&s.span_lo, lo);
-      atomicMax(&s.span_hi, hi);
-    }
-  }
-  __syncthreads();
-  const uint32_t base16 = s.span_lo & ~15u;
-  const bool staged = s.span_hi > base16 && s.span_hi - base16 <= kStageBytes;
-  if (staged) {
-    const uint32_t nv = (s.span_hi - base16 + 15) / 16;
-    const uint4* src = reinterpret_cast<const uint4*>(a.arena + base16);
-    for (uint32_t i = tid; i < nv; i += T) s.stage[i] = src[i];
-  }
-  __syncthreads();
-  // Rebase offsets as integers: an LDS pointer minus a large arena offset would wrap the
-  // 32-bit LDS address before its conversion to a flat pointer.
-  const uint8_t* stage_bytes = reinterpret_cast<const uint8_t*>(s.stage);
-
-  // ---- 1. probe + encode -------------------------------------------------------------
-  uint32_t cnt = 0, rbeg = 0, kinfo = 0, koff = 0;
-  if (p < a.n && d.x < a.db.n_plats) {
-    if (staged)
-      probe_encode<T, KW, MB, KG, FILT, GM, AB>(a, s, tid, p, d, stage_bytes + (d.y - base16), stage_bytes + (d.z - base16),
-                                          cnt, rbeg, kinfo, koff);
-    else
-      probe_encode<T, KW, MB, KG, FILT, GM, AB>(a, s, tid, p, d, a.arena + d.y, a.arena + d.z, cnt, rbeg, kinfo, koff);
-  }
-  s.rbeg[tid] = rbeg;
-  s.kinfo[tid] = kinfo;
-  s.koff[tid] = koff;
+// The sweep of tile t (packages t * 256 ..) given each lane's package record r.
+template <int K, int MB, bool FILT>
+__device__ __forceinline__ void sweep_tile(const SweepArgs& a, SweepShared<FILT>& s, uint32_t* madv, uint8_t* mq,
+                                           uint8_t* map, uint32_t t, uint32_t tid, const PkgRec& r) {
+  const uint32_t lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s.tile = t;
+  const uint32_t p = t * kTile + tid;
+  s.k0[tid] = r.k0;
+  s.k1[tid] = r.k1;
+  s.kinfo[tid] = r.meta.z;
+  s.koff[tid] = r.meta.w;
   if constexpr (FILT) s.pattr[tid] = (a.attr && p < a.n) ? a.attr[p] : make_uint2(PA_ARCH_NONE, 0xFFFFFFFFu);
+  // compact the packages that have rows (ballot) and scan their row counts
+  const uint32_t cnt = r.meta.y;
+  const unsigned long long bal = __ballot(cnt != 0);
+  const uint32_t lrank = __popcll(bal & ((1ull << lane) - 1ull));
+  if (lane == 0) s.wsum[1][wave] = uint32_t(__popcll(bal));
+  uint32_t excl = 0;
+  const uint32_t total = block_exscan<kTile>(s.wsum[0], cnt, tid, excl);  // its barriers publish wsum[1]
+  uint32_t nrank = lrank, nnz = 0;
+#pragma unroll
+  for (int w = 0; w < kTile / 64; w++) {
+    const uint32_t c = s.wsum[1][w];
+    nrank += (uint32_t(w) < wave) ? c : 0;
+    nnz += c;
+  }
+  if (cnt) {
+    s.nz_scan[nrank] = excl;
+    s.nz_rd[nrank] = r.meta.x - excl;
+    s.nz_q[nrank] = tid;
+  }
+  if (tid == 0) s.nz_scan[nnz] = total;
+  __syncthreads();
+  if (total <= kMapCap) {  // pair -> nz rank map: every lane fills a contiguous run of it
+    const uint32_t per = (total + kTile - 1) / kTile;
+    uint32_t j = tid * per;
+    const uint32_t je = min(j + per, total);
+    if (j < je) {
+      uint32_t rr = pair_rank(s, nnz, j);
+      for (; j < je; j++) {
+        while (s.nz_scan[rr + 1] <= j) rr++;
+        map[j] = uint8_t(rr);
+      }
+    }
+    __syncthreads();
+  }
 
-  // ---- 2. scan of row counts ------------------------------------------------------------
-  const uint32_t total_pairs = block_scan<T>(s, cnt, tid);
+  const uint32_t nm = sweep<K, MB, FILT, false>(a, s, madv, mq, map, nnz, total, tid, 0);
 
-  // ---- 3+4. pair sweep with LDS compaction -----------------------------------------------
-  const uint32_t nm = (AB == 1 || AB >= 3) ? (total_pairs & 1u) : sweep<T, KW, MB, KG, FILT, false, AB>(a, s, total_pairs, tid, 0);
-
-  // ---- reserve the tile's output segment (one atomic per tile, no inter-tile waiting) -----
+  // the tile's output segment: one atomic reservation, no waiting on other tiles; the
+  // tile directory gives the global (package, advisory) order
   if (tid == 0) {
-    const unsigned long long base = nm ? atomicAdd(&a.ctl[0], (unsigned long long)nm) : 0ull;
+    s.base = nm ? atomicAdd(&a.ctl[0], (unsigned long long)nm) : 0ull;
     TileDir e;
-    e.base = base;
+    e.base = s.base;
     e.count = nm;
     e.pad = 0;
-    a.dir[tile] = e;
-    s.base = base;
+    a.dir[a.t0 + t] = e;
   }
   __syncthreads();
   const unsigned long long base = s.base;
-
-  // ---- 5. store the tile's matches -------------------------------------------------------
   if (nm <= uint32_t(MB)) {
-    for (uint32_t i = tid; i < nm; i += T)
-      if (base + i < a.out_cap) a.out[base + i] = s.mbuf[i];
+    const uint32_t pb = a.out_base + a.p0 + t * kTile;
+    for (uint32_t i = tid; i < nm; i += kTile) {
+      if (base + i < a.out_cap) {
+        a.out_pkg[base + i] = pb + mq[i];
+        a.out_adv[base + i] = madv[i];
+      }
+    }
   } else {
-    sweep<T, KW, MB, KG, FILT, true, AB>(a, s, total_pairs, tid, base);  // rare: more matches than the LDS buffer
+    sweep<K, MB, FILT, true>(a, s, madv, mq, map, nnz, total, tid, base);  // rare: more matches than the buffer
   }
 }
 
-template <int T, int KW, int MB, bool KG, uint32_t GM, int AB>
-void launch_one(uint32_t n_tiles, hipStream_t st, const MatchArgs& a) {
-  hipLaunchKernelGGL((match_kernel<T, KW, MB, KG, GM, AB>), dim3(n_tiles), dim3(T), 0, st, a);
+template <int K, int MB, bool FILT>
+__global__ __launch_bounds__(kTile) void sweep_kernel(SweepArgs a) {
+  __shared__ SweepShared<FILT> s;
+  __shared__ uint32_t madv[MB];
+  __shared__ uint8_t mq[MB];
+  __shared__ uint8_t map[kMapCap];  // pair -> nz rank of its package
+  const uint32_t tid = threadIdx.x, t = blockIdx.x;
+  const uint32_t p = t * kTile + tid;
+  PkgRec r;
+  r.meta = make_uint4(0, 0, 0, 0);
+  r.k0 = r.k1 = 0;
+  if (p < a.n) r = a.rec[p];
+  sweep_tile<K, MB, FILT>(a, s, madv, mq, map, t, tid, r);
+}
+
+// Probe and sweep of one tile in one workgroup (the record stays in registers/LDS): tiles
+// of one CU sit in different phases, so one tile's probe latency overlaps another's sweep.
+template <uint32_t GM, int K, int MB, bool FILT>
+__global__ __launch_bounds__(kTile) void fused_kernel(FusedArgs fa) {
+  constexpr uint32_t kStageVec = kStage / 16 + 2;
+  constexpr uint32_t kMbufVec = (MB * 5 + 15) / 16;
+  __shared__ uint4 buf[kStageVec > kMbufVec ? kStageVec : kMbufVec];  // strings (probe), then matches (sweep)
+  __shared__ SweepShared<FILT> s;
+  __shared__ uint8_t map[kMapCap];
+  const ProbeArgs& a = fa.pa;
+  const uint32_t tid = threadIdx.x, t = blockIdx.x;
+  const uint32_t p = t * kTile + tid;
+  uint2 d = make_uint2(0xFFFFFFFFu, 0);
+  if (p < a.n) d = a.pk[p];
+  const uint32_t nlen = d.y & 0xFFFFu, vlen = d.y >> 16;
+  uint32_t off = 0;
+  block_exscan<kTile>(s.wsum[0], nlen + vlen, tid, off);
+  const uint64_t w0 = a.tile_off[t], w1 = a.tile_off[t + 1];
+  const uint64_t base16 = w0 & ~uint64_t(15);
+  const bool staged = w1 - base16 <= kStage;
+  if (staged) {
+    const uint32_t nv = uint32_t((w1 - base16 + 15) / 16);
+    const uint4* src = reinterpret_cast<const uint4*>(a.arena + base16);
+    for (uint32_t i = tid; i < nv; i += kTile) buf[i] = src[i];
+    if (tid < 2) buf[nv + tid] = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  PkgRec r;
+  r.meta = make_uint4(0, 0, 0, 0);
+  r.k0 = r.k1 = 0;
+  if (p < a.n && d.x < a.db.n_plats) {
+    if (staged) {
+      const uint8_t* sb = reinterpret_cast<const uint8_t*>(buf) + uint32_t(w0 - base16) + off;
+      probe_one<GM, uint32_t>(a, p, d.x, nlen, vlen, sb, sb + nlen, r);
+    } else {
+      const uint8_t* gb = a.arena + w0 + off;
+      probe_one<GM, uint32_t>(a, p, d.x, nlen, vlen, gb, gb + nlen, r);
+    }
+  }
+  __syncthreads();  // the strings are dead: buf becomes the match buffer
+  uint32_t* madv = reinterpret_cast<uint32_t*>(buf);
+  sweep_tile<K, MB, FILT>(fa.sa, s, madv, reinterpret_cast<uint8_t*>(madv + MB), map, t, tid, r);
+}
+
+template <uint32_t GM, int DIAG = 0>
+void launch_probe(uint32_t n_tiles, hipStream_t st, const ProbeArgs& a) {
+  hipLaunchKernelGGL((probe_kernel<GM, DIAG>), dim3(n_tiles), dim3(kTile), 0, st, a);
+}
+
+template <int K, int MB, bool FILT>
+void launch_sweep(uint32_t n_tiles, hipStream_t st, const SweepArgs& a) {
+  hipLaunchKernelGGL((sweep_kernel<K, MB, FILT>), dim3(n_tiles), dim3(kTile), 0, st, a);
+}
+
+template <uint32_t GM, int K, int MB, bool FILT>
+void launch_fused(uint32_t n_tiles, hipStream_t st, const FusedArgs& a) {
+  hipLaunchKernelGGL((fused_kernel<GM, K, MB, FILT>), dim3(n_tiles), dim3(kTile), 0, st, a);
 }
 
 }  // namespace

@@ -1,0 +1,68 @@
+// End-to-end pipelined match pass: a host batch (pinned) in, the per-package advisory lists
+// (CSR, pinned) out, with the PCIe copies overlapping the kernels.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "engine.h"
+
+namespace tvm {
+
+struct OrderArgs {
+  const TileDir* dir;
+  const uint32_t* pkg;
+  const uint32_t* adv;
+  uint32_t* csr_adv;
+  uint32_t* row_end;
+  uint64_t cap;                // match buffers' capacity (pkg / adv / csr_adv)
+  unsigned long long* status;  // look-back word per tile (zeroed before the pass)
+  unsigned long long* ticket;  // this launch's ticket counter (zeroed before the pass)
+  uint32_t t0;                 // first tile of this launch
+  uint32_t n;                  // packages in the batch
+};
+void launch_order(uint32_t n_tiles, hipStream_t st, const OrderArgs& a);
+
+// One batch's pipeline state.  prepare() pins the batch's host arrays (hipHostRegister),
+// sizes the device batch, the match buffers and the pinned result buffers; run() then
+// streams the batch through in chunks of whole tiles:
+//   copy stream    H2D of chunk c (package words, tile offsets, string bytes, attributes);
+//   kernel stream  (after chunk c's copy) the match kernels + order_kernel over chunk c;
+//   result stream  (after chunk c's kernels) D2H of chunk c's row ends, then - once the host
+//                  has read the chunk's last row end - of its advisory indices;
+// so chunk c+1's H2D and chunk c-1's D2H run under chunk c's kernels.
+class Pipeline {
+ public:
+  ~Pipeline();
+  bool prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uint32_t chunk_packages, std::string& err);
+  // One pass.  total = matches (> match_cap: nothing valid, re-prepare with a larger cap);
+  // err_pkg = first poisoned package or -1.
+  bool run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& err_pkg, uint64_t& err_bits, std::string& err);
+  const uint32_t* adv() const { return adv_h_; }
+  const uint32_t* row_end() const { return row_end_h_; }
+  uint64_t cap() const { return cap_; }
+  uint64_t h2d_bytes() const { return h2d_; }
+  uint64_t d2h_bytes() const { return d2h_; }
+  uint32_t chunks() const { return uint32_t(bounds_.size() - 1); }
+
+ private:
+  void release();
+  int dev_ = -1;
+  hipStream_t s_h2d_ = nullptr, s_k_ = nullptr, s_d2h_ = nullptr;
+  std::vector<hipEvent_t> ev_h_, ev_k_, ev_r_;
+  std::vector<uint32_t> bounds_;     // chunk c = tiles [bounds_[c], bounds_[c + 1])
+  std::vector<uint64_t> toff_;       // tile offsets + the arena end (registered)
+  std::vector<void*> registered_;
+  DevBatch db_;
+  DevMatches m_;
+  uint32_t* csr_adv_d_ = nullptr;
+  uint32_t* row_end_d_ = nullptr;
+  unsigned long long* status_d_ = nullptr;
+  unsigned long long* tickets_d_ = nullptr;
+  uint32_t* adv_h_ = nullptr;
+  uint32_t* row_end_h_ = nullptr;
+  unsigned long long* ctl_h_ = nullptr;
+  uint64_t cap_ = 0, h2d_ = 0, d2h_ = 0;
+  Engine* eng_ = nullptr;
+};
+
+}  // namespace tvm

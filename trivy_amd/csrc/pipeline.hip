@@ -1,0 +1,209 @@
+// End-to-end pipelined match pass (pipeline.h): PCIe copies on their own streams overlap
+// the match kernels, chunk by chunk.  Every buffer is sized once in prepare(); a pass
+// allocates nothing.
+#include "pipeline.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace tvm {
+
+namespace {
+
+bool ok(hipError_t e, const char* what, std::string& err) {
+  if (e == hipSuccess) return true;
+  err = std::string(what) + ": " + hipGetErrorString(e);
+  return false;
+}
+
+}  // namespace
+
+Pipeline::~Pipeline() { release(); }
+
+void Pipeline::release() {
+  if (dev_ < 0) return;
+  (void)hipSetDevice(dev_);
+  if (s_k_) (void)hipStreamSynchronize(s_k_);
+  if (s_d2h_) (void)hipStreamSynchronize(s_d2h_);
+  if (s_h2d_) (void)hipStreamSynchronize(s_h2d_);
+  if (eng_) {
+    eng_->free_batch(db_);
+    eng_->free_matches(m_);
+  }
+  for (void* p : {static_cast<void*>(csr_adv_d_), static_cast<void*>(row_end_d_), static_cast<void*>(status_d_),
+                  static_cast<void*>(tickets_d_)})
+    if (p) (void)hipFree(p);
+  for (void* p : {static_cast<void*>(adv_h_), static_cast<void*>(row_end_h_), static_cast<void*>(ctl_h_)})
+    if (p) (void)hipHostFree(p);
+  for (void* p : registered_) (void)hipHostUnregister(p);
+  registered_.clear();
+  for (auto* v : {&ev_h_, &ev_k_, &ev_r_}) {
+    for (hipEvent_t e : *v) (void)hipEventDestroy(e);
+    v->clear();
+  }
+  for (hipStream_t s : {s_h2d_, s_k_, s_d2h_})
+    if (s) (void)hipStreamDestroy(s);
+  s_h2d_ = s_k_ = s_d2h_ = nullptr;
+  csr_adv_d_ = row_end_d_ = nullptr;
+  status_d_ = tickets_d_ = nullptr;
+  adv_h_ = row_end_h_ = nullptr;
+  ctl_h_ = nullptr;
+  eng_ = nullptr;
+  dev_ = -1;
+}
+
+bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uint32_t chunk_packages,
+                       std::string& err) {
+  release();
+  eng_ = &eng;
+  dev_ = eng.device();
+  (void)hipSetDevice(dev_);
+  const uint32_t n_tiles = hb.n_tiles();
+  const uint32_t chunk_tiles = std::max<uint32_t>(1, (chunk_packages + kTile - 1) / kTile);
+  bounds_.clear();
+  for (uint32_t t = 0; t < n_tiles; t += chunk_tiles) bounds_.push_back(t);
+  bounds_.push_back(n_tiles);
+  if (n_tiles == 0) bounds_ = {0, 0};
+  const uint32_t nc = uint32_t(bounds_.size() - 1);
+  toff_ = hb.tile_off;
+  toff_.push_back(hb.arena.size());
+  cap_ = std::max<uint64_t>(match_cap, 1);
+  if (cap_ >= (1ull << 32)) {
+    err = "pipeline: row ends are 32-bit; split the batch below 2^32 matches";
+    return false;
+  }
+  for (auto* v : {&ev_h_, &ev_k_, &ev_r_}) {
+    v->resize(nc);
+    for (hipEvent_t& e : *v)
+      if (!ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate", err)) return false;
+  }
+  if (!ok(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking), "hipStreamCreate", err) ||
+      !ok(hipStreamCreateWithFlags(&s_k_, hipStreamNonBlocking), "hipStreamCreate", err) ||
+      !ok(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking), "hipStreamCreate", err))
+    return false;
+  // pin the caller's host arrays in place: the copies are DMA from them, no staging memcpy
+  auto reg = [&](const void* p, size_t bytes) {
+    if (!bytes) return true;
+    if (!ok(hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault), "hipHostRegister", err)) return false;
+    registered_.push_back(const_cast<void*>(p));
+    return true;
+  };
+  if (!reg(hb.pk.data(), hb.pk.size() * sizeof(uint2)) || !reg(hb.arena.data(), hb.arena.size()) ||
+      !reg(toff_.data(), toff_.size() * 8) || !reg(hb.attr.data(), hb.attr.size() * sizeof(uint2)))
+    return false;
+  if (!eng.alloc_batch(hb, db_, err) || !eng.alloc_matches(cap_, db_.n, m_, err)) return false;
+  if (!hb.cpe_bits.empty() && hb.cpe_words) {  // CPE sets: small, copied once here
+    void* p = nullptr;
+    if (!ok(hipMalloc(&p, hb.cpe_bits.size() * 4), "hipMalloc(cpe sets)", err) ||
+        !ok(hipMemcpy(p, hb.cpe_bits.data(), hb.cpe_bits.size() * 4, hipMemcpyHostToDevice), "H2D cpe", err))
+      return false;
+    db_.cpe_bits = static_cast<uint32_t*>(p);
+    db_.cpe_words = hb.cpe_words;
+    db_.n_cpe_sets = uint32_t(hb.cpe_bits.size() / hb.cpe_words);
+  }
+  const size_t n = std::max<size_t>(hb.pk.size(), 1);
+  void* p = nullptr;
+  if (!ok(hipMalloc(&p, cap_ * 4), "hipMalloc(csr)", err)) return false;
+  csr_adv_d_ = static_cast<uint32_t*>(p);
+  if (!ok(hipMalloc(&p, n * 4), "hipMalloc(row ends)", err)) return false;
+  row_end_d_ = static_cast<uint32_t*>(p);
+  if (!ok(hipMalloc(&p, std::max<size_t>(n_tiles, 1) * 8), "hipMalloc(status)", err)) return false;
+  status_d_ = static_cast<unsigned long long*>(p);
+  if (!ok(hipMalloc(&p, std::max<size_t>(nc, 1) * 8), "hipMalloc(tickets)", err)) return false;
+  tickets_d_ = static_cast<unsigned long long*>(p);
+  if (!ok(hipHostMalloc(&p, cap_ * 4, hipHostMallocDefault), "hipHostMalloc(adv)", err)) return false;
+  adv_h_ = static_cast<uint32_t*>(p);
+  if (!ok(hipHostMalloc(&p, n * 4, hipHostMallocDefault), "hipHostMalloc(row ends)", err)) return false;
+  row_end_h_ = static_cast<uint32_t*>(p);
+  if (!ok(hipHostMalloc(&p, 64, hipHostMallocDefault), "hipHostMalloc(ctl)", err)) return false;
+  ctl_h_ = static_cast<unsigned long long*>(p);
+  return true;
+}
+
+bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& err_pkg, uint64_t& err_bits,
+                   std::string& err) {
+  total = 0;
+  err_pkg = -1;
+  err_bits = 0;
+  h2d_ = d2h_ = 0;
+  if (!eng_ || db_.n != hb.pk.size()) {
+    err = "pipeline: prepare() the batch first";
+    return false;
+  }
+  (void)hipSetDevice(dev_);
+  const uint32_t nc = chunks();
+  const uint32_t n = db_.n;
+  if (!ok(hipMemsetAsync(m_.ctl, 0, 64, s_k_), "memset(ctl)", err) ||
+      !ok(hipMemsetAsync(status_d_, 0, std::max<size_t>(db_.n_tiles, 1) * 8, s_k_), "memset(status)", err) ||
+      !ok(hipMemsetAsync(tickets_d_, 0, std::max<size_t>(nc, 1) * 8, s_k_), "memset(tickets)", err))
+    return false;
+  // 1. every chunk's H2D on the copy stream (DMA from the pinned host arrays)
+  for (uint32_t c = 0; c < nc; c++) {
+    const uint32_t t0 = bounds_[c], t1 = bounds_[c + 1];
+    const size_t p0 = size_t(t0) * kTile, p1 = std::min<size_t>(size_t(t1) * kTile, n);
+    const uint64_t a0 = toff_[t0], a1 = toff_[t1];
+    if (!ok(hipMemcpyAsync(db_.pk + p0, hb.pk.data() + p0, (p1 - p0) * sizeof(uint2), hipMemcpyHostToDevice, s_h2d_),
+            "H2D packages", err) ||
+        !ok(hipMemcpyAsync(db_.tile_off + t0, toff_.data() + t0, (t1 - t0 + 1) * 8, hipMemcpyHostToDevice, s_h2d_),
+            "H2D tile offsets", err) ||
+        (a1 > a0 && !ok(hipMemcpyAsync(db_.arena + a0, hb.arena.data() + a0, a1 - a0, hipMemcpyHostToDevice, s_h2d_),
+                        "H2D strings", err)) ||
+        (!hb.attr.empty() &&
+         !ok(hipMemcpyAsync(db_.attr + p0, hb.attr.data() + p0, (p1 - p0) * sizeof(uint2), hipMemcpyHostToDevice, s_h2d_),
+             "H2D attributes", err)) ||
+        !ok(hipEventRecord(ev_h_[c], s_h2d_), "hipEventRecord", err))
+      return false;
+    h2d_ += (p1 - p0) * sizeof(uint2) + (t1 - t0 + 1) * 8 + (a1 - a0) + (hb.attr.empty() ? 0 : (p1 - p0) * sizeof(uint2));
+  }
+  // 2. kernels per chunk, each behind its chunk's copy
+  for (uint32_t c = 0; c < nc; c++) {
+    const uint32_t t0 = bounds_[c], t1 = bounds_[c + 1];
+    if (!ok(hipStreamWaitEvent(s_k_, ev_h_[c], 0), "hipStreamWaitEvent", err) ||
+        !eng.launch_tiles(db_, m_, t0, t1, s_k_, s_k_, nullptr, err))
+      return false;
+    OrderArgs oa;
+    oa.dir = m_.dir;
+    oa.pkg = m_.pkg;
+    oa.adv = m_.adv;
+    oa.csr_adv = csr_adv_d_;
+    oa.row_end = row_end_d_;
+    oa.cap = cap_;
+    oa.status = status_d_;
+    oa.ticket = tickets_d_ + c;
+    oa.t0 = t0;
+    oa.n = n;
+    if (t1 > t0) launch_order(t1 - t0, s_k_, oa);
+    if (!ok(hipGetLastError(), "order kernel launch", err) || !ok(hipEventRecord(ev_k_[c], s_k_), "hipEventRecord", err))
+      return false;
+  }
+  if (!ok(hipMemcpyAsync(ctl_h_, m_.ctl, 64, hipMemcpyDeviceToHost, s_k_), "D2H ctl", err)) return false;
+  // 3. results per chunk: row ends, then (once the host knows where the chunk ends) its advisories
+  uint64_t start = 0;
+  for (uint32_t c = 0; c < nc; c++) {
+    const uint32_t t0 = bounds_[c], t1 = bounds_[c + 1];
+    const size_t p0 = size_t(t0) * kTile, p1 = std::min<size_t>(size_t(t1) * kTile, n);
+    if (p1 == p0) continue;
+    if (!ok(hipStreamWaitEvent(s_d2h_, ev_k_[c], 0), "hipStreamWaitEvent", err) ||
+        !ok(hipMemcpyAsync(row_end_h_ + p0, row_end_d_ + p0, (p1 - p0) * 4, hipMemcpyDeviceToHost, s_d2h_),
+            "D2H row ends", err) ||
+        !ok(hipEventRecord(ev_r_[c], s_d2h_), "hipEventRecord", err) ||
+        !ok(hipEventSynchronize(ev_r_[c]), "hipEventSynchronize", err))
+      return false;
+    const uint64_t end = row_end_h_[p1 - 1];
+    if (end > cap_) break;  // overflow: the caller re-prepares with the total below
+    if (end > start &&
+        !ok(hipMemcpyAsync(adv_h_ + start, csr_adv_d_ + start, (end - start) * 4, hipMemcpyDeviceToHost, s_d2h_),
+            "D2H advisories", err))
+      return false;
+    d2h_ += (p1 - p0) * 4 + (end - start) * 4;
+    start = end;
+  }
+  if (!ok(hipStreamSynchronize(s_d2h_), "pipeline D2H", err) || !ok(hipStreamSynchronize(s_k_), "pipeline kernels", err))
+    return false;
+  total = ctl_h_[0];
+  err_pkg = ctl_h_[1] ? int64_t(n - ctl_h_[1]) : -1;
+  err_bits = ctl_h_[3];
+  return true;
+}
+
+}  // namespace tvm

@@ -163,12 +163,12 @@ class FillEngine {
                 std::string& err);
   // Batch path: decisions for the device match pairs {pkg, adv} (resolved records), on
   // `stream`; the pair count is read from n_dev on the device (at most cap pairs).
-  bool launch_pairs(const uint2* pairs, const unsigned long long* n_dev, uint64_t cap, uint4* out, hipStream_t stream,
+  bool launch_pairs(const uint32_t* adv, const unsigned long long* n_dev, uint64_t cap, uint4* out, hipStream_t stream,
                     std::string& err);
   uint64_t table_bytes() const { return table_bytes_; }
   const VulnTable& table() const { return *t_; }
   // Algorithmic HBM bytes of one batch-path launch over these pairs (host copy).
-  uint64_t pair_bytes(const std::vector<uint2>& pairs) const;
+  uint64_t pair_bytes(const std::vector<uint32_t>& adv) const;
   const FillDev& dev() const { return *d_; }
   int device() const { return dev_; }
 
@@ -192,7 +192,7 @@ class BatchFilter {
   // Filters the n device pairs (with their FillInfo decisions) on `st`; synchronises once
   // to learn the survivor count.  ignore: sorted vulnerability ranks (VulnTable::vuln_rank);
   // vex: sorted (package << 32 | vulnerability rank) findings a VEX document drops.
-  bool run(const FillDev& t, const uint2* pairs, const uint4* fill, uint64_t n, const std::vector<uint32_t>& ignore,
+  bool run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv, const uint4* fill, uint64_t n, const std::vector<uint32_t>& ignore,
            const std::vector<uint64_t>& vex, uint32_t n_ranks, uint32_t sev_mask, uint32_t status_mask,
            hipStream_t st, std::string& err);
   uint64_t survivors() const { return survivors_; }

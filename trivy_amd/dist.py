@@ -1,12 +1,14 @@
-"""Node-level sharding of package batches over GPUs.
+"""Node-level sharding of one package batch over GPUs.
 
 One process per GPU (torch.distributed; backend "nccl" is RCCL on ROCm, "gloo" on CPU for
-tests).  Packages are independent, so the batch is split into contiguous shards - by
-package count, or by predicted pair count (Σ advisories per package, from a host-side
-pre-probe) so a Zipf-heavy key does not leave one GPU behind - and each rank matches its
-shard against its own replica of the advisory tables: no collective on the data path.
-Match lists stay on their GPU; `gather_pairs` brings them to one rank when a caller needs
-the merged set (sizes all-gathered first, then one gather of the variable-length lists).
+tests).  The advisory tables are replicated on every GPU; ONE global batch is cut into
+contiguous shards on target (result) boundaries - so a result is never split across ranks
+and result.Filter's per-result dedup / order stays valid - balanced by predicted work: the
+Σ advisory rows of each target from a host-side pre-probe of the DB index
+(tvm_db_rows_many), not by package count, so a Zipf-heavy key ("linux") does not leave one
+GPU behind.  Each rank matches its shard; the match lists then come to one rank through an
+exact-size gather (all-gather of the per-rank counts, then one point-to-point receive per
+rank into the root's buffer, no padding): 8 bytes per match (package u32, advisory u32).
 """
 import time
 
@@ -23,14 +25,15 @@ def world():
 
 
 def shard(n, rank, world_size):
-    """Contiguous [begin, end) of n packages for `rank` (sizes differ by at most one)."""
+    """Contiguous [begin, end) of n items for `rank` (sizes differ by at most one)."""
     q, r = divmod(n, world_size)
     begin = rank * q + min(rank, r)
     return begin, begin + q + (1 if rank < r else 0)
 
 
 def balanced_shards(weights, world_size):
-    """Contiguous shard boundaries (world_size + 1 entries) with near-equal Σ weights."""
+    """Contiguous boundaries (world_size + 1 entries) over len(weights) items with near-equal
+    Σ weights; every boundary falls between items."""
     w = np.asarray(weights, dtype=np.float64)
     if len(w) == 0:
         return [0] * (world_size + 1)
@@ -43,6 +46,17 @@ def balanced_shards(weights, world_size):
     for k in range(1, len(bounds)):
         bounds[k] = min(max(bounds[k], bounds[k - 1]), len(w))
     return bounds
+
+
+def target_shards(target_begin, n_packages, pkg_weights, world_size):
+    """Shards of a batch on target boundaries.  target_begin: first package of every target
+    (ascending); pkg_weights: predicted work per package (e.g. rows + 1).  Returns
+    world_size + 1 package boundaries."""
+    tb = np.asarray(list(target_begin) + [n_packages], dtype=np.int64)
+    csum = np.concatenate([[0.0], np.cumsum(np.asarray(pkg_weights, dtype=np.float64))])
+    tw = csum[tb[1:]] - csum[tb[:-1]]
+    tbounds = balanced_shards(tw, world_size)
+    return [int(tb[t]) for t in tbounds]
 
 
 def max_over_ranks(x, device="cpu"):
@@ -71,29 +85,49 @@ def timed(step, steps, warmup, sync=lambda: None, device="cpu"):
     return max_over_ranks(time.perf_counter() - t0, device)
 
 
-def gather_pairs(pairs, pkg_offset, dst=0):
-    """Gathers every rank's (package, advisory) pairs to rank `dst`.
+class MatchGather:
+    """Exact-size gather of every rank's match columns to `root`.
 
-    pairs: int64 tensor [m, 2] of this rank's matches with shard-local package indices;
-    pkg_offset: this rank's first global package index.  Returns the merged [M, 2] tensor
-    in global package order on `dst`, None elsewhere."""
-    rank, ws = world()
-    local = pairs.to(torch.int64).clone()
-    if local.numel():
-        local[:, 0] += pkg_offset
-    if ws == 1:
-        return local
-    dev = local.device
-    n = torch.tensor([local.shape[0]], dtype=torch.int64, device=dev)
-    sizes = [torch.zeros_like(n) for _ in range(ws)]
-    dist.all_gather(sizes, n)
-    sizes = [int(s.item()) for s in sizes]
-    cap = max(max(sizes), 1)
-    buf = torch.zeros((cap, 2), dtype=torch.int64, device=dev)
-    buf[:local.shape[0]] = local
-    if rank == dst:
-        parts = [torch.zeros((cap, 2), dtype=torch.int64, device=dev) for _ in range(ws)]
-        dist.gather(buf, gather_list=parts, dst=dst)
-        return torch.cat([p[:s] for p, s in zip(parts, sizes)])
-    dist.gather(buf, dst=dst)
-    return None
+    pkg / adv: this rank's uint32 columns as int32 tensors (their first n entries are the
+    matches; package indices already global).  The root keeps one receive buffer per rank
+    sized by the largest count seen (grown on demand), so a steady-state gather allocates
+    nothing."""
+
+    def __init__(self, device, root=0):
+        self.device = device
+        self.root = root
+        self.bufs = {}
+
+    def __call__(self, pkg, adv, n):
+        rank, ws = world()
+        if ws == 1:
+            return [(pkg[:n], adv[:n])]
+        cnt = torch.tensor([n], dtype=torch.int64, device=self.device)
+        counts = [torch.zeros_like(cnt) for _ in range(ws)]
+        dist.all_gather(counts, cnt)
+        counts = [int(c.item()) for c in counts]
+        if rank != self.root:
+            if n:
+                ops = [dist.P2POp(dist.isend, pkg[:n].contiguous(), self.root),
+                       dist.P2POp(dist.isend, adv[:n].contiguous(), self.root)]
+                for r in dist.batch_isend_irecv(ops):
+                    r.wait()
+            return None
+        ops, parts = [], []
+        for r in range(ws):
+            if r == rank:
+                parts.append((pkg[:n], adv[:n]))
+                continue
+            c = counts[r]
+            bp, ba = self.bufs.get(r, (None, None))
+            if bp is None or bp.numel() < c:
+                bp = torch.empty(max(c, 1), dtype=torch.int32, device=self.device)
+                ba = torch.empty(max(c, 1), dtype=torch.int32, device=self.device)
+                self.bufs[r] = (bp, ba)
+            parts.append((bp[:c], ba[:c]))
+            if c:
+                ops += [dist.P2POp(dist.irecv, bp[:c], r), dist.P2POp(dist.irecv, ba[:c], r)]
+        if ops:
+            for q in dist.batch_isend_irecv(ops):
+                q.wait()
+        return parts
