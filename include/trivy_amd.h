@@ -190,11 +190,30 @@ int64_t tvm_batch_add(tvm_batch* b, tvm_engine* e, const char* bucket, tvm_str n
  * form of what tvm_ospkg_detect derives from tvm_package): TVM_ATTR_ARCH takes one arch
  * string per package (rocky.go arch entries, redhat.go arch filter), TVM_ATTR_KSPLICE tags
  * each package with the ksplice token of its release (oracle.go:46-53, 77). */
-enum { TVM_ATTR_ARCH = 1, TVM_ATTR_KSPLICE = 2 };
+enum { TVM_ATTR_ARCH = 1, TVM_ATTR_KSPLICE = 2, TVM_ATTR_CPESET = 4 };
 int64_t tvm_batch_add_many_ex(tvm_batch* b, tvm_engine* e, const char* bucket, size_t n, const char* arena,
                               const uint64_t* name_off, const uint32_t* name_len, const uint64_t* ver_off,
                               const uint32_t* ver_len, const uint64_t* arch_off, const uint32_t* arch_len,
                               uint32_t flags);
+/* Red Hat: registers the CPE set of one (content sets, NVR) combination - redhat.go:112-120:
+ * BuildInfo.ContentSets and "Nvr-Arch", or the release's default content sets and "" without
+ * BuildInfo - resolved through the "Red Hat CPE" buckets; returns its id for TVM_ATTR_CPESET
+ * (one per distinct combination, typically one per image), or -1. */
+int64_t tvm_batch_cpe_set(tvm_batch* b, tvm_engine* e, const tvm_str* content_sets, size_t n, tvm_str nvr);
+/* Optional per-package attribute columns of tvm_batch_add_many_attrs. */
+typedef struct {
+  const uint64_t* arch_off; /* TVM_ATTR_ARCH: arch string per package in the arena */
+  const uint32_t* arch_len;
+  const uint32_t* cpe_set;  /* TVM_ATTR_CPESET: tvm_batch_cpe_set id per package (Red Hat) */
+} tvm_attr_cols;
+/* tvm_batch_add_many plus attributes (the batch form of what tvm_ospkg_detect derives from
+ * tvm_package): TVM_ATTR_ARCH (redhat.go:129-135 arch filter, rocky arch entries),
+ * TVM_ATTR_KSPLICE (oracle.go:46-53, 77), TVM_ATTR_CPESET (the Red Hat CPE-set intersection of
+ * trivy-db's redhat-oval Get).  The name is the lookup name the driver uses (Red Hat:
+ * addModularNamespace, redhat.go:207-220). */
+int64_t tvm_batch_add_many_attrs(tvm_batch* b, tvm_engine* e, const char* bucket, size_t n, const char* arena,
+                                 const uint64_t* name_off, const uint32_t* name_len, const uint64_t* ver_off,
+                                 const uint32_t* ver_len, const tvm_attr_cols* attrs, uint32_t flags);
 /* n packages of one bucket from a byte arena; returns the batch index of the first. */
 int64_t tvm_batch_add_many(tvm_batch* b, tvm_engine* e, const char* bucket, size_t n, const char* arena,
                            const uint64_t* name_off, const uint32_t* name_len, const uint64_t* ver_off,
@@ -265,6 +284,16 @@ int tvm_pipeline_run(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* 
 int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row_end, uint64_t* n_matches);
 /* Bytes the last pass copied: [0] host to device, [1] device to host, [2] chunks. */
 int tvm_pipeline_stats(tvm_batch* b, uint64_t out[3]);
+
+/* ---- Red Hat on the batch path ----------------------------------------------------------
+ * After tvm_match_launch (+ sync): the Red Hat driver's epilogue for every package of the
+ * batch's "Red Hat"-bucket targets at once - the per-CVE merge of redhat.go:146-187 (first
+ * advisory of a VulnerabilityID gives Status / Severity; fixed advisories union their
+ * VendorIDs and raise FixedVersion to the greatest rpm version; sorted by VulnerabilityID per
+ * package) grouped on the GPU.  Vulns carry pkg_index = batch index, InstalledVersion = the
+ * batch version, copy flags PKG_ID | PKG_NAME | IDENTIFIER | LAYER (the caller copies them from
+ * its package, whose Name is the plain name, not the modular lookup name). */
+int tvm_match_redhat_result(tvm_engine* e, tvm_batch* b, tvm_result* out, char* err, size_t errlen);
 
 /* ---- vulnerability detail: FillInfo ------------------------------------------------ */
 /* One detected vulnerability as FillInfo reads it (vulnerability.go:60-109). */

@@ -17,6 +17,7 @@
 #include "libdb.h"
 #include "libver.h"
 #include "pipeline.h"
+#include "redhat.h"
 #include "vulninfo.h"
 
 using namespace tvm;
@@ -31,6 +32,14 @@ struct tvm_engine {
   std::shared_mutex mu;  // calls share; swap is exclusive (listen.go:154-190 quiesce)
   std::unique_ptr<Engine> eng;
   std::unique_ptr<FillEngine> fill;
+  std::mutex rh_mu;                   // lazily built Red Hat fixed-version ranks (device)
+  uint32_t* rh_rank = nullptr;
+  ~tvm_engine() {
+    if (rh_rank) {
+      (void)hipSetDevice(device);
+      (void)hipFree(rh_rank);
+    }
+  }
   tvm_db* db = nullptr;
   int device = 0;
 };
@@ -43,6 +52,7 @@ struct tvm_batch {
   uint64_t fill_cap = 0;
   std::vector<uint32_t> target_begin;  // first package of every result (one per add call)
   BatchFilter filter;                  // tvm_match_filter state
+  RedHatMerge rh;                      // tvm_match_redhat_result state
   std::unique_ptr<Pipeline> pipe;      // tvm_pipeline_* state
   uint32_t pkg_base = 0;               // tvm_batch_set_package_base
   uint64_t pipe_total = 0;
@@ -240,6 +250,10 @@ int tvm_engine_swap(tvm_engine* e, tvm_db* db, char* err, size_t errlen) {
   e->eng.reset(fresh);
   e->fill.reset(fresh_fill);
   e->db = db;
+  if (e->rh_rank) {
+    (void)hipFree(e->rh_rank);
+    e->rh_rank = nullptr;
+  }
   return TVM_OK;
 }
 
@@ -383,11 +397,45 @@ int64_t tvm_batch_add_many_ex(tvm_batch* b, tvm_engine* e, const char* bucket, s
                               const uint64_t* name_off, const uint32_t* name_len, const uint64_t* ver_off,
                               const uint32_t* ver_len, const uint64_t* arch_off, const uint32_t* arch_len,
                               uint32_t flags) {
-  if (!b || !e || !bucket || b->uploaded || (flags & ~uint32_t(TVM_ATTR_ARCH | TVM_ATTR_KSPLICE)) ||
+  if (flags & TVM_ATTR_CPESET) return -1;  // needs the set column: tvm_batch_add_many_attrs
+  tvm_attr_cols cols{arch_off, arch_len, nullptr};
+  return tvm_batch_add_many_attrs(b, e, bucket, n, arena, name_off, name_len, ver_off, ver_len, &cols, flags);
+}
+
+int64_t tvm_batch_cpe_set(tvm_batch* b, tvm_engine* e, const tvm_str* content_sets, size_t n, tvm_str nvr) {
+  if (!b || !e || b->uploaded || (n && !content_sets)) return -1;
+  const DB& db = e->eng->db();
+  HostBatch& hb = b->hb;
+  const uint32_t words = std::max<uint32_t>((db.n_cpe + 31) / 32, 1);
+  if (hb.cpe_words == 0) hb.cpe_words = words;
+  if (hb.cpe_words != words) return -1;
+  std::vector<std::string_view> repos, nvrs;
+  for (size_t i = 0; i < n; i++) repos.push_back(sv(content_sets[i]));
+  nvrs.push_back(sv(nvr));
+  const size_t id = hb.cpe_bits.size() / words;
+  hb.cpe_bits.resize(hb.cpe_bits.size() + words, 0u);
+  uint32_t* bits = hb.cpe_bits.data() + id * words;
+  for (int64_t c : db.redhat_cpes(repos, nvrs))
+    if (c >= 0 && uint64_t(c) < uint64_t(words) * 32) bits[c >> 5] |= 1u << (c & 31);
+  return int64_t(id);
+}
+
+int64_t tvm_batch_add_many_attrs(tvm_batch* b, tvm_engine* e, const char* bucket, size_t n, const char* arena,
+                                 const uint64_t* name_off, const uint32_t* name_len, const uint64_t* ver_off,
+                                 const uint32_t* ver_len, const tvm_attr_cols* cols, uint32_t flags) {
+  const uint32_t known = TVM_ATTR_ARCH | TVM_ATTR_KSPLICE | TVM_ATTR_CPESET;
+  if (!b || !e || !bucket || b->uploaded || (flags & ~known) ||
+      ((flags & TVM_ATTR_KSPLICE) && (flags & TVM_ATTR_CPESET)) ||  // one attribute word: tag or CPE set
       (n && (!arena || !name_off || !name_len || !ver_off || !ver_len)) ||
-      (n && (flags & TVM_ATTR_ARCH) && (!arch_off || !arch_len)))
+      (n && (flags & (TVM_ATTR_ARCH | TVM_ATTR_CPESET)) && !cols) ||
+      (n && (flags & TVM_ATTR_ARCH) && (!cols->arch_off || !cols->arch_len)) ||
+      (n && (flags & TVM_ATTR_CPESET) && !cols->cpe_set))
     return -1;
   const DB& db = e->eng->db();
+  const size_t n_sets = b->hb.cpe_words ? b->hb.cpe_bits.size() / b->hb.cpe_words : 0;
+  if (flags & TVM_ATTR_CPESET)
+    for (size_t i = 0; i < n; i++)
+      if (cols->cpe_set[i] >= n_sets) return -1;
   int32_t plat = db.find_plat(bucket);
   const uint32_t pid = plat < 0 ? 0xFFFFFFFFu : uint32_t(plat);
   const int64_t first = int64_t(b->hb.pk.size());
@@ -396,12 +444,17 @@ int64_t tvm_batch_add_many_ex(tvm_batch* b, tvm_engine* e, const char* bucket, s
   for (size_t i = 0; i < n; i++) {
     const std::string_view ver(arena + ver_off[i], ver_len[i]);
     uint2 a = make_uint2(PA_ARCH_NONE, 0xFFFFFFFFu);
-    if (flags & TVM_ATTR_ARCH) a.x = db.arch_id(std::string_view(arena + arch_off[i], arch_len[i]));
+    if (flags & TVM_ATTR_ARCH) {
+      const std::string_view arch(arena + cols->arch_off[i], cols->arch_len[i]);
+      a.x = db.arch_id(arch) | (arch == "noarch" ? PA_NOARCH : 0u);  // redhat.go:129 "noarch" matches any
+    }
     if (flags & TVM_ATTR_KSPLICE) {
       const size_t dash = ver.find('-');  // release = text after the first '-' (rpm split, rpm.c)
       a.y = db.ksplice_id(extract_ksplice(dash == std::string_view::npos ? std::string_view() : ver.substr(dash + 1)));
     }
-    b->hb.add(pid, std::string_view(arena + name_off[i], name_len[i]), ver, a);
+    if (flags & TVM_ATTR_CPESET) a.y = cols->cpe_set[i];
+    if (flags) b->hb.add(pid, std::string_view(arena + name_off[i], name_len[i]), ver, a);
+    else b->hb.add(pid, std::string_view(arena + name_off[i], name_len[i]), ver);
   }
   return first;
 }
@@ -1041,5 +1094,58 @@ int tvm_batch_upload_into(tvm_engine* e, tvm_batch* b, void* pkg_dev, void* adv_
   b->m.adv = static_cast<uint32_t*>(adv_dev);
   b->m.cap = cap;
   b->external_out = true;
+  return TVM_OK;
+}
+
+// ---- Red Hat batch epilogue (redhat.hip) -------------------------------------------------
+
+int tvm_match_redhat_result(tvm_engine* e, tvm_batch* b, tvm_result* out, char* err, size_t errlen) {
+  if (!e || !b || !out || !b->uploaded) return TVM_EINVAL;
+  memset(out, 0, sizeof(*out));
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  (void)hipSetDevice(e->device);
+  hipStream_t st = e->eng->stream();
+  uint64_t n = 0;
+  if (hipStreamSynchronize(st) != hipSuccess || tvm_match_status(e, b, &n, nullptr, nullptr)) return TVM_EDEVICE;
+  if (n > b->m.cap) {
+    set_err(err, errlen, "tvm_match_redhat_result: the match buffer overflowed");
+    return TVM_EINVAL;
+  }
+  const DB& db = e->eng->db();
+  {
+    std::lock_guard<std::mutex> g(e->rh_mu);
+    if (!e->rh_rank) {
+      const std::vector<uint32_t> r = redhat_fixed_ranks(db);
+      void* p = nullptr;
+      if (hipMalloc(&p, std::max<size_t>(r.size(), 1) * 4) != hipSuccess ||
+          (!r.empty() && hipMemcpy(p, r.data(), r.size() * 4, hipMemcpyHostToDevice) != hipSuccess)) {
+        set_err(err, errlen, "tvm_match_redhat_result: fixed-version ranks upload failed");
+        return TVM_EDEVICE;
+      }
+      e->rh_rank = static_cast<uint32_t*>(p);
+    }
+  }
+  RhInputs in;
+  in.pk = b->dev.pk;
+  in.plats = nullptr;
+  in.n_plats = uint32_t(db.plat_info.size());
+  in.pkg = b->m.pkg;
+  in.adv = b->m.adv;
+  in.n_dev = b->m.ctl;
+  in.n_matches = n;
+  in.pkg_base = b->dev.pkg_base;
+  in.adv_rank = e->fill->dev().adv_rank;
+  in.fixed_rank = e->rh_rank;
+  in.plats = e->eng->device_plats();
+  std::vector<RhRec> recs;
+  std::vector<uint32_t> contrib;
+  std::string msg;
+  if (!b->rh.run(in, recs, contrib, st, msg)) {
+    set_err(err, errlen, msg);
+    return TVM_EDEVICE;
+  }
+  std::vector<Vuln> vulns;
+  redhat_batch_vulns(db, b->hb, recs, contrib, b->dev.pkg_base, vulns);
+  export_result(db, std::move(vulns), false, out);
   return TVM_OK;
 }

@@ -5,6 +5,7 @@
 // (which DetectedVulnerability fields are set, Red Hat's per-CVE merge).  The
 // per-(package, advisory) loop runs in one GPU launch per call (Engine::match_host).
 #include "drivers.h"
+#include "redhat.h"
 #include "vulninfo.h"
 
 #include <algorithm>
@@ -695,6 +696,65 @@ void detector_fill_fields(uint8_t drv, const Advisory& a, DetFill& f) {
       break;
     default:
       f.fixed = !a.fixed.empty();
+  }
+}
+
+
+// ---- Red Hat batch epilogue (redhat.hip groups, host fields) ------------------------------
+
+std::vector<uint32_t> redhat_fixed_ranks(const DB& db) {
+  // rank of every Red Hat advisory's FixedVersion in go-rpm-version order (ties share a
+  // rank); RH_NONE for unfixed advisories and other drivers' (the merge never reads them)
+  std::vector<uint32_t> rank(db.advs.size(), RH_NONE);
+  std::vector<std::pair<std::vector<uint8_t>, uint32_t>> keys;
+  for (const Key& k : db.keys) {
+    if (k.plat >= db.plats.size() || db.plats[k.plat].drv != DRV_REDHAT) continue;
+    for (uint32_t a : k.advs) {
+      if (db.advs[a].fixed.empty()) continue;
+      std::vector<uint8_t> kb;
+      VecSink s{&kb};
+      rpm_encode(reinterpret_cast<const uint8_t*>(db.advs[a].fixed.data()), uint32_t(db.advs[a].fixed.size()), s);
+      keys.emplace_back(std::move(kb), a);
+    }
+  }
+  std::sort(keys.begin(), keys.end());
+  uint32_t r = 0;
+  for (size_t i = 0; i < keys.size(); i++) {
+    if (i && keys[i].first != keys[i - 1].first) r++;
+    rank[keys[i].second] = r;
+  }
+  return rank;
+}
+
+void redhat_batch_vulns(const DB& db, const HostBatch& hb, const std::vector<RhRec>& recs,
+                        const std::vector<uint32_t>& contrib, uint32_t pkg_base, std::vector<Vuln>& out) {
+  for (const RhRec& r : recs) {
+    const uint32_t pk = r.pkg - pkg_base;
+    const Advisory& a = db.advs[r.base];
+    Vuln v;
+    v.pkg = pk;
+    v.copy = COPY_PKG_ID | COPY_PKG_NAME | COPY_IDENTIFIER | COPY_LAYER;
+    v.vuln_id = a.vuln_id;
+    v.installed = std::string(hb.version(pk));
+    v.status = int32_t(a.status);
+    v.severity_source = "redhat";
+    v.severity = severity_name(a.severity);
+    if (r.best != RH_NONE) v.fixed = rpm_string(db.advs[r.best].fixed);
+    // VendorIDs (redhat.go:163-170): a lone fixed first member keeps its list as is; every
+    // merge of a fixed member makes it the sorted, de-duplicated union (ustrings.Unique)
+    uint32_t n_fixed = 0;
+    for (uint32_t j = r.start; j < r.start + r.len; j++) n_fixed += !db.advs[contrib[j]].fixed.empty();
+    if (n_fixed == 1 && !a.fixed.empty()) {
+      v.vendor_ids = a.vendor_ids;
+    } else if (n_fixed) {
+      for (uint32_t j = r.start; j < r.start + r.len; j++) {
+        const Advisory& m = db.advs[contrib[j]];
+        if (!m.fixed.empty()) v.vendor_ids.insert(v.vendor_ids.end(), m.vendor_ids.begin(), m.vendor_ids.end());
+      }
+      std::sort(v.vendor_ids.begin(), v.vendor_ids.end());
+      v.vendor_ids.erase(std::unique(v.vendor_ids.begin(), v.vendor_ids.end()), v.vendor_ids.end());
+    }
+    out.push_back(std::move(v));
   }
 }
 

@@ -84,6 +84,13 @@ DetectStatus library_detect(Engine& eng, std::string_view lib_type, const std::v
 // (*Driver).DetectVulnerabilities (driver.go:111-137) for each package, errors unwrapped.
 DetectStatus library_detect_vulnerabilities(Engine& eng, std::string_view lib_type, const std::vector<Pkg>& pkgs,
                                             std::vector<Vuln>& out, std::string& err);
+// Red Hat batch epilogue: rpm-order rank of every Red Hat advisory's FixedVersion
+// (RH_NONE when unfixed), and the DetectedVulnerability of every merged group (redhat.hip)
+// - Vuln.pkg is the batch index, InstalledVersion the batch version string.
+struct RhRec;
+std::vector<uint32_t> redhat_fixed_ranks(const DB& db);
+void redhat_batch_vulns(const DB& db, const HostBatch& hb, const std::vector<RhRec>& recs,
+                        const std::vector<uint32_t>& contrib, uint32_t pkg_base, std::vector<Vuln>& out);
 // vulnerability.NormalizePkgName (trivy-db): pip names lower-cased, "_" -> "-".
 std::string normalize_pkg_name(std::string_view eco, std::string_view name);
 

@@ -138,6 +138,7 @@ class Engine {
   bool match_host(const HostBatch& hb, std::vector<uint2>& out, int64_t& err_pkg, std::string& err);
 
   const DB& db() const { return *db_; }
+  const PlatInfo* device_plats() const { return d_.plats; }
 
   // Sweep-kernel variant (pairs per lane / LDS buffer); returns the previous one.  Default
   // 0 = "auto", overridable with the TVM_VARIANT environment variable at open().

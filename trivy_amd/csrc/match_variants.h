@@ -17,4 +17,4 @@ constexpr int kNumTuned = 0 TVM_MATCH_VARIANTS(TVM_VARIANT_COUNT_);
 #undef TVM_VARIANT_COUNT_
 
 // Variant (index into the list) the engine launches by default.
-constexpr int kAutoVariant = 0;
+constexpr int kAutoVariant = 1;  // fused_k4_m2048: fastest on C2 (bench.py --sweep, MI355X)
