@@ -95,6 +95,12 @@ class C2:
             if b0 >= b and b1 <= e:
                 mb.add_arena(self.sdb.platforms[p], b1 - b0, arena, noff[b0:], nlen[b0:], voff[b0:], vlen[b0:])
 
+    def vuln_ids(self):
+        return self.sdb.vuln_ids()
+
+    def adv_vuln_id(self, db, a):
+        return self.sdb.adv_vid[a]
+
     def cpu_baseline(self, budget_s, threads):
         from oracle import match as om
         from tools.synth import SynthBatch
@@ -144,6 +150,18 @@ class Mix:
 
     def load(self, db, vulns=False):
         self.sdb.put(db)
+        if vulns:  # bucket "vulnerability" over every advisory's VulnerabilityID (FillInfo / Filter / VEX legs)
+            from tools.synth_vuln import vuln_arena
+            self._vids = self.sm.MixDB.vuln_ids_of(self.sdb)
+            db.put_arena(*vuln_arena(self._vids))
+        self.has_vulns = vulns
+
+    def vuln_ids(self):
+        return self._vids
+
+    def adv_vuln_id(self, db, a):
+        from trivy_amd.batch import advisory_vuln_id
+        return advisory_vuln_id(db, a)
 
     def targets(self):
         out = []
@@ -171,9 +189,7 @@ class Mix:
             lo, hi = max(b, s) - s, min(e, s + len(g["key"])) - s
             if hi <= lo:
                 continue
-            bucket, kind = self.sdb.plats[p]
-            mb.add_many(bucket, g["name"][lo:hi], g["ver"][lo:hi],
-                        arches=g["arch"][lo:hi] if "arch" in g else None, ksplice=(kind == "oracle"))
+            self.sm.add_slice(mb, self.sdb, p, g, lo, hi)
 
     def cpu_baseline(self, budget_s, threads):
         import oracle.drivers as od
@@ -190,6 +206,13 @@ class Mix:
                 t = time.perf_counter()
                 if kind in sm.LANG_OF:
                     ol.detect(recs, sm.LANG_OF[kind], pkgs)
+                elif kind == "redhat":
+                    recs = od.Records(self.sdb.records_for({"Red Hat": {g["name"][i].decode() for i in idx},
+                                                            "Red Hat CPE": {"repository", "nvr", "cpe"}}))
+                    t = time.perf_counter()
+                    for rel in (7, 8, 9):
+                        od.driver_detect("redhat", str(rel), None,
+                                         [pk for pk, i in zip(pkgs, idx) if int(g["rhrel"][i]) == rel], recs, None)
                 else:
                     fam, fmt = sm.DRIVER_OF[kind]
                     od.driver_detect(fam, fmt.format(bucket.split(" ")[-1]), None, pkgs, recs, None)
@@ -261,7 +284,7 @@ def main():
     t0 = time.perf_counter()
     wl = C2(args) if args.config == "c2" else Mix(args, args.config)
     db = trivy_amd.DB()
-    wl.load(db, vulns=args.config == "c2" and not args.no_fill)
+    wl.load(db, vulns=args.config in ("c2", "c5") and not args.no_fill)
     eng = trivy_amd.Engine(db.finalize(), local)
     log(rank, f"[bench] {wl.name}: db {wl.n_keys} keys, {wl.n_adv} advisories, tables "
               f"{eng.table_bytes()/1e6:.1f} MB ({time.perf_counter()-t0:.1f}s)")
@@ -370,7 +393,7 @@ def main():
         fill_gbs = fill_bytes / (fill_ms / 1e3) / 1e9
         fill = {"kernel_ms": fill_ms, "matches_per_s": total / (fill_ms / 1e3),
                 "algorithmic_bytes_per_launch": fill_bytes, "achieved_GBs": fill_gbs,
-                "frac": fill_gbs / HBM_PEAK_GBS, "db_vulnerabilities": len(wl.sdb.vuln_ids())}
+                "frac": fill_gbs / HBM_PEAK_GBS, "db_vulnerabilities": len(wl.vuln_ids())}
         # result.Filter (filter.go:60-139) behind FillInfo: default options (every severity),
         # per result dedup + BySeverity order; wall time per call incl. its one sync
         mb.fill()
@@ -382,7 +405,7 @@ def main():
         # sampled from the match list, as the host compile (trivy_amd/vex.py) would emit them
         pr = mb.pairs()
         pick = np.random.default_rng(5).choice(len(pr), size=max(1, len(pr) // 100), replace=False)
-        vex = (pr[pick, 0], [wl.sdb.adv_vid[a] for a in pr[pick, 1].tolist()])
+        vex = (pr[pick, 0] - sb, [wl.adv_vuln_id(db, a) for a in pr[pick, 1].tolist()])
         vopts = mb.filter_opts(vex=vex)
         vkept = mb.filter(vopts)
         vex_ms = mb.filter_time(vopts, max(3, args.steps // 4))

@@ -43,6 +43,23 @@ def test_mix_batch_parity(cfg):
         pkgs = sm.driver_packages(sdb, p, g, idx)
         roots = sm.C3_ROOTS.get(kind, [bucket])
         recs = sdb.records_for({r: {x["Name"] for x in pkgs} for r in roots})
+        if kind == "redhat":  # per-CVE merge: the batch epilogue (GPU) vs drop-in vs oracle
+            names = {g["name"][i].decode() for i in idx}
+            recs = sdb.records_for({"Red Hat": names, "Red Hat CPE": {"repository", "nvr", "cpe"}})
+            want, got = [], []
+            for rel in (7, 8, 9):
+                sub = [pk for pk, i in zip(pkgs, idx) if int(g["rhrel"][i]) == rel]
+                want += od.driver_detect("redhat", str(rel), None, sub, od.Records(recs), None)
+                got += ospkg.Scanner(eng, "redhat").detect(str(rel), None, sub)
+            assert canon(got) == canon(want), bucket
+            every = sm.driver_packages(sdb, p, g, np.arange(len(g["key"])))
+            batch_vulns = mb.redhat_result({first + i: pk for i, pk in enumerate(every)})
+            sampled = {pk["ID"] for pk in pkgs}
+            assert canon([v for v in batch_vulns if v.get("PkgID") in sampled]) == canon(want), bucket
+            rh_checked = len(want)
+            assert rh_checked > 100 and any(len(v.get("VendorIDs", [])) > 1 for v in want)
+            checked += len(want)
+            continue
         if kind in sm.LANG_OF:
             want = ol.detect(od.Records(recs), sm.LANG_OF[kind], pkgs)
             got = library.detect(eng, sm.LANG_OF[kind], pkgs)

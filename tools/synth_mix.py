@@ -17,9 +17,10 @@ from tools.synth import _SYL, _counts
 
 # (batch bucket, kind, DB roots) - OS buckets are their own root; language buckets scan
 # every root with the "eco::" prefix (pkg/detector/library/driver.go:124-131)
-C5_PLATS = [("Oracle Linux 8", "oracle"), ("Oracle Linux 9", "oracle"), ("alma 8", "alma"), ("alma 9", "alma"),
-            ("alpine 3.19", "alpine"), ("alpine 3.20", "alpine"), ("rocky 8", "rocky"), ("rocky 9", "rocky")]
-C5_WEIGHTS = [8, 8, 18, 18, 12, 12, 12, 12]
+C5_PLATS = [("Oracle Linux 8", "oracle"), ("Oracle Linux 9", "oracle"), ("Red Hat", "redhat"), ("alma 8", "alma"),
+            ("alma 9", "alma"), ("alpine 3.19", "alpine"), ("alpine 3.20", "alpine"), ("rocky 8", "rocky"),
+            ("rocky 9", "rocky")]
+C5_WEIGHTS = [5, 5, 30, 8, 8, 15, 15, 7, 7]  # RHEL family 70 (Red Hat 30) / Alpine 30
 C3_PLATS = [("go::", "go"), ("maven::", "maven"), ("npm::", "npm"), ("pip::", "pip")]
 C3_WEIGHTS = [15, 20, 40, 25]
 # C4 (BASELINE config 4): one mixed batch, OS packages 60 % / language packages 40 %
@@ -29,7 +30,20 @@ C3_ROOTS = {"go": ["go::GitHub Security Advisory Go", "go::The Go Vulnerability 
             "maven": ["maven::GitHub Security Advisory Maven"], "npm": ["npm::GitHub Security Advisory npm"],
             "pip": ["pip::GitHub Security Advisory pip"]}
 DRIVER_OF = {"alma": ("alma", "{}"), "rocky": ("rocky", "{}"), "oracle": ("oracle", "{}"),
-             "alpine": ("alpine", "{}.1")}
+             "alpine": ("alpine", "{}.1"), "redhat": ("redhat", "{}")}
+# Red Hat (one "Red Hat" bucket for every release; the CPE sets pick the release):
+# CPE indices per release and the repositories / NVRs the "Red Hat CPE" buckets map to them
+RH_CPES = {7: [0, 1], 8: [2, 3], 9: [4, 5]}
+RH_CPE_NAMES = ["cpe:/o:redhat:enterprise_linux:7::server", "cpe:/o:redhat:enterprise_linux:7::client",
+                "cpe:/a:redhat:enterprise_linux:8::appstream", "cpe:/o:redhat:enterprise_linux:8::baseos",
+                "cpe:/a:redhat:enterprise_linux:9::appstream", "cpe:/o:redhat:enterprise_linux:9::baseos"]
+RH_DEFAULT_CS = {7: ["rhel-7-server-rpms", "rhel-7-server-extras-rpms"],
+                 8: ["rhel-8-for-x86_64-baseos-rpms", "rhel-8-for-x86_64-appstream-rpms"],
+                 9: ["rhel-9-for-x86_64-baseos-rpms", "rhel-9-for-x86_64-appstream-rpms"]}
+RH_REPOS = {"rhel-7-server-rpms": [0], "rhel-7-server-extras-rpms": [0, 1],
+            "rhel-8-for-x86_64-baseos-rpms": [3], "rhel-8-for-x86_64-appstream-rpms": [2],
+            "rhel-9-for-x86_64-baseos-rpms": [5], "rhel-9-for-x86_64-appstream-rpms": [4]}
+RH_NVRS = {f"ubi{r}-container-{r}.{k}-{k + 1}-x86_64": RH_CPES[r] for r in (7, 8, 9) for k in range(4)}
 LANG_OF = {"go": "gomod", "maven": "jar", "npm": "npm", "pip": "pip"}
 ARCHES = [b"x86_64", b"aarch64", b"noarch", b"i686"]
 
@@ -62,6 +76,20 @@ class MixDB:
             lens = np.stack([n for _, n in c], axis=1).reshape(-1)
             db.put_arena(len(recs), depth, arena, np.ascontiguousarray(off), np.ascontiguousarray(lens))
         return db
+
+    @staticmethod
+    def vuln_ids_of(mdb):
+        """Distinct VulnerabilityIDs the drivers report (Red Hat: the entries' CVE IDs, else
+        the bucket key), in byte order - the keys of the "vulnerability" bucket."""
+        ids = set()
+        for path, v in mdb.records:
+            if path[0] == "Red Hat":
+                for e in json.loads(v).get("Entries", []):
+                    for c in e.get("Cves", []):
+                        ids.add(c.get("ID") or path[2])
+            elif path[0] != "Red Hat CPE":
+                ids.add(path[2])
+        return sorted((i.encode() for i in ids))
 
     def records_for(self, names_by_root):
         """Fixture-format records of the given (root -> names) buckets + data sources."""
@@ -125,6 +153,16 @@ def make_mix_db(plats, keys_per_plat, seed=0x5EED, mean_adv=6, max_adv=400):
             sources.append((("data-source", r), json.dumps({"ID": kind, "Name": f"{r} source", "URL": f"https://{kind}"})))
         el = _os_ver(bucket).split(".")[0]
         by_root = {r: [] for r in roots}
+        if kind == "redhat":  # 5 % modular keys: "module:stream::name" (redhat.go:207-220)
+            names = sorted(set(names) | {f"{n}:{1 + i % 3}.{i % 5}::{n}" for i, n in enumerate(names) if i % 20 == 7},
+                           key=str.encode)
+            cnt = _counts(rng, len(names), mean_adv, max_adv)
+            for r, cps in RH_REPOS.items():
+                records.append((("Red Hat CPE", "repository", r), json.dumps(cps)))
+            for r, cps in RH_NVRS.items():
+                records.append((("Red Hat CPE", "nvr", r), json.dumps(cps)))
+            for i, c in enumerate(RH_CPE_NAMES):
+                records.append((("Red Hat CPE", "cpe", str(i)), json.dumps(c)))
         for i, name in enumerate(names):
             ma, mi = int(rng.integers(0, 12)), int(rng.integers(0, 20))
             flag = int(rng.random() < 0.05) * int(rng.integers(1, 3))  # rpm epoch / oracle ksplice
@@ -132,7 +170,6 @@ def make_mix_db(plats, keys_per_plat, seed=0x5EED, mean_adv=6, max_adv=400):
             key_plat.append(p)
             key_base.append((ma, mi, flag))
             for j in range(int(cnt[i])):
-                vid = f"CVE-{2010 + (j * 31 + i) % 15}-{10000 + j}"
                 f = int(rng.integers(0, 40))
                 r = int(rng.integers(1, 9))
                 if kind == "alpine":
@@ -142,6 +179,25 @@ def make_mix_db(plats, keys_per_plat, seed=0x5EED, mean_adv=6, max_adv=400):
                 elif kind == "oracle":
                     ks = flag if rng.random() < 0.5 else 0
                     val = {"FixedVersion": _rpm(0, ma, mi, f, r, el, ks)}
+                elif kind == "redhat":
+                    rel = int(rng.choice([7, 8, 9]))
+                    ent = {"Affected": RH_CPES[rel]}
+                    if rng.random() < 0.1:
+                        ent["Arches"] = ["x86_64"] if rng.random() < 0.5 else ["aarch64", "x86_64"]
+                    pool = max(2, int(cnt[i]) // 2)  # CVEs repeat across a package's advisories: merges
+                    cve = f"CVE-{2016 + (i + j) % 8}-{20000 + (i * 7 + j % pool) % 9000}"
+                    if rng.random() < 0.25:  # unfixed, keyed by its CVE
+                        vid = cve
+                        ent.update({"Cves": [{"Severity": int(rng.integers(0, 5))}], "FixedVersion": "",
+                                    "Status": int(rng.choice([3, 5, 6]))})
+                    else:
+                        vid = f"RHSA-{2015 + j % 9}:{1000 + (i * 13 + j) % 9000}"
+                        cves = [{"ID": cve, "Severity": int(rng.integers(0, 5))}]
+                        if rng.random() < 0.3:
+                            cves.append({"ID": f"CVE-{2016 + (i + j + 1) % 8}-{20000 + (i * 7 + (j + 1) % pool) % 9000}",
+                                         "Severity": int(rng.integers(0, 5))})
+                        ent.update({"Cves": cves, "FixedVersion": _rpm(flag, ma, mi, f, r, f"{rel}_{r % 3}", 0)})
+                    val = {"Entries": [ent]}
                 elif kind == "rocky":
                     ents = [{"FixedVersion": _rpm(flag, ma, mi, f, r, el, 0), "Arches": ["aarch64", "x86_64"]}]
                     if rng.random() < 0.3:
@@ -149,6 +205,8 @@ def make_mix_db(plats, keys_per_plat, seed=0x5EED, mean_adv=6, max_adv=400):
                     val = {"Entries": ents}
                 else:
                     val = _lib_adv(rng, kind, ma, mi, f)
+                if kind != "redhat":
+                    vid = f"CVE-{2010 + (j * 31 + i) % 15}-{10000 + j}"
                 root = roots[0] if len(roots) == 1 or rng.random() < 0.7 else roots[1]
                 by_root[root].append(((root, name, vid), json.dumps(val)))
                 if len(roots) > 1 and rng.random() < 0.1:  # the same ID in the other source too
@@ -208,7 +266,32 @@ def make_mix_batch(db, n, weights, seed, miss=0.25, zipf=2.5):
         mmp = _cat(_s(ma), b".", _s(mi), b".", _s(patch))
         g = {"key": np.where(missing, -1, key), "name": names}
         el = _os_ver(bucket).split(".")[0].encode()
-        if kind == "alpine":
+        if kind == "redhat":
+            # one RHEL release per image (target of 400 packages): it picks the default
+            # content sets; 20 % of images carry BuildInfo (content sets + container NVR)
+            nt = (m + 399) // 400
+            rel_t = rng.choice([7, 8, 9], nt)
+            bi_t = rng.random(nt) < 0.2
+            nvr_t = np.array([f"ubi{r}-container-{r}.{k}-{k + 1}" for r, k in zip(rel_t, rng.integers(0, 4, nt))],
+                             dtype="S")
+            t = np.arange(m) // 400
+            keyname = np.array(db.keys, dtype=object)[key].astype("S")
+            modular = np.char.find(keyname, b"::") >= 0
+            plain = np.array([k.split(b"::")[-1] for k in keyname], dtype="S")
+            g["pname"] = np.where(missing, names, plain)
+            g["label"] = np.where(modular & ~missing,
+                                  _cat(np.array([k.split(b"::")[0] for k in keyname], dtype="S"), b":20210101:abcdef12"),
+                                  b"")
+            g["rhrel"] = rel_t[t]
+            g["bi"] = bi_t[t]
+            g["nvr"] = nvr_t[t]
+            relv = _cat(_s(rel), b".el", _s(rel_t[t]), b"_", _s(rel % 3))
+            epoch = np.where(rng.random(m) < 0.9, flag, 0)
+            g["version"], g["rel"], g["epoch"] = mmp, relv, epoch
+            full = _cat(mmp, b"-", relv)
+            g["ver"] = np.where(epoch > 0, _cat(_s(epoch), b":", full), full)
+            g["arch"] = np.array(ARCHES, dtype="S")[rng.choice(4, m, p=[0.6, 0.15, 0.2, 0.05])]
+        elif kind == "alpine":
             g["ver"] = _cat(mmp, b"-r", _s(rel))
             g["rel"] = np.full(m, b"", dtype="S1")
             g["epoch"] = np.zeros(m, dtype=np.int64)
@@ -242,14 +325,32 @@ def make_mix_batch(db, n, weights, seed, miss=0.25, zipf=2.5):
     return MixBatch(groups)
 
 
+def rh_cpe_key(g, i):
+    """(content sets, NVR) of Red Hat package i (redhat.go:112-120)."""
+    r = int(g["rhrel"][i])
+    if g["bi"][i]:
+        return tuple(RH_DEFAULT_CS[r]), g["nvr"][i].decode() + "-x86_64"
+    return tuple(RH_DEFAULT_CS[r]), ""
+
+
+def add_slice(mb, db, p, g, lo, hi):
+    """Adds rows [lo, hi) of group g (platform p) to a MatchBatch; returns the first index."""
+    bucket, kind = db.plats[p]
+    arches = g["arch"][lo:hi] if "arch" in g else None
+    if kind != "redhat":
+        return mb.add_many(bucket, g["name"][lo:hi], g["ver"][lo:hi], arches=arches, ksplice=(kind == "oracle"))
+    ids, sets = np.zeros(hi - lo, dtype=np.uint32), {}
+    for i in range(lo, hi):
+        k = rh_cpe_key(g, i)
+        if k not in sets:
+            sets[k] = mb.cpe_set(list(k[0]), k[1])
+        ids[i - lo] = sets[k]
+    return mb.add_many(bucket, g["name"][lo:hi], g["ver"][lo:hi], arches=arches, cpe_sets=ids)
+
+
 def add_to(mb, db, batch):
     """Adds every group to a trivy_amd.batch.MatchBatch; returns [(plat, first index)]."""
-    out = []
-    for p, g in batch.groups:
-        bucket, kind = db.plats[p]
-        first = mb.add_many(bucket, g["name"], g["ver"], arches=g.get("arch"), ksplice=(kind == "oracle"))
-        out.append((p, first))
-    return out
+    return [(p, add_slice(mb, db, p, g, 0, len(g["key"]))) for p, g in batch.groups]
 
 
 def driver_packages(db, p, g, idx):
@@ -261,10 +362,18 @@ def driver_packages(db, p, g, idx):
         if kind in LANG_OF:
             pk.append({"Name": name, "Version": g["ver"][i].decode(), "ID": f"p{i}"})
             continue
+        if kind == "redhat":
+            name = g["pname"][i].decode()
         d = {"ID": f"p{i}", "Name": name, "Version": g["version"][i].decode(), "Release": g["rel"][i].decode(),
              "Epoch": int(g["epoch"][i]), "SrcName": name, "SrcVersion": g["version"][i].decode(),
              "SrcRelease": g["rel"][i].decode(), "SrcEpoch": int(g["epoch"][i])}
         if "arch" in g:
             d["Arch"] = g["arch"][i].decode()
+        if kind == "redhat":
+            if g["label"][i]:
+                d["Modularitylabel"] = g["label"][i].decode()
+            if g["bi"][i]:
+                cs, nvr = rh_cpe_key(g, i)
+                d["BuildInfo"] = {"ContentSets": list(cs), "Nvr": g["nvr"][i].decode(), "Arch": "x86_64"}
         pk.append(d)
     return pk

@@ -51,6 +51,10 @@ class Vuln(ctypes.Structure):
     ]
 
 
+class AttrCols(ctypes.Structure):
+    _fields_ = [("arch_off", ctypes.c_void_p), ("arch_len", ctypes.c_void_p), ("cpe_set", ctypes.c_void_p)]
+
+
 class Result(ctypes.Structure):
     _fields_ = [("vulns", ctypes.POINTER(Vuln)), ("n", ctypes.c_size_t), ("eosl", ctypes.c_int32),
                 ("priv", ctypes.c_void_p)]
@@ -117,6 +121,11 @@ _SIG = [
                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_void_p, ctypes.c_uint32]),
     ("tvm_batch_size", ctypes.c_int64, [_P]),
+    ("tvm_batch_cpe_set", ctypes.c_int64, [_P, _P, ctypes.c_void_p, ctypes.c_size_t, Str]),
+    ("tvm_batch_add_many_attrs", ctypes.c_int64, [_P, _P, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_void_p, ctypes.c_uint32]),
+    ("tvm_match_redhat_result", ctypes.c_int, [_P, _P, ctypes.POINTER(Result), ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_batch_upload", ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_match_launch", ctypes.c_int, [_P, _P, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_engine_sync", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t]),

@@ -14,7 +14,7 @@ import numpy as np
 
 from ._lib import lib, errbuf
 
-ATTR_ARCH, ATTR_KSPLICE = 1, 2
+ATTR_ARCH, ATTR_KSPLICE, ATTR_CPESET = 1, 2, 4
 
 
 def _packed(col):
@@ -51,21 +51,51 @@ class MatchBatch:
         self.h = lib().tvm_batch_new()
         self.total = None
 
-    def add_many(self, bucket, names, versions, arches=None, ksplice=False):
-        """Adds len(names) packages of one platform bucket; returns the first index."""
+    def add_many(self, bucket, names, versions, arches=None, ksplice=False, cpe_sets=None):
+        """Adds len(names) packages of one platform bucket; returns the first index.
+        cpe_sets: per package a cpe_set() id (Red Hat)."""
         if not len(names):
             return len(self)
+        from ._lib import AttrCols
         cols = [names, versions] + ([arches] if arches is not None else [])
         arena, c = arena_of(*cols)
         flags = (ATTR_ARCH if arches is not None else 0) | (ATTR_KSPLICE if ksplice else 0)
         ao, al = c[2] if arches is not None else (None, None)
-        first = lib().tvm_batch_add_many_ex(
+        cs = None
+        if cpe_sets is not None:
+            flags |= ATTR_CPESET
+            cs = np.ascontiguousarray(cpe_sets, dtype=np.uint32)
+        attrs = AttrCols(ao.ctypes.data if ao is not None else None, al.ctypes.data if al is not None else None,
+                         cs.ctypes.data if cs is not None else None)
+        first = lib().tvm_batch_add_many_attrs(
             self.h, self.engine.h, bucket.encode(), len(names), arena, c[0][0].ctypes.data, c[0][1].ctypes.data,
-            c[1][0].ctypes.data, c[1][1].ctypes.data, ao.ctypes.data if ao is not None else None,
-            al.ctypes.data if al is not None else None, flags)
+            c[1][0].ctypes.data, c[1][1].ctypes.data, ctypes.byref(attrs), flags)
         if first < 0:
-            raise RuntimeError("tvm_batch_add_many_ex rejected the packages")
+            raise RuntimeError("tvm_batch_add_many_attrs rejected the packages")
         return first
+
+    def cpe_set(self, content_sets, nvr=""):
+        """Registers a Red Hat (content sets, NVR) CPE set (redhat.go:112-120); returns its id."""
+        from ._lib import Str, s
+        keep = [s(x) for x in content_sets]
+        arr = (Str * max(len(keep), 1))(*keep)
+        i = lib().tvm_batch_cpe_set(self.h, self.engine.h, arr, len(keep), s(nvr))
+        if i < 0:
+            raise RuntimeError("tvm_batch_cpe_set failed")
+        return i
+
+    def redhat_result(self, pkgs):
+        """The Red Hat driver's epilogue for the batch's Red Hat packages (GPU per-CVE merge,
+        tvm_match_redhat_result); pkgs: the package dicts in batch order (Name, ID, ...)."""
+        from ._lib import Result
+        from .detector.ospkg import _convert
+        res, e = Result(), errbuf()
+        self._check(lib().tvm_match_redhat_result(self.engine.h, self.h, ctypes.byref(res), e, len(e)), e,
+                    "tvm_match_redhat_result")
+        try:
+            return _convert(res, pkgs)
+        finally:
+            lib().tvm_result_free(ctypes.byref(res))
 
     def add_arena(self, bucket, n, arena, name_off, name_len, ver_off, ver_len):
         """Adds n packages whose name/version bytes already sit in one arena (u64 offsets,
