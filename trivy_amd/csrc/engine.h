@@ -15,7 +15,9 @@ namespace tvm {
 
 class DB;
 
-constexpr int kTile = 256;  // packages per tile (workgroup) of both match kernels
+constexpr int kTile = 256;   // packages per tile (workgroup) of the match kernels
+constexpr int kGroup = 64;   // packages per offset group (one wavefront); tile_off is per group
+constexpr int kGroupsPerTile = kTile / kGroup;
 
 // Device view of the flattened tables (db.h device images).
 struct DevDB {
@@ -32,8 +34,8 @@ struct DevDB {
 
 // A package batch.  pk[i] = {plat, name_len | ver_len << 16}; the name and version bytes
 // of every package sit back to back in `arena`, package after package, so offsets are
-// implicit: tile_off[t] is the arena offset of package t * kTile (the kernels scan the
-// lengths within a tile).  plat = 0xFFFFFFFF when the bucket is absent.  Lengths
+// implicit: tile_off[g] is the arena offset of package g * kGroup (the kernels scan the
+// lengths within a 64-package group, one wavefront).  plat = 0xFFFFFFFF when the bucket is absent.  Lengths
 // saturate at 0xFFFF (the stored bytes are cut to match).  Optional per-package attributes
 // (common.h PA_*), present when the batch touches rows with filters: attr[i] = {arch id |
 // PA_NOARCH, ksplice tag or CPE-set id}; CPE set s is the bitset cpe_bits[s * cpe_words ..
@@ -49,6 +51,7 @@ struct HostBatch {
   void add(uint32_t plat, std::string_view name, std::string_view ver, uint2 a);
   size_t size() const { return pk.size(); }
   uint32_t n_tiles() const { return uint32_t((pk.size() + kTile - 1) / kTile); }
+  uint32_t n_groups() const { return uint32_t((pk.size() + kGroup - 1) / kGroup); }
   // arena offset of package i's name (O(kTile) per call); all of them at once
   uint64_t name_off(size_t i) const;
   void name_offsets(std::vector<uint64_t>& off) const;
@@ -152,9 +155,6 @@ class Engine {
   int variant_ = 0;
   std::atomic<int> last_launched_{-1};
   hipStream_t stream_ = nullptr;
-  hipStream_t stream2_ = nullptr;           // sweep chunks (overlap the next chunk's probe)
-  std::vector<hipEvent_t> ev_;              // probe-done events, one per chunk in flight
-  hipEvent_t ev_done_ = nullptr;
   const DB* db_ = nullptr;
   DevDB d_;
   std::vector<void*> allocs_;

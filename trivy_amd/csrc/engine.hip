@@ -15,7 +15,9 @@ namespace tvm {
 
 // kern_*.hip
 ProbeFn probe_fn_DEB();
+#ifdef TVM_DIAG
 ProbeFn probe_fn_DEB_diag(int d);
+#endif
 ProbeFn probe_fn_OS();
 ProbeFn probe_fn_ALL();
 const SweepFn* sweep_table(bool filt);
@@ -33,10 +35,6 @@ constexpr const char* kVariantNames[] = {
 // Grammar-set index of a batch: 0 = dpkg only, 1 = OS grammars, 2 = any.
 int grammar_index(uint32_t gm) { return (gm & ~GM_DEB) == 0 ? 0 : (gm & ~GM_OS) == 0 ? 1 : 2; }
 constexpr int kNumVariants = 1 + kNumTuned;
-// A pass is cut into up to kMaxChunks chunks of at least kMinChunkTiles tiles: chunk c's
-// probe (main stream) overlaps chunk c-1's sweep (second stream) on the same CUs.
-constexpr int kMaxChunks = 8;
-constexpr uint32_t kMinChunkTiles = 512;
 constexpr bool kFusedVariant[] = {
 #define TVM_F_(F, K, MB, NAME) F != 0,
     TVM_MATCH_VARIANTS(TVM_F_)
@@ -53,8 +51,10 @@ FusedFn fused_fn(uint32_t gm, int vi) {
 
 
 ProbeFn probe_fn(uint32_t gm) {
+#ifdef TVM_DIAG  // measurement builds only (make DIAG=1): probe with parts switched off
   static const int diag = std::getenv("TVM_PROBE_DIAG") ? std::atoi(std::getenv("TVM_PROBE_DIAG")) : 0;
   if (diag && grammar_index(gm) == 0) return probe_fn_DEB_diag(diag);
+#endif
   switch (grammar_index(gm)) {
     case 0: return probe_fn_DEB();
     case 1: return probe_fn_OS();
@@ -101,7 +101,7 @@ int resolve_variant(int v, uint32_t) { return v == 0 ? 1 + kAutoVariant : v; }
 // ---- HostBatch ------------------------------------------------------------------------------
 
 void HostBatch::add(uint32_t plat, std::string_view name, std::string_view ver) {
-  if (pk.size() % kTile == 0) tile_off.push_back(arena.size());
+  if (pk.size() % kGroup == 0) tile_off.push_back(arena.size());
   const size_t nl = std::min<size_t>(name.size(), 0xFFFF), vl = std::min<size_t>(ver.size(), 0xFFFF);
   pk.push_back(make_uint2(plat, uint32_t(nl) | (uint32_t(vl) << 16)));
   arena.insert(arena.end(), name.begin(), name.begin() + nl);
@@ -117,9 +117,9 @@ void HostBatch::add(uint32_t plat, std::string_view name, std::string_view ver, 
 }
 
 uint64_t HostBatch::name_off(size_t i) const {
-  const size_t t = i / kTile;
+  const size_t t = i / kGroup;
   uint64_t o = tile_off[t];
-  for (size_t j = t * kTile; j < i; j++) o += (pk[j].y & 0xFFFFu) + (pk[j].y >> 16);
+  for (size_t j = t * kGroup; j < i; j++) o += (pk[j].y & 0xFFFFu) + (pk[j].y >> 16);
   return o;
 }
 
@@ -156,9 +156,6 @@ Engine::~Engine() {
   if (dev_ >= 0) (void)hipSetDevice(dev_);
   for (void* p : allocs_) (void)hipFree(p);
   if (spill_) (void)hipFree(spill_);
-  for (hipEvent_t e : ev_) (void)hipEventDestroy(e);
-  if (ev_done_) (void)hipEventDestroy(ev_done_);
-  if (stream2_) (void)hipStreamDestroy(stream2_);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -177,18 +174,10 @@ Engine* Engine::open(const DB& db, int device, std::string& err) {
   e->db_ = &db;
   if (const char* v = std::getenv("TVM_VARIANT")) e->set_variant(std::atoi(v));
   if (!hip_ok(hipSetDevice(device), "hipSetDevice", err) ||
-      !hip_ok(hipStreamCreateWithFlags(&e->stream_, hipStreamNonBlocking), "hipStreamCreate", err) ||
-      !hip_ok(hipStreamCreateWithFlags(&e->stream2_, hipStreamNonBlocking), "hipStreamCreate", err) ||
-      !hip_ok(hipEventCreateWithFlags(&e->ev_done_, hipEventDisableTiming), "hipEventCreate", err)) {
+      !hip_ok(hipStreamCreateWithFlags(&e->stream_, hipStreamNonBlocking), "hipStreamCreate", err)) {
     delete e;
     return nullptr;
   }
-  e->ev_.resize(kMaxChunks);
-  for (hipEvent_t& ev : e->ev_)
-    if (!hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate", err)) {
-      delete e;
-      return nullptr;
-    }
   Slot* sl; uint8_t* na; Row* rows; uint64_t* kw; PlatInfo* pl; RowAux* ax; uint32_t* ai;
   bool ok = upload_vec(db.aux, &ax, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.aux_ids, &ai, e->allocs_, e->table_bytes_, err) &&
@@ -260,7 +249,7 @@ bool Engine::alloc_batch(const HostBatch& hb, DevBatch& b, std::string& err) {
   }
   // +32 B tail: the kernels stage whole 16-byte lines and read names as dword triples
   return dmalloc(&b.pk, hb.pk.size(), "hipMalloc(batch)", err) &&
-         dmalloc(&b.tile_off, size_t(b.n_tiles) + 1, "hipMalloc(tile offsets)", err) &&
+         dmalloc(&b.tile_off, size_t(b.n_tiles) * kGroupsPerTile + 1, "hipMalloc(group offsets)", err) &&
          dmalloc(&b.arena, (hb.arena.size() + 32 + 15) & ~size_t(15), "hipMalloc(batch arena)", err) &&
          (hb.attr.empty() || dmalloc(&b.attr, hb.attr.size(), "hipMalloc(batch attr)", err)) &&
          dmalloc(&b.rec, hb.pk.size(), "hipMalloc(package records)", err) &&
@@ -269,8 +258,8 @@ bool Engine::alloc_batch(const HostBatch& hb, DevBatch& b, std::string& err) {
 
 bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
   if (!alloc_batch(hb, b, err)) return false;
-  std::vector<uint64_t> toff(hb.tile_off);
-  toff.push_back(hb.arena.size());
+  std::vector<uint64_t> toff(hb.tile_off);  // + the arena end, then padded to whole tiles
+  toff.resize(size_t(hb.n_tiles()) * kGroupsPerTile + 1, hb.arena.size());
   if (!hb.pk.empty() && !hip_ok(hipMemcpy(b.pk, hb.pk.data(), hb.pk.size() * sizeof(uint2), hipMemcpyHostToDevice),
                                 "H2D batch", err))
     return false;
@@ -356,7 +345,7 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
   ProbeArgs pa;
   pa.db = d_;
   pa.pk = b.pk + p0;
-  pa.tile_off = b.tile_off + t_begin;
+  pa.tile_off = b.tile_off + size_t(t_begin) * kGroupsPerTile;
   pa.arena = b.arena;
   pa.n = n;
   pa.p0 = p0;
@@ -410,21 +399,9 @@ bool Engine::launch(const DevBatch& b, const DevMatches& m, hipStream_t st, std:
   if (!ensure_scratch(b.spill_words, err)) return false;
   if (!hip_ok(hipMemsetAsync(m.ctl, 0, 8 * sizeof(unsigned long long), st), "memset(ctl)", err)) return false;
   if (b.n_tiles == 0) return true;
-  // chunk overlap on two streams (TVM_OVERLAP=1): measured slower than one launch
-  static const bool overlap = std::getenv("TVM_OVERLAP") != nullptr;
-  const uint32_t chunks =
-      overlap ? std::max<uint32_t>(1, std::min<uint32_t>(kMaxChunks, b.n_tiles / kMinChunkTiles)) : 1u;
-  if (chunks == 1) return launch_tiles(b, m, 0, b.n_tiles, st, st, nullptr, err);
-  // chunk c: probe on st, sweep on stream2_ behind the probe's event; st then waits for the
-  // last sweep, so a caller synchronising st sees the whole pass
-  const uint32_t per = (b.n_tiles + chunks - 1) / chunks;
-  if (!hip_ok(hipEventRecord(ev_done_, st), "hipEventRecord", err) ||
-      !hip_ok(hipStreamWaitEvent(stream2_, ev_done_, 0), "hipStreamWaitEvent", err))  // ctl zeroed first
-    return false;
-  for (uint32_t c = 0; c < chunks; c++)
-    if (!launch_tiles(b, m, c * per, std::min(b.n_tiles, (c + 1) * per), st, stream2_, ev_[c], err)) return false;
-  return hip_ok(hipEventRecord(ev_done_, stream2_), "hipEventRecord", err) &&
-         hip_ok(hipStreamWaitEvent(st, ev_done_, 0), "hipStreamWaitEvent", err);
+  // one launch over every tile (cutting the pass into chunks whose probe overlaps the
+  // previous chunk's sweep on a second stream measured slower: DESIGN.md §4)
+  return launch_tiles(b, m, 0, b.n_tiles, st, st, nullptr, err);
 }
 
 bool Engine::match_host(const HostBatch& hb, std::vector<uint2>& out, int64_t& err_pkg, std::string& err) {

@@ -4,7 +4,9 @@
 
 namespace tvm {
 ProbeFn probe_fn_DEB() { return &launch_probe<GM_DEB>; }
-ProbeFn probe_fn_DEB_diag(int d) {  // TEMP measurement
+#ifdef TVM_DIAG  // measurement builds only (make DIAG=1)
+ProbeFn probe_fn_DEB_diag(int d) {
   return d == 1 ? &launch_probe<GM_DEB, 1> : d == 2 ? &launch_probe<GM_DEB, 2> : &launch_probe<GM_DEB, 3>;
 }
+#endif
 }  // namespace tvm

@@ -48,7 +48,7 @@ constexpr uint32_t kMapCap = 4096;  // tiles with at most this many pairs map pa
 struct ProbeArgs {
   DevDB db;
   const uint2* pk;           // chunk-relative: {plat, name_len | ver_len << 16}
-  const uint64_t* tile_off;  // chunk-relative: arena offset of each tile's first package (+1)
+  const uint64_t* tile_off;  // chunk-relative: arena offset of each 64-package group (+1)
   const uint8_t* arena;
   uint32_t n;                // packages in this launch
   uint32_t p0;               // batch index of the launch's first package
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(kTile) void probe_kernel(ProbeArgs a) {
   const uint32_t nlen = d.y & 0xFFFFu, vlen = d.y >> 16;
   uint32_t off = 0;
   block_exscan<kTile>(wsum, nlen + vlen, tid, off);
-  const uint64_t w0 = a.tile_off[t], w1 = a.tile_off[t + 1];
+  const uint64_t w0 = a.tile_off[t * kGroupsPerTile], w1 = a.tile_off[(t + 1) * kGroupsPerTile];
   const uint64_t base16 = w0 & ~uint64_t(15);
   const bool staged = w1 - base16 <= kStage;
   if (staged) {
@@ -349,9 +349,9 @@ __device__ __forceinline__ int cmp_be(uint64_t a0, uint64_t a1, const uint64_t* 
 }
 
 // Interval test of tile package q's installed key against one row (global index ridx).
-template <bool FILT>
-__device__ __forceinline__ bool eval_row(const SweepArgs& a, const SweepShared<FILT>& s, uint32_t q, uint32_t p,
-                                         const Row& row, uint32_t ridx) {
+template <bool FILT, class S>
+__device__ __forceinline__ bool eval_row(const SweepArgs& a, const S& s, uint32_t q, uint32_t p, const Row& row,
+                                         uint32_t ridx) {
   const uint32_t ki = s.kinfo[q];
   if constexpr (FILT) {
     if ((row.adv & ROW_FILTER) && !aux_pass(a, ridx, s.pattr[q], ki)) return false;
@@ -557,7 +557,9 @@ __global__ __launch_bounds__(kTile) void sweep_kernel(SweepArgs a) {
 
 // Probe and sweep of one tile in one workgroup (the record stays in registers/LDS): tiles
 // of one CU sit in different phases, so one tile's probe latency overlaps another's sweep.
-template <uint32_t GM, int K, int MB, bool FILT>
+// DIAG (measurement only, wrong match lists by construction; "diag_*" variants): bit 0 skips
+// the version encoder, bit 1 the index probe, bit 2 the sweep.
+template <uint32_t GM, int K, int MB, bool FILT, int DIAG = 0>
 __global__ __launch_bounds__(kTile) void fused_kernel(FusedArgs fa) {
   constexpr uint32_t kStageVec = kStage / 16 + 2;
   constexpr uint32_t kMbufVec = (MB * 5 + 15) / 16;
@@ -572,7 +574,7 @@ __global__ __launch_bounds__(kTile) void fused_kernel(FusedArgs fa) {
   const uint32_t nlen = d.y & 0xFFFFu, vlen = d.y >> 16;
   uint32_t off = 0;
   block_exscan<kTile>(s.wsum[0], nlen + vlen, tid, off);
-  const uint64_t w0 = a.tile_off[t], w1 = a.tile_off[t + 1];
+  const uint64_t w0 = a.tile_off[t * kGroupsPerTile], w1 = a.tile_off[(t + 1) * kGroupsPerTile];
   const uint64_t base16 = w0 & ~uint64_t(15);
   const bool staged = w1 - base16 <= kStage;
   if (staged) {
@@ -588,12 +590,13 @@ __global__ __launch_bounds__(kTile) void fused_kernel(FusedArgs fa) {
   if (p < a.n && d.x < a.db.n_plats) {
     if (staged) {
       const uint8_t* sb = reinterpret_cast<const uint8_t*>(buf) + uint32_t(w0 - base16) + off;
-      probe_one<GM, uint32_t>(a, p, d.x, nlen, vlen, sb, sb + nlen, r);
+      probe_one<GM, uint32_t, DIAG & 3>(a, p, d.x, nlen, vlen, sb, sb + nlen, r);
     } else {
       const uint8_t* gb = a.arena + w0 + off;
-      probe_one<GM, uint32_t>(a, p, d.x, nlen, vlen, gb, gb + nlen, r);
+      probe_one<GM, uint32_t, DIAG & 3>(a, p, d.x, nlen, vlen, gb, gb + nlen, r);
     }
   }
+  if (DIAG & 4) r.meta.y = 0;  // no rows: the sweep does nothing
   __syncthreads();  // the strings are dead: buf becomes the match buffer
   uint32_t* madv = reinterpret_cast<uint32_t*>(buf);
   sweep_tile<K, MB, FILT>(fa.sa, s, madv, reinterpret_cast<uint8_t*>(madv + MB), map, t, tid, r);
@@ -609,9 +612,9 @@ void launch_sweep(uint32_t n_tiles, hipStream_t st, const SweepArgs& a) {
   hipLaunchKernelGGL((sweep_kernel<K, MB, FILT>), dim3(n_tiles), dim3(kTile), 0, st, a);
 }
 
-template <uint32_t GM, int K, int MB, bool FILT>
+template <uint32_t GM, int K, int MB, bool FILT, int DIAG = 0>
 void launch_fused(uint32_t n_tiles, hipStream_t st, const FusedArgs& a) {
-  hipLaunchKernelGGL((fused_kernel<GM, K, MB, FILT>), dim3(n_tiles), dim3(kTile), 0, st, a);
+  hipLaunchKernelGGL((fused_kernel<GM, K, MB, FILT, DIAG>), dim3(n_tiles), dim3(kTile), 0, st, a);
 }
 
 }  // namespace

@@ -65,8 +65,8 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
   bounds_.push_back(n_tiles);
   if (n_tiles == 0) bounds_ = {0, 0};
   const uint32_t nc = uint32_t(bounds_.size() - 1);
-  toff_ = hb.tile_off;
-  toff_.push_back(hb.arena.size());
+  toff_ = hb.tile_off;  // per 64-package group, + the arena end, padded to whole tiles
+  toff_.resize(size_t(n_tiles) * kGroupsPerTile + 1, hb.arena.size());
   cap_ = std::max<uint64_t>(match_cap, 1);
   if (cap_ >= (1ull << 32)) {
     err = "pipeline: row ends are 32-bit; split the batch below 2^32 matches";
@@ -141,11 +141,12 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
   for (uint32_t c = 0; c < nc; c++) {
     const uint32_t t0 = bounds_[c], t1 = bounds_[c + 1];
     const size_t p0 = size_t(t0) * kTile, p1 = std::min<size_t>(size_t(t1) * kTile, n);
-    const uint64_t a0 = toff_[t0], a1 = toff_[t1];
+    const size_t g0 = size_t(t0) * kGroupsPerTile, g1 = size_t(t1) * kGroupsPerTile;
+    const uint64_t a0 = toff_[g0], a1 = toff_[g1];
     if (!ok(hipMemcpyAsync(db_.pk + p0, hb.pk.data() + p0, (p1 - p0) * sizeof(uint2), hipMemcpyHostToDevice, s_h2d_),
             "H2D packages", err) ||
-        !ok(hipMemcpyAsync(db_.tile_off + t0, toff_.data() + t0, (t1 - t0 + 1) * 8, hipMemcpyHostToDevice, s_h2d_),
-            "H2D tile offsets", err) ||
+        !ok(hipMemcpyAsync(db_.tile_off + g0, toff_.data() + g0, (g1 - g0 + 1) * 8, hipMemcpyHostToDevice, s_h2d_),
+            "H2D group offsets", err) ||
         (a1 > a0 && !ok(hipMemcpyAsync(db_.arena + a0, hb.arena.data() + a0, a1 - a0, hipMemcpyHostToDevice, s_h2d_),
                         "H2D strings", err)) ||
         (!hb.attr.empty() &&
@@ -153,7 +154,7 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
              "H2D attributes", err)) ||
         !ok(hipEventRecord(ev_h_[c], s_h2d_), "hipEventRecord", err))
       return false;
-    h2d_ += (p1 - p0) * sizeof(uint2) + (t1 - t0 + 1) * 8 + (a1 - a0) + (hb.attr.empty() ? 0 : (p1 - p0) * sizeof(uint2));
+    h2d_ += (p1 - p0) * sizeof(uint2) + (g1 - g0 + 1) * 8 + (a1 - a0) + (hb.attr.empty() ? 0 : (p1 - p0) * sizeof(uint2));
   }
   // 2. kernels per chunk, each behind its chunk's copy
   for (uint32_t c = 0; c < nc; c++) {
