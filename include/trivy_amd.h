@@ -344,14 +344,45 @@ uint64_t tvm_match_fill_algorithmic_bytes(tvm_engine* e, tvm_batch* b);
 const char* tvm_fill_source_name(tvm_engine* e, uint32_t id);
 
 /* ---- result.Filter over a batch -------------------------------------------------------- */
-/* One tvm_batch_add* call = one Result; its packages' (name, version) are the
- * DetectedVulnerability PkgName / InstalledVersion, PkgPath is empty. */
+/* One tvm_batch_add* call = one Result.  A package's DetectedVulnerability PkgName /
+ * InstalledVersion / PkgPath are its batch (name, version) and "" unless
+ * tvm_batch_set_report names others for packages [first, first + n): Debian / Ubuntu report
+ * the binary package and FormatVersion while they match on the source package
+ * (debian.go:66-83), library packages carry a PkgPath (filter.go:124 dedup key, BySeverity's
+ * last key).  NULL arrays keep the defaults.  Replaces the filter's package layout. */
+int tvm_batch_set_report(tvm_batch* b, uint64_t first, uint64_t n, const tvm_str* names, const tvm_str* versions,
+                         const tvm_str* paths);
+
+/* Ignore-file findings compiled against the batch by the host (trivy_amd/ignore.py; the
+ * reference's IgnoreConfig.MatchVulnerability, ignore.go:86-161).  Rules name a
+ * vulnerability by index into ids and carry the precedence of the finding they came from,
+ * pass << 31 | finding index (pass 0: the finding has no paths or one matched the result's
+ * Target; pass 1: one matched the package's PkgPath): a pair several rules hit is ignored by
+ * the smallest, which is the finding MatchVulnerability returns. */
 typedef struct {
-  uint32_t severity_mask;        /* bit i: SeverityNames[i] is in FilterOption.Severities */
+  const tvm_str* ids;            /* distinct vulnerability IDs */
+  size_t n_ids;
+  const uint32_t* id_ranks;      /* optional: tvm_vuln_rank_many of ids (same engine, no swap
+                                    since), so a call ranks no strings */
+  const uint32_t* all_id;        /* rules for every package */
+  const uint32_t* all_prec;
+  size_t n_all;
+  const uint32_t* pkg_pkg;       /* rules for one package (PURL-scoped findings whose PURL */
+  const uint32_t* pkg_id;        /* matches that package's) */
+  const uint32_t* pkg_prec;
+  size_t n_pkg;
+  const uint32_t* pkg_class;     /* per batch package: its class (NULL: no class rules) */
+  const uint32_t* cls_class;     /* rules for every package of one class (PURL-scoped */
+  const uint32_t* cls_id;        /* findings on packages without a PURL, matchPURL */
+  const uint32_t* cls_prec;      /* ignore.go:116-126; path-scoped findings by Target / */
+  size_t n_cls;                  /* PkgPath) */
+} tvm_ignore_rules;
+
+typedef struct {
+  uint32_t severity_mask;        /* bit i: SeverityNames[i] is in FilterOption.Severities (i <= 4) */
   uint32_t ignore_status_mask;   /* bit s: dbTypes.Status s is in FilterOption.IgnoreStatuses */
-  const tvm_str* ignore_ids;     /* IDs of the ignore file's unexpired findings without paths/PURLs */
-  size_t n_ignore_ids;
-  /* VEX suppressions (pkg/vex, applied after dedup as filter.go:51-53 filterByVEX does):
+  const tvm_ignore_rules* ignore;  /* NULL: no ignore file */
+  /* VEX suppressions (pkg/vex, applied after the dedup as filter.go:51-53 filterByVEX does):
    * entry k drops package vex_pkgs[k]'s finding of vulnerability vex_ids[vex_id_index[k]].
    * The host compiles a VEX document against the batch's package PURLs into these entries
    * (trivy_amd/vex.py: OpenVEX openvex.go:21-54, CycloneDX cyclonedx.go:48-84, CSAF
@@ -359,23 +390,27 @@ typedef struct {
   const uint32_t* vex_pkgs;
   const uint32_t* vex_id_index;
   size_t n_vex;
-  /* Ignore-file findings scoped by PURL (ignore.go MatchVulnerability, applied before the
-   * dedup as filter.go:117-122 does): entry k drops package ignore_pair_pkgs[k]'s finding of
-   * pair_ids[ignore_pair_id_index[k]] (trivy_amd/ignore.py compiles them). */
-  const uint32_t* ignore_pair_pkgs;
-  const uint32_t* ignore_pair_id_index;
-  size_t n_ignore_pairs;
-  /* The distinct vulnerability IDs the two pair lists index, each once. */
-  const tvm_str* pair_ids;
-  size_t n_pair_ids;
+  const tvm_str* vex_ids;        /* distinct vulnerability IDs */
+  size_t n_vex_ids;
+  const uint32_t* vex_id_ranks;  /* optional: tvm_vuln_rank_many of vex_ids */
 } tvm_filter_opts;
+/* The filter's rank of each vulnerability ID (byte order among the DB's advisory IDs;
+ * 0xFFFFFFFF: no advisory has it), computed once when a VEX document or ignore file is
+ * compiled for a batch.  Ranks belong to the engine's current DB. */
+int tvm_vuln_rank_many(tvm_engine* e, const tvm_str* ids, size_t n, uint32_t* ranks);
 /* filterVulnerabilities + sort.Sort(BySeverity) (+ the VEX filter) for every result of the
  * batch, on the GPU, after tvm_match_launch + tvm_match_fill.  n_kept = surviving
- * vulnerabilities. */
-int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint64_t* n_kept, char* err, size_t errlen);
+ * vulnerabilities, n_ignored = findings the ignore file dropped (ModifiedFindings).
+ * Not for a batch with a package base (a shard): results must be whole. */
+int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint64_t* n_kept, uint64_t* n_ignored,
+                     char* err, size_t errlen);
 /* The surviving {package, advisory} pairs (uint32 x2) in report order: results in add
  * order, each in BySeverity order. */
 int tvm_match_filter_fetch(tvm_engine* e, tvm_batch* b, uint32_t* pairs, uint64_t cap, uint64_t* n_out);
+/* The ignored findings as {package, advisory, finding index} (uint32 x3) in detection
+ * order (results in add order, each in its Vulnerabilities order): result.ModifiedFindings
+ * with status "ignored" and the finding's Statement (filter.go:117-122). */
+int tvm_match_filter_ignored(tvm_engine* e, tvm_batch* b, uint32_t* triples, uint64_t cap, uint64_t* n_out);
 /* Wall time of `steps` tvm_match_filter calls (ms total; each call synchronises once). */
 int tvm_match_filter_time(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, int steps, double* ms, char* err,
                           size_t errlen);

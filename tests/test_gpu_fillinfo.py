@@ -194,6 +194,7 @@ def _filter_fixture(seed=9):
     arena, noff, nlen, voff, vlen = batch.arena()
     for p, s, e in batch.targets:
         mb.add_arena(sdb.platforms[p], e - s, arena, noff[s:], nlen[s:], voff[s:], vlen[s:])
+    mb.result_bounds = [(s, e) for _, s, e in batch.targets]
     total, errp, _ = mb.run()
     assert errp == -1 and total > 1000
     pairs = mb.pairs()
@@ -240,19 +241,19 @@ def test_match_filter_batch_vs_oracle(opts):
     got = mb.filtered_pairs(n).tolist()
     findings = [{"ID": i, "Paths": [], "PURLs": [], "ExpiredAt": None, "Statement": ""}
                 for i in opts.get("ignore_ids", ())]
-    want = []
+    want, want_ign = [], []
     for vulns in by_target:
         filled = vi.fill_info(bucket, [{k: x for k, x in v.items() if k != "_pair"} for v in vulns])
         for f, v in zip(filled, vulns):
             f["_pair"] = v["_pair"]
-        kept, _ = of.filter_vulnerabilities("", filled, list(opts["severities"]), opts.get("ignore_statuses", ()),
-                                            findings)
+        kept, ign = of.filter_vulnerabilities("", filled, list(opts["severities"]), opts.get("ignore_statuses", ()),
+                                              findings)
         want += kept or []
+        want_ign += [list(v["_pair"]) + [findings.index(f)] for v, f in ign]
     assert len(got) == len(want), (len(got), len(want))
-    for (pk, adv), w in zip(got, want):
-        wp, wa = w["_pair"]
-        # a duplicate package's copy is interchangeable: same advisory, same (name, version)
-        assert adv == wa and sdb.adv_vid[adv].decode() == w["VulnerabilityID"], (pk, adv, w)
+    # exact pairs: the dedup winner is the reference's first-seen package
+    assert got == [list(w["_pair"]) for w in want]
+    assert mb.ignored_findings().tolist() == want_ign and (not findings or want_ign)
     mb.close()
 
 
@@ -287,7 +288,11 @@ def test_match_filter_batch_vex_vs_oracle(kind):
     at = "cyclonedx" if kind == "cyclonedx" else ""
     sup = VEX.new(text, at, sv.SERIAL, 1).suppressions(purls, refs, result_of, roots)
     opts = dict(severities=("UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"))
+    o2 = mb.filter_opts(vex=sup, **opts)
+    o2.vex_id_ranks = None  # the C-ABI ranks the ID strings itself
+    n2 = mb.filter(o2)
     n = mb.filter(mb.filter_opts(vex=sup, **opts))
+    assert n == n2
     got = mb.filtered_pairs(n).tolist()
     oracle_vex = ov.VEX.new(text, at, sv.SERIAL, 1)
     want, dropped = [], 0
@@ -303,9 +308,7 @@ def test_match_filter_batch_vex_vs_oracle(kind):
         want += after
     assert dropped > 0
     assert len(got) == len(want), (len(got), len(want))
-    for (pk, adv), w in zip(got, want):
-        assert adv == w["_pair"][1] and sdb.adv_vid[adv].decode() == w["VulnerabilityID"], (pk, adv, w)
-        assert purls[pk] == purls[w["_pair"][0]]
+    assert got == [list(w["_pair"]) for w in want]
     mb.close()
 
 
@@ -315,40 +318,112 @@ def test_match_filter_batch_ignore_purls_vs_oracle():
     versionless, qualifier-scoped) equal oracle/filter.py per result."""
     import oracle.filter as of
     from tools import synth_vex as sv
-    from trivy_amd.ignore import split_findings
+    from trivy_amd.ignore import compile_rules
     mb, bucket, by_target, sdb = _filter_fixture()
     purls = [None] * len(mb)
     for vulns in by_target:
         plat = "debian 12" if vulns and vulns[0]["DataSource"]["ID"] == "debian" else "ubuntu 22.04"
         for v in vulns:
-            purls[v["_pair"][0]] = sv.purl_of(plat, v["PkgName"], v["InstalledVersion"],
-                                              "amd64" if len(v["PkgName"]) % 3 else None)
+            # every 7th package has no PURL: PURL-scoped findings match it (matchPURL)
+            purls[v["_pair"][0]] = None if v["_pair"][0] % 7 == 0 else sv.purl_of(
+                plat, v["PkgName"], v["InstalledVersion"], "amd64" if len(v["PkgName"]) % 3 else None)
     rng = np.random.default_rng(21)
     flat = [v for vulns in by_target for v in vulns]
     findings = []
     for k in range(120):
         v = flat[rng.integers(len(flat))]
-        pu = purls[v["_pair"][0]]
+        pu = purls[v["_pair"][0]] or "pkg:deb/debian/%s@%s" % (v["PkgName"], v["InstalledVersion"])
         base, _, q = pu.partition("?")
         pat = [pu, base, base.rpartition("@")[0], base.rpartition("@")[0] + "?arch=amd64"][k % 4]
         findings.append({"ID": v["VulnerabilityID"], "Paths": [], "PURLs": [pat], "ExpiredAt": None, "Statement": ""})
     findings.append({"ID": flat[0]["VulnerabilityID"], "Paths": [], "PURLs": [], "ExpiredAt": None, "Statement": ""})
-    plain, pairs = split_findings(findings, purls)
+    rules = compile_rules(findings, purls)
+    assert rules.pkg_class is not None and len(rules.cls[0]) > 0  # PURL-less packages: class rules
     opts = dict(severities=("UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"))
-    n = mb.filter(mb.filter_opts(ignore_ids=plain, ignore_pairs=pairs, **opts))
+    n = mb.filter(mb.filter_opts(ignore=rules, **opts))
     got = mb.filtered_pairs(n).tolist()
     ofind = [dict(f, PURLs=[of.purl_from_string(x) for x in f["PURLs"]]) for f in findings]
-    want, ignored = [], 0
+    want, want_ign = [], []
     for vulns in by_target:
         filled = vi.fill_info(bucket, [{k: x for k, x in v.items() if k != "_pair"} for v in vulns])
         for f, v in zip(filled, vulns):
             f["_pair"] = v["_pair"]
-            f["PkgIdentifier"] = {"PURL": of.purl_from_string(purls[v["_pair"][0]])}
+            pu = purls[v["_pair"][0]]
+            f["PkgIdentifier"] = {"PURL": of.purl_from_string(pu) if pu else None}
         kept, ig = of.filter_vulnerabilities("", filled, list(opts["severities"]), (), ofind)
-        ignored += len(ig)
+        want_ign += [list(v["_pair"]) + [ofind.index(f)] for v, f in ig]
         want += kept or []
-    assert ignored > 0
+    assert want_ign
+    assert got == [list(w["_pair"]) for w in want]
+    assert mb.ignored_findings().tolist() == want_ign
+    bad = mb.filter_opts(**opts)
+    bad.severity_mask |= 1 << 5  # SeverityNames has 5 entries: higher bits are rejected
+    with pytest.raises(RuntimeError, match="severity_mask"):
+        mb.filter(bad)
+    mb.close()
+
+
+def test_match_filter_batch_report_paths_vs_oracle():
+    """The dedup key and BySeverity on report identities (tvm_batch_set_report): packages that
+    match under different source names but report one (PkgName, InstalledVersion) dedup
+    across packages with DIFFERENT FixedVersions (the greater wins, ties the first seen);
+    PkgPath splits dedup groups and breaks BySeverity ties; path-scoped ignore findings
+    (Target / PkgPath globs, pass order) and ModifiedFindings - all vs oracle/filter.py."""
+    import oracle.filter as of
+    from trivy_amd.ignore import compile_rules
+    mb, bucket, by_target, sdb = _filter_fixture(seed=13)
+    n_pkgs = len(mb)
+    key_of = {bytes(k): i for i, k in enumerate(sdb.key_names)}
+    rname, rver, rpath = [None] * n_pkgs, [None] * n_pkgs, [""] * n_pkgs
+    pkg_name, pkg_ver = {}, {}
+    for vulns in by_target:
+        for v in vulns:
+            pkg_name[v["_pair"][0]], pkg_ver[v["_pair"][0]] = v["PkgName"], v["InstalledVersion"]
+    for pk in range(n_pkgs):
+        nm, ver = pkg_name.get(pk), pkg_ver.get(pk)
+        if nm is None:
+            nm, ver = "none%d" % pk, "0"
+        k = key_of.get(nm.encode(), pk)
+        # keys 25 apart share CVE IDs (tools/synth.py): one binary name per residue class
+        rname[pk] = "bin-%d" % (k % 25) if k % 3 else nm
+        rver[pk] = "1.0" if k % 2 else ver
+        rpath[pk] = "" if pk % 4 else "opt/app%d/lib.jar" % (pk % 3)
+    mb.set_report(0, rname, rver, rpath)
+    targets = ["img%d/layer%d" % (t, t % 3) for t in range(len(by_target))]
+    res = [(targets[t], s, e) for t, (s, e) in enumerate(mb.result_bounds)]
+    rng = np.random.default_rng(5)
+    flat = [v for vulns in by_target for v in vulns]
+    globs = ["**", "img1/**", "img*/layer2", "opt/app1/*.jar", "opt/**", "nomatch/**"]
+    findings = []
+    for k in range(80):
+        v = flat[int(rng.integers(len(flat)))]
+        f = {"ID": v["VulnerabilityID"], "Paths": [], "PURLs": [], "ExpiredAt": None, "Statement": "st%d" % k}
+        if k % 2:
+            f["Paths"] = [globs[int(rng.integers(len(globs)))]]
+        findings.append(f)
+    rules = compile_rules(findings, [None] * n_pkgs, res, rpath)
+    opts = dict(severities=("UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"))
+    n = mb.filter(mb.filter_opts(ignore=rules, **opts))
+    got = mb.filtered_pairs(n).tolist()
+    want, want_ign, cross = [], [], 0
+    for t, vulns in enumerate(by_target):
+        filled = vi.fill_info(bucket, [{k: x for k, x in v.items() if k != "_pair"} for v in vulns])
+        for f, v in zip(filled, vulns):
+            pk = v["_pair"][0]
+            f["_pair"] = v["_pair"]
+            f["PkgName"], f["InstalledVersion"], f["PkgPath"] = rname[pk], rver[pk], rpath[pk]
+            if not rpath[pk]:
+                f.pop("PkgPath")
+        kept, ig = of.filter_vulnerabilities(targets[t], filled, list(opts["severities"]), (), findings)
+        want_ign += [list(v["_pair"]) + [findings.index(f)] for v, f in ig]
+        want += kept or []
+        seen = {}
+        for f in filled:  # dedup keys held by two packages with different FixedVersions
+            key = (f["VulnerabilityID"], f["PkgName"], f["InstalledVersion"], f.get("PkgPath", ""))
+            seen.setdefault(key, set()).add((f["_pair"][0], f.get("FixedVersion", "")))
+        cross += sum(1 for s in seen.values() if len({x[0] for x in s}) > 1 and len({x[1] for x in s}) > 1)
+    assert cross > 0 and want_ign
     assert len(got) == len(want), (len(got), len(want))
-    for (pk, adv), w in zip(got, want):
-        assert adv == w["_pair"][1] and purls[pk] == purls[w["_pair"][0]], (pk, adv, w)
+    assert got == [list(w["_pair"]) for w in want]
+    assert mb.ignored_findings().tolist() == want_ign
     mb.close()

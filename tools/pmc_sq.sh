@@ -8,7 +8,7 @@ OUT=$R/gpurun_out/${PMC_TAG:-sq}
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
-ARGS="--steps 3 --warmup 1 --no-cpu --no-fill ${BENCH_ARGS:-}"
+ARGS="--steps 3 --warmup 1 --no-cpu --no-e2e ${NOFILL---no-fill} ${BENCH_ARGS:-}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_trace -o run --output-format csv -- python3 $R/bench.py $ARGS > $OUT/prof_trace.log 2>&1
 pmc() {  # name, counters...
   local name=$1; shift

@@ -15,7 +15,8 @@ import os
 import statistics
 import sys
 
-KERNELS = ("probe_kernel", "sweep_kernel", "match_kernel", "fill_pairs_kernel")
+KERNELS = ("probe_kernel", "sweep_kernel", "fused_kernel", "match_kernel", "fill_pairs_kernel", "filter_mark",
+           "filter_select", "filter_place", "order_kernel")
 
 
 def kname(name):

@@ -75,12 +75,20 @@ class FillResult(ctypes.Structure):
     _fields_ = [("items", ctypes.POINTER(FillOut)), ("n", ctypes.c_size_t), ("priv", ctypes.c_void_p)]
 
 
+class IgnoreRulesC(ctypes.Structure):
+    _fields_ = [("ids", ctypes.POINTER(Str)), ("n_ids", ctypes.c_size_t), ("id_ranks", ctypes.c_void_p),
+                ("all_id", ctypes.c_void_p), ("all_prec", ctypes.c_void_p), ("n_all", ctypes.c_size_t),
+                ("pkg_pkg", ctypes.c_void_p), ("pkg_id", ctypes.c_void_p), ("pkg_prec", ctypes.c_void_p),
+                ("n_pkg", ctypes.c_size_t), ("pkg_class", ctypes.c_void_p),
+                ("cls_class", ctypes.c_void_p), ("cls_id", ctypes.c_void_p), ("cls_prec", ctypes.c_void_p),
+                ("n_cls", ctypes.c_size_t)]
+
+
 class FilterOpts(ctypes.Structure):
     _fields_ = [("severity_mask", ctypes.c_uint32), ("ignore_status_mask", ctypes.c_uint32),
-                ("ignore_ids", ctypes.POINTER(Str)), ("n_ignore_ids", ctypes.c_size_t),
+                ("ignore", ctypes.POINTER(IgnoreRulesC)),
                 ("vex_pkgs", ctypes.c_void_p), ("vex_id_index", ctypes.c_void_p), ("n_vex", ctypes.c_size_t),
-                ("ignore_pair_pkgs", ctypes.c_void_p), ("ignore_pair_id_index", ctypes.c_void_p),
-                ("n_ignore_pairs", ctypes.c_size_t), ("pair_ids", ctypes.POINTER(Str)), ("n_pair_ids", ctypes.c_size_t)]
+                ("vex_ids", ctypes.POINTER(Str)), ("n_vex_ids", ctypes.c_size_t), ("vex_id_ranks", ctypes.c_void_p)]
 
 
 # (name, restype, argtypes) for every exported symbol of include/trivy_amd.h
@@ -168,9 +176,14 @@ _SIG = [
     ("tvm_match_fill_algorithmic_bytes", ctypes.c_uint64, [_P, _P]),
     ("tvm_fill_source_name", ctypes.c_char_p, [_P, ctypes.c_uint32]),
     ("tvm_match_filter", ctypes.c_int, [_P, _P, ctypes.POINTER(FilterOpts), ctypes.POINTER(ctypes.c_uint64),
-                                        ctypes.c_char_p, ctypes.c_size_t]),
+                                        ctypes.POINTER(ctypes.c_uint64), ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_match_filter_fetch", ctypes.c_int, [_P, _P, ctypes.c_void_p, ctypes.c_uint64,
                                               ctypes.POINTER(ctypes.c_uint64)]),
+    ("tvm_match_filter_ignored", ctypes.c_int, [_P, _P, ctypes.c_void_p, ctypes.c_uint64,
+                                                ctypes.POINTER(ctypes.c_uint64)]),
+    ("tvm_vuln_rank_many", ctypes.c_int, [_P, ctypes.POINTER(Str), ctypes.c_size_t, ctypes.c_void_p]),
+    ("tvm_batch_set_report", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(Str),
+                                            ctypes.POINTER(Str), ctypes.POINTER(Str)]),
     ("tvm_match_filter_time", ctypes.c_int, [_P, _P, ctypes.POINTER(FilterOpts), ctypes.c_int,
                                              ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, ctypes.c_size_t]),
 ]

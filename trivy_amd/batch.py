@@ -254,40 +254,83 @@ class MatchBatch:
         return lib().tvm_match_fill_algorithmic_bytes(self.engine.h, self.h)
 
     # ---- result.Filter per result (tvm_match_filter*) ----
-    @staticmethod
-    def filter_opts(severities=("UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"), ignore_statuses=(), ignore_ids=(),
-                    vex=None, ignore_pairs=None):
-        """FilterOption's vulnerability part.  ignore_ids: the ignore file's plain IDs;
-        ignore_pairs: (package indices, IDs) of its PURL-scoped findings
-        (trivy_amd.ignore.pair_suppressions); vex: (package indices, IDs) from
-        trivy_amd.vex.VEX.suppressions (None: no VEX document)."""
-        from ._lib import FilterOpts, Str
+    def set_report(self, first, names=None, versions=None, paths=None):
+        """DetectedVulnerability PkgName / InstalledVersion / PkgPath of packages [first,
+        first + n) where they differ from the batch (name, version) / "" (tvm_batch_set_report)."""
+        from ._lib import Str
+        cols, keep = [], []
+        n = None
+        for col in (names, versions, paths):
+            if col is None:
+                cols.append(None)
+                continue
+            blobs = [x.encode() if isinstance(x, str) else bytes(x) for x in col]
+            if n is not None and len(blobs) != n:
+                raise ValueError("report columns differ in length")
+            n = len(blobs)
+            arr = (Str * max(n, 1))(*[Str(b, len(b)) for b in blobs])
+            keep.append((blobs, arr))
+            cols.append(arr)
+        if n is None:
+            return
+        if lib().tvm_batch_set_report(self.h, first, n, *cols):
+            raise ValueError("tvm_batch_set_report: bad range")
+
+    def vuln_ranks(self, str_array, n):
+        """tvm_vuln_rank_many over a Str array (uint32, 0xFFFFFFFF = unknown ID)."""
+        r = np.zeros(max(n, 1), dtype=np.uint32)
+        if lib().tvm_vuln_rank_many(self.engine.h, str_array, n, r.ctypes.data):
+            raise RuntimeError("tvm_vuln_rank_many failed")
+        return r
+
+    def filter_opts(self, severities=("UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"), ignore_statuses=(),
+                    ignore_ids=(), ignore=None, vex=None):
+        """FilterOption's vulnerability part.  ignore: trivy_amd.ignore.IgnoreRules compiled
+        for this batch; ignore_ids: shorthand for a plain .trivyignore (IDs in file order);
+        vex: (package indices, IDs) from trivy_amd.vex.VEX.suppressions (None: no VEX
+        document)."""
+        from ._lib import FilterOpts, IgnoreRulesC, Str
+        from .ignore import plain_rules
         names = ["UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"]
-        ids = [i.encode() if isinstance(i, str) else bytes(i) for i in ignore_ids]
-        arr = (Str * max(len(ids), 1))(*[Str(b, len(b)) for b in ids])
-        uniq, lists = {}, []
-        for pairs in (vex, ignore_pairs):
-            ppk, pids = pairs if pairs is not None else (np.zeros(0, dtype=np.uint32), [])
-            ppk = np.ascontiguousarray(ppk, dtype=np.uint32)
-            if len(ppk) != len(pids):
+        strs = lambda xs: (lambda bl: (bl, (Str * max(len(bl), 1))(*[Str(b, len(b)) for b in bl])))(  # noqa: E731
+            [i.encode() if isinstance(i, str) else bytes(i) for i in xs])
+        ptr = lambda a: a.ctypes.data if a is not None and len(a) else None  # noqa: E731
+        keep = []
+        if ignore is None and ignore_ids:
+            ignore = plain_rules(list(ignore_ids), 0)
+        rc = None
+        if ignore is not None:
+            (aid, aprec), (ppk, pid, pprec), (ccl, cid, cprec), pcls = ignore.arrays()
+            ids = strs(ignore.ids)
+            ranks = self.vuln_ranks(ids[1], len(ids[0]))  # once per compile, not per filter call
+            keep.append(ranks)
+            rc = IgnoreRulesC(ids[1], len(ids[0]), ranks.ctypes.data, ptr(aid), ptr(aprec), len(aid), ptr(ppk), ptr(pid), ptr(pprec),
+                              len(ppk), ptr(pcls), ptr(ccl), ptr(cid), ptr(cprec), len(ccl))
+            keep += [ids, aid, aprec, ppk, pid, pprec, ccl, cid, cprec, pcls, rc]
+        uniq = {}
+        vpk, vidx = np.zeros(0, dtype=np.uint32), np.zeros(0, dtype=np.uint32)
+        if vex is not None:
+            vpk = np.ascontiguousarray(vex[0], dtype=np.uint32)
+            if len(vpk) != len(vex[1]):
                 raise ValueError("one vulnerability ID per package index")
-            lists.append((ppk, np.array([uniq.setdefault(i, len(uniq)) for i in pids], dtype=np.uint32)))
-        ublobs = [i.encode() if isinstance(i, str) else bytes(i) for i in uniq]
-        uarr = (Str * max(len(ublobs), 1))(*[Str(b, len(b)) for b in ublobs])
-        (vpk, vidx), (ipk, iidx) = lists
-        ptr = lambda a: a.ctypes.data if len(a) else None  # noqa: E731
-        o = FilterOpts(sum(1 << names.index(x) for x in severities), sum(1 << s for s in ignore_statuses), arr,
-                       len(ids), ptr(vpk), ptr(vidx), len(vpk), ptr(ipk), ptr(iidx), len(ipk), uarr, len(ublobs))
-        o._keep = (ids, arr, lists, ublobs, uarr)
+            vidx = np.array([uniq.setdefault(i, len(uniq)) for i in vex[1]], dtype=np.uint32)
+        vids = strs(list(uniq))
+        vranks = self.vuln_ranks(vids[1], len(vids[0]))
+        o = FilterOpts(sum(1 << names.index(x) for x in severities), sum(1 << s for s in ignore_statuses),
+                       ctypes.pointer(rc) if rc is not None else None, ptr(vpk), ptr(vidx), len(vpk), vids[1],
+                       len(vids[0]), vranks.ctypes.data)
+        o._keep = (keep, vpk, vidx, vids, vranks)
         return o
 
     def filter(self, opts):
-        """filterVulnerabilities + BySeverity for every result (after launch() + fill());
-        returns the number of surviving vulnerabilities."""
+        """filterVulnerabilities + BySeverity (+ VEX) for every result (after launch() +
+        fill()); returns the number of surviving vulnerabilities (self.n_ignored: the
+        ignored findings)."""
         e = errbuf()
-        n = ctypes.c_uint64()
-        self._check(lib().tvm_match_filter(self.engine.h, self.h, ctypes.byref(opts), ctypes.byref(n), e, len(e)), e,
-                    "tvm_match_filter")
+        n, ni = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(lib().tvm_match_filter(self.engine.h, self.h, ctypes.byref(opts), ctypes.byref(n),
+                                           ctypes.byref(ni), e, len(e)), e, "tvm_match_filter")
+        self.n_ignored = ni.value
         return n.value
 
     def filtered_pairs(self, n):
@@ -295,6 +338,16 @@ class MatchBatch:
         got = ctypes.c_uint64()
         if lib().tvm_match_filter_fetch(self.engine.h, self.h, out.ctypes.data, n, ctypes.byref(got)):
             raise RuntimeError("tvm_match_filter_fetch failed")
+        return out[:got.value]
+
+    def ignored_findings(self):
+        """ModifiedFindings of the last filter(): (n, 3) uint32 {package, advisory, finding
+        index} in detection order."""
+        n = getattr(self, "n_ignored", 0)
+        out = np.zeros((n, 3), dtype=np.uint32)
+        got = ctypes.c_uint64()
+        if lib().tvm_match_filter_ignored(self.engine.h, self.h, out.ctypes.data, n, ctypes.byref(got)):
+            raise RuntimeError("tvm_match_filter_ignored failed")
         return out[:got.value]
 
     def filter_time(self, opts, steps):

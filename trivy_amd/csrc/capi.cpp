@@ -50,8 +50,13 @@ struct tvm_batch {
   DevMatches m;
   uint4* fill_out = nullptr;  // tvm_match_fill decisions, parallel to the match columns
   uint64_t fill_cap = 0;
+  uint2* fill_side() const { return reinterpret_cast<uint2*>(fill_out + fill_cap); }
   std::vector<uint32_t> target_begin;  // first package of every result (one per add call)
   BatchFilter filter;                  // tvm_match_filter state
+  // tvm_batch_set_report: per package PkgName / InstalledVersion / PkgPath overrides
+  // (rep[f][i] counts where rep_has[f][i] is set; shorter vectors = defaults beyond)
+  std::vector<std::string> rep[3];
+  std::vector<uint8_t> rep_has[3];
   RedHatMerge rh;                      // tvm_match_redhat_result state
   std::unique_ptr<Pipeline> pipe;      // tvm_pipeline_* state
   uint32_t pkg_base = 0;               // tvm_batch_set_package_base
@@ -478,6 +483,7 @@ int tvm_batch_upload(tvm_engine* e, tvm_batch* b, uint64_t cap, char* err, size_
   }
   b->dev.pkg_base = b->pkg_base;
   b->uploaded = true;
+  b->filter.reset_packages();
   b->device = e->device;
   return TVM_OK;
 }
@@ -785,14 +791,15 @@ int tvm_match_fill(tvm_engine* e, tvm_batch* b, char* err, size_t errlen) {
     if (b->fill_out) (void)hipFree(b->fill_out);
     b->fill_out = nullptr;
     b->fill_cap = 0;
-    if (hipMalloc(&b->fill_out, std::max<uint64_t>(b->m.cap, 1) * sizeof(uint4)) != hipSuccess) {
+    // decisions, then the filter's hand-off words (uint2) in the same allocation
+    if (hipMalloc(&b->fill_out, std::max<uint64_t>(b->m.cap, 1) * (sizeof(uint4) + sizeof(uint2))) != hipSuccess) {
       set_err(err, errlen, "hipMalloc(fill decisions) failed");
       return TVM_EDEVICE;
     }
     b->fill_cap = b->m.cap;
   }
   std::string msg;
-  if (!e->fill->launch_pairs(b->m.adv, b->m.ctl, b->m.cap, b->fill_out, e->eng->stream(), msg)) {
+  if (!e->fill->launch_pairs(b->m.adv, b->m.ctl, b->m.cap, b->fill_out, b->fill_side(), e->eng->stream(), msg)) {
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
   }
@@ -832,7 +839,7 @@ int tvm_match_fill_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char
   std::string msg;
   float f = 0;
   bool ok = hipEventCreate(&t0) == hipSuccess && hipEventCreate(&t1) == hipSuccess && hipEventRecord(t0, st) == hipSuccess;
-  for (int i = 0; ok && i < steps; i++) ok = e->fill->launch_pairs(b->m.adv, b->m.ctl, b->m.cap, b->fill_out, st, msg);
+  for (int i = 0; ok && i < steps; i++) ok = e->fill->launch_pairs(b->m.adv, b->m.ctl, b->m.cap, b->fill_out, b->fill_side(), st, msg);
   ok = ok && hipEventRecord(t1, st) == hipSuccess && hipEventSynchronize(t1) == hipSuccess &&
        hipEventElapsedTime(&f, t0, t1) == hipSuccess;
   if (t0) (void)hipEventDestroy(t0);
@@ -862,53 +869,107 @@ const char* tvm_fill_source_name(tvm_engine* e, uint32_t id) {
 
 // ---- result.Filter over a batch (filter.go:60-139, filter.hip) --------------------------
 
+int tvm_batch_set_report(tvm_batch* b, uint64_t first, uint64_t n, const tvm_str* names, const tvm_str* versions,
+                         const tvm_str* paths) {
+  const uint64_t size = b ? b->hb.pk.size() : 0;
+  if (!b || first > size || n > size - first) return TVM_EINVAL;
+  const tvm_str* cols[3] = {names, versions, paths};
+  for (int f = 0; f < 3; f++) {
+    if (!cols[f]) continue;
+    if (b->rep[f].size() < first + n) {
+      b->rep[f].resize(first + n);
+      b->rep_has[f].resize(first + n, 0);
+    }
+    for (uint64_t i = 0; i < n; i++) {
+      b->rep[f][first + i] = std::string(sv(cols[f][i]));
+      b->rep_has[f][first + i] = 1;
+    }
+  }
+  b->filter.reset_packages();
+  return TVM_OK;
+}
+
 namespace {
 
-// Per package: rank of (result, name, version) in result-major byte order, and whether
-// the triple repeats within its result (types.BySeverity's PkgName/InstalledVersion order
-// and filterVulnerabilities' dedup key; batch packages carry no PkgPath).
-void package_ranks(const tvm_batch* b, std::vector<uint32_t>& rank, std::vector<uint8_t>& dup) {
+// The filter's package layout (FilterPackages): within every result (one add call) the
+// packages sorted by (PkgName, InstalledVersion, PkgPath, index) - types.BySeverity's
+// package keys and filterVulnerabilities' dedup key (filter.go:124); PkgName /
+// InstalledVersion default to the batch (name, version), PkgPath to "".
+//   The reference's dedup key is the string "vulnID/pkgName/installed/pkgPath"; comparing
+// the fields instead differs only when a field itself holds a '/' that shifts the split
+// (e.g. an InstalledVersion with a '/'), which no package grammar produces.
+void package_layout(const tvm_batch* b, FilterPackages& fp) {
   const size_t n = b->hb.pk.size();
-  rank.assign(n, 0);
-  dup.assign(n, 0);
-  std::vector<uint32_t> bounds(b->target_begin);
-  bounds.push_back(uint32_t(n));
   std::vector<uint64_t> off;
   b->hb.name_offsets(off);
-  auto name = [&](uint32_t i) {
-    return std::string_view(reinterpret_cast<const char*>(b->hb.arena.data()) + off[i], b->hb.pk[i].y & 0xFFFFu);
+  const char* arena = reinterpret_cast<const char*>(b->hb.arena.data());
+  auto field = [&](int f, uint32_t i) -> std::string_view {
+    if (i < b->rep_has[f].size() && b->rep_has[f][i]) return b->rep[f][i];
+    if (f == 0) return std::string_view(arena + off[i], b->hb.pk[i].y & 0xFFFFu);
+    if (f == 1) return std::string_view(arena + off[i] + (b->hb.pk[i].y & 0xFFFFu), b->hb.pk[i].y >> 16);
+    return std::string_view();
   };
-  auto ver = [&](uint32_t i) {
-    return std::string_view(reinterpret_cast<const char*>(b->hb.arena.data()) + off[i] + (b->hb.pk[i].y & 0xFFFFu),
-                            b->hb.pk[i].y >> 16);
-  };
-  uint32_t next = 0;
-  std::vector<uint32_t> idx;
+  fp.perm.resize(n);
+  fp.grp_b.assign(n, 0);
+  fp.grp_e.assign(n, 0);
+  fp.dkey.assign(n, 0);
+  fp.prank.assign(n, 0);
+  fp.dup.assign(n, 0);
+  std::vector<uint32_t> bounds(b->target_begin);
+  bounds.push_back(uint32_t(n));
+  uint32_t next_d = 0;
   for (size_t t = 0; t + 1 < bounds.size(); t++) {
-    idx.clear();
-    for (uint32_t i = bounds[t]; i < bounds[t + 1]; i++) idx.push_back(i);
-    std::sort(idx.begin(), idx.end(), [&](uint32_t x, uint32_t y) {
-      const int c = name(x).compare(name(y));
-      return c != 0 ? c < 0 : ver(x) < ver(y);
+    uint32_t* idx = fp.perm.data() + bounds[t];
+    const uint32_t len = bounds[t + 1] - bounds[t];
+    for (uint32_t k = 0; k < len; k++) idx[k] = bounds[t] + k;
+    std::sort(idx, idx + len, [&](uint32_t x, uint32_t y) {
+      for (int f = 0; f < 3; f++) {
+        const int c = field(f, x).compare(field(f, y));
+        if (c) return c < 0;
+      }
+      return x < y;
     });
-    for (size_t k = 0; k < idx.size(); k++) {
-      const bool same = k && name(idx[k]) == name(idx[k - 1]) && ver(idx[k]) == ver(idx[k - 1]);
-      if (k && !same) next++;
-      rank[idx[k]] = next;
-      if (same) dup[idx[k]] = dup[idx[k - 1]] = 1;
+    for (uint32_t k = 0; k < len;) {  // groups of equal (PkgName, InstalledVersion)
+      uint32_t e = k + 1;
+      while (e < len && field(0, idx[e]) == field(0, idx[k]) && field(1, idx[e]) == field(1, idx[k])) e++;
+      uint32_t pr = 0;
+      for (uint32_t m = k; m < e; m++) {
+        const uint32_t p = idx[m];
+        const bool same_path = m > k && field(2, p) == field(2, idx[m - 1]);
+        if (m > k && !same_path) pr++;
+        if (m > k && !same_path) next_d++;
+        fp.grp_b[p] = bounds[t] + k;
+        fp.grp_e[p] = bounds[t] + e;
+        fp.prank[p] = pr;
+        fp.dkey[p] = next_d;
+        if (same_path) fp.dup[p] = fp.dup[idx[m - 1]] = 1;
+      }
+      next_d++;
+      k = e;
     }
-    if (!idx.empty()) next++;
   }
 }
 
 }  // namespace
 
-int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint64_t* n_kept, char* err,
-                     size_t errlen) {
-  if (!e || !b || !o || !b->uploaded || (o->n_ignore_ids && !o->ignore_ids) ||
-      (o->n_vex && (!o->vex_pkgs || !o->vex_id_index)) ||
-      (o->n_ignore_pairs && (!o->ignore_pair_pkgs || !o->ignore_pair_id_index)) || (o->n_pair_ids && !o->pair_ids))
+int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint64_t* n_kept, uint64_t* n_ignored,
+                     char* err, size_t errlen) {
+  if (!e || !b || !o || !b->uploaded || (o->n_vex && (!o->vex_pkgs || !o->vex_id_index)) ||
+      (o->n_vex_ids && !o->vex_ids && !o->vex_id_ranks))
     return TVM_EINVAL;
+  const tvm_ignore_rules* ig = o->ignore;
+  if (ig && ((ig->n_ids && !ig->ids && !ig->id_ranks) || (ig->n_all && (!ig->all_id || !ig->all_prec)) ||
+             (ig->n_pkg && (!ig->pkg_pkg || !ig->pkg_id || !ig->pkg_prec)) ||
+             (ig->n_cls && (!ig->pkg_class || !ig->cls_class || !ig->cls_id || !ig->cls_prec))))
+    return TVM_EINVAL;
+  if (o->severity_mask >> 5) {  // SeverityNames has 5 entries (UNKNOWN..CRITICAL)
+    set_err(err, errlen, "tvm_match_filter: severity_mask has bits above CRITICAL (4)");
+    return TVM_EINVAL;
+  }
+  if (b->pkg_base) {
+    set_err(err, errlen, "tvm_match_filter: the batch is a shard (package base set); filter whole results");
+    return TVM_EINVAL;
+  }
   std::shared_lock<std::shared_mutex> lk(e->mu);
   (void)hipSetDevice(e->device);
   hipStream_t st = e->eng->stream();
@@ -923,52 +984,71 @@ int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint
   }
   std::string msg;
   if (!b->filter.has_packages()) {
-    std::vector<uint32_t> rank;
-    std::vector<uint8_t> dup;
-    package_ranks(b, rank, dup);
-    if (!b->filter.set_packages(rank, dup, msg)) {
+    FilterPackages fp;
+    package_layout(b, fp);
+    if (!b->filter.set_packages(fp, msg)) {
       set_err(err, errlen, msg);
       return TVM_EDEVICE;
     }
   }
   const VulnTable& vt = e->fill->table();
-  std::vector<uint32_t> ignore;
-  for (size_t i = 0; i < o->n_ignore_ids; i++) {
-    const uint32_t r = vt.vuln_rank(std::string_view(o->ignore_ids[i].p ? o->ignore_ids[i].p : "", o->ignore_ids[i].n));
-    if (r != 0xFFFFFFFFu) ignore.push_back(r);
-  }
-  std::sort(ignore.begin(), ignore.end());
-  ignore.erase(std::unique(ignore.begin(), ignore.end()), ignore.end());
-  // VEX suppressions as (package << 32 | vulnerability rank) keys, sorted on the GPU; each
-  // distinct ID is ranked once; IDs unknown to the DB cannot name a detected vulnerability
-  // and drop out here
-  // Ignore-file pairs share the array, tagged with bit 31 of the rank word (ranks use < 31
-  // bits): filter_mark looks up the tagged key (before the dedup), filter_select the plain one.
-  std::vector<uint32_t> id_rank(o->n_pair_ids);
-  for (size_t i = 0; i < o->n_pair_ids; i++)
-    id_rank[i] = vt.vuln_rank(std::string_view(o->pair_ids[i].p ? o->pair_ids[i].p : "", o->pair_ids[i].n));
-  std::vector<uint64_t> vex;
-  vex.reserve(o->n_vex + o->n_ignore_pairs);
   const uint64_t n_pkgs = uint64_t(tvm_batch_size(b));
-  for (int list = 0; list < 2; list++) {
-    const uint32_t* pk = list ? o->ignore_pair_pkgs : o->vex_pkgs;
-    const uint32_t* ix = list ? o->ignore_pair_id_index : o->vex_id_index;
-    const size_t cnt = list ? o->n_ignore_pairs : o->n_vex;
-    for (size_t i = 0; i < cnt; i++) {
-      if (pk[i] >= n_pkgs || ix[i] >= o->n_pair_ids) {
-        set_err(err, errlen, "tvm_match_filter: VEX / ignore pair package or ID index out of range");
-        return TVM_EINVAL;
-      }
-      const uint32_t r = id_rank[ix[i]];
-      if (r < 0x80000000u) vex.push_back((uint64_t(pk[i]) << 32) | r | (list ? 0x80000000ull : 0ull));
+  FilterRules rules;
+  // each distinct ID ranked once; IDs unknown to the DB cannot name a detected
+  // vulnerability, so their rules drop out here
+  auto ranks = [&](const tvm_str* ids, size_t k, const uint32_t* given) {
+    std::vector<uint32_t> r(k);
+    for (size_t i = 0; i < k; i++) r[i] = given ? given[i] : vt.vuln_rank(sv(ids[i]));
+    return r;
+  };
+  bool bad = false;
+  auto add = [&](uint64_t tag, uint32_t subject, uint32_t id_index, const std::vector<uint32_t>& rk, uint32_t prec) {
+    if (id_index >= rk.size() || subject >= (1u << 30)) {
+      bad = true;
+      return;
+    }
+    if (rk[id_index] == 0xFFFFFFFFu) return;
+    rules.keys.push_back((tag << 62) | (uint64_t(subject) << 32) | rk[id_index]);
+    rules.prec.push_back(prec);
+    rules.kinds |= 1u << tag;
+  };
+  if (ig) {
+    const std::vector<uint32_t> rk = ranks(ig->ids, ig->n_ids, ig->id_ranks);
+    for (size_t i = 0; i < ig->n_all; i++) add(RULE_ALL, 0, ig->all_id[i], rk, ig->all_prec[i]);
+    for (size_t i = 0; i < ig->n_pkg; i++)
+      if (ig->pkg_pkg[i] >= n_pkgs) bad = true;
+      else add(RULE_PKG, ig->pkg_pkg[i], ig->pkg_id[i], rk, ig->pkg_prec[i]);
+    for (size_t i = 0; i < ig->n_cls; i++) add(RULE_CLS, ig->cls_class[i], ig->cls_id[i], rk, ig->cls_prec[i]);
+    if (rules.kinds & (1u << RULE_CLS)) {
+      rules.pkg_class.assign(ig->pkg_class, ig->pkg_class + n_pkgs);
+      for (uint32_t c : rules.pkg_class) bad |= c >= (1u << 30);
     }
   }
-  if (!b->filter.run(e->fill->dev(), b->m.pkg, b->m.adv, b->fill_out, n, ignore, vex, vt.n_vuln_ranks(), o->severity_mask,
+  if (o->n_vex) {
+    const std::vector<uint32_t> rk = ranks(o->vex_ids, o->n_vex_ids, o->vex_id_ranks);
+    for (size_t i = 0; i < o->n_vex; i++)
+      if (o->vex_pkgs[i] >= n_pkgs) bad = true;
+      else add(RULE_VEX, o->vex_pkgs[i], o->vex_id_index[i], rk, 0);
+  }
+  if (bad) {
+    set_err(err, errlen, "tvm_match_filter: rule / VEX package, class or ID index out of range");
+    return TVM_EINVAL;
+  }
+  if (!b->filter.run(e->fill->dev(), b->m.pkg, b->m.adv, b->fill_side(), n, rules, vt.n_vuln_ranks(), o->severity_mask,
                      o->ignore_status_mask, st, msg)) {
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
   }
   if (n_kept) *n_kept = b->filter.survivors();
+  if (n_ignored) *n_ignored = b->filter.ignored();
+  return TVM_OK;
+}
+
+int tvm_vuln_rank_many(tvm_engine* e, const tvm_str* ids, size_t n, uint32_t* ranks) {
+  if (!e || (n && (!ids || !ranks))) return TVM_EINVAL;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  const VulnTable& vt = e->fill->table();
+  for (size_t i = 0; i < n; i++) ranks[i] = vt.vuln_rank(sv(ids[i]));
   return TVM_OK;
 }
 
@@ -984,12 +1064,28 @@ int tvm_match_filter_fetch(tvm_engine* e, tvm_batch* b, uint32_t* pairs, uint64_
   return TVM_OK;
 }
 
+int tvm_match_filter_ignored(tvm_engine* e, tvm_batch* b, uint32_t* triples, uint64_t cap, uint64_t* n_out) {
+  if (!e || !b || (cap && !triples)) return TVM_EINVAL;
+  (void)hipSetDevice(e->device);
+  std::vector<uint32_t> out;
+  std::string msg;
+  if (!b->filter.fetch_ignored(out, e->eng->stream(), msg)) return TVM_EDEVICE;
+  const uint64_t k = std::min<uint64_t>(cap, out.size() / 3);
+  for (uint64_t i = 0; i < k; i++) {
+    triples[3 * i] = out[3 * i];
+    triples[3 * i + 1] = out[3 * i + 1];
+    triples[3 * i + 2] = out[3 * i + 2] & 0x7FFFFFFFu;  // the finding index (precedence without the pass)
+  }
+  if (n_out) *n_out = k;
+  return TVM_OK;
+}
+
 int tvm_match_filter_time(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, int steps, double* ms, char* err,
                           size_t errlen) {
   if (!ms || steps <= 0) return TVM_EINVAL;
   const auto t0 = std::chrono::steady_clock::now();
   for (int i = 0; i < steps; i++) {
-    const int rc = tvm_match_filter(e, b, o, nullptr, err, errlen);
+    const int rc = tvm_match_filter(e, b, o, nullptr, nullptr, err, errlen);
     if (rc) return rc;
   }
   *ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -32,6 +32,7 @@ struct FillArgs {
   const unsigned long long* n_dev;  // PAIRS: match count written by the match kernel
   uint64_t n;            // ITEMS: item count; PAIRS: pair-buffer capacity
   uint4* out;
+  uint2* side;           // PAIRS (optional): the filter's hand-off word per pair
 };
 
 __device__ __forceinline__ uint32_t probe_id(const FillDev& t, const uint8_t* id, uint32_t n) {
@@ -120,7 +121,11 @@ __global__ __launch_bounds__(kFillTile) void fill_pairs_kernel(FillArgs a) {
   for (uint64_t i = uint64_t(blockIdx.x) * kFillTile + threadIdx.x; i < n; i += stride) {
     const uint32_t adv = a.adv[i];
     const uint4 item = adv < a.t.n_advs ? a.t.adv_items[adv] : make_uint4(0, SRC_NONE << 16, 0, FILL_NOT_FOUND);
-    a.out[i] = decide(a.t, item, item.w);
+    const uint4 o = decide(a.t, item, item.w);
+    a.out[i] = o;
+    if (a.side)  // result.Filter reads this word, not the decision (filter.hip filter_mark)
+      a.side[i] = make_uint2(adv < a.t.n_advs ? a.t.adv_rank[adv].x : 0xFFFFFFFFu,
+                             fill_pair_severity(o, item) | ((o.y & 31u) << 8));
   }
 }
 
@@ -219,7 +224,7 @@ bool FillEngine::run_host(const std::vector<uint4>& items, const std::vector<uin
 }
 
 bool FillEngine::launch_pairs(const uint32_t* adv, const unsigned long long* n_dev, uint64_t cap, uint4* out,
-                              hipStream_t stream, std::string& err) {
+                              uint2* side, hipStream_t stream, std::string& err) {
   if (cap == 0) return true;
   FillArgs a{};
   a.t = *d_;
@@ -227,6 +232,7 @@ bool FillEngine::launch_pairs(const uint32_t* adv, const unsigned long long* n_d
   a.n_dev = n_dev;
   a.n = cap;
   a.out = out;
+  a.side = side;
   // enough waves to cover the chip many times over, capped so the stride loop does the rest
   const uint64_t blocks = std::min<uint64_t>((cap + kFillTile - 1) / kFillTile, 256ull * 64);
   hipLaunchKernelGGL(fill_pairs_kernel, dim3(uint32_t(blocks)), dim3(kFillTile), 0, stream, a);

@@ -3,33 +3,49 @@
 //
 // Reference semantics per Result (= one tvm_batch_add* call):
 //   filter.go:104-114   drop by severity ("" counts as UNKNOWN) and by ignored status;
-//   filter.go:117-122   drop vulnerabilities whose ID the ignore file lists;
+//   filter.go:117-122   drop what the ignore file matches (MatchVulnerability: ID, paths
+//                       against Target then PkgPath, PURLs) into ModifiedFindings;
 //   filter.go:124-130   dedup on "vulnID/pkgName/installed/pkgPath": the greater
 //                       FixedVersion string wins (shouldOverwrite, :345-348), ties keep
 //                       the first seen;
+//   filter.go:51-53     the VEX filter over the deduplicated list;
 //   filter.go:77        sort.Sort(types.BySeverity) (pkg/types/vulnerability.go:41-58):
 //                       PkgName, InstalledVersion, severity descending, VulnerabilityID,
 //                       PkgPath.
-// All strings are replaced by ranks fixed before the launch: the vulnerability ID and
-// output FixedVersion of every advisory (load time, vulninfo.cpp) and the (name, version)
-// of every package within its result (host, once per batch).  Then:
-//   filter_count_dup  pairs of packages whose (result, name, version) repeats (sizes the
-//                  dedup table for them alone; one host synchronisation);
-//   filter_mark    per pair: severity/status/ignore test; duplicates (packages whose
-//                  (result, name, version) repeats) race into an open-addressing table
-//                  with one 64-bit atomicMax of (FixedVersion rank, -package) per key;
-//   filter_select  losers drop out; then the VEX filter (filter.go:51-53, after dedup):
-//                  a survivor whose (package, vulnerability rank) the host-compiled VEX
-//                  suppression list holds (binary search) drops out too; survivors keep
-//                  the BySeverity sort key
-//                  (package rank << (b + 3) | (4 - severity) << b | vulnerability rank,
-//                  b = bits of the DB's vulnerability-rank count);
-//   radix sort     hipcub DeviceRadixSort over (key, pair index), dropped pairs last;
-//   filter_gather  the surviving {package, advisory} pairs in report order.
+// Strings are ranks fixed before the launch: every advisory's vulnerability ID and output
+// FixedVersion (load time, vulninfo.cpp), every package's place in its result's
+// (PkgName, InstalledVersion, PkgPath) order (host, once per batch: FilterPackages).
+//
+// The match list arrives grouped by package (each tile's segment is in package order, a
+// package's advisories in trivy-db Get order), so no sort is needed:
+//   filter_count_dup  pairs of packages whose dedup key repeats (sizes the cross-package
+//                     dedup table; one host synchronisation, only when packages repeat);
+//   filter_mark    per pair: severity / status; ignore rules (one hash-set probe per rule
+//                  kind, smallest precedence wins); run bounds of every package and whether
+//                  its IDs are strictly increasing; packages that repeat race into the
+//                  dedup table with one 64-bit atomicMax of (FixedVersion rank, -package)
+//                  per (dedup key, vulnerability);
+//   filter_select  dedup: the table winner, then - only in runs whose IDs are not strictly
+//                  increasing (one ID from two data sources, Red Hat's per-RHSA rows) - the
+//                  first of the package's own pairs with the greatest FixedVersion; then
+//                  VEX; per package six counters (survivors per severity, ignored), one
+//                  atomic per package run per wave;
+//   scans          survivor offsets of the package groups in perm order, ignored offsets
+//                  in package order;
+//   filter_place   a survivor of a package alone in its group whose run is ID-sorted (the
+//                  bucket order of one trivy-db key: the common case) is placed in O(1):
+//                  group offset + the package's survivors of higher severity + its
+//                  same-severity survivors before it in the run (a block-wide prefix count
+//                  over the 256-pair chunk plus, for the run that enters the chunk, the
+//                  count over its earlier pairs); groups of several packages (same PkgName
+//                  and InstalledVersion) and unsorted runs count keys over the group's runs;
+//                  ignored findings go to their package's offset + their rank in the run
+//                  (detection order).
 // Integer work bound by HBM traffic (pairs, decisions, ranks); no MFMA.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstring>
 
 #include "vulninfo.h"
 
@@ -37,30 +53,50 @@ namespace tvm {
 
 namespace {
 
-constexpr int kFilterBlock = 256;
-constexpr unsigned long long kEmpty = ~0ull;  // sort key of a dropped pair
+constexpr int kBlock = 256;
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;       // key of a dropped pair / no precedence
+constexpr unsigned long long kNoKey = ~0ull;   // empty rule-table slot
+constexpr int kClasses = 6;                    // per-package counters: survivors of severity 0..4, ignored
+constexpr int kIgnClass = 5;
+constexpr int kNoClass = 7;
+constexpr int kChunkBits = 10;                 // packed in-chunk counters (chunk = kBlock pairs)
 
 struct FilterArgs {
   FillDev t;
-  const uint32_t* pkg;  // the ordered match list (package, advisory columns)
+  const uint32_t* pkg;  // the match list (package, advisory columns), grouped by package
   const uint32_t* adv;
-  const uint4* fill;
+  const uint2* side;  // FillInfo's hand-off word per pair: {ID rank, severity index | status << 8}
   uint64_t n;
-  const uint32_t* pkg_rank;     // per package: rank of (result, name, version) in the batch
-  const uint8_t* pkg_dup;       // per package: its (result, name, version) repeats
-  const uint32_t* ignore;       // sorted vulnerability ranks of the ignore file
-  uint32_t n_ignore;
-  const unsigned long long* vex;  // sorted (package << 32 | tag << 31 | vulnerability rank):
-                                  // tag 0 VEX suppression, tag 1 ignore-file pair
-  uint32_t n_vex;
-  uint32_t sev_mask, status_mask;
-  uint32_t id_bits;             // sort key: package rank << (id_bits + 3) | (4 - severity) << id_bits | ID rank
-  unsigned long long* table;    // {key, value} pairs, 2^k entries (dup pairs only)
+  uint32_t n_pkgs;
+  // per package (FilterPackages)
+  const uint32_t* perm;
+  const uint32_t* grp_b;
+  const uint32_t* grp_e;
+  const uint32_t* dkey;
+  const uint32_t* prank;
+  const uint8_t* dup;
+  const uint32_t* pkg_class;
+  // per package, per call
+  uint8_t* uns;        // its run's IDs are not strictly increasing
+  uint32_t* run_b;     // the package's pairs are [run_b, run_e) of the list
+  uint32_t* run_e;
+  uint32_t* cnt;       // kClasses counters per package
+  const uint32_t* off;      // survivor offset of perm position j (exclusive scan)
+  const uint32_t* ign_off;  // ignored offset of package p
+  // per pair
+  uint32_t* mkey;  // after filter_mark: (4 - severity) << id_bits | ID rank, or kEmpty
+  uint32_t* skey;  // after filter_select: the survivors' mkey, else kEmpty
+  uint32_t* ign;   // precedence of the ignoring rule, kEmpty = not ignored
+  uint32_t* mine;  // dedup-table slot of a repeating package's pair
+  // tables
+  const unsigned long long* rules;  // {key, precedence} x 2^k
+  uint64_t rule_mask;
+  uint32_t kinds;  // bit k: rules of tag k exist
+  unsigned long long* table;  // dedup {key + 1, value} x 2^k
   uint64_t table_mask;
-  unsigned long long* sort_key;
-  unsigned long long* mine;     // dup pairs: the table slot filter_mark put the pair's key in
-  uint32_t* idx;
-  unsigned long long* count;
+  uint32_t sev_mask, status_mask, id_bits;
+  uint2* out;      // survivors in report order
+  uint32_t* iout;  // ignored {package, advisory, finding} in detection order
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t h) {
@@ -72,56 +108,70 @@ __device__ __forceinline__ uint64_t mix64(uint64_t h) {
   return h;
 }
 
-// Severity index of a pair after FillInfo (0..4; 5 = a string outside SeverityNames).
-__device__ __forceinline__ uint32_t pair_severity(const FillDev& t, uint4 d, uint4 it) {
-  const uint32_t det = it.y & 0xFFu;  // the detector's package-specific severity (0xFF none)
-  if (d.x == FILL_NOT_FOUND) return (it.z & FI_SEV_SRC) && det < 5 ? det : 0u;  // unchanged; "" -> UNKNOWN
-  const uint32_t code = d.z & 0xFFFFu;
-  if (code < 5) return code;
-  if (code == SEV_KEEP) return det < 5 ? det : 0u;
-  if (code == SEV_RAW) return 5u;  // a DB string that is not a severity name never passes
-  return 0u;                       // SEV_OOR prints UNKNOWN
+// Precedence stored for a rule key (kEmpty when the set lacks it).
+__device__ __forceinline__ uint32_t rule_find(const FilterArgs& a, unsigned long long key) {
+  for (uint64_t s = mix64(key) & a.rule_mask;; s = (s + 1) & a.rule_mask) {
+    const unsigned long long k = a.rules[2 * s];
+    if (k == key) return uint32_t(a.rules[2 * s + 1]);
+    if (k == kNoKey) return kEmpty;
+  }
 }
 
-__global__ __launch_bounds__(kFilterBlock) void filter_mark(FilterArgs a) {
-  const uint64_t stride = uint64_t(gridDim.x) * kFilterBlock;
-  for (uint64_t i = uint64_t(blockIdx.x) * kFilterBlock + threadIdx.x; i < a.n; i += stride) {
-    const uint2 p = make_uint2(a.pkg[i], a.adv[i]);
-    const uint4 d = a.fill[i];
-    const uint4 it = a.t.adv_items[p.y];
-    const uint2 rk = a.t.adv_rank[p.y];
-    const uint32_t sev = pair_severity(a.t, d, it);
-    bool keep = ((a.sev_mask >> sev) & 1u) && !((a.status_mask >> (d.y & 31u)) & 1u);
-    if (keep && a.n_ignore) {  // binary search of the ignore file's vulnerability ranks
-      uint32_t lo = 0, hi = a.n_ignore;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (a.ignore[mid] < rk.x) lo = mid + 1;
-        else hi = mid;
-      }
-      keep = !(lo < a.n_ignore && a.ignore[lo] == rk.x);
+__device__ __forceinline__ unsigned long long rule_key(uint64_t tag, uint32_t subject, uint32_t rank) {
+  return (tag << 62) | (uint64_t(subject) << 32) | rank;
+}
+
+// The counter class of a pair after filter_select.
+__device__ __forceinline__ uint32_t pair_class(const FilterArgs& a, uint32_t skey, uint64_t i) {
+  if (skey != kEmpty) return 4u - (skey >> a.id_bits);
+  if ((a.kinds & 7u) && a.ign[i] != kEmpty) return kIgnClass;
+  return kNoClass;
+}
+
+__global__ __launch_bounds__(kBlock) void rules_insert(const unsigned long long* keys, const uint32_t* prec,
+                                                       uint64_t n, unsigned long long* table, uint64_t mask) {
+  const uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const unsigned long long key = keys[i];
+  for (uint64_t s = mix64(key) & mask;; s = (s + 1) & mask) {
+    const unsigned long long prev = atomicCAS(&table[2 * s], kNoKey, key);
+    if (prev == kNoKey || prev == key) {
+      atomicMin(reinterpret_cast<unsigned int*>(&table[2 * s + 1]), prec[i]);
+      return;
     }
-    if (keep && a.n_vex) {  // ignore findings scoped by PURL: tagged keys, before the dedup
-      const unsigned long long key = (uint64_t(p.x) << 32) | 0x80000000ull | rk.x;
-      uint32_t lo = 0, hi = a.n_vex;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (a.vex[mid] < key) lo = mid + 1;
-        else hi = mid;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void filter_mark(FilterArgs a) {
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride) {
+    const uint32_t p = a.pkg[i];
+    const uint2 sd = a.side[i];
+    const uint32_t vr = sd.x, sev = sd.y & 0xFFu;
+    // run bounds (the list is grouped by package) and whether the run is ID-sorted
+    if (i == 0 || a.pkg[i - 1] != p) a.run_b[p] = uint32_t(i);
+    else if (a.side[i - 1].x >= vr) a.uns[p] = 1;
+    if (i + 1 == a.n || a.pkg[i + 1] != p) a.run_e[p] = uint32_t(i + 1);
+    bool keep = ((a.sev_mask >> sev) & 1u) && !((a.status_mask >> ((sd.y >> 8) & 31u)) & 1u);
+    if (a.kinds & 7u) {  // ignore rules: the smallest precedence is the finding Match returns
+      uint32_t prec = kEmpty;
+      if (keep) {  // severity / status drop first (filter.go:108-114), silently
+        if (a.kinds & (1u << RULE_ALL)) prec = min(prec, rule_find(a, rule_key(RULE_ALL, 0, vr)));
+        if (a.kinds & (1u << RULE_PKG)) prec = min(prec, rule_find(a, rule_key(RULE_PKG, p, vr)));
+        if (a.kinds & (1u << RULE_CLS)) prec = min(prec, rule_find(a, rule_key(RULE_CLS, a.pkg_class[p], vr)));
+        keep = prec == kEmpty;
       }
-      keep = !(lo < a.n_vex && a.vex[lo] == key);
+      a.ign[i] = prec;
     }
-    const unsigned long long key = (uint64_t(a.pkg_rank[p.x]) << 32) | rk.x;
-    const unsigned long long val = (uint64_t(rk.y) << 32) | (0xFFFFFFFFu - p.x);
-    a.idx[i] = uint32_t(i);
-    a.sort_key[i] = keep ? (uint64_t(a.pkg_rank[p.x]) << (a.id_bits + 3)) | (uint64_t(4u - sev) << a.id_bits) | rk.x
-                         : kEmpty;
-    if (keep && a.pkg_dup[p.x]) {  // table entries: {key + 1 (0 = empty), max value}, zeroed
+    a.mkey[i] = keep ? ((4u - sev) << a.id_bits) | vr : kEmpty;
+    if (keep && a.dup[p]) {  // table entries: {key + 1 (0 = empty), max value}, zeroed
+      const unsigned long long key = (uint64_t(a.dkey[p]) << 32) | vr;
+      const unsigned long long val = (uint64_t(a.t.adv_rank[a.adv[i]].y) << 32) | (0xFFFFFFFFu - p);
       for (uint64_t s = mix64(key) & a.table_mask;; s = (s + 1) & a.table_mask) {
         const unsigned long long prev = atomicCAS(&a.table[2 * s], 0ull, key + 1);
         if (prev == 0ull || prev == key + 1) {
           atomicMax(&a.table[2 * s + 1], val);
-          a.mine[i] = s;  // filter_select reads the winner straight from this slot
+          a.mine[i] = uint32_t(s);
           break;
         }
       }
@@ -129,70 +179,186 @@ __global__ __launch_bounds__(kFilterBlock) void filter_mark(FilterArgs a) {
   }
 }
 
-__global__ __launch_bounds__(kFilterBlock) void filter_select(FilterArgs a) {
-  __shared__ uint32_t wsum[kFilterBlock / 64];
-  const uint64_t stride = uint64_t(gridDim.x) * kFilterBlock;
-  uint32_t live_n = 0;  // survivors seen by this lane; one counter atomic per block at the end
-  for (uint64_t i = uint64_t(blockIdx.x) * kFilterBlock + threadIdx.x; i < a.n; i += stride) {
-    bool live = a.sort_key[i] != kEmpty;
-    const uint2 p = make_uint2(a.pkg[i], a.adv[i]);
-    if (live && a.pkg_dup[p.x]) {  // the slot filter_mark inserted this pair's key into
-      const unsigned long long own = (uint64_t(a.t.adv_rank[p.y].y) << 32) | (0xFFFFFFFFu - p.x);
-      if (a.table[2 * a.mine[i] + 1] != own) {
-        a.sort_key[i] = kEmpty;  // another duplicate won (greater FixedVersion, or first seen)
-        live = false;
+__global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  const uint32_t id_mask = (1u << a.id_bits) - 1u;
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t b0 = uint64_t(blockIdx.x) * kBlock; b0 < a.n; b0 += stride) {  // wave-uniform trip count
+    const uint64_t i = b0 + threadIdx.x;
+    const bool valid = i < a.n;
+    uint32_t p = 0xFFFFFFFFu, key = kEmpty;
+    if (valid) {
+      p = a.pkg[i];
+      key = a.mkey[i];
+      if (key != kEmpty) {
+        const uint32_t vr = key & id_mask;
+        const bool dup = a.dup[p], uns = a.uns[p];
+        // the FixedVersion rank is needed only to dedup (repeating packages, unsorted runs)
+        const uint32_t fr = (dup || uns) ? a.t.adv_rank[a.adv[i]].y : 0u;
+        if (dup && a.table[2 * uint64_t(a.mine[i]) + 1] != ((uint64_t(fr) << 32) | (0xFFFFFFFFu - p)))
+          key = kEmpty;  // another package won the (dedup key, ID): greater FixedVersion or first seen
+        if (key != kEmpty && uns) {  // the package's own pairs of this ID: the first with the greatest FixedVersion
+          const uint32_t rb = a.run_b[p], re = a.run_e[p];
+          for (uint32_t j = rb; j < re; j++) {
+            if (j == uint32_t(i)) continue;
+            const uint32_t kj = a.mkey[j];
+            if (kj == kEmpty || (kj & id_mask) != vr) continue;
+            const uint32_t fj = a.t.adv_rank[a.adv[j]].y;
+            if (fj > fr || (fj == fr && j < uint32_t(i))) {
+              key = kEmpty;
+              break;
+            }
+          }
+        }
+        if (key != kEmpty && (a.kinds & (1u << RULE_VEX)) && rule_find(a, rule_key(RULE_VEX, p, vr)) != kEmpty)
+          key = kEmpty;  // VEX: openvex.go:35-40 / cyclonedx.go:56-60 / csaf.go:36-40 drop it
       }
+      a.skey[i] = key;
     }
-    if (live && a.n_vex) {  // VEX: openvex.go:35-40 / cyclonedx.go:56-60 / csaf.go:36-40 drop it
-      const unsigned long long key = (uint64_t(p.x) << 32) | a.t.adv_rank[p.y].x;
-      uint32_t lo = 0, hi = a.n_vex;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (a.vex[mid] < key) lo = mid + 1;
-        else hi = mid;
-      }
-      if (lo < a.n_vex && a.vex[lo] == key) {
-        a.sort_key[i] = kEmpty;
-        live = false;
-      }
-    }
-    live_n += live ? 1u : 0u;
-  }
+    // per-package class counters: the head lane of each package run inside the wave adds
+    // the run's members of every class (the list is grouped by package)
+    const uint32_t cls = valid ? pair_class(a, key, i) : kNoClass;
+    const uint32_t prev_p = __shfl_up(p, 1, 64);
+    const bool head = valid && (lane == 0 || prev_p != p);
+    const unsigned long long heads = __ballot(head);
+    const unsigned long long above = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
+    const uint32_t end = above ? uint32_t(__builtin_ctzll(above)) : 64u;
+    const unsigned long long span = (end == 64 ? ~0ull : ((1ull << end) - 1)) & (~0ull << lane);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) live_n += __shfl_xor(live_n, o, 64);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = live_n;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int w = 0; w < kFilterBlock / 64; w++) t += wsum[w];
-    if (t) atomicAdd(a.count, (unsigned long long)t);
+    for (uint32_t c = 0; c < uint32_t(kClasses); c++) {
+      const unsigned long long m = __ballot(cls == c);
+      if (head && (m & span)) atomicAdd(&a.cnt[uint64_t(p) * kClasses + c], uint32_t(__popcll(m & span)));
+    }
   }
 }
 
-// Pairs whose package's (result, name, version) repeats: the only ones that enter the dedup
-// table, so the table is sized (and cleared) for them alone.
-__global__ __launch_bounds__(kFilterBlock) void filter_count_dup(const uint32_t* pkg, const uint8_t* pkg_dup,
-                                                                 uint64_t n, unsigned long long* count) {
-  __shared__ uint32_t wsum[kFilterBlock / 64];
-  const uint64_t stride = uint64_t(gridDim.x) * kFilterBlock;
+// Number of keys in the run [rb, re) below key (or at most key).
+__device__ __forceinline__ uint32_t count_below(const uint32_t* skey, uint32_t rb, uint32_t re, uint32_t key,
+                                                bool inclusive) {
   uint32_t c = 0;
-  for (uint64_t i = uint64_t(blockIdx.x) * kFilterBlock + threadIdx.x; i < n; i += stride) c += pkg_dup[pkg[i]];
+  for (uint32_t j = rb; j < re; j++) {
+    const uint32_t k = skey[j];
+    c += (k < key || (inclusive && k == key)) ? 1u : 0u;
+  }
+  return c;
+}
+
+// One-hot of a class in the packed in-chunk counters (kChunkBits per class).
+__device__ __forceinline__ unsigned long long one_hot(uint32_t cls) {
+  return cls < uint32_t(kClasses) ? 1ull << (kChunkBits * cls) : 0ull;
+}
+__device__ __forceinline__ uint32_t chunk_field(unsigned long long v, uint32_t cls) {
+  return uint32_t(v >> (kChunkBits * cls)) & ((1u << kChunkBits) - 1u);
+}
+
+__global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
+  __shared__ unsigned long long pre[kBlock];   // exclusive packed class counts of the chunk
+  __shared__ unsigned long long wsum[kBlock / 64];
+  __shared__ uint32_t carry[kClasses];         // classes of the entering run before the chunk
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t c0 = uint64_t(blockIdx.x) * kBlock; c0 < a.n; c0 += stride) {
+    const uint64_t i = c0 + tid;
+    const bool valid = i < a.n;
+    const uint32_t key = valid ? a.skey[i] : kEmpty;
+    const uint32_t cls = valid ? pair_class(a, key, i) : kNoClass;
+    const uint32_t p = valid ? a.pkg[i] : 0u;
+    // block-wide exclusive prefix of the packed one-hot counters (counts <= 256 per field)
+    unsigned long long x = one_hot(cls);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long y = __shfl_up(x, o, 64);
+      if (lane >= uint32_t(o)) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    if (tid < uint32_t(kClasses)) carry[tid] = 0;
+    __syncthreads();
+    unsigned long long wbase = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; w++) wbase += (uint32_t(w) < wave) ? wsum[w] : 0ull;
+    pre[tid] = wbase + x - one_hot(cls);
+    // the run entering the chunk: its classes before c0, counted by the whole block
+    const uint32_t p0 = a.pkg[c0];
+    const uint32_t rb0 = a.run_b[p0];
+    for (uint64_t j = rb0 + tid; j < c0; j += kBlock) {
+      const uint32_t cj = pair_class(a, a.skey[j], j);
+      if (cj < uint32_t(kClasses)) atomicAdd(&carry[cj], 1u);
+    }
+    __syncthreads();
+    if (valid && cls < uint32_t(kClasses)) {
+      const uint32_t rb = a.run_b[p];
+      // pairs of this package before pair i that share its class
+      const uint64_t rs = rb > c0 ? rb : c0;
+      uint32_t before = chunk_field(pre[tid] - pre[rs - c0], cls) + (rb < c0 ? carry[cls] : 0u);
+      if (cls == uint32_t(kIgnClass)) {  // ModifiedFindings in detection order
+        const uint64_t at = uint64_t(a.ign_off[p]) + before;
+        if (at < a.n) {
+          uint32_t* o = a.iout + 3 * at;
+          o[0] = p;
+          o[1] = a.adv[i];
+          o[2] = a.ign[i];
+        }
+      } else {
+        const uint32_t gb = a.grp_b[p], ge = a.grp_e[p];
+        uint32_t r;
+        if (ge - gb == 1 && !a.uns[p]) {  // ID-sorted run alone in its group: severity desc, then run order
+          r = before;
+          for (uint32_t s = cls + 1; s < 5; s++) r += a.cnt[uint64_t(p) * kClasses + s];
+        } else if (ge - gb == 1) {
+          r = count_below(a.skey, rb, a.run_e[p], key, false);
+        } else {  // packages sharing (PkgName, InstalledVersion): merge by (severity, ID, PkgPath)
+          r = 0;
+          const uint32_t pr = a.prank[p];
+          for (uint32_t g = gb; g < ge; g++) {
+            const uint32_t q = a.perm[g];
+            if (q != p) {
+              uint32_t any = 0;
+              for (int s = 0; s < 5; s++) any |= a.cnt[uint64_t(q) * kClasses + s];
+              if (!any) continue;  // no survivors (its run bounds may be stale)
+            }
+            r += count_below(a.skey, a.run_b[q], a.run_e[q], key, q != p && a.prank[q] < pr);
+          }
+        }
+        const uint64_t at = uint64_t(a.off[gb]) + r;
+        if (at < a.n) a.out[at] = make_uint2(p, a.adv[i]);  // always true for a list grouped by package
+      }
+    }
+    __syncthreads();  // pre / carry are rewritten by the next chunk
+  }
+}
+
+// Pairs whose package's dedup key repeats: the only ones that enter the dedup table, so
+// the table is sized (and cleared) for them alone.
+__global__ __launch_bounds__(kBlock) void filter_count_dup(const uint32_t* pkg, const uint8_t* dup, uint64_t n,
+                                                           unsigned long long* count) {
+  __shared__ uint32_t wsum[kBlock / 64];
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  uint32_t c = 0;
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) c += dup[pkg[i]];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t t = 0;
-    for (int w = 0; w < kFilterBlock / 64; w++) t += wsum[w];
+    for (int w = 0; w < kBlock / 64; w++) t += wsum[w];
     if (t) atomicAdd(count, (unsigned long long)t);
   }
 }
 
-__global__ __launch_bounds__(kFilterBlock) void filter_gather(const uint32_t* pkg, const uint32_t* adv,
-                                                              const uint32_t* idx, uint64_t n, uint2* out) {
-  const uint64_t i = uint64_t(blockIdx.x) * kFilterBlock + threadIdx.x;
-  if (i < n) out[i] = make_uint2(pkg[idx[i]], adv[idx[i]]);
-}
+// Scan inputs (one trailing zero, so the exclusive scan's last element is the total):
+// survivors of the package at perm position j / ignored findings of package j.
+struct GroupCount {
+  const uint32_t* perm;  // nullptr: package j itself, ignored findings
+  const uint32_t* cnt;
+  uint32_t n;
+  __host__ __device__ uint32_t operator()(uint32_t j) const {
+    if (j >= n) return 0u;
+    if (!perm) return cnt[uint64_t(j) * kClasses + kIgnClass];
+    const uint32_t* c = cnt + uint64_t(perm[j]) * kClasses;
+    return c[0] + c[1] + c[2] + c[3] + c[4];
+  }
+};
 
 bool ok(hipError_t e, const char* what, std::string& err) {
   if (e == hipSuccess) return true;
@@ -200,54 +366,86 @@ bool ok(hipError_t e, const char* what, std::string& err) {
   return false;
 }
 
+template <class T>
+T* as(void* p) {
+  return static_cast<T*>(p);
+}
+
 }  // namespace
 
+// buffers: 0 perm, 1 grp_b, 2 grp_e, 3 dkey, 4 prank, 5 dup, 6 counters, 7 uns, 8 run_b,
+// 9 run_e, 10 off, 11 ign_off, 12 mkey, 13 skey, 14 ign, 15 mine, 16 dedup table,
+// 17 rule table, 18 rule keys, 19 rule precedences, 20 pkg_class, 21 out pairs,
+// 22 ignored out, 23 scan temp / dup count
 BatchFilter::~BatchFilter() {
   for (void* p : bufs_)
     if (p) (void)hipFree(p);
+  if (pin_) (void)hipHostFree(pin_);
 }
 
-bool BatchFilter::grow(void*& p, uint64_t& cap, uint64_t need, std::string& err) {
-  if (cap >= need) return true;
-  if (p) (void)hipFree(p);
-  p = nullptr;
-  cap = 0;
-  if (!ok(hipMalloc(&p, std::max<uint64_t>(need, 1)), "hipMalloc(filter)", err)) return false;
-  cap = need;
+bool BatchFilter::grow(int i, uint64_t need, std::string& err) {
+  if (caps_[i] >= need && bufs_[i]) return true;
+  if (bufs_[i]) (void)hipFree(bufs_[i]);
+  bufs_[i] = nullptr;
+  caps_[i] = 0;
+  if (!ok(hipMalloc(&bufs_[i], std::max<uint64_t>(need, 16)), "hipMalloc(filter)", err)) return false;
+  caps_[i] = std::max<uint64_t>(need, 16);
   return true;
 }
 
-bool BatchFilter::set_packages(const std::vector<uint32_t>& pkg_rank, const std::vector<uint8_t>& pkg_dup,
-                               std::string& err) {
-  any_dup_ = std::any_of(pkg_dup.begin(), pkg_dup.end(), [](uint8_t x) { return x != 0; });
-  n_pkgs_ = pkg_rank.size();
-  return grow(bufs_[0], caps_[0], pkg_rank.size() * 4, err) && grow(bufs_[1], caps_[1], pkg_dup.size(), err) &&
-         (pkg_rank.empty() || ok(hipMemcpy(bufs_[0], pkg_rank.data(), pkg_rank.size() * 4, hipMemcpyHostToDevice),
-                                 "hipMemcpy(pkg ranks)", err)) &&
-         (pkg_dup.empty() ||
-          ok(hipMemcpy(bufs_[1], pkg_dup.data(), pkg_dup.size(), hipMemcpyHostToDevice), "hipMemcpy(pkg dup)", err));
+bool BatchFilter::set_packages(const FilterPackages& fp, std::string& err) {
+  const uint64_t n = fp.perm.size();
+  n_pkgs_ = 0;
+  if (n >= (1ull << 30)) {
+    err = "filter: at most 2^30 packages per batch";
+    return false;
+  }
+  any_dup_ = std::any_of(fp.dup.begin(), fp.dup.end(), [](uint8_t x) { return x != 0; });
+  const std::vector<uint32_t>* cols[5] = {&fp.perm, &fp.grp_b, &fp.grp_e, &fp.dkey, &fp.prank};
+  for (int k = 0; k < 5; k++)
+    if (cols[k]->size() != n || !grow(k, n * 4, err) ||
+        (n && !ok(hipMemcpy(bufs_[k], cols[k]->data(), n * 4, hipMemcpyHostToDevice), "hipMemcpy(filter packages)",
+                  err)))
+      return false;
+  if (fp.dup.size() != n || !grow(5, n, err) ||
+      (n && !ok(hipMemcpy(bufs_[5], fp.dup.data(), n, hipMemcpyHostToDevice), "hipMemcpy(filter dup)", err)))
+    return false;
+  for (int k : {8, 9, 20})
+    if (!grow(k, n * 4, err)) return false;
+  if (!grow(6, n * 4 * kClasses, err) || !grow(7, n, err) || !grow(10, (n + 1) * 4, err) ||
+      !grow(11, (n + 1) * 4, err))
+    return false;
+  n_pkgs_ = n;
+  return true;
 }
 
-bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv, const uint4* fill, uint64_t n,
-                      const std::vector<uint32_t>& ignore, const std::vector<uint64_t>& vex, uint32_t n_ranks,
-                      uint32_t sev_mask, uint32_t status_mask, hipStream_t st, std::string& err) {
+bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv, const uint2* side, uint64_t n,
+                      const FilterRules& rules, uint32_t n_ranks, uint32_t sev_mask, uint32_t status_mask,
+                      hipStream_t st, std::string& err) {
   n_ = n;
-  survivors_ = 0;
+  survivors_ = ignored_ = 0;
   if (n == 0) return true;
-  if (n > 0xFFFFFFFFull || vex.size() > 0xFFFFFFFFull) {
+  if (n >= 0xFFFFFFFFull) {
     err = "filter: too many pairs";
     return false;
   }
-  const uint32_t blocks = uint32_t(std::min<uint64_t>((n + kFilterBlock - 1) / kFilterBlock, 256ull * 64));
-  uint64_t tcap = 0;  // dedup table: 2^k >= 2 x the pairs that can enter it (load <= 0.5, probes end)
+  uint32_t id_bits = 1;
+  while (id_bits < 32 && (uint64_t(1) << id_bits) < n_ranks) id_bits++;
+  if (id_bits > 29) {
+    err = "filter: more than 2^29 vulnerability IDs";
+    return false;
+  }
+  const uint32_t blocks = uint32_t(std::min<uint64_t>((n + kBlock - 1) / kBlock, 256ull * 64));
+  const uint64_t np = n_pkgs_;
+  // dedup table: 2^k >= 2 x the pairs that can enter it (load <= 0.5, probes end)
+  uint64_t tcap = 0;
   if (any_dup_) {
     unsigned long long dup_n = 0;
-    if (!grow(bufs_[10], caps_[10], 8, err) || !ok(hipMemsetAsync(bufs_[10], 0, 8, st), "memset(dup count)", err))
-      return false;
-    hipLaunchKernelGGL(filter_count_dup, dim3(blocks), dim3(kFilterBlock), 0, st, pkg,
-                       static_cast<const uint8_t*>(bufs_[1]), n, static_cast<unsigned long long*>(bufs_[10]));
+    if (!grow(23, 16, err) || !ok(hipMemsetAsync(bufs_[23], 0, 8, st), "memset(dup count)", err)) return false;
+    hipLaunchKernelGGL(filter_count_dup, dim3(blocks), dim3(kBlock), 0, st, pkg, as<const uint8_t>(bufs_[5]), n,
+                       as<unsigned long long>(bufs_[23]));
     if (!ok(hipGetLastError(), "filter_count_dup", err) ||
-        !ok(hipMemcpyAsync(&dup_n, bufs_[10], 8, hipMemcpyDeviceToHost, st), "D2H dup count", err) ||
+        !ok(hipMemcpyAsync(&dup_n, bufs_[23], 8, hipMemcpyDeviceToHost, st), "D2H dup count", err) ||
         !ok(hipStreamSynchronize(st), "filter sync", err))
       return false;
     if (dup_n) {
@@ -255,97 +453,125 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
       while (tcap < 2 * dup_n) tcap <<= 1;
     }
   }
-  // sort only the key bits in use: package rank (< 2^pkg_bits, never all ones) << (id_bits
-  // + 3) | severity | ID rank (< 2^id_bits); a dropped pair's all-ones key stays the largest
-  uint32_t id_bits = 1;
-  while (id_bits < 32 && (uint64_t(1) << id_bits) < n_ranks) id_bits++;
-  int pkg_bits = 1;
-  while (pkg_bits < 32 && (uint64_t(1) << pkg_bits) <= n_pkgs_) pkg_bits++;
-  const int end_bit = int(id_bits) + 3 + pkg_bits;
-  if (end_bit > 64) {
-    err = "filter: sort key wider than 64 bits";
+  const uint64_t nr = rules.keys.size();
+  uint64_t rcap = 0;
+  if (nr) {
+    rcap = 16;
+    while (rcap < 2 * nr) rcap <<= 1;
+  }
+  const bool has_ign = (rules.kinds & 7u) != 0;
+  using Count = hipcub::CountingInputIterator<uint32_t>;
+  using In = hipcub::TransformInputIterator<uint32_t, GroupCount, Count>;
+  size_t scan_bytes = 0;
+  if (!ok(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, In(Count(0), GroupCount{nullptr, nullptr, 0}),
+                                           static_cast<uint32_t*>(nullptr), int(np + 1), st),
+          "hipcub scan sizing", err))
+    return false;
+  if (!grow(12, n * 4, err) || !grow(13, n * 4, err) || (has_ign && !grow(14, n * 4, err)) ||
+      (tcap && (!grow(15, n * 4, err) || !grow(16, tcap * 16, err))) || (rcap && !grow(17, rcap * 16, err)) ||
+      (nr && (!grow(18, nr * 8, err) || !grow(19, nr * 4, err))) || !grow(21, n * 8, err) ||
+      (has_ign && !grow(22, n * 12, err)) || !grow(23, std::max<uint64_t>(scan_bytes, 16), err))
+    return false;
+  if (!rules.pkg_class.empty() && rules.pkg_class.size() != np) {
+    err = "filter: one class per package";
     return false;
   }
-  size_t sort_bytes = 0;
-  if (!ok(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, static_cast<unsigned long long*>(nullptr),
-                                             static_cast<unsigned long long*>(nullptr), static_cast<uint32_t*>(nullptr),
-                                             static_cast<uint32_t*>(nullptr), int(n), 0, end_bit, st),
-          "hipcub sort sizing", err))
-    return false;
-  // 2 ignore, 3 table, 4 sort keys in, 5 sort keys out, 6 mine, 7 idx in, 8 idx out, 9 temp, 10 count,
-  // 11 out pairs, 12 VEX suppressions
-  if (!grow(bufs_[2], caps_[2], std::max<size_t>(ignore.size(), 1) * 4, err) ||
-      !grow(bufs_[3], caps_[3], std::max<uint64_t>(tcap, 1) * 16, err) || !grow(bufs_[4], caps_[4], n * 8, err) ||
-      !grow(bufs_[5], caps_[5], n * 8, err) || !grow(bufs_[6], caps_[6], n * 8, err) ||
-      !grow(bufs_[7], caps_[7], n * 4, err) || !grow(bufs_[8], caps_[8], n * 4, err) ||
-      !grow(bufs_[9], caps_[9], sort_bytes, err) || !grow(bufs_[10], caps_[10], 8, err) ||
-      !grow(bufs_[11], caps_[11], n * 8, err) || !grow(bufs_[12], caps_[12], std::max<size_t>(vex.size(), 1) * 8, err))
-    return false;
-  if (!vex.empty()) {  // unsorted keys in (bufs_[5], free until the main sort) -> sorted in bufs_[12]
-    size_t vb = 0;
-    if (!ok(hipcub::DeviceRadixSort::SortKeys(nullptr, vb, static_cast<unsigned long long*>(nullptr),
-                                              static_cast<unsigned long long*>(nullptr), int(vex.size()), 0, 64, st),
-            "hipcub vex sort sizing", err) ||
-        !grow(bufs_[9], caps_[9], std::max(sort_bytes, vb), err) ||
-        !grow(bufs_[5], caps_[5], std::max<uint64_t>(n, vex.size()) * 8, err) ||
-        !ok(hipMemcpyAsync(bufs_[5], vex.data(), vex.size() * 8, hipMemcpyHostToDevice, st), "H2D vex", err) ||
-        !ok(hipcub::DeviceRadixSort::SortKeys(bufs_[9], vb, static_cast<unsigned long long*>(bufs_[5]),
-                                              static_cast<unsigned long long*>(bufs_[12]), int(vex.size()), 0, 64, st),
-            "hipcub vex sort", err))
+  if (nr) {  // the rule hash set, built on the device from one pinned upload
+    if (pin_cap_ < nr * 12) {
+      if (pin_) (void)hipHostFree(pin_);
+      pin_ = nullptr;
+      pin_cap_ = 0;
+      if (!ok(hipHostMalloc(&pin_, nr * 12, hipHostMallocDefault), "hipHostMalloc(filter rules)", err)) return false;
+      pin_cap_ = nr * 12;
+    }
+    memcpy(pin_, rules.keys.data(), nr * 8);
+    memcpy(static_cast<char*>(pin_) + nr * 8, rules.prec.data(), nr * 4);
+    if (!ok(hipMemcpyAsync(bufs_[18], pin_, nr * 8, hipMemcpyHostToDevice, st), "H2D rules", err) ||
+        !ok(hipMemcpyAsync(bufs_[19], static_cast<char*>(pin_) + nr * 8, nr * 4, hipMemcpyHostToDevice, st),
+            "H2D rule prec", err) ||
+        !ok(hipMemsetAsync(bufs_[17], 0xFF, rcap * 16, st), "memset(rules)", err))
       return false;
+    hipLaunchKernelGGL(rules_insert, dim3(uint32_t((nr + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                       as<const unsigned long long>(bufs_[18]), as<const uint32_t>(bufs_[19]), nr,
+                       as<unsigned long long>(bufs_[17]), rcap - 1);
+    if (!ok(hipGetLastError(), "rules_insert", err)) return false;
   }
-  if (!ignore.empty() &&
-      !ok(hipMemcpyAsync(bufs_[2], ignore.data(), ignore.size() * 4, hipMemcpyHostToDevice, st), "H2D ignore", err))
+  if (!rules.pkg_class.empty() &&
+      !ok(hipMemcpyAsync(bufs_[20], rules.pkg_class.data(), np * 4, hipMemcpyHostToDevice, st), "H2D classes", err))
     return false;
-  if (tcap && !ok(hipMemsetAsync(bufs_[3], 0, tcap * 16, st), "memset(filter table)", err)) return false;
-  if (!ok(hipMemsetAsync(bufs_[10], 0, 8, st), "memset(count)", err)) return false;
+  if ((tcap && !ok(hipMemsetAsync(bufs_[16], 0, tcap * 16, st), "memset(dedup table)", err)) ||
+      !ok(hipMemsetAsync(bufs_[6], 0, np * 4 * kClasses, st), "memset(counters)", err) ||
+      !ok(hipMemsetAsync(bufs_[7], 0, np, st), "memset(uns)", err))
+    return false;
   FilterArgs a{};
   a.t = t;
   a.pkg = pkg;
   a.adv = adv;
-  a.fill = fill;
+  a.side = side;
   a.n = n;
-  a.pkg_rank = static_cast<const uint32_t*>(bufs_[0]);
-  a.pkg_dup = static_cast<const uint8_t*>(bufs_[1]);
-  a.ignore = static_cast<const uint32_t*>(bufs_[2]);
-  a.n_ignore = uint32_t(ignore.size());
-  a.vex = static_cast<const unsigned long long*>(bufs_[12]);
-  a.n_vex = uint32_t(vex.size());
-  a.sev_mask = sev_mask;
-  a.id_bits = id_bits;
-  a.status_mask = status_mask;
-  a.table = static_cast<unsigned long long*>(bufs_[3]);
+  a.n_pkgs = uint32_t(np);
+  a.perm = as<const uint32_t>(bufs_[0]);
+  a.grp_b = as<const uint32_t>(bufs_[1]);
+  a.grp_e = as<const uint32_t>(bufs_[2]);
+  a.dkey = as<const uint32_t>(bufs_[3]);
+  a.prank = as<const uint32_t>(bufs_[4]);
+  a.dup = as<const uint8_t>(bufs_[5]);
+  a.pkg_class = as<const uint32_t>(bufs_[20]);
+  a.cnt = as<uint32_t>(bufs_[6]);
+  a.uns = as<uint8_t>(bufs_[7]);
+  a.run_b = as<uint32_t>(bufs_[8]);
+  a.run_e = as<uint32_t>(bufs_[9]);
+  a.off = as<const uint32_t>(bufs_[10]);
+  a.ign_off = as<const uint32_t>(bufs_[11]);
+  a.mkey = as<uint32_t>(bufs_[12]);
+  a.skey = as<uint32_t>(bufs_[13]);
+  a.ign = as<uint32_t>(bufs_[14]);
+  a.mine = as<uint32_t>(bufs_[15]);
+  a.rules = as<const unsigned long long>(bufs_[17]);
+  a.rule_mask = rcap ? rcap - 1 : 0;
+  a.kinds = rules.kinds;
+  a.table = as<unsigned long long>(bufs_[16]);
   a.table_mask = tcap ? tcap - 1 : 0;
-  a.sort_key = static_cast<unsigned long long*>(bufs_[4]);
-  a.mine = static_cast<unsigned long long*>(bufs_[6]);
-  a.idx = static_cast<uint32_t*>(bufs_[7]);
-  a.count = static_cast<unsigned long long*>(bufs_[10]);
-  hipLaunchKernelGGL(filter_mark, dim3(blocks), dim3(kFilterBlock), 0, st, a);
-  hipLaunchKernelGGL(filter_select, dim3(blocks), dim3(kFilterBlock), 0, st, a);
-  if (!ok(hipGetLastError(), "filter launch", err)) return false;
-  if (!ok(hipcub::DeviceRadixSort::SortPairs(bufs_[9], sort_bytes, a.sort_key,
-                                             static_cast<unsigned long long*>(bufs_[5]), a.idx,
-                                             static_cast<uint32_t*>(bufs_[8]), int(n), 0, end_bit, st),
-          "hipcub sort", err))
+  a.sev_mask = sev_mask;
+  a.status_mask = status_mask;
+  a.id_bits = id_bits;
+  a.out = as<uint2>(bufs_[21]);
+  a.iout = as<uint32_t>(bufs_[22]);
+  hipLaunchKernelGGL(filter_mark, dim3(blocks), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(filter_select, dim3(blocks), dim3(kBlock), 0, st, a);
+  if (!ok(hipGetLastError(), "filter launch", err) ||
+      !ok(hipcub::DeviceScan::ExclusiveSum(bufs_[23], scan_bytes, In(Count(0), GroupCount{a.perm, a.cnt, uint32_t(np)}),
+                                           as<uint32_t>(bufs_[10]), int(np + 1), st),
+          "hipcub scan", err) ||
+      (has_ign &&
+       !ok(hipcub::DeviceScan::ExclusiveSum(bufs_[23], scan_bytes, In(Count(0), GroupCount{nullptr, a.cnt, uint32_t(np)}),
+                                            as<uint32_t>(bufs_[11]), int(np + 1), st),
+           "hipcub scan", err)))
     return false;
-  unsigned long long cnt = 0;
-  if (!ok(hipMemcpyAsync(&cnt, bufs_[10], 8, hipMemcpyDeviceToHost, st), "D2H count", err) ||
+  hipLaunchKernelGGL(filter_place, dim3(blocks), dim3(kBlock), 0, st, a);
+  uint32_t tot[2] = {0, 0};
+  if (!ok(hipGetLastError(), "filter_place", err) ||
+      !ok(hipMemcpyAsync(&tot[0], as<uint32_t>(bufs_[10]) + np, 4, hipMemcpyDeviceToHost, st), "D2H kept", err) ||
+      (has_ign && !ok(hipMemcpyAsync(&tot[1], as<uint32_t>(bufs_[11]) + np, 4, hipMemcpyDeviceToHost, st),
+                      "D2H ignored", err)) ||
       !ok(hipStreamSynchronize(st), "filter sync", err))
     return false;
-  survivors_ = cnt;
-  if (cnt) {
-    hipLaunchKernelGGL(filter_gather, dim3(uint32_t((cnt + kFilterBlock - 1) / kFilterBlock)), dim3(kFilterBlock), 0,
-                       st, pkg, adv, static_cast<const uint32_t*>(bufs_[8]), uint64_t(cnt),
-                       static_cast<uint2*>(bufs_[11]));
-    if (!ok(hipGetLastError(), "filter gather", err)) return false;
-  }
+  survivors_ = tot[0];
+  ignored_ = tot[1];
   return true;
 }
 
 bool BatchFilter::fetch(std::vector<uint2>& out, hipStream_t st, std::string& err) {
   out.assign(survivors_, make_uint2(0, 0));
   if (!survivors_) return true;
-  return ok(hipMemcpyAsync(out.data(), bufs_[11], survivors_ * 8, hipMemcpyDeviceToHost, st), "D2H filtered", err) &&
+  return ok(hipMemcpyAsync(out.data(), bufs_[21], survivors_ * 8, hipMemcpyDeviceToHost, st), "D2H filtered", err) &&
+         ok(hipStreamSynchronize(st), "filter sync", err);
+}
+
+bool BatchFilter::fetch_ignored(std::vector<uint32_t>& out3, hipStream_t st, std::string& err) {
+  out3.assign(ignored_ * 3, 0);
+  if (!ignored_) return true;
+  return ok(hipMemcpyAsync(out3.data(), bufs_[22], ignored_ * 12, hipMemcpyDeviceToHost, st), "D2H ignored", err) &&
          ok(hipStreamSynchronize(st), "filter sync", err);
 }
 

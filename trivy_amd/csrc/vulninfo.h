@@ -154,6 +154,19 @@ struct FillDev {
   uint32_t n_advs;
   uint32_t ghsa, nvd;
 };
+// Severity index of a batch pair after FillInfo, as filterVulnerabilities reads it (0..4;
+// 5 = a DB string outside SeverityNames, which no severity filter passes).  d = the fill
+// decision, it = the advisory's item.
+__host__ __device__ inline uint32_t fill_pair_severity(uint4 d, uint4 it) {
+  const uint32_t det = it.y & 0xFFu;  // the detector's package-specific severity (0xFF none)
+  if (d.x == FILL_NOT_FOUND) return (it.z & FI_SEV_SRC) && det < 5 ? det : 0u;  // unchanged; "" -> UNKNOWN
+  const uint32_t code = d.z & 0xFFFFu;
+  if (code < 5) return code;
+  if (code == SEV_KEEP) return det < 5 ? det : 0u;
+  if (code == SEV_RAW) return 5u;
+  return 0u;  // SEV_OOR prints UNKNOWN
+}
+
 class FillEngine {
  public:
   ~FillEngine();
@@ -163,8 +176,10 @@ class FillEngine {
                 std::string& err);
   // Batch path: decisions for the device match pairs {pkg, adv} (resolved records), on
   // `stream`; the pair count is read from n_dev on the device (at most cap pairs).
-  bool launch_pairs(const uint32_t* adv, const unsigned long long* n_dev, uint64_t cap, uint4* out, hipStream_t stream,
-                    std::string& err);
+  // side (optional): per pair the filter's hand-off word {vulnerability-ID rank, severity
+  // index | status << 8} (filter.hip reads it instead of the 16-B decision).
+  bool launch_pairs(const uint32_t* adv, const unsigned long long* n_dev, uint64_t cap, uint4* out, uint2* side,
+                    hipStream_t stream, std::string& err);
   uint64_t table_bytes() const { return table_bytes_; }
   const VulnTable& table() const { return *t_; }
   // Algorithmic HBM bytes of one batch-path launch over these pairs (host copy).
@@ -182,29 +197,53 @@ class FillEngine {
 };
 
 // result.Filter over a batch's device match list (filter.hip).
+// Per package, fixed once per batch (host): the report order of the packages and the groups
+// the filter compares them in.
+struct FilterPackages {
+  std::vector<uint32_t> perm;          // packages by (result, PkgName, InstalledVersion, PkgPath, index)
+  std::vector<uint32_t> grp_b, grp_e;  // per package: perm range of its (result, PkgName, InstalledVersion)
+  std::vector<uint32_t> dkey;          // per package: id of its (result, PkgName, InstalledVersion, PkgPath)
+  std::vector<uint32_t> prank;         // per package: rank of its PkgPath inside its group
+  std::vector<uint8_t> dup;            // per package: another package shares its dkey
+};
+
+// Host-compiled rules of one call: hash-set entries key = tag << 62 | subject << 32 |
+// vulnerability rank (subject: package or class, < 2^30), value = precedence.
+enum : uint64_t { RULE_ALL = 0, RULE_PKG = 1, RULE_CLS = 2, RULE_VEX = 3 };
+struct FilterRules {
+  std::vector<uint64_t> keys;
+  std::vector<uint32_t> prec;
+  std::vector<uint32_t> pkg_class;  // per package (empty: no class rules)
+  uint32_t kinds = 0;               // bit k: some rule of tag k
+};
+
 class BatchFilter {
  public:
   ~BatchFilter();
-  // Per package: rank of (result, name, version) in result-major byte order (packages
-  // sharing all three share a rank) and whether that triple repeats.
-  bool set_packages(const std::vector<uint32_t>& pkg_rank, const std::vector<uint8_t>& pkg_dup, std::string& err);
+  bool set_packages(const FilterPackages& fp, std::string& err);
   bool has_packages() const { return n_pkgs_ != 0; }
+  void reset_packages() { n_pkgs_ = 0; }
   // Filters the n device pairs (with their FillInfo decisions) on `st`; synchronises once
-  // to learn the survivor count.  ignore: sorted vulnerability ranks (VulnTable::vuln_rank);
-  // vex: sorted (package << 32 | vulnerability rank) findings a VEX document drops.
-  bool run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv, const uint4* fill, uint64_t n, const std::vector<uint32_t>& ignore,
-           const std::vector<uint64_t>& vex, uint32_t n_ranks, uint32_t sev_mask, uint32_t status_mask,
-           hipStream_t st, std::string& err);
+  // (twice when packages repeat) to learn the counts.
+  bool run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv, const uint2* side, uint64_t n,
+           const FilterRules& rules, uint32_t n_ranks, uint32_t sev_mask, uint32_t status_mask, hipStream_t st,
+           std::string& err);
   uint64_t survivors() const { return survivors_; }
+  uint64_t ignored() const { return ignored_; }
   // The surviving {package, advisory} pairs in report order.
   bool fetch(std::vector<uint2>& out, hipStream_t st, std::string& err);
+  // The ignored {package, advisory, precedence} in detection order.
+  bool fetch_ignored(std::vector<uint32_t>& out3, hipStream_t st, std::string& err);
 
  private:
-  void* bufs_[13] = {};
-  uint64_t caps_[13] = {};
-  uint64_t n_ = 0, survivors_ = 0, n_pkgs_ = 0;
+  enum { kBufs = 24 };
+  void* bufs_[kBufs] = {};
+  uint64_t caps_[kBufs] = {};
+  uint64_t n_ = 0, survivors_ = 0, ignored_ = 0, n_pkgs_ = 0;
   bool any_dup_ = false;
-  bool grow(void*& p, uint64_t& cap, uint64_t need, std::string& err);
+  void* pin_ = nullptr;  // pinned staging of the per-call rule upload
+  uint64_t pin_cap_ = 0;
+  bool grow(int i, uint64_t need, std::string& err);
 };
 
 }  // namespace tvm
