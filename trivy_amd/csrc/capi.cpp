@@ -994,43 +994,48 @@ int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint
   const VulnTable& vt = e->fill->table();
   const uint64_t n_pkgs = uint64_t(tvm_batch_size(b));
   FilterRules rules;
-  // each distinct ID ranked once; IDs unknown to the DB cannot name a detected
-  // vulnerability, so their rules drop out here
-  auto ranks = [&](const tvm_str* ids, size_t k, const uint32_t* given) {
-    std::vector<uint32_t> r(k);
+  // each distinct ID ranked once (or by the caller, tvm_vuln_rank_many); IDs unknown to the
+  // DB cannot name a detected vulnerability, so their rules drop out on the device
+  auto ranks = [&](std::vector<uint32_t>& r, const tvm_str* ids, size_t k, const uint32_t* given) {
+    r.resize(k);
     for (size_t i = 0; i < k; i++) r[i] = given ? given[i] : vt.vuln_rank(sv(ids[i]));
-    return r;
   };
-  bool bad = false;
-  auto add = [&](uint64_t tag, uint32_t subject, uint32_t id_index, const std::vector<uint32_t>& rk, uint32_t prec) {
-    if (id_index >= rk.size() || subject >= (1u << 30)) {
-      bad = true;
-      return;
-    }
-    if (rk[id_index] == 0xFFFFFFFFu) return;
-    rules.keys.push_back((tag << 62) | (uint64_t(subject) << 32) | rk[id_index]);
-    rules.prec.push_back(prec);
+  // bounds of the caller's arrays: subject < limit, ID index < ID count (vectorisable scans)
+  auto below = [](const uint32_t* v, size_t k, uint64_t limit) {
+    uint32_t mx = 0;
+    for (size_t i = 0; i < k; i++) mx = std::max(mx, v[i]);
+    return k == 0 || mx < limit;
+  };
+  bool good = true;
+  auto list = [&](uint64_t tag, const uint32_t* subject, uint64_t subject_limit, const uint32_t* id, const uint32_t* prec,
+                  size_t k, int table) {
+    if (!k) return;
+    good &= below(id, k, rules.rank[table].size()) && (!subject || below(subject, k, subject_limit));
+    RuleList& l = rules.lists[rules.n_lists++];
+    l.tag = tag;
+    l.subject = subject;
+    l.id = id;
+    l.prec = prec;
+    l.n = k;
+    l.table = table;
     rules.kinds |= 1u << tag;
   };
+  const uint64_t lim = std::min<uint64_t>(n_pkgs, 1ull << 30);
   if (ig) {
-    const std::vector<uint32_t> rk = ranks(ig->ids, ig->n_ids, ig->id_ranks);
-    for (size_t i = 0; i < ig->n_all; i++) add(RULE_ALL, 0, ig->all_id[i], rk, ig->all_prec[i]);
-    for (size_t i = 0; i < ig->n_pkg; i++)
-      if (ig->pkg_pkg[i] >= n_pkgs) bad = true;
-      else add(RULE_PKG, ig->pkg_pkg[i], ig->pkg_id[i], rk, ig->pkg_prec[i]);
-    for (size_t i = 0; i < ig->n_cls; i++) add(RULE_CLS, ig->cls_class[i], ig->cls_id[i], rk, ig->cls_prec[i]);
-    if (rules.kinds & (1u << RULE_CLS)) {
-      rules.pkg_class.assign(ig->pkg_class, ig->pkg_class + n_pkgs);
-      for (uint32_t c : rules.pkg_class) bad |= c >= (1u << 30);
+    ranks(rules.rank[0], ig->ids, ig->n_ids, ig->id_ranks);
+    list(RULE_ALL, nullptr, 0, ig->all_id, ig->all_prec, ig->n_all, 0);
+    list(RULE_PKG, ig->pkg_pkg, lim, ig->pkg_id, ig->pkg_prec, ig->n_pkg, 0);
+    list(RULE_CLS, ig->cls_class, 1ull << 30, ig->cls_id, ig->cls_prec, ig->n_cls, 0);
+    if (ig->n_cls) {
+      rules.pkg_class = ig->pkg_class;
+      good &= below(ig->pkg_class, n_pkgs, 1ull << 30);
     }
   }
   if (o->n_vex) {
-    const std::vector<uint32_t> rk = ranks(o->vex_ids, o->n_vex_ids, o->vex_id_ranks);
-    for (size_t i = 0; i < o->n_vex; i++)
-      if (o->vex_pkgs[i] >= n_pkgs) bad = true;
-      else add(RULE_VEX, o->vex_pkgs[i], o->vex_id_index[i], rk, 0);
+    ranks(rules.rank[1], o->vex_ids, o->n_vex_ids, o->vex_id_ranks);
+    list(RULE_VEX, o->vex_pkgs, lim, o->vex_id_index, nullptr, o->n_vex, 1);
   }
-  if (bad) {
+  if (!good) {
     set_err(err, errlen, "tvm_match_filter: rule / VEX package, class or ID index out of range");
     return TVM_EINVAL;
   }

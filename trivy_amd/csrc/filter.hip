@@ -60,6 +60,14 @@ constexpr int kClasses = 6;                    // per-package counters: survivor
 constexpr int kIgnClass = 5;
 constexpr int kNoClass = 7;
 constexpr int kChunkBits = 10;                 // packed in-chunk counters (chunk = kBlock pairs)
+// Per-package flag bits: static (set_packages) FL_DUP / FL_SINGLE, per call FL_UNS (mark),
+// FL_PKG / FL_VEX (rules_insert: the package has per-package rules, probe only those).
+enum : uint32_t { FL_DUP = 1, FL_UNS = 2, FL_PKG = 4, FL_VEX = 8, FL_SINGLE = 16 };
+
+// Sets flag bits of package p in a byte array padded to whole words (word atomics).
+__device__ __forceinline__ void set_flag(uint8_t* fl, uint32_t p, uint32_t bits) {
+  atomicOr(reinterpret_cast<unsigned int*>(fl + (p & ~3u)), bits << (8 * (p & 3u)));
+}
 
 struct FilterArgs {
   FillDev t;
@@ -74,10 +82,10 @@ struct FilterArgs {
   const uint32_t* grp_e;
   const uint32_t* dkey;
   const uint32_t* prank;
-  const uint8_t* dup;
+  const uint8_t* dup;   // static flags: FL_DUP | FL_SINGLE
   const uint32_t* pkg_class;
   // per package, per call
-  uint8_t* uns;        // its run's IDs are not strictly increasing
+  uint8_t* fl;         // per-call flags (FL_*), seeded from the static ones
   uint32_t* run_b;     // the package's pairs are [run_b, run_e) of the list
   uint32_t* run_e;
   uint32_t* cnt;       // kClasses counters per package
@@ -128,15 +136,35 @@ __device__ __forceinline__ uint32_t pair_class(const FilterArgs& a, uint32_t ske
   return kNoClass;
 }
 
-__global__ __launch_bounds__(kBlock) void rules_insert(const unsigned long long* keys, const uint32_t* prec,
-                                                       uint64_t n, unsigned long long* table, uint64_t mask) {
-  const uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
-  if (i >= n) return;
-  const unsigned long long key = keys[i];
+// Rule lists as uploaded: entry e of list k is (subject, ID index, precedence).
+struct RuleDev {
+  const uint32_t* subject[4];
+  const uint32_t* id[4];
+  const uint32_t* prec[4];
+  const uint32_t* rank[4];
+  uint64_t end[4];  // cumulative entry counts
+  uint32_t tag[4];
+  int n_lists;
+};
+
+__global__ __launch_bounds__(kBlock) void rules_insert(RuleDev r, unsigned long long* table, uint64_t mask,
+                                                       uint8_t* fl) {
+  const uint64_t g = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  int k = 0;
+  while (k < r.n_lists && g >= r.end[k]) k++;
+  if (k == r.n_lists) return;
+  const uint64_t e = g - (k ? r.end[k - 1] : 0);
+  const uint32_t rank = r.rank[k][r.id[k][e]];
+  if (rank == kEmpty) return;  // an ID no advisory has: nothing to match
+  const uint32_t subject = r.subject[k] ? r.subject[k][e] : 0u;
+  const uint32_t prec = r.prec[k] ? r.prec[k][e] : 0u;
+  const unsigned long long key = rule_key(r.tag[k], subject, rank);
+  if (r.tag[k] == RULE_PKG || r.tag[k] == RULE_VEX)  // flag the subject package: probe only those
+    set_flag(fl, subject, r.tag[k] == RULE_PKG ? FL_PKG : FL_VEX);
   for (uint64_t s = mix64(key) & mask;; s = (s + 1) & mask) {
     const unsigned long long prev = atomicCAS(&table[2 * s], kNoKey, key);
     if (prev == kNoKey || prev == key) {
-      atomicMin(reinterpret_cast<unsigned int*>(&table[2 * s + 1]), prec[i]);
+      atomicMin(reinterpret_cast<unsigned int*>(&table[2 * s + 1]), prec);
       return;
     }
   }
@@ -150,21 +178,21 @@ __global__ __launch_bounds__(kBlock) void filter_mark(FilterArgs a) {
     const uint32_t vr = sd.x, sev = sd.y & 0xFFu;
     // run bounds (the list is grouped by package) and whether the run is ID-sorted
     if (i == 0 || a.pkg[i - 1] != p) a.run_b[p] = uint32_t(i);
-    else if (a.side[i - 1].x >= vr) a.uns[p] = 1;
+    else if (a.side[i - 1].x >= vr && !(a.fl[p] & FL_UNS)) set_flag(a.fl, p, FL_UNS);
     if (i + 1 == a.n || a.pkg[i + 1] != p) a.run_e[p] = uint32_t(i + 1);
     bool keep = ((a.sev_mask >> sev) & 1u) && !((a.status_mask >> ((sd.y >> 8) & 31u)) & 1u);
     if (a.kinds & 7u) {  // ignore rules: the smallest precedence is the finding Match returns
       uint32_t prec = kEmpty;
       if (keep) {  // severity / status drop first (filter.go:108-114), silently
         if (a.kinds & (1u << RULE_ALL)) prec = min(prec, rule_find(a, rule_key(RULE_ALL, 0, vr)));
-        if (a.kinds & (1u << RULE_PKG)) prec = min(prec, rule_find(a, rule_key(RULE_PKG, p, vr)));
+        if ((a.kinds & (1u << RULE_PKG)) && (a.fl[p] & FL_PKG)) prec = min(prec, rule_find(a, rule_key(RULE_PKG, p, vr)));
         if (a.kinds & (1u << RULE_CLS)) prec = min(prec, rule_find(a, rule_key(RULE_CLS, a.pkg_class[p], vr)));
         keep = prec == kEmpty;
       }
       a.ign[i] = prec;
     }
     a.mkey[i] = keep ? ((4u - sev) << a.id_bits) | vr : kEmpty;
-    if (keep && a.dup[p]) {  // table entries: {key + 1 (0 = empty), max value}, zeroed
+    if (keep && (a.dup[p] & FL_DUP)) {  // table entries: {key + 1 (0 = empty), max value}, zeroed
       const unsigned long long key = (uint64_t(a.dkey[p]) << 32) | vr;
       const unsigned long long val = (uint64_t(a.t.adv_rank[a.adv[i]].y) << 32) | (0xFFFFFFFFu - p);
       for (uint64_t s = mix64(key) & a.table_mask;; s = (s + 1) & a.table_mask) {
@@ -192,7 +220,8 @@ __global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
       key = a.mkey[i];
       if (key != kEmpty) {
         const uint32_t vr = key & id_mask;
-        const bool dup = a.dup[p], uns = a.uns[p];
+        const uint32_t f = a.fl[p];
+        const bool dup = f & FL_DUP, uns = f & FL_UNS;
         // the FixedVersion rank is needed only to dedup (repeating packages, unsorted runs)
         const uint32_t fr = (dup || uns) ? a.t.adv_rank[a.adv[i]].y : 0u;
         if (dup && a.table[2 * uint64_t(a.mine[i]) + 1] != ((uint64_t(fr) << 32) | (0xFFFFFFFFu - p)))
@@ -210,7 +239,8 @@ __global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
             }
           }
         }
-        if (key != kEmpty && (a.kinds & (1u << RULE_VEX)) && rule_find(a, rule_key(RULE_VEX, p, vr)) != kEmpty)
+        if (key != kEmpty && (a.kinds & (1u << RULE_VEX)) && (f & FL_VEX) &&
+            rule_find(a, rule_key(RULE_VEX, p, vr)) != kEmpty)
           key = kEmpty;  // VEX: openvex.go:35-40 / cyclonedx.go:56-60 / csaf.go:36-40 drop it
       }
       a.skey[i] = key;
@@ -255,6 +285,8 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
   __shared__ unsigned long long pre[kBlock];   // exclusive packed class counts of the chunk
   __shared__ unsigned long long wsum[kBlock / 64];
   __shared__ uint32_t carry[kClasses];         // classes of the entering run before the chunk
+  __shared__ uint32_t base[kBlock][kClasses];  // at a package's first lane in the chunk: its bases
+  __shared__ uint32_t pflag[kBlock];           //   and flags (loaded once per package and chunk)
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
   for (uint64_t c0 = uint64_t(blockIdx.x) * kBlock; c0 < a.n; c0 += stride) {
@@ -263,6 +295,8 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
     const uint32_t key = valid ? a.skey[i] : kEmpty;
     const uint32_t cls = valid ? pair_class(a, key, i) : kNoClass;
     const uint32_t p = valid ? a.pkg[i] : 0u;
+    const uint32_t rb = valid ? a.run_b[p] : 0u;
+    const uint64_t rs = rb > c0 ? rb : c0;  // the package's first pair in this chunk
     // block-wide exclusive prefix of the packed one-hot counters (counts <= 256 per field)
     unsigned long long x = one_hot(cls);
 #pragma unroll
@@ -272,26 +306,39 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
     }
     if (lane == 63) wsum[wave] = x;
     if (tid < uint32_t(kClasses)) carry[tid] = 0;
+    if (valid && i == rs) {  // the package's first lane: its placement bases, once
+      const uint32_t f = a.fl[p];
+      pflag[tid] = f;
+      if ((f & (FL_SINGLE | FL_UNS)) == FL_SINGLE) {
+        // ID-sorted run alone in its group: severity desc, then run order
+        uint32_t acc = a.off[a.grp_b[p]];
+        const uint32_t* c = a.cnt + uint64_t(p) * kClasses;
+        for (int sv = 4; sv >= 0; sv--) {
+          base[tid][sv] = acc;
+          acc += c[sv];
+        }
+      }
+      if (a.kinds & 7u) base[tid][kIgnClass] = a.ign_off[p];
+    }
     __syncthreads();
     unsigned long long wbase = 0;
 #pragma unroll
     for (int w = 0; w < kBlock / 64; w++) wbase += (uint32_t(w) < wave) ? wsum[w] : 0ull;
     pre[tid] = wbase + x - one_hot(cls);
     // the run entering the chunk: its classes before c0, counted by the whole block
-    const uint32_t p0 = a.pkg[c0];
-    const uint32_t rb0 = a.run_b[p0];
+    const uint32_t rb0 = a.run_b[a.pkg[c0]];
     for (uint64_t j = rb0 + tid; j < c0; j += kBlock) {
       const uint32_t cj = pair_class(a, a.skey[j], j);
       if (cj < uint32_t(kClasses)) atomicAdd(&carry[cj], 1u);
     }
     __syncthreads();
     if (valid && cls < uint32_t(kClasses)) {
-      const uint32_t rb = a.run_b[p];
+      const uint32_t h = uint32_t(rs - c0);
       // pairs of this package before pair i that share its class
-      const uint64_t rs = rb > c0 ? rb : c0;
-      uint32_t before = chunk_field(pre[tid] - pre[rs - c0], cls) + (rb < c0 ? carry[cls] : 0u);
+      const uint32_t before = chunk_field(pre[tid] - pre[h], cls) + (rb < c0 ? carry[cls] : 0u);
+      const uint32_t f = pflag[h];
       if (cls == uint32_t(kIgnClass)) {  // ModifiedFindings in detection order
-        const uint64_t at = uint64_t(a.ign_off[p]) + before;
+        const uint64_t at = uint64_t(base[h][kIgnClass]) + before;
         if (at < a.n) {
           uint32_t* o = a.iout + 3 * at;
           o[0] = p;
@@ -299,31 +346,32 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
           o[2] = a.ign[i];
         }
       } else {
-        const uint32_t gb = a.grp_b[p], ge = a.grp_e[p];
-        uint32_t r;
-        if (ge - gb == 1 && !a.uns[p]) {  // ID-sorted run alone in its group: severity desc, then run order
-          r = before;
-          for (uint32_t s = cls + 1; s < 5; s++) r += a.cnt[uint64_t(p) * kClasses + s];
-        } else if (ge - gb == 1) {
-          r = count_below(a.skey, rb, a.run_e[p], key, false);
-        } else {  // packages sharing (PkgName, InstalledVersion): merge by (severity, ID, PkgPath)
-          r = 0;
-          const uint32_t pr = a.prank[p];
-          for (uint32_t g = gb; g < ge; g++) {
-            const uint32_t q = a.perm[g];
-            if (q != p) {
-              uint32_t any = 0;
-              for (int s = 0; s < 5; s++) any |= a.cnt[uint64_t(q) * kClasses + s];
-              if (!any) continue;  // no survivors (its run bounds may be stale)
+        uint64_t at;
+        if ((f & (FL_SINGLE | FL_UNS)) == FL_SINGLE) {
+          at = uint64_t(base[h][cls]) + before;
+        } else {
+          const uint32_t gb = a.grp_b[p], ge = a.grp_e[p];
+          uint32_t r = 0;
+          if (ge - gb == 1) {
+            r = count_below(a.skey, rb, a.run_e[p], key, false);
+          } else {  // packages sharing (PkgName, InstalledVersion): merge by (severity, ID, PkgPath)
+            const uint32_t pr = a.prank[p];
+            for (uint32_t g = gb; g < ge; g++) {
+              const uint32_t q = a.perm[g];
+              if (q != p) {
+                uint32_t any = 0;
+                for (int sv = 0; sv < 5; sv++) any |= a.cnt[uint64_t(q) * kClasses + sv];
+                if (!any) continue;  // no survivors (its run bounds may be stale)
+              }
+              r += count_below(a.skey, a.run_b[q], a.run_e[q], key, q != p && a.prank[q] < pr);
             }
-            r += count_below(a.skey, a.run_b[q], a.run_e[q], key, q != p && a.prank[q] < pr);
           }
+          at = uint64_t(a.off[gb]) + r;
         }
-        const uint64_t at = uint64_t(a.off[gb]) + r;
         if (at < a.n) a.out[at] = make_uint2(p, a.adv[i]);  // always true for a list grouped by package
       }
     }
-    __syncthreads();  // pre / carry are rewritten by the next chunk
+    __syncthreads();  // pre / carry / base are rewritten by the next chunk
   }
 }
 
@@ -334,7 +382,7 @@ __global__ __launch_bounds__(kBlock) void filter_count_dup(const uint32_t* pkg, 
   __shared__ uint32_t wsum[kBlock / 64];
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
   uint32_t c = 0;
-  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) c += dup[pkg[i]];
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) c += dup[pkg[i]] & FL_DUP;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
@@ -373,7 +421,7 @@ T* as(void* p) {
 
 }  // namespace
 
-// buffers: 0 perm, 1 grp_b, 2 grp_e, 3 dkey, 4 prank, 5 dup, 6 counters, 7 uns, 8 run_b,
+// buffers: 0 perm, 1 grp_b, 2 grp_e, 3 dkey, 4 prank, 5 static flags, 6 counters, 7 flags, 8 run_b,
 // 9 run_e, 10 off, 11 ign_off, 12 mkey, 13 skey, 14 ign, 15 mine, 16 dedup table,
 // 17 rule table, 18 rule keys, 19 rule precedences, 20 pkg_class, 21 out pairs,
 // 22 ignored out, 23 scan temp / dup count
@@ -407,12 +455,19 @@ bool BatchFilter::set_packages(const FilterPackages& fp, std::string& err) {
         (n && !ok(hipMemcpy(bufs_[k], cols[k]->data(), n * 4, hipMemcpyHostToDevice), "hipMemcpy(filter packages)",
                   err)))
       return false;
-  if (fp.dup.size() != n || !grow(5, n, err) ||
-      (n && !ok(hipMemcpy(bufs_[5], fp.dup.data(), n, hipMemcpyHostToDevice), "hipMemcpy(filter dup)", err)))
+  if (fp.dup.size() != n) {
+    err = "filter: one dup flag per package";
+    return false;
+  }
+  std::vector<uint8_t> fl(n);
+  for (uint64_t p = 0; p < n; p++)
+    fl[p] = uint8_t((fp.dup[p] ? FL_DUP : 0u) | (fp.grp_e[p] - fp.grp_b[p] == 1 ? FL_SINGLE : 0u));
+  if (!grow(5, (n + 3) & ~3ull, err) ||
+      (n && !ok(hipMemcpy(bufs_[5], fl.data(), n, hipMemcpyHostToDevice), "hipMemcpy(filter flags)", err)))
     return false;
   for (int k : {8, 9, 20})
     if (!grow(k, n * 4, err)) return false;
-  if (!grow(6, n * 4 * kClasses, err) || !grow(7, n, err) || !grow(10, (n + 1) * 4, err) ||
+  if (!grow(6, n * 4 * kClasses, err) || !grow(7, (n + 3) & ~3ull, err) || !grow(10, (n + 1) * 4, err) ||
       !grow(11, (n + 1) * 4, err))
     return false;
   n_pkgs_ = n;
@@ -453,7 +508,7 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
       while (tcap < 2 * dup_n) tcap <<= 1;
     }
   }
-  const uint64_t nr = rules.keys.size();
+  const uint64_t nr = rules.size();
   uint64_t rcap = 0;
   if (nr) {
     rcap = 16;
@@ -469,39 +524,60 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
     return false;
   if (!grow(12, n * 4, err) || !grow(13, n * 4, err) || (has_ign && !grow(14, n * 4, err)) ||
       (tcap && (!grow(15, n * 4, err) || !grow(16, tcap * 16, err))) || (rcap && !grow(17, rcap * 16, err)) ||
-      (nr && (!grow(18, nr * 8, err) || !grow(19, nr * 4, err))) || !grow(21, n * 8, err) ||
+      !grow(21, n * 8, err) ||
       (has_ign && !grow(22, n * 12, err)) || !grow(23, std::max<uint64_t>(scan_bytes, 16), err))
     return false;
-  if (!rules.pkg_class.empty() && rules.pkg_class.size() != np) {
-    err = "filter: one class per package";
-    return false;
-  }
-  if (nr) {  // the rule hash set, built on the device from one pinned upload
-    if (pin_cap_ < nr * 12) {
+  // per-call flags start as the static ones (FL_DUP, FL_SINGLE)
+  if (np && !ok(hipMemcpyAsync(bufs_[7], bufs_[5], np, hipMemcpyDeviceToDevice, st), "D2D flags", err)) return false;
+  if (nr) {  // the rule hash set, built on the device from one pinned upload of the raw lists
+    // staging layout: rank tables, then per list subject / id / prec columns (4 B each)
+    uint64_t words = rules.rank[0].size() + rules.rank[1].size();
+    for (int k = 0; k < rules.n_lists; k++)
+      words += rules.lists[k].n * (1 + (rules.lists[k].subject ? 1 : 0) + (rules.lists[k].prec ? 1 : 0));
+    if (pin_cap_ < words * 4) {
       if (pin_) (void)hipHostFree(pin_);
       pin_ = nullptr;
       pin_cap_ = 0;
-      if (!ok(hipHostMalloc(&pin_, nr * 12, hipHostMallocDefault), "hipHostMalloc(filter rules)", err)) return false;
-      pin_cap_ = nr * 12;
+      if (!ok(hipHostMalloc(&pin_, words * 4, hipHostMallocDefault), "hipHostMalloc(filter rules)", err)) return false;
+      pin_cap_ = words * 4;
     }
-    memcpy(pin_, rules.keys.data(), nr * 8);
-    memcpy(static_cast<char*>(pin_) + nr * 8, rules.prec.data(), nr * 4);
-    if (!ok(hipMemcpyAsync(bufs_[18], pin_, nr * 8, hipMemcpyHostToDevice, st), "H2D rules", err) ||
-        !ok(hipMemcpyAsync(bufs_[19], static_cast<char*>(pin_) + nr * 8, nr * 4, hipMemcpyHostToDevice, st),
-            "H2D rule prec", err) ||
+    if (!grow(18, words * 4, err)) return false;
+    uint32_t* h = static_cast<uint32_t*>(pin_);
+    const uint32_t* d = as<const uint32_t>(bufs_[18]);
+    uint64_t at = 0;
+    auto put = [&](const uint32_t* src, uint64_t cnt) {
+      memcpy(h + at, src, cnt * 4);
+      const uint32_t* where = d + at;
+      at += cnt;
+      return where;
+    };
+    const uint32_t* rank_dev[2] = {put(rules.rank[0].data(), rules.rank[0].size()),
+                                   put(rules.rank[1].data(), rules.rank[1].size())};
+    RuleDev rd{};
+    rd.n_lists = rules.n_lists;
+    uint64_t end = 0;
+    for (int k = 0; k < rules.n_lists; k++) {
+      const RuleList& l = rules.lists[k];
+      rd.subject[k] = l.subject ? put(l.subject, l.n) : nullptr;
+      rd.id[k] = put(l.id, l.n);
+      rd.prec[k] = l.prec ? put(l.prec, l.n) : nullptr;
+      rd.rank[k] = rank_dev[l.table];
+      rd.tag[k] = uint32_t(l.tag);
+      end += l.n;
+      rd.end[k] = end;
+    }
+    if (!ok(hipMemcpyAsync(bufs_[18], pin_, words * 4, hipMemcpyHostToDevice, st), "H2D rules", err) ||
         !ok(hipMemsetAsync(bufs_[17], 0xFF, rcap * 16, st), "memset(rules)", err))
       return false;
-    hipLaunchKernelGGL(rules_insert, dim3(uint32_t((nr + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
-                       as<const unsigned long long>(bufs_[18]), as<const uint32_t>(bufs_[19]), nr,
-                       as<unsigned long long>(bufs_[17]), rcap - 1);
+    hipLaunchKernelGGL(rules_insert, dim3(uint32_t((nr + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, rd,
+                       as<unsigned long long>(bufs_[17]), rcap - 1, as<uint8_t>(bufs_[7]));
     if (!ok(hipGetLastError(), "rules_insert", err)) return false;
   }
-  if (!rules.pkg_class.empty() &&
-      !ok(hipMemcpyAsync(bufs_[20], rules.pkg_class.data(), np * 4, hipMemcpyHostToDevice, st), "H2D classes", err))
+  if (rules.pkg_class &&
+      !ok(hipMemcpyAsync(bufs_[20], rules.pkg_class, np * 4, hipMemcpyHostToDevice, st), "H2D classes", err))
     return false;
   if ((tcap && !ok(hipMemsetAsync(bufs_[16], 0, tcap * 16, st), "memset(dedup table)", err)) ||
-      !ok(hipMemsetAsync(bufs_[6], 0, np * 4 * kClasses, st), "memset(counters)", err) ||
-      !ok(hipMemsetAsync(bufs_[7], 0, np, st), "memset(uns)", err))
+      !ok(hipMemsetAsync(bufs_[6], 0, np * 4 * kClasses, st), "memset(counters)", err))
     return false;
   FilterArgs a{};
   a.t = t;
@@ -518,7 +594,7 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   a.dup = as<const uint8_t>(bufs_[5]);
   a.pkg_class = as<const uint32_t>(bufs_[20]);
   a.cnt = as<uint32_t>(bufs_[6]);
-  a.uns = as<uint8_t>(bufs_[7]);
+  a.fl = as<uint8_t>(bufs_[7]);
   a.run_b = as<uint32_t>(bufs_[8]);
   a.run_e = as<uint32_t>(bufs_[9]);
   a.off = as<const uint32_t>(bufs_[10]);

@@ -207,14 +207,30 @@ struct FilterPackages {
   std::vector<uint8_t> dup;            // per package: another package shares its dkey
 };
 
-// Host-compiled rules of one call: hash-set entries key = tag << 62 | subject << 32 |
-// vulnerability rank (subject: package or class, < 2^30), value = precedence.
+// Host-compiled rules of one call, as the caller's arrays: list k holds n entries (subject
+// = package or class, index into its ID-rank table, precedence); the device builds the
+// hash-set keys tag << 62 | subject << 32 | vulnerability rank (subject < 2^30) and
+// inserts them, keeping the smallest precedence per key.
 enum : uint64_t { RULE_ALL = 0, RULE_PKG = 1, RULE_CLS = 2, RULE_VEX = 3 };
+struct RuleList {
+  uint64_t tag = 0;
+  const uint32_t* subject = nullptr;  // nullptr: subject 0 (RULE_ALL)
+  const uint32_t* id = nullptr;
+  const uint32_t* prec = nullptr;     // nullptr: 0 (VEX)
+  uint64_t n = 0;
+  int table = 0;                      // 0: ignore-file ID ranks, 1: VEX ID ranks
+};
 struct FilterRules {
-  std::vector<uint64_t> keys;
-  std::vector<uint32_t> prec;
-  std::vector<uint32_t> pkg_class;  // per package (empty: no class rules)
-  uint32_t kinds = 0;               // bit k: some rule of tag k
+  RuleList lists[4];
+  int n_lists = 0;
+  std::vector<uint32_t> rank[2];     // ID index -> vulnerability rank (0xFFFFFFFF unknown)
+  const uint32_t* pkg_class = nullptr;  // per package (nullptr: no class rules)
+  uint32_t kinds = 0;                // bit k: some rule of tag k
+  uint64_t size() const {
+    uint64_t t = 0;
+    for (int k = 0; k < n_lists; k++) t += lists[k].n;
+    return t;
+  }
 };
 
 class BatchFilter {
