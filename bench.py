@@ -115,7 +115,7 @@ class C2:
             dt = time.perf_counter() - t
         return {"value": done / dt, "unit": "packages/s", "cores": threads, "kind": "port",
                 "sample": f"{done // n} passes over the first {n} packages of the same batch, oracle/match.c "
-                          f"orc_match with {threads} threads (os.cpu_count() of this host), {dt:.1f}s"}
+                          f"orc_match with {threads} threads (this host's CPU share), {dt:.1f}s"}
 
 
 class Mix:
@@ -247,7 +247,7 @@ def main():
     ap.add_argument("--pkgs-per-target", type=int, default=400)
     ap.add_argument("--packages", type=int, default=0, help="c3/c4/c5: packages of the global batch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0: os.cpu_count()")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: OMP_NUM_THREADS, else os.cpu_count()")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-fill", action="store_true", help="c2: skip the FillInfo / Filter legs")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end pipelined pass")
@@ -442,7 +442,9 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        threads = args.cpu_threads or os.cpu_count() or 1
+        # the box's CPU share: OMP_NUM_THREADS is set to it there (os.cpu_count() shows the
+        # whole machine, whose other cores belong to other jobs)
+        threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", 0) or 0) or os.cpu_count() or 1
         cpu = wl.cpu_baseline(args.cpu_seconds, threads if args.config == "c2" else 1)
 
     traffic = pmc_traffic(wl.name)

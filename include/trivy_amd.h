@@ -244,6 +244,11 @@ uint64_t tvm_match_algorithmic_bytes(tvm_engine* e, tvm_batch* b);
 int tvm_version_key(int grammar, const char* s, size_t n, uint8_t* out, size_t cap);
 /* Version class of a library grammar (npm: 1 pre-release; PEP 440: bits local/pre/post), -1 on error. */
 int tvm_version_class(int grammar, const char* s, size_t n);
+/* Host run of the match kernel's lane-serial dpkg key builder (verkey.h deb_fast_key) on
+ * s placed `shift` (0..3) bytes past a dword boundary (tests: it must equal tvm_version_key
+ * for the dpkg grammar).  Key length, -1 when the version does not parse, -2 when the
+ * kernel hands the version to the generic encoder. */
+int tvm_deb_fast_key_host(const char* s, size_t n, uint32_t shift, uint8_t* out, size_t cap);
 /* Host-side compare.IsVulnerable through the load-time interval compiler (tests): 1/0, -1
  * when the advisory JSON does not decode. */
 int tvm_lib_is_vulnerable_host(int grammar, const char* ver, size_t ver_len, const char* advisory_json,

@@ -651,6 +651,23 @@ int tvm_version_class(int grammar, const char* s, size_t n) {
   return int(cls);
 }
 
+int tvm_deb_fast_key_host(const char* s, size_t n, uint32_t shift, uint8_t* out, size_t cap) {
+  if (!s || n > 4096 || shift > 3) return -3;
+  uint8_t tab[128];
+  for (uint32_t c = 0; c < 128; c++) tab[c] = deb_fast_code(c);
+  std::vector<uint32_t> buf((shift + n) / 4 + 4, 0xA5A5A5A5u);  // padded like the LDS stage window
+  uint8_t* b = reinterpret_cast<uint8_t*>(buf.data()) + shift;
+  std::memcpy(b, s, n);
+  uint8_t kb[kFastKeyStride];
+  std::memset(kb, 0xEE, sizeof kb);
+  uint32_t len = 0;
+  const uint32_t st = deb_fast_key(b, uint32_t(n), kb, tab, len);
+  if (st == FAST_INVALID) return -1;
+  if (st == FAST_FALLBACK) return -2;
+  for (uint32_t i = 0; i < len && i < cap; i++) out[i] = kb[i];
+  return int(len);
+}
+
 int tvm_lib_is_vulnerable_host(int grammar, const char* ver, size_t ver_len, const char* advisory_json,
                                size_t json_len) {
   Advisory a;

@@ -200,11 +200,53 @@ __device__ __forceinline__ bool name_eq_slot(const uint8_t* s, uint32_t n, const
   return eq;
 }
 
+// Index probe of one package given its key state (shared by the fast and generic paths).
+template <class P>
+__device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uint32_t plat, const PlatInfo& pi,
+                                            uint32_t nlen, const uint8_t* name, bool valid, uint32_t& rbeg,
+                                            uint32_t& cnt);
+
 // One package: encode, hash, probe.  P = uint32_t in the LDS or global address space of s.
+// kb / tab: the lane's LDS key buffer and the dpkg code table (nullptr: generic encoder only).
 template <uint32_t GM, class P, int DIAG = 0>
 __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32_t plat, uint32_t nlen, uint32_t vlen,
-                                          const uint8_t* name, const uint8_t* ver, PkgRec& r) {
+                                          const uint8_t* name, const uint8_t* ver, PkgRec& r, uint8_t* kb = nullptr,
+                                          const uint8_t* tab = nullptr) {
   const PlatInfo pi = a.db.plats[plat];
+  if (!(DIAG & 1) && kb && ((GM >> CMP_DEB) & 1u) && pi.cmp == CMP_DEB) {
+    uint32_t kl = 0;
+    const uint32_t st = deb_fast_key(ver, vlen, kb, tab, kl);
+    if (st != FAST_FALLBACK) {
+      const bool valid = st == FAST_OK;
+      const uint32_t* kw = reinterpret_cast<const uint32_t*>(kb);
+      uint32_t kinfo = (valid ? (kl & KI_LEN) | KI_VALID : 0u), koff = 0;
+      r.k0 = r.k1 = 0;
+      if (valid) {
+        const uint64_t m0 = uint64_t(kw[0]) | (uint64_t(kw[1]) << 32), m1 = uint64_t(kw[2]) | (uint64_t(kw[3]) << 32);
+        r.k0 = be_word(m0, kl < 8 ? kl : 8);
+        r.k1 = kl > 8 ? be_word(m1, kl < 16 ? kl - 8 : 8) : 0ull;
+        if (kl > 16 && kl <= kKeyWords * 8) {
+          a.tail[p] = make_uint4(kw[4], kw[5], kw[6], kw[7]);
+        } else if (kl > kKeyWords * 8) {  // 33..39 bytes: the whole key into the spill area
+          const uint32_t need = (kl + 7) / 8;
+          const unsigned long long o = atomicAdd(&a.ctl[2], (unsigned long long)need);
+          if (o + need > a.spill_cap) {
+            atomicOr(&a.ctl[3], (unsigned long long)ERR_SPILL);
+            kinfo = 0;
+          } else {
+            uint32_t* dst = reinterpret_cast<uint32_t*>(a.spill + o);
+            for (uint32_t i = 0; i < 2 * need; i++) dst[i] = kw[i];
+            koff = uint32_t(o);
+            kinfo |= KI_SPILL;
+          }
+        }
+      }
+      uint32_t cnt = 0, rbeg = 0;
+      probe_lookup<P>(a, p, plat, pi, nlen, name, (kinfo & KI_VALID) != 0, rbeg, cnt);
+      r.meta = make_uint4(rbeg, cnt, kinfo, koff);
+      return;
+    }
+  }
   uint64_t* tslot = reinterpret_cast<uint64_t*>(a.tail + p);
   HeadSink hs(tslot);
   uint32_t cls = 0;
@@ -237,9 +279,17 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
   r.k0 = valid && kl ? be_word(hs.w0, kl < 8 ? kl : 8) : 0ull;
   r.k1 = valid && kl > 8 ? be_word(hs.w1, kl < 16 ? kl - 8 : 8) : 0ull;
   uint32_t cnt = 0, rbeg = 0;
+  if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, valid, rbeg, cnt);
+  r.meta = make_uint4(rbeg, cnt, kinfo, koff);
+}
+
+template <class P>
+__device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uint32_t plat, const PlatInfo& pi,
+                                            uint32_t nlen, const uint8_t* name, bool valid, uint32_t& rbeg,
+                                            uint32_t& cnt) {
   // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup;
   // lookup-first drivers (ubuntu.go:86-92) probe first, so a poisoned key still raises
-  if (!(DIAG & 2) && (valid || (pi.flags & PLAT_LOOKUP_FIRST))) {
+  if (valid || (pi.flags & PLAT_LOOKUP_FIRST)) {
     const uint64_t h = name_hash<P>(plat, name, nlen);
     for (uint64_t i = h & a.db.slot_mask;; i = (i + 1) & a.db.slot_mask) {
       const uint4* sp = reinterpret_cast<const uint4*>(a.db.slots + i);
@@ -257,14 +307,16 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
       break;
     }
   }
-  r.meta = make_uint4(rbeg, cnt, kinfo, koff);
 }
 
 template <uint32_t GM, int DIAG = 0>
 __global__ __launch_bounds__(kTile) void probe_kernel(ProbeArgs a) {
   __shared__ uint4 stage[kStage / 16 + 2];  // +2: the dword reads of a name's last word run past its end
   __shared__ uint32_t wsum[kTile / 64];
+  __shared__ uint32_t kbuf[kTile * kFastKeyStride / 4];  // per-lane dpkg key (deb_fast_key)
+  __shared__ uint8_t tab[128];
   const uint32_t tid = threadIdx.x, t = blockIdx.x;
+  if (tid < 128) tab[tid] = deb_fast_code(tid);
   const uint32_t p = t * kTile + tid;
   uint2 d = make_uint2(0xFFFFFFFFu, 0);
   if (p < a.n) d = a.pk[p];
@@ -287,7 +339,8 @@ __global__ __launch_bounds__(kTile) void probe_kernel(ProbeArgs a) {
   if (p < a.n && d.x < a.db.n_plats) {
     if (staged) {
       const uint8_t* sb = reinterpret_cast<const uint8_t*>(stage) + uint32_t(w0 - base16) + off;
-      probe_one<GM, uint32_t, DIAG>(a, p, d.x, nlen, vlen, sb, sb + nlen, r);
+      probe_one<GM, uint32_t, DIAG>(a, p, d.x, nlen, vlen, sb, sb + nlen, r,
+                                    reinterpret_cast<uint8_t*>(kbuf) + tid * kFastKeyStride, tab);
     } else {
       const uint8_t* gb = a.arena + w0 + off;
       probe_one<GM, uint32_t, DIAG>(a, p, d.x, nlen, vlen, gb, gb + nlen, r);
@@ -559,13 +612,28 @@ __global__ __launch_bounds__(kTile) void sweep_kernel(SweepArgs a) {
 // of one CU sit in different phases, so one tile's probe latency overlaps another's sweep.
 // DIAG (measurement only, wrong match lists by construction; "diag_*" variants): bit 0 skips
 // the version encoder, bit 1 the index probe, bit 2 the sweep.
-template <uint32_t GM, int K, int MB, bool FILT, int DIAG = 0>
-__global__ __launch_bounds__(kTile) void fused_kernel(FusedArgs fa) {
+template <uint32_t GM, int K, int MB, bool FILT, int DIAG = 0, int WPE = 1>
+__global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
   constexpr uint32_t kStageVec = kStage / 16 + 2;
   constexpr uint32_t kMbufVec = (MB * 5 + 15) / 16;
   __shared__ uint4 buf[kStageVec > kMbufVec ? kStageVec : kMbufVec];  // strings (probe), then matches (sweep)
-  __shared__ SweepShared<FILT> s;
-  __shared__ uint8_t map[kMapCap];
+  // the probe's per-lane dpkg keys + code table share LDS with the sweep's state (the scan
+  // below is done with s.wsum before the table is written)
+  struct SweepPart {
+    SweepShared<FILT> s;
+    uint8_t map[kMapCap];
+  };
+  struct ProbePart {
+    uint32_t kbuf[kTile * kFastKeyStride / 4];
+    uint8_t tab[128];
+  };
+  static_assert(sizeof(ProbePart) <= sizeof(SweepPart), "the probe's LDS fits in the sweep's");
+  __shared__ union {
+    SweepPart sw;
+    ProbePart pr;
+  } u;
+  SweepShared<FILT>& s = u.sw.s;
+  uint8_t* map = u.sw.map;
   const ProbeArgs& a = fa.pa;
   const uint32_t tid = threadIdx.x, t = blockIdx.x;
   const uint32_t p = t * kTile + tid;
@@ -583,6 +651,7 @@ __global__ __launch_bounds__(kTile) void fused_kernel(FusedArgs fa) {
     for (uint32_t i = tid; i < nv; i += kTile) buf[i] = src[i];
     if (tid < 2) buf[nv + tid] = make_uint4(0, 0, 0, 0);
   }
+  if (tid < 128) u.pr.tab[tid] = deb_fast_code(tid);
   __syncthreads();
   PkgRec r;
   r.meta = make_uint4(0, 0, 0, 0);
@@ -590,7 +659,8 @@ __global__ __launch_bounds__(kTile) void fused_kernel(FusedArgs fa) {
   if (p < a.n && d.x < a.db.n_plats) {
     if (staged) {
       const uint8_t* sb = reinterpret_cast<const uint8_t*>(buf) + uint32_t(w0 - base16) + off;
-      probe_one<GM, uint32_t, DIAG & 3>(a, p, d.x, nlen, vlen, sb, sb + nlen, r);
+      probe_one<GM, uint32_t, DIAG & 3>(a, p, d.x, nlen, vlen, sb, sb + nlen, r,
+                                        reinterpret_cast<uint8_t*>(u.pr.kbuf) + tid * kFastKeyStride, u.pr.tab);
     } else {
       const uint8_t* gb = a.arena + w0 + off;
       probe_one<GM, uint32_t, DIAG & 3>(a, p, d.x, nlen, vlen, gb, gb + nlen, r);
@@ -612,9 +682,9 @@ void launch_sweep(uint32_t n_tiles, hipStream_t st, const SweepArgs& a) {
   hipLaunchKernelGGL((sweep_kernel<K, MB, FILT>), dim3(n_tiles), dim3(kTile), 0, st, a);
 }
 
-template <uint32_t GM, int K, int MB, bool FILT, int DIAG = 0>
+template <uint32_t GM, int K, int MB, bool FILT, int DIAG = 0, int WPE = 1>
 void launch_fused(uint32_t n_tiles, hipStream_t st, const FusedArgs& a) {
-  hipLaunchKernelGGL((fused_kernel<GM, K, MB, FILT, DIAG>), dim3(n_tiles), dim3(kTile), 0, st, a);
+  hipLaunchKernelGGL((fused_kernel<GM, K, MB, FILT, DIAG, WPE>), dim3(n_tiles), dim3(kTile), 0, st, a);
 }
 
 }  // namespace

@@ -7,6 +7,8 @@
 
 #define TVM_MATCH_VARIANTS_PRODUCT(X) \
   X(1, 4, 2048, "fused_k4_m2048")     \
+  X(2, 4, 2048, "fused_k4_m2048_o6")  \
+  X(3, 4, 2048, "fused_k4_m2048_o8")  \
   X(1, 2, 2048, "fused_k2_m2048")     \
   X(1, 1, 2048, "fused_k1_m2048")     \
   X(0, 2, 2048, "split_k2_m2048")     \
@@ -24,6 +26,9 @@
 #else
 #define TVM_MATCH_VARIANTS(X) TVM_MATCH_VARIANTS_PRODUCT(X)
 #endif
+
+// Fused F = 2 / 3: the same kernel compiled for at least 6 / 8 waves per SIMD (register cap).
+#define TVM_FUSED_WPE(F) ((F) == 2 ? 6 : (F) == 3 ? 8 : 1)
 
 #define TVM_VARIANT_COUNT_(F, K, MB, NAME) +1
 constexpr int kNumTuned = 0 TVM_MATCH_VARIANTS(TVM_VARIANT_COUNT_);

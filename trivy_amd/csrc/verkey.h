@@ -273,6 +273,155 @@ TVM_HD bool deb_encode(const uint8_t* s, uint32_t n, Sink& o) {
   return true;
 }
 
+// ---- dpkg sort key, lane-serial over dwords (the match kernel's common case) -------------
+//
+// The same key as verkey.h deb_encode (go-deb-version order, layout documented there) for
+// versions that are all ASCII with an epoch of at most 9 digits, digit runs of at most 9
+// significant digits and a key of at most kFastKeyCap bytes - everything else returns
+// FAST_FALLBACK and takes the generic encoder.  It differs in how it runs, not in what it
+// produces (host test: tests/test_fastdeb_host.py runs this very function against
+// deb_encode):
+//   * the version is read from LDS a dword at a time (aligned reads + v_alignbyte) and its
+//     bytes taken with constant shifts, instead of one ds_read_u8 per byte per pass;
+//   * one SWAR pre-pass per dword finds the first / last ':' and the last '-' and flags
+//     non-ASCII bytes (exact per-byte equality masks, no per-byte branch);
+//   * the emission pass is branch-free per byte: the number token TERM_k + k big-endian
+//     bytes and the next code byte are always written at the lane's key position in LDS,
+//     and only the position advance depends on the byte, so lanes at different points of
+//     their strings never diverge; character codes and validity come from a 128-byte LDS
+//     table (code 0 = not in go-deb-version's ASCII sets).
+constexpr uint32_t kFastKeyStride = 44;  // LDS bytes per lane: 11 dwords, co-prime with the 64 banks
+constexpr uint32_t kFastKeyCap = 39;     // longest key kept (a write lands at most 4 bytes past the cap)
+enum : uint32_t { FAST_INVALID = 0, FAST_OK = 1, FAST_FALLBACK = 2 };
+
+// Code byte of each ASCII non-digit for deb_part, 0 where go-deb-version rejects the byte
+// (verifyUpstreamVersion / verifyDebianRevision): filled per workgroup into LDS.
+TVM_HD uint8_t deb_fast_code(uint32_t c) {
+  const bool ok = c < 64 ? ((kDebOk0 >> c) & 1u) : c < 128 ? ((kDebOk1 >> (c - 64)) & 1u) : false;
+  return ok ? deb_code_ascii(uint8_t(c)) : uint8_t(0);
+}
+
+// Bit 7 of byte i set iff byte i of x equals the byte of pat (exact, no borrow artefacts).
+TVM_HD uint32_t byte_eq_mask(uint32_t x, uint32_t pat) {
+  const uint32_t t = x ^ pat;
+  return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
+}
+
+// Dword i of a byte string at any alignment (bytes 4i .. 4i+3, little-endian); the words
+// past the end may hold anything (callers mask), but must be readable.
+TVM_HD uint32_t str_dword(const uint32_t* base, uint32_t sh, uint32_t i) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __builtin_amdgcn_alignbyte(base[i + 1], base[i], sh);
+#else
+  return uint32_t(((uint64_t(base[i + 1]) << 32) | base[i]) >> (8 * sh));
+#endif
+}
+
+// Key of dpkg version s[0, n) into kb[0, len) (kb: kFastKeyStride writable bytes).
+// Returns FAST_OK, FAST_INVALID (go-deb-version NewVersion error) or FAST_FALLBACK.
+TVM_HD uint32_t deb_fast_key(const uint8_t* s, uint32_t n, uint8_t* kb, const uint8_t* tab, uint32_t& len) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(s);
+  const uint32_t* base = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+  const uint32_t sh = uint32_t(a & 3);
+  // pre-pass: first and last ':', last '-', any byte >= 0x80
+  uint32_t colon = n, lcolon = n, dash = n, high = 0;
+  for (uint32_t j = 0; j < n; j += 4) {
+    uint32_t x = str_dword(base, sh, j >> 2);
+    if (n - j < 4) x &= (1u << (8 * (n - j))) - 1u;
+    high |= x;
+    const uint32_t md = byte_eq_mask(x, 0x2D2D2D2Du), mc = byte_eq_mask(x, 0x3A3A3A3Au);
+    if (md) dash = j + ((31u - uint32_t(__builtin_clz(md))) >> 3);
+    if (mc) {
+      if (colon == n) colon = j + (uint32_t(__builtin_ctz(mc)) >> 3);
+      lcolon = j + ((31u - uint32_t(__builtin_clz(mc))) >> 3);
+    }
+  }
+  if (high & 0x80808080u) return FAST_FALLBACK;
+  // epoch: 1..9 digits before the first ':' (signs, overflow, empty: the generic parser)
+  uint32_t epoch = 0, r0 = 0;
+  if (colon < n) {
+    if (colon == 0 || colon > 9) return FAST_FALLBACK;
+    for (uint32_t i = 0; i < colon; i++) {
+      const uint32_t d = uint32_t(s[i]) - '0';
+      if (d >= 10) return FAST_FALLBACK;
+      epoch = epoch * 10u + d;
+    }
+    r0 = colon + 1;
+  }
+  const bool has_rev = dash < n && dash >= r0;
+  if (r0 >= (has_rev ? dash : n) || uint32_t(s[r0]) - '0' >= 10u) return FAST_INVALID;
+  if (has_rev && lcolon < n && lcolon > dash) return FAST_INVALID;
+  const uint32_t split = has_rev ? dash : 0xFFFFFFFFu;
+  // EPOCH
+  const uint32_t ke = epoch ? (39u - uint32_t(__builtin_clz(epoch))) >> 3 : 0u;
+  const uint32_t eb = ke ? epoch << (32 - 8 * ke) : 0u;
+  kb[0] = uint8_t(ke);
+  kb[1] = uint8_t(eb >> 24);
+  kb[2] = uint8_t(eb >> 16);
+  kb[3] = uint8_t(eb >> 8);
+  kb[4] = uint8_t(eb);
+  uint32_t pos = 1 + ke;
+  // PART(upstream) PART(revision): per byte, always write the pending number token and the
+  // byte's code at the current position; advance only over what the byte emits
+  uint32_t v = 0, sig = 0, pd = 0, bad = 0, ovf = 0;
+  for (uint32_t j = r0 & ~3u; j < n; j += 4) {
+    const uint32_t x = str_dword(base, sh, j >> 2);
+#pragma unroll
+    for (uint32_t b = 0; b < 4; b++) {
+      const uint32_t jj = j + b;
+      const uint32_t c = (x >> (8 * b)) & 0xFFu;
+      const uint32_t in = (jj >= r0) & (jj < n);
+      const uint32_t d = c - '0';
+      const uint32_t isd = d < 10u;
+      const uint32_t sp = jj == split;
+      const uint32_t code = tab[c & 0x7Fu];
+      // number token of the run ending here (v = 0 gives TERM0: the empty run at a split)
+      const uint32_t k = v ? (39u - uint32_t(__builtin_clz(v))) >> 3 : 0u;
+      const uint32_t vb = k ? v << (32 - 8 * k) : 0u;
+      uint8_t* o = kb + (pos < kFastKeyCap ? pos : kFastKeyCap);
+      o[0] = uint8_t(DEB_TERM0 + k);
+      o[1] = uint8_t(vb >> 24);
+      o[2] = uint8_t(vb >> 16);
+      o[3] = uint8_t(vb >> 8);
+      o[4] = uint8_t(vb);
+      const uint32_t flush = in & (isd ^ 1u) & (pd | sp);
+      const uint32_t p1 = pos + (flush ? k + 1 : 0u);
+      kb[p1 < kFastKeyCap ? p1 : kFastKeyCap] = sp ? uint8_t(DEB_END) : uint8_t(code);
+      pos = p1 + (in & (isd ^ 1u));
+      bad |= in & (isd ^ 1u) & (sp ^ 1u) & (code == 0u);
+      const uint32_t nv = v * 10u + d;
+      sig = in ? (isd ? sig + (nv != 0u) : 0u) : sig;  // significant digits of the current run
+      ovf |= sig > 9u;
+      v = in ? (isd ? nv : 0u) : v;
+      pd = in ? isd : pd;
+    }
+  }
+  if (bad) return FAST_INVALID;
+  if (ovf) return FAST_FALLBACK;  // a run may exceed 32 bits (or clamp at MaxInt64)
+  // end of the last part, then PART("") when there is no revision
+  {
+    const uint32_t k = v ? (39u - uint32_t(__builtin_clz(v))) >> 3 : 0u;
+    const uint32_t vb = k ? v << (32 - 8 * k) : 0u;
+    uint8_t* o = kb + (pos < kFastKeyCap ? pos : kFastKeyCap);
+    o[0] = uint8_t(DEB_TERM0 + k);
+    o[1] = uint8_t(vb >> 24);
+    o[2] = uint8_t(vb >> 16);
+    o[3] = uint8_t(vb >> 8);
+    o[4] = uint8_t(vb);
+    pos += k + 1;
+    kb[pos < kFastKeyCap ? pos : kFastKeyCap] = DEB_END;
+    pos++;
+    if (!has_rev) {
+      kb[pos < kFastKeyCap ? pos : kFastKeyCap] = DEB_TERM0;
+      kb[pos + 1 < kFastKeyCap ? pos + 1 : kFastKeyCap] = DEB_END;
+      pos += 2;
+    }
+  }
+  if (pos > kFastKeyCap) return FAST_FALLBACK;
+  len = pos;
+  return FAST_OK;
+}
+
 // ------------------------------------------------------------------- signed integers -----
 // Order-preserving variable-length code of a signed 64-bit value: v >= 0 as 0x80+k then
 // k big-endian bytes (k minimal, 0 for v = 0); v < 0 as 0x7F-k then the k bytes of
