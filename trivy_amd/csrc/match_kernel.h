@@ -309,6 +309,22 @@ __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uin
   }
 }
 
+// A tile's string window (nv 16-byte words, nv <= kStage / 16) into LDS, plus two zero
+// words: every lane issues its (at most kStage / 16 / kTile) loads before storing any.
+__device__ __forceinline__ void stage_window(uint4* buf, const uint8_t* src8, uint32_t nv, uint32_t tid) {
+  constexpr uint32_t SV = (kStage / 16 + kTile - 1) / kTile;
+  const uint4* src = reinterpret_cast<const uint4*>(src8);
+  if (nv) {
+    uint4 v[SV];
+#pragma unroll
+    for (uint32_t k = 0; k < SV; k++) v[k] = src[min(tid + k * kTile, nv - 1)];
+#pragma unroll
+    for (uint32_t k = 0; k < SV; k++)
+      if (tid + k * kTile < nv) buf[tid + k * kTile] = v[k];
+  }
+  if (tid < 2) buf[nv + tid] = make_uint4(0, 0, 0, 0);
+}
+
 template <uint32_t GM, int DIAG = 0>
 __global__ __launch_bounds__(kTile) void probe_kernel(ProbeArgs a) {
   __shared__ uint4 stage[kStage / 16 + 2];  // +2: the dword reads of a name's last word run past its end
@@ -320,18 +336,13 @@ __global__ __launch_bounds__(kTile) void probe_kernel(ProbeArgs a) {
   const uint32_t p = t * kTile + tid;
   uint2 d = make_uint2(0xFFFFFFFFu, 0);
   if (p < a.n) d = a.pk[p];
+  const uint64_t w0 = a.tile_off[t * kGroupsPerTile], w1 = a.tile_off[(t + 1) * kGroupsPerTile];
   const uint32_t nlen = d.y & 0xFFFFu, vlen = d.y >> 16;
   uint32_t off = 0;
   block_exscan<kTile>(wsum, nlen + vlen, tid, off);
-  const uint64_t w0 = a.tile_off[t * kGroupsPerTile], w1 = a.tile_off[(t + 1) * kGroupsPerTile];
   const uint64_t base16 = w0 & ~uint64_t(15);
   const bool staged = w1 - base16 <= kStage;
-  if (staged) {
-    const uint32_t nv = uint32_t((w1 - base16 + 15) / 16);
-    const uint4* src = reinterpret_cast<const uint4*>(a.arena + base16);
-    for (uint32_t i = tid; i < nv; i += kTile) stage[i] = src[i];
-    if (tid < 2) stage[nv + tid] = make_uint4(0, 0, 0, 0);
-  }
+  if (staged) stage_window(stage, a.arena + base16, uint32_t((w1 - base16 + 15) / 16), tid);
   __syncthreads();
   PkgRec r;
   r.meta = make_uint4(0, 0, 0, 0);
@@ -401,32 +412,50 @@ __device__ __forceinline__ int cmp_be(uint64_t a0, uint64_t a1, const uint64_t* 
   return key_cmp(atail, na - 16, btail, nb - 16);
 }
 
+// sign(installed - bound) from the big-endian 16-byte heads alone, branch-free: valid
+// unless both heads tie and both keys are longer than 16 bytes (`tie`, then cmp_be).
+__device__ __forceinline__ int cmp_head(uint64_t a0, uint64_t a1, uint32_t na, uint64_t b0, uint64_t b1, uint32_t nb,
+                                        bool& tie) {
+  const bool eq0 = a0 == b0, eq = eq0 && a1 == b1;
+  const bool lt = a0 < b0 || (eq0 && a1 < b1);
+  tie = eq && na > 16 && nb > 16;
+  const int byl = (na > nb) - (na < nb);
+  return eq ? byl : (lt ? -1 : 1);
+}
+
 // Interval test of tile package q's installed key against one row (global index ridx).
+// The common case (a bound decided by the inline 16-byte heads) runs without branches;
+// a 16-byte tie reads the key tails, a lower bound (library / rpm ranges) its key head.
 template <bool FILT, class S>
 __device__ __forceinline__ bool eval_row(const SweepArgs& a, const S& s, uint32_t q, uint32_t p, const Row& row,
                                          uint32_t ridx) {
   const uint32_t ki = s.kinfo[q];
-  if constexpr (FILT) {
-    if ((row.adv & ROW_FILTER) && !aux_pass(a, ridx, s.pattr[q], ki)) return false;
-  }
-  if (row.adv & ROW_ALWAYS) return true;
-  if (!(ki & KI_VALID)) return false;
   const uint32_t kl = ki & KI_LEN;
   const uint64_t k0 = s.k0[q], k1 = s.k1[q];
-  const uint64_t* ktail = (ki & KI_SPILL) ? a.spill + s.koff[q] + 2 : reinterpret_cast<const uint64_t*>(a.tail + p);
-  bool m = true;
-  if (!(row.hi_len & KEY_INF)) {
-    const uint64_t* hw = a.db.key_words + row.hi_off;
-    const int c = cmp_be(k0, k1, ktail, kl, row.hi_pre0, row.hi_pre1, hw + 2, row.hi_len & KEY_LEN_MASK);
-    m = (row.hi_len & KEY_INCL) ? c <= 0 : c < 0;
+  const uint32_t nh = row.hi_len & KEY_LEN_MASK;
+  bool tie = false;
+  int c = cmp_head(k0, k1, kl, row.hi_pre0, row.hi_pre1, nh, tie);
+  const bool hi_inf = (row.hi_len & KEY_INF) != 0;
+  if (tie && !hi_inf) {  // rare: same 16-byte head, both keys longer
+    const uint64_t* ktail =
+        (ki & KI_SPILL) ? a.spill + s.koff[q] + 2 : reinterpret_cast<const uint64_t*>(a.tail + p);
+    c = key_cmp(ktail, kl - 16, a.db.key_words + row.hi_off + 2, nh - 16);
   }
-  if (m && !(row.lo_len & KEY_INF)) {  // rare (library / rpm ranges): the bound's head from the arena
+  bool m = hi_inf || ((row.hi_len & KEY_INCL) ? c <= 0 : c < 0);
+  if (!(row.lo_len & KEY_INF) && m) {  // rare (library / rpm ranges): the bound's head from the arena
+    const uint64_t* ktail =
+        (ki & KI_SPILL) ? a.spill + s.koff[q] + 2 : reinterpret_cast<const uint64_t*>(a.tail + p);
     const uint64_t* lw = a.db.key_words + row.lo_off;
     const uint32_t nl = row.lo_len & KEY_LEN_MASK;
     const uint64_t l0 = nl ? be_word(lw[0], nl < 8 ? nl : 8) : 0ull;
     const uint64_t l1 = nl > 8 ? be_word(lw[1], nl < 16 ? nl - 8 : 8) : 0ull;
-    const int c = cmp_be(k0, k1, ktail, kl, l0, l1, lw + 2, nl);
-    m = (row.lo_len & KEY_INCL) ? c >= 0 : c > 0;
+    const int cl = cmp_be(k0, k1, ktail, kl, l0, l1, lw + 2, nl);
+    m = (row.lo_len & KEY_INCL) ? cl >= 0 : cl > 0;
+  }
+  m = m && (ki & KI_VALID);
+  m = m || (row.adv & ROW_ALWAYS);
+  if constexpr (FILT) {
+    if (m && (row.adv & ROW_FILTER)) m = aux_pass(a, ridx, s.pattr[q], ki);
   }
   return m;
 }
@@ -461,24 +490,35 @@ __device__ __forceinline__ uint32_t sweep(const SweepArgs& a, SweepShared<FILT>&
   const bool use_map = total <= kMapCap;
   uint32_t nm = 0, round = 0;
   for (uint32_t b0 = 0; b0 < total; b0 += kTile * K, round++) {
+    // every lane issues its K row loads back to back, unconditionally (pairs past the end
+    // re-read the tile's last pair), so the K loads are in flight together and the lane
+    // waits once; a load under a branch would be waited for before the next one issues
     Row row[K];
     uint32_t qq[K], rid[K];
+    if (use_map) {
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        const uint32_t j = min(b0 + k * kTile + tid, total - 1);
+        rid[k] = map[j];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < K; k++) rid[k] = pair_rank(s, nnz, min(b0 + k * kTile + tid, total - 1));
+    }
 #pragma unroll
     for (int k = 0; k < K; k++) {
-      const uint32_t j = b0 + k * kTile + tid;
-      qq[k] = 0;
-      rid[k] = 0;
-      if (j < total) {
-        const uint32_t r = use_map ? uint32_t(map[j]) : pair_rank(s, nnz, j);
-        qq[k] = s.nz_q[r];
-        rid[k] = j + s.nz_rd[r];
-        row[k] = a.db.rows[rid[k]];
-      }
+      const uint32_t r = rid[k];
+      qq[k] = s.nz_q[r];
+      rid[k] = min(b0 + k * kTile + tid, total - 1) + s.nz_rd[r];
     }
+#pragma unroll
+    for (int k = 0; k < K; k++) row[k] = a.db.rows[rid[k]];
     uint32_t mask = 0;
 #pragma unroll
-    for (int k = 0; k < K; k++)
-      if (b0 + k * kTile + tid < total && eval_row<FILT>(a, s, qq[k], pbase + qq[k], row[k], rid[k])) mask |= 1u << k;
+    for (int k = 0; k < K; k++) {
+      const bool m = eval_row<FILT>(a, s, qq[k], pbase + qq[k], row[k], rid[k]);
+      mask |= (m && b0 + k * kTile + tid < total) ? 1u << k : 0u;
+    }
     uint32_t* ws = s.wsum2[round & 1];
     unsigned long long bal[K];
 #pragma unroll
@@ -639,18 +679,13 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
   const uint32_t p = t * kTile + tid;
   uint2 d = make_uint2(0xFFFFFFFFu, 0);
   if (p < a.n) d = a.pk[p];
+  const uint64_t w0 = a.tile_off[t * kGroupsPerTile], w1 = a.tile_off[(t + 1) * kGroupsPerTile];  // before the scan's barriers
   const uint32_t nlen = d.y & 0xFFFFu, vlen = d.y >> 16;
   uint32_t off = 0;
   block_exscan<kTile>(s.wsum[0], nlen + vlen, tid, off);
-  const uint64_t w0 = a.tile_off[t * kGroupsPerTile], w1 = a.tile_off[(t + 1) * kGroupsPerTile];
   const uint64_t base16 = w0 & ~uint64_t(15);
   const bool staged = w1 - base16 <= kStage;
-  if (staged) {
-    const uint32_t nv = uint32_t((w1 - base16 + 15) / 16);
-    const uint4* src = reinterpret_cast<const uint4*>(a.arena + base16);
-    for (uint32_t i = tid; i < nv; i += kTile) buf[i] = src[i];
-    if (tid < 2) buf[nv + tid] = make_uint4(0, 0, 0, 0);
-  }
+  if (staged) stage_window(buf, a.arena + base16, uint32_t((w1 - base16 + 15) / 16), tid);
   if (tid < 128) u.pr.tab[tid] = deb_fast_code(tid);
   __syncthreads();
   PkgRec r;
