@@ -225,21 +225,8 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
         const uint64_t m0 = uint64_t(kw[0]) | (uint64_t(kw[1]) << 32), m1 = uint64_t(kw[2]) | (uint64_t(kw[3]) << 32);
         r.k0 = be_word(m0, kl < 8 ? kl : 8);
         r.k1 = kl > 8 ? be_word(m1, kl < 16 ? kl - 8 : 8) : 0ull;
-        if (kl > 16 && kl <= kKeyWords * 8) {
-          a.tail[p] = make_uint4(kw[4], kw[5], kw[6], kw[7]);
-        } else if (kl > kKeyWords * 8) {  // 33..39 bytes: the whole key into the spill area
-          const uint32_t need = (kl + 7) / 8;
-          const unsigned long long o = atomicAdd(&a.ctl[2], (unsigned long long)need);
-          if (o + need > a.spill_cap) {
-            atomicOr(&a.ctl[3], (unsigned long long)ERR_SPILL);
-            kinfo = 0;
-          } else {
-            uint32_t* dst = reinterpret_cast<uint32_t*>(a.spill + o);
-            for (uint32_t i = 0; i < 2 * need; i++) dst[i] = kw[i];
-            koff = uint32_t(o);
-            kinfo |= KI_SPILL;
-          }
-        }
+        static_assert(kFastKeyCap <= kKeyWords * 8, "fast keys fit head + tail slot");
+        if (kl > 16) a.tail[p] = make_uint4(kw[4], kw[5], kw[6], kw[7]);
       }
       uint32_t cnt = 0, rbeg = 0;
       probe_lookup<P>(a, p, plat, pi, nlen, name, (kinfo & KI_VALID) != 0, rbeg, cnt);

@@ -291,7 +291,7 @@ TVM_HD bool deb_encode(const uint8_t* s, uint32_t n, Sink& o) {
 //     their strings never diverge; character codes and validity come from a 128-byte LDS
 //     table (code 0 = not in go-deb-version's ASCII sets).
 constexpr uint32_t kFastKeyStride = 44;  // LDS bytes per lane: 11 dwords, co-prime with the 64 banks
-constexpr uint32_t kFastKeyCap = 39;     // longest key kept (a write lands at most 4 bytes past the cap)
+constexpr uint32_t kFastKeyCap = 32;     // longest key kept (writes land at most 5 bytes past the clamped position)
 enum : uint32_t { FAST_INVALID = 0, FAST_OK = 1, FAST_FALLBACK = 2 };
 
 // Code byte of each ASCII non-digit for deb_part, 0 where go-deb-version rejects the byte
@@ -315,6 +315,49 @@ TVM_HD uint32_t str_dword(const uint32_t* base, uint32_t sh, uint32_t i) {
 #else
   return uint32_t(((uint64_t(base[i + 1]) << 32) | base[i]) >> (8 * sh));
 #endif
+}
+
+TVM_HD uint32_t clz32(uint32_t v) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return uint32_t(__clz(int(v)));  // 32 for 0
+#else
+  return v ? uint32_t(__builtin_clz(v)) : 32u;
+#endif
+}
+
+// Emission state of deb_fast_key: key position, value of the digit run so far, previous
+// byte a digit, a rejected byte seen, a run over 9 significant digits seen.
+struct DebFastState {
+  uint32_t pos, v;
+  bool pd, bad, ovf;
+};
+
+// One byte of a part (c < 0x80; split: the '-' between upstream and revision).  The token
+// of a run that ends here (TERM_k + k big-endian bytes; v = 0 gives TERM0, the empty run
+// a split closes) and the byte's code (END at the split) are written unconditionally at
+// pos; only the advance depends on the byte, so the loop has no branch.
+TVM_HD void deb_fast_byte(uint32_t c, bool split, uint8_t* kb, const uint8_t* tab, DebFastState& st) {
+  const uint32_t d = c - '0';
+  const bool isd = d < 10u;
+  const uint32_t code = tab[c & 0x7Fu];
+  const uint32_t v = st.v;
+  const uint32_t k = (39u - clz32(v)) >> 3;     // bytes of v (0 for v = 0)
+  const uint32_t vb = v << ((32u - 8u * k) & 31u);  // v = 0 when k = 0, so the shift wrap is harmless
+  const uint32_t at = st.pos < kFastKeyCap ? st.pos : kFastKeyCap;
+  uint8_t* o = kb + at;
+  o[0] = uint8_t(DEB_TERM0 + k);
+  o[1] = uint8_t(vb >> 24);
+  o[2] = uint8_t(vb >> 16);
+  o[3] = uint8_t(vb >> 8);
+  o[4] = uint8_t(vb);
+  const bool flush = !isd && (st.pd || split);
+  const uint32_t tk = flush ? k + 1 : 0u;
+  o[tk] = split ? uint8_t(DEB_END) : uint8_t(code);
+  st.pos += tk + (isd ? 0u : 1u);
+  st.bad = st.bad || (!isd && !split && code == 0u);
+  st.ovf = st.ovf || (isd && v >= 100000000u);  // a 10th significant digit
+  st.v = isd ? (v << 3) + (v << 1) + d : 0u;
+  st.pd = isd;
 }
 
 // Key of dpkg version s[0, n) into kb[0, len) (kb: kFastKeyStride writable bytes).
@@ -362,46 +405,28 @@ TVM_HD uint32_t deb_fast_key(const uint8_t* s, uint32_t n, uint8_t* kb, const ui
   kb[4] = uint8_t(eb);
   uint32_t pos = 1 + ke;
   // PART(upstream) PART(revision): per byte, always write the pending number token and the
-  // byte's code at the current position; advance only over what the byte emits
-  uint32_t v = 0, sig = 0, pd = 0, bad = 0, ovf = 0;
-  for (uint32_t j = r0 & ~3u; j < n; j += 4) {
-    const uint32_t x = str_dword(base, sh, j >> 2);
+  // byte's code at the current position (clamped to the buffer); advance only over what the
+  // byte emits.  Bytes from r0 on: whole dwords, then the last 0..3 bytes one by one.
+  DebFastState st{pos, 0u, false, false, false};
+  const uint8_t* s2 = s + r0;
+  const uint32_t m = n - r0, sp2 = has_rev ? dash - r0 : 0xFFFFFFFFu;
+  const uintptr_t a2 = reinterpret_cast<uintptr_t>(s2);
+  const uint32_t* base2 = reinterpret_cast<const uint32_t*>(a2 & ~uintptr_t(3));
+  const uint32_t sh2 = uint32_t(a2 & 3);
+  for (uint32_t j = 0; j + 4 <= m; j += 4) {
+    const uint32_t x = str_dword(base2, sh2, j >> 2);
 #pragma unroll
-    for (uint32_t b = 0; b < 4; b++) {
-      const uint32_t jj = j + b;
-      const uint32_t c = (x >> (8 * b)) & 0xFFu;
-      const uint32_t in = (jj >= r0) & (jj < n);
-      const uint32_t d = c - '0';
-      const uint32_t isd = d < 10u;
-      const uint32_t sp = jj == split;
-      const uint32_t code = tab[c & 0x7Fu];
-      // number token of the run ending here (v = 0 gives TERM0: the empty run at a split)
-      const uint32_t k = v ? (39u - uint32_t(__builtin_clz(v))) >> 3 : 0u;
-      const uint32_t vb = k ? v << (32 - 8 * k) : 0u;
-      uint8_t* o = kb + (pos < kFastKeyCap ? pos : kFastKeyCap);
-      o[0] = uint8_t(DEB_TERM0 + k);
-      o[1] = uint8_t(vb >> 24);
-      o[2] = uint8_t(vb >> 16);
-      o[3] = uint8_t(vb >> 8);
-      o[4] = uint8_t(vb);
-      const uint32_t flush = in & (isd ^ 1u) & (pd | sp);
-      const uint32_t p1 = pos + (flush ? k + 1 : 0u);
-      kb[p1 < kFastKeyCap ? p1 : kFastKeyCap] = sp ? uint8_t(DEB_END) : uint8_t(code);
-      pos = p1 + (in & (isd ^ 1u));
-      bad |= in & (isd ^ 1u) & (sp ^ 1u) & (code == 0u);
-      const uint32_t nv = v * 10u + d;
-      sig = in ? (isd ? sig + (nv != 0u) : 0u) : sig;  // significant digits of the current run
-      ovf |= sig > 9u;
-      v = in ? (isd ? nv : 0u) : v;
-      pd = in ? isd : pd;
-    }
+    for (uint32_t b = 0; b < 4; b++) deb_fast_byte((x >> (8 * b)) & 0xFFu, j + b == sp2, kb, tab, st);
   }
-  if (bad) return FAST_INVALID;
-  if (ovf) return FAST_FALLBACK;  // a run may exceed 32 bits (or clamp at MaxInt64)
+  for (uint32_t j = m & ~3u; j < m; j++) deb_fast_byte(s2[j], j == sp2, kb, tab, st);
+  if (st.bad) return FAST_INVALID;
+  if (st.ovf) return FAST_FALLBACK;  // a run may exceed 32 bits (or clamp at MaxInt64)
+  pos = st.pos;
+  const uint32_t v = st.v;
   // end of the last part, then PART("") when there is no revision
   {
-    const uint32_t k = v ? (39u - uint32_t(__builtin_clz(v))) >> 3 : 0u;
-    const uint32_t vb = k ? v << (32 - 8 * k) : 0u;
+    const uint32_t k = (39u - clz32(v)) >> 3;
+    const uint32_t vb = v << ((32u - 8u * k) & 31u);
     uint8_t* o = kb + (pos < kFastKeyCap ? pos : kFastKeyCap);
     o[0] = uint8_t(DEB_TERM0 + k);
     o[1] = uint8_t(vb >> 24);
