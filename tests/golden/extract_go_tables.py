@@ -46,6 +46,8 @@ FILES = [
     "pkg/result/filter_test.go",
     "pkg/fanal/analyzer/pkg/dpkg/dpkg_test.go",
     "pkg/fanal/analyzer/pkg/apk/apk_test.go",
+    "pkg/fanal/analyzer/pkg/rpm/rpm_test.go",
+    "pkg/fanal/analyzer/pkg/rpm/rpmqa_test.go",
 ]
 
 # trivy-db / trivy constants used in the tables (values from trivy-db pkg/types and
