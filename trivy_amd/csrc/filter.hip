@@ -170,37 +170,64 @@ __global__ __launch_bounds__(kBlock) void rules_insert(RuleDev r, unsigned long 
   }
 }
 
+// Pairs per thread per step of the streaming kernels: every lane issues the loads of kU
+// pairs (coalesced, kBlock apart) before it uses any, so kU gathers of per-package state
+// are in flight together instead of one dependent chain per pair.
+constexpr int kU = 4;
+
 __global__ __launch_bounds__(kBlock) void filter_mark(FilterArgs a) {
-  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
-  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride) {
-    const uint32_t p = a.pkg[i];
-    const uint2 sd = a.side[i];
-    const uint32_t vr = sd.x, sev = sd.y & 0xFFu;
-    // run bounds (the list is grouped by package) and whether the run is ID-sorted
-    if (i == 0 || a.pkg[i - 1] != p) a.run_b[p] = uint32_t(i);
-    else if (a.side[i - 1].x >= vr && !(a.fl[p] & FL_UNS)) set_flag(a.fl, p, FL_UNS);
-    if (i + 1 == a.n || a.pkg[i + 1] != p) a.run_e[p] = uint32_t(i + 1);
-    bool keep = ((a.sev_mask >> sev) & 1u) && !((a.status_mask >> ((sd.y >> 8) & 31u)) & 1u);
-    if (a.kinds & 7u) {  // ignore rules: the smallest precedence is the finding Match returns
-      uint32_t prec = kEmpty;
-      if (keep) {  // severity / status drop first (filter.go:108-114), silently
-        if (a.kinds & (1u << RULE_ALL)) prec = min(prec, rule_find(a, rule_key(RULE_ALL, 0, vr)));
-        if ((a.kinds & (1u << RULE_PKG)) && (a.fl[p] & FL_PKG)) prec = min(prec, rule_find(a, rule_key(RULE_PKG, p, vr)));
-        if (a.kinds & (1u << RULE_CLS)) prec = min(prec, rule_find(a, rule_key(RULE_CLS, a.pkg_class[p], vr)));
-        keep = prec == kEmpty;
-      }
-      a.ign[i] = prec;
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock * kU;
+  const uint64_t n = a.n;
+  for (uint64_t b0 = uint64_t(blockIdx.x) * kBlock * kU; b0 < n; b0 += stride) {
+    uint32_t p[kU], pp[kU], pn[kU], f[kU], dp[kU];
+    uint2 sd[kU];
+    uint32_t vprev[kU];
+#pragma unroll
+    for (int k = 0; k < kU; k++) {
+      const uint64_t i = min(b0 + uint64_t(k) * kBlock + threadIdx.x, n - 1);
+      p[k] = a.pkg[i];
+      sd[k] = a.side[i];
+      pp[k] = i ? a.pkg[i - 1] : 0xFFFFFFFFu;
+      pn[k] = i + 1 < n ? a.pkg[i + 1] : 0xFFFFFFFFu;
+      vprev[k] = i ? a.side[i - 1].x : 0u;
     }
-    a.mkey[i] = keep ? ((4u - sev) << a.id_bits) | vr : kEmpty;
-    if (keep && (a.dup[p] & FL_DUP)) {  // table entries: {key + 1 (0 = empty), max value}, zeroed
-      const unsigned long long key = (uint64_t(a.dkey[p]) << 32) | vr;
-      const unsigned long long val = (uint64_t(a.t.adv_rank[a.adv[i]].y) << 32) | (0xFFFFFFFFu - p);
-      for (uint64_t s = mix64(key) & a.table_mask;; s = (s + 1) & a.table_mask) {
-        const unsigned long long prev = atomicCAS(&a.table[2 * s], 0ull, key + 1);
-        if (prev == 0ull || prev == key + 1) {
-          atomicMax(&a.table[2 * s + 1], val);
-          a.mine[i] = uint32_t(s);
-          break;
+#pragma unroll
+    for (int k = 0; k < kU; k++) {
+      f[k] = a.fl[p[k]];
+      dp[k] = a.dup[p[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < kU; k++) {
+      const uint64_t i = b0 + uint64_t(k) * kBlock + threadIdx.x;
+      if (i >= n) break;
+      const uint32_t pk = p[k];
+      const uint32_t vr = sd[k].x, sev = sd[k].y & 0xFFu;
+      // run bounds (the list is grouped by package) and whether the run is ID-sorted
+      if (pp[k] != pk) a.run_b[pk] = uint32_t(i);
+      else if (vprev[k] >= vr && !(f[k] & FL_UNS)) set_flag(a.fl, pk, FL_UNS);
+      if (pn[k] != pk) a.run_e[pk] = uint32_t(i + 1);
+      bool keep = ((a.sev_mask >> sev) & 1u) && !((a.status_mask >> ((sd[k].y >> 8) & 31u)) & 1u);
+      if (a.kinds & 7u) {  // ignore rules: the smallest precedence is the finding Match returns
+        uint32_t prec = kEmpty;
+        if (keep) {  // severity / status drop first (filter.go:108-114), silently
+          if (a.kinds & (1u << RULE_ALL)) prec = min(prec, rule_find(a, rule_key(RULE_ALL, 0, vr)));
+          if ((a.kinds & (1u << RULE_PKG)) && (f[k] & FL_PKG)) prec = min(prec, rule_find(a, rule_key(RULE_PKG, pk, vr)));
+          if (a.kinds & (1u << RULE_CLS)) prec = min(prec, rule_find(a, rule_key(RULE_CLS, a.pkg_class[pk], vr)));
+          keep = prec == kEmpty;
+        }
+        a.ign[i] = prec;
+      }
+      a.mkey[i] = keep ? ((4u - sev) << a.id_bits) | vr : kEmpty;
+      if (keep && (dp[k] & FL_DUP)) {  // table entries: {key + 1 (0 = empty), max value}, zeroed
+        const unsigned long long key = (uint64_t(a.dkey[pk]) << 32) | vr;
+        const unsigned long long val = (uint64_t(a.t.adv_rank[a.adv[i]].y) << 32) | (0xFFFFFFFFu - pk);
+        for (uint64_t s = mix64(key) & a.table_mask;; s = (s + 1) & a.table_mask) {
+          const unsigned long long prev = atomicCAS(&a.table[2 * s], 0ull, key + 1);
+          if (prev == 0ull || prev == key + 1) {
+            atomicMax(&a.table[2 * s + 1], val);
+            a.mine[i] = uint32_t(s);
+            break;
+          }
         }
       }
     }
@@ -208,56 +235,67 @@ __global__ __launch_bounds__(kBlock) void filter_mark(FilterArgs a) {
 }
 
 __global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
-  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock * kU;
   const uint32_t id_mask = (1u << a.id_bits) - 1u;
   const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t b0 = uint64_t(blockIdx.x) * kBlock; b0 < a.n; b0 += stride) {  // wave-uniform trip count
-    const uint64_t i = b0 + threadIdx.x;
-    const bool valid = i < a.n;
-    uint32_t p = 0xFFFFFFFFu, key = kEmpty;
-    if (valid) {
-      p = a.pkg[i];
-      key = a.mkey[i];
-      if (key != kEmpty) {
-        const uint32_t vr = key & id_mask;
-        const uint32_t f = a.fl[p];
-        const bool dup = f & FL_DUP, uns = f & FL_UNS;
-        // the FixedVersion rank is needed only to dedup (repeating packages, unsorted runs)
-        const uint32_t fr = (dup || uns) ? a.t.adv_rank[a.adv[i]].y : 0u;
-        if (dup && a.table[2 * uint64_t(a.mine[i]) + 1] != ((uint64_t(fr) << 32) | (0xFFFFFFFFu - p)))
-          key = kEmpty;  // another package won the (dedup key, ID): greater FixedVersion or first seen
-        if (key != kEmpty && uns) {  // the package's own pairs of this ID: the first with the greatest FixedVersion
-          const uint32_t rb = a.run_b[p], re = a.run_e[p];
-          for (uint32_t j = rb; j < re; j++) {
-            if (j == uint32_t(i)) continue;
-            const uint32_t kj = a.mkey[j];
-            if (kj == kEmpty || (kj & id_mask) != vr) continue;
-            const uint32_t fj = a.t.adv_rank[a.adv[j]].y;
-            if (fj > fr || (fj == fr && j < uint32_t(i))) {
-              key = kEmpty;
-              break;
+  const uint64_t n = a.n;
+  for (uint64_t b0 = uint64_t(blockIdx.x) * kBlock * kU; b0 < n; b0 += stride) {  // wave-uniform trip count
+    uint32_t pv[kU], kv[kU], fv[kU];
+#pragma unroll
+    for (int k = 0; k < kU; k++) {
+      const uint64_t i = min(b0 + uint64_t(k) * kBlock + threadIdx.x, n - 1);
+      pv[k] = a.pkg[i];
+      kv[k] = a.mkey[i];
+    }
+#pragma unroll
+    for (int k = 0; k < kU; k++) fv[k] = a.fl[pv[k]];
+#pragma unroll
+    for (int k = 0; k < kU; k++) {
+      const uint64_t i = b0 + uint64_t(k) * kBlock + threadIdx.x;
+      const bool valid = i < n;
+      uint32_t p = valid ? pv[k] : 0xFFFFFFFFu, key = valid ? kv[k] : kEmpty;
+      if (valid) {
+        if (key != kEmpty) {
+          const uint32_t vr = key & id_mask;
+          const uint32_t f = fv[k];
+          const bool dup = f & FL_DUP, uns = f & FL_UNS;
+          // the FixedVersion rank is needed only to dedup (repeating packages, unsorted runs)
+          const uint32_t fr = (dup || uns) ? a.t.adv_rank[a.adv[i]].y : 0u;
+          if (dup && a.table[2 * uint64_t(a.mine[i]) + 1] != ((uint64_t(fr) << 32) | (0xFFFFFFFFu - p)))
+            key = kEmpty;  // another package won the (dedup key, ID): greater FixedVersion or first seen
+          if (key != kEmpty && uns) {  // the package's own pairs of this ID: the first with the greatest FixedVersion
+            const uint32_t rb = a.run_b[p], re = a.run_e[p];
+            for (uint32_t j = rb; j < re; j++) {
+              if (j == uint32_t(i)) continue;
+              const uint32_t kj = a.mkey[j];
+              if (kj == kEmpty || (kj & id_mask) != vr) continue;
+              const uint32_t fj = a.t.adv_rank[a.adv[j]].y;
+              if (fj > fr || (fj == fr && j < uint32_t(i))) {
+                key = kEmpty;
+                break;
+              }
             }
           }
+          if (key != kEmpty && (a.kinds & (1u << RULE_VEX)) && (f & FL_VEX) &&
+              rule_find(a, rule_key(RULE_VEX, p, vr)) != kEmpty)
+            key = kEmpty;  // VEX: openvex.go:35-40 / cyclonedx.go:56-60 / csaf.go:36-40 drop it
         }
-        if (key != kEmpty && (a.kinds & (1u << RULE_VEX)) && (f & FL_VEX) &&
-            rule_find(a, rule_key(RULE_VEX, p, vr)) != kEmpty)
-          key = kEmpty;  // VEX: openvex.go:35-40 / cyclonedx.go:56-60 / csaf.go:36-40 drop it
+        a.skey[i] = key;
       }
-      a.skey[i] = key;
-    }
-    // per-package class counters: the head lane of each package run inside the wave adds
-    // the run's members of every class (the list is grouped by package)
-    const uint32_t cls = valid ? pair_class(a, key, i) : kNoClass;
-    const uint32_t prev_p = __shfl_up(p, 1, 64);
-    const bool head = valid && (lane == 0 || prev_p != p);
-    const unsigned long long heads = __ballot(head);
-    const unsigned long long above = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
-    const uint32_t end = above ? uint32_t(__builtin_ctzll(above)) : 64u;
-    const unsigned long long span = (end == 64 ? ~0ull : ((1ull << end) - 1)) & (~0ull << lane);
+      // per-package class counters: the head lane of each package run inside the wave adds
+      // the run's members of every class (the list is grouped by package)
+      const uint32_t cls = valid ? pair_class(a, key, i) : kNoClass;
+      const uint32_t prev_p = __shfl_up(p, 1, 64);
+      const bool head = valid && (lane == 0 || prev_p != p);
+      const unsigned long long heads = __ballot(head);
+      const unsigned long long above = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
+      const uint32_t end = above ? uint32_t(__builtin_ctzll(above)) : 64u;
+      const unsigned long long span = (end == 64 ? ~0ull : ((1ull << end) - 1)) & (~0ull << lane);
 #pragma unroll
-    for (uint32_t c = 0; c < uint32_t(kClasses); c++) {
-      const unsigned long long m = __ballot(cls == c);
-      if (head && (m & span)) atomicAdd(&a.cnt[uint64_t(p) * kClasses + c], uint32_t(__popcll(m & span)));
+      for (uint32_t c = 0; c < uint32_t(kClasses); c++) {
+        const unsigned long long m = __ballot(cls == c);
+        if (head && (m & span)) atomicAdd(&a.cnt[uint64_t(p) * kClasses + c], uint32_t(__popcll(m & span)));
+      }
     }
   }
 }
@@ -491,6 +529,8 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
     return false;
   }
   const uint32_t blocks = uint32_t(std::min<uint64_t>((n + kBlock - 1) / kBlock, 256ull * 64));
+  const uint32_t blocks_u = uint32_t(std::min<uint64_t>((n + kBlock * kU - 1) / (kBlock * kU), 256ull * 32));
+  sev_mask &= 0x1Fu;  // SeverityNames only: a bit for "out of range" (5) would pass a severity 4 - 5 can't order
   const uint64_t np = n_pkgs_;
   // dedup table: 2^k >= 2 x the pairs that can enter it (load <= 0.5, probes end)
   uint64_t tcap = 0;
@@ -613,8 +653,8 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   a.id_bits = id_bits;
   a.out = as<uint2>(bufs_[21]);
   a.iout = as<uint32_t>(bufs_[22]);
-  hipLaunchKernelGGL(filter_mark, dim3(blocks), dim3(kBlock), 0, st, a);
-  hipLaunchKernelGGL(filter_select, dim3(blocks), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(filter_mark, dim3(blocks_u), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(filter_select, dim3(blocks_u), dim3(kBlock), 0, st, a);
   if (!ok(hipGetLastError(), "filter launch", err) ||
       !ok(hipcub::DeviceScan::ExclusiveSum(bufs_[23], scan_bytes, In(Count(0), GroupCount{a.perm, a.cnt, uint32_t(np)}),
                                            as<uint32_t>(bufs_[10]), int(np + 1), st),
