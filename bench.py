@@ -437,8 +437,39 @@ def main():
             found = res.n
             lib().tvm_result_free(ctypes.byref(res))
         c_ms = (time.perf_counter() - t_c) * 1e3 / n_calls
+        # the same call from 8 threads at once (a twirp server / k8s worker pool): the engine
+        # coalesces the queued calls into shared launches (tvm_engine_dropin_stats)
+        import threading
+        st0 = (ctypes.c_uint64 * 3)()
+        lib().tvm_engine_dropin_stats(eng.h, st0)
+        n_thr, per_thr, fails = 8, 200, []
+
+        def caller():
+            r2, e2 = L.Result(), L.errbuf()
+            for _ in range(per_thr):
+                if lib().tvm_ospkg_driver_detect(eng.h, b"debian", b"12", None, arr, len(pk), now, ctypes.byref(r2),
+                                                 e2, len(e2)):
+                    fails.append(e2.value.decode())
+                    return
+                if r2.n != found:
+                    fails.append(f"{r2.n} != {found} vulnerabilities")
+                lib().tvm_result_free(ctypes.byref(r2))
+        ths = [threading.Thread(target=caller) for _ in range(n_thr)]
+        t_c = time.perf_counter()
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        conc_s = time.perf_counter() - t_c
+        if fails:
+            raise RuntimeError(f"concurrent drop-in calls: {fails[:3]}")
+        st1 = (ctypes.c_uint64 * 3)()
+        lib().tvm_engine_dropin_stats(eng.h, st1)
         dropin = {"workload": "c1-shaped: 100 debian-12 packages per call", "c_abi_ms_per_call": c_ms,
-                  "vulnerabilities_per_call": found}
+                  "vulnerabilities_per_call": found,
+                  "concurrent": {"threads": n_thr, "calls": n_thr * per_thr,
+                                 "calls_per_s": n_thr * per_thr / conc_s, "launches": st1[0] - st0[0],
+                                 "calls_sharing_a_launch": st1[2] - st0[2]}}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -142,6 +142,10 @@ void tvm_engine_close(tvm_engine* e);
 /* Atomically replaces the engine's tables (waits for in-flight calls; server hot update). */
 int tvm_engine_swap(tvm_engine* e, tvm_db* db, char* err, size_t errlen);
 uint64_t tvm_engine_table_bytes(const tvm_engine* e);
+/* Drop-in path counters since open/swap: out3 = {launches, calls served, calls that shared
+ * a launch with others}.  Concurrent driver calls (ospkg / library Detect) are coalesced
+ * into one launch per batch of queued calls (twirp server.go:45, k8s scanner.go:141). */
+int tvm_engine_dropin_stats(tvm_engine* e, uint64_t* out3);
 /* Integrity check: re-reads every device table and compares it with the host image. */
 int tvm_engine_verify(tvm_engine* e, char* err, size_t errlen);
 /* Tuning knob: selects the match-kernel variant (tile size / LDS budget); returns the

@@ -157,6 +157,7 @@ _SIG = [
     ("tvm_pipeline_stats", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     ("tvm_version_key", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p,
                                        ctypes.c_size_t]),
+    ("tvm_engine_dropin_stats", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     ("tvm_deb_fast_key_host", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p,
                                              ctypes.c_size_t]),
     ("tvm_db_advisory_vuln_id", ctypes.c_char_p, [_P, ctypes.c_uint32]),

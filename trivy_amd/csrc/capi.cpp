@@ -264,6 +264,13 @@ int tvm_engine_swap(tvm_engine* e, tvm_db* db, char* err, size_t errlen) {
 
 uint64_t tvm_engine_table_bytes(const tvm_engine* e) { return e ? e->eng->table_bytes() : 0; }
 
+int tvm_engine_dropin_stats(tvm_engine* e, uint64_t* out3) {
+  if (!e || !out3) return TVM_EINVAL;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  e->eng->dropin_stats(out3);
+  return TVM_OK;
+}
+
 int tvm_engine_verify(tvm_engine* e, char* err, size_t errlen) {
   if (!e) return TVM_EINVAL;
   std::unique_lock<std::shared_mutex> lk(e->mu);

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <memory>
 #include <cstdint>
 #include <mutex>
 #include <string>
@@ -82,6 +83,8 @@ struct DevBatch {
   uint64_t spill_words = 0;  // scratch for installed keys longer than 32 bytes
   uint32_t gm = 0;           // grammar bits (1 << Cmp) of the batch's platforms (libver.h GM_*)
   uint32_t pkg_base = 0;     // added to the package index of every match (multi-GPU shards)
+  uint64_t* spill = nullptr;  // the batch's own long-key scratch (drop-in contexts); nullptr: the engine's
+  uint64_t spill_cap = 0;
   // probe -> sweep hand-off (device only)
   PkgRec* rec = nullptr;
   uint4* tail = nullptr;  // key bytes 16..31 per package
@@ -137,8 +140,14 @@ class Engine {
   static bool fetch_ordered(const DevMatches& m, uint32_t n_pkgs, uint64_t total, std::vector<uint2>& out,
                             hipStream_t st, std::string& err);
 
-  // Convenience: upload, match, download. out = pairs; err_pkg = first poisoned package or -1.
+  // The drop-in path (one driver Detect call): upload, match, download. out = pairs;
+  // err_pkg = first poisoned package or -1.  Thread-safe: concurrent calls are coalesced
+  // into one launch (the caller that finds no launch running leads and serves every call
+  // queued meanwhile) over pooled device buffers and pinned staging - no per-call
+  // allocation (engine.hip "drop-in path").
   bool match_host(const HostBatch& hb, std::vector<uint2>& out, int64_t& err_pkg, std::string& err);
+  // Drop-in counters: {launches, calls served, calls that shared a launch}.
+  void dropin_stats(uint64_t out[3]);
 
   const DB& db() const { return *db_; }
   const PlatInfo* device_plats() const { return d_.plats; }
@@ -162,8 +171,13 @@ class Engine {
   // per-launch scratch
   uint64_t* spill_ = nullptr;
   uint64_t spill_cap_ = 0;
-  std::mutex call_mu_;  // serialises host-synchronous calls sharing the scratch buffers
   bool ensure_scratch(uint64_t spill_words, std::string& err);
+  struct Dropin;
+  struct DropinReq;
+  std::unique_ptr<Dropin> dropin_;
+  std::mutex dropin_init_mu_;
+  Dropin* dropin(std::string& err);
+  bool dropin_run(Dropin& d, DropinReq* const* reqs, size_t n, std::string& err);
 };
 
 // Kernel variants: count and names (engine.hip; 0 = "auto").

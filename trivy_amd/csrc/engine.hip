@@ -4,6 +4,10 @@
 #include "engine.h"
 
 #include <algorithm>
+#include <mutex>
+#include <memory>
+#include <deque>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 
@@ -154,6 +158,7 @@ void HostBatch::clear() {
 
 Engine::~Engine() {
   if (dev_ >= 0) (void)hipSetDevice(dev_);
+  dropin_.reset();
   for (void* p : allocs_) (void)hipFree(p);
   if (spill_) (void)hipFree(spill_);
   if (stream_) (void)hipStreamDestroy(stream_);
@@ -353,8 +358,8 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
   pa.rec = b.rec + p0;
   pa.tail = b.tail + p0;
   pa.ctl = m.ctl;
-  pa.spill = spill_;
-  pa.spill_cap = spill_cap_;
+  pa.spill = b.spill ? b.spill : spill_;
+  pa.spill_cap = b.spill ? b.spill_cap : spill_cap_;
   const bool fused = kFusedVariant[vi - 1];
   if (!fused) {
     probe_fn(b.gm)(nt, pst, pa);
@@ -367,7 +372,7 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
   sa.db = d_;
   sa.rec = b.rec + p0;
   sa.tail = b.tail + p0;
-  sa.spill = spill_;
+  sa.spill = b.spill ? b.spill : spill_;
   sa.attr = b.attr ? b.attr + p0 : nullptr;
   sa.cpe_bits = b.cpe_bits;
   sa.cpe_words = b.cpe_words;
@@ -396,7 +401,7 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
 
 bool Engine::launch(const DevBatch& b, const DevMatches& m, hipStream_t st, std::string& err) {
   (void)hipSetDevice(dev_);
-  if (!ensure_scratch(b.spill_words, err)) return false;
+  if (!b.spill && !ensure_scratch(b.spill_words, err)) return false;
   if (!hip_ok(hipMemsetAsync(m.ctl, 0, 8 * sizeof(unsigned long long), st), "memset(ctl)", err)) return false;
   if (b.n_tiles == 0) return true;
   // one launch over every tile (cutting the pass into chunks whose probe overlaps the
@@ -404,42 +409,298 @@ bool Engine::launch(const DevBatch& b, const DevMatches& m, hipStream_t st, std:
   return launch_tiles(b, m, 0, b.n_tiles, st, st, nullptr, err);
 }
 
+// ---- drop-in path: pooled buffers + coalescing of concurrent calls -------------------------
+//
+// The reference serves concurrent Detect calls (twirp server, server.go:45; the k8s
+// scanner's worker pool, scanner.go:141) each with its own bbolt read transaction.  Here a
+// call is a small batch (one target), so launches - not bandwidth - bound the rate: calls
+// that arrive while a launch runs queue up, and the next launch serves all of them as one
+// batch (their packages concatenated, pairs handed back by package range).  The first
+// caller that finds no launch running leads; a leader hands over as soon as its own call
+// is served.  Device buffers, pinned staging and the long-key scratch belong to the
+// context and only grow, so a call allocates nothing.  A call whose batch carries package
+// attributes (Red Hat CPE sets, arches) runs in a launch of its own, and a merged launch
+// that meets a poisoned DB key re-runs its calls one by one, so every call sees exactly
+// the error (first poisoned package of ITS batch) it would see alone.
+struct Engine::DropinReq {
+  const HostBatch* hb = nullptr;
+  std::vector<uint2>* out = nullptr;
+  int64_t err_pkg = -1;
+  std::string err;
+  bool ok = false, done = false;
+};
+
+struct Engine::Dropin {
+  int dev = 0;
+  hipStream_t st = nullptr;
+  DevBatch b;  // device buffers at their capacities (the n / n_tiles / gm fields are per launch)
+  uint64_t cap_pk = 0, cap_rec = 0, cap_tail = 0, cap_groups = 0, cap_arena = 0, cap_attr = 0, cap_cpe = 0;
+  uint64_t cap_dir = 0, cap_adv = 0;
+  DevMatches m;
+  uint8_t* pin = nullptr;
+  size_t pin_cap = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<DropinReq*> pending;
+  bool leading = false;
+  uint64_t launches = 0, calls = 0, merged = 0;
+  ~Dropin() {
+    (void)hipSetDevice(dev);
+    for (void* p : {static_cast<void*>(b.pk), static_cast<void*>(b.tile_off), static_cast<void*>(b.arena),
+                    static_cast<void*>(b.attr), static_cast<void*>(b.cpe_bits), static_cast<void*>(b.rec),
+                    static_cast<void*>(b.tail), static_cast<void*>(b.spill), static_cast<void*>(m.pkg),
+                    static_cast<void*>(m.adv), static_cast<void*>(m.dir), static_cast<void*>(m.ctl)})
+      if (p) (void)hipFree(p);
+    if (pin) (void)hipHostFree(pin);
+    if (st) (void)hipStreamDestroy(st);
+  }
+};
+
+Engine::Dropin* Engine::dropin(std::string& err) {
+  std::lock_guard<std::mutex> lk(dropin_init_mu_);
+  if (!dropin_) {
+    (void)hipSetDevice(dev_);
+    auto d = std::make_unique<Dropin>();
+    d->dev = dev_;
+    if (!hip_ok(hipStreamCreateWithFlags(&d->st, hipStreamNonBlocking), "hipStreamCreate(drop-in)", err) ||
+        !dmalloc(&d->m.ctl, 8, "hipMalloc(ctl)", err))
+      return nullptr;
+    dropin_ = std::move(d);
+  }
+  return dropin_.get();
+}
+
+void Engine::dropin_stats(uint64_t out[3]) {
+  std::string e;
+  Dropin* d = dropin(e);
+  if (!d) {
+    out[0] = out[1] = out[2] = 0;
+    return;
+  }
+  std::lock_guard<std::mutex> lk(d->mu);
+  out[0] = d->launches;
+  out[1] = d->calls;
+  out[2] = d->merged;
+}
+
+namespace {
+// Grows a device buffer to at least n elements (contents not kept).
+template <class T>
+bool grow_dev(T*& p, uint64_t& cap, uint64_t n, const char* what, std::string& err) {
+  if (n <= cap && p) return true;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  const uint64_t c = std::max<uint64_t>(n + n / 4, 64);
+  if (!hip_ok(hipMalloc(reinterpret_cast<void**>(&p), c * sizeof(T)), what, err)) {
+    cap = 0;
+    return false;
+  }
+  cap = c;
+  return true;
+}
+}  // namespace
+
+// One launch over the calls reqs[0..n) (n > 1: attribute-free batches, concatenated).
+bool Engine::dropin_run(Dropin& d, DropinReq* const* reqs, size_t n, std::string& err) {
+  (void)hipSetDevice(dev_);
+  HostBatch merged;
+  const HostBatch* hbp = reqs[0]->hb;
+  std::vector<uint32_t> first(n + 1, 0);
+  if (n > 1) {
+    for (size_t k = 0; k < n; k++) {
+      const HostBatch& h = *reqs[k]->hb;
+      first[k] = uint32_t(merged.pk.size());
+      merged.pk.insert(merged.pk.end(), h.pk.begin(), h.pk.end());
+      merged.arena.insert(merged.arena.end(), h.arena.begin(), h.arena.end());
+    }
+    uint64_t o = 0;  // group offsets of the concatenation
+    for (size_t j = 0; j < merged.pk.size(); j++) {
+      if (j % kGroup == 0) merged.tile_off.push_back(o);
+      o += (merged.pk[j].y & 0xFFFFu) + (merged.pk[j].y >> 16);
+    }
+    hbp = &merged;
+  }
+  const HostBatch& hb = *hbp;
+  first[n] = uint32_t(hb.pk.size());
+  DevBatch& b = d.b;
+  b.n = uint32_t(hb.pk.size());
+  b.n_tiles = hb.n_tiles();
+  b.arena_bytes = hb.arena.size();
+  b.gm = grammar_set(hb);
+  b.spill_words = 0;
+  for (const uint2& x : hb.pk) {
+    const uint32_t need = (key_bound_any(x.y >> 16) + 7) / 8;
+    if (need > kKeyWords) b.spill_words += need;
+  }
+  if (!hb.attr.empty() && hb.attr.size() != hb.pk.size()) {
+    err = "batch attributes do not cover every package";
+    return false;
+  }
+  const uint64_t groups = uint64_t(b.n_tiles) * kGroupsPerTile + 1;
+  const uint64_t arena_pad = (hb.arena.size() + 32 + 15) & ~uint64_t(15);
+  if (!grow_dev(b.pk, d.cap_pk, b.n, "hipMalloc(drop-in batch)", err) ||
+      !grow_dev(b.rec, d.cap_rec, b.n, "hipMalloc(drop-in records)", err) ||
+      !grow_dev(b.tail, d.cap_tail, b.n, "hipMalloc(drop-in key tails)", err) ||
+      !grow_dev(b.tile_off, d.cap_groups, groups, "hipMalloc(drop-in group offsets)", err) ||
+      !grow_dev(b.arena, d.cap_arena, arena_pad, "hipMalloc(drop-in arena)", err) ||
+      (!hb.attr.empty() && !grow_dev(b.attr, d.cap_attr, b.n, "hipMalloc(drop-in attr)", err)) ||
+      (b.spill_words && !grow_dev(b.spill, b.spill_cap, b.spill_words, "hipMalloc(drop-in spill)", err)) ||
+      (!hb.cpe_bits.empty() && !grow_dev(b.cpe_bits, d.cap_cpe, hb.cpe_bits.size(), "hipMalloc(drop-in cpe)", err)))
+    return false;
+  // matches: 4 per package to start, the exact count after an overflow
+  uint64_t mcap = std::max<uint64_t>(uint64_t(b.n) * 4, 1024);
+  const uint32_t n_tiles = b.n_tiles;
+  if (!grow_dev(d.m.dir, d.cap_dir, std::max<uint32_t>(n_tiles, 1), "hipMalloc(drop-in tile dir)", err)) return false;
+  d.m.dir_cap = uint32_t(std::min<uint64_t>(d.cap_dir, 0xFFFFFFFFu));
+  // pinned staging: inputs, then the outputs of the same call
+  const size_t in_bytes = b.n * 8 + groups * 8 + hb.arena.size() + hb.attr.size() * 8 + hb.cpe_bits.size() * 4;
+  auto stage = [&](size_t need) {
+    if (need <= d.pin_cap) return true;
+    if (d.pin) (void)hipHostFree(d.pin);
+    d.pin = nullptr;
+    d.pin_cap = 0;
+    const size_t c = need + need / 4 + 4096;
+    if (!hip_ok(hipHostMalloc(reinterpret_cast<void**>(&d.pin), c, hipHostMallocDefault), "hipHostMalloc(drop-in)",
+                err))
+      return false;
+    d.pin_cap = c;
+    return true;
+  };
+  if (!stage(in_bytes + 128)) return false;  // + the control block read back after the launch
+  uint8_t* h = d.pin;
+  size_t at = 0;
+  auto h2d = [&](void* dst, const void* src, size_t bytes, const char* what) {
+    if (!bytes) return true;
+    std::memcpy(h + at, src, bytes);
+    const bool r = hip_ok(hipMemcpyAsync(dst, h + at, bytes, hipMemcpyHostToDevice, d.st), what, err);
+    at += bytes;
+    return r;
+  };
+  std::vector<uint64_t> toff(hb.tile_off);
+  toff.resize(groups, hb.arena.size());
+  b.cpe_words = hb.cpe_words;
+  b.n_cpe_sets = hb.cpe_words ? uint32_t(hb.cpe_bits.size() / hb.cpe_words) : 0;
+  if (!h2d(b.pk, hb.pk.data(), hb.pk.size() * 8, "H2D drop-in batch") ||
+      !h2d(b.tile_off, toff.data(), groups * 8, "H2D drop-in offsets") ||
+      !h2d(b.arena, hb.arena.data(), hb.arena.size(), "H2D drop-in arena") ||
+      !h2d(b.attr, hb.attr.data(), hb.attr.size() * 8, "H2D drop-in attr") ||
+      !h2d(b.cpe_bits, hb.cpe_bits.data(), hb.cpe_bits.size() * 4, "H2D drop-in cpe"))
+    return false;
+  DevBatch bl = b;
+  if (hb.attr.empty()) bl.attr = nullptr;
+  if (hb.cpe_bits.empty()) bl.cpe_bits = nullptr;
+  unsigned long long* ctl = nullptr;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    uint64_t pcap = d.m.cap;
+    if (!grow_dev(d.m.pkg, pcap, mcap, "hipMalloc(drop-in matches)", err) ||
+        !grow_dev(d.m.adv, d.cap_adv, mcap, "hipMalloc(drop-in matches)", err))
+      return false;
+    d.m.cap = std::min(pcap, d.cap_adv);
+    if (!launch(bl, d.m, d.st, err)) return false;
+    ctl = reinterpret_cast<unsigned long long*>(d.pin + ((at + 7) & ~size_t(7)));
+    if (!hip_ok(hipMemcpyAsync(ctl, d.m.ctl, 64, hipMemcpyDeviceToHost, d.st), "D2H ctl", err) ||
+        !hip_ok(hipStreamSynchronize(d.st), "drop-in match", err))
+      return false;
+    if (ctl[3]) {
+      err = "match kernel internal error bits " + std::to_string(ctl[3]);
+      return false;
+    }
+    if (ctl[0] <= d.m.cap) break;
+    mcap = ctl[0];  // output buffer too small: once more with the exact size
+  }
+  const uint64_t total = ctl[0];
+  const uint64_t poisoned = ctl[1];
+  d.launches++;
+  if (poisoned && n > 1) {  // each call alone, so each reports its own first poisoned package
+    for (size_t k = 0; k < n; k++) {
+      DropinReq* r = reqs[k];
+      r->ok = dropin_run(d, &r, 1, r->err);
+    }
+    return true;
+  }
+  // ordered read-back through the pinned buffer: tile directory, then the two columns
+  const size_t out_at = 0;
+  const size_t need = n_tiles * sizeof(TileDir) + total * 8;
+  if (!stage(need)) return false;
+  TileDir* hdir = reinterpret_cast<TileDir*>(d.pin + out_at);
+  uint32_t* hp = reinterpret_cast<uint32_t*>(d.pin + out_at + n_tiles * sizeof(TileDir));
+  uint32_t* ha = hp + total;
+  if ((n_tiles && !hip_ok(hipMemcpyAsync(hdir, d.m.dir, n_tiles * sizeof(TileDir), hipMemcpyDeviceToHost, d.st),
+                          "D2H dir", err)) ||
+      (total && (!hip_ok(hipMemcpyAsync(hp, d.m.pkg, total * 4, hipMemcpyDeviceToHost, d.st), "D2H matches", err) ||
+                 !hip_ok(hipMemcpyAsync(ha, d.m.adv, total * 4, hipMemcpyDeviceToHost, d.st), "D2H matches", err))) ||
+      !hip_ok(hipStreamSynchronize(d.st), "D2H matches", err))
+    return false;
+  for (size_t k = 0; k < n; k++) {
+    reqs[k]->out->clear();
+    reqs[k]->err_pkg = -1;
+    reqs[k]->ok = true;
+  }
+  if (poisoned) reqs[0]->err_pkg = int64_t(b.n - poisoned);  // n == 1 here
+  size_t k = 0;
+  for (uint32_t t = 0; t < n_tiles; t++)
+    for (uint64_t i = hdir[t].base; i < hdir[t].base + hdir[t].count; i++) {
+      const uint32_t p = hp[i];
+      while (p >= first[k + 1]) k++;  // packages ascend along the tile order
+      reqs[k]->out->push_back(make_uint2(p - first[k], ha[i]));
+    }
+  return true;
+}
+
 bool Engine::match_host(const HostBatch& hb, std::vector<uint2>& out, int64_t& err_pkg, std::string& err) {
   out.clear();
   err_pkg = -1;
   if (hb.pk.empty()) return true;
-  std::lock_guard<std::mutex> lk(call_mu_);
-  DevBatch b;
-  if (!upload(hb, b, err)) {
-    free_batch(b);
-    return false;
-  }
-  uint64_t cap = std::max<uint64_t>(hb.pk.size() * 4, 1024);
-  bool ok = true;
-  for (int attempt = 0; attempt < 2 && ok; attempt++) {
-    DevMatches m;
-    ok = alloc_matches(cap, b.n, m, err) && launch(b, m, stream_, err);
-    unsigned long long ctl[8] = {0};
-    if (ok) ok = hip_ok(hipMemcpyAsync(ctl, m.ctl, sizeof(ctl), hipMemcpyDeviceToHost, stream_), "D2H ctl", err) &&
-                 hip_ok(hipStreamSynchronize(stream_), "match kernels", err);
-    if (ok && ctl[3]) {
-      err = "match kernel internal error bits " + std::to_string(ctl[3]);
-      ok = false;
-    }
-    if (ok && ctl[0] > cap) {  // output buffer too small: rerun with the exact size
-      cap = ctl[0];
-      free_matches(m);
+  Dropin* dp = dropin(err);
+  if (!dp) return false;
+  Dropin& d = *dp;
+  DropinReq r;
+  r.hb = &hb;
+  r.out = &out;
+  std::unique_lock<std::mutex> lk(d.mu);
+  d.pending.push_back(&r);
+  d.calls++;
+  while (!r.done) {
+    if (d.leading) {
+      d.cv.wait(lk);
       continue;
     }
-    if (ok) {
-      err_pkg = ctl[1] ? int64_t(b.n - ctl[1]) : -1;
-      ok = fetch_ordered(m, b.n, ctl[0], out, stream_, err);
+    d.leading = true;  // lead: serve queued calls until this one is done
+    while (!r.done && !d.pending.empty()) {
+      std::vector<DropinReq*> grp;
+      const bool attrs = !d.pending.front()->hb->attr.empty() || !d.pending.front()->hb->cpe_bits.empty();
+      uint64_t pk = 0;
+      for (auto it = d.pending.begin(); it != d.pending.end();) {
+        const HostBatch* h = (*it)->hb;
+        const bool a = !h->attr.empty() || !h->cpe_bits.empty();
+        if ((attrs || a) && !grp.empty()) break;  // a call with attributes runs alone
+        if (!grp.empty() && pk + h->pk.size() > (1u << 22)) break;
+        grp.push_back(*it);
+        pk += h->pk.size();
+        it = d.pending.erase(it);
+        if (attrs) break;
+      }
+      if (grp.size() > 1) d.merged += grp.size();
+      lk.unlock();
+      std::string e;
+      if (!dropin_run(d, grp.data(), grp.size(), e))
+        for (DropinReq* q : grp) {
+          q->ok = false;
+          q->err = e;
+        }
+      lk.lock();
+      for (DropinReq* q : grp) q->done = true;
+      d.cv.notify_all();
     }
-    free_matches(m);
-    break;
+    d.leading = false;
+    d.cv.notify_all();  // a waiting caller takes over the queue
   }
-  free_batch(b);
-  return ok;
+  if (!r.ok) {
+    err = r.err;
+    return false;
+  }
+  err_pkg = r.err_pkg;
+  return true;
 }
 
 bool Engine::verify(std::string& err) {

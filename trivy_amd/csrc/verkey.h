@@ -394,7 +394,6 @@ TVM_HD uint32_t deb_fast_key(const uint8_t* s, uint32_t n, uint8_t* kb, const ui
   const bool has_rev = dash < n && dash >= r0;
   if (r0 >= (has_rev ? dash : n) || uint32_t(s[r0]) - '0' >= 10u) return FAST_INVALID;
   if (has_rev && lcolon < n && lcolon > dash) return FAST_INVALID;
-  const uint32_t split = has_rev ? dash : 0xFFFFFFFFu;
   // EPOCH
   const uint32_t ke = epoch ? (39u - uint32_t(__builtin_clz(epoch))) >> 3 : 0u;
   const uint32_t eb = ke ? epoch << (32 - 8 * ke) : 0u;
