@@ -133,6 +133,7 @@ class Mix:
             "c4": (sm.C4_PLATS, sm.C4_WEIGHTS, 20_000, 100_000_000),
             "c5": (sm.C5_PLATS, sm.C5_WEIGHTS, 12_000, 20_000_000)}[which]
         n = args.packages or n
+        self.which, self.kpp = which, kpp
         self.sdb = sm.make_mix_db(plats, kpp)
         self.batch = sm.make_mix_batch(self.sdb, n, weights, seed=2)
         kind = {"c3": "lang", "c4": "os+lang", "c5": "rpm-apk"}[which]
@@ -192,36 +193,62 @@ class Mix:
             self.sm.add_slice(mb, self.sdb, p, g, lo, hi)
 
     def cpu_baseline(self, budget_s, threads):
-        import oracle.drivers as od
-        import oracle.library as ol
-        sm = self.sm
-        per, n_done, dt = 200, 0, 0.0
-        while dt < budget_s:
-            for p, g in self.batch.groups:
-                bucket, kind = self.sdb.plats[p]
-                idx = np.arange(min(per, len(g["key"])))
-                pkgs = sm.driver_packages(self.sdb, p, g, idx)
-                roots = sm.C3_ROOTS.get(kind, [bucket])
-                recs = od.Records(self.sdb.records_for({r: {x["Name"] for x in pkgs} for r in roots}))
+        """The oracle drivers (Python) in `threads` worker processes, each over its own seeded
+        sample batch of the same DB and generator; processes are spawned (fresh
+        interpreters: nothing GPU-side is inherited) and time only their detection loops."""
+        import multiprocessing as mp
+        from concurrent.futures import ProcessPoolExecutor
+        with ProcessPoolExecutor(threads, mp_context=mp.get_context("spawn")) as ex:
+            res = list(ex.map(_mix_cpu_worker, [(self.which, self.kpp, 1000 + w, budget_s) for w in range(threads)]))
+        done = sum(r[0] for r in res)
+        rate = sum(r[0] / r[1] for r in res)
+        return {"value": rate, "unit": "packages/s", "cores": threads, "kind": "port",
+                "sample": f"{done} packages over {threads} processes (each: a seeded 20k-package sample batch of "
+                          f"the same DB, first rows of every platform group), oracle/drivers.py + oracle/library.py "
+                          f"per-driver Detect, ~{budget_s:.0f}s per process (Python)"}
+
+
+def _mix_detect_loop(sm, sdb, batch, budget_s):
+    """Packages detected and seconds spent by the oracle drivers over the first rows of every
+    platform group (doubling) until budget_s of detection time is spent."""
+    import oracle.drivers as od
+    import oracle.library as ol
+    per, n_done, dt = 200, 0, 0.0
+    while dt < budget_s:
+        for p, g in batch.groups:
+            bucket, kind = sdb.plats[p]
+            idx = np.arange(min(per, len(g["key"])))
+            pkgs = sm.driver_packages(sdb, p, g, idx)
+            roots = sm.C3_ROOTS.get(kind, [bucket])
+            recs = od.Records(sdb.records_for({r: {x["Name"] for x in pkgs} for r in roots}))
+            t = time.perf_counter()
+            if kind in sm.LANG_OF:
+                ol.detect(recs, sm.LANG_OF[kind], pkgs)
+            elif kind == "redhat":
+                recs = od.Records(sdb.records_for({"Red Hat": {g["name"][i].decode() for i in idx},
+                                                   "Red Hat CPE": {"repository", "nvr", "cpe"}}))
                 t = time.perf_counter()
-                if kind in sm.LANG_OF:
-                    ol.detect(recs, sm.LANG_OF[kind], pkgs)
-                elif kind == "redhat":
-                    recs = od.Records(self.sdb.records_for({"Red Hat": {g["name"][i].decode() for i in idx},
-                                                            "Red Hat CPE": {"repository", "nvr", "cpe"}}))
-                    t = time.perf_counter()
-                    for rel in (7, 8, 9):
-                        od.driver_detect("redhat", str(rel), None,
-                                         [pk for pk, i in zip(pkgs, idx) if int(g["rhrel"][i]) == rel], recs, None)
-                else:
-                    fam, fmt = sm.DRIVER_OF[kind]
-                    od.driver_detect(fam, fmt.format(bucket.split(" ")[-1]), None, pkgs, recs, None)
-                dt += time.perf_counter() - t
-                n_done += len(idx)
-            per *= 2
-        return {"value": n_done / dt, "unit": "packages/s", "cores": 1, "kind": "port",
-                "sample": f"{n_done} packages (first rows of every platform group), oracle/drivers.py + "
-                          f"oracle/library.py per-driver Detect, 1 thread, {dt:.1f}s (Python)"}
+                for rel in (7, 8, 9):
+                    od.driver_detect("redhat", str(rel), None,
+                                     [pk for pk, i in zip(pkgs, idx) if int(g["rhrel"][i]) == rel], recs, None)
+            else:
+                fam, fmt = sm.DRIVER_OF[kind]
+                od.driver_detect(fam, fmt.format(bucket.split(" ")[-1]), None, pkgs, recs, None)
+            dt += time.perf_counter() - t
+            n_done += len(idx)
+        per *= 2
+    return n_done, dt
+
+
+def _mix_cpu_worker(job):
+    which, kpp, seed, budget_s = job
+    sys.path.insert(0, ROOT)
+    from tools import synth_mix as sm
+    plats, weights = {"c3": (sm.C3_PLATS, sm.C3_WEIGHTS), "c4": (sm.C4_PLATS, sm.C4_WEIGHTS),
+                      "c5": (sm.C5_PLATS, sm.C5_WEIGHTS)}[which]
+    sdb = sm.make_mix_db(plats, kpp)
+    batch = sm.make_mix_batch(sdb, 20000, weights, seed=seed)
+    return _mix_detect_loop(sm, sdb, batch, budget_s)
 
 
 def pmc_traffic(cfg_name):
@@ -476,7 +503,7 @@ def main():
         # the box's CPU share: OMP_NUM_THREADS is set to it there (os.cpu_count() shows the
         # whole machine, whose other cores belong to other jobs)
         threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", 0) or 0) or os.cpu_count() or 1
-        cpu = wl.cpu_baseline(args.cpu_seconds, threads if args.config == "c2" else 1)
+        cpu = wl.cpu_baseline(args.cpu_seconds, threads)
 
     traffic = pmc_traffic(wl.name)
     if rank == 0:

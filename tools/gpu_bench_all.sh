@@ -1,6 +1,7 @@
 #!/bin/bash
 # Bench lines for every workload (run on the GPU box via gpurun): C2 (headline, with the
-# CPU baseline), then the C3 language-package and C5 rpm/apk mixes.
+# CPU baseline), then the C3 language-package, C5 rpm/apk and C4 mixed OS+language (one
+# GPU's 12.5M-package share) mixes.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
@@ -12,4 +13,5 @@ run() {  # name, limit, args...
   cat $OUT/bench_$name.json; tail -3 $OUT/bench_$name.err
   return $rc
 }
-run c2 400 ${C2_ARGS:-} && run c3 300 --config c3 --cpu-seconds 5 && run c5 500 --config c5 --cpu-seconds 5
+run c2 400 ${C2_ARGS:-} && run c3 300 --config c3 --cpu-seconds 5 && run c5 500 --config c5 --cpu-seconds 5 &&
+  run c4 600 --config c4 --packages 12500000 --cpu-seconds 5
