@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Harvest the SBOM-scan vectors of the reference's integration tests (DATA).
 
-TEST INFRASTRUCTURE.  integration/sbom_test.go:30-82 scans three CycloneDX SBOMs
+TEST INFRASTRUCTURE.  integration/sbom_test.go:30-153 scans three CycloneDX SBOMs and the centos-7 image again as an
+in-toto attestation, SPDX tag-value and SPDX JSON
 (integration/testdata/fixtures/sbom/*, copied as data to tests/golden/sbom/) against the
 integration DB (integration/testdata/fixtures/db, converted to
 tests/golden/fixtures/integration/) and compares with integration/testdata/*.json.golden.
@@ -18,7 +19,11 @@ FIELDS = ["VulnerabilityID", "PkgID", "PkgName", "InstalledVersion", "FixedVersi
 CASES = [("centos7 cyclonedx", "centos-7-cyclonedx.json", "centos-7.json.golden"),
          ("fluentd-multiple-lockfiles cyclonedx", "fluentd-multiple-lockfiles-cyclonedx.json",
           "fluentd-multiple-lockfiles.json.golden"),
-         ("minikube KBOM", "minikube-kbom.json", "minikube-kbom.json.golden")]
+         ("minikube KBOM", "minikube-kbom.json", "minikube-kbom.json.golden"),
+         # integration/sbom_test.go:84-153: the same image as in-toto, SPDX tag-value, SPDX JSON
+         ("centos7 in in-toto attestation", "centos-7-cyclonedx.intoto.jsonl", "centos-7.json.golden"),
+         ("centos7 spdx tag-value", "centos-7-spdx.txt", "centos-7.json.golden"),
+         ("centos7 spdx json", "centos-7-spdx.json", "centos-7.json.golden")]
 
 
 def main(ref="/root/reference"):

@@ -1,6 +1,7 @@
 """SBOM decode (trivy_amd/sbom.py, mirror of pkg/sbom) pinned by the reference's SBOM
-integration tests (integration/sbom_test.go:30-82): the three CycloneDX SBOMs decoded and
-run through the detectors must give every golden's detector-produced vulnerabilities.
+integration tests (integration/sbom_test.go:30-153): the three CycloneDX SBOMs, and the
+centos-7 image as an in-toto attestation, SPDX tag-value and SPDX JSON, decoded and run
+through the detectors must give every golden's detector-produced vulnerabilities.
 
 CPU: decode + the oracle's detectors (oracle/drivers.py, oracle/library.py).
 GPU: decode + the product detectors over the C-ABI (the `trivy sbom` path end to end)."""
@@ -23,7 +24,7 @@ NOW = int(datetime.datetime(2021, 8, 25, 12, 20, 30, tzinfo=datetime.timezone.ut
 
 
 def _decode(case):
-    return ts.decode_cyclonedx(open(os.path.join(HERE, "sbom", case["sbom"])).read())
+    return ts.decode(open(os.path.join(HERE, "sbom", case["sbom"])).read())
 
 
 def _check(case, got):
@@ -105,3 +106,49 @@ def test_sbom_scan_on_gpu(case):
     for cls, typ, _target, vulns in ts.scan(eng, d, now=NOW):
         got.setdefault((cls, typ), []).extend(vulns)
     _check(case, got)
+
+
+def test_spdx_rules():
+    """unmarshal.go details: type by SPDXID prefix, purl only from PACKAGE-MANAGER/purl refs,
+    "built package from:" source (rpm epoch:version-release), DESCRIBES skipped, edges only
+    between packages, the Trivy-legacy application (path in sourceInfo, type in name),
+    multi-line <text> values."""
+    tv = """SPDXVersion: SPDX-2.3
+SPDXID: SPDXRef-DOCUMENT
+Creator: Tool: trivy-0.40
+PackageName: alma
+SPDXID: SPDXRef-OperatingSystem-1
+PackageVersion: 9.2
+PackageName: z
+SPDXID: SPDXRef-Package-1
+PackageVersion: 1.2
+PackageSourceInfo: <text>built package from: zsrc 3:1.2-3.el9</text>
+ExternalRef: SECURITY cpe23Type cpe:2.3:a:z:z:1.2
+ExternalRef: PACKAGE-MANAGER purl pkg:rpm/alma/z@1.2-3.el9?arch=x86_64
+PackageAttributionText: <text>PkgID: z@1.2-3.el9.x86_64</text>
+PackageName: gomod
+SPDXID: SPDXRef-Application-1
+PackageSourceInfo: app/go.mod
+PackageName: x
+SPDXID: SPDXRef-Package-2
+PackageVersion: 1.0.0
+ExternalRef: PACKAGE-MANAGER purl pkg:golang/github.com/o/x@1.0.0
+FileName: app/go.mod
+SPDXID: SPDXRef-File-1
+Relationship: SPDXRef-DOCUMENT DESCRIBES SPDXRef-OperatingSystem-1
+Relationship: SPDXRef-OperatingSystem-1 CONTAINS SPDXRef-Package-1
+Relationship: SPDXRef-Application-1 DEPENDS_ON SPDXRef-Package-2
+Relationship: SPDXRef-Application-1 CONTAINS SPDXRef-File-1
+"""
+    d = ts.decode(tv)
+    assert d["OS"] == {"Family": "alma", "Name": "9.2"} and d["Root"]["name"] == "alma"
+    (z,) = d["Packages"]
+    assert (z["Name"], z["Version"], z["Release"], z["ID"]) == ("z", "1.2", "3.el9", "z@1.2-3.el9.x86_64")
+    assert (z["SrcName"], z["SrcEpoch"], z["SrcVersion"], z["SrcRelease"]) == ("zsrc", 3, "1.2", "3.el9")
+    (app,) = d["Applications"]
+    assert app["Type"] == "gomod" and app["FilePath"] == "app/go.mod"
+    assert [lib["Name"] for lib in app["Libraries"]] == ["x"]  # pkgName: the SPDX name (no group)
+    with pytest.raises(ts.SBOMError):
+        ts.decode("not an sbom")
+    with pytest.raises(ts.SBOMError):
+        ts.decode_intoto('{"payloadType": "text/plain", "payload": ""}')

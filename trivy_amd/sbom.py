@@ -166,7 +166,11 @@ def _library(c):
             pkg.setdefault("Layer", {})["DiffID"] = v
     pkg["Identifier"] = {"PURL": c["purl_str"], "BOMRef": c["bom_ref"]}
     pkg["_purl"] = p
-    if purl_class(p) == "os-pkgs":  # fillSrcPkg (the component carries no SrcVersion of its own)
+    if purl_class(p) == "os-pkgs":  # fillSrcPkg (decode.go:260-279)
+        if c.get("src_name") and not pkg.get("SrcName"):  # an SPDX "built package from" source
+            pkg["SrcName"] = c["src_name"]
+        if c.get("src_version"):  # parseSrcVersion (decode.go:282-301)
+            _parse_src_version(pkg, p["type"], c["src_version"])
         if not pkg.get("SrcName"):
             pkg["SrcName"] = pkg["Name"]
         if not pkg.get("SrcVersion"):
@@ -176,6 +180,18 @@ def _library(c):
         if not pkg.get("SrcEpoch"):
             pkg["SrcEpoch"] = pkg.get("Epoch", 0)
     return pkg
+
+
+def _parse_src_version(pkg, typ, ver):
+    if typ == "rpm":  # go-rpm-version NewVersion: Atoi(epoch) before the first ':', release after the first '-'
+        e, sep, rest = ver.partition(":")
+        epoch, v = (int(e) if e.lstrip("+-").isdigit() else 0, rest) if sep else (0, ver)
+        v, _, rel = v.partition("-")
+        pkg["SrcEpoch"], pkg["SrcVersion"], pkg["SrcRelease"] = epoch, v, rel
+    elif typ == "deb":  # go-deb-version NewVersion; a parse error leaves the package as it is
+        from .dpkg import deb_split, deb_valid
+        if deb_valid(ver):
+            pkg["SrcEpoch"], pkg["SrcVersion"], pkg["SrcRelease"] = deb_split(ver)
 
 
 def _sort_pkgs(pkgs):
@@ -201,6 +217,10 @@ def _decode(text):
         bom = json.loads(text)
     except ValueError as e:
         raise SBOMError("failed to decode CycloneDX JSON: %s" % e)
+    return _decode_cdx(bom)
+
+
+def _decode_cdx(bom):
     comps, order = {}, []
     for c in bom.get("components") or []:
         try:
@@ -222,10 +242,18 @@ def _decode(text):
     for d in bom.get("dependencies") or []:
         if d.get("ref") in comps:
             rels[id(comps[d["ref"]])] = [comps[x] for x in d.get("dependsOn") or [] if x in comps]
+    return _decode_bom_meta(order, root, rels, bom.get("serialNumber", ""), bom.get("version", 0))
 
+
+def _decode_bom(order, root, rels):
+    """io/decode.go Decoder.Decode over the format-neutral BOM: components in document
+    order, the root, and relationships {id(parent): [child components]}."""
+    return _decode_bom_meta(order, root, rels, "", 0)
+
+
+def _decode_bom_meta(order, root, rels, serial, version):
     os_c, apps, pkgs = None, {}, {}
-    out = {"OS": None, "Packages": [], "Applications": [], "Root": root,
-           "SerialNumber": bom.get("serialNumber", ""), "Version": bom.get("version", 0)}
+    out = {"OS": None, "Packages": [], "Applications": [], "Root": root, "SerialNumber": serial, "Version": version}
     for c in order:
         if c["type"] == "operating-system":
             if os_c is not None:
@@ -265,6 +293,181 @@ def _decode(text):
     for p in out["Packages"] + [lib for a in out["Applications"] for lib in a["Libraries"]]:
         p.pop("_purl", None)
     return out
+
+
+# ---- SPDX (pkg/sbom/spdx/unmarshal.go) and in-toto attestations (pkg/sbom/sbom.go) ----------------
+SPDX_PURL_CATEGORIES = {"PACKAGE-MANAGER", "PACKAGE_MANAGER"}  # SPDX 2.3 / 2.2 spelling of the category
+
+
+def _spdx_id(x):
+    """tools-golang ElementID: the identifier without its "SPDXRef-" prefix."""
+    return x[len("SPDXRef-"):] if x.startswith("SPDXRef-") else x
+
+
+def _spdx_components(doc):
+    """unmarshal.go: packages -> components (type from the SPDXID prefix, PURL from the
+    PACKAGE-MANAGER purl reference, "built package from:" source, attribution texts as
+    properties, the Trivy-legacy application form), the DESCRIBES target as root, every
+    other relationship between two packages as an edge.  doc: {"creators", "packages":
+    [{SPDXID, name, version, sourceInfo, purls: [(category, type, locator)], attributions}],
+    "relationships": [(a, type, b)]}."""
+    trivy = any(c.startswith("Tool: trivy") for c in doc["creators"])
+    root_id = next((_spdx_id(b) for a, t, b in doc["relationships"] if _spdx_id(a) == "DOCUMENT" and t == "DESCRIBES"),
+                   None)
+    comps, order = {}, []
+    root = None
+    for sp in doc["packages"]:
+        sid = _spdx_id(sp["SPDXID"])
+        typ = ("operating-system" if sid.startswith("OperatingSystem") else
+               "application" if sid.startswith("Application") else "library")
+        c = {"type": typ, "name": sp.get("name", ""), "group": "", "version": sp.get("version", ""), "bom_ref": "",
+             "purl": None, "purl_str": "", "props": []}
+        for cat, rtype, loc in sp.get("purls") or []:
+            if rtype == "purl" and cat in SPDX_PURL_CATEGORIES:
+                c["purl"], c["purl_str"] = parse_purl(loc), loc
+                break
+        src = sp.get("sourceInfo", "")
+        if src.startswith("built package from"):
+            src = src[len("built package from: "):] if src.startswith("built package from: ") else src
+            c["src_name"], _, c["src_version"] = src.partition(" ")
+        for at in sp.get("attributions") or []:
+            k, sep, v = at.partition(": ")
+            if sep:
+                c["props"].append((k, v))
+        if trivy and typ == "application" and sp.get("sourceInfo"):  # older Trivy: path in sourceInfo, type in name
+            c["name"] = sp["sourceInfo"]
+            c["props"].append(("Type", sp.get("name", "")))
+        comps[sid] = c
+        order.append(c)
+        if sid == root_id:
+            root = c
+    rels = {}
+    for a, t, b in doc["relationships"]:
+        if t in ("DESCRIBES", "DESCRIBE"):
+            continue
+        ca, cb = comps.get(_spdx_id(a)), comps.get(_spdx_id(b))
+        if ca is not None and cb is not None:
+            rels.setdefault(id(ca), []).append(cb)
+    return order, root, rels
+
+
+def decode_spdx_json(text):
+    """SPDX JSON (spdx/unmarshal.go UnmarshalJSON) -> the same result as decode_cyclonedx."""
+    try:
+        d = json.loads(text)
+    except ValueError as e:
+        raise SBOMError("failed to load spdx json: %s" % e)
+    doc = {"creators": (d.get("creationInfo") or {}).get("creators") or [], "packages": [], "relationships": []}
+    for p in d.get("packages") or []:
+        doc["packages"].append({
+            "SPDXID": p.get("SPDXID", ""), "name": p.get("name", ""), "version": p.get("versionInfo", ""),
+            "sourceInfo": p.get("sourceInfo", ""), "attributions": p.get("attributionTexts") or [],
+            "purls": [(r.get("referenceCategory", ""), r.get("referenceType", ""), r.get("referenceLocator", ""))
+                      for r in p.get("externalRefs") or []]})
+    for r in d.get("relationships") or []:
+        doc["relationships"].append((r.get("spdxElementId", ""), r.get("relationshipType", ""),
+                                     r.get("relatedSpdxElement", "")))
+    order, root, rels = _spdx_components(doc)
+    return _decode_bom(order, root, rels)
+
+
+def _tv_pairs(text):
+    """SPDX tag-value: (tag, value) per line; <text>...</text> values span lines."""
+    lines = text.split("\n")
+    i = 0
+    while i < len(lines):
+        line = lines[i].rstrip("\r")
+        i += 1
+        if not line.strip() or line.lstrip().startswith("#"):
+            continue
+        tag, sep, val = line.partition(":")
+        if not sep:
+            raise SBOMError("failed to load tag-value spdx: invalid line %d" % i)
+        val = val.strip()
+        if val.startswith("<text>"):
+            val = val[len("<text>"):]
+            while "</text>" not in val and i < len(lines):
+                val += "\n" + lines[i].rstrip("\r")
+                i += 1
+            val = val.split("</text>", 1)[0]
+        yield tag.strip(), val
+
+
+def decode_spdx_tv(text):
+    """SPDX tag-value (spdx/unmarshal.go TVDecoder) -> the same result as decode_cyclonedx."""
+    doc = {"creators": [], "packages": [], "relationships": []}
+    cur = None
+    for tag, val in _tv_pairs(text):
+        if tag == "Creator":
+            doc["creators"].append(val)
+        elif tag == "PackageName":
+            cur = {"SPDXID": "", "name": val, "version": "", "sourceInfo": "", "attributions": [], "purls": []}
+            doc["packages"].append(cur)
+        elif tag in ("FileName", "SnippetSPDXID"):
+            cur = None  # a file / snippet section: its SPDXID is not a package's
+        elif tag == "SPDXID" and cur is not None and not cur["SPDXID"]:
+            cur["SPDXID"] = val
+        elif cur is not None and tag == "PackageVersion":
+            cur["version"] = val
+        elif cur is not None and tag == "PackageSourceInfo":
+            cur["sourceInfo"] = val
+        elif cur is not None and tag == "PackageAttributionText":
+            cur["attributions"].append(val)
+        elif cur is not None and tag == "ExternalRef":
+            f = val.split(None, 2)
+            if len(f) == 3:
+                cur["purls"].append((f[0], f[1], f[2]))
+        elif tag == "Relationship":
+            f = val.split()
+            if len(f) >= 3:
+                doc["relationships"].append((f[0], f[1], f[2]))
+    order, root, rels = _spdx_components(doc)
+    return _decode_bom(order, root, rels)
+
+
+def decode_intoto(text):
+    """An in-toto attestation of a CycloneDX BOM in a DSSE envelope (sbom.go
+    decodeAttestCycloneDXJSONFormat + attestation.Statement.UnmarshalJSON): the first line."""
+    import base64
+    line = text.strip().split("\n", 1)[0]
+    try:
+        env = json.loads(line)
+    except ValueError as e:
+        raise SBOMError("failed to decode as a dsse envelope: %s" % e)
+    if env.get("payloadType") != "application/vnd.in-toto+json":
+        raise SBOMError("invalid attestation payload type: %s" % env.get("payloadType"))
+    try:
+        st = json.loads(base64.b64decode(env.get("payload", ""), validate=True))
+    except (ValueError, TypeError) as e:
+        raise SBOMError("failed to decode attestation payload: %s" % e)
+    if st.get("predicateType") not in ("https://cyclonedx.org/bom", "https://cyclonedx.org/schema"):
+        raise SBOMError("unsupported predicate type: %s" % st.get("predicateType"))
+    pred = st.get("predicate")
+    if not isinstance(pred, dict):
+        raise SBOMError("no predicate")
+    if "Data" in pred:  # legacy cosign predicate: {"Data": <BOM>}
+        pred = pred["Data"] if isinstance(pred["Data"], dict) else json.loads(pred["Data"])
+    return _decode_cdx(pred)
+
+
+def decode(text):
+    """sbom.go DetectFormat + Decode for the formats above."""
+    s = text.lstrip()
+    if s.startswith("{"):
+        try:
+            d = json.loads(s.split("\n", 1)[0]) if s.count("\n") and s.split("\n", 1)[0].rstrip().endswith("}") \
+                else json.loads(s)
+        except ValueError:
+            d = json.loads(s)
+        if d.get("bomFormat") == "CycloneDX":
+            return decode_cyclonedx(text)
+        if str(d.get("spdxVersion", "")).startswith("SPDX-"):
+            return decode_spdx_json(text)
+        if "payloadType" in d:
+            return decode_intoto(text)
+    elif s.startswith("SPDX"):
+        return decode_spdx_tv(text)
+    raise SBOMError("failed to detect SBOM format")
 
 
 def scan(engine, sbom, artifact_name="", now=None):
