@@ -91,7 +91,9 @@ struct alignas(16) RowAux {
 };
 //   AUX_CLASS     library rows: pass if bit <installed version class> of `tag` is set
 //                 (libver.h classes: npm pre-release, PEP 440 local/pre/post).
-enum : uint32_t { AUX_ARCH_RH = 1, AUX_ARCH_IN = 2, AUX_CPE = 4, AUX_TAG = 8, AUX_CLASS = 16 };
+//   AUX_MVN       Maven library rows: the advisory's IsVulnerable program at aux_ids[list_off]
+//                 evaluated pairwise against the installed version (libver.h mvn_program_eval).
+enum : uint32_t { AUX_ARCH_RH = 1, AUX_ARCH_IN = 2, AUX_CPE = 4, AUX_TAG = 8, AUX_CLASS = 16, AUX_MVN = 32 };
 
 // Package attributes (uint2 per package, only for batches that carry filtered rows):
 // x = arch id | PA_NOARCH, y = ksplice tag (oracle) or CPE-set id (redhat).

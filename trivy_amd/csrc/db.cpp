@@ -515,6 +515,27 @@ void DB::flatten_os(uint32_t plat, const Bucket& root, int32_t ds) {
 // Advisory -> interval row(s) of its driver (SURVEY.md §8a' "unfixed" and parse-error
 // columns).  Returns false when the advisory can never be reported (no row).
 bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::vector<uint8_t>& kb) {
+  if (P.drv == DRV_LIBRARY && P.cmp == CMP_MAVEN) {
+    // Maven: ComparableVersion is not an order, so no interval set can
+    // stand for IsVulnerable; the row carries the advisory's program (AUX_MVN) and the
+    // kernel evaluates it pairwise against the installed version
+    std::vector<uint32_t> w;
+    const MvnProgState st = mvn_program(a.vulnerable, a.patched, a.unaffected, w);
+    if (st == MVN_NEVER) return false;
+    Row r{};
+    r.lo_len = r.hi_len = KEY_INF;
+    RowAux x{};
+    r.adv = ai | (st == MVN_ALWAYS ? ROW_ALWAYS : ROW_FILTER);
+    if (st == MVN_PROGRAM) {
+      x.kind = AUX_MVN;
+      x.list_off = uint32_t(aux_ids.size());
+      aux_ids.insert(aux_ids.end(), w.begin(), w.end());
+      has_filters = true;
+    }
+    rows.push_back(r);
+    aux.push_back(x);
+    return true;
+  }
   if (P.drv == DRV_LIBRARY) {
     // compare.IsVulnerable as disjoint intervals per version class (libdb.h); classes
     // sharing an interval share its row; a row that holds for a subset of the classes

@@ -373,6 +373,7 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
   sa.rec = b.rec + p0;
   sa.tail = b.tail + p0;
   sa.spill = b.spill ? b.spill : spill_;
+  sa.arena = b.arena;
   sa.attr = b.attr ? b.attr + p0 : nullptr;
   sa.cpe_bits = b.cpe_bits;
   sa.cpe_words = b.cpe_words;

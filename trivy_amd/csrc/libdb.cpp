@@ -786,6 +786,91 @@ bool mvn_compile(const std::string& constraint, KSet& out) {
   return true;
 }
 
+// The same constraint grammar as an IsVulnerable program for pairwise evaluation (libver.h
+// mvn_program_eval): alternatives = groups, a group = AND of (op, bound text) terms; a
+// Maven range list "[a,b),(c,]" gives one group per range.
+using MvnGroups = std::vector<std::vector<std::pair<uint32_t, std::string>>>;
+
+static bool mvn_text_ok(const std::string& v) {
+  bool ok = false;
+  (void)mvn_key(v, ok);
+  return ok;
+}
+
+bool mvn_groups(const std::string& constraint, MvnGroups& out) {
+  for (const std::string& alt0 : split(constraint, "||")) {
+    const std::string a = trim(alt0);
+    if (!a.empty() && (a[0] == '[' || a[0] == '(')) {
+      size_t pos = 0;
+      while (pos < a.size()) {
+        if (a[pos] == ',' || a[pos] == ' ') {
+          pos++;
+          continue;
+        }
+        if (a[pos] != '[' && a[pos] != '(') return false;
+        const size_t e1 = a.find(']', pos), e2 = a.find(')', pos), end = std::min(e1, e2);
+        if (end == std::string::npos) return false;
+        const std::string body = a.substr(pos + 1, end - pos - 1);
+        const bool lo_incl = a[pos] == '[', hi_incl = a[end] == ']';
+        const size_t comma = body.find(',');
+        std::vector<std::pair<uint32_t, std::string>> g;
+        if (comma != std::string::npos) {
+          const std::string lo = trim(body.substr(0, comma)), hi = trim(body.substr(comma + 1));
+          if (!lo.empty()) {
+            if (!mvn_text_ok(lo)) return false;
+            g.push_back({lo_incl ? MVO_GE : MVO_GT, lo});
+          }
+          if (!hi.empty()) {
+            if (!mvn_text_ok(hi)) return false;
+            g.push_back({hi_incl ? MVO_LE : MVO_LT, hi});
+          }
+        } else {
+          const std::string v = trim(body);
+          if (!(lo_incl && hi_incl) || v.empty() || !mvn_text_ok(v)) return false;
+          g.push_back({MVO_EQ, v});
+        }
+        out.push_back(std::move(g));
+        pos = end + 1;
+      }
+      continue;
+    }
+    std::vector<std::pair<uint32_t, std::string>> g;
+    size_t i = 0;
+    while (i < a.size()) {
+      if (a[i] == ',' || a[i] == ' ' || a[i] == '\t') {
+        i++;
+        continue;
+      }
+      std::string op;
+      for (const char* o : {">=", "<=", "!=", "==", "=", ">", "<"}) {
+        const size_t l = std::strlen(o);
+        if (a.compare(i, l, o) == 0) {
+          op = o;
+          break;
+        }
+      }
+      size_t j = i + op.size();
+      while (j < a.size() && is_ws(a[j])) j++;
+      const size_t vb = j;
+      while (j < a.size() && !is_ws(a[j]) && !std::strchr("<>=!,", a[j])) j++;
+      if (j == vb) return false;
+      const std::string v = a.substr(vb, j - vb);
+      if (!mvn_text_ok(v)) return false;
+      const uint32_t code = op.empty() || op == "=" || op == "==" ? MVO_EQ
+                            : op == "!="                          ? MVO_NE
+                            : op == ">"                           ? MVO_GT
+                            : op == "<"                           ? MVO_LT
+                            : op == ">="                          ? MVO_GE
+                                                                  : MVO_LE;
+      g.push_back({code, v});
+      i = j;
+    }
+    if (g.empty()) return false;
+    out.push_back(std::move(g));
+  }
+  return true;
+}
+
 // ==================================================================== RUBYGEMS =========
 bool gem_compile(const std::string& constraint, KSet& out) {
   out.clear();
@@ -923,6 +1008,55 @@ bool lib_rows_contain(uint8_t cmp, const LibRows& r, const std::string& installe
   if (!encode_version_cls(cmp, U(installed), uint32_t(installed.size()), o, cls)) return false;
   if (cls >= r.cls.size()) return false;
   return contains(r.cls[cls], k);
+}
+
+MvnProgState mvn_program(const std::vector<std::string>& vulnerable, const std::vector<std::string>& patched,
+                         const std::vector<std::string>& unaffected, std::vector<uint32_t>& words) {
+  words.clear();
+  for (const auto* l : {&vulnerable, &patched})
+    for (const std::string& v : *l)
+      if (v.empty()) return MVN_ALWAYS;
+  auto join = [](std::initializer_list<const std::vector<std::string>*> ls) {
+    std::string s;
+    for (const auto* l : ls)
+      for (const std::string& x : *l) s += (s.empty() ? "" : " || ") + x;
+    return s;
+  };
+  MvnGroups vg, sg;
+  if (!vulnerable.empty() && !mvn_groups(join({&vulnerable}), vg)) return MVN_NEVER;
+  if (patched.empty() && unaffected.empty()) {
+    if (vulnerable.empty()) return MVN_NEVER;
+  } else if (!mvn_groups(join({&patched, &unaffected}), sg)) {
+    return MVN_NEVER;
+  }
+  words.push_back(uint32_t(vg.size()) | (uint32_t(sg.size()) << 16));
+  std::vector<std::pair<size_t, const std::string*>> fix;  // (word of the offset, text)
+  for (const MvnGroups* gs : {&vg, &sg})
+    for (const auto& g : *gs) {
+      words.push_back(uint32_t(g.size()));
+      for (const auto& [op, txt] : g) {
+        words.push_back(op | (uint32_t(txt.size()) << 8));
+        fix.push_back({words.size(), &txt});
+        words.push_back(0);
+      }
+    }
+  for (const auto& [w, txt] : fix) {  // texts packed behind the groups, 4 bytes per word
+    words[w] = uint32_t(words.size());
+    std::vector<uint32_t> packed((txt->size() + 3) / 4 + 1, 0);
+    std::memcpy(packed.data(), txt->data(), txt->size());
+    words.insert(words.end(), packed.begin(), packed.end());
+  }
+  return MVN_PROGRAM;
+}
+
+int mvn_is_vulnerable(const std::vector<std::string>& vulnerable, const std::vector<std::string>& patched,
+                      const std::vector<std::string>& unaffected, const std::string& installed) {
+  std::vector<uint32_t> w;
+  const MvnProgState st = mvn_program(vulnerable, patched, unaffected, w);
+  if (st != MVN_PROGRAM) return st == MVN_ALWAYS ? 1 : 0;
+  MvnParse V;
+  if (!mvn_parse(U(installed), uint32_t(installed.size()), V)) return 0;  // NewVersion error: not vulnerable
+  return mvn_program_eval(w.data(), MvnSide{&V, U(installed)}) ? 1 : 0;
 }
 
 }  // namespace tvm

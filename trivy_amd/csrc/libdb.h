@@ -33,6 +33,15 @@ struct LibRows {
   std::vector<KSet> cls;  // ncls entries
 };
 
+// Maven advisories as IsVulnerable programs (libver.h mvn_program_eval): ALWAYS (an empty
+// constraint string), NEVER (unparsable / nothing to match) or a program in `words`.
+enum MvnProgState { MVN_NEVER = 0, MVN_ALWAYS = 1, MVN_PROGRAM = 2 };
+MvnProgState mvn_program(const std::vector<std::string>& vulnerable, const std::vector<std::string>& patched,
+                         const std::vector<std::string>& unaffected, std::vector<uint32_t>& words);
+// compare.IsVulnerable for the Maven grammar, pairwise (host): 1 / 0.
+int mvn_is_vulnerable(const std::vector<std::string>& vulnerable, const std::vector<std::string>& patched,
+                      const std::vector<std::string>& unaffected, const std::string& installed);
+
 // Number of version classes of a grammar (libver.h class bits).
 int lib_classes(uint8_t cmp);
 

@@ -690,6 +690,141 @@ TVM_HD bool mvn_encode(const uint8_t* s, uint32_t n, Sink& o) {
   return true;
 }
 
+// ---- Maven, pairwise: ComparableVersion.compareTo on two parses ----------------------------
+// The sort key above is a total order; ComparableVersion is not, so the
+// library rows of the Maven grammar are evaluated pairwise instead: each advisory becomes a
+// small program (the OR of AND clauses IsVulnerable evaluates, compare.go:20-51) whose terms
+// compare the installed version with the bound's text through mvn_cmp below - Item.compareTo
+// of go-mvn-version exactly, int / string / list against each other and against null.
+// A parse is a spine of lists: list l holds the tokens up to and including the MV_OPEN
+// that starts list l + 1 (a sub-list is always its parent's last item).
+struct MvnSide {
+  const MvnParse* P;
+  const uint8_t* s;
+};
+
+// Next item of the list at or after token k (removed tokens skipped); -1 at the list's end.
+TVM_HD int mvn_next(const MvnParse& P, int k) {
+  for (; k < P.n; k++) {
+    if (!P.t[k].removed) return k;
+    if (P.t[k].kind == MV_OPEN) return -1;  // a removed sub-list ends its (then emptied) parent
+  }
+  return -1;
+}
+
+// Item at token k against null (-1 / 0 / +1).
+TVM_HD int mvn_vs_null(const MvnSide& A, int k) {
+  for (;;) {
+    const MvnTok& t = A.P->t[k];
+    if (t.kind == MV_INT) return t.zero ? 0 : 1;
+    if (t.kind == MV_STR) return t.q < 5 ? -1 : (t.q == 5 ? 0 : 1);
+    const int f = mvn_next(*A.P, k + 1);  // a list: its first item decides (empty: equal)
+    if (f < 0) return 0;
+    k = f;
+  }
+}
+
+TVM_HD int mvn_int_cmp(const MvnSide& A, const MvnTok& x, const MvnSide& B, const MvnTok& y) {
+  uint32_t i = x.b, j = y.b;
+  while (i < x.e && A.s[i] == '0') i++;
+  while (j < y.e && B.s[j] == '0') j++;
+  const uint32_t la = x.e - i, lb = y.e - j;
+  if (la != lb) return la < lb ? -1 : 1;
+  for (; i < x.e; i++, j++)
+    if (A.s[i] != B.s[j]) return A.s[i] < B.s[j] ? -1 : 1;
+  return 0;
+}
+
+// Qualifier order (comparableQualifier): index among the known ones, unknown words after
+// "sp" in byte order of their lower-case text.
+TVM_HD int mvn_str_cmp(const MvnSide& A, const MvnTok& x, const MvnSide& B, const MvnTok& y) {
+  if (x.q != 7 || y.q != 7) return x.q == y.q ? 0 : (x.q < y.q ? -1 : 1);
+  uint32_t i = x.b, j = y.b;
+  for (; i < x.e && j < y.e; i++, j++) {
+    const uint8_t c = lv_lower(A.s[i]), d = lv_lower(B.s[j]);
+    if (c != d) return c < d ? -1 : 1;
+  }
+  return (i < x.e) - (j < y.e);
+}
+
+// ComparableVersion(a).compareTo(b) over two parses.
+TVM_HD int mvn_cmp(const MvnSide& A, const MvnSide& B) {
+  int ka = 0, kb = 0;  // current positions in the current lists of A and B
+  for (;;) {
+    const int x = mvn_next(*A.P, ka), y = mvn_next(*B.P, kb);
+    if (x < 0 && y < 0) return 0;
+    if (x < 0) {
+      const int r = -mvn_vs_null(B, y);
+      if (r) return r;
+      kb = B.P->t[y].kind == MV_OPEN ? B.P->n : y + 1;  // nothing follows a sub-list item
+      ka = A.P->n;
+      continue;
+    }
+    if (y < 0) {
+      const int r = mvn_vs_null(A, x);
+      if (r) return r;
+      ka = A.P->t[x].kind == MV_OPEN ? A.P->n : x + 1;
+      kb = B.P->n;
+      continue;
+    }
+    const MvnTok &tx = A.P->t[x], &ty = B.P->t[y];
+    if (tx.kind == MV_OPEN && ty.kind == MV_OPEN) {  // list vs list: the sub-lists, item by item
+      ka = x + 1;
+      kb = y + 1;
+      continue;
+    }
+    int r;
+    if (tx.kind == MV_INT) r = ty.kind == MV_INT ? mvn_int_cmp(A, tx, B, ty) : 1;   // int > string, list
+    else if (tx.kind == MV_STR) r = ty.kind == MV_STR ? mvn_str_cmp(A, tx, B, ty) : -1;  // string < int, list
+    else r = ty.kind == MV_INT ? -1 : 1;                                          // list < int, > string
+    if (r) return r;
+    ka = x + 1;
+    kb = y + 1;
+  }
+}
+
+// A Maven advisory program (u32 words, built by libdb.cpp mvn_program):
+//   w[0] = n_vulnerable_groups | n_secure_groups << 16, then the groups in that order;
+//   group = n_terms, then per term {op | len << 8, word offset of the bound's text}
+//   (ops MVO_*; the texts are packed 4 bytes per word behind the groups).
+// IsVulnerable: (no vulnerable groups, or one of them holds) and none of the secure groups.
+enum : uint32_t { MVO_EQ = 0, MVO_NE = 1, MVO_GT = 2, MVO_LT = 3, MVO_GE = 4, MVO_LE = 5 };
+
+TVM_HD bool mvn_op(uint32_t op, int c) {
+  switch (op) {
+    case MVO_EQ: return c == 0;
+    case MVO_NE: return c != 0;
+    case MVO_GT: return c > 0;
+    case MVO_LT: return c < 0;
+    case MVO_GE: return c >= 0;
+    default: return c <= 0;
+  }
+}
+
+// The program at w against the installed version (already parsed as V).
+TVM_HD bool mvn_program_eval(const uint32_t* w, const MvnSide& V) {
+  const uint32_t nv = w[0] & 0xFFFFu, ns = w[0] >> 16;
+  uint32_t at = 1;
+  bool vul = nv == 0, sec = false;
+  MvnParse B;
+  for (uint32_t g = 0; g < nv + ns; g++) {
+    const uint32_t nt = w[at++];
+    bool all = true;
+    for (uint32_t t = 0; t < nt; t++) {
+      const uint32_t d = w[at], off = w[at + 1];
+      at += 2;
+      if (!all) continue;
+      const uint8_t* txt = reinterpret_cast<const uint8_t*>(w + off);
+      if (!mvn_parse(txt, d >> 8, B)) return false;  // cannot happen: checked when compiled
+      const MvnSide Bs{&B, txt};
+      all = mvn_op(d & 0xFFu, mvn_cmp(V, Bs));
+    }
+    if (g < nv) vul = vul || all;
+    else sec = sec || all;
+  }
+  return vul && !sec;
+}
+
 // =========================================================================== RUBYGEMS ====
 // github.com/aquasecurity/go-gem-version (go.mod:16), Gem::Version:
 //   \s*( N(.[0-9a-zA-Z]+)* (-[0-9A-Za-z-]+(.[0-9A-Za-z-]+)*)? )?\s*     ("" reads "0")

@@ -65,6 +65,7 @@ struct SweepArgs {
   const PkgRec* rec;         // chunk-relative
   const uint4* tail;
   const uint64_t* spill;
+  const uint8_t* arena;      // the batch's name/version bytes (Maven rows re-read the installed text)
   const uint2* attr;         // per-package attributes (chunk-relative), nullptr when no row filters
   const uint32_t* cpe_bits;
   uint32_t cpe_words;
@@ -210,8 +211,8 @@ __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uin
 // kb / tab: the lane's LDS key buffer and the dpkg code table (nullptr: generic encoder only).
 template <uint32_t GM, class P, int DIAG = 0>
 __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32_t plat, uint32_t nlen, uint32_t vlen,
-                                          const uint8_t* name, const uint8_t* ver, PkgRec& r, uint8_t* kb = nullptr,
-                                          const uint8_t* tab = nullptr) {
+                                          const uint8_t* name, const uint8_t* ver, uint64_t vglob, PkgRec& r,
+                                          uint8_t* kb = nullptr, const uint8_t* tab = nullptr) {
   const PlatInfo pi = a.db.plats[plat];
   if (!(DIAG & 1) && kb && ((GM >> CMP_DEB) & 1u) && pi.cmp == CMP_DEB) {
     uint32_t kl = 0;
@@ -263,6 +264,8 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
   }
   const uint32_t kl = hs.n;
   kinfo |= (kl & KI_LEN) | (valid ? KI_VALID : 0u) | ((cls & KI_CLS_MASK) << KI_CLS_SHIFT);
+  if (((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN)  // Maven rows compare texts (AUX_MVN), not keys:
+    a.tail[p] = make_uint4(uint32_t(vglob), uint32_t(vglob >> 32), vlen, 0u);  // the slot holds where it is
   r.k0 = valid && kl ? be_word(hs.w0, kl < 8 ? kl : 8) : 0ull;
   r.k1 = valid && kl > 8 ? be_word(hs.w1, kl < 16 ? kl - 8 : 8) : 0ull;
   uint32_t cnt = 0, rbeg = 0;
@@ -337,11 +340,11 @@ __global__ __launch_bounds__(kTile) void probe_kernel(ProbeArgs a) {
   if (p < a.n && d.x < a.db.n_plats) {
     if (staged) {
       const uint8_t* sb = reinterpret_cast<const uint8_t*>(stage) + uint32_t(w0 - base16) + off;
-      probe_one<GM, uint32_t, DIAG>(a, p, d.x, nlen, vlen, sb, sb + nlen, r,
+      probe_one<GM, uint32_t, DIAG>(a, p, d.x, nlen, vlen, sb, sb + nlen, w0 + off + nlen, r,
                                     reinterpret_cast<uint8_t*>(kbuf) + tid * kFastKeyStride, tab);
     } else {
       const uint8_t* gb = a.arena + w0 + off;
-      probe_one<GM, uint32_t, DIAG>(a, p, d.x, nlen, vlen, gb, gb + nlen, r);
+      probe_one<GM, uint32_t, DIAG>(a, p, d.x, nlen, vlen, gb, gb + nlen, w0 + off + nlen, r);
     }
   }
   if (p < a.n) a.rec[p] = r;
@@ -364,10 +367,18 @@ struct SweepShared {
   unsigned long long base;
 };
 
-// Per-package predicates of a ROW_FILTER row (common.h RowAux).
-__device__ __forceinline__ bool aux_pass(const SweepArgs& a, uint32_t ridx, uint2 pa, uint32_t ki) {
+// Per-package predicates of a ROW_FILTER row (common.h RowAux); p = the package's index
+// in the launch (its tail slot holds a Maven package's text location, probe_one).
+__device__ __forceinline__ bool aux_pass(const SweepArgs& a, uint32_t ridx, uint2 pa, uint32_t ki, uint32_t p) {
   const RowAux x = a.db.aux[ridx];
   const uint32_t* ids = a.db.aux_ids + x.list_off;
+  if (x.kind & AUX_MVN) {
+    const uint4 t = a.tail[p];
+    const uint8_t* v = a.arena + (uint64_t(t.x) | (uint64_t(t.y) << 32));
+    MvnParse V;
+    if (!mvn_parse(v, t.z, V)) return false;
+    return mvn_program_eval(ids, MvnSide{&V, v});
+  }
   if (x.kind & (AUX_ARCH_RH | AUX_ARCH_IN)) {
     bool ok = (x.kind & AUX_ARCH_RH) && (x.n_arch == 0 || (pa.x & PA_NOARCH));
     const uint32_t arch = pa.x & PA_ARCH_MASK;
@@ -442,7 +453,7 @@ __device__ __forceinline__ bool eval_row(const SweepArgs& a, const S& s, uint32_
   m = m && (ki & KI_VALID);
   m = m || (row.adv & ROW_ALWAYS);
   if constexpr (FILT) {
-    if (m && (row.adv & ROW_FILTER)) m = aux_pass(a, ridx, s.pattr[q], ki);
+    if (m && (row.adv & ROW_FILTER)) m = aux_pass(a, ridx, s.pattr[q], ki, p);
   }
   return m;
 }
@@ -681,11 +692,11 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
   if (p < a.n && d.x < a.db.n_plats) {
     if (staged) {
       const uint8_t* sb = reinterpret_cast<const uint8_t*>(buf) + uint32_t(w0 - base16) + off;
-      probe_one<GM, uint32_t, DIAG & 3>(a, p, d.x, nlen, vlen, sb, sb + nlen, r,
+      probe_one<GM, uint32_t, DIAG & 3>(a, p, d.x, nlen, vlen, sb, sb + nlen, w0 + off + nlen, r,
                                         reinterpret_cast<uint8_t*>(u.pr.kbuf) + tid * kFastKeyStride, u.pr.tab);
     } else {
       const uint8_t* gb = a.arena + w0 + off;
-      probe_one<GM, uint32_t, DIAG & 3>(a, p, d.x, nlen, vlen, gb, gb + nlen, r);
+      probe_one<GM, uint32_t, DIAG & 3>(a, p, d.x, nlen, vlen, gb, gb + nlen, w0 + off + nlen, r);
     }
   }
   if (DIAG & 4) r.meta.y = 0;  // no rows: the sweep does nothing
