@@ -125,6 +125,7 @@ class Engine {
   bool alloc_batch(const HostBatch& hb, DevBatch& b, std::string& err);
   bool upload(const HostBatch& hb, DevBatch& b, std::string& err);
   uint32_t grammar_set(const HostBatch& hb) const;
+  uint64_t scratch_words(const HostBatch& hb) const;
   void free_batch(DevBatch& b);
   bool alloc_matches(uint64_t cap, uint32_t n_pkgs, DevMatches& m, std::string& err);
   void free_matches(DevMatches& m);

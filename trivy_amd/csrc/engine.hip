@@ -237,17 +237,28 @@ uint32_t Engine::grammar_set(const HostBatch& hb) const {
   return gm & GM_ALL;
 }
 
+// Scratch words a batch may need: keys longer than 32 bytes (the widest grammar's bound)
+// and, for Maven packages, the packed parse of the installed version (AUX_MVN rows).
+uint64_t Engine::scratch_words(const HostBatch& hb) const {
+  const auto& pi = db_->plat_info;
+  uint64_t w = 0;
+  for (const uint2& d : hb.pk) {
+    const uint32_t vlen = d.y >> 16;
+    const uint32_t need = (key_bound_any(vlen) + 7) / 8;
+    if (need > kKeyWords) w += need;
+    if (d.x < pi.size() && pi[d.x].cmp == CMP_MAVEN)
+      w += (uint64_t(kMvnPackedWords) * std::min<uint32_t>(2 * vlen + 3, kMvnMaxTok) + 1) / 2;
+  }
+  return w;
+}
+
 bool Engine::alloc_batch(const HostBatch& hb, DevBatch& b, std::string& err) {
   (void)hipSetDevice(dev_);
   b.n = uint32_t(hb.pk.size());
   b.n_tiles = hb.n_tiles();
   b.arena_bytes = hb.arena.size();
-  b.spill_words = 0;
   b.gm = grammar_set(hb);
-  for (const uint2& d : hb.pk) {
-    const uint32_t need = (key_bound_any(d.y >> 16) + 7) / 8;  // the widest grammar bound
-    if (need > kKeyWords) b.spill_words += need;
-  }
+  b.spill_words = scratch_words(hb);
   if (!hb.attr.empty() && hb.attr.size() != hb.pk.size()) {
     err = "batch attributes do not cover every package";
     return false;
@@ -528,11 +539,7 @@ bool Engine::dropin_run(Dropin& d, DropinReq* const* reqs, size_t n, std::string
   b.n_tiles = hb.n_tiles();
   b.arena_bytes = hb.arena.size();
   b.gm = grammar_set(hb);
-  b.spill_words = 0;
-  for (const uint2& x : hb.pk) {
-    const uint32_t need = (key_bound_any(x.y >> 16) + 7) / 8;
-    if (need > kKeyWords) b.spill_words += need;
-  }
+  b.spill_words = scratch_words(hb);
   if (!hb.attr.empty() && hb.attr.size() != hb.pk.size()) {
     err = "batch attributes do not cover every package";
     return false;

@@ -1030,20 +1030,33 @@ MvnProgState mvn_program(const std::vector<std::string>& vulnerable, const std::
     return MVN_NEVER;
   }
   words.push_back(uint32_t(vg.size()) | (uint32_t(sg.size()) << 16));
-  std::vector<std::pair<size_t, const std::string*>> fix;  // (word of the offset, text)
+  struct Fix {
+    size_t at;
+    const std::string* txt;
+  };
+  std::vector<Fix> fix;  // (word holding the term's token offset, text)
   for (const MvnGroups* gs : {&vg, &sg})
     for (const auto& g : *gs) {
       words.push_back(uint32_t(g.size()));
       for (const auto& [op, txt] : g) {
-        words.push_back(op | (uint32_t(txt.size()) << 8));
+        MvnParse P;
+        (void)mvn_parse(U(txt), uint32_t(txt.size()), P);  // checked by mvn_groups
+        words.push_back(op | (uint32_t(P.n) << 8) | (uint32_t(txt.size()) << 16));
         fix.push_back({words.size(), &txt});
+        words.push_back(0);
         words.push_back(0);
       }
     }
-  for (const auto& [w, txt] : fix) {  // texts packed behind the groups, 4 bytes per word
-    words[w] = uint32_t(words.size());
-    std::vector<uint32_t> packed((txt->size() + 3) / 4 + 1, 0);
-    std::memcpy(packed.data(), txt->data(), txt->size());
+  for (const Fix& f : fix) {  // packed parses, then the texts, behind the groups
+    MvnParse P;
+    (void)mvn_parse(U(*f.txt), uint32_t(f.txt->size()), P);
+    words[f.at] = uint32_t(words.size());
+    const size_t base = words.size();
+    words.resize(base + size_t(kMvnPackedWords) * P.n);
+    mvn_pack(P, words.data() + base);
+    words[f.at + 1] = uint32_t(words.size());
+    std::vector<uint32_t> packed((f.txt->size() + 3) / 4 + 1, 0);
+    std::memcpy(packed.data(), f.txt->data(), f.txt->size());
     words.insert(words.end(), packed.begin(), packed.end());
   }
   return MVN_PROGRAM;
@@ -1056,7 +1069,7 @@ int mvn_is_vulnerable(const std::vector<std::string>& vulnerable, const std::vec
   if (st != MVN_PROGRAM) return st == MVN_ALWAYS ? 1 : 0;
   MvnParse V;
   if (!mvn_parse(U(installed), uint32_t(installed.size()), V)) return 0;  // NewVersion error: not vulnerable
-  return mvn_program_eval(w.data(), MvnSide{&V, U(installed)}) ? 1 : 0;
+  return mvn_program_eval(w.data(), MvnParseView{&V, U(installed)}) ? 1 : 0;
 }
 
 }  // namespace tvm

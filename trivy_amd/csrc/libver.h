@@ -694,89 +694,127 @@ TVM_HD bool mvn_encode(const uint8_t* s, uint32_t n, Sink& o) {
 // The sort key above is a total order; ComparableVersion is not, so the
 // library rows of the Maven grammar are evaluated pairwise instead: each advisory becomes a
 // small program (the OR of AND clauses IsVulnerable evaluates, compare.go:20-51) whose terms
-// compare the installed version with the bound's text through mvn_cmp below - Item.compareTo
-// of go-mvn-version exactly, int / string / list against each other and against null.
+// compare the installed version with the bound through mvn_cmp below - Item.compareTo of
+// go-mvn-version exactly, int / string / list against each other and against null.
 // A parse is a spine of lists: list l holds the tokens up to and including the MV_OPEN
-// that starts list l + 1 (a sub-list is always its parent's last item).
-struct MvnSide {
+// that starts list l + 1 (a sub-list is always its parent's last item).  Parses are read
+// through views: a live MvnParse, or tokens packed two words each (w0 = kind | q << 8 |
+// removed << 16 | zero << 24, w1 = b | e << 16) - the bounds' parses are packed into the
+// program at load time and the installed version's into the batch scratch by the probe,
+// so the sweep parses nothing.
+struct MvnParseView {
   const MvnParse* P;
   const uint8_t* s;
+  TVM_HD int n() const { return P->n; }
+  TVM_HD uint32_t kind(int k) const { return P->t[k].kind; }
+  TVM_HD uint32_t q(int k) const { return P->t[k].q; }
+  TVM_HD bool removed(int k) const { return P->t[k].removed; }
+  TVM_HD bool zero(int k) const { return P->t[k].zero; }
+  TVM_HD uint32_t b(int k) const { return P->t[k].b; }
+  TVM_HD uint32_t e(int k) const { return P->t[k].e; }
 };
+struct MvnPackedView {
+  const uint32_t* t;
+  int cnt;
+  const uint8_t* s;
+  TVM_HD int n() const { return cnt; }
+  TVM_HD uint32_t kind(int k) const { return t[2 * k] & 0xFFu; }
+  TVM_HD uint32_t q(int k) const { return (t[2 * k] >> 8) & 0xFFu; }
+  TVM_HD bool removed(int k) const { return (t[2 * k] >> 16) & 0xFFu; }
+  TVM_HD bool zero(int k) const { return t[2 * k] >> 24; }
+  TVM_HD uint32_t b(int k) const { return t[2 * k + 1] & 0xFFFFu; }
+  TVM_HD uint32_t e(int k) const { return t[2 * k + 1] >> 16; }
+};
+constexpr int kMvnPackedWords = 2;  // words per packed token
+
+TVM_HD void mvn_pack(const MvnParse& P, uint32_t* out) {
+  for (int k = 0; k < P.n; k++) {
+    const MvnTok& t = P.t[k];
+    out[2 * k] = uint32_t(t.kind) | (uint32_t(t.q) << 8) | (uint32_t(t.removed) << 16) | (uint32_t(t.zero) << 24);
+    out[2 * k + 1] = (t.b & 0xFFFFu) | (t.e << 16);
+  }
+}
 
 // Next item of the list at or after token k (removed tokens skipped); -1 at the list's end.
-TVM_HD int mvn_next(const MvnParse& P, int k) {
-  for (; k < P.n; k++) {
-    if (!P.t[k].removed) return k;
-    if (P.t[k].kind == MV_OPEN) return -1;  // a removed sub-list ends its (then emptied) parent
+template <class V>
+TVM_HD int mvn_next(const V& A, int k) {
+  for (; k < A.n(); k++) {
+    if (!A.removed(k)) return k;
+    if (A.kind(k) == MV_OPEN) return -1;  // a removed sub-list ends its (then emptied) parent
   }
   return -1;
 }
 
 // Item at token k against null (-1 / 0 / +1).
-TVM_HD int mvn_vs_null(const MvnSide& A, int k) {
+template <class V>
+TVM_HD int mvn_vs_null(const V& A, int k) {
   for (;;) {
-    const MvnTok& t = A.P->t[k];
-    if (t.kind == MV_INT) return t.zero ? 0 : 1;
-    if (t.kind == MV_STR) return t.q < 5 ? -1 : (t.q == 5 ? 0 : 1);
-    const int f = mvn_next(*A.P, k + 1);  // a list: its first item decides (empty: equal)
+    if (A.kind(k) == MV_INT) return A.zero(k) ? 0 : 1;
+    if (A.kind(k) == MV_STR) return A.q(k) < 5 ? -1 : (A.q(k) == 5 ? 0 : 1);
+    const int f = mvn_next(A, k + 1);  // a list: its first item decides (empty: equal)
     if (f < 0) return 0;
     k = f;
   }
 }
 
-TVM_HD int mvn_int_cmp(const MvnSide& A, const MvnTok& x, const MvnSide& B, const MvnTok& y) {
-  uint32_t i = x.b, j = y.b;
-  while (i < x.e && A.s[i] == '0') i++;
-  while (j < y.e && B.s[j] == '0') j++;
-  const uint32_t la = x.e - i, lb = y.e - j;
-  if (la != lb) return la < lb ? -1 : 1;
-  for (; i < x.e; i++, j++)
+template <class VA, class VB>
+TVM_HD int mvn_int_cmp(const VA& A, int x, const VB& B, int y) {
+  uint32_t i = A.b(x), j = B.b(y);
+  const uint32_t ie = A.e(x), je = B.e(y);
+  while (i < ie && A.s[i] == '0') i++;
+  while (j < je && B.s[j] == '0') j++;
+  if (ie - i != je - j) return ie - i < je - j ? -1 : 1;
+  for (; i < ie; i++, j++)
     if (A.s[i] != B.s[j]) return A.s[i] < B.s[j] ? -1 : 1;
   return 0;
 }
 
 // Qualifier order (comparableQualifier): index among the known ones, unknown words after
 // "sp" in byte order of their lower-case text.
-TVM_HD int mvn_str_cmp(const MvnSide& A, const MvnTok& x, const MvnSide& B, const MvnTok& y) {
-  if (x.q != 7 || y.q != 7) return x.q == y.q ? 0 : (x.q < y.q ? -1 : 1);
-  uint32_t i = x.b, j = y.b;
-  for (; i < x.e && j < y.e; i++, j++) {
+template <class VA, class VB>
+TVM_HD int mvn_str_cmp(const VA& A, int x, const VB& B, int y) {
+  const uint32_t qx = A.q(x), qy = B.q(y);
+  if (qx != 7 || qy != 7) return qx == qy ? 0 : (qx < qy ? -1 : 1);
+  uint32_t i = A.b(x), j = B.b(y);
+  const uint32_t ie = A.e(x), je = B.e(y);
+  for (; i < ie && j < je; i++, j++) {
     const uint8_t c = lv_lower(A.s[i]), d = lv_lower(B.s[j]);
     if (c != d) return c < d ? -1 : 1;
   }
-  return (i < x.e) - (j < y.e);
+  return (i < ie) - (j < je);
 }
 
 // ComparableVersion(a).compareTo(b) over two parses.
-TVM_HD int mvn_cmp(const MvnSide& A, const MvnSide& B) {
+template <class VA, class VB>
+TVM_HD int mvn_cmp(const VA& A, const VB& B) {
   int ka = 0, kb = 0;  // current positions in the current lists of A and B
   for (;;) {
-    const int x = mvn_next(*A.P, ka), y = mvn_next(*B.P, kb);
+    const int x = mvn_next(A, ka), y = mvn_next(B, kb);
     if (x < 0 && y < 0) return 0;
     if (x < 0) {
       const int r = -mvn_vs_null(B, y);
       if (r) return r;
-      kb = B.P->t[y].kind == MV_OPEN ? B.P->n : y + 1;  // nothing follows a sub-list item
-      ka = A.P->n;
+      kb = B.kind(y) == MV_OPEN ? B.n() : y + 1;  // nothing follows a sub-list item
+      ka = A.n();
       continue;
     }
     if (y < 0) {
       const int r = mvn_vs_null(A, x);
       if (r) return r;
-      ka = A.P->t[x].kind == MV_OPEN ? A.P->n : x + 1;
-      kb = B.P->n;
+      ka = A.kind(x) == MV_OPEN ? A.n() : x + 1;
+      kb = B.n();
       continue;
     }
-    const MvnTok &tx = A.P->t[x], &ty = B.P->t[y];
-    if (tx.kind == MV_OPEN && ty.kind == MV_OPEN) {  // list vs list: the sub-lists, item by item
+    const uint32_t tx = A.kind(x), ty = B.kind(y);
+    if (tx == MV_OPEN && ty == MV_OPEN) {  // list vs list: the sub-lists, item by item
       ka = x + 1;
       kb = y + 1;
       continue;
     }
     int r;
-    if (tx.kind == MV_INT) r = ty.kind == MV_INT ? mvn_int_cmp(A, tx, B, ty) : 1;   // int > string, list
-    else if (tx.kind == MV_STR) r = ty.kind == MV_STR ? mvn_str_cmp(A, tx, B, ty) : -1;  // string < int, list
-    else r = ty.kind == MV_INT ? -1 : 1;                                          // list < int, > string
+    if (tx == MV_INT) r = ty == MV_INT ? mvn_int_cmp(A, x, B, y) : 1;         // int > string, list
+    else if (tx == MV_STR) r = ty == MV_STR ? mvn_str_cmp(A, x, B, y) : -1;   // string < int, list
+    else r = ty == MV_INT ? -1 : 1;                                            // list < int, > string
     if (r) return r;
     ka = x + 1;
     kb = y + 1;
@@ -785,8 +823,8 @@ TVM_HD int mvn_cmp(const MvnSide& A, const MvnSide& B) {
 
 // A Maven advisory program (u32 words, built by libdb.cpp mvn_program):
 //   w[0] = n_vulnerable_groups | n_secure_groups << 16, then the groups in that order;
-//   group = n_terms, then per term {op | len << 8, word offset of the bound's text}
-//   (ops MVO_*; the texts are packed 4 bytes per word behind the groups).
+//   group = n_terms, then per term {op | n_tokens << 8 | text length << 16, word offset of
+//   the bound's packed tokens, word offset of its text (4 bytes per word)}.
 // IsVulnerable: (no vulnerable groups, or one of them holds) and none of the secure groups.
 enum : uint32_t { MVO_EQ = 0, MVO_NE = 1, MVO_GT = 2, MVO_LT = 3, MVO_GE = 4, MVO_LE = 5 };
 
@@ -801,23 +839,21 @@ TVM_HD bool mvn_op(uint32_t op, int c) {
   }
 }
 
-// The program at w against the installed version (already parsed as V).
-TVM_HD bool mvn_program_eval(const uint32_t* w, const MvnSide& V) {
+// The program at w against the installed version's parse V.
+template <class V>
+TVM_HD bool mvn_program_eval(const uint32_t* w, const V& inst) {
   const uint32_t nv = w[0] & 0xFFFFu, ns = w[0] >> 16;
   uint32_t at = 1;
   bool vul = nv == 0, sec = false;
-  MvnParse B;
   for (uint32_t g = 0; g < nv + ns; g++) {
     const uint32_t nt = w[at++];
     bool all = true;
     for (uint32_t t = 0; t < nt; t++) {
-      const uint32_t d = w[at], off = w[at + 1];
-      at += 2;
+      const uint32_t d = w[at], tok = w[at + 1], txt = w[at + 2];
+      at += 3;
       if (!all) continue;
-      const uint8_t* txt = reinterpret_cast<const uint8_t*>(w + off);
-      if (!mvn_parse(txt, d >> 8, B)) return false;  // cannot happen: checked when compiled
-      const MvnSide Bs{&B, txt};
-      all = mvn_op(d & 0xFFu, mvn_cmp(V, Bs));
+      const MvnPackedView B{w + tok, int((d >> 8) & 0xFFu), reinterpret_cast<const uint8_t*>(w + txt)};
+      all = mvn_op(d & 0xFFu, mvn_cmp(inst, B));
     }
     if (g < nv) vul = vul || all;
     else sec = sec || all;

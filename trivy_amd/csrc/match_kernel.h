@@ -262,10 +262,29 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
       kinfo |= KI_SPILL;
     }
   }
+  if (((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN) {
+    // Maven rows compare parses, not keys (AUX_MVN): the installed version's parse, packed
+    // into the batch scratch, and its text location take the tail slot
+    uint32_t off = 0, nt = 0;
+    if (valid) {
+      MvnParse mp;
+      if (mvn_parse(ver, vlen, mp)) {
+        const uint32_t need = (kMvnPackedWords * mp.n + 1) / 2;
+        const unsigned long long o = atomicAdd(&a.ctl[2], (unsigned long long)need);
+        if (o + need > a.spill_cap) {
+          atomicOr(&a.ctl[3], (unsigned long long)ERR_SPILL);
+          valid = false;
+        } else {
+          mvn_pack(mp, reinterpret_cast<uint32_t*>(a.spill + o));
+          off = uint32_t(o);
+          nt = uint32_t(mp.n);
+        }
+      }
+    }
+    a.tail[p] = make_uint4(off, nt | (vlen << 16), uint32_t(vglob), uint32_t(vglob >> 32));
+  }
   const uint32_t kl = hs.n;
   kinfo |= (kl & KI_LEN) | (valid ? KI_VALID : 0u) | ((cls & KI_CLS_MASK) << KI_CLS_SHIFT);
-  if (((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN)  // Maven rows compare texts (AUX_MVN), not keys:
-    a.tail[p] = make_uint4(uint32_t(vglob), uint32_t(vglob >> 32), vlen, 0u);  // the slot holds where it is
   r.k0 = valid && kl ? be_word(hs.w0, kl < 8 ? kl : 8) : 0ull;
   r.k1 = valid && kl > 8 ? be_word(hs.w1, kl < 16 ? kl - 8 : 8) : 0ull;
   uint32_t cnt = 0, rbeg = 0;
@@ -372,12 +391,11 @@ struct SweepShared {
 __device__ __forceinline__ bool aux_pass(const SweepArgs& a, uint32_t ridx, uint2 pa, uint32_t ki, uint32_t p) {
   const RowAux x = a.db.aux[ridx];
   const uint32_t* ids = a.db.aux_ids + x.list_off;
-  if (x.kind & AUX_MVN) {
+  if (x.kind & AUX_MVN) {  // the installed parse packed by probe_one, the program's packed bounds
     const uint4 t = a.tail[p];
-    const uint8_t* v = a.arena + (uint64_t(t.x) | (uint64_t(t.y) << 32));
-    MvnParse V;
-    if (!mvn_parse(v, t.z, V)) return false;
-    return mvn_program_eval(ids, MvnSide{&V, v});
+    const MvnPackedView V{reinterpret_cast<const uint32_t*>(a.spill + t.x), int(t.y & 0xFFFFu),
+                          a.arena + (uint64_t(t.z) | (uint64_t(t.w) << 32))};
+    return mvn_program_eval(ids, V);
   }
   if (x.kind & (AUX_ARCH_RH | AUX_ARCH_IN)) {
     bool ok = (x.kind & AUX_ARCH_RH) && (x.n_arch == 0 || (pa.x & PA_NOARCH));
