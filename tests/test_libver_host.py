@@ -246,6 +246,9 @@ def test_encoders_never_read_past_the_version(g):
     ("99-rc1", {"PatchedVersions": ["99.jre"]}),
     ("1.0.beta", {"VulnerableVersions": ["[1-sp,2)"]}),
     ("2.0.0", {"VulnerableVersions": ["(,2.0-1]"]}),
+    ("release", {"VulnerableVersions": [">ga.milestone"]}),  # flat lists too: "" item vs end of list
+    ("0.beta.alpha", {"VulnerableVersions": [">sp.m..alpha.milestone"]}),
+    ("m", {"PatchedVersions": [">=0.beta.00.milestone.rc"]}),
 ])
 def test_maven_non_transitive_pairs_exact(ver, adv):
     """The shapes where ComparableVersion is not an order evaluate exactly
