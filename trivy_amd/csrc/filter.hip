@@ -96,6 +96,9 @@ struct FilterArgs {
   uint32_t* skey;  // after filter_select: the survivors' mkey, else kEmpty
   uint32_t* ign;   // precedence of the ignoring rule, kEmpty = not ignored
   uint32_t* mine;  // dedup-table slot of a repeating package's pair
+  uint8_t* pcls;   // after filter_select: the pair's counter class (pair_class)
+  uint32_t* wcarry;  // after filter_count, per 64-pair wave w entered by a run begun earlier:
+                     //   the run's class counts before pair 64w (kClasses each)
   // tables
   const unsigned long long* rules;  // {key, precedence} x 2^k
   uint64_t rule_mask;
@@ -237,7 +240,6 @@ __global__ __launch_bounds__(kBlock) void filter_mark(FilterArgs a) {
 __global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
   const uint64_t stride = uint64_t(gridDim.x) * kBlock * kU;
   const uint32_t id_mask = (1u << a.id_bits) - 1u;
-  const uint32_t lane = threadIdx.x & 63;
   const uint64_t n = a.n;
   for (uint64_t b0 = uint64_t(blockIdx.x) * kBlock * kU; b0 < n; b0 += stride) {  // wave-uniform trip count
     uint32_t pv[kU], kv[kU], fv[kU];
@@ -282,20 +284,66 @@ __global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
         }
         a.skey[i] = key;
       }
-      // per-package class counters: the head lane of each package run inside the wave adds
-      // the run's members of every class (the list is grouped by package)
-      const uint32_t cls = valid ? pair_class(a, key, i) : kNoClass;
-      const uint32_t prev_p = __shfl_up(p, 1, 64);
-      const bool head = valid && (lane == 0 || prev_p != p);
-      const unsigned long long heads = __ballot(head);
-      const unsigned long long above = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
-      const uint32_t end = above ? uint32_t(__builtin_ctzll(above)) : 64u;
-      const unsigned long long span = (end == 64 ? ~0ull : ((1ull << end) - 1)) & (~0ull << lane);
+      if (valid) a.pcls[i] = uint8_t(pair_class(a, key, i));  // counted by filter_count
+    }
+  }
+}
+
+// Per-package class counters from the pairs' classes (the list is grouped by package): the
+// head lane of each package run starting inside a wave stores the run's nonzero class counts
+// (the counters are cleared before filter_select); a run crossing the wave's end - at most one
+// per wave - is finished by the whole wave reading on to the run's end, so no counter is
+// written twice and none atomically. On the way it leaves, at every later wave the run
+// enters, the run's class counts so far (filter_place's carry into a chunk).
+__global__ __launch_bounds__(kBlock) void filter_count(FilterArgs a) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t b0 = uint64_t(blockIdx.x) * kBlock; b0 < a.n; b0 += stride) {  // wave-uniform trip count
+    const uint64_t i = b0 + threadIdx.x;
+    const bool valid = i < a.n;
+    const uint32_t p = valid ? a.pkg[i] : 0xFFFFFFFFu;
+    const uint32_t cls = valid ? a.pcls[i] : kNoClass;
+    const uint32_t prev_p = __shfl_up(p, 1, 64);
+    // lane 0 starts a run only at the run's first pair (else the run started in an earlier wave)
+    const bool head = valid && (lane == 0 ? (i == 0 || a.pkg[i - 1] != p) : prev_p != p);
+    const bool seg = valid && (lane == 0 || prev_p != p);  // first lane of a package in this wave
+    const unsigned long long segs = __ballot(seg);
+    const unsigned long long above = lane == 63 ? 0ull : segs & (~0ull << (lane + 1));
+    const uint32_t end = above ? uint32_t(__builtin_ctzll(above)) : 64u;
+    const unsigned long long span = (end == 64 ? ~0ull : ((1ull << end) - 1)) & (~0ull << lane);
+    uint32_t cc[kClasses];
 #pragma unroll
-      for (uint32_t c = 0; c < uint32_t(kClasses); c++) {
-        const unsigned long long m = __ballot(cls == c);
-        if (head && (m & span)) atomicAdd(&a.cnt[uint64_t(p) * kClasses + c], uint32_t(__popcll(m & span)));
+    for (uint32_t c = 0; c < uint32_t(kClasses); c++) cc[c] = uint32_t(__popcll(__ballot(cls == c) & span));
+    // the wave's last run, when it starts here and goes on past the wave: counted on by all lanes
+    const unsigned long long heads = __ballot(head);
+    const uint32_t last = 63u - uint32_t(__builtin_clzll(segs | 1ull));  // first lane of the last package
+    const bool last_starts = (heads >> last) & 1ull;
+    const uint64_t wend = b0 + (threadIdx.x & ~63u) + 64;  // first pair past this wave
+    const uint32_t lp = __shfl(p, int(last), 64);
+    const uint32_t re = (last_starts && wend < a.n) ? a.run_e[lp] : 0u;  // wave-uniform
+    if (re > wend) {
+      uint32_t more[kClasses];
+#pragma unroll
+      for (int c = 0; c < kClasses; c++) more[c] = __shfl(cc[c], int(last), 64);  // the run so far
+      for (uint64_t j0 = wend; j0 < re; j0 += 64) {  // wave-uniform trip count
+        uint32_t sofar = 0;
+#pragma unroll
+        for (int c = 0; c < kClasses; c++) sofar = lane == uint32_t(c) ? more[c] : sofar;
+        if (lane < uint32_t(kClasses)) a.wcarry[(j0 >> 6) * kClasses + lane] = sofar;
+        const uint64_t j = j0 + lane;
+        const uint32_t cj = j < re ? a.pcls[j] : kNoClass;
+#pragma unroll
+        for (uint32_t c = 0; c < uint32_t(kClasses); c++) more[c] += uint32_t(__popcll(__ballot(cj == c)));
       }
+      if (lane == last)
+#pragma unroll
+        for (int c = 0; c < kClasses; c++) cc[c] = more[c];
+    }
+    if (head) {
+      uint32_t* o = a.cnt + uint64_t(p) * kClasses;
+#pragma unroll
+      for (int c = 0; c < kClasses; c++)
+        if (cc[c]) o[c] = cc[c];
     }
   }
 }
@@ -331,7 +379,7 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
     const uint64_t i = c0 + tid;
     const bool valid = i < a.n;
     const uint32_t key = valid ? a.skey[i] : kEmpty;
-    const uint32_t cls = valid ? pair_class(a, key, i) : kNoClass;
+    const uint32_t cls = valid ? uint32_t(a.pcls[i]) : kNoClass;  // pair_class, from filter_select
     const uint32_t p = valid ? a.pkg[i] : 0u;
     const uint32_t rb = valid ? a.run_b[p] : 0u;
     const uint64_t rs = rb > c0 ? rb : c0;  // the package's first pair in this chunk
@@ -343,7 +391,11 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
       if (lane >= uint32_t(o)) x += y;
     }
     if (lane == 63) wsum[wave] = x;
-    if (tid < uint32_t(kClasses)) carry[tid] = 0;
+    // the run entering the chunk: its classes before c0 (filter_count left them per wave)
+    if (tid < uint32_t(kClasses)) {
+      const uint32_t rb0 = a.run_b[a.pkg[c0]];
+      carry[tid] = rb0 < c0 ? a.wcarry[(c0 >> 6) * kClasses + tid] : 0u;
+    }
     if (valid && i == rs) {  // the package's first lane: its placement bases, once
       const uint32_t f = a.fl[p];
       pflag[tid] = f;
@@ -363,12 +415,6 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
 #pragma unroll
     for (int w = 0; w < kBlock / 64; w++) wbase += (uint32_t(w) < wave) ? wsum[w] : 0ull;
     pre[tid] = wbase + x - one_hot(cls);
-    // the run entering the chunk: its classes before c0, counted by the whole block
-    const uint32_t rb0 = a.run_b[a.pkg[c0]];
-    for (uint64_t j = rb0 + tid; j < c0; j += kBlock) {
-      const uint32_t cj = pair_class(a, a.skey[j], j);
-      if (cj < uint32_t(kClasses)) atomicAdd(&carry[cj], 1u);
-    }
     __syncthreads();
     if (valid && cls < uint32_t(kClasses)) {
       const uint32_t h = uint32_t(rs - c0);
@@ -564,7 +610,7 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
     return false;
   if (!grow(12, n * 4, err) || !grow(13, n * 4, err) || (has_ign && !grow(14, n * 4, err)) ||
       (tcap && (!grow(15, n * 4, err) || !grow(16, tcap * 16, err))) || (rcap && !grow(17, rcap * 16, err)) ||
-      !grow(21, n * 8, err) ||
+      !grow(21, n * 8, err) || !grow(24, n, err) || !grow(25, (n / 64 + 1) * 4 * kClasses, err) ||
       (has_ign && !grow(22, n * 12, err)) || !grow(23, std::max<uint64_t>(scan_bytes, 16), err))
     return false;
   // per-call flags start as the static ones (FL_DUP, FL_SINGLE)
@@ -643,6 +689,8 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   a.skey = as<uint32_t>(bufs_[13]);
   a.ign = as<uint32_t>(bufs_[14]);
   a.mine = as<uint32_t>(bufs_[15]);
+  a.pcls = as<uint8_t>(bufs_[24]);
+  a.wcarry = as<uint32_t>(bufs_[25]);
   a.rules = as<const unsigned long long>(bufs_[17]);
   a.rule_mask = rcap ? rcap - 1 : 0;
   a.kinds = rules.kinds;
@@ -655,6 +703,7 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   a.iout = as<uint32_t>(bufs_[22]);
   hipLaunchKernelGGL(filter_mark, dim3(blocks_u), dim3(kBlock), 0, st, a);
   hipLaunchKernelGGL(filter_select, dim3(blocks_u), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(filter_count, dim3(blocks), dim3(kBlock), 0, st, a);
   if (!ok(hipGetLastError(), "filter launch", err) ||
       !ok(hipcub::DeviceScan::ExclusiveSum(bufs_[23], scan_bytes, In(Count(0), GroupCount{a.perm, a.cnt, uint32_t(np)}),
                                            as<uint32_t>(bufs_[10]), int(np + 1), st),
