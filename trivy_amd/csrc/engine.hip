@@ -100,7 +100,13 @@ const char* variant_name(int v) {
   if (v == 0) return "auto";
   return v > 0 && v < kNumVariants ? kVariantNames[v - 1] : nullptr;
 }
-int resolve_variant(int v, uint32_t) { return v == 0 ? 1 + kAutoVariant : v; }
+// "auto": per grammar set, the fastest variant of bench.py --sweep on MI355X:
+// dpkg-only batches (C2) fused K=4; rpm/apk and mixed batches (C5, C4, C3) fused K=2, whose
+// lower register count keeps 5 waves per SIMD where the filtered K=4 kernel drops to 4.
+int resolve_variant(int v, uint32_t gm) {
+  if (v != 0) return v;
+  return 1 + (grammar_index(gm) == 0 ? kAutoVariant : kAutoVariantFiltered);
+}
 
 // ---- HostBatch ------------------------------------------------------------------------------
 

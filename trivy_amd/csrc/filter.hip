@@ -375,14 +375,35 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
   __shared__ uint32_t pflag[kBlock];           //   and flags (loaded once per package and chunk)
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  // software-pipelined: the next chunk's pair words (and its packages' run starts) are loaded
+  // while this chunk waits on its placement bases and barriers
+  uint32_t n_key = kEmpty, n_cls = kNoClass, n_p = 0, n_adv = 0, n_rb = 0;
+  auto load_pairs = [&](uint64_t c) {
+    const uint64_t j = c + tid;
+    if (j < a.n) {
+      n_key = a.skey[j];
+      n_cls = a.pcls[j];  // pair_class, from filter_select
+      n_p = a.pkg[j];
+      n_adv = a.adv[j];
+    }
+  };
+  {
+    const uint64_t c = uint64_t(blockIdx.x) * kBlock;
+    load_pairs(c);
+    if (c + tid < a.n) n_rb = a.run_b[n_p];
+  }
   for (uint64_t c0 = uint64_t(blockIdx.x) * kBlock; c0 < a.n; c0 += stride) {
     const uint64_t i = c0 + tid;
     const bool valid = i < a.n;
-    const uint32_t key = valid ? a.skey[i] : kEmpty;
-    const uint32_t cls = valid ? uint32_t(a.pcls[i]) : kNoClass;  // pair_class, from filter_select
-    const uint32_t p = valid ? a.pkg[i] : 0u;
-    const uint32_t rb = valid ? a.run_b[p] : 0u;
+    const uint32_t key = valid ? n_key : kEmpty;
+    const uint32_t cls = valid ? n_cls : kNoClass;
+    const uint32_t p = valid ? n_p : 0u;
+    const uint32_t adv = n_adv;
+    const uint32_t rb = valid ? n_rb : 0u;
+    const uint32_t rb0 = __shfl(rb, 0, 64);  // the chunk's first package's run start (wave 0)
     const uint64_t rs = rb > c0 ? rb : c0;  // the package's first pair in this chunk
+    const bool more = c0 + stride < a.n;
+    if (more) load_pairs(c0 + stride);
     // block-wide exclusive prefix of the packed one-hot counters (counts <= 256 per field)
     unsigned long long x = one_hot(cls);
 #pragma unroll
@@ -392,10 +413,7 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
     }
     if (lane == 63) wsum[wave] = x;
     // the run entering the chunk: its classes before c0 (filter_count left them per wave)
-    if (tid < uint32_t(kClasses)) {
-      const uint32_t rb0 = a.run_b[a.pkg[c0]];
-      carry[tid] = rb0 < c0 ? a.wcarry[(c0 >> 6) * kClasses + tid] : 0u;
-    }
+    if (tid < uint32_t(kClasses)) carry[tid] = rb0 < c0 ? a.wcarry[(c0 >> 6) * kClasses + tid] : 0u;
     if (valid && i == rs) {  // the package's first lane: its placement bases, once
       const uint32_t f = a.fl[p];
       pflag[tid] = f;
@@ -410,6 +428,7 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
       }
       if (a.kinds & 7u) base[tid][kIgnClass] = a.ign_off[p];
     }
+    if (more && c0 + stride + tid < a.n) n_rb = a.run_b[n_p];
     __syncthreads();
     unsigned long long wbase = 0;
 #pragma unroll
@@ -426,7 +445,7 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
         if (at < a.n) {
           uint32_t* o = a.iout + 3 * at;
           o[0] = p;
-          o[1] = a.adv[i];
+          o[1] = adv;
           o[2] = a.ign[i];
         }
       } else {
@@ -452,7 +471,7 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
           }
           at = uint64_t(a.off[gb]) + r;
         }
-        if (at < a.n) a.out[at] = make_uint2(p, a.adv[i]);  // always true for a list grouped by package
+        if (at < a.n) a.out[at] = make_uint2(p, adv);  // always true for a list grouped by package
       }
     }
     __syncthreads();  // pre / carry / base are rewritten by the next chunk

@@ -5,8 +5,8 @@
 
 namespace tvm {
 const SweepFn* sweep_table(bool filt) {
-#define TVM_PLAIN_(F, K, MB, NAME) F ? nullptr : &launch_sweep<K, MB, false>,
-#define TVM_FILT_(F, K, MB, NAME) F ? nullptr : &launch_sweep<K, MB, true>,
+#define TVM_PLAIN_(F, K, MB, NAME) F ? nullptr : &launch_sweep<K, MB, 0>,
+#define TVM_FILT_(F, K, MB, NAME) F ? nullptr : &launch_sweep<K, MB, 2>,
   static const SweepFn plain[] = {TVM_MATCH_VARIANTS(TVM_PLAIN_)};
   static const SweepFn filt_[] = {TVM_MATCH_VARIANTS(TVM_FILT_)};
 #undef TVM_PLAIN_

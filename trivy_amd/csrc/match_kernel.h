@@ -371,7 +371,7 @@ __global__ __launch_bounds__(kTile) void probe_kernel(ProbeArgs a) {
 
 // ---- sweep_kernel helpers ---------------------------------------------------------------
 
-template <bool FILT>
+template <int FILT>
 struct SweepShared {
   uint64_t k0[kTile], k1[kTile];  // key heads by tile package
   uint32_t kinfo[kTile];
@@ -388,10 +388,14 @@ struct SweepShared {
 
 // Per-package predicates of a ROW_FILTER row (common.h RowAux); p = the package's index
 // in the launch (its tail slot holds a Maven package's text location, probe_one).
+// FILT (the sweep's template flag): 0 no row filters, 1 filters without Maven programs (the OS
+// grammar set, whose rows never carry AUX_MVN: keeps the program evaluator's registers out of
+// that kernel), 2 all filters.
+template <int FILT>
 __device__ __forceinline__ bool aux_pass(const SweepArgs& a, uint32_t ridx, uint2 pa, uint32_t ki, uint32_t p) {
   const RowAux x = a.db.aux[ridx];
   const uint32_t* ids = a.db.aux_ids + x.list_off;
-  if (x.kind & AUX_MVN) {  // the installed parse packed by probe_one, the program's packed bounds
+  if (FILT >= 2 && (x.kind & AUX_MVN)) {  // the installed parse packed by probe_one, the program's packed bounds
     const uint4 t = a.tail[p];
     const MvnPackedView V{reinterpret_cast<const uint32_t*>(a.spill + t.x), int(t.y & 0xFFFFu),
                           a.arena + (uint64_t(t.z) | (uint64_t(t.w) << 32))};
@@ -442,7 +446,7 @@ __device__ __forceinline__ int cmp_head(uint64_t a0, uint64_t a1, uint32_t na, u
 // Interval test of tile package q's installed key against one row (global index ridx).
 // The common case (a bound decided by the inline 16-byte heads) runs without branches;
 // a 16-byte tie reads the key tails, a lower bound (library / rpm ranges) its key head.
-template <bool FILT, class S>
+template <int FILT, class S>
 __device__ __forceinline__ bool eval_row(const SweepArgs& a, const S& s, uint32_t q, uint32_t p, const Row& row,
                                          uint32_t ridx) {
   const uint32_t ki = s.kinfo[q];
@@ -471,13 +475,13 @@ __device__ __forceinline__ bool eval_row(const SweepArgs& a, const S& s, uint32_
   m = m && (ki & KI_VALID);
   m = m || (row.adv & ROW_ALWAYS);
   if constexpr (FILT) {
-    if (m && (row.adv & ROW_FILTER)) m = aux_pass(a, ridx, s.pattr[q], ki, p);
+    if (m && (row.adv & ROW_FILTER)) m = aux_pass<FILT>(a, ridx, s.pattr[q], ki, p);
   }
   return m;
 }
 
 // Tile package (nz rank) of pair j by binary search of the nz scan (tiles too large for the map).
-template <bool FILT>
+template <int FILT>
 __device__ __forceinline__ uint32_t pair_rank(const SweepShared<FILT>& s, uint32_t nnz, uint32_t j) {
   uint32_t lo = 0, hi = nnz;  // last r with nz_scan[r] <= j
   while (hi - lo > 1) {
@@ -495,7 +499,7 @@ __device__ __forceinline__ uint32_t pair_rank(const SweepShared<FILT>& s, uint32
 // one barrier per round for the wave totals - into the LDS buffer while it has room
 // (pass 1, which also counts matches per package), or straight to the output at base +
 // position (DIRECT: pass 2, for a tile with more matches than the buffer).
-template <int K, int MB, bool FILT, bool DIRECT>
+template <int K, int MB, int FILT, bool DIRECT>
 __device__ __forceinline__ uint32_t sweep(const SweepArgs& a, SweepShared<FILT>& s, uint32_t* madv, uint8_t* mq,
                                           const uint8_t* map, uint32_t nnz, uint32_t total, uint32_t tid,
                                           unsigned long long base) {
@@ -576,7 +580,7 @@ __device__ __forceinline__ uint32_t sweep(const SweepArgs& a, SweepShared<FILT>&
 }
 
 // The sweep of tile t (packages t * 256 ..) given each lane's package record r.
-template <int K, int MB, bool FILT>
+template <int K, int MB, int FILT>
 __device__ __forceinline__ void sweep_tile(const SweepArgs& a, SweepShared<FILT>& s, uint32_t* madv, uint8_t* mq,
                                            uint8_t* map, uint32_t t, uint32_t tid, const PkgRec& r) {
   const uint32_t lane = tid & 63, wave = tid >> 6;
@@ -649,7 +653,7 @@ __device__ __forceinline__ void sweep_tile(const SweepArgs& a, SweepShared<FILT>
   }
 }
 
-template <int K, int MB, bool FILT>
+template <int K, int MB, int FILT>
 __global__ __launch_bounds__(kTile) void sweep_kernel(SweepArgs a) {
   __shared__ SweepShared<FILT> s;
   __shared__ uint32_t madv[MB];
@@ -668,7 +672,7 @@ __global__ __launch_bounds__(kTile) void sweep_kernel(SweepArgs a) {
 // of one CU sit in different phases, so one tile's probe latency overlaps another's sweep.
 // DIAG (measurement only, wrong match lists by construction; "diag_*" variants): bit 0 skips
 // the version encoder, bit 1 the index probe, bit 2 the sweep.
-template <uint32_t GM, int K, int MB, bool FILT, int DIAG = 0, int WPE = 1>
+template <uint32_t GM, int K, int MB, int FILT, int DIAG = 0, int WPE = 1>
 __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
   constexpr uint32_t kStageVec = kStage / 16 + 2;
   constexpr uint32_t kMbufVec = (MB * 5 + 15) / 16;
@@ -728,12 +732,12 @@ void launch_probe(uint32_t n_tiles, hipStream_t st, const ProbeArgs& a) {
   hipLaunchKernelGGL((probe_kernel<GM, DIAG>), dim3(n_tiles), dim3(kTile), 0, st, a);
 }
 
-template <int K, int MB, bool FILT>
+template <int K, int MB, int FILT>
 void launch_sweep(uint32_t n_tiles, hipStream_t st, const SweepArgs& a) {
   hipLaunchKernelGGL((sweep_kernel<K, MB, FILT>), dim3(n_tiles), dim3(kTile), 0, st, a);
 }
 
-template <uint32_t GM, int K, int MB, bool FILT, int DIAG = 0, int WPE = 1>
+template <uint32_t GM, int K, int MB, int FILT, int DIAG = 0, int WPE = 1>
 void launch_fused(uint32_t n_tiles, hipStream_t st, const FusedArgs& a) {
   hipLaunchKernelGGL((fused_kernel<GM, K, MB, FILT, DIAG, WPE>), dim3(n_tiles), dim3(kTile), 0, st, a);
 }

@@ -35,4 +35,5 @@ constexpr int kNumTuned = 0 TVM_MATCH_VARIANTS(TVM_VARIANT_COUNT_);
 #undef TVM_VARIANT_COUNT_
 
 // Variant (index into the list) the engine launches by default.
-constexpr int kAutoVariant = 0;  // fused_k4_m2048: fastest on C2 and C5 (bench.py --sweep, MI355X)  // fused_k4_m2048: fastest on C2 (bench.py --sweep, MI355X)
+constexpr int kAutoVariant = 0;          // fused_k4_m2048: fastest on C2 (dpkg only)
+constexpr int kAutoVariantFiltered = 3;  // fused_k2_m2048: fastest on C5 / C4 (bench.py --sweep, MI355X)
