@@ -303,6 +303,24 @@ int tvm_pipeline_stats(tvm_batch* b, uint64_t out[3]);
  * batch version, copy flags PKG_ID | PKG_NAME | IDENTIFIER | LAYER (the caller copies them from
  * its package, whose Name is the plain name, not the modular lookup name). */
 int tvm_match_redhat_result(tvm_engine* e, tvm_batch* b, tvm_result* out, char* err, size_t errlen);
+/* Enqueues the same per-CVE merge on the engine stream (no host round trip) and makes the
+ * MERGED list the batch's match list: from here until the next tvm_match_launch, the pairs
+ * of tvm_match_status / _fetch / _fill / _fill_fetch / _filter are, for Red Hat packages,
+ * one {package, advisory} per (package, VulnerabilityID) in VulnerabilityID order, where the
+ * advisory is the representative member (the one with the greatest FixedVersion when any
+ * member is fixed - its FixedVersion is the merged one - else the first); the first member
+ * still supplies Status and Severity to FillInfo (redhat.go:140-171 -> vulnerability.go:60).
+ * Pairs of other drivers' packages are unchanged.  This is the reference's order of work:
+ * DetectVulnerabilities (merged) -> FillInfo -> result.Filter, all on the device. */
+int tvm_match_redhat_merge(tvm_engine* e, tvm_batch* b, char* err, size_t errlen);
+/* After tvm_match_redhat_merge (+ sync): the merged Red Hat vulnerabilities of the listed
+ * {package, advisory} pairs (e.g. tvm_match_filter_fetch's survivors), as
+ * tvm_match_redhat_result builds them; pairs of other drivers are skipped. */
+int tvm_match_redhat_vulns(tvm_engine* e, tvm_batch* b, const uint32_t* pairs, uint64_t n, tvm_result* out,
+                           char* err, size_t errlen);
+/* Times `steps` back-to-back merges on the engine stream with HIP events (ms total); leaves
+ * the batch on its merged list. */
+int tvm_match_redhat_merge_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err, size_t errlen);
 
 /* ---- vulnerability detail: FillInfo ------------------------------------------------ */
 /* One detected vulnerability as FillInfo reads it (vulnerability.go:60-109). */
@@ -338,7 +356,9 @@ int tvm_fill_info(tvm_engine* e, const tvm_fill_in* in, size_t n, tvm_fill_resul
 void tvm_fill_result_free(tvm_fill_result* r);
 /* Batch path: enqueue FillInfo over the batch's device match list right behind
  * tvm_match_launch (same stream, no host round trip); each (package, advisory) pair is
- * filled as its driver's Detect would have populated it (no Red Hat per-CVE merge). */
+ * filled as its driver's Detect would have populated it - after tvm_match_redhat_merge, a
+ * Red Hat pair as its merged DetectedVulnerability (Status / Severity of the first member,
+ * FixedVersion of the representative). */
 int tvm_match_fill(tvm_engine* e, tvm_batch* b, char* err, size_t errlen);
 /* After sync: per pair, in tvm_match_fetch order, 4 uint32: {vulnerability record
  * (0xFFFFFFFF = not found), status, severity code

@@ -1,5 +1,5 @@
-"""GPU: the rpm/apk (BASELINE.json C5) and language-package (C3) workloads through the batch
-API - 400k packages per run over a generated DB of each config's platform mix - checked
+"""GPU: the rpm/apk (BASELINE.json C5), language-package (C3) and mixed OS + language (C4)
+workloads through the batch API - 400k packages per run over a generated DB of each config's platform mix - checked
 per platform on a random sample against (1) the per-driver C-ABI entry points
 (tvm_ospkg_driver_detect / tvm_library_detect, one launch per sample) and (2) the oracle's
 drivers (oracle/drivers.py, oracle/library.py).  (2) pins the semantics, (1) vs the batch
@@ -14,7 +14,11 @@ from tools import synth_mix as sm
 
 pytestmark = pytest.mark.gpu
 
-CFGS = {"c5": (sm.C5_PLATS, sm.C5_WEIGHTS, 3000), "c3": (sm.C3_PLATS, sm.C3_WEIGHTS, 5000)}
+# C4 (BASELINE config 4): the mixed batch - dpkg (Debian / Ubuntu), the Red Hat family
+# (Red Hat CPE sets + merge, Oracle ksplice, alma, rocky arches), Alpine and four lockfile
+# ecosystems interleaved in one launch of the all-grammar kernel
+CFGS = {"c5": (sm.C5_PLATS, sm.C5_WEIGHTS, 3000), "c3": (sm.C3_PLATS, sm.C3_WEIGHTS, 5000),
+        "c4": (sm.C4_PLATS, sm.C4_WEIGHTS, 2500)}
 
 
 @pytest.mark.parametrize("cfg", list(CFGS))

@@ -23,14 +23,19 @@ C5_PLATS = [("Oracle Linux 8", "oracle"), ("Oracle Linux 9", "oracle"), ("Red Ha
 C5_WEIGHTS = [5, 5, 30, 8, 8, 15, 15, 7, 7]  # RHEL family 70 (Red Hat 30) / Alpine 30
 C3_PLATS = [("go::", "go"), ("maven::", "maven"), ("npm::", "npm"), ("pip::", "pip")]
 C3_WEIGHTS = [15, 20, 40, 25]
-# C4 (BASELINE config 4): one mixed batch, OS packages 60 % / language packages 40 %
-C4_PLATS = [("Oracle Linux 9", "oracle"), ("alma 9", "alma"), ("alpine 3.20", "alpine"), ("rocky 9", "rocky")] + C3_PLATS
-C4_WEIGHTS = [12, 18, 15, 15] + [6, 8, 16, 10]
+# C4 (BASELINE config 4): one mixed batch, OS packages 60 % / language packages 40 %: the
+# dpkg fleet (Debian / Ubuntu), the Red Hat family (Red Hat with CPE sets and modular keys,
+# Oracle with ksplice, alma, rocky arch entries), Alpine, and the four lockfile ecosystems
+C4_PLATS = [("Oracle Linux 9", "oracle"), ("Red Hat", "redhat"), ("alma 9", "alma"), ("alpine 3.20", "alpine"),
+            ("debian 12", "debian"), ("rocky 9", "rocky"), ("ubuntu 22.04", "ubuntu")] + C3_PLATS
+C4_WEIGHTS = [4, 12, 6, 8, 14, 6, 10] + [6, 8, 16, 10]
 C3_ROOTS = {"go": ["go::GitHub Security Advisory Go", "go::The Go Vulnerability Database"],
             "maven": ["maven::GitHub Security Advisory Maven"], "npm": ["npm::GitHub Security Advisory npm"],
             "pip": ["pip::GitHub Security Advisory pip"]}
 DRIVER_OF = {"alma": ("alma", "{}"), "rocky": ("rocky", "{}"), "oracle": ("oracle", "{}"),
-             "alpine": ("alpine", "{}.1"), "redhat": ("redhat", "{}")}
+             "alpine": ("alpine", "{}.1"), "redhat": ("redhat", "{}"), "debian": ("debian", "{}"),
+             "ubuntu": ("ubuntu", "{}")}
+DPKG = ("debian", "ubuntu")
 # Red Hat (one "Red Hat" bucket for every release; the CPE sets pick the release):
 # CPE indices per release and the repositories / NVRs the "Red Hat CPE" buckets map to them
 RH_CPES = {7: [0, 1], 8: [2, 3], 9: [4, 5]}
@@ -142,6 +147,12 @@ def _lib_adv(rng, kind, ma, mi, f):
     return adv
 
 
+def _deb(ep, ma, mi, p, r, ubuntu, tilde):
+    v = f"{ma}.{mi}.{p}" + ("~rc1" if tilde else "") + "-" + (f"{r}ubuntu0.{r % 7}" if ubuntu else
+                                                             (f"{r}+deb12u{r % 5}" if r % 3 == 0 else f"{r}"))
+    return f"{ep}:{v}" if ep else v
+
+
 def make_mix_db(plats, keys_per_plat, seed=0x5EED, mean_adv=6, max_adv=400):
     rng = np.random.default_rng(seed)
     keys, key_plat, key_base, records, sources = [], [], [], [], []
@@ -172,7 +183,12 @@ def make_mix_db(plats, keys_per_plat, seed=0x5EED, mean_adv=6, max_adv=400):
             for j in range(int(cnt[i])):
                 f = int(rng.integers(0, 40))
                 r = int(rng.integers(1, 9))
-                if kind == "alpine":
+                if kind in DPKG:  # debian.go / ubuntu.go: unfixed (15 %) reported; Debian severity
+                    fx = "" if rng.random() < 0.15 else _deb(flag, ma, mi, f, r, kind == "ubuntu", rng.random() < 0.03)
+                    val = {"FixedVersion": fx}
+                    if rng.random() < 0.25:
+                        val.update({"Severity": int(rng.integers(1, 5)), "Status": int(rng.integers(0, 8))})
+                elif kind == "alpine":
                     val = {"FixedVersion": f"{ma}.{mi}.{f}-r{r}" if rng.random() > 0.01 else "0"}
                 elif kind == "alma":
                     val = {"FixedVersion": _rpm(flag, ma, mi, f, r, el, 0)}
@@ -291,6 +307,16 @@ def make_mix_batch(db, n, weights, seed, miss=0.25, zipf=2.5):
             full = _cat(mmp, b"-", relv)
             g["ver"] = np.where(epoch > 0, _cat(_s(epoch), b":", full), full)
             g["arch"] = np.array(ARCHES, dtype="S")[rng.choice(4, m, p=[0.6, 0.15, 0.2, 0.05])]
+        elif kind in DPKG:  # SrcVersion / SrcRelease / SrcEpoch formatted as utils.FormatSrcVersion
+            up = np.where(rng.random(m) < 0.03, _cat(mmp, b"~rc1"), mmp)
+            if kind == "ubuntu":
+                relv = _cat(_s(rel), b"ubuntu0.", _s(rel % 7))
+            else:
+                relv = np.where(rel % 3 == 0, _cat(_s(rel), b"+deb12u", _s(rel % 5)), _s(rel))
+            epoch = np.where(rng.random(m) < 0.9, flag, 0)
+            g["version"], g["rel"], g["epoch"] = up, relv, epoch
+            full = _cat(up, b"-", relv)
+            g["ver"] = np.where(epoch > 0, _cat(_s(epoch), b":", full), full)
         elif kind == "alpine":
             g["ver"] = _cat(mmp, b"-r", _s(rel))
             g["rel"] = np.full(m, b"", dtype="S1")

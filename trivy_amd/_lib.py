@@ -134,6 +134,11 @@ _SIG = [
                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                   ctypes.c_void_p, ctypes.c_uint32]),
     ("tvm_match_redhat_result", ctypes.c_int, [_P, _P, ctypes.POINTER(Result), ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_match_redhat_merge", ctypes.c_int, [_P, _P, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_match_redhat_merge_time", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                                   ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_match_redhat_vulns", ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, ctypes.POINTER(Result), ctypes.c_char_p,
+                                              ctypes.c_size_t]),
     ("tvm_batch_upload", ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_match_launch", ctypes.c_int, [_P, _P, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_engine_sync", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t]),

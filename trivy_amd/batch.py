@@ -97,6 +97,36 @@ class MatchBatch:
         finally:
             lib().tvm_result_free(ctypes.byref(res))
 
+    def redhat_merge(self):
+        """Enqueue the per-CVE merge on the device (tvm_match_redhat_merge): from now until
+        the next launch the batch's match list - pairs(), fill(), filter() - is the merged
+        one (Red Hat packages: one pair per (package, VulnerabilityID))."""
+        e = errbuf()
+        self._check(lib().tvm_match_redhat_merge(self.engine.h, self.h, e, len(e)), e, "tvm_match_redhat_merge")
+        return self
+
+    def redhat_merge_time(self, steps):
+        """ms per merge over `steps` back-to-back merges (HIP events on the engine stream)."""
+        ms = ctypes.c_double()
+        e = errbuf()
+        self._check(lib().tvm_match_redhat_merge_time(self.engine.h, self.h, steps, ctypes.byref(ms), e, len(e)), e,
+                    "tvm_match_redhat_merge_time")
+        return ms.value / steps
+
+    def redhat_vulns(self, pairs, pkgs):
+        """The merged Red Hat DetectedVulnerabilities of the given merged-list pairs (e.g.
+        filtered_pairs()), in that order; pairs of other drivers are skipped."""
+        from ._lib import Result
+        from .detector.ospkg import _convert
+        pr = np.ascontiguousarray(pairs, dtype=np.uint32).reshape(-1, 2)
+        res, e = Result(), errbuf()
+        self._check(lib().tvm_match_redhat_vulns(self.engine.h, self.h, pr.ctypes.data if len(pr) else None, len(pr),
+                                                 ctypes.byref(res), e, len(e)), e, "tvm_match_redhat_vulns")
+        try:
+            return _convert(res, pkgs)
+        finally:
+            lib().tvm_result_free(ctypes.byref(res))
+
     def add_arena(self, bucket, n, arena, name_off, name_len, ver_off, ver_len):
         """Adds n packages whose name/version bytes already sit in one arena (u64 offsets,
         u32 lengths as numpy arrays); returns the first index."""

@@ -9,6 +9,7 @@
 #include <mutex>
 #include <shared_mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "db.h"
@@ -42,6 +43,7 @@ struct tvm_engine {
   }
   tvm_db* db = nullptr;
   int device = 0;
+  uint64_t gen = 0;  // table generation: tvm_engine_swap increments it (under the exclusive lock)
 };
 
 struct tvm_batch {
@@ -57,13 +59,20 @@ struct tvm_batch {
   // (rep[f][i] counts where rep_has[f][i] is set; shorter vectors = defaults beyond)
   std::vector<std::string> rep[3];
   std::vector<uint8_t> rep_has[3];
-  RedHatMerge rh;                      // tvm_match_redhat_result state
+  RedHatMerge rh;                      // tvm_match_redhat_merge / _result state
+  bool merged = false;                 // the merged list (rh) is the current match list
   std::unique_ptr<Pipeline> pipe;      // tvm_pipeline_* state
   uint32_t pkg_base = 0;               // tvm_batch_set_package_base
   uint64_t pipe_total = 0;
   bool external_out = false;  // m.pkg / m.adv belong to the caller (tvm_batch_upload_into)
-  bool uploaded = false;
+  bool uploaded = false;      // dev / m hold real device buffers
+  bool pinned = false;        // tvm_pipeline_prepare pinned the host arrays: no more adds
   int device = 0;
+  // The engine and table generation the batch's platform / arch / CPE ids were resolved
+  // against (bound at the first call that names an engine); after tvm_engine_swap the
+  // batch must be rebuilt, since the new DB numbers its platforms differently.
+  const tvm_engine* owner = nullptr;
+  uint64_t gen = 0;
 };
 
 namespace {
@@ -76,6 +85,24 @@ void set_err(char* err, size_t errlen, const std::string& msg) {
 }
 
 std::string_view sv(const tvm_str& s) { return s.p ? std::string_view(s.p, s.n) : std::string_view(); }
+
+// Binds a batch to (engine, generation) on first use; false when it belongs to another
+// engine or to tables a swap has replaced.  Callers hold the engine's lock (shared).
+bool bind(tvm_batch* b, const tvm_engine* e) {
+  if (!b->owner) {
+    b->owner = e;
+    b->gen = e->gen;
+    return true;
+  }
+  return b->owner == e && b->gen == e->gen;
+}
+
+// The batch's current match list: the merged one after tvm_match_redhat_merge.
+const DevMatches& cur(const tvm_batch* b) { return b->merged ? b->rh.merged().m : b->m; }
+const uint32_t* cur_base(const tvm_batch* b) { return b->merged ? b->rh.merged().base : nullptr; }
+
+constexpr const char* kStale =
+    "batch was built against other tables (another engine, or before tvm_engine_swap): rebuild it";
 
 std::vector<Pkg> to_pkgs(const tvm_package* pkgs, size_t n) {
   std::vector<Pkg> out(n);
@@ -255,6 +282,7 @@ int tvm_engine_swap(tvm_engine* e, tvm_db* db, char* err, size_t errlen) {
   e->eng.reset(fresh);
   e->fill.reset(fresh_fill);
   e->db = db;
+  e->gen++;
   if (e->rh_rank) {
     (void)hipFree(e->rh_rank);
     e->rh_rank = nullptr;
@@ -366,7 +394,8 @@ void tvm_batch_free(tvm_batch* b) {
     (void)hipSetDevice(b->device);
     for (void* p : {static_cast<void*>(b->dev.pk), static_cast<void*>(b->dev.tile_off), static_cast<void*>(b->dev.arena),
                     static_cast<void*>(b->dev.attr), static_cast<void*>(b->dev.cpe_bits), static_cast<void*>(b->dev.rec),
-                    static_cast<void*>(b->dev.tail), static_cast<void*>(b->external_out ? nullptr : b->m.pkg),
+                    static_cast<void*>(b->dev.tail), static_cast<void*>(b->dev.spill),
+                    static_cast<void*>(b->external_out ? nullptr : b->m.pkg),
                     static_cast<void*>(b->external_out ? nullptr : b->m.adv), static_cast<void*>(b->m.dir),
                     static_cast<void*>(b->m.ctl),
                     static_cast<void*>(b->fill_out)})
@@ -383,7 +412,9 @@ static void reserve_more(HostBatch& hb, size_t n) {
 }
 
 int64_t tvm_batch_add(tvm_batch* b, tvm_engine* e, const char* bucket, tvm_str name, tvm_str version) {
-  if (!b || !e || !bucket || b->uploaded) return -1;
+  if (!b || !e || !bucket || b->uploaded || b->pinned) return -1;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e)) return -1;
   b->target_begin.push_back(uint32_t(b->hb.pk.size()));
   int32_t plat = e->eng->db().find_plat(bucket);
   b->hb.add(plat < 0 ? 0xFFFFFFFFu : uint32_t(plat), sv(name), sv(version));
@@ -393,8 +424,11 @@ int64_t tvm_batch_add(tvm_batch* b, tvm_engine* e, const char* bucket, tvm_str n
 int64_t tvm_batch_add_many(tvm_batch* b, tvm_engine* e, const char* bucket, size_t n, const char* arena,
                            const uint64_t* name_off, const uint32_t* name_len, const uint64_t* ver_off,
                            const uint32_t* ver_len) {
-  if (!b || !e || !bucket || b->uploaded || (n && (!arena || !name_off || !name_len || !ver_off || !ver_len)))
+  if (!b || !e || !bucket || b->uploaded || b->pinned ||
+      (n && (!arena || !name_off || !name_len || !ver_off || !ver_len)))
     return -1;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e)) return -1;
   int32_t plat = e->eng->db().find_plat(bucket);
   const uint32_t pid = plat < 0 ? 0xFFFFFFFFu : uint32_t(plat);
   const int64_t first = int64_t(b->hb.pk.size());
@@ -415,7 +449,9 @@ int64_t tvm_batch_add_many_ex(tvm_batch* b, tvm_engine* e, const char* bucket, s
 }
 
 int64_t tvm_batch_cpe_set(tvm_batch* b, tvm_engine* e, const tvm_str* content_sets, size_t n, tvm_str nvr) {
-  if (!b || !e || b->uploaded || (n && !content_sets)) return -1;
+  if (!b || !e || b->uploaded || b->pinned || (n && !content_sets)) return -1;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e)) return -1;
   const DB& db = e->eng->db();
   HostBatch& hb = b->hb;
   const uint32_t words = std::max<uint32_t>((db.n_cpe + 31) / 32, 1);
@@ -436,13 +472,15 @@ int64_t tvm_batch_add_many_attrs(tvm_batch* b, tvm_engine* e, const char* bucket
                                  const uint64_t* name_off, const uint32_t* name_len, const uint64_t* ver_off,
                                  const uint32_t* ver_len, const tvm_attr_cols* cols, uint32_t flags) {
   const uint32_t known = TVM_ATTR_ARCH | TVM_ATTR_KSPLICE | TVM_ATTR_CPESET;
-  if (!b || !e || !bucket || b->uploaded || (flags & ~known) ||
+  if (!b || !e || !bucket || b->uploaded || b->pinned || (flags & ~known) ||
       ((flags & TVM_ATTR_KSPLICE) && (flags & TVM_ATTR_CPESET)) ||  // one attribute word: tag or CPE set
       (n && (!arena || !name_off || !name_len || !ver_off || !ver_len)) ||
       (n && (flags & (TVM_ATTR_ARCH | TVM_ATTR_CPESET)) && !cols) ||
       (n && (flags & TVM_ATTR_ARCH) && (!cols->arch_off || !cols->arch_len)) ||
       (n && (flags & TVM_ATTR_CPESET) && !cols->cpe_set))
     return -1;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e)) return -1;
   const DB& db = e->eng->db();
   const size_t n_sets = b->hb.cpe_words ? b->hb.cpe_bits.size() / b->hb.cpe_words : 0;
   if (flags & TVM_ATTR_CPESET)
@@ -477,10 +515,14 @@ int tvm_batch_upload(tvm_engine* e, tvm_batch* b, uint64_t cap, char* err, size_
   if (!e || !b) return TVM_EINVAL;
   std::shared_lock<std::shared_mutex> lk(e->mu);
   std::string msg;
+  if (!bind(b, e)) {
+    set_err(err, errlen, kStale);
+    return TVM_EINVAL;
+  }
   if (b->uploaded) {
-    e->eng->free_batch(b->dev);
+    Engine::free_batch(b->device, b->dev);
     if (b->external_out) b->m.pkg = b->m.adv = nullptr;
-    e->eng->free_matches(b->m);
+    Engine::free_matches(b->device, b->m);
     b->external_out = false;
     b->uploaded = false;
   }
@@ -504,7 +546,13 @@ int tvm_batch_set_package_base(tvm_batch* b, uint32_t base) {
 
 int tvm_match_launch(tvm_engine* e, tvm_batch* b, char* err, size_t errlen) {
   if (!e || !b || !b->uploaded) return TVM_EINVAL;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e)) {
+    set_err(err, errlen, kStale);
+    return TVM_EINVAL;
+  }
   std::string msg;
+  b->merged = false;
   if (!e->eng->launch(b->dev, b->m, e->eng->stream(), msg)) {
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
@@ -524,12 +572,13 @@ int tvm_engine_sync(tvm_engine* e, char* err, size_t errlen) {
 
 int tvm_match_status(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* err_pkg, uint64_t* err_bits) {
   if (!e || !b || !b->uploaded) return TVM_EINVAL;
-  unsigned long long ctl[8];
+  unsigned long long ctl[8], mctl[8];
   (void)hipSetDevice(e->device);
   if (hipMemcpy(ctl, b->m.ctl, sizeof(ctl), hipMemcpyDeviceToHost) != hipSuccess) return TVM_EDEVICE;
-  if (n_matches) *n_matches = ctl[0];
+  if (b->merged && hipMemcpy(mctl, cur(b).ctl, sizeof(mctl), hipMemcpyDeviceToHost) != hipSuccess) return TVM_EDEVICE;
+  if (n_matches) *n_matches = b->merged ? mctl[0] : ctl[0];
   if (err_pkg) *err_pkg = ctl[1] ? int64_t(b->dev.n - ctl[1]) : -1;
-  if (err_bits) *err_bits = ctl[3];
+  if (err_bits) *err_bits = ctl[3] | (b->merged ? mctl[3] : 0ull);
   return TVM_OK;
 }
 
@@ -538,11 +587,11 @@ int tvm_match_fetch(tvm_engine* e, tvm_batch* b, uint32_t* pairs, uint64_t cap, 
   int rc = tvm_match_status(e, b, &n, nullptr, nullptr);
   if (rc) return rc;
   if (n_out) *n_out = 0;
-  if (n > b->m.cap) return TVM_EINVAL;  // device buffer overflowed: re-upload with a larger cap
+  if (n > cur(b).cap) return TVM_EINVAL;  // device buffer overflowed: re-upload with a larger cap
   std::vector<uint2> ordered;
   std::string msg;
   (void)hipSetDevice(e->device);
-  if (!Engine::fetch_ordered(b->m, b->dev.n, n, ordered, e->eng->stream(), msg)) return TVM_EDEVICE;
+  if (!Engine::fetch_ordered(cur(b), b->dev.n, n, ordered, e->eng->stream(), msg)) return TVM_EDEVICE;
   n = std::min<uint64_t>(n, cap);
   if (n) memcpy(pairs, ordered.data(), n * sizeof(uint2));
   if (n_out) *n_out = n;
@@ -554,7 +603,7 @@ int tvm_match_copy_device(tvm_engine* e, tvm_batch* b, void* dst, uint64_t cap, 
   int rc = tvm_match_status(e, b, &n, nullptr, nullptr);
   if (rc) return rc;
   if (n_out) *n_out = 0;
-  if (n > b->m.cap) return TVM_EINVAL;
+  if (b->merged || n > b->m.cap) return TVM_EINVAL;  // raw lists only
   n = std::min<uint64_t>(n, cap);
   (void)hipSetDevice(e->device);
   hipStream_t st = e->eng->stream();
@@ -570,6 +619,11 @@ int tvm_match_copy_device(tvm_engine* e, tvm_batch* b, void* dst, uint64_t cap, 
 
 int tvm_match_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err, size_t errlen) {
   if (!e || !b || !b->uploaded || steps <= 0 || !ms) return TVM_EINVAL;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e)) {
+    set_err(err, errlen, kStale);
+    return TVM_EINVAL;
+  }
   (void)hipSetDevice(e->device);
   hipEvent_t t0 = nullptr, t1 = nullptr;
   hipStream_t st = e->eng->stream();
@@ -579,6 +633,7 @@ int tvm_match_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err
     msg = "hipEvent setup failed";
     rc = TVM_EDEVICE;
   }
+  b->merged = false;
   for (int i = 0; rc == TVM_OK && i < steps; i++)
     if (!e->eng->launch(b->dev, b->m, st, msg)) rc = TVM_EDEVICE;
   float f = 0;
@@ -811,20 +866,25 @@ void tvm_fill_result_free(tvm_fill_result* r) {
 int tvm_match_fill(tvm_engine* e, tvm_batch* b, char* err, size_t errlen) {
   if (!e || !b || !b->uploaded) return TVM_EINVAL;
   std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e)) {
+    set_err(err, errlen, kStale);
+    return TVM_EINVAL;
+  }
   (void)hipSetDevice(e->device);
-  if (b->fill_cap < b->m.cap) {
+  const DevMatches& m = cur(b);
+  if (b->fill_cap < m.cap) {
     if (b->fill_out) (void)hipFree(b->fill_out);
     b->fill_out = nullptr;
     b->fill_cap = 0;
     // decisions, then the filter's hand-off words (uint2) in the same allocation
-    if (hipMalloc(&b->fill_out, std::max<uint64_t>(b->m.cap, 1) * (sizeof(uint4) + sizeof(uint2))) != hipSuccess) {
+    if (hipMalloc(&b->fill_out, std::max<uint64_t>(m.cap, 1) * (sizeof(uint4) + sizeof(uint2))) != hipSuccess) {
       set_err(err, errlen, "hipMalloc(fill decisions) failed");
       return TVM_EDEVICE;
     }
-    b->fill_cap = b->m.cap;
+    b->fill_cap = m.cap;
   }
   std::string msg;
-  if (!e->fill->launch_pairs(b->m.adv, b->m.ctl, b->m.cap, b->fill_out, b->fill_side(), e->eng->stream(), msg)) {
+  if (!e->fill->launch_pairs(m.adv, cur_base(b), m.ctl, m.cap, b->fill_out, b->fill_side(), e->eng->stream(), msg)) {
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
   }
@@ -839,11 +899,11 @@ int tvm_match_fill_fetch(tvm_engine* e, tvm_batch* b, uint32_t* out4, uint64_t c
   int rc = tvm_match_status(e, b, &n, nullptr, nullptr);
   if (rc) return rc;
   if (n_out) *n_out = 0;
-  if (n > b->m.cap || n > b->fill_cap) return TVM_EINVAL;
+  if (n > cur(b).cap || n > b->fill_cap) return TVM_EINVAL;
   const uint32_t n_tiles = (b->dev.n + kTile - 1) / kTile;
   std::vector<TileDir> dir(n_tiles);
   std::vector<uint4> raw(n);
-  if ((n_tiles && hipMemcpy(dir.data(), b->m.dir, n_tiles * sizeof(TileDir), hipMemcpyDeviceToHost) != hipSuccess) ||
+  if ((n_tiles && hipMemcpy(dir.data(), cur(b).dir, n_tiles * sizeof(TileDir), hipMemcpyDeviceToHost) != hipSuccess) ||
       (n && hipMemcpy(raw.data(), b->fill_out, n * sizeof(uint4), hipMemcpyDeviceToHost) != hipSuccess))
     return TVM_EDEVICE;
   uint64_t k = 0;
@@ -864,7 +924,9 @@ int tvm_match_fill_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char
   std::string msg;
   float f = 0;
   bool ok = hipEventCreate(&t0) == hipSuccess && hipEventCreate(&t1) == hipSuccess && hipEventRecord(t0, st) == hipSuccess;
-  for (int i = 0; ok && i < steps; i++) ok = e->fill->launch_pairs(b->m.adv, b->m.ctl, b->m.cap, b->fill_out, b->fill_side(), st, msg);
+  const DevMatches& m = cur(b);
+  for (int i = 0; ok && i < steps; i++)
+    ok = e->fill->launch_pairs(m.adv, cur_base(b), m.ctl, m.cap, b->fill_out, b->fill_side(), st, msg);
   ok = ok && hipEventRecord(t1, st) == hipSuccess && hipEventSynchronize(t1) == hipSuccess &&
        hipEventElapsedTime(&f, t0, t1) == hipSuccess;
   if (t0) (void)hipEventDestroy(t0);
@@ -879,11 +941,15 @@ int tvm_match_fill_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char
 
 uint64_t tvm_match_fill_algorithmic_bytes(tvm_engine* e, tvm_batch* b) {
   uint64_t n = 0;
-  if (!e || !b || tvm_match_status(e, b, &n, nullptr, nullptr) || n > b->m.cap) return 0;
-  std::vector<uint32_t> adv(n);
+  if (!e || !b || tvm_match_status(e, b, &n, nullptr, nullptr) || n > cur(b).cap) return 0;
+  std::vector<uint32_t> adv(n), base;
   (void)hipSetDevice(e->device);
-  if (n && hipMemcpy(adv.data(), b->m.adv, n * 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
-  return e->fill->pair_bytes(adv);
+  if (n && hipMemcpy(adv.data(), cur(b).adv, n * 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  if (cur_base(b)) {
+    base.resize(n);
+    if (n && hipMemcpy(base.data(), cur_base(b), n * 4, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  }
+  return e->fill->pair_bytes(adv, base);
 }
 
 const char* tvm_fill_source_name(tvm_engine* e, uint32_t id) {
@@ -996,6 +1062,10 @@ int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint
     return TVM_EINVAL;
   }
   std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e)) {
+    set_err(err, errlen, kStale);
+    return TVM_EINVAL;
+  }
   (void)hipSetDevice(e->device);
   hipStream_t st = e->eng->stream();
   if (hipStreamSynchronize(st) != hipSuccess) return TVM_EDEVICE;
@@ -1003,7 +1073,7 @@ int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint
   int64_t errp = -1;
   int rc = tvm_match_status(e, b, &n, &errp, nullptr);
   if (rc) return rc;
-  if (n > b->m.cap || n > b->fill_cap) {
+  if (n > cur(b).cap || n > b->fill_cap) {
     set_err(err, errlen, "tvm_match_filter: run tvm_match_launch + tvm_match_fill with a large enough match buffer first");
     return TVM_EINVAL;
   }
@@ -1064,7 +1134,7 @@ int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint
     set_err(err, errlen, "tvm_match_filter: rule / VEX package, class or ID index out of range");
     return TVM_EINVAL;
   }
-  if (!b->filter.run(e->fill->dev(), b->m.pkg, b->m.adv, b->fill_side(), n, rules, vt.n_vuln_ranks(), o->severity_mask,
+  if (!b->filter.run(e->fill->dev(), cur(b).pkg, cur(b).adv, b->fill_side(), n, rules, vt.n_vuln_ranks(), o->severity_mask,
                      o->ignore_status_mask, st, msg)) {
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
@@ -1128,6 +1198,10 @@ int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32
                          size_t errlen) {
   if (!e || !b || chunk_packages == 0) return TVM_EINVAL;
   std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e)) {
+    set_err(err, errlen, kStale);
+    return TVM_EINVAL;
+  }
   b->pipe.reset(new Pipeline());
   std::string msg;
   if (!b->pipe->prepare(*e->eng, b->hb, match_cap, chunk_packages, msg)) {
@@ -1135,7 +1209,7 @@ int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
   }
-  b->uploaded = true;  // the batch is pinned in place: no more adds
+  b->pinned = true;  // the host arrays are registered in place: no more adds
   return TVM_OK;
 }
 
@@ -1143,6 +1217,10 @@ int tvm_pipeline_run(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* 
                      size_t errlen) {
   if (!e || !b || !b->pipe) return TVM_EINVAL;
   std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e)) {
+    set_err(err, errlen, kStale);
+    return TVM_EINVAL;
+  }
   std::string msg;
   uint64_t total = 0, bits = 0;
   int64_t ep = -1;
@@ -1225,53 +1303,164 @@ int tvm_batch_upload_into(tvm_engine* e, tvm_batch* b, void* pkg_dev, void* adv_
 
 // ---- Red Hat batch epilogue (redhat.hip) -------------------------------------------------
 
+namespace {
+
+// rpm-order ranks of the Red Hat advisories' fixed versions, built on first use (device).
+bool ensure_rh_rank(tvm_engine* e, std::string& err) {
+  std::lock_guard<std::mutex> g(e->rh_mu);
+  if (e->rh_rank) return true;
+  const std::vector<uint32_t> r = redhat_fixed_ranks(e->eng->db());
+  void* p = nullptr;
+  if (hipMalloc(&p, std::max<size_t>(r.size(), 1) * 4) != hipSuccess ||
+      (!r.empty() && hipMemcpy(p, r.data(), r.size() * 4, hipMemcpyHostToDevice) != hipSuccess)) {
+    if (p) (void)hipFree(p);
+    err = "redhat merge: fixed-version ranks upload failed";
+    return false;
+  }
+  e->rh_rank = static_cast<uint32_t*>(p);
+  return true;
+}
+
+RhInputs rh_inputs(tvm_engine* e, tvm_batch* b) {
+  RhInputs in;
+  in.pk = b->dev.pk;
+  in.plats = e->eng->device_plats();
+  in.n_plats = uint32_t(e->eng->db().plat_info.size());
+  in.raw = &b->m;
+  in.n_tiles = b->dev.n_tiles;
+  in.pkg_base = b->dev.pkg_base;
+  in.adv_rank = e->fill->dev().adv_rank;
+  in.fixed_rank = e->rh_rank;
+  return in;
+}
+
+// Enqueues the merge (caller holds the shared lock and has checked the batch).
+bool rh_launch(tvm_engine* e, tvm_batch* b, std::string& err) {
+  (void)hipSetDevice(e->device);
+  if (!ensure_rh_rank(e, err)) return false;
+  const RhInputs in = rh_inputs(e, b);
+  if (!b->rh.launch(in, e->eng->stream(), err)) return false;
+  b->merged = true;
+  return true;
+}
+
+// Merged Red Hat vulnerabilities of the merged list's entries `want` (all when null).
+bool rh_vulns(tvm_engine* e, tvm_batch* b, const std::vector<uint2>* want, std::vector<Vuln>& vulns, std::string& err) {
+  const DB& db = e->eng->db();
+  std::vector<uint32_t> pkg, adv, base, contrib;
+  std::vector<uint2> grp;
+  if (!b->rh.fetch(rh_inputs(e, b), pkg, adv, base, grp, contrib, e->eng->stream(), err)) return false;
+  const auto& pi = db.plat_info;
+  std::vector<RhRec> recs;
+  std::unordered_map<uint64_t, size_t> at;  // (package, representative) -> merged entry
+  for (size_t i = 0; i < pkg.size(); i++) {
+    const uint32_t plat = b->hb.pk[pkg[i] - b->dev.pkg_base].x;
+    if (plat >= pi.size() || pi[plat].drv != DRV_REDHAT) continue;
+    RhRec r{};
+    r.pkg = pkg[i];
+    r.base = base[i];
+    r.best = db.advs[adv[i]].fixed.empty() ? RH_NONE : adv[i];
+    r.start = grp[i].x;
+    r.len = grp[i].y;
+    if (want) at.emplace((uint64_t(pkg[i]) << 32) | adv[i], recs.size());
+    recs.push_back(r);
+  }
+  if (want) {
+    std::vector<RhRec> sel;
+    for (const uint2& q : *want) {
+      auto it = at.find((uint64_t(q.x) << 32) | q.y);
+      if (it != at.end()) sel.push_back(recs[it->second]);
+    }
+    recs.swap(sel);
+  }
+  redhat_batch_vulns(db, b->hb, recs, contrib, b->dev.pkg_base, vulns);
+  return true;
+}
+
+}  // namespace
+
+int tvm_match_redhat_merge(tvm_engine* e, tvm_batch* b, char* err, size_t errlen) {
+  if (!e || !b || !b->uploaded) return TVM_EINVAL;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e)) {
+    set_err(err, errlen, kStale);
+    return TVM_EINVAL;
+  }
+  std::string msg;
+  if (b->merged) return TVM_OK;  // already the merged list of the last launch
+  if (!rh_launch(e, b, msg)) {
+    set_err(err, errlen, msg);
+    return TVM_EDEVICE;
+  }
+  return TVM_OK;
+}
+
 int tvm_match_redhat_result(tvm_engine* e, tvm_batch* b, tvm_result* out, char* err, size_t errlen) {
   if (!e || !b || !out || !b->uploaded) return TVM_EINVAL;
   memset(out, 0, sizeof(*out));
   std::shared_lock<std::shared_mutex> lk(e->mu);
-  (void)hipSetDevice(e->device);
-  hipStream_t st = e->eng->stream();
-  uint64_t n = 0;
-  if (hipStreamSynchronize(st) != hipSuccess || tvm_match_status(e, b, &n, nullptr, nullptr)) return TVM_EDEVICE;
-  if (n > b->m.cap) {
-    set_err(err, errlen, "tvm_match_redhat_result: the match buffer overflowed");
+  if (!bind(b, e)) {
+    set_err(err, errlen, kStale);
     return TVM_EINVAL;
   }
-  const DB& db = e->eng->db();
-  {
-    std::lock_guard<std::mutex> g(e->rh_mu);
-    if (!e->rh_rank) {
-      const std::vector<uint32_t> r = redhat_fixed_ranks(db);
-      void* p = nullptr;
-      if (hipMalloc(&p, std::max<size_t>(r.size(), 1) * 4) != hipSuccess ||
-          (!r.empty() && hipMemcpy(p, r.data(), r.size() * 4, hipMemcpyHostToDevice) != hipSuccess)) {
-        set_err(err, errlen, "tvm_match_redhat_result: fixed-version ranks upload failed");
-        return TVM_EDEVICE;
-      }
-      e->rh_rank = static_cast<uint32_t*>(p);
-    }
-  }
-  RhInputs in;
-  in.pk = b->dev.pk;
-  in.plats = nullptr;
-  in.n_plats = uint32_t(db.plat_info.size());
-  in.pkg = b->m.pkg;
-  in.adv = b->m.adv;
-  in.n_dev = b->m.ctl;
-  in.n_matches = n;
-  in.pkg_base = b->dev.pkg_base;
-  in.adv_rank = e->fill->dev().adv_rank;
-  in.fixed_rank = e->rh_rank;
-  in.plats = e->eng->device_plats();
-  std::vector<RhRec> recs;
-  std::vector<uint32_t> contrib;
   std::string msg;
-  if (!b->rh.run(in, recs, contrib, st, msg)) {
+  std::vector<Vuln> vulns;
+  if ((!b->merged && !rh_launch(e, b, msg)) || !rh_vulns(e, b, nullptr, vulns, msg)) {
+    set_err(err, errlen, "tvm_match_redhat_result: " + msg);
+    return TVM_EDEVICE;
+  }
+  export_result(e->eng->db(), std::move(vulns), false, out);
+  return TVM_OK;
+}
+
+int tvm_match_redhat_vulns(tvm_engine* e, tvm_batch* b, const uint32_t* pairs, uint64_t n, tvm_result* out, char* err,
+                           size_t errlen) {
+  if (!e || !b || !out || !b->uploaded || (n && !pairs)) return TVM_EINVAL;
+  memset(out, 0, sizeof(*out));
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e) || !b->merged) {
+    set_err(err, errlen, b->merged ? kStale : "tvm_match_redhat_vulns: run tvm_match_redhat_merge first");
+    return TVM_EINVAL;
+  }
+  std::vector<uint2> want(n);
+  for (uint64_t i = 0; i < n; i++) want[i] = make_uint2(pairs[2 * i], pairs[2 * i + 1]);
+  std::string msg;
+  std::vector<Vuln> vulns;
+  if (!rh_vulns(e, b, &want, vulns, msg)) {
+    set_err(err, errlen, "tvm_match_redhat_vulns: " + msg);
+    return TVM_EDEVICE;
+  }
+  export_result(e->eng->db(), std::move(vulns), false, out);
+  return TVM_OK;
+}
+
+int tvm_match_redhat_merge_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err, size_t errlen) {
+  if (!e || !b || !b->uploaded || steps <= 0 || !ms) return TVM_EINVAL;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e)) {
+    set_err(err, errlen, kStale);
+    return TVM_EINVAL;
+  }
+  (void)hipSetDevice(e->device);
+  std::string msg;
+  if (!rh_launch(e, b, msg)) {  // sizes the buffers and builds the ranks outside the timed region
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
   }
-  std::vector<Vuln> vulns;
-  redhat_batch_vulns(db, b->hb, recs, contrib, b->dev.pkg_base, vulns);
-  export_result(db, std::move(vulns), false, out);
+  hipStream_t st = e->eng->stream();
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+  float f = 0;
+  bool ok = hipEventCreate(&t0) == hipSuccess && hipEventCreate(&t1) == hipSuccess && hipEventRecord(t0, st) == hipSuccess;
+  const RhInputs in = rh_inputs(e, b);
+  for (int i = 0; ok && i < steps; i++) ok = b->rh.launch(in, st, msg);
+  ok = ok && hipEventRecord(t1, st) == hipSuccess && hipEventSynchronize(t1) == hipSuccess &&
+       hipEventElapsedTime(&f, t0, t1) == hipSuccess;
+  if (t0) (void)hipEventDestroy(t0);
+  if (t1) (void)hipEventDestroy(t1);
+  if (!ok) {
+    set_err(err, errlen, msg.empty() ? "hipEvent timing failed" : msg);
+    return TVM_EDEVICE;
+  }
+  *ms = f;
   return TVM_OK;
 }

@@ -451,6 +451,7 @@ void DB::flatten_os(uint32_t plat, const Bucket& root, int32_t ds) {
       if (!key.poisoned) key.err = "failed to unmarshal advisory JSON: " + e;
       key.poisoned = true;
     };
+    std::vector<Advisory> rh;  // Red Hat: the key's advisories in Get order, numbered below
     for (const auto& [vid, val] : bkt.kv) {
       std::string err;
       if (val.empty()) continue;  // trivy-db forEach skips empty values
@@ -472,8 +473,7 @@ void DB::flatten_os(uint32_t plat, const Bucket& root, int32_t ds) {
               a.vuln_id = c.id;
               a.vendor_ids = {vid};
             }
-            key.advs.push_back(uint32_t(advs.size()));
-            advs.push_back(std::move(a));
+            rh.push_back(std::move(a));
           }
         }
         continue;
@@ -504,6 +504,16 @@ void DB::flatten_os(uint32_t plat, const Bucket& root, int32_t ds) {
         continue;
       }
       a.entries.clear();
+      key.advs.push_back(uint32_t(advs.size()));
+      advs.push_back(std::move(a));
+    }
+    // Red Hat: numbered in (VulnerabilityID, Get order) order - a stable sort, so the
+    // advisories of one CVE stay in Get order.  redhat.go:146-187 keys its merge by the ID
+    // (first matched member in Get order wins, fixed members merge) and sorts the result
+    // by ID, so this order changes nothing in the output; it makes a package's matches
+    // arrive grouped by ID, and the batch merge (redhat.hip) a single pass without a sort.
+    std::stable_sort(rh.begin(), rh.end(), [](const Advisory& x, const Advisory& y) { return x.vuln_id < y.vuln_id; });
+    for (Advisory& a : rh) {
       key.advs.push_back(uint32_t(advs.size()));
       advs.push_back(std::move(a));
     }

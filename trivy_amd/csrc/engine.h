@@ -83,7 +83,7 @@ struct DevBatch {
   uint64_t spill_words = 0;  // scratch for installed keys longer than 32 bytes
   uint32_t gm = 0;           // grammar bits (1 << Cmp) of the batch's platforms (libver.h GM_*)
   uint32_t pkg_base = 0;     // added to the package index of every match (multi-GPU shards)
-  uint64_t* spill = nullptr;  // the batch's own long-key scratch (drop-in contexts); nullptr: the engine's
+  uint64_t* spill = nullptr;  // the batch's own long-key / Maven-parse scratch (never shared between batches)
   uint64_t spill_cap = 0;
   // probe -> sweep hand-off (device only)
   PkgRec* rec = nullptr;
@@ -126,9 +126,11 @@ class Engine {
   bool upload(const HostBatch& hb, DevBatch& b, std::string& err);
   uint32_t grammar_set(const HostBatch& hb) const;
   uint64_t scratch_words(const HostBatch& hb) const;
-  void free_batch(DevBatch& b);
+  // Frees a batch's / a match list's device buffers (device = the GPU they live on; no
+  // engine state is touched, so a batch outlives a hot swap of the engine's tables).
+  static void free_batch(int device, DevBatch& b);
   bool alloc_matches(uint64_t cap, uint32_t n_pkgs, DevMatches& m, std::string& err);
-  void free_matches(DevMatches& m);
+  static void free_matches(int device, DevMatches& m);
 
   // Enqueues one match pass (probe + sweep over every tile) on `stream`; no host sync.
   bool launch(const DevBatch& b, const DevMatches& m, hipStream_t stream, std::string& err);
@@ -169,10 +171,6 @@ class Engine {
   DevDB d_;
   std::vector<void*> allocs_;
   uint64_t table_bytes_ = 0;
-  // per-launch scratch
-  uint64_t* spill_ = nullptr;
-  uint64_t spill_cap_ = 0;
-  bool ensure_scratch(uint64_t spill_words, std::string& err);
   struct Dropin;
   struct DropinReq;
   std::unique_ptr<Dropin> dropin_;

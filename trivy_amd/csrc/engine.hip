@@ -166,7 +166,6 @@ Engine::~Engine() {
   if (dev_ >= 0) (void)hipSetDevice(dev_);
   dropin_.reset();
   for (void* p : allocs_) (void)hipFree(p);
-  if (spill_) (void)hipFree(spill_);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -219,17 +218,6 @@ int Engine::set_variant(int v) {
   return old;
 }
 
-bool Engine::ensure_scratch(uint64_t spill_words, std::string& err) {
-  if (spill_words > spill_cap_) {
-    if (spill_) (void)hipFree(spill_);
-    spill_ = nullptr;
-    const uint64_t cap = std::max<uint64_t>(spill_words, 4096);
-    if (!hip_ok(hipMalloc(&spill_, cap * 8), "hipMalloc(spill)", err)) return false;
-    spill_cap_ = cap;
-  }
-  return true;
-}
-
 // Grammar bits (1 << Cmp) of the platforms a batch touches.
 uint32_t Engine::grammar_set(const HostBatch& hb) const {
   const auto& pi = db_->plat_info;
@@ -269,13 +257,16 @@ bool Engine::alloc_batch(const HostBatch& hb, DevBatch& b, std::string& err) {
     err = "batch attributes do not cover every package";
     return false;
   }
+  // every batch owns its scratch: launches of different batches (pipeline streams, the
+  // engine stream, other threads) never write the same words
+  b.spill_cap = std::max<uint64_t>(b.spill_words, 64);
   // +32 B tail: the kernels stage whole 16-byte lines and read names as dword triples
-  return dmalloc(&b.pk, hb.pk.size(), "hipMalloc(batch)", err) &&
+  return dmalloc(&b.spill, b.spill_cap, "hipMalloc(batch scratch)", err) && dmalloc(&b.pk, hb.pk.size(), "hipMalloc(batch)", err) &&
          dmalloc(&b.tile_off, size_t(b.n_tiles) * kGroupsPerTile + 1, "hipMalloc(group offsets)", err) &&
          dmalloc(&b.arena, (hb.arena.size() + 32 + 15) & ~size_t(15), "hipMalloc(batch arena)", err) &&
          (hb.attr.empty() || dmalloc(&b.attr, hb.attr.size(), "hipMalloc(batch attr)", err)) &&
          dmalloc(&b.rec, hb.pk.size(), "hipMalloc(package records)", err) &&
-         dmalloc(&b.tail, hb.pk.size(), "hipMalloc(key tails)", err) && ensure_scratch(b.spill_words, err);
+         dmalloc(&b.tail, hb.pk.size(), "hipMalloc(key tails)", err);
 }
 
 bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
@@ -303,11 +294,11 @@ bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
   return true;
 }
 
-void Engine::free_batch(DevBatch& b) {
-  (void)hipSetDevice(dev_);
+void Engine::free_batch(int device, DevBatch& b) {
+  (void)hipSetDevice(device);
   for (void* p : {static_cast<void*>(b.pk), static_cast<void*>(b.tile_off), static_cast<void*>(b.arena),
                   static_cast<void*>(b.attr), static_cast<void*>(b.cpe_bits), static_cast<void*>(b.rec),
-                  static_cast<void*>(b.tail)})
+                  static_cast<void*>(b.tail), static_cast<void*>(b.spill)})
     if (p) (void)hipFree(p);
   b = DevBatch{};
 }
@@ -320,8 +311,8 @@ bool Engine::alloc_matches(uint64_t cap, uint32_t n_pkgs, DevMatches& m, std::st
          dmalloc(&m.dir, m.dir_cap, "hipMalloc(tile dir)", err) && dmalloc(&m.ctl, 8, "hipMalloc(ctl)", err);
 }
 
-void Engine::free_matches(DevMatches& m) {
-  (void)hipSetDevice(dev_);
+void Engine::free_matches(int device, DevMatches& m) {
+  (void)hipSetDevice(device);
   for (void* p : {static_cast<void*>(m.pkg), static_cast<void*>(m.adv), static_cast<void*>(m.dir),
                   static_cast<void*>(m.ctl)})
     if (p) (void)hipFree(p);
@@ -375,8 +366,12 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
   pa.rec = b.rec + p0;
   pa.tail = b.tail + p0;
   pa.ctl = m.ctl;
-  pa.spill = b.spill ? b.spill : spill_;
-  pa.spill_cap = b.spill ? b.spill_cap : spill_cap_;
+  if (!b.spill || b.spill_cap < b.spill_words) {
+    err = "batch scratch missing or smaller than the batch needs";
+    return false;
+  }
+  pa.spill = b.spill;
+  pa.spill_cap = b.spill_cap;
   const bool fused = kFusedVariant[vi - 1];
   if (!fused) {
     probe_fn(b.gm)(nt, pst, pa);
@@ -389,7 +384,7 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
   sa.db = d_;
   sa.rec = b.rec + p0;
   sa.tail = b.tail + p0;
-  sa.spill = b.spill ? b.spill : spill_;
+  sa.spill = b.spill;
   sa.arena = b.arena;
   sa.attr = b.attr ? b.attr + p0 : nullptr;
   sa.cpe_bits = b.cpe_bits;
@@ -419,7 +414,6 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
 
 bool Engine::launch(const DevBatch& b, const DevMatches& m, hipStream_t st, std::string& err) {
   (void)hipSetDevice(dev_);
-  if (!b.spill && !ensure_scratch(b.spill_words, err)) return false;
   if (!hip_ok(hipMemsetAsync(m.ctl, 0, 8 * sizeof(unsigned long long), st), "memset(ctl)", err)) return false;
   if (b.n_tiles == 0) return true;
   // one launch over every tile (cutting the pass into chunks whose probe overlaps the

@@ -29,6 +29,7 @@ struct FillArgs {
   const uint4* items;    // ITEMS
   const uint8_t* arena;  // ITEMS: vulnerability-ID bytes
   const uint32_t* adv;   // PAIRS: the ordered match list's advisory column
+  const uint32_t* base;  // PAIRS (merged Red Hat lists): the member whose Status / Severity the entry keeps
   const unsigned long long* n_dev;  // PAIRS: match count written by the match kernel
   uint64_t n;            // ITEMS: item count; PAIRS: pair-buffer capacity
   uint4* out;
@@ -120,7 +121,15 @@ __global__ __launch_bounds__(kFillTile) void fill_pairs_kernel(FillArgs a) {
   const uint64_t stride = uint64_t(gridDim.x) * kFillTile;
   for (uint64_t i = uint64_t(blockIdx.x) * kFillTile + threadIdx.x; i < n; i += stride) {
     const uint32_t adv = a.adv[i];
-    const uint4 item = adv < a.t.n_advs ? a.t.adv_items[adv] : make_uint4(0, SRC_NONE << 16, 0, FILL_NOT_FOUND);
+    uint4 item = adv < a.t.n_advs ? a.t.adv_items[adv] : make_uint4(0, SRC_NONE << 16, 0, FILL_NOT_FOUND);
+    if (a.base) {  // merged Red Hat entry: FixedVersion of adv (the representative), the rest of base
+      const uint32_t b = a.base[i];
+      if (b != adv && b < a.t.n_advs) {
+        const uint32_t fixed = item.z & FI_FIXED;
+        item = a.t.adv_items[b];
+        item.z = (item.z & ~FI_FIXED) | fixed;
+      }
+    }
     const uint4 o = decide(a.t, item, item.w);
     a.out[i] = o;
     if (a.side)  // result.Filter reads this word, not the decision (filter.hip filter_mark)
@@ -223,12 +232,13 @@ bool FillEngine::run_host(const std::vector<uint4>& items, const std::vector<uin
   return hip_ok(hipStreamSynchronize(stream_), "fill sync", err) && ok;
 }
 
-bool FillEngine::launch_pairs(const uint32_t* adv, const unsigned long long* n_dev, uint64_t cap, uint4* out,
-                              uint2* side, hipStream_t stream, std::string& err) {
+bool FillEngine::launch_pairs(const uint32_t* adv, const uint32_t* base, const unsigned long long* n_dev, uint64_t cap,
+                              uint4* out, uint2* side, hipStream_t stream, std::string& err) {
   if (cap == 0) return true;
   FillArgs a{};
   a.t = *d_;
   a.adv = adv;
+  a.base = base;
   a.n_dev = n_dev;
   a.n = cap;
   a.out = out;
@@ -239,12 +249,18 @@ bool FillEngine::launch_pairs(const uint32_t* adv, const unsigned long long* n_d
   return hip_ok(hipGetLastError(), "fill_kernel launch", err);
 }
 
-uint64_t FillEngine::pair_bytes(const std::vector<uint32_t>& adv) const {
+uint64_t FillEngine::pair_bytes(const std::vector<uint32_t>& adv, const std::vector<uint32_t>& base) const {
   // per pair: its advisory index (4) + the advisory's item (16) + the record (16) + its
-  // entry words (4 each) + the decision (16); no cache-reuse credit
+  // entry words (4 each) + the decision (16) + the side word (8); merged lists: + the
+  // base index (4) and, where it differs, the base's item (16); no cache-reuse credit
   uint64_t b = 0;
-  for (const uint32_t a : adv) {
-    b += 4 + 16 + 16;
+  for (size_t i = 0; i < adv.size(); i++) {
+    uint32_t a = adv[i];
+    b += 4 + 16 + 16 + 8;
+    if (!base.empty()) {
+      b += 4;
+      if (base[i] != a) b += 16, a = base[i];
+    }
     if (a < t_->adv_items.size()) {
       const uint32_t rec = t_->adv_items[a].w;
       if (rec != FILL_NOT_FOUND) b += 16 + 4ull * t_->recs[rec].y;

@@ -62,7 +62,7 @@ class Pipeline {
   uint32_t* row_end_h_ = nullptr;
   unsigned long long* ctl_h_ = nullptr;
   uint64_t cap_ = 0, h2d_ = 0, d2h_ = 0;
-  Engine* eng_ = nullptr;
+  bool prepared_ = false;  // no Engine pointer: the batch may outlive a hot swap (the C-ABI checks the generation)
 };
 
 }  // namespace tvm

@@ -26,10 +26,8 @@ void Pipeline::release() {
   if (s_k_) (void)hipStreamSynchronize(s_k_);
   if (s_d2h_) (void)hipStreamSynchronize(s_d2h_);
   if (s_h2d_) (void)hipStreamSynchronize(s_h2d_);
-  if (eng_) {
-    eng_->free_batch(db_);
-    eng_->free_matches(m_);
-  }
+  Engine::free_batch(dev_, db_);
+  Engine::free_matches(dev_, m_);
   for (void* p : {static_cast<void*>(csr_adv_d_), static_cast<void*>(row_end_d_), static_cast<void*>(status_d_),
                   static_cast<void*>(tickets_d_)})
     if (p) (void)hipFree(p);
@@ -48,14 +46,14 @@ void Pipeline::release() {
   status_d_ = tickets_d_ = nullptr;
   adv_h_ = row_end_h_ = nullptr;
   ctl_h_ = nullptr;
-  eng_ = nullptr;
+  prepared_ = false;
   dev_ = -1;
 }
 
 bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uint32_t chunk_packages,
                        std::string& err) {
   release();
-  eng_ = &eng;
+
   dev_ = eng.device();
   (void)hipSetDevice(dev_);
   const uint32_t n_tiles = hb.n_tiles();
@@ -117,6 +115,7 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
   row_end_h_ = static_cast<uint32_t*>(p);
   if (!ok(hipHostMalloc(&p, 64, hipHostMallocDefault), "hipHostMalloc(ctl)", err)) return false;
   ctl_h_ = static_cast<unsigned long long*>(p);
+  prepared_ = true;
   return true;
 }
 
@@ -126,7 +125,7 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
   err_pkg = -1;
   err_bits = 0;
   h2d_ = d2h_ = 0;
-  if (!eng_ || db_.n != hb.pk.size()) {
+  if (!prepared_ || db_.n != hb.pk.size()) {
     err = "pipeline: prepare() the batch first";
     return false;
   }

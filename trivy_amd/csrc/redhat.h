@@ -1,4 +1,5 @@
-// Red Hat per-CVE merge of a batch's match list (redhat.hip; redhat.go:146-187).
+// Red Hat per-CVE merge of a batch's match list on the device (redhat.hip;
+// pkg/detector/ospkg/redhat/redhat.go:146-187).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -7,6 +8,7 @@
 #include <vector>
 
 #include "common.h"
+#include "engine.h"
 
 namespace tvm {
 
@@ -14,21 +16,33 @@ constexpr uint32_t RH_NONE = 0xFFFFFFFFu;
 
 // One merged vulnerability of one package: the group of the package's matches that share a
 // VulnerabilityID.  base = the first member (Get order: Status, Severity, Custom); best =
-// the member with the greatest fixed version (RH_NONE: all unfixed); members = sorted
-// positions [start, start + len) of the contrib array.
+// the member with the greatest fixed version (RH_NONE: all unfixed); members = positions
+// [start, start + len) of the raw match list (contrib[i] = advisory at raw position i).
 struct RhRec {
   uint32_t pkg, base, best, start, len;
   uint32_t pad[3];
 };
 
+// The merged match list, device resident, in the layout of DevMatches (tile directory +
+// columns + control block) so that FillInfo, result.Filter and the ordered fetch read it
+// like a raw list.  Per entry: pkg, adv = the representative advisory (best when a member
+// is fixed, else base: its FixedVersion is the merged FixedVersion), base = the first
+// member, grp = {raw position of the first member, member count}.  Pairs of packages of
+// other drivers pass through as groups of one (adv = base).
+struct RhMerged {
+  DevMatches m;          // m.pkg / m.adv / m.dir / m.ctl ([0] entries, [3] error bits)
+  uint32_t* base = nullptr;
+  uint2* grp = nullptr;
+  uint64_t cap = 0;
+};
+enum : uint32_t { ERR_RH_ORDER = 4 };  // a Red Hat package's IDs were not grouped (load-time order broken)
+
 struct RhInputs {
   const uint2* pk;                  // device batch packages
   const PlatInfo* plats;
   uint32_t n_plats;
-  const uint32_t* pkg;              // device match columns
-  const uint32_t* adv;
-  const unsigned long long* n_dev;  // device match count
-  uint64_t n_matches;               // host copy (the buffers' valid length)
+  const DevMatches* raw;            // the match kernel's list
+  uint32_t n_tiles;
   uint32_t pkg_base;
   const uint2* adv_rank;            // FillDev::adv_rank (.x vulnerability-ID rank)
   const uint32_t* fixed_rank;       // per advisory: rpm order rank of FixedVersion, RH_NONE = unfixed
@@ -37,14 +51,19 @@ struct RhInputs {
 class RedHatMerge {
  public:
   ~RedHatMerge();
-  // records in (package, VulnerabilityID) order; contrib[i] = advisory at sorted position i
-  bool run(const RhInputs& in, std::vector<RhRec>& recs, std::vector<uint32_t>& contrib, hipStream_t st,
-           std::string& err);
+  // Enqueues the merge on `st` (no host synchronisation); the result stays in merged().
+  bool launch(const RhInputs& in, hipStream_t st, std::string& err);
+  const RhMerged& merged() const { return out_; }
+  // After launch: the merged list in (package, VulnerabilityID) order as host columns
+  // (pkg, adv, base, grp) and the raw list's advisory column in raw positions (contrib);
+  // synchronises `st`.
+  bool fetch(const RhInputs& in, std::vector<uint32_t>& pkg, std::vector<uint32_t>& adv, std::vector<uint32_t>& base,
+             std::vector<uint2>& grp, std::vector<uint32_t>& contrib, hipStream_t st, std::string& err);
 
  private:
-  void* bufs_[10] = {};
-  size_t caps_[10] = {};
-  bool grow(int i, size_t need, std::string& err);
+  int dev_ = -1;
+  RhMerged out_;
+  void release();
 };
 
 }  // namespace tvm

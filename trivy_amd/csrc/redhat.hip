@@ -5,19 +5,19 @@
 // VulnerabilityID: an unfixed advisory enters only if the ID is new (first seen wins); a
 // fixed one (installed < fixed) enters, or merges into the existing entry - VendorIDs
 // unioned (ustrings.Unique), FixedVersion raised to the greater rpm version - and the
-// result is sorted by VulnerabilityID.  Here, over every (package, advisory) pair of the
-// batch's Red Hat packages at once:
-//   rh_keys    key = package << 32 | vulnerability-ID rank (byte order = Go string order);
-//              pairs of other drivers get the all-ones key (they sort last, no group);
-//   radix sort (hipcub, stable: equal keys keep the match list's per-package Get order);
-//   rh_heads   a group starts where the key changes;
-//   select     group heads in order (hipcub DeviceSelect::Flagged);
-//   rh_records per group: the first member (Status / Severity / Custom), the member with the
-//              greatest fixed version (rpm order rank computed at load time; ties keep the
-//              first, as LessThan does), the members' range (the host unions their VendorIDs).
-// Integer / byte work bound by memory traffic: no MFMA.
-#include <hipcub/hipcub.hpp>
-
+// result is sorted by VulnerabilityID.
+//
+// The flattener numbers each Red Hat key's advisories in (VulnerabilityID, Get order)
+// order (db.cpp flatten_os), and the match kernel emits a package's matches in advisory
+// order, so a package's members of one CVE are adjacent and in Get order, and the CVEs
+// ascend.  The merge is therefore one pass per tile segment, no sort:
+//   count   a pair heads a group unless it is a Red Hat pair continuing its predecessor's
+//           (package, ID-rank); one reservation per tile for the tile's group count;
+//   emit    block scan of the head flags; each head lane walks its group (a few pairs) for
+//           the member with the greatest fixed version (rpm-order rank computed at load
+//           time; ties keep the first, as LessThan does) and writes {pkg, representative,
+//           base, raw range}.
+// Integer work bound by memory traffic (about 8 B read + 20 B written per pair); no MFMA.
 #include <algorithm>
 #include <string>
 
@@ -28,78 +28,132 @@ namespace tvm {
 namespace {
 
 constexpr int kBlock = 256;
-constexpr unsigned long long kNone = ~0ull;
+constexpr int kWaves = kBlock / 64;
+constexpr uint32_t kNoKey = 0xFFFFFFFFu;
 
 struct MergeArgs {
+  const TileDir* dir;
+  const uint32_t* pkg;         // raw match columns
+  const uint32_t* adv;
   const uint2* pk;             // batch packages {plat, lengths}
   const PlatInfo* plats;
   uint32_t n_plats;
-  const uint32_t* pkg;         // match columns
-  const uint32_t* adv;
-  const unsigned long long* n_dev;  // match count (device)
-  uint64_t cap;
   uint32_t pkg_base;
   const uint2* adv_rank;       // .x = vulnerability-ID rank
-  const uint32_t* fixed_rank;  // rpm order rank of the advisory's fixed version, kNoFix = unfixed
-  unsigned long long* keys;
-  uint32_t* idx;
-  const unsigned long long* skeys;
-  const uint32_t* sidx;
-  uint8_t* flags;
-  const uint32_t* heads;
-  const uint32_t* n_heads;
-  RhRec* recs;
-  uint32_t* contrib;           // advisory of every sorted position
+  const uint32_t* fixed_rank;  // RH_NONE = unfixed
+  uint64_t raw_cap;
+  TileDir* mdir;
+  uint32_t* mpkg;
+  uint32_t* madv;
+  uint32_t* mbase;
+  uint2* mgrp;
+  uint64_t mcap;
+  unsigned long long* mctl;
 };
 
-__global__ __launch_bounds__(kBlock) void rh_keys(MergeArgs a) {
-  const uint64_t n = *a.n_dev < a.cap ? *a.n_dev : a.cap;
-  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
-  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.cap; i += stride) {
-    unsigned long long k = kNone;
-    if (i < n) {
-      const uint32_t p = a.pkg[i], ad = a.adv[i];
-      const uint32_t plat = a.pk[p - a.pkg_base].x;
-      if (plat < a.n_plats && a.plats[plat].drv == DRV_REDHAT) k = (uint64_t(p) << 32) | a.adv_rank[ad].x;
+// Group key of raw position i: the vulnerability-ID rank of a Red Hat pair, kNoKey else.
+__device__ __forceinline__ uint32_t group_key(const MergeArgs& a, uint32_t p, uint32_t ad) {
+  const uint32_t plat = a.pk[p - a.pkg_base].x;
+  const bool rh = plat < a.n_plats && a.plats[plat].drv == DRV_REDHAT;
+  return rh ? a.adv_rank[ad].x : kNoKey;
+}
+
+// Exclusive block scan of one flag per lane; returns the block total.
+__device__ __forceinline__ uint32_t block_flag_scan(bool f, uint32_t tid, uint32_t* ws, uint32_t& excl) {
+  const uint32_t lane = tid & 63, wave = tid >> 6;
+  const unsigned long long bal = __ballot(f);
+  if (lane == 0) ws[wave] = uint32_t(__popcll(bal));
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kWaves; w++) {
+    const uint32_t c = ws[w];
+    off += uint32_t(w) < wave ? c : 0u;
+    tot += c;
+  }
+  excl = off + uint32_t(__popcll(bal & ((1ull << lane) - 1ull)));
+  __syncthreads();  // ws is reused by the next chunk
+  return tot;
+}
+
+__global__ __launch_bounds__(kBlock) void rh_merge_kernel(MergeArgs a) {
+  __shared__ uint32_t ws[kWaves];
+  __shared__ unsigned long long s_out;
+  const uint32_t t = blockIdx.x, tid = threadIdx.x;
+  const TileDir d = a.dir[t];
+  const uint64_t b0 = d.base;
+  const uint32_t cnt = d.count;
+  if (b0 + cnt > a.raw_cap) {  // an overflowed match list: nothing valid to merge
+    if (tid == 0) {
+      a.mdir[t] = TileDir{0, 0, 0};
+      atomicOr(a.mctl + 3, 1ull);
     }
-    a.keys[i] = k;
-    a.idx[i] = uint32_t(i);
+    return;
   }
-}
-
-__global__ __launch_bounds__(kBlock) void rh_heads(MergeArgs a) {
-  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
-  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < a.cap; i += stride) {
-    const unsigned long long k = a.skeys[i];
-    a.flags[i] = k != kNone && (i == 0 || a.skeys[i - 1] != k);
-    a.contrib[i] = a.adv[a.sidx[i]];
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void rh_records(MergeArgs a) {
-  const uint32_t nh = *a.n_heads;
-  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
-  for (uint64_t h = uint64_t(blockIdx.x) * kBlock + threadIdx.x; h < nh; h += stride) {
-    const uint32_t s = a.heads[h];
-    const unsigned long long k = a.skeys[s];
-    const uint32_t base = a.contrib[s];
-    uint32_t best = RH_NONE, best_r = 0, j = s;
-    for (; j < a.cap && a.skeys[j] == k; j++) {
-      const uint32_t ad = a.contrib[j];
-      const uint32_t r = a.fixed_rank[ad];
-      if (r != RH_NONE && (best == RH_NONE || r > best_r)) {
-        best = ad;
-        best_r = r;
+  // pass 1: heads of the tile's segment
+  uint32_t heads = 0;
+  bool order_bad = false;
+  for (uint32_t c = 0; c < cnt; c += kBlock) {
+    bool h = false;
+    if (c + tid < cnt) {
+      const uint64_t i = b0 + c + tid;
+      const uint32_t p = a.pkg[i], k = group_key(a, p, a.adv[i]);
+      h = true;
+      if (k != kNoKey && c + tid > 0) {
+        const uint32_t pp = a.pkg[i - 1];
+        if (pp == p) {
+          const uint32_t kp = group_key(a, pp, a.adv[i - 1]);
+          h = kp != k;
+          order_bad |= kp > k;
+        }
       }
     }
-    RhRec o;
-    o.pkg = uint32_t(k >> 32);
-    o.base = base;
-    o.best = best;
-    o.start = s;
-    o.len = j - s;
-    o.pad[0] = o.pad[1] = o.pad[2] = 0;
-    a.recs[h] = o;
+    uint32_t ex;
+    heads += block_flag_scan(h, tid, ws, ex);
+  }
+  if (order_bad) atomicOr(a.mctl + 3, (unsigned long long)ERR_RH_ORDER);
+  if (tid == 0) {
+    const unsigned long long o = atomicAdd(a.mctl, (unsigned long long)heads);
+    s_out = o;
+    a.mdir[t] = TileDir{o, o + heads <= a.mcap ? heads : 0u, 0};
+  }
+  __syncthreads();
+  const unsigned long long o0 = s_out;
+  if (o0 + heads > a.mcap) return;  // cannot happen (merged <= raw); the count tells the host
+  // pass 2: emit one entry per group
+  uint32_t done = 0;
+  for (uint32_t c = 0; c < cnt; c += kBlock) {
+    bool h = false;
+    uint32_t p = 0, ad = 0, k = kNoKey;
+    const uint64_t i = b0 + c + tid;
+    if (c + tid < cnt) {
+      p = a.pkg[i];
+      ad = a.adv[i];
+      k = group_key(a, p, ad);
+      h = k == kNoKey || c + tid == 0 || a.pkg[i - 1] != p || group_key(a, p, a.adv[i - 1]) != k;
+    }
+    uint32_t ex;
+    const uint32_t n = block_flag_scan(h, tid, ws, ex);
+    if (h) {
+      uint32_t best = RH_NONE, best_r = 0, len = 1;
+      if (k != kNoKey) {
+        const uint32_t r0 = a.fixed_rank[ad];
+        if (r0 != RH_NONE) best = ad, best_r = r0;
+        for (uint64_t j = i + 1; j < b0 + cnt && a.pkg[j] == p; j++) {
+          const uint32_t aj = a.adv[j];
+          if (a.adv_rank[aj].x != k) break;
+          const uint32_t r = a.fixed_rank[aj];
+          if (r != RH_NONE && (best == RH_NONE || r > best_r)) best = aj, best_r = r;
+          len++;
+        }
+      }
+      const uint64_t o = o0 + done + ex;
+      a.mpkg[o] = p;
+      a.madv[o] = best != RH_NONE ? best : ad;
+      a.mbase[o] = ad;
+      a.mgrp[o] = make_uint2(uint32_t(i), len);
+    }
+    done += n;
   }
 }
 
@@ -111,92 +165,117 @@ bool ok(hipError_t e, const char* what, std::string& err) {
 
 }  // namespace
 
-RedHatMerge::~RedHatMerge() {
-  for (void* p : bufs_)
-    if (p) (void)hipFree(p);
+void RedHatMerge::release() {
+  if (dev_ < 0) return;
+  (void)hipSetDevice(dev_);
+  Engine::free_matches(dev_, out_.m);
+  if (out_.base) (void)hipFree(out_.base);
+  if (out_.grp) (void)hipFree(out_.grp);
+  out_ = RhMerged{};
 }
 
-bool RedHatMerge::grow(int i, size_t need, std::string& err) {
-  if (caps_[i] >= need) return true;
-  if (bufs_[i]) (void)hipFree(bufs_[i]);
-  bufs_[i] = nullptr;
-  caps_[i] = 0;
-  if (!ok(hipMalloc(&bufs_[i], std::max<size_t>(need, 1)), "hipMalloc(redhat merge)", err)) return false;
-  caps_[i] = need;
-  return true;
-}
+RedHatMerge::~RedHatMerge() { release(); }
 
-bool RedHatMerge::run(const RhInputs& in, std::vector<RhRec>& recs, std::vector<uint32_t>& contrib, hipStream_t st,
-                      std::string& err) {
-  recs.clear();
-  contrib.clear();
-  const uint64_t cap = in.n_matches;
-  if (cap == 0) return true;
-  if (cap > 0x7FFFFFFFull) {
-    err = "redhat merge: too many matches";
-    return false;
+bool RedHatMerge::launch(const RhInputs& in, hipStream_t st, std::string& err) {
+  const DevMatches& raw = *in.raw;
+  int dev = 0;
+  if (!ok(hipGetDevice(&dev), "hipGetDevice", err)) return false;
+  if (out_.cap < raw.cap || out_.m.dir_cap < in.n_tiles || dev != dev_) {
+    release();
+    dev_ = dev;
+    const uint64_t cap = raw.cap;
+    const uint32_t nt = std::max<uint32_t>(in.n_tiles, 1);
+    void *p = nullptr, *q = nullptr, *r = nullptr, *s = nullptr, *t = nullptr, *c = nullptr;
+    const bool good = ok(hipMalloc(&p, cap * 4), "hipMalloc(merged)", err) &&
+                      ok(hipMalloc(&q, cap * 4), "hipMalloc(merged)", err) &&
+                      ok(hipMalloc(&r, cap * 4), "hipMalloc(merged)", err) &&
+                      ok(hipMalloc(&s, cap * 8), "hipMalloc(merged)", err) &&
+                      ok(hipMalloc(&t, nt * sizeof(TileDir)), "hipMalloc(merged dir)", err) &&
+                      ok(hipMalloc(&c, 64), "hipMalloc(merged ctl)", err);
+    out_.m.pkg = static_cast<uint32_t*>(p);
+    out_.m.adv = static_cast<uint32_t*>(q);
+    out_.base = static_cast<uint32_t*>(r);
+    out_.grp = static_cast<uint2*>(s);
+    out_.m.dir = static_cast<TileDir*>(t);
+    out_.m.ctl = static_cast<unsigned long long*>(c);
+    out_.m.cap = out_.cap = cap;
+    out_.m.dir_cap = nt;
+    if (!good) {
+      release();
+      return false;
+    }
   }
-  size_t sort_bytes = 0, sel_bytes = 0;
-  if (!ok(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, static_cast<unsigned long long*>(nullptr),
-                                             static_cast<unsigned long long*>(nullptr), static_cast<uint32_t*>(nullptr),
-                                             static_cast<uint32_t*>(nullptr), int(cap), 0, 64, st),
-          "hipcub sort sizing", err) ||
-      !ok(hipcub::DeviceSelect::Flagged(nullptr, sel_bytes, hipcub::CountingInputIterator<uint32_t>(0),
-                                        static_cast<const uint8_t*>(nullptr), static_cast<uint32_t*>(nullptr),
-                                        static_cast<uint32_t*>(nullptr), int(cap), st),
-          "hipcub select sizing", err))
-    return false;
-  // 0 keys, 1 idx, 2 sorted keys, 3 sorted idx, 4 flags, 5 heads, 6 head count, 7 records, 8 contrib, 9 temp
-  if (!grow(0, cap * 8, err) || !grow(1, cap * 4, err) || !grow(2, cap * 8, err) || !grow(3, cap * 4, err) ||
-      !grow(4, cap, err) || !grow(5, cap * 4, err) || !grow(6, 4, err) || !grow(7, cap * sizeof(RhRec), err) ||
-      !grow(8, cap * 4, err) || !grow(9, std::max(sort_bytes, sel_bytes), err))
-    return false;
+  if (!ok(hipMemsetAsync(out_.m.ctl, 0, 64, st), "memset(merged ctl)", err)) return false;
+  if (in.n_tiles == 0) return true;
   MergeArgs a{};
+  a.dir = raw.dir;
+  a.pkg = raw.pkg;
+  a.adv = raw.adv;
   a.pk = in.pk;
   a.plats = in.plats;
   a.n_plats = in.n_plats;
-  a.pkg = in.pkg;
-  a.adv = in.adv;
-  a.n_dev = in.n_dev;
-  a.cap = cap;
   a.pkg_base = in.pkg_base;
   a.adv_rank = in.adv_rank;
   a.fixed_rank = in.fixed_rank;
-  a.keys = static_cast<unsigned long long*>(bufs_[0]);
-  a.idx = static_cast<uint32_t*>(bufs_[1]);
-  a.skeys = static_cast<unsigned long long*>(bufs_[2]);
-  a.sidx = static_cast<uint32_t*>(bufs_[3]);
-  a.flags = static_cast<uint8_t*>(bufs_[4]);
-  a.heads = static_cast<uint32_t*>(bufs_[5]);
-  a.n_heads = static_cast<uint32_t*>(bufs_[6]);
-  a.recs = static_cast<RhRec*>(bufs_[7]);
-  a.contrib = static_cast<uint32_t*>(bufs_[8]);
-  const uint32_t blocks = uint32_t(std::min<uint64_t>((cap + kBlock - 1) / kBlock, 256ull * 32));
-  hipLaunchKernelGGL(rh_keys, dim3(blocks), dim3(kBlock), 0, st, a);
-  if (!ok(hipGetLastError(), "rh_keys", err) ||
-      !ok(hipcub::DeviceRadixSort::SortPairs(bufs_[9], sort_bytes, a.keys, static_cast<unsigned long long*>(bufs_[2]),
-                                             a.idx, static_cast<uint32_t*>(bufs_[3]), int(cap), 0, 64, st),
-          "hipcub sort", err))
-    return false;
-  hipLaunchKernelGGL(rh_heads, dim3(blocks), dim3(kBlock), 0, st, a);
-  if (!ok(hipGetLastError(), "rh_heads", err) ||
-      !ok(hipcub::DeviceSelect::Flagged(bufs_[9], sel_bytes, hipcub::CountingInputIterator<uint32_t>(0), a.flags,
-                                        static_cast<uint32_t*>(bufs_[5]), static_cast<uint32_t*>(bufs_[6]), int(cap),
-                                        st),
-          "hipcub select", err))
-    return false;
-  hipLaunchKernelGGL(rh_records, dim3(blocks), dim3(kBlock), 0, st, a);
-  uint32_t nh = 0;
-  if (!ok(hipGetLastError(), "rh_records", err) ||
-      !ok(hipMemcpyAsync(&nh, bufs_[6], 4, hipMemcpyDeviceToHost, st), "D2H head count", err) ||
+  a.raw_cap = raw.cap;
+  a.mdir = out_.m.dir;
+  a.mpkg = out_.m.pkg;
+  a.madv = out_.m.adv;
+  a.mbase = out_.base;
+  a.mgrp = out_.grp;
+  a.mcap = out_.cap;
+  a.mctl = out_.m.ctl;
+  hipLaunchKernelGGL(rh_merge_kernel, dim3(in.n_tiles), dim3(kBlock), 0, st, a);
+  return ok(hipGetLastError(), "rh_merge_kernel", err);
+}
+
+bool RedHatMerge::fetch(const RhInputs& in, std::vector<uint32_t>& pkg, std::vector<uint32_t>& adv,
+                        std::vector<uint32_t>& base, std::vector<uint2>& grp, std::vector<uint32_t>& contrib,
+                        hipStream_t st, std::string& err) {
+  pkg.clear();
+  adv.clear();
+  base.clear();
+  grp.clear();
+  contrib.clear();
+  unsigned long long ctl[8] = {}, rctl[8] = {};
+  if (!ok(hipMemcpyAsync(ctl, out_.m.ctl, sizeof ctl, hipMemcpyDeviceToHost, st), "D2H merged ctl", err) ||
+      !ok(hipMemcpyAsync(rctl, in.raw->ctl, sizeof rctl, hipMemcpyDeviceToHost, st), "D2H ctl", err) ||
       !ok(hipStreamSynchronize(st), "redhat merge", err))
     return false;
-  recs.resize(nh);
-  contrib.resize(cap);
-  return (!nh || ok(hipMemcpyAsync(recs.data(), bufs_[7], nh * sizeof(RhRec), hipMemcpyDeviceToHost, st),
-                    "D2H records", err)) &&
-         ok(hipMemcpyAsync(contrib.data(), bufs_[8], cap * 4, hipMemcpyDeviceToHost, st), "D2H contrib", err) &&
-         ok(hipStreamSynchronize(st), "redhat merge", err);
+  if (ctl[3] & ERR_RH_ORDER) {
+    err = "redhat merge: a Red Hat package's advisories are not grouped by VulnerabilityID";
+    return false;
+  }
+  if (ctl[3] || rctl[0] > in.raw->cap || ctl[0] > out_.cap) {
+    err = "redhat merge: the match buffer overflowed";
+    return false;
+  }
+  const uint64_t n = ctl[0], nr = rctl[0];
+  std::vector<TileDir> dir(in.n_tiles);
+  std::vector<uint32_t> p(n), a(n), b(n);
+  std::vector<uint2> g(n);
+  contrib.resize(nr);
+  if ((in.n_tiles && !ok(hipMemcpyAsync(dir.data(), out_.m.dir, in.n_tiles * sizeof(TileDir), hipMemcpyDeviceToHost, st),
+                         "D2H merged dir", err)) ||
+      (n && (!ok(hipMemcpyAsync(p.data(), out_.m.pkg, n * 4, hipMemcpyDeviceToHost, st), "D2H merged", err) ||
+             !ok(hipMemcpyAsync(a.data(), out_.m.adv, n * 4, hipMemcpyDeviceToHost, st), "D2H merged", err) ||
+             !ok(hipMemcpyAsync(b.data(), out_.base, n * 4, hipMemcpyDeviceToHost, st), "D2H merged", err) ||
+             !ok(hipMemcpyAsync(g.data(), out_.grp, n * 8, hipMemcpyDeviceToHost, st), "D2H merged", err))) ||
+      (nr && !ok(hipMemcpyAsync(contrib.data(), in.raw->adv, nr * 4, hipMemcpyDeviceToHost, st), "D2H contrib", err)) ||
+      !ok(hipStreamSynchronize(st), "redhat merge", err))
+    return false;
+  pkg.reserve(n);
+  adv.reserve(n);
+  base.reserve(n);
+  grp.reserve(n);
+  for (const TileDir& d : dir)
+    for (uint64_t i = d.base; i < d.base + d.count; i++) {
+      pkg.push_back(p[i]);
+      adv.push_back(a[i]);
+      base.push_back(b[i]);
+      grp.push_back(g[i]);
+    }
+  return true;
 }
 
 }  // namespace tvm

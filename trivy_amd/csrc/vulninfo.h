@@ -178,12 +178,14 @@ class FillEngine {
   // `stream`; the pair count is read from n_dev on the device (at most cap pairs).
   // side (optional): per pair the filter's hand-off word {vulnerability-ID rank, severity
   // index | status << 8} (filter.hip reads it instead of the 16-B decision).
-  bool launch_pairs(const uint32_t* adv, const unsigned long long* n_dev, uint64_t cap, uint4* out, uint2* side,
-                    hipStream_t stream, std::string& err);
+  // base (optional, merged Red Hat lists): per pair the member that supplies Status /
+  // Severity; adv then only decides FixedVersion != "".
+  bool launch_pairs(const uint32_t* adv, const uint32_t* base, const unsigned long long* n_dev, uint64_t cap,
+                    uint4* out, uint2* side, hipStream_t stream, std::string& err);
   uint64_t table_bytes() const { return table_bytes_; }
   const VulnTable& table() const { return *t_; }
   // Algorithmic HBM bytes of one batch-path launch over these pairs (host copy).
-  uint64_t pair_bytes(const std::vector<uint32_t>& adv) const;
+  uint64_t pair_bytes(const std::vector<uint32_t>& adv, const std::vector<uint32_t>& base) const;
   const FillDev& dev() const { return *d_; }
   int device() const { return dev_; }
 
