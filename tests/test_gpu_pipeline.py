@@ -81,3 +81,91 @@ def test_pipeline_poisoned_and_empty(oracle_built):
     empty = MatchBatch(eng).pipeline_prepare(chunk_packages=256)
     assert empty.pipeline_run()[:2] == (0, -1)
     empty.close()
+
+
+def test_concurrent_batches_keep_their_scratch():
+    """Every batch owns its kernel scratch (installed keys over 32 bytes, Maven parses): a
+    pipelined pass on its own streams and device-resident launches of other batches at the
+    same time, from three threads, give each batch its serial result."""
+    import threading
+
+    import trivy_amd
+    from tools import synth_mix as sm
+    from trivy_amd.batch import MatchBatch
+    sdb = sm.make_mix_db([("maven::", "maven"), ("npm::", "npm")], 1500, seed=3)
+    eng = trivy_amd.Engine(sdb.put(trivy_amd.DB()).finalize(), 0)
+    groups = [sm.make_mix_batch(sdb, 40_000, [3, 1], seed=s) for s in (1, 2, 3)]
+    for g in groups:  # long versions: keys beyond 32 bytes take the scratch too
+        for _, cols in g.groups:
+            cols["ver"] = np.where(np.arange(len(cols["ver"])) % 5 == 0,
+                                   np.char.add(cols["ver"], b".1.2.3.4.5.6.7.8.9.10.11.12.13"), cols["ver"])
+
+    def make(g):
+        mb = MatchBatch(eng)
+        sm.add_to(mb, sdb, g)
+        return mb
+    serial = []
+    for g in groups:
+        mb = make(g)
+        mb.run()
+        serial.append(mb.pairs())
+        mb.close()
+    assert all(len(s) > 5000 for s in serial)
+    pipe = make(groups[0]).pipeline_prepare(match_cap=len(serial[0]), chunk_packages=4096)
+    dev = [make(g).upload(len(s)) for g, s in zip(groups[1:], serial[1:])]
+    bad = []
+
+    def run_pipe():
+        for _ in range(6):
+            total, errp, _ = pipe.pipeline_run()
+            pk, ad = _pairs_of(*pipe.pipeline_csr())
+            if not (total == len(serial[0]) and np.array_equal(np.stack([pk, ad], 1), serial[0])):
+                bad.append("pipeline")
+
+    def run_dev(k):
+        for _ in range(6):
+            dev[k].launch()
+            if not np.array_equal(dev[k].pairs(), serial[k + 1]):
+                bad.append(f"batch {k + 1}")
+    ths = [threading.Thread(target=run_pipe)] + [threading.Thread(target=run_dev, args=(k,)) for k in range(2)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not bad, bad[:5]
+    for mb in [pipe] + dev:
+        mb.close()
+
+
+def test_batches_refused_after_swap(oracle_built):
+    """A batch resolves its platforms against the tables it was built on: after
+    tvm_engine_swap its pipeline pass and its launches are refused (not run on mixed
+    tables), freeing it touches nothing of the swapped-out engine, and a batch rebuilt on
+    the new tables matches like the oracle."""
+    import trivy_amd
+    from test_gpu_parity import build_engine
+    sdb = make_db(["debian 12", "ubuntu 22.04"], 400, seed=5)
+    sdb2 = make_db(["debian 11", "debian 12", "ubuntu 22.04"], 500, seed=6)
+    eng = build_engine(sdb)
+    batch = make_batch(sdb, 6, 300, [1, 1], seed=2)
+    pipe = _fill(eng, sdb, batch).pipeline_prepare(chunk_packages=512)
+    assert pipe.pipeline_run()[1] == -1
+    dev = _fill(eng, sdb, batch)
+    dev.run()
+    eng2 = build_engine(sdb2)  # only for its DB handle
+    eng.swap(eng2.db)
+    with pytest.raises(RuntimeError, match="rebuild"):
+        pipe.pipeline_run()
+    with pytest.raises(RuntimeError, match="rebuild"):
+        dev.launch()
+    with pytest.raises(RuntimeError):
+        dev.upload()
+    pipe.close()
+    dev.close()
+    batch2 = make_batch(sdb2, 6, 300, [1, 1, 1], seed=3)
+    fresh = _fill(eng, sdb2, batch2)
+    total, errp, _ = fresh.run()
+    opk, oad = om.match(om.Prepared(sdb2, batch2), n_threads=4)
+    got = fresh.pairs()
+    assert errp == -1 and np.array_equal(got[:, 0], opk) and np.array_equal(got[:, 1], oad)
+    fresh.close()

@@ -152,3 +152,66 @@ Relationship: SPDXRef-Application-1 CONTAINS SPDXRef-File-1
         ts.decode("not an sbom")
     with pytest.raises(ts.SBOMError):
         ts.decode_intoto('{"payloadType": "text/plain", "payload": ""}')
+
+
+# pkg/sbom/spdx/unmarshal_test.go:20-338, the fields this decoder produces, transcribed as
+# data; the inputs are the reference's spdx/testdata/happy files (tests/golden/sbom/spdx_happy)
+_L3 = "sha256:3c79e832b1b4891a1cb4a326ef8524e0bd14a2537150ac0e203a5677176c1ca1"
+_YARGS = {"Type": "node-pkg", "FilePath": "", "Libraries": [
+    {"ID": "yargs-parser@21.1.1", "Name": "yargs-parser", "Version": "21.1.1",
+     "FilePath": "node_modules/yargs-parser/package.json"}]}
+SPDX_HAPPY = {
+    "bom.json": {"OS": {"Family": "alpine", "Name": "3.16.0"},
+                 "Packages": [{"ID": "musl@1.2.3-r0", "Name": "musl", "Version": "1.2.3-r0", "SrcName": "musl",
+                               "SrcVersion": "1.2.3-r0",
+                               "Layer": "sha256:dd565ff850e7003356e2b252758f9bdc1ff2803f61e995e24c7844f6297f8fc3"}],
+                 "Applications": [
+                     {"Type": "composer", "FilePath": "app/composer/composer.lock", "Libraries": [
+                         {"ID": "pear/log@1.13.1", "Name": "pear/log", "Version": "1.13.1", "Layer": _L3},
+                         {"ID": "pear/pear_exception@v1.0.0", "Name": "pear/pear_exception", "Version": "v1.0.0",
+                          "Layer": _L3}]},
+                     {"Type": "gobinary", "FilePath": "app/gobinary/gobinary", "Libraries": [
+                         {"ID": "github.com/package-url/packageurl-go@v0.1.1-0.20220203205134-d70459300c8a",
+                          "Name": "github.com/package-url/packageurl-go",
+                          "Version": "v0.1.1-0.20220203205134-d70459300c8a", "Layer": _L3}]},
+                     {"Type": "jar", "FilePath": "", "Libraries": [
+                         {"ID": "org.codehaus.mojo:child-project:1.0", "Name": "org.codehaus.mojo:child-project",
+                          "Version": "1.0", "Layer": _L3}]},
+                     {"Type": "node-pkg", "FilePath": "", "Libraries": [
+                         {"ID": "bootstrap@5.0.2", "Name": "bootstrap", "Version": "5.0.2", "Layer": _L3}]}]},
+    "with-hasfiles-bom.json": {"OS": None, "Packages": [], "Applications": [_YARGS]},
+    "with-files-in-relationships-bom.json": {"OS": None, "Packages": [], "Applications": [_YARGS]},
+    "with-file-as-relationship-parent.json": {"OS": None, "Packages": [], "Applications": []},
+    "os-only-bom.json": {"OS": {"Family": "alpine", "Name": "3.16.0"}, "Packages": [], "Applications": []},
+    "empty-bom.json": {"OS": None, "Packages": [], "Applications": []},
+}
+_PKG_KEYS = ("ID", "Name", "Version", "SrcName", "SrcVersion", "FilePath")
+
+
+def _pkg_view(p):
+    v = {k: p[k] for k in _PKG_KEYS if p.get(k)}
+    if (p.get("Layer") or {}).get("DiffID"):
+        v["Layer"] = p["Layer"]["DiffID"]
+    return v
+
+
+@pytest.mark.parametrize("name", sorted(SPDX_HAPPY))
+def test_spdx_unmarshal_happy(name):
+    """SPDX JSON decode, incl. file paths from hasFiles / CONTAINS-File relationships
+    (unmarshal.go:107-132, 187-195 -> decode.go:224-227), vs unmarshal_test.go."""
+    want = SPDX_HAPPY[name]
+    d = ts.decode(open(os.path.join(HERE, "sbom", "spdx_happy", name)).read())
+    os_ = d["OS"] if d["OS"] and d["OS"].get("Family") else None
+    assert os_ == want["OS"]
+    assert [_pkg_view(p) for p in d["Packages"]] == want["Packages"]
+    got_apps = [{"Type": a["Type"], "FilePath": a["FilePath"], "Libraries": [_pkg_view(x) for x in a["Libraries"]]}
+                for a in d["Applications"]]
+    assert got_apps == want["Applications"]
+
+
+def test_decode_malformed_json_is_sbom_error():
+    """sbom.go DetectFormat: input that starts like JSON but does not decode is no known
+    format - an SBOMError, like every other decode failure."""
+    for text in ('{"bomFormat": "CycloneDX", ', "{not json}\n{", "[1, 2]"):
+        with pytest.raises(ts.SBOMError, match="failed to detect SBOM format"):
+            ts.decode(text)

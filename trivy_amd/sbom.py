@@ -164,6 +164,9 @@ def _library(c):
             pkg.setdefault("Layer", {})["Digest"] = v
         elif k == "LayerDiffID":
             pkg.setdefault("Layer", {})["DiffID"] = v
+    for f in c.get("files") or []:  # decode.go:224-227: the first file path, unless a property set one
+        if f and not pkg.get("FilePath"):
+            pkg["FilePath"] = f
     pkg["Identifier"] = {"PURL": c["purl_str"], "BOMRef": c["bom_ref"]}
     pkg["_purl"] = p
     if purl_class(p) == "os-pkgs":  # fillSrcPkg (decode.go:260-279)
@@ -312,6 +315,13 @@ def _spdx_components(doc):
     [{SPDXID, name, version, sourceInfo, purls: [(category, type, locator)], attributions}],
     "relationships": [(a, type, b)]}."""
     trivy = any(c.startswith("Tool: trivy") for c in doc["creators"])
+    # parseFiles (unmarshal.go:107-132): a CONTAINS (or "CONTAIN") relationship from a package
+    # to a File element gives the package that file's path (the last such relationship wins)
+    files = doc.get("files") or {}
+    file_of = {}
+    for a, t, b in doc["relationships"]:
+        if t in ("CONTAINS", "CONTAIN") and _spdx_id(b).startswith("File") and _spdx_id(b) in files:
+            file_of[_spdx_id(a)] = files[_spdx_id(b)]
     root_id = next((_spdx_id(b) for a, t, b in doc["relationships"] if _spdx_id(a) == "DOCUMENT" and t == "DESCRIBES"),
                    None)
     comps, order = {}, []
@@ -337,6 +347,10 @@ def _spdx_components(doc):
         if trivy and typ == "application" and sp.get("sourceInfo"):  # older Trivy: path in sourceInfo, type in name
             c["name"] = sp["sourceInfo"]
             c["props"].append(("Type", sp.get("name", "")))
+        if sid in file_of:  # unmarshal.go:187-195: else the package's own first file
+            c["files"] = [file_of[sid]]
+        elif sp.get("files"):
+            c["files"] = [sp["files"][0]]
         comps[sid] = c
         order.append(c)
         if sid == root_id:
@@ -357,8 +371,12 @@ def decode_spdx_json(text):
         d = json.loads(text)
     except ValueError as e:
         raise SBOMError("failed to load spdx json: %s" % e)
-    doc = {"creators": (d.get("creationInfo") or {}).get("creators") or [], "packages": [], "relationships": []}
+    doc = {"creators": (d.get("creationInfo") or {}).get("creators") or [], "packages": [], "relationships": [],
+           "files": {_spdx_id(f.get("SPDXID", "")): f.get("fileName", "") for f in d.get("files") or []}}
+    has_files = []
     for p in d.get("packages") or []:
+        # tools-golang turns the deprecated hasFiles into CONTAINS relationships (spdx/tools-golang#201)
+        has_files += [(p.get("SPDXID", ""), "CONTAINS", f) for f in p.get("hasFiles") or []]
         doc["packages"].append({
             "SPDXID": p.get("SPDXID", ""), "name": p.get("name", ""), "version": p.get("versionInfo", ""),
             "sourceInfo": p.get("sourceInfo", ""), "attributions": p.get("attributionTexts") or [],
@@ -367,6 +385,7 @@ def decode_spdx_json(text):
     for r in d.get("relationships") or []:
         doc["relationships"].append((r.get("spdxElementId", ""), r.get("relationshipType", ""),
                                      r.get("relatedSpdxElement", "")))
+    doc["relationships"] += has_files
     order, root, rels = _spdx_components(doc)
     return _decode_bom(order, root, rels)
 
@@ -395,16 +414,25 @@ def _tv_pairs(text):
 
 def decode_spdx_tv(text):
     """SPDX tag-value (spdx/unmarshal.go TVDecoder) -> the same result as decode_cyclonedx."""
-    doc = {"creators": [], "packages": [], "relationships": []}
-    cur = None
+    doc = {"creators": [], "packages": [], "relationships": [], "files": {}}
+    cur = cur_file = last_pkg = None
     for tag, val in _tv_pairs(text):
         if tag == "Creator":
             doc["creators"].append(val)
         elif tag == "PackageName":
-            cur = {"SPDXID": "", "name": val, "version": "", "sourceInfo": "", "attributions": [], "purls": []}
+            cur = {"SPDXID": "", "name": val, "version": "", "sourceInfo": "", "attributions": [], "purls": [],
+                   "files": []}
             doc["packages"].append(cur)
-        elif tag in ("FileName", "SnippetSPDXID"):
-            cur = None  # a file / snippet section: its SPDXID is not a package's
+            last_pkg, cur_file = cur, None
+        elif tag == "FileName":  # a file section; a file that follows a package is one of its files
+            cur, cur_file = None, {"name": val, "id": ""}
+            if last_pkg is not None:
+                last_pkg["files"].append(val)
+        elif tag == "SnippetSPDXID":
+            cur = cur_file = None  # a snippet section: its SPDXID is not a package's
+        elif tag == "SPDXID" and cur_file is not None and not cur_file["id"]:
+            cur_file["id"] = val
+            doc["files"][_spdx_id(val)] = cur_file["name"]
         elif tag == "SPDXID" and cur is not None and not cur["SPDXID"]:
             cur["SPDXID"] = val
         elif cur is not None and tag == "PackageVersion":
@@ -458,7 +486,12 @@ def decode(text):
             d = json.loads(s.split("\n", 1)[0]) if s.count("\n") and s.split("\n", 1)[0].rstrip().endswith("}") \
                 else json.loads(s)
         except ValueError:
-            d = json.loads(s)
+            try:
+                d = json.loads(s)
+            except ValueError:  # sbom.go DetectFormat: undecodable JSON is no known format
+                raise SBOMError("failed to detect SBOM format") from None
+        if not isinstance(d, dict):
+            raise SBOMError("failed to detect SBOM format")
         if d.get("bomFormat") == "CycloneDX":
             return decode_cyclonedx(text)
         if str(d.get("spdxVersion", "")).startswith("SPDX-"):
