@@ -10,8 +10,9 @@ unfixed).  The pinned trivy-db cannot be fetched offline, hence synthetic data
 RHEL-family/Alpine workloads (tools/synth_mix.py) - extra measurements, not the headline.
 
 One step = one pass of the hot path over ONE global batch resident in HBM: the match
-kernels (probe + interval sweep), and with N > 1 GPUs the exact-size gather of every
-rank's match list (8 B per match) to rank 0 over RCCL.  The batch is sharded into
+kernels (probe + interval sweep), and with N > 1 GPUs the order kernel on every rank (its
+shard's per-package advisory lists, CSR) and the exact-size gather of those lists to rank 0
+over RCCL (4 B per match + 4 B per package), where they land in global batch order.  The batch is sharded into
 contiguous shards on target boundaries, balanced by predicted advisory rows (host
 pre-probe); the tables are replicated per GPU.  Strong scaling: the global batch is the
 same at every N; value = global packages x steps / max-over-ranks wall time.
@@ -251,16 +252,35 @@ def _mix_cpu_worker(job):
     return _mix_detect_loop(sm, sdb, batch, budget_s)
 
 
-def pmc_traffic(cfg_name):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, when it matches."""
-    p = os.path.join(ROOT, "profiles", "pmc_summary.json")
+def kernel_source_hash():
+    """sha1 over the sources the match kernels are compiled from (headers + kern_*.hip): ties a
+    committed PMC summary to the build it was measured on."""
+    import glob
+    import hashlib
+    h = hashlib.sha1()
+    csrc = os.path.join(ROOT, "trivy_amd", "csrc")
+    for f in sorted(glob.glob(os.path.join(csrc, "*.h")) + glob.glob(os.path.join(csrc, "kern_*.hip"))):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(config, workload, variant, src_hash):
+    """HBM bytes (raw FETCH_SIZE + WRITE_SIZE) of one full-grid launch of the match kernel from
+    the committed rocprofv3 summary of this config (tools/pmc_summary.py --json), or the reason
+    it cannot be used: a summary of another workload, kernel variant or kernel source is refused."""
+    p = os.path.join(ROOT, "profiles", f"pmc_summary_{config}.json")
     if not os.path.exists(p):
-        return None
+        return None, f"no profiles/pmc_summary_{config}.json"
     with open(p) as f:
         d = json.load(f)
-    if d.get("workload") != cfg_name:
-        return None
-    return d.get("hbm_bytes_per_launch")
+    for k, want in (("workload", workload), ("kernel_variant", variant), ("kernel_source", src_hash)):
+        if d.get(k) != want:
+            return None, f"profiles/pmc_summary_{config}.json is for {k}={d.get(k)!r}, this run is {want!r}"
+    return d["hbm_bytes_per_launch"], {"kernel": d["kernel"], "grid": d["grid"], "fetch_bytes_raw": d["fetch_bytes_raw"],
+                                       "write_bytes": d["write_bytes"], "avg_ns_full_grid": d["avg_ns_full_grid"],
+                                       "source": f"profiles/pmc_summary_{config}.json", "note": d["note"]}
 
 
 def main():
@@ -329,11 +349,11 @@ def main():
     total, errp, bits = mb.run()
     if bits or errp != -1:
         raise RuntimeError(f"engine error bits={bits} poisoned_pkg={errp}")
-    gather, cols = None, None
-    if world > 1:  # match columns written straight into the tensors the gather sends
-        cols = [torch.empty(max(total, 1), dtype=torch.int32, device=gdev) for _ in range(2)]
-        mb.upload_into(*cols)
-        gather = td.MatchGather(cdev)
+    gather, csr = None, None
+    if world > 1:  # the order kernel writes this rank's per-package lists (CSR) into the tensors the gather sends
+        csr = (torch.empty(max(total, 1), dtype=torch.int32, device=gdev),
+               torch.empty(max(n_local, 1), dtype=torch.int32, device=gdev))
+        gather = td.CSRGather(cdev)
     log(rank, f"[bench] shard {sb}..{se} of {wl.n}: {n_local} packages, {total} matches, "
               f"{int(rows[sb:se].sum())} predicted rows ({time.perf_counter()-t0:.1f}s)")
 
@@ -358,10 +378,11 @@ def main():
         mb.launch(1)  # the diagnostics left wrong counts behind
 
     def do_gather():
+        mb.order_into(*csr)  # per-package lists in batch order on this rank's GPU (synchronised)
         if backend == "nccl":
-            gather(cols[0], cols[1], total)
+            gather(csr[0], csr[1], total, n_local)
         else:  # gloo rehearsal: through host memory
-            gather(cols[0][:total].cpu(), cols[1][:total].cpu(), total)
+            gather(csr[0][:total].cpu(), csr[1][:n_local].cpu(), total, n_local)
 
     # ---- timed region: match pass (+ gather to rank 0) over the global batch -----------------
     def step():
@@ -514,11 +535,13 @@ def main():
         threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", 0) or 0) or os.cpu_count() or 1
         cpu = wl.cpu_baseline(args.cpu_seconds, threads)
 
-    traffic = pmc_traffic(wl.name)
+    src_hash = kernel_source_hash()
+    traffic, traffic_src = pmc_traffic(args.config, wl.name, vname, src_hash)
     if rank == 0:
         par = f"tables replicated, one global batch sharded x{world} on target boundaries by predicted rows"
         if world > 1:
-            par += ", exact-size gather of the match lists to rank 0 inside the timed step"
+            par += (", per-rank order kernel (per-package lists, CSR) + exact-size CSR gather to rank 0 in "
+                    "global batch order inside the timed step")
         line = {
             "metric": "packages matched/sec (node)",
             "value": value,
@@ -533,10 +556,10 @@ def main():
             "dtype": "u8",
             "data": "synthetic (seeded trivy-db + SBOM batch, tools/synth.py / tools/synth_mix.py)",
             "config": {"workload": wl.name, "packages": wl.n, "packages_rank0": n_local, "matches_rank0": total,
-                       "kernel_variant": vname, "db_keys": wl.n_keys, "db_advisories": wl.n_adv,
+                       "kernel_variant": vname, "kernel_source": src_hash, "db_keys": wl.n_keys, "db_advisories": wl.n_adv,
                        "platforms": wl.plats, "parallelism": par},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_from": traffic_src,
                          "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": kernel_ms,
                          "achieved_is": "algorithmic bytes (SURVEY §8d, no cache-reuse credit) / kernel time"},
             "cpu_baseline": cpu,

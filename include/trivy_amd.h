@@ -238,6 +238,15 @@ int tvm_match_fetch(tvm_engine* e, tvm_batch* b, uint32_t* pairs, uint64_t cap, 
  * package order within a tile, tiles in completion order (sort by (pkg, adv) to canonicalise).
  * For multi-GPU gathers that keep the match list off the host. */
 int tvm_match_copy_device(tvm_engine* e, tvm_batch* b, void* dst, uint64_t cap, uint64_t* n_out);
+/* The last pass's per-package advisory lists (CSR, (package, advisory) order) written into
+ * caller-owned device buffers on the engine's GPU, then synchronised: package p's advisories
+ * are csr_adv[row_end[p-1] .. row_end[p]) (row_end[-1] = 0; p counted from the batch's first
+ * package, so a shard's offsets start at 0).  The ordered form a multi-GPU gather sends to the
+ * root (4 B per match + 4 B per package), replacing the reference's per-target result slices
+ * (pkg/scanner/local/scan.go:170-194 scanVulnerabilities collects them per target).  TVM_EINVAL when the pass
+ * overflowed its match buffer or cap is below the match count (*n_out = the count). */
+int tvm_match_order_into(tvm_engine* e, tvm_batch* b, void* csr_adv_dev, void* row_end_dev, uint64_t cap,
+                         uint64_t* n_out, char* err, size_t errlen);
 /* Times `steps` back-to-back launches with HIP events on the engine stream (ms total). */
 int tvm_match_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err, size_t errlen);
 /* Algorithmic bytes of one pass (DESIGN.md "roofline"), computed on the host from the batch. */

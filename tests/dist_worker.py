@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""Two-rank check of the sharded match + gather on ONE GPU (ranks share the device, gloo
-collectives through host memory): one global batch, shards on target boundaries balanced by
-predicted rows, every rank matches its shard with global package indices, the exact-size
-gather brings every rank's list to rank 0, which compares it with a single-rank match of
-the whole batch.  Run by tests/test_gpu_dist.py under torch.distributed.run."""
+"""TEST HELPER (not collected by pytest): two-rank check of the sharded match + gather on ONE
+GPU (ranks share the device, gloo collectives through host memory).  One global batch,
+shards on target boundaries balanced by predicted rows; every rank matches its shard through
+the product engine, the order kernel turns its matches into per-package lists (CSR), and
+the CSR gather brings them to rank 0 in global batch order.  Rank 0 compares them, with no
+sort, with the oracle's match of the whole batch (oracle/match.c), and the raw pair gather
+with the oracle as a multiset.  Run by tests/test_gpu_dist.py under torch.distributed.run."""
 import os
 import sys
 
@@ -20,6 +22,7 @@ def main():
     from trivy_amd._lib import lib
     from trivy_amd.batch import MatchBatch
     from tools.synth import make_db, make_batch
+    from oracle import match as om
     dist.init_process_group("gloo")
     rank, ws = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
@@ -50,16 +53,22 @@ def main():
     mb.upload_into(*cols).launch()
     assert mb.status()[0] == total
     parts = td.MatchGather("cpu")(cols[0][:total].cpu(), cols[1][:total].cpu(), total)
+    csr_adv = torch.empty(max(total, 1), dtype=torch.int32, device="cuda:0")
+    row_end = torch.empty(max(se - sb, 1), dtype=torch.int32, device="cuda:0")
+    assert mb.order_into(csr_adv, row_end) == total
+    g = td.CSRGather("cpu")(csr_adv[:total].cpu(), row_end[:se - sb].cpu(), total, se - sb)
     if rank == 0:
+        opk, oad = om.match(om.Prepared(sdb, batch), n_threads=4)
+        # ordered CSR in global batch order, compared as is
+        want_end = np.cumsum(np.bincount(opk, minlength=len(batch)))
+        assert np.array_equal(g[0].numpy().view(np.uint32), oad.astype(np.uint32)), "CSR advisories"
+        assert np.array_equal(g[1].numpy().astype(np.int64), want_end), "CSR row ends"
+        # raw pairs: each rank's list is in tile order, so compare as a (package, advisory) set
         merged = np.stack([torch.cat([p for p, _ in parts]).numpy().view(np.uint32),
                            torch.cat([a for _, a in parts]).numpy().view(np.uint32)], axis=1)
-        full = fill(MatchBatch(eng), 0, len(batch))
-        full.run()
-        ref = full.pairs()
-        # each rank's list is in tile order, shards in rank order: compare as (package, advisory) sets
         got = merged[np.lexsort((merged[:, 1], merged[:, 0]))]
-        assert got.shape == ref.shape and np.array_equal(got, ref), (got.shape, ref.shape)
-        print(f"DIST OK {ws} ranks, shards {bounds}, {len(ref)} matches", flush=True)
+        assert np.array_equal(got, np.stack([opk, oad], axis=1).astype(np.uint32)), (got.shape, len(opk))
+        print(f"DIST OK {ws} ranks, shards {bounds}, {len(opk)} matches (CSR and pairs equal the oracle)", flush=True)
     dist.barrier()
     dist.destroy_process_group()
 

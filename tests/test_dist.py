@@ -65,6 +65,12 @@ def _rows(sdb, batch):
     return np.array([cnt.get((int(p), n), 0) + 1 for p, n in zip(batch.plat, batch.names)], dtype=np.float64)
 
 
+def _csr(pk, ad, n):
+    """(advisories, row ends) of n packages from (package, advisory)-ordered pairs."""
+    row_end = np.cumsum(np.bincount(np.asarray(pk, dtype=np.int64), minlength=n)[:n])
+    return np.asarray(ad, dtype=np.int32), row_end.astype(np.int32)
+
+
 def _worker(rank, ws, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=ws)
@@ -79,12 +85,16 @@ def _worker(rank, ws, port, q):
         pkg = torch.tensor(np.asarray(pk, dtype=np.int64) + b, dtype=torch.int32)
         adv = torch.tensor(np.asarray(ad, dtype=np.int64), dtype=torch.int32)
         parts = td.MatchGather("cpu")(pkg, adv, len(pk))
+        # the ordered form: every rank's CSR (offsets from its shard's first package)
+        ca, cr = _csr(np.asarray(pk), ad, e - b)
+        g = td.CSRGather("cpu")(torch.from_numpy(ca), torch.from_numpy(cr), len(ca), e - b)
+        csr = None if g is None else (g[0].tolist(), g[1].tolist())
         wall = td.timed(lambda: None, steps=3, warmup=1)
         m = td.max_over_ranks(float(rank + 1))
         merged = None
         if parts is not None:
             merged = (torch.cat([p for p, _ in parts]).tolist(), torch.cat([a for _, a in parts]).tolist())
-        q.put((rank, merged, wall >= 0, m, (b, e)))
+        q.put((rank, merged, wall >= 0, m, (b, e), csr))
     finally:
         dist.destroy_process_group()
 
@@ -98,13 +108,18 @@ def test_sharded_match_gathers_to_single_rank_result(oracle_built):
     ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    out = {r: (m, ok, mx, span) for r, m, ok, mx, span in (q.get(timeout=100) for _ in ps)}
+    out = {r: (m, ok, mx, span, csr) for r, m, ok, mx, span, csr in (q.get(timeout=100) for _ in ps)}
     for p in ps:
         p.join(timeout=30)
         assert p.exitcode == 0
-    merged, ok, mx, span0 = out[0]
+    merged, ok, mx, span0, csr = out[0]
     assert ok and mx == 2.0 and out[1][2] == 2.0 and out[1][0] is None
     assert span0[0] == 0 and span0[1] == out[1][3][0] and 0 < span0[1]  # both ranks got work
     sdb, batch = _global_batch()
     opk, oad = om.match(om.Prepared(sdb, batch), n_threads=2)
     assert merged[0] == [int(x) for x in opk] and merged[1] == [int(x) for x in oad]
+    # the ordered gather: the root holds the whole batch's per-package lists in batch order,
+    # equal to the oracle's CSR without any sort
+    assert out[1][4] is None
+    ca, cr = _csr(opk, oad, len(batch))
+    assert csr[0] == ca.tolist() and csr[1] == cr.tolist()

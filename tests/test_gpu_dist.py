@@ -1,7 +1,8 @@
-"""GPU: the multi-GPU path on one box - two ranks share the one MI355X (gloo collectives),
-each matches its shard of ONE global batch (target-boundary shards balanced by predicted
-rows, global package indices), the exact-size gather brings both lists to rank 0, and the
-merged pairs equal a single-rank match of the whole batch (tools/dist_check.py)."""
+"""GPU: the multi-GPU path on one box - two ranks share the one MI355X (gloo collectives;
+RCCL refuses two ranks on one device), each matches its shard of ONE global batch
+(target-boundary shards balanced by predicted rows), orders it into per-package lists (CSR)
+on the device, and the CSR gather brings them to rank 0 in batch order, where they equal the
+oracle's match of the whole batch without a sort (tests/dist_worker.py)."""
 import os
 import socket
 import subprocess
@@ -20,6 +21,6 @@ def test_two_ranks_gather_equals_single_rank():
     s.close()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-                        "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tools", "dist_check.py")],
+                        "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tests", "dist_worker.py")],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "DIST OK 2 ranks" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])

@@ -148,7 +148,7 @@ def test_batches_refused_after_swap(oracle_built):
     sdb2 = make_db(["debian 11", "debian 12", "ubuntu 22.04"], 500, seed=6)
     eng = build_engine(sdb)
     batch = make_batch(sdb, 6, 300, [1, 1], seed=2)
-    pipe = _fill(eng, sdb, batch).pipeline_prepare(chunk_packages=512)
+    pipe = _fill(eng, sdb, batch).pipeline_prepare(match_cap=1 << 17, chunk_packages=512)
     assert pipe.pipeline_run()[1] == -1
     dev = _fill(eng, sdb, batch)
     dev.run()

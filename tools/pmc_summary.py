@@ -1,12 +1,20 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 outputs (tools/profile_round.sh, tools/pmc_sq.sh) per match kernel.
+"""Summarise rocprofv3 outputs (tools/profile_round.sh, tools/pmc_sq.sh) per kernel AND grid.
 
-For every kernel of the match path (probe_kernel, sweep_kernel) prints the kernel-trace
-average duration and the per-dispatch median of every collected counter, plus per-wave
-instruction counts when SQ_WAVES was collected.  FETCH_SIZE / WRITE_SIZE are KiB
-(rocprofv3); per MI355X_MICROARCH.md §HBM, FETCH_SIZE reports half the bytes of wide
-coalesced streaming reads on gfx950 (only the staging loads here are that shape), so the
-raw figure is given.  The last line is JSON (profiles/pmc_summary.json form).
+Usage: pmc_summary.py OUT_DIR [--config c2] [--bench OUT_DIR/bench.json] [--json PATH]
+
+Every dispatch is grouped by (kernel, Grid_Size): the full-batch launches of the match kernel
+(one grid = the whole batch) are kept apart from the end-to-end pipeline's chunk launches and
+from other kernels, so "per launch" always means one full-grid launch.  For each group: the
+kernel-trace average duration (run_kernel_trace.csv) and the per-dispatch median of every
+collected counter.  FETCH_SIZE / WRITE_SIZE are KiB (rocprofv3).
+
+With --json, the match kernel's full-grid group (the largest grid among the match kernels) is
+written as the summary bench.py reads for `roofline.traffic`: raw FETCH + WRITE bytes per
+full-grid launch, the kernel's name, the bench variant and the kernel-source hash of the
+build that was profiled (bench.py refuses a summary whose hash or variant differs from the
+running build).  MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE counts half the bytes of a
+wide (16 B/lane) coalesced streaming read; the raw counter is reported, the note says so.
 """
 import csv
 import glob
@@ -15,8 +23,9 @@ import os
 import statistics
 import sys
 
-KERNELS = ("probe_kernel", "sweep_kernel", "fused_kernel", "match_kernel", "fill_pairs_kernel", "filter_mark",
-           "filter_select", "filter_place", "order_kernel")
+KERNELS = ("probe_kernel", "sweep_kernel", "fused_kernel", "persist_kernel", "match_kernel", "fill_pairs_kernel",
+           "filter_mark", "filter_select", "filter_count", "filter_place", "order_kernel", "redhat_merge")
+MATCH = ("fused_kernel", "persist_kernel", "match_kernel")
 
 
 def kname(name):
@@ -26,42 +35,84 @@ def kname(name):
     return None
 
 
-def main(out):
-    res = {"kernels": {}}
-    for stats in glob.glob(os.path.join(out, "**", "run_kernel_stats.csv"), recursive=True):
-        for r in csv.DictReader(open(stats)):
-            k = kname(r["Name"])
-            if k:
-                d = res["kernels"].setdefault(k, {"counters": {}})
-                d["name"] = r["Name"]
-                d["avg_ns"] = float(r["AverageNs"])
-                d["calls"] = int(r["Calls"])
-    for f in sorted(glob.glob(os.path.join(out, "**", "run_counter_collection.csv"), recursive=True)):
-        vals = {}
+def collect(out):
+    groups = {}  # (short, full name, grid) -> {"counters": {name: [values]}, "dur": [ns]}
+
+    def grp(r, name_col):
+        k = kname(r[name_col])
+        if not k or "diag" in r[name_col]:
+            return None
+        if r.get("Grid_Size"):
+            grid = int(float(r["Grid_Size"]))
+        else:  # kernel-trace rows give the grid per dimension
+            grid = 1
+            for ax in "XYZ":
+                grid *= int(float(r.get(f"Grid_Size_{ax}") or 1))
+        return groups.setdefault((k, r[name_col], grid), {"counters": {}, "dur": []})
+
+    for f in glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            k = kname(r["Kernel_Name"])
-            if not k or "diag" in r["Kernel_Name"]:
-                continue
-            vals.setdefault((k, r["Counter_Name"]), []).append(float(r["Counter_Value"]))
-        for (k, c), v in vals.items():
-            res["kernels"].setdefault(k, {"counters": {}})["counters"][c] = statistics.median(v)
-    for k, d in res["kernels"].items():
-        c = d["counters"]
+            g = grp(r, "Kernel_Name")
+            if g is not None:
+                g["dur"].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    for f in sorted(glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True)):
+        for r in csv.DictReader(open(f)):
+            g = grp(r, "Kernel_Name")
+            if g is not None:
+                g["counters"].setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    return groups
+
+
+def main(argv):
+    out = argv[0]
+    opt = dict(zip(argv[1::2], argv[2::2]))
+    groups = collect(out)
+    rows = []
+    for (k, full, grid), g in sorted(groups.items(), key=lambda x: (x[0][0], -x[0][2])):
+        c = {n: statistics.median(v) for n, v in g["counters"].items()}
+        d = {"kernel": full, "short": k, "grid": grid, "counters": c,
+             "launches_traced": len(g["dur"]), "avg_ns": statistics.mean(g["dur"]) if g["dur"] else None}
         if "FETCH_SIZE" in c:
-            d["fetch_bytes_per_launch"] = c["FETCH_SIZE"] * 1024
+            d["fetch_bytes_raw"] = c["FETCH_SIZE"] * 1024
         if "WRITE_SIZE" in c:
-            d["write_bytes_per_launch"] = c["WRITE_SIZE"] * 1024
+            d["write_bytes"] = c["WRITE_SIZE"] * 1024
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            d["hbm_bytes_per_launch"] = (c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
-        print(f"== {k}  avg {d.get('avg_ns', 0) / 1e3:.1f} us over {d.get('calls', 0)} calls")
+            d["hbm_bytes_raw"] = d["fetch_bytes_raw"] + d["write_bytes"]
+        rows.append(d)
+        avg = f"avg {d['avg_ns'] / 1e3:.1f} us over {d['launches_traced']} traced launches" if d["avg_ns"] else "no trace"
+        print(f"== {k}  grid {grid}  {avg}\n   {full}")
+        waves = c.get("SQ_WAVES")
         for n, v in sorted(c.items()):
-            per = f"   ({v / c['SQ_WAVES']:,.1f} per wave)" if "SQ_WAVES" in c and n.startswith("SQ_INSTS") else ""
+            per = f"   ({v / waves:,.1f} per wave)" if waves and n.startswith("SQ_INSTS") else ""
             print(f"{n:>28}: {v:,.1f}{per}")
-        for n in ("fetch_bytes_per_launch", "write_bytes_per_launch", "hbm_bytes_per_launch"):
+        for n in ("fetch_bytes_raw", "write_bytes", "hbm_bytes_raw"):
             if n in d:
-                print(f"{n:>28}: {d[n]:,.1f}")
-    print(json.dumps(res))
+                print(f"{n:>28}: {d[n]:,.0f} per launch")
+    if "--json" in opt:
+        match = [d for d in rows if d["short"] in MATCH and "hbm_bytes_raw" in d]
+        if not match:
+            print("no match-kernel FETCH/WRITE counters found", file=sys.stderr)
+            return 1
+        top = max(match, key=lambda d: d["grid"])
+        bench = {}
+        if opt.get("--bench") and os.path.exists(opt["--bench"]):
+            txt = open(opt["--bench"]).read().strip().splitlines()
+            bench = json.loads(txt[-1]) if txt else {}
+        cfg = bench.get("config", {})
+        summ = {"config": opt.get("--config"), "workload": cfg.get("workload"), "kernel": top["kernel"],
+                "kernel_variant": cfg.get("kernel_variant"), "kernel_source": cfg.get("kernel_source"),
+                "grid": top["grid"], "avg_ns_full_grid": top["avg_ns"],
+                "fetch_bytes_raw": top["fetch_bytes_raw"], "write_bytes": top["write_bytes"],
+                "hbm_bytes_per_launch": top["hbm_bytes_raw"],
+                "note": "raw FETCH_SIZE + WRITE_SIZE of one full-grid launch (median over the profiled launches); "
+                        "MI355X_MICROARCH.md §HBM: gfx950 FETCH_SIZE counts half the bytes of 16-B/lane coalesced "
+                        "streaming reads (the staging and row loads have that shape), so the raw fetch is a lower "
+                        "bound on the bytes the kernel moved from beyond L2"}
+        with open(opt["--json"], "w") as f:
+            json.dump(summ, f, indent=1)
+        print(json.dumps(summ))
+    return 0
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    sys.exit(main(sys.argv[1:]))

@@ -146,6 +146,8 @@ _SIG = [
                                         ctypes.POINTER(ctypes.c_uint64)]),
     ("tvm_match_fetch", ctypes.c_int, [_P, _P, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     ("tvm_match_copy_device", ctypes.c_int, [_P, _P, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
+    ("tvm_match_order_into", ctypes.c_int, [_P, _P, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                            ctypes.POINTER(ctypes.c_uint64), ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_match_time", ctypes.c_int, [_P, _P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_char_p,
                                       ctypes.c_size_t]),
     ("tvm_match_algorithmic_bytes", ctypes.c_uint64, [_P, _P]),

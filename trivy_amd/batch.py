@@ -169,6 +169,17 @@ class MatchBatch:
         self._cols = (pkg, adv)
         return self
 
+    def order_into(self, csr_adv, row_end):
+        """The last pass's per-package advisory lists as CSR, written by the order kernel into
+        caller device buffers (int32 torch tensors on the engine's GPU: csr_adv >= the match
+        count, row_end = one entry per package of this batch); returns the match count."""
+        if row_end.numel() < len(self) or csr_adv.dtype.itemsize != 4 or row_end.dtype.itemsize != 4:
+            raise ValueError("row_end needs one 4-byte entry per package, csr_adv 4-byte entries")
+        e, n = errbuf(), ctypes.c_uint64()
+        self._check(lib().tvm_match_order_into(self.engine.h, self.h, csr_adv.data_ptr(), row_end.data_ptr(),
+                                               csr_adv.numel(), ctypes.byref(n), e, len(e)), e, "tvm_match_order_into")
+        return n.value
+
     def launch(self, k=1, sync=True):
         e = errbuf()
         for _ in range(k):

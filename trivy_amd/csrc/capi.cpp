@@ -64,6 +64,8 @@ struct tvm_batch {
   std::unique_ptr<Pipeline> pipe;      // tvm_pipeline_* state
   uint32_t pkg_base = 0;               // tvm_batch_set_package_base
   uint64_t pipe_total = 0;
+  unsigned long long* order_scratch = nullptr;  // tvm_match_order_into: ticket + look-back word per tile
+  uint32_t order_cap = 0;
   bool external_out = false;  // m.pkg / m.adv belong to the caller (tvm_batch_upload_into)
   bool uploaded = false;      // dev / m hold real device buffers
   bool pinned = false;        // tvm_pipeline_prepare pinned the host arrays: no more adds
@@ -390,6 +392,10 @@ tvm_batch* tvm_batch_new(void) { return new tvm_batch(); }
 void tvm_batch_free(tvm_batch* b) {
   if (!b) return;
   b->pipe.reset();
+  if (b->order_scratch) {
+    (void)hipSetDevice(b->device);
+    (void)hipFree(b->order_scratch);
+  }
   if (b->uploaded) {
     (void)hipSetDevice(b->device);
     for (void* p : {static_cast<void*>(b->dev.pk), static_cast<void*>(b->dev.tile_off), static_cast<void*>(b->dev.arena),
@@ -614,6 +620,57 @@ int tvm_match_copy_device(tvm_engine* e, tvm_batch* b, void* dst, uint64_t cap, 
             hipStreamSynchronize(st) != hipSuccess))
     return TVM_EDEVICE;
   if (n_out) *n_out = n;
+  return TVM_OK;
+}
+
+int tvm_match_order_into(tvm_engine* e, tvm_batch* b, void* csr_adv_dev, void* row_end_dev, uint64_t cap,
+                         uint64_t* n_out, char* err, size_t errlen) {
+  uint64_t n = 0;
+  int rc = tvm_match_status(e, b, &n, nullptr, nullptr);
+  if (rc) return rc;
+  if (n_out) *n_out = n;
+  if (b->merged || n > b->m.cap || n > cap || !row_end_dev || (n && !csr_adv_dev)) return TVM_EINVAL;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e)) {
+    set_err(err, errlen, kStale);
+    return TVM_EINVAL;
+  }
+  (void)hipSetDevice(e->device);
+  hipStream_t st = e->eng->stream();
+  const uint32_t nt = b->dev.n_tiles;
+  if (nt == 0) return TVM_OK;
+  if (b->order_cap < nt + 1) {
+    if (b->order_scratch) (void)hipFree(b->order_scratch);
+    b->order_scratch = nullptr;
+    b->order_cap = 0;
+    void* p = nullptr;
+    if (hipMalloc(&p, size_t(nt + 1) * 8) != hipSuccess) {
+      set_err(err, errlen, "hipMalloc(order scratch) failed");
+      return TVM_EDEVICE;
+    }
+    b->order_scratch = static_cast<unsigned long long*>(p);
+    b->order_cap = nt + 1;
+  }
+  OrderArgs oa;
+  oa.dir = b->m.dir;
+  oa.pkg = b->m.pkg;
+  oa.adv = b->m.adv;
+  oa.csr_adv = static_cast<uint32_t*>(csr_adv_dev);
+  oa.row_end = static_cast<uint32_t*>(row_end_dev);
+  oa.cap = std::min<uint64_t>(cap, b->m.cap);
+  oa.ticket = b->order_scratch;
+  oa.status = b->order_scratch + 1;
+  oa.t0 = 0;
+  oa.n = b->dev.n;
+  oa.pkg_base = b->dev.pkg_base;
+  if (hipMemsetAsync(b->order_scratch, 0, size_t(nt + 1) * 8, st) != hipSuccess) return TVM_EDEVICE;
+  launch_order(nt, st, oa);
+  const hipError_t le = hipGetLastError();
+  const hipError_t se = le == hipSuccess ? hipStreamSynchronize(st) : le;
+  if (se != hipSuccess) {
+    set_err(err, errlen, std::string("order kernel: ") + hipGetErrorString(se));
+    return TVM_EDEVICE;
+  }
   return TVM_OK;
 }
 

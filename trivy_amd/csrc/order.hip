@@ -63,7 +63,7 @@ __global__ __launch_bounds__(kTile) void order_kernel(OrderArgs a) {
   const unsigned long long b = base;
   const bool fits = d.base + d.count <= a.cap && b + d.count <= a.cap;
   if (fits)
-    for (uint32_t i = tid; i < d.count; i += kTile) atomicAdd(&cnt[a.pkg[d.base + i] - p_first], 1u);
+    for (uint32_t i = tid; i < d.count; i += kTile) atomicAdd(&cnt[a.pkg[d.base + i] - a.pkg_base - p_first], 1u);
   __syncthreads();
   if (fits)
     for (uint32_t i = tid; i < d.count; i += kTile) a.csr_adv[b + i] = a.adv[d.base + i];

@@ -19,6 +19,7 @@ struct OrderArgs {
   unsigned long long* ticket;  // this launch's ticket counter (zeroed before the pass)
   uint32_t t0;                 // first tile of this launch
   uint32_t n;                  // packages in the batch
+  uint32_t pkg_base = 0;       // added to every package index the match kernels wrote (a shard's first package)
 };
 void launch_order(uint32_t n_tiles, hipStream_t st, const OrderArgs& a);
 

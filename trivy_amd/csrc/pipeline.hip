@@ -172,6 +172,7 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
     oa.ticket = tickets_d_ + c;
     oa.t0 = t0;
     oa.n = n;
+    oa.pkg_base = db_.pkg_base;
     if (t1 > t0) launch_order(t1 - t0, s_k_, oa);
     if (!ok(hipGetLastError(), "order kernel launch", err) || !ok(hipEventRecord(ev_k_[c], s_k_), "hipEventRecord", err))
       return false;

@@ -85,6 +85,77 @@ def timed(step, steps, warmup, sync=lambda: None, device="cpu"):
     return max_over_ranks(time.perf_counter() - t0, device)
 
 
+class CSRGather:
+    """Exact-size gather of every rank's ORDERED per-package advisory lists to `root`, which
+    ends up holding the whole batch's lists in global batch order with no host sort.
+
+    Each rank hands its shard's CSR (MatchBatch.order_into: csr_adv = the advisory indices in
+    (package, advisory) order, row_end[i] = end of the shard's i-th package's list, offsets
+    from 0) as int32 tensors.  Shards are contiguous package ranges in rank order, so the root
+    receives rank r's advisories straight into its slice of one global array and its row ends
+    into the next package slice, then adds the advisories of ranks < r to those row ends: 4 B
+    per match + 4 B per package over the wire, one device-side add, no reordering.  Buffers
+    only grow, so a steady-state gather allocates nothing."""
+
+    def __init__(self, device, root=0):
+        self.device = device
+        self.root = root
+        self.adv = None
+        self.row_end = None
+
+    def _grow(self, n_adv, n_pkg):
+        if self.adv is None or self.adv.numel() < n_adv:
+            self.adv = torch.empty(max(n_adv, 1), dtype=torch.int32, device=self.device)
+        if self.row_end is None or self.row_end.numel() < n_pkg:
+            self.row_end = torch.empty(max(n_pkg, 1), dtype=torch.int32, device=self.device)
+
+    def __call__(self, csr_adv, row_end, n_matches, n_pkgs):
+        """Returns (adv, row_end) of the whole batch on the root, None elsewhere."""
+        rank, ws = world()
+        if ws == 1:
+            return csr_adv[:n_matches], row_end[:n_pkgs]
+        cnt = torch.tensor([n_matches, n_pkgs], dtype=torch.int64, device=self.device)
+        counts = [torch.zeros_like(cnt) for _ in range(ws)]
+        dist.all_gather(counts, cnt)
+        counts = [(int(c[0].item()), int(c[1].item())) for c in counts]
+        if rank != self.root:
+            ops = []
+            if n_matches:
+                ops.append(dist.P2POp(dist.isend, csr_adv[:n_matches].contiguous(), self.root))
+            if n_pkgs:
+                ops.append(dist.P2POp(dist.isend, row_end[:n_pkgs].contiguous(), self.root))
+            if ops:
+                for r in dist.batch_isend_irecv(ops):
+                    r.wait()
+            return None
+        t_adv = sum(c[0] for c in counts)
+        t_pkg = sum(c[1] for c in counts)
+        if t_adv >= 1 << 31:
+            raise ValueError("row ends are 32-bit: gather below 2^31 matches at a time")
+        self._grow(t_adv, t_pkg)
+        ops, a0, p0, fix = [], 0, 0, []
+        for r, (na, npk) in enumerate(counts):
+            dst_a, dst_p = self.adv[a0:a0 + na], self.row_end[p0:p0 + npk]
+            if r == rank:
+                dst_a.copy_(csr_adv[:na])
+                dst_p.copy_(row_end[:npk])
+            else:
+                if na:
+                    ops.append(dist.P2POp(dist.irecv, dst_a, r))
+                if npk:
+                    ops.append(dist.P2POp(dist.irecv, dst_p, r))
+            if a0 and npk:
+                fix.append((dst_p, a0))
+            a0 += na
+            p0 += npk
+        if ops:
+            for q in dist.batch_isend_irecv(ops):
+                q.wait()
+        for dst_p, off in fix:
+            dst_p.add_(off)
+        return self.adv[:t_adv], self.row_end[:t_pkg]
+
+
 class MatchGather:
     """Exact-size gather of every rank's match columns to `root`.
 
