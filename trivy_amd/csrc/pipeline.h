@@ -23,14 +23,27 @@ struct OrderArgs {
 };
 void launch_order(uint32_t n_tiles, hipStream_t st, const OrderArgs& a);
 
+struct CopyOutArgs {
+  const uint32_t* row_end;  // device CSR (order_kernel)
+  const uint32_t* csr_adv;
+  uint4* row_end_h;         // device addresses of the pinned host result (16-B aligned, padded)
+  uint4* adv_h;
+  uint32_t p0, p1;          // the chunk's packages, p0 a multiple of kTile, p1 > p0
+  uint64_t cap;             // advisory capacity (a range beyond it is cut)
+};
+void launch_copy_out(hipStream_t st, const CopyOutArgs& a);
+
 // One batch's pipeline state.  prepare() pins the batch's host arrays (hipHostRegister),
 // sizes the device batch, the match buffers and the pinned result buffers; run() then
 // streams the batch through in chunks of whole tiles:
-//   copy stream    H2D of chunk c (package words, tile offsets, string bytes, attributes);
-//   kernel stream  (after chunk c's copy) the match kernels + order_kernel over chunk c;
-//   result stream  (after chunk c's kernels) D2H of chunk c's row ends, then - once the host
-//                  has read the chunk's last row end - of its advisory indices;
-// so chunk c+1's H2D and chunk c-1's D2H run under chunk c's kernels.
+//   copy stream    DMA of chunk c to HBM (package words, tile offsets, string bytes, attributes);
+//   kernel stream  (after chunk c's copy) the match kernels + order_kernel over chunk c
+//                  (per-package advisory lists, CSR, in HBM);
+//   result stream  (after chunk c's order kernel) copy_out_kernel, whose 16-byte stores put
+//                  the chunk's advisory indices and row ends straight into the pinned host
+//                  result (zero-copy: the link's other direction, no DMA, and the chunk's
+//                  range is read on the device, so the host never waits per chunk);
+// so chunk c+1's upload and chunk c-1's result writes run under chunk c's kernels.
 class Pipeline {
  public:
   ~Pipeline();
@@ -48,19 +61,21 @@ class Pipeline {
  private:
   void release();
   int dev_ = -1;
-  hipStream_t s_h2d_ = nullptr, s_k_ = nullptr, s_d2h_ = nullptr;
-  std::vector<hipEvent_t> ev_h_, ev_k_, ev_r_;
+  hipStream_t s_h2d_ = nullptr, s_k_ = nullptr, s_o_ = nullptr;
+  std::vector<hipEvent_t> ev_h_, ev_k_;
   std::vector<uint32_t> bounds_;     // chunk c = tiles [bounds_[c], bounds_[c + 1])
   std::vector<uint64_t> toff_;       // tile offsets + the arena end (registered)
   std::vector<void*> registered_;
   DevBatch db_;
   DevMatches m_;
-  uint32_t* csr_adv_d_ = nullptr;
-  uint32_t* row_end_d_ = nullptr;
   unsigned long long* status_d_ = nullptr;
   unsigned long long* tickets_d_ = nullptr;
   uint32_t* adv_h_ = nullptr;
   uint32_t* row_end_h_ = nullptr;
+  uint32_t* csr_adv_d_ = nullptr;   // device CSR (order_kernel)
+  uint32_t* row_end_d_ = nullptr;
+  uint32_t* adv_hd_ = nullptr;      // device addresses of adv_h_ / row_end_h_ (copy_out_kernel stores)
+  uint32_t* row_end_hd_ = nullptr;
   unsigned long long* ctl_h_ = nullptr;
   uint64_t cap_ = 0, h2d_ = 0, d2h_ = 0;
   bool prepared_ = false;  // no Engine pointer: the batch may outlive a hot swap (the C-ABI checks the generation)

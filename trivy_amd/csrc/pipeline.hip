@@ -1,5 +1,5 @@
-// End-to-end pipelined match pass (pipeline.h): PCIe copies on their own streams overlap
-// the match kernels, chunk by chunk.  Every buffer is sized once in prepare(); a pass
+// End-to-end pipelined match pass (pipeline.h): the batch's DMA upload, the match kernels
+// and the order kernel's direct writes of the result into host memory overlap chunk by chunk.  Every buffer is sized once in prepare(); a pass
 // allocates nothing.
 #include "pipeline.h"
 
@@ -24,7 +24,7 @@ void Pipeline::release() {
   if (dev_ < 0) return;
   (void)hipSetDevice(dev_);
   if (s_k_) (void)hipStreamSynchronize(s_k_);
-  if (s_d2h_) (void)hipStreamSynchronize(s_d2h_);
+  if (s_o_) (void)hipStreamSynchronize(s_o_);
   if (s_h2d_) (void)hipStreamSynchronize(s_h2d_);
   Engine::free_batch(dev_, db_);
   Engine::free_matches(dev_, m_);
@@ -35,13 +35,14 @@ void Pipeline::release() {
     if (p) (void)hipHostFree(p);
   for (void* p : registered_) (void)hipHostUnregister(p);
   registered_.clear();
-  for (auto* v : {&ev_h_, &ev_k_, &ev_r_}) {
+  for (auto* v : {&ev_h_, &ev_k_}) {
     for (hipEvent_t e : *v) (void)hipEventDestroy(e);
     v->clear();
   }
-  for (hipStream_t s : {s_h2d_, s_k_, s_d2h_})
+  for (hipStream_t s : {s_h2d_, s_k_, s_o_})
     if (s) (void)hipStreamDestroy(s);
-  s_h2d_ = s_k_ = s_d2h_ = nullptr;
+  s_h2d_ = s_k_ = s_o_ = nullptr;
+  adv_hd_ = row_end_hd_ = nullptr;
   csr_adv_d_ = row_end_d_ = nullptr;
   status_d_ = tickets_d_ = nullptr;
   adv_h_ = row_end_h_ = nullptr;
@@ -70,14 +71,14 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
     err = "pipeline: row ends are 32-bit; split the batch below 2^32 matches";
     return false;
   }
-  for (auto* v : {&ev_h_, &ev_k_, &ev_r_}) {
+  for (auto* v : {&ev_h_, &ev_k_}) {
     v->resize(nc);
     for (hipEvent_t& e : *v)
       if (!ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate", err)) return false;
   }
   if (!ok(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking), "hipStreamCreate", err) ||
       !ok(hipStreamCreateWithFlags(&s_k_, hipStreamNonBlocking), "hipStreamCreate", err) ||
-      !ok(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking), "hipStreamCreate", err))
+      !ok(hipStreamCreateWithFlags(&s_o_, hipStreamNonBlocking), "hipStreamCreate", err))
     return false;
   // pin the caller's host arrays in place: the copies are DMA from them, no staging memcpy
   auto reg = [&](const void* p, size_t bytes) {
@@ -100,19 +101,28 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
     db_.n_cpe_sets = uint32_t(hb.cpe_bits.size() / hb.cpe_words);
   }
   const size_t n = std::max<size_t>(hb.pk.size(), 1);
+  // CSR buffers padded to whole 16-byte units (copy_out_kernel moves units)
+  const size_t cap4 = (cap_ + 3) & ~size_t(3), n4 = (size_t(n_tiles) * kTile + 3) & ~size_t(3);
   void* p = nullptr;
-  if (!ok(hipMalloc(&p, cap_ * 4), "hipMalloc(csr)", err)) return false;
+  if (!ok(hipMalloc(&p, cap4 * 4), "hipMalloc(csr)", err)) return false;
   csr_adv_d_ = static_cast<uint32_t*>(p);
-  if (!ok(hipMalloc(&p, n * 4), "hipMalloc(row ends)", err)) return false;
+  if (!ok(hipMalloc(&p, std::max<size_t>(n4, 4) * 4), "hipMalloc(row ends)", err)) return false;
   row_end_d_ = static_cast<uint32_t*>(p);
   if (!ok(hipMalloc(&p, std::max<size_t>(n_tiles, 1) * 8), "hipMalloc(status)", err)) return false;
   status_d_ = static_cast<unsigned long long*>(p);
   if (!ok(hipMalloc(&p, std::max<size_t>(nc, 1) * 8), "hipMalloc(tickets)", err)) return false;
   tickets_d_ = static_cast<unsigned long long*>(p);
-  if (!ok(hipHostMalloc(&p, cap_ * 4, hipHostMallocDefault), "hipHostMalloc(adv)", err)) return false;
+  // the result lives in pinned host memory that the order kernel writes directly over PCIe
+  // (measured, profiles/r03/pcie_probe.txt: kernel stores to host memory 55 GB/s, a DMA
+  // device-to-host copy 28.6 GB/s; the DMA engine then only carries the batch upward)
+  if (!ok(hipHostMalloc(&p, cap4 * 4, hipHostMallocDefault), "hipHostMalloc(adv)", err)) return false;
   adv_h_ = static_cast<uint32_t*>(p);
-  if (!ok(hipHostMalloc(&p, n * 4, hipHostMallocDefault), "hipHostMalloc(row ends)", err)) return false;
+  if (!ok(hipHostMalloc(&p, std::max<size_t>(n4, 4) * 4, hipHostMallocDefault), "hipHostMalloc(row ends)", err)) return false;
   row_end_h_ = static_cast<uint32_t*>(p);
+  if (!ok(hipHostGetDevicePointer(&p, adv_h_, 0), "hipHostGetDevicePointer(adv)", err)) return false;
+  adv_hd_ = static_cast<uint32_t*>(p);
+  if (!ok(hipHostGetDevicePointer(&p, row_end_h_, 0), "hipHostGetDevicePointer(row ends)", err)) return false;
+  row_end_hd_ = static_cast<uint32_t*>(p);
   if (!ok(hipHostMalloc(&p, 64, hipHostMallocDefault), "hipHostMalloc(ctl)", err)) return false;
   ctl_h_ = static_cast<unsigned long long*>(p);
   prepared_ = true;
@@ -136,7 +146,13 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
       !ok(hipMemsetAsync(status_d_, 0, std::max<size_t>(db_.n_tiles, 1) * 8, s_k_), "memset(status)", err) ||
       !ok(hipMemsetAsync(tickets_d_, 0, std::max<size_t>(nc, 1) * 8, s_k_), "memset(tickets)", err))
     return false;
-  // 1. every chunk's H2D on the copy stream (DMA from the pinned host arrays)
+  // Per chunk: its upload on the copy stream (DMA from the pinned host arrays); behind it
+  // the match kernels + the order kernel (device CSR) on the kernel stream; behind those, on
+  // the result stream, copy_out_kernel, which stores the chunk's lists straight into the
+  // pinned host result.  Chunks are issued in order, upload first, so chunk c's kernels and
+  // result writes are queued before chunk c+1's upload is (the runtime may block the host
+  // in a copy call until the copy ran: measured, profiles/r03/e2e_timeline_*.txt); the host
+  // waits once, at the end.
   for (uint32_t c = 0; c < nc; c++) {
     const uint32_t t0 = bounds_[c], t1 = bounds_[c + 1];
     const size_t p0 = size_t(t0) * kTile, p1 = std::min<size_t>(size_t(t1) * kTile, n);
@@ -154,10 +170,7 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
         !ok(hipEventRecord(ev_h_[c], s_h2d_), "hipEventRecord", err))
       return false;
     h2d_ += (p1 - p0) * sizeof(uint2) + (g1 - g0 + 1) * 8 + (a1 - a0) + (hb.attr.empty() ? 0 : (p1 - p0) * sizeof(uint2));
-  }
-  // 2. kernels per chunk, each behind its chunk's copy
-  for (uint32_t c = 0; c < nc; c++) {
-    const uint32_t t0 = bounds_[c], t1 = bounds_[c + 1];
+    if (t1 == t0) continue;
     if (!ok(hipStreamWaitEvent(s_k_, ev_h_[c], 0), "hipStreamWaitEvent", err) ||
         !eng.launch_tiles(db_, m_, t0, t1, s_k_, s_k_, nullptr, err))
       return false;
@@ -173,34 +186,26 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
     oa.t0 = t0;
     oa.n = n;
     oa.pkg_base = db_.pkg_base;
-    if (t1 > t0) launch_order(t1 - t0, s_k_, oa);
-    if (!ok(hipGetLastError(), "order kernel launch", err) || !ok(hipEventRecord(ev_k_[c], s_k_), "hipEventRecord", err))
+    launch_order(t1 - t0, s_k_, oa);
+    if (!ok(hipGetLastError(), "order kernel launch", err) || !ok(hipEventRecord(ev_k_[c], s_k_), "hipEventRecord", err) ||
+        !ok(hipStreamWaitEvent(s_o_, ev_k_[c], 0), "hipStreamWaitEvent", err))
       return false;
+    CopyOutArgs ca;
+    ca.row_end = row_end_d_;
+    ca.csr_adv = csr_adv_d_;
+    ca.row_end_h = reinterpret_cast<uint4*>(row_end_hd_);
+    ca.adv_h = reinterpret_cast<uint4*>(adv_hd_);
+    ca.p0 = t0 * kTile;
+    ca.p1 = std::min<uint32_t>(t1 * kTile, n);
+    ca.cap = cap_;
+    launch_copy_out(s_o_, ca);
+    if (!ok(hipGetLastError(), "copy-out kernel launch", err)) return false;
   }
-  if (!ok(hipMemcpyAsync(ctl_h_, m_.ctl, 64, hipMemcpyDeviceToHost, s_k_), "D2H ctl", err)) return false;
-  // 3. results per chunk: row ends, then (once the host knows where the chunk ends) its advisories
-  uint64_t start = 0;
-  for (uint32_t c = 0; c < nc; c++) {
-    const uint32_t t0 = bounds_[c], t1 = bounds_[c + 1];
-    const size_t p0 = size_t(t0) * kTile, p1 = std::min<size_t>(size_t(t1) * kTile, n);
-    if (p1 == p0) continue;
-    if (!ok(hipStreamWaitEvent(s_d2h_, ev_k_[c], 0), "hipStreamWaitEvent", err) ||
-        !ok(hipMemcpyAsync(row_end_h_ + p0, row_end_d_ + p0, (p1 - p0) * 4, hipMemcpyDeviceToHost, s_d2h_),
-            "D2H row ends", err) ||
-        !ok(hipEventRecord(ev_r_[c], s_d2h_), "hipEventRecord", err) ||
-        !ok(hipEventSynchronize(ev_r_[c]), "hipEventSynchronize", err))
-      return false;
-    const uint64_t end = row_end_h_[p1 - 1];
-    if (end > cap_) break;  // overflow: the caller re-prepares with the total below
-    if (end > start &&
-        !ok(hipMemcpyAsync(adv_h_ + start, csr_adv_d_ + start, (end - start) * 4, hipMemcpyDeviceToHost, s_d2h_),
-            "D2H advisories", err))
-      return false;
-    d2h_ += (p1 - p0) * 4 + (end - start) * 4;
-    start = end;
-  }
-  if (!ok(hipStreamSynchronize(s_d2h_), "pipeline D2H", err) || !ok(hipStreamSynchronize(s_k_), "pipeline kernels", err))
+  if (!ok(hipStreamSynchronize(s_k_), "pipeline kernels", err) ||
+      !ok(hipMemcpyAsync(ctl_h_, m_.ctl, 64, hipMemcpyDeviceToHost, s_k_), "D2H ctl", err) ||
+      !ok(hipStreamSynchronize(s_k_), "D2H ctl", err) || !ok(hipStreamSynchronize(s_o_), "pipeline results", err))
     return false;
+  d2h_ = uint64_t(n) * 4 + std::min<uint64_t>(ctl_h_[0], cap_) * 4;
   total = ctl_h_[0];
   err_pkg = ctl_h_[1] ? int64_t(n - ctl_h_[1]) : -1;
   err_bits = ctl_h_[3];
