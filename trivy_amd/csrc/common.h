@@ -90,7 +90,7 @@ struct alignas(16) RowAux {
   uint16_t n_cpe;
 };
 //   AUX_CLASS     library rows: pass if bit <installed version class> of `tag` is set
-//                 (libver.h classes: npm pre-release, PEP 440 local/pre/post).
+//                 (libver.h classes: npm pre-release, PEP 440 local/pre/post, Maven numeric).
 //   AUX_MVN       Maven library rows: the advisory's IsVulnerable program at aux_ids[list_off]
 //                 evaluated pairwise against the installed version (libver.h mvn_program_eval).
 enum : uint32_t { AUX_ARCH_RH = 1, AUX_ARCH_IN = 2, AUX_CPE = 4, AUX_TAG = 8, AUX_CLASS = 16, AUX_MVN = 32 };

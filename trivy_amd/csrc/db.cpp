@@ -525,10 +525,14 @@ void DB::flatten_os(uint32_t plat, const Bucket& root, int32_t ds) {
 // Advisory -> interval row(s) of its driver (SURVEY.md §8a' "unfixed" and parse-error
 // columns).  Returns false when the advisory can never be reported (no row).
 bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::vector<uint8_t>& kb) {
+  // Maven: ComparableVersion is not an order, so in general no interval set
+  // can stand for IsVulnerable: the row carries the advisory's program (AUX_MVN) and the
+  // kernel evaluates it pairwise against the installed version.  Hybrid: when every bound
+  // text is numeric (libver.h mvn_numeric), numeric installed versions (class 1) are
+  // compared in the key order, which is exact on that domain - the advisory's intervals
+  // as class-1 rows below, and the program row only for class 0.
+  bool mvn_hybrid = false;
   if (P.drv == DRV_LIBRARY && P.cmp == CMP_MAVEN) {
-    // Maven: ComparableVersion is not an order, so no interval set can
-    // stand for IsVulnerable; the row carries the advisory's program (AUX_MVN) and the
-    // kernel evaluates it pairwise against the installed version
     std::vector<uint32_t> w;
     const MvnProgState st = mvn_program(a.vulnerable, a.patched, a.unaffected, w);
     if (st == MVN_NEVER) return false;
@@ -537,21 +541,25 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
     RowAux x{};
     r.adv = ai | (st == MVN_ALWAYS ? ROW_ALWAYS : ROW_FILTER);
     if (st == MVN_PROGRAM) {
-      x.kind = AUX_MVN;
+      mvn_hybrid = mvn_bounds_numeric(a.vulnerable, a.patched, a.unaffected) &&
+                   lib_compile_advisory(P.cmp, a.vulnerable, a.patched, a.unaffected).ok;
+      x.kind = AUX_MVN | (mvn_hybrid ? AUX_CLASS : 0u);
+      x.tag = mvn_hybrid ? 1u : 0u;  // class 0 only
       x.list_off = uint32_t(aux_ids.size());
       aux_ids.insert(aux_ids.end(), w.begin(), w.end());
       has_filters = true;
     }
     rows.push_back(r);
     aux.push_back(x);
-    return true;
+    if (!mvn_hybrid) return true;
   }
   if (P.drv == DRV_LIBRARY) {
     // compare.IsVulnerable as disjoint intervals per version class (libdb.h); classes
     // sharing an interval share its row; a row that holds for a subset of the classes
     // carries an AUX_CLASS filter.
-    const LibRows lr = lib_compile_advisory(P.cmp, a.vulnerable, a.patched, a.unaffected);
-    if (lr.always) {
+    LibRows lr = lib_compile_advisory(P.cmp, a.vulnerable, a.patched, a.unaffected);
+    if (mvn_hybrid) lr.cls[0].clear();  // class 0 has the program row
+    if (lr.always && !mvn_hybrid) {
       Row r{};
       r.adv = ai | ROW_ALWAYS;
       r.lo_len = r.hi_len = KEY_INF;
@@ -598,7 +606,7 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
       rows.push_back(r);
       aux.push_back(x);
     }
-    return !ivs.empty();
+    return mvn_hybrid || !ivs.empty();
   }
   Row r{};
   r.adv = ai;

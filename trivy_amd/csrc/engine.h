@@ -112,6 +112,37 @@ struct DevMatches {
 };
 enum : uint32_t { ERR_SPILL = 1, ERR_TILES = 2 };
 
+// The end-to-end pipeline's result move for one chunk (packages [p0, p1)): the chunk's
+// per-package advisory lists (device CSR from order_kernel) into the pinned host result
+// through 16-byte kernel stores (kernel stores into host memory: 55 GB/s; a DMA
+// device-to-host copy: 28.6 GB/s; profiles/r03/pcie_probe.txt).  The chunk's advisory range
+// is read from the device row ends, so the host never waits per chunk.  Run by extra
+// workgroups of the next chunk's match launch (Engine::launch_tiles), so the link writes
+// overlap that chunk's matching, or by copy_out_kernel for the last chunk.
+struct CopyOutArgs {
+  const uint32_t* row_end = nullptr;  // device CSR
+  const uint32_t* csr_adv = nullptr;
+  uint4* row_end_h = nullptr;         // device addresses of the pinned host result (16-B aligned, padded)
+  uint4* adv_h = nullptr;
+  uint32_t p0 = 0, p1 = 0;            // p0 a multiple of 4, p1 > p0
+  uint64_t cap = 0;                   // advisory capacity (an overflowed pass's range is cut to it)
+};
+
+// Whole 16-byte units are moved: the words before the chunk's range are the previous chunk's
+// (final) and those after it are rewritten by the next chunk's move, which runs later.
+__device__ __forceinline__ void copy_out_range(const CopyOutArgs& a, uint64_t tid, uint64_t stride) {
+  const uint64_t s0 = a.p0 ? a.row_end[a.p0 - 1] : 0, e0 = a.row_end[a.p1 - 1];
+  const uint64_t e = e0 < a.cap ? e0 : a.cap, s = s0 < e ? s0 : e;
+  const uint64_t u0 = s / 4, nu = (e + 3) / 4 - u0;                    // advisory units
+  const uint64_t r0 = a.p0 / 4, nr = (uint64_t(a.p1) + 3) / 4 - r0;    // row-end units
+  const uint4* csr = reinterpret_cast<const uint4*>(a.csr_adv);
+  const uint4* re = reinterpret_cast<const uint4*>(a.row_end);
+  for (uint64_t i = tid; i < nu + nr; i += stride) {
+    if (i < nu) a.adv_h[u0 + i] = csr[u0 + i];
+    else a.row_end_h[r0 + (i - nu)] = re[r0 + (i - nu)];
+  }
+}
+
 class Engine {
  public:
   ~Engine();
@@ -136,8 +167,10 @@ class Engine {
   bool launch(const DevBatch& b, const DevMatches& m, hipStream_t stream, std::string& err);
   // The pass over tiles [t_begin, t_end) only: probe on `probe_st`, sweep on `sweep_st`
   // behind event `ev` (the caller zeroes m.ctl once before the first chunk).
+  // co: a previous chunk's result move, run by extra workgroups of this launch (fused
+  // variants) or by its own kernel ahead of it (split variants).
   bool launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_begin, uint32_t t_end, hipStream_t probe_st,
-                    hipStream_t sweep_st, hipEvent_t ev, std::string& err);
+                    hipStream_t sweep_st, hipEvent_t ev, std::string& err, const CopyOutArgs* co = nullptr);
 
   // After the pass: the match list as {package, advisory} pairs in (package, advisory) order.
   static bool fetch_ordered(const DevMatches& m, uint32_t n_pkgs, uint64_t total, std::vector<uint2>& out,

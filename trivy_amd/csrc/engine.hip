@@ -14,6 +14,7 @@
 #include "db.h"
 #include "match_kernel.h"
 #include "match_variants.h"
+#include "pipeline.h"
 
 namespace tvm {
 
@@ -342,7 +343,7 @@ bool Engine::fetch_ordered(const DevMatches& m, uint32_t n_pkgs, uint64_t total,
 }
 
 bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_begin, uint32_t t_end, hipStream_t pst,
-                          hipStream_t sst, hipEvent_t ev, std::string& err) {
+                          hipStream_t sst, hipEvent_t ev, std::string& err, const CopyOutArgs* co) {
   (void)hipSetDevice(dev_);
   if (t_end > b.n_tiles) t_end = b.n_tiles;
   if (t_begin >= t_end) return true;
@@ -374,6 +375,7 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
   pa.spill_cap = b.spill_cap;
   const bool fused = kFusedVariant[vi - 1];
   if (!fused) {
+    if (co) launch_copy_out(pst, *co);
     probe_fn(b.gm)(nt, pst, pa);
     if (!hip_ok(hipGetLastError(), "probe kernel launch", err)) return false;
     if (sst != pst && (!hip_ok(hipEventRecord(ev, pst), "hipEventRecord", err) ||
@@ -404,6 +406,10 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
     FusedArgs fa;
     fa.pa = pa;
     fa.sa = sa;
+    if (co) {
+      fa.co = *co;
+      fa.n_copy = kCopyWorkgroups;
+    }
     fused_fn(b.gm, vi)(nt, pst, fa);
     return hip_ok(hipGetLastError(), "match kernel launch", err);
   }

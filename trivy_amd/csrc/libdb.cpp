@@ -945,6 +945,7 @@ int lib_classes(uint8_t cmp) {
   switch (cmp) {
     case CMP_NPM: return 2;
     case CMP_PEP440: return 8;
+    case CMP_MAVEN: return 2;  // 1 = numeric (libver.h mvn_numeric)
     default: return 1;
   }
 }
@@ -974,7 +975,7 @@ LibRows lib_compile_advisory(uint8_t cmp, const std::vector<std::string>& vulner
   for (const auto* l : {&vulnerable, &patched})
     for (const std::string& v : *l)
       if (v.empty()) {
-        r.always = true;
+        r.ok = r.always = true;
         return r;
       }
   auto join = [](const std::vector<std::string>& a, const std::vector<std::string>& b) {
@@ -992,11 +993,13 @@ LibRows lib_compile_advisory(uint8_t cmp, const std::vector<std::string>& vulner
   if (!vulnerable.empty() && !lib_compile_constraint(cmp, join(vulnerable, {}), m)) return r;
   if (patched.empty() && unaffected.empty()) {
     if (!vulnerable.empty()) r.cls = m;
+    r.ok = true;
     return r;
   }
   VS sec;
   if (!lib_compile_constraint(cmp, join(patched, unaffected), sec)) return r;
   r.cls = vs_and(m, vs_not(sec));
+  r.ok = true;
   return r;
 }
 
@@ -1060,6 +1063,19 @@ MvnProgState mvn_program(const std::vector<std::string>& vulnerable, const std::
     words.insert(words.end(), packed.begin(), packed.end());
   }
   return MVN_PROGRAM;
+}
+
+bool mvn_bounds_numeric(const std::vector<std::string>& vulnerable, const std::vector<std::string>& patched,
+                        const std::vector<std::string>& unaffected) {
+  for (const auto* l : {&vulnerable, &patched, &unaffected})
+    for (const std::string& c : *l) {
+      MvnGroups g;
+      if (!mvn_groups(c, g)) return false;
+      for (const auto& alt : g)
+        for (const auto& [op, txt] : alt)
+          if (!mvn_numeric(U(txt), uint32_t(txt.size()))) return false;
+    }
+  return true;
 }
 
 int mvn_is_vulnerable(const std::vector<std::string>& vulnerable, const std::vector<std::string>& patched,

@@ -28,6 +28,7 @@ using KSet = std::vector<KInterval>;  // sorted, disjoint, non-empty intervals
 // A compiled advisory: either "always" (an empty constraint string: reported even for an
 // unparsable installed version, compare.go:23-28) or per-class interval sets.
 struct LibRows {
+  bool ok = false;      // the constraints compiled (false: cls holds nothing)
   bool always = false;
   int ncls = 1;
   std::vector<KSet> cls;  // ncls entries
@@ -36,6 +37,10 @@ struct LibRows {
 // Maven advisories as IsVulnerable programs (libver.h mvn_program_eval): ALWAYS (an empty
 // constraint string), NEVER (unparsable / nothing to match) or a program in `words`.
 enum MvnProgState { MVN_NEVER = 0, MVN_ALWAYS = 1, MVN_PROGRAM = 2 };
+// Every bound text of the advisory's constraints is numeric (libver.h mvn_numeric): the
+// advisory then also compiles to key-order intervals, exact for numeric installed versions.
+bool mvn_bounds_numeric(const std::vector<std::string>& vulnerable, const std::vector<std::string>& patched,
+                        const std::vector<std::string>& unaffected);
 MvnProgState mvn_program(const std::vector<std::string>& vulnerable, const std::vector<std::string>& patched,
                          const std::vector<std::string>& unaffected, std::vector<uint32_t>& words);
 // compare.IsVulnerable for the Maven grammar, pairwise (host): 1 / 0.

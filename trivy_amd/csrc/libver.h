@@ -682,6 +682,28 @@ TVM_HD void mvn_emit(const uint8_t* s, const MvnParse& P, Sink& o) {
   for (int d = 0; d <= depth; d++) o.put(0x30);
 }
 
+// Maven version class 1 ("numeric"): digit runs of 1..9 digits joined by single dots
+// ("1.2.3").  ComparableVersion parses such a text into a flat list of int items, and two
+// such lists compare as their zero-padded integer sequences - a total order, which the sort
+// key reproduces exactly.  Every other text is class 0 and is compared through the
+// pairwise program: the hybrid of db.cpp DB::compile_rows.
+TVM_HD bool mvn_numeric(const uint8_t* s, uint32_t n) {
+  if (n == 0) return false;
+  uint32_t run = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const uint8_t c = s[i];
+    if (c >= '0' && c <= '9') {
+      if (++run > 9) return false;
+    } else if (c == '.') {
+      if (run == 0) return false;
+      run = 0;
+    } else {
+      return false;
+    }
+  }
+  return run > 0;
+}
+
 template <class Sink>
 TVM_HD bool mvn_encode(const uint8_t* s, uint32_t n, Sink& o) {
   MvnParse P;
@@ -987,7 +1009,9 @@ TVM_HD bool encode_version_cls(uint8_t cmp, const uint8_t* s, uint32_t n, Sink& 
     case CMP_BITNAMI: return gen_encode(s, n, true, o);
     case CMP_NPM: return npm_encode(s, n, o, cls);
     case CMP_PEP440: return pep_encode(s, n, o, cls);
-    case CMP_MAVEN: return mvn_encode(s, n, o);
+    case CMP_MAVEN:
+      cls = mvn_numeric(s, n) ? 1u : 0u;
+      return mvn_encode(s, n, o);
     case CMP_GEM: return gem_encode(s, n, o);
     default: return encode_version(cmp, s, n, o);
   }

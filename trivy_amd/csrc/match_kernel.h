@@ -85,7 +85,10 @@ struct SweepArgs {
 struct FusedArgs {
   ProbeArgs pa;
   SweepArgs sa;
+  CopyOutArgs co;       // end-to-end pipeline: the previous chunk's result move ...
+  uint32_t n_copy = 0;  // ... by workgroups [0, n_copy) of this launch (0: none)
 };
+constexpr uint32_t kCopyWorkgroups = 128;  // PCIe-bound: a few workgroups, the tiles keep the rest
 
 using ProbeFn = void (*)(uint32_t n_tiles, hipStream_t st, const ProbeArgs& a);
 using SweepFn = void (*)(uint32_t n_tiles, hipStream_t st, const SweepArgs& a);
@@ -395,6 +398,9 @@ template <int FILT>
 __device__ __forceinline__ bool aux_pass(const SweepArgs& a, uint32_t ridx, uint2 pa, uint32_t ki, uint32_t p) {
   const RowAux x = a.db.aux[ridx];
   const uint32_t* ids = a.db.aux_ids + x.list_off;
+  // the class first: a Maven hybrid program row is rejected for numeric versions before its
+  // program would run
+  if ((x.kind & AUX_CLASS) && !((x.tag >> ((ki >> KI_CLS_SHIFT) & KI_CLS_MASK)) & 1u)) return false;
   if (FILT >= 2 && (x.kind & AUX_MVN)) {  // the installed parse packed by probe_one, the program's packed bounds
     const uint4 t = a.tail[p];
     const MvnPackedView V{reinterpret_cast<const uint32_t*>(a.spill + t.x), int(t.y & 0xFFFFu),
@@ -418,7 +424,6 @@ __device__ __forceinline__ bool aux_pass(const SweepArgs& a, uint32_t ridx, uint
     if (!ok) return false;
   }
   if ((x.kind & AUX_TAG) && x.tag != pa.y) return false;
-  if ((x.kind & AUX_CLASS) && !((x.tag >> ((ki >> KI_CLS_SHIFT) & KI_CLS_MASK)) & 1u)) return false;
   return true;
 }
 
@@ -695,7 +700,11 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
   SweepShared<FILT>& s = u.sw.s;
   uint8_t* map = u.sw.map;
   const ProbeArgs& a = fa.pa;
-  const uint32_t tid = threadIdx.x, t = blockIdx.x;
+  if (blockIdx.x < fa.n_copy) {  // pipeline: the previous chunk's result move, dispatched first so the link writes overlap the tiles
+    copy_out_range(fa.co, uint64_t(blockIdx.x) * kTile + threadIdx.x, uint64_t(fa.n_copy) * kTile);
+    return;
+  }
+  const uint32_t tid = threadIdx.x, t = blockIdx.x - fa.n_copy;
   const uint32_t p = t * kTile + tid;
   uint2 d = make_uint2(0xFFFFFFFFu, 0);
   if (p < a.n) d = a.pk[p];
@@ -739,7 +748,7 @@ void launch_sweep(uint32_t n_tiles, hipStream_t st, const SweepArgs& a) {
 
 template <uint32_t GM, int K, int MB, int FILT, int DIAG = 0, int WPE = 1>
 void launch_fused(uint32_t n_tiles, hipStream_t st, const FusedArgs& a) {
-  hipLaunchKernelGGL((fused_kernel<GM, K, MB, FILT, DIAG, WPE>), dim3(n_tiles), dim3(kTile), 0, st, a);
+  hipLaunchKernelGGL((fused_kernel<GM, K, MB, FILT, DIAG, WPE>), dim3(n_tiles + a.n_copy), dim3(kTile), 0, st, a);
 }
 
 }  // namespace

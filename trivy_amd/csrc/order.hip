@@ -84,26 +84,8 @@ __global__ __launch_bounds__(kTile) void order_kernel(OrderArgs a) {
   if (p < a.n) a.row_end[p] = uint32_t(b + off + x);
 }
 
-// One pipeline chunk's result (packages [p0, p1)) from the device CSR into the pinned host
-// result: 16-byte stores per lane, grid-stride (kernel stores reach 55 GB/s into host memory
-// where a DMA device-to-host copy reaches 28.6, profiles/r03/pcie_probe.txt).  The chunk's
-// advisory range comes from the device row ends, so the host never waits per chunk.  Whole
-// 16-byte units are copied: the words before the range are the previous chunk's (final) and
-// those after it are rewritten by the next chunk's copy, which runs later on the same stream.
 __global__ __launch_bounds__(256) void copy_out_kernel(CopyOutArgs a) {
-  // an overflowed pass (matches > cap) has row ends past the buffers: the range is clamped
-  // to the capacity (the host sees the total and prepares again)
-  const uint64_t s0 = a.p0 ? a.row_end[a.p0 - 1] : 0, e0 = a.row_end[a.p1 - 1];
-  const uint64_t e = e0 < a.cap ? e0 : a.cap, s = s0 < e ? s0 : e;
-  const uint64_t u0 = s / 4, nu = (e + 3) / 4 - u0;  // csr units (4 advisories each)
-  const uint64_t r0 = a.p0 / 4, nr = (uint64_t(a.p1) + 3) / 4 - r0;  // row-end units
-  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-  const uint4* csr = reinterpret_cast<const uint4*>(a.csr_adv);
-  const uint4* re = reinterpret_cast<const uint4*>(a.row_end);
-  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nu + nr; i += stride) {
-    if (i < nu) a.adv_h[u0 + i] = csr[u0 + i];
-    else a.row_end_h[r0 + (i - nu)] = re[r0 + (i - nu)];
-  }
+  copy_out_range(a, uint64_t(blockIdx.x) * blockDim.x + threadIdx.x, uint64_t(gridDim.x) * blockDim.x);
 }
 
 }  // namespace
@@ -113,7 +95,8 @@ void launch_order(uint32_t n_tiles, hipStream_t st, const OrderArgs& a) {
 }
 
 void launch_copy_out(hipStream_t st, const CopyOutArgs& a) {
-  hipLaunchKernelGGL(copy_out_kernel, dim3(128), dim3(256), 0, st, a);  // PCIe-bound: few workgroups, the match kernels keep the CUs
+  hipLaunchKernelGGL(copy_out_kernel, dim3(256), dim3(256), 0, st, a);
 }
+
 
 }  // namespace tvm

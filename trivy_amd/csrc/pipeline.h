@@ -1,5 +1,5 @@
 // End-to-end pipelined match pass: a host batch (pinned) in, the per-package advisory lists
-// (CSR, pinned) out, with the PCIe copies overlapping the kernels.
+// (CSR, pinned) out, with the link transfers overlapping the kernels.
 #pragma once
 #include <string>
 #include <vector>
@@ -22,28 +22,21 @@ struct OrderArgs {
   uint32_t pkg_base = 0;       // added to every package index the match kernels wrote (a shard's first package)
 };
 void launch_order(uint32_t n_tiles, hipStream_t st, const OrderArgs& a);
+void launch_copy_out(hipStream_t st, const CopyOutArgs& a);  // engine.h copy_out_range as its own kernel
 
-struct CopyOutArgs {
-  const uint32_t* row_end;  // device CSR (order_kernel)
-  const uint32_t* csr_adv;
-  uint4* row_end_h;         // device addresses of the pinned host result (16-B aligned, padded)
-  uint4* adv_h;
-  uint32_t p0, p1;          // the chunk's packages, p0 a multiple of kTile, p1 > p0
-  uint64_t cap;             // advisory capacity (a range beyond it is cut)
-};
-void launch_copy_out(hipStream_t st, const CopyOutArgs& a);
 
 // One batch's pipeline state.  prepare() pins the batch's host arrays (hipHostRegister),
 // sizes the device batch, the match buffers and the pinned result buffers; run() then
 // streams the batch through in chunks of whole tiles:
 //   copy stream    DMA of chunk c to HBM (package words, tile offsets, string bytes, attributes);
-//   kernel stream  (after chunk c's copy) the match kernels + order_kernel over chunk c
-//                  (per-package advisory lists, CSR, in HBM);
-//   result stream  (after chunk c's order kernel) copy_out_kernel, whose 16-byte stores put
-//                  the chunk's advisory indices and row ends straight into the pinned host
-//                  result (zero-copy: the link's other direction, no DMA, and the chunk's
-//                  range is read on the device, so the host never waits per chunk);
-// so chunk c+1's upload and chunk c-1's result writes run under chunk c's kernels.
+//   kernel stream  (after chunk c's upload) one match launch whose first workgroups move chunk
+//                  c-1's result into the pinned host result (engine.h CopyOutArgs: 16-byte
+//                  kernel stores, the link's other direction, range read on the device) while
+//                  the rest match chunk c; then order_kernel over chunk c (CSR in HBM);
+// so chunk c+1's upload and chunk c-1's result move run under chunk c's matching, and the
+// host waits once, at the end.  (Measured alternatives, DESIGN.md §7: a DMA device-to-host
+// copy runs at half the rate of kernel stores, and a result kernel on its own stream did
+// not overlap the match kernels on this runtime.)
 class Pipeline {
  public:
   ~Pipeline();
@@ -61,8 +54,8 @@ class Pipeline {
  private:
   void release();
   int dev_ = -1;
-  hipStream_t s_h2d_ = nullptr, s_k_ = nullptr, s_o_ = nullptr;
-  std::vector<hipEvent_t> ev_h_, ev_k_;
+  hipStream_t s_h2d_ = nullptr, s_k_ = nullptr;
+  std::vector<hipEvent_t> ev_h_;
   std::vector<uint32_t> bounds_;     // chunk c = tiles [bounds_[c], bounds_[c + 1])
   std::vector<uint64_t> toff_;       // tile offsets + the arena end (registered)
   std::vector<void*> registered_;
@@ -74,7 +67,7 @@ class Pipeline {
   uint32_t* row_end_h_ = nullptr;
   uint32_t* csr_adv_d_ = nullptr;   // device CSR (order_kernel)
   uint32_t* row_end_d_ = nullptr;
-  uint32_t* adv_hd_ = nullptr;      // device addresses of adv_h_ / row_end_h_ (copy_out_kernel stores)
+  uint32_t* adv_hd_ = nullptr;      // device addresses of adv_h_ / row_end_h_ (result-move stores)
   uint32_t* row_end_hd_ = nullptr;
   unsigned long long* ctl_h_ = nullptr;
   uint64_t cap_ = 0, h2d_ = 0, d2h_ = 0;

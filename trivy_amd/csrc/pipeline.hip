@@ -24,7 +24,6 @@ void Pipeline::release() {
   if (dev_ < 0) return;
   (void)hipSetDevice(dev_);
   if (s_k_) (void)hipStreamSynchronize(s_k_);
-  if (s_o_) (void)hipStreamSynchronize(s_o_);
   if (s_h2d_) (void)hipStreamSynchronize(s_h2d_);
   Engine::free_batch(dev_, db_);
   Engine::free_matches(dev_, m_);
@@ -35,13 +34,11 @@ void Pipeline::release() {
     if (p) (void)hipHostFree(p);
   for (void* p : registered_) (void)hipHostUnregister(p);
   registered_.clear();
-  for (auto* v : {&ev_h_, &ev_k_}) {
-    for (hipEvent_t e : *v) (void)hipEventDestroy(e);
-    v->clear();
-  }
-  for (hipStream_t s : {s_h2d_, s_k_, s_o_})
+  for (hipEvent_t e : ev_h_) (void)hipEventDestroy(e);
+  ev_h_.clear();
+  for (hipStream_t s : {s_h2d_, s_k_})
     if (s) (void)hipStreamDestroy(s);
-  s_h2d_ = s_k_ = s_o_ = nullptr;
+  s_h2d_ = s_k_ = nullptr;
   adv_hd_ = row_end_hd_ = nullptr;
   csr_adv_d_ = row_end_d_ = nullptr;
   status_d_ = tickets_d_ = nullptr;
@@ -71,14 +68,11 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
     err = "pipeline: row ends are 32-bit; split the batch below 2^32 matches";
     return false;
   }
-  for (auto* v : {&ev_h_, &ev_k_}) {
-    v->resize(nc);
-    for (hipEvent_t& e : *v)
-      if (!ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate", err)) return false;
-  }
+  ev_h_.resize(nc);
+  for (hipEvent_t& e : ev_h_)
+    if (!ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate", err)) return false;
   if (!ok(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking), "hipStreamCreate", err) ||
-      !ok(hipStreamCreateWithFlags(&s_k_, hipStreamNonBlocking), "hipStreamCreate", err) ||
-      !ok(hipStreamCreateWithFlags(&s_o_, hipStreamNonBlocking), "hipStreamCreate", err))
+      !ok(hipStreamCreateWithFlags(&s_k_, hipStreamNonBlocking), "hipStreamCreate", err))
     return false;
   // pin the caller's host arrays in place: the copies are DMA from them, no staging memcpy
   auto reg = [&](const void* p, size_t bytes) {
@@ -101,7 +95,7 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
     db_.n_cpe_sets = uint32_t(hb.cpe_bits.size() / hb.cpe_words);
   }
   const size_t n = std::max<size_t>(hb.pk.size(), 1);
-  // CSR buffers padded to whole 16-byte units (copy_out_kernel moves units)
+  // CSR buffers padded to whole 16-byte units (the result move copies units)
   const size_t cap4 = (cap_ + 3) & ~size_t(3), n4 = (size_t(n_tiles) * kTile + 3) & ~size_t(3);
   void* p = nullptr;
   if (!ok(hipMalloc(&p, cap4 * 4), "hipMalloc(csr)", err)) return false;
@@ -112,7 +106,7 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
   status_d_ = static_cast<unsigned long long*>(p);
   if (!ok(hipMalloc(&p, std::max<size_t>(nc, 1) * 8), "hipMalloc(tickets)", err)) return false;
   tickets_d_ = static_cast<unsigned long long*>(p);
-  // the result lives in pinned host memory that the order kernel writes directly over PCIe
+  // the result lives in pinned host memory that the result move writes directly over PCIe
   // (measured, profiles/r03/pcie_probe.txt: kernel stores to host memory 55 GB/s, a DMA
   // device-to-host copy 28.6 GB/s; the DMA engine then only carries the batch upward)
   if (!ok(hipHostMalloc(&p, cap4 * 4, hipHostMallocDefault), "hipHostMalloc(adv)", err)) return false;
@@ -146,15 +140,25 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
       !ok(hipMemsetAsync(status_d_, 0, std::max<size_t>(db_.n_tiles, 1) * 8, s_k_), "memset(status)", err) ||
       !ok(hipMemsetAsync(tickets_d_, 0, std::max<size_t>(nc, 1) * 8, s_k_), "memset(tickets)", err))
     return false;
-  // Per chunk: its upload on the copy stream (DMA from the pinned host arrays); behind it
-  // the match kernels + the order kernel (device CSR) on the kernel stream; behind those, on
-  // the result stream, copy_out_kernel, which stores the chunk's lists straight into the
-  // pinned host result.  Chunks are issued in order, upload first, so chunk c's kernels and
-  // result writes are queued before chunk c+1's upload is (the runtime may block the host
-  // in a copy call until the copy ran: measured, profiles/r03/e2e_timeline_*.txt); the host
-  // waits once, at the end.
+  // Per chunk: its upload on the copy stream; behind it, on the kernel stream, one match
+  // launch whose first workgroups move the previous chunk's result out, then the order
+  // kernel.  All work is queued up front (measured: the calls never block); the host waits
+  // once, at the end.
+  auto copy_args = [&](uint32_t c) {
+    CopyOutArgs ca;
+    ca.row_end = row_end_d_;
+    ca.csr_adv = csr_adv_d_;
+    ca.row_end_h = reinterpret_cast<uint4*>(row_end_hd_);
+    ca.adv_h = reinterpret_cast<uint4*>(adv_hd_);
+    ca.p0 = bounds_[c] * kTile;
+    ca.p1 = std::min<uint32_t>(bounds_[c + 1] * kTile, n);
+    ca.cap = cap_;
+    return ca;
+  };
+  int64_t prev = -1;  // the last chunk matched, whose result has not been moved yet
   for (uint32_t c = 0; c < nc; c++) {
     const uint32_t t0 = bounds_[c], t1 = bounds_[c + 1];
+    if (t1 == t0) continue;
     const size_t p0 = size_t(t0) * kTile, p1 = std::min<size_t>(size_t(t1) * kTile, n);
     const size_t g0 = size_t(t0) * kGroupsPerTile, g1 = size_t(t1) * kGroupsPerTile;
     const uint64_t a0 = toff_[g0], a1 = toff_[g1];
@@ -167,13 +171,12 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
         (!hb.attr.empty() &&
          !ok(hipMemcpyAsync(db_.attr + p0, hb.attr.data() + p0, (p1 - p0) * sizeof(uint2), hipMemcpyHostToDevice, s_h2d_),
              "H2D attributes", err)) ||
-        !ok(hipEventRecord(ev_h_[c], s_h2d_), "hipEventRecord", err))
+        !ok(hipEventRecord(ev_h_[c], s_h2d_), "hipEventRecord", err) ||
+        !ok(hipStreamWaitEvent(s_k_, ev_h_[c], 0), "hipStreamWaitEvent", err))
       return false;
     h2d_ += (p1 - p0) * sizeof(uint2) + (g1 - g0 + 1) * 8 + (a1 - a0) + (hb.attr.empty() ? 0 : (p1 - p0) * sizeof(uint2));
-    if (t1 == t0) continue;
-    if (!ok(hipStreamWaitEvent(s_k_, ev_h_[c], 0), "hipStreamWaitEvent", err) ||
-        !eng.launch_tiles(db_, m_, t0, t1, s_k_, s_k_, nullptr, err))
-      return false;
+    const CopyOutArgs prev_co = prev >= 0 ? copy_args(uint32_t(prev)) : CopyOutArgs{};
+    if (!eng.launch_tiles(db_, m_, t0, t1, s_k_, s_k_, nullptr, err, prev >= 0 ? &prev_co : nullptr)) return false;
     OrderArgs oa;
     oa.dir = m_.dir;
     oa.pkg = m_.pkg;
@@ -187,23 +190,15 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
     oa.n = n;
     oa.pkg_base = db_.pkg_base;
     launch_order(t1 - t0, s_k_, oa);
-    if (!ok(hipGetLastError(), "order kernel launch", err) || !ok(hipEventRecord(ev_k_[c], s_k_), "hipEventRecord", err) ||
-        !ok(hipStreamWaitEvent(s_o_, ev_k_[c], 0), "hipStreamWaitEvent", err))
-      return false;
-    CopyOutArgs ca;
-    ca.row_end = row_end_d_;
-    ca.csr_adv = csr_adv_d_;
-    ca.row_end_h = reinterpret_cast<uint4*>(row_end_hd_);
-    ca.adv_h = reinterpret_cast<uint4*>(adv_hd_);
-    ca.p0 = t0 * kTile;
-    ca.p1 = std::min<uint32_t>(t1 * kTile, n);
-    ca.cap = cap_;
-    launch_copy_out(s_o_, ca);
+    if (!ok(hipGetLastError(), "order kernel launch", err)) return false;
+    prev = c;
+  }
+  if (prev >= 0) {
+    launch_copy_out(s_k_, copy_args(uint32_t(prev)));
     if (!ok(hipGetLastError(), "copy-out kernel launch", err)) return false;
   }
-  if (!ok(hipStreamSynchronize(s_k_), "pipeline kernels", err) ||
-      !ok(hipMemcpyAsync(ctl_h_, m_.ctl, 64, hipMemcpyDeviceToHost, s_k_), "D2H ctl", err) ||
-      !ok(hipStreamSynchronize(s_k_), "D2H ctl", err) || !ok(hipStreamSynchronize(s_o_), "pipeline results", err))
+  if (!ok(hipMemcpyAsync(ctl_h_, m_.ctl, 64, hipMemcpyDeviceToHost, s_k_), "D2H ctl", err) ||
+      !ok(hipStreamSynchronize(s_k_), "pipeline", err))
     return false;
   d2h_ = uint64_t(n) * 4 + std::min<uint64_t>(ctl_h_[0], cap_) * 4;
   total = ctl_h_[0];
