@@ -109,20 +109,26 @@ class C2:
         n = min(self.n, 500_000)
         sub = SynthBatch(batch.plat[:n], batch.names[:n], batch.versions[:n], [])
         prep = om.Prepared(self.sdb, sub)
-        done, dt, t = 0, 0.0, time.perf_counter()
-        while dt < budget_s:  # whole passes over the sample until the budget is spent
-            om.match(prep, n_threads=threads)
-            done += n
-            dt = time.perf_counter() - t
-        return {"value": done / dt, "unit": "packages/s", "cores": threads, "kind": "port",
-                "sample": f"{done // n} passes over the first {n} packages of the same batch, oracle/match.c "
-                          f"orc_match with {threads} threads (this host's CPU share), {dt:.1f}s"}
+        rates = {}
+        for t in sorted({1, threads}):
+            done, dt, t0 = 0, 0.0, time.perf_counter()
+            while dt < budget_s / 2:  # whole passes over the sample until half the budget is spent
+                om.match(prep, n_threads=t)
+                done += n
+                dt = time.perf_counter() - t0
+            rates[t] = done / dt
+        return {"value": rates[threads], "unit": "packages/s", "cores": threads, "kind": "port",
+                "value_1thread": rates[1], "cpu_model": cpu_model(),
+                "sample": f"passes over the first {n} packages of the same batch, oracle/match.c orc_match (C, "
+                          f"pthreads) with {threads} threads (this host's CPU share) and with 1 thread, "
+                          f"~{budget_s / 2:.0f}s each"}
 
 
 class Mix:
     """C3 (language packages), C5 (rpm + apk) and C4 (mixed OS + language) batches of
     tools/synth_mix.py; a group (one platform's packages) is cut into targets of
-    `per_target` packages.  CPU baseline: the Python oracle drivers on a bounded sample."""
+    `per_target` packages.  CPU baseline: the C port of the driver loops (oracle/mixmatch.c) on a
+    bounded sample batch, at 1 and N threads."""
 
     per_target = 400
 
@@ -194,62 +200,41 @@ class Mix:
             self.sm.add_slice(mb, self.sdb, p, g, lo, hi)
 
     def cpu_baseline(self, budget_s, threads):
-        """The oracle drivers (Python) in `threads` worker processes, each over its own seeded
-        sample batch of the same DB and generator; processes are spawned (fresh
-        interpreters: nothing GPU-side is inherited) and time only their detection loops."""
-        import multiprocessing as mp
-        from concurrent.futures import ProcessPoolExecutor
-        with ProcessPoolExecutor(threads, mp_context=mp.get_context("spawn")) as ex:
-            res = list(ex.map(_mix_cpu_worker, [(self.which, self.kpp, 1000 + w, budget_s) for w in range(threads)]))
-        done = sum(r[0] for r in res)
-        rate = sum(r[0] / r[1] for r in res)
-        return {"value": rate, "unit": "packages/s", "cores": threads, "kind": "port",
-                "sample": f"{done} packages over {threads} processes (each: a seeded 20k-package sample batch of "
-                          f"the same DB, first rows of every platform group), oracle/drivers.py + oracle/library.py "
-                          f"per-driver Detect, ~{budget_s:.0f}s per process (Python)"}
+        """The native C port of the driver loops (oracle/mixmatch.c + oracle/libcmp.c, pinned by
+        tests/test_cport.py to oracle/drivers.py + oracle/library.py and the reference's
+        compare_test.go tables) over a bounded sample batch of the same DB and generator, at
+        1 thread and at `threads` threads.  The advisories of the sample's keys are decoded once
+        beforehand (oracle/mix_c.py), which makes this a conservative - fast - baseline: the
+        reference decodes them per call."""
+        from oracle import mix_c
+        n = {"c3": 200_000, "c4": 200_000, "c5": 200_000}[self.which]
+        sb = self.sm.make_mix_batch(self.sdb, n, {"c3": self.sm.C3_WEIGHTS, "c4": self.sm.C4_WEIGHTS,
+                                                  "c5": self.sm.C5_WEIGHTS}[self.which], seed=1000)
+        prep = mix_c.Prepared(self.sm, self.sdb, [(p, g, list(range(len(g["key"])))) for p, g in sb.groups])
+        rates = {}
+        for t in sorted({1, threads}):
+            done, dt, t0 = 0, 0.0, time.perf_counter()
+            while dt < budget_s / 2:
+                mix_c.match(prep, n_threads=t)
+                done += prep.n
+                dt = time.perf_counter() - t0
+            rates[t] = done / dt
+        return {"value": rates[threads], "unit": "packages/s", "cores": threads, "kind": "port",
+                "value_1thread": rates[1], "cpu_model": cpu_model(),
+                "sample": f"passes over a seeded {prep.n}-package sample batch of the same DB and generator, "
+                          f"oracle/mixmatch.c orc_mix_match (C, pthreads; advisories decoded once beforehand) with "
+                          f"{threads} threads (this host's CPU share) and with 1 thread, ~{budget_s / 2:.0f}s each"}
 
 
-def _mix_detect_loop(sm, sdb, batch, budget_s):
-    """Packages detected and seconds spent by the oracle drivers over the first rows of every
-    platform group (doubling) until budget_s of detection time is spent."""
-    import oracle.drivers as od
-    import oracle.library as ol
-    per, n_done, dt = 200, 0, 0.0
-    while dt < budget_s:
-        for p, g in batch.groups:
-            bucket, kind = sdb.plats[p]
-            idx = np.arange(min(per, len(g["key"])))
-            pkgs = sm.driver_packages(sdb, p, g, idx)
-            roots = sm.C3_ROOTS.get(kind, [bucket])
-            recs = od.Records(sdb.records_for({r: {x["Name"] for x in pkgs} for r in roots}))
-            t = time.perf_counter()
-            if kind in sm.LANG_OF:
-                ol.detect(recs, sm.LANG_OF[kind], pkgs)
-            elif kind == "redhat":
-                recs = od.Records(sdb.records_for({"Red Hat": {g["name"][i].decode() for i in idx},
-                                                   "Red Hat CPE": {"repository", "nvr", "cpe"}}))
-                t = time.perf_counter()
-                for rel in (7, 8, 9):
-                    od.driver_detect("redhat", str(rel), None,
-                                     [pk for pk, i in zip(pkgs, idx) if int(g["rhrel"][i]) == rel], recs, None)
-            else:
-                fam, fmt = sm.DRIVER_OF[kind]
-                od.driver_detect(fam, fmt.format(bucket.split(" ")[-1]), None, pkgs, recs, None)
-            dt += time.perf_counter() - t
-            n_done += len(idx)
-        per *= 2
-    return n_done, dt
-
-
-def _mix_cpu_worker(job):
-    which, kpp, seed, budget_s = job
-    sys.path.insert(0, ROOT)
-    from tools import synth_mix as sm
-    plats, weights = {"c3": (sm.C3_PLATS, sm.C3_WEIGHTS), "c4": (sm.C4_PLATS, sm.C4_WEIGHTS),
-                      "c5": (sm.C5_PLATS, sm.C5_WEIGHTS)}[which]
-    sdb = sm.make_mix_db(plats, kpp)
-    batch = sm.make_mix_batch(sdb, 20000, weights, seed=seed)
-    return _mix_detect_loop(sm, sdb, batch, budget_s)
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def kernel_source_hash():

@@ -70,21 +70,25 @@ class Prepared:
 
 
 def match(prep, n_threads=1, cap=None):
-    """Returns (pkg array, adv array) or raises with the first poisoned package index."""
+    """Returns (pkg array, adv array) or raises with the first poisoned package index.  The
+    output buffers live in prep and are reused (fresh arrays per call cost page faults that
+    serialise the threads); the returned arrays are views into them."""
     L = _lib()
     L.orc_match.restype = ctypes.c_int64
     L.orc_match.argtypes = [ctypes.POINTER(OrcDB), ctypes.POINTER(OrcBatch), ctypes.c_int, _I64, _I64,
                             ctypes.c_int64]
-    cap = cap or max(16, prep.batch.n * 8)
+    out = getattr(prep, "_out", None)
+    if out is None or (cap and len(out[0]) < cap):
+        c = cap or max(16, prep.batch.n * 8)
+        out = prep._out = (np.zeros(c, dtype=np.int64), np.zeros(c, dtype=np.int64))
     while True:
-        pk = np.empty(cap, dtype=np.int64)
-        ad = np.empty(cap, dtype=np.int64)
-        n = L.orc_match(ctypes.byref(prep.db), ctypes.byref(prep.batch), n_threads, _p(pk, _I64), _p(ad, _I64), cap)
+        pk, ad = out
+        n = L.orc_match(ctypes.byref(prep.db), ctypes.byref(prep.batch), n_threads, _p(pk, _I64), _p(ad, _I64), len(pk))
         if n < 0:
             raise PoisonedKey(-1 - n)
-        if n <= cap:
-            return pk[:n], ad[:n]
-        cap = int(n)
+        if n <= len(pk):
+            return pk[:n].copy(), ad[:n].copy()
+        out = prep._out = (np.zeros(int(n), dtype=np.int64), np.zeros(int(n), dtype=np.int64))
 
 
 class PoisonedKey(Exception):

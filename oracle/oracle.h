@@ -99,6 +99,70 @@ typedef struct {
 int64_t orc_match(const orc_db* db, const orc_batch* b, int n_threads,
                   int64_t* out_pkg, int64_t* out_adv, int64_t cap);
 
+/* ---- library comparers (libcmp.c): matchVersion per grammar, 1 / 0, -1 on a parse error -- */
+enum { ORC_LIB_GENERIC = 1, ORC_LIB_NPM = 2, ORC_LIB_PEP440 = 3, ORC_LIB_MAVEN = 4 };
+enum { ORC_LIB_HAS_VULN = 1, ORC_LIB_HAS_SECURE = 2, ORC_LIB_ALWAYS = 4 };
+int orc_lib_match(int grammar, const char* ver, size_t nv, const char* c, size_t nc);
+/* compare.IsVulnerable (compare.go:21-55): vuln / sec = the advisory's Vulnerable /
+ * Patched+Unaffected lists joined with " || " (flags say which lists exist) */
+int orc_lib_is_vulnerable(int grammar, const char* ver, size_t nv, uint32_t flags, const char* vuln, size_t nvu,
+                          const char* sec, size_t nse);
+
+/* ---- mixed-workload driver loops (mixmatch.c): the native CPU baseline of C3 / C4 / C5 ----
+ * Advisories pre-decoded per (platform, lookup name) as "entries" (one per advisory; rocky:
+ * one per arch entry; Red Hat: one per (advisory, entry, CVE)).  Per package the driver of
+ * its platform runs the reference's loop over the key's entries. */
+enum {
+  ORC_MX_DEBIAN = 1, ORC_MX_UBUNTU = 2, ORC_MX_ALPINE = 3, ORC_MX_ALMA = 4, ORC_MX_ROCKY = 5, ORC_MX_ORACLE = 6,
+  ORC_MX_REDHAT = 7, ORC_MX_LIB = 8,
+};
+typedef struct {
+  int32_t n_plat;
+  const int32_t* plat_driver;   /* ORC_MX_* */
+  const int32_t* plat_grammar;  /* ORC_LIB_* for ORC_MX_LIB */
+  int32_t n_keys;
+  const int32_t* key_plat;
+  const char* key_name_arena;
+  const uint64_t* key_name_off;
+  const uint32_t* key_name_len;
+  const int64_t* key_begin;     /* n_keys + 1: the key's entries */
+  /* entries */
+  const char* arena;            /* every entry string */
+  const uint64_t* fixed_off;    /* FixedVersion ("" = unfixed) */
+  const uint32_t* fixed_len;
+  const uint64_t* aff_off;      /* alpine AffectedVersion */
+  const uint32_t* aff_len;
+  const uint64_t* vul_off;      /* library lists (see orc_lib_is_vulnerable) */
+  const uint32_t* vul_len;
+  const uint64_t* sec_off;
+  const uint32_t* sec_len;
+  const uint32_t* lib_flags;
+  const int32_t* vid;           /* vulnerability ID index (Red Hat merge key, parity checks) */
+  const int64_t* ids_begin;     /* n_entries + 1 into ids: n_arch arch ids, then CPE indices */
+  const int32_t* n_arch;
+  const int32_t* ids;
+} orc_mix_db;
+typedef struct {
+  int64_t n;
+  const int32_t* plat;          /* -1: no bucket */
+  const char* name_arena;       /* the driver's lookup name (modular namespace applied) */
+  const uint64_t* name_off;
+  const uint32_t* name_len;
+  const char* ver_arena;        /* the version the driver compares (formatted) */
+  const uint64_t* ver_off;
+  const uint32_t* ver_len;
+  const int32_t* arch;          /* arch id, -1 none; noarch_id = noarch */
+  int32_t noarch_id;
+  const uint8_t* skip;          /* 1: the driver skips the package */
+  const int64_t* cpe_begin;     /* Red Hat: n + 1 into cpe_ids (the package's CPE set) */
+  const int32_t* cpe_ids;
+} orc_mix_batch;
+/* (package, entry) pairs of every detected vulnerability, per package in the driver's output
+ * order (Red Hat: one per VulnerabilityID after the merge - the entry that decided it).
+ * Returns the count (call again with a larger buffer when > cap). */
+int64_t orc_mix_match(const orc_mix_db* db, const orc_mix_batch* b, int n_threads, int64_t* out_pkg,
+                      int64_t* out_entry, int64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -5,7 +5,7 @@
 
 namespace tvm {
 const FusedFn* fused_table_OS() {
-#define TVM_FUSED_(F, K, MB, NAME) F ? &launch_fused<GM_OS, K, MB, 1, (F >= 10 ? F - 10 : 0), TVM_FUSED_WPE(F)> : nullptr,
+#define TVM_FUSED_(F, K, MB, NAME) fused_entry<GM_OS, 1, F, K, MB>(),
   static const FusedFn t[] = {TVM_MATCH_VARIANTS(TVM_FUSED_)};
 #undef TVM_FUSED_
   return t;

@@ -38,6 +38,7 @@
 #pragma once
 #include "engine.h"
 #include "libver.h"
+#include "match_variants.h"
 
 namespace tvm {
 
@@ -337,6 +338,33 @@ __device__ __forceinline__ void stage_window(uint4* buf, const uint8_t* src8, ui
   if (tid < 2) buf[nv + tid] = make_uint4(0, 0, 0, 0);
 }
 
+// Per-wave staging (fused_kernel SEG bit 1): wave w stages its own 64-package group's window
+// (tile_off[g] .. tile_off[g + 1], at most kStage / 4 bytes) into its quarter of the buffer,
+// with a wave scan of the lengths - no workgroup barrier before the probe.
+__device__ __forceinline__ uint32_t wave_exscan(uint32_t v, uint32_t lane) {
+  uint32_t x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= uint32_t(d)) x += y;
+  }
+  return x - v;
+}
+
+__device__ __forceinline__ void stage_window_wave(uint4* buf, const uint8_t* src8, uint32_t nv, uint32_t lane) {
+  constexpr uint32_t SV = (kStage / 4 / 16 + 63) / 64;
+  const uint4* src = reinterpret_cast<const uint4*>(src8);
+  if (nv) {
+    uint4 v[SV];
+#pragma unroll
+    for (uint32_t k = 0; k < SV; k++) v[k] = src[min(lane + k * 64, nv - 1)];
+#pragma unroll
+    for (uint32_t k = 0; k < SV; k++)
+      if (lane + k * 64 < nv) buf[lane + k * 64] = v[k];
+  }
+  if (lane < 2) buf[nv + lane] = make_uint4(0, 0, 0, 0);
+}
+
 template <uint32_t GM, int DIAG = 0>
 __global__ __launch_bounds__(kTile) void probe_kernel(ProbeArgs a) {
   __shared__ uint4 stage[kStage / 16 + 2];  // +2: the dword reads of a name's last word run past its end
@@ -584,8 +612,60 @@ __device__ __forceinline__ uint32_t sweep(const SweepArgs& a, SweepShared<FILT>&
   return nm;
 }
 
+// SEG form of the sweep: wave w takes the contiguous pairs [s0, s1) of the tile (a quarter,
+// in 64-pair units) in rounds of K x 64 and compacts its matches into its own quarter of the
+// LDS buffer, so no round waits on the other waves (the shared form needs a workgroup
+// barrier per round to place matches across waves); the waves' counts are combined once,
+// after the sweep.  DIRECT: the wave's re-sweep straight to the output (base = its offset).
+template <int K, int MBW, int FILT, bool DIRECT>
+__device__ __forceinline__ uint32_t sweep_seg(const SweepArgs& a, const SweepShared<FILT>& s, uint32_t* madv,
+                                              uint8_t* mq, const uint8_t* map, uint32_t nnz, uint32_t total,
+                                              uint32_t s0, uint32_t s1, uint32_t lane, unsigned long long base) {
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  const uint32_t pbase = s.tile * kTile;
+  const bool use_map = total <= kMapCap;
+  uint32_t nm = 0;
+  for (uint32_t b0 = s0; b0 < s1; b0 += 64 * K) {
+    Row row[K];
+    uint32_t qq[K], rid[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint32_t j = min(b0 + k * 64 + lane, s1 - 1);
+      rid[k] = use_map ? uint32_t(map[j]) : pair_rank(s, nnz, j);
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint32_t r = rid[k];
+      qq[k] = s.nz_q[r];
+      rid[k] = min(b0 + k * 64 + lane, s1 - 1) + s.nz_rd[r];
+    }
+#pragma unroll
+    for (int k = 0; k < K; k++) row[k] = a.db.rows[rid[k]];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const bool m = eval_row<FILT>(a, s, qq[k], pbase + qq[k], row[k], rid[k]) && b0 + k * 64 + lane < s1;
+      const unsigned long long bal = __ballot(m);
+      if (m) {
+        const uint32_t pos = nm + uint32_t(__popcll(bal & lt));
+        const uint32_t adv = row[k].adv & ROW_ADV_MASK;
+        if (DIRECT) {
+          if (base + pos < a.out_cap) {
+            a.out_pkg[base + pos] = a.out_base + a.p0 + pbase + qq[k];
+            a.out_adv[base + pos] = adv;
+          }
+        } else if (pos < uint32_t(MBW)) {
+          madv[pos] = adv;
+          mq[pos] = uint8_t(qq[k]);
+        }
+      }
+      nm += uint32_t(__popcll(bal));
+    }
+  }
+  return nm;
+}
+
 // The sweep of tile t (packages t * 256 ..) given each lane's package record r.
-template <int K, int MB, int FILT>
+template <int K, int MB, int FILT, int SEG = 0>
 __device__ __forceinline__ void sweep_tile(const SweepArgs& a, SweepShared<FILT>& s, uint32_t* madv, uint8_t* mq,
                                            uint8_t* map, uint32_t t, uint32_t tid, const PkgRec& r) {
   const uint32_t lane = tid & 63, wave = tid >> 6;
@@ -631,6 +711,45 @@ __device__ __forceinline__ void sweep_tile(const SweepArgs& a, SweepShared<FILT>
     __syncthreads();
   }
 
+  if constexpr (SEG != 0) {
+    constexpr int MBW = MB / 4;
+    const uint32_t seg = ((total + 4 * 64 - 1) / (4 * 64)) * 64;  // a wave's share, whole 64-pair units
+    const uint32_t s0 = min(total, wave * seg), s1 = min(total, s0 + seg);
+    uint32_t* madv_w = madv + wave * MBW;
+    uint8_t* mq_w = mq + wave * MBW;
+    const uint32_t nmw = sweep_seg<K, MBW, FILT, false>(a, s, madv_w, mq_w, map, nnz, total, s0, s1, lane, 0);
+    if (lane == 0) s.wsum[0][wave] = nmw;  // the row-count scan is done with wsum[0]
+    __syncthreads();
+    uint32_t woff = 0, nm = 0;
+#pragma unroll
+    for (int w = 0; w < kTile / 64; w++) {
+      const uint32_t c = s.wsum[0][w];
+      woff += (uint32_t(w) < wave) ? c : 0;
+      nm += c;
+    }
+    if (tid == 0) {
+      s.base = nm ? atomicAdd(&a.ctl[0], (unsigned long long)nm) : 0ull;
+      TileDir e;
+      e.base = s.base;
+      e.count = nm;
+      e.pad = 0;
+      a.dir[a.t0 + t] = e;
+    }
+    __syncthreads();
+    const unsigned long long base = s.base + woff;
+    if (nmw <= uint32_t(MBW)) {
+      const uint32_t pb = a.out_base + a.p0 + t * kTile;
+      for (uint32_t i = lane; i < nmw; i += 64) {
+        if (base + i < a.out_cap) {
+          a.out_pkg[base + i] = pb + mq_w[i];
+          a.out_adv[base + i] = madv_w[i];
+        }
+      }
+    } else {
+      sweep_seg<K, MBW, FILT, true>(a, s, madv_w, mq_w, map, nnz, total, s0, s1, lane, base);  // rare
+    }
+    return;
+  }
   const uint32_t nm = sweep<K, MB, FILT, false>(a, s, madv, mq, map, nnz, total, tid, 0);
 
   // the tile's output segment: one atomic reservation, no waiting on other tiles; the
@@ -677,9 +796,9 @@ __global__ __launch_bounds__(kTile) void sweep_kernel(SweepArgs a) {
 // of one CU sit in different phases, so one tile's probe latency overlaps another's sweep.
 // DIAG (measurement only, wrong match lists by construction; "diag_*" variants): bit 0 skips
 // the version encoder, bit 1 the index probe, bit 2 the sweep.
-template <uint32_t GM, int K, int MB, int FILT, int DIAG = 0, int WPE = 1>
+template <uint32_t GM, int K, int MB, int FILT, int DIAG = 0, int WPE = 1, int SEG = 0>
 __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
-  constexpr uint32_t kStageVec = kStage / 16 + 2;
+  constexpr uint32_t kStageVec = kStage / 16 + 8;  // + two zero words per wave window (per-wave staging)
   constexpr uint32_t kMbufVec = (MB * 5 + 15) / 16;
   __shared__ uint4 buf[kStageVec > kMbufVec ? kStageVec : kMbufVec];  // strings (probe), then matches (sweep)
   // the probe's per-lane dpkg keys + code table share LDS with the sweep's state (the scan
@@ -708,21 +827,34 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
   const uint32_t p = t * kTile + tid;
   uint2 d = make_uint2(0xFFFFFFFFu, 0);
   if (p < a.n) d = a.pk[p];
-  const uint64_t w0 = a.tile_off[t * kGroupsPerTile], w1 = a.tile_off[(t + 1) * kGroupsPerTile];  // before the scan's barriers
+  constexpr bool kWaveStage = (SEG & 2) != 0;
+  const uint32_t g = t * kGroupsPerTile + (kWaveStage ? (tid >> 6) : 0u);  // the window's first group
+  const uint64_t w0 = a.tile_off[g], w1 = a.tile_off[kWaveStage ? g + 1 : (t + 1) * kGroupsPerTile];  // before the scan's barriers
   const uint32_t nlen = d.y & 0xFFFFu, vlen = d.y >> 16;
   uint32_t off = 0;
-  block_exscan<kTile>(s.wsum[0], nlen + vlen, tid, off);
+  uint4* sbuf = buf;  // this lane's staging window
   const uint64_t base16 = w0 & ~uint64_t(15);
-  const bool staged = w1 - base16 <= kStage;
-  if (staged) stage_window(buf, a.arena + base16, uint32_t((w1 - base16 + 15) / 16), tid);
-  if (tid < 128) u.pr.tab[tid] = deb_fast_code(tid);
-  __syncthreads();
+  bool staged;
+  if constexpr (kWaveStage) {
+    off = wave_exscan(nlen + vlen, tid & 63);
+    sbuf = buf + (tid >> 6) * (kStage / 4 / 16 + 2);
+    staged = w1 - base16 <= kStage / 4;
+    if (staged) stage_window_wave(sbuf, a.arena + base16, uint32_t((w1 - base16 + 15) / 16), tid & 63);
+    if (tid < 128) u.pr.tab[tid] = deb_fast_code(tid);
+    __syncthreads();  // the code table (one wave's LDS traffic alone is ordered)
+  } else {
+    block_exscan<kTile>(s.wsum[0], nlen + vlen, tid, off);
+    staged = w1 - base16 <= kStage;
+    if (staged) stage_window(buf, a.arena + base16, uint32_t((w1 - base16 + 15) / 16), tid);
+    if (tid < 128) u.pr.tab[tid] = deb_fast_code(tid);
+    __syncthreads();
+  }
   PkgRec r;
   r.meta = make_uint4(0, 0, 0, 0);
   r.k0 = r.k1 = 0;
   if (p < a.n && d.x < a.db.n_plats) {
     if (staged) {
-      const uint8_t* sb = reinterpret_cast<const uint8_t*>(buf) + uint32_t(w0 - base16) + off;
+      const uint8_t* sb = reinterpret_cast<const uint8_t*>(sbuf) + uint32_t(w0 - base16) + off;
       probe_one<GM, uint32_t, DIAG & 3>(a, p, d.x, nlen, vlen, sb, sb + nlen, w0 + off + nlen, r,
                                         reinterpret_cast<uint8_t*>(u.pr.kbuf) + tid * kFastKeyStride, u.pr.tab);
     } else {
@@ -733,7 +865,7 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
   if (DIAG & 4) r.meta.y = 0;  // no rows: the sweep does nothing
   __syncthreads();  // the strings are dead: buf becomes the match buffer
   uint32_t* madv = reinterpret_cast<uint32_t*>(buf);
-  sweep_tile<K, MB, FILT>(fa.sa, s, madv, reinterpret_cast<uint8_t*>(madv + MB), map, t, tid, r);
+  sweep_tile<K, MB, FILT, SEG>(fa.sa, s, madv, reinterpret_cast<uint8_t*>(madv + MB), map, t, tid, r);
 }
 
 template <uint32_t GM, int DIAG = 0>
@@ -746,9 +878,20 @@ void launch_sweep(uint32_t n_tiles, hipStream_t st, const SweepArgs& a) {
   hipLaunchKernelGGL((sweep_kernel<K, MB, FILT>), dim3(n_tiles), dim3(kTile), 0, st, a);
 }
 
-template <uint32_t GM, int K, int MB, int FILT, int DIAG = 0, int WPE = 1>
+template <uint32_t GM, int K, int MB, int FILT, int DIAG = 0, int WPE = 1, int SEG = 0>
 void launch_fused(uint32_t n_tiles, hipStream_t st, const FusedArgs& a) {
-  hipLaunchKernelGGL((fused_kernel<GM, K, MB, FILT, DIAG, WPE>), dim3(n_tiles + a.n_copy), dim3(kTile), 0, st, a);
+  hipLaunchKernelGGL((fused_kernel<GM, K, MB, FILT, DIAG, WPE, SEG>), dim3(n_tiles + a.n_copy), dim3(kTile), 0, st, a);
+}
+
+// Table entry of variant (F, K, MB) for grammar set GM / row-filter level FILT
+// (match_variants.h: F = 0 split, 1-3 fused, 4 fused with per-wave sweep segments, 5 also
+// per-wave staging, 11-15 fused measurement builds).
+template <uint32_t GM, int FILT, int F, int K, int MB>
+constexpr FusedFn fused_entry() {
+  if constexpr (F == 0) return nullptr;
+  else if constexpr (F == 4) return &launch_fused<GM, K, MB, FILT, 0, 1, 1>;
+  else if constexpr (F == 5) return &launch_fused<GM, K, MB, FILT, 0, 1, 3>;
+  else return &launch_fused<GM, K, MB, FILT, (F >= 10 ? F - 10 : 0), TVM_FUSED_WPE(F)>;
 }
 
 }  // namespace

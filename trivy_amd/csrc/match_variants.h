@@ -5,14 +5,14 @@
 // kAutoVariant.
 #pragma once
 
-#define TVM_MATCH_VARIANTS_PRODUCT(X) \
-  X(1, 4, 2048, "fused_k4_m2048")     \
-  X(2, 4, 2048, "fused_k4_m2048_o6")  \
-  X(3, 4, 2048, "fused_k4_m2048_o8")  \
-  X(1, 2, 2048, "fused_k2_m2048")     \
-  X(1, 1, 2048, "fused_k1_m2048")     \
-  X(0, 2, 2048, "split_k2_m2048")     \
-  X(0, 4, 2048, "split_k4_m2048")
+#define TVM_MATCH_VARIANTS_PRODUCT(X)  \
+  X(1, 4, 2048, "fused_k4_m2048")      \
+  X(1, 2, 2048, "fused_k2_m2048")      \
+  X(1, 1, 2048, "fused_k1_m2048")      \
+  X(0, 2, 2048, "split_k2_m2048")      \
+  X(0, 4, 2048, "split_k4_m2048")      \
+  X(4, 4, 2400, "fused_k4_m2400_seg")  \
+  X(5, 4, 2400, "fused_k4_m2400_wseg")
 
 // Measurement-only variants (wrong match lists by construction): built only with
 // `make DIAG=1` (-DTVM_DIAG), never reachable in the product library.
@@ -27,7 +27,8 @@
 #define TVM_MATCH_VARIANTS(X) TVM_MATCH_VARIANTS_PRODUCT(X)
 #endif
 
-// Fused F = 2 / 3: the same kernel compiled for at least 6 / 8 waves per SIMD (register cap).
+// Fused F = 2 / 3: the same kernel compiled for at least 6 / 8 waves per SIMD (register cap;
+// measured within 1 % on C2, rounds 2-3, not in the list any more).
 #define TVM_FUSED_WPE(F) ((F) == 2 ? 6 : (F) == 3 ? 8 : 1)
 
 #define TVM_VARIANT_COUNT_(F, K, MB, NAME) +1
@@ -35,5 +36,9 @@ constexpr int kNumTuned = 0 TVM_MATCH_VARIANTS(TVM_VARIANT_COUNT_);
 #undef TVM_VARIANT_COUNT_
 
 // Variant (index into the list) the engine launches by default.
-constexpr int kAutoVariant = 0;          // fused_k4_m2048: fastest on C2 (dpkg only)
-constexpr int kAutoVariantFiltered = 3;  // fused_k2_m2048: fastest on C5 / C4 (bench.py --sweep, MI355X)
+// bench.py --sweep on MI355X (profiles/r03/sweep_c2.txt, sweep_c3.txt): per-wave staging +
+// sweep segments are fastest for dpkg-only batches (C2 0.485 -> 0.469 ms); for the filtered
+// grammar sets (rpm/apk/library rows, uneven per-pair cost) the shared K=2 sweep stays fastest
+// (C3 0.257 ms against 0.34-0.36 ms in segments).
+constexpr int kAutoVariant = 6;          // fused_k4_m2400_wseg
+constexpr int kAutoVariantFiltered = 1;  // fused_k2_m2048
