@@ -192,12 +192,14 @@ class Mix:
         return out
 
     def fill(self, mb, b=0, e=None):
+        """Packages [b, e) (whole targets), one add call - one Result (result.Filter's scope:
+        its dedup and order) - per target of per_target packages, as the images / lockfiles
+        of a fleet arrive."""
         e = self.n if e is None else e
         for s, (p, g) in zip(self.starts, self.batch.groups):
             lo, hi = max(b, s) - s, min(e, s + len(g["key"])) - s
-            if hi <= lo:
-                continue
-            self.sm.add_slice(mb, self.sdb, p, g, lo, hi)
+            for t0 in range(lo, hi, self.per_target):
+                self.sm.add_slice(mb, self.sdb, p, g, t0, min(hi, t0 + self.per_target))
 
     def cpu_baseline(self, budget_s, threads):
         """The native C port of the driver loops (oracle/mixmatch.c + oracle/libcmp.c, pinned by
