@@ -285,7 +285,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-fill", action="store_true", help="c2: skip the FillInfo / Filter legs")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end pipelined pass")
-    ap.add_argument("--chunk", type=int, default=1 << 19, help="end-to-end pass: packages per pipeline chunk")
+    ap.add_argument("--chunk", type=int, default=1 << 20, help="end-to-end pass: packages per pipeline chunk")
     ap.add_argument("--dropin", action="store_true",
                     help="c2: also time 100-package requests through the per-target driver path")
     ap.add_argument("--variant", type=int, default=None, help="match-path variant (tvm_engine_set_variant)")
@@ -416,8 +416,13 @@ def main():
         e2e = {"packages_per_s": wl.n / (med / 1e3), "ms_per_pass": med, "passes": len(ms),
                "h2d_bytes": st["h2d_bytes"], "d2h_bytes": st["d2h_bytes"], "chunks": st["chunks"],
                "pcie_GBs": (st["h2d_bytes"] + st["d2h_bytes"]) / (med / 1e3) / 1e9,
-               "inside": "H2D of the batch (package words, tile offsets, name/version bytes) from pinned host "
-                         "memory + match kernels + order kernel + D2H of the per-package advisory lists (CSR)"}
+               "transport_form": st["transport_form"], "prepare_encode_ms": st["encode_ms"],
+               "inside": "H2D of the batch from pinned host memory (its transport form: each distinct name / "
+                         "version string once + per-package references, one DMA per chunk) + the kernel that "
+                         "rebuilds each chunk in HBM + match kernels + the per-package advisory lists (CSR) "
+                         "written into pinned host memory by the next launch's first workgroups",
+               "outside": "prepare (once per batch: pinning, sizing, building the transport form, "
+                          "prepare_encode_ms on one host thread)"}
         mp.close()
 
     fill = None

@@ -289,9 +289,14 @@ int tvm_batch_upload_into(tvm_engine* e, tvm_batch* b, void* pkg_dev, void* adv_
  * matched as soon as it lands, and its per-package advisory lists come back (CSR) while
  * the next chunk is matched.  This is what a cgo caller pays per batch of targets
  * (detect.go:63 / library/detect.go:11 called for every target of a scan). */
-/* Pins the batch (no more adds afterwards) and sizes every device / pinned buffer. */
-int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32_t chunk_packages, char* err,
-                         size_t errlen);
+/* Pins the batch (no more adds afterwards) and sizes every device / pinned buffer.  Unless
+ * flags has TVM_PIPE_RAW, the batch travels in its transport form when it has one (every
+ * name and version under 256 bytes, at most 255 platforms): each distinct name and each
+ * distinct version string crosses the link once, packages carry references to them, and
+ * the GPU rebuilds the batch's arrays chunk by chunk (one DMA per chunk). */
+enum { TVM_PIPE_RAW = 1 };
+int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32_t chunk_packages, uint32_t flags,
+                         char* err, size_t errlen);
 /* One pass; ms = wall time of the call.  TVM_EINVAL with *n_matches set when the matches do
  * not fit match_cap (prepare again with a larger one). */
 int tvm_pipeline_run(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* err_pkg, double* ms, char* err,
@@ -300,8 +305,9 @@ int tvm_pipeline_run(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* 
  * tvm_batch_free): package p's advisory indices are adv[row_end[p-1] .. row_end[p])
  * (row_end[-1] = 0), in (package, advisory) order. */
 int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row_end, uint64_t* n_matches);
-/* Bytes the last pass copied: [0] host to device, [1] device to host, [2] chunks. */
-int tvm_pipeline_stats(tvm_batch* b, uint64_t out[3]);
+/* [0] bytes the last pass copied host to device, [1] device to host, [2] chunks, [3] 1 when
+ * the batch travels in its transport form, [4] prepare's host time building it (us). */
+int tvm_pipeline_stats(tvm_batch* b, uint64_t out[5]);
 
 /* ---- Red Hat on the batch path ----------------------------------------------------------
  * After tvm_match_launch (+ sync): the Red Hat driver's epilogue for every package of the

@@ -1,5 +1,6 @@
-"""GPU: the end-to-end pipelined pass (tvm_pipeline_*: chunked H2D of a host batch, match,
-order_kernel, D2H of the per-package advisory lists as CSR) gives exactly the oracle's
+"""GPU: the end-to-end pipelined pass (tvm_pipeline_*: chunked H2D of a host batch - its
+transport form, rebuilt in HBM by unpack_kernel, or its raw arrays - match, the result move
+of the per-package advisory lists into host memory as CSR) gives exactly the oracle's
 (package, advisory) pairs, for chunk sizes that do and do not divide the batch, and
 reports overflow / poisoned keys like the device-resident path."""
 import numpy as np
@@ -32,12 +33,13 @@ def world():
     return sdb, build_engine(sdb)
 
 
+@pytest.mark.parametrize("raw", [False, True])
 @pytest.mark.parametrize("chunk", [256, 1000, 4096, 1 << 19])
-def test_pipeline_matches_oracle(world, chunk, oracle_built):
+def test_pipeline_matches_oracle(world, chunk, raw, oracle_built):
     sdb, eng = world
     batch = make_batch(sdb, 37, 333, [2, 2, 1], seed=chunk)  # 12321 packages: ragged last tile
     opk, oad = om.match(om.Prepared(sdb, batch), n_threads=8)
-    mb = _fill(eng, sdb, batch).pipeline_prepare(match_cap=len(opk) + 5, chunk_packages=chunk)
+    mb = _fill(eng, sdb, batch).pipeline_prepare(match_cap=len(opk) + 5, chunk_packages=chunk, raw=raw)
     for _ in range(2):  # a second pass over the same pinned batch gives the same lists
         total, errp, ms = mb.pipeline_run()
         assert errp == -1 and total == len(opk) and ms > 0
@@ -47,7 +49,39 @@ def test_pipeline_matches_oracle(world, chunk, oracle_built):
     st = mb.pipeline_stats()
     assert st["chunks"] == -(-len(batch) // (-(-chunk // 256) * 256)) and st["h2d_bytes"] > 0
     assert st["d2h_bytes"] == 4 * (len(batch) + len(opk))
+    assert st["transport_form"] == (not raw)
     mb.close()
+
+
+def test_pipeline_transport_form_edges(oracle_built):
+    """The transport form against the oracle where it differs from the raw arrays: empty
+    versions, names repeated across chunks (referenced back into earlier chunks' strings),
+    a version equal to a name; and a string of 256 bytes, which has no transport form (the
+    batch goes raw)."""
+    from test_gpu_parity import build_engine
+    from tools.synth import SynthBatch
+    sdb = make_db(["debian 12", "ubuntu 22.04"], 500, seed=8)
+    eng = build_engine(sdb)
+    base = make_batch(sdb, 12, 300, [1, 1], seed=4)
+    names, vers = list(base.names), list(base.versions)
+    for i in range(0, len(names), 7):
+        vers[i] = b""
+    for i in range(3, len(names), 11):
+        vers[i] = names[i]
+    for long_one in (False, True):
+        v2 = list(vers)
+        if long_one:
+            v2[100] = b"1." + b"9" * 254
+        plat = [p for p, b0, b1 in base.targets]
+        targets = list(base.targets)
+        batch = SynthBatch(base.plat, names, v2, targets)
+        opk, oad = om.match(om.Prepared(sdb, batch), n_threads=4)
+        mb = _fill(eng, sdb, batch).pipeline_prepare(match_cap=len(opk) + 1, chunk_packages=512)
+        assert mb.pipeline_stats()["transport_form"] == (not long_one)
+        total, errp, _ = mb.pipeline_run()
+        pk, ad = _pairs_of(*mb.pipeline_csr())
+        assert total == len(opk) and np.array_equal(pk, opk) and np.array_equal(ad, oad), (long_one, plat[:3])
+        mb.close()
 
 
 def test_pipeline_overflow_then_exact(world, oracle_built):

@@ -156,7 +156,8 @@ _SIG = [
     ("tvm_batch_set_package_base", ctypes.c_int, [_P, ctypes.c_uint32]),
     ("tvm_batch_upload_into", ctypes.c_int, [_P, _P, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                              ctypes.c_char_p, ctypes.c_size_t]),
-    ("tvm_pipeline_prepare", ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_pipeline_prepare", ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p,
+                                            ctypes.c_size_t]),
     ("tvm_pipeline_run", ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64),
                                         ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_pipeline_result", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),

@@ -227,11 +227,12 @@ class MatchBatch:
         return lib().tvm_match_algorithmic_bytes(self.engine.h, self.h)
 
     # ---- end-to-end pipelined pass (tvm_pipeline_*) ----
-    def pipeline_prepare(self, match_cap=None, chunk_packages=1 << 19):
-        """Pins the batch and sizes the pipeline (host batch -> GPU -> host CSR)."""
+    def pipeline_prepare(self, match_cap=None, chunk_packages=1 << 19, raw=False):
+        """Pins the batch and sizes the pipeline (host batch -> GPU -> host CSR).  raw: upload
+        the batch's own arrays instead of its transport form (TVM_PIPE_RAW)."""
         e = errbuf()
         cap = match_cap if match_cap is not None else max(1024, 8 * len(self))
-        self._check(lib().tvm_pipeline_prepare(self.engine.h, self.h, cap, chunk_packages, e, len(e)), e,
+        self._check(lib().tvm_pipeline_prepare(self.engine.h, self.h, cap, chunk_packages, 1 if raw else 0, e, len(e)), e,
                     "tvm_pipeline_prepare")
         self.pipe_cap = cap
         return self
@@ -260,10 +261,11 @@ class MatchBatch:
         return a, r
 
     def pipeline_stats(self):
-        out = (ctypes.c_uint64 * 3)()
+        out = (ctypes.c_uint64 * 5)()
         if lib().tvm_pipeline_stats(self.h, out):
             raise RuntimeError("tvm_pipeline_stats")
-        return {"h2d_bytes": out[0], "d2h_bytes": out[1], "chunks": out[2]}
+        return {"h2d_bytes": out[0], "d2h_bytes": out[1], "chunks": out[2], "transport_form": bool(out[3]),
+                "encode_ms": out[4] / 1e3}
 
     # ---- FillInfo fused behind the match list (tvm_match_fill*) ----
     def fill(self, sync=True):

@@ -1251,9 +1251,9 @@ int tvm_match_filter_time(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o,
 
 // ---- end-to-end pipelined pass (pipeline.hip) -------------------------------------------
 
-int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32_t chunk_packages, char* err,
-                         size_t errlen) {
-  if (!e || !b || chunk_packages == 0) return TVM_EINVAL;
+int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32_t chunk_packages, uint32_t flags,
+                         char* err, size_t errlen) {
+  if (!e || !b || chunk_packages == 0 || (flags & ~uint32_t(TVM_PIPE_RAW))) return TVM_EINVAL;
   std::shared_lock<std::shared_mutex> lk(e->mu);
   if (!bind(b, e)) {
     set_err(err, errlen, kStale);
@@ -1261,7 +1261,7 @@ int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32
   }
   b->pipe.reset(new Pipeline());
   std::string msg;
-  if (!b->pipe->prepare(*e->eng, b->hb, match_cap, chunk_packages, msg)) {
+  if (!b->pipe->prepare(*e->eng, b->hb, match_cap, chunk_packages, !(flags & TVM_PIPE_RAW), msg)) {
     b->pipe.reset();
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
@@ -1311,11 +1311,13 @@ int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row
   return TVM_OK;
 }
 
-int tvm_pipeline_stats(tvm_batch* b, uint64_t out[3]) {
+int tvm_pipeline_stats(tvm_batch* b, uint64_t out[5]) {
   if (!b || !b->pipe || !out) return TVM_EINVAL;
   out[0] = b->pipe->h2d_bytes();
   out[1] = b->pipe->d2h_bytes();
   out[2] = b->pipe->chunks();
+  out[3] = b->pipe->transport_form() ? 1 : 0;
+  out[4] = b->pipe->encode_us();
   return TVM_OK;
 }
 

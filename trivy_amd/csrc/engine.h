@@ -112,35 +112,123 @@ struct DevMatches {
 };
 enum : uint32_t { ERR_SPILL = 1, ERR_TILES = 2 };
 
-// The end-to-end pipeline's result move for one chunk (packages [p0, p1)): the chunk's
-// per-package advisory lists (device CSR from order_kernel) into the pinned host result
-// through 16-byte kernel stores (kernel stores into host memory: 55 GB/s; a DMA
-// device-to-host copy: 28.6 GB/s; profiles/r03/pcie_probe.txt).  The chunk's advisory range
-// is read from the device row ends, so the host never waits per chunk.  Run by extra
-// workgroups of the next chunk's match launch (Engine::launch_tiles), so the link writes
-// overlap that chunk's matching, or by copy_out_kernel for the last chunk.
+// The end-to-end pipeline's result move for one chunk (tiles [t0, t1)): the chunk's match
+// segments, straight from the tile directory, become the per-package advisory lists (CSR)
+// in the pinned host result - no CSR in HBM, no separate order kernel.  A tile's segment is
+// already in package order (the match kernels compact in lane order), so the move only
+// places it: tile t's lists start at chunk_base[c] + the counts of the chunk's tiles before
+// t, and its 256 row ends are that base + the inclusive scan of its per-package counts.
+// Stores into host memory are 16-byte kernel stores (55 GB/s; a DMA device-to-host copy
+// runs at 28.6 GB/s, profiles/r03/pcie_probe.txt), so each segment is realigned in registers to
+// the destination's 16-byte units.  Run by the first workgroups of the next chunk's match
+// launch (Engine::launch_tiles), so the link writes overlap that chunk's matching, or by
+// copy_out_kernel for the last chunk.  chunk_base[0] = 0 is set by the host; the move of
+// chunk c writes chunk_base[c + 1].
 struct CopyOutArgs {
-  const uint32_t* row_end = nullptr;  // device CSR
-  const uint32_t* csr_adv = nullptr;
-  uint4* row_end_h = nullptr;         // device addresses of the pinned host result (16-B aligned, padded)
-  uint4* adv_h = nullptr;
-  uint32_t p0 = 0, p1 = 0;            // p0 a multiple of 4, p1 > p0
-  uint64_t cap = 0;                   // advisory capacity (an overflowed pass's range is cut to it)
+  const TileDir* dir = nullptr;       // the chunk's match list
+  const uint32_t* pkg = nullptr;
+  const uint32_t* adv = nullptr;
+  uint32_t* row_end_h = nullptr;      // device addresses of the pinned host result (16-B aligned,
+  uint32_t* adv_h = nullptr;          // row ends padded to whole tiles, advisories to whole units)
+  unsigned long long* chunk_base = nullptr;
+  uint32_t c = 0;                     // chunk index
+  uint32_t t0 = 0, t1 = 0;            // the chunk's tiles
+  uint32_t pkg_base = 0;              // subtracted from the match list's package indices
+  uint64_t cap = 0;                   // match / result capacity (an overflowed pass moves no advisories)
 };
+constexpr uint32_t kCopyLdsWords = kTile + 8;  // copy_out_tiles' LDS: counts + scratch
+constexpr uint32_t kCopyWorkgroups = 256;      // workgroups of a result move
 
-// Whole 16-byte units are moved: the words before the chunk's range are the previous chunk's
-// (final) and those after it are rewritten by the next chunk's move, which runs later.
-__device__ __forceinline__ void copy_out_range(const CopyOutArgs& a, uint64_t tid, uint64_t stride) {
-  const uint64_t s0 = a.p0 ? a.row_end[a.p0 - 1] : 0, e0 = a.row_end[a.p1 - 1];
-  const uint64_t e = e0 < a.cap ? e0 : a.cap, s = s0 < e ? s0 : e;
-  const uint64_t u0 = s / 4, nu = (e + 3) / 4 - u0;                    // advisory units
-  const uint64_t r0 = a.p0 / 4, nr = (uint64_t(a.p1) + 3) / 4 - r0;    // row-end units
-  const uint4* csr = reinterpret_cast<const uint4*>(a.csr_adv);
-  const uint4* re = reinterpret_cast<const uint4*>(a.row_end);
-  for (uint64_t i = tid; i < nu + nr; i += stride) {
-    if (i < nu) a.adv_h[u0 + i] = csr[u0 + i];
-    else a.row_end_h[r0 + (i - nu)] = re[r0 + (i - nu)];
+__device__ __forceinline__ uint32_t copy_block_sum(uint32_t v, uint32_t* red, uint32_t tid) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((tid & 63) == 0) red[tid >> 6] = v;
+  __syncthreads();
+  uint32_t s = 0;
+#pragma unroll
+  for (int w = 0; w < kTile / 64; w++) s += red[w];
+  return s;
+}
+
+// Workgroup `wg` of `n_wg` moves a contiguous run of the chunk's tiles, one tile after the
+// other (measured, DESIGN.md §7: one workgroup per tile moved the chunk slower, at 36 GB/s
+// beside the match tiles against 40 GB/s here).  lds: kCopyLdsWords words of the caller's
+// shared memory (the match kernel lends its staging buffer).
+__device__ __forceinline__ void copy_out_tiles(const CopyOutArgs& a, uint32_t wg, uint32_t n_wg, uint32_t* lds) {
+  uint32_t* cnt = lds;
+  uint32_t* red = lds + kTile;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t nt = a.t1 - a.t0;
+  const uint32_t r0 = a.t0 + uint32_t(uint64_t(nt) * wg / n_wg), r1 = a.t0 + uint32_t(uint64_t(nt) * (wg + 1) / n_wg);
+  uint32_t pre = 0;  // counts of the chunk's tiles before the run (a pass's total fits 32 bits: cap < 2^32)
+  for (uint32_t u = a.t0 + tid; u < r0; u += kTile) pre += a.dir[u].count;
+  unsigned long long b = a.chunk_base[a.c] + copy_block_sum(pre, red, tid);
+  for (uint32_t t = r0; t < r1; t++) {
+    const TileDir d = a.dir[t];
+    cnt[tid] = 0;
+    __syncthreads();
+    const bool fits = d.base + d.count <= a.cap && b + d.count <= a.cap;
+    const uint32_t p_first = t * kTile;
+    if (fits)
+      for (uint32_t i0 = 0; i0 < d.count; i0 += 4 * kTile) {  // four loads in flight per lane
+        uint32_t q[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const uint32_t i = i0 + u * kTile + tid;
+          q[u] = i < d.count ? a.pkg[d.base + i] - a.pkg_base - p_first : kTile;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if (q[u] < kTile) atomicAdd(&cnt[q[u]], 1u);
+      }
+    __syncthreads();
+    uint32_t x = cnt[tid];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (lane >= uint32_t(o)) x += y;
+    }
+    if (lane == 63) red[wave] = x;
+    __syncthreads();
+    for (uint32_t w = 0; w < wave; w++) x += red[w];
+    cnt[tid] = uint32_t(b) + x;  // row end of package p_first + tid (row ends are 32-bit)
+    __syncthreads();
+    // the segment, realigned in registers to the destination's 16-byte units
+    const uint64_t u0 = b >> 2, nu = fits ? ((b + d.count + 3) >> 2) - u0 : 0;
+    const uint32_t sh = uint32_t(b & 3);
+    if (tid < kTile / 4)
+      reinterpret_cast<uint4*>(a.row_end_h)[p_first / 4 + tid] = reinterpret_cast<const uint4*>(cnt)[tid];
+    constexpr int kU = 4;
+    for (uint64_t j0 = 0; j0 < nu; j0 += uint64_t(kU) * kTile) {
+      uint32_t v[kU][4];
+#pragma unroll
+      for (int k = 0; k < kU; k++) {
+        const uint64_t j = j0 + uint64_t(k) * kTile + tid;
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+          const int64_t i = int64_t(j * 4 + w) - int64_t(sh);  // segment index of the unit's word w
+          v[k][w] = (j < nu && i >= 0 && i < int64_t(d.count)) ? a.adv[d.base + uint64_t(i)] : 0u;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kU; k++) {
+        const uint64_t j = j0 + uint64_t(k) * kTile + tid;
+        if (j >= nu) continue;
+        const int64_t i0 = int64_t(j * 4) - int64_t(sh);
+        if (i0 >= 0 && i0 + 4 <= int64_t(d.count)) {
+          reinterpret_cast<uint4*>(a.adv_h)[u0 + j] = make_uint4(v[k][0], v[k][1], v[k][2], v[k][3]);
+        } else {  // the segment's first or last unit, shared with a neighbour tile: its own words only
+#pragma unroll
+          for (int w = 0; w < 4; w++)
+            if (i0 + w >= 0 && i0 + w < int64_t(d.count)) a.adv_h[(u0 + j) * 4 + w] = v[k][w];
+        }
+      }
+    }
+    b += d.count;
+    __syncthreads();  // cnt is rewritten by the next tile
   }
+  if (wg == n_wg - 1 && tid == 0) a.chunk_base[a.c + 1] = b;
 }
 
 class Engine {

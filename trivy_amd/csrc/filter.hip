@@ -99,6 +99,7 @@ struct FilterArgs {
   uint8_t* pcls;   // after filter_select: the pair's counter class (pair_class)
   uint32_t* wcarry;  // after filter_count, per 64-pair wave w entered by a run begun earlier:
                      //   the run's class counts before pair 64w (kClasses each)
+  const uint8_t* vx;  // per pair: a VEX statement names its (package, ID) (vex_mark)
   // tables
   const unsigned long long* rules;  // {key, precedence} x 2^k
   uint64_t rule_mask;
@@ -171,6 +172,41 @@ __global__ __launch_bounds__(kBlock) void rules_insert(RuleDev r, unsigned long 
       return;
     }
   }
+}
+
+// VEX statements (package, ID) applied to the pairs directly: each statement finds its
+// package's run of the list (filter_mark's run_b / run_e; the list is grouped by package),
+// bisects it for the ID (runs are ID-sorted unless FL_UNS) and marks that pair, so
+// filter_select tests one byte per pair instead of probing a hash set.  run_b of a package
+// without pairs is stale: a start is taken only where it really is the first pair of that
+// package.
+__global__ __launch_bounds__(kBlock) void vex_mark(RuleDev r, const uint32_t* pkg, const uint2* side,
+                                                   const uint32_t* run_b, const uint32_t* run_e, const uint8_t* fl,
+                                                   uint64_t n, uint8_t* vx) {
+  const uint64_t g = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  int k = 0;
+  while (k < r.n_lists && g >= r.end[k]) k++;
+  if (k == r.n_lists) return;
+  const uint64_t e = g - (k ? r.end[k - 1] : 0);
+  const uint32_t rank = r.rank[k][r.id[k][e]];
+  if (rank == kEmpty) return;
+  if (!r.subject[k]) return;
+  const uint32_t p = r.subject[k][e];
+  const uint32_t rb = run_b[p];
+  if (rb >= n || pkg[rb] != p || (rb && pkg[rb - 1] == p)) return;  // no pairs (stale start)
+  const uint32_t re = run_e[p];  // written by this call's filter_mark, as rb was
+  if (fl[p] & FL_UNS) {  // IDs not increasing along the run (two data sources of one ID): every pair
+    for (uint32_t j = rb; j < re; j++)
+      if (side[j].x == rank) vx[j] = 1;
+    return;
+  }
+  uint32_t lo = rb, hi = re;  // strictly increasing IDs: the one pair, by bisection (runs can be thousands long)
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (side[mid].x < rank) lo = mid + 1;
+    else hi = mid;
+  }
+  if (lo < re && side[lo].x == rank) vx[lo] = 1;
 }
 
 // Pairs per thread per step of the streaming kernels: every lane issues the loads of kU
@@ -278,8 +314,7 @@ __global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
               }
             }
           }
-          if (key != kEmpty && (a.kinds & (1u << RULE_VEX)) && (f & FL_VEX) &&
-              rule_find(a, rule_key(RULE_VEX, p, vr)) != kEmpty)
+          if (key != kEmpty && (a.kinds & (1u << RULE_VEX)) && a.vx[i])
             key = kEmpty;  // VEX: openvex.go:35-40 / cyclonedx.go:56-60 / csaf.go:36-40 drop it
         }
         a.skey[i] = key;
@@ -597,23 +632,72 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   const uint32_t blocks_u = uint32_t(std::min<uint64_t>((n + kBlock * kU - 1) / (kBlock * kU), 256ull * 32));
   sev_mask &= 0x1Fu;  // SeverityNames only: a bit for "out of range" (5) would pass a severity 4 - 5 can't order
   const uint64_t np = n_pkgs_;
+  // The rule lists go up in one pinned copy, staged while the GPU counts repeating pairs.
+  // Ignore rules (ALL / PKG / CLS) become a hash set (rules_insert); VEX statements mark
+  // their pairs directly once the package runs are known (vex_mark, after filter_mark).
+  const uint64_t nr_all = rules.size();
+  RuleDev rd{}, vd{};  // hash-set lists, VEX lists
+  uint64_t nr = 0, nv = 0;
+  if (nr_all) {
+    uint64_t words = rules.rank[0].size() + rules.rank[1].size();
+    for (int k = 0; k < rules.n_lists; k++)
+      words += rules.lists[k].n * (1 + (rules.lists[k].subject ? 1 : 0) + (rules.lists[k].prec ? 1 : 0));
+    if (pin_cap_ < words * 4) {
+      if (pin_) (void)hipHostFree(pin_);
+      pin_ = nullptr;
+      pin_cap_ = 0;
+      if (!ok(hipHostMalloc(&pin_, words * 4, hipHostMallocDefault), "hipHostMalloc(filter rules)", err)) return false;
+      pin_cap_ = words * 4;
+    }
+    if (!grow(18, words * 4, err)) return false;
+  }
+  if (any_dup_ && !grow(23, 16, err)) return false;
   // dedup table: 2^k >= 2 x the pairs that can enter it (load <= 0.5, probes end)
   uint64_t tcap = 0;
+  unsigned long long dup_n = 0;
   if (any_dup_) {
-    unsigned long long dup_n = 0;
-    if (!grow(23, 16, err) || !ok(hipMemsetAsync(bufs_[23], 0, 8, st), "memset(dup count)", err)) return false;
+    if (!ok(hipMemsetAsync(bufs_[23], 0, 8, st), "memset(dup count)", err)) return false;
     hipLaunchKernelGGL(filter_count_dup, dim3(blocks), dim3(kBlock), 0, st, pkg, as<const uint8_t>(bufs_[5]), n,
                        as<unsigned long long>(bufs_[23]));
     if (!ok(hipGetLastError(), "filter_count_dup", err) ||
-        !ok(hipMemcpyAsync(&dup_n, bufs_[23], 8, hipMemcpyDeviceToHost, st), "D2H dup count", err) ||
-        !ok(hipStreamSynchronize(st), "filter sync", err))
+        !ok(hipMemcpyAsync(&dup_n, bufs_[23], 8, hipMemcpyDeviceToHost, st), "D2H dup count", err))
       return false;
+  }
+  if (nr_all) {  // staging layout: rank tables, then per list subject / id / prec columns (4 B each)
+    uint32_t* h = static_cast<uint32_t*>(pin_);
+    const uint32_t* d = as<const uint32_t>(bufs_[18]);
+    uint64_t at = 0;
+    auto put = [&](const uint32_t* src, uint64_t cnt) {
+      memcpy(h + at, src, cnt * 4);
+      const uint32_t* where = d + at;
+      at += cnt;
+      return where;
+    };
+    const uint32_t* rank_dev[2] = {put(rules.rank[0].data(), rules.rank[0].size()),
+                                   put(rules.rank[1].data(), rules.rank[1].size())};
+    for (int k = 0; k < rules.n_lists; k++) {
+      const RuleList& l = rules.lists[k];
+      const bool vex = l.tag == RULE_VEX;
+      RuleDev& r = vex ? vd : rd;
+      uint64_t& cnt = vex ? nv : nr;
+      const int i = r.n_lists++;
+      r.subject[i] = l.subject ? put(l.subject, l.n) : nullptr;
+      r.id[i] = put(l.id, l.n);
+      r.prec[i] = l.prec ? put(l.prec, l.n) : nullptr;
+      r.rank[i] = rank_dev[l.table];
+      r.tag[i] = uint32_t(l.tag);
+      cnt += l.n;
+      r.end[i] = cnt;
+    }
+    if (!ok(hipMemcpyAsync(bufs_[18], pin_, at * 4, hipMemcpyHostToDevice, st), "H2D rules", err)) return false;
+  }
+  if (any_dup_) {
+    if (!ok(hipStreamSynchronize(st), "filter sync", err)) return false;
     if (dup_n) {
       tcap = 16;
       while (tcap < 2 * dup_n) tcap <<= 1;
     }
   }
-  const uint64_t nr = rules.size();
   uint64_t rcap = 0;
   if (nr) {
     rcap = 16;
@@ -630,54 +714,18 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   if (!grow(12, n * 4, err) || !grow(13, n * 4, err) || (has_ign && !grow(14, n * 4, err)) ||
       (tcap && (!grow(15, n * 4, err) || !grow(16, tcap * 16, err))) || (rcap && !grow(17, rcap * 16, err)) ||
       !grow(21, n * 8, err) || !grow(24, n, err) || !grow(25, (n / 64 + 1) * 4 * kClasses, err) ||
-      (has_ign && !grow(22, n * 12, err)) || !grow(23, std::max<uint64_t>(scan_bytes, 16), err))
+      (has_ign && !grow(22, n * 12, err)) || !grow(23, std::max<uint64_t>(scan_bytes, 16), err) ||
+      (nv && !grow(26, n, err)))
     return false;
   // per-call flags start as the static ones (FL_DUP, FL_SINGLE)
   if (np && !ok(hipMemcpyAsync(bufs_[7], bufs_[5], np, hipMemcpyDeviceToDevice, st), "D2D flags", err)) return false;
-  if (nr) {  // the rule hash set, built on the device from one pinned upload of the raw lists
-    // staging layout: rank tables, then per list subject / id / prec columns (4 B each)
-    uint64_t words = rules.rank[0].size() + rules.rank[1].size();
-    for (int k = 0; k < rules.n_lists; k++)
-      words += rules.lists[k].n * (1 + (rules.lists[k].subject ? 1 : 0) + (rules.lists[k].prec ? 1 : 0));
-    if (pin_cap_ < words * 4) {
-      if (pin_) (void)hipHostFree(pin_);
-      pin_ = nullptr;
-      pin_cap_ = 0;
-      if (!ok(hipHostMalloc(&pin_, words * 4, hipHostMallocDefault), "hipHostMalloc(filter rules)", err)) return false;
-      pin_cap_ = words * 4;
-    }
-    if (!grow(18, words * 4, err)) return false;
-    uint32_t* h = static_cast<uint32_t*>(pin_);
-    const uint32_t* d = as<const uint32_t>(bufs_[18]);
-    uint64_t at = 0;
-    auto put = [&](const uint32_t* src, uint64_t cnt) {
-      memcpy(h + at, src, cnt * 4);
-      const uint32_t* where = d + at;
-      at += cnt;
-      return where;
-    };
-    const uint32_t* rank_dev[2] = {put(rules.rank[0].data(), rules.rank[0].size()),
-                                   put(rules.rank[1].data(), rules.rank[1].size())};
-    RuleDev rd{};
-    rd.n_lists = rules.n_lists;
-    uint64_t end = 0;
-    for (int k = 0; k < rules.n_lists; k++) {
-      const RuleList& l = rules.lists[k];
-      rd.subject[k] = l.subject ? put(l.subject, l.n) : nullptr;
-      rd.id[k] = put(l.id, l.n);
-      rd.prec[k] = l.prec ? put(l.prec, l.n) : nullptr;
-      rd.rank[k] = rank_dev[l.table];
-      rd.tag[k] = uint32_t(l.tag);
-      end += l.n;
-      rd.end[k] = end;
-    }
-    if (!ok(hipMemcpyAsync(bufs_[18], pin_, words * 4, hipMemcpyHostToDevice, st), "H2D rules", err) ||
-        !ok(hipMemsetAsync(bufs_[17], 0xFF, rcap * 16, st), "memset(rules)", err))
-      return false;
+  if (nr) {  // the rule hash set, built on the device
+    if (!ok(hipMemsetAsync(bufs_[17], 0xFF, rcap * 16, st), "memset(rules)", err)) return false;
     hipLaunchKernelGGL(rules_insert, dim3(uint32_t((nr + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, rd,
                        as<unsigned long long>(bufs_[17]), rcap - 1, as<uint8_t>(bufs_[7]));
     if (!ok(hipGetLastError(), "rules_insert", err)) return false;
   }
+  if (nv && !ok(hipMemsetAsync(bufs_[26], 0, n, st), "memset(vex marks)", err)) return false;
   if (rules.pkg_class &&
       !ok(hipMemcpyAsync(bufs_[20], rules.pkg_class, np * 4, hipMemcpyHostToDevice, st), "H2D classes", err))
     return false;
@@ -712,7 +760,7 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   a.wcarry = as<uint32_t>(bufs_[25]);
   a.rules = as<const unsigned long long>(bufs_[17]);
   a.rule_mask = rcap ? rcap - 1 : 0;
-  a.kinds = rules.kinds;
+  a.kinds = nv ? rules.kinds : rules.kinds & ~(1u << RULE_VEX);  // (empty VEX lists: nothing to test)
   a.table = as<unsigned long long>(bufs_[16]);
   a.table_mask = tcap ? tcap - 1 : 0;
   a.sev_mask = sev_mask;
@@ -720,7 +768,11 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   a.id_bits = id_bits;
   a.out = as<uint2>(bufs_[21]);
   a.iout = as<uint32_t>(bufs_[22]);
+  a.vx = as<const uint8_t>(bufs_[26]);
   hipLaunchKernelGGL(filter_mark, dim3(blocks_u), dim3(kBlock), 0, st, a);
+  if (nv) hipLaunchKernelGGL(vex_mark, dim3(uint32_t((nv + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, vd, pkg, side,
+                             as<const uint32_t>(bufs_[8]), as<const uint32_t>(bufs_[9]), as<const uint8_t>(bufs_[7]), n,
+                             as<uint8_t>(bufs_[26]));
   hipLaunchKernelGGL(filter_select, dim3(blocks_u), dim3(kBlock), 0, st, a);
   hipLaunchKernelGGL(filter_count, dim3(blocks), dim3(kBlock), 0, st, a);
   if (!ok(hipGetLastError(), "filter launch", err) ||

@@ -89,7 +89,6 @@ struct FusedArgs {
   CopyOutArgs co;       // end-to-end pipeline: the previous chunk's result move ...
   uint32_t n_copy = 0;  // ... by workgroups [0, n_copy) of this launch (0: none)
 };
-constexpr uint32_t kCopyWorkgroups = 128;  // PCIe-bound: a few workgroups, the tiles keep the rest
 
 using ProbeFn = void (*)(uint32_t n_tiles, hipStream_t st, const ProbeArgs& a);
 using SweepFn = void (*)(uint32_t n_tiles, hipStream_t st, const SweepArgs& a);
@@ -820,7 +819,8 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
   uint8_t* map = u.sw.map;
   const ProbeArgs& a = fa.pa;
   if (blockIdx.x < fa.n_copy) {  // pipeline: the previous chunk's result move, dispatched first so the link writes overlap the tiles
-    copy_out_range(fa.co, uint64_t(blockIdx.x) * kTile + threadIdx.x, uint64_t(fa.n_copy) * kTile);
+    static_assert(sizeof(buf) >= kCopyLdsWords * 4, "the result move borrows the staging buffer");
+    copy_out_tiles(fa.co, blockIdx.x, fa.n_copy, reinterpret_cast<uint32_t*>(buf));
     return;
   }
   const uint32_t tid = threadIdx.x, t = blockIdx.x - fa.n_copy;

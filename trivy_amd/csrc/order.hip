@@ -84,8 +84,9 @@ __global__ __launch_bounds__(kTile) void order_kernel(OrderArgs a) {
   if (p < a.n) a.row_end[p] = uint32_t(b + off + x);
 }
 
-__global__ __launch_bounds__(256) void copy_out_kernel(CopyOutArgs a) {
-  copy_out_range(a, uint64_t(blockIdx.x) * blockDim.x + threadIdx.x, uint64_t(gridDim.x) * blockDim.x);
+__global__ __launch_bounds__(kTile) void copy_out_kernel(CopyOutArgs a) {
+  __shared__ uint32_t lds[kCopyLdsWords];
+  copy_out_tiles(a, blockIdx.x, gridDim.x, lds);
 }
 
 }  // namespace
@@ -95,7 +96,7 @@ void launch_order(uint32_t n_tiles, hipStream_t st, const OrderArgs& a) {
 }
 
 void launch_copy_out(hipStream_t st, const CopyOutArgs& a) {
-  hipLaunchKernelGGL(copy_out_kernel, dim3(256), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(copy_out_kernel, dim3(kCopyWorkgroups), dim3(kTile), 0, st, a);
 }
 
 

@@ -22,17 +22,17 @@ struct OrderArgs {
   uint32_t pkg_base = 0;       // added to every package index the match kernels wrote (a shard's first package)
 };
 void launch_order(uint32_t n_tiles, hipStream_t st, const OrderArgs& a);
-void launch_copy_out(hipStream_t st, const CopyOutArgs& a);  // engine.h copy_out_range as its own kernel
+void launch_copy_out(hipStream_t st, const CopyOutArgs& a);  // engine.h copy_out_tiles as its own kernel
 
 
 // One batch's pipeline state.  prepare() pins the batch's host arrays (hipHostRegister),
 // sizes the device batch, the match buffers and the pinned result buffers; run() then
 // streams the batch through in chunks of whole tiles:
 //   copy stream    DMA of chunk c to HBM (package words, tile offsets, string bytes, attributes);
-//   kernel stream  (after chunk c's upload) one match launch whose first workgroups move chunk
-//                  c-1's result into the pinned host result (engine.h CopyOutArgs: 16-byte
-//                  kernel stores, the link's other direction, range read on the device) while
-//                  the rest match chunk c; then order_kernel over chunk c (CSR in HBM);
+//   kernel stream  (after chunk c's upload) one match launch whose first workgroups turn
+//                  chunk c-1's match segments into the pinned host CSR (engine.h
+//                  copy_out_tiles: 16-byte kernel stores, the link's other direction) while
+//                  the rest match chunk c;
 // so chunk c+1's upload and chunk c-1's result move run under chunk c's matching, and the
 // host waits once, at the end.  (Measured alternatives, DESIGN.md §7: a DMA device-to-host
 // copy runs at half the rate of kernel stores, and a result kernel on its own stream did
@@ -40,7 +40,9 @@ void launch_copy_out(hipStream_t st, const CopyOutArgs& a);  // engine.h copy_ou
 class Pipeline {
  public:
   ~Pipeline();
-  bool prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uint32_t chunk_packages, std::string& err);
+  // transport: send the batch in its transport form when it has one (see build_wire)
+  bool prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uint32_t chunk_packages, bool transport,
+               std::string& err);
   // One pass.  total = matches (> match_cap: nothing valid, re-prepare with a larger cap);
   // err_pkg = first poisoned package or -1.
   bool run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& err_pkg, uint64_t& err_bits, std::string& err);
@@ -50,9 +52,30 @@ class Pipeline {
   uint64_t h2d_bytes() const { return h2d_; }
   uint64_t d2h_bytes() const { return d2h_; }
   uint32_t chunks() const { return uint32_t(bounds_.size() - 1); }
+  bool transport_form() const { return !wc_.empty(); }
+  uint64_t encode_us() const { return encode_us_; }
 
  private:
   void release();
+  // The batch's transport form (pinned wire_h_, mirrored at the same offsets in wire_d_):
+  // per chunk one contiguous block {name ref u32, version ref u32, lengths u16 (name | version
+  // << 8), platform index u8 per package; the chunk's group offsets (u64, the arena's
+  // tile_off); attributes (uint2) when the batch has them; the bytes of the names and
+  // versions first seen in this chunk}.  A reference is the wire offset of the string's
+  // first occurrence, so a repeated name or version crosses the link once; unpack_kernel
+  // rebuilds the chunk's pk / tile_off / arena / attr in HBM.  false (wc_ empty): no
+  // transport form (a string of 256 bytes or more, more than 255 platforms, or 4 GiB).
+  bool build_wire(const HostBatch& hb, std::string& err);
+  struct WireChunk {
+    uint64_t off = 0, bytes = 0;                          // block in wire_h_ / wire_d_
+    uint64_t o_nref = 0, o_vref = 0, o_lens = 0, o_plat = 0, o_toff = 0, o_attr = 0;  // section offsets (absolute)
+    uint32_t m = 0, groups = 0;                           // packages, 64-package groups (whole tiles)
+  };
+  std::vector<WireChunk> wc_;
+  uint8_t* wire_h_ = nullptr;
+  uint8_t* wire_d_ = nullptr;
+  uint32_t* ptab_d_ = nullptr;  // platform index -> platform id
+  uint64_t encode_us_ = 0;
   int dev_ = -1;
   hipStream_t s_h2d_ = nullptr, s_k_ = nullptr;
   std::vector<hipEvent_t> ev_h_;
@@ -61,12 +84,9 @@ class Pipeline {
   std::vector<void*> registered_;
   DevBatch db_;
   DevMatches m_;
-  unsigned long long* status_d_ = nullptr;
-  unsigned long long* tickets_d_ = nullptr;
+  unsigned long long* chunk_base_d_ = nullptr;  // chunk c's first CSR position (written by chunk c-1's move)
   uint32_t* adv_h_ = nullptr;
   uint32_t* row_end_h_ = nullptr;
-  uint32_t* csr_adv_d_ = nullptr;   // device CSR (order_kernel)
-  uint32_t* row_end_d_ = nullptr;
   uint32_t* adv_hd_ = nullptr;      // device addresses of adv_h_ / row_end_h_ (result-move stores)
   uint32_t* row_end_hd_ = nullptr;
   unsigned long long* ctl_h_ = nullptr;

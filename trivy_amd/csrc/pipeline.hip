@@ -4,7 +4,11 @@
 #include "pipeline.h"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <unordered_map>
 
 namespace tvm {
 
@@ -16,7 +20,176 @@ bool ok(hipError_t e, const char* what, std::string& err) {
   return false;
 }
 
+uint64_t align16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
+
+__device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ d, const uint8_t* __restrict__ s, uint32_t n) {
+  for (uint32_t k = 0; k < n; k += 8) {
+    uint8_t t[8];
+#pragma unroll
+    for (uint32_t u = 0; u < 8; u++) t[u] = k + u < n ? s[k + u] : 0;
+#pragma unroll
+    for (uint32_t u = 0; u < 8; u++)
+      if (k + u < n) d[k + u] = t[u];
+  }
+}
+
+struct UnpackArgs {
+  const uint8_t* wire;
+  const uint32_t* nref;
+  const uint32_t* vref;
+  const uint16_t* lens;
+  const uint8_t* plat;
+  const uint64_t* toff;
+  const uint2* attr_in;
+  const uint32_t* ptab;
+  uint2* pk;
+  uint64_t* tile_off;
+  uint8_t* arena;
+  uint2* attr;
+  uint32_t p0, m, g0, groups;
+};
+
+// One chunk of the transport form -> the batch's own arrays in HBM (pk, tile_off, arena,
+// attr: exactly what a raw upload would have put there).  One wavefront per 64-package
+// group: the group's arena offset comes with the chunk, each package's offset within it is
+// a wave scan of the lengths, and every lane copies its name and version bytes from their
+// first occurrence in the wire buffer.
+__global__ __launch_bounds__(256) void unpack_kernel(UnpackArgs a) {
+  const uint32_t lane = threadIdx.x & 63, gl = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gl >= a.groups) return;  // whole wavefronts
+  const uint32_t i = gl * 64 + lane;
+  uint32_t nl = 0, vl = 0, nr = 0, vr = 0;
+  if (i < a.m) {
+    const uint32_t ln = a.lens[i];
+    nl = ln & 255u;
+    vl = ln >> 8;
+    nr = a.nref[i];
+    vr = a.vref[i];
+    a.pk[a.p0 + i] = make_uint2(a.ptab[a.plat[i]], nl | (vl << 16));
+    if (a.attr) a.attr[a.p0 + i] = a.attr_in[i];
+  }
+  const uint64_t g_off = a.toff[gl];
+  if (lane == 0) {
+    a.tile_off[a.g0 + gl] = g_off;
+    if (gl + 1 == a.groups) a.tile_off[a.g0 + gl + 1] = a.toff[gl + 1];  // the next chunk's first group: read by this chunk's last tile
+  }
+  const uint32_t len = nl + vl;
+  uint32_t x = len;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= uint32_t(o)) x += y;
+  }
+  // 8 loads in flight per lane before any store (the wire and the arena never overlap)
+  uint8_t* __restrict__ d = a.arena + g_off + (x - len);
+  copy_bytes(d, a.wire + nr, nl);
+  copy_bytes(d + nl, a.wire + vr, vl);
+}
+
 }  // namespace
+
+bool Pipeline::build_wire(const HostBatch& hb, std::string& err) {
+  const auto start = std::chrono::steady_clock::now();
+  const size_t n = hb.pk.size();
+  wc_.clear();
+  if (n == 0) return true;
+  // platforms -> u8 indices
+  std::vector<uint32_t> ptab;
+  std::unordered_map<uint32_t, uint8_t> pidx;
+  for (const uint2& d : hb.pk) {
+    if ((d.y & 0xFFFFu) > 255 || (d.y >> 16) > 255) return true;  // no transport form
+    if (pidx.find(d.x) == pidx.end()) {
+      if (ptab.size() == 255) return true;
+      pidx.emplace(d.x, uint8_t(ptab.size()));
+      ptab.push_back(d.x);
+    }
+  }
+  const bool has_attr = !hb.attr.empty();
+  const uint32_t nc = chunks();
+  // upper bound of the wire size: every string new
+  uint64_t bound = 0;
+  for (uint32_t c = 0; c < nc; c++) {
+    const uint64_t m = std::min<uint64_t>(uint64_t(bounds_[c + 1]) * kTile, n) - std::min<uint64_t>(uint64_t(bounds_[c]) * kTile, n);
+    bound += 6 * 16 + m * 11 + (uint64_t(bounds_[c + 1] - bounds_[c]) * kGroupsPerTile + 1) * 8 + (has_attr ? m * 8 : 0);
+  }
+  bound += hb.arena.size() + 16;
+  if (bound >= (1ull << 32)) return true;  // references are 32-bit
+  void* p = nullptr;
+  if (!ok(hipHostMalloc(&p, bound, hipHostMallocDefault), "hipHostMalloc(transport form)", err)) return false;
+  wire_h_ = static_cast<uint8_t*>(p);
+  if (!ok(hipMalloc(&p, bound), "hipMalloc(transport form)", err)) return false;
+  wire_d_ = static_cast<uint8_t*>(p);
+  if (!ok(hipMalloc(&p, ptab.size() * 4), "hipMalloc(platform table)", err) ||
+      !ok(hipMemcpy(p, ptab.data(), ptab.size() * 4, hipMemcpyHostToDevice), "H2D platform table", err))
+    return false;
+  ptab_d_ = static_cast<uint32_t*>(p);
+  // distinct strings: open addressing over indices into `uniq` (its first arena offset,
+  // length and wire reference)
+  struct U {
+    uint64_t aoff;
+    uint32_t ref;
+    uint32_t len;
+  };
+  std::vector<U> uniq;
+  uniq.reserve(n / 2 + 16);
+  size_t cap = 16;
+  while (cap < 4 * n) cap <<= 1;
+  std::vector<uint32_t> table(cap, 0xFFFFFFFFu);
+  const uint8_t* ar = hb.arena.data();
+  uint64_t heap = 0;  // next free byte of the current chunk's string section
+  auto ref_of = [&](uint64_t aoff, uint32_t len) -> uint32_t {
+    if (len == 0) return 0;
+    uint64_t h = 1469598103934665603ull;
+    for (uint32_t k = 0; k < len; k++) h = (h ^ ar[aoff + k]) * 1099511628211ull;
+    h ^= h >> 29;
+    for (size_t slot = size_t(h) & (cap - 1);; slot = (slot + 1) & (cap - 1)) {
+      const uint32_t u = table[slot];
+      if (u == 0xFFFFFFFFu) {
+        table[slot] = uint32_t(uniq.size());
+        std::memcpy(wire_h_ + heap, ar + aoff, len);
+        uniq.push_back({aoff, uint32_t(heap), len});
+        heap += len;
+        return uint32_t(heap - len);
+      }
+      const U& e = uniq[u];
+      if (e.len == len && std::memcmp(ar + e.aoff, ar + aoff, len) == 0) return e.ref;
+    }
+  };
+  uint64_t pos = 0, aoff = 0;
+  for (uint32_t c = 0; c < nc; c++) {
+    WireChunk w;
+    const size_t p0 = std::min<size_t>(size_t(bounds_[c]) * kTile, n), p1 = std::min<size_t>(size_t(bounds_[c + 1]) * kTile, n);
+    w.m = uint32_t(p1 - p0);
+    w.groups = (bounds_[c + 1] - bounds_[c]) * kGroupsPerTile;
+    w.off = pos;
+    w.o_nref = pos;
+    w.o_vref = align16(w.o_nref + 4ull * w.m);
+    w.o_lens = align16(w.o_vref + 4ull * w.m);
+    w.o_plat = align16(w.o_lens + 2ull * w.m);
+    w.o_toff = align16(w.o_plat + w.m);
+    w.o_attr = align16(w.o_toff + 8ull * (w.groups + 1));
+    heap = align16(w.o_attr + (has_attr ? 8ull * w.m : 0));
+    auto* nref = reinterpret_cast<uint32_t*>(wire_h_ + w.o_nref);
+    auto* vref = reinterpret_cast<uint32_t*>(wire_h_ + w.o_vref);
+    auto* lens = reinterpret_cast<uint16_t*>(wire_h_ + w.o_lens);
+    uint8_t* pl = wire_h_ + w.o_plat;
+    for (size_t i = p0; i < p1; i++) {
+      const uint32_t nl = hb.pk[i].y & 0xFFFFu, vl = hb.pk[i].y >> 16;
+      nref[i - p0] = ref_of(aoff, nl);
+      vref[i - p0] = ref_of(aoff + nl, vl);
+      lens[i - p0] = uint16_t(nl | (vl << 8));
+      pl[i - p0] = pidx[hb.pk[i].x];
+      aoff += nl + vl;
+    }
+    std::memcpy(wire_h_ + w.o_toff, toff_.data() + size_t(bounds_[c]) * kGroupsPerTile, 8ull * (w.groups + 1));
+    if (has_attr) std::memcpy(wire_h_ + w.o_attr, hb.attr.data() + p0, 8ull * w.m);
+    pos = align16(heap);
+    w.bytes = pos - w.off;
+    wc_.push_back(w);
+  }
+  encode_us_ = uint64_t(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - start).count());
+  return true;
+}
 
 Pipeline::~Pipeline() { release(); }
 
@@ -27,9 +200,14 @@ void Pipeline::release() {
   if (s_h2d_) (void)hipStreamSynchronize(s_h2d_);
   Engine::free_batch(dev_, db_);
   Engine::free_matches(dev_, m_);
-  for (void* p : {static_cast<void*>(csr_adv_d_), static_cast<void*>(row_end_d_), static_cast<void*>(status_d_),
-                  static_cast<void*>(tickets_d_)})
+  for (void* p : {static_cast<void*>(chunk_base_d_), static_cast<void*>(wire_d_), static_cast<void*>(ptab_d_)})
     if (p) (void)hipFree(p);
+  if (wire_h_) (void)hipHostFree(wire_h_);
+  wire_h_ = nullptr;
+  wire_d_ = nullptr;
+  ptab_d_ = nullptr;
+  wc_.clear();
+  encode_us_ = 0;
   for (void* p : {static_cast<void*>(adv_h_), static_cast<void*>(row_end_h_), static_cast<void*>(ctl_h_)})
     if (p) (void)hipHostFree(p);
   for (void* p : registered_) (void)hipHostUnregister(p);
@@ -40,15 +218,14 @@ void Pipeline::release() {
     if (s) (void)hipStreamDestroy(s);
   s_h2d_ = s_k_ = nullptr;
   adv_hd_ = row_end_hd_ = nullptr;
-  csr_adv_d_ = row_end_d_ = nullptr;
-  status_d_ = tickets_d_ = nullptr;
+  chunk_base_d_ = nullptr;
   adv_h_ = row_end_h_ = nullptr;
   ctl_h_ = nullptr;
   prepared_ = false;
   dev_ = -1;
 }
 
-bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uint32_t chunk_packages,
+bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uint32_t chunk_packages, bool transport,
                        std::string& err) {
   release();
 
@@ -81,8 +258,10 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
     registered_.push_back(const_cast<void*>(p));
     return true;
   };
-  if (!reg(hb.pk.data(), hb.pk.size() * sizeof(uint2)) || !reg(hb.arena.data(), hb.arena.size()) ||
-      !reg(toff_.data(), toff_.size() * 8) || !reg(hb.attr.data(), hb.attr.size() * sizeof(uint2)))
+  if (transport && !build_wire(hb, err)) return false;
+  if (wc_.empty() &&
+      (!reg(hb.pk.data(), hb.pk.size() * sizeof(uint2)) || !reg(hb.arena.data(), hb.arena.size()) ||
+       !reg(toff_.data(), toff_.size() * 8) || !reg(hb.attr.data(), hb.attr.size() * sizeof(uint2))))
     return false;
   if (!eng.alloc_batch(hb, db_, err) || !eng.alloc_matches(cap_, db_.n, m_, err)) return false;
   if (!hb.cpe_bits.empty() && hb.cpe_words) {  // CPE sets: small, copied once here
@@ -94,18 +273,11 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
     db_.cpe_words = hb.cpe_words;
     db_.n_cpe_sets = uint32_t(hb.cpe_bits.size() / hb.cpe_words);
   }
-  const size_t n = std::max<size_t>(hb.pk.size(), 1);
   // CSR buffers padded to whole 16-byte units (the result move copies units)
   const size_t cap4 = (cap_ + 3) & ~size_t(3), n4 = (size_t(n_tiles) * kTile + 3) & ~size_t(3);
   void* p = nullptr;
-  if (!ok(hipMalloc(&p, cap4 * 4), "hipMalloc(csr)", err)) return false;
-  csr_adv_d_ = static_cast<uint32_t*>(p);
-  if (!ok(hipMalloc(&p, std::max<size_t>(n4, 4) * 4), "hipMalloc(row ends)", err)) return false;
-  row_end_d_ = static_cast<uint32_t*>(p);
-  if (!ok(hipMalloc(&p, std::max<size_t>(n_tiles, 1) * 8), "hipMalloc(status)", err)) return false;
-  status_d_ = static_cast<unsigned long long*>(p);
-  if (!ok(hipMalloc(&p, std::max<size_t>(nc, 1) * 8), "hipMalloc(tickets)", err)) return false;
-  tickets_d_ = static_cast<unsigned long long*>(p);
+  if (!ok(hipMalloc(&p, (size_t(nc) + 1) * 8), "hipMalloc(chunk bases)", err)) return false;
+  chunk_base_d_ = static_cast<unsigned long long*>(p);
   // the result lives in pinned host memory that the result move writes directly over PCIe
   // (measured, profiles/r03/pcie_probe.txt: kernel stores to host memory 55 GB/s, a DMA
   // device-to-host copy 28.6 GB/s; the DMA engine then only carries the batch upward)
@@ -137,24 +309,41 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
   const uint32_t nc = chunks();
   const uint32_t n = db_.n;
   if (!ok(hipMemsetAsync(m_.ctl, 0, 64, s_k_), "memset(ctl)", err) ||
-      !ok(hipMemsetAsync(status_d_, 0, std::max<size_t>(db_.n_tiles, 1) * 8, s_k_), "memset(status)", err) ||
-      !ok(hipMemsetAsync(tickets_d_, 0, std::max<size_t>(nc, 1) * 8, s_k_), "memset(tickets)", err))
+      !ok(hipMemsetAsync(chunk_base_d_, 0, 8, s_k_), "memset(chunk base)", err))
     return false;
   // Per chunk: its upload on the copy stream; behind it, on the kernel stream, one match
-  // launch whose first workgroups move the previous chunk's result out, then the order
-  // kernel.  All work is queued up front (measured: the calls never block); the host waits
-  // once, at the end.
+  // launch whose first workgroups move the previous chunk's result out (engine.h
+  // copy_out_tiles: tile directory -> host CSR).  All work is queued up front (measured: the
+  // calls never block); the host waits once, at the end.
   auto copy_args = [&](uint32_t c) {
     CopyOutArgs ca;
-    ca.row_end = row_end_d_;
-    ca.csr_adv = csr_adv_d_;
-    ca.row_end_h = reinterpret_cast<uint4*>(row_end_hd_);
-    ca.adv_h = reinterpret_cast<uint4*>(adv_hd_);
-    ca.p0 = bounds_[c] * kTile;
-    ca.p1 = std::min<uint32_t>(bounds_[c + 1] * kTile, n);
+    ca.dir = m_.dir;
+    ca.pkg = m_.pkg;
+    ca.adv = m_.adv;
+    ca.row_end_h = row_end_hd_;
+    ca.adv_h = adv_hd_;
+    ca.chunk_base = chunk_base_d_;
+    ca.c = c;
+    ca.t0 = bounds_[c];
+    ca.t1 = bounds_[c + 1];
+    ca.pkg_base = db_.pkg_base;
     ca.cap = cap_;
     return ca;
   };
+  // measurement only: TVM_PIPE_TRACE=1 prints the host time spent in each call of a pass;
+  // TVM_PIPE_COPIES_FIRST=1 queues every chunk's upload before any kernel
+  static const bool trace = std::getenv("TVM_PIPE_TRACE") != nullptr;
+  static const bool copies_first = std::getenv("TVM_PIPE_COPIES_FIRST") != nullptr;
+  const auto T0 = std::chrono::steady_clock::now();
+  auto us = [&]() { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - T0).count(); };
+  if (copies_first && !wc_.empty())
+    for (uint32_t c = 0; c < nc; c++) {
+      const WireChunk& w = wc_[c];
+      if (!ok(hipMemcpyAsync(wire_d_ + w.off, wire_h_ + w.off, w.bytes, hipMemcpyHostToDevice, s_h2d_), "H2D chunk", err) ||
+          !ok(hipEventRecord(ev_h_[c], s_h2d_), "hipEventRecord", err))
+        return false;
+      if (trace) std::fprintf(stderr, "pipe c%u copy queued %.1f us\n", c, us());
+    }
   int64_t prev = -1;  // the last chunk matched, whose result has not been moved yet
   for (uint32_t c = 0; c < nc; c++) {
     const uint32_t t0 = bounds_[c], t1 = bounds_[c + 1];
@@ -162,7 +351,37 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
     const size_t p0 = size_t(t0) * kTile, p1 = std::min<size_t>(size_t(t1) * kTile, n);
     const size_t g0 = size_t(t0) * kGroupsPerTile, g1 = size_t(t1) * kGroupsPerTile;
     const uint64_t a0 = toff_[g0], a1 = toff_[g1];
-    if (!ok(hipMemcpyAsync(db_.pk + p0, hb.pk.data() + p0, (p1 - p0) * sizeof(uint2), hipMemcpyHostToDevice, s_h2d_),
+    if (!wc_.empty()) {  // transport form: one DMA, then the chunk is rebuilt in HBM
+      const WireChunk& w = wc_[c];
+      if (!copies_first &&
+          (!ok(hipMemcpyAsync(wire_d_ + w.off, wire_h_ + w.off, w.bytes, hipMemcpyHostToDevice, s_h2d_), "H2D chunk", err) ||
+           !ok(hipEventRecord(ev_h_[c], s_h2d_), "hipEventRecord", err)))
+        return false;
+      if (trace) std::fprintf(stderr, "pipe c%u copy %.1f us\n", c, us());
+      if (!ok(hipStreamWaitEvent(s_k_, ev_h_[c], 0), "hipStreamWaitEvent", err)) return false;
+      if (trace) std::fprintf(stderr, "pipe c%u wait %.1f us\n", c, us());
+      h2d_ += w.bytes;
+      UnpackArgs ua;
+      ua.wire = wire_d_;
+      ua.nref = reinterpret_cast<const uint32_t*>(wire_d_ + w.o_nref);
+      ua.vref = reinterpret_cast<const uint32_t*>(wire_d_ + w.o_vref);
+      ua.lens = reinterpret_cast<const uint16_t*>(wire_d_ + w.o_lens);
+      ua.plat = wire_d_ + w.o_plat;
+      ua.toff = reinterpret_cast<const uint64_t*>(wire_d_ + w.o_toff);
+      ua.attr_in = reinterpret_cast<const uint2*>(wire_d_ + w.o_attr);
+      ua.ptab = ptab_d_;
+      ua.pk = db_.pk;
+      ua.tile_off = db_.tile_off;
+      ua.arena = db_.arena;
+      ua.attr = hb.attr.empty() ? nullptr : db_.attr;
+      ua.p0 = uint32_t(p0);
+      ua.m = w.m;
+      ua.g0 = uint32_t(g0);
+      ua.groups = w.groups;
+      hipLaunchKernelGGL(unpack_kernel, dim3((w.groups + 3) / 4), dim3(256), 0, s_k_, ua);
+      if (!ok(hipGetLastError(), "unpack kernel launch", err)) return false;
+      if (trace) std::fprintf(stderr, "pipe c%u unpack %.1f us\n", c, us());
+    } else if (!ok(hipMemcpyAsync(db_.pk + p0, hb.pk.data() + p0, (p1 - p0) * sizeof(uint2), hipMemcpyHostToDevice, s_h2d_),
             "H2D packages", err) ||
         !ok(hipMemcpyAsync(db_.tile_off + g0, toff_.data() + g0, (g1 - g0 + 1) * 8, hipMemcpyHostToDevice, s_h2d_),
             "H2D group offsets", err) ||
@@ -172,34 +391,24 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
          !ok(hipMemcpyAsync(db_.attr + p0, hb.attr.data() + p0, (p1 - p0) * sizeof(uint2), hipMemcpyHostToDevice, s_h2d_),
              "H2D attributes", err)) ||
         !ok(hipEventRecord(ev_h_[c], s_h2d_), "hipEventRecord", err) ||
-        !ok(hipStreamWaitEvent(s_k_, ev_h_[c], 0), "hipStreamWaitEvent", err))
+        !ok(hipStreamWaitEvent(s_k_, ev_h_[c], 0), "hipStreamWaitEvent", err)) {
       return false;
-    h2d_ += (p1 - p0) * sizeof(uint2) + (g1 - g0 + 1) * 8 + (a1 - a0) + (hb.attr.empty() ? 0 : (p1 - p0) * sizeof(uint2));
+    } else {
+      h2d_ += (p1 - p0) * sizeof(uint2) + (g1 - g0 + 1) * 8 + (a1 - a0) + (hb.attr.empty() ? 0 : (p1 - p0) * sizeof(uint2));
+    }
     const CopyOutArgs prev_co = prev >= 0 ? copy_args(uint32_t(prev)) : CopyOutArgs{};
     if (!eng.launch_tiles(db_, m_, t0, t1, s_k_, s_k_, nullptr, err, prev >= 0 ? &prev_co : nullptr)) return false;
-    OrderArgs oa;
-    oa.dir = m_.dir;
-    oa.pkg = m_.pkg;
-    oa.adv = m_.adv;
-    oa.csr_adv = csr_adv_d_;
-    oa.row_end = row_end_d_;
-    oa.cap = cap_;
-    oa.status = status_d_;
-    oa.ticket = tickets_d_ + c;
-    oa.t0 = t0;
-    oa.n = n;
-    oa.pkg_base = db_.pkg_base;
-    launch_order(t1 - t0, s_k_, oa);
-    if (!ok(hipGetLastError(), "order kernel launch", err)) return false;
+    if (trace) std::fprintf(stderr, "pipe c%u match %.1f us\n", c, us());
     prev = c;
   }
   if (prev >= 0) {
     launch_copy_out(s_k_, copy_args(uint32_t(prev)));
     if (!ok(hipGetLastError(), "copy-out kernel launch", err)) return false;
   }
-  if (!ok(hipMemcpyAsync(ctl_h_, m_.ctl, 64, hipMemcpyDeviceToHost, s_k_), "D2H ctl", err) ||
-      !ok(hipStreamSynchronize(s_k_), "pipeline", err))
-    return false;
+  if (!ok(hipMemcpyAsync(ctl_h_, m_.ctl, 64, hipMemcpyDeviceToHost, s_k_), "D2H ctl", err)) return false;
+  if (trace) std::fprintf(stderr, "pipe ctl queued %.1f us\n", us());
+  if (!ok(hipStreamSynchronize(s_k_), "pipeline", err)) return false;
+  if (trace) std::fprintf(stderr, "pipe done %.1f us\n", us());
   d2h_ = uint64_t(n) * 4 + std::min<uint64_t>(ctl_h_[0], cap_) * 4;
   total = ctl_h_[0];
   err_pkg = ctl_h_[1] ? int64_t(n - ctl_h_[1]) : -1;
