@@ -309,6 +309,11 @@ def test_match_filter_batch_vex_vs_oracle(kind):
     assert dropped > 0
     assert len(got) == len(want), (len(got), len(want))
     assert got == [list(w["_pair"]) for w in want]
+    # a statement naming a package the batch does not have is refused (checked on the device)
+    bad = (np.concatenate([np.asarray(sup[0], dtype=np.uint32), [len(mb)]]), list(sup[1]) + [sup[1][0]])
+    with pytest.raises(RuntimeError, match="out of range"):
+        mb.filter(mb.filter_opts(vex=bad, **opts))
+    assert mb.filter(mb.filter_opts(vex=sup, **opts)) == n
     mb.close()
 
 

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -1102,6 +1103,7 @@ void package_layout(const tvm_batch* b, FilterPackages& fp) {
 
 int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint64_t* n_kept, uint64_t* n_ignored,
                      char* err, size_t errlen) {
+  const auto t_call = std::chrono::steady_clock::now();
   if (!e || !b || !o || !b->uploaded || (o->n_vex && (!o->vex_pkgs || !o->vex_id_index)) ||
       (o->n_vex_ids && !o->vex_ids && !o->vex_id_ranks))
     return TVM_EINVAL;
@@ -1162,7 +1164,8 @@ int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint
   auto list = [&](uint64_t tag, const uint32_t* subject, uint64_t subject_limit, const uint32_t* id, const uint32_t* prec,
                   size_t k, int table) {
     if (!k) return;
-    good &= below(id, k, rules.rank[table].size()) && (!subject || below(subject, k, subject_limit));
+    if (tag != RULE_VEX)  // VEX statements (the long lists) are checked by the kernel that applies them
+      good &= below(id, k, rules.rank[table].size()) && (!subject || below(subject, k, subject_limit));
     RuleList& l = rules.lists[rules.n_lists++];
     l.tag = tag;
     l.subject = subject;
@@ -1191,10 +1194,13 @@ int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint
     set_err(err, errlen, "tvm_match_filter: rule / VEX package, class or ID index out of range");
     return TVM_EINVAL;
   }
+  if (std::getenv("TVM_FILTER_TRACE"))
+    std::fprintf(stderr, "filter C-ABI prologue %.1f us\n",
+                 std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_call).count());
   if (!b->filter.run(e->fill->dev(), cur(b).pkg, cur(b).adv, b->fill_side(), n, rules, vt.n_vuln_ranks(), o->severity_mask,
                      o->ignore_status_mask, st, msg)) {
     set_err(err, errlen, msg);
-    return TVM_EDEVICE;
+    return msg.find("out of range") != std::string::npos ? TVM_EINVAL : TVM_EDEVICE;
   }
   if (n_kept) *n_kept = b->filter.survivors();
   if (n_ignored) *n_ignored = b->filter.ignored();

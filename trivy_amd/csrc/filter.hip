@@ -46,6 +46,10 @@
 
 #include <algorithm>
 #include <cstring>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <thread>
 
 #include "vulninfo.h"
 
@@ -99,7 +103,6 @@ struct FilterArgs {
   uint8_t* pcls;   // after filter_select: the pair's counter class (pair_class)
   uint32_t* wcarry;  // after filter_count, per 64-pair wave w entered by a run begun earlier:
                      //   the run's class counts before pair 64w (kClasses each)
-  const uint8_t* vx;  // per pair: a VEX statement names its (package, ID) (vex_mark)
   // tables
   const unsigned long long* rules;  // {key, precedence} x 2^k
   uint64_t rule_mask;
@@ -174,30 +177,40 @@ __global__ __launch_bounds__(kBlock) void rules_insert(RuleDev r, unsigned long 
   }
 }
 
-// VEX statements (package, ID) applied to the pairs directly: each statement finds its
-// package's run of the list (filter_mark's run_b / run_e; the list is grouped by package),
-// bisects it for the ID (runs are ID-sorted unless FL_UNS) and marks that pair, so
-// filter_select tests one byte per pair instead of probing a hash set.  run_b of a package
-// without pairs is stale: a start is taken only where it really is the first pair of that
-// package.
+// VEX (applied after the dedup, to survivors, as filter.go:51-53 does): each statement
+// finds its package's run of the list (filter_mark's run_b / run_e; the list is grouped by
+// package), bisects it for the ID (runs are ID-sorted unless FL_UNS) and drops that pair if
+// filter_select kept it - no hash probe per survivor.  run_b of a package without pairs is
+// stale: a start is taken only where it really is the first pair of that package.  The
+// statements' indices are checked here rather than by a host scan before the call (*bad).
 __global__ __launch_bounds__(kBlock) void vex_mark(RuleDev r, const uint32_t* pkg, const uint2* side,
                                                    const uint32_t* run_b, const uint32_t* run_e, const uint8_t* fl,
-                                                   uint64_t n, uint8_t* vx) {
+                                                   uint64_t n, uint32_t n_pkgs, uint32_t n_ids, uint32_t* skey,
+                                                   uint8_t* pcls, uint32_t* bad) {
   const uint64_t g = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
   int k = 0;
   while (k < r.n_lists && g >= r.end[k]) k++;
   if (k == r.n_lists) return;
   const uint64_t e = g - (k ? r.end[k - 1] : 0);
-  const uint32_t rank = r.rank[k][r.id[k][e]];
+  const uint32_t idx = r.id[k][e], p = r.subject[k][e];
+  if (idx >= n_ids || p >= n_pkgs) {
+    atomicOr(bad, 1u);
+    return;
+  }
+  const uint32_t rank = r.rank[k][idx];
   if (rank == kEmpty) return;
-  if (!r.subject[k]) return;
-  const uint32_t p = r.subject[k][e];
   const uint32_t rb = run_b[p];
   if (rb >= n || pkg[rb] != p || (rb && pkg[rb - 1] == p)) return;  // no pairs (stale start)
   const uint32_t re = run_e[p];  // written by this call's filter_mark, as rb was
+  auto drop = [&](uint32_t j) {
+    if (skey[j] != kEmpty) {  // a survivor (so not ignored): it leaves every counter class
+      skey[j] = kEmpty;
+      pcls[j] = uint8_t(kNoClass);
+    }
+  };
   if (fl[p] & FL_UNS) {  // IDs not increasing along the run (two data sources of one ID): every pair
     for (uint32_t j = rb; j < re; j++)
-      if (side[j].x == rank) vx[j] = 1;
+      if (side[j].x == rank) drop(j);
     return;
   }
   uint32_t lo = rb, hi = re;  // strictly increasing IDs: the one pair, by bisection (runs can be thousands long)
@@ -206,7 +219,7 @@ __global__ __launch_bounds__(kBlock) void vex_mark(RuleDev r, const uint32_t* pk
     if (side[mid].x < rank) lo = mid + 1;
     else hi = mid;
   }
-  if (lo < re && side[lo].x == rank) vx[lo] = 1;
+  if (lo < re && side[lo].x == rank) drop(lo);
 }
 
 // Pairs per thread per step of the streaming kernels: every lane issues the loads of kU
@@ -314,8 +327,6 @@ __global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
               }
             }
           }
-          if (key != kEmpty && (a.kinds & (1u << RULE_VEX)) && a.vx[i])
-            key = kEmpty;  // VEX: openvex.go:35-40 / cyclonedx.go:56-60 / csaf.go:36-40 drop it
         }
         a.skey[i] = key;
       }
@@ -617,6 +628,14 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
                       hipStream_t st, std::string& err) {
   n_ = n;
   survivors_ = ignored_ = 0;
+  // measurement only: TVM_FILTER_TRACE=1 prints the host time at each step of a call
+  static const bool trace = std::getenv("TVM_FILTER_TRACE") != nullptr;
+  const auto T0 = std::chrono::steady_clock::now();
+  auto mark = [&](const char* what) {
+    if (trace)
+      std::fprintf(stderr, "filter %s %.1f us\n", what,
+                   std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - T0).count());
+  };
   if (n == 0) return true;
   if (n >= 0xFFFFFFFFull) {
     err = "filter: too many pairs";
@@ -637,7 +656,8 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   // their pairs directly once the package runs are known (vex_mark, after filter_mark).
   const uint64_t nr_all = rules.size();
   RuleDev rd{}, vd{};  // hash-set lists, VEX lists
-  uint64_t nr = 0, nv = 0;
+  uint64_t nr = 0, nv = 0, nr_c = 0, nv_c = 0;  // entries per kind (totals; staged so far)
+  for (int k = 0; k < rules.n_lists; k++) (rules.lists[k].tag == RULE_VEX ? nv : nr) += rules.lists[k].n;
   if (nr_all) {
     uint64_t words = rules.rank[0].size() + rules.rank[1].size();
     for (int k = 0; k < rules.n_lists; k++)
@@ -663,34 +683,66 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
         !ok(hipMemcpyAsync(&dup_n, bufs_[23], 8, hipMemcpyDeviceToHost, st), "D2H dup count", err))
       return false;
   }
-  if (nr_all) {  // staging layout: rank tables, then per list subject / id / prec columns (4 B each)
-    uint32_t* h = static_cast<uint32_t*>(pin_);
-    const uint32_t* d = as<const uint32_t>(bufs_[18]);
-    uint64_t at = 0;
+  // staging layout: per phase a rank table, then per list subject / id / prec columns (4 B
+  // each); phase 0 = the ignore lists (filter_mark needs their hash set), phase 1 = VEX
+  // (its host copy runs on a helper thread from here on, its upload is queued behind
+  // filter_select: the kernel that needs it runs after)
+  uint32_t* const h = static_cast<uint32_t*>(pin_);
+  const uint32_t* const d = nr_all ? as<const uint32_t>(bufs_[18]) : nullptr;
+  uint64_t at = 0, ph_b[3] = {0, 0, 0};
+  struct Job {
+    uint32_t* dst;
+    const uint32_t* src;
+    uint64_t cnt;
+  };
+  std::vector<Job> jobs[2];
+  for (int phase = 0; phase < 2; phase++) {
+    ph_b[phase] = at;
+    const uint32_t* rank_dev = nullptr;
     auto put = [&](const uint32_t* src, uint64_t cnt) {
-      memcpy(h + at, src, cnt * 4);
+      jobs[phase].push_back({h + at, src, cnt});
       const uint32_t* where = d + at;
       at += cnt;
       return where;
     };
-    const uint32_t* rank_dev[2] = {put(rules.rank[0].data(), rules.rank[0].size()),
-                                   put(rules.rank[1].data(), rules.rank[1].size())};
     for (int k = 0; k < rules.n_lists; k++) {
       const RuleList& l = rules.lists[k];
-      const bool vex = l.tag == RULE_VEX;
-      RuleDev& r = vex ? vd : rd;
-      uint64_t& cnt = vex ? nv : nr;
+      if ((l.tag == RULE_VEX) != (phase == 1)) continue;
+      if (!rank_dev) rank_dev = put(rules.rank[l.table].data(), rules.rank[l.table].size());
+      RuleDev& r = phase ? vd : rd;
+      uint64_t& cnt = phase ? nv_c : nr_c;
       const int i = r.n_lists++;
       r.subject[i] = l.subject ? put(l.subject, l.n) : nullptr;
       r.id[i] = put(l.id, l.n);
       r.prec[i] = l.prec ? put(l.prec, l.n) : nullptr;
-      r.rank[i] = rank_dev[l.table];
+      r.rank[i] = rank_dev;
       r.tag[i] = uint32_t(l.tag);
       cnt += l.n;
       r.end[i] = cnt;
     }
-    if (!ok(hipMemcpyAsync(bufs_[18], pin_, at * 4, hipMemcpyHostToDevice, st), "H2D rules", err)) return false;
   }
+  ph_b[2] = at;
+  auto copy_jobs = [](const std::vector<Job>& js) {
+    for (const Job& jb : js) memcpy(jb.dst, jb.src, jb.cnt * 4);
+  };
+  std::thread vex_copy;
+  if (!jobs[1].empty()) vex_copy = std::thread(copy_jobs, std::cref(jobs[1]));
+  struct Joiner {
+    std::thread& t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } joiner{vex_copy};
+  auto upload = [&](int phase) {
+    const uint64_t a0 = ph_b[phase], a1 = ph_b[phase + 1];
+    return a1 == a0 || ok(hipMemcpyAsync(static_cast<uint8_t*>(bufs_[18]) + a0 * 4, static_cast<uint8_t*>(pin_) + a0 * 4,
+                                         (a1 - a0) * 4, hipMemcpyHostToDevice, st),
+                          "H2D rules", err);
+  };
+  copy_jobs(jobs[0]);
+  if (!upload(0)) return false;
+  mark("staged ignore lists");
+  mark("dup sync");
   if (any_dup_) {
     if (!ok(hipStreamSynchronize(st), "filter sync", err)) return false;
     if (dup_n) {
@@ -715,7 +767,7 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
       (tcap && (!grow(15, n * 4, err) || !grow(16, tcap * 16, err))) || (rcap && !grow(17, rcap * 16, err)) ||
       !grow(21, n * 8, err) || !grow(24, n, err) || !grow(25, (n / 64 + 1) * 4 * kClasses, err) ||
       (has_ign && !grow(22, n * 12, err)) || !grow(23, std::max<uint64_t>(scan_bytes, 16), err) ||
-      (nv && !grow(26, n, err)))
+      !grow(26, 16, err))
     return false;
   // per-call flags start as the static ones (FL_DUP, FL_SINGLE)
   if (np && !ok(hipMemcpyAsync(bufs_[7], bufs_[5], np, hipMemcpyDeviceToDevice, st), "D2D flags", err)) return false;
@@ -725,7 +777,7 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
                        as<unsigned long long>(bufs_[17]), rcap - 1, as<uint8_t>(bufs_[7]));
     if (!ok(hipGetLastError(), "rules_insert", err)) return false;
   }
-  if (nv && !ok(hipMemsetAsync(bufs_[26], 0, n, st), "memset(vex marks)", err)) return false;
+  if (!ok(hipMemsetAsync(bufs_[26], 0, 4, st), "memset(bad index)", err)) return false;
   if (rules.pkg_class &&
       !ok(hipMemcpyAsync(bufs_[20], rules.pkg_class, np * 4, hipMemcpyHostToDevice, st), "H2D classes", err))
     return false;
@@ -768,12 +820,15 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   a.id_bits = id_bits;
   a.out = as<uint2>(bufs_[21]);
   a.iout = as<uint32_t>(bufs_[22]);
-  a.vx = as<const uint8_t>(bufs_[26]);
   hipLaunchKernelGGL(filter_mark, dim3(blocks_u), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(filter_select, dim3(blocks_u), dim3(kBlock), 0, st, a);
+  mark("select launched");
+  if (vex_copy.joinable()) vex_copy.join();
+  if (!upload(1)) return false;  // the VEX lists go up while mark / select run
+  mark("vex staged");
   if (nv) hipLaunchKernelGGL(vex_mark, dim3(uint32_t((nv + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, vd, pkg, side,
                              as<const uint32_t>(bufs_[8]), as<const uint32_t>(bufs_[9]), as<const uint8_t>(bufs_[7]), n,
-                             as<uint8_t>(bufs_[26]));
-  hipLaunchKernelGGL(filter_select, dim3(blocks_u), dim3(kBlock), 0, st, a);
+                             uint32_t(np), uint32_t(rules.rank[1].size()), a.skey, a.pcls, as<uint32_t>(bufs_[26]));
   hipLaunchKernelGGL(filter_count, dim3(blocks), dim3(kBlock), 0, st, a);
   if (!ok(hipGetLastError(), "filter launch", err) ||
       !ok(hipcub::DeviceScan::ExclusiveSum(bufs_[23], scan_bytes, In(Count(0), GroupCount{a.perm, a.cnt, uint32_t(np)}),
@@ -785,14 +840,20 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
            "hipcub scan", err)))
     return false;
   hipLaunchKernelGGL(filter_place, dim3(blocks), dim3(kBlock), 0, st, a);
-  uint32_t tot[2] = {0, 0};
+  uint32_t tot[2] = {0, 0}, bad = 0;
   if (!ok(hipGetLastError(), "filter_place", err) ||
       !ok(hipMemcpyAsync(&tot[0], as<uint32_t>(bufs_[10]) + np, 4, hipMemcpyDeviceToHost, st), "D2H kept", err) ||
+      (nv && !ok(hipMemcpyAsync(&bad, bufs_[26], 4, hipMemcpyDeviceToHost, st), "D2H index check", err)) ||
       (has_ign && !ok(hipMemcpyAsync(&tot[1], as<uint32_t>(bufs_[11]) + np, 4, hipMemcpyDeviceToHost, st),
                       "D2H ignored", err)) ||
       !ok(hipStreamSynchronize(st), "filter sync", err))
     return false;
+  if (bad) {
+    err = "tvm_match_filter: rule / VEX package, class or ID index out of range";
+    return false;
+  }
   survivors_ = tot[0];
+  mark("done");
   ignored_ = tot[1];
   return true;
 }
