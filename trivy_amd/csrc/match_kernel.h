@@ -820,6 +820,7 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
   const ProbeArgs& a = fa.pa;
   if (blockIdx.x < fa.n_copy) {  // pipeline: the previous chunk's result move, dispatched first so the link writes overlap the tiles
     static_assert(sizeof(buf) >= kCopyLdsWords * 4, "the result move borrows the staging buffer");
+    __builtin_amdgcn_s_setprio(3);  // its waves issue ahead of the match waves sharing the CU: the link is the bound
     copy_out_tiles(fa.co, blockIdx.x, fa.n_copy, reinterpret_cast<uint32_t*>(buf));
     return;
   }

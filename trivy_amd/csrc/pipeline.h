@@ -33,6 +33,7 @@ void launch_copy_out(hipStream_t st, const CopyOutArgs& a);  // engine.h copy_ou
 //                  chunk c-1's match segments into the pinned host CSR (engine.h
 //                  copy_out_tiles: 16-byte kernel stores, the link's other direction) while
 //                  the rest match chunk c;
+//   row-end stream DMA of chunk c-1's row ends (left in HBM by that result move) to the host;
 // so chunk c+1's upload and chunk c-1's result move run under chunk c's matching, and the
 // host waits once, at the end.  (Measured alternatives, DESIGN.md §7: a DMA device-to-host
 // copy runs at half the rate of kernel stores, and a result kernel on its own stream did
@@ -77,8 +78,9 @@ class Pipeline {
   uint32_t* ptab_d_ = nullptr;  // platform index -> platform id
   uint64_t encode_us_ = 0;
   int dev_ = -1;
-  hipStream_t s_h2d_ = nullptr, s_k_ = nullptr;
-  std::vector<hipEvent_t> ev_h_;
+  hipStream_t s_h2d_ = nullptr, s_k_ = nullptr, s_d2h_ = nullptr;
+  std::vector<hipEvent_t> ev_h_, ev_k_;  // chunk uploaded / chunk's result move done
+  uint32_t* row_end_d_ = nullptr;        // row ends in HBM when the DMA engine carries them up
   std::vector<uint32_t> bounds_;     // chunk c = tiles [bounds_[c], bounds_[c + 1])
   std::vector<uint64_t> toff_;       // tile offsets + the arena end (registered)
   std::vector<void*> registered_;
