@@ -130,6 +130,15 @@ int tvm_db_put_many(tvm_db* db, size_t n, const tvm_str* paths, size_t depth, co
  * slices off[r*(depth+1) + j], len[...] (j = depth is the value). */
 int tvm_db_put_arena(tvm_db* db, size_t n, size_t depth, const char* arena, const uint64_t* off,
                      const uint32_t* len);
+/* A bbolt file image (trivy.db as downloaded; the reference opens it with go.etcd.io/bbolt,
+ * pkg/db/db.go:89-110): every record, (bucket path..., key) -> value, goes through
+ * tvm_db_put.  Read-only walk of the current meta page's tree; a malformed file fails with
+ * TVM_EINVAL and a message (records put before the failure stay). */
+int tvm_db_put_bbolt(tvm_db* db, const void* bytes, size_t len, char* err, size_t errlen);
+/* The same walk, reporting each record to `visit` (path = buckets + key, `depth` items);
+ * a nonzero return from visit stops the walk (TVM_EINVAL). */
+typedef int (*tvm_bbolt_visit)(void* ctx, const tvm_str* path, size_t depth, const char* value, size_t vlen);
+int tvm_bbolt_walk(const void* bytes, size_t len, tvm_bbolt_visit visit, void* ctx, char* err, size_t errlen);
 /* Decode + flatten into device images. Must be called once, before tvm_engine_open. */
 int tvm_db_finalize(tvm_db* db, char* err, size_t errlen);
 /* Statistics: [0] platforms [1] keys [2] advisories [3] interval rows [4] key-arena bytes */

@@ -100,6 +100,9 @@ _SIG = [
     ("tvm_db_free", None, [_P]),
     ("tvm_db_put", ctypes.c_int, [_P, ctypes.POINTER(Str), ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_db_put_many", ctypes.c_int, [_P, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    ("tvm_db_put_bbolt", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_bbolt_walk", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_db_put_arena", ctypes.c_int, [_P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p]),
     ("tvm_db_finalize", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t]),

@@ -18,6 +18,7 @@
 #include "engine.h"
 #include "libdb.h"
 #include "libver.h"
+#include "bbolt.h"
 #include "pipeline.h"
 #include "redhat.h"
 #include "vulninfo.h"
@@ -195,6 +196,45 @@ int tvm_db_put(tvm_db* db, const tvm_str* path, size_t depth, const char* value,
   std::vector<std::string> p(depth);
   for (size_t i = 0; i < depth; i++) p[i] = std::string(sv(path[i]));
   db->db.put(p, std::string_view(value ? value : "", value ? vlen : 0));
+  return TVM_OK;
+}
+
+int tvm_bbolt_walk(const void* bytes, size_t len, tvm_bbolt_visit visit, void* ctx, char* err, size_t errlen) {
+  if ((!bytes && len) || !visit) return TVM_EINVAL;
+  std::vector<tvm_str> p;
+  std::string msg;
+  const bool ok = tvm::bbolt_walk(
+      static_cast<const uint8_t*>(bytes), len,
+      [&](const std::vector<std::string_view>& path, std::string_view v) {
+        p.resize(path.size());
+        for (size_t i = 0; i < path.size(); i++) p[i] = tvm_str{path[i].data(), path[i].size()};
+        return visit(ctx, p.data(), p.size(), v.data(), v.size()) == 0;
+      },
+      msg);
+  if (!ok) {
+    set_err(err, errlen, msg);
+    return TVM_EINVAL;
+  }
+  return TVM_OK;
+}
+
+int tvm_db_put_bbolt(tvm_db* db, const void* bytes, size_t len, char* err, size_t errlen) {
+  if (!db || db->finalized || (!bytes && len)) return TVM_EINVAL;
+  std::vector<std::string> p;
+  std::string msg;
+  const bool ok = tvm::bbolt_walk(
+      static_cast<const uint8_t*>(bytes), len,
+      [&](const std::vector<std::string_view>& path, std::string_view v) {
+        p.resize(path.size());
+        for (size_t i = 0; i < path.size(); i++) p[i].assign(path[i]);
+        db->db.put(p, v);
+        return true;
+      },
+      msg);
+  if (!ok) {
+    set_err(err, errlen, msg);
+    return TVM_EINVAL;
+  }
   return TVM_OK;
 }
 

@@ -46,6 +46,13 @@ class DB:
             if rc:
                 raise ValueError(f"tvm_db_put_many failed ({rc})")
 
+    def put_bbolt(self, data):
+        """Every record of a bbolt file image (trivy.db) - tvm_db_put_bbolt."""
+        e = errbuf()
+        rc = lib().tvm_db_put_bbolt(self.h, data, len(data), e, len(e))
+        if rc:
+            raise ValueError(e.value.decode())
+
     def put_arena(self, n, depth, arena, off, lens):
         """n records of `depth` path components + value, packed in one arena (record r's
         strings are items r*(depth+1) .. r*(depth+1)+depth; off u64 / lens u32 per item)."""
@@ -70,6 +77,31 @@ class DB:
         h, self.h = getattr(self, "h", None), None
         if h and _lib._lib is not None:
             _lib._lib.tvm_db_free(h)
+
+
+class _RawStr(ctypes.Structure):  # tvm_str with the pointer kept raw (keys may hold any byte)
+    _fields_ = [("p", ctypes.c_void_p), ("n", ctypes.c_size_t)]
+
+
+BBOLT_VISIT = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(_RawStr), ctypes.c_size_t,
+                               ctypes.c_void_p, ctypes.c_size_t)
+
+
+def bbolt_records(data):
+    """[(path tuple of bytes (buckets..., key), value bytes)] of a bbolt file image, in the
+    walk's (bucket, key) order (tvm_bbolt_walk)."""
+    out = []
+
+    def visit(_ctx, path, depth, value, vlen):
+        out.append((tuple(ctypes.string_at(path[i].p, path[i].n) for i in range(depth)),
+                    ctypes.string_at(value, vlen) if vlen else b""))
+        return 0
+    cb = BBOLT_VISIT(visit)
+    e = errbuf()
+    rc = lib().tvm_bbolt_walk(data, len(data), ctypes.cast(cb, ctypes.c_void_p), None, e, len(e))
+    if rc:
+        raise ValueError(e.value.decode())
+    return out
 
 
 def load_fixture_files(paths):
