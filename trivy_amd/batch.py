@@ -12,6 +12,7 @@ import ctypes
 
 import numpy as np
 
+from . import _lib
 from ._lib import lib, errbuf
 
 ATTR_ARCH, ATTR_KSPLICE, ATTR_CPESET = 1, 2, 4
@@ -403,7 +404,6 @@ class MatchBatch:
     def close(self):
         h, self.h = getattr(self, "h", None), None
         if h:
-            from . import _lib
             if _lib._lib is not None:
                 _lib._lib.tvm_batch_free(h)
 
