@@ -70,14 +70,15 @@ __device__ __forceinline__ uint32_t probe_id(const FillDev& t, const uint8_t* id
   }
 }
 
-__device__ __forceinline__ uint4 decide(const FillDev& t, uint4 item, uint32_t rec) {
+// r = t.recs[rec] (loaded by the caller, so a batch of pairs has its record loads in flight
+// together); ignored when rec is FILL_NOT_FOUND
+__device__ __forceinline__ uint4 decide_r(const FillDev& t, uint4 item, uint32_t rec, uint4 r) {
   // vulnerability.go:64-68: the status rule runs before the lookup
   uint32_t status = item.z & 0xFFu;
   if (item.z & FI_FIXED) status = 3;       // StatusFixed
   else if (status == 0) status = 2;        // StatusAffected
   uint4 o = make_uint4(FILL_NOT_FOUND, status, 0u | (SRC_NONE << 16), URL_NONE);
   if (rec == FILL_NOT_FOUND) return o;
-  const uint4 r = t.recs[rec];
   if (r.w & REC_BAD) return o;             // GetVulnerability decode error: logged, skipped
   o.x = rec;
   const uint32_t src = item.y >> 16;
@@ -106,6 +107,10 @@ __device__ __forceinline__ uint4 decide(const FillDev& t, uint4 item, uint32_t r
   return o;
 }
 
+__device__ __forceinline__ uint4 decide(const FillDev& t, uint4 item, uint32_t rec) {
+  return decide_r(t, item, rec, rec == FILL_NOT_FOUND ? make_uint4(0, 0, 0, 0) : t.recs[rec]);
+}
+
 // Drop-in path: one lane per item.
 __global__ __launch_bounds__(kFillTile) void fill_items_kernel(FillArgs a) {
   const uint64_t i = uint64_t(blockIdx.x) * kFillTile + threadIdx.x;
@@ -116,25 +121,51 @@ __global__ __launch_bounds__(kFillTile) void fill_items_kernel(FillArgs a) {
 
 // Batch path: grid-stride over the match kernel's pair buffer; the pair count is read on
 // the device (no host round trip between the two launches).
+// kU pairs per lane per step, each level of the pair -> advisory item -> record chain loaded
+// for all of them before the next level is used (the chain is latency-bound: one pair per
+// lane kept one gather in flight).
+constexpr int kFillU = 4;
 __global__ __launch_bounds__(kFillTile) void fill_pairs_kernel(FillArgs a) {
   const uint64_t n = *a.n_dev < a.n ? *a.n_dev : a.n;
-  const uint64_t stride = uint64_t(gridDim.x) * kFillTile;
-  for (uint64_t i = uint64_t(blockIdx.x) * kFillTile + threadIdx.x; i < n; i += stride) {
-    const uint32_t adv = a.adv[i];
-    uint4 item = adv < a.t.n_advs ? a.t.adv_items[adv] : make_uint4(0, SRC_NONE << 16, 0, FILL_NOT_FOUND);
+  const uint64_t stride = uint64_t(gridDim.x) * kFillTile * kFillU;
+  for (uint64_t i0 = uint64_t(blockIdx.x) * kFillTile * kFillU + threadIdx.x; i0 < n; i0 += stride) {
+    uint32_t adv[kFillU], rank[kFillU];
+    uint4 item[kFillU], r[kFillU];
+#pragma unroll
+    for (int k = 0; k < kFillU; k++) {
+      const uint64_t i = i0 + uint64_t(k) * kFillTile;
+      adv[k] = i < n ? a.adv[i] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int k = 0; k < kFillU; k++) {
+      const bool known = adv[k] < a.t.n_advs;
+      item[k] = known ? a.t.adv_items[adv[k]] : make_uint4(0, SRC_NONE << 16, 0, FILL_NOT_FOUND);
+      rank[k] = (a.side && known) ? a.t.adv_rank[adv[k]].x : 0xFFFFFFFFu;
+    }
     if (a.base) {  // merged Red Hat entry: FixedVersion of adv (the representative), the rest of base
-      const uint32_t b = a.base[i];
-      if (b != adv && b < a.t.n_advs) {
-        const uint32_t fixed = item.z & FI_FIXED;
-        item = a.t.adv_items[b];
-        item.z = (item.z & ~FI_FIXED) | fixed;
+#pragma unroll
+      for (int k = 0; k < kFillU; k++) {
+        const uint64_t i = i0 + uint64_t(k) * kFillTile;
+        const uint32_t b = i < n ? a.base[i] : adv[k];
+        if (b != adv[k] && b < a.t.n_advs) {
+          const uint32_t fixed = item[k].z & FI_FIXED;
+          item[k] = a.t.adv_items[b];
+          item[k].z = (item[k].z & ~FI_FIXED) | fixed;
+        }
       }
     }
-    const uint4 o = decide(a.t, item, item.w);
-    a.out[i] = o;
-    if (a.side)  // result.Filter reads this word, not the decision (filter.hip filter_mark)
-      a.side[i] = make_uint2(adv < a.t.n_advs ? a.t.adv_rank[adv].x : 0xFFFFFFFFu,
-                             fill_pair_severity(o, item) | ((o.y & 31u) << 8));
+#pragma unroll
+    for (int k = 0; k < kFillU; k++)
+      r[k] = item[k].w != FILL_NOT_FOUND ? a.t.recs[item[k].w] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < kFillU; k++) {
+      const uint64_t i = i0 + uint64_t(k) * kFillTile;
+      if (i >= n) break;
+      const uint4 o = decide_r(a.t, item[k], item[k].w, r[k]);
+      a.out[i] = o;
+      if (a.side)  // result.Filter reads this word, not the decision (filter.hip filter_mark)
+        a.side[i] = make_uint2(rank[k], fill_pair_severity(o, item[k]) | ((o.y & 31u) << 8));
+    }
   }
 }
 
@@ -244,7 +275,7 @@ bool FillEngine::launch_pairs(const uint32_t* adv, const uint32_t* base, const u
   a.out = out;
   a.side = side;
   // enough waves to cover the chip many times over, capped so the stride loop does the rest
-  const uint64_t blocks = std::min<uint64_t>((cap + kFillTile - 1) / kFillTile, 256ull * 64);
+  const uint64_t blocks = std::min<uint64_t>((cap + kFillTile * kFillU - 1) / (kFillTile * kFillU), 256ull * 32);
   hipLaunchKernelGGL(fill_pairs_kernel, dim3(uint32_t(blocks)), dim3(kFillTile), 0, stream, a);
   return hip_ok(hipGetLastError(), "fill_kernel launch", err);
 }
