@@ -408,7 +408,14 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
     fa.sa = sa;
     if (co) {
       fa.co = *co;
-      fa.n_copy = kCopyWorkgroups;
+      // 64 workgroups move a chunk's results beside its match tiles (measured, C2 end-to-end:
+      // 64 3.10 ms, 128 3.13, 192 3.13, 256 3.25, 512 3.43, 1024 3.39;
+      // profiles/r03/e2e_copy_width.txt); TVM_COPY_WG overrides it for measurement
+      static const uint32_t n_copy = [] {
+        const char* v = std::getenv("TVM_COPY_WG");
+        return v ? uint32_t(std::max(1, std::atoi(v))) : 64u;
+      }();
+      fa.n_copy = n_copy;
     }
     fused_fn(b.gm, vi)(nt, pst, fa);
     return hip_ok(hipGetLastError(), "match kernel launch", err);
