@@ -349,6 +349,7 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
   // TVM_PIPE_COPIES_FIRST=1 queues every chunk's upload before any kernel
   static const bool trace = std::getenv("TVM_PIPE_TRACE") != nullptr;
   static const bool copies_first = std::getenv("TVM_PIPE_COPIES_FIRST") != nullptr;
+  static const bool unpack_on_copy = std::getenv("TVM_PIPE_UNPACK_ON_COPY") != nullptr && !copies_first;
   // the DMA engine carries chunk c's row ends up (third stream) once its result move is done
   auto rowend_up = [&](uint32_t c) {
     if (!rowend_dma) return true;
@@ -377,14 +378,6 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
     const uint64_t a0 = toff_[g0], a1 = toff_[g1];
     if (!wc_.empty()) {  // transport form: one DMA, then the chunk is rebuilt in HBM
       const WireChunk& w = wc_[c];
-      if (!copies_first &&
-          (!ok(hipMemcpyAsync(wire_d_ + w.off, wire_h_ + w.off, w.bytes, hipMemcpyHostToDevice, s_h2d_), "H2D chunk", err) ||
-           !ok(hipEventRecord(ev_h_[c], s_h2d_), "hipEventRecord", err)))
-        return false;
-      if (trace) std::fprintf(stderr, "pipe c%u copy %.1f us\n", c, us());
-      if (!ok(hipStreamWaitEvent(s_k_, ev_h_[c], 0), "hipStreamWaitEvent", err)) return false;
-      if (trace) std::fprintf(stderr, "pipe c%u wait %.1f us\n", c, us());
-      h2d_ += w.bytes;
       UnpackArgs ua;
       ua.wire = wire_d_;
       ua.nref = reinterpret_cast<const uint32_t*>(wire_d_ + w.o_nref);
@@ -402,9 +395,23 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
       ua.m = w.m;
       ua.g0 = uint32_t(g0);
       ua.groups = w.groups;
-      hipLaunchKernelGGL(unpack_kernel, dim3((w.groups + 3) / 4), dim3(256), 0, s_k_, ua);
-      if (!ok(hipGetLastError(), "unpack kernel launch", err)) return false;
-      if (trace) std::fprintf(stderr, "pipe c%u unpack %.1f us\n", c, us());
+      h2d_ += w.bytes;
+      if (!copies_first &&
+          !ok(hipMemcpyAsync(wire_d_ + w.off, wire_h_ + w.off, w.bytes, hipMemcpyHostToDevice, s_h2d_), "H2D chunk", err))
+        return false;
+      if (unpack_on_copy) {  // behind its own upload: it runs while the kernel stream is still on chunk c-1
+        hipLaunchKernelGGL(unpack_kernel, dim3((w.groups + 3) / 4), dim3(256), 0, s_h2d_, ua);
+        if (!ok(hipGetLastError(), "unpack kernel launch", err) || !ok(hipEventRecord(ev_h_[c], s_h2d_), "hipEventRecord", err) ||
+            !ok(hipStreamWaitEvent(s_k_, ev_h_[c], 0), "hipStreamWaitEvent", err))
+          return false;
+      } else {
+        if ((!copies_first && !ok(hipEventRecord(ev_h_[c], s_h2d_), "hipEventRecord", err)) ||
+            !ok(hipStreamWaitEvent(s_k_, ev_h_[c], 0), "hipStreamWaitEvent", err))
+          return false;
+        hipLaunchKernelGGL(unpack_kernel, dim3((w.groups + 3) / 4), dim3(256), 0, s_k_, ua);
+        if (!ok(hipGetLastError(), "unpack kernel launch", err)) return false;
+      }
+      if (trace) std::fprintf(stderr, "pipe c%u upload + unpack queued %.1f us\n", c, us());
     } else if (!ok(hipMemcpyAsync(db_.pk + p0, hb.pk.data() + p0, (p1 - p0) * sizeof(uint2), hipMemcpyHostToDevice, s_h2d_),
             "H2D packages", err) ||
         !ok(hipMemcpyAsync(db_.tile_off + g0, toff_.data() + g0, (g1 - g0 + 1) * 8, hipMemcpyHostToDevice, s_h2d_),
