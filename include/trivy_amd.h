@@ -303,17 +303,23 @@ int tvm_batch_upload_into(tvm_engine* e, tvm_batch* b, void* pkg_dev, void* adv_
  * name and version under 256 bytes, at most 255 platforms): each distinct name and each
  * distinct version string crosses the link once, packages carry references to them, and
  * the GPU rebuilds the batch's arrays chunk by chunk (one DMA per chunk). */
-enum { TVM_PIPE_RAW = 1 };
+enum { TVM_PIPE_RAW = 1, TVM_PIPE_ADV32 = 2 };
 int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32_t chunk_packages, uint32_t flags,
                          char* err, size_t errlen);
 /* One pass; ms = wall time of the call.  TVM_EINVAL with *n_matches set when the matches do
  * not fit match_cap (prepare again with a larger one). */
 int tvm_pipeline_run(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* err_pkg, double* ms, char* err,
                      size_t errlen);
-/* The last pass's result (library-owned pinned memory, valid until the next pass or
+/* The last pass's result (library-owned memory, valid until the next pass or
  * tvm_batch_free): package p's advisory indices are adv[row_end[p-1] .. row_end[p])
- * (row_end[-1] = 0), in (package, advisory) order. */
+ * (row_end[-1] = 0), in (package, advisory) order.  When the DB has fewer than 2^24
+ * advisories (and prepare had no TVM_PIPE_ADV32) the indices cross the link as 3 bytes
+ * each; this call then widens them into a 4-byte array on the host once per pass. */
 int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row_end, uint64_t* n_matches);
+/* The result as it arrived in pinned host memory: index i is the `width`-byte (3 or 4)
+ * little-endian integer at adv + width * i. */
+int tvm_pipeline_result_raw(tvm_batch* b, const void** adv, uint32_t* width, const uint32_t** row_end,
+                            uint64_t* n_matches);
 /* [0] bytes the last pass copied host to device, [1] device to host, [2] chunks, [3] 1 when
  * the batch travels in its transport form, [4] prepare's host time building it (us). */
 int tvm_pipeline_stats(tvm_batch* b, uint64_t out[5]);

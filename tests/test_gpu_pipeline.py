@@ -33,22 +33,24 @@ def world():
     return sdb, build_engine(sdb)
 
 
-@pytest.mark.parametrize("raw", [False, True])
+@pytest.mark.parametrize("raw,adv32", [(False, False), (True, False), (False, True)])
 @pytest.mark.parametrize("chunk", [256, 1000, 4096, 1 << 19])
-def test_pipeline_matches_oracle(world, chunk, raw, oracle_built):
+def test_pipeline_matches_oracle(world, chunk, raw, adv32, oracle_built):
     sdb, eng = world
     batch = make_batch(sdb, 37, 333, [2, 2, 1], seed=chunk)  # 12321 packages: ragged last tile
     opk, oad = om.match(om.Prepared(sdb, batch), n_threads=8)
-    mb = _fill(eng, sdb, batch).pipeline_prepare(match_cap=len(opk) + 5, chunk_packages=chunk, raw=raw)
+    mb = _fill(eng, sdb, batch).pipeline_prepare(match_cap=len(opk) + 5, chunk_packages=chunk, raw=raw, adv32=adv32)
     for _ in range(2):  # a second pass over the same pinned batch gives the same lists
         total, errp, ms = mb.pipeline_run()
         assert errp == -1 and total == len(opk) and ms > 0
         adv, rend = mb.pipeline_csr()
         pk, ad = _pairs_of(adv, rend)
         assert np.array_equal(pk, opk) and np.array_equal(ad, oad)
+        araw, width = mb.pipeline_csr_raw()  # the bytes as they crossed the link
+        assert width == (4 if adv32 else 3) and np.array_equal(araw, oad)
     st = mb.pipeline_stats()
     assert st["chunks"] == -(-len(batch) // (-(-chunk // 256) * 256)) and st["h2d_bytes"] > 0
-    assert st["d2h_bytes"] == 4 * (len(batch) + len(opk))
+    assert st["d2h_bytes"] == 4 * len(batch) + (4 if adv32 else 3) * len(opk)
     assert st["transport_form"] == (not raw)
     mb.close()
 

@@ -165,6 +165,8 @@ _SIG = [
                                         ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_pipeline_result", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p),
                                            ctypes.POINTER(ctypes.c_uint64)]),
+    ("tvm_pipeline_result_raw", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint32),
+                                               ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64)]),
     ("tvm_pipeline_stats", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     ("tvm_version_key", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p,
                                        ctypes.c_size_t]),

@@ -228,12 +228,14 @@ class MatchBatch:
         return lib().tvm_match_algorithmic_bytes(self.engine.h, self.h)
 
     # ---- end-to-end pipelined pass (tvm_pipeline_*) ----
-    def pipeline_prepare(self, match_cap=None, chunk_packages=1 << 19, raw=False):
+    def pipeline_prepare(self, match_cap=None, chunk_packages=1 << 19, raw=False, adv32=False):
         """Pins the batch and sizes the pipeline (host batch -> GPU -> host CSR).  raw: upload
-        the batch's own arrays instead of its transport form (TVM_PIPE_RAW)."""
+        the batch's own arrays instead of its transport form (TVM_PIPE_RAW); adv32: 4-byte
+        advisory indices in the result even when 3 bytes hold them (TVM_PIPE_ADV32)."""
         e = errbuf()
         cap = match_cap if match_cap is not None else max(1024, 8 * len(self))
-        self._check(lib().tvm_pipeline_prepare(self.engine.h, self.h, cap, chunk_packages, 1 if raw else 0, e, len(e)), e,
+        flags = (1 if raw else 0) | (2 if adv32 else 0)
+        self._check(lib().tvm_pipeline_prepare(self.engine.h, self.h, cap, chunk_packages, flags, e, len(e)), e,
                     "tvm_pipeline_prepare")
         self.pipe_cap = cap
         return self
@@ -260,6 +262,21 @@ class MatchBatch:
         r = np.ctypeslib.as_array((ctypes.c_uint32 * max(m, 1)).from_address(rend.value))[:m].copy() \
             if m else np.zeros(0, np.uint32)
         return a, r
+
+    def pipeline_csr_raw(self):
+        """(adv uint32[matches] decoded from the bytes as they arrived, width 3 or 4) of the last
+        pass - tvm_pipeline_result_raw."""
+        adv, rend, n, w = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_uint32()
+        if lib().tvm_pipeline_result_raw(self.h, ctypes.byref(adv), ctypes.byref(w), ctypes.byref(rend), ctypes.byref(n)):
+            raise RuntimeError("tvm_pipeline_result_raw: no valid pass")
+        k, width = n.value, w.value
+        if not k:
+            return np.zeros(0, np.uint32), width
+        raw = np.ctypeslib.as_array((ctypes.c_uint8 * (k * width)).from_address(adv.value)).reshape(k, width)
+        out = np.zeros(k, np.uint32)
+        for j in range(width):
+            out |= raw[:, j].astype(np.uint32) << (8 * j)
+        return out, width
 
     def pipeline_stats(self):
         out = (ctypes.c_uint64 * 5)()

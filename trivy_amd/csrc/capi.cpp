@@ -66,6 +66,8 @@ struct tvm_batch {
   std::unique_ptr<Pipeline> pipe;      // tvm_pipeline_* state
   uint32_t pkg_base = 0;               // tvm_batch_set_package_base
   uint64_t pipe_total = 0;
+  uint64_t pipe_runs = 0, pipe_wide_for = ~0ull;  // passes run; the pass pipe_wide was widened for
+  std::vector<uint32_t> pipe_wide;                // 3-byte result indices widened (tvm_pipeline_result)
   unsigned long long* order_scratch = nullptr;  // tvm_match_order_into: ticket + look-back word per tile
   uint32_t order_cap = 0;
   bool external_out = false;  // m.pkg / m.adv belong to the caller (tvm_batch_upload_into)
@@ -1299,7 +1301,7 @@ int tvm_match_filter_time(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o,
 
 int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32_t chunk_packages, uint32_t flags,
                          char* err, size_t errlen) {
-  if (!e || !b || chunk_packages == 0 || (flags & ~uint32_t(TVM_PIPE_RAW))) return TVM_EINVAL;
+  if (!e || !b || chunk_packages == 0 || (flags & ~uint32_t(TVM_PIPE_RAW | TVM_PIPE_ADV32))) return TVM_EINVAL;
   std::shared_lock<std::shared_mutex> lk(e->mu);
   if (!bind(b, e)) {
     set_err(err, errlen, kStale);
@@ -1307,7 +1309,8 @@ int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32
   }
   b->pipe.reset(new Pipeline());
   std::string msg;
-  if (!b->pipe->prepare(*e->eng, b->hb, match_cap, chunk_packages, !(flags & TVM_PIPE_RAW), msg)) {
+  const bool packed = !(flags & TVM_PIPE_ADV32) && e->db->db.advs.size() < (1ull << 24);
+  if (!b->pipe->prepare(*e->eng, b->hb, match_cap, chunk_packages, !(flags & TVM_PIPE_RAW), packed, msg)) {
     b->pipe.reset();
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
@@ -1339,6 +1342,7 @@ int tvm_pipeline_run(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* 
     return TVM_EDEVICE;
   }
   b->pipe_total = total;
+  b->pipe_runs++;
   if (n_matches) *n_matches = total;
   if (err_pkg) *err_pkg = ep;
   if (ms) *ms = dt;
@@ -1351,7 +1355,28 @@ int tvm_pipeline_run(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* 
 
 int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row_end, uint64_t* n_matches) {
   if (!b || !b->pipe || b->pipe_total > b->pipe->cap()) return TVM_EINVAL;
+  if (adv && b->pipe->packed()) {  // widen the 3-byte indices once per pass (host side, after the pass)
+    if (b->pipe_wide_for != b->pipe_runs) {
+      const uint8_t* p = reinterpret_cast<const uint8_t*>(b->pipe->adv());
+      b->pipe_wide.resize(b->pipe_total);
+      for (uint64_t i = 0; i < b->pipe_total; i++)
+        b->pipe_wide[i] = uint32_t(p[3 * i]) | uint32_t(p[3 * i + 1]) << 8 | uint32_t(p[3 * i + 2]) << 16;
+      b->pipe_wide_for = b->pipe_runs;
+    }
+    *adv = b->pipe_wide.data();
+  } else if (adv) {
+    *adv = b->pipe->adv();
+  }
+  if (row_end) *row_end = b->pipe->row_end();
+  if (n_matches) *n_matches = b->pipe_total;
+  return TVM_OK;
+}
+
+int tvm_pipeline_result_raw(tvm_batch* b, const void** adv, uint32_t* width, const uint32_t** row_end,
+                            uint64_t* n_matches) {
+  if (!b || !b->pipe || b->pipe_total > b->pipe->cap()) return TVM_EINVAL;
   if (adv) *adv = b->pipe->adv();
+  if (width) *width = b->pipe->packed() ? 3 : 4;
   if (row_end) *row_end = b->pipe->row_end();
   if (n_matches) *n_matches = b->pipe_total;
   return TVM_OK;

@@ -135,6 +135,7 @@ struct CopyOutArgs {
   uint32_t t0 = 0, t1 = 0;            // the chunk's tiles
   uint32_t pkg_base = 0;              // subtracted from the match list's package indices
   uint64_t cap = 0;                   // match / result capacity (an overflowed pass moves no advisories)
+  uint32_t packed = 0;                // 1: advisories as 3-byte little-endian indices (the DB has < 2^24)
 };
 constexpr uint32_t kCopyLdsWords = kTile + 8;  // copy_out_tiles' LDS: counts + scratch
 constexpr uint32_t kCopyWorkgroups = 256;      // workgroups of a result move
@@ -194,11 +195,51 @@ __device__ __forceinline__ void copy_out_tiles(const CopyOutArgs& a, uint32_t wg
     for (uint32_t w = 0; w < wave; w++) x += red[w];
     cnt[tid] = uint32_t(b) + x;  // row end of package p_first + tid (row ends are 32-bit)
     __syncthreads();
+    if (tid < kTile / 4)
+      reinterpret_cast<uint4*>(a.row_end_h)[p_first / 4 + tid] = reinterpret_cast<const uint4*>(cnt)[tid];
+    if (a.packed) {  // 3 bytes per advisory: destination bytes [3b, 3(b + count)) in 16-byte units
+      const uint64_t B0 = 3 * b, B1 = 3 * (b + d.count), U0 = B0 >> 4, nu = fits ? ((B1 + 15) >> 4) - U0 : 0;
+      uint8_t* dst = reinterpret_cast<uint8_t*>(a.adv_h);
+      constexpr int kP = 2;
+      for (uint64_t j0 = 0; j0 < nu; j0 += uint64_t(kP) * kTile) {
+        uint32_t id[kP][6];
+#pragma unroll
+        for (int k = 0; k < kP; k++) {
+          const uint64_t j = j0 + uint64_t(k) * kTile + tid, g0 = ((U0 + j) * 16) / 3;
+#pragma unroll
+          for (int t = 0; t < 6; t++) {
+            const int64_t i = int64_t(g0 + t) - int64_t(b);  // segment index of the unit's t-th advisory
+            id[k][t] = (j < nu && i >= 0 && i < int64_t(d.count)) ? a.adv[d.base + uint64_t(i)] : 0u;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < kP; k++) {
+          const uint64_t j = j0 + uint64_t(k) * kTile + tid;
+          if (j >= nu) continue;
+          const uint64_t G0 = (U0 + j) * 16, g0 = G0 / 3;
+          const uint32_t r = uint32_t(G0 - g0 * 3);  // byte of advisory g0 the unit starts at
+          uint32_t wv[4] = {0, 0, 0, 0};
+#pragma unroll
+          for (int q = 0; q < 16; q++) {
+            const uint32_t t = (r + q) / 3, kb = (r + q) % 3;
+            wv[q >> 2] |= ((id[k][t] >> (8 * kb)) & 0xFFu) << (8 * (q & 3));
+          }
+          if (G0 >= B0 && G0 + 16 <= B1) {
+            reinterpret_cast<uint4*>(dst)[U0 + j] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+          } else {  // a unit shared with a neighbour tile: its own bytes only
+#pragma unroll
+            for (int q = 0; q < 16; q++)
+              if (G0 + q >= B0 && G0 + q < B1) dst[G0 + q] = uint8_t(wv[q >> 2] >> (8 * (q & 3)));
+          }
+        }
+      }
+      b += d.count;
+      __syncthreads();  // cnt is rewritten by the next tile
+      continue;
+    }
     // the segment, realigned in registers to the destination's 16-byte units
     const uint64_t u0 = b >> 2, nu = fits ? ((b + d.count + 3) >> 2) - u0 : 0;
     const uint32_t sh = uint32_t(b & 3);
-    if (tid < kTile / 4)
-      reinterpret_cast<uint4*>(a.row_end_h)[p_first / 4 + tid] = reinterpret_cast<const uint4*>(cnt)[tid];
     constexpr int kU = 4;
     for (uint64_t j0 = 0; j0 < nu; j0 += uint64_t(kU) * kTile) {
       uint32_t v[kU][4];

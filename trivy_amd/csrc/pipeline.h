@@ -42,12 +42,14 @@ class Pipeline {
  public:
   ~Pipeline();
   // transport: send the batch in its transport form when it has one (see build_wire)
+  // packed: the result's advisory indices travel as 3 bytes each (the DB has < 2^24)
   bool prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uint32_t chunk_packages, bool transport,
-               std::string& err);
+               bool packed, std::string& err);
   // One pass.  total = matches (> match_cap: nothing valid, re-prepare with a larger cap);
   // err_pkg = first poisoned package or -1.
   bool run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& err_pkg, uint64_t& err_bits, std::string& err);
-  const uint32_t* adv() const { return adv_h_; }
+  const uint32_t* adv() const { return adv_h_; }  // 4-byte indices, or 3-byte ones when packed()
+  bool packed() const { return packed_; }
   const uint32_t* row_end() const { return row_end_h_; }
   uint64_t cap() const { return cap_; }
   uint64_t h2d_bytes() const { return h2d_; }
@@ -93,7 +95,8 @@ class Pipeline {
   uint32_t* row_end_hd_ = nullptr;
   unsigned long long* ctl_h_ = nullptr;
   uint64_t cap_ = 0, h2d_ = 0, d2h_ = 0;
-  bool prepared_ = false;  // no Engine pointer: the batch may outlive a hot swap (the C-ABI checks the generation)
+  bool prepared_ = false;
+  bool packed_ = false;  // no Engine pointer: the batch may outlive a hot swap (the C-ABI checks the generation)
 };
 
 }  // namespace tvm

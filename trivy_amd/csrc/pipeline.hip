@@ -231,7 +231,7 @@ void Pipeline::release() {
 }
 
 bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uint32_t chunk_packages, bool transport,
-                       std::string& err) {
+                       bool packed, std::string& err) {
   release();
 
   dev_ = eng.device();
@@ -246,6 +246,7 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
   toff_ = hb.tile_off;  // per 64-package group, + the arena end, padded to whole tiles
   toff_.resize(size_t(n_tiles) * kGroupsPerTile + 1, hb.arena.size());
   cap_ = std::max<uint64_t>(match_cap, 1);
+  packed_ = packed;
   if (cap_ >= (1ull << 32)) {
     err = "pipeline: row ends are 32-bit; split the batch below 2^32 matches";
     return false;
@@ -343,6 +344,7 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
     ca.t1 = bounds_[c + 1];
     ca.pkg_base = db_.pkg_base;
     ca.cap = cap_;
+    ca.packed = packed_ ? 1u : 0u;
     return ca;
   };
   // measurement only: TVM_PIPE_TRACE=1 prints the host time spent in each call of a pass;
@@ -441,7 +443,7 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
   if (trace) std::fprintf(stderr, "pipe ctl queued %.1f us\n", us());
   if (!ok(hipStreamSynchronize(s_k_), "pipeline", err) || !ok(hipStreamSynchronize(s_d2h_), "pipeline", err)) return false;
   if (trace) std::fprintf(stderr, "pipe done %.1f us\n", us());
-  d2h_ = uint64_t(n) * 4 + std::min<uint64_t>(ctl_h_[0], cap_) * 4;
+  d2h_ = uint64_t(n) * 4 + std::min<uint64_t>(ctl_h_[0], cap_) * (packed_ ? 3 : 4);
   total = ctl_h_[0];
   err_pkg = ctl_h_[1] ? int64_t(n - ctl_h_[1]) : -1;
   err_bits = ctl_h_[3];
