@@ -43,3 +43,15 @@ def oracle_built():
     import subprocess
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
     return True
+
+
+@pytest.fixture(autouse=True)
+def _device_drained(request):
+    """After each GPU test, wait for the device and surface any asynchronous fault here, so
+    the test whose launch faulted is the one that fails (not the next one's first copy)."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
