@@ -270,9 +270,27 @@ def pmc_traffic(config, workload, variant, src_hash):
                                        "source": f"profiles/pmc_summary_{config}.json", "note": d["note"]}
 
 
+def launch_ranks(n):
+    """N ranks of this script through torch.distributed.run on one node (127.0.0.1, a free
+    port), one per GPU; returns the launcher's exit status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL / tensor sharing need dmabuf IPC on this host
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without WORLD_SIZE in the environment, N > 1 launches N ranks "
+                         "through torch.distributed.run itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", choices=["c2", "c3", "c4", "c5"], default="c2")
@@ -291,10 +309,19 @@ def main():
     ap.add_argument("--variant", type=int, default=None, help="match-path variant (tvm_engine_set_variant)")
     ap.add_argument("--sweep", type=int, default=0,
                     help="time every match-path variant over N interleaved rounds (stderr table) first")
+    ap.add_argument("--dump-csr", default=None,
+                    help="rank 0 writes the whole batch's per-package advisory lists (CSR, as gathered) to this "
+                         ".npz after the timed region (checked against the oracle by tests/test_gpu_bench_dist.py)")
     args = ap.parse_args()
 
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N`: start the N ranks here, before this process touches a GPU
+        # (no torch import yet), and hand back rank 0's line and the launcher's exit status
+        return launch_ranks(args.gpus)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
+    if args.gpus is not None and world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     local = int(os.environ.get("LOCAL_RANK", 0))
     import torch
     import torch.distributed as dist
@@ -367,9 +394,9 @@ def main():
     def do_gather():
         mb.order_into(*csr)  # per-package lists in batch order on this rank's GPU (synchronised)
         if backend == "nccl":
-            gather(csr[0], csr[1], total, n_local)
-        else:  # gloo rehearsal: through host memory
-            gather(csr[0][:total].cpu(), csr[1][:n_local].cpu(), total, n_local)
+            return gather(csr[0], csr[1], total, n_local)
+        # gloo rehearsal: through host memory
+        return gather(csr[0][:total].cpu(), csr[1][:n_local].cpu(), total, n_local)
 
     # ---- timed region: match pass (+ gather to rank 0) over the global batch -----------------
     def step():
@@ -396,6 +423,18 @@ def main():
             do_gather()
         sync()
         gather_ms = td.max_over_ranks(time.perf_counter() - g0, cdev) * 1e3 / args.steps
+
+    if args.dump_csr:  # the lists as the timed step leaves them at rank 0, for the parity test
+        if gather is not None:
+            got = do_gather()
+            if rank == 0:
+                adv, rend = (t.cpu().numpy().astype(np.uint32) for t in got)
+        else:
+            pr = mb.pairs()
+            adv = pr[:, 1].astype(np.uint32)
+            rend = np.cumsum(np.bincount(pr[:, 0] - sb, minlength=n_local)).astype(np.uint32)
+        if rank == 0:
+            np.savez(args.dump_csr, adv=adv, row_end=rend, n_gpus=world)
 
     # ---- end-to-end pipelined pass over PCIe (N = 1) -------------------------------------------
     e2e = None
@@ -570,4 +609,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -237,7 +237,12 @@ int tvm_batch_upload(tvm_engine* e, tvm_batch* b, uint64_t match_cap, char* err,
 /* Enqueues one match pass on the engine stream (async). */
 int tvm_match_launch(tvm_engine* e, tvm_batch* b, char* err, size_t errlen);
 int tvm_engine_sync(tvm_engine* e, char* err, size_t errlen);
-/* After sync: total matches, first poisoned package (-1 none), internal error bits. */
+/* Waits for every stream of the library on `device` (hipDeviceSynchronize inside the library's
+ * own HIP runtime instance) and reports any pending asynchronous error.  Test and health-check
+ * hook; no reference counterpart. */
+int tvm_device_sync(int device, char* err, size_t errlen);
+/* Total matches, first poisoned package (-1 none), internal error bits (read on the engine
+ * stream, behind the batch's launches). */
 int tvm_match_status(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* err_pkg, uint64_t* err_bits);
 /* Copies up to cap pairs {pkg_index, advisory_index} (uint32 x2) to host in (package,
  * advisory) order.  TVM_EINVAL when the device match buffer overflowed (n_matches > the

@@ -52,6 +52,11 @@ def _device_drained(request):
     yield
     if request.node.get_closest_marker("gpu") is None:
         return
-    import torch
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
+    from trivy_amd import _lib
+    if _lib._lib is None:  # the test never loaded the library: nothing of ours can be queued
+        return
+    # hipDeviceSynchronize + hipGetLastError inside libtrivy_amd's own HIP runtime instance,
+    # so the library's streams (engine, pipeline, drop-in) are drained whatever torch loaded
+    e = _lib.errbuf()
+    if _lib._lib.tvm_device_sync(0, e, len(e)):
+        pytest.fail(f"asynchronous device error after {request.node.nodeid}: {e.value.decode()}")

@@ -98,3 +98,18 @@ def test_malformed_files_fail_cleanly():
     struct.pack_into("<IIQ", loop, root * 4096 + 16, 16, 1, root)
     with pytest.raises(ValueError):
         bbolt_records(bytes(loop))
+
+
+def test_page_referenced_twice_is_refused():
+    """A crafted branch whose elements all name one child would be walked count^depth times
+    (a denial of service on an untrusted trivy.db): every page may be reached once."""
+    img = bytearray(bolt_write.write(_fixture_records()[:50], per_leaf=4))
+    root = struct.unpack_from("<Q", img, 16 + 16)[0]
+    leaf = next(p for p in range(3, len(img) // 4096)
+                if p != root and struct.unpack_from("<H", img, p * 4096 + 8)[0] == 0x02)
+    n = 200
+    struct.pack_into("<QHHI", img, root * 4096, root, 0x01, n, 0)
+    for i in range(n):  # zero-length keys, every element naming the same leaf page
+        struct.pack_into("<IIQ", img, root * 4096 + 16 + 16 * i, 16 * (n - i), 0, leaf)
+    with pytest.raises(ValueError, match="twice"):
+        bbolt_records(bytes(img))

@@ -1,0 +1,41 @@
+"""GPU: `python bench.py --gpus 2` really runs two ranks (bench.py launches them itself through
+torch.distributed.run when WORLD_SIZE is unset), and the per-package advisory lists its timed
+step gathers at rank 0 equal the oracle's match of the whole global batch (oracle/match.c),
+element for element, in batch order.  Both ranks share the one MI355X of the box, so the
+collectives run over gloo (TVM_BENCH_BACKEND=gloo; RCCL refuses two ranks on one device)."""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+pytestmark = pytest.mark.gpu
+
+
+def test_bench_two_ranks_csr_equals_oracle(tmp_path, oracle_built):
+    sys.path.insert(0, ROOT)
+    import bench
+    from oracle import match as om
+    dump = str(tmp_path / "csr.npz")
+    flags = ["--config", "c2", "--keys-per-plat", "3000", "--targets", "200", "--pkgs-per-target", "400"]
+    env = dict(os.environ, TVM_BENCH_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                        "--no-cpu", "--no-e2e", "--no-fill", "--dump-csr", dump] + flags,
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["packages"] == 200 * 400
+    assert line["config"]["packages_rank0"] < line["config"]["packages"]  # rank 0 matched a shard only
+    got = np.load(dump)
+    assert int(got["n_gpus"]) == 2
+    wl = bench.C2(argparse.Namespace(keys_per_plat=3000, targets=200, pkgs_per_target=400))
+    opk, oad = om.match(om.Prepared(wl.sdb, wl.batch), n_threads=8)
+    want_end = np.cumsum(np.bincount(opk, minlength=wl.n)).astype(np.uint32)
+    assert np.array_equal(got["adv"], oad.astype(np.uint32))
+    assert np.array_equal(got["row_end"], want_end)

@@ -145,6 +145,7 @@ _SIG = [
     ("tvm_batch_upload", ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_match_launch", ctypes.c_int, [_P, _P, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_engine_sync", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_device_sync", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_match_status", ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64),
                                         ctypes.POINTER(ctypes.c_uint64)]),
     ("tvm_match_fetch", ctypes.c_int, [_P, _P, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),

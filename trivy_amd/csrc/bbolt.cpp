@@ -46,6 +46,7 @@ struct Walker {
   const BboltVisit& visit;
   std::string& err;
   std::vector<std::string_view> path;
+  std::vector<uint8_t> seen;  // file pages already walked: in a valid tree each page is reached once
 
   bool fail(const std::string& m) {
     err = "bbolt: " + m;
@@ -54,6 +55,11 @@ struct Walker {
   // page `id` as a byte range [p, p + span)
   bool page(uint64_t id, const uint8_t*& p, size_t& span) {
     if (psz == 0 || id >= (len / psz)) return fail("page id out of range");
+    // a crafted file whose branch elements all name one child would otherwise be walked
+    // exponentially often (count^depth): reject any page reached twice
+    if (seen.size() != len / psz) seen.assign(len / psz, 0);
+    if (seen[size_t(id)]) return fail("page referenced twice");
+    seen[size_t(id)] = 1;
     const size_t off = size_t(id) * psz;
     if (off + 16 > len) return fail("page past the end of the file");
     p = b + off;
@@ -113,7 +119,7 @@ struct Walker {
 }  // namespace
 
 bool bbolt_walk(const uint8_t* bytes, size_t len, const BboltVisit& visit, std::string& err) {
-  Walker w{bytes, len, 0, visit, err, {}};
+  Walker w{bytes, len, 0, visit, err, {}, {}};
   // the current meta page: magic, version, checksum; larger txid wins
   int best = -1;
   uint64_t best_tx = 0, root = 0;

@@ -313,6 +313,22 @@ tvm_engine* tvm_engine_open(tvm_db* db, int device, char* err, size_t errlen) {
 
 void tvm_engine_close(tvm_engine* e) { delete e; }
 
+int tvm_device_sync(int device, char* err, size_t errlen) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+    set_err(err, errlen, "tvm_device_sync: no such HIP device");
+    return TVM_EDEVICE;
+  }
+  (void)hipSetDevice(device);
+  hipError_t st = hipDeviceSynchronize();
+  if (st == hipSuccess) st = hipGetLastError();
+  if (st != hipSuccess) {
+    set_err(err, errlen, std::string("tvm_device_sync: ") + hipGetErrorString(st));
+    return TVM_EDEVICE;
+  }
+  return TVM_OK;
+}
+
 int tvm_engine_swap(tvm_engine* e, tvm_db* db, char* err, size_t errlen) {
   if (!e || !db || !db->finalized) return TVM_EINVAL;
   std::string msg;
@@ -324,7 +340,8 @@ int tvm_engine_swap(tvm_engine* e, tvm_db* db, char* err, size_t errlen) {
     return TVM_EDEVICE;
   }
   std::unique_lock<std::shared_mutex> lk(e->mu);
-  e->eng.reset(fresh);
+  (void)hipSetDevice(e->device);
+  e->eng.reset(fresh);  // ~Engine drains its streams before it frees the tables
   e->fill.reset(fresh_fill);
   e->db = db;
   e->gen++;
@@ -611,6 +628,8 @@ int tvm_match_launch(tvm_engine* e, tvm_batch* b, char* err, size_t errlen) {
 
 int tvm_engine_sync(tvm_engine* e, char* err, size_t errlen) {
   if (!e) return TVM_EINVAL;
+  std::shared_lock<std::shared_mutex> lk(e->mu);  // a concurrent swap must not free the engine under us
+  (void)hipSetDevice(e->device);
   hipError_t st = hipStreamSynchronize(e->eng->stream());
   if (st != hipSuccess) {
     set_err(err, errlen, std::string("hipStreamSynchronize: ") + hipGetErrorString(st));
@@ -619,16 +638,28 @@ int tvm_engine_sync(tvm_engine* e, char* err, size_t errlen) {
   return TVM_OK;
 }
 
-int tvm_match_status(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* err_pkg, uint64_t* err_bits) {
+// tvm_match_status with the engine's lock already held (shared) by the caller
+static int match_status_locked(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* err_pkg, uint64_t* err_bits) {
   if (!e || !b || !b->uploaded) return TVM_EINVAL;
   unsigned long long ctl[8], mctl[8];
   (void)hipSetDevice(e->device);
-  if (hipMemcpy(ctl, b->m.ctl, sizeof(ctl), hipMemcpyDeviceToHost) != hipSuccess) return TVM_EDEVICE;
-  if (b->merged && hipMemcpy(mctl, cur(b).ctl, sizeof(mctl), hipMemcpyDeviceToHost) != hipSuccess) return TVM_EDEVICE;
+  // the counters are read on the engine stream, behind the batch's launches (a plain
+  // hipMemcpy runs on the null stream, which does not wait for the non-blocking engine stream)
+  hipStream_t st = e->eng->stream();
+  if (hipMemcpyAsync(ctl, b->m.ctl, sizeof(ctl), hipMemcpyDeviceToHost, st) != hipSuccess) return TVM_EDEVICE;
+  if (b->merged && hipMemcpyAsync(mctl, cur(b).ctl, sizeof(mctl), hipMemcpyDeviceToHost, st) != hipSuccess)
+    return TVM_EDEVICE;
+  if (hipStreamSynchronize(st) != hipSuccess) return TVM_EDEVICE;
   if (n_matches) *n_matches = b->merged ? mctl[0] : ctl[0];
   if (err_pkg) *err_pkg = ctl[1] ? int64_t(b->dev.n - ctl[1]) : -1;
   if (err_bits) *err_bits = ctl[3] | (b->merged ? mctl[3] : 0ull);
   return TVM_OK;
+}
+
+int tvm_match_status(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* err_pkg, uint64_t* err_bits) {
+  if (!e || !b || !b->uploaded) return TVM_EINVAL;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  return match_status_locked(e, b, n_matches, err_pkg, err_bits);
 }
 
 int tvm_match_fetch(tvm_engine* e, tvm_batch* b, uint32_t* pairs, uint64_t cap, uint64_t* n_out) {
@@ -1172,7 +1203,7 @@ int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint
   if (hipStreamSynchronize(st) != hipSuccess) return TVM_EDEVICE;
   uint64_t n = 0;
   int64_t errp = -1;
-  int rc = tvm_match_status(e, b, &n, &errp, nullptr);
+  int rc = match_status_locked(e, b, &n, &errp, nullptr);
   if (rc) return rc;
   if (n > cur(b).cap || n > b->fill_cap) {
     set_err(err, errlen, "tvm_match_filter: run tvm_match_launch + tvm_match_fill with a large enough match buffer first");
@@ -1308,6 +1339,8 @@ int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32
     return TVM_EINVAL;
   }
   b->pipe.reset(new Pipeline());
+  b->pipe_total = 0;  // no valid pass of the new pipeline yet
+  b->pipe_wide_for = ~0ull;
   std::string msg;
   const bool packed = !(flags & TVM_PIPE_ADV32) && e->db->db.advs.size() < (1ull << 24);
   if (!b->pipe->prepare(*e->eng, b->hb, match_cap, chunk_packages, !(flags & TVM_PIPE_RAW), packed, msg)) {
@@ -1315,7 +1348,7 @@ int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
   }
-  b->pinned = true;  // the host arrays are registered in place: no more adds
+  b->pinned = true;  // the pipeline was sized for exactly these packages: no more adds
   return TVM_OK;
 }
 
@@ -1331,6 +1364,8 @@ int tvm_pipeline_run(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* 
   uint64_t total = 0, bits = 0;
   int64_t ep = -1;
   const auto t0 = std::chrono::steady_clock::now();
+  b->pipe_total = 0;  // a failed pass leaves no result behind
+  b->pipe_wide_for = ~0ull;
   const bool ok = b->pipe->run(*e->eng, b->hb, total, ep, bits, msg);
   const double dt = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (!ok) {

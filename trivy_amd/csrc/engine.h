@@ -110,7 +110,9 @@ struct DevMatches {
   // poisoned pkg (0 = none), [2] spill words used, [3] error bits
   unsigned long long* ctl = nullptr;
 };
-enum : uint32_t { ERR_SPILL = 1, ERR_TILES = 2 };
+// ERR_BOUNDS: a result move or an unpack found an index beyond the buffer it was sized for
+// (the store is dropped and the pass fails; never expected: a guard, not a code path)
+enum : uint32_t { ERR_SPILL = 1, ERR_TILES = 2, ERR_BOUNDS = 4 };
 
 // The end-to-end pipeline's result move for one chunk (tiles [t0, t1)): the chunk's match
 // segments, straight from the tile directory, become the per-package advisory lists (CSR)
@@ -136,6 +138,9 @@ struct CopyOutArgs {
   uint32_t pkg_base = 0;              // subtracted from the match list's package indices
   uint64_t cap = 0;                   // match / result capacity (an overflowed pass moves no advisories)
   uint32_t packed = 0;                // 1: advisories as 3-byte little-endian indices (the DB has < 2^24)
+  uint64_t adv_units = 0;             // 16-byte units of adv_h
+  uint64_t row_end_units = 0;         // 16-byte units of row_end_h
+  unsigned long long* ctl = nullptr;  // the pass's control block: ctl[3] |= ERR_BOUNDS on a guard hit
 };
 constexpr uint32_t kCopyLdsWords = kTile + 8;  // copy_out_tiles' LDS: counts + scratch
 constexpr uint32_t kCopyWorkgroups = 256;      // workgroups of a result move
@@ -195,10 +200,19 @@ __device__ __forceinline__ void copy_out_tiles(const CopyOutArgs& a, uint32_t wg
     for (uint32_t w = 0; w < wave; w++) x += red[w];
     cnt[tid] = uint32_t(b) + x;  // row end of package p_first + tid (row ends are 32-bit)
     __syncthreads();
-    if (tid < kTile / 4)
-      reinterpret_cast<uint4*>(a.row_end_h)[p_first / 4 + tid] = reinterpret_cast<const uint4*>(cnt)[tid];
+    if (tid < kTile / 4) {
+      if (p_first / 4 + tid < a.row_end_units)
+        reinterpret_cast<uint4*>(a.row_end_h)[p_first / 4 + tid] = reinterpret_cast<const uint4*>(cnt)[tid];
+      else
+        atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
+    }
     if (a.packed) {  // 3 bytes per advisory: destination bytes [3b, 3(b + count)) in 16-byte units
-      const uint64_t B0 = 3 * b, B1 = 3 * (b + d.count), U0 = B0 >> 4, nu = fits ? ((B1 + 15) >> 4) - U0 : 0;
+      const uint64_t B0 = 3 * b, B1 = 3 * (b + d.count), U0 = B0 >> 4;
+      uint64_t nu = fits ? ((B1 + 15) >> 4) - U0 : 0;
+      if (U0 + nu > a.adv_units) {  // guard: never expected (adv_h holds 4 * cap bytes)
+        if (tid == 0) atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
+        nu = 0;
+      }
       uint8_t* dst = reinterpret_cast<uint8_t*>(a.adv_h);
       constexpr int kP = 2;
       for (uint64_t j0 = 0; j0 < nu; j0 += uint64_t(kP) * kTile) {
@@ -238,7 +252,12 @@ __device__ __forceinline__ void copy_out_tiles(const CopyOutArgs& a, uint32_t wg
       continue;
     }
     // the segment, realigned in registers to the destination's 16-byte units
-    const uint64_t u0 = b >> 2, nu = fits ? ((b + d.count + 3) >> 2) - u0 : 0;
+    const uint64_t u0 = b >> 2;
+    uint64_t nu = fits ? ((b + d.count + 3) >> 2) - u0 : 0;
+    if (u0 + nu > a.adv_units) {  // guard: never expected
+      if (tid == 0) atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
+      nu = 0;
+    }
     const uint32_t sh = uint32_t(b & 3);
     constexpr int kU = 4;
     for (uint64_t j0 = 0; j0 < nu; j0 += uint64_t(kU) * kTile) {

@@ -165,6 +165,7 @@ void HostBatch::clear() {
 
 Engine::~Engine() {
   if (dev_ >= 0) (void)hipSetDevice(dev_);
+  if (stream_) (void)hipStreamSynchronize(stream_);  // no queued launch may outlive the tables
   dropin_.reset();
   for (void* p : allocs_) (void)hipFree(p);
   if (stream_) (void)hipStreamDestroy(stream_);

@@ -25,8 +25,8 @@ void launch_order(uint32_t n_tiles, hipStream_t st, const OrderArgs& a);
 void launch_copy_out(hipStream_t st, const CopyOutArgs& a);  // engine.h copy_out_tiles as its own kernel
 
 
-// One batch's pipeline state.  prepare() pins the batch's host arrays (hipHostRegister),
-// sizes the device batch, the match buffers and the pinned result buffers; run() then
+// One batch's pipeline state.  prepare() builds the batch's pinned transport form (or a
+// pinned copy of its raw arrays), sizes the device batch, the match buffers and the pinned result buffers; run() then
 // streams the batch through in chunks of whole tiles:
 //   copy stream    DMA of chunk c to HBM (package words, tile offsets, string bytes, attributes);
 //   kernel stream  (after chunk c's upload) one match launch whose first workgroups turn
@@ -84,8 +84,14 @@ class Pipeline {
   std::vector<hipEvent_t> ev_h_, ev_k_;  // chunk uploaded / chunk's result move done
   uint32_t* row_end_d_ = nullptr;        // row ends in HBM when the DMA engine carries them up
   std::vector<uint32_t> bounds_;     // chunk c = tiles [bounds_[c], bounds_[c + 1])
-  std::vector<uint64_t> toff_;       // tile offsets + the arena end (registered)
-  std::vector<void*> registered_;
+  std::vector<uint64_t> toff_;       // tile offsets + the arena end
+  // raw form: the batch's arrays in one pinned block (stage_raw)
+  uint8_t* raw_h_ = nullptr;
+  uint2* raw_pk_ = nullptr;
+  uint64_t* raw_toff_ = nullptr;
+  uint8_t* raw_arena_ = nullptr;
+  uint2* raw_attr_ = nullptr;
+  bool stage_raw(const HostBatch& hb, std::string& err);
   DevBatch db_;
   DevMatches m_;
   unsigned long long* chunk_base_d_ = nullptr;  // chunk c's first CSR position (written by chunk c-1's move)
@@ -95,6 +101,8 @@ class Pipeline {
   uint32_t* row_end_hd_ = nullptr;
   unsigned long long* ctl_h_ = nullptr;
   uint64_t cap_ = 0, h2d_ = 0, d2h_ = 0;
+  uint64_t wire_bytes_ = 0;                       // size of wire_h_ / wire_d_
+  uint64_t adv_units_ = 0, row_end_units_ = 0;    // 16-byte units of adv_h_ / row_end_h_ (guards)
   bool prepared_ = false;
   bool packed_ = false;  // no Engine pointer: the batch may outlive a hot swap (the C-ABI checks the generation)
 };

@@ -47,6 +47,9 @@ struct UnpackArgs {
   uint8_t* arena;
   uint2* attr;
   uint32_t p0, m, g0, groups;
+  uint64_t arena_cap;       // bytes of the batch arena (guard)
+  uint64_t wire_cap;        // bytes of the device wire buffer (guard)
+  unsigned long long* ctl;  // ctl[3] |= ERR_BOUNDS on a guard hit
 };
 
 // One chunk of the transport form -> the batch's own arrays in HBM (pk, tile_off, arena,
@@ -80,8 +83,15 @@ __global__ __launch_bounds__(256) void unpack_kernel(UnpackArgs a) {
     const uint32_t y = __shfl_up(x, o, 64);
     if (lane >= uint32_t(o)) x += y;
   }
+  // guard (never expected: build_wire and alloc_batch size both sides): an out-of-range
+  // reference or destination fails the pass instead of touching memory
+  const uint64_t dst = g_off + (x - len);
+  if (dst + len > a.arena_cap || uint64_t(nr) + nl > a.wire_cap || uint64_t(vr) + vl > a.wire_cap) {
+    atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
+    return;
+  }
   // 8 loads in flight per lane before any store (the wire and the arena never overlap)
-  uint8_t* __restrict__ d = a.arena + g_off + (x - len);
+  uint8_t* __restrict__ d = a.arena + dst;
   copy_bytes(d, a.wire + nr, nl);
   copy_bytes(d + nl, a.wire + vr, vl);
 }
@@ -110,7 +120,8 @@ bool Pipeline::build_wire(const HostBatch& hb, std::string& err) {
   uint64_t bound = 0;
   for (uint32_t c = 0; c < nc; c++) {
     const uint64_t m = std::min<uint64_t>(uint64_t(bounds_[c + 1]) * kTile, n) - std::min<uint64_t>(uint64_t(bounds_[c]) * kTile, n);
-    bound += 6 * 16 + m * 11 + (uint64_t(bounds_[c + 1] - bounds_[c]) * kGroupsPerTile + 1) * 8 + (has_attr ? m * 8 : 0);
+    // 7 sections per chunk, each start 16-byte aligned (+ the chunk end): 8 alignment pads
+    bound += 8 * 16 + m * 11 + (uint64_t(bounds_[c + 1] - bounds_[c]) * kGroupsPerTile + 1) * 8 + (has_attr ? m * 8 : 0);
   }
   bound += hb.arena.size() + 16;
   if (bound >= (1ull << 32)) return true;  // references are 32-bit
@@ -119,6 +130,7 @@ bool Pipeline::build_wire(const HostBatch& hb, std::string& err) {
   wire_h_ = static_cast<uint8_t*>(p);
   if (!ok(hipMalloc(&p, bound), "hipMalloc(transport form)", err)) return false;
   wire_d_ = static_cast<uint8_t*>(p);
+  wire_bytes_ = bound;
   if (!ok(hipMalloc(&p, ptab.size() * 4), "hipMalloc(platform table)", err) ||
       !ok(hipMemcpy(p, ptab.data(), ptab.size() * 4, hipMemcpyHostToDevice), "H2D platform table", err))
     return false;
@@ -187,7 +199,34 @@ bool Pipeline::build_wire(const HostBatch& hb, std::string& err) {
     w.bytes = pos - w.off;
     wc_.push_back(w);
   }
+  if (pos > bound) {  // cannot happen (the bound counts every string as new); never DMA past the buffer
+    err = "pipeline: transport form larger than its bound";
+    return false;
+  }
   encode_us_ = uint64_t(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - start).count());
+  return true;
+}
+
+// The raw form: the batch's arrays copied once into one pinned staging block (round 3
+// pinned the caller's std::vector storage in place with hipHostRegister; heap vectors are
+// not page-aligned, so a registration covered neighbouring heap objects' pages and two of a
+// batch's registrations could share a page - the staging copy keeps the pinned range owned).
+bool Pipeline::stage_raw(const HostBatch& hb, std::string& err) {
+  const size_t b_pk = align16(hb.pk.size() * sizeof(uint2)), b_toff = align16(toff_.size() * 8),
+               b_arena = align16(hb.arena.size()), b_attr = align16(hb.attr.size() * sizeof(uint2));
+  void* p = nullptr;
+  if (!ok(hipHostMalloc(&p, std::max<size_t>(b_pk + b_toff + b_arena + b_attr, 16), hipHostMallocDefault),
+          "hipHostMalloc(raw staging)", err))
+    return false;
+  raw_h_ = static_cast<uint8_t*>(p);
+  raw_pk_ = reinterpret_cast<uint2*>(raw_h_);
+  raw_toff_ = reinterpret_cast<uint64_t*>(raw_h_ + b_pk);
+  raw_arena_ = raw_h_ + b_pk + b_toff;
+  raw_attr_ = reinterpret_cast<uint2*>(raw_h_ + b_pk + b_toff + b_arena);
+  if (!hb.pk.empty()) std::memcpy(raw_pk_, hb.pk.data(), hb.pk.size() * sizeof(uint2));
+  if (!toff_.empty()) std::memcpy(raw_toff_, toff_.data(), toff_.size() * 8);
+  if (!hb.arena.empty()) std::memcpy(raw_arena_, hb.arena.data(), hb.arena.size());
+  if (!hb.attr.empty()) std::memcpy(raw_attr_, hb.attr.data(), hb.attr.size() * sizeof(uint2));
   return true;
 }
 
@@ -204,15 +243,16 @@ void Pipeline::release() {
   for (void* p : {static_cast<void*>(chunk_base_d_), static_cast<void*>(wire_d_), static_cast<void*>(ptab_d_)})
     if (p) (void)hipFree(p);
   if (wire_h_) (void)hipHostFree(wire_h_);
+  if (raw_h_) (void)hipHostFree(raw_h_);
   wire_h_ = nullptr;
+  raw_h_ = nullptr;
+  wire_bytes_ = 0;
   wire_d_ = nullptr;
   ptab_d_ = nullptr;
   wc_.clear();
   encode_us_ = 0;
   for (void* p : {static_cast<void*>(adv_h_), static_cast<void*>(row_end_h_), static_cast<void*>(ctl_h_)})
     if (p) (void)hipHostFree(p);
-  for (void* p : registered_) (void)hipHostUnregister(p);
-  registered_.clear();
   for (hipEvent_t e : ev_h_) (void)hipEventDestroy(e);
   for (hipEvent_t e : ev_k_) (void)hipEventDestroy(e);
   ev_h_.clear();
@@ -261,18 +301,8 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
       !ok(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking), "hipStreamCreate", err) ||
       !ok(hipStreamCreateWithFlags(&s_k_, hipStreamNonBlocking), "hipStreamCreate", err))
     return false;
-  // pin the caller's host arrays in place: the copies are DMA from them, no staging memcpy
-  auto reg = [&](const void* p, size_t bytes) {
-    if (!bytes) return true;
-    if (!ok(hipHostRegister(const_cast<void*>(p), bytes, hipHostRegisterDefault), "hipHostRegister", err)) return false;
-    registered_.push_back(const_cast<void*>(p));
-    return true;
-  };
   if (transport && !build_wire(hb, err)) return false;
-  if (wc_.empty() &&
-      (!reg(hb.pk.data(), hb.pk.size() * sizeof(uint2)) || !reg(hb.arena.data(), hb.arena.size()) ||
-       !reg(toff_.data(), toff_.size() * 8) || !reg(hb.attr.data(), hb.attr.size() * sizeof(uint2))))
-    return false;
+  if (wc_.empty() && !stage_raw(hb, err)) return false;
   if (!eng.alloc_batch(hb, db_, err) || !eng.alloc_matches(cap_, db_.n, m_, err)) return false;
   if (!hb.cpe_bits.empty() && hb.cpe_words) {  // CPE sets: small, copied once here
     void* p = nullptr;
@@ -285,6 +315,8 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
   }
   // CSR buffers padded to whole 16-byte units (the result move copies units)
   const size_t cap4 = (cap_ + 3) & ~size_t(3), n4 = (size_t(n_tiles) * kTile + 3) & ~size_t(3);
+  adv_units_ = cap4 / 4;
+  row_end_units_ = std::max<size_t>(n4, 4) / 4;
   void* p = nullptr;
   if (!ok(hipMalloc(&p, (size_t(nc) + 1) * 8), "hipMalloc(chunk bases)", err)) return false;
   chunk_base_d_ = static_cast<unsigned long long*>(p);
@@ -345,6 +377,9 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
     ca.pkg_base = db_.pkg_base;
     ca.cap = cap_;
     ca.packed = packed_ ? 1u : 0u;
+    ca.adv_units = adv_units_;
+    ca.row_end_units = row_end_units_;
+    ca.ctl = m_.ctl;
     return ca;
   };
   // measurement only: TVM_PIPE_TRACE=1 prints the host time spent in each call of a pass;
@@ -397,6 +432,9 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
       ua.m = w.m;
       ua.g0 = uint32_t(g0);
       ua.groups = w.groups;
+      ua.arena_cap = db_.arena_bytes;
+      ua.wire_cap = wire_bytes_;
+      ua.ctl = m_.ctl;
       h2d_ += w.bytes;
       if (!copies_first &&
           !ok(hipMemcpyAsync(wire_d_ + w.off, wire_h_ + w.off, w.bytes, hipMemcpyHostToDevice, s_h2d_), "H2D chunk", err))
@@ -414,14 +452,14 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
         if (!ok(hipGetLastError(), "unpack kernel launch", err)) return false;
       }
       if (trace) std::fprintf(stderr, "pipe c%u upload + unpack queued %.1f us\n", c, us());
-    } else if (!ok(hipMemcpyAsync(db_.pk + p0, hb.pk.data() + p0, (p1 - p0) * sizeof(uint2), hipMemcpyHostToDevice, s_h2d_),
+    } else if (!ok(hipMemcpyAsync(db_.pk + p0, raw_pk_ + p0, (p1 - p0) * sizeof(uint2), hipMemcpyHostToDevice, s_h2d_),
             "H2D packages", err) ||
-        !ok(hipMemcpyAsync(db_.tile_off + g0, toff_.data() + g0, (g1 - g0 + 1) * 8, hipMemcpyHostToDevice, s_h2d_),
+        !ok(hipMemcpyAsync(db_.tile_off + g0, raw_toff_ + g0, (g1 - g0 + 1) * 8, hipMemcpyHostToDevice, s_h2d_),
             "H2D group offsets", err) ||
-        (a1 > a0 && !ok(hipMemcpyAsync(db_.arena + a0, hb.arena.data() + a0, a1 - a0, hipMemcpyHostToDevice, s_h2d_),
+        (a1 > a0 && !ok(hipMemcpyAsync(db_.arena + a0, raw_arena_ + a0, a1 - a0, hipMemcpyHostToDevice, s_h2d_),
                         "H2D strings", err)) ||
         (!hb.attr.empty() &&
-         !ok(hipMemcpyAsync(db_.attr + p0, hb.attr.data() + p0, (p1 - p0) * sizeof(uint2), hipMemcpyHostToDevice, s_h2d_),
+         !ok(hipMemcpyAsync(db_.attr + p0, raw_attr_ + p0, (p1 - p0) * sizeof(uint2), hipMemcpyHostToDevice, s_h2d_),
              "H2D attributes", err)) ||
         !ok(hipEventRecord(ev_h_[c], s_h2d_), "hipEventRecord", err) ||
         !ok(hipStreamWaitEvent(s_k_, ev_h_[c], 0), "hipStreamWaitEvent", err)) {
