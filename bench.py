@@ -460,9 +460,37 @@ def main():
                          "version string once + per-package references, one DMA per chunk) + the kernel that "
                          "rebuilds each chunk in HBM + match kernels + the per-package advisory lists (CSR) "
                          "written into pinned host memory by the next launch's first workgroups",
-               "outside": "prepare (once per batch: pinning, sizing, building the transport form, "
-                          "prepare_encode_ms on one host thread)"}
+               "prepare_ms": st["prepare_ms"],
+               "outside": "prepare (once per batch: sizing, building the transport form on the host threads "
+                          "(prepare_encode_ms); the batch is re-run, see fresh_batch for batches seen once)"}
         mp.close()
+
+    # ---- fresh batches: each batch prepared and matched once (a fleet scan's steady state) ----
+    fresh = None
+    if world == 1 and not args.no_e2e and rank == 0:
+        runs = []
+        for _ in range(4):  # the first warms the block cache (pool.h); the median of the rest is reported
+            tb = time.perf_counter()
+            mf = MatchBatch(eng)
+            wl.fill(mf)
+            tp = time.perf_counter()
+            mf.pipeline_prepare(match_cap=total, chunk_packages=args.chunk, raw=True)
+            tr = time.perf_counter()
+            got, ep, _ = mf.pipeline_run()
+            te = time.perf_counter()
+            if got != total or ep != -1:
+                raise RuntimeError("fresh-batch pass disagrees with the device-resident pass")
+            st = mf.pipeline_stats()
+            runs.append({"build_ms": (tp - tb) * 1e3, "prepare_ms": (tr - tp) * 1e3, "pass_ms": (te - tr) * 1e3,
+                         "h2d_bytes": st["h2d_bytes"], "d2h_bytes": st["d2h_bytes"]})
+            mf.close()
+        steady = sorted(runs[1:], key=lambda r: r["prepare_ms"] + r["pass_ms"])
+        med = steady[len(steady) // 2]
+        fresh = dict(med, packages_per_s=wl.n / ((med["prepare_ms"] + med["pass_ms"]) / 1e3), batches=len(runs),
+                     form="raw (pinned staging copy on the host threads; no per-batch string dedup)",
+                     inside="prepare (freeze, size, pinned staging copy, buffers from the block cache) + one "
+                            "pipelined pass (upload, match, per-package advisory lists back in pinned host memory)",
+                     outside="build_ms: the caller adding the batch's packages (tvm_batch_add_many per target)")
 
     fill = None
     if rank == 0 and wl.has_vulns and world == 1:
@@ -599,6 +627,8 @@ def main():
             line["gather_ms"] = gather_ms
         if e2e is not None:
             line["end_to_end"] = e2e
+        if fresh is not None:
+            line["fresh_batch"] = fresh
         if fill is not None:
             line["fill_info"] = fill
         if dropin is not None:

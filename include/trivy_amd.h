@@ -299,11 +299,13 @@ int tvm_batch_upload_into(tvm_engine* e, tvm_batch* b, void* pkg_dev, void* adv_
 
 /* ---- end-to-end pipelined pass ---------------------------------------------------------
  * The whole detector path for a host-side batch in one call: the batch goes to the GPU in
- * chunks (DMA from the batch's own host arrays, pinned in place by prepare), each chunk is
+ * chunks (DMA from a pinned copy prepare builds on the host threads), each chunk is
  * matched as soon as it lands, and its per-package advisory lists come back (CSR) while
  * the next chunk is matched.  This is what a cgo caller pays per batch of targets
  * (detect.go:63 / library/detect.go:11 called for every target of a scan). */
-/* Pins the batch (no more adds afterwards) and sizes every device / pinned buffer.  Unless
+/* Freezes the batch (no more adds afterwards) and sizes every device / pinned buffer (taken
+ * from a process-wide block cache, so a fresh batch allocates nothing once one of its size has
+ * run; host threads: TVM_HOST_THREADS, else OMP_NUM_THREADS, else all).  Unless
  * flags has TVM_PIPE_RAW, the batch travels in its transport form when it has one (every
  * name and version under 256 bytes, at most 255 platforms): each distinct name and each
  * distinct version string crosses the link once, packages carry references to them, and
@@ -328,6 +330,23 @@ int tvm_pipeline_result_raw(tvm_batch* b, const void** adv, uint32_t* width, con
 /* [0] bytes the last pass copied host to device, [1] device to host, [2] chunks, [3] 1 when
  * the batch travels in its transport form, [4] prepare's host time building it (us). */
 int tvm_pipeline_stats(tvm_batch* b, uint64_t out[5]);
+/* The transport form prepare would build for n packages (platform ids as the batch holds
+ * them, 0xFFFFFFFF = absent bucket), on the host alone (no device; test and inspection hook).
+ * With out = NULL only the sizes are returned.  chunks: 10 values per
+ * chunk {offset, bytes, name-ref / version-ref / lengths / platform / group-offset / attribute
+ * section offsets, packages, groups}; plats: platform index -> platform id.  *bytes = 0:
+ * the batch has no transport form. */
+int tvm_wire_encode(size_t n, const uint32_t* plat, const char* arena, const uint64_t* name_off, const uint32_t* name_len,
+                    const uint64_t* ver_off, const uint32_t* ver_len, uint32_t chunk_packages, int threads, void* out,
+                    uint64_t cap, uint64_t* bytes,
+                    uint64_t* chunks, uint64_t chunks_cap, uint64_t* n_chunks, uint32_t* plats, uint32_t plats_cap,
+                    uint32_t* n_plats);
+/* Host time of the last prepare (us): building the transport form, and the whole call. */
+int tvm_pipeline_times(tvm_batch* b, uint64_t* encode_us, uint64_t* prepare_us);
+/* The block cache behind batch buffers: {cached device bytes, cached pinned host bytes, hits,
+ * misses}; tvm_pool_trim frees every cached block. */
+void tvm_pool_stats(uint64_t out[4]);
+void tvm_pool_trim(void);
 
 /* ---- Red Hat on the batch path ----------------------------------------------------------
  * After tvm_match_launch (+ sync): the Red Hat driver's epilogue for every package of the

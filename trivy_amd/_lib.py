@@ -146,6 +146,15 @@ _SIG = [
     ("tvm_match_launch", ctypes.c_int, [_P, _P, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_engine_sync", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_device_sync", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_pipeline_times", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    ("tvm_pool_stats", None, [ctypes.POINTER(ctypes.c_uint64)]),
+    ("tvm_wire_encode", ctypes.c_int, [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                                       ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p, ctypes.c_uint64,
+                                       ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p, ctypes.c_uint32,
+                                       ctypes.POINTER(ctypes.c_uint32)]),
+    ("tvm_pool_trim", None, []),
     ("tvm_match_status", ctypes.c_int, [_P, _P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64),
                                         ctypes.POINTER(ctypes.c_uint64)]),
     ("tvm_match_fetch", ctypes.c_int, [_P, _P, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),

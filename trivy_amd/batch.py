@@ -282,8 +282,10 @@ class MatchBatch:
         out = (ctypes.c_uint64 * 5)()
         if lib().tvm_pipeline_stats(self.h, out):
             raise RuntimeError("tvm_pipeline_stats")
+        enc, prep = ctypes.c_uint64(), ctypes.c_uint64()
+        lib().tvm_pipeline_times(self.h, ctypes.byref(enc), ctypes.byref(prep))
         return {"h2d_bytes": out[0], "d2h_bytes": out[1], "chunks": out[2], "transport_form": bool(out[3]),
-                "encode_ms": out[4] / 1e3}
+                "encode_ms": out[4] / 1e3, "prepare_ms": prep.value / 1e3}
 
     # ---- FillInfo fused behind the match list (tvm_match_fill*) ----
     def fill(self, sync=True):

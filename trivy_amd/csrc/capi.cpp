@@ -20,6 +20,8 @@
 #include "libver.h"
 #include "bbolt.h"
 #include "pipeline.h"
+#include "pool.h"
+#include "wire.h"
 #include "redhat.h"
 #include "vulninfo.h"
 
@@ -1416,6 +1418,63 @@ int tvm_pipeline_result_raw(tvm_batch* b, const void** adv, uint32_t* width, con
   if (n_matches) *n_matches = b->pipe_total;
   return TVM_OK;
 }
+
+int tvm_wire_encode(size_t n, const uint32_t* plat, const char* arena, const uint64_t* name_off, const uint32_t* name_len,
+                    const uint64_t* ver_off, const uint32_t* ver_len, uint32_t chunk_packages, int threads, void* out,
+                    uint64_t cap, uint64_t* bytes,
+                    uint64_t* chunks, uint64_t chunks_cap, uint64_t* n_chunks, uint32_t* plats, uint32_t plats_cap,
+                    uint32_t* n_plats) {
+  if (!bytes || !n_chunks || !n_plats || chunk_packages == 0 || threads < 1 ||
+      (n && (!plat || !arena || !name_off || !name_len || !ver_off || !ver_len)))
+    return TVM_EINVAL;
+  HostBatch hb;
+  for (size_t i = 0; i < n; i++)
+    hb.add(plat[i], std::string_view(arena + name_off[i], name_len[i]), std::string_view(arena + ver_off[i], ver_len[i]));
+  const uint32_t n_tiles = hb.n_tiles(), chunk_tiles = (chunk_packages + kTile - 1) / kTile;
+  std::vector<uint32_t> bounds;
+  for (uint32_t t = 0; t < n_tiles; t += chunk_tiles) bounds.push_back(t);
+  bounds.push_back(n_tiles);
+  if (n_tiles == 0) bounds = {0, 0};
+  std::vector<uint64_t> toff = hb.tile_off;
+  toff.resize(size_t(n_tiles) * kGroupsPerTile + 1, hb.arena.size());
+  WireEncoder enc;
+  std::string msg;
+  if (!enc.plan(hb, toff, bounds, threads, msg)) {
+    *bytes = 0;
+    *n_chunks = 0;
+    *n_plats = 0;
+    return msg.empty() ? TVM_OK : TVM_EINVAL;  // no transport form: zero bytes
+  }
+  *bytes = enc.bytes();
+  *n_chunks = enc.chunks().size();
+  *n_plats = uint32_t(enc.platforms().size());
+  if (!out) return TVM_OK;
+  if (cap < enc.bytes() || chunks_cap < enc.chunks().size() || plats_cap < enc.platforms().size() || !chunks || !plats)
+    return TVM_EINVAL;
+  enc.emit(static_cast<uint8_t*>(out));
+  for (size_t c = 0; c < enc.chunks().size(); c++) {
+    const WireChunk& w = enc.chunks()[c];
+    const uint64_t v[10] = {w.off, w.bytes, w.o_nref, w.o_vref, w.o_lens, w.o_plat, w.o_toff, w.o_attr, w.m, w.groups};
+    std::memcpy(chunks + 10 * c, v, sizeof(v));
+  }
+  std::memcpy(plats, enc.platforms().data(), enc.platforms().size() * 4);
+  return TVM_OK;
+}
+
+int tvm_pipeline_times(tvm_batch* b, uint64_t* encode_us, uint64_t* prepare_us) {
+  if (!b || !b->pipe) return TVM_EINVAL;
+  if (encode_us) *encode_us = b->pipe->encode_us();
+  if (prepare_us) *prepare_us = b->pipe->prepare_us();
+  return TVM_OK;
+}
+
+void tvm_pool_stats(uint64_t out[4]) {
+  unsigned long long o[4];
+  pool_stats(o);
+  for (int i = 0; i < 4; i++) out[i] = o[i];
+}
+
+void tvm_pool_trim(void) { pool_trim(); }
 
 int tvm_pipeline_stats(tvm_batch* b, uint64_t out[5]) {
   if (!b || !b->pipe || !out) return TVM_EINVAL;

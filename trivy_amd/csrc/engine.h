@@ -301,15 +301,17 @@ class Engine {
 
   // Device-resident batch management.  alloc_batch sizes the device buffers without
   // copying (the pipelined path copies chunk by chunk); upload = alloc + copy.
-  bool alloc_batch(const HostBatch& hb, DevBatch& b, std::string& err);
+  // pooled: the buffers come from / go back to the process-wide block cache (pool.h; the
+  // pipeline's per-batch buffers), else plain hipMalloc / hipFree
+  bool alloc_batch(const HostBatch& hb, DevBatch& b, std::string& err, bool pooled = false);
   bool upload(const HostBatch& hb, DevBatch& b, std::string& err);
   uint32_t grammar_set(const HostBatch& hb) const;
   uint64_t scratch_words(const HostBatch& hb) const;
   // Frees a batch's / a match list's device buffers (device = the GPU they live on; no
   // engine state is touched, so a batch outlives a hot swap of the engine's tables).
-  static void free_batch(int device, DevBatch& b);
-  bool alloc_matches(uint64_t cap, uint32_t n_pkgs, DevMatches& m, std::string& err);
-  static void free_matches(int device, DevMatches& m);
+  static void free_batch(int device, DevBatch& b, bool pooled = false);
+  bool alloc_matches(uint64_t cap, uint32_t n_pkgs, DevMatches& m, std::string& err, bool pooled = false);
+  static void free_matches(int device, DevMatches& m, bool pooled = false);
 
   // Enqueues one match pass (probe + sweep over every tile) on `stream`; no host sync.
   bool launch(const DevBatch& b, const DevMatches& m, hipStream_t stream, std::string& err);

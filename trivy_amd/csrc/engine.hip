@@ -2,6 +2,8 @@
 // upload, variant selection and launch of the two match kernels (match_kernel.h,
 // instantiated in kern_*.hip), and read-back of the ordered match list.
 #include "engine.h"
+#include "host_par.h"
+#include "pool.h"
 
 #include <algorithm>
 #include <mutex>
@@ -86,12 +88,25 @@ bool upload_vec(const std::vector<T>& v, T** dst, std::vector<void*>& allocs, ui
   return true;
 }
 
+// pool_dev >= 0: the block comes from the process-wide cache of that device (pool.h)
 template <class T>
-bool dmalloc(T** p, size_t count, const char* what, std::string& err) {
+bool dmalloc(T** p, size_t count, const char* what, std::string& err, int pool_dev = -1) {
   void* q = nullptr;
-  if (!hip_ok(hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T)), what, err)) return false;
+  const size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+  if (pool_dev >= 0) {
+    q = pool_device_get(pool_dev, bytes, what, err);
+    if (!q) return false;
+  } else if (!hip_ok(hipMalloc(&q, bytes), what, err)) {
+    return false;
+  }
   *p = static_cast<T*>(q);
   return true;
+}
+
+void dfree(void* p, bool pooled, int device) {
+  if (!p) return;
+  if (pooled) pool_device_put(device, p);
+  else (void)hipFree(p);
 }
 
 }  // namespace
@@ -223,33 +238,42 @@ int Engine::set_variant(int v) {
 // Grammar bits (1 << Cmp) of the platforms a batch touches.
 uint32_t Engine::grammar_set(const HostBatch& hb) const {
   const auto& pi = db_->plat_info;
-  std::vector<uint8_t> seen(pi.size(), 0);
-  uint32_t gm = 0;
-  for (const uint2& d : hb.pk)
-    if (d.x < pi.size() && !seen[d.x]) {
-      seen[d.x] = 1;
-      gm |= 1u << pi[d.x].cmp;
+  std::atomic<uint32_t> gm{0};
+  range_for(hb.pk.size(), 1 << 18, [&](size_t a, size_t b) {  // host threads: a fresh batch's prepare
+    uint32_t g = 0, last = 0xFFFFFFFFu;
+    for (size_t i = a; i < b; i++) {
+      const uint32_t p = hb.pk[i].x;
+      if (p != last && p < pi.size()) g |= 1u << pi[p].cmp;
+      last = p;
     }
-  return gm & GM_ALL;
+    gm.fetch_or(g, std::memory_order_relaxed);
+  });
+  return gm.load() & GM_ALL;
 }
 
 // Scratch words a batch may need: keys longer than 32 bytes (the widest grammar's bound)
 // and, for Maven packages, the packed parse of the installed version (AUX_MVN rows).
 uint64_t Engine::scratch_words(const HostBatch& hb) const {
   const auto& pi = db_->plat_info;
-  uint64_t w = 0;
-  for (const uint2& d : hb.pk) {
-    const uint32_t vlen = d.y >> 16;
-    const uint32_t need = (key_bound_any(vlen) + 7) / 8;
-    if (need > kKeyWords) w += need;
-    if (d.x < pi.size() && pi[d.x].cmp == CMP_MAVEN)
-      w += (uint64_t(kMvnPackedWords) * std::min<uint32_t>(2 * vlen + 3, kMvnMaxTok) + 1) / 2;
-  }
-  return w;
+  std::atomic<uint64_t> total{0};
+  range_for(hb.pk.size(), 1 << 18, [&](size_t a, size_t b) {
+    uint64_t w = 0;
+    for (size_t i = a; i < b; i++) {
+      const uint2 d = hb.pk[i];
+      const uint32_t vlen = d.y >> 16;
+      const uint32_t need = (key_bound_any(vlen) + 7) / 8;
+      if (need > kKeyWords) w += need;
+      if (d.x < pi.size() && pi[d.x].cmp == CMP_MAVEN)
+        w += (uint64_t(kMvnPackedWords) * std::min<uint32_t>(2 * vlen + 3, kMvnMaxTok) + 1) / 2;
+    }
+    total.fetch_add(w, std::memory_order_relaxed);
+  });
+  return total.load();
 }
 
-bool Engine::alloc_batch(const HostBatch& hb, DevBatch& b, std::string& err) {
+bool Engine::alloc_batch(const HostBatch& hb, DevBatch& b, std::string& err, bool pooled) {
   (void)hipSetDevice(dev_);
+  const int pd = pooled ? dev_ : -1;
   b.n = uint32_t(hb.pk.size());
   b.n_tiles = hb.n_tiles();
   b.arena_bytes = hb.arena.size();
@@ -263,12 +287,13 @@ bool Engine::alloc_batch(const HostBatch& hb, DevBatch& b, std::string& err) {
   // engine stream, other threads) never write the same words
   b.spill_cap = std::max<uint64_t>(b.spill_words, 64);
   // +32 B tail: the kernels stage whole 16-byte lines and read names as dword triples
-  return dmalloc(&b.spill, b.spill_cap, "hipMalloc(batch scratch)", err) && dmalloc(&b.pk, hb.pk.size(), "hipMalloc(batch)", err) &&
-         dmalloc(&b.tile_off, size_t(b.n_tiles) * kGroupsPerTile + 1, "hipMalloc(group offsets)", err) &&
-         dmalloc(&b.arena, (hb.arena.size() + 32 + 15) & ~size_t(15), "hipMalloc(batch arena)", err) &&
-         (hb.attr.empty() || dmalloc(&b.attr, hb.attr.size(), "hipMalloc(batch attr)", err)) &&
-         dmalloc(&b.rec, hb.pk.size(), "hipMalloc(package records)", err) &&
-         dmalloc(&b.tail, hb.pk.size(), "hipMalloc(key tails)", err);
+  return dmalloc(&b.spill, b.spill_cap, "hipMalloc(batch scratch)", err, pd) &&
+         dmalloc(&b.pk, hb.pk.size(), "hipMalloc(batch)", err, pd) &&
+         dmalloc(&b.tile_off, size_t(b.n_tiles) * kGroupsPerTile + 1, "hipMalloc(group offsets)", err, pd) &&
+         dmalloc(&b.arena, (hb.arena.size() + 32 + 15) & ~size_t(15), "hipMalloc(batch arena)", err, pd) &&
+         (hb.attr.empty() || dmalloc(&b.attr, hb.attr.size(), "hipMalloc(batch attr)", err, pd)) &&
+         dmalloc(&b.rec, hb.pk.size(), "hipMalloc(package records)", err, pd) &&
+         dmalloc(&b.tail, hb.pk.size(), "hipMalloc(key tails)", err, pd);
 }
 
 bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
@@ -296,28 +321,30 @@ bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
   return true;
 }
 
-void Engine::free_batch(int device, DevBatch& b) {
+void Engine::free_batch(int device, DevBatch& b, bool pooled) {
   (void)hipSetDevice(device);
   for (void* p : {static_cast<void*>(b.pk), static_cast<void*>(b.tile_off), static_cast<void*>(b.arena),
-                  static_cast<void*>(b.attr), static_cast<void*>(b.cpe_bits), static_cast<void*>(b.rec),
-                  static_cast<void*>(b.tail), static_cast<void*>(b.spill)})
-    if (p) (void)hipFree(p);
+                  static_cast<void*>(b.attr), static_cast<void*>(b.rec), static_cast<void*>(b.tail),
+                  static_cast<void*>(b.spill)})
+    dfree(p, pooled, device);
+  dfree(b.cpe_bits, false, device);  // never pooled (copied by the caller)
   b = DevBatch{};
 }
 
-bool Engine::alloc_matches(uint64_t cap, uint32_t n_pkgs, DevMatches& m, std::string& err) {
+bool Engine::alloc_matches(uint64_t cap, uint32_t n_pkgs, DevMatches& m, std::string& err, bool pooled) {
   (void)hipSetDevice(dev_);
+  const int pd = pooled ? dev_ : -1;
   m.cap = std::max<uint64_t>(cap, 1);
   m.dir_cap = std::max<uint32_t>((n_pkgs + kTile - 1) / kTile, 1);
-  return dmalloc(&m.pkg, m.cap, "hipMalloc(matches)", err) && dmalloc(&m.adv, m.cap, "hipMalloc(matches)", err) &&
-         dmalloc(&m.dir, m.dir_cap, "hipMalloc(tile dir)", err) && dmalloc(&m.ctl, 8, "hipMalloc(ctl)", err);
+  return dmalloc(&m.pkg, m.cap, "hipMalloc(matches)", err, pd) && dmalloc(&m.adv, m.cap, "hipMalloc(matches)", err, pd) &&
+         dmalloc(&m.dir, m.dir_cap, "hipMalloc(tile dir)", err, pd) && dmalloc(&m.ctl, 8, "hipMalloc(ctl)", err, pd);
 }
 
-void Engine::free_matches(int device, DevMatches& m) {
+void Engine::free_matches(int device, DevMatches& m, bool pooled) {
   (void)hipSetDevice(device);
   for (void* p : {static_cast<void*>(m.pkg), static_cast<void*>(m.adv), static_cast<void*>(m.dir),
                   static_cast<void*>(m.ctl)})
-    if (p) (void)hipFree(p);
+    dfree(p, pooled, device);
   m = DevMatches{};
 }
 

@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "wire.h"
 
 namespace tvm {
 
@@ -56,29 +57,20 @@ class Pipeline {
   uint64_t d2h_bytes() const { return d2h_; }
   uint32_t chunks() const { return uint32_t(bounds_.size() - 1); }
   bool transport_form() const { return !wc_.empty(); }
-  uint64_t encode_us() const { return encode_us_; }
+  uint64_t encode_us() const { return encode_us_; }    // building the transport form (host threads)
+  uint64_t prepare_us() const { return prepare_us_; }  // the whole prepare(), encode included
 
  private:
   void release();
-  // The batch's transport form (pinned wire_h_, mirrored at the same offsets in wire_d_):
-  // per chunk one contiguous block {name ref u32, version ref u32, lengths u16 (name | version
-  // << 8), platform index u8 per package; the chunk's group offsets (u64, the arena's
-  // tile_off); attributes (uint2) when the batch has them; the bytes of the names and
-  // versions first seen in this chunk}.  A reference is the wire offset of the string's
-  // first occurrence, so a repeated name or version crosses the link once; unpack_kernel
-  // rebuilds the chunk's pk / tile_off / arena / attr in HBM.  false (wc_ empty): no
+  // The batch's transport form (wire.h; pinned wire_h_, mirrored at the same offsets in
+  // wire_d_), built on the host threads.  false: prepare fails; true with wc_ empty: no
   // transport form (a string of 256 bytes or more, more than 255 platforms, or 4 GiB).
   bool build_wire(const HostBatch& hb, std::string& err);
-  struct WireChunk {
-    uint64_t off = 0, bytes = 0;                          // block in wire_h_ / wire_d_
-    uint64_t o_nref = 0, o_vref = 0, o_lens = 0, o_plat = 0, o_toff = 0, o_attr = 0;  // section offsets (absolute)
-    uint32_t m = 0, groups = 0;                           // packages, 64-package groups (whole tiles)
-  };
   std::vector<WireChunk> wc_;
   uint8_t* wire_h_ = nullptr;
   uint8_t* wire_d_ = nullptr;
   uint32_t* ptab_d_ = nullptr;  // platform index -> platform id
-  uint64_t encode_us_ = 0;
+  uint64_t encode_us_ = 0, prepare_us_ = 0;
   int dev_ = -1;
   hipStream_t s_h2d_ = nullptr, s_k_ = nullptr, s_d2h_ = nullptr;
   std::vector<hipEvent_t> ev_h_, ev_k_;  // chunk uploaded / chunk's result move done

@@ -2,13 +2,17 @@
 // and the order kernel's direct writes of the result into host memory overlap chunk by chunk.  Every buffer is sized once in prepare(); a pass
 // allocates nothing.
 #include "pipeline.h"
+#include "host_par.h"
+#include "pool.h"
+#include "wire.h"
 
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <unordered_map>
+#include <memory>
+#include <mutex>
 
 namespace tvm {
 
@@ -21,6 +25,15 @@ bool ok(hipError_t e, const char* what, std::string& err) {
 }
 
 uint64_t align16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
+
+std::mutex& enc_mu() {
+  static std::mutex m;
+  return m;
+}
+std::vector<std::unique_ptr<WireEncoder>>& enc_pool() {
+  static auto* v = new std::vector<std::unique_ptr<WireEncoder>>();  // never destroyed (static teardown)
+  return *v;
+}
 
 __device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ d, const uint8_t* __restrict__ s, uint32_t n) {
   for (uint32_t k = 0; k < n; k += 8) {
@@ -98,111 +111,42 @@ __global__ __launch_bounds__(256) void unpack_kernel(UnpackArgs a) {
 
 }  // namespace
 
+// Encoders are kept between batches (their per-package arrays only grow): a fresh batch's
+// preparation then touches no new pages.
+static WireEncoder* take_encoder() {
+  std::lock_guard<std::mutex> lk(enc_mu());
+  auto& v = enc_pool();
+  if (v.empty()) return new WireEncoder();
+  WireEncoder* e = v.back().release();
+  v.pop_back();
+  return e;
+}
+
+static void give_encoder(WireEncoder* e) {
+  e->clear();
+  std::lock_guard<std::mutex> lk(enc_mu());
+  auto& v = enc_pool();
+  if (v.size() < 4) v.emplace_back(e);
+  else delete e;
+}
+
 bool Pipeline::build_wire(const HostBatch& hb, std::string& err) {
   const auto start = std::chrono::steady_clock::now();
-  const size_t n = hb.pk.size();
   wc_.clear();
-  if (n == 0) return true;
-  // platforms -> u8 indices
-  std::vector<uint32_t> ptab;
-  std::unordered_map<uint32_t, uint8_t> pidx;
-  for (const uint2& d : hb.pk) {
-    if ((d.y & 0xFFFFu) > 255 || (d.y >> 16) > 255) return true;  // no transport form
-    if (pidx.find(d.x) == pidx.end()) {
-      if (ptab.size() == 255) return true;
-      pidx.emplace(d.x, uint8_t(ptab.size()));
-      ptab.push_back(d.x);
-    }
-  }
-  const bool has_attr = !hb.attr.empty();
-  const uint32_t nc = chunks();
-  // upper bound of the wire size: every string new
-  uint64_t bound = 0;
-  for (uint32_t c = 0; c < nc; c++) {
-    const uint64_t m = std::min<uint64_t>(uint64_t(bounds_[c + 1]) * kTile, n) - std::min<uint64_t>(uint64_t(bounds_[c]) * kTile, n);
-    // 7 sections per chunk, each start 16-byte aligned (+ the chunk end): 8 alignment pads
-    bound += 8 * 16 + m * 11 + (uint64_t(bounds_[c + 1] - bounds_[c]) * kGroupsPerTile + 1) * 8 + (has_attr ? m * 8 : 0);
-  }
-  bound += hb.arena.size() + 16;
-  if (bound >= (1ull << 32)) return true;  // references are 32-bit
-  void* p = nullptr;
-  if (!ok(hipHostMalloc(&p, bound, hipHostMallocDefault), "hipHostMalloc(transport form)", err)) return false;
-  wire_h_ = static_cast<uint8_t*>(p);
-  if (!ok(hipMalloc(&p, bound), "hipMalloc(transport form)", err)) return false;
-  wire_d_ = static_cast<uint8_t*>(p);
-  wire_bytes_ = bound;
-  if (!ok(hipMalloc(&p, ptab.size() * 4), "hipMalloc(platform table)", err) ||
-      !ok(hipMemcpy(p, ptab.data(), ptab.size() * 4, hipMemcpyHostToDevice), "H2D platform table", err))
+  std::unique_ptr<WireEncoder, void (*)(WireEncoder*)> enc(take_encoder(), give_encoder);
+  if (!enc->plan(hb, toff_, bounds_, host_threads(), err)) return err.empty();  // no form: the batch goes raw
+  const uint64_t bytes = std::max<uint64_t>(enc->bytes(), 16);
+  if (!(wire_h_ = static_cast<uint8_t*>(pool_host_get(bytes, "hipHostMalloc(transport form)", err))) ||
+      !(wire_d_ = static_cast<uint8_t*>(pool_device_get(dev_, bytes, "hipMalloc(transport form)", err))))
     return false;
+  wire_bytes_ = bytes;
+  const auto& ptab = enc->platforms();
+  void* p = pool_device_get(dev_, ptab.size() * 4, "hipMalloc(platform table)", err);
+  if (!p) return false;
   ptab_d_ = static_cast<uint32_t*>(p);
-  // distinct strings: open addressing over indices into `uniq` (its first arena offset,
-  // length and wire reference)
-  struct U {
-    uint64_t aoff;
-    uint32_t ref;
-    uint32_t len;
-  };
-  std::vector<U> uniq;
-  uniq.reserve(n / 2 + 16);
-  size_t cap = 16;
-  while (cap < 4 * n) cap <<= 1;
-  std::vector<uint32_t> table(cap, 0xFFFFFFFFu);
-  const uint8_t* ar = hb.arena.data();
-  uint64_t heap = 0;  // next free byte of the current chunk's string section
-  auto ref_of = [&](uint64_t aoff, uint32_t len) -> uint32_t {
-    if (len == 0) return 0;
-    uint64_t h = 1469598103934665603ull;
-    for (uint32_t k = 0; k < len; k++) h = (h ^ ar[aoff + k]) * 1099511628211ull;
-    h ^= h >> 29;
-    for (size_t slot = size_t(h) & (cap - 1);; slot = (slot + 1) & (cap - 1)) {
-      const uint32_t u = table[slot];
-      if (u == 0xFFFFFFFFu) {
-        table[slot] = uint32_t(uniq.size());
-        std::memcpy(wire_h_ + heap, ar + aoff, len);
-        uniq.push_back({aoff, uint32_t(heap), len});
-        heap += len;
-        return uint32_t(heap - len);
-      }
-      const U& e = uniq[u];
-      if (e.len == len && std::memcmp(ar + e.aoff, ar + aoff, len) == 0) return e.ref;
-    }
-  };
-  uint64_t pos = 0, aoff = 0;
-  for (uint32_t c = 0; c < nc; c++) {
-    WireChunk w;
-    const size_t p0 = std::min<size_t>(size_t(bounds_[c]) * kTile, n), p1 = std::min<size_t>(size_t(bounds_[c + 1]) * kTile, n);
-    w.m = uint32_t(p1 - p0);
-    w.groups = (bounds_[c + 1] - bounds_[c]) * kGroupsPerTile;
-    w.off = pos;
-    w.o_nref = pos;
-    w.o_vref = align16(w.o_nref + 4ull * w.m);
-    w.o_lens = align16(w.o_vref + 4ull * w.m);
-    w.o_plat = align16(w.o_lens + 2ull * w.m);
-    w.o_toff = align16(w.o_plat + w.m);
-    w.o_attr = align16(w.o_toff + 8ull * (w.groups + 1));
-    heap = align16(w.o_attr + (has_attr ? 8ull * w.m : 0));
-    auto* nref = reinterpret_cast<uint32_t*>(wire_h_ + w.o_nref);
-    auto* vref = reinterpret_cast<uint32_t*>(wire_h_ + w.o_vref);
-    auto* lens = reinterpret_cast<uint16_t*>(wire_h_ + w.o_lens);
-    uint8_t* pl = wire_h_ + w.o_plat;
-    for (size_t i = p0; i < p1; i++) {
-      const uint32_t nl = hb.pk[i].y & 0xFFFFu, vl = hb.pk[i].y >> 16;
-      nref[i - p0] = ref_of(aoff, nl);
-      vref[i - p0] = ref_of(aoff + nl, vl);
-      lens[i - p0] = uint16_t(nl | (vl << 8));
-      pl[i - p0] = pidx[hb.pk[i].x];
-      aoff += nl + vl;
-    }
-    std::memcpy(wire_h_ + w.o_toff, toff_.data() + size_t(bounds_[c]) * kGroupsPerTile, 8ull * (w.groups + 1));
-    if (has_attr) std::memcpy(wire_h_ + w.o_attr, hb.attr.data() + p0, 8ull * w.m);
-    pos = align16(heap);
-    w.bytes = pos - w.off;
-    wc_.push_back(w);
-  }
-  if (pos > bound) {  // cannot happen (the bound counts every string as new); never DMA past the buffer
-    err = "pipeline: transport form larger than its bound";
-    return false;
-  }
+  if (!ok(hipMemcpy(p, ptab.data(), ptab.size() * 4, hipMemcpyHostToDevice), "H2D platform table", err)) return false;
+  enc->emit(wire_h_);
+  wc_ = enc->chunks();
   encode_us_ = uint64_t(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - start).count());
   return true;
 }
@@ -214,19 +158,17 @@ bool Pipeline::build_wire(const HostBatch& hb, std::string& err) {
 bool Pipeline::stage_raw(const HostBatch& hb, std::string& err) {
   const size_t b_pk = align16(hb.pk.size() * sizeof(uint2)), b_toff = align16(toff_.size() * 8),
                b_arena = align16(hb.arena.size()), b_attr = align16(hb.attr.size() * sizeof(uint2));
-  void* p = nullptr;
-  if (!ok(hipHostMalloc(&p, std::max<size_t>(b_pk + b_toff + b_arena + b_attr, 16), hipHostMallocDefault),
-          "hipHostMalloc(raw staging)", err))
-    return false;
+  void* p = pool_host_get(std::max<size_t>(b_pk + b_toff + b_arena + b_attr, 16), "hipHostMalloc(raw staging)", err);
+  if (!p) return false;
   raw_h_ = static_cast<uint8_t*>(p);
   raw_pk_ = reinterpret_cast<uint2*>(raw_h_);
   raw_toff_ = reinterpret_cast<uint64_t*>(raw_h_ + b_pk);
   raw_arena_ = raw_h_ + b_pk + b_toff;
   raw_attr_ = reinterpret_cast<uint2*>(raw_h_ + b_pk + b_toff + b_arena);
-  if (!hb.pk.empty()) std::memcpy(raw_pk_, hb.pk.data(), hb.pk.size() * sizeof(uint2));
-  if (!toff_.empty()) std::memcpy(raw_toff_, toff_.data(), toff_.size() * 8);
-  if (!hb.arena.empty()) std::memcpy(raw_arena_, hb.arena.data(), hb.arena.size());
-  if (!hb.attr.empty()) std::memcpy(raw_attr_, hb.attr.data(), hb.attr.size() * sizeof(uint2));
+  par_memcpy(raw_pk_, hb.pk.data(), hb.pk.size() * sizeof(uint2));
+  par_memcpy(raw_toff_, toff_.data(), toff_.size() * 8);
+  par_memcpy(raw_arena_, hb.arena.data(), hb.arena.size());
+  par_memcpy(raw_attr_, hb.attr.data(), hb.attr.size() * sizeof(uint2));
   return true;
 }
 
@@ -238,12 +180,15 @@ void Pipeline::release() {
   if (s_k_) (void)hipStreamSynchronize(s_k_);
   if (s_h2d_) (void)hipStreamSynchronize(s_h2d_);
   if (s_d2h_) (void)hipStreamSynchronize(s_d2h_);
-  Engine::free_batch(dev_, db_);
-  Engine::free_matches(dev_, m_);
-  for (void* p : {static_cast<void*>(chunk_base_d_), static_cast<void*>(wire_d_), static_cast<void*>(ptab_d_)})
-    if (p) (void)hipFree(p);
-  if (wire_h_) (void)hipHostFree(wire_h_);
-  if (raw_h_) (void)hipHostFree(raw_h_);
+  // every block goes back to the process-wide cache (pool.h): the streams are drained
+  Engine::free_batch(dev_, db_, true);
+  Engine::free_matches(dev_, m_, true);
+  for (void* p : {static_cast<void*>(chunk_base_d_), static_cast<void*>(wire_d_), static_cast<void*>(ptab_d_),
+                  static_cast<void*>(row_end_d_)})
+    pool_device_put(dev_, p);
+  for (void* p : {static_cast<void*>(wire_h_), static_cast<void*>(raw_h_), static_cast<void*>(adv_h_),
+                  static_cast<void*>(row_end_h_), static_cast<void*>(ctl_h_)})
+    pool_host_put(p);
   wire_h_ = nullptr;
   raw_h_ = nullptr;
   wire_bytes_ = 0;
@@ -251,13 +196,10 @@ void Pipeline::release() {
   ptab_d_ = nullptr;
   wc_.clear();
   encode_us_ = 0;
-  for (void* p : {static_cast<void*>(adv_h_), static_cast<void*>(row_end_h_), static_cast<void*>(ctl_h_)})
-    if (p) (void)hipHostFree(p);
   for (hipEvent_t e : ev_h_) (void)hipEventDestroy(e);
   for (hipEvent_t e : ev_k_) (void)hipEventDestroy(e);
   ev_h_.clear();
   ev_k_.clear();
-  if (row_end_d_) (void)hipFree(row_end_d_);
   row_end_d_ = nullptr;
   for (hipStream_t s : {s_h2d_, s_k_, s_d2h_})
     if (s) (void)hipStreamDestroy(s);
@@ -273,7 +215,7 @@ void Pipeline::release() {
 bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uint32_t chunk_packages, bool transport,
                        bool packed, std::string& err) {
   release();
-
+  const auto start = std::chrono::steady_clock::now();
   dev_ = eng.device();
   (void)hipSetDevice(dev_);
   const uint32_t n_tiles = hb.n_tiles();
@@ -303,7 +245,7 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
     return false;
   if (transport && !build_wire(hb, err)) return false;
   if (wc_.empty() && !stage_raw(hb, err)) return false;
-  if (!eng.alloc_batch(hb, db_, err) || !eng.alloc_matches(cap_, db_.n, m_, err)) return false;
+  if (!eng.alloc_batch(hb, db_, err, true) || !eng.alloc_matches(cap_, db_.n, m_, err, true)) return false;
   if (!hb.cpe_bits.empty() && hb.cpe_words) {  // CPE sets: small, copied once here
     void* p = nullptr;
     if (!ok(hipMalloc(&p, hb.cpe_bits.size() * 4), "hipMalloc(cpe sets)", err) ||
@@ -318,24 +260,25 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
   adv_units_ = cap4 / 4;
   row_end_units_ = std::max<size_t>(n4, 4) / 4;
   void* p = nullptr;
-  if (!ok(hipMalloc(&p, (size_t(nc) + 1) * 8), "hipMalloc(chunk bases)", err)) return false;
+  if (!(p = pool_device_get(dev_, (size_t(nc) + 1) * 8, "hipMalloc(chunk bases)", err))) return false;
   chunk_base_d_ = static_cast<unsigned long long*>(p);
   // the result lives in pinned host memory that the result move writes directly over PCIe
   // (measured, profiles/r03/pcie_probe.txt: kernel stores to host memory 55 GB/s, a DMA
   // device-to-host copy 28.6 GB/s; the DMA engine then only carries the batch upward)
-  if (!ok(hipHostMalloc(&p, cap4 * 4, hipHostMallocDefault), "hipHostMalloc(adv)", err)) return false;
+  if (!(p = pool_host_get(cap4 * 4, "hipHostMalloc(adv)", err))) return false;
   adv_h_ = static_cast<uint32_t*>(p);
-  if (!ok(hipHostMalloc(&p, std::max<size_t>(n4, 4) * 4, hipHostMallocDefault), "hipHostMalloc(row ends)", err)) return false;
+  if (!(p = pool_host_get(std::max<size_t>(n4, 4) * 4, "hipHostMalloc(row ends)", err))) return false;
   row_end_h_ = static_cast<uint32_t*>(p);
   if (!ok(hipHostGetDevicePointer(&p, adv_h_, 0), "hipHostGetDevicePointer(adv)", err)) return false;
   adv_hd_ = static_cast<uint32_t*>(p);
   if (!ok(hipHostGetDevicePointer(&p, row_end_h_, 0), "hipHostGetDevicePointer(row ends)", err)) return false;
   row_end_hd_ = static_cast<uint32_t*>(p);
-  if (!ok(hipMalloc(&p, std::max<size_t>(n4, 4) * 4), "hipMalloc(row ends)", err)) return false;
+  if (!(p = pool_device_get(dev_, std::max<size_t>(n4, 4) * 4, "hipMalloc(row ends)", err))) return false;
   row_end_d_ = static_cast<uint32_t*>(p);
-  if (!ok(hipHostMalloc(&p, 64, hipHostMallocDefault), "hipHostMalloc(ctl)", err)) return false;
+  if (!(p = pool_host_get(64, "hipHostMalloc(ctl)", err))) return false;
   ctl_h_ = static_cast<unsigned long long*>(p);
   prepared_ = true;
+  prepare_us_ = uint64_t(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - start).count());
   return true;
 }
 
