@@ -112,7 +112,7 @@ struct DevMatches {
 };
 // ERR_BOUNDS: a result move or an unpack found an index beyond the buffer it was sized for
 // (the store is dropped and the pass fails; never expected: a guard, not a code path)
-enum : uint32_t { ERR_SPILL = 1, ERR_TILES = 2, ERR_BOUNDS = 4 };
+enum : uint32_t { ERR_SPILL = 1, ERR_TILES = 2, ERR_BOUNDS = 8 };  // 4 is redhat.h ERR_RH_ORDER
 
 // The end-to-end pipeline's result move for one chunk (tiles [t0, t1)): the chunk's match
 // segments, straight from the tile directory, become the per-package advisory lists (CSR)
@@ -209,7 +209,7 @@ __device__ __forceinline__ void copy_out_tiles(const CopyOutArgs& a, uint32_t wg
     if (a.packed) {  // 3 bytes per advisory: destination bytes [3b, 3(b + count)) in 16-byte units
       const uint64_t B0 = 3 * b, B1 = 3 * (b + d.count), U0 = B0 >> 4;
       uint64_t nu = fits ? ((B1 + 15) >> 4) - U0 : 0;
-      if (U0 + nu > a.adv_units) {  // guard: never expected (adv_h holds 4 * cap bytes)
+      if (nu && U0 + nu > a.adv_units) {  // guard: never expected (adv_h holds 4 * cap bytes; an overflowed tile moves nothing)
         if (tid == 0) atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
         nu = 0;
       }
@@ -254,7 +254,7 @@ __device__ __forceinline__ void copy_out_tiles(const CopyOutArgs& a, uint32_t wg
     // the segment, realigned in registers to the destination's 16-byte units
     const uint64_t u0 = b >> 2;
     uint64_t nu = fits ? ((b + d.count + 3) >> 2) - u0 : 0;
-    if (u0 + nu > a.adv_units) {  // guard: never expected
+    if (nu && u0 + nu > a.adv_units) {  // guard: never expected
       if (tid == 0) atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
       nu = 0;
     }
