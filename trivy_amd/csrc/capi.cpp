@@ -1552,6 +1552,7 @@ RhInputs rh_inputs(tvm_engine* e, tvm_batch* b) {
   in.n_plats = uint32_t(e->eng->db().plat_info.size());
   in.raw = &b->m;
   in.n_tiles = b->dev.n_tiles;
+  in.n = b->dev.n;
   in.pkg_base = b->dev.pkg_base;
   in.adv_rank = e->fill->dev().adv_rank;
   in.fixed_rank = e->rh_rank;

@@ -43,6 +43,7 @@ struct RhInputs {
   uint32_t n_plats;
   const DevMatches* raw;            // the match kernel's list
   uint32_t n_tiles;
+  uint32_t n;                       // packages in the batch (tile t = packages [256 t, 256 t + 256))
   uint32_t pkg_base;
   const uint2* adv_rank;            // FillDev::adv_rank (.x vulnerability-ID rank)
   const uint32_t* fixed_rank;       // per advisory: rpm order rank of FixedVersion, RH_NONE = unfixed
