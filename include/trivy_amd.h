@@ -348,6 +348,31 @@ int tvm_pipeline_times(tvm_batch* b, uint64_t* encode_us, uint64_t* prepare_us);
 void tvm_pool_stats(uint64_t out[4]);
 void tvm_pool_trim(void);
 
+/* ---- SBOM decode (the detector input of `trivy sbom`) ------------------------------------
+ * Native CycloneDX JSON decode: pkg/sbom/cyclonedx/unmarshal.go:63-230 + pkg/sbom/io/decode.go:
+ * 47-380 (the OS component, OS packages by the OS's dependencies or else of one PURL type,
+ * applications by their Type property or one per language type, sorted).  The result holds
+ * the detector input as tvm_package records (valid until tvm_sbom_free), ready for
+ * tvm_ospkg_detect (app = -1) and tvm_library_detect (app = 0..n_apps-1). */
+typedef struct tvm_sbom tvm_sbom;
+int tvm_sbom_decode_cyclonedx(const char* text, size_t len, tvm_sbom** out, char* err, size_t errlen);
+void tvm_sbom_free(tvm_sbom* s);
+int tvm_sbom_info(const tvm_sbom* s, int32_t* has_os, tvm_str* os_family, tvm_str* os_name, tvm_str* serial,
+                  int64_t* version, size_t* n_apps);
+/* app = -1: the OS packages (type / file_path empty); else application app's Type, FilePath
+ * and libraries. */
+int tvm_sbom_packages(const tvm_sbom* s, int64_t app, tvm_str* type, tvm_str* file_path, const tvm_package** pkgs,
+                      size_t* n);
+/* Fields of package i beyond tvm_package: PkgIdentifier (PURL, BOMRef), Layer (Digest, DiffID),
+ * and which optional fields the SBOM set (bits: 1 Arch, 2 Epoch, 4 Release, 8 Modularitylabel,
+ * 16 FilePath, 32 SrcName, 64 SrcVersion, 128 SrcRelease, 256 SrcEpoch, 512 Layer.Digest,
+ * 1024 Layer.DiffID). */
+typedef struct {
+  tvm_str purl, bom_ref, layer_digest, layer_diff_id;
+  uint32_t present;
+} tvm_sbom_extra;
+int tvm_sbom_package_extra(const tvm_sbom* s, int64_t app, size_t i, tvm_sbom_extra* out);
+
 /* ---- Red Hat on the batch path ----------------------------------------------------------
  * After tvm_match_launch (+ sync): the Red Hat driver's epilogue for every package of the
  * batch's "Red Hat"-bucket targets at once - the per-CVE merge of redhat.go:146-187 (first

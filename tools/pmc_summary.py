@@ -24,7 +24,8 @@ import statistics
 import sys
 
 KERNELS = ("probe_kernel", "sweep_kernel", "fused_kernel", "persist_kernel", "match_kernel", "fill_pairs_kernel",
-           "filter_mark", "filter_select", "filter_count", "filter_place", "order_kernel", "redhat_merge")
+           "filter_mark", "filter_select", "filter_count_dup", "filter_count", "filter_place", "rules_insert", "vex_mark",
+           "order_kernel", "rh_merge_kernel", "unpack_kernel", "copy_out_kernel")
 MATCH = ("fused_kernel", "persist_kernel", "match_kernel")
 
 

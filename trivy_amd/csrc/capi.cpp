@@ -21,6 +21,7 @@
 #include "bbolt.h"
 #include "pipeline.h"
 #include "pool.h"
+#include "sbom.h"
 #include "wire.h"
 #include "redhat.h"
 #include "vulninfo.h"
@@ -1687,5 +1688,73 @@ int tvm_match_redhat_merge_time(tvm_engine* e, tvm_batch* b, int steps, double* 
     return TVM_EDEVICE;
   }
   *ms = f;
+  return TVM_OK;
+}
+
+// ---- native CycloneDX decode (sbom.cpp) ---------------------------------------------------
+
+struct tvm_sbom {
+  Sbom s;
+};
+
+int tvm_sbom_decode_cyclonedx(const char* text, size_t len, tvm_sbom** out, char* err, size_t errlen) {
+  if (!out || (len && !text)) return TVM_EINVAL;
+  *out = nullptr;
+  auto* h = new tvm_sbom();
+  std::string msg;
+  if (!decode_cyclonedx(std::string_view(text, len), h->s, msg)) {
+    delete h;
+    set_err(err, errlen, msg);
+    return TVM_EINVAL;
+  }
+  *out = h;
+  return TVM_OK;
+}
+
+void tvm_sbom_free(tvm_sbom* s) { delete s; }
+
+int tvm_sbom_info(const tvm_sbom* h, int32_t* has_os, tvm_str* os_family, tvm_str* os_name, tvm_str* serial,
+                  int64_t* version, size_t* n_apps) {
+  if (!h) return TVM_EINVAL;
+  const Sbom& s = h->s;
+  if (has_os) *has_os = s.has_os ? 1 : 0;
+  if (os_family) *os_family = tvm_str{s.os_family.data(), s.os_family.size()};
+  if (os_name) *os_name = tvm_str{s.os_name.data(), s.os_name.size()};
+  if (serial) *serial = tvm_str{s.serial.data(), s.serial.size()};
+  if (version) *version = s.version;
+  if (n_apps) *n_apps = s.apps.size();
+  return TVM_OK;
+}
+
+int tvm_sbom_packages(const tvm_sbom* h, int64_t app, tvm_str* type, tvm_str* file_path, const tvm_package** pkgs,
+                      size_t* n) {
+  if (!h || app < -1 || (app >= 0 && size_t(app) >= h->s.apps.size())) return TVM_EINVAL;
+  const Sbom& s = h->s;
+  if (app < 0) {
+    if (type) *type = tvm_str{nullptr, 0};
+    if (file_path) *file_path = tvm_str{nullptr, 0};
+    if (pkgs) *pkgs = s.view.data();
+    if (n) *n = s.view.size();
+    return TVM_OK;
+  }
+  const SbomApp& a = s.apps[size_t(app)];
+  if (type) *type = tvm_str{a.type.data(), a.type.size()};
+  if (file_path) *file_path = tvm_str{a.file_path.data(), a.file_path.size()};
+  if (pkgs) *pkgs = a.view.data();
+  if (n) *n = a.view.size();
+  return TVM_OK;
+}
+
+int tvm_sbom_package_extra(const tvm_sbom* h, int64_t app, size_t i, tvm_sbom_extra* out) {
+  if (!h || !out || app < -1 || (app >= 0 && size_t(app) >= h->s.apps.size())) return TVM_EINVAL;
+  const std::vector<SbomPkg>& v = app < 0 ? h->s.packages : h->s.apps[size_t(app)].libs;
+  if (i >= v.size()) return TVM_EINVAL;
+  const SbomPkg& p = v[i];
+  auto ts = [](std::string_view x) { return tvm_str{x.data(), x.size()}; };
+  out->purl = ts(p.purl);
+  out->bom_ref = ts(p.bom_ref);
+  out->layer_digest = ts(p.layer_digest);
+  out->layer_diff_id = ts(p.layer_diff_id);
+  out->present = p.present;
   return TVM_OK;
 }

@@ -1,0 +1,821 @@
+// Native CycloneDX decoder (sbom.h).
+#include "sbom.h"
+
+#include <algorithm>
+#include <cstring>
+#include <unordered_map>
+
+namespace tvm {
+
+namespace {
+
+constexpr std::string_view kNamespace = "aquasecurity:trivy:";
+
+// ---- a strict JSON reader that parses the members the decode needs and skips the rest ----
+
+struct Reader {
+  const char* s;
+  size_t n, i = 0;
+  std::deque<std::string>& owned;
+  std::string err;
+  int depth = 0;
+
+  bool fail(const char* m) {
+    if (err.empty()) err = std::string(m) + " at offset " + std::to_string(i);
+    return false;
+  }
+  void ws() {
+    while (i < n && (s[i] == ' ' || s[i] == '\t' || s[i] == '\n' || s[i] == '\r')) i++;
+  }
+  bool peek(char c) {
+    ws();
+    return i < n && s[i] == c;
+  }
+  bool eat(char c) {
+    ws();
+    if (i < n && s[i] == c) {
+      i++;
+      return true;
+    }
+    return false;
+  }
+  static int hexv(char c) {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+  }
+  static void put_utf8(std::string& o, uint32_t cp) {
+    if (cp < 0x80) {
+      o += char(cp);
+    } else if (cp < 0x800) {
+      o += char(0xC0 | (cp >> 6));
+      o += char(0x80 | (cp & 0x3F));
+    } else if (cp < 0x10000) {
+      o += char(0xE0 | (cp >> 12));
+      o += char(0x80 | ((cp >> 6) & 0x3F));
+      o += char(0x80 | (cp & 0x3F));
+    } else {
+      o += char(0xF0 | (cp >> 18));
+      o += char(0x80 | ((cp >> 12) & 0x3F));
+      o += char(0x80 | ((cp >> 6) & 0x3F));
+      o += char(0x80 | (cp & 0x3F));
+    }
+  }
+  bool hex4(uint32_t& v) {
+    if (i + 4 > n) return fail("short \\u escape");
+    v = 0;
+    for (int k = 0; k < 4; k++) {
+      const int h = hexv(s[i + k]);
+      if (h < 0) return fail("bad \\u escape");
+      v = v << 4 | uint32_t(h);
+    }
+    i += 4;
+    return true;
+  }
+  // a string token: a view into the text, or its unescaped copy
+  bool str(std::string_view& out) {
+    ws();
+    if (i >= n || s[i] != '"') return fail("expected a string");
+    const size_t a = ++i;
+    while (i < n && s[i] != '"' && s[i] != '\\') {
+      if (uint8_t(s[i]) < 0x20) return fail("control character in string");
+      i++;
+    }
+    if (i >= n) return fail("unterminated string");
+    if (s[i] == '"') {
+      out = std::string_view(s + a, i - a);
+      i++;
+      return true;
+    }
+    std::string o(s + a, i - a);
+    while (i < n && s[i] != '"') {
+      const char c = s[i];
+      if (uint8_t(c) < 0x20) return fail("control character in string");
+      if (c != '\\') {
+        o += c;
+        i++;
+        continue;
+      }
+      if (++i >= n) return fail("unterminated escape");
+      const char e = s[i++];
+      switch (e) {
+        case '"': o += '"'; break;
+        case '\\': o += '\\'; break;
+        case '/': o += '/'; break;
+        case 'b': o += '\b'; break;
+        case 'f': o += '\f'; break;
+        case 'n': o += '\n'; break;
+        case 'r': o += '\r'; break;
+        case 't': o += '\t'; break;
+        case 'u': {
+          uint32_t v;
+          if (!hex4(v)) return false;
+          if (v >= 0xD800 && v < 0xDC00 && i + 6 <= n && s[i] == '\\' && s[i + 1] == 'u') {
+            const size_t save = i;
+            i += 2;
+            uint32_t w;
+            if (!hex4(w)) return false;
+            if (w >= 0xDC00 && w < 0xE000) v = 0x10000 + ((v - 0xD800) << 10) + (w - 0xDC00);
+            else i = save, v = 0xFFFD;
+          } else if (v >= 0xD800 && v < 0xE000) {
+            v = 0xFFFD;  // a lone surrogate
+          }
+          put_utf8(o, v);
+          break;
+        }
+        default: return fail("bad escape");
+      }
+    }
+    if (i >= n) return fail("unterminated string");
+    i++;
+    owned.push_back(std::move(o));
+    out = owned.back();
+    return true;
+  }
+  bool number(std::string_view& lit) {
+    ws();
+    const size_t a = i;
+    if (i < n && s[i] == '-') i++;
+    if (i >= n) return fail("bad number");
+    if (s[i] == '0') {
+      i++;
+    } else if (s[i] >= '1' && s[i] <= '9') {
+      while (i < n && s[i] >= '0' && s[i] <= '9') i++;
+    } else {
+      return fail("bad number");
+    }
+    if (i < n && s[i] == '.') {
+      i++;
+      if (i >= n || s[i] < '0' || s[i] > '9') return fail("bad number");
+      while (i < n && s[i] >= '0' && s[i] <= '9') i++;
+    }
+    if (i < n && (s[i] == 'e' || s[i] == 'E')) {
+      i++;
+      if (i < n && (s[i] == '+' || s[i] == '-')) i++;
+      if (i >= n || s[i] < '0' || s[i] > '9') return fail("bad number");
+      while (i < n && s[i] >= '0' && s[i] <= '9') i++;
+    }
+    lit = std::string_view(s + a, i - a);
+    return true;
+  }
+  bool literal(const char* w) {
+    const size_t l = std::strlen(w);
+    if (i + l > n || std::memcmp(s + i, w, l) != 0) return fail("bad literal");
+    i += l;
+    return true;
+  }
+  bool skip() {
+    ws();
+    if (i >= n) return fail("unexpected end of input");
+    const char c = s[i];
+    if (c == '"') {
+      std::string_view v;
+      return str(v);
+    }
+    if (c == '{' || c == '[') {
+      if (++depth > 10000) return fail("nesting too deep");
+      i++;
+      const char close = c == '{' ? '}' : ']';
+      if (eat(close)) {
+        depth--;
+        return true;
+      }
+      for (;;) {
+        if (c == '{') {
+          std::string_view k;
+          if (!str(k) || !eat(':') ) return fail("expected ':'");
+        }
+        if (!skip()) return false;
+        if (eat(',')) continue;
+        if (eat(close)) break;
+        return fail("expected ',' or a closing bracket");
+      }
+      depth--;
+      return true;
+    }
+    if (c == 't') return literal("true");
+    if (c == 'f') return literal("false");
+    if (c == 'n') return literal("null");
+    std::string_view lit;
+    return number(lit);
+  }
+  // members of an object: f(key) parses the value (returns false on error)
+  template <class F>
+  bool object(F&& f) {
+    if (!eat('{')) return fail("expected an object");
+    if (eat('}')) return true;
+    for (;;) {
+      std::string_view k;
+      if (!str(k)) return false;
+      if (!eat(':')) return fail("expected ':'");
+      if (!f(k)) return false;
+      if (eat(',')) continue;
+      if (eat('}')) return true;
+      return fail("expected ',' or '}'");
+    }
+  }
+  template <class F>
+  bool array(F&& f) {
+    if (!eat('[')) return fail("expected an array");
+    if (eat(']')) return true;
+    for (;;) {
+      if (!f()) return false;
+      if (eat(',')) continue;
+      if (eat(']')) return true;
+      return fail("expected ',' or ']'");
+    }
+  }
+  // a string member value; other JSON kinds read as "" (validated and skipped)
+  bool str_or_empty(std::string_view& out) {
+    if (peek('"')) return str(out);
+    out = {};
+    return skip();
+  }
+};
+
+// ---- PURL (packageurl-go FromString as trivy_amd/sbom.py parse_purl restates it) ----------
+
+struct Purl {
+  std::string_view type, ns, name, version, subpath;
+  std::vector<std::pair<std::string_view, std::string_view>> quals;  // (lower-cased key, value), in order
+};
+
+struct Strs {
+  std::deque<std::string>& owned;
+  std::string_view keep(std::string&& x) {
+    owned.push_back(std::move(x));
+    return owned.back();
+  }
+  // urllib.parse.unquote: %XX decoded, malformed escapes kept
+  std::string_view unq(std::string_view x) {
+    if (x.find('%') == std::string_view::npos) return x;
+    std::string o;
+    o.reserve(x.size());
+    for (size_t k = 0; k < x.size(); k++) {
+      if (x[k] == '%' && k + 2 < x.size()) {
+        const int h = Reader::hexv(x[k + 1]), l = Reader::hexv(x[k + 2]);
+        if (h >= 0 && l >= 0) {
+          o += char(h * 16 + l);
+          k += 2;
+          continue;
+        }
+      }
+      o += x[k];
+    }
+    return keep(std::move(o));
+  }
+  std::string_view lower(std::string_view x) {
+    bool any = false;
+    for (char c : x) any |= c >= 'A' && c <= 'Z';
+    if (!any) return x;
+    std::string o(x);
+    for (char& c : o)
+      if (c >= 'A' && c <= 'Z') c = char(c - 'A' + 'a');
+    return keep(std::move(o));
+  }
+  std::string_view join(std::string_view a, std::string_view sep, std::string_view b) {
+    std::string o;
+    o.reserve(a.size() + sep.size() + b.size());
+    o.append(a).append(sep).append(b);
+    return keep(std::move(o));
+  }
+};
+
+std::string_view strip(std::string_view x, char c) {
+  while (!x.empty() && x.front() == c) x.remove_prefix(1);
+  while (!x.empty() && x.back() == c) x.remove_suffix(1);
+  return x;
+}
+
+// nullptr, or the error trivy_amd/sbom.py parse_purl raises
+const char* parse_purl(std::string_view s, Strs& S, Purl& p) {
+  if (s.substr(0, 4) != "pkg:") return "failed to parse PURL: scheme is not \"pkg\"";
+  std::string_view rest = s.substr(4);
+  while (!rest.empty() && rest.front() == '/') rest.remove_prefix(1);
+  p = Purl{};
+  if (const size_t h = rest.find('#'); h != std::string_view::npos) {
+    const std::string_view sp = strip(rest.substr(h + 1), '/');
+    rest = rest.substr(0, h);
+    std::string o;
+    bool first = true;
+    for (size_t a = 0; a <= sp.size();) {
+      size_t b = sp.find('/', a);
+      if (b == std::string_view::npos) b = sp.size();
+      const std::string_view seg = sp.substr(a, b - a);
+      if (!seg.empty() && seg != "." && seg != "..") {
+        if (!first) o += '/';
+        o.append(S.unq(seg));
+        first = false;
+      }
+      a = b + 1;
+    }
+    p.subpath = S.keep(std::move(o));
+  }
+  if (const size_t q = rest.find('?'); q != std::string_view::npos) {
+    const std::string_view qs = rest.substr(q + 1);
+    rest = rest.substr(0, q);
+    for (size_t a = 0; a <= qs.size();) {
+      size_t b = qs.find('&', a);
+      if (b == std::string_view::npos) b = qs.size();
+      const std::string_view kv = qs.substr(a, b - a);
+      const size_t e = kv.find('=');
+      const std::string_view k = kv.substr(0, e), v = e == std::string_view::npos ? std::string_view() : kv.substr(e + 1);
+      if (!kv.empty() && !v.empty()) p.quals.emplace_back(S.lower(k), S.unq(v));
+      a = b + 1;
+    }
+  }
+  const size_t sl = rest.find('/');
+  const std::string_view typ = rest.substr(0, sl);
+  rest = sl == std::string_view::npos ? std::string_view() : rest.substr(sl + 1);
+  if (typ.empty() || rest.empty()) return "failed to parse PURL: missing type or name";
+  if (const size_t at = rest.rfind('@'); at != std::string_view::npos) {
+    p.version = S.unq(rest.substr(at + 1));
+    rest = rest.substr(0, at);
+  }
+  rest = strip(rest, '/');
+  // segments: all but the last form the namespace (empty ones dropped), the last the name
+  const size_t last = rest.rfind('/');
+  p.name = S.unq(last == std::string_view::npos ? rest : rest.substr(last + 1));
+  if (last != std::string_view::npos) {
+    const std::string_view nsraw = rest.substr(0, last);
+    std::string o;
+    for (size_t a = 0; a <= nsraw.size();) {
+      size_t b = nsraw.find('/', a);
+      if (b == std::string_view::npos) b = nsraw.size();
+      const std::string_view seg = S.unq(nsraw.substr(a, b - a));
+      if (!seg.empty()) {
+        if (!o.empty()) o += '/';
+        o.append(seg);
+      }
+      a = b + 1;
+    }
+    p.ns = S.keep(std::move(o));
+  }
+  p.type = S.lower(typ);
+  return nullptr;
+}
+
+// purl.go:130-179 LangType
+std::string_view lang_type(const Purl& p) {
+  static const std::unordered_map<std::string_view, std::string_view> lang = {
+      {"composer", "composer"}, {"maven", "jar"},  {"gem", "gemspec"},     {"conda", "conda-pkg"}, {"pypi", "python-pkg"},
+      {"golang", "gobinary"},   {"npm", "node-pkg"}, {"cargo", "cargo"},   {"nuget", "nuget"},     {"swift", "swift"},
+      {"cocoapods", "cocoapods"}, {"hex", "hex"},  {"conan", "conan"},     {"pub", "pub"},         {"bitnami", "bitnami"}};
+  static const std::unordered_map<std::string_view, std::string_view> k8s = {
+      {"eks", "eks"}, {"gke", "gke"}, {"aks", "aks"}, {"ocp", "ocp"}, {"", "kubernetes"}};
+  if (p.type == "k8s") {
+    auto it = k8s.find(p.ns);
+    return it == k8s.end() ? std::string_view() : it->second;
+  }
+  auto it = lang.find(p.type);
+  return it == lang.end() ? std::string_view() : it->second;
+}
+
+bool is_os_type(std::string_view t) { return t == "apk" || t == "deb" || t == "rpm"; }
+
+// purl.go:181-193 Class: 1 os-pkgs, 2 lang-pkgs, 0 neither
+int purl_class(const Purl& p) { return is_os_type(p.type) ? 1 : (lang_type(p).empty() ? 0 : 2); }
+
+bool ascii_digits(std::string_view v) {
+  if (v.empty()) return false;
+  for (char c : v)
+    if (c < '0' || c > '9') return false;
+  return true;
+}
+
+// Python int() of a property value as trivy_amd/sbom.py applies it (an optional sign, then
+// digits; surrounding whitespace allowed)
+bool py_int(std::string_view v, int64_t& out) {
+  while (!v.empty() && (v.front() == ' ' || v.front() == '\t' || v.front() == '\n')) v.remove_prefix(1);
+  while (!v.empty() && (v.back() == ' ' || v.back() == '\t' || v.back() == '\n')) v.remove_suffix(1);
+  bool neg = false;
+  if (!v.empty() && (v.front() == '+' || v.front() == '-')) {
+    neg = v.front() == '-';
+    v.remove_prefix(1);
+  }
+  if (!ascii_digits(v) || v.size() > 18) return false;
+  int64_t x = 0;
+  for (char c : v) x = x * 10 + (c - '0');
+  out = neg ? -x : x;
+  return true;
+}
+
+struct Comp {
+  std::string_view type, name, group, version, bom_ref, purl_str;
+  std::vector<std::pair<std::string_view, std::string_view>> props;  // namespace prefix removed
+  bool has_purl = false;
+  Purl purl;
+};
+
+enum CompType : uint8_t { CT_OTHER, CT_CONTAINER, CT_APPLICATION, CT_LIBRARY, CT_OS, CT_PLATFORM };
+
+CompType comp_type(std::string_view t) {
+  if (t == "library") return CT_LIBRARY;
+  if (t == "application") return CT_APPLICATION;
+  if (t == "operating-system") return CT_OS;
+  if (t == "container") return CT_CONTAINER;
+  if (t == "platform") return CT_PLATFORM;
+  return CT_OTHER;
+}
+
+bool read_component(Reader& R, Comp& c, size_t* members = nullptr) {
+  c = Comp{};
+  return R.object([&](std::string_view k) {
+    if (members) ++*members;
+    if (k == "type") return R.str_or_empty(c.type);
+    if (k == "name") return R.str_or_empty(c.name);
+    if (k == "group") return R.str_or_empty(c.group);
+    if (k == "version") return R.str_or_empty(c.version);
+    if (k == "bom-ref") return R.str_or_empty(c.bom_ref);
+    if (k == "purl") return R.str_or_empty(c.purl_str);
+    if (k == "properties") {
+      c.props.clear();
+      if (!R.peek('[')) return R.skip();
+      return R.array([&] {
+        std::string_view pn, pv;
+        if (!R.peek('{')) return R.skip();
+        if (!R.object([&](std::string_view f) {
+              if (f == "name") return R.str_or_empty(pn);
+              if (f == "value") return R.str_or_empty(pv);
+              return R.skip();
+            }))
+          return false;
+        if (pn.substr(0, kNamespace.size()) == kNamespace) pn.remove_prefix(kNamespace.size());
+        c.props.emplace_back(pn, pv);
+        return true;
+      });
+    }
+    return R.skip();
+  });
+}
+
+struct Dep {
+  std::string_view ref;
+  std::vector<std::string_view> on;
+  bool has_ref = false;
+};
+
+}  // namespace
+
+bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
+  out = Sbom{};
+  out.text.assign(text_in.data(), text_in.size());
+  Reader R{out.text.data(), out.text.size(), 0, out.owned, {}, 0};
+  Strs S{out.owned};
+  std::vector<Comp> comps;
+  Comp root;
+  bool has_root = false;
+  std::vector<Dep> deps;
+  std::string_view serial;
+  int64_t version = 0;
+  // the document: the members the decode reads, the rest validated and skipped (a repeated
+  // member: the last one wins, as a JSON decode into a map does)
+  const bool ok = R.object([&](std::string_view k) {
+    if (k == "components") {
+      comps.clear();
+      if (!R.peek('[')) return R.skip();
+      return R.array([&] {
+        comps.emplace_back();
+        if (!R.peek('{')) {
+          comps.pop_back();
+          return R.skip();
+        }
+        return read_component(R, comps.back());
+      });
+    }
+    if (k == "metadata") {
+      has_root = false;
+      if (!R.peek('{')) return R.skip();
+      return R.object([&](std::string_view f) {
+        if (f != "component") return R.skip();
+        if (!R.peek('{')) {
+          has_root = false;
+          return R.skip();
+        }
+        size_t members = 0;
+        const bool good = read_component(R, root, &members);
+        has_root = members > 0;  // an empty metadata component is no root
+        return good;
+      });
+    }
+    if (k == "dependencies") {
+      deps.clear();
+      if (!R.peek('[')) return R.skip();
+      return R.array([&] {
+        if (!R.peek('{')) return R.skip();
+        deps.emplace_back();
+        Dep& d = deps.back();
+        return R.object([&](std::string_view f) {
+          if (f == "ref") {
+            d.has_ref = R.peek('"');
+            return R.str_or_empty(d.ref);
+          }
+          if (f == "dependsOn") {
+            d.on.clear();
+            if (!R.peek('[')) return R.skip();
+            return R.array([&] {
+              std::string_view x;
+              if (!R.peek('"')) return R.skip();
+              if (!R.str(x)) return false;
+              d.on.push_back(x);
+              return true;
+            });
+          }
+          return R.skip();
+        });
+      });
+    }
+    if (k == "serialNumber") return R.str_or_empty(serial);
+    if (k == "version") {
+      std::string_view lit;
+      if (R.peek('"') || R.peek('{') || R.peek('[') || R.peek('t') || R.peek('f') || R.peek('n')) {
+        version = 0;
+        return R.skip();
+      }
+      if (!R.number(lit)) return false;
+      int64_t v = 0;
+      version = py_int(lit, v) ? v : 0;
+      return true;
+    }
+    return R.skip();
+  });
+  R.ws();
+  if (!ok || R.i != R.n) {
+    err = "failed to decode CycloneDX JSON: " + (R.err.empty() ? std::string("trailing data") : R.err);
+    return false;
+  }
+  out.serial = serial;
+  out.version = version;
+
+  // parseComponents: unsupported types dropped, a component whose PURL does not parse skipped
+  std::vector<Comp*> order;
+  order.reserve(comps.size() + 1);
+  for (Comp& c : comps) {
+    if (comp_type(c.type) == CT_OTHER) continue;
+    if (!c.purl_str.empty()) {
+      if (parse_purl(c.purl_str, S, c.purl)) continue;  // parseComponents logs and skips it
+      c.has_purl = true;
+    }
+    order.push_back(&c);
+  }
+  if (has_root) {
+    if (comp_type(root.type) == CT_OTHER) {
+      err = "failed to parse root component: unsupported component type";
+      return false;
+    }
+    if (!root.purl_str.empty()) {
+      if (const char* e = parse_purl(root.purl_str, S, root.purl)) {
+        err = e;
+        return false;
+      }
+      root.has_purl = true;
+    }
+    order.push_back(&root);
+  }
+  // bom-ref -> component (a later one with the same ref replaces an earlier one)
+  std::unordered_map<std::string_view, Comp*> by_ref;
+  by_ref.reserve(order.size() * 2);
+  for (Comp* c : order) by_ref[c->bom_ref] = c;
+  std::unordered_map<const Comp*, std::vector<Comp*>> rels;
+  for (const Dep& d : deps) {
+    if (!d.has_ref) continue;
+    auto it = by_ref.find(d.ref);
+    if (it == by_ref.end()) continue;
+    std::vector<Comp*>& v = rels[it->second];
+    v.clear();
+    for (std::string_view x : d.on) {
+      auto jt = by_ref.find(x);
+      if (jt != by_ref.end()) v.push_back(jt->second);
+    }
+  }
+
+  // Decoder.Decode
+  const Comp* os_c = nullptr;
+  struct App {
+    const Comp* c;
+    std::string_view type, file_path;
+  };
+  std::vector<App> apps;
+  std::unordered_map<const Comp*, size_t> pkg_of;  // component -> index in pkgs (live ones)
+  std::vector<SbomPkg> pkgs;
+  std::vector<const Comp*> pkg_comp;
+  std::vector<uint8_t> taken;
+  static const std::string_view kAggregating[] = {"python-pkg", "conda-pkg", "gemspec", "node-pkg", "jar"};
+  for (const Comp* c : order) {
+    const CompType ct = comp_type(c->type);
+    if (ct == CT_OS) {
+      if (os_c) {
+        err = "failed to decode components: multiple OS components are not supported";
+        return false;
+      }
+      os_c = c;
+      out.has_os = true;
+      out.os_family = c->name;
+      out.os_name = c->version;
+      continue;
+    }
+    if (ct == CT_APPLICATION) {
+      std::string_view t;
+      bool has_t = false;
+      for (auto& [k, v] : c->props)
+        if (k == "Type") {
+          t = v;
+          has_t = true;
+          break;
+        }
+      if (has_t && !t.empty()) {
+        const bool agg = std::find(std::begin(kAggregating), std::end(kAggregating), t) != std::end(kAggregating);
+        apps.push_back(App{c, t, agg ? std::string_view() : c->name});
+        continue;
+      }
+    }
+    // decodeLibrary
+    if (!c->has_purl) continue;
+    const Purl& p = c->purl;
+    const int cls = purl_class(p);
+    if (!cls) continue;
+    SbomPkg k;
+    const bool maven = p.type == "maven" || p.type == "gradle";
+    k.name = p.name;
+    if (!p.ns.empty() && cls != 1) k.name = S.join(p.ns, maven ? ":" : "/", p.name);
+    if (!p.subpath.empty() && p.type == "cocoapods") k.name = S.join(p.name, "/", p.subpath);
+    k.version = p.version;
+    for (auto& [qk, qv] : p.quals) {
+      if (qk == "arch") {
+        k.arch = qv;
+        k.present |= SP_ARCH;
+      } else if (qk == "modularitylabel") {
+        k.modularitylabel = qv;
+        k.present |= SP_MODULARITY;
+      } else if (qk == "epoch") {
+        std::string_view d = qv;
+        while (!d.empty() && (d.front() == '+' || d.front() == '-')) d.remove_prefix(1);
+        int64_t e;
+        if (ascii_digits(d) && py_int(qv, e)) {
+          k.epoch = e;
+          k.present |= SP_EPOCH;
+        }
+      }
+    }
+    if (p.type == "rpm") {  // go-rpm-version: [epoch:]version[-release], the release after the last '-'
+      std::string_view v = p.version;
+      if (const size_t col = v.find(':'); col != std::string_view::npos) v = v.substr(col + 1);
+      const size_t dash = v.rfind('-');
+      k.version = dash == std::string_view::npos ? v : v.substr(0, dash);
+      k.release = dash == std::string_view::npos ? std::string_view() : v.substr(dash + 1);
+      k.present |= SP_RELEASE;
+    }
+    if (p.type != "cocoapods") k.name = c->group.empty() ? c->name : S.join(c->group, maven ? ":" : "/", c->name);
+    // dependency.ID (pkg/dependency/id.go:9-27)
+    {
+      const std::string_view lt = lang_type(p);
+      if (p.version.empty()) {
+        k.id = k.name;
+      } else if (lt == "conan") {
+        k.id = S.join(k.name, "/", p.version);
+      } else if ((lt == "gomod" || lt == "gobinary") && p.version.front() != 'v') {
+        k.id = S.join(k.name, "@v", p.version);
+      } else if (lt == "jar" || lt == "pom" || lt == "gradle") {
+        k.id = S.join(k.name, ":", p.version);
+      } else {
+        k.id = S.join(k.name, "@", p.version);
+      }
+    }
+    for (auto& [pk, pv] : c->props) {
+      if (pk == "PkgID") {
+        k.id = pv;
+      } else if (pk == "FilePath") {
+        k.file_path = pv;
+        k.present |= SP_FILEPATH;
+      } else if (pk == "SrcName") {
+        k.src_name = pv;
+        k.present |= SP_SRCNAME;
+      } else if (pk == "SrcVersion") {
+        k.src_version = pv;
+        k.present |= SP_SRCVERSION;
+      } else if (pk == "SrcRelease") {
+        k.src_release = pv;
+        k.present |= SP_SRCRELEASE;
+      } else if (pk == "Modularitylabel") {
+        k.modularitylabel = pv;
+        k.present |= SP_MODULARITY;
+      } else if (pk == "SrcEpoch") {
+        int64_t e;
+        if (!py_int(pv, e)) {
+          err = "failed to decode components: failed to decode library: invalid src epoch";
+          return false;
+        }
+        k.src_epoch = e;
+        k.present |= SP_SRCEPOCH;
+      } else if (pk == "LayerDigest") {
+        k.layer_digest = pv;
+        k.present |= SP_LAYER_DIGEST;
+      } else if (pk == "LayerDiffID") {
+        k.layer_diff_id = pv;
+        k.present |= SP_LAYER_DIFFID;
+      }
+    }
+    k.purl = c->purl_str;
+    k.bom_ref = c->bom_ref;
+    if (cls == 1) {  // fillSrcPkg (decode.go:260-279): empty source fields default to the binary's
+      if (k.src_name.empty()) k.src_name = k.name;
+      if (k.src_version.empty()) k.src_version = k.version;
+      if (k.src_release.empty()) k.src_release = k.release;
+      if (k.src_epoch == 0) k.src_epoch = k.epoch;
+      k.present |= SP_SRCNAME | SP_SRCVERSION | SP_SRCRELEASE | SP_SRCEPOCH;
+    }
+    pkg_of[c] = pkgs.size();
+    pkgs.push_back(k);
+    pkg_comp.push_back(c);
+  }
+  taken.assign(pkgs.size(), 0);
+  auto take = [&](const Comp* d, std::vector<SbomPkg>& dst) {
+    auto it = pkg_of.find(d);
+    if (it == pkg_of.end() || taken[it->second]) return;
+    taken[it->second] = 1;
+    dst.push_back(pkgs[it->second]);
+  };
+  if (os_c) {
+    auto it = rels.find(os_c);
+    if (it != rels.end())
+      for (const Comp* d : it->second) take(d, out.packages);
+  }
+  for (const App& a : apps) {
+    SbomApp app;
+    app.type = a.type;
+    app.file_path = a.file_path;
+    auto it = rels.find(a.c);
+    if (it != rels.end())
+      for (const Comp* d : it->second) take(d, app.libs);
+    out.apps.push_back(std::move(app));
+  }
+  // the rest: OS packages of one PURL type, one application per language type
+  std::vector<std::string_view> os_types, lang_types;
+  std::vector<std::vector<SbomPkg>> os_rest, lang_rest;
+  for (size_t k = 0; k < pkgs.size(); k++) {
+    if (taken[k]) continue;
+    const Purl& p = pkg_comp[k]->purl;
+    const bool os = purl_class(p) == 1;
+    auto& types = os ? os_types : lang_types;
+    auto& groups = os ? os_rest : lang_rest;
+    const std::string_view key = os ? p.type : lang_type(p);
+    size_t g = std::find(types.begin(), types.end(), key) - types.begin();
+    if (g == types.size()) {
+      types.push_back(key);
+      groups.emplace_back();
+    }
+    groups[g].push_back(pkgs[k]);
+  }
+  if (os_rest.size() > 1) {
+    err = "failed to aggregate packages: multiple types of OS packages in SBOM are not supported";
+    return false;
+  }
+  auto by_name = [](const SbomPkg& a, const SbomPkg& b) {  // Packages.Less (artifact.go:203-211), byte order
+    if (a.name != b.name) return a.name < b.name;
+    if (a.version != b.version) return a.version < b.version;
+    return a.file_path < b.file_path;
+  };
+  if (!os_rest.empty() && out.has_os && !out.os_family.empty()) {
+    std::stable_sort(os_rest[0].begin(), os_rest[0].end(), by_name);
+    out.packages.insert(out.packages.end(), os_rest[0].begin(), os_rest[0].end());
+  }
+  for (size_t g = 0; g < lang_rest.size(); g++) {
+    std::stable_sort(lang_rest[g].begin(), lang_rest[g].end(), by_name);
+    SbomApp app;
+    app.type = lang_types[g];
+    app.libs = std::move(lang_rest[g]);
+    out.apps.push_back(std::move(app));
+  }
+  std::stable_sort(out.apps.begin(), out.apps.end(), [](const SbomApp& a, const SbomApp& b) {
+    if (a.type != b.type) return a.type < b.type;
+    return a.file_path < b.file_path;
+  });
+  // detector input views
+  auto ts = [](std::string_view v) { return tvm_str{v.data(), v.size()}; };
+  auto view = [&](const std::vector<SbomPkg>& src, std::vector<tvm_package>& dst) {
+    dst.resize(src.size());
+    for (size_t k = 0; k < src.size(); k++) {
+      const SbomPkg& p = src[k];
+      tvm_package& q = dst[k];
+      std::memset(&q, 0, sizeof q);
+      q.id = ts(p.id);
+      q.name = ts(p.name);
+      q.version = ts(p.version);
+      q.release = ts(p.release);
+      q.arch = ts(p.arch);
+      q.epoch = p.epoch;
+      q.src_name = ts(p.src_name);
+      q.src_version = ts(p.src_version);
+      q.src_release = ts(p.src_release);
+      q.src_epoch = p.src_epoch;
+      q.modularitylabel = ts(p.modularitylabel);
+      q.file_path = ts(p.file_path);
+    }
+  };
+  view(out.packages, out.view);
+  for (SbomApp& a : out.apps) view(a.libs, a.view);
+  return true;
+}
+
+}  // namespace tvm

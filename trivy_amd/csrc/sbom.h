@@ -1,0 +1,64 @@
+// Native CycloneDX decoder: a CycloneDX JSON document -> the detector input (the OS, its
+// packages, the language applications and their libraries) without an intermediate DOM.
+//
+// Restates pkg/sbom/cyclonedx/unmarshal.go:63-230 (parseBOM / parseComponent: supported
+// component types, PURL, "aquasecurity:trivy:" properties, the metadata component as root,
+// dependencies as relationships between known bom-refs) and pkg/sbom/io/decode.go:47-380
+// (Decoder.Decode: one OS component at most, applications by their Type property,
+// decodeLibrary, fillSrcPkg, the OS's and each application's dependencies, the rest as OS
+// packages of one PURL type and one application per language type, sorted), with the PURL
+// rules of pkg/purl/purl.go:130-243 and packageurl-go's parser.  The Python restatement
+// trivy_amd/sbom.py (pinned by the integration SBOM goldens) is the checker: the two agree
+// field for field (tests/test_sbom_native.py).
+//
+// One pass over the text: the top-level members the decode needs are parsed straight into
+// component records (strings are views into the text unless they hold escapes), everything
+// else is validated and skipped.  Packages come out as the tvm_package records the
+// detectors take.
+#pragma once
+#include <cstdint>
+#include <deque>
+#include <string>
+#include <string_view>
+#include <vector>
+
+#include "../../include/trivy_amd.h"
+
+namespace tvm {
+
+// Optional ftypes.Package fields a decoded package carries (the Python mirror's dict keys).
+enum : uint32_t {
+  SP_ARCH = 1, SP_EPOCH = 2, SP_RELEASE = 4, SP_MODULARITY = 8, SP_FILEPATH = 16, SP_SRCNAME = 32,
+  SP_SRCVERSION = 64, SP_SRCRELEASE = 128, SP_SRCEPOCH = 256, SP_LAYER_DIGEST = 512, SP_LAYER_DIFFID = 1024,
+};
+
+struct SbomPkg {
+  std::string_view id, name, version, release, arch, src_name, src_version, src_release, modularitylabel, file_path;
+  std::string_view purl, bom_ref, layer_digest, layer_diff_id;
+  int64_t epoch = 0, src_epoch = 0;
+  uint32_t present = 0;  // SP_*
+};
+
+struct SbomApp {
+  std::string_view type, file_path;
+  std::vector<SbomPkg> libs;
+  std::vector<tvm_package> view;  // libs as detector input
+};
+
+struct Sbom {
+  bool has_os = false;
+  std::string_view os_family, os_name, serial;
+  int64_t version = 0;
+  std::vector<SbomPkg> packages;  // OS packages
+  std::vector<tvm_package> view;
+  std::vector<SbomApp> apps;
+  std::string text;               // the document (the views point into it)
+  std::deque<std::string> owned;  // strings built by the decode (unescaped, joined, split)
+};
+
+// false: err holds the reference's message ("failed to decode CycloneDX JSON: ...",
+// "failed to parse root component: ...", "failed to decode components: ...",
+// "failed to aggregate packages: ...").
+bool decode_cyclonedx(std::string_view text, Sbom& out, std::string& err);
+
+}  // namespace tvm
