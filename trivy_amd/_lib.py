@@ -31,6 +31,22 @@ class Package(ctypes.Structure):
     ]
 
 
+class RawStr(ctypes.Structure):  # tvm_str read back from the library (not NUL-terminated)
+    _fields_ = [("p", ctypes.c_void_p), ("n", ctypes.c_size_t)]
+
+    def bytes(self):
+        return ctypes.string_at(self.p, self.n) if self.n else b""
+
+
+class RawPackage(ctypes.Structure):  # tvm_package read back (tvm_sbom_packages)
+    _fields_ = [(n, RawStr if t is Str else t) for n, t in Package._fields_]
+
+
+class SbomExtra(ctypes.Structure):
+    _fields_ = [("purl", RawStr), ("bom_ref", RawStr), ("layer_digest", RawStr), ("layer_diff_id", RawStr),
+                ("present", ctypes.c_uint32)]
+
+
 class Repository(ctypes.Structure):
     _fields_ = [("family", Str), ("release", Str)]
 
@@ -148,6 +164,16 @@ _SIG = [
     ("tvm_device_sync", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_pipeline_times", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     ("tvm_pool_stats", None, [ctypes.POINTER(ctypes.c_uint64)]),
+    ("tvm_sbom_decode_cyclonedx", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p),
+                                                 ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_sbom_free", None, [ctypes.c_void_p]),
+    ("tvm_sbom_info", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(RawStr),
+                                     ctypes.POINTER(RawStr), ctypes.POINTER(RawStr), ctypes.POINTER(ctypes.c_int64),
+                                     ctypes.POINTER(ctypes.c_size_t)]),
+    ("tvm_sbom_packages", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(RawStr), ctypes.POINTER(RawStr),
+                                         ctypes.POINTER(ctypes.POINTER(RawPackage)), ctypes.POINTER(ctypes.c_size_t)]),
+    ("tvm_sbom_package_extra", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_size_t,
+                                              ctypes.POINTER(SbomExtra)]),
     ("tvm_wire_encode", ctypes.c_int, [ctypes.c_size_t, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,

@@ -3,6 +3,9 @@
 
 #include <algorithm>
 #include <cstring>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <unordered_map>
 
 namespace tvm {
@@ -16,7 +19,7 @@ constexpr std::string_view kNamespace = "aquasecurity:trivy:";
 struct Reader {
   const char* s;
   size_t n, i = 0;
-  std::deque<std::string>& owned;
+  Sbom& owned;
   std::string err;
   int depth = 0;
 
@@ -129,8 +132,7 @@ struct Reader {
     }
     if (i >= n) return fail("unterminated string");
     i++;
-    owned.push_back(std::move(o));
-    out = owned.back();
+    out = owned.keep(o);
     return true;
   }
   bool number(std::string_view& lit) {
@@ -236,17 +238,22 @@ struct Reader {
 
 // ---- PURL (packageurl-go FromString as trivy_amd/sbom.py parse_purl restates it) ----------
 
+using KV = std::pair<std::string_view, std::string_view>;
+
 struct Purl {
   std::string_view type, ns, name, version, subpath;
-  std::vector<std::pair<std::string_view, std::string_view>> quals;  // (lower-cased key, value), in order
+  uint32_t q0 = 0, nq = 0;  // qualifiers (lower-cased key, value), in order: Pools::quals[q0, q0 + nq)
+};
+
+// Shared storage of every component's properties and qualifiers (no vector per component).
+struct Pools {
+  std::vector<KV> props, quals;
 };
 
 struct Strs {
-  std::deque<std::string>& owned;
-  std::string_view keep(std::string&& x) {
-    owned.push_back(std::move(x));
-    return owned.back();
-  }
+  Sbom& owned;
+  Pools& pools;
+  std::string_view keep(const std::string& x) { return owned.keep(x); }
   // urllib.parse.unquote: %XX decoded, malformed escapes kept
   std::string_view unq(std::string_view x) {
     if (x.find('%') == std::string_view::npos) return x;
@@ -263,7 +270,7 @@ struct Strs {
       }
       o += x[k];
     }
-    return keep(std::move(o));
+    return keep(o);
   }
   std::string_view lower(std::string_view x) {
     bool any = false;
@@ -272,14 +279,9 @@ struct Strs {
     std::string o(x);
     for (char& c : o)
       if (c >= 'A' && c <= 'Z') c = char(c - 'A' + 'a');
-    return keep(std::move(o));
+    return keep(o);
   }
-  std::string_view join(std::string_view a, std::string_view sep, std::string_view b) {
-    std::string o;
-    o.reserve(a.size() + sep.size() + b.size());
-    o.append(a).append(sep).append(b);
-    return keep(std::move(o));
-  }
+  std::string_view join(std::string_view a, std::string_view sep, std::string_view b) { return owned.keep(a, sep, b); }
 };
 
 std::string_view strip(std::string_view x, char c) {
@@ -294,6 +296,7 @@ const char* parse_purl(std::string_view s, Strs& S, Purl& p) {
   std::string_view rest = s.substr(4);
   while (!rest.empty() && rest.front() == '/') rest.remove_prefix(1);
   p = Purl{};
+  p.q0 = uint32_t(S.pools.quals.size());
   if (const size_t h = rest.find('#'); h != std::string_view::npos) {
     const std::string_view sp = strip(rest.substr(h + 1), '/');
     rest = rest.substr(0, h);
@@ -310,7 +313,7 @@ const char* parse_purl(std::string_view s, Strs& S, Purl& p) {
       }
       a = b + 1;
     }
-    p.subpath = S.keep(std::move(o));
+    p.subpath = S.keep(o);
   }
   if (const size_t q = rest.find('?'); q != std::string_view::npos) {
     const std::string_view qs = rest.substr(q + 1);
@@ -321,7 +324,10 @@ const char* parse_purl(std::string_view s, Strs& S, Purl& p) {
       const std::string_view kv = qs.substr(a, b - a);
       const size_t e = kv.find('=');
       const std::string_view k = kv.substr(0, e), v = e == std::string_view::npos ? std::string_view() : kv.substr(e + 1);
-      if (!kv.empty() && !v.empty()) p.quals.emplace_back(S.lower(k), S.unq(v));
+      if (!kv.empty() && !v.empty()) {
+        S.pools.quals.emplace_back(S.lower(k), S.unq(v));
+        p.nq++;
+      }
       a = b + 1;
     }
   }
@@ -350,7 +356,7 @@ const char* parse_purl(std::string_view s, Strs& S, Purl& p) {
       }
       a = b + 1;
     }
-    p.ns = S.keep(std::move(o));
+    p.ns = S.keep(o);
   }
   p.type = S.lower(typ);
   return nullptr;
@@ -403,7 +409,7 @@ bool py_int(std::string_view v, int64_t& out) {
 
 struct Comp {
   std::string_view type, name, group, version, bom_ref, purl_str;
-  std::vector<std::pair<std::string_view, std::string_view>> props;  // namespace prefix removed
+  uint32_t p0 = 0, np = 0;  // properties (namespace prefix removed): Pools::props[p0, p0 + np)
   bool has_purl = false;
   Purl purl;
 };
@@ -419,7 +425,7 @@ CompType comp_type(std::string_view t) {
   return CT_OTHER;
 }
 
-bool read_component(Reader& R, Comp& c, size_t* members = nullptr) {
+bool read_component(Reader& R, Pools& P, Comp& c, size_t* members = nullptr) {
   c = Comp{};
   return R.object([&](std::string_view k) {
     if (members) ++*members;
@@ -430,7 +436,8 @@ bool read_component(Reader& R, Comp& c, size_t* members = nullptr) {
     if (k == "bom-ref") return R.str_or_empty(c.bom_ref);
     if (k == "purl") return R.str_or_empty(c.purl_str);
     if (k == "properties") {
-      c.props.clear();
+      c.p0 = uint32_t(P.props.size());  // a repeated member: the last one wins
+      c.np = 0;
       if (!R.peek('[')) return R.skip();
       return R.array([&] {
         std::string_view pn, pv;
@@ -442,7 +449,8 @@ bool read_component(Reader& R, Comp& c, size_t* members = nullptr) {
             }))
           return false;
         if (pn.substr(0, kNamespace.size()) == kNamespace) pn.remove_prefix(kNamespace.size());
-        c.props.emplace_back(pn, pv);
+        P.props.emplace_back(pn, pv);
+        c.np++;
         return true;
       });
     }
@@ -458,11 +466,45 @@ struct Dep {
 
 }  // namespace
 
+std::string_view Sbom::keep(std::string_view a, std::string_view b, std::string_view c) {
+  const size_t n = a.size() + b.size() + c.size();
+  if (n == 0) return {};
+  if (n > chunk_left) {
+    const size_t sz = std::max<size_t>(n, size_t(1) << 20);
+    chunks.emplace_back(new char[sz]);
+    chunk_at = chunks.back().get();
+    chunk_left = sz;
+  }
+  char* d = chunk_at;
+  std::memcpy(d, a.data(), a.size());
+  if (!b.empty()) std::memcpy(d + a.size(), b.data(), b.size());
+  if (!c.empty()) std::memcpy(d + a.size() + b.size(), c.data(), c.size());
+  chunk_at += n;
+  chunk_left -= n;
+  return std::string_view(d, n);
+}
+
+namespace {
+// TVM_SBOM_TRACE=1 (measurement only): per-phase host times on stderr
+struct Lap {
+  bool on = std::getenv("TVM_SBOM_TRACE") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void operator()(const char* what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "sbom %-10s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
+};
+}  // namespace
+
 bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
-  out = Sbom{};
+  Lap lap;
   out.text.assign(text_in.data(), text_in.size());
-  Reader R{out.text.data(), out.text.size(), 0, out.owned, {}, 0};
-  Strs S{out.owned};
+  lap("copy");
+  Reader R{out.text.data(), out.text.size(), 0, out, {}, 0};
+  Pools pools;
+  Strs S{out, pools};
   std::vector<Comp> comps;
   Comp root;
   bool has_root = false;
@@ -481,7 +523,7 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
           comps.pop_back();
           return R.skip();
         }
-        return read_component(R, comps.back());
+        return read_component(R, pools, comps.back());
       });
     }
     if (k == "metadata") {
@@ -494,7 +536,7 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
           return R.skip();
         }
         size_t members = 0;
-        const bool good = read_component(R, root, &members);
+        const bool good = read_component(R, pools, root, &members);
         has_root = members > 0;  // an empty metadata component is no root
         return good;
       });
@@ -547,6 +589,7 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
   }
   out.serial = serial;
   out.version = version;
+  lap("parse");
 
   // parseComponents: unsupported types dropped, a component whose PURL does not parse skipped
   std::vector<Comp*> order;
@@ -573,6 +616,7 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
     }
     order.push_back(&root);
   }
+  lap("purls");
   // bom-ref -> component (a later one with the same ref replaces an earlier one)
   std::unordered_map<std::string_view, Comp*> by_ref;
   by_ref.reserve(order.size() * 2);
@@ -590,6 +634,7 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
     }
   }
 
+  lap("refs");
   // Decoder.Decode
   const Comp* os_c = nullptr;
   struct App {
@@ -597,7 +642,9 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
     std::string_view type, file_path;
   };
   std::vector<App> apps;
-  std::unordered_map<const Comp*, size_t> pkg_of;  // component -> index in pkgs (live ones)
+  // component (index in comps, root last) -> its package in pkgs, -1 for none
+  std::vector<int64_t> pkg_of(comps.size() + 1, -1);
+  auto comp_index = [&](const Comp* c) { return c == &root ? comps.size() : size_t(c - comps.data()); };
   std::vector<SbomPkg> pkgs;
   std::vector<const Comp*> pkg_comp;
   std::vector<uint8_t> taken;
@@ -618,8 +665,8 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
     if (ct == CT_APPLICATION) {
       std::string_view t;
       bool has_t = false;
-      for (auto& [k, v] : c->props)
-        if (k == "Type") {
+      for (uint32_t q = c->p0; q < c->p0 + c->np; q++)
+        if (const auto& [k, v] = pools.props[q]; k == "Type") {
           t = v;
           has_t = true;
           break;
@@ -641,7 +688,8 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
     if (!p.ns.empty() && cls != 1) k.name = S.join(p.ns, maven ? ":" : "/", p.name);
     if (!p.subpath.empty() && p.type == "cocoapods") k.name = S.join(p.name, "/", p.subpath);
     k.version = p.version;
-    for (auto& [qk, qv] : p.quals) {
+    for (uint32_t q = p.q0; q < p.q0 + p.nq; q++) {
+      const auto& [qk, qv] = pools.quals[q];
       if (qk == "arch") {
         k.arch = qv;
         k.present |= SP_ARCH;
@@ -675,14 +723,15 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
       } else if (lt == "conan") {
         k.id = S.join(k.name, "/", p.version);
       } else if ((lt == "gomod" || lt == "gobinary") && p.version.front() != 'v') {
-        k.id = S.join(k.name, "@v", p.version);
+        k.id = out.keep(k.name, "@v", p.version);
       } else if (lt == "jar" || lt == "pom" || lt == "gradle") {
         k.id = S.join(k.name, ":", p.version);
       } else {
         k.id = S.join(k.name, "@", p.version);
       }
     }
-    for (auto& [pk, pv] : c->props) {
+    for (uint32_t q = c->p0; q < c->p0 + c->np; q++) {
+      const auto& [pk, pv] = pools.props[q];
       if (pk == "PkgID") {
         k.id = pv;
       } else if (pk == "FilePath") {
@@ -725,16 +774,17 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
       if (k.src_epoch == 0) k.src_epoch = k.epoch;
       k.present |= SP_SRCNAME | SP_SRCVERSION | SP_SRCRELEASE | SP_SRCEPOCH;
     }
-    pkg_of[c] = pkgs.size();
+    pkg_of[comp_index(c)] = int64_t(pkgs.size());
     pkgs.push_back(k);
     pkg_comp.push_back(c);
   }
+  lap("libraries");
   taken.assign(pkgs.size(), 0);
   auto take = [&](const Comp* d, std::vector<SbomPkg>& dst) {
-    auto it = pkg_of.find(d);
-    if (it == pkg_of.end() || taken[it->second]) return;
-    taken[it->second] = 1;
-    dst.push_back(pkgs[it->second]);
+    const int64_t k = pkg_of[comp_index(d)];
+    if (k < 0 || taken[size_t(k)]) return;
+    taken[size_t(k)] = 1;
+    dst.push_back(pkgs[size_t(k)]);
   };
   if (os_c) {
     auto it = rels.find(os_c);
@@ -791,6 +841,7 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
     if (a.type != b.type) return a.type < b.type;
     return a.file_path < b.file_path;
   });
+  lap("assemble");
   // detector input views
   auto ts = [](std::string_view v) { return tvm_str{v.data(), v.size()}; };
   auto view = [&](const std::vector<SbomPkg>& src, std::vector<tvm_package>& dst) {
@@ -815,6 +866,7 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
   };
   view(out.packages, out.view);
   for (SbomApp& a : out.apps) view(a.libs, a.view);
+  lap("views");
   return true;
 }
 

@@ -17,7 +17,7 @@
 // detectors take.
 #pragma once
 #include <cstdint>
-#include <deque>
+#include <memory>
 #include <string>
 #include <string_view>
 #include <vector>
@@ -52,8 +52,12 @@ struct Sbom {
   std::vector<SbomPkg> packages;  // OS packages
   std::vector<tvm_package> view;
   std::vector<SbomApp> apps;
-  std::string text;               // the document (the views point into it)
-  std::deque<std::string> owned;  // strings built by the decode (unescaped, joined, split)
+  std::string text;  // the document (the views point into it)
+  // strings built by the decode (unescaped, joined): a bump arena of chunks that never move
+  std::vector<std::unique_ptr<char[]>> chunks;
+  size_t chunk_left = 0;
+  char* chunk_at = nullptr;
+  std::string_view keep(std::string_view a, std::string_view b = {}, std::string_view c = {});
 };
 
 // false: err holds the reference's message ("failed to decode CycloneDX JSON: ...",

@@ -298,6 +298,128 @@ def _decode_bom_meta(order, root, rels, serial, version):
     return out
 
 
+# ---- the native decoder (trivy_amd/csrc/sbom.cpp, tvm_sbom_*) ------------------------------------
+_SP_KEYS = [(1, "Arch"), (2, "Epoch"), (4, "Release"), (8, "Modularitylabel"), (16, "FilePath"), (32, "SrcName"),
+            (64, "SrcVersion"), (128, "SrcRelease"), (256, "SrcEpoch")]
+
+
+class NativeSBOM:
+    """A CycloneDX document decoded by the library (no Python objects per component): the
+    OS, and per target (-1 = the OS packages, 0.. = applications) a tvm_package array the
+    detectors take as it is (tvm_ospkg_detect / tvm_library_detect)."""
+
+    def __init__(self, text):
+        import ctypes
+        from ._lib import lib, errbuf
+        data = text.encode() if isinstance(text, str) else bytes(text)
+        h, e = ctypes.c_void_p(), errbuf()
+        if lib().tvm_sbom_decode_cyclonedx(data, len(data), ctypes.byref(h), e, len(e)):
+            raise SBOMError(e.value.decode())
+        self.h = h
+        from ._lib import RawStr
+        has_os, fam, name, serial = ctypes.c_int32(), RawStr(), RawStr(), RawStr()
+        ver, napps = ctypes.c_int64(), ctypes.c_size_t()
+        lib().tvm_sbom_info(h, ctypes.byref(has_os), ctypes.byref(fam), ctypes.byref(name), ctypes.byref(serial),
+                            ctypes.byref(ver), ctypes.byref(napps))
+        self.os = {"Family": fam.bytes().decode(), "Name": name.bytes().decode()} if has_os.value else None
+        self.serial, self.version, self.n_apps = serial.bytes().decode(), ver.value, napps.value
+
+    def target(self, app):
+        """(Type, FilePath, tvm_package pointer, n) of target `app` (-1: the OS packages)."""
+        import ctypes
+        from ._lib import lib, RawStr, RawPackage
+        t, fp, pk, n = RawStr(), RawStr(), ctypes.POINTER(RawPackage)(), ctypes.c_size_t()
+        lib().tvm_sbom_packages(self.h, app, ctypes.byref(t), ctypes.byref(fp), ctypes.byref(pk), ctypes.byref(n))
+        return t.bytes().decode(), fp.bytes().decode(), pk, n.value
+
+    def packages(self, app):
+        """The packages of target `app` as trivy_amd/sbom.py's dicts (checker / inspection)."""
+        import ctypes
+        from ._lib import lib, SbomExtra
+        _, _, pk, n = self.target(app)
+        out = []
+        ex = SbomExtra()
+        for i in range(n):
+            p = pk[i]
+            lib().tvm_sbom_package_extra(self.h, app, i, ctypes.byref(ex))
+            d = {"Name": p.name.bytes().decode(), "Version": p.version.bytes().decode(), "ID": p.id.bytes().decode()}
+            vals = {"Arch": p.arch.bytes().decode(), "Epoch": p.epoch, "Release": p.release.bytes().decode(),
+                    "Modularitylabel": p.modularitylabel.bytes().decode(), "FilePath": p.file_path.bytes().decode(),
+                    "SrcName": p.src_name.bytes().decode(), "SrcVersion": p.src_version.bytes().decode(),
+                    "SrcRelease": p.src_release.bytes().decode(), "SrcEpoch": p.src_epoch}
+            for bit, k in _SP_KEYS:
+                if ex.present & bit:
+                    d[k] = vals[k]
+            if ex.present & (512 | 1024):
+                d["Layer"] = {}
+                if ex.present & 512:
+                    d["Layer"]["Digest"] = ex.layer_digest.bytes().decode()
+                if ex.present & 1024:
+                    d["Layer"]["DiffID"] = ex.layer_diff_id.bytes().decode()
+            d["Identifier"] = {"PURL": ex.purl.bytes().decode(), "BOMRef": ex.bom_ref.bytes().decode()}
+            out.append(d)
+        return out
+
+    def as_dict(self):
+        """The decode in trivy_amd/sbom.py's form (without the root component)."""
+        apps = []
+        for a in range(self.n_apps):
+            t, fp, _, _ = self.target(a)
+            apps.append({"Type": t, "FilePath": fp, "Libraries": self.packages(a)})
+        return {"OS": self.os, "Packages": self.packages(-1), "Applications": apps,
+                "SerialNumber": self.serial, "Version": self.version}
+
+    def close(self):
+        h, self.h = getattr(self, "h", None), None
+        if h:
+            from . import _lib
+            if _lib._lib is not None:
+                _lib._lib.tvm_sbom_free(h)
+
+    def __del__(self):
+        self.close()
+
+
+def decode_cyclonedx_native(text):
+    return NativeSBOM(text)
+
+
+def scan_native(engine, nsbom, artifact_name="", now=None):
+    """scan() over a NativeSBOM: the library's tvm_package arrays go to tvm_ospkg_detect /
+    tvm_library_detect as they are (no per-package Python objects on the way in)."""
+    import ctypes
+    from ._lib import lib, errbuf, Package, Result, TVM_EUNSUPPORTED_TYPE
+    from .detector.ospkg import _convert, _now, DetectError, UnsupportedOSError
+    results = []
+
+    def run(fn, app, *head):
+        _, _, pk, n = nsbom.target(app)
+        res, e = Result(), errbuf()
+        rc = fn(engine.h, *head, ctypes.cast(pk, ctypes.POINTER(Package)), n, *(() if app >= 0 else (_now(now),)),
+                ctypes.byref(res), e, len(e))
+        if rc == TVM_EUNSUPPORTED_TYPE:
+            return None
+        if rc == 2 and app < 0:
+            raise UnsupportedOSError("unsupported os")
+        if rc:
+            raise DetectError(e.value.decode())
+        try:
+            return _convert(res, nsbom.packages(app))
+        finally:
+            lib().tvm_result_free(ctypes.byref(res))
+
+    if nsbom.os is not None and nsbom.os["Family"]:
+        fam, name = nsbom.os["Family"], nsbom.os["Name"]
+        vulns = run(lib().tvm_ospkg_detect, -1, fam.encode(), name.encode(), None)
+        results.append(("os-pkgs", fam, "%s (%s %s)" % (artifact_name, fam, name), vulns))
+    for a in range(nsbom.n_apps):
+        t, fp, _, _ = nsbom.target(a)
+        vulns = run(lib().tvm_library_detect, a, t.encode())
+        if vulns is not None:
+            results.append(("lang-pkgs", t, fp, vulns))
+    return results
+
+
 # ---- SPDX (pkg/sbom/spdx/unmarshal.go) and in-toto attestations (pkg/sbom/sbom.go) ----------------
 SPDX_PURL_CATEGORIES = {"PACKAGE-MANAGER", "PACKAGE_MANAGER"}  # SPDX 2.3 / 2.2 spelling of the category
 
