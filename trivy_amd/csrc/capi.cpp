@@ -466,7 +466,7 @@ void tvm_batch_free(tvm_batch* b) {
                     static_cast<void*>(b->dev.tail), static_cast<void*>(b->dev.spill),
                     static_cast<void*>(b->external_out ? nullptr : b->m.pkg),
                     static_cast<void*>(b->external_out ? nullptr : b->m.adv), static_cast<void*>(b->m.dir),
-                    static_cast<void*>(b->m.ctl),
+                    static_cast<void*>(b->m.ctl), static_cast<void*>(b->dev.tile_list),
                     static_cast<void*>(b->fill_out)})
       if (p) (void)hipFree(p);
   }

@@ -17,6 +17,7 @@ namespace tvm {
 class DB;
 
 constexpr int kTile = 256;   // packages per tile (workgroup) of the match kernels
+constexpr int kLibClassesMax = 5;  // single-ecosystem library grammar classes (DevBatch::tile_list)
 constexpr int kGroup = 64;   // packages per offset group (one wavefront); tile_off is per group
 constexpr int kGroupsPerTile = kTile / kGroup;
 
@@ -88,6 +89,11 @@ struct DevBatch {
   // probe -> sweep hand-off (device only)
   PkgRec* rec = nullptr;
   uint4* tail = nullptr;  // key bytes 16..31 per package
+  // library batches (grammar set beyond the OS ones), device-resident path: the tiles ordered
+  // by grammar class, class c = tile_list[class_begin[c], class_begin[c + 1]); classes 0..4
+  // are one ecosystem each (libver.h GM_NPM, GM_PEP, GM_GEN, GM_GEM, GM_MVN), 5 mixed tiles
+  uint32_t* tile_list = nullptr;
+  uint32_t class_begin[kLibClassesMax + 2] = {};
 };
 
 // Device-side results of one match pass: the per-package advisory lists as two columns
@@ -336,6 +342,7 @@ class Engine {
   void dropin_stats(uint64_t out[3]);
 
   const DB& db() const { return *db_; }
+  static constexpr int kLibClasses = kLibClassesMax;
   const PlatInfo* device_plats() const { return d_.plats; }
 
   // Sweep-kernel variant (pairs per lane / LDS buffer); returns the previous one.  Default
@@ -359,6 +366,7 @@ class Engine {
   std::unique_ptr<Dropin> dropin_;
   std::mutex dropin_init_mu_;
   Dropin* dropin(std::string& err);
+  bool classify_tiles(const HostBatch& hb, DevBatch& b, std::string& err) const;
   bool dropin_run(Dropin& d, DropinReq* const* reqs, size_t n, std::string& err);
 };
 

@@ -1001,20 +1001,41 @@ TVM_HD bool gem_encode(const uint8_t* s, uint32_t n, Sink& o) {
 }
 
 // ------------------------------------------------------------------ grammar dispatch ----
-template <class Sink>
-TVM_HD bool encode_version_cls(uint8_t cmp, const uint8_t* s, uint32_t n, Sink& o, uint32_t& cls) {
+// Only the grammars of set GM are compiled in (a kernel specialised for go-version tiles
+// carries neither the Maven parse nor the RubyGems segment arrays, and so no scratch).
+template <uint32_t GM, class Sink>
+TVM_HD bool encode_version_cls_gm(uint8_t cmp, const uint8_t* s, uint32_t n, Sink& o, uint32_t& cls) {
   cls = 0;
-  switch (cmp) {
-    case CMP_GENERIC: return gen_encode(s, n, false, o);
-    case CMP_BITNAMI: return gen_encode(s, n, true, o);
-    case CMP_NPM: return npm_encode(s, n, o, cls);
-    case CMP_PEP440: return pep_encode(s, n, o, cls);
-    case CMP_MAVEN:
+  if constexpr ((GM >> 4) & 1u) {  // CMP_GENERIC
+    if (cmp == CMP_GENERIC) return gen_encode(s, n, false, o);
+  }
+  if constexpr ((GM >> 9) & 1u) {  // CMP_BITNAMI
+    if (cmp == CMP_BITNAMI) return gen_encode(s, n, true, o);
+  }
+  if constexpr ((GM >> 5) & 1u) {  // CMP_NPM
+    if (cmp == CMP_NPM) return npm_encode(s, n, o, cls);
+  }
+  if constexpr ((GM >> 6) & 1u) {  // CMP_PEP440
+    if (cmp == CMP_PEP440) return pep_encode(s, n, o, cls);
+  }
+  if constexpr ((GM >> 7) & 1u) {  // CMP_MAVEN
+    if (cmp == CMP_MAVEN) {
       cls = mvn_numeric(s, n) ? 1u : 0u;
       return mvn_encode(s, n, o);
-    case CMP_GEM: return gem_encode(s, n, o);
-    default: return encode_version(cmp, s, n, o);
+    }
   }
+  if constexpr ((GM >> 8) & 1u) {  // CMP_GEM
+    if (cmp == CMP_GEM) return gem_encode(s, n, o);
+  }
+  if constexpr ((GM & 0xEu) != 0) {  // the OS grammars
+    if (cmp == CMP_DEB || cmp == CMP_APK || cmp == CMP_RPM) return encode_version(cmp, s, n, o);
+  }
+  return false;
+}
+
+template <class Sink>
+TVM_HD bool encode_version_cls(uint8_t cmp, const uint8_t* s, uint32_t n, Sink& o, uint32_t& cls) {
+  return encode_version_cls_gm<0x3FEu>(cmp, s, n, o, cls);
 }
 
 // Grammar sets a match kernel is specialised for (bit c = Cmp c): a batch whose platforms
@@ -1024,6 +1045,12 @@ enum : uint32_t {
   GM_DEB = 1u << CMP_DEB,
   GM_OS = GM_DEB | (1u << CMP_APK) | (1u << CMP_RPM),
   GM_ALL = 0x3FEu,
+  // single-ecosystem library sets: a library batch's tiles run the kernel of their grammar
+  GM_NPM = 1u << CMP_NPM,
+  GM_PEP = 1u << CMP_PEP440,
+  GM_GEN = (1u << CMP_GENERIC) | (1u << CMP_BITNAMI),
+  GM_GEM = 1u << CMP_GEM,
+  GM_MVN = 1u << CMP_MAVEN,
 };
 
 template <uint32_t GM, class Sink>
@@ -1035,7 +1062,7 @@ TVM_HD bool encode_version_gm(uint8_t cmp, const uint8_t* s, uint32_t n, Sink& o
   } else if constexpr ((GM & ~GM_OS) == 0) {
     return encode_version(cmp, s, n, o);
   } else {
-    return encode_version_cls(cmp, s, n, o, cls);
+    return encode_version_cls_gm<GM>(cmp, s, n, o, cls);
   }
 }
 

@@ -88,6 +88,7 @@ struct FusedArgs {
   SweepArgs sa;
   CopyOutArgs co;       // end-to-end pipeline: the previous chunk's result move ...
   uint32_t n_copy = 0;  // ... by workgroups [0, n_copy) of this launch (0: none)
+  const uint32_t* tiles = nullptr;  // workgroup w matches launch tile tiles[w] (nullptr: tile w); grammar-class launches
 };
 
 using ProbeFn = void (*)(uint32_t n_tiles, hipStream_t st, const ProbeArgs& a);
@@ -824,7 +825,7 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
     copy_out_tiles(fa.co, blockIdx.x, fa.n_copy, reinterpret_cast<uint32_t*>(buf));
     return;
   }
-  const uint32_t tid = threadIdx.x, t = blockIdx.x - fa.n_copy;
+  const uint32_t tid = threadIdx.x, t = fa.tiles ? fa.tiles[blockIdx.x - fa.n_copy] : blockIdx.x - fa.n_copy;
   const uint32_t p = t * kTile + tid;
   uint2 d = make_uint2(0xFFFFFFFFu, 0);
   if (p < a.n) d = a.pk[p];

@@ -64,6 +64,8 @@ class RedHatMerge {
  private:
   int dev_ = -1;
   RhMerged out_;
+  uint32_t* counts_ = nullptr;            // per tile: merged entries (rh_count_kernel)
+  unsigned long long* bases_ = nullptr;   // per tile: output base (rh_scan_kernel)
   void release();
 };
 

@@ -12,7 +12,9 @@
 // order, so a package's members of one CVE are adjacent and in Get order, and the CVEs
 // ascend.  The merge is therefore one pass per tile segment, no sort:
 //   count   a pair heads a group unless it is a Red Hat pair continuing its predecessor's
-//           (package, ID-rank); one reservation per tile for the tile's group count;
+//           (package, ID-rank); per tile its group count (a tile without Red Hat
+//           packages: its pair count, no reads of the pairs);
+//   scan    the tiles' output bases (one workgroup);
 //   emit    block scan of the head flags; each head lane walks its group (a few pairs) for
 //           the member with the greatest fixed version (rpm-order rank computed at load
 //           time; ties keep the first, as LessThan does) and writes {pkg, representative,
@@ -77,59 +79,34 @@ __device__ __forceinline__ uint32_t block_flag_scan(bool f, uint32_t tid, uint32
   return tot;
 }
 
-__global__ __launch_bounds__(kBlock) void rh_merge_kernel(MergeArgs a) {
+// Does tile t hold a Red Hat package?  (Tiles without one pass their pairs through.)
+__device__ __forceinline__ bool tile_has_redhat(const MergeArgs& a, uint32_t t, uint32_t tid) {
+  const uint32_t p = t * kBlock + tid;
+  const uint32_t plat = p < a.n ? a.pk[p].x : 0xFFFFFFFFu;
+  return __syncthreads_or(plat < a.n_plats && a.plats[plat].drv == DRV_REDHAT) != 0;
+}
+
+// Pass 1: the merged entry count of every tile (the groups of its segment) into counts[t].
+// The tiles' output bases then come from a scan (rh_scan_kernel), not from an atomic
+// reservation per tile: 78k same-address atomics serialised the round-3 kernel (C5: 0.95 ms,
+// SQ_WAIT_ANY / SQ_WAVE_CYCLES = 0.95).
+__global__ __launch_bounds__(kBlock) void rh_count_kernel(MergeArgs a, uint32_t* counts) {
   __shared__ uint32_t ws[kWaves];
-  __shared__ unsigned long long s_out;
   const uint32_t t = blockIdx.x, tid = threadIdx.x;
   const TileDir d = a.dir[t];
   const uint64_t b0 = d.base;
   const uint32_t cnt = d.count;
   if (b0 + cnt > a.raw_cap) {  // an overflowed match list: nothing valid to merge
     if (tid == 0) {
-      a.mdir[t] = TileDir{0, 0, 0};
+      counts[t] = 0;
       atomicOr(a.mctl + 3, 1ull);
     }
     return;
   }
-  // A tile without Red Hat packages (every pair its own group) passes through: one
-  // reservation, then a coalesced copy - no head scans, no group keys (C5: 70 % of pairs)
-  {
-    const uint32_t p = t * kBlock + tid;
-    const uint32_t plat = p < a.n ? a.pk[p].x : 0xFFFFFFFFu;
-    const bool rh_pkg = plat < a.n_plats && a.plats[plat].drv == DRV_REDHAT;
-    if (!__syncthreads_or(rh_pkg)) {
-      if (tid == 0) {
-        const unsigned long long o = cnt ? atomicAdd(a.mctl, (unsigned long long)cnt) : 0ull;
-        s_out = o;
-        a.mdir[t] = TileDir{o, o + cnt <= a.mcap ? cnt : 0u, 0};
-      }
-      __syncthreads();
-      const unsigned long long o0 = s_out;
-      if (o0 + cnt > a.mcap) return;
-      constexpr int kU = 4;  // loads of four pairs in flight per lane before the stores
-      for (uint32_t c = 0; c < cnt; c += kU * kBlock) {
-        uint32_t pp[kU], aa[kU];
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-          const uint32_t i = c + u * kBlock + tid;
-          pp[u] = i < cnt ? a.pkg[b0 + i] : 0u;
-          aa[u] = i < cnt ? a.adv[b0 + i] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < kU; u++) {
-          const uint32_t i = c + u * kBlock + tid;
-          if (i < cnt) {
-            a.mpkg[o0 + i] = pp[u];
-            a.madv[o0 + i] = aa[u];
-            a.mbase[o0 + i] = aa[u];
-            a.mgrp[o0 + i] = make_uint2(uint32_t(b0 + i), 1u);
-          }
-        }
-      }
-      return;
-    }
+  if (!tile_has_redhat(a, t, tid)) {  // every pair its own group
+    if (tid == 0) counts[t] = cnt;
+    return;
   }
-  // pass 1: heads of the tile's segment
   uint32_t heads = 0;
   bool order_bad = false;
   for (uint32_t c = 0; c < cnt; c += kBlock) {
@@ -151,15 +128,79 @@ __global__ __launch_bounds__(kBlock) void rh_merge_kernel(MergeArgs a) {
     heads += block_flag_scan(h, tid, ws, ex);
   }
   if (order_bad) atomicOr(a.mctl + 3, (unsigned long long)ERR_RH_ORDER);
-  if (tid == 0) {
-    const unsigned long long o = atomicAdd(a.mctl, (unsigned long long)heads);
-    s_out = o;
-    a.mdir[t] = TileDir{o, o + heads <= a.mcap ? heads : 0u, 0};
+  if (tid == 0) counts[t] = heads;
+}
+
+// Exclusive scan of the tiles' counts into bases (one workgroup; n_tiles / 1024 values per
+// thread, then a block scan of the thread sums); the total goes to mctl[0].
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void rh_scan_kernel(const uint32_t* counts, unsigned long long* bases,
+                                                               uint32_t n_tiles, unsigned long long* mctl) {
+  __shared__ unsigned long long part[kScanThreads / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t per = (n_tiles + kScanThreads - 1) / kScanThreads;
+  const uint32_t b = min(n_tiles, tid * per), e = min(n_tiles, b + per);
+  unsigned long long sum = 0;
+  for (uint32_t t = b; t < e; t++) sum += counts[t];
+  unsigned long long x = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(x, o, 64);
+    if (lane >= uint32_t(o)) x += y;
   }
+  if (lane == 63) part[wave] = x;
   __syncthreads();
-  const unsigned long long o0 = s_out;
-  if (o0 + heads > a.mcap) return;  // cannot happen (merged <= raw); the count tells the host
-  // pass 2: emit one entry per group
+  unsigned long long off = 0, tot = 0;
+  for (uint32_t w = 0; w < kScanThreads / 64; w++) {
+    off += w < wave ? part[w] : 0ull;
+    tot += part[w];
+  }
+  unsigned long long run = off + x - sum;
+  for (uint32_t t = b; t < e; t++) {
+    bases[t] = run;
+    run += counts[t];
+  }
+  if (tid == 0) mctl[0] = tot;
+}
+
+// Pass 2: each tile writes its merged entries at its base: a coalesced copy for a tile
+// without Red Hat packages, else one entry per group (the member with the greatest fixed
+// version; ties keep the first, as LessThan does).
+__global__ __launch_bounds__(kBlock) void rh_emit_kernel(MergeArgs a, const uint32_t* counts,
+                                                         const unsigned long long* bases) {
+  __shared__ uint32_t ws[kWaves];
+  const uint32_t t = blockIdx.x, tid = threadIdx.x;
+  const TileDir d = a.dir[t];
+  const uint64_t b0 = d.base;
+  const uint32_t cnt = d.count;
+  const unsigned long long o0 = bases[t];
+  const uint32_t heads = counts[t];
+  const bool fits = b0 + cnt <= a.raw_cap && o0 + heads <= a.mcap;
+  if (tid == 0) a.mdir[t] = TileDir{o0, fits ? heads : 0u, 0};
+  if (!fits) return;  // cannot happen (merged <= raw); the counts tell the host
+  if (!tile_has_redhat(a, t, tid)) {
+    constexpr int kU = 4;  // loads of four pairs in flight per lane before the stores
+    for (uint32_t c = 0; c < cnt; c += kU * kBlock) {
+      uint32_t pp[kU], aa[kU];
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const uint32_t i = c + u * kBlock + tid;
+        pp[u] = i < cnt ? a.pkg[b0 + i] : 0u;
+        aa[u] = i < cnt ? a.adv[b0 + i] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const uint32_t i = c + u * kBlock + tid;
+        if (i < cnt) {
+          a.mpkg[o0 + i] = pp[u];
+          a.madv[o0 + i] = aa[u];
+          a.mbase[o0 + i] = aa[u];
+          a.mgrp[o0 + i] = make_uint2(uint32_t(b0 + i), 1u);
+        }
+      }
+    }
+    return;
+  }
   uint32_t done = 0;
   for (uint32_t c = 0; c < cnt; c += kBlock) {
     bool h = false;
@@ -210,6 +251,10 @@ void RedHatMerge::release() {
   Engine::free_matches(dev_, out_.m);
   if (out_.base) (void)hipFree(out_.base);
   if (out_.grp) (void)hipFree(out_.grp);
+  if (counts_) (void)hipFree(counts_);
+  if (bases_) (void)hipFree(bases_);
+  counts_ = nullptr;
+  bases_ = nullptr;
   out_ = RhMerged{};
 }
 
@@ -224,13 +269,17 @@ bool RedHatMerge::launch(const RhInputs& in, hipStream_t st, std::string& err) {
     dev_ = dev;
     const uint64_t cap = raw.cap;
     const uint32_t nt = std::max<uint32_t>(in.n_tiles, 1);
-    void *p = nullptr, *q = nullptr, *r = nullptr, *s = nullptr, *t = nullptr, *c = nullptr;
+    void *p = nullptr, *q = nullptr, *r = nullptr, *s = nullptr, *t = nullptr, *c = nullptr, *u = nullptr, *v = nullptr;
     const bool good = ok(hipMalloc(&p, cap * 4), "hipMalloc(merged)", err) &&
                       ok(hipMalloc(&q, cap * 4), "hipMalloc(merged)", err) &&
                       ok(hipMalloc(&r, cap * 4), "hipMalloc(merged)", err) &&
                       ok(hipMalloc(&s, cap * 8), "hipMalloc(merged)", err) &&
                       ok(hipMalloc(&t, nt * sizeof(TileDir)), "hipMalloc(merged dir)", err) &&
-                      ok(hipMalloc(&c, 64), "hipMalloc(merged ctl)", err);
+                      ok(hipMalloc(&c, 64), "hipMalloc(merged ctl)", err) &&
+                      ok(hipMalloc(&u, nt * 4), "hipMalloc(merge counts)", err) &&
+                      ok(hipMalloc(&v, nt * 8), "hipMalloc(merge bases)", err);
+    counts_ = static_cast<uint32_t*>(u);
+    bases_ = static_cast<unsigned long long*>(v);
     out_.m.pkg = static_cast<uint32_t*>(p);
     out_.m.adv = static_cast<uint32_t*>(q);
     out_.base = static_cast<uint32_t*>(r);
@@ -265,8 +314,10 @@ bool RedHatMerge::launch(const RhInputs& in, hipStream_t st, std::string& err) {
   a.mgrp = out_.grp;
   a.mcap = out_.cap;
   a.mctl = out_.m.ctl;
-  hipLaunchKernelGGL(rh_merge_kernel, dim3(in.n_tiles), dim3(kBlock), 0, st, a);
-  return ok(hipGetLastError(), "rh_merge_kernel", err);
+  hipLaunchKernelGGL(rh_count_kernel, dim3(in.n_tiles), dim3(kBlock), 0, st, a, counts_);
+  hipLaunchKernelGGL(rh_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, counts_, bases_, in.n_tiles, out_.m.ctl);
+  hipLaunchKernelGGL(rh_emit_kernel, dim3(in.n_tiles), dim3(kBlock), 0, st, a, counts_, bases_);
+  return ok(hipGetLastError(), "rh_merge kernels", err);
 }
 
 bool RedHatMerge::fetch(const RhInputs& in, std::vector<uint32_t>& pkg, std::vector<uint32_t>& adv,
