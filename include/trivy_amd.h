@@ -355,7 +355,10 @@ void tvm_pool_trim(void);
  * the detector input as tvm_package records (valid until tvm_sbom_free), ready for
  * tvm_ospkg_detect (app = -1) and tvm_library_detect (app = 0..n_apps-1). */
 typedef struct tvm_sbom tvm_sbom;
-int tvm_sbom_decode_cyclonedx(const char* text, size_t len, tvm_sbom** out, char* err, size_t errlen);
+/* flags: TVM_SBOM_BORROW = the result points into `text`, which must stay valid until
+ * tvm_sbom_free (no copy of the document); else the document is copied. */
+enum { TVM_SBOM_BORROW = 1 };
+int tvm_sbom_decode_cyclonedx(const char* text, size_t len, uint32_t flags, tvm_sbom** out, char* err, size_t errlen);
 void tvm_sbom_free(tvm_sbom* s);
 int tvm_sbom_info(const tvm_sbom* s, int32_t* has_os, tvm_str* os_family, tvm_str* os_name, tvm_str* serial,
                   int64_t* version, size_t* n_apps);

@@ -164,7 +164,8 @@ _SIG = [
     ("tvm_device_sync", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_pipeline_times", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     ("tvm_pool_stats", None, [ctypes.POINTER(ctypes.c_uint64)]),
-    ("tvm_sbom_decode_cyclonedx", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p),
+    ("tvm_sbom_decode_cyclonedx", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
+                                                 ctypes.POINTER(ctypes.c_void_p),
                                                  ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_sbom_free", None, [ctypes.c_void_p]),
     ("tvm_sbom_info", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(RawStr),

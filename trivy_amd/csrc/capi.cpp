@@ -1697,12 +1697,12 @@ struct tvm_sbom {
   Sbom s;
 };
 
-int tvm_sbom_decode_cyclonedx(const char* text, size_t len, tvm_sbom** out, char* err, size_t errlen) {
-  if (!out || (len && !text)) return TVM_EINVAL;
+int tvm_sbom_decode_cyclonedx(const char* text, size_t len, uint32_t flags, tvm_sbom** out, char* err, size_t errlen) {
+  if (!out || (len && !text) || (flags & ~uint32_t(TVM_SBOM_BORROW))) return TVM_EINVAL;
   *out = nullptr;
   auto* h = new tvm_sbom();
   std::string msg;
-  if (!decode_cyclonedx(std::string_view(text, len), h->s, msg)) {
+  if (!decode_cyclonedx(std::string_view(text, len), h->s, msg, (flags & TVM_SBOM_BORROW) != 0)) {
     delete h;
     set_err(err, errlen, msg);
     return TVM_EINVAL;
@@ -1722,34 +1722,27 @@ int tvm_sbom_info(const tvm_sbom* h, int32_t* has_os, tvm_str* os_family, tvm_st
   if (os_name) *os_name = tvm_str{s.os_name.data(), s.os_name.size()};
   if (serial) *serial = tvm_str{s.serial.data(), s.serial.size()};
   if (version) *version = s.version;
-  if (n_apps) *n_apps = s.apps.size();
+  if (n_apps) *n_apps = s.targets.empty() ? 0 : s.targets.size() - 1;
   return TVM_OK;
 }
 
 int tvm_sbom_packages(const tvm_sbom* h, int64_t app, tvm_str* type, tvm_str* file_path, const tvm_package** pkgs,
                       size_t* n) {
-  if (!h || app < -1 || (app >= 0 && size_t(app) >= h->s.apps.size())) return TVM_EINVAL;
+  if (!h || app < -1 || size_t(app + 1) >= h->s.targets.size()) return TVM_EINVAL;
   const Sbom& s = h->s;
-  if (app < 0) {
-    if (type) *type = tvm_str{nullptr, 0};
-    if (file_path) *file_path = tvm_str{nullptr, 0};
-    if (pkgs) *pkgs = s.view.data();
-    if (n) *n = s.view.size();
-    return TVM_OK;
-  }
-  const SbomApp& a = s.apps[size_t(app)];
-  if (type) *type = tvm_str{a.type.data(), a.type.size()};
-  if (file_path) *file_path = tvm_str{a.file_path.data(), a.file_path.size()};
-  if (pkgs) *pkgs = a.view.data();
-  if (n) *n = a.view.size();
+  const SbomTarget& t = s.targets[size_t(app + 1)];
+  if (type) *type = tvm_str{t.type.data(), t.type.size()};
+  if (file_path) *file_path = tvm_str{t.file_path.data(), t.file_path.size()};
+  if (pkgs) *pkgs = s.view.data() + t.begin;
+  if (n) *n = t.end - t.begin;
   return TVM_OK;
 }
 
 int tvm_sbom_package_extra(const tvm_sbom* h, int64_t app, size_t i, tvm_sbom_extra* out) {
-  if (!h || !out || app < -1 || (app >= 0 && size_t(app) >= h->s.apps.size())) return TVM_EINVAL;
-  const std::vector<SbomPkg>& v = app < 0 ? h->s.packages : h->s.apps[size_t(app)].libs;
-  if (i >= v.size()) return TVM_EINVAL;
-  const SbomPkg& p = v[i];
+  if (!h || !out || app < -1 || size_t(app + 1) >= h->s.targets.size()) return TVM_EINVAL;
+  const SbomTarget& t = h->s.targets[size_t(app + 1)];
+  if (i >= t.end - t.begin) return TVM_EINVAL;
+  const SbomExtra& p = h->s.extra[t.begin + i];
   auto ts = [](std::string_view x) { return tvm_str{x.data(), x.size()}; };
   out->purl = ts(p.purl);
   out->bom_ref = ts(p.bom_ref);

@@ -501,7 +501,12 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
       }();
       fa.n_copy = n_copy;
     }
-    fused_fn(b.gm, vi)(nt, pst, fa);
+    const FusedFn fn = fused_fn(b.gm, vi);
+    if (!fn) {
+      err = std::string("match-path variant ") + kVariantNames[vi - 1] + " is not built for this batch's grammar set";
+      return false;
+    }
+    fn(nt, pst, fa);
     return hip_ok(hipGetLastError(), "match kernel launch", err);
   }
   const bool filt = (b.gm & ~GM_DEB) != 0;

@@ -324,8 +324,9 @@ __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uin
 
 // A tile's string window (nv 16-byte words, nv <= kStage / 16) into LDS, plus two zero
 // words: every lane issues its (at most kStage / 16 / kTile) loads before storing any.
+template <uint32_t STG = kStage>
 __device__ __forceinline__ void stage_window(uint4* buf, const uint8_t* src8, uint32_t nv, uint32_t tid) {
-  constexpr uint32_t SV = (kStage / 16 + kTile - 1) / kTile;
+  constexpr uint32_t SV = (STG / 16 + kTile - 1) / kTile;
   const uint4* src = reinterpret_cast<const uint4*>(src8);
   if (nv) {
     uint4 v[SV];
@@ -351,8 +352,9 @@ __device__ __forceinline__ uint32_t wave_exscan(uint32_t v, uint32_t lane) {
   return x - v;
 }
 
+template <uint32_t STG = kStage>
 __device__ __forceinline__ void stage_window_wave(uint4* buf, const uint8_t* src8, uint32_t nv, uint32_t lane) {
-  constexpr uint32_t SV = (kStage / 4 / 16 + 63) / 64;
+  constexpr uint32_t SV = (STG / 4 / 16 + 63) / 64;
   const uint4* src = reinterpret_cast<const uint4*>(src8);
   if (nv) {
     uint4 v[SV];
@@ -796,9 +798,11 @@ __global__ __launch_bounds__(kTile) void sweep_kernel(SweepArgs a) {
 // of one CU sit in different phases, so one tile's probe latency overlaps another's sweep.
 // DIAG (measurement only, wrong match lists by construction; "diag_*" variants): bit 0 skips
 // the version encoder, bit 1 the index probe, bit 2 the sweep.
-template <uint32_t GM, int K, int MB, int FILT, int DIAG = 0, int WPE = 1, int SEG = 0>
+// STG: LDS bytes for the tile's string window (smaller: more tiles resident per CU, more
+// windows read from global memory instead).
+template <uint32_t GM, int K, int MB, int FILT, int DIAG = 0, int WPE = 1, int SEG = 0, uint32_t STG = kStage>
 __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
-  constexpr uint32_t kStageVec = kStage / 16 + 8;  // + two zero words per wave window (per-wave staging)
+  constexpr uint32_t kStageVec = STG / 16 + 8;  // + two zero words per wave window (per-wave staging)
   constexpr uint32_t kMbufVec = (MB * 5 + 15) / 16;
   __shared__ uint4 buf[kStageVec > kMbufVec ? kStageVec : kMbufVec];  // strings (probe), then matches (sweep)
   // the probe's per-lane dpkg keys + code table share LDS with the sweep's state (the scan
@@ -839,15 +843,15 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
   bool staged;
   if constexpr (kWaveStage) {
     off = wave_exscan(nlen + vlen, tid & 63);
-    sbuf = buf + (tid >> 6) * (kStage / 4 / 16 + 2);
-    staged = w1 - base16 <= kStage / 4;
-    if (staged) stage_window_wave(sbuf, a.arena + base16, uint32_t((w1 - base16 + 15) / 16), tid & 63);
+    sbuf = buf + (tid >> 6) * (STG / 4 / 16 + 2);
+    staged = w1 - base16 <= STG / 4;
+    if (staged) stage_window_wave<STG>(sbuf, a.arena + base16, uint32_t((w1 - base16 + 15) / 16), tid & 63);
     if (tid < 128) u.pr.tab[tid] = deb_fast_code(tid);
     __syncthreads();  // the code table (one wave's LDS traffic alone is ordered)
   } else {
     block_exscan<kTile>(s.wsum[0], nlen + vlen, tid, off);
-    staged = w1 - base16 <= kStage;
-    if (staged) stage_window(buf, a.arena + base16, uint32_t((w1 - base16 + 15) / 16), tid);
+    staged = w1 - base16 <= STG;
+    if (staged) stage_window<STG>(buf, a.arena + base16, uint32_t((w1 - base16 + 15) / 16), tid);
     if (tid < 128) u.pr.tab[tid] = deb_fast_code(tid);
     __syncthreads();
   }
@@ -880,9 +884,9 @@ void launch_sweep(uint32_t n_tiles, hipStream_t st, const SweepArgs& a) {
   hipLaunchKernelGGL((sweep_kernel<K, MB, FILT>), dim3(n_tiles), dim3(kTile), 0, st, a);
 }
 
-template <uint32_t GM, int K, int MB, int FILT, int DIAG = 0, int WPE = 1, int SEG = 0>
+template <uint32_t GM, int K, int MB, int FILT, int DIAG = 0, int WPE = 1, int SEG = 0, uint32_t STG = kStage>
 void launch_fused(uint32_t n_tiles, hipStream_t st, const FusedArgs& a) {
-  hipLaunchKernelGGL((fused_kernel<GM, K, MB, FILT, DIAG, WPE, SEG>), dim3(n_tiles + a.n_copy), dim3(kTile), 0, st, a);
+  hipLaunchKernelGGL((fused_kernel<GM, K, MB, FILT, DIAG, WPE, SEG, STG>), dim3(n_tiles + a.n_copy), dim3(kTile), 0, st, a);
 }
 
 // Table entry of variant (F, K, MB) for grammar set GM / row-filter level FILT
@@ -893,6 +897,11 @@ constexpr FusedFn fused_entry() {
   if constexpr (F == 0) return nullptr;
   else if constexpr (F == 4) return &launch_fused<GM, K, MB, FILT, 0, 1, 1>;
   else if constexpr (F == 5) return &launch_fused<GM, K, MB, FILT, 0, 1, 3>;
+  // per-wave staging + segments with a smaller string window and match buffer, so that more
+  // tiles are resident per CU (dpkg-only batches; not built for the other grammar sets)
+  else if constexpr ((F == 6 || F == 7) && GM != GM_DEB) return nullptr;
+  else if constexpr (F == 6) return &launch_fused<GM, K, MB, FILT, 0, 6, 3, 8192>;
+  else if constexpr (F == 7) return &launch_fused<GM, K, MB, FILT, 0, 8, 3, 6144>;
   else return &launch_fused<GM, K, MB, FILT, (F >= 10 ? F - 10 : 0), TVM_FUSED_WPE(F)>;
 }
 

@@ -81,10 +81,24 @@ struct Reader {
     ws();
     if (i >= n || s[i] != '"') return fail("expected a string");
     const size_t a = ++i;
+    // eight bytes at a time to the first quote, backslash or control byte (SWAR)
+    constexpr uint64_t kOnes = 0x0101010101010101ull, kHigh = 0x8080808080808080ull;
+    while (i + 8 <= n) {
+      uint64_t w;
+      std::memcpy(&w, s + i, 8);
+      const uint64_t q = w ^ (kOnes * '"'), b = w ^ (kOnes * '\\');
+      const uint64_t hit = ((q - kOnes) & ~q) | ((b - kOnes) & ~b) | ((w - kOnes * 0x20) & ~w);
+      if (hit & kHigh) {
+        i += size_t(__builtin_ctzll(hit & kHigh)) >> 3;
+        break;
+      }
+      i += 8;
+    }
     while (i < n && s[i] != '"' && s[i] != '\\') {
       if (uint8_t(s[i]) < 0x20) return fail("control character in string");
       i++;
     }
+    if (i < n && uint8_t(s[i]) < 0x20) return fail("control character in string");
     if (i >= n) return fail("unterminated string");
     if (s[i] == '"') {
       out = std::string_view(s + a, i - a);
@@ -458,6 +472,59 @@ bool read_component(Reader& R, Pools& P, Comp& c, size_t* members = nullptr) {
   });
 }
 
+// bom-ref -> component: open addressing over (hash, component); a later put of the same
+// ref replaces the earlier component (a JSON decode into a map keeps the last)
+class RefMap {
+ public:
+  explicit RefMap(size_t n) {
+    size_t cap = 16;
+    while (cap < 2 * n + 2) cap <<= 1;
+    e_.assign(cap, E{0, nullptr});
+    mask_ = cap - 1;
+  }
+  void put(std::string_view k, Comp* c) {
+    const uint64_t h = hash(k);
+    for (size_t i = h & mask_;; i = (i + 1) & mask_) {
+      if (!e_[i].c) {
+        e_[i] = E{h, c};
+        return;
+      }
+      if (e_[i].h == h && e_[i].c->bom_ref == k) {
+        e_[i].c = c;
+        return;
+      }
+    }
+  }
+  Comp* get(std::string_view k) const {
+    const uint64_t h = hash(k);
+    for (size_t i = h & mask_;; i = (i + 1) & mask_) {
+      if (!e_[i].c) return nullptr;
+      if (e_[i].h == h && e_[i].c->bom_ref == k) return e_[i].c;
+    }
+  }
+
+ private:
+  struct E {
+    uint64_t h;
+    Comp* c;
+  };
+  std::vector<E> e_;
+  size_t mask_ = 0;
+  static uint64_t hash(std::string_view k) {
+    uint64_t h = 1469598103934665603ull ^ k.size();
+    size_t i = 0;
+    for (; i + 8 <= k.size(); i += 8) {
+      uint64_t w;
+      std::memcpy(&w, k.data() + i, 8);
+      h = (h ^ w) * 0x9E3779B97F4A7C15ull;
+      h ^= h >> 29;
+    }
+    for (; i < k.size(); i++) h = (h ^ uint8_t(k[i])) * 1099511628211ull;
+    h ^= h >> 32;
+    return h * 0xD6E8FEB86659FD93ull;
+  }
+};
+
 struct Dep {
   std::string_view ref;
   std::vector<std::string_view> on;
@@ -498,14 +565,21 @@ struct Lap {
 };
 }  // namespace
 
-bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
+bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err, bool borrow) {
   Lap lap;
-  out.text.assign(text_in.data(), text_in.size());
+  std::string_view text = text_in;
+  if (!borrow) {
+    out.text.assign(text_in.data(), text_in.size());
+    text = out.text;
+  }
   lap("copy");
-  Reader R{out.text.data(), out.text.size(), 0, out, {}, 0};
+  Reader R{text.data(), text.size(), 0, out, {}, 0};
   Pools pools;
+  pools.props.reserve(text.size() / 128 + 16);
+  pools.quals.reserve(text.size() / 256 + 16);
   Strs S{out, pools};
   std::vector<Comp> comps;
+  comps.reserve(text.size() / 256 + 16);  // a component is a few hundred bytes of JSON
   Comp root;
   bool has_root = false;
   std::vector<Dep> deps;
@@ -618,20 +692,17 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
   }
   lap("purls");
   // bom-ref -> component (a later one with the same ref replaces an earlier one)
-  std::unordered_map<std::string_view, Comp*> by_ref;
-  by_ref.reserve(order.size() * 2);
-  for (Comp* c : order) by_ref[c->bom_ref] = c;
+  RefMap by_ref(order.size());
+  for (Comp* c : order) by_ref.put(c->bom_ref, c);
   std::unordered_map<const Comp*, std::vector<Comp*>> rels;
   for (const Dep& d : deps) {
     if (!d.has_ref) continue;
-    auto it = by_ref.find(d.ref);
-    if (it == by_ref.end()) continue;
-    std::vector<Comp*>& v = rels[it->second];
+    Comp* parent = by_ref.get(d.ref);
+    if (!parent) continue;
+    std::vector<Comp*>& v = rels[parent];
     v.clear();
-    for (std::string_view x : d.on) {
-      auto jt = by_ref.find(x);
-      if (jt != by_ref.end()) v.push_back(jt->second);
-    }
+    for (std::string_view x : d.on)
+      if (Comp* child = by_ref.get(x)) v.push_back(child);
   }
 
   lap("refs");
@@ -647,6 +718,8 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
   auto comp_index = [&](const Comp* c) { return c == &root ? comps.size() : size_t(c - comps.data()); };
   std::vector<SbomPkg> pkgs;
   std::vector<const Comp*> pkg_comp;
+  pkgs.reserve(order.size());
+  pkg_comp.reserve(order.size());
   std::vector<uint8_t> taken;
   static const std::string_view kAggregating[] = {"python-pkg", "conda-pkg", "gemspec", "node-pkg", "jar"};
   for (const Comp* c : order) {
@@ -780,29 +853,30 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
   }
   lap("libraries");
   taken.assign(pkgs.size(), 0);
-  auto take = [&](const Comp* d, std::vector<SbomPkg>& dst) {
+  // targets as index lists into pkgs: the OS packages, then every application
+  std::vector<std::vector<uint32_t>> tidx(1);
+  std::vector<std::pair<std::string_view, std::string_view>> tmeta(1);
+  auto take = [&](const Comp* d, std::vector<uint32_t>& dst) {
     const int64_t k = pkg_of[comp_index(d)];
     if (k < 0 || taken[size_t(k)]) return;
     taken[size_t(k)] = 1;
-    dst.push_back(pkgs[size_t(k)]);
+    dst.push_back(uint32_t(k));
   };
   if (os_c) {
     auto it = rels.find(os_c);
     if (it != rels.end())
-      for (const Comp* d : it->second) take(d, out.packages);
+      for (const Comp* d : it->second) take(d, tidx[0]);
   }
   for (const App& a : apps) {
-    SbomApp app;
-    app.type = a.type;
-    app.file_path = a.file_path;
+    tidx.emplace_back();
+    tmeta.emplace_back(a.type, a.file_path);
     auto it = rels.find(a.c);
     if (it != rels.end())
-      for (const Comp* d : it->second) take(d, app.libs);
-    out.apps.push_back(std::move(app));
+      for (const Comp* d : it->second) take(d, tidx.back());
   }
   // the rest: OS packages of one PURL type, one application per language type
   std::vector<std::string_view> os_types, lang_types;
-  std::vector<std::vector<SbomPkg>> os_rest, lang_rest;
+  std::vector<std::vector<uint32_t>> os_rest, lang_rest;
   for (size_t k = 0; k < pkgs.size(); k++) {
     if (taken[k]) continue;
     const Purl& p = pkg_comp[k]->purl;
@@ -815,40 +889,47 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
       types.push_back(key);
       groups.emplace_back();
     }
-    groups[g].push_back(pkgs[k]);
+    groups[g].push_back(uint32_t(k));
   }
   if (os_rest.size() > 1) {
     err = "failed to aggregate packages: multiple types of OS packages in SBOM are not supported";
     return false;
   }
-  auto by_name = [](const SbomPkg& a, const SbomPkg& b) {  // Packages.Less (artifact.go:203-211), byte order
+  auto by_name = [&](uint32_t x, uint32_t y) {  // Packages.Less (artifact.go:203-211), byte order
+    const SbomPkg &a = pkgs[x], &b = pkgs[y];
     if (a.name != b.name) return a.name < b.name;
     if (a.version != b.version) return a.version < b.version;
     return a.file_path < b.file_path;
   };
   if (!os_rest.empty() && out.has_os && !out.os_family.empty()) {
     std::stable_sort(os_rest[0].begin(), os_rest[0].end(), by_name);
-    out.packages.insert(out.packages.end(), os_rest[0].begin(), os_rest[0].end());
+    tidx[0].insert(tidx[0].end(), os_rest[0].begin(), os_rest[0].end());
   }
   for (size_t g = 0; g < lang_rest.size(); g++) {
     std::stable_sort(lang_rest[g].begin(), lang_rest[g].end(), by_name);
-    SbomApp app;
-    app.type = lang_types[g];
-    app.libs = std::move(lang_rest[g]);
-    out.apps.push_back(std::move(app));
+    tidx.push_back(std::move(lang_rest[g]));
+    tmeta.emplace_back(lang_types[g], std::string_view());
   }
-  std::stable_sort(out.apps.begin(), out.apps.end(), [](const SbomApp& a, const SbomApp& b) {
-    if (a.type != b.type) return a.type < b.type;
-    return a.file_path < b.file_path;
+  // applications ordered by (Type, FilePath), stable
+  std::vector<size_t> order_apps(tidx.size() - 1);
+  for (size_t a = 0; a < order_apps.size(); a++) order_apps[a] = a + 1;
+  std::stable_sort(order_apps.begin(), order_apps.end(), [&](size_t x, size_t y) {
+    if (tmeta[x].first != tmeta[y].first) return tmeta[x].first < tmeta[y].first;
+    return tmeta[x].second < tmeta[y].second;
   });
   lap("assemble");
-  // detector input views
+  // detector input: every target's packages contiguous (tvm_package + the extra fields)
+  size_t total = tidx[0].size();
+  for (size_t a : order_apps) total += tidx[a].size();
+  out.view.reserve(total);
+  out.extra.reserve(total);
   auto ts = [](std::string_view v) { return tvm_str{v.data(), v.size()}; };
-  auto view = [&](const std::vector<SbomPkg>& src, std::vector<tvm_package>& dst) {
-    dst.resize(src.size());
-    for (size_t k = 0; k < src.size(); k++) {
-      const SbomPkg& p = src[k];
-      tvm_package& q = dst[k];
+  size_t at = 0;
+  auto emit = [&](const std::vector<uint32_t>& idx, std::string_view type, std::string_view fp) {
+    out.targets.push_back(SbomTarget{type, fp, at, at + idx.size()});
+    for (uint32_t k : idx) {
+      const SbomPkg& p = pkgs[k];
+      tvm_package q;
       std::memset(&q, 0, sizeof q);
       q.id = ts(p.id);
       q.name = ts(p.name);
@@ -862,10 +943,13 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err) {
       q.src_epoch = p.src_epoch;
       q.modularitylabel = ts(p.modularitylabel);
       q.file_path = ts(p.file_path);
+      out.view.push_back(q);
+      out.extra.push_back(SbomExtra{p.purl, p.bom_ref, p.layer_digest, p.layer_diff_id, p.present});
+      at++;
     }
   };
-  view(out.packages, out.view);
-  for (SbomApp& a : out.apps) view(a.libs, a.view);
+  emit(tidx[0], {}, {});
+  for (size_t a : order_apps) emit(tidx[a], tmeta[a].first, tmeta[a].second);
   lap("views");
   return true;
 }

@@ -32,27 +32,31 @@ enum : uint32_t {
   SP_SRCVERSION = 64, SP_SRCRELEASE = 128, SP_SRCEPOCH = 256, SP_LAYER_DIGEST = 512, SP_LAYER_DIFFID = 1024,
 };
 
-struct SbomPkg {
+struct SbomPkg {  // a decoded library (decodeLibrary) before it is placed in its target
   std::string_view id, name, version, release, arch, src_name, src_version, src_release, modularitylabel, file_path;
   std::string_view purl, bom_ref, layer_digest, layer_diff_id;
   int64_t epoch = 0, src_epoch = 0;
   uint32_t present = 0;  // SP_*
 };
 
-struct SbomApp {
+struct SbomExtra {  // the fields of a package beyond tvm_package
+  std::string_view purl, bom_ref, layer_digest, layer_diff_id;
+  uint32_t present = 0;  // SP_*
+};
+
+struct SbomTarget {  // target 0: the OS packages; then the applications, sorted
   std::string_view type, file_path;
-  std::vector<SbomPkg> libs;
-  std::vector<tvm_package> view;  // libs as detector input
+  size_t begin = 0, end = 0;  // its packages: view / extra [begin, end)
 };
 
 struct Sbom {
   bool has_os = false;
   std::string_view os_family, os_name, serial;
   int64_t version = 0;
-  std::vector<SbomPkg> packages;  // OS packages
-  std::vector<tvm_package> view;
-  std::vector<SbomApp> apps;
-  std::string text;  // the document (the views point into it)
+  std::vector<tvm_package> view;  // detector input, target after target
+  std::vector<SbomExtra> extra;
+  std::vector<SbomTarget> targets;
+  std::string text;  // the document when it is copied (the views point into it or the caller's)
   // strings built by the decode (unescaped, joined): a bump arena of chunks that never move
   std::vector<std::unique_ptr<char[]>> chunks;
   size_t chunk_left = 0;
@@ -63,6 +67,7 @@ struct Sbom {
 // false: err holds the reference's message ("failed to decode CycloneDX JSON: ...",
 // "failed to parse root component: ...", "failed to decode components: ...",
 // "failed to aggregate packages: ...").
-bool decode_cyclonedx(std::string_view text, Sbom& out, std::string& err);
+// borrow: the views point into `text` itself, which must then outlive `out`; else it is copied.
+bool decode_cyclonedx(std::string_view text, Sbom& out, std::string& err, bool borrow = false);
 
 }  // namespace tvm

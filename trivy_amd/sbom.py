@@ -313,9 +313,10 @@ class NativeSBOM:
         from ._lib import lib, errbuf
         data = text.encode() if isinstance(text, str) else bytes(text)
         h, e = ctypes.c_void_p(), errbuf()
-        if lib().tvm_sbom_decode_cyclonedx(data, len(data), ctypes.byref(h), e, len(e)):
+        # TVM_SBOM_BORROW: the decode points into `data`, which this object keeps alive
+        if lib().tvm_sbom_decode_cyclonedx(data, len(data), 1, ctypes.byref(h), e, len(e)):
             raise SBOMError(e.value.decode())
-        self.h = h
+        self.h, self._data = h, data
         from ._lib import RawStr
         has_os, fam, name, serial = ctypes.c_int32(), RawStr(), RawStr(), RawStr()
         ver, napps = ctypes.c_int64(), ctypes.c_size_t()
