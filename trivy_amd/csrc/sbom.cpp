@@ -1,12 +1,16 @@
 // Native CycloneDX decoder (sbom.h).
 #include "sbom.h"
 
+#include "host_par.h"
+
 #include <algorithm>
 #include <cstring>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <unordered_map>
+
+#include <sys/mman.h>
 
 namespace tvm {
 
@@ -19,7 +23,7 @@ constexpr std::string_view kNamespace = "aquasecurity:trivy:";
 struct Reader {
   const char* s;
   size_t n, i = 0;
-  Sbom& owned;
+  Arena& owned;
   std::string err;
   int depth = 0;
 
@@ -256,17 +260,21 @@ using KV = std::pair<std::string_view, std::string_view>;
 
 struct Purl {
   std::string_view type, ns, name, version, subpath;
-  uint32_t q0 = 0, nq = 0;  // qualifiers (lower-cased key, value), in order: Pools::quals[q0, q0 + nq)
+  uint32_t q0 = 0, nq = 0;  // qualifiers (lower-cased key, value), in order: Pools::quals[qt][q0, q0 + nq)
+  uint32_t qt = 0;
 };
 
-// Shared storage of every component's properties and qualifiers (no vector per component).
+// Shared storage of every component's properties (the parse) and qualifiers (one vector per
+// parallel piece of the PURL pass): no vector per component.
 struct Pools {
-  std::vector<KV> props, quals;
+  HugeVec<KV> props;
+  std::vector<std::vector<KV>> quals;
 };
 
 struct Strs {
-  Sbom& owned;
-  Pools& pools;
+  Arena& owned;
+  std::vector<KV>& quals;
+  uint32_t qt;
   std::string_view keep(const std::string& x) { return owned.keep(x); }
   // urllib.parse.unquote: %XX decoded, malformed escapes kept
   std::string_view unq(std::string_view x) {
@@ -310,7 +318,8 @@ const char* parse_purl(std::string_view s, Strs& S, Purl& p) {
   std::string_view rest = s.substr(4);
   while (!rest.empty() && rest.front() == '/') rest.remove_prefix(1);
   p = Purl{};
-  p.q0 = uint32_t(S.pools.quals.size());
+  p.qt = S.qt;
+  p.q0 = uint32_t(S.quals.size());
   if (const size_t h = rest.find('#'); h != std::string_view::npos) {
     const std::string_view sp = strip(rest.substr(h + 1), '/');
     rest = rest.substr(0, h);
@@ -339,7 +348,7 @@ const char* parse_purl(std::string_view s, Strs& S, Purl& p) {
       const size_t e = kv.find('=');
       const std::string_view k = kv.substr(0, e), v = e == std::string_view::npos ? std::string_view() : kv.substr(e + 1);
       if (!kv.empty() && !v.empty()) {
-        S.pools.quals.emplace_back(S.lower(k), S.unq(v));
+        S.quals.emplace_back(S.lower(k), S.unq(v));
         p.nq++;
       }
       a = b + 1;
@@ -479,11 +488,11 @@ class RefMap {
   explicit RefMap(size_t n) {
     size_t cap = 16;
     while (cap < 2 * n + 2) cap <<= 1;
-    e_.assign(cap, E{0, nullptr});
+    e_.assign(cap, E{0, nullptr});  // (HugeVec)
     mask_ = cap - 1;
   }
-  void put(std::string_view k, Comp* c) {
-    const uint64_t h = hash(k);
+  void put(std::string_view k, Comp* c) { put(k, c, hash(k)); }
+  void put(std::string_view k, Comp* c, uint64_t h) {
     for (size_t i = h & mask_;; i = (i + 1) & mask_) {
       if (!e_[i].c) {
         e_[i] = E{h, c};
@@ -508,8 +517,10 @@ class RefMap {
     uint64_t h;
     Comp* c;
   };
-  std::vector<E> e_;
+  HugeVec<E> e_;
   size_t mask_ = 0;
+
+ public:
   static uint64_t hash(std::string_view k) {
     uint64_t h = 1469598103934665603ull ^ k.size();
     size_t i = 0;
@@ -533,21 +544,49 @@ struct Dep {
 
 }  // namespace
 
-std::string_view Sbom::keep(std::string_view a, std::string_view b, std::string_view c) {
+void* huge_alloc(size_t bytes) {
+  constexpr size_t kHuge = size_t(2) << 20;
+  if (bytes < kHuge) {
+    void* p = std::malloc(std::max<size_t>(bytes, 1));
+    if (!p) throw std::bad_alloc();
+    return p;
+  }
+  const size_t len = (bytes + kHuge - 1) & ~(kHuge - 1);
+  void* p = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) throw std::bad_alloc();
+  (void)madvise(p, len, MADV_HUGEPAGE);
+  return p;
+}
+
+void huge_free(void* p, size_t bytes) {
+  constexpr size_t kHuge = size_t(2) << 20;
+  if (!p) return;
+  if (bytes < kHuge) {
+    std::free(p);
+    return;
+  }
+  munmap(p, (bytes + kHuge - 1) & ~(kHuge - 1));
+}
+
+Arena::~Arena() {
+  for (const Chunk& c : chunks) huge_free(c.p, c.n);
+}
+
+std::string_view Arena::keep(std::string_view a, std::string_view b, std::string_view c) {
   const size_t n = a.size() + b.size() + c.size();
   if (n == 0) return {};
-  if (n > chunk_left) {
-    const size_t sz = std::max<size_t>(n, size_t(1) << 20);
-    chunks.emplace_back(new char[sz]);
-    chunk_at = chunks.back().get();
-    chunk_left = sz;
+  if (n > left) {
+    const size_t sz = std::max<size_t>(n, size_t(2) << 20);
+    chunks.push_back(Chunk{static_cast<char*>(huge_alloc(sz)), sz});
+    at = chunks.back().p;
+    left = sz;
   }
-  char* d = chunk_at;
+  char* d = at;
   std::memcpy(d, a.data(), a.size());
   if (!b.empty()) std::memcpy(d + a.size(), b.data(), b.size());
   if (!c.empty()) std::memcpy(d + a.size() + b.size(), c.data(), c.size());
-  chunk_at += n;
-  chunk_left -= n;
+  at += n;
+  left -= n;
   return std::string_view(d, n);
 }
 
@@ -573,12 +612,10 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err, boo
     text = out.text;
   }
   lap("copy");
-  Reader R{text.data(), text.size(), 0, out, {}, 0};
+  Reader R{text.data(), text.size(), 0, out.arena(0), {}, 0};
   Pools pools;
   pools.props.reserve(text.size() / 128 + 16);
-  pools.quals.reserve(text.size() / 256 + 16);
-  Strs S{out, pools};
-  std::vector<Comp> comps;
+  HugeVec<Comp> comps;
   comps.reserve(text.size() / 256 + 16);  // a component is a few hundred bytes of JSON
   Comp root;
   bool has_root = false;
@@ -666,22 +703,36 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err, boo
   lap("parse");
 
   // parseComponents: unsupported types dropped, a component whose PURL does not parse skipped
+  // (the PURLs in parallel pieces, each with its own arena and qualifier vector)
+  const int T = host_threads();
+  const size_t pieces = std::max<size_t>(1, std::min<size_t>(size_t(T) * 4, comps.size() / 4096));
+  pools.quals.resize(pieces + 1);
+  std::vector<uint8_t> keep_comp(comps.size(), 0);
+  for (size_t k = 0; k <= pieces; k++) out.arena(k + 1);
+  dynamic_for(T, pieces, [&](size_t k) {
+    Strs S{*out.arenas[k + 1], pools.quals[k], uint32_t(k)};
+    const size_t a = comps.size() * k / pieces, b = comps.size() * (k + 1) / pieces;
+    for (size_t i = a; i < b; i++) {
+      Comp& c = comps[i];
+      if (comp_type(c.type) == CT_OTHER) continue;
+      if (!c.purl_str.empty()) {
+        if (parse_purl(c.purl_str, S, c.purl)) continue;  // parseComponents logs and skips it
+        c.has_purl = true;
+      }
+      keep_comp[i] = 1;
+    }
+  });
   std::vector<Comp*> order;
   order.reserve(comps.size() + 1);
-  for (Comp& c : comps) {
-    if (comp_type(c.type) == CT_OTHER) continue;
-    if (!c.purl_str.empty()) {
-      if (parse_purl(c.purl_str, S, c.purl)) continue;  // parseComponents logs and skips it
-      c.has_purl = true;
-    }
-    order.push_back(&c);
-  }
+  for (size_t i = 0; i < comps.size(); i++)
+    if (keep_comp[i]) order.push_back(&comps[i]);
   if (has_root) {
     if (comp_type(root.type) == CT_OTHER) {
       err = "failed to parse root component: unsupported component type";
       return false;
     }
     if (!root.purl_str.empty()) {
+      Strs S{*out.arenas[pieces + 1], pools.quals[pieces], uint32_t(pieces)};
       if (const char* e = parse_purl(root.purl_str, S, root.purl)) {
         err = e;
         return false;
@@ -693,16 +744,26 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err, boo
   lap("purls");
   // bom-ref -> component (a later one with the same ref replaces an earlier one)
   RefMap by_ref(order.size());
-  for (Comp* c : order) by_ref.put(c->bom_ref, c);
+  {
+    std::vector<uint64_t> h(order.size());
+    range_for(order.size(), 8192, [&](size_t a, size_t b) {
+      for (size_t i = a; i < b; i++) h[i] = RefMap::hash(order[i]->bom_ref);
+    });
+    for (size_t i = 0; i < order.size(); i++) by_ref.put(order[i]->bom_ref, order[i], h[i]);
+  }
   std::unordered_map<const Comp*, std::vector<Comp*>> rels;
   for (const Dep& d : deps) {
     if (!d.has_ref) continue;
     Comp* parent = by_ref.get(d.ref);
     if (!parent) continue;
     std::vector<Comp*>& v = rels[parent];
+    std::vector<Comp*> found(d.on.size());
+    range_for(d.on.size(), 8192, [&](size_t a, size_t b) {
+      for (size_t i = a; i < b; i++) found[i] = by_ref.get(d.on[i]);
+    });
     v.clear();
-    for (std::string_view x : d.on)
-      if (Comp* child = by_ref.get(x)) v.push_back(child);
+    for (Comp* child : found)
+      if (child) v.push_back(child);
   }
 
   lap("refs");
@@ -716,18 +777,19 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err, boo
   // component (index in comps, root last) -> its package in pkgs, -1 for none
   std::vector<int64_t> pkg_of(comps.size() + 1, -1);
   auto comp_index = [&](const Comp* c) { return c == &root ? comps.size() : size_t(c - comps.data()); };
-  std::vector<SbomPkg> pkgs;
-  std::vector<const Comp*> pkg_comp;
-  pkgs.reserve(order.size());
-  pkg_comp.reserve(order.size());
-  std::vector<uint8_t> taken;
+  // pass A (in order): the OS, the applications, the library candidates; the first error in
+  // component order is the one the reference reports
   static const std::string_view kAggregating[] = {"python-pkg", "conda-pkg", "gemspec", "node-pkg", "jar"};
-  for (const Comp* c : order) {
+  std::vector<uint32_t> cand;  // positions in `order` of the components decodeLibrary reads
+  cand.reserve(order.size());
+  size_t os_err_at = order.size();
+  for (size_t oi = 0; oi < order.size(); oi++) {
+    const Comp* c = order[oi];
     const CompType ct = comp_type(c->type);
     if (ct == CT_OS) {
       if (os_c) {
-        err = "failed to decode components: multiple OS components are not supported";
-        return false;
+        os_err_at = oi;
+        break;
       }
       os_c = c;
       out.has_os = true;
@@ -750,19 +812,19 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err, boo
         continue;
       }
     }
-    // decodeLibrary
-    if (!c->has_purl) continue;
+    if (c->has_purl && purl_class(c->purl)) cand.push_back(uint32_t(oi));
+  }
+  // decodeLibrary of one component; false: its SrcEpoch property is not an integer
+  auto decode_lib = [&](const Comp* c, Strs& S, SbomPkg& k) -> bool {
     const Purl& p = c->purl;
     const int cls = purl_class(p);
-    if (!cls) continue;
-    SbomPkg k;
     const bool maven = p.type == "maven" || p.type == "gradle";
     k.name = p.name;
     if (!p.ns.empty() && cls != 1) k.name = S.join(p.ns, maven ? ":" : "/", p.name);
     if (!p.subpath.empty() && p.type == "cocoapods") k.name = S.join(p.name, "/", p.subpath);
     k.version = p.version;
     for (uint32_t q = p.q0; q < p.q0 + p.nq; q++) {
-      const auto& [qk, qv] = pools.quals[q];
+      const auto& [qk, qv] = pools.quals[p.qt][q];
       if (qk == "arch") {
         k.arch = qv;
         k.present |= SP_ARCH;
@@ -796,7 +858,7 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err, boo
       } else if (lt == "conan") {
         k.id = S.join(k.name, "/", p.version);
       } else if ((lt == "gomod" || lt == "gobinary") && p.version.front() != 'v') {
-        k.id = out.keep(k.name, "@v", p.version);
+        k.id = S.owned.keep(k.name, "@v", p.version);
       } else if (lt == "jar" || lt == "pom" || lt == "gradle") {
         k.id = S.join(k.name, ":", p.version);
       } else {
@@ -824,10 +886,7 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err, boo
         k.present |= SP_MODULARITY;
       } else if (pk == "SrcEpoch") {
         int64_t e;
-        if (!py_int(pv, e)) {
-          err = "failed to decode components: failed to decode library: invalid src epoch";
-          return false;
-        }
+        if (!py_int(pv, e)) return false;  // "invalid src epoch"
         k.src_epoch = e;
         k.present |= SP_SRCEPOCH;
       } else if (pk == "LayerDigest") {
@@ -847,11 +906,37 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err, boo
       if (k.src_epoch == 0) k.src_epoch = k.epoch;
       k.present |= SP_SRCNAME | SP_SRCVERSION | SP_SRCRELEASE | SP_SRCEPOCH;
     }
-    pkg_of[comp_index(c)] = int64_t(pkgs.size());
-    pkgs.push_back(k);
-    pkg_comp.push_back(c);
+    return true;
+  };
+  // pass B (parallel pieces, each with its own arena): the libraries
+  HugeVec<SbomPkg> pkgs(cand.size());
+  std::vector<uint8_t> bad(cand.size(), 0);
+  {
+    const size_t lp = std::max<size_t>(1, std::min<size_t>(size_t(T) * 4, cand.size() / 4096));
+    const size_t a0 = out.arenas.size();
+    for (size_t k = 0; k < lp; k++) out.arena(a0 + k);
+    dynamic_for(T, lp, [&](size_t k) {
+      std::vector<KV> unused;
+      Strs S{*out.arenas[a0 + k], unused, 0};
+      const size_t a = cand.size() * k / lp, b = cand.size() * (k + 1) / lp;
+      for (size_t j = a; j < b; j++) bad[j] = decode_lib(order[cand[j]], S, pkgs[j]) ? 0 : 1;
+    });
   }
-  lap("libraries");
+  for (size_t j = 0; j < cand.size() && cand[j] < os_err_at; j++)
+    if (bad[j]) {
+      err = "failed to decode components: failed to decode library: invalid src epoch";
+      return false;
+    }
+  if (os_err_at < order.size()) {
+    err = "failed to decode components: multiple OS components are not supported";
+    return false;
+  }
+  std::vector<const Comp*> pkg_comp(cand.size());
+  for (size_t j = 0; j < cand.size(); j++) {
+    pkg_comp[j] = order[cand[j]];
+    pkg_of[comp_index(pkg_comp[j])] = int64_t(j);
+  }
+  std::vector<uint8_t> taken;
   taken.assign(pkgs.size(), 0);
   // targets as index lists into pkgs: the OS packages, then every application
   std::vector<std::vector<uint32_t>> tidx(1);
@@ -918,18 +1003,28 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err, boo
     return tmeta[x].second < tmeta[y].second;
   });
   lap("assemble");
-  // detector input: every target's packages contiguous (tvm_package + the extra fields)
-  size_t total = tidx[0].size();
-  for (size_t a : order_apps) total += tidx[a].size();
-  out.view.reserve(total);
-  out.extra.reserve(total);
+  // detector input: every target's packages contiguous (tvm_package + the extra fields),
+  // filled in parallel pieces
+  std::vector<uint32_t> flat;
+  {
+    size_t total = tidx[0].size();
+    for (size_t a : order_apps) total += tidx[a].size();
+    flat.reserve(total);
+  }
+  auto place = [&](const std::vector<uint32_t>& idx, std::string_view type, std::string_view fp) {
+    out.targets.push_back(SbomTarget{type, fp, flat.size(), flat.size() + idx.size()});
+    flat.insert(flat.end(), idx.begin(), idx.end());
+  };
+  place(tidx[0], {}, {});
+  for (size_t a : order_apps) place(tidx[a], tmeta[a].first, tmeta[a].second);
+  out.n_view = flat.size();
+  out.view.resize(flat.size());
+  out.extra.resize(flat.size());
   auto ts = [](std::string_view v) { return tvm_str{v.data(), v.size()}; };
-  size_t at = 0;
-  auto emit = [&](const std::vector<uint32_t>& idx, std::string_view type, std::string_view fp) {
-    out.targets.push_back(SbomTarget{type, fp, at, at + idx.size()});
-    for (uint32_t k : idx) {
-      const SbomPkg& p = pkgs[k];
-      tvm_package q;
+  range_for(flat.size(), 16384, [&](size_t a, size_t b) {
+    for (size_t at = a; at < b; at++) {
+      const SbomPkg& p = pkgs[flat[at]];
+      tvm_package& q = out.view[at];
       std::memset(&q, 0, sizeof q);
       q.id = ts(p.id);
       q.name = ts(p.name);
@@ -943,13 +1038,9 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err, boo
       q.src_epoch = p.src_epoch;
       q.modularitylabel = ts(p.modularitylabel);
       q.file_path = ts(p.file_path);
-      out.view.push_back(q);
-      out.extra.push_back(SbomExtra{p.purl, p.bom_ref, p.layer_digest, p.layer_diff_id, p.present});
-      at++;
+      out.extra[at] = SbomExtra{p.purl, p.bom_ref, p.layer_digest, p.layer_diff_id, p.present};
     }
-  };
-  emit(tidx[0], {}, {});
-  for (size_t a : order_apps) emit(tidx[a], tmeta[a].first, tmeta[a].second);
+  });
   lap("views");
   return true;
 }

@@ -49,19 +49,55 @@ struct SbomTarget {  // target 0: the OS packages; then the applications, sorted
   size_t begin = 0, end = 0;  // its packages: view / extra [begin, end)
 };
 
+// Large decode arrays come from anonymous mappings advised for transparent huge pages: a 1M-
+// component document touches ~1 GB of fresh memory, and at 4 KB pages the page faults alone
+// cost as much as the parse (measured: tools/sbom_rate.py, TVM_SBOM_TRACE=1).
+void* huge_alloc(size_t bytes);
+void huge_free(void* p, size_t bytes);
+
+template <class T>
+struct HugeAlloc {
+  using value_type = T;
+  HugeAlloc() = default;
+  template <class U>
+  HugeAlloc(const HugeAlloc<U>&) {}
+  T* allocate(size_t n) { return static_cast<T*>(huge_alloc(n * sizeof(T))); }
+  void deallocate(T* p, size_t n) { huge_free(p, n * sizeof(T)); }
+  template <class U>
+  bool operator==(const HugeAlloc<U>&) const { return true; }
+  template <class U>
+  bool operator!=(const HugeAlloc<U>&) const { return false; }
+};
+template <class T>
+using HugeVec = std::vector<T, HugeAlloc<T>>;
+
+// Strings built by the decode (unescaped, joined): a bump arena of chunks that never move.
+struct Arena {
+  struct Chunk {
+    char* p;
+    size_t n;
+  };
+  std::vector<Chunk> chunks;
+  size_t left = 0;
+  char* at = nullptr;
+  std::string_view keep(std::string_view a, std::string_view b = {}, std::string_view c = {});
+  ~Arena();
+};
+
 struct Sbom {
   bool has_os = false;
   std::string_view os_family, os_name, serial;
   int64_t version = 0;
-  std::vector<tvm_package> view;  // detector input, target after target
-  std::vector<SbomExtra> extra;
+  HugeVec<tvm_package> view;  // detector input, target after target
+  HugeVec<SbomExtra> extra;
+  size_t n_view = 0;
   std::vector<SbomTarget> targets;
   std::string text;  // the document when it is copied (the views point into it or the caller's)
-  // strings built by the decode (unescaped, joined): a bump arena of chunks that never move
-  std::vector<std::unique_ptr<char[]>> chunks;
-  size_t chunk_left = 0;
-  char* chunk_at = nullptr;
-  std::string_view keep(std::string_view a, std::string_view b = {}, std::string_view c = {});
+  std::vector<std::unique_ptr<Arena>> arenas;  // [0]: the parse; then one per parallel piece
+  Arena& arena(size_t k) {
+    while (arenas.size() <= k) arenas.emplace_back(new Arena());
+    return *arenas[k];
+  }
 };
 
 // false: err holds the reference's message ("failed to decode CycloneDX JSON: ...",
