@@ -9,13 +9,14 @@ unfixed).  The pinned trivy-db cannot be fetched offline, hence synthetic data
 (tools/synth.py).  --config c3 / c4 / c5: the language-package, mixed OS+language and
 RHEL-family/Alpine workloads (tools/synth_mix.py) - extra measurements, not the headline.
 
-One step = one pass of the hot path over ONE global batch resident in HBM: the match
-kernels (probe + interval sweep), and with N > 1 GPUs the order kernel on every rank (its
-shard's per-package advisory lists, CSR) and the exact-size gather of those lists to rank 0
-over RCCL (4 B per match + 4 B per package), where they land in global batch order.  The batch is sharded into
-contiguous shards on target boundaries, balanced by predicted advisory rows (host
-pre-probe); the tables are replicated per GPU.  Strong scaling: the global batch is the
-same at every N; value = global packages x steps / max-over-ranks wall time.
+One step = one pass of the hot path over a batch resident in HBM: the match kernels (probe +
+interval sweep).  With N > 1 GPUs (one process per GPU; `python bench.py --gpus N` starts the N
+ranks itself) every rank matches its own batch of the config against its replica of the
+tables: packages are independent, so the step has no collective (weak scaling, value = N x
+packages x steps / max-over-ranks wall time).  --gather instead cuts ONE global batch into
+contiguous shards on target boundaries (balanced by predicted advisory rows) and adds the
+per-rank order kernel (per-package lists, CSR) and the exact-size gather of those lists to rank
+0 over RCCL to the step (strong scaling).
 
 Also reported (rank 0): roofline of the match kernels (algorithmic bytes per launch / HIP
 event time, vs the 8 TB/s HBM peak), the end-to-end pipelined pass over PCIe
@@ -309,6 +310,10 @@ def main():
     ap.add_argument("--variant", type=int, default=None, help="match-path variant (tvm_engine_set_variant)")
     ap.add_argument("--sweep", type=int, default=0,
                     help="time every match-path variant over N interleaved rounds (stderr table) first")
+    ap.add_argument("--gather", action="store_true",
+                    help="strong scaling: ONE global batch sharded across the ranks on target boundaries, each "
+                         "rank's per-package lists gathered to rank 0 over RCCL inside the timed step (default: "
+                         "weak scaling, every rank matches its own batch of the config, no collective in the step)")
     ap.add_argument("--dump-csr", default=None,
                     help="rank 0 writes the whole batch's per-package advisory lists (CSR, as gathered) to this "
                          ".npz after the timed region (checked against the oracle by tests/test_gpu_bench_dist.py)")
@@ -352,8 +357,14 @@ def main():
 
     # ---- this rank's shard of the global batch ----------------------------------------------
     t0 = time.perf_counter()
+    # weak scaling (default): every rank matches a whole batch of the config - packages are
+    # independent and the tables are replicated, so the step needs no collective (SURVEY.md
+    # §8e); --gather: strong scaling over one global batch + the CSR gather to rank 0
     rows = wl.rows(db)
-    bounds = td.target_shards(wl.targets(), wl.n, rows.astype(np.float64) + 1.0, world)
+    if args.gather:
+        bounds = td.target_shards(wl.targets(), wl.n, rows.astype(np.float64) + 1.0, world)
+    else:
+        bounds = [0] * (rank + 1) + [wl.n] * (world - rank)
     sb, se = bounds[rank], bounds[rank + 1]
     mb = MatchBatch(eng)
     wl.fill(mb, sb, se)
@@ -364,7 +375,7 @@ def main():
     if bits or errp != -1:
         raise RuntimeError(f"engine error bits={bits} poisoned_pkg={errp}")
     gather, csr = None, None
-    if world > 1:  # the order kernel writes this rank's per-package lists (CSR) into the tensors the gather sends
+    if world > 1 and args.gather:  # the order kernel writes this rank's per-package lists (CSR) into the tensors the gather sends
         csr = (torch.empty(max(total, 1), dtype=torch.int32, device=gdev),
                torch.empty(max(n_local, 1), dtype=torch.int32, device=gdev))
         gather = td.CSRGather(cdev)
@@ -408,7 +419,8 @@ def main():
     wall = td.timed(step, steps=args.steps, warmup=args.warmup, sync=sync, device=cdev)
     if mb.status() != (total, -1, 0):
         raise RuntimeError("timed passes disagree with the first pass")
-    value = wl.n * args.steps / wall
+    n_job = wl.n * (1 if args.gather else world)  # packages all ranks match per step
+    value = n_job * args.steps / wall
     vname = lib().tvm_variant_name(lib().tvm_engine_last_variant(eng.h)).decode()
 
     # kernel-only time of this rank's pass (HIP events on the engine stream) for the roofline
@@ -597,10 +609,14 @@ def main():
     src_hash = kernel_source_hash()
     traffic, traffic_src = pmc_traffic(args.config, wl.name, vname, src_hash)
     if rank == 0:
-        par = f"tables replicated, one global batch sharded x{world} on target boundaries by predicted rows"
-        if world > 1:
-            par += (", per-rank order kernel (per-package lists, CSR) + exact-size CSR gather to rank 0 in "
-                    "global batch order inside the timed step")
+        if args.gather:
+            par = f"dp{world}: tables replicated, one global batch sharded x{world} on target boundaries by predicted rows"
+            if world > 1:
+                par += (", per-rank order kernel (per-package lists, CSR) + exact-size CSR gather to rank 0 in "
+                        "global batch order inside the timed step")
+        else:
+            par = (f"dp{world}: tables replicated, every rank matches its own {wl.n}-package batch of the config "
+                   "(packages are independent: no collective in the step)")
         line = {
             "metric": "packages matched/sec (node)",
             "value": value,
@@ -610,11 +626,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": wall * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "strong" if args.gather else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded trivy-db + SBOM batch, tools/synth.py / tools/synth_mix.py)",
-            "config": {"workload": wl.name, "packages": wl.n, "packages_rank0": n_local, "matches_rank0": total,
+            "config": {"workload": wl.name, "packages": wl.n, "packages_per_step": n_job, "packages_rank0": n_local,
+                       "matches_rank0": total,
                        "kernel_variant": vname, "kernel_source": src_hash, "db_keys": wl.n_keys, "db_advisories": wl.n_adv,
                        "platforms": wl.plats, "parallelism": par},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

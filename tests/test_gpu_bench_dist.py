@@ -1,8 +1,10 @@
 """GPU: `python bench.py --gpus 2` really runs two ranks (bench.py launches them itself through
-torch.distributed.run when WORLD_SIZE is unset), and the per-package advisory lists its timed
-step gathers at rank 0 equal the oracle's match of the whole global batch (oracle/match.c),
-element for element, in batch order.  Both ranks share the one MI355X of the box, so the
-collectives run over gloo (TVM_BENCH_BACKEND=gloo; RCCL refuses two ranks on one device)."""
+torch.distributed.run when WORLD_SIZE is unset).  Weak scaling (the default): every rank
+matches its own batch of the config and the line counts both; its lists equal the oracle's.
+--gather (strong scaling): the per-package advisory lists the timed step gathers at rank 0
+equal the oracle's match of the whole global batch (oracle/match.c), element for element, in
+batch order.  Both ranks share the one MI355X of the box, so the collectives run over gloo
+(TVM_BENCH_BACKEND=gloo; RCCL refuses two ranks on one device)."""
 import argparse
 import json
 import os
@@ -17,7 +19,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.gpu
 
 
-def test_bench_two_ranks_csr_equals_oracle(tmp_path, oracle_built):
+@pytest.mark.parametrize("gather", [True, False])
+def test_bench_two_ranks_csr_equals_oracle(tmp_path, oracle_built, gather):
     sys.path.insert(0, ROOT)
     import bench
     from oracle import match as om
@@ -26,12 +29,17 @@ def test_bench_two_ranks_csr_equals_oracle(tmp_path, oracle_built):
     env = dict(os.environ, TVM_BENCH_BACKEND="gloo")
     env.pop("WORLD_SIZE", None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
-                        "--no-cpu", "--no-e2e", "--no-fill", "--dump-csr", dump] + flags,
+                        "--no-cpu", "--no-e2e", "--no-fill", "--dump-csr", dump] + flags + (["--gather"] if gather else []),
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["config"]["packages"] == 200 * 400
-    assert line["config"]["packages_rank0"] < line["config"]["packages"]  # rank 0 matched a shard only
+    if gather:  # rank 0 matched a shard only; the step's packages are the global batch
+        assert line["scaling"] == "strong" and line["config"]["packages_rank0"] < line["config"]["packages"]
+        assert line["config"]["packages_per_step"] == 200 * 400
+    else:  # every rank matched the whole batch of the config
+        assert line["scaling"] == "weak" and line["config"]["packages_rank0"] == 200 * 400
+        assert line["config"]["packages_per_step"] == 2 * 200 * 400
     got = np.load(dump)
     assert int(got["n_gpus"]) == 2
     wl = bench.C2(argparse.Namespace(keys_per_plat=3000, targets=200, pkgs_per_target=400))
