@@ -162,6 +162,9 @@ int tvm_engine_verify(tvm_engine* e, char* err, size_t errlen);
  * variant 0 = "auto" (default): the tuned variant for the batch's grammar set. */
 int tvm_engine_set_variant(tvm_engine* e, int v);
 const char* tvm_variant_name(int v);
+/* Batches variant v runs: bit 0 dpkg-only, bit 1 OS grammars (dpkg / apk / rpm), bit 2 any
+ * grammar; a launch of a variant not built for the batch fails with TVM_EDEVICE. */
+int tvm_variant_grammar_sets(int v);
 /* Variant index the engine's most recent launch ran (auto resolved); -1 before any. */
 int tvm_engine_last_variant(tvm_engine* e);
 

@@ -98,7 +98,7 @@ def test_mix_variants_agree(cfg):
     batch = sm.make_mix_batch(sdb, 60_000, weights, seed=23)
     ref = None
     try:
-        for v in variants():
+        for v in variants(grammar_set=4 if cfg in ("c3", "c4") else 2):
             lib().tvm_engine_set_variant(eng.h, v)
             mb = MatchBatch(eng)
             sm.add_to(mb, sdb, batch)

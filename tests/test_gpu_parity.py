@@ -123,12 +123,14 @@ def test_empty_batch(world):
     assert total == 0 and errp == -1
 
 
-def variants():
-    """Indices of the non-ablation match-kernel variants (engine.hip kVariants)."""
+def variants(grammar_set=1):
+    """Indices of the non-ablation match-kernel variants (engine.hip kVariants) built for the
+    grammar set (bit 0 dpkg-only, 1 OS grammars, 2 any)."""
     from trivy_amd._lib import lib
     out, v = [], 0
     while lib().tvm_variant_name(v):
-        if not lib().tvm_variant_name(v).decode().startswith(("ablate", "diag")):
+        if not lib().tvm_variant_name(v).decode().startswith(("ablate", "diag")) and \
+                lib().tvm_variant_grammar_sets(v) & grammar_set:
             out.append(v)
         v += 1
     return out

@@ -130,6 +130,7 @@ _SIG = [
     ("tvm_engine_verify", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_engine_set_variant", ctypes.c_int, [_P, ctypes.c_int]),
     ("tvm_variant_name", ctypes.c_char_p, [ctypes.c_int]),
+    ("tvm_variant_grammar_sets", ctypes.c_int, [ctypes.c_int]),
     ("tvm_engine_last_variant", ctypes.c_int, [_P]),
     ("tvm_ospkg_detect", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(Repository),
                                         ctypes.POINTER(Package), ctypes.c_size_t, ctypes.c_int64,

@@ -382,6 +382,7 @@ int tvm_engine_set_variant(tvm_engine* e, int v) {
 }
 
 const char* tvm_variant_name(int v) { return variant_name(v); }
+int tvm_variant_grammar_sets(int v) { return variant_grammar_sets(v); }
 
 int tvm_engine_last_variant(tvm_engine* e) {
   if (!e) return -1;

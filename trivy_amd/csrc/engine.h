@@ -373,6 +373,7 @@ class Engine {
 // Kernel variants: count and names (engine.hip; 0 = "auto").
 int num_variants();
 const char* variant_name(int v);
+int variant_grammar_sets(int v);  // bit 0 dpkg-only, 1 OS grammars, 2 all grammars
 int resolve_variant(int v, uint32_t gm);
 
 }  // namespace tvm

@@ -117,6 +117,14 @@ const char* variant_name(int v) {
   if (v == 0) return "auto";
   return v > 0 && v < kNumVariants ? kVariantNames[v - 1] : nullptr;
 }
+// Grammar sets variant v is built for: bit 0 dpkg-only, bit 1 OS grammars, bit 2 all grammars.
+int variant_grammar_sets(int v) {
+  if (v == 0) return 7;
+  if (v < 0 || v >= kNumVariants) return 0;
+  if (!kFusedVariant[v - 1]) return 7;
+  return (fused_table_DEB()[v - 1] ? 1 : 0) | (fused_table_OS()[v - 1] ? 2 : 0) | (fused_table_ALL()[v - 1] ? 4 : 0);
+}
+
 // "auto": per grammar set, the fastest variant of bench.py --sweep on MI355X:
 // dpkg-only batches (C2) fused K=4; rpm/apk and mixed batches (C5, C4, C3) fused K=2, whose
 // lower register count keeps 5 waves per SIMD where the filtered K=4 kernel drops to 4.
