@@ -221,8 +221,26 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
   const uint32_t n_tiles = hb.n_tiles();
   const uint32_t chunk_tiles = std::max<uint32_t>(1, (chunk_packages + kTile - 1) / kTile);
   bounds_.clear();
-  for (uint32_t t = 0; t < n_tiles; t += chunk_tiles) bounds_.push_back(t);
-  bounds_.push_back(n_tiles);
+  // A batch of several chunks starts and ends with a quarter chunk: the first match launch
+  // waits for one upload and the last result move runs alone, so short first and last
+  // chunks shorten the pipeline's fill and drain (TVM_PIPE_NORAMP=1: equal chunks)
+  static const bool no_ramp = std::getenv("TVM_PIPE_NORAMP") != nullptr;
+  const uint32_t q = std::max<uint32_t>(1, chunk_tiles / 4);
+  if (!no_ramp && n_tiles >= 3 * chunk_tiles) {
+    uint32_t t = 0;
+    bounds_.push_back(0);
+    t += q;
+    bounds_.push_back(t);
+    while (n_tiles - t > chunk_tiles + q) {
+      t += chunk_tiles;
+      bounds_.push_back(t);
+    }
+    if (n_tiles - t > q) bounds_.push_back(n_tiles - q);
+    bounds_.push_back(n_tiles);
+  } else {
+    for (uint32_t t = 0; t < n_tiles; t += chunk_tiles) bounds_.push_back(t);
+    bounds_.push_back(n_tiles);
+  }
   if (n_tiles == 0) bounds_ = {0, 0};
   const uint32_t nc = uint32_t(bounds_.size() - 1);
   toff_ = hb.tile_off;  // per 64-package group, + the arena end, padded to whole tiles
