@@ -367,6 +367,11 @@ class Engine {
   std::mutex dropin_init_mu_;
   Dropin* dropin(std::string& err);
   bool classify_tiles(const HostBatch& hb, DevBatch& b, std::string& err) const;
+  // library batches' grammar-class launches: one stream per class, fork / join events
+  std::mutex class_mu_;
+  bool class_ready_ = false;
+  hipStream_t class_st_[kLibClassesMax + 1] = {};
+  hipEvent_t class_ev_[kLibClassesMax + 2] = {};
   bool dropin_run(Dropin& d, DropinReq* const* reqs, size_t n, std::string& err);
 };
 

@@ -190,6 +190,11 @@ void HostBatch::clear() {
 Engine::~Engine() {
   if (dev_ >= 0) (void)hipSetDevice(dev_);
   if (stream_) (void)hipStreamSynchronize(stream_);  // no queued launch may outlive the tables
+  if (class_ready_) {
+    for (hipStream_t cs : class_st_) (void)hipStreamSynchronize(cs);
+    for (hipStream_t cs : class_st_) (void)hipStreamDestroy(cs);
+    for (hipEvent_t ev : class_ev_) (void)hipEventDestroy(ev);
+  }
   dropin_.reset();
   for (void* p : allocs_) (void)hipFree(p);
   if (stream_) (void)hipStreamDestroy(stream_);
@@ -481,16 +486,31 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
   if (fused && b.tile_list && variant_ == 0 && t_begin == 0 && t_end == b.n_tiles && !co) {
     // a library batch: one launch per grammar class over its tiles (tile list), each kernel
     // carrying only its ecosystem's encoder (engine.h DevBatch::tile_list)
+    // the class kernels run side by side on the engine's class streams (one after the other
+    // on one stream, each small grid drains before the next starts: C3 0.26 -> 0.49 ms)
     FusedArgs fa;
     fa.pa = pa;
     fa.sa = sa;
+    std::lock_guard<std::mutex> lk(class_mu_);
+    if (!class_ready_) {
+      for (hipStream_t& cs : class_st_)
+        if (!hip_ok(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "hipStreamCreate", err)) return false;
+      for (hipEvent_t& ev : class_ev_)
+        if (!hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate", err)) return false;
+      class_ready_ = true;
+    }
+    if (!hip_ok(hipEventRecord(class_ev_[kLibClasses + 1], pst), "hipEventRecord", err)) return false;
     for (int c = 0; c <= kLibClasses; c++) {
       const uint32_t cb = b.class_begin[c], ce = b.class_begin[c + 1];
       if (ce == cb) continue;
       fa.tiles = b.tile_list + cb;
       const FusedFn fn = c < kLibClasses ? fused_lib_fn(c) : fused_fn(b.gm, vi);
-      fn(ce - cb, pst, fa);
-      if (!hip_ok(hipGetLastError(), "match kernel launch", err)) return false;
+      if (!hip_ok(hipStreamWaitEvent(class_st_[c], class_ev_[kLibClasses + 1], 0), "hipStreamWaitEvent", err)) return false;
+      fn(ce - cb, class_st_[c], fa);
+      if (!hip_ok(hipGetLastError(), "match kernel launch", err) ||
+          !hip_ok(hipEventRecord(class_ev_[c], class_st_[c]), "hipEventRecord", err) ||
+          !hip_ok(hipStreamWaitEvent(pst, class_ev_[c], 0), "hipStreamWaitEvent", err))
+        return false;
     }
     return true;
   }

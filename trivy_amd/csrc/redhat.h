@@ -65,7 +65,10 @@ class RedHatMerge {
   int dev_ = -1;
   RhMerged out_;
   uint32_t* counts_ = nullptr;            // per tile: merged entries (rh_count_kernel)
-  unsigned long long* bases_ = nullptr;   // per tile: output base (rh_scan_kernel)
+  unsigned long long* bases_ = nullptr;   // per tile: output base (exclusive scan of counts_)
+  uint8_t* flags_ = nullptr;              // per tile: 1 = holds Red Hat packages
+  void* scan_tmp_ = nullptr;              // the scan's temporary storage
+  size_t scan_tmp_bytes_ = 0;
   void release();
 };
 

@@ -14,7 +14,7 @@
 //   count   a pair heads a group unless it is a Red Hat pair continuing its predecessor's
 //           (package, ID-rank); per tile its group count (a tile without Red Hat
 //           packages: its pair count, no reads of the pairs);
-//   scan    the tiles' output bases (one workgroup);
+//   scan    the tiles' output bases (rocPRIM device scan);
 //   emit    block scan of the head flags; each head lane walks its group (a few pairs) for
 //           the member with the greatest fixed version (rpm-order rank computed at load
 //           time; ties keep the first, as LessThan does) and writes {pkg, representative,
@@ -22,6 +22,8 @@
 // Integer work bound by memory traffic (about 8 B read + 20 B written per pair); no MFMA.
 #include <algorithm>
 #include <string>
+
+#include <rocprim/device/device_scan.hpp>
 
 #include "redhat.h"
 
@@ -90,7 +92,7 @@ __device__ __forceinline__ bool tile_has_redhat(const MergeArgs& a, uint32_t t, 
 // The tiles' output bases then come from a scan (rh_scan_kernel), not from an atomic
 // reservation per tile: 78k same-address atomics serialised the round-3 kernel (C5: 0.95 ms,
 // SQ_WAIT_ANY / SQ_WAVE_CYCLES = 0.95).
-__global__ __launch_bounds__(kBlock) void rh_count_kernel(MergeArgs a, uint32_t* counts) {
+__global__ __launch_bounds__(kBlock) void rh_count_kernel(MergeArgs a, uint32_t* counts, uint8_t* rh_flags) {
   __shared__ uint32_t ws[kWaves];
   const uint32_t t = blockIdx.x, tid = threadIdx.x;
   const TileDir d = a.dir[t];
@@ -99,12 +101,14 @@ __global__ __launch_bounds__(kBlock) void rh_count_kernel(MergeArgs a, uint32_t*
   if (b0 + cnt > a.raw_cap) {  // an overflowed match list: nothing valid to merge
     if (tid == 0) {
       counts[t] = 0;
+      rh_flags[t] = 0;
       atomicOr(a.mctl + 3, 1ull);
     }
     return;
   }
   if (!tile_has_redhat(a, t, tid)) {  // every pair its own group
     if (tid == 0) counts[t] = cnt;
+    if (tid == 0) rh_flags[t] = 0;
     return;
   }
   uint32_t heads = 0;
@@ -128,46 +132,21 @@ __global__ __launch_bounds__(kBlock) void rh_count_kernel(MergeArgs a, uint32_t*
     heads += block_flag_scan(h, tid, ws, ex);
   }
   if (order_bad) atomicOr(a.mctl + 3, (unsigned long long)ERR_RH_ORDER);
-  if (tid == 0) counts[t] = heads;
+  if (tid == 0) {
+    counts[t] = heads;
+    rh_flags[t] = 1;
+  }
 }
 
-// Exclusive scan of the tiles' counts into bases (one workgroup; n_tiles / 1024 values per
-// thread, then a block scan of the thread sums); the total goes to mctl[0].
-constexpr int kScanThreads = 1024;
-__global__ __launch_bounds__(kScanThreads) void rh_scan_kernel(const uint32_t* counts, unsigned long long* bases,
-                                                               uint32_t n_tiles, unsigned long long* mctl) {
-  __shared__ unsigned long long part[kScanThreads / 64];
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t per = (n_tiles + kScanThreads - 1) / kScanThreads;
-  const uint32_t b = min(n_tiles, tid * per), e = min(n_tiles, b + per);
-  unsigned long long sum = 0;
-  for (uint32_t t = b; t < e; t++) sum += counts[t];
-  unsigned long long x = sum;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned long long y = __shfl_up(x, o, 64);
-    if (lane >= uint32_t(o)) x += y;
-  }
-  if (lane == 63) part[wave] = x;
-  __syncthreads();
-  unsigned long long off = 0, tot = 0;
-  for (uint32_t w = 0; w < kScanThreads / 64; w++) {
-    off += w < wave ? part[w] : 0ull;
-    tot += part[w];
-  }
-  unsigned long long run = off + x - sum;
-  for (uint32_t t = b; t < e; t++) {
-    bases[t] = run;
-    run += counts[t];
-  }
-  if (tid == 0) mctl[0] = tot;
-}
+// The tiles' output bases: an exclusive scan of the counts (rocPRIM's single-pass decoupled
+// look-back scan, RedHatMerge::launch); the last tile writes the total.
 
 // Pass 2: each tile writes its merged entries at its base: a coalesced copy for a tile
 // without Red Hat packages, else one entry per group (the member with the greatest fixed
 // version; ties keep the first, as LessThan does).
 __global__ __launch_bounds__(kBlock) void rh_emit_kernel(MergeArgs a, const uint32_t* counts,
-                                                         const unsigned long long* bases) {
+                                                         const unsigned long long* bases, const uint8_t* rh_flags,
+                                                         uint32_t n_tiles) {
   __shared__ uint32_t ws[kWaves];
   const uint32_t t = blockIdx.x, tid = threadIdx.x;
   const TileDir d = a.dir[t];
@@ -176,9 +155,12 @@ __global__ __launch_bounds__(kBlock) void rh_emit_kernel(MergeArgs a, const uint
   const unsigned long long o0 = bases[t];
   const uint32_t heads = counts[t];
   const bool fits = b0 + cnt <= a.raw_cap && o0 + heads <= a.mcap;
-  if (tid == 0) a.mdir[t] = TileDir{o0, fits ? heads : 0u, 0};
+  if (tid == 0) {
+    a.mdir[t] = TileDir{o0, fits ? heads : 0u, 0};
+    if (t + 1 == n_tiles) a.mctl[0] = o0 + heads;  // the merged total
+  }
   if (!fits) return;  // cannot happen (merged <= raw); the counts tell the host
-  if (!tile_has_redhat(a, t, tid)) {
+  if (!rh_flags[t]) {
     constexpr int kU = 4;  // loads of four pairs in flight per lane before the stores
     for (uint32_t c = 0; c < cnt; c += kU * kBlock) {
       uint32_t pp[kU], aa[kU];
@@ -251,10 +233,13 @@ void RedHatMerge::release() {
   Engine::free_matches(dev_, out_.m);
   if (out_.base) (void)hipFree(out_.base);
   if (out_.grp) (void)hipFree(out_.grp);
-  if (counts_) (void)hipFree(counts_);
-  if (bases_) (void)hipFree(bases_);
+  for (void* x : {static_cast<void*>(counts_), static_cast<void*>(bases_), static_cast<void*>(flags_), scan_tmp_})
+    if (x) (void)hipFree(x);
   counts_ = nullptr;
   bases_ = nullptr;
+  flags_ = nullptr;
+  scan_tmp_ = nullptr;
+  scan_tmp_bytes_ = 0;
   out_ = RhMerged{};
 }
 
@@ -269,7 +254,8 @@ bool RedHatMerge::launch(const RhInputs& in, hipStream_t st, std::string& err) {
     dev_ = dev;
     const uint64_t cap = raw.cap;
     const uint32_t nt = std::max<uint32_t>(in.n_tiles, 1);
-    void *p = nullptr, *q = nullptr, *r = nullptr, *s = nullptr, *t = nullptr, *c = nullptr, *u = nullptr, *v = nullptr;
+    void *p = nullptr, *q = nullptr, *r = nullptr, *s = nullptr, *t = nullptr, *c = nullptr, *u = nullptr, *v = nullptr,
+         *f = nullptr;
     const bool good = ok(hipMalloc(&p, cap * 4), "hipMalloc(merged)", err) &&
                       ok(hipMalloc(&q, cap * 4), "hipMalloc(merged)", err) &&
                       ok(hipMalloc(&r, cap * 4), "hipMalloc(merged)", err) &&
@@ -277,9 +263,11 @@ bool RedHatMerge::launch(const RhInputs& in, hipStream_t st, std::string& err) {
                       ok(hipMalloc(&t, nt * sizeof(TileDir)), "hipMalloc(merged dir)", err) &&
                       ok(hipMalloc(&c, 64), "hipMalloc(merged ctl)", err) &&
                       ok(hipMalloc(&u, nt * 4), "hipMalloc(merge counts)", err) &&
-                      ok(hipMalloc(&v, nt * 8), "hipMalloc(merge bases)", err);
+                      ok(hipMalloc(&v, nt * 8), "hipMalloc(merge bases)", err) &&
+                      ok(hipMalloc(&f, nt), "hipMalloc(merge flags)", err);
     counts_ = static_cast<uint32_t*>(u);
     bases_ = static_cast<unsigned long long*>(v);
+    flags_ = static_cast<uint8_t*>(f);
     out_.m.pkg = static_cast<uint32_t*>(p);
     out_.m.adv = static_cast<uint32_t*>(q);
     out_.base = static_cast<uint32_t*>(r);
@@ -314,10 +302,26 @@ bool RedHatMerge::launch(const RhInputs& in, hipStream_t st, std::string& err) {
   a.mgrp = out_.grp;
   a.mcap = out_.cap;
   a.mctl = out_.m.ctl;
-  hipLaunchKernelGGL(rh_count_kernel, dim3(in.n_tiles), dim3(kBlock), 0, st, a, counts_);
-  hipLaunchKernelGGL(rh_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, counts_, bases_, in.n_tiles, out_.m.ctl);
-  hipLaunchKernelGGL(rh_emit_kernel, dim3(in.n_tiles), dim3(kBlock), 0, st, a, counts_, bases_);
-  return ok(hipGetLastError(), "rh_merge kernels", err);
+  hipLaunchKernelGGL(rh_count_kernel, dim3(in.n_tiles), dim3(kBlock), 0, st, a, counts_, flags_);
+  if (!ok(hipGetLastError(), "rh_count_kernel", err)) return false;
+  size_t need = 0;
+  if (!ok(rocprim::exclusive_scan(nullptr, need, counts_, bases_, 0ull, in.n_tiles,
+                                  rocprim::plus<unsigned long long>(), st),
+          "rocprim scan (size)", err))
+    return false;
+  if (need > scan_tmp_bytes_) {
+    if (scan_tmp_) (void)hipFree(scan_tmp_);
+    scan_tmp_ = nullptr;
+    scan_tmp_bytes_ = 0;
+    if (!ok(hipMalloc(&scan_tmp_, need), "hipMalloc(merge scan)", err)) return false;
+    scan_tmp_bytes_ = need;
+  }
+  if (!ok(rocprim::exclusive_scan(scan_tmp_, need, counts_, bases_, 0ull, in.n_tiles,
+                                  rocprim::plus<unsigned long long>(), st),
+          "rocprim scan", err))
+    return false;
+  hipLaunchKernelGGL(rh_emit_kernel, dim3(in.n_tiles), dim3(kBlock), 0, st, a, counts_, bases_, flags_, in.n_tiles);
+  return ok(hipGetLastError(), "rh_emit_kernel", err);
 }
 
 bool RedHatMerge::fetch(const RhInputs& in, std::vector<uint32_t>& pkg, std::vector<uint32_t>& adv,
