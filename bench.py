@@ -304,6 +304,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-fill", action="store_true", help="c2: skip the FillInfo / Filter legs")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end pipelined pass")
+    ap.add_argument("--e2e-form", choices=["delta", "csr"], default="delta",
+                    help="result form of the end-to-end pass: the delta form (TVM_PIPE_DELTA, decoded to the CSR on "
+                         "the host after the pass) or the 3-byte CSR")
     ap.add_argument("--chunk", type=int, default=1 << 20, help="end-to-end pass: packages per pipeline chunk")
     ap.add_argument("--dropin", action="store_true",
                     help="c2: also time 100-package requests through the per-target driver path")
@@ -451,20 +454,40 @@ def main():
     # ---- end-to-end pipelined pass over PCIe (N = 1) -------------------------------------------
     e2e = None
     if world == 1 and not args.no_e2e and rank == 0:
+        delta = args.e2e_form == "delta"
+
+        def passes(mp, k):
+            ms, dec = [], []
+            for _ in range(k):
+                got, ep, m = mp.pipeline_run()
+                if got != total or ep != -1:
+                    raise RuntimeError("end-to-end pass disagrees with the device-resident pass")
+                ms.append(m)
+                dec.append(mp.pipeline_decode_ms())
+            return sorted(ms)[len(ms) // 2], sorted(dec)[len(dec) // 2]
+
         mp = MatchBatch(eng)
         wl.fill(mp)
-        mp.pipeline_prepare(match_cap=total, chunk_packages=args.chunk)
+        mp.pipeline_prepare(match_cap=total, chunk_packages=args.chunk, delta=delta)
         for _ in range(max(1, args.warmup)):
             mp.pipeline_run()
-        ms = []
-        for _ in range(max(3, args.steps // 4)):
-            got, ep, m = mp.pipeline_run()
-            if got != total or ep != -1:
-                raise RuntimeError("end-to-end pass disagrees with the device-resident pass")
-            ms.append(m)
+        npass = max(3, args.steps // 4)
+        med, dec = passes(mp, npass)
         st = mp.pipeline_stats()
-        med = sorted(ms)[len(ms) // 2]
-        e2e = {"packages_per_s": wl.n / (med / 1e3), "ms_per_pass": med, "passes": len(ms),
+        csr_form = None
+        if delta:  # the same batch with the result as the 3-byte CSR, for comparison
+            mp.pipeline_prepare(match_cap=total, chunk_packages=args.chunk)
+            mp.pipeline_run()
+            cmed, cdec = passes(mp, npass)
+            cst = mp.pipeline_stats()
+            csr_form = {"packages_per_s": wl.n / (cmed / 1e3), "ms_per_pass": cmed, "d2h_bytes": cst["d2h_bytes"],
+                        "widen_ms": cdec}
+        e2e = {"packages_per_s": wl.n / (med / 1e3), "ms_per_pass": med, "passes": npass,
+               "result_form": "delta (TVM_PIPE_DELTA)" if delta else "CSR, 3-byte indices",
+               "decode_ms": dec, "packages_per_s_with_decode": wl.n / ((med + dec) / 1e3),
+               "decode_is": "tvm_pipeline_result on the host threads after the pass: the CSR (row ends + 4-byte "
+                            "indices) from the bytes that crossed the link",
+               "csr_form": csr_form,
                "h2d_bytes": st["h2d_bytes"], "d2h_bytes": st["d2h_bytes"], "chunks": st["chunks"],
                "pcie_GBs": (st["h2d_bytes"] + st["d2h_bytes"]) / (med / 1e3) / 1e9,
                "transport_form": st["transport_form"], "prepare_encode_ms": st["encode_ms"],
@@ -486,9 +509,11 @@ def main():
             mf = MatchBatch(eng)
             wl.fill(mf)
             tp = time.perf_counter()
-            mf.pipeline_prepare(match_cap=total, chunk_packages=args.chunk, raw=True)
+            mf.pipeline_prepare(match_cap=total, chunk_packages=args.chunk, raw=True,
+                                delta=args.e2e_form == "delta")
             tr = time.perf_counter()
             got, ep, _ = mf.pipeline_run()
+            mf.pipeline_decode_ms()
             te = time.perf_counter()
             if got != total or ep != -1:
                 raise RuntimeError("fresh-batch pass disagrees with the device-resident pass")
@@ -501,7 +526,9 @@ def main():
         fresh = dict(med, packages_per_s=wl.n / ((med["prepare_ms"] + med["pass_ms"]) / 1e3), batches=len(runs),
                      form="raw (pinned staging copy on the host threads; no per-batch string dedup)",
                      inside="prepare (freeze, size, pinned staging copy, buffers from the block cache) + one "
-                            "pipelined pass (upload, match, per-package advisory lists back in pinned host memory)",
+                            "pipelined pass (upload, match, per-package advisory lists back in pinned host memory) "
+                            "+ the host decode of the result into the CSR",
+                     result_form=args.e2e_form,
                      outside="build_ms: the caller adding the batch's packages (tvm_batch_add_many per target)")
 
     fill = None

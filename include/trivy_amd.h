@@ -313,7 +313,12 @@ int tvm_batch_upload_into(tvm_engine* e, tvm_batch* b, void* pkg_dev, void* adv_
  * name and version under 256 bytes, at most 255 platforms): each distinct name and each
  * distinct version string crosses the link once, packages carry references to them, and
  * the GPU rebuilds the batch's arrays chunk by chunk (one DMA per chunk). */
-enum { TVM_PIPE_RAW = 1, TVM_PIPE_ADV32 = 2 };
+/* TVM_PIPE_DELTA: the per-package lists cross the link in the delta form
+ * (trivy_amd/csrc/delta_form.h: per tile 256 count bytes, then each package's first advisory
+ * index as 3 bytes and the next ones as 1-byte differences; ~1.4 bytes a match instead of 3
+ * + a 4-byte row end per package); tvm_pipeline_result decodes it on the host threads, once
+ * per pass.  Needs a DB of fewer than 2^24 advisories (not with TVM_PIPE_ADV32). */
+enum { TVM_PIPE_RAW = 1, TVM_PIPE_ADV32 = 2, TVM_PIPE_DELTA = 4 };
 int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32_t chunk_packages, uint32_t flags,
                          char* err, size_t errlen);
 /* One pass; ms = wall time of the call.  TVM_EINVAL with *n_matches set when the matches do
@@ -329,7 +334,17 @@ int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row
 /* The result as it arrived in pinned host memory: index i is the `width`-byte (3 or 4)
  * little-endian integer at adv + width * i. */
 int tvm_pipeline_result_raw(tvm_batch* b, const void** adv, uint32_t* width, const uint32_t** row_end,
-                            uint64_t* n_matches);
+                            uint64_t* n_matches);  /* TVM_EINVAL for a TVM_PIPE_DELTA pipeline */
+/* A TVM_PIPE_DELTA pass's result as it arrived: tile t's stream of tile_info[2t + 1] bytes at
+ * stream + tvm_delta_region(t, CSR position of its first match), tile_info[2t] its matches. */
+int tvm_pipeline_result_delta(tvm_batch* b, const void** stream, uint64_t* stream_bytes, const uint32_t** tile_info,
+                              uint32_t* n_tiles, uint64_t* n_matches);
+/* Decodes delta-form streams into the CSR: adv (n_matches entries), row_end (n_tiles * 256:
+ * the CSR position after each package's list).  Host only (the decode tvm_pipeline_result
+ * runs; test and inspection hook). */
+int tvm_delta_decode(const void* stream, uint64_t stream_bytes, const uint32_t* tile_info, uint32_t n_tiles,
+                     uint64_t n_matches, uint32_t* adv, uint32_t* row_end, char* err, size_t errlen);
+uint64_t tvm_delta_region(uint32_t tile, uint64_t first_match);
 /* [0] bytes the last pass copied host to device, [1] device to host, [2] chunks, [3] 1 when
  * the batch travels in its transport form, [4] prepare's host time building it (us). */
 int tvm_pipeline_stats(tvm_batch* b, uint64_t out[5]);

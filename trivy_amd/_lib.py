@@ -206,6 +206,13 @@ _SIG = [
     ("tvm_pipeline_result_raw", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint32),
                                                ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64)]),
     ("tvm_pipeline_stats", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
+    ("tvm_pipeline_result_delta", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64),
+                                                 ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint32),
+                                                 ctypes.POINTER(ctypes.c_uint64)]),
+    ("tvm_delta_decode", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32,
+                                        ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p,
+                                        ctypes.c_size_t]),
+    ("tvm_delta_region", ctypes.c_uint64, [ctypes.c_uint32, ctypes.c_uint64]),
     ("tvm_version_key", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p,
                                        ctypes.c_size_t]),
     ("tvm_engine_dropin_stats", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),

@@ -9,6 +9,7 @@ its platform bucket (the string a driver would pass to Get: "debian 12", "alma 9
 its arch / ksplice attributes; one launch returns every (package, advisory) pair.
 """
 import ctypes
+import time
 
 import numpy as np
 
@@ -228,13 +229,15 @@ class MatchBatch:
         return lib().tvm_match_algorithmic_bytes(self.engine.h, self.h)
 
     # ---- end-to-end pipelined pass (tvm_pipeline_*) ----
-    def pipeline_prepare(self, match_cap=None, chunk_packages=1 << 19, raw=False, adv32=False):
+    def pipeline_prepare(self, match_cap=None, chunk_packages=1 << 19, raw=False, adv32=False, delta=False):
         """Pins the batch and sizes the pipeline (host batch -> GPU -> host CSR).  raw: upload
         the batch's own arrays instead of its transport form (TVM_PIPE_RAW); adv32: 4-byte
-        advisory indices in the result even when 3 bytes hold them (TVM_PIPE_ADV32)."""
+        advisory indices in the result even when 3 bytes hold them (TVM_PIPE_ADV32); delta:
+        the result crosses the link in the delta form (TVM_PIPE_DELTA, decoded by
+        pipeline_csr)."""
         e = errbuf()
         cap = match_cap if match_cap is not None else max(1024, 8 * len(self))
-        flags = (1 if raw else 0) | (2 if adv32 else 0)
+        flags = (1 if raw else 0) | (2 if adv32 else 0) | (4 if delta else 0)
         self._check(lib().tvm_pipeline_prepare(self.engine.h, self.h, cap, chunk_packages, flags, e, len(e)), e,
                     "tvm_pipeline_prepare")
         self.pipe_cap = cap
@@ -277,6 +280,26 @@ class MatchBatch:
         for j in range(width):
             out |= raw[:, j].astype(np.uint32) << (8 * j)
         return out, width
+
+    def pipeline_decode_ms(self):
+        """tvm_pipeline_result's host time for the last pass (the delta form decoded, or the
+        3-byte indices widened, into the CSR; once per pass), ms."""
+        adv, rend, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+        t0 = time.perf_counter()
+        if lib().tvm_pipeline_result(self.h, ctypes.byref(adv), ctypes.byref(rend), ctypes.byref(n)):
+            raise RuntimeError("tvm_pipeline_result: no valid pass")
+        return (time.perf_counter() - t0) * 1e3
+
+    def pipeline_delta(self):
+        """The last TVM_PIPE_DELTA pass's result as it arrived: (stream uint8 view, tile_info
+        uint32[n_tiles, 2] = {matches, stream bytes}, matches) - tvm_pipeline_result_delta."""
+        s, sb, ti, nt, n = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_void_p(), ctypes.c_uint32(), ctypes.c_uint64()
+        if lib().tvm_pipeline_result_delta(self.h, ctypes.byref(s), ctypes.byref(sb), ctypes.byref(ti),
+                                           ctypes.byref(nt), ctypes.byref(n)):
+            raise RuntimeError("tvm_pipeline_result_delta: no valid delta pass")
+        stream = np.ctypeslib.as_array((ctypes.c_uint8 * sb.value).from_address(s.value))
+        info = np.ctypeslib.as_array((ctypes.c_uint32 * max(2 * nt.value, 1)).from_address(ti.value))[:2 * nt.value]
+        return stream, info.reshape(-1, 2).copy(), n.value
 
     def pipeline_stats(self):
         out = (ctypes.c_uint64 * 5)()

@@ -19,6 +19,7 @@
 #include "libdb.h"
 #include "libver.h"
 #include "bbolt.h"
+#include "delta_form.h"
 #include "pipeline.h"
 #include "pool.h"
 #include "sbom.h"
@@ -70,7 +71,8 @@ struct tvm_batch {
   uint32_t pkg_base = 0;               // tvm_batch_set_package_base
   uint64_t pipe_total = 0;
   uint64_t pipe_runs = 0, pipe_wide_for = ~0ull;  // passes run; the pass pipe_wide was widened for
-  std::vector<uint32_t> pipe_wide;                // 3-byte result indices widened (tvm_pipeline_result)
+  std::vector<uint32_t> pipe_wide;                // 3-byte result indices widened / the delta form decoded (tvm_pipeline_result)
+  std::vector<uint32_t> pipe_rowend;              // the delta form's row ends (tvm_pipeline_result)
   unsigned long long* order_scratch = nullptr;  // tvm_match_order_into: ticket + look-back word per tile
   uint32_t order_cap = 0;
   bool external_out = false;  // m.pkg / m.adv belong to the caller (tvm_batch_upload_into)
@@ -467,7 +469,7 @@ void tvm_batch_free(tvm_batch* b) {
                     static_cast<void*>(b->dev.tail), static_cast<void*>(b->dev.spill),
                     static_cast<void*>(b->external_out ? nullptr : b->m.pkg),
                     static_cast<void*>(b->external_out ? nullptr : b->m.adv), static_cast<void*>(b->m.dir),
-                    static_cast<void*>(b->m.ctl), static_cast<void*>(b->dev.tile_list),
+                    static_cast<void*>(b->m.ctl),
                     static_cast<void*>(b->fill_out)})
       if (p) (void)hipFree(p);
   }
@@ -603,6 +605,7 @@ int tvm_batch_upload(tvm_engine* e, tvm_batch* b, uint64_t cap, char* err, size_
   b->dev.pkg_base = b->pkg_base;
   b->uploaded = true;
   b->filter.reset_packages();
+  b->rh.forget_tiles();
   b->device = e->device;
   return TVM_OK;
 }
@@ -1336,7 +1339,9 @@ int tvm_match_filter_time(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o,
 
 int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32_t chunk_packages, uint32_t flags,
                          char* err, size_t errlen) {
-  if (!e || !b || chunk_packages == 0 || (flags & ~uint32_t(TVM_PIPE_RAW | TVM_PIPE_ADV32))) return TVM_EINVAL;
+  if (!e || !b || chunk_packages == 0 || (flags & ~uint32_t(TVM_PIPE_RAW | TVM_PIPE_ADV32 | TVM_PIPE_DELTA)) ||
+      ((flags & TVM_PIPE_DELTA) && (flags & TVM_PIPE_ADV32)))
+    return TVM_EINVAL;
   std::shared_lock<std::shared_mutex> lk(e->mu);
   if (!bind(b, e)) {
     set_err(err, errlen, kStale);
@@ -1347,7 +1352,13 @@ int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32
   b->pipe_wide_for = ~0ull;
   std::string msg;
   const bool packed = !(flags & TVM_PIPE_ADV32) && e->db->db.advs.size() < (1ull << 24);
-  if (!b->pipe->prepare(*e->eng, b->hb, match_cap, chunk_packages, !(flags & TVM_PIPE_RAW), packed, msg)) {
+  const bool delta = (flags & TVM_PIPE_DELTA) != 0;
+  if (delta && !packed) {
+    b->pipe.reset();
+    set_err(err, errlen, "TVM_PIPE_DELTA: the delta form carries 3-byte advisory indices (the DB has 2^24 or more)");
+    return TVM_EINVAL;
+  }
+  if (!b->pipe->prepare(*e->eng, b->hb, match_cap, chunk_packages, !(flags & TVM_PIPE_RAW), packed, delta, msg)) {
     b->pipe.reset();
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
@@ -1394,6 +1405,22 @@ int tvm_pipeline_run(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* 
 
 int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row_end, uint64_t* n_matches) {
   if (!b || !b->pipe || b->pipe_total > b->pipe->cap()) return TVM_EINVAL;
+  if (b->pipe->delta()) {  // decode the delta form into the CSR once per pass (host threads, after the pass)
+    if (b->pipe_wide_for != b->pipe_runs) {
+      const Pipeline& P = *b->pipe;
+      b->pipe_wide.resize(std::max<uint64_t>(b->pipe_total, 1));
+      b->pipe_rowend.resize(std::max<size_t>(size_t(P.n_tiles()) * kTile, 1));
+      std::string msg;
+      if (!delta_decode(P.delta_stream(), P.delta_stream_size(), P.delta_tiles(), P.n_tiles(), b->pipe_total,
+                        b->pipe_wide.data(), b->pipe_rowend.data(), msg))
+        return TVM_EDEVICE;
+      b->pipe_wide_for = b->pipe_runs;
+    }
+    if (adv) *adv = b->pipe_wide.data();
+    if (row_end) *row_end = b->pipe_rowend.data();
+    if (n_matches) *n_matches = b->pipe_total;
+    return TVM_OK;
+  }
   if (adv && b->pipe->packed()) {  // widen the 3-byte indices once per pass (host side, after the pass)
     if (b->pipe_wide_for != b->pipe_runs) {
       const uint8_t* p = reinterpret_cast<const uint8_t*>(b->pipe->adv());
@@ -1413,13 +1440,38 @@ int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row
 
 int tvm_pipeline_result_raw(tvm_batch* b, const void** adv, uint32_t* width, const uint32_t** row_end,
                             uint64_t* n_matches) {
-  if (!b || !b->pipe || b->pipe_total > b->pipe->cap()) return TVM_EINVAL;
+  if (!b || !b->pipe || b->pipe_total > b->pipe->cap() || b->pipe->delta()) return TVM_EINVAL;
   if (adv) *adv = b->pipe->adv();
   if (width) *width = b->pipe->packed() ? 3 : 4;
   if (row_end) *row_end = b->pipe->row_end();
   if (n_matches) *n_matches = b->pipe_total;
   return TVM_OK;
 }
+
+int tvm_pipeline_result_delta(tvm_batch* b, const void** stream, uint64_t* stream_bytes, const uint32_t** tile_info,
+                              uint32_t* n_tiles, uint64_t* n_matches) {
+  if (!b || !b->pipe || !b->pipe->delta() || b->pipe_total > b->pipe->cap()) return TVM_EINVAL;
+  if (stream) *stream = b->pipe->delta_stream();
+  if (stream_bytes) *stream_bytes = b->pipe->delta_stream_size();
+  if (tile_info) *tile_info = reinterpret_cast<const uint32_t*>(b->pipe->delta_tiles());
+  if (n_tiles) *n_tiles = b->pipe->n_tiles();
+  if (n_matches) *n_matches = b->pipe_total;
+  return TVM_OK;
+}
+
+int tvm_delta_decode(const void* stream, uint64_t stream_bytes, const uint32_t* tile_info, uint32_t n_tiles,
+                     uint64_t n_matches, uint32_t* adv, uint32_t* row_end, char* err, size_t errlen) {
+  if ((n_tiles && (!stream || !tile_info || !row_end)) || (n_matches && !adv)) return TVM_EINVAL;
+  std::string msg;
+  if (!delta_decode(static_cast<const uint8_t*>(stream), stream_bytes, reinterpret_cast<const uint2*>(tile_info),
+                    n_tiles, n_matches, adv, row_end, msg)) {
+    set_err(err, errlen, msg);
+    return TVM_EINVAL;
+  }
+  return TVM_OK;
+}
+
+uint64_t tvm_delta_region(uint32_t tile, uint64_t first_match) { return delta_region(tile, first_match); }
 
 int tvm_wire_encode(size_t n, const uint32_t* plat, const char* arena, const uint64_t* name_off, const uint32_t* name_len,
                     const uint64_t* ver_off, const uint32_t* ver_len, uint32_t chunk_packages, int threads, void* out,

@@ -1,0 +1,89 @@
+// Host decode of the delta result form (delta_form.h).
+#include "delta_form.h"
+
+#include <atomic>
+#include <vector>
+
+#include "engine.h"
+#include "host_par.h"
+
+namespace tvm {
+
+bool delta_decode(const uint8_t* stream, uint64_t stream_bytes, const uint2* tile_info, uint32_t n_tiles,
+                  uint64_t total, uint32_t* adv, uint32_t* row_end, std::string& err) {
+  std::vector<uint64_t> b(size_t(n_tiles) + 1, 0);
+  for (uint32_t t = 0; t < n_tiles; t++) b[t + 1] = b[t] + tile_info[t].x;
+  if (b[n_tiles] != total) {
+    err = "delta form: the tiles' counts do not add up to the pass's matches";
+    return false;
+  }
+  std::atomic<bool> bad{false};
+  range_for(n_tiles, 64, [&](size_t t0, size_t t1) {
+    for (size_t t = t0; t < t1 && !bad.load(std::memory_order_relaxed); t++) {
+      const uint64_t pos0 = b[t], count = tile_info[t].x, bytes = tile_info[t].y;
+      uint32_t* re = row_end + t * kTile;
+      if (count == 0) {
+        for (int p = 0; p < kTile; p++) re[p] = uint32_t(pos0);
+        continue;
+      }
+      const uint64_t r = delta_region(uint32_t(t), pos0);
+      if (bytes < kTile || r + bytes > stream_bytes) {
+        bad = true;
+        break;
+      }
+      const uint8_t* h = stream + r;
+      const uint8_t* q = h + kTile;
+      const uint8_t* end = h + bytes;
+      uint32_t* o = adv + pos0;
+      uint32_t* const o_end = adv + pos0 + count;
+      for (int p = 0; p < kTile; p++) {
+        uint64_t k = h[p];
+        if (k == 255) {
+          if (end - q < 4) {
+            bad = true;
+            break;
+          }
+          k = uint32_t(q[0]) | uint32_t(q[1]) << 8 | uint32_t(q[2]) << 16 | uint32_t(q[3]) << 24;
+          q += 4;
+        }
+        if (k) {
+          if (uint64_t(o_end - o) < k || end - q < 3) {
+            bad = true;
+            break;
+          }
+          uint32_t a = uint32_t(q[0]) | uint32_t(q[1]) << 8 | uint32_t(q[2]) << 16;
+          q += 3;
+          *o++ = a;
+          for (uint64_t j = 1; j < k; j++) {
+            if (q >= end) {
+              bad = true;
+              break;
+            }
+            const uint8_t x = *q++;
+            if (x) {
+              a += x;
+            } else {
+              if (end - q < 3) {
+                bad = true;
+                break;
+              }
+              a = uint32_t(q[0]) | uint32_t(q[1]) << 8 | uint32_t(q[2]) << 16;
+              q += 3;
+            }
+            *o++ = a;
+          }
+          if (bad.load(std::memory_order_relaxed)) break;
+        }
+        re[p] = uint32_t(o - adv);
+      }
+      if (o != o_end || q != end) bad = true;
+    }
+  });
+  if (bad) {
+    err = "delta form: a tile's stream is inconsistent with its count";
+    return false;
+  }
+  return true;
+}
+
+}  // namespace tvm

@@ -17,7 +17,6 @@ namespace tvm {
 class DB;
 
 constexpr int kTile = 256;   // packages per tile (workgroup) of the match kernels
-constexpr int kLibClassesMax = 5;  // single-ecosystem library grammar classes (DevBatch::tile_list)
 constexpr int kGroup = 64;   // packages per offset group (one wavefront); tile_off is per group
 constexpr int kGroupsPerTile = kTile / kGroup;
 
@@ -89,11 +88,6 @@ struct DevBatch {
   // probe -> sweep hand-off (device only)
   PkgRec* rec = nullptr;
   uint4* tail = nullptr;  // key bytes 16..31 per package
-  // library batches (grammar set beyond the OS ones), device-resident path: the tiles ordered
-  // by grammar class, class c = tile_list[class_begin[c], class_begin[c + 1]); classes 0..4
-  // are one ecosystem each (libver.h GM_NPM, GM_PEP, GM_GEN, GM_GEM, GM_MVN), 5 mixed tiles
-  uint32_t* tile_list = nullptr;
-  uint32_t class_begin[kLibClassesMax + 2] = {};
 };
 
 // Device-side results of one match pass: the per-package advisory lists as two columns
@@ -147,9 +141,120 @@ struct CopyOutArgs {
   uint64_t adv_units = 0;             // 16-byte units of adv_h
   uint64_t row_end_units = 0;         // 16-byte units of row_end_h
   unsigned long long* ctl = nullptr;  // the pass's control block: ctl[3] |= ERR_BOUNDS on a guard hit
+  // delta form (instead of the CSR; delta_form.h): tile t's byte stream at stream_h +
+  // delta_region(t, b), its {matches, stream bytes} at tile_info_h[t]
+  uint32_t delta = 0;
+  uint8_t* stream_h = nullptr;
+  uint64_t stream_units = 0;          // 16-byte units of stream_h
+  uint2* tile_info_h = nullptr;
 };
-constexpr uint32_t kCopyLdsWords = kTile + 8;  // copy_out_tiles' LDS: counts + scratch
+constexpr uint32_t kDeltaStage = 2080;  // copy_out_tiles' delta staging bytes: header + one chunk's worst case + a carried unit
+constexpr uint32_t kCopyLdsWords = kTile + 8 + kDeltaStage / 4;  // copy_out_tiles' LDS: counts + scratch + delta staging
+
+// The delta result form: tile t's stream starts at this (16-byte aligned) byte of the stream
+// buffer, b = the CSR position of the tile's first match.  Consecutive tiles' starts are at
+// least 273 + 5 * count bytes apart, more than a stream of `count` matches can take (256
+// count bytes + at most 4 bytes per match + 4 per package of 255 or more + the last unit).
+__host__ __device__ inline uint64_t delta_region(uint32_t t, uint64_t b) { return ((288ull * t + 5ull * b) >> 4) << 4; }
+inline uint64_t delta_stream_bytes(uint32_t n_tiles, uint64_t cap) { return 288ull * n_tiles + 5ull * cap + 64; }
 constexpr uint32_t kCopyWorkgroups = 256;      // workgroups of a result move
+
+// Exclusive block scan of v; tot = the block's sum.  red: kTile / 64 words of LDS.
+__device__ __forceinline__ uint32_t copy_block_scan(uint32_t v, uint32_t* red, uint32_t tid, uint32_t& tot) {
+  const uint32_t lane = tid & 63, wave = tid >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= uint32_t(o)) x += y;
+  }
+  __syncthreads();  // red is free
+  if (lane == 63) red[wave] = x;
+  __syncthreads();
+  uint32_t pre = 0;
+  tot = 0;
+#pragma unroll
+  for (int w = 0; w < kTile / 64; w++) {
+    const uint32_t r = red[w];
+    pre += uint32_t(w) < wave ? r : 0u;
+    tot += r;
+  }
+  return pre + x - v;
+}
+
+// Tile t's matches [base, base + count) as its delta stream (delta_form.h): 256 count bytes
+// (255: the count follows as 4 bytes at the start of the package's list), then per package
+// with matches its first advisory as 3 bytes and every next one as the byte difference from
+// the one before (1..255), or 0 + 3 bytes when it does not fit.  Assembled in LDS (sb) one
+// chunk of 256 matches at a time and stored to the pinned stream in whole 16-byte units.
+// cnt: the tile's per-package counts; returns the stream's bytes.
+__device__ __forceinline__ uint32_t copy_out_delta(const CopyOutArgs& a, uint32_t t, uint64_t b, const TileDir& d,
+                                                   uint32_t p_first, const uint32_t* cnt, uint32_t* red, uint8_t* sb) {
+  const uint32_t tid = threadIdx.x;
+  const uint64_t u0 = delta_region(t, b) >> 4;
+  uint4* dst = reinterpret_cast<uint4*>(a.stream_h);
+  const uint32_t c = cnt[tid];
+  sb[tid] = uint8_t(c < 255u ? c : 255u);
+  uint32_t fill = kTile;  // bytes staged
+  uint64_t done = 0;      // units stored
+  bool bad = false;
+  auto flush = [&](uint32_t units) {
+    for (uint32_t u = tid; u < units; u += kTile) {
+      if (u0 + done + u < a.stream_units)
+        dst[u0 + done + u] = reinterpret_cast<const uint4*>(sb)[u];
+      else
+        bad = true;
+    }
+  };
+  for (uint32_t i0 = 0; i0 < d.count; i0 += kTile) {
+    const uint32_t i = i0 + tid;
+    uint32_t sz = 0, ad = 0, q = 0, pc = 0;
+    bool first = false;
+    if (i < d.count) {
+      const uint32_t pk = a.pkg[d.base + i];
+      ad = a.adv[d.base + i];
+      first = i == 0 || a.pkg[d.base + i - 1] != pk;
+      if (first) {
+        pc = cnt[(pk - a.pkg_base - p_first) & (kTile - 1)];
+        sz = pc >= 255u ? 7u : 3u;
+      } else {
+        q = ad - a.adv[d.base + i - 1];
+        sz = q - 1u < 255u ? 1u : 4u;
+      }
+    }
+    uint32_t tot;
+    uint8_t* o = sb + fill + copy_block_scan(sz, red, tid, tot);
+    if (sz == 1) {
+      o[0] = uint8_t(q);
+    } else if (sz) {
+      if (sz == 7) {
+        o[0] = uint8_t(pc), o[1] = uint8_t(pc >> 8), o[2] = uint8_t(pc >> 16), o[3] = uint8_t(pc >> 24);
+        o += 4;
+      } else if (!first) {
+        *o++ = 0;  // escape: an absolute index follows
+      }
+      o[0] = uint8_t(ad), o[1] = uint8_t(ad >> 8), o[2] = uint8_t(ad >> 16);
+    }
+    fill += tot;
+    __syncthreads();
+    const uint32_t full = fill >> 4, rem = fill & 15u;
+    flush(full);
+    const uint8_t keep = tid < rem ? sb[16 * full + tid] : uint8_t(0);
+    __syncthreads();
+    if (tid < rem) sb[tid] = keep;
+    done += full;
+    fill = rem;
+    __syncthreads();
+  }
+  // the rest: the header of a tile with fewer matches than one chunk's worth of units, the
+  // last partial unit (zero padded)
+  const uint32_t units = (fill + 15u) >> 4;
+  if (tid < units * 16u && tid >= fill) sb[tid] = 0;
+  __syncthreads();
+  flush(units);
+  if (bad) atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
+  return uint32_t(done * 16 + fill);
+}
 
 __device__ __forceinline__ uint32_t copy_block_sum(uint32_t v, uint32_t* red, uint32_t tid) {
 #pragma unroll
@@ -195,6 +300,15 @@ __device__ __forceinline__ void copy_out_tiles(const CopyOutArgs& a, uint32_t wg
           if (q[u] < kTile) atomicAdd(&cnt[q[u]], 1u);
       }
     __syncthreads();
+    if (a.delta) {  // the delta form: the counts go into the stream's header, no row ends
+      uint32_t bytes = 0;
+      if (fits && d.count)
+        bytes = copy_out_delta(a, t, b, d, p_first, cnt, red, reinterpret_cast<uint8_t*>(lds + kTile + 8));
+      if (tid == 0) a.tile_info_h[t] = make_uint2(d.count, bytes);
+      b += d.count;
+      __syncthreads();  // cnt is rewritten by the next tile
+      continue;
+    }
     uint32_t x = cnt[tid];
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -342,7 +456,6 @@ class Engine {
   void dropin_stats(uint64_t out[3]);
 
   const DB& db() const { return *db_; }
-  static constexpr int kLibClasses = kLibClassesMax;
   const PlatInfo* device_plats() const { return d_.plats; }
 
   // Sweep-kernel variant (pairs per lane / LDS buffer); returns the previous one.  Default
@@ -366,12 +479,6 @@ class Engine {
   std::unique_ptr<Dropin> dropin_;
   std::mutex dropin_init_mu_;
   Dropin* dropin(std::string& err);
-  bool classify_tiles(const HostBatch& hb, DevBatch& b, std::string& err) const;
-  // library batches' grammar-class launches: one stream per class, fork / join events
-  std::mutex class_mu_;
-  bool class_ready_ = false;
-  hipStream_t class_st_[kLibClassesMax + 1] = {};
-  hipEvent_t class_ev_[kLibClassesMax + 2] = {};
   bool dropin_run(Dropin& d, DropinReq* const* reqs, size_t n, std::string& err);
 };
 

@@ -31,7 +31,6 @@ const SweepFn* sweep_table(bool filt);
 const FusedFn* fused_table_DEB();
 const FusedFn* fused_table_OS();
 const FusedFn* fused_table_ALL();
-FusedFn fused_lib_fn(int cls);  // kern_fused_lib.hip
 
 namespace {
 
@@ -190,11 +189,6 @@ void HostBatch::clear() {
 Engine::~Engine() {
   if (dev_ >= 0) (void)hipSetDevice(dev_);
   if (stream_) (void)hipStreamSynchronize(stream_);  // no queued launch may outlive the tables
-  if (class_ready_) {
-    for (hipStream_t cs : class_st_) (void)hipStreamSynchronize(cs);
-    for (hipStream_t cs : class_st_) (void)hipStreamDestroy(cs);
-    for (hipEvent_t ev : class_ev_) (void)hipEventDestroy(ev);
-  }
   dropin_.reset();
   for (void* p : allocs_) (void)hipFree(p);
   if (stream_) (void)hipStreamDestroy(stream_);
@@ -325,7 +319,6 @@ bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
   if (!hb.attr.empty() &&
       !hip_ok(hipMemcpy(b.attr, hb.attr.data(), hb.attr.size() * sizeof(uint2), hipMemcpyHostToDevice), "H2D attr", err))
     return false;
-  if (grammar_index(b.gm) == 2 && !classify_tiles(hb, b, err)) return false;
   if (!hb.cpe_bits.empty() && hb.cpe_words) {
     if (!dmalloc(&b.cpe_bits, hb.cpe_bits.size(), "hipMalloc(cpe sets)", err) ||
         !hip_ok(hipMemcpy(b.cpe_bits, hb.cpe_bits.data(), hb.cpe_bits.size() * 4, hipMemcpyHostToDevice), "H2D cpe", err))
@@ -336,43 +329,6 @@ bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
   return true;
 }
 
-// Library batches: each tile's grammar class (the single ecosystem grammar set of its
-// packages, libver.h GM_NPM .. GM_MVN, or "mixed"), and the tiles ordered by class.
-bool Engine::classify_tiles(const HostBatch& hb, DevBatch& b, std::string& err) const {
-  static const uint32_t kClassGm[kLibClasses] = {GM_NPM, GM_PEP, GM_GEN, GM_GEM, GM_MVN};
-  const auto& pi = db_->plat_info;
-  const uint32_t nt = b.n_tiles;
-  std::vector<uint8_t> cls(nt);
-  range_for(nt, 256, [&](size_t t0, size_t t1) {
-    for (size_t t = t0; t < t1; t++) {
-      uint32_t gm = 0, last = 0xFFFFFFFFu;
-      const size_t p1 = std::min<size_t>(hb.pk.size(), (t + 1) * kTile);
-      for (size_t p = t * kTile; p < p1; p++) {
-        const uint32_t pl = hb.pk[p].x;
-        if (pl != last && pl < pi.size()) gm |= 1u << pi[pl].cmp;
-        last = pl;
-      }
-      int c = kLibClasses;
-      for (int k = 0; k < kLibClasses; k++)
-        if ((gm & ~kClassGm[k]) == 0) {
-          c = k;
-          break;
-        }
-      cls[t] = uint8_t(c);
-    }
-  });
-  uint32_t cnt[kLibClasses + 1] = {};
-  for (uint8_t c : cls) cnt[c]++;
-  b.class_begin[0] = 0;
-  for (int c = 0; c <= kLibClasses; c++) b.class_begin[c + 1] = b.class_begin[c] + cnt[c];
-  std::vector<uint32_t> list(nt);
-  uint32_t at[kLibClasses + 1];
-  std::copy(b.class_begin, b.class_begin + kLibClasses + 1, at);
-  for (uint32_t t = 0; t < nt; t++) list[at[cls[t]]++] = t;
-  return dmalloc(&b.tile_list, std::max<size_t>(nt, 1), "hipMalloc(tile list)", err) &&
-         (nt == 0 || hip_ok(hipMemcpy(b.tile_list, list.data(), nt * 4, hipMemcpyHostToDevice), "H2D tile list", err));
-}
-
 void Engine::free_batch(int device, DevBatch& b, bool pooled) {
   (void)hipSetDevice(device);
   for (void* p : {static_cast<void*>(b.pk), static_cast<void*>(b.tile_off), static_cast<void*>(b.arena),
@@ -380,7 +336,6 @@ void Engine::free_batch(int device, DevBatch& b, bool pooled) {
                   static_cast<void*>(b.spill)})
     dfree(p, pooled, device);
   dfree(b.cpe_bits, false, device);  // never pooled (copied by the caller)
-  dfree(b.tile_list, false, device);
   b = DevBatch{};
 }
 
@@ -483,37 +438,6 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
   sa.out_adv = m.adv;
   sa.out_cap = m.cap;
   sa.ctl = m.ctl;
-  if (fused && b.tile_list && variant_ == 0 && t_begin == 0 && t_end == b.n_tiles && !co) {
-    // a library batch: one launch per grammar class over its tiles (tile list), each kernel
-    // carrying only its ecosystem's encoder (engine.h DevBatch::tile_list)
-    // the class kernels run side by side on the engine's class streams (one after the other
-    // on one stream, each small grid drains before the next starts: C3 0.26 -> 0.49 ms)
-    FusedArgs fa;
-    fa.pa = pa;
-    fa.sa = sa;
-    std::lock_guard<std::mutex> lk(class_mu_);
-    if (!class_ready_) {
-      for (hipStream_t& cs : class_st_)
-        if (!hip_ok(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "hipStreamCreate", err)) return false;
-      for (hipEvent_t& ev : class_ev_)
-        if (!hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate", err)) return false;
-      class_ready_ = true;
-    }
-    if (!hip_ok(hipEventRecord(class_ev_[kLibClasses + 1], pst), "hipEventRecord", err)) return false;
-    for (int c = 0; c <= kLibClasses; c++) {
-      const uint32_t cb = b.class_begin[c], ce = b.class_begin[c + 1];
-      if (ce == cb) continue;
-      fa.tiles = b.tile_list + cb;
-      const FusedFn fn = c < kLibClasses ? fused_lib_fn(c) : fused_fn(b.gm, vi);
-      if (!hip_ok(hipStreamWaitEvent(class_st_[c], class_ev_[kLibClasses + 1], 0), "hipStreamWaitEvent", err)) return false;
-      fn(ce - cb, class_st_[c], fa);
-      if (!hip_ok(hipGetLastError(), "match kernel launch", err) ||
-          !hip_ok(hipEventRecord(class_ev_[c], class_st_[c]), "hipEventRecord", err) ||
-          !hip_ok(hipStreamWaitEvent(pst, class_ev_[c], 0), "hipStreamWaitEvent", err))
-        return false;
-    }
-    return true;
-  }
   if (fused) {
     FusedArgs fa;
     fa.pa = pa;

@@ -1045,12 +1045,6 @@ enum : uint32_t {
   GM_DEB = 1u << CMP_DEB,
   GM_OS = GM_DEB | (1u << CMP_APK) | (1u << CMP_RPM),
   GM_ALL = 0x3FEu,
-  // single-ecosystem library sets: a library batch's tiles run the kernel of their grammar
-  GM_NPM = 1u << CMP_NPM,
-  GM_PEP = 1u << CMP_PEP440,
-  GM_GEN = (1u << CMP_GENERIC) | (1u << CMP_BITNAMI),
-  GM_GEM = 1u << CMP_GEM,
-  GM_MVN = 1u << CMP_MAVEN,
 };
 
 template <uint32_t GM, class Sink>

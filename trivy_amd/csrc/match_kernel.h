@@ -88,7 +88,6 @@ struct FusedArgs {
   SweepArgs sa;
   CopyOutArgs co;       // end-to-end pipeline: the previous chunk's result move ...
   uint32_t n_copy = 0;  // ... by workgroups [0, n_copy) of this launch (0: none)
-  const uint32_t* tiles = nullptr;  // workgroup w matches launch tile tiles[w] (nullptr: tile w); grammar-class launches
 };
 
 using ProbeFn = void (*)(uint32_t n_tiles, hipStream_t st, const ProbeArgs& a);
@@ -829,7 +828,7 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
     copy_out_tiles(fa.co, blockIdx.x, fa.n_copy, reinterpret_cast<uint32_t*>(buf));
     return;
   }
-  const uint32_t tid = threadIdx.x, t = fa.tiles ? fa.tiles[blockIdx.x - fa.n_copy] : blockIdx.x - fa.n_copy;
+  const uint32_t tid = threadIdx.x, t = blockIdx.x - fa.n_copy;
   const uint32_t p = t * kTile + tid;
   uint2 d = make_uint2(0xFFFFFFFFu, 0);
   if (p < a.n) d = a.pk[p];
@@ -897,11 +896,6 @@ constexpr FusedFn fused_entry() {
   if constexpr (F == 0) return nullptr;
   else if constexpr (F == 4) return &launch_fused<GM, K, MB, FILT, 0, 1, 1>;
   else if constexpr (F == 5) return &launch_fused<GM, K, MB, FILT, 0, 1, 3>;
-  // per-wave staging + segments with a smaller string window and match buffer, so that more
-  // tiles are resident per CU (dpkg-only batches; not built for the other grammar sets)
-  else if constexpr ((F == 6 || F == 7) && GM != GM_DEB) return nullptr;
-  else if constexpr (F == 6) return &launch_fused<GM, K, MB, FILT, 0, 6, 3, 8192>;
-  else if constexpr (F == 7) return &launch_fused<GM, K, MB, FILT, 0, 8, 3, 6144>;
   else return &launch_fused<GM, K, MB, FILT, (F >= 10 ? F - 10 : 0), TVM_FUSED_WPE(F)>;
 }
 

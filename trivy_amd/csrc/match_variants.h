@@ -12,9 +12,7 @@
   X(0, 2, 2048, "split_k2_m2048")      \
   X(0, 4, 2048, "split_k4_m2048")      \
   X(4, 4, 2400, "fused_k4_m2400_seg")  \
-  X(5, 4, 2400, "fused_k4_m2400_wseg")  \
-  X(6, 4, 1600, "fused_k4_m1600_wseg_s8k") \
-  X(7, 4, 1200, "fused_k4_m1200_wseg_s6k")
+  X(5, 4, 2400, "fused_k4_m2400_wseg")
 
 // Measurement-only variants (wrong match lists by construction): built only with
 // `make DIAG=1` (-DTVM_DIAG), never reachable in the product library.

@@ -85,8 +85,8 @@ __global__ __launch_bounds__(kTile) void order_kernel(OrderArgs a) {
 }
 
 __global__ __launch_bounds__(kTile) void copy_out_kernel(CopyOutArgs a) {
-  __shared__ uint32_t lds[kCopyLdsWords];
-  copy_out_tiles(a, blockIdx.x, gridDim.x, lds);
+  __shared__ uint4 lds[kCopyLdsWords / 4];  // 16-byte aligned: the delta staging is read as units
+  copy_out_tiles(a, blockIdx.x, gridDim.x, reinterpret_cast<uint32_t*>(lds));
 }
 
 }  // namespace

@@ -43,15 +43,22 @@ class Pipeline {
  public:
   ~Pipeline();
   // transport: send the batch in its transport form when it has one (see build_wire)
-  // packed: the result's advisory indices travel as 3 bytes each (the DB has < 2^24)
+  // packed: the result's advisory indices travel as 3 bytes each (the DB has < 2^24);
+  // delta (implies packed): the result travels in the delta form (delta_form.h), no CSR
   bool prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uint32_t chunk_packages, bool transport,
-               bool packed, std::string& err);
+               bool packed, bool delta, std::string& err);
   // One pass.  total = matches (> match_cap: nothing valid, re-prepare with a larger cap);
   // err_pkg = first poisoned package or -1.
   bool run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& err_pkg, uint64_t& err_bits, std::string& err);
   const uint32_t* adv() const { return adv_h_; }  // 4-byte indices, or 3-byte ones when packed()
   bool packed() const { return packed_; }
   const uint32_t* row_end() const { return row_end_h_; }
+  bool delta() const { return delta_; }
+  // the delta form of the last pass: the streams and the per-tile {count, bytes}
+  const uint8_t* delta_stream() const { return stream_h_; }
+  uint64_t delta_stream_size() const { return stream_bytes_; }
+  const uint2* delta_tiles() const { return tile_info_h_; }
+  uint32_t n_tiles() const { return bounds_.empty() ? 0 : bounds_.back(); }
   uint64_t cap() const { return cap_; }
   uint64_t h2d_bytes() const { return h2d_; }
   uint64_t d2h_bytes() const { return d2h_; }
@@ -96,6 +103,12 @@ class Pipeline {
   uint64_t wire_bytes_ = 0;                       // size of wire_h_ / wire_d_
   uint64_t adv_units_ = 0, row_end_units_ = 0;    // 16-byte units of adv_h_ / row_end_h_ (guards)
   bool prepared_ = false;
+  bool delta_ = false;
+  uint8_t* stream_h_ = nullptr;  // delta form (pinned) and the device addresses the result move stores through
+  uint8_t* stream_hd_ = nullptr;
+  uint64_t stream_bytes_ = 0;
+  uint2* tile_info_h_ = nullptr;
+  uint2* tile_info_hd_ = nullptr;
   bool packed_ = false;  // no Engine pointer: the batch may outlive a hot swap (the C-ABI checks the generation)
 };
 

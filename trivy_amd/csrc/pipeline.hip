@@ -187,8 +187,13 @@ void Pipeline::release() {
                   static_cast<void*>(row_end_d_)})
     pool_device_put(dev_, p);
   for (void* p : {static_cast<void*>(wire_h_), static_cast<void*>(raw_h_), static_cast<void*>(adv_h_),
-                  static_cast<void*>(row_end_h_), static_cast<void*>(ctl_h_)})
+                  static_cast<void*>(row_end_h_), static_cast<void*>(ctl_h_), static_cast<void*>(stream_h_),
+                  static_cast<void*>(tile_info_h_)})
     pool_host_put(p);
+  stream_h_ = stream_hd_ = nullptr;
+  tile_info_h_ = tile_info_hd_ = nullptr;
+  stream_bytes_ = 0;
+  delta_ = false;
   wire_h_ = nullptr;
   raw_h_ = nullptr;
   wire_bytes_ = 0;
@@ -213,7 +218,7 @@ void Pipeline::release() {
 }
 
 bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uint32_t chunk_packages, bool transport,
-                       bool packed, std::string& err) {
+                       bool packed, bool delta, std::string& err) {
   release();
   const auto start = std::chrono::steady_clock::now();
   dev_ = eng.device();
@@ -246,7 +251,8 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
   toff_ = hb.tile_off;  // per 64-package group, + the arena end, padded to whole tiles
   toff_.resize(size_t(n_tiles) * kGroupsPerTile + 1, hb.arena.size());
   cap_ = std::max<uint64_t>(match_cap, 1);
-  packed_ = packed;
+  packed_ = packed || delta;
+  delta_ = delta;
   if (cap_ >= (1ull << 32)) {
     err = "pipeline: row ends are 32-bit; split the batch below 2^32 matches";
     return false;
@@ -280,6 +286,22 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
   void* p = nullptr;
   if (!(p = pool_device_get(dev_, (size_t(nc) + 1) * 8, "hipMalloc(chunk bases)", err))) return false;
   chunk_base_d_ = static_cast<unsigned long long*>(p);
+  if (delta_) {  // the delta form: streams + tile info, written by the result move; no CSR buffers
+    stream_bytes_ = delta_stream_bytes(n_tiles, cap_);
+    if (!(p = pool_host_get(stream_bytes_, "hipHostMalloc(delta streams)", err))) return false;
+    stream_h_ = static_cast<uint8_t*>(p);
+    if (!ok(hipHostGetDevicePointer(&p, stream_h_, 0), "hipHostGetDevicePointer(delta streams)", err)) return false;
+    stream_hd_ = static_cast<uint8_t*>(p);
+    if (!(p = pool_host_get((size_t(n_tiles) + 2) * sizeof(uint2), "hipHostMalloc(tile info)", err))) return false;
+    tile_info_h_ = static_cast<uint2*>(p);
+    if (!ok(hipHostGetDevicePointer(&p, tile_info_h_, 0), "hipHostGetDevicePointer(tile info)", err)) return false;
+    tile_info_hd_ = static_cast<uint2*>(p);
+    if (!(p = pool_host_get(64, "hipHostMalloc(ctl)", err))) return false;
+    ctl_h_ = static_cast<unsigned long long*>(p);
+    prepared_ = true;
+    prepare_us_ = uint64_t(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - start).count());
+    return true;
+  }
   // the result lives in pinned host memory that the result move writes directly over PCIe
   // (measured, profiles/r03/pcie_probe.txt: kernel stores to host memory 55 GB/s, a DMA
   // device-to-host copy 28.6 GB/s; the DMA engine then only carries the batch upward)
@@ -323,7 +345,7 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
   // the result move leaves the row ends in HBM and the DMA engine carries them up on a third
   // stream while the kernels store the advisories (measured: 3.32 -> 3.20 ms per C2 pass; the
   // kernel stores alone reach 36-40 GB/s beside the match tiles)
-  constexpr bool rowend_dma = true;
+  const bool rowend_dma = !delta_;
   auto copy_args = [&](uint32_t c) {
     CopyOutArgs ca;
     ca.dir = m_.dir;
@@ -341,6 +363,10 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
     ca.adv_units = adv_units_;
     ca.row_end_units = row_end_units_;
     ca.ctl = m_.ctl;
+    ca.delta = delta_ ? 1u : 0u;
+    ca.stream_h = stream_hd_;
+    ca.stream_units = stream_bytes_ / 16;
+    ca.tile_info_h = tile_info_hd_;
     return ca;
   };
   // measurement only: TVM_PIPE_TRACE=1 prints the host time spent in each call of a pass;
@@ -442,7 +468,12 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
   if (trace) std::fprintf(stderr, "pipe ctl queued %.1f us\n", us());
   if (!ok(hipStreamSynchronize(s_k_), "pipeline", err) || !ok(hipStreamSynchronize(s_d2h_), "pipeline", err)) return false;
   if (trace) std::fprintf(stderr, "pipe done %.1f us\n", us());
-  d2h_ = uint64_t(n) * 4 + std::min<uint64_t>(ctl_h_[0], cap_) * (packed_ ? 3 : 4);
+  if (delta_) {
+    d2h_ = 0;
+    for (uint32_t t = 0; t < n_tiles(); t++) d2h_ += sizeof(uint2) + ((tile_info_h_[t].y + 15) & ~15u);
+  } else {
+    d2h_ = uint64_t(n) * 4 + std::min<uint64_t>(ctl_h_[0], cap_) * (packed_ ? 3 : 4);
+  }
   total = ctl_h_[0];
   err_pkg = ctl_h_[1] ? int64_t(n - ctl_h_[1]) : -1;
   err_bits = ctl_h_[3];

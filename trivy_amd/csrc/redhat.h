@@ -55,9 +55,11 @@ class RedHatMerge {
   // Enqueues the merge on `st` (no host synchronisation); the result stays in merged().
   bool launch(const RhInputs& in, hipStream_t st, std::string& err);
   const RhMerged& merged() const { return out_; }
+  // The batch's packages changed (a new upload): the per-tile Red Hat flags are recomputed.
+  void forget_tiles() { flags_valid_ = false; }
   // After launch: the merged list in (package, VulnerabilityID) order as host columns
   // (pkg, adv, base, grp) and the raw list's advisory column in raw positions (contrib);
-  // synchronises `st`.
+  // synchronises `st`.  grp is defined for the entries of Red Hat packages (the groups).
   bool fetch(const RhInputs& in, std::vector<uint32_t>& pkg, std::vector<uint32_t>& adv, std::vector<uint32_t>& base,
              std::vector<uint2>& grp, std::vector<uint32_t>& contrib, hipStream_t st, std::string& err);
 
@@ -67,6 +69,10 @@ class RedHatMerge {
   uint32_t* counts_ = nullptr;            // per tile: merged entries (rh_count_kernel)
   unsigned long long* bases_ = nullptr;   // per tile: output base (exclusive scan of counts_)
   uint8_t* flags_ = nullptr;              // per tile: 1 = holds Red Hat packages
+  bool flags_valid_ = false;              // flags_ holds the tiles of (flags_pk_, flags_n_, flags_plats_)
+  const uint2* flags_pk_ = nullptr;
+  const PlatInfo* flags_plats_ = nullptr;
+  uint32_t flags_n_ = 0;
   void* scan_tmp_ = nullptr;              // the scan's temporary storage
   size_t scan_tmp_bytes_ = 0;
   void release();
