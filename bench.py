@@ -141,11 +141,13 @@ class Mix:
             "c4": (sm.C4_PLATS, sm.C4_WEIGHTS, 20_000, 100_000_000),
             "c5": (sm.C5_PLATS, sm.C5_WEIGHTS, 12_000, 20_000_000)}[which]
         n = args.packages or n
+        if os.environ.get("TVM_BENCH_WEIGHTS"):  # measurement only: another platform mix (named in the workload)
+            weights = [float(x) for x in os.environ["TVM_BENCH_WEIGHTS"].split(",")]
         self.which, self.kpp = which, kpp
         self.sdb = sm.make_mix_db(plats, kpp)
         self.batch = sm.make_mix_batch(self.sdb, n, weights, seed=2)
         kind = {"c3": "lang", "c4": "os+lang", "c5": "rpm-apk"}[which]
-        self.name = f"{which}-{kind}-{n}"
+        self.name = f"{which}-{kind}-{n}" + (f"-w{os.environ['TVM_BENCH_WEIGHTS']}" if os.environ.get("TVM_BENCH_WEIGHTS") else "")
         self.n = len(self.batch)
         self.n_adv = self.sdb.n_adv
         self.n_keys = len(self.sdb.keys)
@@ -241,13 +243,15 @@ def cpu_model():
 
 
 def kernel_source_hash():
-    """sha1 over the sources the match kernels are compiled from (headers + kern_*.hip): ties a
+    """sha1 over the sources the match kernels are compiled from (their headers + kern_*.hip): ties a
     committed PMC summary to the build it was measured on."""
     import glob
     import hashlib
     h = hashlib.sha1()
     csrc = os.path.join(ROOT, "trivy_amd", "csrc")
-    for f in sorted(glob.glob(os.path.join(csrc, "*.h")) + glob.glob(os.path.join(csrc, "kern_*.hip"))):
+    # the match kernels' translation units and the headers they include (Makefile HDRS_KERN)
+    kern_hdrs = ["common.h", "engine.h", "libver.h", "verkey.h", "unicode_tab.h", "match_kernel.h", "match_variants.h"]
+    for f in sorted([os.path.join(csrc, h) for h in kern_hdrs] + glob.glob(os.path.join(csrc, "kern_*.hip"))):
         h.update(os.path.basename(f).encode())
         with open(f, "rb") as fh:
             h.update(fh.read())
@@ -484,9 +488,11 @@ def main():
                         "widen_ms": cdec}
         e2e = {"packages_per_s": wl.n / (med / 1e3), "ms_per_pass": med, "passes": npass,
                "result_form": "delta (TVM_PIPE_DELTA)" if delta else "CSR, 3-byte indices",
-               "decode_ms": dec, "packages_per_s_with_decode": wl.n / ((med + dec) / 1e3),
-               "decode_is": "tvm_pipeline_result on the host threads after the pass: the CSR (row ends + 4-byte "
-                            "indices) from the bytes that crossed the link",
+               "result_access_ms": dec,
+               "result_is": ("the CSR (row ends + 4-byte indices) in pinned host memory, decoded from the delta form by "
+                             "the host threads inside the pass, chunk by chunk behind the GPU" if delta else
+                             "3-byte indices + row ends in pinned host memory; tvm_pipeline_result widens the indices "
+                             "after the pass (result_access_ms)"),
                "csr_form": csr_form,
                "h2d_bytes": st["h2d_bytes"], "d2h_bytes": st["d2h_bytes"], "chunks": st["chunks"],
                "pcie_GBs": (st["h2d_bytes"] + st["d2h_bytes"]) / (med / 1e3) / 1e9,

@@ -316,8 +316,9 @@ int tvm_batch_upload_into(tvm_engine* e, tvm_batch* b, void* pkg_dev, void* adv_
 /* TVM_PIPE_DELTA: the per-package lists cross the link in the delta form
  * (trivy_amd/csrc/delta_form.h: per tile 256 count bytes, then each package's first advisory
  * index as 3 bytes and the next ones as 1-byte differences; ~1.4 bytes a match instead of 3
- * + a 4-byte row end per package); tvm_pipeline_result decodes it on the host threads, once
- * per pass.  Needs a DB of fewer than 2^24 advisories (not with TVM_PIPE_ADV32). */
+ * + a 4-byte row end per package), and tvm_pipeline_run decodes it into the CSR on the host
+ * threads chunk by chunk while the GPU works on the later chunks (the call's time includes
+ * it).  Needs a DB of fewer than 2^24 advisories (not with TVM_PIPE_ADV32). */
 enum { TVM_PIPE_RAW = 1, TVM_PIPE_ADV32 = 2, TVM_PIPE_DELTA = 4 };
 int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32_t chunk_packages, uint32_t flags,
                          char* err, size_t errlen);

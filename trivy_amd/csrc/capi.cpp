@@ -20,6 +20,7 @@
 #include "libver.h"
 #include "bbolt.h"
 #include "delta_form.h"
+#include "host_par.h"
 #include "pipeline.h"
 #include "pool.h"
 #include "sbom.h"
@@ -71,8 +72,7 @@ struct tvm_batch {
   uint32_t pkg_base = 0;               // tvm_batch_set_package_base
   uint64_t pipe_total = 0;
   uint64_t pipe_runs = 0, pipe_wide_for = ~0ull;  // passes run; the pass pipe_wide was widened for
-  std::vector<uint32_t> pipe_wide;                // 3-byte result indices widened / the delta form decoded (tvm_pipeline_result)
-  std::vector<uint32_t> pipe_rowend;              // the delta form's row ends (tvm_pipeline_result)
+  std::vector<uint32_t> pipe_wide;                // 3-byte result indices widened (tvm_pipeline_result)
   unsigned long long* order_scratch = nullptr;  // tvm_match_order_into: ticket + look-back word per tile
   uint32_t order_cap = 0;
   bool external_out = false;  // m.pkg / m.adv belong to the caller (tvm_batch_upload_into)
@@ -1405,23 +1405,7 @@ int tvm_pipeline_run(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* 
 
 int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row_end, uint64_t* n_matches) {
   if (!b || !b->pipe || b->pipe_total > b->pipe->cap()) return TVM_EINVAL;
-  if (b->pipe->delta()) {  // decode the delta form into the CSR once per pass (host threads, after the pass)
-    if (b->pipe_wide_for != b->pipe_runs) {
-      const Pipeline& P = *b->pipe;
-      b->pipe_wide.resize(std::max<uint64_t>(b->pipe_total, 1));
-      b->pipe_rowend.resize(std::max<size_t>(size_t(P.n_tiles()) * kTile, 1));
-      std::string msg;
-      if (!delta_decode(P.delta_stream(), P.delta_stream_size(), P.delta_tiles(), P.n_tiles(), b->pipe_total,
-                        b->pipe_wide.data(), b->pipe_rowend.data(), msg))
-        return TVM_EDEVICE;
-      b->pipe_wide_for = b->pipe_runs;
-    }
-    if (adv) *adv = b->pipe_wide.data();
-    if (row_end) *row_end = b->pipe_rowend.data();
-    if (n_matches) *n_matches = b->pipe_total;
-    return TVM_OK;
-  }
-  if (adv && b->pipe->packed()) {  // widen the 3-byte indices once per pass (host side, after the pass)
+  if (adv && b->pipe->packed() && !b->pipe->delta()) {  // widen the 3-byte indices once per pass (host side, after the pass)
     if (b->pipe_wide_for != b->pipe_runs) {
       const uint8_t* p = reinterpret_cast<const uint8_t*>(b->pipe->adv());
       b->pipe_wide.resize(b->pipe_total);
@@ -1617,6 +1601,19 @@ RhInputs rh_inputs(tvm_engine* e, tvm_batch* b) {
 bool rh_launch(tvm_engine* e, tvm_batch* b, std::string& err) {
   (void)hipSetDevice(e->device);
   if (!ensure_rh_rank(e, err)) return false;
+  if (!b->rh.tiles_known()) {  // once per upload: which tiles hold Red Hat packages
+    const auto& pi = e->eng->db().plat_info;
+    const size_t n = b->hb.pk.size();
+    std::vector<uint8_t> flags(b->dev.n_tiles, 0);
+    range_for(flags.size(), 64, [&](size_t t0, size_t t1) {
+      for (size_t t = t0; t < t1; t++)
+        for (size_t p = t * kTile; p < std::min(n, (t + 1) * kTile) && !flags[t]; p++) {
+          const uint32_t plat = b->hb.pk[p].x;
+          flags[t] = plat < pi.size() && pi[plat].drv == DRV_REDHAT;
+        }
+    });
+    if (!b->rh.set_tiles(flags, err)) return false;
+  }
   const RhInputs in = rh_inputs(e, b);
   if (!b->rh.launch(in, e->eng->stream(), err)) return false;
   b->merged = true;

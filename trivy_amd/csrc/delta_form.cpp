@@ -9,6 +9,65 @@
 
 namespace tvm {
 
+bool delta_decode_tile(const uint8_t* stream, uint64_t stream_bytes, uint32_t t, uint64_t pos0, uint2 info,
+                       uint32_t* adv, uint32_t* row_end) {
+  const uint64_t count = info.x, bytes = info.y;
+  uint32_t* re = row_end + size_t(t) * kTile;
+  if (count == 0) {
+    for (int p = 0; p < kTile; p++) re[p] = uint32_t(pos0);
+    return true;
+  }
+  const uint64_t r = delta_region(t, pos0);
+  if (bytes < kTile || r + bytes > stream_bytes) return false;
+  const uint8_t* h = stream + r;
+  const uint8_t* q = h + kTile;
+  const uint8_t* end = h + bytes;
+  uint32_t* o = adv + pos0;
+  uint32_t* const o_end = adv + pos0 + count;
+  for (int p = 0; p < kTile; p++) {
+    uint64_t k = h[p];
+    if (k == 255) {
+      if (end - q < 4) return false;
+      k = uint32_t(q[0]) | uint32_t(q[1]) << 8 | uint32_t(q[2]) << 16 | uint32_t(q[3]) << 24;
+      q += 4;
+    }
+    if (k) {
+      // every entry takes 1..4 bytes: the list fits when 4 k bytes are left, else check each
+      if (uint64_t(o_end - o) < k || end - q < 3) return false;
+      uint32_t a = uint32_t(q[0]) | uint32_t(q[1]) << 8 | uint32_t(q[2]) << 16;
+      q += 3;
+      *o++ = a;
+      if (uint64_t(end - q) >= 4 * (k - 1)) {
+        for (uint64_t j = 1; j < k; j++) {
+          const uint8_t x = *q++;
+          if (x) {
+            a += x;
+          } else {
+            a = uint32_t(q[0]) | uint32_t(q[1]) << 8 | uint32_t(q[2]) << 16;
+            q += 3;
+          }
+          *o++ = a;
+        }
+      } else {
+        for (uint64_t j = 1; j < k; j++) {
+          if (q >= end) return false;
+          const uint8_t x = *q++;
+          if (x) {
+            a += x;
+          } else {
+            if (end - q < 3) return false;
+            a = uint32_t(q[0]) | uint32_t(q[1]) << 8 | uint32_t(q[2]) << 16;
+            q += 3;
+          }
+          *o++ = a;
+        }
+      }
+    }
+    re[p] = uint32_t(o - adv);
+  }
+  return o == o_end && q == end;
+}
+
 bool delta_decode(const uint8_t* stream, uint64_t stream_bytes, const uint2* tile_info, uint32_t n_tiles,
                   uint64_t total, uint32_t* adv, uint32_t* row_end, std::string& err) {
   std::vector<uint64_t> b(size_t(n_tiles) + 1, 0);
@@ -19,65 +78,8 @@ bool delta_decode(const uint8_t* stream, uint64_t stream_bytes, const uint2* til
   }
   std::atomic<bool> bad{false};
   range_for(n_tiles, 64, [&](size_t t0, size_t t1) {
-    for (size_t t = t0; t < t1 && !bad.load(std::memory_order_relaxed); t++) {
-      const uint64_t pos0 = b[t], count = tile_info[t].x, bytes = tile_info[t].y;
-      uint32_t* re = row_end + t * kTile;
-      if (count == 0) {
-        for (int p = 0; p < kTile; p++) re[p] = uint32_t(pos0);
-        continue;
-      }
-      const uint64_t r = delta_region(uint32_t(t), pos0);
-      if (bytes < kTile || r + bytes > stream_bytes) {
-        bad = true;
-        break;
-      }
-      const uint8_t* h = stream + r;
-      const uint8_t* q = h + kTile;
-      const uint8_t* end = h + bytes;
-      uint32_t* o = adv + pos0;
-      uint32_t* const o_end = adv + pos0 + count;
-      for (int p = 0; p < kTile; p++) {
-        uint64_t k = h[p];
-        if (k == 255) {
-          if (end - q < 4) {
-            bad = true;
-            break;
-          }
-          k = uint32_t(q[0]) | uint32_t(q[1]) << 8 | uint32_t(q[2]) << 16 | uint32_t(q[3]) << 24;
-          q += 4;
-        }
-        if (k) {
-          if (uint64_t(o_end - o) < k || end - q < 3) {
-            bad = true;
-            break;
-          }
-          uint32_t a = uint32_t(q[0]) | uint32_t(q[1]) << 8 | uint32_t(q[2]) << 16;
-          q += 3;
-          *o++ = a;
-          for (uint64_t j = 1; j < k; j++) {
-            if (q >= end) {
-              bad = true;
-              break;
-            }
-            const uint8_t x = *q++;
-            if (x) {
-              a += x;
-            } else {
-              if (end - q < 3) {
-                bad = true;
-                break;
-              }
-              a = uint32_t(q[0]) | uint32_t(q[1]) << 8 | uint32_t(q[2]) << 16;
-              q += 3;
-            }
-            *o++ = a;
-          }
-          if (bad.load(std::memory_order_relaxed)) break;
-        }
-        re[p] = uint32_t(o - adv);
-      }
-      if (o != o_end || q != end) bad = true;
-    }
+    for (size_t t = t0; t < t1 && !bad.load(std::memory_order_relaxed); t++)
+      if (!delta_decode_tile(stream, stream_bytes, uint32_t(t), b[t], tile_info[t], adv, row_end)) bad = true;
   });
   if (bad) {
     err = "delta form: a tile's stream is inconsistent with its count";

@@ -26,5 +26,9 @@ namespace tvm {
 // host threads.  false (err set) when the streams are inconsistent with tile_info / total.
 bool delta_decode(const uint8_t* stream, uint64_t stream_bytes, const uint2* tile_info, uint32_t n_tiles,
                   uint64_t total, uint32_t* adv, uint32_t* row_end, std::string& err);
+// One tile (info = its {count, bytes}, pos0 = the CSR position of its first match): its 256
+// row ends and its advisories; false when its stream is inconsistent with info.
+bool delta_decode_tile(const uint8_t* stream, uint64_t stream_bytes, uint32_t t, uint64_t pos0, uint2 info,
+                       uint32_t* adv, uint32_t* row_end);
 
 }  // namespace tvm

@@ -2,8 +2,11 @@
 #pragma once
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <utility>
 #include <vector>
@@ -59,5 +62,64 @@ inline void par_memcpy(void* dst, const void* src, size_t bytes) {
     std::memcpy(static_cast<char*>(dst) + a, static_cast<const char*>(src) + a, b - a);
   });
 }
+
+// A process-wide pool of host_threads() - 1 parked threads for work that recurs many times
+// per call (the pipeline's per-chunk result decode: spawning threads per chunk cost more than
+// the decode).  One job at a time; the caller takes part.
+class WorkerPool {
+ public:
+  static WorkerPool& get() {
+    static WorkerPool* p = new WorkerPool(host_threads());  // never destroyed: its threads stay parked
+    return *p;
+  }
+  int size() const { return n_ + 1; }
+  // f(i) for i in [0, n), handed out one at a time
+  void parallel_for(size_t n, const std::function<void(size_t)>& f) {
+    if (n == 0) return;
+    std::lock_guard<std::mutex> one(job_mu_);
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = &f;
+      total_ = n;
+      next_.store(0, std::memory_order_relaxed);
+      busy_ = n_;
+      gen_++;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return busy_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  explicit WorkerPool(int threads) : n_(std::max(0, threads - 1)) {
+    for (int i = 0; i < n_; i++) std::thread([this] { loop(); }).detach();
+  }
+  void work() {
+    for (size_t i; (i = next_.fetch_add(1, std::memory_order_relaxed)) < total_;) (*job_)(i);
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+      }
+      work();
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--busy_ == 0) done_cv_.notify_one();
+    }
+  }
+  const int n_;
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(size_t)>* job_ = nullptr;
+  size_t total_ = 0;
+  std::atomic<size_t> next_{0};
+  int busy_ = 0;
+  uint64_t gen_ = 0;
+};
 
 }  // namespace tvm

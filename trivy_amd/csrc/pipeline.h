@@ -44,13 +44,14 @@ class Pipeline {
   ~Pipeline();
   // transport: send the batch in its transport form when it has one (see build_wire)
   // packed: the result's advisory indices travel as 3 bytes each (the DB has < 2^24);
-  // delta (implies packed): the result travels in the delta form (delta_form.h), no CSR
+  // delta (implies packed): the result travels in the delta form (delta_form.h) and run()
+  // decodes it into the CSR on the host threads chunk by chunk, overlapping the GPU
   bool prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uint32_t chunk_packages, bool transport,
                bool packed, bool delta, std::string& err);
   // One pass.  total = matches (> match_cap: nothing valid, re-prepare with a larger cap);
   // err_pkg = first poisoned package or -1.
   bool run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& err_pkg, uint64_t& err_bits, std::string& err);
-  const uint32_t* adv() const { return adv_h_; }  // 4-byte indices, or 3-byte ones when packed()
+  const uint32_t* adv() const { return adv_h_; }  // 4-byte indices, or 3-byte ones when packed() and not delta()
   bool packed() const { return packed_; }
   const uint32_t* row_end() const { return row_end_h_; }
   bool delta() const { return delta_; }
@@ -109,6 +110,7 @@ class Pipeline {
   uint64_t stream_bytes_ = 0;
   uint2* tile_info_h_ = nullptr;
   uint2* tile_info_hd_ = nullptr;
+  std::vector<uint64_t> tile_pos_;  // CSR position of each tile's first match (the decode)
   bool packed_ = false;  // no Engine pointer: the batch may outlive a hot swap (the C-ABI checks the generation)
 };
 

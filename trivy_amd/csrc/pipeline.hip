@@ -2,6 +2,7 @@
 // and the order kernel's direct writes of the result into host memory overlap chunk by chunk.  Every buffer is sized once in prepare(); a pass
 // allocates nothing.
 #include "pipeline.h"
+#include "delta_form.h"
 #include "host_par.h"
 #include "pool.h"
 #include "wire.h"
@@ -296,6 +297,14 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
     tile_info_h_ = static_cast<uint2*>(p);
     if (!ok(hipHostGetDevicePointer(&p, tile_info_h_, 0), "hipHostGetDevicePointer(tile info)", err)) return false;
     tile_info_hd_ = static_cast<uint2*>(p);
+    // the CSR the pass decodes the streams into, chunk by chunk (pooled: a fresh batch of a
+    // size seen before touches no new pages)
+    const size_t cap4 = (cap_ + 3) & ~size_t(3), n4 = (size_t(n_tiles) * kTile + 3) & ~size_t(3);
+    if (!(p = pool_host_get(cap4 * 4, "hipHostMalloc(adv)", err))) return false;
+    adv_h_ = static_cast<uint32_t*>(p);
+    if (!(p = pool_host_get(std::max<size_t>(n4, 4) * 4, "hipHostMalloc(row ends)", err))) return false;
+    row_end_h_ = static_cast<uint32_t*>(p);
+    tile_pos_.assign(size_t(n_tiles) + 1, 0);
     if (!(p = pool_host_get(64, "hipHostMalloc(ctl)", err))) return false;
     ctl_h_ = static_cast<unsigned long long*>(p);
     prepared_ = true;
@@ -374,9 +383,10 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
   static const bool trace = std::getenv("TVM_PIPE_TRACE") != nullptr;
   static const bool copies_first = std::getenv("TVM_PIPE_COPIES_FIRST") != nullptr;
   static const bool unpack_on_copy = std::getenv("TVM_PIPE_UNPACK_ON_COPY") != nullptr && !copies_first;
-  // the DMA engine carries chunk c's row ends up (third stream) once its result move is done
+  // chunk c's result move is done (ev_k_[c]): the DMA engine carries its row ends up (third
+  // stream), or the host decodes its delta streams
   auto rowend_up = [&](uint32_t c) {
-    if (!rowend_dma) return true;
+    if (!rowend_dma) return ok(hipEventRecord(ev_k_[c], s_k_), "hipEventRecord", err);
     const size_t q0 = size_t(bounds_[c]) * kTile, q1 = size_t(bounds_[c + 1]) * kTile;
     return ok(hipEventRecord(ev_k_[c], s_k_), "hipEventRecord", err) &&
            ok(hipStreamWaitEvent(s_d2h_, ev_k_[c], 0), "hipStreamWaitEvent", err) &&
@@ -466,6 +476,35 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
   }
   if (!ok(hipMemcpyAsync(ctl_h_, m_.ctl, 64, hipMemcpyDeviceToHost, s_k_), "D2H ctl", err)) return false;
   if (trace) std::fprintf(stderr, "pipe ctl queued %.1f us\n", us());
+  // the delta form: the host threads decode each chunk's streams into the CSR as soon as its
+  // result move is done, while the GPU works on the chunks after it
+  bool decoded = true;
+  if (delta_) {
+    uint64_t pos = 0;
+    for (uint32_t c = 0; c < nc && decoded; c++) {
+      const uint32_t t0 = bounds_[c], t1 = bounds_[c + 1];
+      if (t1 == t0) continue;
+      if (!ok(hipEventSynchronize(ev_k_[c]), "pipeline", err)) return false;
+      for (uint32_t t = t0; t < t1; t++) {
+        tile_pos_[t] = pos;
+        pos += tile_info_h_[t].x;
+      }
+      if (pos > cap_) {  // an overflowed pass: its streams are incomplete, the total says so below
+        decoded = false;
+        break;
+      }
+      std::atomic<bool> bad{false};
+      constexpr uint32_t kPiece = 16;  // tiles per work item
+      WorkerPool::get().parallel_for((t1 - t0 + kPiece - 1) / kPiece, [&](size_t k) {
+        const uint32_t a0 = t0 + uint32_t(k) * kPiece, a1 = std::min(t1, a0 + kPiece);
+        for (uint32_t t = a0; t < a1; t++)
+          if (!delta_decode_tile(stream_h_, stream_bytes_, t, tile_pos_[t], tile_info_h_[t], adv_h_, row_end_h_))
+            bad = true;
+      });
+      if (bad) decoded = false;
+      if (trace) std::fprintf(stderr, "pipe c%u decoded %.1f us\n", c, us());
+    }
+  }
   if (!ok(hipStreamSynchronize(s_k_), "pipeline", err) || !ok(hipStreamSynchronize(s_d2h_), "pipeline", err)) return false;
   if (trace) std::fprintf(stderr, "pipe done %.1f us\n", us());
   if (delta_) {
@@ -473,6 +512,10 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
     for (uint32_t t = 0; t < n_tiles(); t++) d2h_ += sizeof(uint2) + ((tile_info_h_[t].y + 15) & ~15u);
   } else {
     d2h_ = uint64_t(n) * 4 + std::min<uint64_t>(ctl_h_[0], cap_) * (packed_ ? 3 : 4);
+  }
+  if (delta_ && !decoded && ctl_h_[0] <= cap_ && !ctl_h_[3] && !ctl_h_[1]) {
+    err = "pipeline: the delta form of the result is inconsistent with the tiles' counts";
+    return false;
   }
   total = ctl_h_[0];
   err_pkg = ctl_h_[1] ? int64_t(n - ctl_h_[1]) : -1;

@@ -55,8 +55,12 @@ class RedHatMerge {
   // Enqueues the merge on `st` (no host synchronisation); the result stays in merged().
   bool launch(const RhInputs& in, hipStream_t st, std::string& err);
   const RhMerged& merged() const { return out_; }
-  // The batch's packages changed (a new upload): the per-tile Red Hat flags are recomputed.
-  void forget_tiles() { flags_valid_ = false; }
+  // Which of the batch's tiles hold Red Hat packages (flags[t] = 1), computed on the host
+  // once per upload (the caller holds the packages' platforms): the merge's kernels give those
+  // tiles a workgroup each and pass the others' pairs through a wave per tile.
+  bool set_tiles(const std::vector<uint8_t>& flags, std::string& err);
+  bool tiles_known() const { return tiles_known_; }
+  void forget_tiles() { tiles_known_ = false; }  // the batch's packages changed (a new upload)
   // After launch: the merged list in (package, VulnerabilityID) order as host columns
   // (pkg, adv, base, grp) and the raw list's advisory column in raw positions (contrib);
   // synchronises `st`.  grp is defined for the entries of Red Hat packages (the groups).
@@ -68,11 +72,13 @@ class RedHatMerge {
   RhMerged out_;
   uint32_t* counts_ = nullptr;            // per tile: merged entries (rh_count_kernel)
   unsigned long long* bases_ = nullptr;   // per tile: output base (exclusive scan of counts_)
-  uint8_t* flags_ = nullptr;              // per tile: 1 = holds Red Hat packages
-  bool flags_valid_ = false;              // flags_ holds the tiles of (flags_pk_, flags_n_, flags_plats_)
-  const uint2* flags_pk_ = nullptr;
-  const PlatInfo* flags_plats_ = nullptr;
-  uint32_t flags_n_ = 0;
+  // the batch's tiles (set_tiles): per tile 1 = holds Red Hat packages, and their list
+  uint8_t* flags_ = nullptr;
+  uint32_t* rh_list_ = nullptr;
+  uint32_t n_rh_ = 0;
+  size_t flags_cap_ = 0;
+  int tiles_dev_ = -1;
+  bool tiles_known_ = false;
   void* scan_tmp_ = nullptr;              // the scan's temporary storage
   size_t scan_tmp_bytes_ = 0;
   void release();

@@ -81,38 +81,34 @@ __device__ __forceinline__ uint32_t block_flag_scan(bool f, uint32_t tid, uint32
   return tot;
 }
 
-// Does tile t hold a Red Hat package?  (Tiles without one pass their pairs through.)
-__device__ __forceinline__ bool tile_has_redhat(const MergeArgs& a, uint32_t t, uint32_t tid) {
-  const uint32_t p = t * kBlock + tid;
-  const uint32_t plat = p < a.n ? a.pk[p].x : 0xFFFFFFFFu;
-  return __syncthreads_or(plat < a.n_plats && a.plats[plat].drv == DRV_REDHAT) != 0;
-}
-
-// Pass 1: the merged entry count of every tile (the groups of its segment) into counts[t].
-// The tiles' output bases then come from a scan (rocPRIM), not from an atomic reservation
-// per tile: 78k same-address atomics serialised the round-3 kernel (C5: 0.95 ms,
-// SQ_WAIT_ANY / SQ_WAVE_CYCLES = 0.95).  KNOWN: rh_flags already holds the batch's per-tile
-// Red Hat flags (an earlier merge of the same upload), so a tile without Red Hat packages
-// reads its directory entry only, not its packages.
-template <bool KNOWN>
-__global__ __launch_bounds__(kBlock) void rh_count_kernel(MergeArgs a, uint32_t* counts, uint8_t* rh_flags) {
+// Pass 1: the merged entry count of every tile into counts[t].  The tiles' output bases then
+// come from a scan (rocPRIM), not from an atomic reservation per tile: 78k same-address
+// atomics serialised the round-3 kernel (C5: 0.95 ms, SQ_WAIT_ANY / SQ_WAVE_CYCLES = 0.95).
+// Workgroups [0, n_rh) take the tiles that hold Red Hat packages (rh_list: the groups of
+// their segments, a block scan per 256 pairs); the rest one lane per tile for all others,
+// whose pairs are groups of one (a workgroup per such tile spent its time being dispatched).
+__global__ __launch_bounds__(kBlock) void rh_count_kernel(MergeArgs a, uint32_t* counts, const uint8_t* rh_flags,
+                                                          const uint32_t* rh_list, uint32_t n_rh, uint32_t n_tiles) {
   __shared__ uint32_t ws[kWaves];
-  const uint32_t t = blockIdx.x, tid = threadIdx.x;
+  const uint32_t tid = threadIdx.x;
+  if (blockIdx.x >= n_rh) {
+    const uint32_t t = (blockIdx.x - n_rh) * kBlock + tid;
+    if (t >= n_tiles || rh_flags[t]) return;
+    const TileDir d = a.dir[t];
+    const bool fits = d.base + d.count <= a.raw_cap;
+    counts[t] = fits ? d.count : 0u;
+    if (!fits) atomicOr(a.mctl + 3, 1ull);  // an overflowed match list: nothing valid to merge
+    return;
+  }
+  const uint32_t t = rh_list[blockIdx.x];
   const TileDir d = a.dir[t];
   const uint64_t b0 = d.base;
   const uint32_t cnt = d.count;
-  if (b0 + cnt > a.raw_cap) {  // an overflowed match list: nothing valid to merge
+  if (b0 + cnt > a.raw_cap) {
     if (tid == 0) {
       counts[t] = 0;
-      rh_flags[t] = 0;
       atomicOr(a.mctl + 3, 1ull);
     }
-    return;
-  }
-  const bool rh = KNOWN ? rh_flags[t] != 0 : tile_has_redhat(a, t, tid);
-  if (!rh) {  // every pair its own group
-    if (tid == 0) counts[t] = cnt;
-    if (!KNOWN && tid == 0) rh_flags[t] = 0;
     return;
   }
   uint32_t heads = 0;
@@ -136,50 +132,49 @@ __global__ __launch_bounds__(kBlock) void rh_count_kernel(MergeArgs a, uint32_t*
     heads += block_flag_scan(h, tid, ws, ex);
   }
   if (order_bad) atomicOr(a.mctl + 3, (unsigned long long)ERR_RH_ORDER);
-  if (tid == 0) {
-    counts[t] = heads;
-    if (!KNOWN) rh_flags[t] = 1;
-  }
+  if (tid == 0) counts[t] = heads;
 }
 
 // The tiles' output bases: an exclusive scan of the counts (rocPRIM's single-pass decoupled
-// look-back scan, RedHatMerge::launch); the last tile writes the total.
+// look-back scan, RedHatMerge::launch).
 
-// Pass 2: each tile writes its merged entries at its base: a coalesced copy for a tile
-// without Red Hat packages, else one entry per group (the member with the greatest fixed
-// version; ties keep the first, as LessThan does).  The member range (grp) is written for
-// the tiles with Red Hat packages only: its one reader is the host's Red Hat vulnerability
-// build (rh_vulns), which reads it for Red Hat packages only, so a pass-through tile moves
-// 8 bytes in and 12 out per pair, not 20.
+// Pass 2: each tile writes its merged entries at its base.  Workgroups [0, n_rh): the Red Hat
+// tiles, one entry per group (the member with the greatest fixed version; ties keep the
+// first, as LessThan does) and its member range (grp), which only the host's Red Hat
+// vulnerability build reads (rh_vulns, for Red Hat packages).  The rest: one wave per tile,
+// a coalesced copy (pairs pass through as groups of one: 8 bytes in, 12 out per pair).  The
+// tile directory entry and, at the last tile, the merged total go with the tile.
 __global__ __launch_bounds__(kBlock) void rh_emit_kernel(MergeArgs a, const uint32_t* counts,
                                                          const unsigned long long* bases, const uint8_t* rh_flags,
-                                                         uint32_t n_tiles) {
+                                                         const uint32_t* rh_list, uint32_t n_rh, uint32_t n_tiles) {
   __shared__ uint32_t ws[kWaves];
-  const uint32_t t = blockIdx.x, tid = threadIdx.x;
-  const TileDir d = a.dir[t];
-  const uint64_t b0 = d.base;
-  const uint32_t cnt = d.count;
-  const unsigned long long o0 = bases[t];
-  const uint32_t heads = counts[t];
-  const bool fits = b0 + cnt <= a.raw_cap && o0 + heads <= a.mcap;
-  if (tid == 0) {
-    a.mdir[t] = TileDir{o0, fits ? heads : 0u, 0};
-    if (t + 1 == n_tiles) a.mctl[0] = o0 + heads;  // the merged total
-  }
-  if (!fits) return;  // cannot happen (merged <= raw); the counts tell the host
-  if (!rh_flags[t]) {
+  const uint32_t tid = threadIdx.x;
+  if (blockIdx.x >= n_rh) {
+    const uint32_t lane = tid & 63, t = (blockIdx.x - n_rh) * kWaves + (tid >> 6);
+    if (t >= n_tiles || rh_flags[t]) return;
+    const TileDir d = a.dir[t];
+    const uint64_t b0 = d.base;
+    const uint32_t cnt = d.count;
+    const unsigned long long o0 = bases[t];
+    const uint32_t heads = counts[t];
+    const bool fits = b0 + cnt <= a.raw_cap && o0 + heads <= a.mcap;
+    if (lane == 0) {
+      a.mdir[t] = TileDir{o0, fits ? heads : 0u, 0};
+      if (t + 1 == n_tiles) a.mctl[0] = o0 + heads;  // the merged total
+    }
+    if (!fits) return;
     constexpr int kU = 4;  // loads of four pairs in flight per lane before the stores
-    for (uint32_t c = 0; c < cnt; c += kU * kBlock) {
+    for (uint32_t c = 0; c < cnt; c += kU * 64) {
       uint32_t pp[kU], aa[kU];
 #pragma unroll
       for (int u = 0; u < kU; u++) {
-        const uint32_t i = c + u * kBlock + tid;
+        const uint32_t i = c + u * 64 + lane;
         pp[u] = i < cnt ? a.pkg[b0 + i] : 0u;
         aa[u] = i < cnt ? a.adv[b0 + i] : 0u;
       }
 #pragma unroll
       for (int u = 0; u < kU; u++) {
-        const uint32_t i = c + u * kBlock + tid;
+        const uint32_t i = c + u * 64 + lane;
         if (i < cnt) {
           a.mpkg[o0 + i] = pp[u];
           a.madv[o0 + i] = aa[u];
@@ -189,6 +184,18 @@ __global__ __launch_bounds__(kBlock) void rh_emit_kernel(MergeArgs a, const uint
     }
     return;
   }
+  const uint32_t t = rh_list[blockIdx.x];
+  const TileDir d = a.dir[t];
+  const uint64_t b0 = d.base;
+  const uint32_t cnt = d.count;
+  const unsigned long long o0 = bases[t];
+  const uint32_t heads = counts[t];
+  const bool fits = b0 + cnt <= a.raw_cap && o0 + heads <= a.mcap;
+  if (tid == 0) {
+    a.mdir[t] = TileDir{o0, fits ? heads : 0u, 0};
+    if (t + 1 == n_tiles) a.mctl[0] = o0 + heads;
+  }
+  if (!fits) return;  // cannot happen (merged <= raw); the counts tell the host
   uint32_t done = 0;
   for (uint32_t c = 0; c < cnt; c += kBlock) {
     bool h = false;
@@ -239,18 +246,58 @@ void RedHatMerge::release() {
   Engine::free_matches(dev_, out_.m);
   if (out_.base) (void)hipFree(out_.base);
   if (out_.grp) (void)hipFree(out_.grp);
-  for (void* x : {static_cast<void*>(counts_), static_cast<void*>(bases_), static_cast<void*>(flags_), scan_tmp_})
+  for (void* x : {static_cast<void*>(counts_), static_cast<void*>(bases_), scan_tmp_})
     if (x) (void)hipFree(x);
   counts_ = nullptr;
   bases_ = nullptr;
-  flags_ = nullptr;
-  flags_valid_ = false;
   scan_tmp_ = nullptr;
   scan_tmp_bytes_ = 0;
   out_ = RhMerged{};
 }
 
-RedHatMerge::~RedHatMerge() { release(); }
+RedHatMerge::~RedHatMerge() {
+  release();
+  if (tiles_dev_ >= 0) {
+    (void)hipSetDevice(tiles_dev_);
+    if (flags_) (void)hipFree(flags_);
+    if (rh_list_) (void)hipFree(rh_list_);
+  }
+}
+
+bool RedHatMerge::set_tiles(const std::vector<uint8_t>& flags, std::string& err) {
+  int dev = 0;
+  if (!ok(hipGetDevice(&dev), "hipGetDevice", err)) return false;
+  std::vector<uint32_t> list;
+  for (uint32_t t = 0; t < flags.size(); t++)
+    if (flags[t]) list.push_back(t);
+  if (flags.size() > flags_cap_ || dev != tiles_dev_) {
+    if (tiles_dev_ >= 0) {
+      (void)hipSetDevice(tiles_dev_);
+      if (flags_) (void)hipFree(flags_);
+      if (rh_list_) (void)hipFree(rh_list_);
+      (void)hipSetDevice(dev);
+    }
+    flags_ = nullptr;
+    rh_list_ = nullptr;
+    flags_cap_ = 0;
+    tiles_dev_ = dev;
+    void *f = nullptr, *l = nullptr;
+    const size_t cap = std::max<size_t>(flags.size(), 1);
+    if (!ok(hipMalloc(&f, cap), "hipMalloc(merge flags)", err) || !ok(hipMalloc(&l, cap * 4), "hipMalloc(merge list)", err)) {
+      if (f) (void)hipFree(f);
+      return false;
+    }
+    flags_ = static_cast<uint8_t*>(f);
+    rh_list_ = static_cast<uint32_t*>(l);
+    flags_cap_ = cap;
+  }
+  if ((!flags.empty() && !ok(hipMemcpy(flags_, flags.data(), flags.size(), hipMemcpyHostToDevice), "H2D merge flags", err)) ||
+      (!list.empty() && !ok(hipMemcpy(rh_list_, list.data(), list.size() * 4, hipMemcpyHostToDevice), "H2D merge list", err)))
+    return false;
+  n_rh_ = uint32_t(list.size());
+  tiles_known_ = true;
+  return true;
+}
 
 bool RedHatMerge::launch(const RhInputs& in, hipStream_t st, std::string& err) {
   const DevMatches& raw = *in.raw;
@@ -261,8 +308,7 @@ bool RedHatMerge::launch(const RhInputs& in, hipStream_t st, std::string& err) {
     dev_ = dev;
     const uint64_t cap = raw.cap;
     const uint32_t nt = std::max<uint32_t>(in.n_tiles, 1);
-    void *p = nullptr, *q = nullptr, *r = nullptr, *s = nullptr, *t = nullptr, *c = nullptr, *u = nullptr, *v = nullptr,
-         *f = nullptr;
+    void *p = nullptr, *q = nullptr, *r = nullptr, *s = nullptr, *t = nullptr, *c = nullptr, *u = nullptr, *v = nullptr;
     const bool good = ok(hipMalloc(&p, cap * 4), "hipMalloc(merged)", err) &&
                       ok(hipMalloc(&q, cap * 4), "hipMalloc(merged)", err) &&
                       ok(hipMalloc(&r, cap * 4), "hipMalloc(merged)", err) &&
@@ -270,11 +316,9 @@ bool RedHatMerge::launch(const RhInputs& in, hipStream_t st, std::string& err) {
                       ok(hipMalloc(&t, nt * sizeof(TileDir)), "hipMalloc(merged dir)", err) &&
                       ok(hipMalloc(&c, 64), "hipMalloc(merged ctl)", err) &&
                       ok(hipMalloc(&u, nt * 4), "hipMalloc(merge counts)", err) &&
-                      ok(hipMalloc(&v, nt * 8), "hipMalloc(merge bases)", err) &&
-                      ok(hipMalloc(&f, nt), "hipMalloc(merge flags)", err);
+                      ok(hipMalloc(&v, nt * 8), "hipMalloc(merge bases)", err);
     counts_ = static_cast<uint32_t*>(u);
     bases_ = static_cast<unsigned long long*>(v);
-    flags_ = static_cast<uint8_t*>(f);
     out_.m.pkg = static_cast<uint32_t*>(p);
     out_.m.adv = static_cast<uint32_t*>(q);
     out_.base = static_cast<uint32_t*>(r);
@@ -309,17 +353,13 @@ bool RedHatMerge::launch(const RhInputs& in, hipStream_t st, std::string& err) {
   a.mgrp = out_.grp;
   a.mcap = out_.cap;
   a.mctl = out_.m.ctl;
-  // the per-tile flags depend on the batch's packages and the platforms only: computed by the
-  // first merge after an upload, reused by the next ones
-  const bool known = flags_valid_ && flags_pk_ == in.pk && flags_plats_ == in.plats && flags_n_ == in.n;
-  if (known)
-    hipLaunchKernelGGL(rh_count_kernel<true>, dim3(in.n_tiles), dim3(kBlock), 0, st, a, counts_, flags_);
-  else
-    hipLaunchKernelGGL(rh_count_kernel<false>, dim3(in.n_tiles), dim3(kBlock), 0, st, a, counts_, flags_);
-  flags_valid_ = true;
-  flags_pk_ = in.pk;
-  flags_plats_ = in.plats;
-  flags_n_ = in.n;
+  if (!tiles_known_) {
+    err = "redhat merge: the batch's Red Hat tiles are not set (set_tiles)";
+    return false;
+  }
+  const uint32_t g_count = n_rh_ + (in.n_tiles + kBlock - 1) / kBlock, g_emit = n_rh_ + (in.n_tiles + kWaves - 1) / kWaves;
+  hipLaunchKernelGGL(rh_count_kernel, dim3(g_count), dim3(kBlock), 0, st, a, counts_, flags_, rh_list_, n_rh_,
+                     in.n_tiles);
   if (!ok(hipGetLastError(), "rh_count_kernel", err)) return false;
   size_t need = 0;
   if (!ok(rocprim::exclusive_scan(nullptr, need, counts_, bases_, 0ull, in.n_tiles,
@@ -337,7 +377,8 @@ bool RedHatMerge::launch(const RhInputs& in, hipStream_t st, std::string& err) {
                                   rocprim::plus<unsigned long long>(), st),
           "rocprim scan", err))
     return false;
-  hipLaunchKernelGGL(rh_emit_kernel, dim3(in.n_tiles), dim3(kBlock), 0, st, a, counts_, bases_, flags_, in.n_tiles);
+  hipLaunchKernelGGL(rh_emit_kernel, dim3(g_emit), dim3(kBlock), 0, st, a, counts_, bases_, flags_, rh_list_, n_rh_,
+                     in.n_tiles);
   return ok(hipGetLastError(), "rh_emit_kernel", err);
 }
 
