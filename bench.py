@@ -147,7 +147,8 @@ class Mix:
         self.sdb = sm.make_mix_db(plats, kpp)
         self.batch = sm.make_mix_batch(self.sdb, n, weights, seed=2)
         kind = {"c3": "lang", "c4": "os+lang", "c5": "rpm-apk"}[which]
-        self.name = f"{which}-{kind}-{n}" + (f"-w{os.environ['TVM_BENCH_WEIGHTS']}" if os.environ.get("TVM_BENCH_WEIGHTS") else "")
+        self.name = f"{which}-{kind}-{n}" + (f"-w{os.environ['TVM_BENCH_WEIGHTS']}" if os.environ.get("TVM_BENCH_WEIGHTS") else "") \
+            + (f"-mvnpre{os.environ['TVM_SYNTH_MAVEN_PRE']}" if os.environ.get("TVM_SYNTH_MAVEN_PRE") else "")
         self.n = len(self.batch)
         self.n_adv = self.sdb.n_adv
         self.n_keys = len(self.sdb.keys)

@@ -10,6 +10,7 @@ batch API (bucket + formatted version + attributes) and, for a sample, to the pe
 APIs and to the oracle (tests/test_gpu_mix.py).
 """
 import json
+import os
 
 import numpy as np
 
@@ -342,8 +343,8 @@ def make_mix_batch(db, n, weights, seed, miss=0.25, zipf=2.5):
                 v = np.where(pre < 0.03, _cat(v, b"-beta.", _s(rel)), v)
             elif kind == "pip":
                 v = np.where(pre < 0.03, _cat(v, b"rc", _s(rel)), np.where(pre < 0.05, _cat(v, b".post1"), v))
-            elif kind == "maven":
-                v = np.where(pre < 0.03, _cat(v, b"-rc", _s(rel)), v)
+            elif kind == "maven":  # TVM_SYNTH_MAVEN_PRE: another "-rcN" share (measurement only)
+                v = np.where(pre < float(os.environ.get("TVM_SYNTH_MAVEN_PRE", "0.03")), _cat(v, b"-rc", _s(rel)), v)
             elif kind == "go":
                 v = np.where(pre < 0.5, _cat(b"v", v), v)
             g["ver"] = g["version"] = v

@@ -81,6 +81,41 @@ __device__ __forceinline__ uint32_t block_flag_scan(bool f, uint32_t tid, uint32
   return tot;
 }
 
+// Per package of tile t: 1 = a Red Hat package (its pairs' group keys are their ID ranks).
+__device__ __forceinline__ void tile_redhat_flags(const MergeArgs& a, uint32_t t, uint32_t tid, uint8_t* rhp) {
+  const uint32_t p = t * kBlock + tid;
+  const uint32_t plat = p < a.n ? a.pk[p].x : 0xFFFFFFFFu;
+  rhp[tid] = plat < a.n_plats && a.plats[plat].drv == DRV_REDHAT;
+}
+
+// The lane's pair of chunk c of a tile segment [b0, b0 + cnt): package p, advisory ad and
+// its group key (the ID rank for a Red Hat package, kNoKey else; rhp: the tile's flags).
+__device__ __forceinline__ uint32_t chunk_key(const MergeArgs& a, uint64_t b0, uint32_t c, uint32_t cnt, uint32_t t,
+                                              uint32_t tid, const uint8_t* rhp, uint32_t& p, uint32_t& ad) {
+  if (c + tid >= cnt) return kNoKey;
+  p = a.pkg[b0 + c + tid];
+  ad = a.adv[b0 + c + tid];
+  return rhp[(p - a.pkg_base - t * kBlock) & (kBlock - 1)] ? a.adv_rank[ad].x : kNoKey;
+}
+
+// The (package, key) of the pair before the lane's: the lanes exchange them through LDS
+// (xp / xk); lane 0 takes the previous chunk's last pair (prev_*, advanced here to this
+// chunk's last pair), so each pair's key is gathered once, not again as its successor's
+// predecessor.  left = pairs of the segment from this chunk on.  The caller's next barrier
+// must come before the next chunk's call (block_flag_scan's).
+__device__ __forceinline__ void pair_before(uint32_t tid, uint32_t p, uint32_t k, uint32_t* xp, uint32_t* xk,
+                                            uint32_t& prev_p, uint32_t& prev_k, uint32_t left, uint32_t& pp,
+                                            uint32_t& kp) {
+  xp[tid] = p;
+  xk[tid] = k;
+  __syncthreads();
+  pp = tid ? xp[tid - 1] : prev_p;
+  kp = tid ? xk[tid - 1] : prev_k;
+  const uint32_t last = (left < uint32_t(kBlock) ? left : uint32_t(kBlock)) - 1;
+  prev_p = xp[last];
+  prev_k = xk[last];
+}
+
 // Pass 1: the merged entry count of every tile into counts[t].  The tiles' output bases then
 // come from a scan (rocPRIM), not from an atomic reservation per tile: 78k same-address
 // atomics serialised the round-3 kernel (C5: 0.95 ms, SQ_WAIT_ANY / SQ_WAVE_CYCLES = 0.95).
@@ -90,6 +125,8 @@ __device__ __forceinline__ uint32_t block_flag_scan(bool f, uint32_t tid, uint32
 __global__ __launch_bounds__(kBlock) void rh_count_kernel(MergeArgs a, uint32_t* counts, const uint8_t* rh_flags,
                                                           const uint32_t* rh_list, uint32_t n_rh, uint32_t n_tiles) {
   __shared__ uint32_t ws[kWaves];
+  __shared__ uint8_t rhp[kBlock];
+  __shared__ uint32_t xp[kBlock], xk[kBlock];
   const uint32_t tid = threadIdx.x;
   if (blockIdx.x >= n_rh) {
     const uint32_t t = (blockIdx.x - n_rh) * kBlock + tid;
@@ -101,6 +138,7 @@ __global__ __launch_bounds__(kBlock) void rh_count_kernel(MergeArgs a, uint32_t*
     return;
   }
   const uint32_t t = rh_list[blockIdx.x];
+  tile_redhat_flags(a, t, tid, rhp);
   const TileDir d = a.dir[t];
   const uint64_t b0 = d.base;
   const uint32_t cnt = d.count;
@@ -111,25 +149,23 @@ __global__ __launch_bounds__(kBlock) void rh_count_kernel(MergeArgs a, uint32_t*
     }
     return;
   }
-  uint32_t heads = 0;
+  __syncthreads();  // rhp
+  uint32_t heads = 0, prev_p = 0xFFFFFFFFu, prev_k = kNoKey;
   bool order_bad = false;
   for (uint32_t c = 0; c < cnt; c += kBlock) {
+    const bool v = c + tid < cnt;
+    uint32_t p = 0xFFFFFFFFu, ad = 0;
+    const uint32_t k = chunk_key(a, b0, c, cnt, t, tid, rhp, p, ad);
     bool h = false;
-    if (c + tid < cnt) {
-      const uint64_t i = b0 + c + tid;
-      const uint32_t p = a.pkg[i], k = group_key(a, p, a.adv[i]);
-      h = true;
-      if (k != kNoKey && c + tid > 0) {
-        const uint32_t pp = a.pkg[i - 1];
-        if (pp == p) {
-          const uint32_t kp = group_key(a, pp, a.adv[i - 1]);
-          h = kp != k;
-          order_bad |= kp > k;
-        }
-      }
+    uint32_t pp, kp;
+    pair_before(tid, p, k, xp, xk, prev_p, prev_k, cnt - c, pp, kp);
+    if (v) {
+      const bool cont = k != kNoKey && pp == p;
+      h = !(cont && kp == k);
+      order_bad |= cont && kp > k;
     }
     uint32_t ex;
-    heads += block_flag_scan(h, tid, ws, ex);
+    heads += block_flag_scan(h, tid, ws, ex);  // its barriers also order this chunk's xp / xk reads before the next writes
   }
   if (order_bad) atomicOr(a.mctl + 3, (unsigned long long)ERR_RH_ORDER);
   if (tid == 0) counts[t] = heads;
@@ -148,6 +184,8 @@ __global__ __launch_bounds__(kBlock) void rh_emit_kernel(MergeArgs a, const uint
                                                          const unsigned long long* bases, const uint8_t* rh_flags,
                                                          const uint32_t* rh_list, uint32_t n_rh, uint32_t n_tiles) {
   __shared__ uint32_t ws[kWaves];
+  __shared__ uint8_t rhp[kBlock];
+  __shared__ uint32_t xp[kBlock], xk[kBlock];
   const uint32_t tid = threadIdx.x;
   if (blockIdx.x >= n_rh) {
     const uint32_t lane = tid & 63, t = (blockIdx.x - n_rh) * kWaves + (tid >> 6);
@@ -185,6 +223,7 @@ __global__ __launch_bounds__(kBlock) void rh_emit_kernel(MergeArgs a, const uint
     return;
   }
   const uint32_t t = rh_list[blockIdx.x];
+  tile_redhat_flags(a, t, tid, rhp);
   const TileDir d = a.dir[t];
   const uint64_t b0 = d.base;
   const uint32_t cnt = d.count;
@@ -196,17 +235,16 @@ __global__ __launch_bounds__(kBlock) void rh_emit_kernel(MergeArgs a, const uint
     if (t + 1 == n_tiles) a.mctl[0] = o0 + heads;
   }
   if (!fits) return;  // cannot happen (merged <= raw); the counts tell the host
-  uint32_t done = 0;
+  __syncthreads();  // rhp
+  uint32_t done = 0, prev_p = 0xFFFFFFFFu, prev_k = kNoKey;
   for (uint32_t c = 0; c < cnt; c += kBlock) {
-    bool h = false;
-    uint32_t p = 0, ad = 0, k = kNoKey;
+    const bool v = c + tid < cnt;
     const uint64_t i = b0 + c + tid;
-    if (c + tid < cnt) {
-      p = a.pkg[i];
-      ad = a.adv[i];
-      k = group_key(a, p, ad);
-      h = k == kNoKey || c + tid == 0 || a.pkg[i - 1] != p || group_key(a, p, a.adv[i - 1]) != k;
-    }
+    uint32_t p = 0xFFFFFFFFu, ad = 0;
+    const uint32_t k = chunk_key(a, b0, c, cnt, t, tid, rhp, p, ad);
+    uint32_t pp, kp;
+    pair_before(tid, p, k, xp, xk, prev_p, prev_k, cnt - c, pp, kp);
+    const bool h = v && (k == kNoKey || pp != p || kp != k);
     uint32_t ex;
     const uint32_t n = block_flag_scan(h, tid, ws, ex);
     if (h) {
