@@ -1,13 +1,35 @@
 // Host decode of the delta result form (delta_form.h).
 #include "delta_form.h"
 
+#include <algorithm>
 #include <atomic>
+#include <cstring>
 #include <vector>
 
 #include "engine.h"
 #include "host_par.h"
 
 namespace tvm {
+
+namespace {
+
+// Leading non-zero bytes of q[0, n): 8 bytes per step (the lowest set bit of the SWAR
+// zero-byte mask is exact).
+inline uint64_t nonzero_prefix(const uint8_t* q, uint64_t n) {
+  uint64_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    std::memcpy(&w, q + i, 8);
+    const uint64_t z = (w - 0x0101010101010101ull) & ~w & 0x8080808080808080ull;
+    if (z) return i + (uint64_t(__builtin_ctzll(z)) >> 3);
+  }
+  while (i < n && q[i]) i++;
+  return i;
+}
+
+inline uint32_t le24(const uint8_t* q) { return uint32_t(q[0]) | uint32_t(q[1]) << 8 | uint32_t(q[2]) << 16; }
+
+}  // namespace
 
 bool delta_decode_tile(const uint8_t* stream, uint64_t stream_bytes, uint32_t t, uint64_t pos0, uint2 info,
                        uint32_t* adv, uint32_t* row_end) {
@@ -28,39 +50,32 @@ bool delta_decode_tile(const uint8_t* stream, uint64_t stream_bytes, uint32_t t,
     uint64_t k = h[p];
     if (k == 255) {
       if (end - q < 4) return false;
-      k = uint32_t(q[0]) | uint32_t(q[1]) << 8 | uint32_t(q[2]) << 16 | uint32_t(q[3]) << 24;
+      k = le24(q) | uint32_t(q[3]) << 24;
       q += 4;
     }
     if (k) {
-      // every entry takes 1..4 bytes: the list fits when 4 k bytes are left, else check each
       if (uint64_t(o_end - o) < k || end - q < 3) return false;
-      uint32_t a = uint32_t(q[0]) | uint32_t(q[1]) << 8 | uint32_t(q[2]) << 16;
+      uint32_t a = le24(q);
       q += 3;
       *o++ = a;
-      if (uint64_t(end - q) >= 4 * (k - 1)) {
-        for (uint64_t j = 1; j < k; j++) {
-          const uint8_t x = *q++;
-          if (x) {
-            a += x;
-          } else {
-            a = uint32_t(q[0]) | uint32_t(q[1]) << 8 | uint32_t(q[2]) << 16;
-            q += 3;
-          }
-          *o++ = a;
+      // the rest: runs of one-byte differences (a branch-free running sum), each ended by an
+      // escape (0 + 3 bytes) or by the list's end
+      uint64_t left = k - 1;
+      while (left) {
+        const uint64_t f = nonzero_prefix(q, std::min<uint64_t>(left, uint64_t(end - q)));
+        for (uint64_t i = 0; i < f; i++) {
+          a += q[i];
+          o[i] = a;
         }
-      } else {
-        for (uint64_t j = 1; j < k; j++) {
-          if (q >= end) return false;
-          const uint8_t x = *q++;
-          if (x) {
-            a += x;
-          } else {
-            if (end - q < 3) return false;
-            a = uint32_t(q[0]) | uint32_t(q[1]) << 8 | uint32_t(q[2]) << 16;
-            q += 3;
-          }
-          *o++ = a;
-        }
+        o += f;
+        q += f;
+        left -= f;
+        if (!left) break;
+        if (end - q < 4 || *q != 0) return false;
+        a = le24(q + 1);
+        q += 4;
+        *o++ = a;
+        left--;
       }
     }
     re[p] = uint32_t(o - adv);

@@ -96,7 +96,8 @@ using FusedFn = void (*)(uint32_t n_tiles, hipStream_t st, const FusedArgs& a);
 
 namespace {
 
-enum : uint32_t { KI_VALID = 1u << 31, KI_SPILL = 1u << 30, KI_LEN = 0x3FFFu, KI_CLS_SHIFT = 26, KI_CLS_MASK = 7u };
+// KI_MVN: a Maven package (its rows may carry pairwise programs: the sweep defers those)
+enum : uint32_t { KI_VALID = 1u << 31, KI_SPILL = 1u << 30, KI_MVN = 1u << 29, KI_LEN = 0x3FFFu, KI_CLS_SHIFT = 26, KI_CLS_MASK = 7u };
 
 // Block-wide exclusive scan of v over T lanes (wave shuffles + one LDS exchange); returns
 // the block total.  `wsum` holds T/64 words; two barriers.
@@ -288,6 +289,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
   }
   const uint32_t kl = hs.n;
   kinfo |= (kl & KI_LEN) | (valid ? KI_VALID : 0u) | ((cls & KI_CLS_MASK) << KI_CLS_SHIFT);
+  if (((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN) kinfo |= KI_MVN;
   r.k0 = valid && kl ? be_word(hs.w0, kl < 8 ? kl : 8) : 0ull;
   r.k1 = valid && kl > 8 ? be_word(hs.w1, kl < 16 ? kl - 8 : 8) : 0ull;
   uint32_t cnt = 0, rbeg = 0;
@@ -423,37 +425,46 @@ struct SweepShared {
 // FILT (the sweep's template flag): 0 no row filters, 1 filters without Maven programs (the OS
 // grammar set, whose rows never carry AUX_MVN: keeps the program evaluator's registers out of
 // that kernel), 2 all filters.
+// DEFER: a Maven program is not run here but reported (2) for the round's compacted
+// evaluation (sweep_programs); else 0 / 1 = the predicates fail / hold.
 template <int FILT>
-__device__ __forceinline__ bool aux_pass(const SweepArgs& a, uint32_t ridx, uint2 pa, uint32_t ki, uint32_t p) {
+__device__ __forceinline__ bool mvn_pair(const SweepArgs& a, const uint32_t* ids, uint32_t p) {
+  // the installed parse packed by probe_one, the program's packed bounds
+  const uint4 t = a.tail[p];
+  const MvnPackedView V{reinterpret_cast<const uint32_t*>(a.spill + t.x), int(t.y & 0xFFFFu),
+                        a.arena + (uint64_t(t.z) | (uint64_t(t.w) << 32))};
+  return mvn_program_eval(ids, V);
+}
+
+template <int FILT, bool DEFER = false>
+__device__ __forceinline__ uint32_t aux_pass(const SweepArgs& a, uint32_t ridx, uint2 pa, uint32_t ki, uint32_t p) {
   const RowAux x = a.db.aux[ridx];
   const uint32_t* ids = a.db.aux_ids + x.list_off;
   // the class first: a Maven hybrid program row is rejected for numeric versions before its
   // program would run
-  if ((x.kind & AUX_CLASS) && !((x.tag >> ((ki >> KI_CLS_SHIFT) & KI_CLS_MASK)) & 1u)) return false;
-  if (FILT >= 2 && (x.kind & AUX_MVN)) {  // the installed parse packed by probe_one, the program's packed bounds
-    const uint4 t = a.tail[p];
-    const MvnPackedView V{reinterpret_cast<const uint32_t*>(a.spill + t.x), int(t.y & 0xFFFFu),
-                          a.arena + (uint64_t(t.z) | (uint64_t(t.w) << 32))};
-    return mvn_program_eval(ids, V);
+  if ((x.kind & AUX_CLASS) && !((x.tag >> ((ki >> KI_CLS_SHIFT) & KI_CLS_MASK)) & 1u)) return 0;
+  if (FILT >= 2 && (x.kind & AUX_MVN)) {
+    if constexpr (DEFER) return 2;
+    return mvn_pair<FILT>(a, ids, p) ? 1u : 0u;
   }
   if (x.kind & (AUX_ARCH_RH | AUX_ARCH_IN)) {
     bool ok = (x.kind & AUX_ARCH_RH) && (x.n_arch == 0 || (pa.x & PA_NOARCH));
     const uint32_t arch = pa.x & PA_ARCH_MASK;
     for (uint32_t i = 0; i < x.n_arch && !ok; i++) ok = ids[i] == arch;
-    if (!ok) return false;
+    if (!ok) return 0;
   }
   if (x.kind & AUX_CPE) {
-    if (pa.y >= a.n_cpe_sets) return false;
+    if (pa.y >= a.n_cpe_sets) return 0;
     const uint32_t* set = a.cpe_bits + size_t(pa.y) * a.cpe_words;
     bool ok = false;
     for (uint32_t i = 0; i < x.n_cpe && !ok; i++) {
       const uint32_t c = ids[x.n_arch + i];
       ok = (c >> 5) < a.cpe_words && ((set[c >> 5] >> (c & 31)) & 1u);
     }
-    if (!ok) return false;
+    if (!ok) return 0;
   }
-  if ((x.kind & AUX_TAG) && x.tag != pa.y) return false;
-  return true;
+  if ((x.kind & AUX_TAG) && x.tag != pa.y) return 0;
+  return 1;
 }
 
 // sign(installed key - bound) on the big-endian heads; the tails (memory-order words from
@@ -480,9 +491,9 @@ __device__ __forceinline__ int cmp_head(uint64_t a0, uint64_t a1, uint32_t na, u
 // Interval test of tile package q's installed key against one row (global index ridx).
 // The common case (a bound decided by the inline 16-byte heads) runs without branches;
 // a 16-byte tie reads the key tails, a lower bound (library / rpm ranges) its key head.
-template <int FILT, class S>
-__device__ __forceinline__ bool eval_row(const SweepArgs& a, const S& s, uint32_t q, uint32_t p, const Row& row,
-                                         uint32_t ridx) {
+template <int FILT, bool DEFER = false, class S>
+__device__ __forceinline__ uint32_t eval_row(const SweepArgs& a, const S& s, uint32_t q, uint32_t p, const Row& row,
+                                             uint32_t ridx) {
   const uint32_t ki = s.kinfo[q];
   const uint32_t kl = ki & KI_LEN;
   const uint64_t k0 = s.k0[q], k1 = s.k1[q];
@@ -509,9 +520,56 @@ __device__ __forceinline__ bool eval_row(const SweepArgs& a, const S& s, uint32_
   m = m && (ki & KI_VALID);
   m = m || (row.adv & ROW_ALWAYS);
   if constexpr (FILT) {
-    if (m && (row.adv & ROW_FILTER)) m = aux_pass<FILT>(a, ridx, s.pattr[q], ki, p);
+    if (m && (row.adv & ROW_FILTER)) return aux_pass<FILT, DEFER>(a, ridx, s.pattr[q], ki, p);
   }
-  return m;
+  return m ? 1u : 0u;
+}
+
+// The Maven programs of a sweep round, run compacted (FILT >= 2, tiles with Maven packages):
+// the lanes' deferred pairs (pend: bit k = sub-round k) are queued in LDS and every lane of
+// the workgroup takes one, so a program occupies all 64 lanes of a wave instead of one (a
+// round had its few program pairs spread over the waves, each wave waiting on its own:
+// Maven-only 1M packages took 0.62 ms with 3 % non-numeric versions, 0.34 ms with none).
+// Returns the lane's pass bits; q.res holds 4 bits per lane (K <= 4).
+struct DeferQ {
+  uint32_t* j;    // queued pair indices (cap of them; more are run in batches)
+  uint32_t* res;  // kTile / 8 words
+  uint32_t cap;
+};
+
+template <int K, int FILT>
+__device__ __forceinline__ uint32_t sweep_programs(const SweepArgs& a, const SweepShared<FILT>& s, const uint8_t* map,
+                                                   uint32_t nnz, uint32_t total, uint32_t b0, uint32_t pend,
+                                                   uint32_t tid, const DeferQ& q, uint32_t* ws) {
+  static_assert(K <= 4, "4 result bits per lane");
+  uint32_t excl;
+  const uint32_t n = block_exscan<kTile>(ws, uint32_t(__popc(pend)), tid, excl);
+  if (n == 0) return 0;
+  if (tid < kTile / 8) q.res[tid] = 0;
+  const bool use_map = total <= kMapCap;
+  const uint32_t pbase = s.tile * kTile;
+  for (uint32_t q0 = 0; q0 < n; q0 += q.cap) {
+    uint32_t o = excl;
+#pragma unroll
+    for (int k = 0; k < K; k++)
+      if ((pend >> k) & 1u) {
+        if (o >= q0 && o < q0 + q.cap) q.j[o - q0] = b0 + k * kTile + tid;
+        o++;
+      }
+    __syncthreads();
+    const uint32_t m = min(q.cap, n - q0);
+    for (uint32_t e = tid; e < m; e += kTile) {
+      const uint32_t j = q.j[e];
+      const uint32_t r = use_map ? uint32_t(map[j]) : pair_rank(s, nnz, j);
+      const uint32_t ridx = j + s.nz_rd[r];
+      if (mvn_pair<FILT>(a, a.db.aux_ids + a.db.aux[ridx].list_off, pbase + s.nz_q[r])) {
+        const uint32_t owner = (j - b0) % kTile, kk = (j - b0) / kTile;
+        atomicOr(&q.res[owner >> 3], 1u << ((owner & 7) * 4 + kk));
+      }
+    }
+    __syncthreads();
+  }
+  return (q.res[tid >> 3] >> ((tid & 7) * 4)) & 0xFu;
 }
 
 // Tile package (nz rank) of pair j by binary search of the nz scan (tiles too large for the map).
@@ -536,7 +594,7 @@ __device__ __forceinline__ uint32_t pair_rank(const SweepShared<FILT>& s, uint32
 template <int K, int MB, int FILT, bool DIRECT>
 __device__ __forceinline__ uint32_t sweep(const SweepArgs& a, SweepShared<FILT>& s, uint32_t* madv, uint8_t* mq,
                                           const uint8_t* map, uint32_t nnz, uint32_t total, uint32_t tid,
-                                          unsigned long long base) {
+                                          unsigned long long base, bool mvn, const DeferQ& dq) {
   constexpr int W = kTile / 64;
   const uint32_t lane = tid & 63, wave = tid >> 6;
   const unsigned long long lt = (1ull << lane) - 1ull;
@@ -567,11 +625,16 @@ __device__ __forceinline__ uint32_t sweep(const SweepArgs& a, SweepShared<FILT>&
     }
 #pragma unroll
     for (int k = 0; k < K; k++) row[k] = a.db.rows[rid[k]];
-    uint32_t mask = 0;
+    uint32_t mask = 0, pend = 0;
 #pragma unroll
     for (int k = 0; k < K; k++) {
-      const bool m = eval_row<FILT>(a, s, qq[k], pbase + qq[k], row[k], rid[k]);
-      mask |= (m && b0 + k * kTile + tid < total) ? 1u << k : 0u;
+      const uint32_t e = eval_row<FILT, (FILT >= 2)>(a, s, qq[k], pbase + qq[k], row[k], rid[k]);
+      const bool in = b0 + k * kTile + tid < total;
+      mask |= (e == 1 && in) ? 1u << k : 0u;
+      pend |= (e == 2 && in) ? 1u << k : 0u;
+    }
+    if constexpr (FILT >= 2) {
+      if (mvn) mask |= sweep_programs<K, FILT>(a, s, map, nnz, total, b0, pend, tid, dq, s.wsum[0]);
     }
     uint32_t* ws = s.wsum2[round & 1];
     unsigned long long bal[K];
@@ -644,7 +707,7 @@ __device__ __forceinline__ uint32_t sweep_seg(const SweepArgs& a, const SweepSha
     for (int k = 0; k < K; k++) row[k] = a.db.rows[rid[k]];
 #pragma unroll
     for (int k = 0; k < K; k++) {
-      const bool m = eval_row<FILT>(a, s, qq[k], pbase + qq[k], row[k], rid[k]) && b0 + k * 64 + lane < s1;
+      const bool m = eval_row<FILT>(a, s, qq[k], pbase + qq[k], row[k], rid[k]) != 0 && b0 + k * 64 + lane < s1;
       const unsigned long long bal = __ballot(m);
       if (m) {
         const uint32_t pos = nm + uint32_t(__popcll(bal & lt));
@@ -668,7 +731,8 @@ __device__ __forceinline__ uint32_t sweep_seg(const SweepArgs& a, const SweepSha
 // The sweep of tile t (packages t * 256 ..) given each lane's package record r.
 template <int K, int MB, int FILT, int SEG = 0>
 __device__ __forceinline__ void sweep_tile(const SweepArgs& a, SweepShared<FILT>& s, uint32_t* madv, uint8_t* mq,
-                                           uint8_t* map, uint32_t t, uint32_t tid, const PkgRec& r) {
+                                           uint8_t* map, uint32_t t, uint32_t tid, const PkgRec& r,
+                                           const DeferQ& dq = DeferQ{nullptr, nullptr, 0}) {
   const uint32_t lane = tid & 63, wave = tid >> 6;
   if (tid == 0) s.tile = t;
   const uint32_t p = t * kTile + tid;
@@ -751,7 +815,9 @@ __device__ __forceinline__ void sweep_tile(const SweepArgs& a, SweepShared<FILT>
     }
     return;
   }
-  const uint32_t nm = sweep<K, MB, FILT, false>(a, s, madv, mq, map, nnz, total, tid, 0);
+  // a tile with Maven packages runs its rounds' Maven programs compacted (sweep_programs)
+  const bool mvn = FILT >= 2 && dq.cap && __syncthreads_or((r.meta.z & KI_MVN) != 0);
+  const uint32_t nm = sweep<K, MB, FILT, false>(a, s, madv, mq, map, nnz, total, tid, 0, mvn, dq);
 
   // the tile's output segment: one atomic reservation, no waiting on other tiles; the
   // tile directory gives the global (package, advisory) order
@@ -774,7 +840,7 @@ __device__ __forceinline__ void sweep_tile(const SweepArgs& a, SweepShared<FILT>
       }
     }
   } else {
-    sweep<K, MB, FILT, true>(a, s, madv, mq, map, nnz, total, tid, base);  // rare: more matches than the buffer
+    sweep<K, MB, FILT, true>(a, s, madv, mq, map, nnz, total, tid, base, mvn, dq);  // rare: more matches than the buffer
   }
 }
 
@@ -784,13 +850,15 @@ __global__ __launch_bounds__(kTile) void sweep_kernel(SweepArgs a) {
   __shared__ uint32_t madv[MB];
   __shared__ uint8_t mq[MB];
   __shared__ uint8_t map[kMapCap];  // pair -> nz rank of its package
+  constexpr uint32_t kQ = FILT >= 2 ? 512 : 1;
+  __shared__ uint32_t dqj[kQ], dqres[FILT >= 2 ? kTile / 8 : 1];
   const uint32_t tid = threadIdx.x, t = blockIdx.x;
   const uint32_t p = t * kTile + tid;
   PkgRec r;
   r.meta = make_uint4(0, 0, 0, 0);
   r.k0 = r.k1 = 0;
   if (p < a.n) r = a.rec[p];
-  sweep_tile<K, MB, FILT>(a, s, madv, mq, map, t, tid, r);
+  sweep_tile<K, MB, FILT>(a, s, madv, mq, map, t, tid, r, DeferQ{dqj, dqres, FILT >= 2 ? kQ : 0u});
 }
 
 // Probe and sweep of one tile in one workgroup (the record stays in registers/LDS): tiles
@@ -870,7 +938,12 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
   if (DIAG & 4) r.meta.y = 0;  // no rows: the sweep does nothing
   __syncthreads();  // the strings are dead: buf becomes the match buffer
   uint32_t* madv = reinterpret_cast<uint32_t*>(buf);
-  sweep_tile<K, MB, FILT, SEG>(fa.sa, s, madv, reinterpret_cast<uint8_t*>(madv + MB), map, t, tid, r);
+  // the Maven program queue takes the rest of buf behind the match buffer (FILT >= 2)
+  constexpr uint32_t kBufWords = sizeof(buf) / 4, kMbWords = (uint32_t(MB) * 5 + 3) / 4;
+  constexpr uint32_t kQ = kBufWords > kMbWords + kTile / 8 + 16 ? kBufWords - kMbWords - kTile / 8 : 0;
+  static_assert(FILT < 2 || kQ >= 16, "no room for the Maven program queue");
+  const DeferQ dq{madv + kMbWords + kTile / 8, madv + kMbWords, FILT >= 2 ? kQ : 0u};
+  sweep_tile<K, MB, FILT, SEG>(fa.sa, s, madv, reinterpret_cast<uint8_t*>(madv + MB), map, t, tid, r, dq);
 }
 
 template <uint32_t GM, int DIAG = 0>
@@ -896,7 +969,9 @@ constexpr FusedFn fused_entry() {
   if constexpr (F == 0) return nullptr;
   else if constexpr (F == 4) return &launch_fused<GM, K, MB, FILT, 0, 1, 1>;
   else if constexpr (F == 5) return &launch_fused<GM, K, MB, FILT, 0, 1, 3>;
-  else return &launch_fused<GM, K, MB, FILT, (F >= 10 ? F - 10 : 0), TVM_FUSED_WPE(F)>;
+  // the all-grammar K <= 2 kernels are held at 5 waves per SIMD (96 VGPRs): the Maven program
+  // queue (sweep_programs) took them to 97 and 4 waves
+  else return &launch_fused<GM, K, MB, FILT, (F >= 10 ? F - 10 : 0), (FILT >= 2 && K <= 2 && F == 1) ? 5 : TVM_FUSED_WPE(F)>;
 }
 
 }  // namespace

@@ -479,12 +479,14 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
   // the delta form: the host threads decode each chunk's streams into the CSR as soon as its
   // result move is done, while the GPU works on the chunks after it
   bool decoded = true;
-  if (delta_) {
+  static const bool no_decode = std::getenv("TVM_PIPE_NODECODE") != nullptr;  // measurement only: the bytes alone
+  if (delta_ && !no_decode) {
     uint64_t pos = 0;
     for (uint32_t c = 0; c < nc && decoded; c++) {
       const uint32_t t0 = bounds_[c], t1 = bounds_[c + 1];
       if (t1 == t0) continue;
       if (!ok(hipEventSynchronize(ev_k_[c]), "pipeline", err)) return false;
+      if (trace) std::fprintf(stderr, "pipe c%u moved %.1f us\n", c, us());
       for (uint32_t t = t0; t < t1; t++) {
         tile_pos_[t] = pos;
         pos += tile_info_h_[t].x;
