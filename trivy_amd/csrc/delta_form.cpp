@@ -31,6 +31,42 @@ inline uint32_t le24(const uint8_t* q) { return uint32_t(q[0]) | uint32_t(q[1]) 
 
 }  // namespace
 
+// The common tile (no list of 255 or more): the row ends from the count bytes, then ONE loop
+// over the tile's entries in which nothing branches on the data - an entry is a package's
+// first (3 bytes), a one-byte difference, or an escape (0 + 3 bytes), picked with selects -
+// because a loop per package mispredicted its trip count and its empty packages about
+// twice per package (3.6 ns per entry at 5 entries per package).
+static bool decode_tile_flat(const uint8_t* h, const uint8_t* end, uint64_t pos0, uint64_t count, uint32_t* adv,
+                             uint32_t* re) {
+  uint32_t first[kTile + 1];
+  uint32_t nf = 0, pos = 0;
+  for (int p = 0; p < kTile; p++) {
+    const uint32_t k = h[p];
+    first[nf] = pos;
+    nf += k != 0;
+    pos += k;
+    re[p] = uint32_t(pos0) + pos;
+  }
+  if (pos != count) return false;
+  first[nf] = 0xFFFFFFFFu;
+  const uint8_t* q = h + kTile;
+  uint32_t* o = adv + pos0;
+  uint32_t a = 0, f = 0, next = first[0];
+  for (uint32_t e = 0; e < pos; e++) {
+    uint32_t w;
+    std::memcpy(&w, q, 4);
+    const bool is_first = e == next;
+    f += is_first;
+    next = first[f];
+    const uint32_t x = w & 0xFFu;
+    const bool esc = !is_first && x == 0;
+    a = is_first ? (w & 0xFFFFFFu) : (esc ? (w >> 8) : a + x);
+    q += is_first ? 3 : (esc ? 4 : 1);
+    o[e] = a;
+  }
+  return q == end;
+}
+
 bool delta_decode_tile(const uint8_t* stream, uint64_t stream_bytes, uint32_t t, uint64_t pos0, uint2 info,
                        uint32_t* adv, uint32_t* row_end) {
   const uint64_t count = info.x, bytes = info.y;
@@ -41,6 +77,14 @@ bool delta_decode_tile(const uint8_t* stream, uint64_t stream_bytes, uint32_t t,
   }
   const uint64_t r = delta_region(t, pos0);
   if (bytes < kTile || r + bytes > stream_bytes) return false;
+  {
+    // the flat loop reads at most 4 bytes a match (+ 1 ahead) and trusts the count bytes: a
+    // tile with a 255 count, or whose reads could leave the buffer, takes the loop below
+    bool ext = false;
+    for (int p = 0; p < kTile; p++) ext |= stream[r + p] == 255;
+    if (!ext && r + kTile + 4 * count + 4 <= stream_bytes)
+      return decode_tile_flat(stream + r, stream + r + bytes, pos0, count, adv, re);
+  }
   const uint8_t* h = stream + r;
   const uint8_t* q = h + kTile;
   const uint8_t* end = h + bytes;

@@ -63,7 +63,9 @@ __device__ __forceinline__ uint32_t group_key(const MergeArgs& a, uint32_t p, ui
   return rh ? a.adv_rank[ad].x : kNoKey;
 }
 
-// Exclusive block scan of one flag per lane; returns the block total.
+// Exclusive block scan of one flag per lane; returns the block total.  One barrier: the
+// caller alternates two ws buffers between consecutive calls (the barriers between two calls
+// on one buffer order its reads before its next writes).
 __device__ __forceinline__ uint32_t block_flag_scan(bool f, uint32_t tid, uint32_t* ws, uint32_t& excl) {
   const uint32_t lane = tid & 63, wave = tid >> 6;
   const unsigned long long bal = __ballot(f);
@@ -77,7 +79,6 @@ __device__ __forceinline__ uint32_t block_flag_scan(bool f, uint32_t tid, uint32
     tot += c;
   }
   excl = off + uint32_t(__popcll(bal & ((1ull << lane) - 1ull)));
-  __syncthreads();  // ws is reused by the next chunk
   return tot;
 }
 
@@ -101,8 +102,8 @@ __device__ __forceinline__ uint32_t chunk_key(const MergeArgs& a, uint64_t b0, u
 // The (package, key) of the pair before the lane's: the lanes exchange them through LDS
 // (xp / xk); lane 0 takes the previous chunk's last pair (prev_*, advanced here to this
 // chunk's last pair), so each pair's key is gathered once, not again as its successor's
-// predecessor.  left = pairs of the segment from this chunk on.  The caller's next barrier
-// must come before the next chunk's call (block_flag_scan's).
+// predecessor.  left = pairs of the segment from this chunk on.  Consecutive chunks use
+// alternate xp / xk buffers, with the chunk's other barrier between two uses of one.
 __device__ __forceinline__ void pair_before(uint32_t tid, uint32_t p, uint32_t k, uint32_t* xp, uint32_t* xk,
                                             uint32_t& prev_p, uint32_t& prev_k, uint32_t left, uint32_t& pp,
                                             uint32_t& kp) {
@@ -124,9 +125,8 @@ __device__ __forceinline__ void pair_before(uint32_t tid, uint32_t p, uint32_t k
 // whose pairs are groups of one (a workgroup per such tile spent its time being dispatched).
 __global__ __launch_bounds__(kBlock) void rh_count_kernel(MergeArgs a, uint32_t* counts, const uint8_t* rh_flags,
                                                           const uint32_t* rh_list, uint32_t n_rh, uint32_t n_tiles) {
-  __shared__ uint32_t ws[kWaves];
   __shared__ uint8_t rhp[kBlock];
-  __shared__ uint32_t xp[kBlock], xk[kBlock];
+  __shared__ uint32_t xp[2][kBlock], xk[2][kBlock];
   const uint32_t tid = threadIdx.x;
   if (blockIdx.x >= n_rh) {
     const uint32_t t = (blockIdx.x - n_rh) * kBlock + tid;
@@ -150,22 +150,21 @@ __global__ __launch_bounds__(kBlock) void rh_count_kernel(MergeArgs a, uint32_t*
     return;
   }
   __syncthreads();  // rhp
-  uint32_t heads = 0, prev_p = 0xFFFFFFFFu, prev_k = kNoKey;
+  uint32_t heads = 0, prev_p = 0xFFFFFFFFu, prev_k = kNoKey, par = 0;
   bool order_bad = false;
-  for (uint32_t c = 0; c < cnt; c += kBlock) {
+  for (uint32_t c = 0; c < cnt; c += kBlock, par ^= 1) {
     const bool v = c + tid < cnt;
     uint32_t p = 0xFFFFFFFFu, ad = 0;
     const uint32_t k = chunk_key(a, b0, c, cnt, t, tid, rhp, p, ad);
     bool h = false;
     uint32_t pp, kp;
-    pair_before(tid, p, k, xp, xk, prev_p, prev_k, cnt - c, pp, kp);
+    pair_before(tid, p, k, xp[par], xk[par], prev_p, prev_k, cnt - c, pp, kp);
     if (v) {
       const bool cont = k != kNoKey && pp == p;
       h = !(cont && kp == k);
       order_bad |= cont && kp > k;
     }
-    uint32_t ex;
-    heads += block_flag_scan(h, tid, ws, ex);  // its barriers also order this chunk's xp / xk reads before the next writes
+    heads += uint32_t(__syncthreads_count(h));
   }
   if (order_bad) atomicOr(a.mctl + 3, (unsigned long long)ERR_RH_ORDER);
   if (tid == 0) counts[t] = heads;
@@ -183,9 +182,9 @@ __global__ __launch_bounds__(kBlock) void rh_count_kernel(MergeArgs a, uint32_t*
 __global__ __launch_bounds__(kBlock) void rh_emit_kernel(MergeArgs a, const uint32_t* counts,
                                                          const unsigned long long* bases, const uint8_t* rh_flags,
                                                          const uint32_t* rh_list, uint32_t n_rh, uint32_t n_tiles) {
-  __shared__ uint32_t ws[kWaves];
+  __shared__ uint32_t ws[2][kWaves];
   __shared__ uint8_t rhp[kBlock];
-  __shared__ uint32_t xp[kBlock], xk[kBlock];
+  __shared__ uint32_t xp[2][kBlock], xk[2][kBlock];
   const uint32_t tid = threadIdx.x;
   if (blockIdx.x >= n_rh) {
     const uint32_t lane = tid & 63, t = (blockIdx.x - n_rh) * kWaves + (tid >> 6);
@@ -236,17 +235,17 @@ __global__ __launch_bounds__(kBlock) void rh_emit_kernel(MergeArgs a, const uint
   }
   if (!fits) return;  // cannot happen (merged <= raw); the counts tell the host
   __syncthreads();  // rhp
-  uint32_t done = 0, prev_p = 0xFFFFFFFFu, prev_k = kNoKey;
-  for (uint32_t c = 0; c < cnt; c += kBlock) {
+  uint32_t done = 0, prev_p = 0xFFFFFFFFu, prev_k = kNoKey, par = 0;
+  for (uint32_t c = 0; c < cnt; c += kBlock, par ^= 1) {
     const bool v = c + tid < cnt;
     const uint64_t i = b0 + c + tid;
     uint32_t p = 0xFFFFFFFFu, ad = 0;
     const uint32_t k = chunk_key(a, b0, c, cnt, t, tid, rhp, p, ad);
     uint32_t pp, kp;
-    pair_before(tid, p, k, xp, xk, prev_p, prev_k, cnt - c, pp, kp);
+    pair_before(tid, p, k, xp[par], xk[par], prev_p, prev_k, cnt - c, pp, kp);
     const bool h = v && (k == kNoKey || pp != p || kp != k);
     uint32_t ex;
-    const uint32_t n = block_flag_scan(h, tid, ws, ex);
+    const uint32_t n = block_flag_scan(h, tid, ws[par], ex);
     if (h) {
       uint32_t best = RH_NONE, best_r = 0, len = 1;
       if (k != kNoKey) {
