@@ -520,8 +520,7 @@ def main():
             mf.pipeline_prepare(match_cap=total, chunk_packages=args.chunk, raw=True,
                                 delta=args.e2e_form == "delta")
             tr = time.perf_counter()
-            got, ep, _ = mf.pipeline_run()
-            mf.pipeline_decode_ms()
+            got, ep, _ = mf.pipeline_run()  # the result: the CSR in pinned host memory (3-byte indices, or decoded from the delta form inside the pass)
             te = time.perf_counter()
             if got != total or ep != -1:
                 raise RuntimeError("fresh-batch pass disagrees with the device-resident pass")
@@ -534,8 +533,8 @@ def main():
         fresh = dict(med, packages_per_s=wl.n / ((med["prepare_ms"] + med["pass_ms"]) / 1e3), batches=len(runs),
                      form="raw (pinned staging copy on the host threads; no per-batch string dedup)",
                      inside="prepare (freeze, size, pinned staging copy, buffers from the block cache) + one "
-                            "pipelined pass (upload, match, per-package advisory lists back in pinned host memory) "
-                            "+ the host decode of the result into the CSR",
+                            "pipelined pass (upload, match, per-package advisory lists back in pinned host memory "
+                            "as the CSR: 3-byte indices + row ends, or decoded from the delta form inside the pass)",
                      result_form=args.e2e_form,
                      outside="build_ms: the caller adding the batch's packages (tvm_batch_add_many per target)")
 

@@ -1409,8 +1409,10 @@ int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row
     if (b->pipe_wide_for != b->pipe_runs) {
       const uint8_t* p = reinterpret_cast<const uint8_t*>(b->pipe->adv());
       b->pipe_wide.resize(b->pipe_total);
-      for (uint64_t i = 0; i < b->pipe_total; i++)
-        b->pipe_wide[i] = uint32_t(p[3 * i]) | uint32_t(p[3 * i + 1]) << 8 | uint32_t(p[3 * i + 2]) << 16;
+      uint32_t* w = b->pipe_wide.data();
+      range_for(b->pipe_total, size_t(1) << 18, [&](size_t i0, size_t i1) {
+        for (size_t i = i0; i < i1; i++) w[i] = uint32_t(p[3 * i]) | uint32_t(p[3 * i + 1]) << 8 | uint32_t(p[3 * i + 2]) << 16;
+      });
       b->pipe_wide_for = b->pipe_runs;
     }
     *adv = b->pipe_wide.data();

@@ -114,7 +114,9 @@ struct alignas(16) SlotVal {
   uint32_t row_begin;
   uint32_t row_count;
 };
-enum : uint32_t { SLOT_POISONED = 1u << 31, SLOT_LEN_MASK = 0x7FFFFFFFu };
+// SLOT_MVN_C0 / C1: the key has a Maven program row (AUX_MVN) that admits installed versions
+// of class 0 / 1 (libver.h mvn_numeric): the probe packs a Maven package's parse only then.
+enum : uint32_t { SLOT_POISONED = 1u << 31, SLOT_MVN_C0 = 1u << 30, SLOT_MVN_C1 = 1u << 29, SLOT_LEN_MASK = 0x1FFFFFFFu };
 // Device hash slot: one 64-B cache line holding the hash, the row range and the first
 // kSlotNameWords*8 bytes of the name (memory order, zero padded), so a probe verifies the
 // name from the same line it read the hash from; longer names finish against the name

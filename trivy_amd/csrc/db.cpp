@@ -741,9 +741,17 @@ void DB::build_index() {
     uint64_t i = h & slot_mask;
     while (slot_hash[i]) i = (i + 1) & slot_mask;
     slot_hash[i] = h;
+    // which installed-version classes meet a Maven program row of the key (the probe packs a
+    // Maven package's parse only for those)
+    uint32_t mvn = 0;
+    for (uint32_t r = row_begin[k]; r < row_begin[k] + row_count[k]; r++) {
+      if (!(rows[r].adv & ROW_FILTER) || !(aux[r].kind & AUX_MVN)) continue;
+      const uint32_t admits = (aux[r].kind & AUX_CLASS) ? aux[r].tag : ~0u;
+      mvn |= ((admits & 1u) ? SLOT_MVN_C0 : 0u) | ((admits & 2u) ? SLOT_MVN_C1 : 0u);
+    }
     SlotVal v;
     v.name_off = uint32_t(name_arena.size());
-    v.name_len = uint32_t(key.name.size()) | (key.poisoned ? SLOT_POISONED : 0);
+    v.name_len = uint32_t(key.name.size()) | (key.poisoned ? SLOT_POISONED : 0) | mvn;
     v.row_begin = row_begin[k];
     v.row_count = row_count[k];
     slot_val[i] = v;

@@ -209,7 +209,7 @@ __device__ __forceinline__ bool name_eq_slot(const uint8_t* s, uint32_t n, const
 template <class P>
 __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uint32_t plat, const PlatInfo& pi,
                                             uint32_t nlen, const uint8_t* name, bool valid, uint32_t& rbeg,
-                                            uint32_t& cnt);
+                                            uint32_t& cnt, uint32_t* sflags = nullptr);
 
 // One package: encode, hash, probe.  P = uint32_t in the LDS or global address space of s.
 // kb / tab: the lane's LDS key buffer and the dpkg code table (nullptr: generic encoder only).
@@ -266,11 +266,15 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
       kinfo |= KI_SPILL;
     }
   }
+  uint32_t cnt = 0, rbeg = 0, sflags = 0;
+  if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, valid, rbeg, cnt, &sflags);
   if (((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN) {
     // Maven rows compare parses, not keys (AUX_MVN): the installed version's parse, packed
-    // into the batch scratch, and its text location take the tail slot
+    // into the batch scratch, and its text location take the tail slot - only when the key
+    // has a program row that admits the version's class (SLOT_MVN_C0 / C1: most numeric
+    // versions meet hybrid advisories only, whose program rows reject them by class)
     uint32_t off = 0, nt = 0;
-    if (valid) {
+    if (valid && (sflags & (cls == 1 ? SLOT_MVN_C1 : SLOT_MVN_C0))) {
       MvnParse mp;
       if (mvn_parse(ver, vlen, mp)) {
         const uint32_t need = (kMvnPackedWords * mp.n + 1) / 2;
@@ -292,15 +296,13 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
   if (((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN) kinfo |= KI_MVN;
   r.k0 = valid && kl ? be_word(hs.w0, kl < 8 ? kl : 8) : 0ull;
   r.k1 = valid && kl > 8 ? be_word(hs.w1, kl < 16 ? kl - 8 : 8) : 0ull;
-  uint32_t cnt = 0, rbeg = 0;
-  if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, valid, rbeg, cnt);
   r.meta = make_uint4(rbeg, cnt, kinfo, koff);
 }
 
 template <class P>
 __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uint32_t plat, const PlatInfo& pi,
                                             uint32_t nlen, const uint8_t* name, bool valid, uint32_t& rbeg,
-                                            uint32_t& cnt) {
+                                            uint32_t& cnt, uint32_t* sflags) {
   // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup;
   // lookup-first drivers (ubuntu.go:86-92) probe first, so a poisoned key still raises
   if (valid || (pi.flags & PLAT_LOOKUP_FIRST)) {
@@ -317,6 +319,7 @@ __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uin
       } else if (valid) {
         cnt = q0.w;
         rbeg = q0.z;
+        if (sflags) *sflags = q1.x & (SLOT_MVN_C0 | SLOT_MVN_C1);
       }
       break;
     }
