@@ -1056,7 +1056,7 @@ MvnProgState mvn_program(const std::vector<std::string>& vulnerable, const std::
     words[f.at] = uint32_t(words.size());
     const size_t base = words.size();
     words.resize(base + size_t(kMvnPackedWords) * P.n);
-    mvn_pack(P, words.data() + base);
+    mvn_pack(P, U(*f.txt), words.data() + base);
     words[f.at + 1] = uint32_t(words.size());
     std::vector<uint32_t> packed((f.txt->size() + 3) / 4 + 1, 0);
     std::memcpy(packed.data(), f.txt->data(), f.txt->size());

@@ -724,9 +724,27 @@ TVM_HD bool mvn_encode(const uint8_t* s, uint32_t n, Sink& o) {
 // removed << 16 | zero << 24, w1 = b | e << 16) - the bounds' parses are packed into the
 // program at load time and the installed version's into the batch scratch by the probe,
 // so the sweep parses nothing.
+// An int token of at most 9 significant digits: its value (the packed form carries it).
+TVM_HD bool mvn_small_int(const uint8_t* s, uint32_t b, uint32_t e, uint32_t& v) {
+  while (b < e && s[b] == '0') b++;
+  if (e - b > 9) return false;
+  v = 0;
+  for (; b < e; b++) v = v * 10 + uint32_t(s[b] - '0');
+  return true;
+}
+
 struct MvnParseView {
   const MvnParse* P;
   const uint8_t* s;
+  TVM_HD bool has_val(int k) const {
+    uint32_t v;
+    return P->t[k].kind == MV_INT && mvn_small_int(s, P->t[k].b, P->t[k].e, v);
+  }
+  TVM_HD uint32_t val(int k) const {
+    uint32_t v = 0;
+    (void)mvn_small_int(s, P->t[k].b, P->t[k].e, v);
+    return v;
+  }
   TVM_HD int n() const { return P->n; }
   TVM_HD uint32_t kind(int k) const { return P->t[k].kind; }
   TVM_HD uint32_t q(int k) const { return P->t[k].q; }
@@ -735,6 +753,11 @@ struct MvnParseView {
   TVM_HD uint32_t b(int k) const { return P->t[k].b; }
   TVM_HD uint32_t e(int k) const { return P->t[k].e; }
 };
+// Packed tokens: w0 = kind | q << 8 | removed << 16 | zero << 24 | MVP_VAL, w1 = b | e << 16,
+// or for an int of at most 9 significant digits (MVP_VAL) its value: the pairwise compare
+// of two such ints reads no text (mvn_int_cmp), which took most of a program's dependent
+// loads.
+enum : uint32_t { MVP_VAL = 1u << 25 };
 struct MvnPackedView {
   const uint32_t* t;
   int cnt;
@@ -743,17 +766,26 @@ struct MvnPackedView {
   TVM_HD uint32_t kind(int k) const { return t[2 * k] & 0xFFu; }
   TVM_HD uint32_t q(int k) const { return (t[2 * k] >> 8) & 0xFFu; }
   TVM_HD bool removed(int k) const { return (t[2 * k] >> 16) & 0xFFu; }
-  TVM_HD bool zero(int k) const { return t[2 * k] >> 24; }
+  TVM_HD bool zero(int k) const { return (t[2 * k] >> 24) & 1u; }
+  TVM_HD bool has_val(int k) const { return (t[2 * k] & MVP_VAL) != 0; }
+  TVM_HD uint32_t val(int k) const { return t[2 * k + 1]; }
   TVM_HD uint32_t b(int k) const { return t[2 * k + 1] & 0xFFFFu; }
   TVM_HD uint32_t e(int k) const { return t[2 * k + 1] >> 16; }
 };
 constexpr int kMvnPackedWords = 2;  // words per packed token
 
-TVM_HD void mvn_pack(const MvnParse& P, uint32_t* out) {
+TVM_HD void mvn_pack(const MvnParse& P, const uint8_t* s, uint32_t* out) {
   for (int k = 0; k < P.n; k++) {
     const MvnTok& t = P.t[k];
-    out[2 * k] = uint32_t(t.kind) | (uint32_t(t.q) << 8) | (uint32_t(t.removed) << 16) | (uint32_t(t.zero) << 24);
-    out[2 * k + 1] = (t.b & 0xFFFFu) | (t.e << 16);
+    uint32_t w0 = uint32_t(t.kind) | (uint32_t(t.q) << 8) | (uint32_t(t.removed) << 16) | (uint32_t(t.zero) << 24);
+    uint32_t w1 = (t.b & 0xFFFFu) | (t.e << 16);
+    uint32_t v;
+    if (t.kind == MV_INT && mvn_small_int(s, t.b, t.e, v)) {
+      w0 |= MVP_VAL;
+      w1 = v;
+    }
+    out[2 * k] = w0;
+    out[2 * k + 1] = w1;
   }
 }
 
@@ -781,6 +813,13 @@ TVM_HD int mvn_vs_null(const V& A, int k) {
 
 template <class VA, class VB>
 TVM_HD int mvn_int_cmp(const VA& A, int x, const VB& B, int y) {
+  const bool va = A.has_val(x), vb = B.has_val(y);
+  if (va && vb) {  // both below 10^9: the values (digit count, then digits, is the number order)
+    const uint32_t p = A.val(x), q = B.val(y);
+    return p == q ? 0 : (p < q ? -1 : 1);
+  }
+  if (va) return -1;  // has_val is exact on both views: the other has 10 or more significant digits
+  if (vb) return 1;
   uint32_t i = A.b(x), j = B.b(y);
   const uint32_t ie = A.e(x), je = B.e(y);
   while (i < ie && A.s[i] == '0') i++;

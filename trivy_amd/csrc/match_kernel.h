@@ -283,7 +283,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
           atomicOr(&a.ctl[3], (unsigned long long)ERR_SPILL);
           valid = false;
         } else {
-          mvn_pack(mp, reinterpret_cast<uint32_t*>(a.spill + o));
+          mvn_pack(mp, ver, reinterpret_cast<uint32_t*>(a.spill + o));
           off = uint32_t(o);
           nt = uint32_t(mp.n);
         }
