@@ -3,7 +3,7 @@
 # C4; C2 line.
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/${NAME:-r04k}
+OUT=$R/gpurun_out/${NAME:-r04l}
 mkdir -p $OUT
 cd $R
 export TMPDIR=/tmp
