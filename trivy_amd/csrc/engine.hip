@@ -272,7 +272,7 @@ uint64_t Engine::scratch_words(const HostBatch& hb) const {
       const uint32_t need = (key_bound_any(vlen) + 7) / 8;
       if (need > kKeyWords) w += need;
       if (d.x < pi.size() && pi[d.x].cmp == CMP_MAVEN)
-        w += (uint64_t(kMvnPackedHead) + uint64_t(kMvnPackedWords) * std::min<uint32_t>(2 * vlen + 3, kMvnMaxTok) + 1) / 2;
+        w += (uint64_t(kMvnPackedWords) * std::min<uint32_t>(2 * vlen + 3, kMvnMaxTok) + 1) / 2;
     }
     total.fetch_add(w, std::memory_order_relaxed);
   });

@@ -1053,9 +1053,9 @@ MvnProgState mvn_program(const std::vector<std::string>& vulnerable, const std::
   for (const Fix& f : fix) {  // packed parses, then the texts, behind the groups
     MvnParse P;
     (void)mvn_parse(U(*f.txt), uint32_t(f.txt->size()), P);
+    words[f.at] = uint32_t(words.size());
     const size_t base = words.size();
-    words[f.at] = uint32_t(base + kMvnPackedHead);  // the tokens; their head in front
-    words.resize(base + kMvnPackedHead + size_t(kMvnPackedWords) * P.n);
+    words.resize(base + size_t(kMvnPackedWords) * P.n);
     mvn_pack(P, U(*f.txt), words.data() + base);
     words[f.at + 1] = uint32_t(words.size());
     std::vector<uint32_t> packed((f.txt->size() + 3) / 4 + 1, 0);
@@ -1085,10 +1085,7 @@ int mvn_is_vulnerable(const std::vector<std::string>& vulnerable, const std::vec
   if (st != MVN_PROGRAM) return st == MVN_ALWAYS ? 1 : 0;
   MvnParse V;
   if (!mvn_parse(U(installed), uint32_t(installed.size()), V)) return 0;  // NewVersion error: not vulnerable
-  const MvnParseView IV{&V, U(installed)};
-  uint32_t iv[3] = {0, 0, 0};
-  const int im = mvn_lead(IV, iv);
-  return mvn_program_eval(w.data(), IV, im, iv) ? 1 : 0;
+  return mvn_program_eval(w.data(), MvnParseView{&V, U(installed)}) ? 1 : 0;
 }
 
 }  // namespace tvm

@@ -773,31 +773,8 @@ struct MvnPackedView {
   TVM_HD uint32_t e(int k) const { return t[2 * k + 1] >> 16; }
 };
 constexpr int kMvnPackedWords = 2;  // words per packed token
-// A packed parse starts with a head of kMvnPackedHead words: {m, v0, v1, v2} = the values of
-// its first m <= 3 items when they are ints below 10^9 (the top-level run mvn_cmp compares
-// first).  Two versions whose runs differ inside their common length compare as the first
-// differing value: a program term is then decided from the heads, without a token walk.
-constexpr int kMvnPackedHead = 4;
 
-template <class V>
-TVM_HD int mvn_next(const V& A, int k);
-
-template <class V>
-TVM_HD int mvn_lead(const V& A, uint32_t v[3]) {
-  int m = 0;
-  for (int k = 0; m < 3;) {
-    const int x = mvn_next(A, k);
-    if (x < 0 || A.kind(x) != MV_INT || !A.has_val(x)) break;
-    v[m++] = A.val(x);
-    k = x + 1;
-  }
-  return m;
-}
-
-// out: kMvnPackedHead head words, then kMvnPackedWords per token; the view of the tokens
-// starts behind the head (mvn_head reads it back).
 TVM_HD void mvn_pack(const MvnParse& P, const uint8_t* s, uint32_t* out) {
-  out += kMvnPackedHead;
   for (int k = 0; k < P.n; k++) {
     const MvnTok& t = P.t[k];
     uint32_t w0 = uint32_t(t.kind) | (uint32_t(t.q) << 8) | (uint32_t(t.removed) << 16) | (uint32_t(t.zero) << 24);
@@ -810,12 +787,6 @@ TVM_HD void mvn_pack(const MvnParse& P, const uint8_t* s, uint32_t* out) {
     out[2 * k] = w0;
     out[2 * k + 1] = w1;
   }
-  uint32_t v[3] = {0, 0, 0};
-  const int m = mvn_lead(MvnPackedView{out, P.n, s}, v);
-  out[-4] = uint32_t(m);
-  out[-3] = v[0];
-  out[-2] = v[1];
-  out[-1] = v[2];
 }
 
 // Next item of the list at or after token k (removed tokens skipped); -1 at the list's end.
@@ -929,11 +900,9 @@ TVM_HD bool mvn_op(uint32_t op, int c) {
   }
 }
 
-// The program at w against the installed version's parse V; im / iv = its mvn_lead.  A term
-// whose bound's head differs from the installed head inside their common run is decided
-// there; the rest walk the tokens (mvn_cmp).
+// The program at w against the installed version's parse V.
 template <class V>
-TVM_HD bool mvn_program_eval(const uint32_t* w, const V& inst, int im, const uint32_t* iv) {
+TVM_HD bool mvn_program_eval(const uint32_t* w, const V& inst) {
   const uint32_t nv = w[0] & 0xFFFFu, ns = w[0] >> 16;
   uint32_t at = 1;
   bool vul = nv == 0, sec = false;
@@ -944,15 +913,8 @@ TVM_HD bool mvn_program_eval(const uint32_t* w, const V& inst, int im, const uin
       const uint32_t d = w[at], tok = w[at + 1], txt = w[at + 2];
       at += 3;
       if (!all) continue;
-      const uint32_t* bh = w + tok - kMvnPackedHead;
-      const int m = im < int(bh[0]) ? im : int(bh[0]);
-      int c = 0;
-      for (int i = 0; i < m && c == 0; i++) c = iv[i] == bh[1 + i] ? 0 : (iv[i] < bh[1 + i] ? -1 : 1);
-      if (c == 0) {
-        const MvnPackedView B{w + tok, int((d >> 8) & 0xFFu), reinterpret_cast<const uint8_t*>(w + txt)};
-        c = mvn_cmp(inst, B);
-      }
-      all = mvn_op(d & 0xFFu, c);
+      const MvnPackedView B{w + tok, int((d >> 8) & 0xFFu), reinterpret_cast<const uint8_t*>(w + txt)};
+      all = mvn_op(d & 0xFFu, mvn_cmp(inst, B));
     }
     if (g < nv) vul = vul || all;
     else sec = sec || all;

@@ -277,7 +277,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
     if (valid && (sflags & (cls == 1 ? SLOT_MVN_C1 : SLOT_MVN_C0))) {
       MvnParse mp;
       if (mvn_parse(ver, vlen, mp)) {
-        const uint32_t need = (kMvnPackedHead + kMvnPackedWords * mp.n + 1) / 2;
+        const uint32_t need = (kMvnPackedWords * mp.n + 1) / 2;
         const unsigned long long o = atomicAdd(&a.ctl[2], (unsigned long long)need);
         if (o + need > a.spill_cap) {
           atomicOr(&a.ctl[3], (unsigned long long)ERR_SPILL);
@@ -434,11 +434,9 @@ template <int FILT>
 __device__ __forceinline__ bool mvn_pair(const SweepArgs& a, const uint32_t* ids, uint32_t p) {
   // the installed parse packed by probe_one, the program's packed bounds
   const uint4 t = a.tail[p];
-  const uint32_t* h = reinterpret_cast<const uint32_t*>(a.spill + t.x);  // head, then the tokens
-  const MvnPackedView V{h + kMvnPackedHead, int(t.y & 0xFFFFu), a.arena + (uint64_t(t.z) | (uint64_t(t.w) << 32))};
-  const uint2 h0 = reinterpret_cast<const uint2*>(h)[0], h1 = reinterpret_cast<const uint2*>(h)[1];  // 8-B aligned
-  const uint32_t iv[3] = {h0.y, h1.x, h1.y};
-  return mvn_program_eval(ids, V, int(h0.x), iv);
+  const MvnPackedView V{reinterpret_cast<const uint32_t*>(a.spill + t.x), int(t.y & 0xFFFFu),
+                        a.arena + (uint64_t(t.z) | (uint64_t(t.w) << 32))};
+  return mvn_program_eval(ids, V);
 }
 
 template <int FILT, bool DEFER = false>
