@@ -93,6 +93,7 @@ struct FilterArgs {
   uint32_t* run_b;     // the package's pairs are [run_b, run_e) of the list
   uint32_t* run_e;
   uint32_t* cnt;       // kClasses counters per package
+  uint32_t* surv;      // per package: its survivors (counters 0..4 summed), what the placement scan reads
   const uint32_t* off;      // survivor offset of perm position j (exclusive scan)
   const uint32_t* ign_off;  // ignored offset of package p
   // per pair
@@ -390,6 +391,8 @@ __global__ __launch_bounds__(kBlock) void filter_count(FilterArgs a) {
 #pragma unroll
       for (int c = 0; c < kClasses; c++)
         if (cc[c]) o[c] = cc[c];
+      const uint32_t s = cc[0] + cc[1] + cc[2] + cc[3] + cc[4];
+      if (s) a.surv[p] = s;
     }
   }
 }
@@ -508,9 +511,7 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
             for (uint32_t g = gb; g < ge; g++) {
               const uint32_t q = a.perm[g];
               if (q != p) {
-                uint32_t any = 0;
-                for (int sv = 0; sv < 5; sv++) any |= a.cnt[uint64_t(q) * kClasses + sv];
-                if (!any) continue;  // no survivors (its run bounds may be stale)
+                if (!a.surv[q]) continue;  // no survivors (its run bounds may be stale)
               }
               r += count_below(a.skey, a.run_b[q], a.run_e[q], key, q != p && a.prank[q] < pr);
             }
@@ -544,16 +545,17 @@ __global__ __launch_bounds__(kBlock) void filter_count_dup(const uint32_t* pkg, 
 }
 
 // Scan inputs (one trailing zero, so the exclusive scan's last element is the total):
-// survivors of the package at perm position j / ignored findings of package j.
+// survivors of the package at perm position j (its filter_count sum: one 4-byte gather, not
+// five counters of a 24-byte row - C5's scan read 409 MB for 20M packages) / ignored
+// findings of package j.
 struct GroupCount {
   const uint32_t* perm;  // nullptr: package j itself, ignored findings
-  const uint32_t* cnt;
+  const uint32_t* cnt;   // perm: the survivor sums; else the counters
   uint32_t n;
   __host__ __device__ uint32_t operator()(uint32_t j) const {
     if (j >= n) return 0u;
     if (!perm) return cnt[uint64_t(j) * kClasses + kIgnClass];
-    const uint32_t* c = cnt + uint64_t(perm[j]) * kClasses;
-    return c[0] + c[1] + c[2] + c[3] + c[4];
+    return cnt[perm[j]];
   }
 };
 
@@ -616,7 +618,7 @@ bool BatchFilter::set_packages(const FilterPackages& fp, std::string& err) {
     return false;
   for (int k : {8, 9, 20})
     if (!grow(k, n * 4, err)) return false;
-  if (!grow(6, n * 4 * kClasses, err) || !grow(7, (n + 3) & ~3ull, err) || !grow(10, (n + 1) * 4, err) ||
+  if (!grow(6, n * 4 * (kClasses + 1), err) || !grow(7, (n + 3) & ~3ull, err) || !grow(10, (n + 1) * 4, err) ||
       !grow(11, (n + 1) * 4, err))
     return false;
   n_pkgs_ = n;
@@ -782,7 +784,7 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
       !ok(hipMemcpyAsync(bufs_[20], rules.pkg_class, np * 4, hipMemcpyHostToDevice, st), "H2D classes", err))
     return false;
   if ((tcap && !ok(hipMemsetAsync(bufs_[16], 0, tcap * 16, st), "memset(dedup table)", err)) ||
-      !ok(hipMemsetAsync(bufs_[6], 0, np * 4 * kClasses, st), "memset(counters)", err))
+      !ok(hipMemsetAsync(bufs_[6], 0, np * 4 * (kClasses + 1), st), "memset(counters)", err))
     return false;
   FilterArgs a{};
   a.t = t;
@@ -799,6 +801,7 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   a.dup = as<const uint8_t>(bufs_[5]);
   a.pkg_class = as<const uint32_t>(bufs_[20]);
   a.cnt = as<uint32_t>(bufs_[6]);
+  a.surv = as<uint32_t>(bufs_[6]) + np * kClasses;
   a.fl = as<uint8_t>(bufs_[7]);
   a.run_b = as<uint32_t>(bufs_[8]);
   a.run_e = as<uint32_t>(bufs_[9]);
@@ -831,7 +834,7 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
                              uint32_t(np), uint32_t(rules.rank[1].size()), a.skey, a.pcls, as<uint32_t>(bufs_[26]));
   hipLaunchKernelGGL(filter_count, dim3(blocks), dim3(kBlock), 0, st, a);
   if (!ok(hipGetLastError(), "filter launch", err) ||
-      !ok(hipcub::DeviceScan::ExclusiveSum(bufs_[23], scan_bytes, In(Count(0), GroupCount{a.perm, a.cnt, uint32_t(np)}),
+      !ok(hipcub::DeviceScan::ExclusiveSum(bufs_[23], scan_bytes, In(Count(0), GroupCount{a.perm, a.surv, uint32_t(np)}),
                                            as<uint32_t>(bufs_[10]), int(np + 1), st),
           "hipcub scan", err) ||
       (has_ign &&
