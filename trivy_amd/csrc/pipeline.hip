@@ -354,7 +354,10 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
   // the result move leaves the row ends in HBM and the DMA engine carries them up on a third
   // stream while the kernels store the advisories (measured: 3.32 -> 3.20 ms per C2 pass; the
   // kernel stores alone reach 36-40 GB/s beside the match tiles)
-  const bool rowend_dma = !delta_;
+  // TVM_PIPE_ROWEND_STORE=1 (measurement): the result move stores the row ends too, so no
+  // device-to-host DMA shares the copy engines with the uploads
+  static const bool rowend_store = std::getenv("TVM_PIPE_ROWEND_STORE") != nullptr;
+  const bool rowend_dma = !delta_ && !rowend_store;
   auto copy_args = [&](uint32_t c) {
     CopyOutArgs ca;
     ca.dir = m_.dir;
