@@ -147,9 +147,15 @@ struct CopyOutArgs {
   uint8_t* stream_h = nullptr;
   uint64_t stream_units = 0;          // 16-byte units of stream_h
   uint2* tile_info_h = nullptr;
+  uint32_t block_move = 0;            // 1: the CSR move a workgroup per tile (round 3) instead of a wave per tile
 };
 constexpr uint32_t kDeltaStage = 2080;  // copy_out_tiles' delta staging bytes: header + one chunk's worst case + a carried unit
-constexpr uint32_t kCopyLdsWords = kTile + 8 + kDeltaStage / 4;  // copy_out_tiles' LDS: counts + scratch + delta staging
+constexpr uint32_t kCopyRunMax = kTile;  // tiles per prefix segment of the wave-per-tile move
+// copy_out_tiles' LDS: counts + scratch + delta staging (workgroup per tile), or the run's
+// tile offsets + a 256-entry count array per wave (wave per tile)
+constexpr uint32_t kCopyLdsWordsBlock = kTile + 8 + kDeltaStage / 4;
+constexpr uint32_t kCopyLdsWordsWave = 2 * kCopyRunMax + 8 + (kTile / 64) * kTile;
+constexpr uint32_t kCopyLdsWords = kCopyLdsWordsBlock > kCopyLdsWordsWave ? kCopyLdsWordsBlock : kCopyLdsWordsWave;
 
 // The delta result form: tile t's stream starts at this (16-byte aligned) byte of the stream
 // buffer, b = the CSR position of the tile's first match.  Consecutive tiles' starts are at
@@ -272,7 +278,7 @@ __device__ __forceinline__ uint32_t copy_block_sum(uint32_t v, uint32_t* red, ui
 // other (measured, DESIGN.md §7: one workgroup per tile moved the chunk slower, at 36 GB/s
 // beside the match tiles against 40 GB/s here).  lds: kCopyLdsWords words of the caller's
 // shared memory (the match kernel lends its staging buffer).
-__device__ __forceinline__ void copy_out_tiles(const CopyOutArgs& a, uint32_t wg, uint32_t n_wg, uint32_t* lds) {
+__device__ __forceinline__ void copy_out_tiles_block(const CopyOutArgs& a, uint32_t wg, uint32_t n_wg, uint32_t* lds) {
   uint32_t* cnt = lds;
   uint32_t* red = lds + kTile;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -407,6 +413,155 @@ __device__ __forceinline__ void copy_out_tiles(const CopyOutArgs& a, uint32_t wg
     }
     b += d.count;
     __syncthreads();  // cnt is rewritten by the next tile
+  }
+  if (wg == n_wg - 1 && tid == 0) a.chunk_base[a.c + 1] = b;
+}
+
+// One tile's CSR move by one wave (lane of 64): its per-package counts in the wave's own LDS
+// array (no workgroup barrier: one wave's LDS operations are ordered), the 256 row ends
+// from a wave scan (4 packages a lane, one 16-byte store each), then the segment realigned to
+// the destination's 16-byte units (3- or 4-byte indices).  b = the tile's first CSR position.
+__device__ __forceinline__ void copy_out_tile_wave(const CopyOutArgs& a, uint32_t t, uint64_t b, uint32_t lane,
+                                                   uint32_t* cw) {
+  const TileDir d = a.dir[t];
+  const bool fits = d.base + d.count <= a.cap && b + d.count <= a.cap;
+  const uint32_t p_first = t * kTile;
+  reinterpret_cast<uint4*>(cw)[lane] = make_uint4(0, 0, 0, 0);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (fits)
+    for (uint32_t i0 = 0; i0 < d.count; i0 += 4 * 64) {  // four loads in flight per lane
+      uint32_t q[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t i = i0 + u * 64 + lane;
+        q[u] = i < d.count ? a.pkg[d.base + i] - a.pkg_base - p_first : kTile;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        if (q[u] < kTile) atomicAdd(&cw[q[u]], 1u);
+    }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const uint4 c4 = reinterpret_cast<const uint4*>(cw)[lane];
+  const uint32_t s0 = c4.x, s1 = s0 + c4.y, s2 = s1 + c4.z, s3 = s2 + c4.w;
+  uint32_t x = s3;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= uint32_t(o)) x += y;
+  }
+  const uint32_t e = uint32_t(b) + x - s3;  // row ends are 32-bit
+  if (p_first / 4 + lane < a.row_end_units)
+    reinterpret_cast<uint4*>(a.row_end_h)[p_first / 4 + lane] = make_uint4(e + s0, e + s1, e + s2, e + s3);
+  else
+    atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
+  if (a.packed) {  // 3 bytes per advisory: destination bytes [3b, 3(b + count)) in 16-byte units
+    const uint64_t B0 = 3 * b, B1 = 3 * (b + d.count), U0 = B0 >> 4;
+    uint64_t nu = fits && d.count ? ((B1 + 15) >> 4) - U0 : 0;
+    if (nu && U0 + nu > a.adv_units) {  // guard: never expected
+      if (lane == 0) atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
+      nu = 0;
+    }
+    uint8_t* dst = reinterpret_cast<uint8_t*>(a.adv_h);
+    constexpr int kP = 2;
+    for (uint64_t j0 = 0; j0 < nu; j0 += uint64_t(kP) * 64) {
+      uint32_t id[kP][6];
+#pragma unroll
+      for (int k = 0; k < kP; k++) {
+        const uint64_t j = j0 + uint64_t(k) * 64 + lane, g0 = ((U0 + j) * 16) / 3;
+#pragma unroll
+        for (int tt = 0; tt < 6; tt++) {
+          const int64_t i = int64_t(g0 + tt) - int64_t(b);  // segment index of the unit's tt-th advisory
+          id[k][tt] = (j < nu && i >= 0 && i < int64_t(d.count)) ? a.adv[d.base + uint64_t(i)] : 0u;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kP; k++) {
+        const uint64_t j = j0 + uint64_t(k) * 64 + lane;
+        if (j >= nu) continue;
+        const uint64_t G0 = (U0 + j) * 16, g0 = G0 / 3;
+        const uint32_t r = uint32_t(G0 - g0 * 3);  // byte of advisory g0 the unit starts at
+        uint32_t wv[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+          const uint32_t tt = (r + q) / 3, kb = (r + q) % 3;
+          wv[q >> 2] |= ((id[k][tt] >> (8 * kb)) & 0xFFu) << (8 * (q & 3));
+        }
+        if (G0 >= B0 && G0 + 16 <= B1) {
+          reinterpret_cast<uint4*>(dst)[U0 + j] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        } else {  // a unit shared with a neighbour tile: its own bytes only
+#pragma unroll
+          for (int q = 0; q < 16; q++)
+            if (G0 + q >= B0 && G0 + q < B1) dst[G0 + q] = uint8_t(wv[q >> 2] >> (8 * (q & 3)));
+        }
+      }
+    }
+    return;
+  }
+  const uint64_t u0 = b >> 2;
+  uint64_t nu = fits && d.count ? ((b + d.count + 3) >> 2) - u0 : 0;
+  if (nu && u0 + nu > a.adv_units) {  // guard: never expected
+    if (lane == 0) atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
+    nu = 0;
+  }
+  const uint32_t sh = uint32_t(b & 3);
+  constexpr int kU = 4;
+  for (uint64_t j0 = 0; j0 < nu; j0 += uint64_t(kU) * 64) {
+    uint32_t v[kU][4];
+#pragma unroll
+    for (int k = 0; k < kU; k++) {
+      const uint64_t j = j0 + uint64_t(k) * 64 + lane;
+#pragma unroll
+      for (int w = 0; w < 4; w++) {
+        const int64_t i = int64_t(j * 4 + w) - int64_t(sh);  // segment index of the unit's word w
+        v[k][w] = (j < nu && i >= 0 && i < int64_t(d.count)) ? a.adv[d.base + uint64_t(i)] : 0u;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kU; k++) {
+      const uint64_t j = j0 + uint64_t(k) * 64 + lane;
+      if (j >= nu) continue;
+      const int64_t i0 = int64_t(j * 4) - int64_t(sh);
+      if (i0 >= 0 && i0 + 4 <= int64_t(d.count)) {
+        reinterpret_cast<uint4*>(a.adv_h)[u0 + j] = make_uint4(v[k][0], v[k][1], v[k][2], v[k][3]);
+      } else {  // the segment's first or last unit, shared with a neighbour tile: its own words only
+#pragma unroll
+        for (int w = 0; w < 4; w++)
+          if (i0 + w >= 0 && i0 + w < int64_t(d.count)) a.adv_h[(u0 + j) * 4 + w] = v[k][w];
+      }
+    }
+  }
+}
+
+// Workgroup `wg` of `n_wg` moves a contiguous run of the chunk's tiles: the CSR offsets of
+// the run's tiles from one block scan per 256 tiles, then each wave moves every fourth tile
+// on its own (round 4: a workgroup per tile in turn waited on its count pass, scan and move
+// one tile at a time; the kernel trace showed each 1M-package chunk's move taking ~450 us
+// beside 180 us of matching).  The delta form keeps the workgroup-per-tile encoder.
+__device__ __forceinline__ void copy_out_tiles(const CopyOutArgs& a, uint32_t wg, uint32_t n_wg, uint32_t* lds) {
+  if (a.delta || a.block_move) {
+    copy_out_tiles_block(a, wg, n_wg, lds);
+    return;
+  }
+  unsigned long long* pre = reinterpret_cast<unsigned long long*>(lds);  // kCopyRunMax offsets
+  uint32_t* red = lds + 2 * kCopyRunMax;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t* cw = red + 8 + wave * kTile;
+  const uint32_t nt = a.t1 - a.t0;
+  const uint32_t r0 = a.t0 + uint32_t(uint64_t(nt) * wg / n_wg), r1 = a.t0 + uint32_t(uint64_t(nt) * (wg + 1) / n_wg);
+  uint32_t before = 0;  // counts of the chunk's tiles before the run (a pass's total fits 32 bits: cap < 2^32)
+  for (uint32_t u = a.t0 + tid; u < r0; u += kTile) before += a.dir[u].count;
+  unsigned long long b = a.chunk_base[a.c] + copy_block_sum(before, red, tid);
+  for (uint32_t s0 = r0; s0 < r1; s0 += kCopyRunMax) {
+    const uint32_t s1 = min(r1, s0 + kCopyRunMax);
+    uint32_t tot;
+    const uint32_t ex = copy_block_scan(s0 + tid < s1 ? a.dir[s0 + tid].count : 0u, red, tid, tot);
+    pre[tid] = b + ex;
+    __syncthreads();
+    for (uint32_t t = s0 + wave; t < s1; t += kTile / 64) copy_out_tile_wave(a, t, pre[t - s0], lane, cw);
+    b += tot;
+    __syncthreads();  // pre is rewritten by the next segment
   }
   if (wg == n_wg - 1 && tid == 0) a.chunk_base[a.c + 1] = b;
 }

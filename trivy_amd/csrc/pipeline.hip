@@ -357,6 +357,8 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
   // TVM_PIPE_ROWEND_STORE=1 (measurement): the result move stores the row ends too, so no
   // device-to-host DMA shares the copy engines with the uploads
   static const bool rowend_store = std::getenv("TVM_PIPE_ROWEND_STORE") != nullptr;
+  // TVM_COPY_BLOCK=1 (measurement): the round-3 result move, a workgroup per tile
+  static const bool block_move = std::getenv("TVM_COPY_BLOCK") != nullptr;
   const bool rowend_dma = !delta_ && !rowend_store;
   auto copy_args = [&](uint32_t c) {
     CopyOutArgs ca;
@@ -379,6 +381,7 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
     ca.stream_h = stream_hd_;
     ca.stream_units = stream_bytes_ / 16;
     ca.tile_info_h = tile_info_hd_;
+    ca.block_move = block_move ? 1u : 0u;
     return ca;
   };
   // measurement only: TVM_PIPE_TRACE=1 prints the host time spent in each call of a pass;
