@@ -444,12 +444,13 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
     fa.sa = sa;
     if (co) {
       fa.co = *co;
-      // 64 workgroups move a chunk's results beside its match tiles (measured, C2 end-to-end:
-      // 64 3.10 ms, 128 3.13, 192 3.13, 256 3.25, 512 3.43, 1024 3.39;
-      // profiles/r03/e2e_copy_width.txt); TVM_COPY_WG overrides it for measurement
+      // 128 workgroups move a chunk's results beside its match tiles (measured, C2 end-to-end
+      // with the wave-per-tile move: 32 3.60 ms, 64 2.81, 128 2.77; round 3's workgroup-per-tile
+      // move: 64 3.10, 128 3.13, 256 3.25, profiles/r03/e2e_copy_width.txt); TVM_COPY_WG
+      // overrides it for measurement
       static const uint32_t n_copy = [] {
         const char* v = std::getenv("TVM_COPY_WG");
-        return v ? uint32_t(std::max(1, std::atoi(v))) : 64u;
+        return v ? uint32_t(std::max(1, std::atoi(v))) : 128u;
       }();
       // the delta form's encode is latency-bound per tile (a block scan per 256 matches), not
       // link-bound: more workgroups (TVM_COPY_WG_DELTA overrides it for measurement)
