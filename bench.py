@@ -309,10 +309,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-fill", action="store_true", help="c2: skip the FillInfo / Filter legs")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end pipelined pass")
-    ap.add_argument("--e2e-form", choices=["delta", "csr"], default="csr",
+    ap.add_argument("--e2e-form", choices=["delta", "csr", "byte"], default="csr",
                     help="result form of the end-to-end pass: the 3-byte CSR, or the delta form (TVM_PIPE_DELTA, "
                          "decoded to the CSR on the host threads inside the pass; measured slower, DESIGN.md §7); "
-                         "the other form is timed beside it (other_form)")
+                         "the other forms are timed beside it (other_forms)")
     ap.add_argument("--chunk", type=int, default=1 << 20, help="end-to-end pass: packages per pipeline chunk")
     ap.add_argument("--dropin", action="store_true",
                     help="c2: also time 100-package requests through the per-target driver path")
@@ -460,7 +460,9 @@ def main():
     # ---- end-to-end pipelined pass over PCIe (N = 1) -------------------------------------------
     e2e = None
     if world == 1 and not args.no_e2e and rank == 0:
-        delta = args.e2e_form == "delta"
+        forms = {"csr": {}, "byte": {"byte": True}, "delta": {"delta": True}}
+        form_name = {"csr": "CSR, 3-byte indices", "byte": "byte form (TVM_PIPE_BYTE), decoded inside the pass",
+                     "delta": "delta form (TVM_PIPE_DELTA), decoded inside the pass"}
 
         def passes(mp, k):
             ms, dec = [], []
@@ -474,28 +476,32 @@ def main():
 
         mp = MatchBatch(eng)
         wl.fill(mp)
-        mp.pipeline_prepare(match_cap=total, chunk_packages=args.chunk, delta=delta)
+        mp.pipeline_prepare(match_cap=total, chunk_packages=args.chunk, **forms[args.e2e_form])
         for _ in range(max(1, args.warmup)):
             mp.pipeline_run()
         npass = max(3, args.steps // 4)
         med, dec = passes(mp, npass)
         st = mp.pipeline_stats()
-        other = None  # the same batch in the other result form, for comparison
-        mp.pipeline_prepare(match_cap=total, chunk_packages=args.chunk, delta=not delta)
-        mp.pipeline_run()
-        omed, odec = passes(mp, npass)
-        ost = mp.pipeline_stats()
-        other = {"result_form": "CSR, 3-byte indices" if delta else "delta (TVM_PIPE_DELTA), decoded inside the pass",
-                 "packages_per_s": wl.n / (omed / 1e3), "ms_per_pass": omed, "d2h_bytes": ost["d2h_bytes"],
-                 "result_access_ms": odec}
+        other = []  # the same batch in the other result forms, for comparison
+        for f in forms:
+            if f == args.e2e_form:
+                continue
+            mp.pipeline_prepare(match_cap=total, chunk_packages=args.chunk, **forms[f])
+            mp.pipeline_run()
+            omed, odec = passes(mp, npass)
+            ost = mp.pipeline_stats()
+            other.append({"result_form": form_name[f], "packages_per_s": wl.n / (omed / 1e3), "ms_per_pass": omed,
+                          "d2h_bytes": ost["d2h_bytes"], "result_access_ms": odec})
+        delta = args.e2e_form != "csr"
         e2e = {"packages_per_s": wl.n / (med / 1e3), "ms_per_pass": med, "passes": npass,
-               "result_form": "delta (TVM_PIPE_DELTA)" if delta else "CSR, 3-byte indices",
+               "result_form": form_name[args.e2e_form],
                "result_access_ms": dec,
-               "result_is": ("the CSR (row ends + 4-byte indices) in pinned host memory, decoded from the delta form by "
-                             "the host threads inside the pass, chunk by chunk behind the GPU" if delta else
+               "result_is": ("the CSR (row ends + 4-byte indices) in pinned host memory, decoded from the "
+                             f"{args.e2e_form} form by the host threads inside the pass, chunk by chunk behind the GPU"
+                             if delta else
                              "3-byte indices + row ends in pinned host memory; tvm_pipeline_result widens the indices "
                              "after the pass (result_access_ms)"),
-               "other_form": other,
+               "other_forms": other,
                "h2d_bytes": st["h2d_bytes"], "d2h_bytes": st["d2h_bytes"], "chunks": st["chunks"],
                "pcie_GBs": (st["h2d_bytes"] + st["d2h_bytes"]) / (med / 1e3) / 1e9,
                "transport_form": st["transport_form"], "prepare_encode_ms": st["encode_ms"],
@@ -518,7 +524,7 @@ def main():
             wl.fill(mf)
             tp = time.perf_counter()
             mf.pipeline_prepare(match_cap=total, chunk_packages=args.chunk, raw=True,
-                                delta=args.e2e_form == "delta")
+                                **{"csr": {}, "byte": {"byte": True}, "delta": {"delta": True}}[args.e2e_form])
             tr = time.perf_counter()
             got, ep, _ = mf.pipeline_run()  # the result: the CSR in pinned host memory (3-byte indices, or decoded from the delta form inside the pass)
             te = time.perf_counter()

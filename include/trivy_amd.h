@@ -319,7 +319,13 @@ int tvm_batch_upload_into(tvm_engine* e, tvm_batch* b, void* pkg_dev, void* adv_
  * + a 4-byte row end per package), and tvm_pipeline_run decodes it into the CSR on the host
  * threads chunk by chunk while the GPU works on the later chunks (the call's time includes
  * it).  Needs a DB of fewer than 2^24 advisories (not with TVM_PIPE_ADV32). */
-enum { TVM_PIPE_RAW = 1, TVM_PIPE_ADV32 = 2, TVM_PIPE_DELTA = 4 };
+/* TVM_PIPE_BYTE: one byte per match at its CSR position (the low byte of a package's first
+ * advisory index, the package's high 16 bits apart, then 1-byte differences; larger steps
+ * escape to a sparse 4-byte array) beside the usual row ends (trivy_amd/csrc/byte_form.h);
+ * every position is known without a scan, so the result move writes whole words in place and
+ * tvm_pipeline_run decodes each chunk into the CSR behind the GPU.  Needs a DB of fewer than
+ * 2^24 advisories; not with TVM_PIPE_ADV32 or TVM_PIPE_DELTA. */
+enum { TVM_PIPE_RAW = 1, TVM_PIPE_ADV32 = 2, TVM_PIPE_DELTA = 4, TVM_PIPE_BYTE = 8 };
 int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32_t chunk_packages, uint32_t flags,
                          char* err, size_t errlen);
 /* One pass; ms = wall time of the call.  TVM_EINVAL with *n_matches set when the matches do
@@ -335,7 +341,7 @@ int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row
 /* The result as it arrived in pinned host memory: index i is the `width`-byte (3 or 4)
  * little-endian integer at adv + width * i. */
 int tvm_pipeline_result_raw(tvm_batch* b, const void** adv, uint32_t* width, const uint32_t** row_end,
-                            uint64_t* n_matches);  /* TVM_EINVAL for a TVM_PIPE_DELTA pipeline */
+                            uint64_t* n_matches);  /* TVM_EINVAL for a TVM_PIPE_DELTA / TVM_PIPE_BYTE pipeline */
 /* A TVM_PIPE_DELTA pass's result as it arrived: tile t's stream of tile_info[2t + 1] bytes at
  * stream + tvm_delta_region(t, CSR position of its first match), tile_info[2t] its matches. */
 int tvm_pipeline_result_delta(tvm_batch* b, const void** stream, uint64_t* stream_bytes, const uint32_t** tile_info,
@@ -346,6 +352,11 @@ int tvm_pipeline_result_delta(tvm_batch* b, const void** stream, uint64_t* strea
 int tvm_delta_decode(const void* stream, uint64_t stream_bytes, const uint32_t* tile_info, uint32_t n_tiles,
                      uint64_t n_matches, uint32_t* adv, uint32_t* row_end, char* err, size_t errlen);
 uint64_t tvm_delta_region(uint32_t tile, uint64_t first_match);
+/* Decodes a TVM_PIPE_BYTE result (bytes / hi / wide as trivy_amd/csrc/byte_form.h lays them
+ * out, row_end: n_tiles * 256 row ends) into adv; returns the escapes met, -1 on bad
+ * arguments.  Host only (the decode tvm_pipeline_run runs; test and inspection hook). */
+int64_t tvm_byte_decode(const uint8_t* bytes, const uint16_t* hi, const uint32_t* wide, const uint32_t* row_end,
+                        uint32_t n_tiles, uint32_t* adv);
 /* [0] bytes the last pass copied host to device, [1] device to host, [2] chunks, [3] 1 when
  * the batch travels in its transport form, [4] prepare's host time building it (us). */
 int tvm_pipeline_stats(tvm_batch* b, uint64_t out[5]);

@@ -82,3 +82,24 @@ def test_native_decode_refuses_inconsistent_streams():
 def test_region_matches_reference():
     for t, b in [(0, 0), (1, 7), (5, 1000), (70000, 3 << 30)]:
         assert lib().tvm_delta_region(t, b) == dr.region(t, b)
+
+
+# ---- the byte form (trivy_amd/csrc/byte_form.h, TVM_PIPE_BYTE) ----------------------------
+
+@pytest.mark.parametrize("kind,n_pkgs", [("plain", 1000), ("heavy", 700), ("empty_tiles", 1100), ("plain", 1)])
+def test_byte_form_native_decode_equals_reference(kind, n_pkgs):
+    import byte_ref as br
+    rng = np.random.default_rng(n_pkgs + 7)
+    adv, rend = _csr(rng, n_pkgs, kind)
+    nt = -(-n_pkgs // 256)
+    b, hi, wide, n_esc = br.encode(adv, rend, nt)
+    rpad = np.zeros(nt * 256, np.uint32)
+    rpad[:len(rend)] = rend
+    rpad[len(rend):] = rend[-1] if len(rend) else 0
+    assert np.array_equal(br.decode(b, hi, wide, rpad, len(adv)), adv)
+    out = np.zeros(max(len(adv), 1), np.uint32)
+    bb = np.concatenate([b, np.zeros(16, np.uint8)])
+    esc = lib().tvm_byte_decode(bb.ctypes.data, hi.ctypes.data, np.ascontiguousarray(wide).ctypes.data,
+                                rpad.ctypes.data, nt, out.ctypes.data)
+    assert esc == n_esc and (n_pkgs < 10 or n_esc > 0)
+    assert np.array_equal(out[:len(adv)], adv)

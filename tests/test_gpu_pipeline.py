@@ -33,16 +33,18 @@ def world():
     return sdb, build_engine(sdb)
 
 
-@pytest.mark.parametrize("raw,adv32,delta", [(False, False, False), (True, False, False), (False, True, False),
-                                             (False, False, True), (True, False, True)])
+@pytest.mark.parametrize("raw,adv32,delta,byte", [(False, False, False, False), (True, False, False, False),
+                                                  (False, True, False, False), (False, False, True, False),
+                                                  (True, False, True, False), (False, False, False, True),
+                                                  (True, False, False, True)])
 @pytest.mark.parametrize("chunk", [256, 1000, 4096, 1 << 19])
-def test_pipeline_matches_oracle(world, chunk, raw, adv32, delta, oracle_built):
+def test_pipeline_matches_oracle(world, chunk, raw, adv32, delta, byte, oracle_built):
     import delta_ref as dr
     sdb, eng = world
     batch = make_batch(sdb, 37, 333, [2, 2, 1], seed=chunk)  # 12321 packages: ragged last tile
     opk, oad = om.match(om.Prepared(sdb, batch), n_threads=8)
     mb = _fill(eng, sdb, batch).pipeline_prepare(match_cap=len(opk) + 5, chunk_packages=chunk, raw=raw, adv32=adv32,
-                                                 delta=delta)
+                                                 delta=delta, byte=byte)
     for _ in range(2):  # a second pass over the same pinned batch gives the same lists
         total, errp, ms = mb.pipeline_run()
         assert errp == -1 and total == len(opk) and ms > 0
@@ -53,6 +55,9 @@ def test_pipeline_matches_oracle(world, chunk, raw, adv32, delta, oracle_built):
             stream, info, n = mb.pipeline_delta()
             radv, rrend = dr.decode(stream, info)
             assert n == total and np.array_equal(radv, oad) and np.array_equal(rrend[:len(batch)], rend[:len(batch)])
+            with pytest.raises(RuntimeError):
+                mb.pipeline_csr_raw()
+        elif byte:
             with pytest.raises(RuntimeError):
                 mb.pipeline_csr_raw()
         else:
@@ -66,6 +71,9 @@ def test_pipeline_matches_oracle(world, chunk, raw, adv32, delta, oracle_built):
     if delta:
         stream, info, _ = mb.pipeline_delta()
         assert st["d2h_bytes"] == 8 * len(info) + int(((info[:, 1].astype(np.int64) + 15) // 16 * 16).sum())
+        assert st["d2h_bytes"] < 4 * len(batch) + 3 * len(opk)
+    elif byte:  # bytes + high halves + row ends (+ 4 per escape)
+        assert st["d2h_bytes"] >= len(opk) + 2 * nt * 256 + 4 * len(batch)
         assert st["d2h_bytes"] < 4 * len(batch) + 3 * len(opk)
     else:
         assert st["d2h_bytes"] == 4 * len(batch) + (4 if adv32 else 3) * len(opk)
@@ -88,11 +96,43 @@ def test_pipeline_delta_heavy_lists(oracle_built):
     batch = SynthBatch(base.plat, names, vers, list(base.targets))
     opk, oad = om.match(om.Prepared(sdb, batch), n_threads=4)
     assert np.bincount(opk).max() >= 255
-    mb = _fill(eng, sdb, batch).pipeline_prepare(match_cap=len(opk) + 1, chunk_packages=512, delta=True)
-    total, errp, _ = mb.pipeline_run()
-    pk, ad = _pairs_of(*mb.pipeline_csr())
-    assert total == len(opk) and np.array_equal(pk[:len(opk)], opk) and np.array_equal(ad[:len(opk)], oad)
+    for form in ("delta", "byte"):
+        mb = _fill(eng, sdb, batch).pipeline_prepare(match_cap=len(opk) + 1, chunk_packages=512, **{form: True})
+        total, errp, _ = mb.pipeline_run()
+        pk, ad = _pairs_of(*mb.pipeline_csr())
+        assert total == len(opk) and np.array_equal(pk[:len(opk)], opk) and np.array_equal(ad[:len(opk)], oad), form
+        mb.close()
+
+
+def test_pipeline_byte_form_escapes():
+    """The byte form's escapes on the GPU: a mixed OS + language batch (keys spanning two DB
+    roots, Red Hat releases) gives steps beyond 254 and backwards between a package's indices;
+    the decoded lists equal the device-resident pass's pairs."""
+    import trivy_amd
+    from tools import synth_mix as sm
+    from trivy_amd.batch import MatchBatch
+    sdb = sm.make_mix_db(sm.C4_PLATS, 2000, seed=0x5151)
+    eng = trivy_amd.Engine(sdb.put(trivy_amd.DB()).finalize(), 0)
+    batch = sm.make_mix_batch(sdb, 120_000, sm.C4_WEIGHTS, seed=29)
+    mb = MatchBatch(eng)
+    sm.add_to(mb, sdb, batch)
+    total, errp, bits = mb.run()
+    pr = mb.pairs().astype(np.int64)
+    n = len(mb)
+    want_end = np.cumsum(np.bincount(pr[:, 0], minlength=n)).astype(np.uint32)
+    first = np.ones(len(pr), bool)
+    first[1:] = pr[1:, 0] != pr[:-1, 0]
+    step = np.diff(pr[:, 1], prepend=0)
+    assert np.count_nonzero(~first & ((step < 1) | (step > 254))) > 0  # the case under test
+    mp = MatchBatch(eng)
+    sm.add_to(mp, sdb, batch)
+    mp.pipeline_prepare(match_cap=len(pr) + 1, chunk_packages=16384, byte=True)
+    got, errp2, _ = mp.pipeline_run()
+    adv, rend = mp.pipeline_csr()
+    assert got == total and errp2 == errp
+    assert np.array_equal(rend[:n], want_end) and np.array_equal(adv[:got], pr[:, 1].astype(np.uint32))
     mb.close()
+    mp.close()
 
 
 def test_pipeline_transport_form_edges(oracle_built):

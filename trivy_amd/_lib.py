@@ -213,6 +213,8 @@ _SIG = [
                                         ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p,
                                         ctypes.c_size_t]),
     ("tvm_delta_region", ctypes.c_uint64, [ctypes.c_uint32, ctypes.c_uint64]),
+    ("tvm_byte_decode", ctypes.c_int64, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_uint32, ctypes.c_void_p]),
     ("tvm_version_key", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p,
                                        ctypes.c_size_t]),
     ("tvm_engine_dropin_stats", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),

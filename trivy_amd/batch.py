@@ -229,15 +229,16 @@ class MatchBatch:
         return lib().tvm_match_algorithmic_bytes(self.engine.h, self.h)
 
     # ---- end-to-end pipelined pass (tvm_pipeline_*) ----
-    def pipeline_prepare(self, match_cap=None, chunk_packages=1 << 19, raw=False, adv32=False, delta=False):
+    def pipeline_prepare(self, match_cap=None, chunk_packages=1 << 19, raw=False, adv32=False, delta=False,
+                         byte=False):
         """Pins the batch and sizes the pipeline (host batch -> GPU -> host CSR).  raw: upload
         the batch's own arrays instead of its transport form (TVM_PIPE_RAW); adv32: 4-byte
         advisory indices in the result even when 3 bytes hold them (TVM_PIPE_ADV32); delta:
         the result crosses the link in the delta form (TVM_PIPE_DELTA, decoded by
-        pipeline_csr)."""
+        pipeline_csr); byte: the byte form (TVM_PIPE_BYTE, decoded inside the pass)."""
         e = errbuf()
         cap = match_cap if match_cap is not None else max(1024, 8 * len(self))
-        flags = (1 if raw else 0) | (2 if adv32 else 0) | (4 if delta else 0)
+        flags = (1 if raw else 0) | (2 if adv32 else 0) | (4 if delta else 0) | (8 if byte else 0)
         self._check(lib().tvm_pipeline_prepare(self.engine.h, self.h, cap, chunk_packages, flags, e, len(e)), e,
                     "tvm_pipeline_prepare")
         self.pipe_cap = cap

@@ -19,6 +19,7 @@
 #include "libdb.h"
 #include "libver.h"
 #include "bbolt.h"
+#include "byte_form.h"
 #include "delta_form.h"
 #include "host_par.h"
 #include "pipeline.h"
@@ -1339,8 +1340,10 @@ int tvm_match_filter_time(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o,
 
 int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32_t chunk_packages, uint32_t flags,
                          char* err, size_t errlen) {
-  if (!e || !b || chunk_packages == 0 || (flags & ~uint32_t(TVM_PIPE_RAW | TVM_PIPE_ADV32 | TVM_PIPE_DELTA)) ||
-      ((flags & TVM_PIPE_DELTA) && (flags & TVM_PIPE_ADV32)))
+  if (!e || !b || chunk_packages == 0 ||
+      (flags & ~uint32_t(TVM_PIPE_RAW | TVM_PIPE_ADV32 | TVM_PIPE_DELTA | TVM_PIPE_BYTE)) ||
+      ((flags & (TVM_PIPE_DELTA | TVM_PIPE_BYTE)) && (flags & TVM_PIPE_ADV32)) ||
+      ((flags & TVM_PIPE_DELTA) && (flags & TVM_PIPE_BYTE)))
     return TVM_EINVAL;
   std::shared_lock<std::shared_mutex> lk(e->mu);
   if (!bind(b, e)) {
@@ -1352,13 +1355,13 @@ int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32
   b->pipe_wide_for = ~0ull;
   std::string msg;
   const bool packed = !(flags & TVM_PIPE_ADV32) && e->db->db.advs.size() < (1ull << 24);
-  const bool delta = (flags & TVM_PIPE_DELTA) != 0;
-  if (delta && !packed) {
+  const bool delta = (flags & TVM_PIPE_DELTA) != 0, byte = (flags & TVM_PIPE_BYTE) != 0;
+  if ((delta || byte) && !packed) {
     b->pipe.reset();
-    set_err(err, errlen, "TVM_PIPE_DELTA: the delta form carries 3-byte advisory indices (the DB has 2^24 or more)");
+    set_err(err, errlen, "TVM_PIPE_DELTA / TVM_PIPE_BYTE: the form carries 3-byte advisory indices (the DB has 2^24 or more)");
     return TVM_EINVAL;
   }
-  if (!b->pipe->prepare(*e->eng, b->hb, match_cap, chunk_packages, !(flags & TVM_PIPE_RAW), packed, delta, msg)) {
+  if (!b->pipe->prepare(*e->eng, b->hb, match_cap, chunk_packages, !(flags & TVM_PIPE_RAW), packed, delta, byte, msg)) {
     b->pipe.reset();
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
@@ -1405,7 +1408,7 @@ int tvm_pipeline_run(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* 
 
 int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row_end, uint64_t* n_matches) {
   if (!b || !b->pipe || b->pipe_total > b->pipe->cap()) return TVM_EINVAL;
-  if (adv && b->pipe->packed() && !b->pipe->delta()) {  // widen the 3-byte indices once per pass (host side, after the pass)
+  if (adv && b->pipe->packed() && !b->pipe->delta() && !b->pipe->byte_form()) {  // widen the 3-byte indices once per pass (host side, after the pass)
     if (b->pipe_wide_for != b->pipe_runs) {
       const uint8_t* p = reinterpret_cast<const uint8_t*>(b->pipe->adv());
       b->pipe_wide.resize(b->pipe_total);
@@ -1426,7 +1429,7 @@ int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row
 
 int tvm_pipeline_result_raw(tvm_batch* b, const void** adv, uint32_t* width, const uint32_t** row_end,
                             uint64_t* n_matches) {
-  if (!b || !b->pipe || b->pipe_total > b->pipe->cap() || b->pipe->delta()) return TVM_EINVAL;
+  if (!b || !b->pipe || b->pipe_total > b->pipe->cap() || b->pipe->delta() || b->pipe->byte_form()) return TVM_EINVAL;
   if (adv) *adv = b->pipe->adv();
   if (width) *width = b->pipe->packed() ? 3 : 4;
   if (row_end) *row_end = b->pipe->row_end();
@@ -1458,6 +1461,14 @@ int tvm_delta_decode(const void* stream, uint64_t stream_bytes, const uint32_t* 
 }
 
 uint64_t tvm_delta_region(uint32_t tile, uint64_t first_match) { return delta_region(tile, first_match); }
+
+int64_t tvm_byte_decode(const uint8_t* bytes, const uint16_t* hi, const uint32_t* wide, const uint32_t* row_end,
+                        uint32_t n_tiles, uint32_t* adv) {
+  if (n_tiles && (!bytes || !hi || !wide || !row_end || !adv)) return -1;
+  int64_t esc = 0;
+  for (uint32_t t = 0; t < n_tiles; t++) esc += byte_decode_tile(bytes, hi, wide, row_end, t, adv);
+  return esc;
+}
 
 int tvm_wire_encode(size_t n, const uint32_t* plat, const char* arena, const uint64_t* name_off, const uint32_t* name_len,
                     const uint64_t* ver_off, const uint32_t* ver_len, uint32_t chunk_packages, int threads, void* out,

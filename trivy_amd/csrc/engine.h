@@ -148,6 +148,11 @@ struct CopyOutArgs {
   uint64_t stream_units = 0;          // 16-byte units of stream_h
   uint2* tile_info_h = nullptr;
   uint32_t block_move = 0;            // 1: the CSR move a workgroup per tile (round 3) instead of a wave per tile
+  // byte form (byte_form.h): one byte per match at its CSR position in adv_h, the high 16 bits
+  // of each package's first advisory at hi_h[package], escaped values at wide_h[position]
+  uint32_t byte_form = 0;
+  uint16_t* hi_h = nullptr;
+  uint32_t* wide_h = nullptr;
 };
 constexpr uint32_t kDeltaStage = 2080;  // copy_out_tiles' delta staging bytes: header + one chunk's worst case + a carried unit
 constexpr uint32_t kCopyRunMax = kTile;  // tiles per prefix segment of the wave-per-tile move
@@ -417,6 +422,70 @@ __device__ __forceinline__ void copy_out_tiles_block(const CopyOutArgs& a, uint3
   if (wg == n_wg - 1 && tid == 0) a.chunk_base[a.c + 1] = b;
 }
 
+// The byte form of one tile's segment (byte_form.h), by one wave: match i of the segment is
+// the byte at CSR position b + i - the low byte of its advisory index when it is its
+// package's first (the package's high 16 bits go to hi_h[package]), else the difference
+// from the one before when that is 1..254, else 0xFF with the index at wide_h[b + i].  Each
+// lane assembles four consecutive bytes (one destination word) from the five advisories they
+// depend on; hw: the wave's 256 high halves (LDS), stored once per tile as 512 bytes.
+__device__ __forceinline__ void copy_out_tile_bytes(const CopyOutArgs& a, const TileDir& d, bool fits, uint64_t b,
+                                                    uint32_t p_first, uint32_t lane, uint16_t* hw) {
+  // hw overlays the counts the caller has read: every lane's read before any lane's write
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  reinterpret_cast<uint2*>(hw)[lane] = make_uint2(0, 0);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const uint64_t w0 = b >> 2;
+  const uint32_t sh = uint32_t(b & 3);
+  uint64_t nw = fits && d.count ? ((b + d.count + 3) >> 2) - w0 : 0;
+  if (nw && w0 + nw > a.adv_units * 4) {  // guard: never expected (adv_h holds cap + 16 bytes)
+    if (lane == 0) atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
+    nw = 0;
+  }
+  for (uint64_t j = lane; j < nw; j += 64) {
+    const int64_t i0 = int64_t(j * 4) - int64_t(sh);  // segment index of the word's first byte
+    uint32_t pk[5], ad[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) {  // matches i0 - 1 .. i0 + 3
+      const int64_t i = i0 - 1 + k;
+      const bool in = i >= 0 && i < int64_t(d.count);
+      pk[k] = in ? a.pkg[d.base + uint64_t(i)] : 0xFFFFFFFFu;
+      ad[k] = in ? a.adv[d.base + uint64_t(i)] : 0u;
+    }
+    uint32_t word = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int64_t i = i0 + k;
+      if (i < 0 || i >= int64_t(d.count)) continue;
+      const bool first = pk[k] != pk[k + 1];  // i == 0 reads pk[k] = none
+      const uint32_t q = ad[k + 1] - ad[k];
+      uint32_t v;
+      if (first) {
+        v = ad[k + 1] & 0xFFu;
+        hw[(pk[k + 1] - a.pkg_base - p_first) & (kTile - 1)] = uint16_t(ad[k + 1] >> 8);
+      } else if (q - 1u < 254u) {
+        v = q;
+      } else {
+        v = 0xFFu;
+        a.wide_h[b + uint64_t(i)] = ad[k + 1];
+      }
+      word |= v << (8 * k);
+    }
+    if (i0 >= 0 && i0 + 4 <= int64_t(d.count)) {
+      a.adv_h[w0 + j] = word;
+    } else {  // the segment's first or last word, shared with a neighbour tile: its own bytes only
+      uint8_t* dst = reinterpret_cast<uint8_t*>(a.adv_h) + (w0 + j) * 4;
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (i0 + k >= 0 && i0 + k < int64_t(d.count)) dst[k] = uint8_t(word >> (8 * k));
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  reinterpret_cast<uint2*>(a.hi_h)[(p_first >> 2) + lane] = reinterpret_cast<const uint2*>(hw)[lane];
+}
+
 // One tile's CSR move by one wave (lane of 64): its per-package counts in the wave's own LDS
 // array (no workgroup barrier: one wave's LDS operations are ordered), the 256 row ends
 // from a wave scan (4 packages a lane, one 16-byte store each), then the segment realigned to
@@ -456,6 +525,10 @@ __device__ __forceinline__ void copy_out_tile_wave(const CopyOutArgs& a, uint32_
     reinterpret_cast<uint4*>(a.row_end_h)[p_first / 4 + lane] = make_uint4(e + s0, e + s1, e + s2, e + s3);
   else
     atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
+  if (a.byte_form) {
+    copy_out_tile_bytes(a, d, fits, b, p_first, lane, reinterpret_cast<uint16_t*>(cw));
+    return;
+  }
   if (a.packed) {  // 3 bytes per advisory: destination bytes [3b, 3(b + count)) in 16-byte units
     const uint64_t B0 = 3 * b, B1 = 3 * (b + d.count), U0 = B0 >> 4;
     uint64_t nu = fits && d.count ? ((B1 + 15) >> 4) - U0 : 0;

@@ -46,8 +46,9 @@ class Pipeline {
   // packed: the result's advisory indices travel as 3 bytes each (the DB has < 2^24);
   // delta (implies packed): the result travels in the delta form (delta_form.h) and run()
   // decodes it into the CSR on the host threads chunk by chunk, overlapping the GPU
+  // byte (implies packed): the byte form (byte_form.h), decoded by run() like the delta form
   bool prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uint32_t chunk_packages, bool transport,
-               bool packed, bool delta, std::string& err);
+               bool packed, bool delta, bool byte, std::string& err);
   // One pass.  total = matches (> match_cap: nothing valid, re-prepare with a larger cap);
   // err_pkg = first poisoned package or -1.
   bool run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& err_pkg, uint64_t& err_bits, std::string& err);
@@ -55,6 +56,7 @@ class Pipeline {
   bool packed() const { return packed_; }
   const uint32_t* row_end() const { return row_end_h_; }
   bool delta() const { return delta_; }
+  bool byte_form() const { return byte_; }
   // the delta form of the last pass: the streams and the per-tile {count, bytes}
   const uint8_t* delta_stream() const { return stream_h_; }
   uint64_t delta_stream_size() const { return stream_bytes_; }
@@ -111,6 +113,14 @@ class Pipeline {
   uint2* tile_info_h_ = nullptr;
   uint2* tile_info_hd_ = nullptr;
   std::vector<uint64_t> tile_pos_;  // CSR position of each tile's first match (the decode)
+  bool byte_ = false;               // the byte form: bytes / high halves / escapes (pinned, device-mapped)
+  uint8_t* bytes_h_ = nullptr;
+  uint8_t* bytes_hd_ = nullptr;
+  uint16_t* hi_h_ = nullptr;
+  uint16_t* hi_hd_ = nullptr;
+  uint32_t* wide_h_ = nullptr;
+  uint32_t* wide_hd_ = nullptr;
+  std::vector<hipEvent_t> ev_d_;    // chunk's row ends landed (the byte form's decode waits on it)
   bool packed_ = false;  // no Engine pointer: the batch may outlive a hot swap (the C-ABI checks the generation)
 };
 

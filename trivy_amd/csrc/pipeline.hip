@@ -2,6 +2,7 @@
 // and the order kernel's direct writes of the result into host memory overlap chunk by chunk.  Every buffer is sized once in prepare(); a pass
 // allocates nothing.
 #include "pipeline.h"
+#include "byte_form.h"
 #include "delta_form.h"
 #include "host_par.h"
 #include "pool.h"
@@ -189,8 +190,15 @@ void Pipeline::release() {
     pool_device_put(dev_, p);
   for (void* p : {static_cast<void*>(wire_h_), static_cast<void*>(raw_h_), static_cast<void*>(adv_h_),
                   static_cast<void*>(row_end_h_), static_cast<void*>(ctl_h_), static_cast<void*>(stream_h_),
-                  static_cast<void*>(tile_info_h_)})
+                  static_cast<void*>(tile_info_h_), static_cast<void*>(bytes_h_), static_cast<void*>(hi_h_),
+                  static_cast<void*>(wide_h_)})
     pool_host_put(p);
+  bytes_h_ = bytes_hd_ = nullptr;
+  hi_h_ = hi_hd_ = nullptr;
+  wide_h_ = wide_hd_ = nullptr;
+  byte_ = false;
+  for (hipEvent_t e : ev_d_) (void)hipEventDestroy(e);
+  ev_d_.clear();
   stream_h_ = stream_hd_ = nullptr;
   tile_info_h_ = tile_info_hd_ = nullptr;
   stream_bytes_ = 0;
@@ -219,7 +227,7 @@ void Pipeline::release() {
 }
 
 bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uint32_t chunk_packages, bool transport,
-                       bool packed, bool delta, std::string& err) {
+                       bool packed, bool delta, bool byte, std::string& err) {
   release();
   const auto start = std::chrono::steady_clock::now();
   dev_ = eng.device();
@@ -252,8 +260,9 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
   toff_ = hb.tile_off;  // per 64-package group, + the arena end, padded to whole tiles
   toff_.resize(size_t(n_tiles) * kGroupsPerTile + 1, hb.arena.size());
   cap_ = std::max<uint64_t>(match_cap, 1);
-  packed_ = packed || delta;
+  packed_ = packed || delta || byte;
   delta_ = delta;
+  byte_ = byte && !delta;
   if (cap_ >= (1ull << 32)) {
     err = "pipeline: row ends are 32-bit; split the batch below 2^32 matches";
     return false;
@@ -264,6 +273,11 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
     if (!ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate", err)) return false;
   for (hipEvent_t& e : ev_h_)
     if (!ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate", err)) return false;
+  if (byte_) {
+    ev_d_.resize(nc);
+    for (hipEvent_t& e : ev_d_)
+      if (!ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate", err)) return false;
+  }
   if (!ok(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking), "hipStreamCreate", err) ||
       !ok(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking), "hipStreamCreate", err) ||
       !ok(hipStreamCreateWithFlags(&s_k_, hipStreamNonBlocking), "hipStreamCreate", err))
@@ -324,6 +338,20 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
   row_end_hd_ = static_cast<uint32_t*>(p);
   if (!(p = pool_device_get(dev_, std::max<size_t>(n4, 4) * 4, "hipMalloc(row ends)", err))) return false;
   row_end_d_ = static_cast<uint32_t*>(p);
+  if (byte_) {  // the byte form's three arrays, written by the result move; adv_h_ holds the decoded CSR
+    if (!(p = pool_host_get(cap4 + 64, "hipHostMalloc(bytes)", err))) return false;
+    bytes_h_ = static_cast<uint8_t*>(p);
+    if (!ok(hipHostGetDevicePointer(&p, bytes_h_, 0), "hipHostGetDevicePointer(bytes)", err)) return false;
+    bytes_hd_ = static_cast<uint8_t*>(p);
+    if (!(p = pool_host_get(std::max<size_t>(n4, 4) * 2, "hipHostMalloc(high halves)", err))) return false;
+    hi_h_ = static_cast<uint16_t*>(p);
+    if (!ok(hipHostGetDevicePointer(&p, hi_h_, 0), "hipHostGetDevicePointer(high halves)", err)) return false;
+    hi_hd_ = static_cast<uint16_t*>(p);
+    if (!(p = pool_host_get(cap4 * 4, "hipHostMalloc(escapes)", err))) return false;
+    wide_h_ = static_cast<uint32_t*>(p);
+    if (!ok(hipHostGetDevicePointer(&p, wide_h_, 0), "hipHostGetDevicePointer(escapes)", err)) return false;
+    wide_hd_ = static_cast<uint32_t*>(p);
+  }
   if (!(p = pool_host_get(64, "hipHostMalloc(ctl)", err))) return false;
   ctl_h_ = static_cast<unsigned long long*>(p);
   prepared_ = true;
@@ -382,6 +410,13 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
     ca.stream_units = stream_bytes_ / 16;
     ca.tile_info_h = tile_info_hd_;
     ca.block_move = block_move ? 1u : 0u;
+    if (byte_) {
+      ca.byte_form = 1;
+      ca.adv_h = reinterpret_cast<uint32_t*>(bytes_hd_);
+      ca.adv_units = (cap_ + 64) / 16;
+      ca.hi_h = hi_hd_;
+      ca.wide_h = wide_hd_;
+    }
     return ca;
   };
   // measurement only: TVM_PIPE_TRACE=1 prints the host time spent in each call of a pass;
@@ -397,7 +432,8 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
     return ok(hipEventRecord(ev_k_[c], s_k_), "hipEventRecord", err) &&
            ok(hipStreamWaitEvent(s_d2h_, ev_k_[c], 0), "hipStreamWaitEvent", err) &&
            ok(hipMemcpyAsync(row_end_h_ + q0, row_end_d_ + q0, (q1 - q0) * 4, hipMemcpyDeviceToHost, s_d2h_),
-              "D2H row ends", err);
+              "D2H row ends", err) &&
+           (!byte_ || ok(hipEventRecord(ev_d_[c], s_d2h_), "hipEventRecord", err));
   };
   const auto T0 = std::chrono::steady_clock::now();
   auto us = [&]() { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - T0).count(); };
@@ -486,6 +522,29 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
   // result move is done, while the GPU works on the chunks after it
   bool decoded = true;
   static const bool no_decode = std::getenv("TVM_PIPE_NODECODE") != nullptr;  // measurement only: the bytes alone
+  uint64_t escapes = 0;
+  if (byte_ && !no_decode) {  // each chunk decoded once its move and its row ends have landed
+    for (uint32_t c = 0; c < nc; c++) {
+      const uint32_t t0 = bounds_[c], t1 = bounds_[c + 1];
+      if (t1 == t0) continue;
+      if (!ok(hipEventSynchronize(ev_d_[c]), "pipeline", err)) return false;
+      if (trace) std::fprintf(stderr, "pipe c%u moved %.1f us\n", c, us());
+      if (row_end_h_[size_t(t1) * kTile - 1] > cap_) {  // an overflowed pass: the total says so below
+        decoded = false;
+        break;
+      }
+      std::atomic<uint64_t> esc{0};
+      constexpr uint32_t kPiece = 16;  // tiles per work item
+      WorkerPool::get().parallel_for((t1 - t0 + kPiece - 1) / kPiece, [&](size_t k) {
+        const uint32_t a0 = t0 + uint32_t(k) * kPiece, a1 = std::min(t1, a0 + kPiece);
+        uint64_t e = 0;
+        for (uint32_t t = a0; t < a1; t++) e += byte_decode_tile(bytes_h_, hi_h_, wide_h_, row_end_h_, t, adv_h_);
+        esc += e;
+      });
+      escapes += esc;
+      if (trace) std::fprintf(stderr, "pipe c%u decoded %.1f us\n", c, us());
+    }
+  }
   if (delta_ && !no_decode) {
     uint64_t pos = 0;
     for (uint32_t c = 0; c < nc && decoded; c++) {
@@ -518,10 +577,12 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
   if (delta_) {
     d2h_ = 0;
     for (uint32_t t = 0; t < n_tiles(); t++) d2h_ += sizeof(uint2) + ((tile_info_h_[t].y + 15) & ~15u);
+  } else if (byte_) {  // bytes + high halves + row ends + escapes
+    d2h_ = std::min<uint64_t>(ctl_h_[0], cap_) + uint64_t(n_tiles()) * kTile * 2 + uint64_t(n) * 4 + escapes * 4;
   } else {
     d2h_ = uint64_t(n) * 4 + std::min<uint64_t>(ctl_h_[0], cap_) * (packed_ ? 3 : 4);
   }
-  if (delta_ && !decoded && ctl_h_[0] <= cap_ && !ctl_h_[3] && !ctl_h_[1]) {
+  if ((delta_ || byte_) && !decoded && ctl_h_[0] <= cap_ && !ctl_h_[3] && !ctl_h_[1]) {
     err = "pipeline: the delta form of the result is inconsistent with the tiles' counts";
     return false;
   }
