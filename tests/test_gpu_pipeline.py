@@ -104,34 +104,33 @@ def test_pipeline_delta_heavy_lists(oracle_built):
         mb.close()
 
 
-def test_pipeline_byte_form_escapes():
-    """The byte form's escapes on the GPU: a mixed OS + language batch (keys spanning two DB
-    roots, Red Hat releases) gives steps beyond 254 and backwards between a package's indices;
-    the decoded lists equal the device-resident pass's pairs."""
-    import trivy_amd
-    from tools import synth_mix as sm
-    from trivy_amd.batch import MatchBatch
-    sdb = sm.make_mix_db(sm.C4_PLATS, 2000, seed=0x5151)
-    eng = trivy_amd.Engine(sdb.put(trivy_amd.DB()).finalize(), 0)
-    batch = sm.make_mix_batch(sdb, 120_000, sm.C4_WEIGHTS, seed=29)
-    mb = MatchBatch(eng)
-    sm.add_to(mb, sdb, batch)
-    total, errp, bits = mb.run()
-    pr = mb.pairs().astype(np.int64)
-    n = len(mb)
-    want_end = np.cumsum(np.bincount(pr[:, 0], minlength=n)).astype(np.uint32)
-    first = np.ones(len(pr), bool)
-    first[1:] = pr[1:, 0] != pr[:-1, 0]
-    step = np.diff(pr[:, 1], prepend=0)
+def test_pipeline_byte_form_escapes(oracle_built):
+    """The byte form's escapes on the GPU: the heavy key's advisories are fixed below the
+    installed version except every 300th, so a "linux" package matches advisories 300 apart -
+    steps beyond 254, which travel as escapes (0xFF + the index in the sparse wide array) -
+    beside ordinary packages; equal to the oracle."""
+    from test_gpu_parity import build_engine
+    from tools.synth import SynthBatch
+    sdb = make_db(["debian 12"], 400, seed=33, max_adv=3000)
+    lk = sdb.key_names.index(b"linux")
+    b0, b1 = int(sdb.adv_begin[lk]), int(sdb.adv_begin[lk + 1])
+    for a in range(b0, b1):
+        sdb.adv_fixed[a] = b"99.0-1" if (a - b0) % 300 == 7 else b"0.0.1-1"
+    eng = build_engine(sdb)
+    base = make_batch(sdb, 4, 300, [1], seed=3)
+    names, vers = list(base.names), list(base.versions)
+    for i in range(5, len(names), 41):
+        names[i], vers[i] = b"linux", b"1.0-1"
+    batch = SynthBatch(base.plat, names, vers, list(base.targets))
+    opk, oad = om.match(om.Prepared(sdb, batch), n_threads=4)
+    first = np.ones(len(opk), bool)
+    first[1:] = opk[1:] != opk[:-1]
+    step = np.diff(oad.astype(np.int64), prepend=0)
     assert np.count_nonzero(~first & ((step < 1) | (step > 254))) > 0  # the case under test
-    mp = MatchBatch(eng)
-    sm.add_to(mp, sdb, batch)
-    mp.pipeline_prepare(match_cap=len(pr) + 1, chunk_packages=16384, byte=True)
-    got, errp2, _ = mp.pipeline_run()
-    adv, rend = mp.pipeline_csr()
-    assert got == total and errp2 == errp
-    assert np.array_equal(rend[:n], want_end) and np.array_equal(adv[:got], pr[:, 1].astype(np.uint32))
-    mb.close()
+    mp = _fill(eng, sdb, batch).pipeline_prepare(match_cap=len(opk) + 1, chunk_packages=512, byte=True)
+    total, errp, _ = mp.pipeline_run()
+    pk, ad = _pairs_of(*mp.pipeline_csr())
+    assert total == len(opk) and np.array_equal(pk[:len(opk)], opk) and np.array_equal(ad[:len(opk)], oad)
     mp.close()
 
 
