@@ -16,18 +16,23 @@ uint32_t byte_decode_tile(const uint8_t* A, const uint16_t* hi, const uint32_t* 
   // there, any other adds its byte (a loop keyed on the next first position made that
   // position, loaded through the package counter, part of the chain: 3.8 ns a match).
   thread_local std::vector<uint8_t> flag;
+  thread_local std::vector<uint32_t> fval;
   const uint32_t* re = row_end + size_t(t) * kTile;
   const uint16_t* h = hi + size_t(t) * kTile;
   const uint32_t b = t ? row_end[size_t(t) * kTile - 1] : 0u, end = re[kTile - 1];
   if (end <= b) return 0;
   const uint32_t count = end - b;
-  if (flag.size() < count) flag.resize(count);
+  if (flag.size() < count) {
+    flag.resize(count);
+    fval.resize(count);
+  }
   uint8_t* fl = flag.data();
+  uint32_t* fv = fval.data();
   std::memset(fl, 0, count);
   uint32_t prev = b;
   for (uint32_t p = 0; p < uint32_t(kTile); p++) {
     if (re[p] != prev) {
-      adv[prev] = (uint32_t(h[p]) << 8) | A[prev];
+      fv[prev - b] = (uint32_t(h[p]) << 8) | A[prev];
       fl[prev - b] = 1;
     }
     prev = re[p];
@@ -36,7 +41,7 @@ uint32_t byte_decode_tile(const uint8_t* A, const uint16_t* hi, const uint32_t* 
   uint32_t* o = adv + b;
   const uint8_t* x = A + b;
   for (uint32_t i = 0; i < count; i++) {
-    const uint32_t xi = x[i], pre = o[i];
+    const uint32_t xi = x[i], pre = fv[i];
     const bool f = fl[i] != 0;
     if (!f && xi == 0xFFu) {  // rare
       a = wide[b + i];

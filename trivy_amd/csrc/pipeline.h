@@ -52,7 +52,8 @@ class Pipeline {
   // One pass.  total = matches (> match_cap: nothing valid, re-prepare with a larger cap);
   // err_pkg = first poisoned package or -1.
   bool run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& err_pkg, uint64_t& err_bits, std::string& err);
-  const uint32_t* adv() const { return adv_h_; }  // 4-byte indices, or 3-byte ones when packed() and not delta()
+  // 4-byte indices (the decoded CSR for the delta / byte forms), or 3-byte ones when packed()
+  const uint32_t* adv() const { return (delta_ || byte_) ? csr_h_ : adv_h_; }
   bool packed() const { return packed_; }
   const uint32_t* row_end() const { return row_end_h_; }
   bool delta() const { return delta_; }
@@ -113,6 +114,7 @@ class Pipeline {
   uint2* tile_info_h_ = nullptr;
   uint2* tile_info_hd_ = nullptr;
   std::vector<uint64_t> tile_pos_;  // CSR position of each tile's first match (the decode)
+  uint32_t* csr_h_ = nullptr;       // delta / byte forms: the decoded advisory indices (pageable, pool_heap_get)
   bool byte_ = false;               // the byte form: bytes / high halves / escapes (pinned, device-mapped)
   uint8_t* bytes_h_ = nullptr;
   uint8_t* bytes_hd_ = nullptr;

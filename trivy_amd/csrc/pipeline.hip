@@ -193,6 +193,8 @@ void Pipeline::release() {
                   static_cast<void*>(tile_info_h_), static_cast<void*>(bytes_h_), static_cast<void*>(hi_h_),
                   static_cast<void*>(wide_h_)})
     pool_host_put(p);
+  pool_heap_put(csr_h_);
+  csr_h_ = nullptr;
   bytes_h_ = bytes_hd_ = nullptr;
   hi_h_ = hi_hd_ = nullptr;
   wide_h_ = wide_hd_ = nullptr;
@@ -314,8 +316,10 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
     // the CSR the pass decodes the streams into, chunk by chunk (pooled: a fresh batch of a
     // size seen before touches no new pages)
     const size_t cap4 = (cap_ + 3) & ~size_t(3), n4 = (size_t(n_tiles) * kTile + 3) & ~size_t(3);
-    if (!(p = pool_host_get(cap4 * 4, "hipHostMalloc(adv)", err))) return false;
-    adv_h_ = static_cast<uint32_t*>(p);
+    if (!(csr_h_ = static_cast<uint32_t*>(pool_heap_get(cap4 * 4)))) {
+      err = "pipeline: host memory for the decoded result";
+      return false;
+    }
     if (!(p = pool_host_get(std::max<size_t>(n4, 4) * 4, "hipHostMalloc(row ends)", err))) return false;
     row_end_h_ = static_cast<uint32_t*>(p);
     tile_pos_.assign(size_t(n_tiles) + 1, 0);
@@ -351,6 +355,10 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
     wide_h_ = static_cast<uint32_t*>(p);
     if (!ok(hipHostGetDevicePointer(&p, wide_h_, 0), "hipHostGetDevicePointer(escapes)", err)) return false;
     wide_hd_ = static_cast<uint32_t*>(p);
+    if (!(csr_h_ = static_cast<uint32_t*>(pool_heap_get(cap4 * 4)))) {
+      err = "pipeline: host memory for the decoded result";
+      return false;
+    }
   }
   if (!(p = pool_host_get(64, "hipHostMalloc(ctl)", err))) return false;
   ctl_h_ = static_cast<unsigned long long*>(p);
@@ -538,7 +546,7 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
       WorkerPool::get().parallel_for((t1 - t0 + kPiece - 1) / kPiece, [&](size_t k) {
         const uint32_t a0 = t0 + uint32_t(k) * kPiece, a1 = std::min(t1, a0 + kPiece);
         uint64_t e = 0;
-        for (uint32_t t = a0; t < a1; t++) e += byte_decode_tile(bytes_h_, hi_h_, wide_h_, row_end_h_, t, adv_h_);
+        for (uint32_t t = a0; t < a1; t++) e += byte_decode_tile(bytes_h_, hi_h_, wide_h_, row_end_h_, t, csr_h_);
         esc += e;
       });
       escapes += esc;
@@ -565,7 +573,7 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
       WorkerPool::get().parallel_for((t1 - t0 + kPiece - 1) / kPiece, [&](size_t k) {
         const uint32_t a0 = t0 + uint32_t(k) * kPiece, a1 = std::min(t1, a0 + kPiece);
         for (uint32_t t = a0; t < a1; t++)
-          if (!delta_decode_tile(stream_h_, stream_bytes_, t, tile_pos_[t], tile_info_h_[t], adv_h_, row_end_h_))
+          if (!delta_decode_tile(stream_h_, stream_bytes_, t, tile_pos_[t], tile_info_h_[t], csr_h_, row_end_h_))
             bad = true;
       });
       if (bad) decoded = false;

@@ -11,6 +11,9 @@
 
 namespace tvm {
 
+void* huge_alloc(size_t bytes);  // sbom.cpp: anonymous mappings advised for transparent huge pages
+void huge_free(void* p, size_t bytes);
+
 namespace {
 
 // Free bytes kept per kind before blocks are really freed (a C2 pipeline holds ~0.5 GB of
@@ -28,6 +31,7 @@ struct Pool {
   std::mutex mu;
   std::map<int, Kind> dev;  // per device
   Kind host;
+  Kind heap;  // pageable (pool_heap_*)
   unsigned long long hits = 0, misses = 0;
 };
 
@@ -52,8 +56,8 @@ void shrink(Kind& k, size_t keep, FreeFn&& fr) {
   while (k.cached > keep && !k.free_.empty()) {
     auto it = std::prev(k.free_.end());
     k.cached -= it->first;
+    fr(it->second);  // before its capacity is forgotten (the heap kind's free needs it)
     k.cap_.erase(it->second);
-    fr(it->second);
     k.free_.erase(it);
   }
 }
@@ -150,6 +154,34 @@ void pool_host_put(void* p) {
   shrink(P.host, kKeepHost, [](void* q) { (void)hipHostFree(q); });
 }
 
+void* pool_heap_get(size_t bytes) {
+  Pool& P = pool();
+  bytes = round_up(bytes);
+  {
+    std::lock_guard<std::mutex> lk(P.mu);
+    if (void* p = take(P.heap, bytes)) return p;
+  }
+  void* p = huge_alloc(bytes);
+  if (!p) return nullptr;
+  std::lock_guard<std::mutex> lk(P.mu);
+  P.heap.cap_[p] = bytes;
+  return p;
+}
+
+void pool_heap_put(void* p) {
+  if (!p) return;
+  Pool& P = pool();
+  std::lock_guard<std::mutex> lk(P.mu);
+  auto it = P.heap.cap_.find(p);
+  if (it == P.heap.cap_.end()) return;
+  P.heap.free_.emplace(it->second, p);
+  P.heap.cached += it->second;
+  shrink(P.heap, kKeepHost, [&](void* q) {
+    auto c = P.heap.cap_.find(q);
+    huge_free(q, c == P.heap.cap_.end() ? 0 : c->second);
+  });
+}
+
 void pool_trim() {
   Pool& P = pool();
   std::lock_guard<std::mutex> lk(P.mu);
@@ -159,6 +191,10 @@ void pool_trim() {
       (void)hipFree(q);
     });
   shrink(P.host, 0, [](void* q) { (void)hipHostFree(q); });
+  shrink(P.heap, 0, [&](void* q) {
+    auto c = P.heap.cap_.find(q);
+    huge_free(q, c == P.heap.cap_.end() ? 0 : c->second);
+  });
 }
 
 void pool_stats(unsigned long long out[4]) {

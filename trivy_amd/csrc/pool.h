@@ -18,6 +18,10 @@ void* pool_device_get(int device, size_t bytes, const char* what, std::string& e
 void pool_device_put(int device, void* p);
 void* pool_host_get(size_t bytes, const char* what, std::string& err);  // pinned, device-mapped
 void pool_host_put(void* p);
+// Pageable host blocks (huge-page mappings) for what only the host reads and writes: the CSR
+// a pass decodes its result into (pinned memory is no place for a CPU loop's stores).
+void* pool_heap_get(size_t bytes);
+void pool_heap_put(void* p);
 // Frees every cached block (tests; a process that wants its memory back).
 void pool_trim();
 // {cached device bytes, cached host bytes, hits, misses}
