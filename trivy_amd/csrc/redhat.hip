@@ -15,7 +15,7 @@
 //           (package, ID-rank); per tile its group count (a tile without Red Hat
 //           packages: its pair count, no reads of the pairs);
 //   scan    the tiles' output bases (rocPRIM device scan);
-//   emit    block scan of the head flags; each head lane walks its group (a few pairs) for
+//   emit    a wave per tile: ballot prefix of the head flags; each head lane walks its group (a few pairs) for
 //           the member with the greatest fixed version (rpm-order rank computed at load
 //           time; ties keep the first, as LessThan does) and writes {pkg, representative,
 //           base, raw range}.
@@ -63,73 +63,56 @@ __device__ __forceinline__ uint32_t group_key(const MergeArgs& a, uint32_t p, ui
   return rh ? a.adv_rank[ad].x : kNoKey;
 }
 
-// Exclusive block scan of one flag per lane; returns the block total.  One barrier: the
-// caller alternates two ws buffers between consecutive calls (the barriers between two calls
-// on one buffer order its reads before its next writes).
-__device__ __forceinline__ uint32_t block_flag_scan(bool f, uint32_t tid, uint32_t* ws, uint32_t& excl) {
-  const uint32_t lane = tid & 63, wave = tid >> 6;
-  const unsigned long long bal = __ballot(f);
-  if (lane == 0) ws[wave] = uint32_t(__popcll(bal));
-  __syncthreads();
-  uint32_t off = 0, tot = 0;
+// Per package of tile t: 1 = a Red Hat package (its pairs' group keys are their ID ranks);
+// one wave fills its own 256 flags (4 a lane) in LDS.
+__device__ __forceinline__ void tile_redhat_flags(const MergeArgs& a, uint32_t t, uint32_t lane, uint8_t* rhp) {
 #pragma unroll
-  for (int w = 0; w < kWaves; w++) {
-    const uint32_t c = ws[w];
-    off += uint32_t(w) < wave ? c : 0u;
-    tot += c;
+  for (int k = 0; k < 4; k++) {
+    const uint32_t p = t * kBlock + lane * 4 + k;
+    const uint32_t plat = p < a.n ? a.pk[p].x : 0xFFFFFFFFu;
+    rhp[lane * 4 + k] = plat < a.n_plats && a.plats[plat].drv == DRV_REDHAT;
   }
-  excl = off + uint32_t(__popcll(bal & ((1ull << lane) - 1ull)));
-  return tot;
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
 }
 
-// Per package of tile t: 1 = a Red Hat package (its pairs' group keys are their ID ranks).
-__device__ __forceinline__ void tile_redhat_flags(const MergeArgs& a, uint32_t t, uint32_t tid, uint8_t* rhp) {
-  const uint32_t p = t * kBlock + tid;
-  const uint32_t plat = p < a.n ? a.pk[p].x : 0xFFFFFFFFu;
-  rhp[tid] = plat < a.n_plats && a.plats[plat].drv == DRV_REDHAT;
-}
-
-// The lane's pair of chunk c of a tile segment [b0, b0 + cnt): package p, advisory ad and
-// its group key (the ID rank for a Red Hat package, kNoKey else; rhp: the tile's flags).
+// The lane's pair of chunk c (64 pairs) of a tile segment [b0, b0 + cnt): package p,
+// advisory ad and its group key (the ID rank for a Red Hat package, kNoKey else).
 __device__ __forceinline__ uint32_t chunk_key(const MergeArgs& a, uint64_t b0, uint32_t c, uint32_t cnt, uint32_t t,
-                                              uint32_t tid, const uint8_t* rhp, uint32_t& p, uint32_t& ad) {
-  if (c + tid >= cnt) return kNoKey;
-  p = a.pkg[b0 + c + tid];
-  ad = a.adv[b0 + c + tid];
+                                              uint32_t lane, const uint8_t* rhp, uint32_t& p, uint32_t& ad) {
+  if (c + lane >= cnt) return kNoKey;
+  p = a.pkg[b0 + c + lane];
+  ad = a.adv[b0 + c + lane];
   return rhp[(p - a.pkg_base - t * kBlock) & (kBlock - 1)] ? a.adv_rank[ad].x : kNoKey;
 }
 
-// The (package, key) of the pair before the lane's: the lanes exchange them through LDS
-// (xp / xk); lane 0 takes the previous chunk's last pair (prev_*, advanced here to this
-// chunk's last pair), so each pair's key is gathered once, not again as its successor's
-// predecessor.  left = pairs of the segment from this chunk on.  Consecutive chunks use
-// alternate xp / xk buffers, with the chunk's other barrier between two uses of one.
-__device__ __forceinline__ void pair_before(uint32_t tid, uint32_t p, uint32_t k, uint32_t* xp, uint32_t* xk,
-                                            uint32_t& prev_p, uint32_t& prev_k, uint32_t left, uint32_t& pp,
-                                            uint32_t& kp) {
-  xp[tid] = p;
-  xk[tid] = k;
-  __syncthreads();
-  pp = tid ? xp[tid - 1] : prev_p;
-  kp = tid ? xk[tid - 1] : prev_k;
-  const uint32_t last = (left < uint32_t(kBlock) ? left : uint32_t(kBlock)) - 1;
-  prev_p = xp[last];
-  prev_k = xk[last];
+// The (package, key) of the pair before the lane's, by shuffle; lane 0 takes the previous
+// chunk's last pair (prev_*, advanced here to this chunk's last), so each pair's key is
+// gathered once.  left = pairs of the segment from this chunk on.
+__device__ __forceinline__ void pair_before(uint32_t lane, uint32_t p, uint32_t k, uint32_t& prev_p, uint32_t& prev_k,
+                                            uint32_t left, uint32_t& pp, uint32_t& kp) {
+  const uint32_t up = __shfl_up(p, 1, 64), uk = __shfl_up(k, 1, 64);
+  pp = lane ? up : prev_p;
+  kp = lane ? uk : prev_k;
+  const int last = int((left < 64u ? left : 64u) - 1);
+  prev_p = __shfl(p, last, 64);
+  prev_k = __shfl(k, last, 64);
 }
 
 // Pass 1: the merged entry count of every tile into counts[t].  The tiles' output bases then
 // come from a scan (rocPRIM), not from an atomic reservation per tile: 78k same-address
 // atomics serialised the round-3 kernel (C5: 0.95 ms, SQ_WAIT_ANY / SQ_WAVE_CYCLES = 0.95).
-// Workgroups [0, n_rh) take the tiles that hold Red Hat packages (rh_list: the groups of
-// their segments, a block scan per 256 pairs); the rest one lane per tile for all others,
-// whose pairs are groups of one (a workgroup per such tile spent its time being dispatched).
+// Workgroups [0, nb_rh) take the tiles that hold Red Hat packages, one wave each (rh_list;
+// the groups of their segments, 64 pairs a step, no workgroup barrier); the rest one lane per
+// tile for all others, whose pairs are groups of one (a workgroup per such tile spent its
+// time being dispatched).
 __global__ __launch_bounds__(kBlock) void rh_count_kernel(MergeArgs a, uint32_t* counts, const uint8_t* rh_flags,
                                                           const uint32_t* rh_list, uint32_t n_rh, uint32_t n_tiles) {
-  __shared__ uint8_t rhp[kBlock];
-  __shared__ uint32_t xp[2][kBlock], xk[2][kBlock];
-  const uint32_t tid = threadIdx.x;
-  if (blockIdx.x >= n_rh) {
-    const uint32_t t = (blockIdx.x - n_rh) * kBlock + tid;
+  __shared__ uint8_t rhp_all[kWaves][kBlock];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t nb_rh = (n_rh + kWaves - 1) / kWaves;
+  if (blockIdx.x >= nb_rh) {
+    const uint32_t t = (blockIdx.x - nb_rh) * kBlock + tid;
     if (t >= n_tiles || rh_flags[t]) return;
     const TileDir d = a.dir[t];
     const bool fits = d.base + d.count <= a.raw_cap;
@@ -137,57 +120,58 @@ __global__ __launch_bounds__(kBlock) void rh_count_kernel(MergeArgs a, uint32_t*
     if (!fits) atomicOr(a.mctl + 3, 1ull);  // an overflowed match list: nothing valid to merge
     return;
   }
-  const uint32_t t = rh_list[blockIdx.x];
-  tile_redhat_flags(a, t, tid, rhp);
+  const uint32_t r = blockIdx.x * kWaves + wave;
+  if (r >= n_rh) return;  // wave-uniform; no workgroup barrier follows
+  const uint32_t t = rh_list[r];
+  uint8_t* rhp = rhp_all[wave];
+  tile_redhat_flags(a, t, lane, rhp);
   const TileDir d = a.dir[t];
   const uint64_t b0 = d.base;
   const uint32_t cnt = d.count;
   if (b0 + cnt > a.raw_cap) {
-    if (tid == 0) {
+    if (lane == 0) {
       counts[t] = 0;
       atomicOr(a.mctl + 3, 1ull);
     }
     return;
   }
-  __syncthreads();  // rhp
-  uint32_t heads = 0, prev_p = 0xFFFFFFFFu, prev_k = kNoKey, par = 0;
+  uint32_t heads = 0, prev_p = 0xFFFFFFFFu, prev_k = kNoKey;
   bool order_bad = false;
-  for (uint32_t c = 0; c < cnt; c += kBlock, par ^= 1) {
-    const bool v = c + tid < cnt;
+  for (uint32_t c = 0; c < cnt; c += 64) {
+    const bool v = c + lane < cnt;
     uint32_t p = 0xFFFFFFFFu, ad = 0;
-    const uint32_t k = chunk_key(a, b0, c, cnt, t, tid, rhp, p, ad);
-    bool h = false;
+    const uint32_t k = chunk_key(a, b0, c, cnt, t, lane, rhp, p, ad);
     uint32_t pp, kp;
-    pair_before(tid, p, k, xp[par], xk[par], prev_p, prev_k, cnt - c, pp, kp);
+    pair_before(lane, p, k, prev_p, prev_k, cnt - c, pp, kp);
+    bool h = false;
     if (v) {
       const bool cont = k != kNoKey && pp == p;
       h = !(cont && kp == k);
       order_bad |= cont && kp > k;
     }
-    heads += uint32_t(__syncthreads_count(h));
+    heads += uint32_t(__popcll(__ballot(h)));
   }
-  if (order_bad) atomicOr(a.mctl + 3, (unsigned long long)ERR_RH_ORDER);
-  if (tid == 0) counts[t] = heads;
+  if (__ballot(order_bad) && lane == 0) atomicOr(a.mctl + 3, (unsigned long long)ERR_RH_ORDER);
+  if (lane == 0) counts[t] = heads;
 }
 
 // The tiles' output bases: an exclusive scan of the counts (rocPRIM's single-pass decoupled
 // look-back scan, RedHatMerge::launch).
 
-// Pass 2: each tile writes its merged entries at its base.  Workgroups [0, n_rh): the Red Hat
-// tiles, one entry per group (the member with the greatest fixed version; ties keep the
-// first, as LessThan does) and its member range (grp), which only the host's Red Hat
-// vulnerability build reads (rh_vulns, for Red Hat packages).  The rest: one wave per tile,
-// a coalesced copy (pairs pass through as groups of one: 8 bytes in, 12 out per pair).  The
+// Pass 2: each tile writes its merged entries at its base, one wave per tile.  Workgroups
+// [0, nb_rh): the Red Hat tiles, one entry per group (the member with the greatest fixed
+// version; ties keep the first, as LessThan does) and its member range (grp), which only the
+// host's Red Hat vulnerability build reads (rh_vulns, for Red Hat packages).  The rest: a
+// coalesced copy (pairs pass through as groups of one: 8 bytes in, 12 out per pair).  The
 // tile directory entry and, at the last tile, the merged total go with the tile.
 __global__ __launch_bounds__(kBlock) void rh_emit_kernel(MergeArgs a, const uint32_t* counts,
                                                          const unsigned long long* bases, const uint8_t* rh_flags,
                                                          const uint32_t* rh_list, uint32_t n_rh, uint32_t n_tiles) {
-  __shared__ uint32_t ws[2][kWaves];
-  __shared__ uint8_t rhp[kBlock];
-  __shared__ uint32_t xp[2][kBlock], xk[2][kBlock];
-  const uint32_t tid = threadIdx.x;
-  if (blockIdx.x >= n_rh) {
-    const uint32_t lane = tid & 63, t = (blockIdx.x - n_rh) * kWaves + (tid >> 6);
+  __shared__ uint8_t rhp_all[kWaves][kBlock];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t nb_rh = (n_rh + kWaves - 1) / kWaves;
+  if (blockIdx.x >= nb_rh) {
+    const uint32_t t = (blockIdx.x - nb_rh) * kWaves + wave;
     if (t >= n_tiles || rh_flags[t]) return;
     const TileDir d = a.dir[t];
     const uint64_t b0 = d.base;
@@ -221,31 +205,33 @@ __global__ __launch_bounds__(kBlock) void rh_emit_kernel(MergeArgs a, const uint
     }
     return;
   }
-  const uint32_t t = rh_list[blockIdx.x];
-  tile_redhat_flags(a, t, tid, rhp);
+  const uint32_t r = blockIdx.x * kWaves + wave;
+  if (r >= n_rh) return;
+  const uint32_t t = rh_list[r];
+  uint8_t* rhp = rhp_all[wave];
+  tile_redhat_flags(a, t, lane, rhp);
   const TileDir d = a.dir[t];
   const uint64_t b0 = d.base;
   const uint32_t cnt = d.count;
   const unsigned long long o0 = bases[t];
   const uint32_t heads = counts[t];
   const bool fits = b0 + cnt <= a.raw_cap && o0 + heads <= a.mcap;
-  if (tid == 0) {
+  if (lane == 0) {
     a.mdir[t] = TileDir{o0, fits ? heads : 0u, 0};
     if (t + 1 == n_tiles) a.mctl[0] = o0 + heads;
   }
   if (!fits) return;  // cannot happen (merged <= raw); the counts tell the host
-  __syncthreads();  // rhp
-  uint32_t done = 0, prev_p = 0xFFFFFFFFu, prev_k = kNoKey, par = 0;
-  for (uint32_t c = 0; c < cnt; c += kBlock, par ^= 1) {
-    const bool v = c + tid < cnt;
-    const uint64_t i = b0 + c + tid;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  uint32_t done = 0, prev_p = 0xFFFFFFFFu, prev_k = kNoKey;
+  for (uint32_t c = 0; c < cnt; c += 64) {
+    const bool v = c + lane < cnt;
+    const uint64_t i = b0 + c + lane;
     uint32_t p = 0xFFFFFFFFu, ad = 0;
-    const uint32_t k = chunk_key(a, b0, c, cnt, t, tid, rhp, p, ad);
+    const uint32_t k = chunk_key(a, b0, c, cnt, t, lane, rhp, p, ad);
     uint32_t pp, kp;
-    pair_before(tid, p, k, xp[par], xk[par], prev_p, prev_k, cnt - c, pp, kp);
+    pair_before(lane, p, k, prev_p, prev_k, cnt - c, pp, kp);
     const bool h = v && (k == kNoKey || pp != p || kp != k);
-    uint32_t ex;
-    const uint32_t n = block_flag_scan(h, tid, ws[par], ex);
+    const unsigned long long bal = __ballot(h);
     if (h) {
       uint32_t best = RH_NONE, best_r = 0, len = 1;
       if (k != kNoKey) {
@@ -254,18 +240,18 @@ __global__ __launch_bounds__(kBlock) void rh_emit_kernel(MergeArgs a, const uint
         for (uint64_t j = i + 1; j < b0 + cnt && a.pkg[j] == p; j++) {
           const uint32_t aj = a.adv[j];
           if (a.adv_rank[aj].x != k) break;
-          const uint32_t r = a.fixed_rank[aj];
-          if (r != RH_NONE && (best == RH_NONE || r > best_r)) best = aj, best_r = r;
+          const uint32_t rr = a.fixed_rank[aj];
+          if (rr != RH_NONE && (best == RH_NONE || rr > best_r)) best = aj, best_r = rr;
           len++;
         }
       }
-      const uint64_t o = o0 + done + ex;
+      const uint64_t o = o0 + done + uint32_t(__popcll(bal & lt));
       a.mpkg[o] = p;
       a.madv[o] = best != RH_NONE ? best : ad;
       a.mbase[o] = ad;
       a.mgrp[o] = make_uint2(uint32_t(i), len);
     }
-    done += n;
+    done += uint32_t(__popcll(bal));
   }
 }
 
@@ -394,7 +380,8 @@ bool RedHatMerge::launch(const RhInputs& in, hipStream_t st, std::string& err) {
     err = "redhat merge: the batch's Red Hat tiles are not set (set_tiles)";
     return false;
   }
-  const uint32_t g_count = n_rh_ + (in.n_tiles + kBlock - 1) / kBlock, g_emit = n_rh_ + (in.n_tiles + kWaves - 1) / kWaves;
+  const uint32_t nb_rh = (n_rh_ + kWaves - 1) / kWaves;  // a wave per Red Hat tile
+  const uint32_t g_count = nb_rh + (in.n_tiles + kBlock - 1) / kBlock, g_emit = nb_rh + (in.n_tiles + kWaves - 1) / kWaves;
   hipLaunchKernelGGL(rh_count_kernel, dim3(g_count), dim3(kBlock), 0, st, a, counts_, flags_, rh_list_, n_rh_,
                      in.n_tiles);
   if (!ok(hipGetLastError(), "rh_count_kernel", err)) return false;
