@@ -332,17 +332,19 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
   // the result lives in pinned host memory that the result move writes directly over PCIe
   // (measured, profiles/r03/pcie_probe.txt: kernel stores to host memory 55 GB/s, a DMA
   // device-to-host copy 28.6 GB/s; the DMA engine then only carries the batch upward)
-  if (!(p = pool_host_get(cap4 * 4, "hipHostMalloc(adv)", err))) return false;
-  adv_h_ = static_cast<uint32_t*>(p);
+  if (!byte_) {  // (the byte form has its own arrays, below)
+    if (!(p = pool_host_get(cap4 * 4, "hipHostMalloc(adv)", err))) return false;
+    adv_h_ = static_cast<uint32_t*>(p);
+    if (!ok(hipHostGetDevicePointer(&p, adv_h_, 0), "hipHostGetDevicePointer(adv)", err)) return false;
+    adv_hd_ = static_cast<uint32_t*>(p);
+  }
   if (!(p = pool_host_get(std::max<size_t>(n4, 4) * 4, "hipHostMalloc(row ends)", err))) return false;
   row_end_h_ = static_cast<uint32_t*>(p);
-  if (!ok(hipHostGetDevicePointer(&p, adv_h_, 0), "hipHostGetDevicePointer(adv)", err)) return false;
-  adv_hd_ = static_cast<uint32_t*>(p);
   if (!ok(hipHostGetDevicePointer(&p, row_end_h_, 0), "hipHostGetDevicePointer(row ends)", err)) return false;
   row_end_hd_ = static_cast<uint32_t*>(p);
   if (!(p = pool_device_get(dev_, std::max<size_t>(n4, 4) * 4, "hipMalloc(row ends)", err))) return false;
   row_end_d_ = static_cast<uint32_t*>(p);
-  if (byte_) {  // the byte form's three arrays, written by the result move; adv_h_ holds the decoded CSR
+  if (byte_) {  // the byte form's three arrays, written by the result move; csr_h_ holds the decoded CSR
     if (!(p = pool_host_get(cap4 + 64, "hipHostMalloc(bytes)", err))) return false;
     bytes_h_ = static_cast<uint8_t*>(p);
     if (!ok(hipHostGetDevicePointer(&p, bytes_h_, 0), "hipHostGetDevicePointer(bytes)", err)) return false;
