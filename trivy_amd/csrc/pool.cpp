@@ -7,6 +7,7 @@
 #include <iterator>
 #include <map>
 #include <mutex>
+#include <new>
 #include <unordered_map>
 
 namespace tvm {
@@ -161,7 +162,12 @@ void* pool_heap_get(size_t bytes) {
     std::lock_guard<std::mutex> lk(P.mu);
     if (void* p = take(P.heap, bytes)) return p;
   }
-  void* p = huge_alloc(bytes);
+  void* p = nullptr;
+  try {  // huge_alloc throws on failure; the C-ABI callers get a null block (an error), not an exception
+    p = huge_alloc(bytes);
+  } catch (const std::bad_alloc&) {
+    return nullptr;
+  }
   if (!p) return nullptr;
   std::lock_guard<std::mutex> lk(P.mu);
   P.heap.cap_[p] = bytes;
