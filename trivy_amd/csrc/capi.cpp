@@ -8,6 +8,7 @@
 #include <deque>
 #include <memory>
 #include <mutex>
+#include <new>
 #include <shared_mutex>
 #include <string>
 #include <unordered_map>
@@ -1763,9 +1764,16 @@ struct tvm_sbom {
 int tvm_sbom_decode_cyclonedx(const char* text, size_t len, uint32_t flags, tvm_sbom** out, char* err, size_t errlen) {
   if (!out || (len && !text) || (flags & ~uint32_t(TVM_SBOM_BORROW))) return TVM_EINVAL;
   *out = nullptr;
-  auto* h = new tvm_sbom();
+  auto* h = new (std::nothrow) tvm_sbom();
+  if (!h) return TVM_EINVAL;
   std::string msg;
-  if (!decode_cyclonedx(std::string_view(text, len), h->s, msg, (flags & TVM_SBOM_BORROW) != 0)) {
+  bool good = false;
+  try {  // a document of any size is untrusted input: running out of memory is an error, not an abort
+    good = decode_cyclonedx(std::string_view(text, len), h->s, msg, (flags & TVM_SBOM_BORROW) != 0);
+  } catch (const std::bad_alloc&) {
+    msg = "failed to decode CycloneDX JSON: out of memory";
+  }
+  if (!good) {
     delete h;
     set_err(err, errlen, msg);
     return TVM_EINVAL;
