@@ -43,7 +43,7 @@ struct tvm_engine {
   std::unique_ptr<Engine> eng;
   std::unique_ptr<FillEngine> fill;
   std::mutex rh_mu;                   // lazily built Red Hat fixed-version ranks (device)
-  uint32_t* rh_rank = nullptr;
+  uint2* rh_rank = nullptr;  // per advisory {vulnerability-ID rank, rpm rank of FixedVersion} (Red Hat merge)
   ~tvm_engine() {
     if (rh_rank) {
       (void)hipSetDevice(device);
@@ -1585,15 +1585,19 @@ namespace {
 bool ensure_rh_rank(tvm_engine* e, std::string& err) {
   std::lock_guard<std::mutex> g(e->rh_mu);
   if (e->rh_rank) return true;
+  // the merge's two per-advisory gathers (its group key, its fixed-version rank) in one word pair
   const std::vector<uint32_t> r = redhat_fixed_ranks(e->eng->db());
+  const std::vector<uint2>& ids = e->fill->table().adv_rank;
+  std::vector<uint2> rk(r.size());
+  for (size_t i = 0; i < r.size(); i++) rk[i] = make_uint2(i < ids.size() ? ids[i].x : 0xFFFFFFFFu, r[i]);
   void* p = nullptr;
-  if (hipMalloc(&p, std::max<size_t>(r.size(), 1) * 4) != hipSuccess ||
-      (!r.empty() && hipMemcpy(p, r.data(), r.size() * 4, hipMemcpyHostToDevice) != hipSuccess)) {
+  if (hipMalloc(&p, std::max<size_t>(rk.size(), 1) * sizeof(uint2)) != hipSuccess ||
+      (!rk.empty() && hipMemcpy(p, rk.data(), rk.size() * sizeof(uint2), hipMemcpyHostToDevice) != hipSuccess)) {
     if (p) (void)hipFree(p);
-    err = "redhat merge: fixed-version ranks upload failed";
+    err = "redhat merge: advisory ranks upload failed";
     return false;
   }
-  e->rh_rank = static_cast<uint32_t*>(p);
+  e->rh_rank = static_cast<uint2*>(p);
   return true;
 }
 
@@ -1606,8 +1610,7 @@ RhInputs rh_inputs(tvm_engine* e, tvm_batch* b) {
   in.n_tiles = b->dev.n_tiles;
   in.n = b->dev.n;
   in.pkg_base = b->dev.pkg_base;
-  in.adv_rank = e->fill->dev().adv_rank;
-  in.fixed_rank = e->rh_rank;
+  in.rk = e->rh_rank;
   return in;
 }
 

@@ -45,8 +45,7 @@ struct RhInputs {
   uint32_t n_tiles;
   uint32_t n;                       // packages in the batch (tile t = packages [256 t, 256 t + 256))
   uint32_t pkg_base;
-  const uint2* adv_rank;            // FillDev::adv_rank (.x vulnerability-ID rank)
-  const uint32_t* fixed_rank;       // per advisory: rpm order rank of FixedVersion, RH_NONE = unfixed
+  const uint2* rk;                  // per advisory {vulnerability-ID rank, rpm order rank of FixedVersion (RH_NONE = unfixed)}
 };
 
 class RedHatMerge {

@@ -44,8 +44,7 @@ struct MergeArgs {
   uint32_t n_plats;
   uint32_t pkg_base;
   uint32_t n;                  // packages in the batch
-  const uint2* adv_rank;       // .x = vulnerability-ID rank
-  const uint32_t* fixed_rank;  // RH_NONE = unfixed
+  const uint2* rk;             // {vulnerability-ID rank, fixed-version rank (RH_NONE = unfixed)}
   uint64_t raw_cap;
   TileDir* mdir;
   uint32_t* mpkg;
@@ -60,7 +59,7 @@ struct MergeArgs {
 __device__ __forceinline__ uint32_t group_key(const MergeArgs& a, uint32_t p, uint32_t ad) {
   const uint32_t plat = a.pk[p - a.pkg_base].x;
   const bool rh = plat < a.n_plats && a.plats[plat].drv == DRV_REDHAT;
-  return rh ? a.adv_rank[ad].x : kNoKey;
+  return rh ? a.rk[ad].x : kNoKey;
 }
 
 // Per package of tile t: 1 = a Red Hat package (its pairs' group keys are their ID ranks);
@@ -77,13 +76,19 @@ __device__ __forceinline__ void tile_redhat_flags(const MergeArgs& a, uint32_t t
 }
 
 // The lane's pair of chunk c (64 pairs) of a tile segment [b0, b0 + cnt): package p,
-// advisory ad and its group key (the ID rank for a Red Hat package, kNoKey else).
+// advisory ad, its group key (the ID rank for a Red Hat package, kNoKey else) and, for a
+// Red Hat pair, its fixed-version rank (fr) - one gather for both.
 __device__ __forceinline__ uint32_t chunk_key(const MergeArgs& a, uint64_t b0, uint32_t c, uint32_t cnt, uint32_t t,
-                                              uint32_t lane, const uint8_t* rhp, uint32_t& p, uint32_t& ad) {
+                                              uint32_t lane, const uint8_t* rhp, uint32_t& p, uint32_t& ad,
+                                              uint32_t& fr) {
+  fr = RH_NONE;
   if (c + lane >= cnt) return kNoKey;
   p = a.pkg[b0 + c + lane];
   ad = a.adv[b0 + c + lane];
-  return rhp[(p - a.pkg_base - t * kBlock) & (kBlock - 1)] ? a.adv_rank[ad].x : kNoKey;
+  if (!rhp[(p - a.pkg_base - t * kBlock) & (kBlock - 1)]) return kNoKey;
+  const uint2 r = a.rk[ad];
+  fr = r.y;
+  return r.x;
 }
 
 // The (package, key) of the pair before the lane's, by shuffle; lane 0 takes the previous
@@ -139,8 +144,8 @@ __global__ __launch_bounds__(kBlock) void rh_count_kernel(MergeArgs a, uint32_t*
   bool order_bad = false;
   for (uint32_t c = 0; c < cnt; c += 64) {
     const bool v = c + lane < cnt;
-    uint32_t p = 0xFFFFFFFFu, ad = 0;
-    const uint32_t k = chunk_key(a, b0, c, cnt, t, lane, rhp, p, ad);
+    uint32_t p = 0xFFFFFFFFu, ad = 0, fr;
+    const uint32_t k = chunk_key(a, b0, c, cnt, t, lane, rhp, p, ad, fr);
     uint32_t pp, kp;
     pair_before(lane, p, k, prev_p, prev_k, cnt - c, pp, kp);
     bool h = false;
@@ -226,8 +231,8 @@ __global__ __launch_bounds__(kBlock) void rh_emit_kernel(MergeArgs a, const uint
   for (uint32_t c = 0; c < cnt; c += 64) {
     const bool v = c + lane < cnt;
     const uint64_t i = b0 + c + lane;
-    uint32_t p = 0xFFFFFFFFu, ad = 0;
-    const uint32_t k = chunk_key(a, b0, c, cnt, t, lane, rhp, p, ad);
+    uint32_t p = 0xFFFFFFFFu, ad = 0, fr;
+    const uint32_t k = chunk_key(a, b0, c, cnt, t, lane, rhp, p, ad, fr);
     uint32_t pp, kp;
     pair_before(lane, p, k, prev_p, prev_k, cnt - c, pp, kp);
     const bool h = v && (k == kNoKey || pp != p || kp != k);
@@ -235,13 +240,12 @@ __global__ __launch_bounds__(kBlock) void rh_emit_kernel(MergeArgs a, const uint
     if (h) {
       uint32_t best = RH_NONE, best_r = 0, len = 1;
       if (k != kNoKey) {
-        const uint32_t r0 = a.fixed_rank[ad];
-        if (r0 != RH_NONE) best = ad, best_r = r0;
+        if (fr != RH_NONE) best = ad, best_r = fr;
         for (uint64_t j = i + 1; j < b0 + cnt && a.pkg[j] == p; j++) {
           const uint32_t aj = a.adv[j];
-          if (a.adv_rank[aj].x != k) break;
-          const uint32_t rr = a.fixed_rank[aj];
-          if (rr != RH_NONE && (best == RH_NONE || rr > best_r)) best = aj, best_r = rr;
+          const uint2 rj = a.rk[aj];
+          if (rj.x != k) break;
+          if (rj.y != RH_NONE && (best == RH_NONE || rj.y > best_r)) best = aj, best_r = rj.y;
           len++;
         }
       }
@@ -366,8 +370,7 @@ bool RedHatMerge::launch(const RhInputs& in, hipStream_t st, std::string& err) {
   a.n_plats = in.n_plats;
   a.pkg_base = in.pkg_base;
   a.n = in.n;
-  a.adv_rank = in.adv_rank;
-  a.fixed_rank = in.fixed_rank;
+  a.rk = in.rk;
   a.raw_cap = raw.cap;
   a.mdir = out_.m.dir;
   a.mpkg = out_.m.pkg;
