@@ -3,7 +3,7 @@
 # the filter's survivor-sum scan (kernel trace).
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/${NAME:-r04n}
+OUT=$R/gpurun_out/${NAME:-r04o}
 mkdir -p $OUT
 cd $R
 export TMPDIR=/tmp
