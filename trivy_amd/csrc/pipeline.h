@@ -94,7 +94,9 @@ class Pipeline {
   uint64_t* raw_toff_ = nullptr;
   uint8_t* raw_arena_ = nullptr;
   uint2* raw_attr_ = nullptr;
-  bool stage_raw(const HostBatch& hb, std::string& err);
+  bool stage_raw(const HostBatch& hb, std::string& err);  // allocates; run() copies chunk by chunk
+  void stage_chunk(const HostBatch& hb, size_t p0, size_t p1, size_t g0, size_t g1, uint64_t a0, uint64_t a1);
+  bool raw_staged_ = false;
   DevBatch db_;
   DevMatches m_;
   unsigned long long* chunk_base_d_ = nullptr;  // chunk c's first CSR position (written by chunk c-1's move)
