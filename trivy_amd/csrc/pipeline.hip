@@ -185,7 +185,7 @@ void Pipeline::stage_chunk(const HostBatch& hb, size_t p0, size_t p1, size_t g0,
                    {raw_arena_ + a0, hb.arena.data() + a0, size_t(a1 - a0)},
                    {raw_attr_ + p0, hb.attr.empty() ? nullptr : hb.attr.data() + p0,
                     hb.attr.empty() ? 0 : (p1 - p0) * sizeof(uint2)}};
-  constexpr size_t kPiece = size_t(2) << 20;
+  constexpr size_t kPiece = size_t(256) << 10;  // many more pieces than threads: even shares
   std::vector<std::pair<int, size_t>> pieces;  // (part, offset)
   for (int k = 0; k < 4; k++)
     for (size_t o = 0; o < parts[k].bytes; o += kPiece) pieces.emplace_back(k, o);
