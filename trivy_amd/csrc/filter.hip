@@ -426,7 +426,7 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
   // software-pipelined: the next chunk's pair words (and its packages' run starts) are loaded
   // while this chunk waits on its placement bases and barriers
-  uint32_t n_key = kEmpty, n_cls = kNoClass, n_p = 0, n_adv = 0, n_rb = 0;
+  uint32_t n_key = kEmpty, n_cls = kNoClass, n_p = 0, n_adv = 0, n_rb = 0, n_fl = 0, n_gb = 0;
   auto load_pairs = [&](uint64_t c) {
     const uint64_t j = c + tid;
     if (j < a.n) {
@@ -439,7 +439,11 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
   {
     const uint64_t c = uint64_t(blockIdx.x) * kBlock;
     load_pairs(c);
-    if (c + tid < a.n) n_rb = a.run_b[n_p];
+    if (c + tid < a.n) {
+      n_rb = a.run_b[n_p];
+      n_fl = a.fl[n_p];
+      n_gb = a.grp_b[n_p];
+    }
   }
   for (uint64_t c0 = uint64_t(blockIdx.x) * kBlock; c0 < a.n; c0 += stride) {
     const uint64_t i = c0 + tid;
@@ -449,6 +453,7 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
     const uint32_t p = valid ? n_p : 0u;
     const uint32_t adv = n_adv;
     const uint32_t rb = valid ? n_rb : 0u;
+    const uint32_t pf = n_fl, gb0 = n_gb;  // the package's flags and group (loaded a chunk ahead)
     const uint32_t rb0 = __shfl(rb, 0, 64);  // the chunk's first package's run start (wave 0)
     const uint64_t rs = rb > c0 ? rb : c0;  // the package's first pair in this chunk
     const bool more = c0 + stride < a.n;
@@ -464,11 +469,11 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
     // the run entering the chunk: its classes before c0 (filter_count left them per wave)
     if (tid < uint32_t(kClasses)) carry[tid] = rb0 < c0 ? a.wcarry[(c0 >> 6) * kClasses + tid] : 0u;
     if (valid && i == rs) {  // the package's first lane: its placement bases, once
-      const uint32_t f = a.fl[p];
+      const uint32_t f = pf;
       pflag[tid] = f;
       if ((f & (FL_SINGLE | FL_UNS)) == FL_SINGLE) {
         // ID-sorted run alone in its group: severity desc, then run order
-        uint32_t acc = a.off[a.grp_b[p]];
+        uint32_t acc = a.off[gb0];
         const uint32_t* c = a.cnt + uint64_t(p) * kClasses;
         for (int sv = 4; sv >= 0; sv--) {
           base[tid][sv] = acc;
@@ -477,7 +482,11 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
       }
       if (a.kinds & 7u) base[tid][kIgnClass] = a.ign_off[p];
     }
-    if (more && c0 + stride + tid < a.n) n_rb = a.run_b[n_p];
+    if (more && c0 + stride + tid < a.n) {
+      n_rb = a.run_b[n_p];
+      n_fl = a.fl[n_p];
+      n_gb = a.grp_b[n_p];
+    }
     __syncthreads();
     unsigned long long wbase = 0;
 #pragma unroll
