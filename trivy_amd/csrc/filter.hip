@@ -345,14 +345,29 @@ __global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
 __global__ __launch_bounds__(kBlock) void filter_count(FilterArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  // software-pipelined: the next step's pair words are loaded before this step's counting
+  uint32_t n_p = 0xFFFFFFFFu, n_cls = kNoClass, n_before = 0xFFFFFFFFu;
+  auto load = [&](uint64_t b) {
+    const uint64_t i = b + threadIdx.x;
+    n_p = 0xFFFFFFFFu;
+    n_cls = kNoClass;
+    if (i < a.n) {
+      n_p = a.pkg[i];
+      n_cls = a.pcls[i];
+      if (lane == 0) n_before = i == 0 ? 0xFFFFFFFFu : a.pkg[i - 1];  // lane 0: the pair before the wave
+    }
+  };
+  load(uint64_t(blockIdx.x) * kBlock);
   for (uint64_t b0 = uint64_t(blockIdx.x) * kBlock; b0 < a.n; b0 += stride) {  // wave-uniform trip count
     const uint64_t i = b0 + threadIdx.x;
     const bool valid = i < a.n;
-    const uint32_t p = valid ? a.pkg[i] : 0xFFFFFFFFu;
-    const uint32_t cls = valid ? a.pcls[i] : kNoClass;
+    const uint32_t p = n_p;
+    const uint32_t cls = n_cls;
+    const uint32_t before = n_before;
+    if (b0 + stride < a.n) load(b0 + stride);
     const uint32_t prev_p = __shfl_up(p, 1, 64);
     // lane 0 starts a run only at the run's first pair (else the run started in an earlier wave)
-    const bool head = valid && (lane == 0 ? (i == 0 || a.pkg[i - 1] != p) : prev_p != p);
+    const bool head = valid && (lane == 0 ? (i == 0 || before != p) : prev_p != p);
     const bool seg = valid && (lane == 0 || prev_p != p);  // first lane of a package in this wave
     const unsigned long long segs = __ballot(seg);
     const unsigned long long above = lane == 63 ? 0ull : segs & (~0ull << (lane + 1));
