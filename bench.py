@@ -518,7 +518,7 @@ def main():
     fresh = None
     if world == 1 and not args.no_e2e and rank == 0:
         runs = []
-        for _ in range(4):  # the first warms the block cache (pool.h); the median of the rest is reported
+        for _ in range(6):  # the first warms the block cache (pool.h); the median of the rest is reported
             tb = time.perf_counter()
             mf = MatchBatch(eng)
             wl.fill(mf)
