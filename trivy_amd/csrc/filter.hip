@@ -235,14 +235,26 @@ __global__ __launch_bounds__(kBlock) void filter_mark(FilterArgs a) {
     uint32_t p[kU], pp[kU], pn[kU], f[kU], dp[kU];
     uint2 sd[kU];
     uint32_t vprev[kU];
+    const uint32_t lane = threadIdx.x & 63;
 #pragma unroll
     for (int k = 0; k < kU; k++) {
       const uint64_t i = min(b0 + uint64_t(k) * kBlock + threadIdx.x, n - 1);
       p[k] = a.pkg[i];
       sd[k] = a.side[i];
-      pp[k] = i ? a.pkg[i - 1] : 0xFFFFFFFFu;
-      pn[k] = i + 1 < n ? a.pkg[i + 1] : 0xFFFFFFFFu;
-      vprev[k] = i ? a.side[i - 1].x : 0u;
+      // the neighbours' words come from the neighbouring lanes; only the wave's edge lanes load
+      pp[k] = (lane == 0 && i) ? a.pkg[i - 1] : 0xFFFFFFFFu;
+      vprev[k] = (lane == 0 && i) ? a.side[i - 1].x : 0u;
+      pn[k] = (lane == 63 && i + 1 < n) ? a.pkg[i + 1] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int k = 0; k < kU; k++) {
+      const uint64_t i = min(b0 + uint64_t(k) * kBlock + threadIdx.x, n - 1);
+      const uint32_t up = __shfl_up(p[k], 1, 64), vup = __shfl_up(sd[k].x, 1, 64), dn = __shfl_down(p[k], 1, 64);
+      if (lane != 0) {
+        pp[k] = up;
+        vprev[k] = vup;
+      }
+      if (lane != 63) pn[k] = i + 1 < n ? dn : 0xFFFFFFFFu;
     }
 #pragma unroll
     for (int k = 0; k < kU; k++) {
