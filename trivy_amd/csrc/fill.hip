@@ -84,15 +84,23 @@ __device__ __forceinline__ uint4 decide_r(const FillDev& t, uint4 item, uint32_t
   const uint32_t src = item.y >> 16;
   const uint32_t url_kind = (r.w >> REC_URL_SHIFT) & 0xFu;
   uint32_t v_src = 0xFFFFFFFFu, v_ghsa = 0xFFFFFFFFu, v_nvd = 0xFFFFFFFFu, ref = 0xFFFFFFFFu;
-  for (uint32_t i = 0; i < r.y; i++) {
-    const uint32_t e = t.ents[r.x + i];
-    const uint32_t s = (e >> 16) & 0x7FFFu, v = e & 0xFFFFu;
-    if (e & ENT_URL) {
-      if (s == src) ref = v;
-    } else {
-      if (s == src) v_src = v;
-      if (s == t.ghsa) v_ghsa = v;
-      if (s == t.nvd) v_nvd = v;
+  // entries four at a time: the four loads are in flight together (an entry list is a few words)
+  for (uint32_t i0 = 0; i0 < r.y; i0 += 4) {
+    uint32_t ev[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) ev[u] = i0 + u < r.y ? t.ents[r.x + i0 + u] : 0u;
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) {
+      if (i0 + u >= r.y) break;
+      const uint32_t e = ev[u];
+      const uint32_t s = (e >> 16) & 0x7FFFu, v = e & 0xFFFFu;
+      if (e & ENT_URL) {
+        if (s == src) ref = v;
+      } else {
+        if (s == src) v_src = v;
+        if (s == t.ghsa) v_ghsa = v;
+        if (s == t.nvd) v_nvd = v;
+      }
     }
   }
   uint32_t sev, ssrc = SRC_NONE;
