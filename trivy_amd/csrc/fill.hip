@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kFillTile) void fill_items_kernel(FillArgs a) {
 // kU pairs per lane per step, each level of the pair -> advisory item -> record chain loaded
 // for all of them before the next level is used (the chain is latency-bound: one pair per
 // lane kept one gather in flight).
-constexpr int kFillU = 4;
+constexpr int kFillU = 8;
 __global__ __launch_bounds__(kFillTile) void fill_pairs_kernel(FillArgs a) {
   const uint64_t n = *a.n_dev < a.n ? *a.n_dev : a.n;
   const uint64_t stride = uint64_t(gridDim.x) * kFillTile * kFillU;
