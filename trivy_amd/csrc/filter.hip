@@ -226,7 +226,7 @@ __global__ __launch_bounds__(kBlock) void vex_mark(RuleDev r, const uint32_t* pk
 // Pairs per thread per step of the streaming kernels: every lane issues the loads of kU
 // pairs (coalesced, kBlock apart) before it uses any, so kU gathers of per-package state
 // are in flight together instead of one dependent chain per pair.
-constexpr int kU = 4;
+constexpr int kU = 8;
 
 __global__ __launch_bounds__(kBlock) void filter_mark(FilterArgs a) {
   const uint64_t stride = uint64_t(gridDim.x) * kBlock * kU;
