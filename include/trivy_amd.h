@@ -234,6 +234,13 @@ int64_t tvm_batch_add_many_attrs(tvm_batch* b, tvm_engine* e, const char* bucket
 int64_t tvm_batch_add_many(tvm_batch* b, tvm_engine* e, const char* bucket, size_t n, const char* arena,
                            const uint64_t* name_off, const uint32_t* name_len, const uint64_t* ver_off,
                            const uint32_t* ver_len);
+/* Many targets at once (a fleet's images / lockfiles, one Result each, as one
+ * tvm_batch_add_many per target would add them): target t is packages [target_end[t-1],
+ * target_end[t]) of the columns (target_end[-1] = 0), under root bucket buckets[t].  Returns
+ * the batch index of the first package, -1 on bad arguments. */
+int64_t tvm_batch_add_targets(tvm_batch* b, tvm_engine* e, size_t n_targets, const tvm_str* buckets,
+                              const uint64_t* target_end, const char* arena, const uint64_t* name_off,
+                              const uint32_t* name_len, const uint64_t* ver_off, const uint32_t* ver_len);
 int64_t tvm_batch_size(const tvm_batch* b);
 /* Copies the batch to the device and sizes the match buffer. */
 int tvm_batch_upload(tvm_engine* e, tvm_batch* b, uint64_t match_cap, char* err, size_t errlen);
@@ -244,6 +251,12 @@ int tvm_engine_sync(tvm_engine* e, char* err, size_t errlen);
  * own HIP runtime instance) and reports any pending asynchronous error.  Test and health-check
  * hook; no reference counterpart. */
 int tvm_device_sync(int device, char* err, size_t errlen);
+/* Process teardown: drains every device's queues, joins the library's host worker threads and
+ * frees its cached device / pinned blocks, so that nothing of the library's is left for the
+ * HIP runtime's own teardown at exit.  Call once before the process exits (the Python
+ * binding registers it with atexit); the library stays usable (later calls run without the
+ * worker threads and without block caching).  No reference counterpart. */
+void tvm_shutdown(void);
 /* Total matches, first poisoned package (-1 none), internal error bits (read on the engine
  * stream, behind the batch's launches). */
 int tvm_match_status(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* err_pkg, uint64_t* err_bits);
@@ -313,19 +326,7 @@ int tvm_batch_upload_into(tvm_engine* e, tvm_batch* b, void* pkg_dev, void* adv_
  * name and version under 256 bytes, at most 255 platforms): each distinct name and each
  * distinct version string crosses the link once, packages carry references to them, and
  * the GPU rebuilds the batch's arrays chunk by chunk (one DMA per chunk). */
-/* TVM_PIPE_DELTA: the per-package lists cross the link in the delta form
- * (trivy_amd/csrc/delta_form.h: per tile 256 count bytes, then each package's first advisory
- * index as 3 bytes and the next ones as 1-byte differences; ~1.4 bytes a match instead of 3
- * + a 4-byte row end per package), and tvm_pipeline_run decodes it into the CSR on the host
- * threads chunk by chunk while the GPU works on the later chunks (the call's time includes
- * it).  Needs a DB of fewer than 2^24 advisories (not with TVM_PIPE_ADV32). */
-/* TVM_PIPE_BYTE: one byte per match at its CSR position (the low byte of a package's first
- * advisory index, the package's high 16 bits apart, then 1-byte differences; larger steps
- * escape to a sparse 4-byte array) beside the usual row ends (trivy_amd/csrc/byte_form.h);
- * every position is known without a scan, so the result move writes whole words in place and
- * tvm_pipeline_run decodes each chunk into the CSR behind the GPU.  Needs a DB of fewer than
- * 2^24 advisories; not with TVM_PIPE_ADV32 or TVM_PIPE_DELTA. */
-enum { TVM_PIPE_RAW = 1, TVM_PIPE_ADV32 = 2, TVM_PIPE_DELTA = 4, TVM_PIPE_BYTE = 8 };
+enum { TVM_PIPE_RAW = 1, TVM_PIPE_ADV32 = 2 };
 int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32_t chunk_packages, uint32_t flags,
                          char* err, size_t errlen);
 /* One pass; ms = wall time of the call.  TVM_EINVAL with *n_matches set when the matches do
@@ -341,22 +342,7 @@ int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row
 /* The result as it arrived in pinned host memory: index i is the `width`-byte (3 or 4)
  * little-endian integer at adv + width * i. */
 int tvm_pipeline_result_raw(tvm_batch* b, const void** adv, uint32_t* width, const uint32_t** row_end,
-                            uint64_t* n_matches);  /* TVM_EINVAL for a TVM_PIPE_DELTA / TVM_PIPE_BYTE pipeline */
-/* A TVM_PIPE_DELTA pass's result as it arrived: tile t's stream of tile_info[2t + 1] bytes at
- * stream + tvm_delta_region(t, CSR position of its first match), tile_info[2t] its matches. */
-int tvm_pipeline_result_delta(tvm_batch* b, const void** stream, uint64_t* stream_bytes, const uint32_t** tile_info,
-                              uint32_t* n_tiles, uint64_t* n_matches);
-/* Decodes delta-form streams into the CSR: adv (n_matches entries), row_end (n_tiles * 256:
- * the CSR position after each package's list).  Host only (the decode tvm_pipeline_result
- * runs; test and inspection hook). */
-int tvm_delta_decode(const void* stream, uint64_t stream_bytes, const uint32_t* tile_info, uint32_t n_tiles,
-                     uint64_t n_matches, uint32_t* adv, uint32_t* row_end, char* err, size_t errlen);
-uint64_t tvm_delta_region(uint32_t tile, uint64_t first_match);
-/* Decodes a TVM_PIPE_BYTE result (bytes / hi / wide as trivy_amd/csrc/byte_form.h lays them
- * out, row_end: n_tiles * 256 row ends) into adv; returns the escapes met, -1 on bad
- * arguments.  Host only (the decode tvm_pipeline_run runs; test and inspection hook). */
-int64_t tvm_byte_decode(const uint8_t* bytes, const uint16_t* hi, const uint32_t* wide, const uint32_t* row_end,
-                        uint32_t n_tiles, uint32_t* adv);
+                            uint64_t* n_matches);
 /* [0] bytes the last pass copied host to device, [1] device to host, [2] chunks, [3] 1 when
  * the batch travels in its transport form, [4] prepare's host time building it (us). */
 int tvm_pipeline_stats(tvm_batch* b, uint64_t out[5]);
@@ -433,6 +419,48 @@ int tvm_match_redhat_vulns(tvm_engine* e, tvm_batch* b, const uint32_t* pairs, u
 /* Times `steps` back-to-back merges on the engine stream with HIP events (ms total); leaves
  * the batch on its merged list. */
 int tvm_match_redhat_merge_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err, size_t errlen);
+
+/* ---- DetectedVulnerability sets of a batch ----------------------------------------------
+ * The drivers' epilogues on the batch path: what Driver.Detect returns per target
+ * (debian.go:78-98, ubuntu.go:99-108, alpine.go:94-101, alma.go:64-71, rocky.go:69-76,
+ * oracle.go:70-80, redhat.go:140-187, mariner.go:50-70, ..., library/driver.go:125-132 +
+ * detect.go:33-37), for every match of a batch at once.  A DetectedVulnerability is split in
+ * two parts:
+ *   - its record (tvm_vuln without the package fields): VulnerabilityID, VendorIDs,
+ *     FixedVersion (rpm Version.String() for the drivers that print it, createFixedVersions for
+ *     libraries), Status, SeveritySource / Severity, DataSource, Custom, and copy_flags (which
+ *     fields the caller copies from its package: PkgID, PkgName, PkgIdentifier, Layer).  Record
+ *     r < n_adv_recs is advisory r's, as its driver populates it (shared by every package that
+ *     matches it, built once per DB); r >= n_adv_recs is grp_recs[r - n_adv_recs], a Red Hat
+ *     group of several advisories of one VulnerabilityID merged per redhat.go:146-187;
+ *   - its package: InstalledVersion and PkgPath of the batch package (tvm_batch_report_get),
+ *     PkgID / PkgName / PkgIdentifier / Layer from the caller's own package per copy_flags.
+ * Order: by package, then as the driver reports them (advisory order; Red Hat: VulnerabilityID
+ * order).  Library-owned; free with tvm_vuln_set_free. */
+typedef struct {
+  const uint32_t* pkg;           /* n: batch package index (+ tvm_batch_set_package_base) */
+  const uint32_t* rec;           /* n: record index */
+  size_t n;
+  const tvm_vuln* adv_recs;      /* one per DB advisory (pkg_index 0; package fields "") */
+  size_t n_adv_recs;
+  const tvm_vuln* grp_recs;      /* merged Red Hat groups */
+  size_t n_grp_recs;
+  void* priv;
+} tvm_vuln_set;
+/* After tvm_match_launch: the batch's DetectedVulnerability set.  Batches with Red Hat packages
+ * are merged on the device first (tvm_match_redhat_merge, if it has not run).  TVM_EINVAL when
+ * the pass overflowed its match buffer, met an undecodable advisory or flagged an error. */
+int tvm_match_vulns(tvm_engine* e, tvm_batch* b, tvm_vuln_set* out, char* err, size_t errlen);
+/* The same from the last tvm_pipeline_run's result (host CSR; no Red Hat packages). */
+int tvm_pipeline_vulns(tvm_engine* e, tvm_batch* b, tvm_vuln_set* out, char* err, size_t errlen);
+void tvm_vuln_set_free(tvm_vuln_set* s);
+/* The package side of packages [first, first + n): names = the tvm_batch_set_report PkgName
+ * (p = NULL: the caller's package Name), versions = InstalledVersion (the report's, else the
+ * batch version, which is FormatVersion of the package for every driver comparing the binary
+ * version), paths = PkgPath (report, else empty).  Views into the batch (valid until it changes);
+ * NULL arrays are skipped. */
+int tvm_batch_report_get(const tvm_batch* b, uint64_t first, uint64_t n, tvm_str* names, tvm_str* versions,
+                         tvm_str* paths);
 
 /* ---- vulnerability detail: FillInfo ------------------------------------------------ */
 /* One detected vulnerability as FillInfo reads it (vulnerability.go:60-109). */

@@ -284,11 +284,7 @@ class Records:
                 continue
             for e in ents:
                 if arch in (e.get("Arches") or []):
-                    b = {k: v for k, v in a.items() if k not in ("FixedVersion", "VendorIDs", "Arches")}
-                    for k in ("FixedVersion", "VendorIDs", "Arches"):
-                        if e.get(k):
-                            b[k] = e[k]
-                    out.append(b)
+                    out.append(rocky_entry_advisory(a, e))
         return out
 
     def redhat_cpes(self, content_sets, nvrs):
@@ -319,15 +315,28 @@ class Records:
                 if not any(i in cpes for i in e["Affected"]):
                     continue
                 for c in e["Cves"]:
-                    a = {"Severity": c["Severity"], "FixedVersion": e["FixedVersion"], "Arches": e["Arches"],
-                         "Status": e["Status"]}
-                    if vid.startswith("CVE-"):
-                        a["VulnerabilityID"] = vid
-                    else:
-                        a["VulnerabilityID"] = c["ID"]
-                        a["VendorIDs"] = [vid]
-                    out.append(a)
+                    out.append(redhat_cve_advisory(vid, e, c))
         return out
+
+
+def rocky_entry_advisory(a, e):
+    """trivy-db rocky Get: advisory a as seen through its arch entry e."""
+    b = {k: v for k, v in a.items() if k not in ("FixedVersion", "VendorIDs", "Arches", "Entries")}
+    for k in ("FixedVersion", "VendorIDs", "Arches"):
+        if e.get(k):
+            b[k] = e[k]
+    return b
+
+
+def redhat_cve_advisory(vid, e, c):
+    """trivy-db redhat-oval Get: one advisory per (entry e, CVE c) of bucket key vid."""
+    a = {"Severity": c["Severity"], "FixedVersion": e["FixedVersion"], "Arches": e["Arches"], "Status": e["Status"]}
+    if vid.startswith("CVE-"):
+        a["VulnerabilityID"] = vid
+    else:
+        a["VulnerabilityID"] = c["ID"]
+        a["VendorIDs"] = [vid]
+    return a
 
 
 def format_version(epoch, version, release):
@@ -438,6 +447,25 @@ def _get(db, err, root, name):
 
 
 # --------------------------------------------------------------------- dpkg drivers ----
+def debian_vuln(p, a):
+    """debian.go:78-98: the DetectedVulnerability of package p and advisory a."""
+    v = _base(p, a, fmt(p))
+    if a.get("VendorIDs"):
+        v["VendorIDs"] = a["VendorIDs"]
+    if a.get("Status"):
+        v["Status"] = a["Status"]
+    if a.get("Severity", 0) != 0:
+        v["SeveritySource"] = "debian"
+        v["Severity"] = SEVERITY[a["Severity"]] if 0 < a["Severity"] < 5 else SEVERITY[0]
+    return v
+
+
+def plain_vuln(p, a):
+    """ubuntu.go:99-108, amazon.go:75-83, alpine.go:94-101, wolfi / chainguard: the fields
+    _base sets, InstalledVersion = FormatVersion(pkg)."""
+    return _base(p, a, fmt(p))
+
+
 def debian_detect(db, os_ver, repo, pkgs, now=None):
     root = "debian " + major(os_ver)
     out = []
@@ -446,14 +474,7 @@ def debian_detect(db, os_ver, repo, pkgs, now=None):
         if not deb_valid(src):
             continue
         for a in _get(db, "failed to get debian advisories", root, p.get("SrcName", "")):
-            v = _base(p, a, fmt(p))
-            if a.get("VendorIDs"):
-                v["VendorIDs"] = a["VendorIDs"]
-            if a.get("Status"):
-                v["Status"] = a["Status"]
-            if a.get("Severity", 0) != 0:
-                v["SeveritySource"] = "debian"
-                v["Severity"] = SEVERITY[a["Severity"]] if 0 < a["Severity"] < 5 else SEVERITY[0]
+            v = debian_vuln(p, a)
             fixed = a.get("FixedVersion", "")
             if fixed == "":
                 out.append(v)
@@ -484,7 +505,7 @@ def ubuntu_detect(db, os_ver, repo, pkgs, now):
         if not deb_valid(src):
             continue
         for a in advs:
-            v = _base(p, a, fmt(p))
+            v = plain_vuln(p, a)
             fixed = a.get("FixedVersion", "")
             if fixed == "":
                 out.append(v)
@@ -516,7 +537,7 @@ def amazon_detect(db, os_ver, repo, pkgs, now=None):
             if r == 3:
                 continue
             if r < 0:
-                out.append(_base(p, a, inst))
+                out.append(plain_vuln(p, a))
     return out
 
 
@@ -562,7 +583,7 @@ def alpine_detect(db, os_ver, repo, pkgs, now=None):
             continue
         for a in advs:
             if alpine_vulnerable(src, a):
-                out.append(_base(p, a, fmt(p)))
+                out.append(plain_vuln(p, a))
     return out
 
 
@@ -578,7 +599,7 @@ def _apk_stream_detect(root, err):
             for a in advs:
                 fixed = a.get("FixedVersion", "")
                 if apk_valid(fixed) and apk_cmp(inst, fixed) < 0:
-                    out.append(_base(p, a, inst))
+                    out.append(plain_vuln(p, a))
         return out
     return detect
 
@@ -624,36 +645,49 @@ def redhat_detect(db, os_ver, repo, pkgs, now=None):
         except DecodeError as e:
             raise DecodeError(f"redhat vulnerability detection error: failed to get Red Hat advisories: {e}")
         inst = fmt(p)
-        uniq = {}
-        for a in advs:
-            if a["Arches"] and p.get("Arch", "") != "noarch" and p.get("Arch", "") not in a["Arches"]:
-                continue
-            vid = a["VulnerabilityID"]
-            v = {"VulnerabilityID": vid, "PkgID": p.get("ID"), "PkgName": p.get("Name"), "InstalledVersion": inst,
-                 "PkgIdentifier": p.get("Identifier"), "Status": a["Status"], "Layer": p.get("Layer"),
-                 "SeveritySource": "redhat",
-                 "Severity": SEVERITY[a["Severity"]] if 0 <= a["Severity"] < 5 else SEVERITY[0]}
-            if a["FixedVersion"] == "":
-                if vid not in uniq:
-                    uniq[vid] = v
-                continue
-            if rpm_cmp(inst, a["FixedVersion"]) < 0:
-                v["VendorIDs"] = a.get("VendorIDs")
-                v["FixedVersion"] = rpm_string(a["FixedVersion"])
-                if vid in uniq:
-                    u = uniq[vid]
-                    u["VendorIDs"] = sorted(set((u.get("VendorIDs") or []) + (v["VendorIDs"] or [])))
-                    if rpm_cmp(u.get("FixedVersion") or "", a["FixedVersion"]) < 0:
-                        u["FixedVersion"] = v["FixedVersion"]
-                else:
-                    uniq[vid] = v
-        out += [{k: x for k, x in v.items() if x not in (None, "", [], 0) or k == "VulnerabilityID"}
-                for _, v in sorted(uniq.items())]
+        kept = [a for a in advs
+                if not (a["Arches"] and p.get("Arch", "") != "noarch" and p.get("Arch", "") not in a["Arches"])
+                and (a["FixedVersion"] == "" or rpm_cmp(inst, a["FixedVersion"]) < 0)]
+        out += redhat_uniq(p, inst, kept)
     return out
+
+
+def redhat_uniq(p, inst, advs):
+    """redhat.go:146-187 uniqVulns over package p's advisories that passed the arch filter and
+    (fixed ones) the version check, in Get order; sorted by VulnerabilityID."""
+    uniq = {}
+    for a in advs:
+        vid = a["VulnerabilityID"]
+        v = {"VulnerabilityID": vid, "PkgID": p.get("ID"), "PkgName": p.get("Name"), "InstalledVersion": inst,
+             "PkgIdentifier": p.get("Identifier"), "Status": a["Status"], "Layer": p.get("Layer"),
+             "SeveritySource": "redhat",
+             "Severity": SEVERITY[a["Severity"]] if 0 <= a["Severity"] < 5 else SEVERITY[0]}
+        if a["FixedVersion"] == "":
+            if vid not in uniq:
+                uniq[vid] = v
+            continue
+        v["VendorIDs"] = a.get("VendorIDs")
+        v["FixedVersion"] = rpm_string(a["FixedVersion"])
+        if vid in uniq:
+            u = uniq[vid]
+            u["VendorIDs"] = sorted(set((u.get("VendorIDs") or []) + (v["VendorIDs"] or [])))
+            if rpm_cmp(u.get("FixedVersion") or "", a["FixedVersion"]) < 0:
+                u["FixedVersion"] = v["FixedVersion"]
+        else:
+            uniq[vid] = v
+    return [{k: x for k, x in v.items() if x not in (None, "", [], 0) or k == "VulnerabilityID"}
+            for _, v in sorted(uniq.items())]
 
 
 def _rpm_simple(root_fn, err, name_fn=lambda p: p.get("Name", ""), inst_fn=fmt, fixed_out="raw",
                 skip=lambda p: False, unfixed=False, pkg_id=True, custom=True, getter="get"):
+    def vuln(p, a):
+        """alma.go:64-71, rocky.go:69-76, oracle.go:70-80, suse.go, photon.go, mariner.go:50-70:
+        FixedVersion printed by rpm Version.String() where the driver does."""
+        fixed = a.get("FixedVersion", "")
+        f = rpm_string(fixed) if fixed_out == "string" and fixed else fixed
+        return _base(p, a, fmt(p), fixed=f, pkg_id=pkg_id, custom=custom)
+
     def detect(db, os_ver, repo, pkgs, now=None):
         root = root_fn(os_ver)
         out = []
@@ -671,14 +705,14 @@ def _rpm_simple(root_fn, err, name_fn=lambda p: p.get("Name", ""), inst_fn=fmt, 
             for a in advs:
                 fixed = a.get("FixedVersion", "")
                 if unfixed and fixed == "":
-                    out.append(_base(p, a, fmt(p), fixed="", pkg_id=pkg_id, custom=custom))
+                    out.append(vuln(p, a))
                     continue
                 if getter == "oracle" and extract_ksplice(fixed) != extract_ksplice(p.get("Release", "")):
                     continue
                 if rpm_cmp(cmp_ver, fixed) < 0:
-                    f = rpm_string(fixed) if fixed_out == "string" else fixed
-                    out.append(_base(p, a, fmt(p), fixed=f, pkg_id=pkg_id, custom=custom))
+                    out.append(vuln(p, a))
         return out
+    detect.vuln = vuln
     return detect
 
 
@@ -707,6 +741,47 @@ sles_detect = _rpm_simple(lambda v: "SUSE Linux Enterprise " + v,
                           "failed to get SUSE advisory: failed to get SUSE advisories")
 opensuse_detect = _rpm_simple(lambda v: "openSUSE Leap " + v,
                               "failed to get SUSE advisory: failed to get SUSE advisories")
+
+
+debian_detect.vuln = debian_vuln
+for _d in (ubuntu_detect, amazon_detect, alpine_detect, wolfi_detect, chainguard_detect):
+    _d.vuln = plain_vuln
+
+
+# ----------------------------------------------------------- DetectedVulnerability records ----
+# A DetectedVulnerability is a record (the advisory side) plus its package's fields; the
+# batch-path checks compare records built here from a driver's own epilogue with a stub package.
+COPY_PKG_ID, COPY_PKG_NAME, COPY_IDENTIFIER, COPY_LAYER = 1, 2, 4, 8
+_STUB = {"ID": "\x01id", "Name": "\x01name", "Identifier": {"PURL": "\x01purl"}, "Layer": {"DiffID": "\x01layer"},
+         "FilePath": "\x01path", "Version": "\x01ver"}
+_PKG_FIELDS = {"PkgID": COPY_PKG_ID, "PkgName": COPY_PKG_NAME, "PkgIdentifier": COPY_IDENTIFIER, "Layer": COPY_LAYER}
+
+
+def record_of(v):
+    """(record dict, copy flags) of a DetectedVulnerability built for the stub package: the
+    package fields are dropped and remembered as the flags of the ones the driver copied."""
+    rec, flags = {}, 0
+    for k, x in v.items():
+        if k in _PKG_FIELDS:
+            flags |= _PKG_FIELDS[k]
+        elif k not in ("InstalledVersion", "PkgPath"):
+            rec[k] = x
+    return rec, flags
+
+
+def advisory_record(family, a):
+    """The record OS driver `family` builds from advisory a (its Get form)."""
+    if family in ("redhat", "centos"):
+        return redhat_group_record([a])
+    return record_of(DRIVERS[family][0].vuln(_STUB, a))
+
+
+def redhat_group_record(members):
+    """The record of one merged Red Hat vulnerability from its members (the advisories that
+    entered uniqVulns for one package and VulnerabilityID, Get order)."""
+    out = redhat_uniq(_STUB, "", members)
+    assert len(out) == 1, "members of one VulnerabilityID"
+    return record_of(out[0])
 
 
 # --------------------------------------------------------------------- dispatcher ----

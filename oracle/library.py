@@ -901,14 +901,28 @@ def detect_vulnerabilities(db, lang, pkg_id, name, ver):
         advs = get_advisories_prefix(db, eco + "::", normalize_pkg_name(eco, name))
     except DecodeError as e:
         raise DecodeError(f"failed to get {eco} advisories: failed to unmarshal advisory JSON: {e}")
-    out = []
-    for a in advs:
-        if not is_vulnerable(grammar, ver, a):
-            continue
-        v = {"VulnerabilityID": a["VulnerabilityID"], "PkgID": pkg_id, "PkgName": name, "InstalledVersion": ver,
-             "FixedVersion": create_fixed_versions(a), "DataSource": a.get("DataSource")}
-        out.append({k: x for k, x in v.items() if x})
-    return out
+    return [library_vuln(a, pkg_id, name, ver) for a in advs if is_vulnerable(grammar, ver, a)]
+
+
+def library_vuln(a, pkg_id, name, ver):
+    """driver.go:125-132: the DetectedVulnerability of advisory a for (pkgID, pkgName, pkgVer)."""
+    v = {"VulnerabilityID": a["VulnerabilityID"], "PkgID": pkg_id, "PkgName": name, "InstalledVersion": ver,
+         "FixedVersion": create_fixed_versions(a), "DataSource": a.get("DataSource")}
+    return {k: x for k, x in v.items() if x}
+
+
+def wrap_vuln(v, p):
+    """detect.go:33-37: library.Detect adds the package's Layer, PkgPath and PkgIdentifier."""
+    for k_in, k_out in (("Layer", "Layer"), ("FilePath", "PkgPath"), ("Identifier", "PkgIdentifier")):
+        if p.get(k_in):
+            v[k_out] = p[k_in]
+    return v
+
+
+def advisory_record(a):
+    """The record (drivers.record_of) library.Detect builds from advisory a."""
+    from .drivers import _STUB, record_of
+    return record_of(wrap_vuln(library_vuln(a, _STUB["ID"], _STUB["Name"], _STUB["Version"]), _STUB))
 
 
 def detect(db, lang, pkgs):
@@ -922,9 +936,5 @@ def detect(db, lang, pkgs):
             vs = detect_vulnerabilities(db, lang, p.get("ID", ""), p.get("Name", ""), p.get("Version", ""))
         except DecodeError as e:
             raise DecodeError(f"failed to scan {eco} vulnerabilities: failed to detect {eco} vulnerabilities: {e}")
-        for v in vs:
-            for k_in, k_out in (("Layer", "Layer"), ("FilePath", "PkgPath"), ("Identifier", "PkgIdentifier")):
-                if p.get(k_in):
-                    v[k_out] = p[k_in]
-        out += vs
+        out += [wrap_vuln(v, p) for v in vs]
     return out

@@ -87,14 +87,18 @@ class Prepared:
 
     def __init__(self, sm, sdb, sample):
         self.pkgs = []  # (plat, driver package dict) in sample order
+        self.installed = []  # per package: the InstalledVersion its driver reports
+        self.plat_family = []  # per platform: the OS driver family, or None for a language bucket
         plat_drv, plat_gram = [], []
         for bucket, kind in sdb.plats:
             if kind in sm.LANG_OF:
                 plat_drv.append(MX_LIB)
                 plat_gram.append(GRAMMAR[ol.LANG[sm.LANG_OF[kind]][1]])
+                self.plat_family.append(None)
             else:
                 plat_drv.append(MX[sm.DRIVER_OF[kind][0]])
                 plat_gram.append(0)
+                self.plat_family.append(sm.DRIVER_OF[kind][0])
         arch_id = {}
 
         def aid(a):
@@ -111,6 +115,7 @@ class Prepared:
                 if kind == "redhat":  # the release the driver is called with (one per image)
                     pk["_rel"] = int(g["rhrel"][i])
                 self.pkgs.append((p, pk))
+                self.installed.append(pk.get("Version", "") if kind in sm.LANG_OF else od.fmt(pk))
                 if kind in sm.LANG_OF:
                     nm, ver, sk = ol.normalize_pkg_name(eco, pk.get("Name", "")), pk.get("Version", ""), False
                 else:
@@ -132,12 +137,16 @@ class Prepared:
                 by_root.setdefault(r, set()).add(nm)
         by_root["Red Hat CPE"] = {"repository", "nvr", "cpe"}
         recs = od.Records(sdb.records_for(by_root))
+        cpe_of = {}  # (content sets, nvr) -> the CPE set (one per image, not per package)
         for i, (p, pk) in enumerate(self.pkgs):
             if sdb.plats[p][1] == "redhat":
                 bi = pk.get("BuildInfo")
                 cs, nvr = ((od.REDHAT_DEFAULT_CONTENT_SETS.get(str(pk["_rel"]), []), "")
                            if bi is None else (bi.get("ContentSets") or [], f"{bi.get('Nvr', '')}-{bi.get('Arch', '')}"))
-                cpes[i + 1] = recs.redhat_cpes(cs, [nvr])
+                k = (tuple(cs), nvr)
+                if k not in cpe_of:
+                    cpe_of[k] = recs.redhat_cpes(cs, [nvr])
+                cpes[i + 1] = cpe_of[k]
         # entries per wanted key
         ar = _Arena()
         vids = set()
@@ -154,22 +163,23 @@ class Prepared:
                     if any(v == "" for v in vul + (a.get("PatchedVersions") or [])):
                         fl |= ALWAYS
                     ents.append({"vid": a["VulnerabilityID"], "vul": " || ".join(vul), "sec": " || ".join(sec),
-                                 "flags": fl})
+                                 "flags": fl, "adv": a})
             elif kind == "redhat":
                 for vid, val in recs.raw("Red Hat", nm):
                     for e in od.decode_redhat(val):
                         for c in e["Cves"]:
                             ents.append({"vid": vid if vid.startswith("CVE-") else c["ID"], "fixed": e["FixedVersion"],
-                                         "arches": e["Arches"], "cpes": e["Affected"]})
+                                         "arches": e["Arches"], "cpes": e["Affected"],
+                                         "adv": od.redhat_cve_advisory(vid, e, c)})
             else:
                 for a in recs.get(bucket, nm):
                     if kind == "rocky" and a.get("Entries"):
                         for e in a["Entries"]:
                             ents.append({"vid": a["VulnerabilityID"], "fixed": e.get("FixedVersion", ""),
-                                         "arches": e.get("Arches") or []})
+                                         "arches": e.get("Arches") or [], "adv": od.rocky_entry_advisory(a, e)})
                         continue
                     ents.append({"vid": a["VulnerabilityID"], "fixed": a.get("FixedVersion", ""),
-                                 "aff": a.get("AffectedVersion", ""), "arches": None})
+                                 "aff": a.get("AffectedVersion", ""), "arches": None, "adv": a})
             for e in ents:
                 vids.add(e["vid"])
             keys.append((p, nm, ents))
@@ -217,16 +227,15 @@ class Prepared:
                            _p(c["aff_len"], _U32), _p(c["vul_off"], _U64), _p(c["vul_len"], _U32),
                            _p(c["sec_off"], _U64), _p(c["sec_len"], _U32), _p(c["flags"], _U32), _p(c["vid"], _I32),
                            _p(arr(ids_begin, np.int64), _I64), _p(c["n_arch"], _I32), _p(arr(ids or [0], np.int32), _I32))
-        na, va = _Arena(), _Arena()
-        no, nl, vo, vl = [], [], [], []
-        for nm, ver in zip(names, vers):
-            o, n = na.put(nm)
-            no.append(o)
-            nl.append(n)
-            o, n = va.put(ver)
-            vo.append(o)
-            vl.append(n)
-        nab, vab = na.bytes(), va.bytes()
+        def packed(strs):
+            bs = [x.encode() for x in strs]
+            ln = np.fromiter((len(x) for x in bs), dtype=np.uint32, count=len(bs))
+            off = np.zeros(len(bs), dtype=np.uint64)
+            if len(bs):
+                off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+            return b"".join(bs), off, ln
+        nab, no, nl = packed(names)
+        vab, vo, vl = packed(vers)
         self.keep += [nab, vab]
         cb = np.cumsum([0] + [len(x) for x in cpes[1:]]).astype(np.int64)
         cid = [x for s in cpes[1:] for x in s] or [0]
@@ -237,22 +246,23 @@ class Prepared:
         self.n = len(names)
 
 
-def match(prep, n_threads=1):
+def match(prep, n_threads=1, members=False):
     """(package index array, entry index array) in per-package driver output order.  The
     output buffers live in prep and are reused (fresh arrays per call cost page faults that
-    serialise the threads)."""
+    serialise the threads).  members: after each Red Hat group's entry come its members as
+    -(entry + 1) (ORC_MIX_MEMBERS)."""
     L = _lib()
-    L.orc_mix_match.restype = ctypes.c_int64
-    L.orc_mix_match.argtypes = [ctypes.POINTER(OrcMixDB), ctypes.POINTER(OrcMixBatch), ctypes.c_int, _I64, _I64,
-                                ctypes.c_int64]
+    L.orc_mix_match_ex.restype = ctypes.c_int64
+    L.orc_mix_match_ex.argtypes = [ctypes.POINTER(OrcMixDB), ctypes.POINTER(OrcMixBatch), ctypes.c_int, _I64, _I64,
+                                   ctypes.c_int64, ctypes.c_int]
     while True:
         out = getattr(prep, "_out", None)
         if out is None:
             cap = max(1024, prep.n * 8)
             out = prep._out = (np.zeros(cap, dtype=np.int64), np.zeros(cap, dtype=np.int64))
         pk, en = out
-        n = L.orc_mix_match(ctypes.byref(prep.db), ctypes.byref(prep.batch), n_threads, _p(pk, _I64), _p(en, _I64),
-                            len(pk))
+        n = L.orc_mix_match_ex(ctypes.byref(prep.db), ctypes.byref(prep.batch), n_threads, _p(pk, _I64),
+                               _p(en, _I64), len(pk), 1 if members else 0)
         if n <= len(pk):
             return pk[:n], en[:n]
         prep._out = (np.zeros(int(n), dtype=np.int64), np.zeros(int(n), dtype=np.int64))

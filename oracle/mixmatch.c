@@ -73,6 +73,7 @@ typedef struct {
   int64_t lo, hi;
   int64_t *pk, *en;
   int64_t n, cap;
+  int members; /* ORC_MIX_MEMBERS: after each Red Hat group's entry, its members as -(entry + 1) */
 } job;
 
 static void push(job* j, int64_t p, int64_t e) {
@@ -119,7 +120,12 @@ static int ks_eq(const char* a, size_t na, const char* b, size_t nb) {
 typedef struct {
   int32_t vid;
   int64_t first, best;  /* entries: the first of the ID, the one holding the greatest fixed version */
+  int64_t head, tail;   /* its members (entries that entered the uniq map), a list in mem[] */
 } rhslot;
+
+typedef struct {
+  int64_t e, next;
+} rhmem;
 
 static int rh_cmp(const void* x, const void* y) {
   const rhslot *a = x, *b = y;
@@ -132,6 +138,19 @@ static void* run_job(void* arg) {
   const orc_mix_batch* b = j->b;
   rhslot* rh = NULL;
   int64_t rh_cap = 0;
+  rhmem* mem = NULL;
+  int64_t mem_n = 0, mem_cap = 0;
+#define MEM_ADD(slot, ent)                                                 \
+  do {                                                                     \
+    if (mem_n == mem_cap) {                                                \
+      mem_cap = mem_cap ? mem_cap * 2 : 256;                               \
+      mem = realloc(mem, sizeof(rhmem) * (size_t)mem_cap);                 \
+    }                                                                      \
+    mem[mem_n] = (rhmem){(ent), -1};                                       \
+    if ((slot)->tail >= 0) mem[(slot)->tail].next = mem_n;                 \
+    else (slot)->head = mem_n;                                             \
+    (slot)->tail = mem_n++;                                                \
+  } while (0)
   for (int64_t i = j->lo; i < j->hi; i++) {
     const int32_t plat = b->plat[i];
     if (plat < 0 || plat >= db->n_plat || (b->skip && b->skip[i])) continue;
@@ -212,6 +231,7 @@ static void* run_job(void* arg) {
       }
       case ORC_MX_REDHAT: {
         int64_t nslot = 0;
+        mem_n = 0;
         for (int64_t e = e0; e < e1; e++) {
           const int64_t q0 = db->ids_begin[e], na = db->n_arch[e] > 0 ? db->n_arch[e] : 0, q1 = db->ids_begin[e + 1];
           int cpe_ok = 0; /* one of the entry's affected CPEs in the package's CPE set */
@@ -238,7 +258,9 @@ static void* run_job(void* arg) {
                 rh_cap = rh_cap ? rh_cap * 2 : 64;
                 rh = realloc(rh, sizeof(rhslot) * (size_t)rh_cap);
               }
-              rh[nslot++] = (rhslot){vid, e, e};
+              rh[nslot] = (rhslot){vid, e, e, -1, -1};
+              MEM_ADD(&rh[nslot], e);
+              nslot++;
             }
             continue;
           }
@@ -246,17 +268,24 @@ static void* run_job(void* arg) {
             if (s >= 0) {  /* VendorIDs union; FixedVersion raised to the greatest */
               const int64_t bst = rh[s].best;
               if (orc_rpm_cmp_str(db->arena + db->fixed_off[bst], db->fixed_len[bst], fx, nf) < 0) rh[s].best = e;
+              MEM_ADD(&rh[s], e);
             } else {
               if (nslot == rh_cap) {
                 rh_cap = rh_cap ? rh_cap * 2 : 64;
                 rh = realloc(rh, sizeof(rhslot) * (size_t)rh_cap);
               }
-              rh[nslot++] = (rhslot){vid, e, e};
+              rh[nslot] = (rhslot){vid, e, e, -1, -1};
+              MEM_ADD(&rh[nslot], e);
+              nslot++;
             }
           }
         }
         qsort(rh, (size_t)nslot, sizeof(rhslot), rh_cmp);
-        for (int64_t q = 0; q < nslot; q++) push(j, i, rh[q].best);
+        for (int64_t q = 0; q < nslot; q++) {
+          push(j, i, rh[q].best);
+          if (j->members)
+            for (int64_t x = rh[q].head; x >= 0; x = mem[x].next) push(j, i, -(mem[x].e + 1));
+        }
         break;
       }
       case ORC_MX_LIB: {
@@ -272,11 +301,18 @@ static void* run_job(void* arg) {
     }
   }
   free(rh);
+  free(mem);
+#undef MEM_ADD
   return NULL;
 }
 
 int64_t orc_mix_match(const orc_mix_db* db, const orc_mix_batch* b, int n_threads, int64_t* out_pkg,
                       int64_t* out_entry, int64_t cap) {
+  return orc_mix_match_ex(db, b, n_threads, out_pkg, out_entry, cap, 0);
+}
+
+int64_t orc_mix_match_ex(const orc_mix_db* db, const orc_mix_batch* b, int n_threads, int64_t* out_pkg,
+                         int64_t* out_entry, int64_t cap, int flags) {
   if (n_threads <= 0) n_threads = 1;
   kmap m;
   kmap_build(&m, db);
@@ -287,6 +323,7 @@ int64_t orc_mix_match(const orc_mix_db* db, const orc_mix_batch* b, int n_thread
     jobs[t].db = db;
     jobs[t].b = b;
     jobs[t].m = &m;
+    jobs[t].members = (flags & ORC_MIX_MEMBERS) != 0;
     jobs[t].lo = (int64_t)t * per < b->n ? (int64_t)t * per : b->n;
     jobs[t].hi = jobs[t].lo + per < b->n ? jobs[t].lo + per : b->n;
     if (n_threads == 1) run_job(&jobs[t]);

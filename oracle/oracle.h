@@ -162,6 +162,12 @@ typedef struct {
  * Returns the count (call again with a larger buffer when > cap). */
 int64_t orc_mix_match(const orc_mix_db* db, const orc_mix_batch* b, int n_threads, int64_t* out_pkg,
                       int64_t* out_entry, int64_t cap);
+/* orc_mix_match with flags: ORC_MIX_MEMBERS also emits, after every Red Hat group's entry, the
+ * group's members (the entries that entered redhat.go's uniqVulns map, Get order) as
+ * -(entry + 1) - what the whole-batch DetectedVulnerability checks rebuild the merge from. */
+enum { ORC_MIX_MEMBERS = 1 };
+int64_t orc_mix_match_ex(const orc_mix_db* db, const orc_mix_batch* b, int n_threads, int64_t* out_pkg,
+                         int64_t* out_entry, int64_t cap, int flags);
 
 #ifdef __cplusplus
 }

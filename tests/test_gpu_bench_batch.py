@@ -27,6 +27,11 @@ def test_bench_c2_batch_matches_oracle():
     pairs = mb.pairs()
     opk, oad = om.match(om.Prepared(wl.sdb, wl.batch), n_threads=16)
     assert np.array_equal(pairs[:, 0], opk) and np.array_equal(pairs[:, 1], oad)
+    # the DetectedVulnerability set of the batch (tvm_match_vulns): one per pair, each the
+    # record of its advisory (Debian / Ubuntu epilogues; fields: tests/test_gpu_vulns.py)
+    vs = mb.vulns()
+    assert np.array_equal(vs.pkg, opk) and np.array_equal(vs.rec, oad)
+    vs.close()
     mb.close()
     # the end-to-end pipelined pass (bench.py end_to_end) on the same 4M batch: CSR == oracle
     mp = MatchBatch(eng)
@@ -38,4 +43,7 @@ def test_bench_c2_batch_matches_oracle():
     assert got == total and ep == -1
     assert np.array_equal(np.repeat(np.arange(len(rend), dtype=np.uint32), counts), opk)
     assert np.array_equal(adv, oad)
+    vp = mp.vulns(pipeline=True)
+    assert np.array_equal(vp.pkg, opk) and np.array_equal(vp.rec, oad)
+    vp.close()
     mp.close()

@@ -33,58 +33,53 @@ def world():
     return sdb, build_engine(sdb)
 
 
-@pytest.mark.parametrize("raw,adv32,delta,byte", [(False, False, False, False), (True, False, False, False),
-                                                  (False, True, False, False), (False, False, True, False),
-                                                  (True, False, True, False), (False, False, False, True),
-                                                  (True, False, False, True)])
+def _chunks(nt, ct):
+    """The chunk count prepare() lays out (pipeline.hip): batches of 3+ chunks begin and end
+    with a quarter chunk, whole chunks in between while more than a chunk and a quarter remain."""
+    if nt == 0:
+        return 1
+    q = max(1, ct // 4)
+    if nt < 3 * ct:
+        return -(-nt // ct)
+    bounds, t = [0, q], q
+    while nt - t > ct + q:
+        t += ct
+        bounds.append(t)
+    if nt - t > q:
+        bounds.append(nt - q)
+    bounds.append(nt)
+    return len(bounds) - 1
+
+
+@pytest.mark.parametrize("raw,adv32", [(False, False), (True, False), (False, True)])
 @pytest.mark.parametrize("chunk", [256, 1000, 4096, 1 << 19])
-def test_pipeline_matches_oracle(world, chunk, raw, adv32, delta, byte, oracle_built):
-    import delta_ref as dr
+def test_pipeline_matches_oracle(world, chunk, raw, adv32, oracle_built):
     sdb, eng = world
     batch = make_batch(sdb, 37, 333, [2, 2, 1], seed=chunk)  # 12321 packages: ragged last tile
     opk, oad = om.match(om.Prepared(sdb, batch), n_threads=8)
-    mb = _fill(eng, sdb, batch).pipeline_prepare(match_cap=len(opk) + 5, chunk_packages=chunk, raw=raw, adv32=adv32,
-                                                 delta=delta, byte=byte)
+    mb = _fill(eng, sdb, batch).pipeline_prepare(match_cap=len(opk) + 5, chunk_packages=chunk, raw=raw, adv32=adv32)
     for _ in range(2):  # a second pass over the same pinned batch gives the same lists
         total, errp, ms = mb.pipeline_run()
         assert errp == -1 and total == len(opk) and ms > 0
         adv, rend = mb.pipeline_csr()
         pk, ad = _pairs_of(adv[:total], rend[:len(batch)])
         assert np.array_equal(pk, opk) and np.array_equal(ad, oad)
-        if delta:  # the streams as they crossed the link, decoded by the Python restatement
-            stream, info, n = mb.pipeline_delta()
-            radv, rrend = dr.decode(stream, info)
-            assert n == total and np.array_equal(radv, oad) and np.array_equal(rrend[:len(batch)], rend[:len(batch)])
-            with pytest.raises(RuntimeError):
-                mb.pipeline_csr_raw()
-        elif byte:
-            with pytest.raises(RuntimeError):
-                mb.pipeline_csr_raw()
-        else:
-            araw, width = mb.pipeline_csr_raw()  # the bytes as they crossed the link
-            assert width == (4 if adv32 else 3) and np.array_equal(araw, oad)
+        araw, width = mb.pipeline_csr_raw()  # the bytes as they crossed the link
+        assert width == (4 if adv32 else 3) and np.array_equal(araw, oad)
+        vs = mb.vulns(pipeline=True)  # the DetectedVulnerability set straight from the result as it arrived
+        assert np.array_equal(vs.pkg, opk) and np.array_equal(vs.rec, oad)
+        vs.close()
     st = mb.pipeline_stats()
     ct, nt = -(-chunk // 256), -(-len(batch) // 256)  # tiles per chunk, tiles
-    q = max(1, ct // 4)  # batches of 3+ chunks begin and end with a quarter chunk (pipeline.hip)
-    want = -(-nt // ct) if nt < 3 * ct else 2 + -(-(nt - 2 * q) // ct)
-    assert abs(st["chunks"] - want) <= 1 and st["h2d_bytes"] > 0
-    if delta:
-        stream, info, _ = mb.pipeline_delta()
-        assert st["d2h_bytes"] == 8 * len(info) + int(((info[:, 1].astype(np.int64) + 15) // 16 * 16).sum())
-        assert st["d2h_bytes"] < 4 * len(batch) + 3 * len(opk)
-    elif byte:  # bytes + high halves + row ends (+ 4 per escape)
-        assert st["d2h_bytes"] >= len(opk) + 2 * nt * 256 + 4 * len(batch)
-        assert st["d2h_bytes"] < 4 * len(batch) + 3 * len(opk)
-    else:
-        assert st["d2h_bytes"] == 4 * len(batch) + (4 if adv32 else 3) * len(opk)
+    assert st["chunks"] == _chunks(nt, ct) and st["h2d_bytes"] > 0
+    assert st["d2h_bytes"] == 4 * len(batch) + (4 if adv32 else 3) * len(opk)
     assert st["transport_form"] == (not raw)
     mb.close()
 
 
-def test_pipeline_delta_heavy_lists(oracle_built):
-    """The delta form's escapes on the GPU: "linux" packages at the lowest version match
-    every advisory of the heaviest key (lists of 255 and more: the 4-byte count), beside
-    ordinary packages; equal to the oracle."""
+def test_pipeline_heavy_lists(oracle_built):
+    """Per-package lists of 255 advisories and more ("linux" packages at the lowest version
+    match every advisory of the heaviest key) beside ordinary packages; equal to the oracle."""
     from test_gpu_parity import build_engine
     from tools.synth import SynthBatch
     sdb = make_db(["debian 12"], 400, seed=21, max_adv=700)
@@ -96,42 +91,11 @@ def test_pipeline_delta_heavy_lists(oracle_built):
     batch = SynthBatch(base.plat, names, vers, list(base.targets))
     opk, oad = om.match(om.Prepared(sdb, batch), n_threads=4)
     assert np.bincount(opk).max() >= 255
-    for form in ("delta", "byte"):
-        mb = _fill(eng, sdb, batch).pipeline_prepare(match_cap=len(opk) + 1, chunk_packages=512, **{form: True})
-        total, errp, _ = mb.pipeline_run()
-        pk, ad = _pairs_of(*mb.pipeline_csr())
-        assert total == len(opk) and np.array_equal(pk[:len(opk)], opk) and np.array_equal(ad[:len(opk)], oad), form
-        mb.close()
-
-
-def test_pipeline_byte_form_escapes(oracle_built):
-    """The byte form's escapes on the GPU: the heavy key's advisories are fixed below the
-    installed version except every 300th, so a "linux" package matches advisories 300 apart -
-    steps beyond 254, which travel as escapes (0xFF + the index in the sparse wide array) -
-    beside ordinary packages; equal to the oracle."""
-    from test_gpu_parity import build_engine
-    from tools.synth import SynthBatch
-    sdb = make_db(["debian 12"], 400, seed=33, max_adv=3000)
-    lk = sdb.key_names.index(b"linux")
-    b0, b1 = int(sdb.adv_begin[lk]), int(sdb.adv_begin[lk + 1])
-    for a in range(b0, b1):
-        sdb.adv_fixed[a] = b"99.0-1" if (a - b0) % 300 == 7 else b"0.0.1-1"
-    eng = build_engine(sdb)
-    base = make_batch(sdb, 4, 300, [1], seed=3)
-    names, vers = list(base.names), list(base.versions)
-    for i in range(5, len(names), 41):
-        names[i], vers[i] = b"linux", b"1.0-1"
-    batch = SynthBatch(base.plat, names, vers, list(base.targets))
-    opk, oad = om.match(om.Prepared(sdb, batch), n_threads=4)
-    first = np.ones(len(opk), bool)
-    first[1:] = opk[1:] != opk[:-1]
-    step = np.diff(oad.astype(np.int64), prepend=0)
-    assert np.count_nonzero(~first & ((step < 1) | (step > 254))) > 0  # the case under test
-    mp = _fill(eng, sdb, batch).pipeline_prepare(match_cap=len(opk) + 1, chunk_packages=512, byte=True)
-    total, errp, _ = mp.pipeline_run()
-    pk, ad = _pairs_of(*mp.pipeline_csr())
+    mb = _fill(eng, sdb, batch).pipeline_prepare(match_cap=len(opk) + 1, chunk_packages=512)
+    total, errp, _ = mb.pipeline_run()
+    pk, ad = _pairs_of(*mb.pipeline_csr())
     assert total == len(opk) and np.array_equal(pk[:len(opk)], opk) and np.array_equal(ad[:len(opk)], oad)
-    mp.close()
+    mb.close()
 
 
 def test_pipeline_transport_form_edges(oracle_built):

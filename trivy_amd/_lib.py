@@ -3,6 +3,7 @@
 The native library is the product: there is no Python or CPU fallback for any
 matching step.  Loading fails loudly when libtrivy_amd.so has not been built.
 """
+import atexit
 import ctypes
 import os
 
@@ -65,6 +66,12 @@ class Vuln(ctypes.Structure):
         ("data_source_url", ctypes.c_char_p),
         ("custom_json", ctypes.c_char_p),
     ]
+
+
+class VulnSet(ctypes.Structure):
+    _fields_ = [("pkg", ctypes.POINTER(ctypes.c_uint32)), ("rec", ctypes.POINTER(ctypes.c_uint32)),
+                ("n", ctypes.c_size_t), ("adv_recs", ctypes.POINTER(Vuln)), ("n_adv_recs", ctypes.c_size_t),
+                ("grp_recs", ctypes.POINTER(Vuln)), ("n_grp_recs", ctypes.c_size_t), ("priv", ctypes.c_void_p)]
 
 
 class AttrCols(ctypes.Structure):
@@ -149,6 +156,9 @@ _SIG = [
                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_void_p, ctypes.c_uint32]),
     ("tvm_batch_size", ctypes.c_int64, [_P]),
+    ("tvm_batch_add_targets", ctypes.c_int64, [_P, _P, ctypes.c_size_t, ctypes.POINTER(Str), ctypes.c_void_p,
+                                               ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                               ctypes.c_void_p]),
     ("tvm_batch_cpe_set", ctypes.c_int64, [_P, _P, ctypes.c_void_p, ctypes.c_size_t, Str]),
     ("tvm_batch_add_many_attrs", ctypes.c_int64, [_P, _P, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -163,6 +173,7 @@ _SIG = [
     ("tvm_match_launch", ctypes.c_int, [_P, _P, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_engine_sync", ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_device_sync", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_shutdown", None, []),
     ("tvm_pipeline_times", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     ("tvm_pool_stats", None, [ctypes.POINTER(ctypes.c_uint64)]),
     ("tvm_sbom_decode_cyclonedx", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
@@ -206,15 +217,6 @@ _SIG = [
     ("tvm_pipeline_result_raw", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint32),
                                                ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64)]),
     ("tvm_pipeline_stats", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
-    ("tvm_pipeline_result_delta", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64),
-                                                 ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint32),
-                                                 ctypes.POINTER(ctypes.c_uint64)]),
-    ("tvm_delta_decode", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32,
-                                        ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p,
-                                        ctypes.c_size_t]),
-    ("tvm_delta_region", ctypes.c_uint64, [ctypes.c_uint32, ctypes.c_uint64]),
-    ("tvm_byte_decode", ctypes.c_int64, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                         ctypes.c_uint32, ctypes.c_void_p]),
     ("tvm_version_key", ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p,
                                        ctypes.c_size_t]),
     ("tvm_engine_dropin_stats", ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
@@ -247,6 +249,11 @@ _SIG = [
     ("tvm_vuln_rank_many", ctypes.c_int, [_P, ctypes.POINTER(Str), ctypes.c_size_t, ctypes.c_void_p]),
     ("tvm_batch_set_report", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(Str),
                                             ctypes.POINTER(Str), ctypes.POINTER(Str)]),
+    ("tvm_match_vulns", ctypes.c_int, [_P, _P, ctypes.POINTER(VulnSet), ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_pipeline_vulns", ctypes.c_int, [_P, _P, ctypes.POINTER(VulnSet), ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_vuln_set_free", None, [ctypes.POINTER(VulnSet)]),
+    ("tvm_batch_report_get", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(RawStr),
+                                            ctypes.POINTER(RawStr), ctypes.POINTER(RawStr)]),
     ("tvm_match_filter_time", ctypes.c_int, [_P, _P, ctypes.POINTER(FilterOpts), ctypes.c_int,
                                              ctypes.POINTER(ctypes.c_double), ctypes.c_char_p, ctypes.c_size_t]),
 ]
@@ -268,6 +275,9 @@ def lib():
             f.restype = res
             f.argtypes = args
         _lib = L
+        # drain the library's queues, join its worker threads and free its cached blocks while
+        # the HIP runtime is still up (interpreter exit runs atexit before libraries unload)
+        atexit.register(L.tvm_shutdown)
     return _lib
 
 

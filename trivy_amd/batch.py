@@ -138,6 +138,21 @@ class MatchBatch:
             raise RuntimeError("tvm_batch_add_many rejected the packages")
         return first
 
+    def add_targets(self, buckets, target_end, arena, name_off, name_len, ver_off, ver_len):
+        """Many targets in one call (tvm_batch_add_targets): target t = packages
+        [target_end[t-1], target_end[t]) of the arena columns under buckets[t]."""
+        from ._lib import Str
+        bl = [b.encode() if isinstance(b, str) else bytes(b) for b in buckets]
+        arr = (Str * max(len(bl), 1))(*[Str(b, len(b)) for b in bl])
+        te = np.ascontiguousarray(target_end, dtype=np.uint64)
+        cols = [np.ascontiguousarray(c, dtype=t) for c, t in ((name_off, np.uint64), (name_len, np.uint32),
+                                                              (ver_off, np.uint64), (ver_len, np.uint32))]
+        first = lib().tvm_batch_add_targets(self.h, self.engine.h, len(bl), arr, te.ctypes.data, arena,
+                                            *[c.ctypes.data for c in cols])
+        if first < 0:
+            raise RuntimeError("tvm_batch_add_targets rejected the targets")
+        return first
+
     def __len__(self):
         return lib().tvm_batch_size(self.h)
 
@@ -229,16 +244,13 @@ class MatchBatch:
         return lib().tvm_match_algorithmic_bytes(self.engine.h, self.h)
 
     # ---- end-to-end pipelined pass (tvm_pipeline_*) ----
-    def pipeline_prepare(self, match_cap=None, chunk_packages=1 << 19, raw=False, adv32=False, delta=False,
-                         byte=False):
+    def pipeline_prepare(self, match_cap=None, chunk_packages=1 << 19, raw=False, adv32=False):
         """Pins the batch and sizes the pipeline (host batch -> GPU -> host CSR).  raw: upload
         the batch's own arrays instead of its transport form (TVM_PIPE_RAW); adv32: 4-byte
-        advisory indices in the result even when 3 bytes hold them (TVM_PIPE_ADV32); delta:
-        the result crosses the link in the delta form (TVM_PIPE_DELTA, decoded by
-        pipeline_csr); byte: the byte form (TVM_PIPE_BYTE, decoded inside the pass)."""
+        advisory indices in the result even when 3 bytes hold them (TVM_PIPE_ADV32)."""
         e = errbuf()
         cap = match_cap if match_cap is not None else max(1024, 8 * len(self))
-        flags = (1 if raw else 0) | (2 if adv32 else 0) | (4 if delta else 0) | (8 if byte else 0)
+        flags = (1 if raw else 0) | (2 if adv32 else 0)
         self._check(lib().tvm_pipeline_prepare(self.engine.h, self.h, cap, chunk_packages, flags, e, len(e)), e,
                     "tvm_pipeline_prepare")
         self.pipe_cap = cap
@@ -283,24 +295,13 @@ class MatchBatch:
         return out, width
 
     def pipeline_decode_ms(self):
-        """tvm_pipeline_result's host time for the last pass (the delta form decoded, or the
-        3-byte indices widened, into the CSR; once per pass), ms."""
+        """tvm_pipeline_result's host time for the last pass (the 3-byte indices widened into
+        the 4-byte CSR; once per pass), ms."""
         adv, rend, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
         t0 = time.perf_counter()
         if lib().tvm_pipeline_result(self.h, ctypes.byref(adv), ctypes.byref(rend), ctypes.byref(n)):
             raise RuntimeError("tvm_pipeline_result: no valid pass")
         return (time.perf_counter() - t0) * 1e3
-
-    def pipeline_delta(self):
-        """The last TVM_PIPE_DELTA pass's result as it arrived: (stream uint8 view, tile_info
-        uint32[n_tiles, 2] = {matches, stream bytes}, matches) - tvm_pipeline_result_delta."""
-        s, sb, ti, nt, n = ctypes.c_void_p(), ctypes.c_uint64(), ctypes.c_void_p(), ctypes.c_uint32(), ctypes.c_uint64()
-        if lib().tvm_pipeline_result_delta(self.h, ctypes.byref(s), ctypes.byref(sb), ctypes.byref(ti),
-                                           ctypes.byref(nt), ctypes.byref(n)):
-            raise RuntimeError("tvm_pipeline_result_delta: no valid delta pass")
-        stream = np.ctypeslib.as_array((ctypes.c_uint8 * sb.value).from_address(s.value))
-        info = np.ctypeslib.as_array((ctypes.c_uint32 * max(2 * nt.value, 1)).from_address(ti.value))[:2 * nt.value]
-        return stream, info.reshape(-1, 2).copy(), n.value
 
     def pipeline_stats(self):
         out = (ctypes.c_uint64 * 5)()
@@ -444,6 +445,31 @@ class MatchBatch:
                                                 len(e)), e, "tvm_match_filter_time")
         return ms.value / steps
 
+    # ---- DetectedVulnerability sets (tvm_match_vulns / tvm_pipeline_vulns) ----
+    def vulns(self, pipeline=False):
+        """The batch's DetectedVulnerability set (the drivers' epilogues over every match):
+        a VulnSet with pkg / rec columns and the records (after launch(), or after
+        pipeline_run() with pipeline=True)."""
+        from ._lib import VulnSet as CSet
+        vs, e = CSet(), errbuf()
+        fn = lib().tvm_pipeline_vulns if pipeline else lib().tvm_match_vulns
+        t0 = time.perf_counter()
+        self._check(fn(self.engine.h, self.h, ctypes.byref(vs), e, len(e)), e,
+                    "tvm_pipeline_vulns" if pipeline else "tvm_match_vulns")
+        ms = (time.perf_counter() - t0) * 1e3
+        return VulnSet(self, vs, ms)
+
+    def report(self, first=0, n=None):
+        """(names, installed versions, paths) of packages [first, first + n) as the export pairs
+        them with records (tvm_batch_report_get): names None where the caller's Name applies."""
+        from ._lib import RawStr
+        n = len(self) - first if n is None else n
+        cols = [(RawStr * max(n, 1))() for _ in range(3)]
+        if lib().tvm_batch_report_get(self.h, first, n, *cols):
+            raise ValueError("tvm_batch_report_get: bad range")
+        names = [(c.bytes().decode() if c.p else None) for c in cols[0][:n]]
+        return names, [c.bytes().decode() for c in cols[1][:n]], [c.bytes().decode() for c in cols[2][:n]]
+
     def close(self):
         h, self.h = getattr(self, "h", None), None
         if h:
@@ -452,6 +478,91 @@ class MatchBatch:
 
     def __del__(self):
         self.close()
+
+
+def vuln_record(v):
+    """A tvm_vuln record (the advisory side of a DetectedVulnerability) as a dict of the
+    DetectedVulnerability fields it sets, plus "_copy" = its copy flags."""
+    d = {"VulnerabilityID": v.vulnerability_id.decode(), "_copy": v.copy_flags}
+    if v.n_vendor_ids:
+        d["VendorIDs"] = [v.vendor_ids[k].decode() for k in range(v.n_vendor_ids)]
+    if v.fixed_version:
+        d["FixedVersion"] = v.fixed_version.decode()
+    if v.status:
+        d["Status"] = v.status
+    if v.severity_source:
+        d["SeveritySource"] = v.severity_source.decode()
+    if v.severity:
+        d["Severity"] = v.severity.decode()
+    if v.has_data_source:
+        d["DataSource"] = {k: val.decode() for k, val in [("ID", v.data_source_id), ("Name", v.data_source_name),
+                                                          ("URL", v.data_source_url)] if val}
+    if v.custom_json is not None:
+        d["Custom"] = v.custom_json.decode()
+    return d
+
+
+class VulnSet:
+    """tvm_vuln_set: DetectedVulnerability i = record rec[i] + package pkg[i]."""
+
+    def __init__(self, batch, cset, ms):
+        self.batch, self._c, self.ms = batch, cset, ms
+        n = cset.n
+        self.pkg = np.ctypeslib.as_array(cset.pkg, shape=(n,)).copy() if n else np.zeros(0, np.uint32)
+        self.rec = np.ctypeslib.as_array(cset.rec, shape=(n,)).copy() if n else np.zeros(0, np.uint32)
+        self.n_adv_recs, self.n_grp_recs = cset.n_adv_recs, cset.n_grp_recs
+        self._recs = {}
+
+    def __len__(self):
+        return len(self.pkg)
+
+    def record(self, r):
+        """Record r as a dict (vuln_record)."""
+        r = int(r)
+        d = self._recs.get(r)
+        if d is None:
+            c = self._c
+            d = vuln_record(c.adv_recs[r] if r < c.n_adv_recs else c.grp_recs[r - c.n_adv_recs])
+            self._recs[r] = d
+        return d
+
+    def dicts(self, pkgs=None, report=None):
+        """DetectedVulnerability dicts (small sets): pkgs maps a package index to the caller's
+        package dict (ID, Name, Identifier, Layer copied per the record's flags); report =
+        MatchBatch.report() columns (InstalledVersion, PkgPath, PkgName overrides)."""
+        from ._lib import COPY_IDENTIFIER, COPY_LAYER, COPY_PKG_ID, COPY_PKG_NAME
+        names, vers, paths = report if report is not None else self.batch.report()
+        out = []
+        for p, r in zip(self.pkg.tolist(), self.rec.tolist()):
+            d = dict(self.record(r))
+            fl = d.pop("_copy")
+            pk = (pkgs or {}).get(p, {})
+            if fl & COPY_PKG_ID and pk.get("ID"):
+                d["PkgID"] = pk["ID"]
+            name = names[p] if names[p] is not None else (pk.get("Name") if fl & COPY_PKG_NAME else None)
+            if name:
+                d["PkgName"] = name
+            if paths[p]:
+                d["PkgPath"] = paths[p]
+            if fl & COPY_IDENTIFIER and pk.get("Identifier"):
+                d["PkgIdentifier"] = pk["Identifier"]
+            if vers[p]:
+                d["InstalledVersion"] = vers[p]
+            if fl & COPY_LAYER and pk.get("Layer"):
+                d["Layer"] = pk["Layer"]
+            out.append(d)
+        return out
+
+    def close(self):
+        if self._c is not None and self._c.priv:
+            lib().tvm_vuln_set_free(ctypes.byref(self._c))
+        self._c = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def advisory_vuln_id(db, adv):

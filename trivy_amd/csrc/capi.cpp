@@ -20,8 +20,6 @@
 #include "libdb.h"
 #include "libver.h"
 #include "bbolt.h"
-#include "byte_form.h"
-#include "delta_form.h"
 #include "host_par.h"
 #include "pipeline.h"
 #include "pool.h"
@@ -32,10 +30,20 @@
 
 using namespace tvm;
 
+// The advisory side of every advisory's DetectedVulnerability (drivers.h advisory_templates)
+// in C form, built once per DB on the first batch export.
+struct VulnTemplates {
+  std::vector<tvm::Vuln> v;
+  std::vector<tvm_vuln> c;
+  std::vector<std::vector<const char*>> vp;
+};
+
 struct tvm_db {
   DB db;
   VulnTable vt;  // bucket "vulnerability" (FillInfo tables)
   bool finalized = false;
+  std::mutex tmpl_mu;
+  std::unique_ptr<VulnTemplates> tmpl;
 };
 
 struct tvm_engine {
@@ -148,42 +156,43 @@ struct ResultStore {
   std::vector<std::vector<const char*>> vendor_ptrs;
 };
 
+// One Vuln in C form; vp holds its VendorIDs pointers (both live as long as v).
+void to_c(const DB& db, const Vuln& v, tvm_vuln& c, std::vector<const char*>& vp) {
+  memset(&c, 0, sizeof(c));
+  c.pkg_index = v.pkg;
+  c.copy_flags = v.copy;
+  c.vulnerability_id = v.vuln_id.c_str();
+  if (!v.vendor_ids.empty()) {
+    for (const std::string& s : v.vendor_ids) vp.push_back(s.c_str());
+    c.vendor_ids = vp.data();
+    c.n_vendor_ids = v.vendor_ids.size();
+  }
+  c.pkg_id = v.pkg_id.c_str();
+  c.pkg_name = v.pkg_name.c_str();
+  c.pkg_path = v.pkg_path.c_str();
+  c.installed_version = v.installed.c_str();
+  c.fixed_version = v.fixed.c_str();
+  c.status = v.status;
+  c.severity_source = v.severity_source.c_str();
+  c.severity = v.severity.c_str();
+  if (v.data_source >= 0) {
+    const DataSource& ds = db.sources[size_t(v.data_source)];
+    c.has_data_source = 1;
+    c.data_source_id = ds.id.c_str();
+    c.data_source_name = ds.name.c_str();
+    c.data_source_url = ds.url.c_str();
+  } else {
+    c.data_source_id = c.data_source_name = c.data_source_url = "";
+  }
+  c.custom_json = v.has_custom ? v.custom.c_str() : nullptr;
+}
+
 void export_result(const DB& db, std::vector<Vuln>&& vulns, bool eosl, tvm_result* out) {
   auto* rs = new ResultStore();
   rs->v = std::move(vulns);
   rs->c.resize(rs->v.size());
   rs->vendor_ptrs.resize(rs->v.size());
-  for (size_t i = 0; i < rs->v.size(); i++) {
-    const Vuln& v = rs->v[i];
-    tvm_vuln& c = rs->c[i];
-    memset(&c, 0, sizeof(c));
-    c.pkg_index = v.pkg;
-    c.copy_flags = v.copy;
-    c.vulnerability_id = v.vuln_id.c_str();
-    if (!v.vendor_ids.empty()) {
-      for (const std::string& s : v.vendor_ids) rs->vendor_ptrs[i].push_back(s.c_str());
-      c.vendor_ids = rs->vendor_ptrs[i].data();
-      c.n_vendor_ids = v.vendor_ids.size();
-    }
-    c.pkg_id = v.pkg_id.c_str();
-    c.pkg_name = v.pkg_name.c_str();
-    c.pkg_path = v.pkg_path.c_str();
-    c.installed_version = v.installed.c_str();
-    c.fixed_version = v.fixed.c_str();
-    c.status = v.status;
-    c.severity_source = v.severity_source.c_str();
-    c.severity = v.severity.c_str();
-    if (v.data_source >= 0) {
-      const DataSource& ds = db.sources[size_t(v.data_source)];
-      c.has_data_source = 1;
-      c.data_source_id = ds.id.c_str();
-      c.data_source_name = ds.name.c_str();
-      c.data_source_url = ds.url.c_str();
-    } else {
-      c.data_source_id = c.data_source_name = c.data_source_url = "";
-    }
-    c.custom_json = v.has_custom ? v.custom.c_str() : nullptr;
-  }
+  for (size_t i = 0; i < rs->v.size(); i++) to_c(db, rs->v[i], rs->c[i], rs->vendor_ptrs[i]);
   out->vulns = rs->c.data();
   out->n = rs->c.size();
   out->eosl = eosl ? 1 : 0;
@@ -319,6 +328,17 @@ tvm_engine* tvm_engine_open(tvm_db* db, int device, char* err, size_t errlen) {
 }
 
 void tvm_engine_close(tvm_engine* e) { delete e; }
+
+void tvm_shutdown(void) {
+  // every device the process sees: drain whatever the library queued
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) == hipSuccess)
+    for (int d = 0; d < ndev; d++)
+      if (hipSetDevice(d) == hipSuccess) (void)hipDeviceSynchronize();
+  WorkerPool::shutdown_all();
+  release_encoders();
+  pool_close();
+}
 
 int tvm_device_sync(int device, char* err, size_t errlen) {
   int ndev = 0;
@@ -579,6 +599,43 @@ int64_t tvm_batch_add_many_attrs(tvm_batch* b, tvm_engine* e, const char* bucket
     if (flags & TVM_ATTR_CPESET) a.y = cols->cpe_set[i];
     if (flags) b->hb.add(pid, std::string_view(arena + name_off[i], name_len[i]), ver, a);
     else b->hb.add(pid, std::string_view(arena + name_off[i], name_len[i]), ver);
+  }
+  return first;
+}
+
+int64_t tvm_batch_add_targets(tvm_batch* b, tvm_engine* e, size_t n_targets, const tvm_str* buckets,
+                              const uint64_t* target_end, const char* arena, const uint64_t* name_off,
+                              const uint32_t* name_len, const uint64_t* ver_off, const uint32_t* ver_len) {
+  if (!b || !e || b->uploaded || b->pinned || (n_targets && (!buckets || !target_end)))
+    return -1;
+  const uint64_t n = n_targets ? target_end[n_targets - 1] : 0;
+  if (n && (!arena || !name_off || !name_len || !ver_off || !ver_len)) return -1;
+  for (size_t t = 0; t < n_targets; t++)
+    if (t && target_end[t] < target_end[t - 1]) return -1;
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e)) return -1;
+  const DB& db = e->eng->db();
+  HostBatch& hb = b->hb;
+  const int64_t first = int64_t(hb.pk.size());
+  uint64_t bytes = 0;
+  for (uint64_t i = 0; i < n; i++)
+    bytes += std::min<uint32_t>(name_len[i], 0xFFFF) + std::min<uint32_t>(ver_len[i], 0xFFFF);
+  reserve_more(hb, n);
+  hb.arena.reserve(hb.arena.size() + bytes);
+  hb.tile_off.reserve(hb.tile_off.size() + n / kGroup + 2);
+  std::string_view last_bucket;
+  uint32_t pid = 0xFFFFFFFFu;
+  uint64_t i = 0;
+  for (size_t t = 0; t < n_targets; t++) {
+    const std::string_view bk = sv(buckets[t]);
+    if (t == 0 || bk != last_bucket) {  // a fleet's targets repeat a few platform buckets
+      const int32_t plat = db.find_plat(bk);
+      pid = plat < 0 ? 0xFFFFFFFFu : uint32_t(plat);
+      last_bucket = bk;
+    }
+    b->target_begin.push_back(uint32_t(hb.pk.size()));
+    for (; i < target_end[t]; i++)
+      hb.add(pid, std::string_view(arena + name_off[i], name_len[i]), std::string_view(arena + ver_off[i], ver_len[i]));
   }
   return first;
 }
@@ -1342,9 +1399,7 @@ int tvm_match_filter_time(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o,
 int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32_t chunk_packages, uint32_t flags,
                          char* err, size_t errlen) {
   if (!e || !b || chunk_packages == 0 ||
-      (flags & ~uint32_t(TVM_PIPE_RAW | TVM_PIPE_ADV32 | TVM_PIPE_DELTA | TVM_PIPE_BYTE)) ||
-      ((flags & (TVM_PIPE_DELTA | TVM_PIPE_BYTE)) && (flags & TVM_PIPE_ADV32)) ||
-      ((flags & TVM_PIPE_DELTA) && (flags & TVM_PIPE_BYTE)))
+      (flags & ~uint32_t(TVM_PIPE_RAW | TVM_PIPE_ADV32)))
     return TVM_EINVAL;
   std::shared_lock<std::shared_mutex> lk(e->mu);
   if (!bind(b, e)) {
@@ -1356,13 +1411,7 @@ int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32
   b->pipe_wide_for = ~0ull;
   std::string msg;
   const bool packed = !(flags & TVM_PIPE_ADV32) && e->db->db.advs.size() < (1ull << 24);
-  const bool delta = (flags & TVM_PIPE_DELTA) != 0, byte = (flags & TVM_PIPE_BYTE) != 0;
-  if ((delta || byte) && !packed) {
-    b->pipe.reset();
-    set_err(err, errlen, "TVM_PIPE_DELTA / TVM_PIPE_BYTE: the form carries 3-byte advisory indices (the DB has 2^24 or more)");
-    return TVM_EINVAL;
-  }
-  if (!b->pipe->prepare(*e->eng, b->hb, match_cap, chunk_packages, !(flags & TVM_PIPE_RAW), packed, delta, byte, msg)) {
+  if (!b->pipe->prepare(*e->eng, b->hb, match_cap, chunk_packages, !(flags & TVM_PIPE_RAW), packed, msg)) {
     b->pipe.reset();
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
@@ -1409,7 +1458,7 @@ int tvm_pipeline_run(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* 
 
 int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row_end, uint64_t* n_matches) {
   if (!b || !b->pipe || b->pipe_total > b->pipe->cap()) return TVM_EINVAL;
-  if (adv && b->pipe->packed() && !b->pipe->delta() && !b->pipe->byte_form()) {  // widen the 3-byte indices once per pass (host side, after the pass)
+  if (adv && b->pipe->packed()) {  // widen the 3-byte indices once per pass (host side, after the pass)
     if (b->pipe_wide_for != b->pipe_runs) {
       const uint8_t* p = reinterpret_cast<const uint8_t*>(b->pipe->adv());
       b->pipe_wide.resize(b->pipe_total);
@@ -1430,45 +1479,12 @@ int tvm_pipeline_result(tvm_batch* b, const uint32_t** adv, const uint32_t** row
 
 int tvm_pipeline_result_raw(tvm_batch* b, const void** adv, uint32_t* width, const uint32_t** row_end,
                             uint64_t* n_matches) {
-  if (!b || !b->pipe || b->pipe_total > b->pipe->cap() || b->pipe->delta() || b->pipe->byte_form()) return TVM_EINVAL;
+  if (!b || !b->pipe || b->pipe_total > b->pipe->cap()) return TVM_EINVAL;
   if (adv) *adv = b->pipe->adv();
   if (width) *width = b->pipe->packed() ? 3 : 4;
   if (row_end) *row_end = b->pipe->row_end();
   if (n_matches) *n_matches = b->pipe_total;
   return TVM_OK;
-}
-
-int tvm_pipeline_result_delta(tvm_batch* b, const void** stream, uint64_t* stream_bytes, const uint32_t** tile_info,
-                              uint32_t* n_tiles, uint64_t* n_matches) {
-  if (!b || !b->pipe || !b->pipe->delta() || b->pipe_total > b->pipe->cap()) return TVM_EINVAL;
-  if (stream) *stream = b->pipe->delta_stream();
-  if (stream_bytes) *stream_bytes = b->pipe->delta_stream_size();
-  if (tile_info) *tile_info = reinterpret_cast<const uint32_t*>(b->pipe->delta_tiles());
-  if (n_tiles) *n_tiles = b->pipe->n_tiles();
-  if (n_matches) *n_matches = b->pipe_total;
-  return TVM_OK;
-}
-
-int tvm_delta_decode(const void* stream, uint64_t stream_bytes, const uint32_t* tile_info, uint32_t n_tiles,
-                     uint64_t n_matches, uint32_t* adv, uint32_t* row_end, char* err, size_t errlen) {
-  if ((n_tiles && (!stream || !tile_info || !row_end)) || (n_matches && !adv)) return TVM_EINVAL;
-  std::string msg;
-  if (!delta_decode(static_cast<const uint8_t*>(stream), stream_bytes, reinterpret_cast<const uint2*>(tile_info),
-                    n_tiles, n_matches, adv, row_end, msg)) {
-    set_err(err, errlen, msg);
-    return TVM_EINVAL;
-  }
-  return TVM_OK;
-}
-
-uint64_t tvm_delta_region(uint32_t tile, uint64_t first_match) { return delta_region(tile, first_match); }
-
-int64_t tvm_byte_decode(const uint8_t* bytes, const uint16_t* hi, const uint32_t* wide, const uint32_t* row_end,
-                        uint32_t n_tiles, uint32_t* adv) {
-  if (n_tiles && (!bytes || !hi || !wide || !row_end || !adv)) return -1;
-  int64_t esc = 0;
-  for (uint32_t t = 0; t < n_tiles; t++) esc += byte_decode_tile(bytes, hi, wide, row_end, t, adv);
-  return esc;
 }
 
 int tvm_wire_encode(size_t n, const uint32_t* plat, const char* arena, const uint64_t* name_off, const uint32_t* name_len,
@@ -1755,6 +1771,296 @@ int tvm_match_redhat_merge_time(tvm_engine* e, tvm_batch* b, int steps, double* 
     return TVM_EDEVICE;
   }
   *ms = f;
+  return TVM_OK;
+}
+
+// ---- DetectedVulnerability sets of a batch (the drivers' epilogues on the batch path) -------
+
+namespace {
+
+const VulnTemplates& templates(tvm_db* d) {
+  std::lock_guard<std::mutex> g(d->tmpl_mu);
+  if (!d->tmpl) {
+    auto t = std::make_unique<VulnTemplates>();
+    advisory_templates(d->db, t->v);
+    t->c.resize(t->v.size());
+    t->vp.resize(t->v.size());
+    range_for(t->v.size(), 1 << 14, [&](size_t a, size_t b) {
+      for (size_t i = a; i < b; i++) to_c(d->db, t->v[i], t->c[i], t->vp[i]);
+    });
+    d->tmpl = std::move(t);
+  }
+  return *d->tmpl;
+}
+
+// The refs of a tvm_vuln_set (heap blocks from the pool: a C2 set holds 20.5M of each) and the
+// merged Red Hat groups' records.
+struct VulnSetStore {
+  uint32_t* pkg = nullptr;
+  uint32_t* rec = nullptr;
+  void* pinned = nullptr;  // rec points into it (the order kernel's CSR as it arrived)
+  std::vector<Vuln> gv;
+  std::vector<tvm_vuln> gc;
+  std::vector<std::vector<const char*>> gvp;
+  ~VulnSetStore() {
+    if (pkg) pool_heap_put(pkg);
+    if (pinned) pool_host_put(pinned);
+    else if (rec) pool_heap_put(rec);
+  }
+};
+
+bool batch_has_redhat(const tvm_batch* b, const DB& db) {
+  const auto& pi = db.plat_info;
+  std::atomic<bool> any{false};
+  pool_range_for(b->hb.pk.size(), 1 << 16, [&](size_t a, size_t z) {
+    uint32_t last = 0xFFFFFFFFu;
+    for (size_t i = a; i < z && !any.load(std::memory_order_relaxed); i++) {
+      const uint32_t pl = b->hb.pk[i].x;
+      if (pl == last) continue;
+      last = pl;
+      if (pl < pi.size() && pi[pl].drv == DRV_REDHAT) any.store(true, std::memory_order_relaxed);
+    }
+  });
+  return any.load();
+}
+
+// pkg[] from CSR row ends (package p's matches end at row_end[p]), in parallel over packages.
+void expand_rows(const uint32_t* row_end, size_t n_pkgs, uint32_t pkg_base, uint32_t* pkg) {
+  pool_range_for(n_pkgs, 1 << 14, [&](size_t a, size_t z) {
+    uint32_t at = a ? row_end[a - 1] : 0;
+    for (size_t p = a; p < z; p++) {
+      const uint32_t e = row_end[p];
+      for (; at < e; at++) pkg[at] = uint32_t(p) + pkg_base;
+    }
+  });
+}
+
+void set_out(tvm_db* d, VulnSetStore* st, size_t n, tvm_vuln_set* out) {
+  const VulnTemplates& t = templates(d);
+  out->pkg = st->pkg;
+  out->rec = st->rec;
+  out->n = n;
+  out->adv_recs = t.c.data();
+  out->n_adv_recs = t.c.size();
+  out->grp_recs = st->gc.data();
+  out->n_grp_recs = st->gc.size();
+  out->priv = st;
+}
+
+// The order kernel over the batch's raw list into device buffers (caller holds the shared lock).
+bool order_locked(tvm_engine* e, tvm_batch* b, uint32_t* csr, uint32_t* row_end, uint64_t cap, std::string& err) {
+  (void)hipSetDevice(e->device);
+  hipStream_t st = e->eng->stream();
+  const uint32_t nt = b->dev.n_tiles;
+  if (nt == 0) return true;
+  if (b->order_cap < nt + 1) {
+    if (b->order_scratch) (void)hipFree(b->order_scratch);
+    b->order_scratch = nullptr;
+    b->order_cap = 0;
+    void* p = nullptr;
+    if (hipMalloc(&p, size_t(nt + 1) * 8) != hipSuccess) {
+      err = "hipMalloc(order scratch) failed";
+      return false;
+    }
+    b->order_scratch = static_cast<unsigned long long*>(p);
+    b->order_cap = nt + 1;
+  }
+  OrderArgs oa;
+  oa.dir = b->m.dir;
+  oa.pkg = b->m.pkg;
+  oa.adv = b->m.adv;
+  oa.csr_adv = csr;
+  oa.row_end = row_end;
+  oa.cap = std::min<uint64_t>(cap, b->m.cap);
+  oa.ticket = b->order_scratch;
+  oa.status = b->order_scratch + 1;
+  oa.t0 = 0;
+  oa.n = b->dev.n;
+  oa.pkg_base = b->dev.pkg_base;
+  if (hipMemsetAsync(b->order_scratch, 0, size_t(nt + 1) * 8, st) != hipSuccess) {
+    err = "hipMemsetAsync(order scratch) failed";
+    return false;
+  }
+  launch_order(nt, st, oa);
+  const hipError_t le = hipGetLastError();
+  if (le != hipSuccess) {
+    err = std::string("order kernel: ") + hipGetErrorString(le);
+    return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+int tvm_match_vulns(tvm_engine* e, tvm_batch* b, tvm_vuln_set* out, char* err, size_t errlen) {
+  if (!e || !b || !out || !b->uploaded) return TVM_EINVAL;
+  memset(out, 0, sizeof(*out));
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e)) {
+    set_err(err, errlen, kStale);
+    return TVM_EINVAL;
+  }
+  const DB& db = e->eng->db();
+  std::string msg;
+  (void)hipSetDevice(e->device);
+  // Red Hat packages report merged groups (redhat.go:146-187): the merge runs first
+  if (!b->merged && batch_has_redhat(b, db) && !rh_launch(e, b, msg)) {
+    set_err(err, errlen, "tvm_match_vulns: " + msg);
+    return TVM_EDEVICE;
+  }
+  uint64_t total = 0, bits = 0;
+  int64_t ep = -1;
+  if (match_status_locked(e, b, &total, &ep, &bits) != TVM_OK) {
+    set_err(err, errlen, "tvm_match_vulns: reading the match status failed");
+    return TVM_EDEVICE;
+  }
+  if (bits || ep >= 0 || total > cur(b).cap) {
+    set_err(err, errlen, bits ? "tvm_match_vulns: match kernel internal error bits " + std::to_string(bits)
+                         : ep >= 0 ? "tvm_match_vulns: the batch met an undecodable advisory (package " +
+                                         std::to_string(ep) + ")"
+                                   : "tvm_match_vulns: the match buffer overflowed (upload with a larger cap)");
+    return TVM_EINVAL;
+  }
+  templates(e->db);  // outside the timed part of a caller's second call
+  auto st = std::make_unique<VulnSetStore>();
+  const size_t n_alloc = std::max<uint64_t>(total, 1) * 4;
+  if (!(st->pkg = static_cast<uint32_t*>(pool_heap_get(n_alloc)))) {
+    set_err(err, errlen, "tvm_match_vulns: out of host memory");
+    return TVM_EDEVICE;
+  }
+  if (b->merged) {
+    std::vector<uint32_t> pkg, adv, base, contrib;
+    std::vector<uint2> grp;
+    if (!b->rh.fetch(rh_inputs(e, b), pkg, adv, base, grp, contrib, e->eng->stream(), msg)) {
+      set_err(err, errlen, "tvm_match_vulns: " + msg);
+      return TVM_EDEVICE;
+    }
+    if (!(st->rec = static_cast<uint32_t*>(pool_heap_get(n_alloc)))) {
+      set_err(err, errlen, "tvm_match_vulns: out of host memory");
+      return TVM_EDEVICE;
+    }
+    const auto& pi = db.plat_info;
+    std::vector<RhRec> groups;
+    const uint32_t n_adv = uint32_t(db.advs.size());
+    for (size_t i = 0; i < pkg.size(); i++) {
+      st->pkg[i] = pkg[i];
+      st->rec[i] = adv[i];
+      const uint32_t plat = b->hb.pk[pkg[i] - b->dev.pkg_base].x;
+      if (plat >= pi.size() || pi[plat].drv != DRV_REDHAT || grp[i].y <= 1) continue;
+      RhRec r{};  // a group of several members: its own record (VendorIDs union, greatest FixedVersion)
+      r.pkg = pkg[i];
+      r.base = base[i];
+      r.best = db.advs[adv[i]].fixed.empty() ? RH_NONE : adv[i];
+      r.start = grp[i].x;
+      r.len = grp[i].y;
+      st->rec[i] = n_adv + uint32_t(groups.size());
+      groups.push_back(r);
+    }
+    redhat_batch_vulns(db, b->hb, groups, contrib, b->dev.pkg_base, st->gv);
+    st->gc.resize(st->gv.size());
+    st->gvp.resize(st->gv.size());
+    for (size_t j = 0; j < st->gv.size(); j++) {
+      Vuln& v = st->gv[j];
+      v.pkg = 0;
+      v.installed.clear();  // a package field: the batch export pairs the record with its package
+      to_c(db, v, st->gc[j], st->gvp[j]);
+    }
+    total = pkg.size();
+  } else {
+    // the order kernel writes the per-package lists (CSR) on the device; one DMA each way back
+    const size_t np = b->hb.pk.size();
+    void* dcsr = pool_device_get(e->device, n_alloc, "tvm_match_vulns(csr)", msg);
+    void* drow = dcsr ? pool_device_get(e->device, std::max<size_t>(np, 1) * 4, "tvm_match_vulns(row ends)", msg)
+                      : nullptr;
+    void* hrow = drow ? pool_host_get(std::max<size_t>(np, 1) * 4, "tvm_match_vulns(row ends)", msg) : nullptr;
+    st->pinned = hrow ? pool_host_get(n_alloc, "tvm_match_vulns(csr)", msg) : nullptr;
+    hipStream_t s2 = e->eng->stream();
+    bool ok = st->pinned && order_locked(e, b, static_cast<uint32_t*>(dcsr), static_cast<uint32_t*>(drow), total, msg);
+    ok = ok && (total == 0 || hipMemcpyAsync(st->pinned, dcsr, total * 4, hipMemcpyDeviceToHost, s2) == hipSuccess) &&
+         (np == 0 || hipMemcpyAsync(hrow, drow, np * 4, hipMemcpyDeviceToHost, s2) == hipSuccess) &&
+         hipStreamSynchronize(s2) == hipSuccess;
+    if (ok) expand_rows(static_cast<const uint32_t*>(hrow), np, b->dev.pkg_base, st->pkg);
+    if (dcsr) pool_device_put(e->device, dcsr);
+    if (drow) pool_device_put(e->device, drow);
+    if (hrow) pool_host_put(hrow);
+    if (!ok) {
+      set_err(err, errlen, "tvm_match_vulns: " + (msg.empty() ? std::string("device copy failed") : msg));
+      return TVM_EDEVICE;
+    }
+    st->rec = static_cast<uint32_t*>(st->pinned);
+  }
+  set_out(e->db, st.release(), total, out);
+  return TVM_OK;
+}
+
+int tvm_pipeline_vulns(tvm_engine* e, tvm_batch* b, tvm_vuln_set* out, char* err, size_t errlen) {
+  if (!e || !b || !out || !b->pipe || b->pipe_total > b->pipe->cap()) return TVM_EINVAL;
+  memset(out, 0, sizeof(*out));
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e)) {
+    set_err(err, errlen, kStale);
+    return TVM_EINVAL;
+  }
+  if (batch_has_redhat(b, e->eng->db())) {
+    set_err(err, errlen, "tvm_pipeline_vulns: Red Hat packages are merged per CVE on the device-resident path "
+                         "(tvm_batch_upload + tvm_match_launch + tvm_match_vulns)");
+    return TVM_EINVAL;
+  }
+  templates(e->db);
+  const uint64_t total = b->pipe_total;
+  auto st = std::make_unique<VulnSetStore>();
+  const size_t n_alloc = std::max<uint64_t>(total, 1) * 4;
+  st->pkg = static_cast<uint32_t*>(pool_heap_get(n_alloc));
+  st->rec = st->pkg ? static_cast<uint32_t*>(pool_heap_get(n_alloc)) : nullptr;
+  if (!st->rec) {
+    set_err(err, errlen, "tvm_pipeline_vulns: out of host memory");
+    return TVM_EDEVICE;
+  }
+  const uint32_t* row_end = b->pipe->row_end();
+  const size_t np = b->hb.pk.size();
+  const bool three = b->pipe->packed();
+  const uint8_t* raw = reinterpret_cast<const uint8_t*>(b->pipe->adv());
+  // one pass over the result as it arrived: package column from the row ends, record =
+  // advisory (3-byte indices widened on the way)
+  pool_range_for(np, 1 << 14, [&](size_t a, size_t z) {
+    uint32_t at = a ? row_end[a - 1] : 0;
+    for (size_t p = a; p < z; p++) {
+      const uint32_t end = row_end[p];
+      for (; at < end; at++) {
+        st->pkg[at] = uint32_t(p) + b->pkg_base;
+        st->rec[at] = three ? uint32_t(raw[3 * size_t(at)]) | uint32_t(raw[3 * size_t(at) + 1]) << 8 |
+                                  uint32_t(raw[3 * size_t(at) + 2]) << 16
+                            : reinterpret_cast<const uint32_t*>(raw)[at];
+      }
+    }
+  });
+  set_out(e->db, st.release(), total, out);
+  return TVM_OK;
+}
+
+void tvm_vuln_set_free(tvm_vuln_set* s) {
+  if (!s) return;
+  delete static_cast<VulnSetStore*>(s->priv);
+  memset(s, 0, sizeof(*s));
+}
+
+int tvm_batch_report_get(const tvm_batch* b, uint64_t first, uint64_t n, tvm_str* names, tvm_str* versions,
+                         tvm_str* paths) {
+  const uint64_t size = b ? b->hb.pk.size() : 0;
+  if (!b || first > size || n > size - first) return TVM_EINVAL;
+  const char* arena = reinterpret_cast<const char*>(b->hb.arena.data());
+  uint64_t off = n ? b->hb.name_off(first) : 0;
+  for (uint64_t i = first; i < first + n; i++) {
+    const uint32_t nl = b->hb.pk[i].y & 0xFFFFu, vl = b->hb.pk[i].y >> 16;
+    auto rep = [&](int f, tvm_str dflt) {
+      if (i < b->rep_has[f].size() && b->rep_has[f][i]) return tvm_str{b->rep[f][i].data(), b->rep[f][i].size()};
+      return dflt;
+    };
+    if (names) names[i - first] = rep(0, tvm_str{nullptr, 0});
+    if (versions) versions[i - first] = rep(1, tvm_str{arena + off + nl, vl});
+    if (paths) paths[i - first] = rep(2, tvm_str{nullptr, 0});
+    off += nl + vl;
+  }
   return TVM_OK;
 }
 

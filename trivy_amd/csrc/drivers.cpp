@@ -289,6 +289,40 @@ enum : uint32_t {
   F_ARCH = 32,        // package arch attribute (rocky)
 };
 
+// Per-driver flags of the table drivers (the drivers map below and the batch export).
+uint32_t table_flags(uint8_t drv) {
+  switch (drv) {
+    case DRV_DEBIAN: return F_PKGID | F_CUSTOM | F_DEBIAN;
+    case DRV_ALMA: return F_PKGID | F_CUSTOM | F_RPM_STRING;
+    case DRV_ROCKY: return F_PKGID | F_CUSTOM | F_RPM_STRING | F_ARCH;
+    case DRV_ORACLE: return F_PKGID | F_CUSTOM | F_KSPLICE;
+    case DRV_MARINER: return F_RPM_STRING;  // mariner.go:50-57: no PkgID, no Custom
+    default: return F_PKGID | F_CUSTOM;     // ubuntu, amazon, alpine, wolfi, chainguard, suse, photon
+  }
+}
+
+// The advisory side of a table driver's DetectedVulnerability (e.g. debian.go:78-98,
+// alma.go:64-71): everything but the package fields (PkgID / PkgName / InstalledVersion),
+// which the caller sets from its package.
+void table_epilogue(uint32_t flags, const Advisory& a, Vuln& v) {
+  v.copy = COPY_PKG_NAME | COPY_IDENTIFIER | COPY_LAYER | ((flags & F_PKGID) ? COPY_PKG_ID : 0);
+  v.vuln_id = a.vuln_id;
+  v.data_source = a.data_source;
+  if (flags & F_CUSTOM) {
+    v.has_custom = !a.custom.empty();
+    v.custom = a.custom;
+  }
+  v.fixed = (flags & F_RPM_STRING) && !a.fixed.empty() ? rpm_string(a.fixed) : a.fixed;
+  if (flags & F_DEBIAN) {
+    v.vendor_ids = a.vendor_ids;
+    v.status = int32_t(a.status);
+    if (a.severity != 0) {  // debian.go:92-98 package-specific severity
+      v.severity_source = "debian";
+      v.severity = severity_name(a.severity);
+    }
+  }
+}
+
 struct Spec {
   std::function<std::string(std::string_view os_ver, const Repo* repo, int64_t now)> bucket;
   NameSel name;
@@ -340,28 +374,12 @@ class TableDriver : public OsDriver {
     }
     for (const uint2& m : pairs) {
       const Pkg& p = pkgs[m.x];
-      const Advisory& a = db.advs[m.y];
       Vuln v;
       v.pkg = m.x;
-      v.copy = COPY_PKG_NAME | COPY_IDENTIFIER | COPY_LAYER | ((s_.flags & F_PKGID) ? COPY_PKG_ID : 0);
-      v.vuln_id = a.vuln_id;
-      v.data_source = a.data_source;
-      if (s_.flags & F_CUSTOM) {
-        v.has_custom = !a.custom.empty();
-        v.custom = a.custom;
-      }
+      table_epilogue(s_.flags, db.advs[m.y], v);
       if (s_.flags & F_PKGID) v.pkg_id = std::string(p.id);
       v.pkg_name = std::string(p.name);
       v.installed = format_version(p.epoch, p.version, p.release);
-      v.fixed = (s_.flags & F_RPM_STRING) && !a.fixed.empty() ? rpm_string(a.fixed) : a.fixed;
-      if (s_.flags & F_DEBIAN) {
-        v.vendor_ids = a.vendor_ids;
-        v.status = int32_t(a.status);
-        if (a.severity != 0) {  // debian.go:92-98 package-specific severity
-          v.severity_source = "debian";
-          v.severity = severity_name(a.severity);
-        }
-      }
       out.push_back(std::move(v));
     }
     return true;
@@ -501,49 +519,49 @@ const OsDriver* find_os_driver(std::string_view family) {
     std::map<std::string, std::unique_ptr<OsDriver>, std::less<>> m;
     auto add = [&](const char* fam, Spec s) { m[fam] = std::make_unique<TableDriver>(std::move(s)); };
     add("debian", {[](std::string_view v, const Repo*, int64_t) { return "debian " + os_major(v); }, NAME_SRC, VER_SRC,
-                   F_PKGID | F_CUSTOM | F_DEBIAN, "failed to get debian advisories: ", nullptr,
+                   table_flags(DRV_DEBIAN), "failed to get debian advisories: ", nullptr,
                    eol_of(debian_eol, os_major_s)});
     add("ubuntu", {[](std::string_view v, const Repo*, int64_t now) { return "ubuntu " + ubuntu_release(v, now); },
-                   NAME_SRC, VER_SRC, F_PKGID | F_CUSTOM, "failed to get Ubuntu advisories: ", nullptr,
+                   NAME_SRC, VER_SRC, table_flags(DRV_UBUNTU), "failed to get Ubuntu advisories: ", nullptr,
                    eol_of(ubuntu_eol, nullptr)});
     add("amazon", {[](std::string_view v, const Repo*, int64_t) { return "amazon linux " + amazon_release(v); },
-                   NAME_BIN, VER_BIN, F_PKGID | F_CUSTOM, "failed to get amazon advisories: ", nullptr,
+                   NAME_BIN, VER_BIN, table_flags(DRV_AMAZON), "failed to get amazon advisories: ", nullptr,
                    eol_of(amazon_eol, amazon_release_s)});
     add("alpine", {[](std::string_view v, const Repo* r, int64_t) { return "alpine " + alpine_stream(v, r); },
-                   NAME_SRC_OR_BIN, VER_SRC, F_PKGID | F_CUSTOM, "failed to get alpine advisories: ", nullptr,
+                   NAME_SRC_OR_BIN, VER_SRC, table_flags(DRV_ALPINE), "failed to get alpine advisories: ", nullptr,
                    eol_of(alpine_eol, os_minor_s)});
     add("wolfi", {[](std::string_view, const Repo*, int64_t) { return std::string("wolfi"); }, NAME_SRC_OR_BIN,
-                  VER_BIN, F_PKGID | F_CUSTOM, "failed to get Wolfi advisories: ", nullptr, always});
+                  VER_BIN, table_flags(DRV_WOLFI), "failed to get Wolfi advisories: ", nullptr, always});
     add("chainguard", {[](std::string_view, const Repo*, int64_t) { return std::string("chainguard"); },
-                       NAME_SRC_OR_BIN, VER_BIN, F_PKGID | F_CUSTOM, "failed to get Chainguard advisories: ", nullptr,
+                       NAME_SRC_OR_BIN, VER_BIN, table_flags(DRV_CHAINGUARD), "failed to get Chainguard advisories: ", nullptr,
                        always});
     add("alma", {[](std::string_view v, const Repo*, int64_t) { return "alma " + os_major(v); }, NAME_MODULAR, VER_BIN,
-                 F_PKGID | F_CUSTOM | F_RPM_STRING, "failed to get AlmaLinux advisories: ",
+                 table_flags(DRV_ALMA), "failed to get AlmaLinux advisories: ",
                  [](const Pkg& p) {  // alma.go:53-57
                    return p.release.find(".module_el") != std::string_view::npos && p.modularitylabel.empty();
                  },
                  eol_of(alma_eol, os_major_s)});
     add("rocky", {[](std::string_view v, const Repo*, int64_t) { return "rocky " + os_major(v); }, NAME_MODULAR,
-                  VER_BIN, F_PKGID | F_CUSTOM | F_RPM_STRING | F_ARCH, "failed to get Rocky Linux advisories: ",
+                  VER_BIN, table_flags(DRV_ROCKY), "failed to get Rocky Linux advisories: ",
                   [](const Pkg& p) { return !p.modularitylabel.empty(); },  // rocky.go:52-56
                   eol_of(rocky_eol, os_major_s)});
     add("oracle", {[](std::string_view v, const Repo*, int64_t) { return "Oracle Linux " + os_major(v); }, NAME_BIN,
-                   VER_BIN, F_PKGID | F_CUSTOM | F_KSPLICE, "failed to get Oracle Linux advisory: ", nullptr,
+                   VER_BIN, table_flags(DRV_ORACLE), "failed to get Oracle Linux advisory: ", nullptr,
                    eol_of(oracle_eol, os_major_s)});
     add("opensuse.leap", {[](std::string_view v, const Repo*, int64_t) { return "openSUSE Leap " + std::string(v); },
-                          NAME_BIN, VER_BIN, F_PKGID | F_CUSTOM,
+                          NAME_BIN, VER_BIN, table_flags(DRV_SUSE),
                           "failed to get SUSE advisory: failed to get SUSE advisories: ", nullptr,
                           eol_of(opensuse_eol, nullptr)});
     add("suse linux enterprise server",
         {[](std::string_view v, const Repo*, int64_t) { return "SUSE Linux Enterprise " + std::string(v); }, NAME_BIN,
-         VER_BIN, F_PKGID | F_CUSTOM, "failed to get SUSE advisory: failed to get SUSE advisories: ", nullptr,
+         VER_BIN, table_flags(DRV_SUSE), "failed to get SUSE advisory: failed to get SUSE advisories: ", nullptr,
          eol_of(sles_eol, nullptr)});
     add("photon", {[](std::string_view v, const Repo*, int64_t) { return "Photon OS " + std::string(v); }, NAME_SRC,
-                   VER_BIN, F_PKGID | F_CUSTOM,
+                   VER_BIN, table_flags(DRV_PHOTON),
                    "failed to get Photon Linux advisory: failed to get Photon advisories: ", nullptr,
                    eol_of(photon_eol, nullptr)});
     add("cbl-mariner", {[](std::string_view v, const Repo*, int64_t) { return "CBL-Mariner " + os_minor(v); },
-                        NAME_SRC, VER_SRC, F_RPM_STRING, "failed to get CBL-Mariner advisories: ", nullptr, always});
+                        NAME_SRC, VER_SRC, table_flags(DRV_MARINER), "failed to get CBL-Mariner advisories: ", nullptr, always});
     m["redhat"] = std::make_unique<RedHat>();
     m["centos"] = std::make_unique<RedHat>();
     return m;
@@ -609,6 +627,15 @@ std::string normalize_pkg_name(std::string_view eco, std::string_view name) {
 
 namespace {
 
+// The advisory side of the library driver's DetectedVulnerability (driver.go:125-132;
+// library.Detect adds Layer / PkgIdentifier / PkgPath, detect.go:33-37 when wrap).
+void library_epilogue(bool wrap, const Advisory& a, Vuln& v) {
+  v.copy = COPY_PKG_ID | COPY_PKG_NAME | (wrap ? COPY_IDENTIFIER | COPY_LAYER : 0);
+  v.vuln_id = a.vuln_id;
+  v.fixed = a.lib_fixed;
+  v.data_source = a.data_source;
+}
+
 DetectStatus library_run(Engine& eng, std::string_view lib_type, const std::vector<Pkg>& pkgs, bool wrap,
                          std::vector<Vuln>& out, std::string& err) {
   const char* eco = library_ecosystem(lib_type);
@@ -633,16 +660,12 @@ DetectStatus library_run(Engine& eng, std::string_view lib_type, const std::vect
   }
   for (const uint2& m : pairs) {
     const Pkg& p = pkgs[m.x];
-    const Advisory& a = db.advs[m.y];
     Vuln v;
     v.pkg = m.x;
-    v.copy = COPY_PKG_ID | COPY_PKG_NAME | (wrap ? COPY_IDENTIFIER | COPY_LAYER : 0);
-    v.vuln_id = a.vuln_id;
+    library_epilogue(wrap, db.advs[m.y], v);
     v.pkg_id = std::string(p.id);
     v.pkg_name = std::string(p.name);
     v.installed = std::string(p.version);
-    v.fixed = a.lib_fixed;
-    v.data_source = a.data_source;
     if (wrap) v.pkg_path = std::string(p.file_path);  // detect.go:33-37
     out.push_back(std::move(v));
   }
@@ -724,6 +747,37 @@ std::vector<uint32_t> redhat_fixed_ranks(const DB& db) {
     rank[keys[i].second] = r;
   }
   return rank;
+}
+
+// The advisory side of the Red Hat driver's DetectedVulnerability for a group of one member
+// (redhat.go:140-171: Status and Severity of the member; VendorIDs and the rpm String()
+// FixedVersion only when it is fixed; no DataSource, no Custom).
+void redhat_member_epilogue(const Advisory& a, Vuln& v) {
+  v.copy = COPY_PKG_ID | COPY_PKG_NAME | COPY_IDENTIFIER | COPY_LAYER;
+  v.vuln_id = a.vuln_id;
+  v.status = int32_t(a.status);
+  v.severity_source = "redhat";
+  v.severity = severity_name(a.severity);
+  if (!a.fixed.empty()) {
+    v.vendor_ids = a.vendor_ids;
+    v.fixed = rpm_string(a.fixed);
+  }
+}
+
+void advisory_templates(const DB& db, std::vector<Vuln>& out) {
+  std::vector<uint8_t> drv(db.advs.size(), DRV_NONE);
+  for (const Key& k : db.keys)
+    if (k.plat < db.plats.size())
+      for (uint32_t a : k.advs) drv[a] = db.plats[k.plat].drv;
+  out.assign(db.advs.size(), Vuln());
+  for (size_t i = 0; i < db.advs.size(); i++) {
+    const Advisory& a = db.advs[i];
+    Vuln& v = out[i];
+    v.pkg = 0;
+    if (drv[i] == DRV_LIBRARY) library_epilogue(true, a, v);
+    else if (drv[i] == DRV_REDHAT) redhat_member_epilogue(a, v);
+    else table_epilogue(table_flags(drv[i]), a, v);
+  }
 }
 
 void redhat_batch_vulns(const DB& db, const HostBatch& hb, const std::vector<RhRec>& recs,

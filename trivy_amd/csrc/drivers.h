@@ -91,6 +91,12 @@ struct RhRec;
 std::vector<uint32_t> redhat_fixed_ranks(const DB& db);
 void redhat_batch_vulns(const DB& db, const HostBatch& hb, const std::vector<RhRec>& recs,
                         const std::vector<uint32_t>& contrib, uint32_t pkg_base, std::vector<Vuln>& out);
+// The advisory side of every advisory's DetectedVulnerability as its driver's epilogue
+// populates it (out[adv]; table drivers: table_flags of the advisory's platform, library:
+// library.Detect's fields, Red Hat: a merged group of that one member).  The package fields
+// (PkgID / PkgName / InstalledVersion / PkgPath) are left empty: the batch export pairs these
+// templates with the package of each match.
+void advisory_templates(const DB& db, std::vector<Vuln>& out);
 // vulnerability.NormalizePkgName (trivy-db): pip names lower-cased, "_" -> "-".
 std::string normalize_pkg_name(std::string_view eco, std::string_view name);
 

@@ -141,33 +141,10 @@ struct CopyOutArgs {
   uint64_t adv_units = 0;             // 16-byte units of adv_h
   uint64_t row_end_units = 0;         // 16-byte units of row_end_h
   unsigned long long* ctl = nullptr;  // the pass's control block: ctl[3] |= ERR_BOUNDS on a guard hit
-  // delta form (instead of the CSR; delta_form.h): tile t's byte stream at stream_h +
-  // delta_region(t, b), its {matches, stream bytes} at tile_info_h[t]
-  uint32_t delta = 0;
-  uint8_t* stream_h = nullptr;
-  uint64_t stream_units = 0;          // 16-byte units of stream_h
-  uint2* tile_info_h = nullptr;
-  uint32_t block_move = 0;            // 1: the CSR move a workgroup per tile (round 3) instead of a wave per tile
-  // byte form (byte_form.h): one byte per match at its CSR position in adv_h, the high 16 bits
-  // of each package's first advisory at hi_h[package], escaped values at wide_h[position]
-  uint32_t byte_form = 0;
-  uint16_t* hi_h = nullptr;
-  uint32_t* wide_h = nullptr;
 };
-constexpr uint32_t kDeltaStage = 2080;  // copy_out_tiles' delta staging bytes: header + one chunk's worst case + a carried unit
 constexpr uint32_t kCopyRunMax = kTile;  // tiles per prefix segment of the wave-per-tile move
-// copy_out_tiles' LDS: counts + scratch + delta staging (workgroup per tile), or the run's
-// tile offsets + a 256-entry count array per wave (wave per tile)
-constexpr uint32_t kCopyLdsWordsBlock = kTile + 8 + kDeltaStage / 4;
-constexpr uint32_t kCopyLdsWordsWave = 2 * kCopyRunMax + 8 + (kTile / 64) * kTile;
-constexpr uint32_t kCopyLdsWords = kCopyLdsWordsBlock > kCopyLdsWordsWave ? kCopyLdsWordsBlock : kCopyLdsWordsWave;
-
-// The delta result form: tile t's stream starts at this (16-byte aligned) byte of the stream
-// buffer, b = the CSR position of the tile's first match.  Consecutive tiles' starts are at
-// least 273 + 5 * count bytes apart, more than a stream of `count` matches can take (256
-// count bytes + at most 4 bytes per match + 4 per package of 255 or more + the last unit).
-__host__ __device__ inline uint64_t delta_region(uint32_t t, uint64_t b) { return ((288ull * t + 5ull * b) >> 4) << 4; }
-inline uint64_t delta_stream_bytes(uint32_t n_tiles, uint64_t cap) { return 288ull * n_tiles + 5ull * cap + 64; }
+// copy_out_tiles' LDS: the run's tile offsets + a 256-entry count array per wave
+constexpr uint32_t kCopyLdsWords = 2 * kCopyRunMax + 8 + (kTile / 64) * kTile;
 constexpr uint32_t kCopyWorkgroups = 256;      // workgroups of a result move
 
 // Exclusive block scan of v; tot = the block's sum.  red: kTile / 64 words of LDS.
@@ -193,80 +170,6 @@ __device__ __forceinline__ uint32_t copy_block_scan(uint32_t v, uint32_t* red, u
   return pre + x - v;
 }
 
-// Tile t's matches [base, base + count) as its delta stream (delta_form.h): 256 count bytes
-// (255: the count follows as 4 bytes at the start of the package's list), then per package
-// with matches its first advisory as 3 bytes and every next one as the byte difference from
-// the one before (1..255), or 0 + 3 bytes when it does not fit.  Assembled in LDS (sb) one
-// chunk of 256 matches at a time and stored to the pinned stream in whole 16-byte units.
-// cnt: the tile's per-package counts; returns the stream's bytes.
-__device__ __forceinline__ uint32_t copy_out_delta(const CopyOutArgs& a, uint32_t t, uint64_t b, const TileDir& d,
-                                                   uint32_t p_first, const uint32_t* cnt, uint32_t* red, uint8_t* sb) {
-  const uint32_t tid = threadIdx.x;
-  const uint64_t u0 = delta_region(t, b) >> 4;
-  uint4* dst = reinterpret_cast<uint4*>(a.stream_h);
-  const uint32_t c = cnt[tid];
-  sb[tid] = uint8_t(c < 255u ? c : 255u);
-  uint32_t fill = kTile;  // bytes staged
-  uint64_t done = 0;      // units stored
-  bool bad = false;
-  auto flush = [&](uint32_t units) {
-    for (uint32_t u = tid; u < units; u += kTile) {
-      if (u0 + done + u < a.stream_units)
-        dst[u0 + done + u] = reinterpret_cast<const uint4*>(sb)[u];
-      else
-        bad = true;
-    }
-  };
-  for (uint32_t i0 = 0; i0 < d.count; i0 += kTile) {
-    const uint32_t i = i0 + tid;
-    uint32_t sz = 0, ad = 0, q = 0, pc = 0;
-    bool first = false;
-    if (i < d.count) {
-      const uint32_t pk = a.pkg[d.base + i];
-      ad = a.adv[d.base + i];
-      first = i == 0 || a.pkg[d.base + i - 1] != pk;
-      if (first) {
-        pc = cnt[(pk - a.pkg_base - p_first) & (kTile - 1)];
-        sz = pc >= 255u ? 7u : 3u;
-      } else {
-        q = ad - a.adv[d.base + i - 1];
-        sz = q - 1u < 255u ? 1u : 4u;
-      }
-    }
-    uint32_t tot;
-    uint8_t* o = sb + fill + copy_block_scan(sz, red, tid, tot);
-    if (sz == 1) {
-      o[0] = uint8_t(q);
-    } else if (sz) {
-      if (sz == 7) {
-        o[0] = uint8_t(pc), o[1] = uint8_t(pc >> 8), o[2] = uint8_t(pc >> 16), o[3] = uint8_t(pc >> 24);
-        o += 4;
-      } else if (!first) {
-        *o++ = 0;  // escape: an absolute index follows
-      }
-      o[0] = uint8_t(ad), o[1] = uint8_t(ad >> 8), o[2] = uint8_t(ad >> 16);
-    }
-    fill += tot;
-    __syncthreads();
-    const uint32_t full = fill >> 4, rem = fill & 15u;
-    flush(full);
-    const uint8_t keep = tid < rem ? sb[16 * full + tid] : uint8_t(0);
-    __syncthreads();
-    if (tid < rem) sb[tid] = keep;
-    done += full;
-    fill = rem;
-    __syncthreads();
-  }
-  // the rest: the header of a tile with fewer matches than one chunk's worth of units, the
-  // last partial unit (zero padded)
-  const uint32_t units = (fill + 15u) >> 4;
-  if (tid < units * 16u && tid >= fill) sb[tid] = 0;
-  __syncthreads();
-  flush(units);
-  if (bad) atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
-  return uint32_t(done * 16 + fill);
-}
-
 __device__ __forceinline__ uint32_t copy_block_sum(uint32_t v, uint32_t* red, uint32_t tid) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -277,213 +180,6 @@ __device__ __forceinline__ uint32_t copy_block_sum(uint32_t v, uint32_t* red, ui
 #pragma unroll
   for (int w = 0; w < kTile / 64; w++) s += red[w];
   return s;
-}
-
-// Workgroup `wg` of `n_wg` moves a contiguous run of the chunk's tiles, one tile after the
-// other (measured, DESIGN.md §7: one workgroup per tile moved the chunk slower, at 36 GB/s
-// beside the match tiles against 40 GB/s here).  lds: kCopyLdsWords words of the caller's
-// shared memory (the match kernel lends its staging buffer).
-__device__ __forceinline__ void copy_out_tiles_block(const CopyOutArgs& a, uint32_t wg, uint32_t n_wg, uint32_t* lds) {
-  uint32_t* cnt = lds;
-  uint32_t* red = lds + kTile;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t nt = a.t1 - a.t0;
-  const uint32_t r0 = a.t0 + uint32_t(uint64_t(nt) * wg / n_wg), r1 = a.t0 + uint32_t(uint64_t(nt) * (wg + 1) / n_wg);
-  uint32_t pre = 0;  // counts of the chunk's tiles before the run (a pass's total fits 32 bits: cap < 2^32)
-  for (uint32_t u = a.t0 + tid; u < r0; u += kTile) pre += a.dir[u].count;
-  unsigned long long b = a.chunk_base[a.c] + copy_block_sum(pre, red, tid);
-  for (uint32_t t = r0; t < r1; t++) {
-    const TileDir d = a.dir[t];
-    cnt[tid] = 0;
-    __syncthreads();
-    const bool fits = d.base + d.count <= a.cap && b + d.count <= a.cap;
-    const uint32_t p_first = t * kTile;
-    if (fits)
-      for (uint32_t i0 = 0; i0 < d.count; i0 += 4 * kTile) {  // four loads in flight per lane
-        uint32_t q[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const uint32_t i = i0 + u * kTile + tid;
-          q[u] = i < d.count ? a.pkg[d.base + i] - a.pkg_base - p_first : kTile;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-          if (q[u] < kTile) atomicAdd(&cnt[q[u]], 1u);
-      }
-    __syncthreads();
-    if (a.delta) {  // the delta form: the counts go into the stream's header, no row ends
-      uint32_t bytes = 0;
-      if (fits && d.count)
-        bytes = copy_out_delta(a, t, b, d, p_first, cnt, red, reinterpret_cast<uint8_t*>(lds + kTile + 8));
-      if (tid == 0) a.tile_info_h[t] = make_uint2(d.count, bytes);
-      b += d.count;
-      __syncthreads();  // cnt is rewritten by the next tile
-      continue;
-    }
-    uint32_t x = cnt[tid];
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o, 64);
-      if (lane >= uint32_t(o)) x += y;
-    }
-    if (lane == 63) red[wave] = x;
-    __syncthreads();
-    for (uint32_t w = 0; w < wave; w++) x += red[w];
-    cnt[tid] = uint32_t(b) + x;  // row end of package p_first + tid (row ends are 32-bit)
-    __syncthreads();
-    if (tid < kTile / 4) {
-      if (p_first / 4 + tid < a.row_end_units)
-        reinterpret_cast<uint4*>(a.row_end_h)[p_first / 4 + tid] = reinterpret_cast<const uint4*>(cnt)[tid];
-      else
-        atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
-    }
-    if (a.packed) {  // 3 bytes per advisory: destination bytes [3b, 3(b + count)) in 16-byte units
-      const uint64_t B0 = 3 * b, B1 = 3 * (b + d.count), U0 = B0 >> 4;
-      uint64_t nu = fits ? ((B1 + 15) >> 4) - U0 : 0;
-      if (nu && U0 + nu > a.adv_units) {  // guard: never expected (adv_h holds 4 * cap bytes; an overflowed tile moves nothing)
-        if (tid == 0) atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
-        nu = 0;
-      }
-      uint8_t* dst = reinterpret_cast<uint8_t*>(a.adv_h);
-      constexpr int kP = 2;
-      for (uint64_t j0 = 0; j0 < nu; j0 += uint64_t(kP) * kTile) {
-        uint32_t id[kP][6];
-#pragma unroll
-        for (int k = 0; k < kP; k++) {
-          const uint64_t j = j0 + uint64_t(k) * kTile + tid, g0 = ((U0 + j) * 16) / 3;
-#pragma unroll
-          for (int t = 0; t < 6; t++) {
-            const int64_t i = int64_t(g0 + t) - int64_t(b);  // segment index of the unit's t-th advisory
-            id[k][t] = (j < nu && i >= 0 && i < int64_t(d.count)) ? a.adv[d.base + uint64_t(i)] : 0u;
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < kP; k++) {
-          const uint64_t j = j0 + uint64_t(k) * kTile + tid;
-          if (j >= nu) continue;
-          const uint64_t G0 = (U0 + j) * 16, g0 = G0 / 3;
-          const uint32_t r = uint32_t(G0 - g0 * 3);  // byte of advisory g0 the unit starts at
-          uint32_t wv[4] = {0, 0, 0, 0};
-#pragma unroll
-          for (int q = 0; q < 16; q++) {
-            const uint32_t t = (r + q) / 3, kb = (r + q) % 3;
-            wv[q >> 2] |= ((id[k][t] >> (8 * kb)) & 0xFFu) << (8 * (q & 3));
-          }
-          if (G0 >= B0 && G0 + 16 <= B1) {
-            reinterpret_cast<uint4*>(dst)[U0 + j] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-          } else {  // a unit shared with a neighbour tile: its own bytes only
-#pragma unroll
-            for (int q = 0; q < 16; q++)
-              if (G0 + q >= B0 && G0 + q < B1) dst[G0 + q] = uint8_t(wv[q >> 2] >> (8 * (q & 3)));
-          }
-        }
-      }
-      b += d.count;
-      __syncthreads();  // cnt is rewritten by the next tile
-      continue;
-    }
-    // the segment, realigned in registers to the destination's 16-byte units
-    const uint64_t u0 = b >> 2;
-    uint64_t nu = fits ? ((b + d.count + 3) >> 2) - u0 : 0;
-    if (nu && u0 + nu > a.adv_units) {  // guard: never expected
-      if (tid == 0) atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
-      nu = 0;
-    }
-    const uint32_t sh = uint32_t(b & 3);
-    constexpr int kU = 4;
-    for (uint64_t j0 = 0; j0 < nu; j0 += uint64_t(kU) * kTile) {
-      uint32_t v[kU][4];
-#pragma unroll
-      for (int k = 0; k < kU; k++) {
-        const uint64_t j = j0 + uint64_t(k) * kTile + tid;
-#pragma unroll
-        for (int w = 0; w < 4; w++) {
-          const int64_t i = int64_t(j * 4 + w) - int64_t(sh);  // segment index of the unit's word w
-          v[k][w] = (j < nu && i >= 0 && i < int64_t(d.count)) ? a.adv[d.base + uint64_t(i)] : 0u;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < kU; k++) {
-        const uint64_t j = j0 + uint64_t(k) * kTile + tid;
-        if (j >= nu) continue;
-        const int64_t i0 = int64_t(j * 4) - int64_t(sh);
-        if (i0 >= 0 && i0 + 4 <= int64_t(d.count)) {
-          reinterpret_cast<uint4*>(a.adv_h)[u0 + j] = make_uint4(v[k][0], v[k][1], v[k][2], v[k][3]);
-        } else {  // the segment's first or last unit, shared with a neighbour tile: its own words only
-#pragma unroll
-          for (int w = 0; w < 4; w++)
-            if (i0 + w >= 0 && i0 + w < int64_t(d.count)) a.adv_h[(u0 + j) * 4 + w] = v[k][w];
-        }
-      }
-    }
-    b += d.count;
-    __syncthreads();  // cnt is rewritten by the next tile
-  }
-  if (wg == n_wg - 1 && tid == 0) a.chunk_base[a.c + 1] = b;
-}
-
-// The byte form of one tile's segment (byte_form.h), by one wave: match i of the segment is
-// the byte at CSR position b + i - the low byte of its advisory index when it is its
-// package's first (the package's high 16 bits go to hi_h[package]), else the difference
-// from the one before when that is 1..254, else 0xFF with the index at wide_h[b + i].  Each
-// lane assembles four consecutive bytes (one destination word) from the five advisories they
-// depend on; hw: the wave's 256 high halves (LDS), stored once per tile as 512 bytes.
-__device__ __forceinline__ void copy_out_tile_bytes(const CopyOutArgs& a, const TileDir& d, bool fits, uint64_t b,
-                                                    uint32_t p_first, uint32_t lane, uint16_t* hw) {
-  // hw overlays the counts the caller has read: every lane's read before any lane's write
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  reinterpret_cast<uint2*>(hw)[lane] = make_uint2(0, 0);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  const uint64_t w0 = b >> 2;
-  const uint32_t sh = uint32_t(b & 3);
-  uint64_t nw = fits && d.count ? ((b + d.count + 3) >> 2) - w0 : 0;
-  if (nw && w0 + nw > a.adv_units * 4) {  // guard: never expected (adv_h holds cap + 16 bytes)
-    if (lane == 0) atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
-    nw = 0;
-  }
-  for (uint64_t j = lane; j < nw; j += 64) {
-    const int64_t i0 = int64_t(j * 4) - int64_t(sh);  // segment index of the word's first byte
-    uint32_t pk[5], ad[5];
-#pragma unroll
-    for (int k = 0; k < 5; k++) {  // matches i0 - 1 .. i0 + 3
-      const int64_t i = i0 - 1 + k;
-      const bool in = i >= 0 && i < int64_t(d.count);
-      pk[k] = in ? a.pkg[d.base + uint64_t(i)] : 0xFFFFFFFFu;
-      ad[k] = in ? a.adv[d.base + uint64_t(i)] : 0u;
-    }
-    uint32_t word = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int64_t i = i0 + k;
-      if (i < 0 || i >= int64_t(d.count)) continue;
-      const bool first = pk[k] != pk[k + 1];  // i == 0 reads pk[k] = none
-      const uint32_t q = ad[k + 1] - ad[k];
-      uint32_t v;
-      if (first) {
-        v = ad[k + 1] & 0xFFu;
-        hw[(pk[k + 1] - a.pkg_base - p_first) & (kTile - 1)] = uint16_t(ad[k + 1] >> 8);
-      } else if (q - 1u < 254u) {
-        v = q;
-      } else {
-        v = 0xFFu;
-        a.wide_h[b + uint64_t(i)] = ad[k + 1];
-      }
-      word |= v << (8 * k);
-    }
-    if (i0 >= 0 && i0 + 4 <= int64_t(d.count)) {
-      a.adv_h[w0 + j] = word;
-    } else {  // the segment's first or last word, shared with a neighbour tile: its own bytes only
-      uint8_t* dst = reinterpret_cast<uint8_t*>(a.adv_h) + (w0 + j) * 4;
-#pragma unroll
-      for (int k = 0; k < 4; k++)
-        if (i0 + k >= 0 && i0 + k < int64_t(d.count)) dst[k] = uint8_t(word >> (8 * k));
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  reinterpret_cast<uint2*>(a.hi_h)[(p_first >> 2) + lane] = reinterpret_cast<const uint2*>(hw)[lane];
 }
 
 // One tile's CSR move by one wave (lane of 64): its per-package counts in the wave's own LDS
@@ -525,10 +221,6 @@ __device__ __forceinline__ void copy_out_tile_wave(const CopyOutArgs& a, uint32_
     reinterpret_cast<uint4*>(a.row_end_h)[p_first / 4 + lane] = make_uint4(e + s0, e + s1, e + s2, e + s3);
   else
     atomicOr(a.ctl + 3, (unsigned long long)ERR_BOUNDS);
-  if (a.byte_form) {
-    copy_out_tile_bytes(a, d, fits, b, p_first, lane, reinterpret_cast<uint16_t*>(cw));
-    return;
-  }
   if (a.packed) {  // 3 bytes per advisory: destination bytes [3b, 3(b + count)) in 16-byte units
     const uint64_t B0 = 3 * b, B1 = 3 * (b + d.count), U0 = B0 >> 4;
     uint64_t nu = fits && d.count ? ((B1 + 15) >> 4) - U0 : 0;
@@ -611,12 +303,8 @@ __device__ __forceinline__ void copy_out_tile_wave(const CopyOutArgs& a, uint32_
 // the run's tiles from one block scan per 256 tiles, then each wave moves every fourth tile
 // on its own (round 4: a workgroup per tile in turn waited on its count pass, scan and move
 // one tile at a time; the kernel trace showed each 1M-package chunk's move taking ~450 us
-// beside 180 us of matching).  The delta form keeps the workgroup-per-tile encoder.
+// beside 180 us of matching).
 __device__ __forceinline__ void copy_out_tiles(const CopyOutArgs& a, uint32_t wg, uint32_t n_wg, uint32_t* lds) {
-  if (a.delta || a.block_move) {
-    copy_out_tiles_block(a, wg, n_wg, lds);
-    return;
-  }
   unsigned long long* pre = reinterpret_cast<unsigned long long*>(lds);  // kCopyRunMax offsets
   uint32_t* red = lds + 2 * kCopyRunMax;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;

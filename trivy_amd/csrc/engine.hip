@@ -452,13 +452,7 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
         const char* v = std::getenv("TVM_COPY_WG");
         return v ? uint32_t(std::max(1, std::atoi(v))) : 128u;
       }();
-      // the delta form's encode is latency-bound per tile (a block scan per 256 matches), not
-      // link-bound: more workgroups (TVM_COPY_WG_DELTA overrides it for measurement)
-      static const uint32_t n_copy_delta = [] {
-        const char* v = std::getenv("TVM_COPY_WG_DELTA");
-        return v ? uint32_t(std::max(1, std::atoi(v))) : 128u;
-      }();
-      fa.n_copy = co->delta ? n_copy_delta : n_copy;
+      fa.n_copy = n_copy;
     }
     const FusedFn fn = fused_fn(b.gm, vi);
     if (!fn) {

@@ -64,19 +64,35 @@ inline void par_memcpy(void* dst, const void* src, size_t bytes) {
 }
 
 // A process-wide pool of host_threads() - 1 parked threads for work that recurs many times
-// per call (the pipeline's per-chunk result decode: spawning threads per chunk cost more than
-// the decode).  One job at a time; the caller takes part.
+// per call (the pipeline's per-chunk staging copies: spawning threads per chunk cost more than
+// the copies).  One job at a time; the caller takes part.  shutdown() (tvm_shutdown) joins the
+// threads before the HIP runtime and the C++ runtime tear down; later jobs run on the caller.
 class WorkerPool {
  public:
   static WorkerPool& get() {
-    static WorkerPool* p = new WorkerPool(host_threads());  // never destroyed: its threads stay parked
+    std::lock_guard<std::mutex> g(inst_mu());
+    WorkerPool*& p = inst();
+    if (!p) p = new WorkerPool(host_threads());  // never destroyed: shutdown() stops its threads
     return *p;
+  }
+  // Joins the threads of the pool if one exists (idempotent).
+  static void shutdown_all() {
+    WorkerPool* p;
+    {
+      std::lock_guard<std::mutex> g(inst_mu());
+      p = inst();
+    }
+    if (p) p->shutdown();
   }
   int size() const { return n_ + 1; }
   // f(i) for i in [0, n), handed out one at a time
   void parallel_for(size_t n, const std::function<void(size_t)>& f) {
     if (n == 0) return;
     std::lock_guard<std::mutex> one(job_mu_);
+    if (stopped_) {
+      for (size_t i = 0; i < n; i++) f(i);
+      return;
+    }
     {
       std::lock_guard<std::mutex> lk(mu_);
       job_ = &f;
@@ -91,10 +107,31 @@ class WorkerPool {
     done_cv_.wait(lk, [&] { return busy_ == 0; });
     job_ = nullptr;
   }
+  void shutdown() {
+    std::lock_guard<std::mutex> one(job_mu_);  // no job in flight
+    if (stopped_) return;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+      gen_++;
+    }
+    cv_.notify_all();
+    for (std::thread& t : th_) t.join();
+    th_.clear();
+    stopped_ = true;
+  }
 
  private:
   explicit WorkerPool(int threads) : n_(std::max(0, threads - 1)) {
-    for (int i = 0; i < n_; i++) std::thread([this] { loop(); }).detach();
+    for (int i = 0; i < n_; i++) th_.emplace_back([this] { loop(); });
+  }
+  static std::mutex& inst_mu() {
+    static std::mutex* m = new std::mutex();
+    return *m;
+  }
+  static WorkerPool*& inst() {
+    static WorkerPool* p = nullptr;
+    return p;
   }
   void work() {
     for (size_t i; (i = next_.fetch_add(1, std::memory_order_relaxed)) < total_;) (*job_)(i);
@@ -106,6 +143,7 @@ class WorkerPool {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return gen_ != seen; });
         seen = gen_;
+        if (stop_) return;
       }
       work();
       std::lock_guard<std::mutex> lk(mu_);
@@ -113,6 +151,7 @@ class WorkerPool {
     }
   }
   const int n_;
+  std::vector<std::thread> th_;
   std::mutex job_mu_, mu_;
   std::condition_variable cv_, done_cv_;
   const std::function<void(size_t)>* job_ = nullptr;
@@ -120,6 +159,16 @@ class WorkerPool {
   std::atomic<size_t> next_{0};
   int busy_ = 0;
   uint64_t gen_ = 0;
+  bool stop_ = false, stopped_ = false;
 };
+
+// range_for on the parked WorkerPool threads (no thread start per call: the batch export's
+// loops run a few milliseconds each).  Not from inside another WorkerPool job.
+template <class F>
+void pool_range_for(size_t n, size_t grain, F&& f) {
+  WorkerPool& wp = WorkerPool::get();
+  const size_t pieces = std::max<size_t>(1, std::min<size_t>(size_t(wp.size()) * 4, n / std::max<size_t>(grain, 1)));
+  wp.parallel_for(pieces, [&](size_t k) { f(n * k / pieces, n * (k + 1) / pieces); });
+}
 
 }  // namespace tvm

@@ -870,7 +870,11 @@ __global__ __launch_bounds__(kTile) void sweep_kernel(SweepArgs a) {
 // the version encoder, bit 1 the index probe, bit 2 the sweep.
 // STG: LDS bytes for the tile's string window (smaller: more tiles resident per CU, more
 // windows read from global memory instead).
-template <uint32_t GM, int K, int MB, int FILT, int DIAG = 0, int WPE = 1, int SEG = 0, uint32_t STG = kStage>
+// MOVE: the launch carries the previous pipeline chunk's result move (fa.n_copy workgroups).
+// Device-resident launches instantiate without it: copy_out_tiles inlined into the match
+// kernel cost registers (44 -> 52 VGPRs) and ~10 % of C2's time even where it never ran.
+template <uint32_t GM, int K, int MB, int FILT, int DIAG = 0, int WPE = 1, int SEG = 0, uint32_t STG = kStage,
+          bool MOVE = false>
 __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
   constexpr uint32_t kStageVec = STG / 16 + 8;  // + two zero words per wave window (per-wave staging)
   constexpr uint32_t kMbufVec = (MB * 5 + 15) / 16;
@@ -893,13 +897,15 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
   SweepShared<FILT>& s = u.sw.s;
   uint8_t* map = u.sw.map;
   const ProbeArgs& a = fa.pa;
-  if (blockIdx.x < fa.n_copy) {  // pipeline: the previous chunk's result move, dispatched first so the link writes overlap the tiles
-    static_assert(sizeof(buf) >= kCopyLdsWords * 4, "the result move borrows the staging buffer");
-    __builtin_amdgcn_s_setprio(3);  // its waves issue ahead of the match waves sharing the CU: the link is the bound
-    copy_out_tiles(fa.co, blockIdx.x, fa.n_copy, reinterpret_cast<uint32_t*>(buf));
-    return;
+  if constexpr (MOVE) {
+    if (blockIdx.x < fa.n_copy) {  // pipeline: the previous chunk's result move, dispatched first so the link writes overlap the tiles
+      static_assert(sizeof(buf) >= kCopyLdsWords * 4, "the result move borrows the staging buffer");
+      __builtin_amdgcn_s_setprio(3);  // its waves issue ahead of the match waves sharing the CU: the link is the bound
+      copy_out_tiles(fa.co, blockIdx.x, fa.n_copy, reinterpret_cast<uint32_t*>(buf));
+      return;
+    }
   }
-  const uint32_t tid = threadIdx.x, t = blockIdx.x - fa.n_copy;
+  const uint32_t tid = threadIdx.x, t = blockIdx.x - (MOVE ? fa.n_copy : 0u);
   const uint32_t p = t * kTile + tid;
   uint2 d = make_uint2(0xFFFFFFFFu, 0);
   if (p < a.n) d = a.pk[p];
@@ -961,7 +967,11 @@ void launch_sweep(uint32_t n_tiles, hipStream_t st, const SweepArgs& a) {
 
 template <uint32_t GM, int K, int MB, int FILT, int DIAG = 0, int WPE = 1, int SEG = 0, uint32_t STG = kStage>
 void launch_fused(uint32_t n_tiles, hipStream_t st, const FusedArgs& a) {
-  hipLaunchKernelGGL((fused_kernel<GM, K, MB, FILT, DIAG, WPE, SEG, STG>), dim3(n_tiles + a.n_copy), dim3(kTile), 0, st, a);
+  if (a.n_copy)
+    hipLaunchKernelGGL((fused_kernel<GM, K, MB, FILT, DIAG, WPE, SEG, STG, true>), dim3(n_tiles + a.n_copy), dim3(kTile), 0,
+                       st, a);
+  else
+    hipLaunchKernelGGL((fused_kernel<GM, K, MB, FILT, DIAG, WPE, SEG, STG, false>), dim3(n_tiles), dim3(kTile), 0, st, a);
 }
 
 // Table entry of variant (F, K, MB) for grammar set GM / row-filter level FILT

@@ -85,7 +85,7 @@ __global__ __launch_bounds__(kTile) void order_kernel(OrderArgs a) {
 }
 
 __global__ __launch_bounds__(kTile) void copy_out_kernel(CopyOutArgs a) {
-  __shared__ uint4 lds[kCopyLdsWords / 4];  // 16-byte aligned: the delta staging is read as units
+  __shared__ uint4 lds[kCopyLdsWords / 4];
   copy_out_tiles(a, blockIdx.x, gridDim.x, reinterpret_cast<uint32_t*>(lds));
 }
 

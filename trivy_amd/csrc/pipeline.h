@@ -24,6 +24,7 @@ struct OrderArgs {
 };
 void launch_order(uint32_t n_tiles, hipStream_t st, const OrderArgs& a);
 void launch_copy_out(hipStream_t st, const CopyOutArgs& a);  // engine.h copy_out_tiles as its own kernel
+void release_encoders();  // the transport-form encoders kept between batches (tvm_shutdown)
 
 
 // One batch's pipeline state.  prepare() builds the batch's pinned transport form (or a
@@ -43,25 +44,16 @@ class Pipeline {
  public:
   ~Pipeline();
   // transport: send the batch in its transport form when it has one (see build_wire)
-  // packed: the result's advisory indices travel as 3 bytes each (the DB has < 2^24);
-  // delta (implies packed): the result travels in the delta form (delta_form.h) and run()
-  // decodes it into the CSR on the host threads chunk by chunk, overlapping the GPU
-  // byte (implies packed): the byte form (byte_form.h), decoded by run() like the delta form
+  // packed: the result's advisory indices travel as 3 bytes each (the DB has < 2^24)
   bool prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uint32_t chunk_packages, bool transport,
-               bool packed, bool delta, bool byte, std::string& err);
+               bool packed, std::string& err);
   // One pass.  total = matches (> match_cap: nothing valid, re-prepare with a larger cap);
   // err_pkg = first poisoned package or -1.
   bool run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& err_pkg, uint64_t& err_bits, std::string& err);
-  // 4-byte indices (the decoded CSR for the delta / byte forms), or 3-byte ones when packed()
-  const uint32_t* adv() const { return (delta_ || byte_) ? csr_h_ : adv_h_; }
+  // 4-byte indices, or 3-byte ones when packed()
+  const uint32_t* adv() const { return adv_h_; }
   bool packed() const { return packed_; }
   const uint32_t* row_end() const { return row_end_h_; }
-  bool delta() const { return delta_; }
-  bool byte_form() const { return byte_; }
-  // the delta form of the last pass: the streams and the per-tile {count, bytes}
-  const uint8_t* delta_stream() const { return stream_h_; }
-  uint64_t delta_stream_size() const { return stream_bytes_; }
-  const uint2* delta_tiles() const { return tile_info_h_; }
   uint32_t n_tiles() const { return bounds_.empty() ? 0 : bounds_.back(); }
   uint64_t cap() const { return cap_; }
   uint64_t h2d_bytes() const { return h2d_; }
@@ -109,22 +101,6 @@ class Pipeline {
   uint64_t wire_bytes_ = 0;                       // size of wire_h_ / wire_d_
   uint64_t adv_units_ = 0, row_end_units_ = 0;    // 16-byte units of adv_h_ / row_end_h_ (guards)
   bool prepared_ = false;
-  bool delta_ = false;
-  uint8_t* stream_h_ = nullptr;  // delta form (pinned) and the device addresses the result move stores through
-  uint8_t* stream_hd_ = nullptr;
-  uint64_t stream_bytes_ = 0;
-  uint2* tile_info_h_ = nullptr;
-  uint2* tile_info_hd_ = nullptr;
-  std::vector<uint64_t> tile_pos_;  // CSR position of each tile's first match (the decode)
-  uint32_t* csr_h_ = nullptr;       // delta / byte forms: the decoded advisory indices (pageable, pool_heap_get)
-  bool byte_ = false;               // the byte form: bytes / high halves / escapes (pinned, device-mapped)
-  uint8_t* bytes_h_ = nullptr;
-  uint8_t* bytes_hd_ = nullptr;
-  uint16_t* hi_h_ = nullptr;
-  uint16_t* hi_hd_ = nullptr;
-  uint32_t* wide_h_ = nullptr;
-  uint32_t* wide_hd_ = nullptr;
-  std::vector<hipEvent_t> ev_d_;    // chunk's row ends landed (the byte form's decode waits on it)
   bool packed_ = false;  // no Engine pointer: the batch may outlive a hot swap (the C-ABI checks the generation)
 };
 

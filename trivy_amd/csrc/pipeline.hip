@@ -2,8 +2,6 @@
 // and the order kernel's direct writes of the result into host memory overlap chunk by chunk.  Every buffer is sized once in prepare(); a pass
 // allocates nothing.
 #include "pipeline.h"
-#include "byte_form.h"
-#include "delta_form.h"
 #include "host_par.h"
 #include "pool.h"
 #include "wire.h"
@@ -124,6 +122,11 @@ static WireEncoder* take_encoder() {
   return e;
 }
 
+void release_encoders() {
+  std::lock_guard<std::mutex> lk(enc_mu());
+  enc_pool().clear();
+}
+
 static void give_encoder(WireEncoder* e) {
   e->clear();
   std::lock_guard<std::mutex> lk(enc_mu());
@@ -211,22 +214,8 @@ void Pipeline::release() {
                   static_cast<void*>(row_end_d_)})
     pool_device_put(dev_, p);
   for (void* p : {static_cast<void*>(wire_h_), static_cast<void*>(raw_h_), static_cast<void*>(adv_h_),
-                  static_cast<void*>(row_end_h_), static_cast<void*>(ctl_h_), static_cast<void*>(stream_h_),
-                  static_cast<void*>(tile_info_h_), static_cast<void*>(bytes_h_), static_cast<void*>(hi_h_),
-                  static_cast<void*>(wide_h_)})
+                  static_cast<void*>(row_end_h_), static_cast<void*>(ctl_h_)})
     pool_host_put(p);
-  pool_heap_put(csr_h_);
-  csr_h_ = nullptr;
-  bytes_h_ = bytes_hd_ = nullptr;
-  hi_h_ = hi_hd_ = nullptr;
-  wide_h_ = wide_hd_ = nullptr;
-  byte_ = false;
-  for (hipEvent_t e : ev_d_) (void)hipEventDestroy(e);
-  ev_d_.clear();
-  stream_h_ = stream_hd_ = nullptr;
-  tile_info_h_ = tile_info_hd_ = nullptr;
-  stream_bytes_ = 0;
-  delta_ = false;
   wire_h_ = nullptr;
   raw_h_ = nullptr;
   wire_bytes_ = 0;
@@ -251,7 +240,7 @@ void Pipeline::release() {
 }
 
 bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uint32_t chunk_packages, bool transport,
-                       bool packed, bool delta, bool byte, std::string& err) {
+                       bool packed, std::string& err) {
   release();
   const auto start = std::chrono::steady_clock::now();
   dev_ = eng.device();
@@ -284,9 +273,7 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
   toff_ = hb.tile_off;  // per 64-package group, + the arena end, padded to whole tiles
   toff_.resize(size_t(n_tiles) * kGroupsPerTile + 1, hb.arena.size());
   cap_ = std::max<uint64_t>(match_cap, 1);
-  packed_ = packed || delta || byte;
-  delta_ = delta;
-  byte_ = byte && !delta;
+  packed_ = packed;
   if (cap_ >= (1ull << 32)) {
     err = "pipeline: row ends are 32-bit; split the batch below 2^32 matches";
     return false;
@@ -297,11 +284,6 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
     if (!ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate", err)) return false;
   for (hipEvent_t& e : ev_h_)
     if (!ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate", err)) return false;
-  if (byte_) {
-    ev_d_.resize(nc);
-    for (hipEvent_t& e : ev_d_)
-      if (!ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate", err)) return false;
-  }
   if (!ok(hipStreamCreateWithFlags(&s_h2d_, hipStreamNonBlocking), "hipStreamCreate", err) ||
       !ok(hipStreamCreateWithFlags(&s_d2h_, hipStreamNonBlocking), "hipStreamCreate", err) ||
       !ok(hipStreamCreateWithFlags(&s_k_, hipStreamNonBlocking), "hipStreamCreate", err))
@@ -325,65 +307,19 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
   void* p = nullptr;
   if (!(p = pool_device_get(dev_, (size_t(nc) + 1) * 8, "hipMalloc(chunk bases)", err))) return false;
   chunk_base_d_ = static_cast<unsigned long long*>(p);
-  if (delta_) {  // the delta form: streams + tile info, written by the result move; no CSR buffers
-    stream_bytes_ = delta_stream_bytes(n_tiles, cap_);
-    if (!(p = pool_host_get(stream_bytes_, "hipHostMalloc(delta streams)", err))) return false;
-    stream_h_ = static_cast<uint8_t*>(p);
-    if (!ok(hipHostGetDevicePointer(&p, stream_h_, 0), "hipHostGetDevicePointer(delta streams)", err)) return false;
-    stream_hd_ = static_cast<uint8_t*>(p);
-    if (!(p = pool_host_get((size_t(n_tiles) + 2) * sizeof(uint2), "hipHostMalloc(tile info)", err))) return false;
-    tile_info_h_ = static_cast<uint2*>(p);
-    if (!ok(hipHostGetDevicePointer(&p, tile_info_h_, 0), "hipHostGetDevicePointer(tile info)", err)) return false;
-    tile_info_hd_ = static_cast<uint2*>(p);
-    // the CSR the pass decodes the streams into, chunk by chunk (pooled: a fresh batch of a
-    // size seen before touches no new pages)
-    const size_t cap4 = (cap_ + 3) & ~size_t(3), n4 = (size_t(n_tiles) * kTile + 3) & ~size_t(3);
-    if (!(csr_h_ = static_cast<uint32_t*>(pool_heap_get(cap4 * 4)))) {
-      err = "pipeline: host memory for the decoded result";
-      return false;
-    }
-    if (!(p = pool_host_get(std::max<size_t>(n4, 4) * 4, "hipHostMalloc(row ends)", err))) return false;
-    row_end_h_ = static_cast<uint32_t*>(p);
-    tile_pos_.assign(size_t(n_tiles) + 1, 0);
-    if (!(p = pool_host_get(64, "hipHostMalloc(ctl)", err))) return false;
-    ctl_h_ = static_cast<unsigned long long*>(p);
-    prepared_ = true;
-    prepare_us_ = uint64_t(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - start).count());
-    return true;
-  }
   // the result lives in pinned host memory that the result move writes directly over PCIe
   // (measured, profiles/r03/pcie_probe.txt: kernel stores to host memory 55 GB/s, a DMA
   // device-to-host copy 28.6 GB/s; the DMA engine then only carries the batch upward)
-  if (!byte_) {  // (the byte form has its own arrays, below)
-    if (!(p = pool_host_get(cap4 * 4, "hipHostMalloc(adv)", err))) return false;
-    adv_h_ = static_cast<uint32_t*>(p);
-    if (!ok(hipHostGetDevicePointer(&p, adv_h_, 0), "hipHostGetDevicePointer(adv)", err)) return false;
-    adv_hd_ = static_cast<uint32_t*>(p);
-  }
+  if (!(p = pool_host_get(cap4 * 4, "hipHostMalloc(adv)", err))) return false;
+  adv_h_ = static_cast<uint32_t*>(p);
+  if (!ok(hipHostGetDevicePointer(&p, adv_h_, 0), "hipHostGetDevicePointer(adv)", err)) return false;
+  adv_hd_ = static_cast<uint32_t*>(p);
   if (!(p = pool_host_get(std::max<size_t>(n4, 4) * 4, "hipHostMalloc(row ends)", err))) return false;
   row_end_h_ = static_cast<uint32_t*>(p);
   if (!ok(hipHostGetDevicePointer(&p, row_end_h_, 0), "hipHostGetDevicePointer(row ends)", err)) return false;
   row_end_hd_ = static_cast<uint32_t*>(p);
   if (!(p = pool_device_get(dev_, std::max<size_t>(n4, 4) * 4, "hipMalloc(row ends)", err))) return false;
   row_end_d_ = static_cast<uint32_t*>(p);
-  if (byte_) {  // the byte form's three arrays, written by the result move; csr_h_ holds the decoded CSR
-    if (!(p = pool_host_get(cap4 + 64, "hipHostMalloc(bytes)", err))) return false;
-    bytes_h_ = static_cast<uint8_t*>(p);
-    if (!ok(hipHostGetDevicePointer(&p, bytes_h_, 0), "hipHostGetDevicePointer(bytes)", err)) return false;
-    bytes_hd_ = static_cast<uint8_t*>(p);
-    if (!(p = pool_host_get(std::max<size_t>(n4, 4) * 2, "hipHostMalloc(high halves)", err))) return false;
-    hi_h_ = static_cast<uint16_t*>(p);
-    if (!ok(hipHostGetDevicePointer(&p, hi_h_, 0), "hipHostGetDevicePointer(high halves)", err)) return false;
-    hi_hd_ = static_cast<uint16_t*>(p);
-    if (!(p = pool_host_get(cap4 * 4, "hipHostMalloc(escapes)", err))) return false;
-    wide_h_ = static_cast<uint32_t*>(p);
-    if (!ok(hipHostGetDevicePointer(&p, wide_h_, 0), "hipHostGetDevicePointer(escapes)", err)) return false;
-    wide_hd_ = static_cast<uint32_t*>(p);
-    if (!(csr_h_ = static_cast<uint32_t*>(pool_heap_get(cap4 * 4)))) {
-      err = "pipeline: host memory for the decoded result";
-      return false;
-    }
-  }
   if (!(p = pool_host_get(64, "hipHostMalloc(ctl)", err))) return false;
   ctl_h_ = static_cast<unsigned long long*>(p);
   prepared_ = true;
@@ -413,19 +349,14 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
   // calls never block); the host waits once, at the end.
   // the result move leaves the row ends in HBM and the DMA engine carries them up on a third
   // stream while the kernels store the advisories (measured: 3.32 -> 3.20 ms per C2 pass; the
-  // kernel stores alone reach 36-40 GB/s beside the match tiles)
-  // TVM_PIPE_ROWEND_STORE=1 (measurement): the result move stores the row ends too, so no
-  // device-to-host DMA shares the copy engines with the uploads
-  static const bool rowend_store = std::getenv("TVM_PIPE_ROWEND_STORE") != nullptr;
-  // TVM_COPY_BLOCK=1 (measurement): the round-3 result move, a workgroup per tile
-  static const bool block_move = std::getenv("TVM_COPY_BLOCK") != nullptr;
-  const bool rowend_dma = !delta_ && !rowend_store;
+  // kernel stores alone reach 36-40 GB/s beside the match tiles; the row ends stored by the
+  // move too: 2.93 ms against 2.77)
   auto copy_args = [&](uint32_t c) {
     CopyOutArgs ca;
     ca.dir = m_.dir;
     ca.pkg = m_.pkg;
     ca.adv = m_.adv;
-    ca.row_end_h = rowend_dma ? row_end_d_ : row_end_hd_;
+    ca.row_end_h = row_end_d_;
     ca.adv_h = adv_hd_;
     ca.chunk_base = chunk_base_d_;
     ca.c = c;
@@ -437,46 +368,20 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
     ca.adv_units = adv_units_;
     ca.row_end_units = row_end_units_;
     ca.ctl = m_.ctl;
-    ca.delta = delta_ ? 1u : 0u;
-    ca.stream_h = stream_hd_;
-    ca.stream_units = stream_bytes_ / 16;
-    ca.tile_info_h = tile_info_hd_;
-    ca.block_move = block_move ? 1u : 0u;
-    if (byte_) {
-      ca.byte_form = 1;
-      ca.adv_h = reinterpret_cast<uint32_t*>(bytes_hd_);
-      ca.adv_units = (cap_ + 64) / 16;
-      ca.hi_h = hi_hd_;
-      ca.wide_h = wide_hd_;
-    }
     return ca;
   };
-  // measurement only: TVM_PIPE_TRACE=1 prints the host time spent in each call of a pass;
-  // TVM_PIPE_COPIES_FIRST=1 queues every chunk's upload before any kernel
+  // measurement only: TVM_PIPE_TRACE=1 prints the host time spent in each call of a pass
   static const bool trace = std::getenv("TVM_PIPE_TRACE") != nullptr;
-  static const bool copies_first = std::getenv("TVM_PIPE_COPIES_FIRST") != nullptr;
-  static const bool unpack_on_copy = std::getenv("TVM_PIPE_UNPACK_ON_COPY") != nullptr && !copies_first;
-  // chunk c's result move is done (ev_k_[c]): the DMA engine carries its row ends up (third
-  // stream), or the host decodes its delta streams
+  // chunk c's result move is done (ev_k_[c]): the DMA engine carries its row ends up (third stream)
   auto rowend_up = [&](uint32_t c) {
-    if (!rowend_dma) return ok(hipEventRecord(ev_k_[c], s_k_), "hipEventRecord", err);
     const size_t q0 = size_t(bounds_[c]) * kTile, q1 = size_t(bounds_[c + 1]) * kTile;
     return ok(hipEventRecord(ev_k_[c], s_k_), "hipEventRecord", err) &&
            ok(hipStreamWaitEvent(s_d2h_, ev_k_[c], 0), "hipStreamWaitEvent", err) &&
            ok(hipMemcpyAsync(row_end_h_ + q0, row_end_d_ + q0, (q1 - q0) * 4, hipMemcpyDeviceToHost, s_d2h_),
-              "D2H row ends", err) &&
-           (!byte_ || ok(hipEventRecord(ev_d_[c], s_d2h_), "hipEventRecord", err));
+              "D2H row ends", err);
   };
   const auto T0 = std::chrono::steady_clock::now();
   auto us = [&]() { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - T0).count(); };
-  if (copies_first && !wc_.empty())
-    for (uint32_t c = 0; c < nc; c++) {
-      const WireChunk& w = wc_[c];
-      if (!ok(hipMemcpyAsync(wire_d_ + w.off, wire_h_ + w.off, w.bytes, hipMemcpyHostToDevice, s_h2d_), "H2D chunk", err) ||
-          !ok(hipEventRecord(ev_h_[c], s_h2d_), "hipEventRecord", err))
-        return false;
-      if (trace) std::fprintf(stderr, "pipe c%u copy queued %.1f us\n", c, us());
-    }
   int64_t prev = -1;  // the last chunk matched, whose result has not been moved yet
   for (uint32_t c = 0; c < nc; c++) {
     const uint32_t t0 = bounds_[c], t1 = bounds_[c + 1];
@@ -507,21 +412,12 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
       ua.wire_cap = wire_bytes_;
       ua.ctl = m_.ctl;
       h2d_ += w.bytes;
-      if (!copies_first &&
-          !ok(hipMemcpyAsync(wire_d_ + w.off, wire_h_ + w.off, w.bytes, hipMemcpyHostToDevice, s_h2d_), "H2D chunk", err))
+      if (!ok(hipMemcpyAsync(wire_d_ + w.off, wire_h_ + w.off, w.bytes, hipMemcpyHostToDevice, s_h2d_), "H2D chunk", err) ||
+          !ok(hipEventRecord(ev_h_[c], s_h2d_), "hipEventRecord", err) ||
+          !ok(hipStreamWaitEvent(s_k_, ev_h_[c], 0), "hipStreamWaitEvent", err))
         return false;
-      if (unpack_on_copy) {  // behind its own upload: it runs while the kernel stream is still on chunk c-1
-        hipLaunchKernelGGL(unpack_kernel, dim3((w.groups + 3) / 4), dim3(256), 0, s_h2d_, ua);
-        if (!ok(hipGetLastError(), "unpack kernel launch", err) || !ok(hipEventRecord(ev_h_[c], s_h2d_), "hipEventRecord", err) ||
-            !ok(hipStreamWaitEvent(s_k_, ev_h_[c], 0), "hipStreamWaitEvent", err))
-          return false;
-      } else {
-        if ((!copies_first && !ok(hipEventRecord(ev_h_[c], s_h2d_), "hipEventRecord", err)) ||
-            !ok(hipStreamWaitEvent(s_k_, ev_h_[c], 0), "hipStreamWaitEvent", err))
-          return false;
-        hipLaunchKernelGGL(unpack_kernel, dim3((w.groups + 3) / 4), dim3(256), 0, s_k_, ua);
-        if (!ok(hipGetLastError(), "unpack kernel launch", err)) return false;
-      }
+      hipLaunchKernelGGL(unpack_kernel, dim3((w.groups + 3) / 4), dim3(256), 0, s_k_, ua);
+      if (!ok(hipGetLastError(), "unpack kernel launch", err)) return false;
       if (trace) std::fprintf(stderr, "pipe c%u upload + unpack queued %.1f us\n", c, us());
     } else if ((!raw_staged_ && (stage_chunk(hb, p0, p1, g0, g1, a0, a1), false)) ||
         !ok(hipMemcpyAsync(db_.pk + p0, raw_pk_ + p0, (p1 - p0) * sizeof(uint2), hipMemcpyHostToDevice, s_h2d_),
@@ -552,74 +448,9 @@ bool Pipeline::run(Engine& eng, const HostBatch& hb, uint64_t& total, int64_t& e
   }
   if (!ok(hipMemcpyAsync(ctl_h_, m_.ctl, 64, hipMemcpyDeviceToHost, s_k_), "D2H ctl", err)) return false;
   if (trace) std::fprintf(stderr, "pipe ctl queued %.1f us\n", us());
-  // the delta form: the host threads decode each chunk's streams into the CSR as soon as its
-  // result move is done, while the GPU works on the chunks after it
-  bool decoded = true;
-  static const bool no_decode = std::getenv("TVM_PIPE_NODECODE") != nullptr;  // measurement only: the bytes alone
-  uint64_t escapes = 0;
-  if (byte_ && !no_decode) {  // each chunk decoded once its move and its row ends have landed
-    for (uint32_t c = 0; c < nc; c++) {
-      const uint32_t t0 = bounds_[c], t1 = bounds_[c + 1];
-      if (t1 == t0) continue;
-      if (!ok(hipEventSynchronize(ev_d_[c]), "pipeline", err)) return false;
-      if (trace) std::fprintf(stderr, "pipe c%u moved %.1f us\n", c, us());
-      if (row_end_h_[size_t(t1) * kTile - 1] > cap_) {  // an overflowed pass: the total says so below
-        decoded = false;
-        break;
-      }
-      std::atomic<uint64_t> esc{0};
-      constexpr uint32_t kPiece = 16;  // tiles per work item
-      WorkerPool::get().parallel_for((t1 - t0 + kPiece - 1) / kPiece, [&](size_t k) {
-        const uint32_t a0 = t0 + uint32_t(k) * kPiece, a1 = std::min(t1, a0 + kPiece);
-        uint64_t e = 0;
-        for (uint32_t t = a0; t < a1; t++) e += byte_decode_tile(bytes_h_, hi_h_, wide_h_, row_end_h_, t, csr_h_);
-        esc += e;
-      });
-      escapes += esc;
-      if (trace) std::fprintf(stderr, "pipe c%u decoded %.1f us\n", c, us());
-    }
-  }
-  if (delta_ && !no_decode) {
-    uint64_t pos = 0;
-    for (uint32_t c = 0; c < nc && decoded; c++) {
-      const uint32_t t0 = bounds_[c], t1 = bounds_[c + 1];
-      if (t1 == t0) continue;
-      if (!ok(hipEventSynchronize(ev_k_[c]), "pipeline", err)) return false;
-      if (trace) std::fprintf(stderr, "pipe c%u moved %.1f us\n", c, us());
-      for (uint32_t t = t0; t < t1; t++) {
-        tile_pos_[t] = pos;
-        pos += tile_info_h_[t].x;
-      }
-      if (pos > cap_) {  // an overflowed pass: its streams are incomplete, the total says so below
-        decoded = false;
-        break;
-      }
-      std::atomic<bool> bad{false};
-      constexpr uint32_t kPiece = 16;  // tiles per work item
-      WorkerPool::get().parallel_for((t1 - t0 + kPiece - 1) / kPiece, [&](size_t k) {
-        const uint32_t a0 = t0 + uint32_t(k) * kPiece, a1 = std::min(t1, a0 + kPiece);
-        for (uint32_t t = a0; t < a1; t++)
-          if (!delta_decode_tile(stream_h_, stream_bytes_, t, tile_pos_[t], tile_info_h_[t], csr_h_, row_end_h_))
-            bad = true;
-      });
-      if (bad) decoded = false;
-      if (trace) std::fprintf(stderr, "pipe c%u decoded %.1f us\n", c, us());
-    }
-  }
   if (!ok(hipStreamSynchronize(s_k_), "pipeline", err) || !ok(hipStreamSynchronize(s_d2h_), "pipeline", err)) return false;
   if (trace) std::fprintf(stderr, "pipe done %.1f us\n", us());
-  if (delta_) {
-    d2h_ = 0;
-    for (uint32_t t = 0; t < n_tiles(); t++) d2h_ += sizeof(uint2) + ((tile_info_h_[t].y + 15) & ~15u);
-  } else if (byte_) {  // bytes + high halves + row ends + escapes
-    d2h_ = std::min<uint64_t>(ctl_h_[0], cap_) + uint64_t(n_tiles()) * kTile * 2 + uint64_t(n) * 4 + escapes * 4;
-  } else {
-    d2h_ = uint64_t(n) * 4 + std::min<uint64_t>(ctl_h_[0], cap_) * (packed_ ? 3 : 4);
-  }
-  if ((delta_ || byte_) && !decoded && ctl_h_[0] <= cap_ && !ctl_h_[3] && !ctl_h_[1]) {
-    err = "pipeline: the delta form of the result is inconsistent with the tiles' counts";
-    return false;
-  }
+  d2h_ = uint64_t(n) * 4 + std::min<uint64_t>(ctl_h_[0], cap_) * (packed_ ? 3 : 4);
   total = ctl_h_[0];
   err_pkg = ctl_h_[1] ? int64_t(n - ctl_h_[1]) : -1;
   err_bits = ctl_h_[3];

@@ -34,6 +34,7 @@ struct Pool {
   Kind host;
   Kind heap;  // pageable (pool_heap_*)
   unsigned long long hits = 0, misses = 0;
+  bool closed = false;  // pool_close: blocks put back are freed at once
 };
 
 Pool& pool() {
@@ -109,7 +110,7 @@ void pool_device_put(int device, void* p) {
   }
   k.free_.emplace(it->second, p);
   k.cached += it->second;
-  shrink(k, kKeepDevice, [&](void* q) {
+  shrink(k, P.closed ? 0 : kKeepDevice, [&](void* q) {
     (void)hipSetDevice(device);
     (void)hipFree(q);
   });
@@ -152,7 +153,7 @@ void pool_host_put(void* p) {
   }
   P.host.free_.emplace(it->second, p);
   P.host.cached += it->second;
-  shrink(P.host, kKeepHost, [](void* q) { (void)hipHostFree(q); });
+  shrink(P.host, P.closed ? 0 : kKeepHost, [](void* q) { (void)hipHostFree(q); });
 }
 
 void* pool_heap_get(size_t bytes) {
@@ -182,10 +183,18 @@ void pool_heap_put(void* p) {
   if (it == P.heap.cap_.end()) return;
   P.heap.free_.emplace(it->second, p);
   P.heap.cached += it->second;
-  shrink(P.heap, kKeepHost, [&](void* q) {
+  shrink(P.heap, P.closed ? 0 : kKeepHost, [&](void* q) {
     auto c = P.heap.cap_.find(q);
     huge_free(q, c == P.heap.cap_.end() ? 0 : c->second);
   });
+}
+
+void pool_close() {
+  {
+    std::lock_guard<std::mutex> lk(pool().mu);
+    pool().closed = true;
+  }
+  pool_trim();
 }
 
 void pool_trim() {

@@ -24,6 +24,9 @@ void* pool_heap_get(size_t bytes);
 void pool_heap_put(void* p);
 // Frees every cached block (tests; a process that wants its memory back).
 void pool_trim();
+// pool_trim, and from now on blocks put back are freed at once (tvm_shutdown: nothing of ours
+// may be left for the HIP runtime's own teardown).
+void pool_close();
 // {cached device bytes, cached host bytes, hits, misses}
 void pool_stats(unsigned long long out[4]);
 
