@@ -202,3 +202,39 @@ def test_native_scan_equals_python_scan(name):
     got = ts.scan_native(eng, n, "img", now=NOW)
     n.close()
     assert got == want and any(v for *_, v in got)
+
+
+def _one(purl, props=()):
+    return json.dumps({"bomFormat": "CycloneDX", "components": [
+        {"bom-ref": "os", "type": "operating-system", "name": "centos", "version": "7"},
+        {"bom-ref": "p", "type": "library", "name": "x", "purl": purl,
+         "properties": [{"name": "aquasecurity:trivy:" + k, "value": v} for k, v in props]}],
+        "dependencies": [{"ref": "os", "dependsOn": ["p"]}]})
+
+
+@pytest.mark.parametrize("decode", [_python, _native], ids=["python", "native"])
+def test_go_integer_and_rpm_semantics(decode):
+    """Parity unpinned (no reference test covers these; restated from Go's strconv.Atoi and
+    go-rpm-version): SrcEpoch is strconv.Atoi (decode.go:208-211: no whitespace, a sign, ASCII
+    digits, int64 range; an error fails the decode); the purl epoch qualifier ignores an Atoi
+    error (purl.go:229-233); an rpm purl's version splits at the FIRST '-' (purl.go:238-240, as
+    the comparator does: oracle/rpm.c)."""
+    pkg = lambda text: decode(text)["Packages"][0]  # noqa: E731
+    assert pkg(_one("pkg:rpm/centos/x@1.2-3-4.el7"))["Version"] == "1.2"
+    assert pkg(_one("pkg:rpm/centos/x@1.2-3-4.el7"))["Release"] == "3-4.el7"
+    assert pkg(_one("pkg:rpm/centos/x@2:1.2-3.el7"))["Version"] == "1.2"
+    for bad_epoch in ["+-1", "1 ", "0x1", "١", "9223372036854775808", ""]:
+        assert pkg(_one(f"pkg:rpm/centos/x@1.0-1?epoch={urllib_quote(bad_epoch)}")).get("Epoch", 0) == 0, bad_epoch
+    assert pkg(_one("pkg:rpm/centos/x@1.0-1?epoch=%2B3"))["Epoch"] == 3
+    assert pkg(_one("pkg:rpm/centos/x@1.0-1?epoch=-2"))["Epoch"] == -2
+    assert pkg(_one("pkg:rpm/centos/x@1.0-1", [("SrcEpoch", "9223372036854775807")]))["SrcEpoch"] == (1 << 63) - 1
+    assert pkg(_one("pkg:rpm/centos/x@1.0-1", [("SrcEpoch", "-9223372036854775808")]))["SrcEpoch"] == -(1 << 63)
+    assert pkg(_one("pkg:rpm/centos/x@1.0-1", [("SrcEpoch", "+7")]))["SrcEpoch"] == 7
+    for bad in [" 1", "1 ", "\t1", "9223372036854775808", "1.0", "١", "+", ""]:
+        with pytest.raises(ts.SBOMError, match="invalid src epoch"):
+            decode(_one("pkg:rpm/centos/x@1.0-1", [("SrcEpoch", bad)]))
+
+
+def urllib_quote(s):
+    import urllib.parse
+    return urllib.parse.quote(s, safe="")

@@ -279,9 +279,10 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
       if (mvn_parse(ver, vlen, mp)) {
         const uint32_t need = (kMvnPackedWords * mp.n + 1) / 2;
         const unsigned long long o = atomicAdd(&a.ctl[2], (unsigned long long)need);
-        if (o + need > a.spill_cap) {
+        if (o + need > a.spill_cap) {  // the pass fails (ERR_SPILL); the package keeps no rows
           atomicOr(&a.ctl[3], (unsigned long long)ERR_SPILL);
           valid = false;
+          cnt = rbeg = 0;
         } else {
           mvn_pack(mp, ver, reinterpret_cast<uint32_t*>(a.spill + o));
           off = uint32_t(o);

@@ -413,20 +413,23 @@ bool ascii_digits(std::string_view v) {
   return true;
 }
 
-// Python int() of a property value as trivy_amd/sbom.py applies it (an optional sign, then
-// digits; surrounding whitespace allowed)
-bool py_int(std::string_view v, int64_t& out) {
-  while (!v.empty() && (v.front() == ' ' || v.front() == '\t' || v.front() == '\n')) v.remove_prefix(1);
-  while (!v.empty() && (v.back() == ' ' || v.back() == '\t' || v.back() == '\n')) v.remove_suffix(1);
+// strconv.Atoi (decode.go:209, purl.go:230): an optional sign, then ASCII digits only (no
+// spaces), within int64; false on a syntax or range error
+bool go_atoi(std::string_view v, int64_t& out) {
   bool neg = false;
   if (!v.empty() && (v.front() == '+' || v.front() == '-')) {
     neg = v.front() == '-';
     v.remove_prefix(1);
   }
-  if (!ascii_digits(v) || v.size() > 18) return false;
-  int64_t x = 0;
-  for (char c : v) x = x * 10 + (c - '0');
-  out = neg ? -x : x;
+  if (!ascii_digits(v)) return false;
+  uint64_t x = 0;
+  const uint64_t lim = neg ? (uint64_t(1) << 63) : (uint64_t(1) << 63) - 1;
+  for (char c : v) {
+    const uint64_t d = uint64_t(c - '0');
+    if (x > (lim - d) / 10) return false;
+    x = x * 10 + d;
+  }
+  out = neg ? int64_t(0 - x) : int64_t(x);
   return true;
 }
 
@@ -688,7 +691,7 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err, boo
       }
       if (!R.number(lit)) return false;
       int64_t v = 0;
-      version = py_int(lit, v) ? v : 0;
+      version = go_atoi(lit, v) ? v : 0;
       return true;
     }
     return R.skip();
@@ -832,19 +835,17 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err, boo
         k.modularitylabel = qv;
         k.present |= SP_MODULARITY;
       } else if (qk == "epoch") {
-        std::string_view d = qv;
-        while (!d.empty() && (d.front() == '+' || d.front() == '-')) d.remove_prefix(1);
         int64_t e;
-        if (ascii_digits(d) && py_int(qv, e)) {
+        if (go_atoi(qv, e)) {  // purl.go:229-233: an error leaves Epoch as it is
           k.epoch = e;
           k.present |= SP_EPOCH;
         }
       }
     }
-    if (p.type == "rpm") {  // go-rpm-version: [epoch:]version[-release], the release after the last '-'
+    if (p.type == "rpm") {  // go-rpm-version: [epoch:]version[-release], the release after the FIRST '-' (rpm.c)
       std::string_view v = p.version;
       if (const size_t col = v.find(':'); col != std::string_view::npos) v = v.substr(col + 1);
-      const size_t dash = v.rfind('-');
+      const size_t dash = v.find('-');
       k.version = dash == std::string_view::npos ? v : v.substr(0, dash);
       k.release = dash == std::string_view::npos ? std::string_view() : v.substr(dash + 1);
       k.present |= SP_RELEASE;
@@ -886,7 +887,7 @@ bool decode_cyclonedx(std::string_view text_in, Sbom& out, std::string& err, boo
         k.present |= SP_MODULARITY;
       } else if (pk == "SrcEpoch") {
         int64_t e;
-        if (!py_int(pv, e)) return false;  // "invalid src epoch"
+        if (!go_atoi(pv, e)) return false;  // "invalid src epoch" (decode.go:208-211 strconv.Atoi)
         k.src_epoch = e;
         k.present |= SP_SRCEPOCH;
       } else if (pk == "LayerDigest") {

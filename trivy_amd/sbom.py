@@ -21,6 +21,7 @@ C-ABI).  Host-side JSON work, O(components); it follows:
 """
 import gc
 import json
+import re
 import urllib.parse
 
 NAMESPACE = "aquasecurity:trivy:"
@@ -82,11 +83,24 @@ def purl_class(p):
     return "lang-pkgs" if lang_type(p) else ""
 
 
+def go_atoi(v):
+    """strconv.Atoi: an optional sign, then ASCII digits only (no spaces), within int64; None on
+    error (parity unpinned: restated from Go's strconv, tests/test_sbom.py)."""
+    if not _ATOI.fullmatch(v):
+        return None
+    x = int(v)
+    return x if -(1 << 63) <= x < (1 << 63) else None
+
+
+_ATOI = re.compile(r"[+-]?[0-9]+")
+
+
 def _rpm_split(v):
-    """go-rpm-version NewVersion: [epoch:]version[-release] (the release after the last '-')."""
+    """go-rpm-version NewVersion (purl.go:238-240): [epoch:]version[-release], the release after
+    the FIRST '-' as the comparator splits it (oracle/rpm.c)."""
     if ":" in v:
         v = v.split(":", 1)[1]
-    ver, sep, rel = v.rpartition("-")
+    ver, sep, rel = v.partition("-")
     return (ver, rel) if sep else (v, "")
 
 
@@ -104,8 +118,8 @@ def package_of(p):
             pkg["Arch"] = v
         elif k == "modularitylabel":
             pkg["Modularitylabel"] = v
-        elif k == "epoch" and v.lstrip("+-").isdigit():
-            pkg["Epoch"] = int(v)
+        elif k == "epoch" and go_atoi(v) is not None:  # purl.go:229-233: an error leaves Epoch as it is
+            pkg["Epoch"] = go_atoi(v)
     if p["type"] == "rpm":
         pkg["Version"], pkg["Release"] = _rpm_split(p["version"])
     return pkg
@@ -155,11 +169,11 @@ def _library(c):
             pkg["FilePath"] = v
         elif k in ("SrcName", "SrcVersion", "SrcRelease", "Modularitylabel"):
             pkg[k] = v
-        elif k == "SrcEpoch":
-            try:
-                pkg["SrcEpoch"] = int(v)
-            except ValueError:
+        elif k == "SrcEpoch":  # decode.go:208-211 strconv.Atoi
+            e = go_atoi(v)
+            if e is None:
                 raise SBOMError("failed to decode components: failed to decode library: invalid src epoch")
+            pkg["SrcEpoch"] = e
         elif k == "LayerDigest":
             pkg.setdefault("Layer", {})["Digest"] = v
         elif k == "LayerDiffID":
@@ -188,7 +202,7 @@ def _library(c):
 def _parse_src_version(pkg, typ, ver):
     if typ == "rpm":  # go-rpm-version NewVersion: Atoi(epoch) before the first ':', release after the first '-'
         e, sep, rest = ver.partition(":")
-        epoch, v = (int(e) if e.lstrip("+-").isdigit() else 0, rest) if sep else (0, ver)
+        epoch, v = ((go_atoi(e) or 0), rest) if sep else (0, ver)
         v, _, rel = v.partition("-")
         pkg["SrcEpoch"], pkg["SrcVersion"], pkg["SrcRelease"] = epoch, v, rel
     elif typ == "deb":  # go-deb-version NewVersion; a parse error leaves the package as it is
