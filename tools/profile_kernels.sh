@@ -1,13 +1,13 @@
 #!/bin/bash
-# Round-4 counters for one config (run on the GPU box via gpurun): every kernel of the hot
+# Counters for one config (run on the GPU box via gpurun): every kernel of the hot
 # path with its FillInfo / Red Hat merge / result.Filter legs, not only the match kernel.
 #   CONFIG=c2|c3|c4|c5, EXTRA="bench.py flags", SQ=1 adds the SQ / TCC passes.
-#   out: gpurun_out/r04_<cfg>/{prof_trace,prof_fetch,prof_write,prof_sq,prof_tcc}, pmc_summary.txt
+#   out: gpurun_out/<TAG>_<cfg>/{prof_trace,prof_fetch,prof_write,prof_sq,prof_tcc}, pmc_summary.txt
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 CFG=${CONFIG:-c2}
 EXTRA=${EXTRA:-}
-OUT=$R/gpurun_out/r04_$CFG
+OUT=$R/gpurun_out/${TAG:-prof}_$CFG
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
