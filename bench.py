@@ -483,9 +483,11 @@ def main():
             vs.close()
         vulns = {"ms": sorted(vms)[1], "detected_vulnerabilities": n_v, "merged_group_records": n_grp,
                  "first_call_ms": first_ms,
-                 "is": "tvm_match_vulns after a device-resident pass: (Red Hat per-CVE merge,) order kernel, "
-                       "D2H of the per-package lists, package / record columns on the host threads; records = "
-                       "one per DB advisory built on the first call (first_call_ms) + one per merged Red Hat group"}
+                 "is": "tvm_match_vulns after a device-resident pass: (Red Hat per-CVE merge, group records of "
+                       "several members flagged, scanned and gathered on the device,) the per-package record lists "
+                       "written into pinned host memory by the result move (3-byte indices), the merged groups' "
+                       "records on the host threads; per-advisory records built once per DB on the first call "
+                       "(first_call_ms)"}
         mb.launch(1)
     strong = None
     if world > 1 and not args.gather:  # north_star's multi-GPU path: one global batch, lists gathered at rank 0
@@ -533,7 +535,7 @@ def main():
                          "version string once + per-package references, one DMA per chunk) + the kernel that "
                          "rebuilds each chunk in HBM + match kernels + the per-package advisory lists (CSR) "
                          "written into pinned host memory by the next launch's first workgroups (pass_ms) + "
-                         "tvm_pipeline_vulns: the DetectedVulnerability set (package / record columns) from the "
+                         "tvm_pipeline_vulns: the DetectedVulnerability set (per-package record lists) over the "
                          "result as it arrived (vulns_ms)" + ("" if not has_rh else
                                                              "; Red Hat batches: pass only (the per-CVE merge "
                                                              "runs on the device-resident path, see vulns)"),

@@ -435,15 +435,21 @@ int tvm_match_redhat_merge_time(tvm_engine* e, tvm_batch* b, int steps, double* 
  *     group of several advisories of one VulnerabilityID merged per redhat.go:146-187;
  *   - its package: InstalledVersion and PkgPath of the batch package (tvm_batch_report_get),
  *     PkgID / PkgName / PkgIdentifier / Layer from the caller's own package per copy_flags.
- * Order: by package, then as the driver reports them (advisory order; Red Hat: VulnerabilityID
- * order).  Library-owned; free with tvm_vuln_set_free. */
+ * The set is per-package lists (CSR) of record indices, in pinned memory as the device wrote
+ * them (3-byte indices while the records number below 2^24), so no per-match host pass is
+ * needed to hand it on.  Order: by package, then as the driver reports them (advisory order;
+ * Red Hat: VulnerabilityID order).  Library-owned; free with tvm_vuln_set_free. */
 typedef struct {
-  const uint32_t* pkg;           /* n: batch package index (+ tvm_batch_set_package_base) */
-  const uint32_t* rec;           /* n: record index */
+  const uint32_t* row_end;       /* package first_pkg + p has DetectedVulnerabilities [row_end[p-1], row_end[p])
+                                    (row_end[-1] = 0), p < n_pkgs */
+  size_t n_pkgs;
+  uint32_t first_pkg;            /* batch index of row_end's package 0 (tvm_batch_set_package_base) */
+  const uint8_t* rec;            /* n record indices, rec_width (3 or 4) little-endian bytes each */
+  uint32_t rec_width;
   size_t n;
   const tvm_vuln* adv_recs;      /* one per DB advisory (pkg_index 0; package fields "") */
   size_t n_adv_recs;
-  const tvm_vuln* grp_recs;      /* merged Red Hat groups */
+  const tvm_vuln* grp_recs;      /* merged Red Hat groups: record n_adv_recs + k */
   size_t n_grp_recs;
   void* priv;
 } tvm_vuln_set;
@@ -451,7 +457,8 @@ typedef struct {
  * are merged on the device first (tvm_match_redhat_merge, if it has not run).  TVM_EINVAL when
  * the pass overflowed its match buffer, met an undecodable advisory or flagged an error. */
 int tvm_match_vulns(tvm_engine* e, tvm_batch* b, tvm_vuln_set* out, char* err, size_t errlen);
-/* The same from the last tvm_pipeline_run's result (host CSR; no Red Hat packages). */
+/* The same from the last tvm_pipeline_run's result: the lists that pass left in pinned
+ * memory, no copy (batches without Red Hat packages; valid until the next pass). */
 int tvm_pipeline_vulns(tvm_engine* e, tvm_batch* b, tvm_vuln_set* out, char* err, size_t errlen);
 void tvm_vuln_set_free(tvm_vuln_set* s);
 /* The package side of packages [first, first + n): names = the tvm_batch_set_report PkgName

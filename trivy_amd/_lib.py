@@ -69,7 +69,8 @@ class Vuln(ctypes.Structure):
 
 
 class VulnSet(ctypes.Structure):
-    _fields_ = [("pkg", ctypes.POINTER(ctypes.c_uint32)), ("rec", ctypes.POINTER(ctypes.c_uint32)),
+    _fields_ = [("row_end", ctypes.POINTER(ctypes.c_uint32)), ("n_pkgs", ctypes.c_size_t),
+                ("first_pkg", ctypes.c_uint32), ("rec", ctypes.c_void_p), ("rec_width", ctypes.c_uint32),
                 ("n", ctypes.c_size_t), ("adv_recs", ctypes.POINTER(Vuln)), ("n_adv_recs", ctypes.c_size_t),
                 ("grp_recs", ctypes.POINTER(Vuln)), ("n_grp_recs", ctypes.c_size_t), ("priv", ctypes.c_void_p)]
 

@@ -503,13 +503,23 @@ def vuln_record(v):
 
 
 class VulnSet:
-    """tvm_vuln_set: DetectedVulnerability i = record rec[i] + package pkg[i]."""
+    """tvm_vuln_set: per-package lists (CSR) of record indices; DetectedVulnerability i = record
+    rec[i] + package pkg[i] (the columns are expanded here, numpy)."""
 
     def __init__(self, batch, cset, ms):
         self.batch, self._c, self.ms = batch, cset, ms
-        n = cset.n
-        self.pkg = np.ctypeslib.as_array(cset.pkg, shape=(n,)).copy() if n else np.zeros(0, np.uint32)
-        self.rec = np.ctypeslib.as_array(cset.rec, shape=(n,)).copy() if n else np.zeros(0, np.uint32)
+        n, npk, w = cset.n, cset.n_pkgs, cset.rec_width
+        self.row_end = np.ctypeslib.as_array(cset.row_end, shape=(npk,)).copy() if npk else np.zeros(0, np.uint32)
+        counts = np.diff(np.concatenate([[0], self.row_end.astype(np.int64)]))
+        self.pkg = np.repeat(np.arange(npk, dtype=np.uint32) + np.uint32(cset.first_pkg), counts)
+        if n:
+            raw = np.ctypeslib.as_array((ctypes.c_uint8 * (n * w)).from_address(cset.rec)).reshape(n, w)
+            self.rec = np.zeros(n, np.uint32)
+            for j in range(w):
+                self.rec |= raw[:, j].astype(np.uint32) << np.uint32(8 * j)
+        else:
+            self.rec = np.zeros(0, np.uint32)
+        self.rec_width = w
         self.n_adv_recs, self.n_grp_recs = cset.n_adv_recs, cset.n_grp_recs
         self._recs = {}
 

@@ -16,6 +16,7 @@
 
 #include "db.h"
 #include "drivers.h"
+#include "export.h"
 #include "engine.h"
 #include "libdb.h"
 #include "libver.h"
@@ -1793,20 +1794,13 @@ const VulnTemplates& templates(tvm_db* d) {
   return *d->tmpl;
 }
 
-// The refs of a tvm_vuln_set (heap blocks from the pool: a C2 set holds 20.5M of each) and the
-// merged Red Hat groups' records.
+// What a tvm_vuln_set points into: the export's pinned lists (device-resident path) and the
+// merged Red Hat groups' records; a pipelined pass's set points into its result (no copy).
 struct VulnSetStore {
-  uint32_t* pkg = nullptr;
-  uint32_t* rec = nullptr;
-  void* pinned = nullptr;  // rec points into it (the order kernel's CSR as it arrived)
+  VulnExport ex;
   std::vector<Vuln> gv;
   std::vector<tvm_vuln> gc;
   std::vector<std::vector<const char*>> gvp;
-  ~VulnSetStore() {
-    if (pkg) pool_heap_put(pkg);
-    if (pinned) pool_host_put(pinned);
-    else if (rec) pool_heap_put(rec);
-  }
 };
 
 bool batch_has_redhat(const tvm_batch* b, const DB& db) {
@@ -1824,70 +1818,20 @@ bool batch_has_redhat(const tvm_batch* b, const DB& db) {
   return any.load();
 }
 
-// pkg[] from CSR row ends (package p's matches end at row_end[p]), in parallel over packages.
-void expand_rows(const uint32_t* row_end, size_t n_pkgs, uint32_t pkg_base, uint32_t* pkg) {
-  pool_range_for(n_pkgs, 1 << 14, [&](size_t a, size_t z) {
-    uint32_t at = a ? row_end[a - 1] : 0;
-    for (size_t p = a; p < z; p++) {
-      const uint32_t e = row_end[p];
-      for (; at < e; at++) pkg[at] = uint32_t(p) + pkg_base;
-    }
-  });
-}
-
-void set_out(tvm_db* d, VulnSetStore* st, size_t n, tvm_vuln_set* out) {
+void set_out(tvm_db* d, VulnSetStore* st, const uint32_t* row_end, size_t n_pkgs, uint32_t first_pkg,
+             const uint8_t* rec, uint32_t width, size_t n, tvm_vuln_set* out) {
   const VulnTemplates& t = templates(d);
-  out->pkg = st->pkg;
-  out->rec = st->rec;
+  out->row_end = row_end;
+  out->n_pkgs = n_pkgs;
+  out->first_pkg = first_pkg;
+  out->rec = rec;
+  out->rec_width = width;
   out->n = n;
   out->adv_recs = t.c.data();
   out->n_adv_recs = t.c.size();
   out->grp_recs = st->gc.data();
   out->n_grp_recs = st->gc.size();
   out->priv = st;
-}
-
-// The order kernel over the batch's raw list into device buffers (caller holds the shared lock).
-bool order_locked(tvm_engine* e, tvm_batch* b, uint32_t* csr, uint32_t* row_end, uint64_t cap, std::string& err) {
-  (void)hipSetDevice(e->device);
-  hipStream_t st = e->eng->stream();
-  const uint32_t nt = b->dev.n_tiles;
-  if (nt == 0) return true;
-  if (b->order_cap < nt + 1) {
-    if (b->order_scratch) (void)hipFree(b->order_scratch);
-    b->order_scratch = nullptr;
-    b->order_cap = 0;
-    void* p = nullptr;
-    if (hipMalloc(&p, size_t(nt + 1) * 8) != hipSuccess) {
-      err = "hipMalloc(order scratch) failed";
-      return false;
-    }
-    b->order_scratch = static_cast<unsigned long long*>(p);
-    b->order_cap = nt + 1;
-  }
-  OrderArgs oa;
-  oa.dir = b->m.dir;
-  oa.pkg = b->m.pkg;
-  oa.adv = b->m.adv;
-  oa.csr_adv = csr;
-  oa.row_end = row_end;
-  oa.cap = std::min<uint64_t>(cap, b->m.cap);
-  oa.ticket = b->order_scratch;
-  oa.status = b->order_scratch + 1;
-  oa.t0 = 0;
-  oa.n = b->dev.n;
-  oa.pkg_base = b->dev.pkg_base;
-  if (hipMemsetAsync(b->order_scratch, 0, size_t(nt + 1) * 8, st) != hipSuccess) {
-    err = "hipMemsetAsync(order scratch) failed";
-    return false;
-  }
-  launch_order(nt, st, oa);
-  const hipError_t le = hipGetLastError();
-  if (le != hipSuccess) {
-    err = std::string("order kernel: ") + hipGetErrorString(le);
-    return false;
-  }
-  return true;
 }
 
 }  // namespace
@@ -1914,82 +1858,75 @@ int tvm_match_vulns(tvm_engine* e, tvm_batch* b, tvm_vuln_set* out, char* err, s
     set_err(err, errlen, "tvm_match_vulns: reading the match status failed");
     return TVM_EDEVICE;
   }
-  if (bits || ep >= 0 || total > cur(b).cap) {
+  if (bits || ep >= 0 || total > cur(b).cap || b->m.ctl == nullptr) {
     set_err(err, errlen, bits ? "tvm_match_vulns: match kernel internal error bits " + std::to_string(bits)
                          : ep >= 0 ? "tvm_match_vulns: the batch met an undecodable advisory (package " +
                                          std::to_string(ep) + ")"
                                    : "tvm_match_vulns: the match buffer overflowed (upload with a larger cap)");
     return TVM_EINVAL;
   }
-  templates(e->db);  // outside the timed part of a caller's second call
+  templates(e->db);  // built by the first export of a DB (outside a caller's timed calls)
   auto st = std::make_unique<VulnSetStore>();
-  const size_t n_alloc = std::max<uint64_t>(total, 1) * 4;
-  if (!(st->pkg = static_cast<uint32_t*>(pool_heap_get(n_alloc)))) {
-    set_err(err, errlen, "tvm_match_vulns: out of host memory");
+  ExportList in;
+  in.list = cur(b);
+  in.total = total;
+  in.n_tiles = b->dev.n_tiles;
+  in.pkg_base = b->dev.pkg_base;
+  if (b->merged) {
+    const RhMerged& mg = b->rh.merged();
+    in.rh = true;
+    in.base = mg.base;
+    in.grp = mg.grp;
+    in.raw_adv = b->m.adv;
+    in.raw_cap = b->m.cap;
+    in.pk = b->dev.pk;
+    in.plats = e->eng->device_plats();
+    in.n_plats = uint32_t(db.plat_info.size());
+  }
+  const uint32_t n_adv = uint32_t(db.advs.size());
+  if (!export_vulns(e->device, e->eng->stream(), in, n_adv, st->ex, msg)) {
+    set_err(err, errlen, "tvm_match_vulns: " + msg);
     return TVM_EDEVICE;
   }
-  if (b->merged) {
-    std::vector<uint32_t> pkg, adv, base, contrib;
-    std::vector<uint2> grp;
-    if (!b->rh.fetch(rh_inputs(e, b), pkg, adv, base, grp, contrib, e->eng->stream(), msg)) {
-      set_err(err, errlen, "tvm_match_vulns: " + msg);
-      return TVM_EDEVICE;
+  // the merged Red Hat groups' records (redhat.go:146-187), on the host threads
+  const VulnExport& ex = st->ex;
+  if (ex.n_groups) {
+    std::vector<RhRec> groups(ex.n_groups);
+    for (uint32_t k = 0; k < ex.n_groups; k++) {
+      const uint4 g = ex.groups[k];
+      RhRec& r = groups[k];
+      r.pkg = g.y;
+      r.base = g.z;
+      r.best = db.advs[g.w].fixed.empty() ? RH_NONE : g.w;
+      r.start = ex.moff[k];
+      r.len = ex.moff[k + 1] - ex.moff[k];
     }
-    if (!(st->rec = static_cast<uint32_t*>(pool_heap_get(n_alloc)))) {
-      set_err(err, errlen, "tvm_match_vulns: out of host memory");
-      return TVM_EDEVICE;
-    }
-    const auto& pi = db.plat_info;
-    std::vector<RhRec> groups;
-    const uint32_t n_adv = uint32_t(db.advs.size());
-    for (size_t i = 0; i < pkg.size(); i++) {
-      st->pkg[i] = pkg[i];
-      st->rec[i] = adv[i];
-      const uint32_t plat = b->hb.pk[pkg[i] - b->dev.pkg_base].x;
-      if (plat >= pi.size() || pi[plat].drv != DRV_REDHAT || grp[i].y <= 1) continue;
-      RhRec r{};  // a group of several members: its own record (VendorIDs union, greatest FixedVersion)
-      r.pkg = pkg[i];
-      r.base = base[i];
-      r.best = db.advs[adv[i]].fixed.empty() ? RH_NONE : adv[i];
-      r.start = grp[i].x;
-      r.len = grp[i].y;
-      st->rec[i] = n_adv + uint32_t(groups.size());
-      groups.push_back(r);
-    }
-    redhat_batch_vulns(db, b->hb, groups, contrib, b->dev.pkg_base, st->gv);
+    const size_t pieces = std::min<size_t>(64, (groups.size() + 1023) / 1024);
+    std::vector<std::vector<Vuln>> parts(pieces);
+    pool_range_for(pieces, 1, [&](size_t a, size_t z) {
+      for (size_t q = a; q < z; q++) {
+        const size_t g0 = groups.size() * q / pieces, g1 = groups.size() * (q + 1) / pieces;
+        std::vector<RhRec> sub(groups.begin() + g0, groups.begin() + g1);
+        redhat_batch_vulns(db, b->hb, sub, ex.members, b->dev.pkg_base, parts[q]);
+      }
+    });
+    st->gv.reserve(groups.size());
+    for (auto& pv : parts)
+      for (Vuln& v : pv) st->gv.push_back(std::move(v));
     st->gc.resize(st->gv.size());
     st->gvp.resize(st->gv.size());
-    for (size_t j = 0; j < st->gv.size(); j++) {
-      Vuln& v = st->gv[j];
-      v.pkg = 0;
-      v.installed.clear();  // a package field: the batch export pairs the record with its package
-      to_c(db, v, st->gc[j], st->gvp[j]);
-    }
-    total = pkg.size();
-  } else {
-    // the order kernel writes the per-package lists (CSR) on the device; one DMA each way back
-    const size_t np = b->hb.pk.size();
-    void* dcsr = pool_device_get(e->device, n_alloc, "tvm_match_vulns(csr)", msg);
-    void* drow = dcsr ? pool_device_get(e->device, std::max<size_t>(np, 1) * 4, "tvm_match_vulns(row ends)", msg)
-                      : nullptr;
-    void* hrow = drow ? pool_host_get(std::max<size_t>(np, 1) * 4, "tvm_match_vulns(row ends)", msg) : nullptr;
-    st->pinned = hrow ? pool_host_get(n_alloc, "tvm_match_vulns(csr)", msg) : nullptr;
-    hipStream_t s2 = e->eng->stream();
-    bool ok = st->pinned && order_locked(e, b, static_cast<uint32_t*>(dcsr), static_cast<uint32_t*>(drow), total, msg);
-    ok = ok && (total == 0 || hipMemcpyAsync(st->pinned, dcsr, total * 4, hipMemcpyDeviceToHost, s2) == hipSuccess) &&
-         (np == 0 || hipMemcpyAsync(hrow, drow, np * 4, hipMemcpyDeviceToHost, s2) == hipSuccess) &&
-         hipStreamSynchronize(s2) == hipSuccess;
-    if (ok) expand_rows(static_cast<const uint32_t*>(hrow), np, b->dev.pkg_base, st->pkg);
-    if (dcsr) pool_device_put(e->device, dcsr);
-    if (drow) pool_device_put(e->device, drow);
-    if (hrow) pool_host_put(hrow);
-    if (!ok) {
-      set_err(err, errlen, "tvm_match_vulns: " + (msg.empty() ? std::string("device copy failed") : msg));
-      return TVM_EDEVICE;
-    }
-    st->rec = static_cast<uint32_t*>(st->pinned);
+    pool_range_for(st->gv.size(), 1 << 12, [&](size_t a, size_t z) {
+      for (size_t j = a; j < z; j++) {
+        Vuln& v = st->gv[j];
+        v.pkg = 0;
+        v.installed.clear();  // a package field: the set pairs the record with its package
+        to_c(db, v, st->gc[j], st->gvp[j]);
+      }
+    });
   }
-  set_out(e->db, st.release(), total, out);
+  const VulnSetStore* sp = st.get();
+  set_out(e->db, st.release(), sp->ex.row_end_h, b->hb.pk.size(), b->dev.pkg_base, sp->ex.rec_h, sp->ex.width,
+          sp->ex.n, out);
   return TVM_OK;
 }
 
@@ -2007,34 +1944,9 @@ int tvm_pipeline_vulns(tvm_engine* e, tvm_batch* b, tvm_vuln_set* out, char* err
     return TVM_EINVAL;
   }
   templates(e->db);
-  const uint64_t total = b->pipe_total;
   auto st = std::make_unique<VulnSetStore>();
-  const size_t n_alloc = std::max<uint64_t>(total, 1) * 4;
-  st->pkg = static_cast<uint32_t*>(pool_heap_get(n_alloc));
-  st->rec = st->pkg ? static_cast<uint32_t*>(pool_heap_get(n_alloc)) : nullptr;
-  if (!st->rec) {
-    set_err(err, errlen, "tvm_pipeline_vulns: out of host memory");
-    return TVM_EDEVICE;
-  }
-  const uint32_t* row_end = b->pipe->row_end();
-  const size_t np = b->hb.pk.size();
-  const bool three = b->pipe->packed();
-  const uint8_t* raw = reinterpret_cast<const uint8_t*>(b->pipe->adv());
-  // one pass over the result as it arrived: package column from the row ends, record =
-  // advisory (3-byte indices widened on the way)
-  pool_range_for(np, 1 << 14, [&](size_t a, size_t z) {
-    uint32_t at = a ? row_end[a - 1] : 0;
-    for (size_t p = a; p < z; p++) {
-      const uint32_t end = row_end[p];
-      for (; at < end; at++) {
-        st->pkg[at] = uint32_t(p) + b->pkg_base;
-        st->rec[at] = three ? uint32_t(raw[3 * size_t(at)]) | uint32_t(raw[3 * size_t(at) + 1]) << 8 |
-                                  uint32_t(raw[3 * size_t(at) + 2]) << 16
-                            : reinterpret_cast<const uint32_t*>(raw)[at];
-      }
-    }
-  });
-  set_out(e->db, st.release(), total, out);
+  set_out(e->db, st.release(), b->pipe->row_end(), b->hb.pk.size(), b->pkg_base,
+          reinterpret_cast<const uint8_t*>(b->pipe->adv()), b->pipe->packed() ? 3u : 4u, b->pipe_total, out);
   return TVM_OK;
 }
 
