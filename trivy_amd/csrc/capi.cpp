@@ -1562,20 +1562,8 @@ int tvm_db_rows_many(const tvm_db* db, const char* bucket, size_t n, const char*
   if (!db || !db->finalized || !bucket || (n && (!arena || !name_off || !name_len || !out))) return TVM_EINVAL;
   const DB& d = db->db;
   const int32_t plat = d.find_plat(bucket);
-  for (size_t i = 0; i < n; i++) {
-    out[i] = 0;
-    if (plat < 0 || d.slot_hash.empty()) continue;
-    const std::string_view name(arena + name_off[i], name_len[i]);
-    const uint64_t h = pkg_key_hash(uint32_t(plat), reinterpret_cast<const uint8_t*>(name.data()), uint32_t(name.size()));
-    for (uint64_t s = h & d.slot_mask; d.slot_hash[s]; s = (s + 1) & d.slot_mask) {
-      const SlotVal& v = d.slot_val[s];
-      if (d.slot_hash[s] == h && (v.name_len & SLOT_LEN_MASK) == name.size() &&
-          std::equal(name.begin(), name.end(), d.name_arena.begin() + v.name_off)) {
-        out[i] = v.row_count;
-        break;
-      }
-    }
-  }
+  for (size_t i = 0; i < n; i++)
+    out[i] = plat < 0 ? 0u : d.key_rows(uint32_t(plat), std::string_view(arena + name_off[i], name_len[i]));
   return TVM_OK;
 }
 
@@ -1798,7 +1786,6 @@ const VulnTemplates& templates(tvm_db* d) {
 // merged Red Hat groups' records; a pipelined pass's set points into its result (no copy).
 struct VulnSetStore {
   VulnExport ex;
-  std::vector<Vuln> gv;
   std::vector<tvm_vuln> gc;
   std::vector<std::vector<const char*>> gvp;
 };
@@ -1888,39 +1875,43 @@ int tvm_match_vulns(tvm_engine* e, tvm_batch* b, tvm_vuln_set* out, char* err, s
     set_err(err, errlen, "tvm_match_vulns: " + msg);
     return TVM_EDEVICE;
   }
-  // the merged Red Hat groups' records (redhat.go:146-187), on the host threads
+  // the merged Red Hat groups' records (redhat.go:146-187) on the host threads, from the
+  // members' own records: the first member's (ID, Status, Severity), the representative's
+  // FixedVersion, and VendorIDs - the first member's own when it is the one fixed member, else
+  // the sorted union of the fixed members' (ustrings.Unique) - as pointers into those records
   const VulnExport& ex = st->ex;
   if (ex.n_groups) {
-    std::vector<RhRec> groups(ex.n_groups);
-    for (uint32_t k = 0; k < ex.n_groups; k++) {
-      const uint4 g = ex.groups[k];
-      RhRec& r = groups[k];
-      r.pkg = g.y;
-      r.base = g.z;
-      r.best = db.advs[g.w].fixed.empty() ? RH_NONE : g.w;
-      r.start = ex.moff[k];
-      r.len = ex.moff[k + 1] - ex.moff[k];
-    }
-    const size_t pieces = std::min<size_t>(64, (groups.size() + 1023) / 1024);
-    std::vector<std::vector<Vuln>> parts(pieces);
-    pool_range_for(pieces, 1, [&](size_t a, size_t z) {
-      for (size_t q = a; q < z; q++) {
-        const size_t g0 = groups.size() * q / pieces, g1 = groups.size() * (q + 1) / pieces;
-        std::vector<RhRec> sub(groups.begin() + g0, groups.begin() + g1);
-        redhat_batch_vulns(db, b->hb, sub, ex.members, b->dev.pkg_base, parts[q]);
-      }
-    });
-    st->gv.reserve(groups.size());
-    for (auto& pv : parts)
-      for (Vuln& v : pv) st->gv.push_back(std::move(v));
-    st->gc.resize(st->gv.size());
-    st->gvp.resize(st->gv.size());
-    pool_range_for(st->gv.size(), 1 << 12, [&](size_t a, size_t z) {
-      for (size_t j = a; j < z; j++) {
-        Vuln& v = st->gv[j];
-        v.pkg = 0;
-        v.installed.clear();  // a package field: the set pairs the record with its package
-        to_c(db, v, st->gc[j], st->gvp[j]);
+    const VulnTemplates& tp = templates(e->db);
+    st->gc.resize(ex.n_groups);
+    st->gvp.resize(ex.n_groups);
+    pool_range_for(ex.n_groups, 1 << 10, [&](size_t a, size_t z) {
+      std::vector<const char*> ids;
+      for (size_t k = a; k < z; k++) {
+        const uint4 g = ex.groups[k];
+        const tvm_vuln& base = tp.c[g.z];
+        tvm_vuln& c = st->gc[k];
+        c = base;
+        const bool has_best = !db.advs[g.w].fixed.empty();
+        c.fixed_version = has_best ? tp.c[g.w].fixed_version : "";
+        uint32_t n_fixed = 0;
+        ids.clear();
+        for (uint32_t m = ex.moff[k]; m < ex.moff[k + 1]; m++) {
+          const uint32_t adv = ex.members[m];
+          if (adv >= db.advs.size() || db.advs[adv].fixed.empty()) continue;
+          n_fixed++;
+          const tvm_vuln& mv = tp.c[adv];
+          ids.insert(ids.end(), mv.vendor_ids, mv.vendor_ids + mv.n_vendor_ids);
+        }
+        if (n_fixed == 1 && !db.advs[g.z].fixed.empty()) continue;  // the first member's list as it is
+        c.vendor_ids = nullptr;
+        c.n_vendor_ids = 0;
+        if (!n_fixed) continue;
+        std::sort(ids.begin(), ids.end(), [](const char* x, const char* y) { return std::strcmp(x, y) < 0; });
+        ids.erase(std::unique(ids.begin(), ids.end(), [](const char* x, const char* y) { return !std::strcmp(x, y); }),
+                  ids.end());
+        st->gvp[k] = ids;
+        c.vendor_ids = st->gvp[k].empty() ? nullptr : st->gvp[k].data();
+        c.n_vendor_ids = st->gvp[k].size();
       }
     });
   }

@@ -309,6 +309,18 @@ int32_t DB::find_key(uint32_t plat, std::string_view name) const {
   return -1;
 }
 
+uint32_t DB::key_rows(uint32_t plat, std::string_view name) const {
+  if (slot_hash.empty()) return 0;
+  const uint64_t h = pkg_key_hash(plat, reinterpret_cast<const uint8_t*>(name.data()), uint32_t(name.size()));
+  for (uint64_t i = h & slot_mask; slot_hash[i]; i = (i + 1) & slot_mask) {
+    const SlotVal& v = slot_val[i];
+    if (slot_hash[i] == h && (v.name_len & SLOT_LEN_MASK) == name.size() &&
+        std::equal(name.begin(), name.end(), name_arena.begin() + v.name_off))
+      return v.row_count;
+  }
+  return 0;
+}
+
 std::vector<int64_t> DB::redhat_cpes(const std::vector<std::string_view>& repos,
                                      const std::vector<std::string_view>& nvrs) const {
   std::vector<int64_t> out;

@@ -89,6 +89,9 @@ class DB {
   int32_t find_plat(std::string_view root) const;
   // Host-side lookup of a key index (used by drivers for error text); -1 if absent.
   int32_t find_key(uint32_t plat, std::string_view name) const;
+  // Interval rows of key (plat, name) in the device tables (0: no key) - the host pre-probe of
+  // a package's work (multi-GPU shard balance, heavy-first tile order).
+  uint32_t key_rows(uint32_t plat, std::string_view name) const;
 
   // Red Hat CPE resolution (trivy-db RedHatRepoToCPEs / RedHatNVRToCPEs): the unique CPE
   // indices of content sets + NVRs, in first-seen order.

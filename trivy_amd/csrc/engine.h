@@ -85,6 +85,10 @@ struct DevBatch {
   uint32_t pkg_base = 0;     // added to the package index of every match (multi-GPU shards)
   uint64_t* spill = nullptr;  // the batch's own long-key / Maven-parse scratch (never shared between batches)
   uint64_t spill_cap = 0;
+  // launch order of the tiles (device-resident launches of batches with library grammars:
+  // the heaviest tiles first, so the launch does not end on a tail of Maven-program tiles);
+  // nullptr = tile order
+  uint32_t* tile_map = nullptr;
   // probe -> sweep hand-off (device only)
   PkgRec* rec = nullptr;
   uint4* tail = nullptr;  // key bytes 16..31 per package

@@ -319,6 +319,34 @@ bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
   if (!hb.attr.empty() &&
       !hip_ok(hipMemcpy(b.attr, hb.attr.data(), hb.attr.size() * sizeof(uint2), hipMemcpyHostToDevice), "H2D attr", err))
     return false;
+  static const bool no_order = std::getenv("TVM_NO_TILE_ORDER") != nullptr;  // measurement: tile order
+  if ((b.gm & ~GM_OS) != 0 && b.n_tiles > 1 && !no_order) {
+    // library grammars: per-pair cost is uneven (a Maven program row costs many interval rows),
+    // so the device-resident launch takes the tiles heaviest first (predicted rows from the host
+    // index, Maven rows weighted 8x) and the grid does not end on a tail of heavy tiles
+    const auto& pi = db_->plat_info;
+    std::vector<uint64_t> off;
+    hb.name_offsets(off);
+    std::vector<uint64_t> w(b.n_tiles, 0);
+    range_for(b.n_tiles, 64, [&](size_t t0, size_t t1) {
+      for (size_t t = t0; t < t1; t++) {
+        uint64_t s = 0;
+        for (size_t p = t * kTile; p < std::min(hb.pk.size(), (t + 1) * kTile); p++) {
+          const uint32_t plat = hb.pk[p].x;
+          if (plat >= pi.size()) continue;
+          const std::string_view name(reinterpret_cast<const char*>(hb.arena.data()) + off[p], hb.pk[p].y & 0xFFFFu);
+          s += 1 + uint64_t(db_->key_rows(plat, name)) * (pi[plat].cmp == CMP_MAVEN ? 8 : 1);
+        }
+        w[t] = s;
+      }
+    });
+    std::vector<uint32_t> order(b.n_tiles);
+    for (uint32_t t = 0; t < b.n_tiles; t++) order[t] = t;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return w[x] > w[y]; });
+    if (!dmalloc(&b.tile_map, order.size(), "hipMalloc(tile order)", err) ||
+        !hip_ok(hipMemcpy(b.tile_map, order.data(), order.size() * 4, hipMemcpyHostToDevice), "H2D tile order", err))
+      return false;
+  }
   if (!hb.cpe_bits.empty() && hb.cpe_words) {
     if (!dmalloc(&b.cpe_bits, hb.cpe_bits.size(), "hipMalloc(cpe sets)", err) ||
         !hip_ok(hipMemcpy(b.cpe_bits, hb.cpe_bits.data(), hb.cpe_bits.size() * 4, hipMemcpyHostToDevice), "H2D cpe", err))
@@ -336,6 +364,7 @@ void Engine::free_batch(int device, DevBatch& b, bool pooled) {
                   static_cast<void*>(b.spill)})
     dfree(p, pooled, device);
   dfree(b.cpe_bits, false, device);  // never pooled (copied by the caller)
+  dfree(b.tile_map, false, device);
   b = DevBatch{};
 }
 
@@ -454,6 +483,7 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
       }();
       fa.n_copy = n_copy;
     }
+    if (!co && t_begin == 0 && t_end == b.n_tiles) fa.tile_map = b.tile_map;
     const FusedFn fn = fused_fn(b.gm, vi);
     if (!fn) {
       err = std::string("match-path variant ") + kVariantNames[vi - 1] + " is not built for this batch's grammar set";

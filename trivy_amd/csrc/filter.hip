@@ -18,20 +18,23 @@
 //
 // The match list arrives grouped by package (each tile's segment is in package order, a
 // package's advisories in trivy-db Get order), so no sort is needed:
-//   filter_count_dup  pairs of packages whose dedup key repeats (sizes the cross-package
-//                     dedup table; one host synchronisation, only when packages repeat);
 //   filter_mark    per pair: severity / status; ignore rules (one hash-set probe per rule
 //                  kind, smallest precedence wins); run bounds of every package and whether
-//                  its IDs are strictly increasing; packages that repeat race into the
-//                  dedup table with one 64-bit atomicMax of (FixedVersion rank, -package)
-//                  per (dedup key, vulnerability);
-//   filter_select  dedup: the table winner, then - only in runs whose IDs are not strictly
-//                  increasing (one ID from two data sources, Red Hat's per-RHSA rows) - the
-//                  first of the package's own pairs with the greatest FixedVersion; then
-//                  VEX; per package six counters (survivors per severity, ignored), one
-//                  atomic per package run per wave;
+//                  its IDs are strictly increasing;
+//   filter_select  dedup: a pair of a package whose dedup key repeats looks the ID up in the
+//                  runs of the other packages of that key (bisection of an ID-sorted run) and
+//                  loses to a greater FixedVersion or an equal one seen first; then - only in
+//                  runs whose IDs are not strictly increasing (one ID from two data sources,
+//                  Red Hat's per-RHSA rows) - the first of the package's own pairs with the
+//                  greatest FixedVersion; then the per-package class counters (survivors per
+//                  severity, ignored) from wave ballots: a package whose run lies inside one
+//                  64-pair wave segment stores them, one spread over several adds them
+//                  atomically;
+//   vex_mark       VEX statements drop survivors (and take them off the counters);
 //   scans          survivor offsets of the package groups in perm order, ignored offsets
 //                  in package order;
+//   (round 4 counted in a kernel of its own, filter_count, and deduplicated through a hash
+//   table sized after a host synchronisation; both are gone)
 //   filter_place   a survivor of a package alone in its group whose run is ID-sorted (the
 //                  bucket order of one trivy-db key: the common case) is placed in O(1):
 //                  group offset + the package's survivors of higher severity + its
@@ -86,6 +89,8 @@ struct FilterArgs {
   const uint32_t* grp_e;
   const uint32_t* dkey;
   const uint32_t* prank;
+  const uint32_t* dk_b;  // perm range of the package's dedup key (FL_DUP packages)
+  const uint32_t* dk_e;
   const uint8_t* dup;   // static flags: FL_DUP | FL_SINGLE
   const uint32_t* pkg_class;
   // per package, per call
@@ -100,16 +105,11 @@ struct FilterArgs {
   uint32_t* mkey;  // after filter_mark: (4 - severity) << id_bits | ID rank, or kEmpty
   uint32_t* skey;  // after filter_select: the survivors' mkey, else kEmpty
   uint32_t* ign;   // precedence of the ignoring rule, kEmpty = not ignored
-  uint32_t* mine;  // dedup-table slot of a repeating package's pair
   uint8_t* pcls;   // after filter_select: the pair's counter class (pair_class)
-  uint32_t* wcarry;  // after filter_count, per 64-pair wave w entered by a run begun earlier:
-                     //   the run's class counts before pair 64w (kClasses each)
   // tables
   const unsigned long long* rules;  // {key, precedence} x 2^k
   uint64_t rule_mask;
   uint32_t kinds;  // bit k: rules of tag k exist
-  unsigned long long* table;  // dedup {key + 1, value} x 2^k
-  uint64_t table_mask;
   uint32_t sev_mask, status_mask, id_bits;
   uint2* out;      // survivors in report order
   uint32_t* iout;  // ignored {package, advisory, finding} in detection order
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void rules_insert(RuleDev r, unsigned long 
 __global__ __launch_bounds__(kBlock) void vex_mark(RuleDev r, const uint32_t* pkg, const uint2* side,
                                                    const uint32_t* run_b, const uint32_t* run_e, const uint8_t* fl,
                                                    uint64_t n, uint32_t n_pkgs, uint32_t n_ids, uint32_t* skey,
-                                                   uint8_t* pcls, uint32_t* bad) {
+                                                   uint8_t* pcls, uint32_t* cnt, uint32_t* surv, uint32_t* bad) {
   const uint64_t g = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
   int k = 0;
   while (k < r.n_lists && g >= r.end[k]) k++;
@@ -205,6 +205,8 @@ __global__ __launch_bounds__(kBlock) void vex_mark(RuleDev r, const uint32_t* pk
   const uint32_t re = run_e[p];  // written by this call's filter_mark, as rb was
   auto drop = [&](uint32_t j) {
     if (skey[j] != kEmpty) {  // a survivor (so not ignored): it leaves every counter class
+      atomicSub(&cnt[uint64_t(p) * kClasses + pcls[j]], 1u);
+      atomicSub(&surv[p], 1u);
       skey[j] = kEmpty;
       pcls[j] = uint8_t(kNoClass);
     }
@@ -232,7 +234,7 @@ __global__ __launch_bounds__(kBlock) void filter_mark(FilterArgs a) {
   const uint64_t stride = uint64_t(gridDim.x) * kBlock * kU;
   const uint64_t n = a.n;
   for (uint64_t b0 = uint64_t(blockIdx.x) * kBlock * kU; b0 < n; b0 += stride) {
-    uint32_t p[kU], pp[kU], pn[kU], f[kU], dp[kU];
+    uint32_t p[kU], pp[kU], pn[kU], f[kU];
     uint2 sd[kU];
     uint32_t vprev[kU];
     const uint32_t lane = threadIdx.x & 63;
@@ -257,10 +259,7 @@ __global__ __launch_bounds__(kBlock) void filter_mark(FilterArgs a) {
       if (lane != 63) pn[k] = i + 1 < n ? dn : 0xFFFFFFFFu;
     }
 #pragma unroll
-    for (int k = 0; k < kU; k++) {
-      f[k] = a.fl[p[k]];
-      dp[k] = a.dup[p[k]];
-    }
+    for (int k = 0; k < kU; k++) f[k] = a.fl[p[k]];
 #pragma unroll
     for (int k = 0; k < kU; k++) {
       const uint64_t i = b0 + uint64_t(k) * kBlock + threadIdx.x;
@@ -283,33 +282,51 @@ __global__ __launch_bounds__(kBlock) void filter_mark(FilterArgs a) {
         a.ign[i] = prec;
       }
       a.mkey[i] = keep ? ((4u - sev) << a.id_bits) | vr : kEmpty;
-      if (keep && (dp[k] & FL_DUP)) {  // table entries: {key + 1 (0 = empty), max value}, zeroed
-        const unsigned long long key = (uint64_t(a.dkey[pk]) << 32) | vr;
-        const unsigned long long val = (uint64_t(a.t.adv_rank[a.adv[i]].y) << 32) | (0xFFFFFFFFu - pk);
-        for (uint64_t s = mix64(key) & a.table_mask;; s = (s + 1) & a.table_mask) {
-          const unsigned long long prev = atomicCAS(&a.table[2 * s], 0ull, key + 1);
-          if (prev == 0ull || prev == key + 1) {
-            atomicMax(&a.table[2 * s + 1], val);
-            a.mine[i] = uint32_t(s);
-            break;
-          }
-        }
-      }
     }
   }
+}
+
+// Does package q hold a kept pair of vulnerability rank vr whose FixedVersion rank beats fr
+// (greater, or equal with q seen first)?  q's run: bisection when its IDs are strictly
+// increasing, else a walk.  A package without pairs has a stale run start (rejected).
+__device__ __forceinline__ bool beaten_by(const FilterArgs& a, uint32_t q, uint32_t vr, uint32_t fr, bool q_first) {
+  const uint32_t rb = a.run_b[q];
+  if (rb >= a.n || a.pkg[rb] != q || (rb && a.pkg[rb - 1] == q)) return false;
+  uint32_t lo = rb, hi = a.run_e[q];
+  if (!(a.fl[q] & FL_UNS)) {
+    uint32_t l = lo, h = hi;
+    while (l < h) {
+      const uint32_t mid = (l + h) >> 1;
+      if (a.side[mid].x < vr) l = mid + 1;
+      else h = mid;
+    }
+    lo = l;
+    hi = min(hi, l + 1);
+  }
+  for (uint32_t j = lo; j < hi; j++) {
+    if (a.side[j].x != vr || a.mkey[j] == kEmpty) continue;
+    const uint32_t fj = a.t.adv_rank[a.adv[j]].y;
+    if (fj > fr || (fj == fr && q_first)) return true;
+  }
+  return false;
 }
 
 __global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
   const uint64_t stride = uint64_t(gridDim.x) * kBlock * kU;
   const uint32_t id_mask = (1u << a.id_bits) - 1u;
   const uint64_t n = a.n;
+  const uint32_t lane = threadIdx.x & 63;
   for (uint64_t b0 = uint64_t(blockIdx.x) * kBlock * kU; b0 < n; b0 += stride) {  // wave-uniform trip count
-    uint32_t pv[kU], kv[kU], fv[kU];
+    uint32_t pv[kU], kv[kU], fv[kU], pe[kU], ne[kU];
 #pragma unroll
     for (int k = 0; k < kU; k++) {
       const uint64_t i = min(b0 + uint64_t(k) * kBlock + threadIdx.x, n - 1);
       pv[k] = a.pkg[i];
       kv[k] = a.mkey[i];
+      // the packages just before and after this wave's 64 pairs (edge lanes)
+      const uint64_t s0 = b0 + uint64_t(k) * kBlock + (threadIdx.x & ~63u);
+      pe[k] = (lane == 0 && s0 > 0 && s0 - 1 < n) ? a.pkg[s0 - 1] : 0xFFFFFFFFu;
+      ne[k] = (lane == 63 && s0 + 64 < n) ? a.pkg[s0 + 64] : 0xFFFFFFFFu;
     }
 #pragma unroll
     for (int k = 0; k < kU; k++) fv[k] = a.fl[pv[k]];
@@ -318,6 +335,7 @@ __global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
       const uint64_t i = b0 + uint64_t(k) * kBlock + threadIdx.x;
       const bool valid = i < n;
       uint32_t p = valid ? pv[k] : 0xFFFFFFFFu, key = valid ? kv[k] : kEmpty;
+      uint32_t cls = kNoClass;
       if (valid) {
         if (key != kEmpty) {
           const uint32_t vr = key & id_mask;
@@ -325,8 +343,12 @@ __global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
           const bool dup = f & FL_DUP, uns = f & FL_UNS;
           // the FixedVersion rank is needed only to dedup (repeating packages, unsorted runs)
           const uint32_t fr = (dup || uns) ? a.t.adv_rank[a.adv[i]].y : 0u;
-          if (dup && a.table[2 * uint64_t(a.mine[i]) + 1] != ((uint64_t(fr) << 32) | (0xFFFFFFFFu - p)))
-            key = kEmpty;  // another package won the (dedup key, ID): greater FixedVersion or first seen
+          if (dup) {  // another package of the dedup key with a greater FixedVersion, or an equal one seen first
+            for (uint32_t j = a.dk_b[p], je = a.dk_e[p]; j < je && key != kEmpty; j++) {
+              const uint32_t q = a.perm[j];
+              if (q != p && beaten_by(a, q, vr, fr, q < p)) key = kEmpty;
+            }
+          }
           if (key != kEmpty && uns) {  // the package's own pairs of this ID: the first with the greatest FixedVersion
             const uint32_t rb = a.run_b[p], re = a.run_e[p];
             for (uint32_t j = rb; j < re; j++) {
@@ -342,84 +364,38 @@ __global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
           }
         }
         a.skey[i] = key;
+        cls = pair_class(a, key, i);
+        a.pcls[i] = uint8_t(cls);  // placed by filter_place
       }
-      if (valid) a.pcls[i] = uint8_t(pair_class(a, key, i));  // counted by filter_count
-    }
-  }
-}
-
-// Per-package class counters from the pairs' classes (the list is grouped by package): the
-// head lane of each package run starting inside a wave stores the run's nonzero class counts
-// (the counters are cleared before filter_select); a run crossing the wave's end - at most one
-// per wave - is finished by the whole wave reading on to the run's end, so no counter is
-// written twice and none atomically. On the way it leaves, at every later wave the run
-// enters, the run's class counts so far (filter_place's carry into a chunk).
-__global__ __launch_bounds__(kBlock) void filter_count(FilterArgs a) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
-  // software-pipelined: the next step's pair words are loaded before this step's counting
-  uint32_t n_p = 0xFFFFFFFFu, n_cls = kNoClass, n_before = 0xFFFFFFFFu;
-  auto load = [&](uint64_t b) {
-    const uint64_t i = b + threadIdx.x;
-    n_p = 0xFFFFFFFFu;
-    n_cls = kNoClass;
-    if (i < a.n) {
-      n_p = a.pkg[i];
-      n_cls = a.pcls[i];
-      if (lane == 0) n_before = i == 0 ? 0xFFFFFFFFu : a.pkg[i - 1];  // lane 0: the pair before the wave
-    }
-  };
-  load(uint64_t(blockIdx.x) * kBlock);
-  for (uint64_t b0 = uint64_t(blockIdx.x) * kBlock; b0 < a.n; b0 += stride) {  // wave-uniform trip count
-    const uint64_t i = b0 + threadIdx.x;
-    const bool valid = i < a.n;
-    const uint32_t p = n_p;
-    const uint32_t cls = n_cls;
-    const uint32_t before = n_before;
-    if (b0 + stride < a.n) load(b0 + stride);
-    const uint32_t prev_p = __shfl_up(p, 1, 64);
-    // lane 0 starts a run only at the run's first pair (else the run started in an earlier wave)
-    const bool head = valid && (lane == 0 ? (i == 0 || before != p) : prev_p != p);
-    const bool seg = valid && (lane == 0 || prev_p != p);  // first lane of a package in this wave
-    const unsigned long long segs = __ballot(seg);
-    const unsigned long long above = lane == 63 ? 0ull : segs & (~0ull << (lane + 1));
-    const uint32_t end = above ? uint32_t(__builtin_ctzll(above)) : 64u;
-    const unsigned long long span = (end == 64 ? ~0ull : ((1ull << end) - 1)) & (~0ull << lane);
-    uint32_t cc[kClasses];
+      // per-package class counters over the wave's 64 pairs: the first lane of each package
+      // counts its lanes' classes with six ballots; a package all inside these 64 pairs stores
+      // its counters, one that goes on before or after them adds its share atomically
+      const uint32_t up = __shfl_up(p, 1, 64);
+      const bool head = valid && (lane == 0 || up != p);
+      const unsigned long long heads = __ballot(head);
+      const unsigned long long above = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
+      const uint32_t end = above ? uint32_t(__builtin_ctzll(above)) : 64u;
+      const unsigned long long span = (end == 64 ? ~0ull : ((1ull << end) - 1)) & (~0ull << lane);
+      uint32_t cc[kClasses];
 #pragma unroll
-    for (uint32_t c = 0; c < uint32_t(kClasses); c++) cc[c] = uint32_t(__popcll(__ballot(cls == c) & span));
-    // the wave's last run, when it starts here and goes on past the wave: counted on by all lanes
-    const unsigned long long heads = __ballot(head);
-    const uint32_t last = 63u - uint32_t(__builtin_clzll(segs | 1ull));  // first lane of the last package
-    const bool last_starts = (heads >> last) & 1ull;
-    const uint64_t wend = b0 + (threadIdx.x & ~63u) + 64;  // first pair past this wave
-    const uint32_t lp = __shfl(p, int(last), 64);
-    const uint32_t re = (last_starts && wend < a.n) ? a.run_e[lp] : 0u;  // wave-uniform
-    if (re > wend) {
-      uint32_t more[kClasses];
+      for (uint32_t c = 0; c < uint32_t(kClasses); c++) cc[c] = uint32_t(__popcll(__ballot(cls == c) & span));
+      const uint32_t next = __shfl(ne[k], 63, 64);
+      if (head) {
+        const bool split = (lane == 0 && pe[k] == p) || (end == 64 && next == p);
+        uint32_t* o = a.cnt + uint64_t(p) * kClasses;
+        const uint32_t sum = cc[0] + cc[1] + cc[2] + cc[3] + cc[4];
+        if (split) {
 #pragma unroll
-      for (int c = 0; c < kClasses; c++) more[c] = __shfl(cc[c], int(last), 64);  // the run so far
-      for (uint64_t j0 = wend; j0 < re; j0 += 64) {  // wave-uniform trip count
-        uint32_t sofar = 0;
+          for (int c = 0; c < kClasses; c++)
+            if (cc[c]) atomicAdd(&o[c], cc[c]);
+          if (sum) atomicAdd(&a.surv[p], sum);
+        } else {
 #pragma unroll
-        for (int c = 0; c < kClasses; c++) sofar = lane == uint32_t(c) ? more[c] : sofar;
-        if (lane < uint32_t(kClasses)) a.wcarry[(j0 >> 6) * kClasses + lane] = sofar;
-        const uint64_t j = j0 + lane;
-        const uint32_t cj = j < re ? a.pcls[j] : kNoClass;
-#pragma unroll
-        for (uint32_t c = 0; c < uint32_t(kClasses); c++) more[c] += uint32_t(__popcll(__ballot(cj == c)));
+          for (int c = 0; c < kClasses; c++)
+            if (cc[c]) o[c] = cc[c];
+          if (sum) a.surv[p] = sum;
+        }
       }
-      if (lane == last)
-#pragma unroll
-        for (int c = 0; c < kClasses; c++) cc[c] = more[c];
-    }
-    if (head) {
-      uint32_t* o = a.cnt + uint64_t(p) * kClasses;
-#pragma unroll
-      for (int c = 0; c < kClasses; c++)
-        if (cc[c]) o[c] = cc[c];
-      const uint32_t s = cc[0] + cc[1] + cc[2] + cc[3] + cc[4];
-      if (s) a.surv[p] = s;
     }
   }
 }
@@ -493,8 +469,27 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
       if (lane >= uint32_t(o)) x += y;
     }
     if (lane == 63) wsum[wave] = x;
-    // the run entering the chunk: its classes before c0 (filter_count left them per wave)
-    if (tid < uint32_t(kClasses)) carry[tid] = rb0 < c0 ? a.wcarry[(c0 >> 6) * kClasses + tid] : 0u;
+    // the run entering the chunk: its classes before c0, counted by wave 0 over the shorter
+    // side of the run (before c0, or from c0 on subtracted from the package's totals)
+    if (wave == 0) {
+      uint32_t m = 0;  // lane c < kClasses: class c
+      if (rb0 < c0) {
+        const uint32_t p0 = __shfl(p, 0, 64), re0 = a.run_e[p0];
+        const bool back = c0 - rb0 <= re0 - c0;
+        const uint64_t from = back ? rb0 : c0, to = back ? c0 : re0;
+        for (uint64_t j0 = from; j0 < to; j0 += 64) {  // wave-uniform
+          const uint64_t j = j0 + lane;
+          const uint32_t cj = j < to ? a.pcls[j] : kNoClass;
+#pragma unroll
+          for (uint32_t c = 0; c < uint32_t(kClasses); c++) {
+            const uint32_t k = uint32_t(__popcll(__ballot(cj == c)));
+            if (lane == c) m += k;
+          }
+        }
+        if (!back && lane < uint32_t(kClasses)) m = a.cnt[uint64_t(p0) * kClasses + lane] - m;
+      }
+      if (lane < uint32_t(kClasses)) carry[lane] = m;
+    }
     if (valid && i == rs) {  // the package's first lane: its placement bases, once
       const uint32_t f = pf;
       pflag[tid] = f;
@@ -561,27 +556,8 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
   }
 }
 
-// Pairs whose package's dedup key repeats: the only ones that enter the dedup table, so
-// the table is sized (and cleared) for them alone.
-__global__ __launch_bounds__(kBlock) void filter_count_dup(const uint32_t* pkg, const uint8_t* dup, uint64_t n,
-                                                           unsigned long long* count) {
-  __shared__ uint32_t wsum[kBlock / 64];
-  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
-  uint32_t c = 0;
-  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) c += dup[pkg[i]] & FL_DUP;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int w = 0; w < kBlock / 64; w++) t += wsum[w];
-    if (t) atomicAdd(count, (unsigned long long)t);
-  }
-}
-
 // Scan inputs (one trailing zero, so the exclusive scan's last element is the total):
-// survivors of the package at perm position j (its filter_count sum: one 4-byte gather, not
+// survivors of the package at perm position j (its survivor sum: one 4-byte gather, not
 // five counters of a 24-byte row - C5's scan read 409 MB for 20M packages) / ignored
 // findings of package j.
 struct GroupCount {
@@ -609,9 +585,9 @@ T* as(void* p) {
 }  // namespace
 
 // buffers: 0 perm, 1 grp_b, 2 grp_e, 3 dkey, 4 prank, 5 static flags, 6 counters, 7 flags, 8 run_b,
-// 9 run_e, 10 off, 11 ign_off, 12 mkey, 13 skey, 14 ign, 15 mine, 16 dedup table,
+// 9 run_e, 10 off, 11 ign_off, 12 mkey, 13 skey, 14 ign, 15 dk_b, 16 dk_e,
 // 17 rule table, 18 rule keys, 19 rule precedences, 20 pkg_class, 21 out pairs,
-// 22 ignored out, 23 scan temp / dup count
+// 22 ignored out, 23 scan temp, 24 pair classes, 26 index check
 BatchFilter::~BatchFilter() {
   for (void* p : bufs_)
     if (p) (void)hipFree(p);
@@ -635,7 +611,6 @@ bool BatchFilter::set_packages(const FilterPackages& fp, std::string& err) {
     err = "filter: at most 2^30 packages per batch";
     return false;
   }
-  any_dup_ = std::any_of(fp.dup.begin(), fp.dup.end(), [](uint8_t x) { return x != 0; });
   const std::vector<uint32_t>* cols[5] = {&fp.perm, &fp.grp_b, &fp.grp_e, &fp.dkey, &fp.prank};
   for (int k = 0; k < 5; k++)
     if (cols[k]->size() != n || !grow(k, n * 4, err) ||
@@ -649,6 +624,22 @@ bool BatchFilter::set_packages(const FilterPackages& fp, std::string& err) {
   std::vector<uint8_t> fl(n);
   for (uint64_t p = 0; p < n; p++)
     fl[p] = uint8_t((fp.dup[p] ? FL_DUP : 0u) | (fp.grp_e[p] - fp.grp_b[p] == 1 ? FL_SINGLE : 0u));
+  // the perm range of every package's dedup key (equal keys are adjacent in perm order)
+  std::vector<uint32_t> dkb(n), dke(n);
+  for (uint64_t j = 0; j < n;) {
+    uint64_t e = j + 1;
+    while (e < n && fp.dkey[fp.perm[e]] == fp.dkey[fp.perm[j]]) e++;
+    for (uint64_t m = j; m < e; m++) {
+      dkb[fp.perm[m]] = uint32_t(j);
+      dke[fp.perm[m]] = uint32_t(e);
+    }
+    j = e;
+  }
+  for (int k : {15, 16})
+    if (!grow(k, n * 4, err) ||
+        (n && !ok(hipMemcpy(bufs_[k], (k == 15 ? dkb : dke).data(), n * 4, hipMemcpyHostToDevice), "hipMemcpy(dedup keys)",
+                  err)))
+      return false;
   if (!grow(5, (n + 3) & ~3ull, err) ||
       (n && !ok(hipMemcpy(bufs_[5], fl.data(), n, hipMemcpyHostToDevice), "hipMemcpy(filter flags)", err)))
     return false;
@@ -709,18 +700,6 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
     }
     if (!grow(18, words * 4, err)) return false;
   }
-  if (any_dup_ && !grow(23, 16, err)) return false;
-  // dedup table: 2^k >= 2 x the pairs that can enter it (load <= 0.5, probes end)
-  uint64_t tcap = 0;
-  unsigned long long dup_n = 0;
-  if (any_dup_) {
-    if (!ok(hipMemsetAsync(bufs_[23], 0, 8, st), "memset(dup count)", err)) return false;
-    hipLaunchKernelGGL(filter_count_dup, dim3(blocks), dim3(kBlock), 0, st, pkg, as<const uint8_t>(bufs_[5]), n,
-                       as<unsigned long long>(bufs_[23]));
-    if (!ok(hipGetLastError(), "filter_count_dup", err) ||
-        !ok(hipMemcpyAsync(&dup_n, bufs_[23], 8, hipMemcpyDeviceToHost, st), "D2H dup count", err))
-      return false;
-  }
   // staging layout: per phase a rank table, then per list subject / id / prec columns (4 B
   // each); phase 0 = the ignore lists (filter_mark needs their hash set), phase 1 = VEX
   // (its host copy runs on a helper thread from here on, its upload is queued behind
@@ -780,14 +759,6 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   copy_jobs(jobs[0]);
   if (!upload(0)) return false;
   mark("staged ignore lists");
-  mark("dup sync");
-  if (any_dup_) {
-    if (!ok(hipStreamSynchronize(st), "filter sync", err)) return false;
-    if (dup_n) {
-      tcap = 16;
-      while (tcap < 2 * dup_n) tcap <<= 1;
-    }
-  }
   uint64_t rcap = 0;
   if (nr) {
     rcap = 16;
@@ -802,8 +773,7 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
           "hipcub scan sizing", err))
     return false;
   if (!grow(12, n * 4, err) || !grow(13, n * 4, err) || (has_ign && !grow(14, n * 4, err)) ||
-      (tcap && (!grow(15, n * 4, err) || !grow(16, tcap * 16, err))) || (rcap && !grow(17, rcap * 16, err)) ||
-      !grow(21, n * 8, err) || !grow(24, n, err) || !grow(25, (n / 64 + 1) * 4 * kClasses, err) ||
+      (rcap && !grow(17, rcap * 16, err)) || !grow(21, n * 8, err) || !grow(24, n, err) ||
       (has_ign && !grow(22, n * 12, err)) || !grow(23, std::max<uint64_t>(scan_bytes, 16), err) ||
       !grow(26, 16, err))
     return false;
@@ -819,8 +789,7 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   if (rules.pkg_class &&
       !ok(hipMemcpyAsync(bufs_[20], rules.pkg_class, np * 4, hipMemcpyHostToDevice, st), "H2D classes", err))
     return false;
-  if ((tcap && !ok(hipMemsetAsync(bufs_[16], 0, tcap * 16, st), "memset(dedup table)", err)) ||
-      !ok(hipMemsetAsync(bufs_[6], 0, np * 4 * (kClasses + 1), st), "memset(counters)", err))
+  if (!ok(hipMemsetAsync(bufs_[6], 0, np * 4 * (kClasses + 1), st), "memset(counters)", err))
     return false;
   FilterArgs a{};
   a.t = t;
@@ -834,6 +803,8 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   a.grp_e = as<const uint32_t>(bufs_[2]);
   a.dkey = as<const uint32_t>(bufs_[3]);
   a.prank = as<const uint32_t>(bufs_[4]);
+  a.dk_b = as<const uint32_t>(bufs_[15]);
+  a.dk_e = as<const uint32_t>(bufs_[16]);
   a.dup = as<const uint8_t>(bufs_[5]);
   a.pkg_class = as<const uint32_t>(bufs_[20]);
   a.cnt = as<uint32_t>(bufs_[6]);
@@ -846,14 +817,10 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   a.mkey = as<uint32_t>(bufs_[12]);
   a.skey = as<uint32_t>(bufs_[13]);
   a.ign = as<uint32_t>(bufs_[14]);
-  a.mine = as<uint32_t>(bufs_[15]);
   a.pcls = as<uint8_t>(bufs_[24]);
-  a.wcarry = as<uint32_t>(bufs_[25]);
   a.rules = as<const unsigned long long>(bufs_[17]);
   a.rule_mask = rcap ? rcap - 1 : 0;
   a.kinds = nv ? rules.kinds : rules.kinds & ~(1u << RULE_VEX);  // (empty VEX lists: nothing to test)
-  a.table = as<unsigned long long>(bufs_[16]);
-  a.table_mask = tcap ? tcap - 1 : 0;
   a.sev_mask = sev_mask;
   a.status_mask = status_mask;
   a.id_bits = id_bits;
@@ -867,8 +834,8 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   mark("vex staged");
   if (nv) hipLaunchKernelGGL(vex_mark, dim3(uint32_t((nv + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, vd, pkg, side,
                              as<const uint32_t>(bufs_[8]), as<const uint32_t>(bufs_[9]), as<const uint8_t>(bufs_[7]), n,
-                             uint32_t(np), uint32_t(rules.rank[1].size()), a.skey, a.pcls, as<uint32_t>(bufs_[26]));
-  hipLaunchKernelGGL(filter_count, dim3(blocks), dim3(kBlock), 0, st, a);
+                             uint32_t(np), uint32_t(rules.rank[1].size()), a.skey, a.pcls, a.cnt, a.surv,
+                             as<uint32_t>(bufs_[26]));
   if (!ok(hipGetLastError(), "filter launch", err) ||
       !ok(hipcub::DeviceScan::ExclusiveSum(bufs_[23], scan_bytes, In(Count(0), GroupCount{a.perm, a.surv, uint32_t(np)}),
                                            as<uint32_t>(bufs_[10]), int(np + 1), st),

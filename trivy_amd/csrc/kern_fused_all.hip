@@ -13,13 +13,12 @@ const FusedFn* fused_table_ALL_p1();
 const FusedFn* fused_table_ALL_p2();
 const FusedFn* fused_table_ALL_p3();
 const FusedFn* fused_table_ALL_p4();
-const FusedFn* fused_table_ALL_p5();
 
 const FusedFn* fused_table_ALL() {
   static const std::vector<FusedFn> t = [] {
     std::vector<FusedFn> v(kNumTuned, nullptr);
     for (const FusedFn* part : {fused_table_ALL_p0(), fused_table_ALL_p1(), fused_table_ALL_p2(), fused_table_ALL_p3(),
-                                fused_table_ALL_p4(), fused_table_ALL_p5()}) {
+                                fused_table_ALL_p4()}) {
       for (int i = 0; i < kNumTuned; i++)
         if (part[i]) v[i] = part[i];
     }

@@ -1,13 +1,13 @@
 // One piece of the all-grammar fused_kernel table (kern_fused_all.hip): the variants of part
 // TVM_ALL_PART, nullptr elsewhere.  Parts: 0 fused K=4, 1 fused K=2, 2 fused K=1, 3 per-wave
-// sweep segments, 4 per-wave staging + segments, 5 its persistent form (match_variants.h F / K).
+// sweep segments, 4 per-wave staging + segments (match_variants.h F / K).
 #include "match_kernel.h"
 #include "match_variants.h"
 
 namespace tvm {
 namespace {
 constexpr int fused_all_part(int F, int K) {
-  return F == 1 ? (K == 4 ? 0 : K == 2 ? 1 : 2) : F == 4 ? 3 : F == 5 ? 4 : F == 6 ? 5 : 6 + F;
+  return F == 1 ? (K == 4 ? 0 : K == 2 ? 1 : 2) : F == 4 ? 3 : F == 5 ? 4 : 5 + F;
 }
 template <int F, int K, int MB>
 constexpr FusedFn fused_all_entry() {

@@ -88,6 +88,7 @@ struct FusedArgs {
   SweepArgs sa;
   CopyOutArgs co;       // end-to-end pipeline: the previous chunk's result move ...
   uint32_t n_copy = 0;  // ... by workgroups [0, n_copy) of this launch (0: none)
+  const uint32_t* tile_map = nullptr;  // workgroup -> tile (DevBatch::tile_map; no result move)
 };
 
 using ProbeFn = void (*)(uint32_t n_tiles, hipStream_t st, const ProbeArgs& a);
@@ -906,7 +907,8 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
       return;
     }
   }
-  const uint32_t tid = threadIdx.x, t = blockIdx.x - (MOVE ? fa.n_copy : 0u);
+  const uint32_t tid = threadIdx.x;
+  const uint32_t t = MOVE ? blockIdx.x - fa.n_copy : (fa.tile_map ? fa.tile_map[blockIdx.x] : blockIdx.x);
   const uint32_t p = t * kTile + tid;
   uint2 d = make_uint2(0xFFFFFFFFu, 0);
   if (p < a.n) d = a.pk[p];
@@ -956,122 +958,6 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
   sweep_tile<K, MB, FILT, SEG>(fa.sa, s, madv, reinterpret_cast<uint8_t*>(madv + MB), map, t, tid, r, dq);
 }
 
-// Persistent form of the per-wave-staging fused kernel (SEG = 3): a workgroup takes tiles
-// t = blockIdx.x, + gridDim.x, ... and, while it sweeps tile t, already has the loads of tile
-// t + gridDim.x in flight - its package words, group offsets and string window go to
-// registers behind the probe -> sweep barrier and are stored to LDS at the next iteration's
-// start.  The one-tile form waits on that chain (descriptor -> offsets -> window) at every
-// tile's start with nothing of its own to overlap it.
-template <uint32_t GM, int K, int MB, int FILT, uint32_t STG = kStage>
-__global__ __launch_bounds__(kTile) void fused_pf_kernel(FusedArgs fa) {
-  constexpr int SEG = 3;
-  constexpr uint32_t kStageVec = STG / 16 + 8;
-  constexpr uint32_t kMbufVec = (MB * 5 + 15) / 16;
-  constexpr uint32_t SV = (STG / 4 / 16 + 63) / 64;  // window words per lane
-  __shared__ uint4 buf[kStageVec > kMbufVec ? kStageVec : kMbufVec];
-  struct SweepPart {
-    SweepShared<FILT> s;
-    uint8_t map[kMapCap];
-  };
-  struct ProbePart {
-    uint32_t kbuf[kTile * kFastKeyStride / 4];
-    uint8_t tab[128];
-  };
-  static_assert(sizeof(ProbePart) <= sizeof(SweepPart), "the probe's LDS fits in the sweep's");
-  __shared__ union {
-    SweepPart sw;
-    ProbePart pr;
-  } u;
-  SweepShared<FILT>& s = u.sw.s;
-  uint8_t* map = u.sw.map;
-  const ProbeArgs& a = fa.pa;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t n_tiles = fa.sa.n_tiles;
-  uint4* const sbuf = buf + wave * (STG / 4 / 16 + 2);
-  // the next tile's loads (issued a tile ahead)
-  uint2 d_nx = make_uint2(0xFFFFFFFFu, 0);
-  uint64_t w0_nx = 0, w1_nx = 0;
-  uint4 v_nx[SV];
-  auto fetch = [&](uint32_t tt) {
-    const uint32_t pp = tt * kTile + tid;
-    d_nx = pp < a.n ? a.pk[pp] : make_uint2(0xFFFFFFFFu, 0);
-    const uint32_t g = tt * kGroupsPerTile + wave;
-    w0_nx = a.tile_off[g];
-    w1_nx = a.tile_off[g + 1];
-    const uint64_t b16 = w0_nx & ~uint64_t(15);
-    const uint32_t nv = w1_nx - b16 <= STG / 4 ? uint32_t((w1_nx - b16 + 15) / 16) : 0u;
-    const uint4* src = reinterpret_cast<const uint4*>(a.arena + b16);
-#pragma unroll
-    for (uint32_t k = 0; k < SV; k++) v_nx[k] = nv ? src[min(lane + k * 64, nv - 1)] : make_uint4(0, 0, 0, 0);
-  };
-  uint32_t t = blockIdx.x;
-  if (t < n_tiles) fetch(t);
-  for (; t < n_tiles; t += gridDim.x) {
-    const uint32_t p = t * kTile + tid;
-    const uint2 d = d_nx;
-    const uint64_t w0 = w0_nx, w1 = w1_nx;
-    const uint32_t nlen = d.y & 0xFFFFu, vlen = d.y >> 16;
-    const uint64_t base16 = w0 & ~uint64_t(15);
-    const bool staged = w1 - base16 <= STG / 4;
-    const uint32_t off = wave_exscan(nlen + vlen, lane);
-    if (staged) {
-      const uint32_t nv = uint32_t((w1 - base16 + 15) / 16);
-#pragma unroll
-      for (uint32_t k = 0; k < SV; k++)
-        if (lane + k * 64 < nv) sbuf[lane + k * 64] = v_nx[k];
-      if (lane < 2) sbuf[nv + lane] = make_uint4(0, 0, 0, 0);
-    }
-    if (tid < 128) u.pr.tab[tid] = deb_fast_code(tid);
-    __syncthreads();  // the code table (and the previous tile's sweep state is dead)
-    PkgRec r;
-    r.meta = make_uint4(0, 0, 0, 0);
-    r.k0 = r.k1 = 0;
-    if (p < a.n && d.x < a.db.n_plats) {
-      if (staged) {
-        const uint8_t* sb = reinterpret_cast<const uint8_t*>(sbuf) + uint32_t(w0 - base16) + off;
-        probe_one<GM, uint32_t, 0>(a, p, d.x, nlen, vlen, sb, sb + nlen, w0 + off + nlen, r,
-                                   reinterpret_cast<uint8_t*>(u.pr.kbuf) + tid * kFastKeyStride, u.pr.tab);
-      } else {
-        const uint8_t* gb = a.arena + w0 + off;
-        probe_one<GM, uint32_t, 0>(a, p, d.x, nlen, vlen, gb, gb + nlen, w0 + off + nlen, r);
-      }
-    }
-    __syncthreads();  // the strings are dead: buf becomes the match buffer
-    if (t + gridDim.x < n_tiles) fetch(t + gridDim.x);  // in flight during the sweep
-    uint32_t* madv = reinterpret_cast<uint32_t*>(buf);
-    constexpr uint32_t kBufWords = sizeof(buf) / 4, kMbWords = (uint32_t(MB) * 5 + 3) / 4;
-    constexpr uint32_t kQ = kBufWords > kMbWords + kTile / 8 + 16 ? kBufWords - kMbWords - kTile / 8 : 0;
-    static_assert(FILT < 2 || kQ >= 16, "no room for the Maven program queue");
-    const DeferQ dq{madv + kMbWords + kTile / 8, madv + kMbWords, FILT >= 2 ? kQ : 0u};
-    sweep_tile<K, MB, FILT, SEG>(fa.sa, s, madv, reinterpret_cast<uint8_t*>(madv + MB), map, t, tid, r, dq);
-    __syncthreads();  // the sweep's LDS (match buffer, map) is read until its last store
-  }
-}
-
-// Workgroups of a persistent launch: every CU full at the kernel's occupancy (measured once).
-template <class KernelT>
-uint32_t persistent_grid(KernelT kernel, uint32_t n_tiles) {
-  static const uint32_t slots = [kernel] {
-    int dev = 0, cus = 0, per = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, kTile, 0);
-    return uint32_t(std::max(1, cus) * std::max(1, per));
-  }();
-  return std::max<uint32_t>(1, std::min(n_tiles, slots));
-}
-
-template <uint32_t GM, int K, int MB, int FILT>
-void launch_fused_pf(uint32_t n_tiles, hipStream_t st, const FusedArgs& a) {
-  if (a.n_copy) {  // a pipeline chunk with a result move: the one-tile form carries it
-    hipLaunchKernelGGL((fused_kernel<GM, K, MB, FILT, 0, 1, 3, kStage, true>), dim3(n_tiles + a.n_copy), dim3(kTile), 0,
-                       st, a);
-    return;
-  }
-  const uint32_t grid = persistent_grid(fused_pf_kernel<GM, K, MB, FILT>, n_tiles);
-  hipLaunchKernelGGL((fused_pf_kernel<GM, K, MB, FILT>), dim3(grid), dim3(kTile), 0, st, a);
-}
-
 template <uint32_t GM, int DIAG = 0>
 void launch_probe(uint32_t n_tiles, hipStream_t st, const ProbeArgs& a) {
   hipLaunchKernelGGL((probe_kernel<GM, DIAG>), dim3(n_tiles), dim3(kTile), 0, st, a);
@@ -1099,7 +985,6 @@ constexpr FusedFn fused_entry() {
   if constexpr (F == 0) return nullptr;
   else if constexpr (F == 4) return &launch_fused<GM, K, MB, FILT, 0, 1, 1>;
   else if constexpr (F == 5) return &launch_fused<GM, K, MB, FILT, 0, 1, 3>;
-  else if constexpr (F == 6) return &launch_fused_pf<GM, K, MB, FILT>;
   // the all-grammar K <= 2 kernels are held at 5 waves per SIMD (96 VGPRs): the Maven program
   // queue (sweep_programs) took them to 97 and 4 waves
   else return &launch_fused<GM, K, MB, FILT, (F >= 10 ? F - 10 : 0), (FILT >= 2 && K <= 2 && F == 1) ? 5 : TVM_FUSED_WPE(F)>;

@@ -12,8 +12,7 @@
   X(0, 2, 2048, "split_k2_m2048")      \
   X(0, 4, 2048, "split_k4_m2048")      \
   X(4, 4, 2400, "fused_k4_m2400_seg")  \
-  X(5, 4, 2400, "fused_k4_m2400_wseg")  \
-  X(6, 4, 2400, "fused_k4_m2400_wseg_pf")
+  X(5, 4, 2400, "fused_k4_m2400_wseg")
 
 // Measurement-only variants (wrong match lists by construction): built only with
 // `make DIAG=1` (-DTVM_DIAG), never reachable in the product library.
@@ -28,7 +27,8 @@
 #define TVM_MATCH_VARIANTS(X) TVM_MATCH_VARIANTS_PRODUCT(X)
 #endif
 
-// F = 6: the F = 5 kernel persistent, loading the next tile during the sweep (fused_pf_kernel).
+// Measured and dropped (round 5): F = 5 as a persistent kernel that loads the next tile's package
+// words, offsets and string window during the sweep - C2 0.467 -> 0.634 ms, C5 2.39 -> 4.53 ms.
 // Fused F = 2 / 3: the same kernel compiled for at least 6 / 8 waves per SIMD (register cap;
 // measured within 1 % on C2, rounds 2-3, not in the list any more).
 #define TVM_FUSED_WPE(F) ((F) == 2 ? 6 : (F) == 3 ? 8 : 1)

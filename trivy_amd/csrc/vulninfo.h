@@ -241,8 +241,8 @@ class BatchFilter {
   bool set_packages(const FilterPackages& fp, std::string& err);
   bool has_packages() const { return n_pkgs_ != 0; }
   void reset_packages() { n_pkgs_ = 0; }
-  // Filters the n device pairs (with their FillInfo decisions) on `st`; synchronises once
-  // (twice when packages repeat) to learn the counts.
+  // Filters the n device pairs (with their FillInfo decisions) on `st`; synchronises once, at
+  // the end, to learn the counts.
   bool run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv, const uint2* side, uint64_t n,
            const FilterRules& rules, uint32_t n_ranks, uint32_t sev_mask, uint32_t status_mask, hipStream_t st,
            std::string& err);
@@ -258,7 +258,6 @@ class BatchFilter {
   void* bufs_[kBufs] = {};
   uint64_t caps_[kBufs] = {};
   uint64_t n_ = 0, survivors_ = 0, ignored_ = 0, n_pkgs_ = 0;
-  bool any_dup_ = false;
   void* pin_ = nullptr;  // pinned staging of the per-call rule upload
   uint64_t pin_cap_ = 0;
   bool grow(int i, uint64_t need, std::string& err);
