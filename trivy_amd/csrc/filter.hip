@@ -65,11 +65,25 @@ constexpr uint32_t kEmpty = 0xFFFFFFFFu;       // key of a dropped pair / no pre
 constexpr unsigned long long kNoKey = ~0ull;   // empty rule-table slot
 constexpr int kClasses = 6;                    // per-package counters: survivors of severity 0..4, ignored
 constexpr int kIgnClass = 5;
+constexpr int kCntStride = 8;                  // words per package counter record (32 B: whole-sector stores)
 constexpr int kNoClass = 7;
 constexpr int kChunkBits = 10;                 // packed in-chunk counters (chunk = kBlock pairs)
 // Per-package flag bits: static (set_packages) FL_DUP / FL_SINGLE, per call FL_UNS (mark),
 // FL_PKG / FL_VEX (rules_insert: the package has per-package rules, probe only those).
 enum : uint32_t { FL_DUP = 1, FL_UNS = 2, FL_PKG = 4, FL_VEX = 8, FL_SINGLE = 16 };
+
+// filter_select and filter_place work in chunks of kSpan pairs (select: kUS pairs per lane,
+// place: kP); a package whose run crosses a chunk boundary leaves an edge record per chunk,
+// which filter_edges turns into its counters and the chunks' entering-run carries.
+constexpr int kUS = 4;
+constexpr uint32_t kSpan = uint32_t(kUS) * kBlock;
+// Edge record of a chunk: the package entering it (run started before the chunk) and the
+// package leaving it (run goes on past its end), with their classes inside the chunk; a
+// package spanning the whole chunk is both (in == out, counts in c_in).
+struct Edge {
+  uint32_t p_in, p_out;
+  uint32_t c_in[kClasses], c_out[kClasses];
+};
 
 // Sets flag bits of package p in a byte array padded to whole words (word atomics).
 __device__ __forceinline__ void set_flag(uint8_t* fl, uint32_t p, uint32_t bits) {
@@ -97,7 +111,7 @@ struct FilterArgs {
   uint8_t* fl;         // per-call flags (FL_*), seeded from the static ones
   uint32_t* run_b;     // the package's pairs are [run_b, run_e) of the list
   uint32_t* run_e;
-  uint32_t* cnt;       // kClasses counters per package
+  uint32_t* cnt;       // kClasses counters per package (records of kCntStride words)
   uint32_t* surv;      // per package: its survivors (counters 0..4 summed), what the placement scan reads
   const uint32_t* off;      // survivor offset of perm position j (exclusive scan)
   const uint32_t* ign_off;  // ignored offset of package p
@@ -113,6 +127,10 @@ struct FilterArgs {
   uint32_t sev_mask, status_mask, id_bits;
   uint2* out;      // survivors in report order
   uint32_t* iout;  // ignored {package, advisory, finding} in detection order
+  Edge* edge;      // per select chunk
+  uint32_t* carry_in;  // per chunk, kClasses: the entering run's classes before the chunk
+  uint32_t diag;   // TVM_FILTER_DIAG (measurement): bit 0 no counters in select, bit 1 no dedup,
+                   // bit 5 no slow placements, bit 6 no entering-run carry
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t h) {
@@ -187,7 +205,8 @@ __global__ __launch_bounds__(kBlock) void rules_insert(RuleDev r, unsigned long 
 __global__ __launch_bounds__(kBlock) void vex_mark(RuleDev r, const uint32_t* pkg, const uint2* side,
                                                    const uint32_t* run_b, const uint32_t* run_e, const uint8_t* fl,
                                                    uint64_t n, uint32_t n_pkgs, uint32_t n_ids, uint32_t* skey,
-                                                   uint8_t* pcls, uint32_t* cnt, uint32_t* surv, uint32_t* bad) {
+                                                   uint8_t* pcls, uint32_t* cnt, uint32_t* surv, uint32_t* carry_in,
+                                                   uint32_t* bad) {
   const uint64_t g = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
   int k = 0;
   while (k < r.n_lists && g >= r.end[k]) k++;
@@ -205,8 +224,11 @@ __global__ __launch_bounds__(kBlock) void vex_mark(RuleDev r, const uint32_t* pk
   const uint32_t re = run_e[p];  // written by this call's filter_mark, as rb was
   auto drop = [&](uint32_t j) {
     if (skey[j] != kEmpty) {  // a survivor (so not ignored): it leaves every counter class
-      atomicSub(&cnt[uint64_t(p) * kClasses + pcls[j]], 1u);
+      const uint32_t c = pcls[j];
+      atomicSub(&cnt[uint64_t(p) * kCntStride + c], 1u);
       atomicSub(&surv[p], 1u);
+      // and the entering-run carries of the later chunks its run reaches (filter_place)
+      for (uint64_t h = j / kSpan + 1; h * kSpan < re; h++) atomicSub(&carry_in[h * kClasses + c], 1u);
       skey[j] = kEmpty;
       pcls[j] = uint8_t(kNoClass);
     }
@@ -311,27 +333,47 @@ __device__ __forceinline__ bool beaten_by(const FilterArgs& a, uint32_t q, uint3
   return false;
 }
 
+// A package's counter record (every class, zeros included: whole 32-B sectors) and its
+// survivor sum.
+__device__ __forceinline__ void store_counts(const FilterArgs& a, uint32_t p, const uint32_t* cc, uint32_t sum) {
+  uint4* o = reinterpret_cast<uint4*>(a.cnt + uint64_t(p) * kCntStride);
+  o[0] = make_uint4(cc[0], cc[1], cc[2], cc[3]);
+  o[1] = make_uint4(cc[4], cc[5], 0u, 0u);
+  a.surv[p] = sum;
+}
+
+// LDS slots of filter_select's split runs: one per 64-pair segment boundary of the chunk
+// (+ the chunk's start): classes, survivor sum, package.
+constexpr int kSlots = kUS * (kBlock / 64) + 1;
+
 __global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
-  const uint64_t stride = uint64_t(gridDim.x) * kBlock * kU;
+  __shared__ uint32_t lslot[kSlots][kClasses + 2];
+  if (threadIdx.x < kSlots) {
+#pragma unroll
+    for (int c = 0; c < kClasses + 1; c++) lslot[threadIdx.x][c] = 0;
+    lslot[threadIdx.x][kClasses + 1] = kEmpty;
+  }
+  __syncthreads();
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock * kUS;
   const uint32_t id_mask = (1u << a.id_bits) - 1u;
   const uint64_t n = a.n;
   const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t b0 = uint64_t(blockIdx.x) * kBlock * kU; b0 < n; b0 += stride) {  // wave-uniform trip count
-    uint32_t pv[kU], kv[kU], fv[kU], pe[kU], ne[kU];
+  for (uint64_t b0 = uint64_t(blockIdx.x) * kBlock * kUS; b0 < n; b0 += stride) {  // wave-uniform trip count
+    uint32_t pv[kUS], kv[kUS], fv[kUS], pe[kUS], ne[kUS];
 #pragma unroll
-    for (int k = 0; k < kU; k++) {
+    for (int k = 0; k < kUS; k++) {
       const uint64_t i = min(b0 + uint64_t(k) * kBlock + threadIdx.x, n - 1);
       pv[k] = a.pkg[i];
       kv[k] = a.mkey[i];
       // the packages just before and after this wave's 64 pairs (edge lanes)
       const uint64_t s0 = b0 + uint64_t(k) * kBlock + (threadIdx.x & ~63u);
-      pe[k] = (lane == 0 && s0 > 0 && s0 - 1 < n) ? a.pkg[s0 - 1] : 0xFFFFFFFFu;
-      ne[k] = (lane == 63 && s0 + 64 < n) ? a.pkg[s0 + 64] : 0xFFFFFFFFu;
+      pe[k] = (lane == 0 && s0 > 0 && s0 - 1 < n && !(a.diag & 16)) ? a.pkg[s0 - 1] : 0xFFFFFFFFu;
+      ne[k] = (lane == 63 && s0 + 64 < n && !(a.diag & 16)) ? a.pkg[s0 + 64] : 0xFFFFFFFFu;
     }
 #pragma unroll
-    for (int k = 0; k < kU; k++) fv[k] = a.fl[pv[k]];
+    for (int k = 0; k < kUS; k++) fv[k] = a.fl[pv[k]];
 #pragma unroll
-    for (int k = 0; k < kU; k++) {
+    for (int k = 0; k < kUS; k++) {
       const uint64_t i = b0 + uint64_t(k) * kBlock + threadIdx.x;
       const bool valid = i < n;
       uint32_t p = valid ? pv[k] : 0xFFFFFFFFu, key = valid ? kv[k] : kEmpty;
@@ -343,13 +385,13 @@ __global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
           const bool dup = f & FL_DUP, uns = f & FL_UNS;
           // the FixedVersion rank is needed only to dedup (repeating packages, unsorted runs)
           const uint32_t fr = (dup || uns) ? a.t.adv_rank[a.adv[i]].y : 0u;
-          if (dup) {  // another package of the dedup key with a greater FixedVersion, or an equal one seen first
+          if (dup && !(a.diag & 2)) {  // another package of the dedup key with a greater FixedVersion, or an equal one seen first
             for (uint32_t j = a.dk_b[p], je = a.dk_e[p]; j < je && key != kEmpty; j++) {
               const uint32_t q = a.perm[j];
               if (q != p && beaten_by(a, q, vr, fr, q < p)) key = kEmpty;
             }
           }
-          if (key != kEmpty && uns) {  // the package's own pairs of this ID: the first with the greatest FixedVersion
+          if (key != kEmpty && uns && !(a.diag & 2)) {  // the package's own pairs of this ID: the first with the greatest FixedVersion
             const uint32_t rb = a.run_b[p], re = a.run_e[p];
             for (uint32_t j = rb; j < re; j++) {
               if (j == uint32_t(i)) continue;
@@ -367,9 +409,12 @@ __global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
         cls = pair_class(a, key, i);
         a.pcls[i] = uint8_t(cls);  // placed by filter_place
       }
-      // per-package class counters over the wave's 64 pairs: the first lane of each package
-      // counts its lanes' classes with six ballots; a package all inside these 64 pairs stores
-      // its counters, one that goes on before or after them adds its share atomically
+      // per-package class counters over the wave's 64 pairs (segment g = k * 4 + wave of the
+      // chunk): the first lane of each package counts its lanes' classes with six ballots; a
+      // package all inside the segment stores its record, one that goes on before or after it
+      // adds its share to the chunk's LDS slot of the first segment boundary its run crosses
+      // (0: the chunk's start), flushed below
+      if (a.diag & 1) continue;
       const uint32_t up = __shfl_up(p, 1, 64);
       const bool head = valid && (lane == 0 || up != p);
       const unsigned long long heads = __ballot(head);
@@ -382,22 +427,78 @@ __global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
       const uint32_t next = __shfl(ne[k], 63, 64);
       if (head) {
         const bool split = (lane == 0 && pe[k] == p) || (end == 64 && next == p);
-        uint32_t* o = a.cnt + uint64_t(p) * kClasses;
         const uint32_t sum = cc[0] + cc[1] + cc[2] + cc[3] + cc[4];
         if (split) {
+          const uint32_t rb = a.run_b[p];
+          const uint32_t slot = rb < b0 ? 0u : uint32_t((rb - b0) >> 6) + 1u;
+          uint32_t* o = lslot[slot];
 #pragma unroll
           for (int c = 0; c < kClasses; c++)
             if (cc[c]) atomicAdd(&o[c], cc[c]);
-          if (sum) atomicAdd(&a.surv[p], sum);
+          if (sum) atomicAdd(&o[kClasses], sum);
+          o[kClasses + 1] = p;
         } else {
-#pragma unroll
-          for (int c = 0; c < kClasses; c++)
-            if (cc[c]) o[c] = cc[c];
-          if (sum) a.surv[p] = sum;
+          store_counts(a, p, cc, sum);
         }
       }
     }
+    // the slots: a run inside this chunk stores its record; the chunk's edge record takes the
+    // run that enters it (slot 0) and the one that goes on past its end (filter_edges adds
+    // them up, no atomics)
+    __syncthreads();
+    const uint64_t be = min(b0 + uint64_t(kSpan), n);
+    Edge* e = a.edge + b0 / kSpan;
+    if (threadIdx.x < kSlots) {
+      uint32_t* o = lslot[threadIdx.x];
+      const uint32_t p = o[kClasses + 1];
+      const bool leaves = p != kEmpty && a.run_e[p] > be;
+      if (p != kEmpty) {
+        if (threadIdx.x == 0 || leaves) {
+          uint32_t* c = (threadIdx.x == 0) ? e->c_in : e->c_out;
+#pragma unroll
+          for (int k = 0; k < kClasses; k++) c[k] = o[k];
+          if (threadIdx.x == 0) e->p_in = p;
+          if (leaves) e->p_out = p;
+        } else {
+          uint32_t cc[kClasses];
+#pragma unroll
+          for (int k = 0; k < kClasses; k++) cc[k] = o[k];
+          store_counts(a, p, cc, o[kClasses]);
+        }
+      } else if (threadIdx.x == 0) {
+        e->p_in = kEmpty;
+      }
+      // the chunk's last pair's package: no slot leaves when it ends inside the chunk
+      if (threadIdx.x == 1 && (be == n || a.pkg[be - 1] != a.pkg[be])) e->p_out = kEmpty;
+#pragma unroll
+      for (int c = 0; c < kClasses + 1; c++) o[c] = 0;
+      o[kClasses + 1] = kEmpty;
+    }
+    __syncthreads();
   }
+}
+
+// Runs that cross chunk boundaries: from the chunk where such a run starts, its classes are
+// added up over the chunks it spans (their edge records), each of those chunks gets the
+// classes before it (carry_in, filter_place's entering run), and the total is the package's
+// counter record.  One thread per chunk; a run of L pairs walks L / kSpan records.
+__global__ __launch_bounds__(kBlock) void filter_edges(FilterArgs a, uint32_t n_chunks) {
+  const uint32_t g = blockIdx.x * kBlock + threadIdx.x;
+  if (g >= n_chunks) return;
+  const uint32_t p = a.edge[g].p_out;
+  if (p == kEmpty || a.edge[g].p_in == p) return;  // no run starts in this chunk and leaves it
+  uint32_t acc[kClasses];
+#pragma unroll
+  for (int c = 0; c < kClasses; c++) acc[c] = a.edge[g].c_out[c];
+  for (uint32_t h = g + 1; h < n_chunks; h++) {  // edge[h].p_in == p
+#pragma unroll
+    for (int c = 0; c < kClasses; c++) {
+      a.carry_in[uint64_t(h) * kClasses + c] = acc[c];
+      acc[c] += a.edge[h].c_in[c];
+    }
+    if (a.edge[h].p_out != p) break;  // the run ends in chunk h
+  }
+  store_counts(a, p, acc, acc[0] + acc[1] + acc[2] + acc[3] + acc[4]);
 }
 
 // Number of keys in the run [rb, re) below key (or at most key).
@@ -419,140 +520,191 @@ __device__ __forceinline__ uint32_t chunk_field(unsigned long long v, uint32_t c
   return uint32_t(v >> (kChunkBits * cls)) & ((1u << kChunkBits) - 1u);
 }
 
-__global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
-  __shared__ unsigned long long pre[kBlock];   // exclusive packed class counts of the chunk
-  __shared__ unsigned long long wsum[kBlock / 64];
-  __shared__ uint32_t carry[kClasses];         // classes of the entering run before the chunk
-  __shared__ uint32_t base[kBlock][kClasses];  // at a package's first lane in the chunk: its bases
-  __shared__ uint32_t pflag[kBlock];           //   and flags (loaded once per package and chunk)
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
-  // software-pipelined: the next chunk's pair words (and its packages' run starts) are loaded
-  // while this chunk waits on its placement bases and barriers
-  uint32_t n_key = kEmpty, n_cls = kNoClass, n_p = 0, n_adv = 0, n_rb = 0, n_fl = 0, n_gb = 0;
-  auto load_pairs = [&](uint64_t c) {
-    const uint64_t j = c + tid;
-    if (j < a.n) {
-      n_key = a.skey[j];
-      n_cls = a.pcls[j];  // pair_class, from filter_select
-      n_p = a.pkg[j];
-      n_adv = a.adv[j];
-    }
-  };
-  {
-    const uint64_t c = uint64_t(blockIdx.x) * kBlock;
-    load_pairs(c);
-    if (c + tid < a.n) {
-      n_rb = a.run_b[n_p];
-      n_fl = a.fl[n_p];
-      n_gb = a.grp_b[n_p];
+// filter_place takes spans of kP chunks (kP * kBlock pairs, pair s0 + k * kBlock + tid):
+// the per-span fixed latency (the entering run's carry, the barriers) is paid once per
+// kP * 256 pairs.  Packed class prefixes over a span stay below 2^10 per field.
+constexpr int kP = 4;
+static_assert(kP * kBlock <= (1 << kChunkBits), "span prefixes fit the packed fields");
+static_assert(kP * kBlock == kSpan, "place spans are select chunks (carry_in)");
+
+// A pair's placement inputs, loaded two steps ahead of its span (pair words, then its
+// package's words, then the package's placement base for the pair's class).
+struct PlacePair {
+  uint32_t p, adv, cf;  // package, advisory, class | flags << 8
+  uint32_t rb, gb;      // package run start, group start
+  uint32_t base;        // the pair's output base (SINGLE survivors / ignored), else unused
+};
+
+// (Every field is written unconditionally from locals: stores of struct fields under branches
+// were merged into address selects, which put the span's pair arrays in scratch memory.)
+__device__ __forceinline__ void place_load_pair(const FilterArgs& a, uint64_t i, PlacePair& q) {
+  uint32_t p = 0, adv = 0, cf = kNoClass;
+  if (i < a.n) {
+    p = a.pkg[i];
+    adv = a.adv[i];
+    cf = a.pcls[i];  // pair_class, from filter_select
+  }
+  q.p = p;
+  q.adv = adv;
+  q.cf = cf;
+}
+__device__ __forceinline__ void place_load_pkg(const FilterArgs& a, uint64_t i, PlacePair& q) {
+  uint32_t rb = 0, fl = 0, gb = 0;
+  if (i < a.n) rb = a.run_b[q.p];  // every pair: lane 0's gives the span's entering run
+  if (i < a.n && (q.cf & 0xFFu) < uint32_t(kClasses)) {
+    fl = a.fl[q.p];
+    gb = a.grp_b[q.p];
+  }
+  q.rb = rb;
+  q.cf |= fl << 8;
+  q.gb = gb;
+}
+__device__ __forceinline__ void place_load_base(const FilterArgs& a, uint64_t i, PlacePair& q) {
+  const uint32_t cls = q.cf & 0xFFu, f = q.cf >> 8;
+  uint32_t base = 0;
+  if (i < a.n && cls == uint32_t(kIgnClass)) {
+    base = a.ign_off[q.p];
+  } else if (i < a.n && cls < uint32_t(kClasses) && (f & (FL_SINGLE | FL_UNS)) == FL_SINGLE) {
+    // ID-sorted run alone in its group: severity desc, then run order (class = severity
+    // index: the package's survivors of the classes above come first)
+    const uint32_t* c = a.cnt + uint64_t(q.p) * kCntStride;
+    const uint4 c03 = *reinterpret_cast<const uint4*>(c);
+    const uint32_t c4 = c[4];
+    base = a.off[q.gb] + (cls < 4 ? c4 : 0u) + (cls < 3 ? c03.w : 0u) + (cls < 2 ? c03.z : 0u) + (cls < 1 ? c03.y : 0u);
+  }
+  q.base = base;
+}
+
+// Output position of a survivor (key) of package p in a group of several packages (same
+// PkgName and InstalledVersion: merged by severity, ID, PkgPath) or with an unsorted run:
+// keys counted over the group's runs.  Rare: filter_place runs it once per lane, after the span.
+__device__ __forceinline__ uint64_t place_slow(const FilterArgs& a, uint32_t p, uint32_t rb, uint32_t key) {
+  const uint32_t gb = a.grp_b[p], ge = a.grp_e[p];
+  uint32_t r = 0;
+  if (ge - gb == 1) {
+    r = count_below(a.skey, rb, a.run_e[p], key, false);
+  } else {
+    const uint32_t pr = a.prank[p];
+    for (uint32_t g = gb; g < ge; g++) {
+      const uint32_t q = a.perm[g];
+      if (q != p && !a.surv[q]) continue;  // no survivors (its run bounds may be stale)
+      r += count_below(a.skey, a.run_b[q], a.run_e[q], key, q != p && a.prank[q] < pr);
     }
   }
-  for (uint64_t c0 = uint64_t(blockIdx.x) * kBlock; c0 < a.n; c0 += stride) {
-    const uint64_t i = c0 + tid;
-    const bool valid = i < a.n;
-    const uint32_t key = valid ? n_key : kEmpty;
-    const uint32_t cls = valid ? n_cls : kNoClass;
-    const uint32_t p = valid ? n_p : 0u;
-    const uint32_t adv = n_adv;
-    const uint32_t rb = valid ? n_rb : 0u;
-    const uint32_t pf = n_fl, gb0 = n_gb;  // the package's flags and group (loaded a chunk ahead)
-    const uint32_t rb0 = __shfl(rb, 0, 64);  // the chunk's first package's run start (wave 0)
-    const uint64_t rs = rb > c0 ? rb : c0;  // the package's first pair in this chunk
-    const bool more = c0 + stride < a.n;
-    if (more) load_pairs(c0 + stride);
-    // block-wide exclusive prefix of the packed one-hot counters (counts <= 256 per field)
-    unsigned long long x = one_hot(cls);
+  return uint64_t(a.off[gb]) + r;
+}
+
+__global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
+  __shared__ unsigned long long pre[kP * kBlock];  // exclusive packed class counts over the span
+  __shared__ unsigned long long wsum[kP * (kBlock / 64)];
+  __shared__ uint32_t carry[kClasses];             // classes of the entering run before the span
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t span = uint64_t(kP) * kBlock;
+  const uint64_t stride = uint64_t(gridDim.x) * span;
+  PlacePair cur[kP], nxt[kP];
+  // prologue: this block's first span fully, the next span's pair words
+  const uint64_t first = uint64_t(blockIdx.x) * span;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned long long y = __shfl_up(x, o, 64);
-      if (lane >= uint32_t(o)) x += y;
-    }
-    if (lane == 63) wsum[wave] = x;
-    // the run entering the chunk: its classes before c0, counted by wave 0 over the shorter
-    // side of the run (before c0, or from c0 on subtracted from the package's totals)
-    if (wave == 0) {
-      uint32_t m = 0;  // lane c < kClasses: class c
-      if (rb0 < c0) {
-        const uint32_t p0 = __shfl(p, 0, 64), re0 = a.run_e[p0];
-        const bool back = c0 - rb0 <= re0 - c0;
-        const uint64_t from = back ? rb0 : c0, to = back ? c0 : re0;
-        for (uint64_t j0 = from; j0 < to; j0 += 64) {  // wave-uniform
-          const uint64_t j = j0 + lane;
-          const uint32_t cj = j < to ? a.pcls[j] : kNoClass;
+  for (int k = 0; k < kP; k++) place_load_pair(a, first + k * kBlock + tid, cur[k]);
 #pragma unroll
-          for (uint32_t c = 0; c < uint32_t(kClasses); c++) {
-            const uint32_t k = uint32_t(__popcll(__ballot(cj == c)));
-            if (lane == c) m += k;
-          }
-        }
-        if (!back && lane < uint32_t(kClasses)) m = a.cnt[uint64_t(p0) * kClasses + lane] - m;
-      }
-      if (lane < uint32_t(kClasses)) carry[lane] = m;
+  for (int k = 0; k < kP; k++) place_load_pkg(a, first + k * kBlock + tid, cur[k]);
+#pragma unroll
+  for (int k = 0; k < kP; k++) place_load_base(a, first + k * kBlock + tid, cur[k]);
+#pragma unroll
+  for (int k = 0; k < kP; k++) place_load_pair(a, first + stride + k * kBlock + tid, nxt[k]);
+  for (uint64_t s0 = first; s0 < a.n; s0 += stride) {  // block-uniform trip count
+    const bool more = s0 + stride < a.n;
+    // the next span's package words (its pair words arrived during this block's last span)
+    if (more) {
+#pragma unroll
+      for (int k = 0; k < kP; k++) place_load_pkg(a, s0 + stride + k * kBlock + tid, nxt[k]);
     }
-    if (valid && i == rs) {  // the package's first lane: its placement bases, once
-      const uint32_t f = pf;
-      pflag[tid] = f;
-      if ((f & (FL_SINGLE | FL_UNS)) == FL_SINGLE) {
-        // ID-sorted run alone in its group: severity desc, then run order
-        uint32_t acc = a.off[gb0];
-        const uint32_t* c = a.cnt + uint64_t(p) * kClasses;
-        for (int sv = 4; sv >= 0; sv--) {
-          base[tid][sv] = acc;
-          acc += c[sv];
-        }
+    // per chunk: wave-inclusive packed one-hot class counts
+    unsigned long long x[kP];
+#pragma unroll
+    for (int k = 0; k < kP; k++) {
+      x[k] = one_hot(cur[k].cf & 0xFFu);
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(x[k], o, 64);
+        if (lane >= uint32_t(o)) x[k] += y;
       }
-      if (a.kinds & 7u) base[tid][kIgnClass] = a.ign_off[p];
+      if (lane == 63) wsum[k * (kBlock / 64) + wave] = x[k];
     }
-    if (more && c0 + stride + tid < a.n) {
-      n_rb = a.run_b[n_p];
-      n_fl = a.fl[n_p];
-      n_gb = a.grp_b[n_p];
+    // the run entering the span: its classes before s0 (filter_edges)
+    const uint32_t rb0 = __shfl(cur[0].rb, 0, 64);
+    if (tid < uint32_t(kClasses)) {
+      carry[tid] = rb0 < s0 && !(a.diag & 64) ? a.carry_in[(s0 / kSpan) * kClasses + tid] : 0u;
     }
     __syncthreads();
-    unsigned long long wbase = 0;
+    unsigned long long run = 0;  // sum of the wave totals before (chunk k, this wave)
 #pragma unroll
-    for (int w = 0; w < kBlock / 64; w++) wbase += (uint32_t(w) < wave) ? wsum[w] : 0ull;
-    pre[tid] = wbase + x - one_hot(cls);
+    for (int k = 0; k < kP; k++) {
+      unsigned long long before_w = 0, total_k = 0;
+#pragma unroll
+      for (int w = 0; w < kBlock / 64; w++) {
+        const unsigned long long t = wsum[k * (kBlock / 64) + w];
+        before_w += (uint32_t(w) < wave) ? t : 0ull;
+        total_k += t;
+      }
+      pre[k * kBlock + tid] = run + before_w + x[k] - one_hot(cur[k].cf & 0xFFu);
+      run += total_k;
+    }
     __syncthreads();
-    if (valid && cls < uint32_t(kClasses)) {
-      const uint32_t h = uint32_t(rs - c0);
+    uint32_t slow = 0;
+#pragma unroll
+    for (int k = 0; k < kP; k++) {
+      const uint64_t i = s0 + k * kBlock + tid;
+      const PlacePair& q = cur[k];
+      const uint32_t cls = q.cf & 0xFFu, f = q.cf >> 8;
+      if (i >= a.n || cls >= uint32_t(kClasses)) continue;
+      const uint64_t rs = q.rb > s0 ? q.rb : s0;  // the package's first pair in this span
       // pairs of this package before pair i that share its class
-      const uint32_t before = chunk_field(pre[tid] - pre[h], cls) + (rb < c0 ? carry[cls] : 0u);
-      const uint32_t f = pflag[h];
+      const uint32_t before =
+          chunk_field(pre[k * kBlock + tid] - pre[rs - s0], cls) + (q.rb < s0 ? carry[cls] : 0u);
       if (cls == uint32_t(kIgnClass)) {  // ModifiedFindings in detection order
-        const uint64_t at = uint64_t(base[h][kIgnClass]) + before;
+        const uint64_t at = uint64_t(q.base) + before;
         if (at < a.n) {
           uint32_t* o = a.iout + 3 * at;
-          o[0] = p;
-          o[1] = adv;
+          o[0] = q.p;
+          o[1] = q.adv;
           o[2] = a.ign[i];
         }
-      } else {
-        uint64_t at;
-        if ((f & (FL_SINGLE | FL_UNS)) == FL_SINGLE) {
-          at = uint64_t(base[h][cls]) + before;
-        } else {
-          const uint32_t gb = a.grp_b[p], ge = a.grp_e[p];
-          uint32_t r = 0;
-          if (ge - gb == 1) {
-            r = count_below(a.skey, rb, a.run_e[p], key, false);
-          } else {  // packages sharing (PkgName, InstalledVersion): merge by (severity, ID, PkgPath)
-            const uint32_t pr = a.prank[p];
-            for (uint32_t g = gb; g < ge; g++) {
-              const uint32_t q = a.perm[g];
-              if (q != p) {
-                if (!a.surv[q]) continue;  // no survivors (its run bounds may be stale)
-              }
-              r += count_below(a.skey, a.run_b[q], a.run_e[q], key, q != p && a.prank[q] < pr);
-            }
-          }
-          at = uint64_t(a.off[gb]) + r;
-        }
-        if (at < a.n) a.out[at] = make_uint2(p, adv);  // always true for a list grouped by package
+        continue;
       }
+      if ((f & (FL_SINGLE | FL_UNS)) != FL_SINGLE) {
+        slow |= 1u << k;  // below, once per lane
+        continue;
+      }
+      const uint64_t at = uint64_t(q.base) + before;
+      if (at < a.n) a.out[at] = make_uint2(q.p, q.adv);  // always true for a list grouped by package
     }
-    __syncthreads();  // pre / carry / base are rewritten by the next chunk
+    if (a.diag & 32) slow = 0;
+    while (slow) {  // the slow placements, one code path (static selects of the lane's pair)
+      const uint32_t k = uint32_t(__builtin_ctz(slow));
+      slow &= slow - 1;
+      uint32_t p = 0, rb = 0, adv = 0;
+#pragma unroll
+      for (int kk = 0; kk < kP; kk++)
+        if (uint32_t(kk) == k) {
+          p = cur[kk].p;
+          rb = cur[kk].rb;
+          adv = cur[kk].adv;
+        }
+      const uint64_t at = place_slow(a, p, rb, a.skey[s0 + k * kBlock + tid]);
+      if (at < a.n) a.out[at] = make_uint2(p, adv);
+    }
+    // the next span: its placement bases (its package words arrived during this span), then
+    // the pair words of the span after it
+    if (more) {
+#pragma unroll
+      for (int k = 0; k < kP; k++) place_load_base(a, s0 + stride + k * kBlock + tid, nxt[k]);
+#pragma unroll
+      for (int k = 0; k < kP; k++) cur[k] = nxt[k];
+#pragma unroll
+      for (int k = 0; k < kP; k++) place_load_pair(a, s0 + 2 * stride + k * kBlock + tid, nxt[k]);
+    }
+    __syncthreads();  // pre / carry are rewritten by the next span
   }
 }
 
@@ -566,7 +718,7 @@ struct GroupCount {
   uint32_t n;
   __host__ __device__ uint32_t operator()(uint32_t j) const {
     if (j >= n) return 0u;
-    if (!perm) return cnt[uint64_t(j) * kClasses + kIgnClass];
+    if (!perm) return cnt[uint64_t(j) * kCntStride + kIgnClass];
     return cnt[perm[j]];
   }
 };
@@ -587,7 +739,7 @@ T* as(void* p) {
 // buffers: 0 perm, 1 grp_b, 2 grp_e, 3 dkey, 4 prank, 5 static flags, 6 counters, 7 flags, 8 run_b,
 // 9 run_e, 10 off, 11 ign_off, 12 mkey, 13 skey, 14 ign, 15 dk_b, 16 dk_e,
 // 17 rule table, 18 rule keys, 19 rule precedences, 20 pkg_class, 21 out pairs,
-// 22 ignored out, 23 scan temp, 24 pair classes, 26 index check
+// 22 ignored out, 23 scan temp, 24 pair classes, 26 index check, 27 chunk edges, 28 chunk carries
 BatchFilter::~BatchFilter() {
   for (void* p : bufs_)
     if (p) (void)hipFree(p);
@@ -645,7 +797,7 @@ bool BatchFilter::set_packages(const FilterPackages& fp, std::string& err) {
     return false;
   for (int k : {8, 9, 20})
     if (!grow(k, n * 4, err)) return false;
-  if (!grow(6, n * 4 * (kClasses + 1), err) || !grow(7, (n + 3) & ~3ull, err) || !grow(10, (n + 1) * 4, err) ||
+  if (!grow(6, n * 4 * (kCntStride + 1), err) || !grow(7, (n + 3) & ~3ull, err) || !grow(10, (n + 1) * 4, err) ||
       !grow(11, (n + 1) * 4, err))
     return false;
   n_pkgs_ = n;
@@ -676,8 +828,10 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
     err = "filter: more than 2^29 vulnerability IDs";
     return false;
   }
-  const uint32_t blocks = uint32_t(std::min<uint64_t>((n + kBlock - 1) / kBlock, 256ull * 64));
+  const uint32_t blocks = uint32_t(std::min<uint64_t>((n + kBlock * kP - 1) / (kBlock * kP), 256ull * 8));
   const uint32_t blocks_u = uint32_t(std::min<uint64_t>((n + kBlock * kU - 1) / (kBlock * kU), 256ull * 32));
+  const uint64_t n_chunks = (n + kSpan - 1) / kSpan;
+  const uint32_t blocks_s = uint32_t(std::min<uint64_t>(n_chunks, 256ull * 32));
   sev_mask &= 0x1Fu;  // SeverityNames only: a bit for "out of range" (5) would pass a severity 4 - 5 can't order
   const uint64_t np = n_pkgs_;
   // The rule lists go up in one pinned copy, staged while the GPU counts repeating pairs.
@@ -775,7 +929,7 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   if (!grow(12, n * 4, err) || !grow(13, n * 4, err) || (has_ign && !grow(14, n * 4, err)) ||
       (rcap && !grow(17, rcap * 16, err)) || !grow(21, n * 8, err) || !grow(24, n, err) ||
       (has_ign && !grow(22, n * 12, err)) || !grow(23, std::max<uint64_t>(scan_bytes, 16), err) ||
-      !grow(26, 16, err))
+      !grow(26, 16, err) || !grow(27, n_chunks * sizeof(Edge), err) || !grow(28, n_chunks * 4 * kClasses, err))
     return false;
   // per-call flags start as the static ones (FL_DUP, FL_SINGLE)
   if (np && !ok(hipMemcpyAsync(bufs_[7], bufs_[5], np, hipMemcpyDeviceToDevice, st), "D2D flags", err)) return false;
@@ -789,7 +943,12 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   if (rules.pkg_class &&
       !ok(hipMemcpyAsync(bufs_[20], rules.pkg_class, np * 4, hipMemcpyHostToDevice, st), "H2D classes", err))
     return false;
-  if (!ok(hipMemsetAsync(bufs_[6], 0, np * 4 * (kClasses + 1), st), "memset(counters)", err))
+  // survivor sums of every package (the placement scan reads them all); filter_select /
+  // filter_edges store every counter record of a package with pairs, so the records are
+  // zeroed only when the ignored findings' scan reads every package's
+  if (!ok(has_ign ? hipMemsetAsync(bufs_[6], 0, np * 4 * (kCntStride + 1), st)
+                  : hipMemsetAsync(static_cast<uint32_t*>(bufs_[6]) + np * kCntStride, 0, np * 4, st),
+          "memset(counters)", err))
     return false;
   FilterArgs a{};
   a.t = t;
@@ -808,7 +967,7 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   a.dup = as<const uint8_t>(bufs_[5]);
   a.pkg_class = as<const uint32_t>(bufs_[20]);
   a.cnt = as<uint32_t>(bufs_[6]);
-  a.surv = as<uint32_t>(bufs_[6]) + np * kClasses;
+  a.surv = as<uint32_t>(bufs_[6]) + np * kCntStride;
   a.fl = as<uint8_t>(bufs_[7]);
   a.run_b = as<uint32_t>(bufs_[8]);
   a.run_e = as<uint32_t>(bufs_[9]);
@@ -826,8 +985,14 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   a.id_bits = id_bits;
   a.out = as<uint2>(bufs_[21]);
   a.iout = as<uint32_t>(bufs_[22]);
+  a.edge = as<Edge>(bufs_[27]);
+  a.carry_in = as<uint32_t>(bufs_[28]);
+  static const uint32_t diag = std::getenv("TVM_FILTER_DIAG") ? uint32_t(std::atoi(std::getenv("TVM_FILTER_DIAG"))) : 0u;
+  a.diag = diag;
   hipLaunchKernelGGL(filter_mark, dim3(blocks_u), dim3(kBlock), 0, st, a);
-  hipLaunchKernelGGL(filter_select, dim3(blocks_u), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(filter_select, dim3(blocks_s), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(filter_edges, dim3(uint32_t((n_chunks + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, a,
+                     uint32_t(n_chunks));
   mark("select launched");
   if (vex_copy.joinable()) vex_copy.join();
   if (!upload(1)) return false;  // the VEX lists go up while mark / select run
@@ -835,7 +1000,7 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   if (nv) hipLaunchKernelGGL(vex_mark, dim3(uint32_t((nv + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, vd, pkg, side,
                              as<const uint32_t>(bufs_[8]), as<const uint32_t>(bufs_[9]), as<const uint8_t>(bufs_[7]), n,
                              uint32_t(np), uint32_t(rules.rank[1].size()), a.skey, a.pcls, a.cnt, a.surv,
-                             as<uint32_t>(bufs_[26]));
+                             a.carry_in, as<uint32_t>(bufs_[26]));
   if (!ok(hipGetLastError(), "filter launch", err) ||
       !ok(hipcub::DeviceScan::ExclusiveSum(bufs_[23], scan_bytes, In(Count(0), GroupCount{a.perm, a.surv, uint32_t(np)}),
                                            as<uint32_t>(bufs_[10]), int(np + 1), st),

@@ -207,10 +207,17 @@ __device__ __forceinline__ bool name_eq_slot(const uint8_t* s, uint32_t n, const
 }
 
 // Index probe of one package given its key state (shared by the fast and generic paths).
+// h / q0: the name's hash and the first 16 bytes of its home slot, loaded before the version
+// is encoded so the slot's round trip overlaps the encoder.
 template <class P>
 __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uint32_t plat, const PlatInfo& pi,
-                                            uint32_t nlen, const uint8_t* name, bool valid, uint32_t& rbeg,
-                                            uint32_t& cnt, uint32_t* sflags = nullptr);
+                                            uint32_t nlen, const uint8_t* name, bool valid, uint64_t h, uint4 q0,
+                                            uint32_t& rbeg, uint32_t& cnt, uint32_t* sflags = nullptr);
+
+template <class P>
+__device__ __forceinline__ uint4 home_slot(const ProbeArgs& a, uint64_t h) {
+  return reinterpret_cast<const uint4*>(a.db.slots + (h & a.db.slot_mask))[0];
+}
 
 // One package: encode, hash, probe.  P = uint32_t in the LDS or global address space of s.
 // kb / tab: the lane's LDS key buffer and the dpkg code table (nullptr: generic encoder only).
@@ -219,6 +226,8 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
                                           const uint8_t* name, const uint8_t* ver, uint64_t vglob, PkgRec& r,
                                           uint8_t* kb = nullptr, const uint8_t* tab = nullptr) {
   const PlatInfo pi = a.db.plats[plat];
+  const uint64_t h = (DIAG & 2) ? 0ull : name_hash<P>(plat, name, nlen);
+  const uint4 q0 = (DIAG & 2) ? make_uint4(0, 0, 0, 0) : home_slot<P>(a, h);
   if (!(DIAG & 1) && kb && ((GM >> CMP_DEB) & 1u) && pi.cmp == CMP_DEB) {
     uint32_t kl = 0;
     const uint32_t st = deb_fast_key(ver, vlen, kb, tab, kl);
@@ -235,7 +244,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
         if (kl > 16) a.tail[p] = make_uint4(kw[4], kw[5], kw[6], kw[7]);
       }
       uint32_t cnt = 0, rbeg = 0;
-      probe_lookup<P>(a, p, plat, pi, nlen, name, (kinfo & KI_VALID) != 0, rbeg, cnt);
+      if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, (kinfo & KI_VALID) != 0, h, q0, rbeg, cnt);
       r.meta = make_uint4(rbeg, cnt, kinfo, koff);
       return;
     }
@@ -268,7 +277,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
     }
   }
   uint32_t cnt = 0, rbeg = 0, sflags = 0;
-  if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, valid, rbeg, cnt, &sflags);
+  if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, valid, h, q0, rbeg, cnt, &sflags);
   if (((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN) {
     // Maven rows compare parses, not keys (AUX_MVN): the installed version's parse, packed
     // into the batch scratch, and its text location take the tail slot - only when the key
@@ -303,15 +312,15 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
 
 template <class P>
 __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uint32_t plat, const PlatInfo& pi,
-                                            uint32_t nlen, const uint8_t* name, bool valid, uint32_t& rbeg,
-                                            uint32_t& cnt, uint32_t* sflags) {
+                                            uint32_t nlen, const uint8_t* name, bool valid, uint64_t h,
+                                            uint4 q0, uint32_t& rbeg, uint32_t& cnt, uint32_t* sflags) {
   // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup;
   // lookup-first drivers (ubuntu.go:86-92) probe first, so a poisoned key still raises
   if (valid || (pi.flags & PLAT_LOOKUP_FIRST)) {
-    const uint64_t h = name_hash<P>(plat, name, nlen);
     for (uint64_t i = h & a.db.slot_mask;; i = (i + 1) & a.db.slot_mask) {
       const uint4* sp = reinterpret_cast<const uint4*>(a.db.slots + i);
-      const uint4 q0 = sp[0], q1 = sp[1], q2 = sp[2], q3 = sp[3];  // the whole 64-B slot
+      if (i != (h & a.db.slot_mask)) q0 = sp[0];
+      const uint4 q1 = sp[1], q2 = sp[2], q3 = sp[3];  // the rest of the 64-B slot
       const uint64_t sh = q0.x | (uint64_t(q0.y) << 32);
       if (sh == 0) break;
       if (sh != h) continue;
@@ -985,6 +994,7 @@ constexpr FusedFn fused_entry() {
   if constexpr (F == 0) return nullptr;
   else if constexpr (F == 4) return &launch_fused<GM, K, MB, FILT, 0, 1, 1>;
   else if constexpr (F == 5) return &launch_fused<GM, K, MB, FILT, 0, 1, 3>;
+  else if constexpr (F == 6) return &launch_fused<GM, K, MB, FILT, 0, 6, 3>;
   // the all-grammar K <= 2 kernels are held at 5 waves per SIMD (96 VGPRs): the Maven program
   // queue (sweep_programs) took them to 97 and 4 waves
   else return &launch_fused<GM, K, MB, FILT, (F >= 10 ? F - 10 : 0), (FILT >= 2 && K <= 2 && F == 1) ? 5 : TVM_FUSED_WPE(F)>;

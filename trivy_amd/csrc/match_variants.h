@@ -12,7 +12,9 @@
   X(0, 2, 2048, "split_k2_m2048")      \
   X(0, 4, 2048, "split_k4_m2048")      \
   X(4, 4, 2400, "fused_k4_m2400_seg")  \
-  X(5, 4, 2400, "fused_k4_m2400_wseg")
+  X(5, 4, 2400, "fused_k4_m2400_wseg")  \
+  X(6, 2, 2400, "fused_k2_m2400_wseg6") \
+  X(6, 3, 2400, "fused_k3_m2400_wseg6")
 
 // Measurement-only variants (wrong match lists by construction): built only with
 // `make DIAG=1` (-DTVM_DIAG), never reachable in the product library.

@@ -254,7 +254,7 @@ class BatchFilter {
   bool fetch_ignored(std::vector<uint32_t>& out3, hipStream_t st, std::string& err);
 
  private:
-  enum { kBufs = 27 };
+  enum { kBufs = 29 };
   void* bufs_[kBufs] = {};
   uint64_t caps_[kBufs] = {};
   uint64_t n_ = 0, survivors_ = 0, ignored_ = 0, n_pkgs_ = 0;
