@@ -24,7 +24,7 @@ import statistics
 import sys
 
 KERNELS = ("probe_kernel", "sweep_kernel", "fused_kernel", "persist_kernel", "match_kernel", "fill_pairs_kernel",
-           "filter_mark", "filter_select", "filter_count_dup", "filter_count", "filter_place", "rules_insert", "vex_mark",
+           "filter_mark", "filter_select", "filter_edges", "filter_count_dup", "filter_count", "filter_place", "rules_insert", "vex_mark",
            "order_kernel", "rh_count_kernel", "rh_scan_kernel", "rh_emit_kernel", "unpack_kernel", "copy_out_kernel",
            "wrapped_scan")
 MATCH = ("fused_kernel", "persist_kernel", "match_kernel")

@@ -1267,10 +1267,9 @@ int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint
   }
   (void)hipSetDevice(e->device);
   hipStream_t st = e->eng->stream();
-  if (hipStreamSynchronize(st) != hipSuccess) return TVM_EDEVICE;
   uint64_t n = 0;
   int64_t errp = -1;
-  int rc = match_status_locked(e, b, &n, &errp, nullptr);
+  int rc = match_status_locked(e, b, &n, &errp, nullptr);  // behind the batch's launches on st
   if (rc) return rc;
   if (n > cur(b).cap || n > b->fill_cap) {
     set_err(err, errlen, "tvm_match_filter: run tvm_match_launch + tvm_match_fill with a large enough match buffer first");

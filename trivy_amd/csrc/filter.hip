@@ -72,11 +72,12 @@ constexpr int kChunkBits = 10;                 // packed in-chunk counters (chun
 // FL_PKG / FL_VEX (rules_insert: the package has per-package rules, probe only those).
 enum : uint32_t { FL_DUP = 1, FL_UNS = 2, FL_PKG = 4, FL_VEX = 8, FL_SINGLE = 16 };
 
-// filter_select and filter_place work in chunks of kSpan pairs (select: kUS pairs per lane,
-// place: kP); a package whose run crosses a chunk boundary leaves an edge record per chunk,
-// which filter_edges turns into its counters and the chunks' entering-run carries.
+// filter_select and filter_place give each wave a chunk of its own: kSpan pairs, kUS
+// segments of 64 (pair s0 + k * 64 + lane), no workgroup barrier.  A package whose run crosses
+// a chunk boundary leaves an edge record per chunk, which filter_edges turns into its counters
+// and the chunks' entering-run carries.
 constexpr int kUS = 4;
-constexpr uint32_t kSpan = uint32_t(kUS) * kBlock;
+constexpr uint32_t kSpan = uint32_t(kUS) * 64;
 // Edge record of a chunk: the package entering it (run started before the chunk) and the
 // package leaving it (run goes on past its end), with their classes inside the chunk; a
 // package spanning the whole chunk is both (in == out, counts in c_in).
@@ -289,9 +290,15 @@ __global__ __launch_bounds__(kBlock) void filter_mark(FilterArgs a) {
       const uint32_t pk = p[k];
       const uint32_t vr = sd[k].x, sev = sd[k].y & 0xFFu;
       // run bounds (the list is grouped by package) and whether the run is ID-sorted
-      if (pp[k] != pk) a.run_b[pk] = uint32_t(i);
-      else if (vprev[k] >= vr && !(f[k] & FL_UNS)) set_flag(a.fl, pk, FL_UNS);
-      if (pn[k] != pk) a.run_e[pk] = uint32_t(i + 1);
+      // run bounds only for the packages whose pairs are looked up by package: dedup (FL_DUP),
+      // groups of several packages, and with VEX statements (vex_mark) every package
+      const bool bounds = (a.kinds & (1u << RULE_VEX)) || (f[k] & FL_DUP) || !(f[k] & FL_SINGLE);
+      if (pp[k] != pk) {
+        if (bounds) a.run_b[pk] = uint32_t(i);
+      } else if (vprev[k] >= vr && !(f[k] & FL_UNS)) {
+        set_flag(a.fl, pk, FL_UNS);
+      }
+      if (pn[k] != pk && bounds) a.run_e[pk] = uint32_t(i + 1);
       bool keep = ((a.sev_mask >> sev) & 1u) && !((a.status_mask >> ((sd[k].y >> 8) & 31u)) & 1u);
       if (a.kinds & 7u) {  // ignore rules: the smallest precedence is the finding Match returns
         uint32_t prec = kEmpty;
@@ -335,6 +342,17 @@ __device__ __forceinline__ bool beaten_by(const FilterArgs& a, uint32_t q, uint3
 
 // A package's counter record (every class, zeros included: whole 32-B sectors) and its
 // survivor sum.
+// Runs inside one chunk need only the sum: filter_place counts their classes from the chunk's
+// prefixes (the records are kept when ignore rules need the ignored counts of every package).
+__device__ __forceinline__ void store_sum(const FilterArgs& a, uint32_t p, const uint32_t* cc, uint32_t sum) {
+  if (a.kinds & 7u) {
+    uint4* o = reinterpret_cast<uint4*>(a.cnt + uint64_t(p) * kCntStride);
+    o[0] = make_uint4(cc[0], cc[1], cc[2], cc[3]);
+    o[1] = make_uint4(cc[4], cc[5], 0u, 0u);
+  }
+  a.surv[p] = sum;
+}
+
 __device__ __forceinline__ void store_counts(const FilterArgs& a, uint32_t p, const uint32_t* cc, uint32_t sum) {
   uint4* o = reinterpret_cast<uint4*>(a.cnt + uint64_t(p) * kCntStride);
   o[0] = make_uint4(cc[0], cc[1], cc[2], cc[3]);
@@ -342,139 +360,145 @@ __device__ __forceinline__ void store_counts(const FilterArgs& a, uint32_t p, co
   a.surv[p] = sum;
 }
 
-// LDS slots of filter_select's split runs: one per 64-pair segment boundary of the chunk
-// (+ the chunk's start): classes, survivor sum, package.
-constexpr int kSlots = kUS * (kBlock / 64) + 1;
+// LDS slots of filter_select's split runs, per wave: one per 64-pair segment boundary of the
+// chunk (+ the chunk's start): classes, survivor sum, package.
+constexpr int kSlots = kUS + 1;
+
+__device__ __forceinline__ void lds_order() {  // the wave's own LDS traffic, in program order
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
 
 __global__ __launch_bounds__(kBlock) void filter_select(FilterArgs a) {
-  __shared__ uint32_t lslot[kSlots][kClasses + 2];
-  if (threadIdx.x < kSlots) {
+  __shared__ uint32_t lslot_all[kBlock / 64][kSlots][kClasses + 2];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t g = uint64_t(blockIdx.x) * (kBlock / 64) + wave;  // this wave's chunk
+  const uint64_t n = a.n, s0 = g * kSpan;
+  if (s0 >= n) return;  // whole wave
+  uint32_t (*lslot)[kClasses + 2] = lslot_all[wave];
+  if (lane < uint32_t(kSlots)) {
 #pragma unroll
-    for (int c = 0; c < kClasses + 1; c++) lslot[threadIdx.x][c] = 0;
-    lslot[threadIdx.x][kClasses + 1] = kEmpty;
+    for (int c = 0; c < kClasses + 1; c++) lslot[lane][c] = 0;
+    lslot[lane][kClasses + 1] = kEmpty;
   }
-  __syncthreads();
-  const uint64_t stride = uint64_t(gridDim.x) * kBlock * kUS;
   const uint32_t id_mask = (1u << a.id_bits) - 1u;
-  const uint64_t n = a.n;
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t b0 = uint64_t(blockIdx.x) * kBlock * kUS; b0 < n; b0 += stride) {  // wave-uniform trip count
-    uint32_t pv[kUS], kv[kUS], fv[kUS], pe[kUS], ne[kUS];
+  uint32_t pv[kUS], kv[kUS], fv[kUS], pe[kUS], ne[kUS];
 #pragma unroll
-    for (int k = 0; k < kUS; k++) {
-      const uint64_t i = min(b0 + uint64_t(k) * kBlock + threadIdx.x, n - 1);
-      pv[k] = a.pkg[i];
-      kv[k] = a.mkey[i];
-      // the packages just before and after this wave's 64 pairs (edge lanes)
-      const uint64_t s0 = b0 + uint64_t(k) * kBlock + (threadIdx.x & ~63u);
-      pe[k] = (lane == 0 && s0 > 0 && s0 - 1 < n && !(a.diag & 16)) ? a.pkg[s0 - 1] : 0xFFFFFFFFu;
-      ne[k] = (lane == 63 && s0 + 64 < n && !(a.diag & 16)) ? a.pkg[s0 + 64] : 0xFFFFFFFFu;
-    }
+  for (int k = 0; k < kUS; k++) {
+    const uint64_t sk = s0 + uint64_t(k) * 64, i = min(sk + lane, n - 1);
+    pv[k] = a.pkg[i];
+    kv[k] = a.mkey[i];
+    // the packages just before and after the segment (edge lanes)
+    pe[k] = (lane == 0 && sk > 0) ? a.pkg[sk - 1] : 0xFFFFFFFFu;
+    ne[k] = (lane == 63 && sk + 64 < n) ? a.pkg[sk + 64] : 0xFFFFFFFFu;
+  }
 #pragma unroll
-    for (int k = 0; k < kUS; k++) fv[k] = a.fl[pv[k]];
+  for (int k = 0; k < kUS; k++) fv[k] = a.fl[pv[k]];
+  lds_order();
+  // the slot of the run that goes on from the segment before (0: the run entering the chunk),
+  // and whether the chunk's last run leaves it (wave-uniform, segment by segment)
+  uint32_t open_slot = 0;
+  bool leaving = false;
 #pragma unroll
-    for (int k = 0; k < kUS; k++) {
-      const uint64_t i = b0 + uint64_t(k) * kBlock + threadIdx.x;
-      const bool valid = i < n;
-      uint32_t p = valid ? pv[k] : 0xFFFFFFFFu, key = valid ? kv[k] : kEmpty;
-      uint32_t cls = kNoClass;
-      if (valid) {
-        if (key != kEmpty) {
-          const uint32_t vr = key & id_mask;
-          const uint32_t f = fv[k];
-          const bool dup = f & FL_DUP, uns = f & FL_UNS;
-          // the FixedVersion rank is needed only to dedup (repeating packages, unsorted runs)
-          const uint32_t fr = (dup || uns) ? a.t.adv_rank[a.adv[i]].y : 0u;
-          if (dup && !(a.diag & 2)) {  // another package of the dedup key with a greater FixedVersion, or an equal one seen first
-            for (uint32_t j = a.dk_b[p], je = a.dk_e[p]; j < je && key != kEmpty; j++) {
-              const uint32_t q = a.perm[j];
-              if (q != p && beaten_by(a, q, vr, fr, q < p)) key = kEmpty;
-            }
-          }
-          if (key != kEmpty && uns && !(a.diag & 2)) {  // the package's own pairs of this ID: the first with the greatest FixedVersion
-            const uint32_t rb = a.run_b[p], re = a.run_e[p];
-            for (uint32_t j = rb; j < re; j++) {
-              if (j == uint32_t(i)) continue;
-              const uint32_t kj = a.mkey[j];
-              if (kj == kEmpty || (kj & id_mask) != vr) continue;
-              const uint32_t fj = a.t.adv_rank[a.adv[j]].y;
-              if (fj > fr || (fj == fr && j < uint32_t(i))) {
-                key = kEmpty;
-                break;
-              }
-            }
+  for (int k = 0; k < kUS; k++) {
+    const uint64_t i = s0 + uint64_t(k) * 64 + lane;
+    const bool valid = i < n;
+    uint32_t p = valid ? pv[k] : 0xFFFFFFFFu, key = valid ? kv[k] : kEmpty;
+    uint32_t cls = kNoClass;
+    if (valid) {
+      if (key != kEmpty) {
+        const uint32_t vr = key & id_mask;
+        const uint32_t f = fv[k];
+        const bool dup = f & FL_DUP, uns = f & FL_UNS;
+        // the FixedVersion rank is needed only to dedup (repeating packages, unsorted runs)
+        const uint32_t fr = (dup || uns) ? a.t.adv_rank[a.adv[i]].y : 0u;
+        if (dup && !(a.diag & 2)) {  // another package of the dedup key with a greater FixedVersion, or an equal one seen first
+          for (uint32_t j = a.dk_b[p], je = a.dk_e[p]; j < je && key != kEmpty; j++) {
+            const uint32_t q = a.perm[j];
+            if (q != p && beaten_by(a, q, vr, fr, q < p)) key = kEmpty;
           }
         }
-        a.skey[i] = key;
-        cls = pair_class(a, key, i);
-        a.pcls[i] = uint8_t(cls);  // placed by filter_place
-      }
-      // per-package class counters over the wave's 64 pairs (segment g = k * 4 + wave of the
-      // chunk): the first lane of each package counts its lanes' classes with six ballots; a
-      // package all inside the segment stores its record, one that goes on before or after it
-      // adds its share to the chunk's LDS slot of the first segment boundary its run crosses
-      // (0: the chunk's start), flushed below
-      if (a.diag & 1) continue;
-      const uint32_t up = __shfl_up(p, 1, 64);
-      const bool head = valid && (lane == 0 || up != p);
-      const unsigned long long heads = __ballot(head);
-      const unsigned long long above = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
-      const uint32_t end = above ? uint32_t(__builtin_ctzll(above)) : 64u;
-      const unsigned long long span = (end == 64 ? ~0ull : ((1ull << end) - 1)) & (~0ull << lane);
-      uint32_t cc[kClasses];
-#pragma unroll
-      for (uint32_t c = 0; c < uint32_t(kClasses); c++) cc[c] = uint32_t(__popcll(__ballot(cls == c) & span));
-      const uint32_t next = __shfl(ne[k], 63, 64);
-      if (head) {
-        const bool split = (lane == 0 && pe[k] == p) || (end == 64 && next == p);
-        const uint32_t sum = cc[0] + cc[1] + cc[2] + cc[3] + cc[4];
-        if (split) {
-          const uint32_t rb = a.run_b[p];
-          const uint32_t slot = rb < b0 ? 0u : uint32_t((rb - b0) >> 6) + 1u;
-          uint32_t* o = lslot[slot];
-#pragma unroll
-          for (int c = 0; c < kClasses; c++)
-            if (cc[c]) atomicAdd(&o[c], cc[c]);
-          if (sum) atomicAdd(&o[kClasses], sum);
-          o[kClasses + 1] = p;
-        } else {
-          store_counts(a, p, cc, sum);
+        if (key != kEmpty && uns && !(a.diag & 2)) {  // the package's own pairs of this ID: the first with the greatest FixedVersion
+          uint32_t rb = uint32_t(i), re = uint32_t(i) + 1;  // its run, walked (filter_mark keeps no bounds for it)
+          while (rb > 0 && a.pkg[rb - 1] == p) rb--;
+          while (re < n && a.pkg[re] == p) re++;
+          for (uint32_t j = rb; j < re; j++) {
+            if (j == uint32_t(i)) continue;
+            const uint32_t kj = a.mkey[j];
+            if (kj == kEmpty || (kj & id_mask) != vr) continue;
+            const uint32_t fj = a.t.adv_rank[a.adv[j]].y;
+            if (fj > fr || (fj == fr && j < uint32_t(i))) {
+              key = kEmpty;
+              break;
+            }
+          }
         }
       }
+      a.skey[i] = key;
+      cls = pair_class(a, key, i);
+      a.pcls[i] = uint8_t(cls);  // placed by filter_place
     }
-    // the slots: a run inside this chunk stores its record; the chunk's edge record takes the
-    // run that enters it (slot 0) and the one that goes on past its end (filter_edges adds
-    // them up, no atomics)
-    __syncthreads();
-    const uint64_t be = min(b0 + uint64_t(kSpan), n);
-    Edge* e = a.edge + b0 / kSpan;
-    if (threadIdx.x < kSlots) {
-      uint32_t* o = lslot[threadIdx.x];
-      const uint32_t p = o[kClasses + 1];
-      const bool leaves = p != kEmpty && a.run_e[p] > be;
-      if (p != kEmpty) {
-        if (threadIdx.x == 0 || leaves) {
-          uint32_t* c = (threadIdx.x == 0) ? e->c_in : e->c_out;
+    // per-package class counters over the segment's 64 pairs: the first lane of each package
+    // counts its lanes' classes with six ballots; a package all inside the segment stores its
+    // record, one that goes on before or after it adds its share to the wave's LDS slot of the
+    // first segment boundary its run crosses (0: the chunk's start), flushed below
+    if (a.diag & 1) continue;
+    const uint32_t up = __shfl_up(p, 1, 64);
+    const bool head = valid && (lane == 0 || up != p);
+    const unsigned long long heads = __ballot(head);
+    const unsigned long long above = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
+    const uint32_t end = above ? uint32_t(__builtin_ctzll(above)) : 64u;
+    const unsigned long long span = (end == 64 ? ~0ull : ((1ull << end) - 1)) & (~0ull << lane);
+    uint32_t cc[kClasses];
 #pragma unroll
-          for (int k = 0; k < kClasses; k++) c[k] = o[k];
-          if (threadIdx.x == 0) e->p_in = p;
-          if (leaves) e->p_out = p;
-        } else {
-          uint32_t cc[kClasses];
+    for (uint32_t c = 0; c < uint32_t(kClasses); c++) cc[c] = uint32_t(__popcll(__ballot(cls == c) & span));
+    const uint32_t next = __shfl(ne[k], 63, 64);
+    const bool cont_in = __shfl(pe[k], 0, 64) == __shfl(p, 0, 64);  // lane 0's run started before the segment
+    const uint32_t last = heads ? 63u - uint32_t(__builtin_clzll(heads)) : 0u;
+    const bool cont_out = heads && next == __shfl(p, int(last), 64);   // the segment's last run goes on
+    if (head) {
+      const bool split = (lane == 0 && cont_in) || (end == 64 && next == p);
+      const uint32_t sum = cc[0] + cc[1] + cc[2] + cc[3] + cc[4];
+      if (split) {
+        const uint32_t slot = (lane == 0 && cont_in) ? open_slot : uint32_t(k) + 1u;
+        uint32_t* o = lslot[slot];
 #pragma unroll
-          for (int k = 0; k < kClasses; k++) cc[k] = o[k];
-          store_counts(a, p, cc, o[kClasses]);
-        }
-      } else if (threadIdx.x == 0) {
-        e->p_in = kEmpty;
+        for (int c = 0; c < kClasses; c++)
+          if (cc[c]) atomicAdd(&o[c], cc[c]);
+        if (sum) atomicAdd(&o[kClasses], sum);
+        o[kClasses + 1] = p;
+      } else {
+        store_sum(a, p, cc, sum);
       }
-      // the chunk's last pair's package: no slot leaves when it ends inside the chunk
-      if (threadIdx.x == 1 && (be == n || a.pkg[be - 1] != a.pkg[be])) e->p_out = kEmpty;
-#pragma unroll
-      for (int c = 0; c < kClasses + 1; c++) o[c] = 0;
-      o[kClasses + 1] = kEmpty;
     }
-    __syncthreads();
+    if (cont_out) open_slot = (last == 0 && cont_in) ? open_slot : uint32_t(k) + 1u;
+    leaving = cont_out && k == kUS - 1;
+  }
+  // the slots: a run inside this chunk stores its record; the chunk's edge record takes the run
+  // that enters it (slot 0) and the one that goes on past its end (filter_edges adds them up)
+  lds_order();
+  Edge* e = a.edge + g;
+  if (lane < uint32_t(kSlots)) {
+    const uint32_t* o = lslot[lane];
+    const uint32_t p = o[kClasses + 1];
+    const bool leaves = leaving && lane == open_slot;
+    if (p != kEmpty) {
+      if (lane == 0 || leaves) {
+        uint32_t* c = (lane == 0) ? e->c_in : e->c_out;
+#pragma unroll
+        for (int k = 0; k < kClasses; k++) c[k] = o[k];
+        if (lane == 0) e->p_in = p;
+        if (leaves) e->p_out = p;
+      } else {
+        uint32_t cc[kClasses];
+#pragma unroll
+        for (int k = 0; k < kClasses; k++) cc[k] = o[k];
+        store_sum(a, p, cc, o[kClasses]);
+      }
+    } else if (lane == 0) {
+      e->p_in = kEmpty;
+    }
+    if (lane == 0 && !leaving) e->p_out = kEmpty;  // the chunk's last run ends inside it
   }
 }
 
@@ -501,16 +525,6 @@ __global__ __launch_bounds__(kBlock) void filter_edges(FilterArgs a, uint32_t n_
   store_counts(a, p, acc, acc[0] + acc[1] + acc[2] + acc[3] + acc[4]);
 }
 
-// Number of keys in the run [rb, re) below key (or at most key).
-__device__ __forceinline__ uint32_t count_below(const uint32_t* skey, uint32_t rb, uint32_t re, uint32_t key,
-                                                bool inclusive) {
-  uint32_t c = 0;
-  for (uint32_t j = rb; j < re; j++) {
-    const uint32_t k = skey[j];
-    c += (k < key || (inclusive && k == key)) ? 1u : 0u;
-  }
-  return c;
-}
 
 // One-hot of a class in the packed in-chunk counters (kChunkBits per class).
 __device__ __forceinline__ unsigned long long one_hot(uint32_t cls) {
@@ -520,25 +534,25 @@ __device__ __forceinline__ uint32_t chunk_field(unsigned long long v, uint32_t c
   return uint32_t(v >> (kChunkBits * cls)) & ((1u << kChunkBits) - 1u);
 }
 
-// filter_place takes spans of kP chunks (kP * kBlock pairs, pair s0 + k * kBlock + tid):
-// the per-span fixed latency (the entering run's carry, the barriers) is paid once per
-// kP * 256 pairs.  Packed class prefixes over a span stay below 2^10 per field.
-constexpr int kP = 4;
-static_assert(kP * kBlock <= (1 << kChunkBits), "span prefixes fit the packed fields");
-static_assert(kP * kBlock == kSpan, "place spans are select chunks (carry_in)");
+// filter_place: a wave per chunk (filter_select's), its 256 pairs' packed class prefixes in
+// the wave's LDS, the entering run's classes from filter_edges (carry_in).
+static_assert(kSpan <= (1u << kChunkBits), "chunk prefixes fit the packed fields");
 
 // A pair's placement inputs, loaded two steps ahead of its span (pair words, then its
 // package's words, then the package's placement base for the pair's class).
 struct PlacePair {
-  uint32_t p, adv, cf;  // package, advisory, class | flags << 8
-  uint32_t rb, gb;      // package run start, group start
-  uint32_t base;        // the pair's output base (SINGLE survivors / ignored), else unused
+  uint32_t p, adv, cf;  // package (kEmpty past the list's end), advisory, class | flags << 8
+  uint32_t loc;         // the run in the chunk: first pair | end << 9 | entering << 18 | leaving << 19
+  uint32_t gb;          // group start
+  uint32_t base;        // the pair's output base (SINGLE survivors / ignored), else unused; a run
+                        // inside the chunk adds its survivors of higher severity from the prefixes
 };
+enum : uint32_t { LOC_ENTER = 1u << 18, LOC_LEAVE = 1u << 19 };
 
 // (Every field is written unconditionally from locals: stores of struct fields under branches
-// were merged into address selects, which put the span's pair arrays in scratch memory.)
+// were merged into address selects, which put the chunk's pair arrays in scratch memory.)
 __device__ __forceinline__ void place_load_pair(const FilterArgs& a, uint64_t i, PlacePair& q) {
-  uint32_t p = 0, adv = 0, cf = kNoClass;
+  uint32_t p = kEmpty, adv = 0, cf = kNoClass;
   if (i < a.n) {
     p = a.pkg[i];
     adv = a.adv[i];
@@ -548,25 +562,26 @@ __device__ __forceinline__ void place_load_pair(const FilterArgs& a, uint64_t i,
   q.adv = adv;
   q.cf = cf;
 }
-__device__ __forceinline__ void place_load_pkg(const FilterArgs& a, uint64_t i, PlacePair& q) {
-  uint32_t rb = 0, fl = 0, gb = 0;
-  if (i < a.n) rb = a.run_b[q.p];  // every pair: lane 0's gives the span's entering run
-  if (i < a.n && (q.cf & 0xFFu) < uint32_t(kClasses)) {
+__device__ __forceinline__ void place_load_pkg(const FilterArgs& a, PlacePair& q) {
+  uint32_t fl = 0, gb = 0;
+  if ((q.cf & 0xFFu) < uint32_t(kClasses)) {
     fl = a.fl[q.p];
     gb = a.grp_b[q.p];
   }
-  q.rb = rb;
   q.cf |= fl << 8;
   q.gb = gb;
 }
-__device__ __forceinline__ void place_load_base(const FilterArgs& a, uint64_t i, PlacePair& q) {
+__device__ __forceinline__ void place_load_base(const FilterArgs& a, PlacePair& q) {
   const uint32_t cls = q.cf & 0xFFu, f = q.cf >> 8;
+  const bool inside = !(q.loc & (LOC_ENTER | LOC_LEAVE));
   uint32_t base = 0;
-  if (i < a.n && cls == uint32_t(kIgnClass)) {
+  if (cls == uint32_t(kIgnClass)) {
     base = a.ign_off[q.p];
-  } else if (i < a.n && cls < uint32_t(kClasses) && (f & (FL_SINGLE | FL_UNS)) == FL_SINGLE) {
-    // ID-sorted run alone in its group: severity desc, then run order (class = severity
-    // index: the package's survivors of the classes above come first)
+  } else if (cls < uint32_t(kClasses) && (f & (FL_SINGLE | FL_UNS)) == FL_SINGLE && inside) {
+    base = a.off[q.gb];  // + the run's survivors before it in report order (from the chunk's LDS)
+  } else if (cls < uint32_t(kClasses) && (f & (FL_SINGLE | FL_UNS)) == FL_SINGLE) {
+    // a run crossing the chunk (its record from filter_edges): severity desc, then run order
+    // (class = severity index: the package's survivors of the classes above come first)
     const uint32_t* c = a.cnt + uint64_t(q.p) * kCntStride;
     const uint4 c03 = *reinterpret_cast<const uint4*>(c);
     const uint32_t c4 = c[4];
@@ -575,14 +590,35 @@ __device__ __forceinline__ void place_load_base(const FilterArgs& a, uint64_t i,
   q.base = base;
 }
 
+// Keys in the run [rb, re) below key (or at most key).  16 keys per step (four 16-byte loads
+// in flight): a lane's count over a long group run is a latency chain of re - rb loads otherwise.
+__device__ __forceinline__ uint32_t count_below(const uint32_t* skey, uint32_t rb, uint32_t re, uint32_t key,
+                                                bool inclusive) {
+  auto below = [&](uint32_t k) { return (k < key || (inclusive && k == key)) ? 1u : 0u; };
+  uint32_t c = 0, j = rb;
+  for (; j < re && (j & 3u); j++) c += below(skey[j]);
+  const uint4* v = reinterpret_cast<const uint4*>(skey);
+  for (; j + 16 <= re; j += 16) {
+    const uint4 x0 = v[j / 4], x1 = v[j / 4 + 1], x2 = v[j / 4 + 2], x3 = v[j / 4 + 3];
+    c += below(x0.x) + below(x0.y) + below(x0.z) + below(x0.w) + below(x1.x) + below(x1.y) + below(x1.z) +
+         below(x1.w) + below(x2.x) + below(x2.y) + below(x2.z) + below(x2.w) + below(x3.x) + below(x3.y) +
+         below(x3.z) + below(x3.w);
+  }
+  for (; j < re; j++) c += below(skey[j]);
+  return c;
+}
+
 // Output position of a survivor (key) of package p in a group of several packages (same
 // PkgName and InstalledVersion: merged by severity, ID, PkgPath) or with an unsorted run:
-// keys counted over the group's runs.  Rare: filter_place runs it once per lane, after the span.
-__device__ __forceinline__ uint64_t place_slow(const FilterArgs& a, uint32_t p, uint32_t rb, uint32_t key) {
+// keys counted over the group's runs.  Rare: filter_place runs it once per lane, after the chunk.
+__device__ __forceinline__ uint64_t place_slow(const FilterArgs& a, uint32_t p, uint64_t i, uint32_t key) {
   const uint32_t gb = a.grp_b[p], ge = a.grp_e[p];
   uint32_t r = 0;
-  if (ge - gb == 1) {
-    r = count_below(a.skey, rb, a.run_e[p], key, false);
+  if (ge - gb == 1) {  // an unsorted run alone in its group: its bounds walked (filter_mark keeps none)
+    uint32_t rb = uint32_t(i), re = uint32_t(i) + 1;
+    while (rb > 0 && a.pkg[rb - 1] == p) rb--;
+    while (re < a.n && a.pkg[re] == p) re++;
+    r = count_below(a.skey, rb, re, key, false);
   } else {
     const uint32_t pr = a.prank[p];
     for (uint32_t g = gb; g < ge; g++) {
@@ -595,116 +631,118 @@ __device__ __forceinline__ uint64_t place_slow(const FilterArgs& a, uint32_t p, 
 }
 
 __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
-  __shared__ unsigned long long pre[kP * kBlock];  // exclusive packed class counts over the span
-  __shared__ unsigned long long wsum[kP * (kBlock / 64)];
-  __shared__ uint32_t carry[kClasses];             // classes of the entering run before the span
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint64_t span = uint64_t(kP) * kBlock;
-  const uint64_t stride = uint64_t(gridDim.x) * span;
-  PlacePair cur[kP], nxt[kP];
-  // prologue: this block's first span fully, the next span's pair words
-  const uint64_t first = uint64_t(blockIdx.x) * span;
+  __shared__ unsigned long long pre_all[kBlock / 64][kSpan];  // per wave: exclusive packed class counts
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t g = uint64_t(blockIdx.x) * (kBlock / 64) + wave;  // this wave's chunk
+  const uint64_t s0 = g * kSpan;
+  if (s0 >= a.n) return;  // whole wave
+  unsigned long long* pre = pre_all[wave];
+  PlacePair q[kUS];
 #pragma unroll
-  for (int k = 0; k < kP; k++) place_load_pair(a, first + k * kBlock + tid, cur[k]);
+  for (int k = 0; k < kUS; k++) place_load_pair(a, s0 + k * 64 + lane, q[k]);
+  const uint32_t before_chunk = s0 ? a.pkg[s0 - 1] : kEmpty;
+  const uint32_t after_chunk = s0 + kSpan < a.n ? a.pkg[s0 + kSpan] : kEmpty;
+  // the runs inside the chunk from its package column alone: H[k] bit l = pair k * 64 + l
+  // starts a run in the chunk (past the list's end the sentinel package starts one)
+  unsigned long long H[kUS];
 #pragma unroll
-  for (int k = 0; k < kP; k++) place_load_pkg(a, first + k * kBlock + tid, cur[k]);
+  for (int k = 0; k < kUS; k++) {
+    const uint32_t up = __shfl_up(q[k].p, 1, 64);
+    const uint32_t tail = __shfl(q[k ? k - 1 : 0].p, 63, 64);  // the segment before's last package
+    const uint32_t prev = lane ? up : (k == 0 ? before_chunk : tail);
+    H[k] = __ballot(q[k].p != prev);
+  }
+  {
+    uint32_t first_after = kSpan;  // the first run start past segment k (kSpan: none in the chunk)
+    uint32_t fa[kUS];
 #pragma unroll
-  for (int k = 0; k < kP; k++) place_load_base(a, first + k * kBlock + tid, cur[k]);
-#pragma unroll
-  for (int k = 0; k < kP; k++) place_load_pair(a, first + stride + k * kBlock + tid, nxt[k]);
-  for (uint64_t s0 = first; s0 < a.n; s0 += stride) {  // block-uniform trip count
-    const bool more = s0 + stride < a.n;
-    // the next span's package words (its pair words arrived during this block's last span)
-    if (more) {
-#pragma unroll
-      for (int k = 0; k < kP; k++) place_load_pkg(a, s0 + stride + k * kBlock + tid, nxt[k]);
+    for (int k = kUS - 1; k >= 0; k--) {
+      fa[k] = first_after;
+      if (H[k]) first_after = uint32_t(k) * 64 + uint32_t(__builtin_ctzll(H[k]));
     }
-    // per chunk: wave-inclusive packed one-hot class counts
-    unsigned long long x[kP];
+    int last_start = -1;  // the last run start before segment k (-1: the entering run)
 #pragma unroll
-    for (int k = 0; k < kP; k++) {
-      x[k] = one_hot(cur[k].cf & 0xFFu);
+    for (int k = 0; k < kUS; k++) {
+      const unsigned long long upto = lane == 63 ? ~0ull : (2ull << lane) - 1ull;
+      const unsigned long long mb = H[k] & upto, ma = H[k] & ~upto;
+      const int rs = mb ? k * 64 + 63 - int(__builtin_clzll(mb)) : last_start;
+      const uint32_t re = ma ? uint32_t(k) * 64 + uint32_t(__builtin_ctzll(ma)) : fa[k];
+      const bool leave = re == kSpan && after_chunk == q[k].p;
+      q[k].loc = uint32_t(rs < 0 ? 0 : rs) | (re << 9) | (rs < 0 ? LOC_ENTER : 0u) | (leave ? LOC_LEAVE : 0u);
+      if (H[k]) last_start = k * 64 + 63 - int(__builtin_clzll(H[k]));
+    }
+  }
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const unsigned long long y = __shfl_up(x[k], o, 64);
-        if (lane >= uint32_t(o)) x[k] += y;
+  for (int k = 0; k < kUS; k++) place_load_pkg(a, q[k]);
+#pragma unroll
+  for (int k = 0; k < kUS; k++) place_load_base(a, q[k]);
+  // the run entering the chunk: its classes before s0 (filter_edges), per lane for its class
+  uint32_t carry[kUS];
+#pragma unroll
+  for (int k = 0; k < kUS; k++) {
+    const uint32_t cls = q[k].cf & 0xFFu;
+    carry[k] = ((q[k].loc & LOC_ENTER) && cls < uint32_t(kClasses) && !(a.diag & 64)) ? a.carry_in[g * kClasses + cls] : 0u;
+  }
+  // packed one-hot class prefixes over the chunk, segment by segment
+  unsigned long long run = 0;
+#pragma unroll
+  for (int k = 0; k < kUS; k++) {
+    const unsigned long long oh = one_hot(q[k].cf & 0xFFu);
+    unsigned long long x = oh;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long y = __shfl_up(x, o, 64);
+      if (lane >= uint32_t(o)) x += y;
+    }
+    pre[k * 64 + lane] = run + x - oh;
+    run += __shfl(x, 63, 64);
+  }
+  lds_order();
+  uint32_t slow = 0;
+#pragma unroll
+  for (int k = 0; k < kUS; k++) {
+    const uint64_t i = s0 + k * 64 + lane;
+    const uint32_t cls = q[k].cf & 0xFFu, f = q[k].cf >> 8;
+    if (i >= a.n || cls >= uint32_t(kClasses)) continue;
+    const uint32_t rs = q[k].loc & 511u, re = (q[k].loc >> 9) & 511u;  // the run in the chunk
+    // pairs of this package before pair i that share its class
+    const uint32_t before = chunk_field(pre[k * 64 + lane] - pre[rs], cls) + carry[k];
+    if (cls == uint32_t(kIgnClass)) {  // ModifiedFindings in detection order
+      const uint64_t at = uint64_t(q[k].base) + before;
+      if (at < a.n) {
+        uint32_t* o = a.iout + 3 * at;
+        o[0] = q[k].p;
+        o[1] = q[k].adv;
+        o[2] = a.ign[i];
       }
-      if (lane == 63) wsum[k * (kBlock / 64) + wave] = x[k];
+      continue;
     }
-    // the run entering the span: its classes before s0 (filter_edges)
-    const uint32_t rb0 = __shfl(cur[0].rb, 0, 64);
-    if (tid < uint32_t(kClasses)) {
-      carry[tid] = rb0 < s0 && !(a.diag & 64) ? a.carry_in[(s0 / kSpan) * kClasses + tid] : 0u;
+    if ((f & (FL_SINGLE | FL_UNS)) != FL_SINGLE) {
+      slow |= 1u << k;  // below, once per lane
+      continue;
     }
-    __syncthreads();
-    unsigned long long run = 0;  // sum of the wave totals before (chunk k, this wave)
+    uint64_t at = uint64_t(q[k].base) + before;
+    if (!(q[k].loc & (LOC_ENTER | LOC_LEAVE))) {  // a run inside the chunk: its classes from the prefixes
+      const unsigned long long cnt = (re < kSpan ? pre[re] : run) - pre[rs];
 #pragma unroll
-    for (int k = 0; k < kP; k++) {
-      unsigned long long before_w = 0, total_k = 0;
+      for (uint32_t c = 1; c < 5; c++) at += c > cls ? chunk_field(cnt, c) : 0u;
+    }
+    if (at < a.n) a.out[at] = make_uint2(q[k].p, q[k].adv);  // always true for a list grouped by package
+  }
+  if (a.diag & 32) slow = 0;
+  while (slow) {  // the slow placements, one code path (static selects of the lane's pair)
+    const uint32_t k = uint32_t(__builtin_ctz(slow));
+    slow &= slow - 1;
+    uint32_t p = 0, adv = 0;
 #pragma unroll
-      for (int w = 0; w < kBlock / 64; w++) {
-        const unsigned long long t = wsum[k * (kBlock / 64) + w];
-        before_w += (uint32_t(w) < wave) ? t : 0ull;
-        total_k += t;
+    for (int kk = 0; kk < kUS; kk++)
+      if (uint32_t(kk) == k) {
+        p = q[kk].p;
+        adv = q[kk].adv;
       }
-      pre[k * kBlock + tid] = run + before_w + x[k] - one_hot(cur[k].cf & 0xFFu);
-      run += total_k;
-    }
-    __syncthreads();
-    uint32_t slow = 0;
-#pragma unroll
-    for (int k = 0; k < kP; k++) {
-      const uint64_t i = s0 + k * kBlock + tid;
-      const PlacePair& q = cur[k];
-      const uint32_t cls = q.cf & 0xFFu, f = q.cf >> 8;
-      if (i >= a.n || cls >= uint32_t(kClasses)) continue;
-      const uint64_t rs = q.rb > s0 ? q.rb : s0;  // the package's first pair in this span
-      // pairs of this package before pair i that share its class
-      const uint32_t before =
-          chunk_field(pre[k * kBlock + tid] - pre[rs - s0], cls) + (q.rb < s0 ? carry[cls] : 0u);
-      if (cls == uint32_t(kIgnClass)) {  // ModifiedFindings in detection order
-        const uint64_t at = uint64_t(q.base) + before;
-        if (at < a.n) {
-          uint32_t* o = a.iout + 3 * at;
-          o[0] = q.p;
-          o[1] = q.adv;
-          o[2] = a.ign[i];
-        }
-        continue;
-      }
-      if ((f & (FL_SINGLE | FL_UNS)) != FL_SINGLE) {
-        slow |= 1u << k;  // below, once per lane
-        continue;
-      }
-      const uint64_t at = uint64_t(q.base) + before;
-      if (at < a.n) a.out[at] = make_uint2(q.p, q.adv);  // always true for a list grouped by package
-    }
-    if (a.diag & 32) slow = 0;
-    while (slow) {  // the slow placements, one code path (static selects of the lane's pair)
-      const uint32_t k = uint32_t(__builtin_ctz(slow));
-      slow &= slow - 1;
-      uint32_t p = 0, rb = 0, adv = 0;
-#pragma unroll
-      for (int kk = 0; kk < kP; kk++)
-        if (uint32_t(kk) == k) {
-          p = cur[kk].p;
-          rb = cur[kk].rb;
-          adv = cur[kk].adv;
-        }
-      const uint64_t at = place_slow(a, p, rb, a.skey[s0 + k * kBlock + tid]);
-      if (at < a.n) a.out[at] = make_uint2(p, adv);
-    }
-    // the next span: its placement bases (its package words arrived during this span), then
-    // the pair words of the span after it
-    if (more) {
-#pragma unroll
-      for (int k = 0; k < kP; k++) place_load_base(a, s0 + stride + k * kBlock + tid, nxt[k]);
-#pragma unroll
-      for (int k = 0; k < kP; k++) cur[k] = nxt[k];
-#pragma unroll
-      for (int k = 0; k < kP; k++) place_load_pair(a, s0 + 2 * stride + k * kBlock + tid, nxt[k]);
-    }
-    __syncthreads();  // pre / carry are rewritten by the next span
+    const uint64_t i = s0 + k * 64 + lane;
+    const uint64_t at = place_slow(a, p, i, a.skey[i]);
+    if (at < a.n) a.out[at] = make_uint2(p, adv);
   }
 }
 
@@ -714,7 +752,7 @@ __global__ __launch_bounds__(kBlock) void filter_place(FilterArgs a) {
 // findings of package j.
 struct GroupCount {
   const uint32_t* perm;  // nullptr: package j itself, ignored findings
-  const uint32_t* cnt;   // perm: the survivor sums; else the counters
+  const uint32_t* cnt;   // perm: the survivor sums; else the counter records
   uint32_t n;
   __host__ __device__ uint32_t operator()(uint32_t j) const {
     if (j >= n) return 0u;
@@ -828,10 +866,9 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
     err = "filter: more than 2^29 vulnerability IDs";
     return false;
   }
-  const uint32_t blocks = uint32_t(std::min<uint64_t>((n + kBlock * kP - 1) / (kBlock * kP), 256ull * 8));
   const uint32_t blocks_u = uint32_t(std::min<uint64_t>((n + kBlock * kU - 1) / (kBlock * kU), 256ull * 32));
   const uint64_t n_chunks = (n + kSpan - 1) / kSpan;
-  const uint32_t blocks_s = uint32_t(std::min<uint64_t>(n_chunks, 256ull * 32));
+  const uint32_t blocks_s = uint32_t((n_chunks + kBlock / 64 - 1) / (kBlock / 64));  // a wave per chunk
   sev_mask &= 0x1Fu;  // SeverityNames only: a bit for "out of range" (5) would pass a severity 4 - 5 can't order
   const uint64_t np = n_pkgs_;
   // The rule lists go up in one pinned copy, staged while the GPU counts repeating pairs.
@@ -1010,7 +1047,7 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
                                             as<uint32_t>(bufs_[11]), int(np + 1), st),
            "hipcub scan", err)))
     return false;
-  hipLaunchKernelGGL(filter_place, dim3(blocks), dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL(filter_place, dim3(blocks_s), dim3(kBlock), 0, st, a);
   uint32_t tot[2] = {0, 0}, bad = 0;
   if (!ok(hipGetLastError(), "filter_place", err) ||
       !ok(hipMemcpyAsync(&tot[0], as<uint32_t>(bufs_[10]) + np, 4, hipMemcpyDeviceToHost, st), "D2H kept", err) ||
@@ -1025,6 +1062,31 @@ bool BatchFilter::run(const FillDev& t, const uint32_t* pkg, const uint32_t* adv
   }
   survivors_ = tot[0];
   mark("done");
+  if (std::getenv("TVM_FILTER_STATS")) {  // measurement only: which placement path the pairs take
+    std::vector<uint32_t> hp(n), hb(np), he(np);
+    std::vector<uint8_t> hf(np), hc(n);
+    (void)hipMemcpy(hp.data(), pkg, n * 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(hf.data(), bufs_[7], np, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(hb.data(), bufs_[8], np * 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(he.data(), bufs_[9], np * 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(hc.data(), bufs_[24], n, hipMemcpyDeviceToHost);
+    uint64_t nsingle = 0, uns_in = 0, uns_x = 0, multi = 0, cross = 0, surv_pairs = 0, uns_x_len = 0;
+    for (uint64_t i = 0; i < n; i++) {
+      if (hc[i] >= kClasses) continue;
+      surv_pairs++;
+      const uint32_t p = hp[i], f = hf[p];
+      const uint64_t c0 = i / kSpan * kSpan;
+      const bool inside = hb[p] >= c0 && he[p] <= c0 + kSpan;
+      if (!(f & FL_SINGLE)) multi++;
+      else if (f & FL_UNS) { if (inside) uns_in++; else { uns_x++; uns_x_len += he[p] - hb[p]; } }
+      else if (!inside) cross++;
+      else nsingle++;
+    }
+    std::fprintf(stderr, "filter stats: classed %llu inside-sorted %llu crossing-sorted %llu uns-inside %llu uns-crossing %llu (mean run %.1f) multi %llu\n",
+                 (unsigned long long)surv_pairs, (unsigned long long)nsingle, (unsigned long long)cross,
+                 (unsigned long long)uns_in, (unsigned long long)uns_x, uns_x ? double(uns_x_len) / uns_x : 0.0,
+                 (unsigned long long)multi);
+  }
   ignored_ = tot[1];
   return true;
 }
