@@ -73,6 +73,11 @@ struct tvm_batch {
   uint2* fill_side() const { return reinterpret_cast<uint2*>(fill_out + fill_cap); }
   std::vector<uint32_t> target_begin;  // first package of every result (one per add call)
   BatchFilter filter;                  // tvm_match_filter state
+  // the list's length as last read back (match_status_locked), until the next launch / merge /
+  // upload: tvm_match_filter reads it without a host round trip
+  bool st_valid = false;
+  uint64_t st_n = 0;
+  int64_t st_errp = -1;
   // tvm_batch_set_report: per package PkgName / InstalledVersion / PkgPath overrides
   // (rep[f][i] counts where rep_has[f][i] is set; shorter vectors = defaults beyond)
   std::vector<std::string> rep[3];
@@ -658,6 +663,7 @@ int tvm_batch_upload(tvm_engine* e, tvm_batch* b, uint64_t cap, char* err, size_
     b->external_out = false;
     b->uploaded = false;
   }
+  b->st_valid = false;
   if (!e->eng->upload(b->hb, b->dev, msg) || !e->eng->alloc_matches(cap, b->dev.n, b->m, msg)) {
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
@@ -686,6 +692,7 @@ int tvm_match_launch(tvm_engine* e, tvm_batch* b, char* err, size_t errlen) {
   }
   std::string msg;
   b->merged = false;
+  b->st_valid = false;
   if (!e->eng->launch(b->dev, b->m, e->eng->stream(), msg)) {
     set_err(err, errlen, msg);
     return TVM_EDEVICE;
@@ -717,6 +724,9 @@ static int match_status_locked(tvm_engine* e, tvm_batch* b, uint64_t* n_matches,
   if (b->merged && hipMemcpyAsync(mctl, cur(b).ctl, sizeof(mctl), hipMemcpyDeviceToHost, st) != hipSuccess)
     return TVM_EDEVICE;
   if (hipStreamSynchronize(st) != hipSuccess) return TVM_EDEVICE;
+  b->st_n = b->merged ? mctl[0] : ctl[0];
+  b->st_errp = ctl[1] ? int64_t(b->dev.n - ctl[1]) : -1;
+  b->st_valid = true;
   if (n_matches) *n_matches = b->merged ? mctl[0] : ctl[0];
   if (err_pkg) *err_pkg = ctl[1] ? int64_t(b->dev.n - ctl[1]) : -1;
   if (err_bits) *err_bits = ctl[3] | (b->merged ? mctl[3] : 0ull);
@@ -832,6 +842,7 @@ int tvm_match_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err
     rc = TVM_EDEVICE;
   }
   b->merged = false;
+  b->st_valid = false;
   for (int i = 0; rc == TVM_OK && i < steps; i++)
     if (!e->eng->launch(b->dev, b->m, st, msg)) rc = TVM_EDEVICE;
   float f = 0;
@@ -1267,9 +1278,10 @@ int tvm_match_filter(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o, uint
   }
   (void)hipSetDevice(e->device);
   hipStream_t st = e->eng->stream();
-  uint64_t n = 0;
-  int64_t errp = -1;
-  int rc = match_status_locked(e, b, &n, &errp, nullptr);  // behind the batch's launches on st
+  uint64_t n = b->st_n;
+  int64_t errp = b->st_errp;
+  // the list's length: read back behind the batch's launches on st, once per launch / merge
+  int rc = b->st_valid ? TVM_OK : match_status_locked(e, b, &n, &errp, nullptr);
   if (rc) return rc;
   if (n > cur(b).cap || n > b->fill_cap) {
     set_err(err, errlen, "tvm_match_filter: run tvm_match_launch + tvm_match_fill with a large enough match buffer first");
@@ -1638,6 +1650,7 @@ bool rh_launch(tvm_engine* e, tvm_batch* b, std::string& err) {
   const RhInputs in = rh_inputs(e, b);
   if (!b->rh.launch(in, e->eng->stream(), err)) return false;
   b->merged = true;
+  b->st_valid = false;
   return true;
 }
 

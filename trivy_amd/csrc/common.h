@@ -55,13 +55,18 @@ enum : uint32_t {
 // Keys live in the key arena (8-byte aligned, little-endian words holding the
 // sort-key bytes in memory order).  lo/hi lengths carry flags in their top bits.
 struct alignas(16) Row {
-  uint32_t lo_off;   // word offset into key arena
-  uint32_t hi_off;
+  uint64_t hi_pre0;  // first 24 bytes of the hi key inline as BIG-ENDIAN words, zero padded, so a
+  uint64_t hi_pre1;  // compare is three u64 compares; it needs the key arena only when both keys
+  uint64_t hi_pre2;  // are longer than 24 bytes and their heads tie (dpkg keys are ~10-20 bytes)
   uint32_t adv;      // global advisory index (host-side record)
   uint16_t lo_len;   // bytes | flags
   uint16_t hi_len;
-  uint64_t hi_pre0;  // first 16 bytes of the hi key inline as BIG-ENDIAN words, zero padded, so a
-  uint64_t hi_pre1;  // compare is two u64 compares; most finish here without the key arena
+};
+// Key arena word offsets of a row's bounds (a parallel array, read only for a lower bound or
+// a 24-byte tie).
+struct RowOff {
+  uint32_t lo_off;
+  uint32_t hi_off;
 };
 enum : uint16_t {
   KEY_LEN_MASK = 0x3FFF,

@@ -534,6 +534,12 @@ void DB::flatten_os(uint32_t plat, const Bucket& root, int32_t ds) {
   }
 }
 
+// The hi key's first 24 bytes as the row's big-endian head words (zero padded).
+static void set_head(Row& r, const std::vector<uint8_t>& kb) {
+  uint64_t* w[3] = {&r.hi_pre0, &r.hi_pre1, &r.hi_pre2};
+  for (size_t i = 0; i < kb.size() && i < 24; i++) *w[i / 8] |= uint64_t(kb[i]) << (8 * (7 - i % 8));
+}
+
 // Advisory -> interval row(s) of its driver (SURVEY.md §8a' "unfixed" and parse-error
 // columns).  Returns false when the advisory can never be reported (no row).
 bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::vector<uint8_t>& kb) {
@@ -562,6 +568,7 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
       has_filters = true;
     }
     rows.push_back(r);
+    row_off.push_back(RowOff{});
     aux.push_back(x);
     if (!mvn_hybrid) return true;
   }
@@ -576,6 +583,7 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
       r.adv = ai | ROW_ALWAYS;
       r.lo_len = r.hi_len = KEY_INF;
       rows.push_back(r);
+      row_off.push_back(RowOff{});
       aux.push_back(RowAux{});
       return true;
     }
@@ -596,6 +604,7 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
     const uint32_t all = (1u << lr.ncls) - 1;
     for (const auto& [v, mask] : ivs) {
       Row r{};
+      RowOff o{};
       r.adv = ai;
       r.lo_len = r.hi_len = KEY_INF;
       auto put = [&](const KBound& b, uint32_t& off, uint16_t& len, bool hi) {
@@ -603,11 +612,10 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
         kb.assign(b.k.begin(), b.k.end());
         off = intern_key(kb);
         len = uint16_t(std::min<size_t>(kb.size(), KEY_LEN_MASK) | (b.incl ? KEY_INCL : 0));
-        if (hi)
-          for (size_t i = 0; i < kb.size() && i < 16; i++) (i < 8 ? r.hi_pre0 : r.hi_pre1) |= uint64_t(kb[i]) << (8 * (7 - i % 8));  // big-endian
+        if (hi) set_head(r, kb);
       };
-      put(v.lo, r.lo_off, r.lo_len, false);
-      put(v.hi, r.hi_off, r.hi_len, true);
+      put(v.lo, o.lo_off, r.lo_len, false);
+      put(v.hi, o.hi_off, r.hi_len, true);
       RowAux x{};
       if (mask != all) {
         r.adv |= ROW_FILTER;
@@ -616,11 +624,13 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
         has_filters = true;
       }
       rows.push_back(r);
+      row_off.push_back(o);
       aux.push_back(x);
     }
     return mvn_hybrid || !ivs.empty();
   }
   Row r{};
+  RowOff o{};
   r.adv = ai;
   r.lo_len = KEY_INF;
   r.hi_len = KEY_INF;
@@ -633,8 +643,8 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
     return true;
   };
   auto set_hi = [&](const std::string& v) {
-    if (!encode(v, r.hi_off, r.hi_len)) return false;
-    for (size_t i = 0; i < kb.size() && i < 16; i++) (i < 8 ? r.hi_pre0 : r.hi_pre1) |= uint64_t(kb[i]) << (8 * (7 - i % 8));  // big-endian
+    if (!encode(v, o.hi_off, r.hi_len)) return false;
+    set_head(r, kb);
     return true;
   };
   RowAux x{};
@@ -656,7 +666,7 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
       // alpine.go:122-153: installed >= AffectedVersion when set; unfixed reported
       if (!a.affected.empty()) {
         uint16_t l = 0;
-        if (!encode(a.affected, r.lo_off, l)) return false;
+        if (!encode(a.affected, o.lo_off, l)) return false;
         r.lo_len = uint16_t(l | KEY_INCL);
       }
       if (!a.fixed.empty() && !set_hi(a.fixed)) return false;
@@ -711,6 +721,7 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
     has_filters = true;
   }
   rows.push_back(r);
+  row_off.push_back(o);
   aux.push_back(x);
   return true;
 }
@@ -718,6 +729,7 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
 void DB::build_index() {
   // rows + key arena
   rows.clear();
+  row_off.clear();
   aux.clear();
   aux_ids.clear();
   std::vector<uint8_t> kb;

@@ -26,6 +26,7 @@ struct DevDB {
   uint64_t slot_mask = 0;
   const uint8_t* name_arena = nullptr;
   const Row* rows = nullptr;
+  const RowOff* row_off = nullptr;  // parallel to rows
   const uint64_t* key_words = nullptr;
   const PlatInfo* plats = nullptr;
   uint32_t n_plats = 0;
@@ -66,7 +67,7 @@ struct HostBatch {
 // first 16 bytes as big-endian words.
 struct PkgRec {
   uint4 meta;
-  uint64_t k0, k1;
+  uint64_t k0, k1, k2;  // the installed key's first 24 bytes, big-endian (rows compare 24-byte heads)
 };
 
 struct DevBatch {

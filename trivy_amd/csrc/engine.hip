@@ -213,12 +213,13 @@ Engine* Engine::open(const DB& db, int device, std::string& err) {
     delete e;
     return nullptr;
   }
-  Slot* sl; uint8_t* na; Row* rows; uint64_t* kw; PlatInfo* pl; RowAux* ax; uint32_t* ai;
+  Slot* sl; uint8_t* na; Row* rows; RowOff* ro; uint64_t* kw; PlatInfo* pl; RowAux* ax; uint32_t* ai;
   bool ok = upload_vec(db.aux, &ax, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.aux_ids, &ai, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.slots, &sl, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.name_arena, &na, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.rows, &rows, e->allocs_, e->table_bytes_, err) &&
+            upload_vec(db.row_off, &ro, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.key_words, &kw, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.plat_info, &pl, e->allocs_, e->table_bytes_, err);
   if (!ok) {
@@ -229,6 +230,7 @@ Engine* Engine::open(const DB& db, int device, std::string& err) {
   e->d_.slot_mask = db.slot_mask;
   e->d_.name_arena = na;
   e->d_.rows = rows;
+  e->d_.row_off = ro;
   e->d_.key_words = kw;
   e->d_.plats = pl;
   e->d_.aux = ax;
@@ -812,6 +814,7 @@ bool Engine::verify(std::string& err) {
   return check(d_.slots, db.slots.data(), db.slots.size() * sizeof(Slot), "slots") &&
          check(d_.name_arena, db.name_arena.data(), db.name_arena.size(), "name_arena") &&
          check(d_.rows, db.rows.data(), db.rows.size() * sizeof(Row), "rows") &&
+         check(d_.row_off, db.row_off.data(), db.row_off.size() * sizeof(RowOff), "row_off") &&
          check(d_.key_words, db.key_words.data(), db.key_words.size() * 8, "key_words") &&
          check(d_.plats, db.plat_info.data(), db.plat_info.size() * sizeof(PlatInfo), "plats") &&
          check(d_.aux, db.aux.data(), db.aux.size() * sizeof(RowAux), "aux") &&

@@ -133,13 +133,14 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t* wsum, uint32_t v, uin
 // sizes a long one (which is then re-encoded into the spill area).
 struct HeadSink {
   uint64_t* tail;
-  uint64_t acc = 0, w0 = 0, w1 = 0;
+  uint64_t acc = 0, w0 = 0, w1 = 0, w2 = 0;
   uint32_t n = 0;
   __device__ explicit HeadSink(uint64_t* t) : tail(t) {}
   __device__ __forceinline__ void word(uint32_t w) {
     if (w == 0) w0 = acc;
     else if (w == 1) w1 = acc;
     else if (w < kKeyWords) tail[w - 2] = acc;
+    if (w == 2) w2 = acc;
   }
   __device__ __forceinline__ void put(uint8_t b) {
     acc |= uint64_t(b) << (8 * (n & 7));
@@ -235,11 +236,12 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
       const bool valid = st == FAST_OK;
       const uint32_t* kw = reinterpret_cast<const uint32_t*>(kb);
       uint32_t kinfo = (valid ? (kl & KI_LEN) | KI_VALID : 0u), koff = 0;
-      r.k0 = r.k1 = 0;
+      r.k0 = r.k1 = r.k2 = 0;
       if (valid) {
         const uint64_t m0 = uint64_t(kw[0]) | (uint64_t(kw[1]) << 32), m1 = uint64_t(kw[2]) | (uint64_t(kw[3]) << 32);
         r.k0 = be_word(m0, kl < 8 ? kl : 8);
         r.k1 = kl > 8 ? be_word(m1, kl < 16 ? kl - 8 : 8) : 0ull;
+        r.k2 = kl > 16 ? be_word(uint64_t(kw[4]) | (uint64_t(kw[5]) << 32), kl < 24 ? kl - 16 : 8) : 0ull;
         static_assert(kFastKeyCap <= kKeyWords * 8, "fast keys fit head + tail slot");
         if (kl > 16) a.tail[p] = make_uint4(kw[4], kw[5], kw[6], kw[7]);
       }
@@ -307,6 +309,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
   if (((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN) kinfo |= KI_MVN;
   r.k0 = valid && kl ? be_word(hs.w0, kl < 8 ? kl : 8) : 0ull;
   r.k1 = valid && kl > 8 ? be_word(hs.w1, kl < 16 ? kl - 8 : 8) : 0ull;
+  r.k2 = valid && kl > 16 ? be_word(hs.w2, kl < 24 ? kl - 16 : 8) : 0ull;
   r.meta = make_uint4(rbeg, cnt, kinfo, koff);
 }
 
@@ -403,7 +406,7 @@ __global__ __launch_bounds__(kTile) void probe_kernel(ProbeArgs a) {
   __syncthreads();
   PkgRec r;
   r.meta = make_uint4(0, 0, 0, 0);
-  r.k0 = r.k1 = 0;
+  r.k0 = r.k1 = r.k2 = 0;
   if (p < a.n && d.x < a.db.n_plats) {
     if (staged) {
       const uint8_t* sb = reinterpret_cast<const uint8_t*>(stage) + uint32_t(w0 - base16) + off;
@@ -421,7 +424,7 @@ __global__ __launch_bounds__(kTile) void probe_kernel(ProbeArgs a) {
 
 template <int FILT>
 struct SweepShared {
-  uint64_t k0[kTile], k1[kTile];  // key heads by tile package
+  uint64_t k0[kTile], k1[kTile], k2[kTile];  // key heads by tile package
   uint32_t kinfo[kTile];
   uint32_t koff[kTile];           // spill word offset of a long key (KI_SPILL)
   uint2 pattr[FILT ? kTile : 1];
@@ -491,40 +494,40 @@ __device__ __forceinline__ int cmp_be(uint64_t a0, uint64_t a1, const uint64_t* 
   return key_cmp(atail, na - 16, btail, nb - 16);
 }
 
-// sign(installed - bound) from the big-endian 16-byte heads alone, branch-free: valid
-// unless both heads tie and both keys are longer than 16 bytes (`tie`, then cmp_be).
-__device__ __forceinline__ int cmp_head(uint64_t a0, uint64_t a1, uint32_t na, uint64_t b0, uint64_t b1, uint32_t nb,
-                                        bool& tie) {
-  const bool eq0 = a0 == b0, eq = eq0 && a1 == b1;
-  const bool lt = a0 < b0 || (eq0 && a1 < b1);
-  tie = eq && na > 16 && nb > 16;
+// sign(installed - bound) from the big-endian 24-byte heads alone, branch-free: valid
+// unless both heads tie and both keys are longer than 24 bytes (`tie`: the key tails).
+__device__ __forceinline__ int cmp_head(uint64_t a0, uint64_t a1, uint64_t a2, uint32_t na, uint64_t b0, uint64_t b1,
+                                        uint64_t b2, uint32_t nb, bool& tie) {
+  const bool eq0 = a0 == b0, eq1 = eq0 && a1 == b1, eq = eq1 && a2 == b2;
+  const bool lt = a0 < b0 || (eq0 && a1 < b1) || (eq1 && a2 < b2);
+  tie = eq && na > 24 && nb > 24;
   const int byl = (na > nb) - (na < nb);
   return eq ? byl : (lt ? -1 : 1);
 }
 
 // Interval test of tile package q's installed key against one row (global index ridx).
-// The common case (a bound decided by the inline 16-byte heads) runs without branches;
-// a 16-byte tie reads the key tails, a lower bound (library / rpm ranges) its key head.
+// The common case (a bound decided by the inline 24-byte heads) runs without branches;
+// a 24-byte tie reads the key tails, a lower bound (library / rpm ranges) its key head.
 template <int FILT, bool DEFER = false, class S>
 __device__ __forceinline__ uint32_t eval_row(const SweepArgs& a, const S& s, uint32_t q, uint32_t p, const Row& row,
                                              uint32_t ridx) {
   const uint32_t ki = s.kinfo[q];
   const uint32_t kl = ki & KI_LEN;
-  const uint64_t k0 = s.k0[q], k1 = s.k1[q];
+  const uint64_t k0 = s.k0[q], k1 = s.k1[q], k2 = s.k2[q];
   const uint32_t nh = row.hi_len & KEY_LEN_MASK;
   bool tie = false;
-  int c = cmp_head(k0, k1, kl, row.hi_pre0, row.hi_pre1, nh, tie);
+  int c = cmp_head(k0, k1, k2, kl, row.hi_pre0, row.hi_pre1, row.hi_pre2, nh, tie);
   const bool hi_inf = (row.hi_len & KEY_INF) != 0;
-  if (tie && !hi_inf) {  // rare: same 16-byte head, both keys longer
+  if (tie && !hi_inf) {  // rare: same 24-byte head, both keys longer
     const uint64_t* ktail =
         (ki & KI_SPILL) ? a.spill + s.koff[q] + 2 : reinterpret_cast<const uint64_t*>(a.tail + p);
-    c = key_cmp(ktail, kl - 16, a.db.key_words + row.hi_off + 2, nh - 16);
+    c = key_cmp(ktail + 1, kl - 24, a.db.key_words + a.db.row_off[ridx].hi_off + 3, nh - 24);
   }
   bool m = hi_inf || ((row.hi_len & KEY_INCL) ? c <= 0 : c < 0);
   if (!(row.lo_len & KEY_INF) && m) {  // rare (library / rpm ranges): the bound's head from the arena
     const uint64_t* ktail =
         (ki & KI_SPILL) ? a.spill + s.koff[q] + 2 : reinterpret_cast<const uint64_t*>(a.tail + p);
-    const uint64_t* lw = a.db.key_words + row.lo_off;
+    const uint64_t* lw = a.db.key_words + a.db.row_off[ridx].lo_off;
     const uint32_t nl = row.lo_len & KEY_LEN_MASK;
     const uint64_t l0 = nl ? be_word(lw[0], nl < 8 ? nl : 8) : 0ull;
     const uint64_t l1 = nl > 8 ? be_word(lw[1], nl < 16 ? nl - 8 : 8) : 0ull;
@@ -752,6 +755,7 @@ __device__ __forceinline__ void sweep_tile(const SweepArgs& a, SweepShared<FILT>
   const uint32_t p = t * kTile + tid;
   s.k0[tid] = r.k0;
   s.k1[tid] = r.k1;
+  s.k2[tid] = r.k2;
   s.kinfo[tid] = r.meta.z;
   s.koff[tid] = r.meta.w;
   if constexpr (FILT) s.pattr[tid] = (a.attr && p < a.n) ? a.attr[p] : make_uint2(PA_ARCH_NONE, 0xFFFFFFFFu);
@@ -870,7 +874,7 @@ __global__ __launch_bounds__(kTile) void sweep_kernel(SweepArgs a) {
   const uint32_t p = t * kTile + tid;
   PkgRec r;
   r.meta = make_uint4(0, 0, 0, 0);
-  r.k0 = r.k1 = 0;
+  r.k0 = r.k1 = r.k2 = 0;
   if (p < a.n) r = a.rec[p];
   sweep_tile<K, MB, FILT>(a, s, madv, mq, map, t, tid, r, DeferQ{dqj, dqres, FILT >= 2 ? kQ : 0u});
 }
@@ -945,7 +949,7 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
   }
   PkgRec r;
   r.meta = make_uint4(0, 0, 0, 0);
-  r.k0 = r.k1 = 0;
+  r.k0 = r.k1 = r.k2 = 0;
   if (p < a.n && d.x < a.db.n_plats) {
     if (staged) {
       const uint8_t* sb = reinterpret_cast<const uint8_t*>(sbuf) + uint32_t(w0 - base16) + off;
