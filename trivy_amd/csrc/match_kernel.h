@@ -44,7 +44,8 @@ namespace tvm {
 
 constexpr uint32_t kStage = 12288;  // LDS bytes for a tile's strings (larger windows read global memory)
 constexpr uint32_t kKeyWords = 4;   // key bytes kept per package (head 16 in registers, tail 16 in a slot)
-constexpr uint32_t kMapCap = 4096;  // tiles with at most this many pairs map pair -> package by an LDS byte map
+constexpr uint32_t kMapCap = 4096;  // LDS byte map pair -> package: one entry per pair up to this many pairs,
+                                    // one per 2^shift pairs above (map_shift, map_rank)
 
 struct ProbeArgs {
   DevDB db;
@@ -208,16 +209,17 @@ __device__ __forceinline__ bool name_eq_slot(const uint8_t* s, uint32_t n, const
 }
 
 // Index probe of one package given its key state (shared by the fast and generic paths).
-// h / q0: the name's hash and the first 16 bytes of its home slot, loaded before the version
-// is encoded so the slot's round trip overlaps the encoder.
+// h / q0 / q0n: the name's hash and the first 16 bytes of its home slot and of the slot after
+// it, loaded before the version is encoded so the round trips overlap the encoder (the table
+// is at most half full, but a quarter of the lanes of a wave still probe a second slot).
 template <class P>
 __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uint32_t plat, const PlatInfo& pi,
                                             uint32_t nlen, const uint8_t* name, bool valid, uint64_t h, uint4 q0,
-                                            uint32_t& rbeg, uint32_t& cnt, uint32_t* sflags = nullptr);
+                                            uint4 q0n, uint32_t& rbeg, uint32_t& cnt, uint32_t* sflags = nullptr);
 
 template <class P>
-__device__ __forceinline__ uint4 home_slot(const ProbeArgs& a, uint64_t h) {
-  return reinterpret_cast<const uint4*>(a.db.slots + (h & a.db.slot_mask))[0];
+__device__ __forceinline__ uint4 home_slot(const ProbeArgs& a, uint64_t h, uint32_t step = 0) {
+  return reinterpret_cast<const uint4*>(a.db.slots + ((h + step) & a.db.slot_mask))[0];
 }
 
 // One package: encode, hash, probe.  P = uint32_t in the LDS or global address space of s.
@@ -229,6 +231,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
   const PlatInfo pi = a.db.plats[plat];
   const uint64_t h = (DIAG & 2) ? 0ull : name_hash<P>(plat, name, nlen);
   const uint4 q0 = (DIAG & 2) ? make_uint4(0, 0, 0, 0) : home_slot<P>(a, h);
+  const uint4 q0n = (DIAG & 2) ? make_uint4(0, 0, 0, 0) : home_slot<P>(a, h, 1);
   if (!(DIAG & 1) && kb && ((GM >> CMP_DEB) & 1u) && pi.cmp == CMP_DEB) {
     uint32_t kl = 0;
     const uint32_t st = deb_fast_key(ver, vlen, kb, tab, kl);
@@ -246,7 +249,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
         if (kl > 16) a.tail[p] = make_uint4(kw[4], kw[5], kw[6], kw[7]);
       }
       uint32_t cnt = 0, rbeg = 0;
-      if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, (kinfo & KI_VALID) != 0, h, q0, rbeg, cnt);
+      if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, (kinfo & KI_VALID) != 0, h, q0, q0n, rbeg, cnt);
       r.meta = make_uint4(rbeg, cnt, kinfo, koff);
       return;
     }
@@ -279,7 +282,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
     }
   }
   uint32_t cnt = 0, rbeg = 0, sflags = 0;
-  if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, valid, h, q0, rbeg, cnt, &sflags);
+  if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, valid, h, q0, q0n, rbeg, cnt, &sflags);
   if (((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN) {
     // Maven rows compare parses, not keys (AUX_MVN): the installed version's parse, packed
     // into the batch scratch, and its text location take the tail slot - only when the key
@@ -316,13 +319,15 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
 template <class P>
 __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uint32_t plat, const PlatInfo& pi,
                                             uint32_t nlen, const uint8_t* name, bool valid, uint64_t h,
-                                            uint4 q0, uint32_t& rbeg, uint32_t& cnt, uint32_t* sflags) {
+                                            uint4 q0, uint4 q0n, uint32_t& rbeg, uint32_t& cnt, uint32_t* sflags) {
   // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup;
   // lookup-first drivers (ubuntu.go:86-92) probe first, so a poisoned key still raises
   if (valid || (pi.flags & PLAT_LOOKUP_FIRST)) {
-    for (uint64_t i = h & a.db.slot_mask;; i = (i + 1) & a.db.slot_mask) {
+    uint32_t step = 0;
+    for (uint64_t i = h & a.db.slot_mask;; i = (i + 1) & a.db.slot_mask, step++) {
       const uint4* sp = reinterpret_cast<const uint4*>(a.db.slots + i);
-      if (i != (h & a.db.slot_mask)) q0 = sp[0];
+      if (step == 1) q0 = q0n;
+      else if (step > 1) q0 = sp[0];
       const uint4 q1 = sp[1], q2 = sp[2], q3 = sp[3];  // the rest of the 64-B slot
       const uint64_t sh = q0.x | (uint64_t(q0.y) << 32);
       if (sh == 0) break;
@@ -436,6 +441,14 @@ struct SweepShared {
   uint32_t tile;
   unsigned long long base;
 };
+
+// log2 of the pairs per map entry: 0 up to kMapCap pairs (an entry per pair), else the
+// smallest power of two that fits the tile's pairs into kMapCap entries.
+__device__ __forceinline__ uint32_t map_shift(uint32_t total) {
+  uint32_t sh = 0;
+  while ((total + (1u << sh) - 1) >> sh > kMapCap) sh++;
+  return sh;
+}
 
 // Per-package predicates of a ROW_FILTER row (common.h RowAux); p = the package's index
 // in the launch (its tail slot holds a Maven package's text location, probe_one).
@@ -563,7 +576,7 @@ __device__ __forceinline__ uint32_t sweep_programs(const SweepArgs& a, const Swe
   const uint32_t n = block_exscan<kTile>(ws, uint32_t(__popc(pend)), tid, excl);
   if (n == 0) return 0;
   if (tid < kTile / 8) q.res[tid] = 0;
-  const bool use_map = total <= kMapCap;
+  const uint32_t shift = map_shift(total);
   const uint32_t pbase = s.tile * kTile;
   for (uint32_t q0 = 0; q0 < n; q0 += q.cap) {
     uint32_t o = excl;
@@ -577,7 +590,7 @@ __device__ __forceinline__ uint32_t sweep_programs(const SweepArgs& a, const Swe
     const uint32_t m = min(q.cap, n - q0);
     for (uint32_t e = tid; e < m; e += kTile) {
       const uint32_t j = q.j[e];
-      const uint32_t r = use_map ? uint32_t(map[j]) : pair_rank(s, nnz, j);
+      const uint32_t r = map_rank(s, map, shift, j);
       const uint32_t ridx = j + s.nz_rd[r];
       if (mvn_pair<FILT>(a, a.db.aux_ids + a.db.aux[ridx].list_off, pbase + s.nz_q[r])) {
         const uint32_t owner = (j - b0) % kTile, kk = (j - b0) / kTile;
@@ -589,7 +602,20 @@ __device__ __forceinline__ uint32_t sweep_programs(const SweepArgs& a, const Swe
   return (q.res[tid >> 3] >> ((tid & 7) * 4)) & 0xFu;
 }
 
-// Tile package (nz rank) of pair j by binary search of the nz scan (tiles too large for the map).
+// Tile package (nz rank) of pair j from the map: its entry, or (shift > 0) its bucket's entry
+// advanced over the packages that start inside the bucket before j (a tile has at most 256
+// packages over at least 4096 buckets: rarely a step).  Tiles above kMapCap pairs were a
+// binary search per pair before, and they are the grid's heaviest tiles (C2: 2.6 % of the
+// tiles, 6 % of the pairs).
+template <int FILT>
+__device__ __forceinline__ uint32_t map_rank(const SweepShared<FILT>& s, const uint8_t* map, uint32_t shift, uint32_t j) {
+  if (shift == 0) return map[j];
+  uint32_t r = map[j >> shift];
+  while (s.nz_scan[r + 1] <= j) r++;
+  return r;
+}
+
+// Tile package (nz rank) of pair j by binary search of the nz scan.
 template <int FILT>
 __device__ __forceinline__ uint32_t pair_rank(const SweepShared<FILT>& s, uint32_t nnz, uint32_t j) {
   uint32_t lo = 0, hi = nnz;  // last r with nz_scan[r] <= j
@@ -616,7 +642,7 @@ __device__ __forceinline__ uint32_t sweep(const SweepArgs& a, SweepShared<FILT>&
   const uint32_t lane = tid & 63, wave = tid >> 6;
   const unsigned long long lt = (1ull << lane) - 1ull;
   const uint32_t pbase = s.tile * kTile;
-  const bool use_map = total <= kMapCap;
+  const uint32_t shift = map_shift(total);
   uint32_t nm = 0, round = 0;
   for (uint32_t b0 = 0; b0 < total; b0 += kTile * K, round++) {
     // every lane issues its K row loads back to back, unconditionally (pairs past the end
@@ -624,16 +650,8 @@ __device__ __forceinline__ uint32_t sweep(const SweepArgs& a, SweepShared<FILT>&
     // waits once; a load under a branch would be waited for before the next one issues
     Row row[K];
     uint32_t qq[K], rid[K];
-    if (use_map) {
 #pragma unroll
-      for (int k = 0; k < K; k++) {
-        const uint32_t j = min(b0 + k * kTile + tid, total - 1);
-        rid[k] = map[j];
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < K; k++) rid[k] = pair_rank(s, nnz, min(b0 + k * kTile + tid, total - 1));
-    }
+    for (int k = 0; k < K; k++) rid[k] = map_rank(s, map, shift, min(b0 + k * kTile + tid, total - 1));
 #pragma unroll
     for (int k = 0; k < K; k++) {
       const uint32_t r = rid[k];
@@ -704,7 +722,7 @@ __device__ __forceinline__ uint32_t sweep_seg(const SweepArgs& a, const SweepSha
                                               uint32_t s0, uint32_t s1, uint32_t lane, unsigned long long base) {
   const unsigned long long lt = (1ull << lane) - 1ull;
   const uint32_t pbase = s.tile * kTile;
-  const bool use_map = total <= kMapCap;
+  const uint32_t shift = map_shift(total);
   uint32_t nm = 0;
   for (uint32_t b0 = s0; b0 < s1; b0 += 64 * K) {
     Row row[K];
@@ -712,7 +730,7 @@ __device__ __forceinline__ uint32_t sweep_seg(const SweepArgs& a, const SweepSha
 #pragma unroll
     for (int k = 0; k < K; k++) {
       const uint32_t j = min(b0 + k * 64 + lane, s1 - 1);
-      rid[k] = use_map ? uint32_t(map[j]) : pair_rank(s, nnz, j);
+      rid[k] = map_rank(s, map, shift, j);
     }
 #pragma unroll
     for (int k = 0; k < K; k++) {
@@ -780,15 +798,16 @@ __device__ __forceinline__ void sweep_tile(const SweepArgs& a, SweepShared<FILT>
   }
   if (tid == 0) s.nz_scan[nnz] = total;
   __syncthreads();
-  if (total <= kMapCap) {  // pair -> nz rank map: every lane fills a contiguous run of it
-    const uint32_t per = (total + kTile - 1) / kTile;
-    uint32_t j = tid * per;
-    const uint32_t je = min(j + per, total);
-    if (j < je) {
-      uint32_t rr = pair_rank(s, nnz, j);
-      for (; j < je; j++) {
-        while (s.nz_scan[rr + 1] <= j) rr++;
-        map[j] = uint8_t(rr);
+  {  // pair (bucket of 2^shift pairs) -> nz rank map: every lane fills a contiguous run of it
+    const uint32_t shift = map_shift(total), nb = (total + (1u << shift) - 1) >> shift;
+    const uint32_t per = (nb + kTile - 1) / kTile;
+    uint32_t b = tid * per;
+    const uint32_t be = min(b + per, nb);
+    if (b < be) {
+      uint32_t rr = pair_rank(s, nnz, b << shift);
+      for (; b < be; b++) {
+        while (s.nz_scan[rr + 1] <= (b << shift)) rr++;
+        map[b] = uint8_t(rr);
       }
     }
     __syncthreads();
