@@ -229,9 +229,19 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
                                           const uint8_t* name, const uint8_t* ver, uint64_t vglob, PkgRec& r,
                                           uint8_t* kb = nullptr, const uint8_t* tab = nullptr) {
   const PlatInfo pi = a.db.plats[plat];
-  const uint64_t h = (DIAG & 2) ? 0ull : name_hash<P>(plat, name, nlen);
-  const uint4 q0 = (DIAG & 2) ? make_uint4(0, 0, 0, 0) : home_slot<P>(a, h);
-  const uint4 q0n = (DIAG & 2) ? make_uint4(0, 0, 0, 0) : home_slot<P>(a, h, 1);
+  // the dpkg-only kernels load the slot heads before the encoder; the other grammar sets
+  // after it (their encoders' registers: held across them, the heads made the all-grammar
+  // kernel spill)
+  constexpr bool kPre = GM == GM_DEB;
+  uint64_t h = 0;
+  uint4 q0 = make_uint4(0, 0, 0, 0), q0n = q0;
+  auto heads = [&]() {
+    if (DIAG & 2) return;
+    h = name_hash<P>(plat, name, nlen);
+    q0 = home_slot<P>(a, h);
+    q0n = home_slot<P>(a, h, 1);
+  };
+  if constexpr (kPre) heads();
   if (!(DIAG & 1) && kb && ((GM >> CMP_DEB) & 1u) && pi.cmp == CMP_DEB) {
     uint32_t kl = 0;
     const uint32_t st = deb_fast_key(ver, vlen, kb, tab, kl);
@@ -249,6 +259,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
         if (kl > 16) a.tail[p] = make_uint4(kw[4], kw[5], kw[6], kw[7]);
       }
       uint32_t cnt = 0, rbeg = 0;
+      if constexpr (!kPre) heads();
       if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, (kinfo & KI_VALID) != 0, h, q0, q0n, rbeg, cnt);
       r.meta = make_uint4(rbeg, cnt, kinfo, koff);
       return;
@@ -282,6 +293,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
     }
   }
   uint32_t cnt = 0, rbeg = 0, sflags = 0;
+  if constexpr (!kPre) heads();
   if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, valid, h, q0, q0n, rbeg, cnt, &sflags);
   if (((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN) {
     // Maven rows compare parses, not keys (AUX_MVN): the installed version's parse, packed
@@ -521,9 +533,11 @@ __device__ __forceinline__ int cmp_head(uint64_t a0, uint64_t a1, uint64_t a2, u
 // Interval test of tile package q's installed key against one row (global index ridx).
 // The common case (a bound decided by the inline 24-byte heads) runs without branches;
 // a 24-byte tie reads the key tails, a lower bound (library / rpm ranges) its key head.
+// ro: the row's bound offsets, loaded with the row where lower bounds are common (FILT >= 2:
+// library ranges), else read here on the rare path that needs them.
 template <int FILT, bool DEFER = false, class S>
 __device__ __forceinline__ uint32_t eval_row(const SweepArgs& a, const S& s, uint32_t q, uint32_t p, const Row& row,
-                                             uint32_t ridx) {
+                                             uint32_t ridx, const RowOff& ro) {
   const uint32_t ki = s.kinfo[q];
   const uint32_t kl = ki & KI_LEN;
   const uint64_t k0 = s.k0[q], k1 = s.k1[q], k2 = s.k2[q];
@@ -534,13 +548,13 @@ __device__ __forceinline__ uint32_t eval_row(const SweepArgs& a, const S& s, uin
   if (tie && !hi_inf) {  // rare: same 24-byte head, both keys longer
     const uint64_t* ktail =
         (ki & KI_SPILL) ? a.spill + s.koff[q] + 2 : reinterpret_cast<const uint64_t*>(a.tail + p);
-    c = key_cmp(ktail + 1, kl - 24, a.db.key_words + a.db.row_off[ridx].hi_off + 3, nh - 24);
+    c = key_cmp(ktail + 1, kl - 24, a.db.key_words + (FILT >= 2 ? ro.hi_off : a.db.row_off[ridx].hi_off) + 3, nh - 24);
   }
   bool m = hi_inf || ((row.hi_len & KEY_INCL) ? c <= 0 : c < 0);
   if (!(row.lo_len & KEY_INF) && m) {  // rare (library / rpm ranges): the bound's head from the arena
     const uint64_t* ktail =
         (ki & KI_SPILL) ? a.spill + s.koff[q] + 2 : reinterpret_cast<const uint64_t*>(a.tail + p);
-    const uint64_t* lw = a.db.key_words + a.db.row_off[ridx].lo_off;
+    const uint64_t* lw = a.db.key_words + (FILT >= 2 ? ro.lo_off : a.db.row_off[ridx].lo_off);
     const uint32_t nl = row.lo_len & KEY_LEN_MASK;
     const uint64_t l0 = nl ? be_word(lw[0], nl < 8 ? nl : 8) : 0ull;
     const uint64_t l1 = nl > 8 ? be_word(lw[1], nl < 16 ? nl - 8 : 8) : 0ull;
@@ -649,6 +663,7 @@ __device__ __forceinline__ uint32_t sweep(const SweepArgs& a, SweepShared<FILT>&
     // re-read the tile's last pair), so the K loads are in flight together and the lane
     // waits once; a load under a branch would be waited for before the next one issues
     Row row[K];
+    RowOff ro[K] = {};
     uint32_t qq[K], rid[K];
 #pragma unroll
     for (int k = 0; k < K; k++) rid[k] = map_rank(s, map, shift, min(b0 + k * kTile + tid, total - 1));
@@ -659,11 +674,14 @@ __device__ __forceinline__ uint32_t sweep(const SweepArgs& a, SweepShared<FILT>&
       rid[k] = min(b0 + k * kTile + tid, total - 1) + s.nz_rd[r];
     }
 #pragma unroll
-    for (int k = 0; k < K; k++) row[k] = a.db.rows[rid[k]];
+    for (int k = 0; k < K; k++) {
+      row[k] = a.db.rows[rid[k]];
+      if constexpr (FILT >= 2) ro[k] = a.db.row_off[rid[k]];
+    }
     uint32_t mask = 0, pend = 0;
 #pragma unroll
     for (int k = 0; k < K; k++) {
-      const uint32_t e = eval_row<FILT, (FILT >= 2)>(a, s, qq[k], pbase + qq[k], row[k], rid[k]);
+      const uint32_t e = eval_row<FILT, (FILT >= 2)>(a, s, qq[k], pbase + qq[k], row[k], rid[k], ro[k]);
       const bool in = b0 + k * kTile + tid < total;
       mask |= (e == 1 && in) ? 1u << k : 0u;
       pend |= (e == 2 && in) ? 1u << k : 0u;
@@ -726,6 +744,7 @@ __device__ __forceinline__ uint32_t sweep_seg(const SweepArgs& a, const SweepSha
   uint32_t nm = 0;
   for (uint32_t b0 = s0; b0 < s1; b0 += 64 * K) {
     Row row[K];
+    RowOff ro[K] = {};
     uint32_t qq[K], rid[K];
 #pragma unroll
     for (int k = 0; k < K; k++) {
@@ -739,10 +758,13 @@ __device__ __forceinline__ uint32_t sweep_seg(const SweepArgs& a, const SweepSha
       rid[k] = min(b0 + k * 64 + lane, s1 - 1) + s.nz_rd[r];
     }
 #pragma unroll
-    for (int k = 0; k < K; k++) row[k] = a.db.rows[rid[k]];
+    for (int k = 0; k < K; k++) {
+      row[k] = a.db.rows[rid[k]];
+      if constexpr (FILT >= 2) ro[k] = a.db.row_off[rid[k]];
+    }
 #pragma unroll
     for (int k = 0; k < K; k++) {
-      const bool m = eval_row<FILT>(a, s, qq[k], pbase + qq[k], row[k], rid[k]) != 0 && b0 + k * 64 + lane < s1;
+      const bool m = eval_row<FILT>(a, s, qq[k], pbase + qq[k], row[k], rid[k], ro[k]) != 0 && b0 + k * 64 + lane < s1;
       const unsigned long long bal = __ballot(m);
       if (m) {
         const uint32_t pos = nm + uint32_t(__popcll(bal & lt));
