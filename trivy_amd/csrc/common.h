@@ -54,19 +54,23 @@ enum : uint32_t {
 //   ALWAYS, or v parsed and lo <=/< v and v </<= hi.
 // Keys live in the key arena (8-byte aligned, little-endian words holding the
 // sort-key bytes in memory order).  lo/hi lengths carry flags in their top bits.
-struct alignas(16) Row {
-  uint64_t hi_pre0;  // first 24 bytes of the hi key inline as BIG-ENDIAN words, zero padded, so a
-  uint64_t hi_pre1;  // compare is three u64 compares; it needs the key arena only when both keys
-  uint64_t hi_pre2;  // are longer than 24 bytes and their heads tie (dpkg keys are ~10-20 bytes)
-  uint32_t adv;      // global advisory index (host-side record)
-  uint16_t lo_len;   // bytes | flags
-  uint16_t hi_len;
-};
-// Key arena word offsets of a row's bounds (a parallel array, read only for a lower bound or
-// a 24-byte tie).
+// Key arena word offsets of a row's bounds.
 struct RowOff {
   uint32_t lo_off;
   uint32_t hi_off;
+};
+struct alignas(16) Row {
+  uint64_t hi_pre0;  // the hi key's first bytes inline as BIG-ENDIAN words, zero padded, so a
+  uint64_t hi_pre1;  // compare is two / three u64 compares that rarely touch the key arena
+  union {
+    uint64_t hi_pre2;  // dpkg grammar: key bytes 16..23 (24-byte heads: its version keys are ~10-20
+                       // bytes and tie often at 16); the offsets sit in DB::row_off
+    RowOff off;        // the other grammars: 16-byte heads, offsets inline (their lower bounds,
+                       // library / apk ranges, read the arena at once)
+  };
+  uint32_t adv;      // global advisory index (host-side record)
+  uint16_t lo_len;   // bytes | flags
+  uint16_t hi_len;
 };
 enum : uint16_t {
   KEY_LEN_MASK = 0x3FFF,

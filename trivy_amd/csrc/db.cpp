@@ -534,10 +534,11 @@ void DB::flatten_os(uint32_t plat, const Bucket& root, int32_t ds) {
   }
 }
 
-// The hi key's first 24 bytes as the row's big-endian head words (zero padded).
-static void set_head(Row& r, const std::vector<uint8_t>& kb) {
+// The hi key's first bytes as the row's big-endian head words (zero padded): 24 for the
+// dpkg grammar (Row::hi_pre2), else 16.
+static void set_head(Row& r, const std::vector<uint8_t>& kb, bool h24) {
   uint64_t* w[3] = {&r.hi_pre0, &r.hi_pre1, &r.hi_pre2};
-  for (size_t i = 0; i < kb.size() && i < 24; i++) *w[i / 8] |= uint64_t(kb[i]) << (8 * (7 - i % 8));
+  for (size_t i = 0; i < kb.size() && i < (h24 ? 24u : 16u); i++) *w[i / 8] |= uint64_t(kb[i]) << (8 * (7 - i % 8));
 }
 
 // Advisory -> interval row(s) of its driver (SURVEY.md §8a' "unfixed" and parse-error
@@ -612,7 +613,7 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
         kb.assign(b.k.begin(), b.k.end());
         off = intern_key(kb);
         len = uint16_t(std::min<size_t>(kb.size(), KEY_LEN_MASK) | (b.incl ? KEY_INCL : 0));
-        if (hi) set_head(r, kb);
+        if (hi) set_head(r, kb, false);
       };
       put(v.lo, o.lo_off, r.lo_len, false);
       put(v.hi, o.hi_off, r.hi_len, true);
@@ -623,6 +624,7 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
         x.tag = mask;
         has_filters = true;
       }
+      r.off = o;  // library rows: 16-byte heads, offsets inline
       rows.push_back(r);
       row_off.push_back(o);
       aux.push_back(x);
@@ -644,7 +646,7 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
   };
   auto set_hi = [&](const std::string& v) {
     if (!encode(v, o.hi_off, r.hi_len)) return false;
-    set_head(r, kb);
+    set_head(r, kb, P.cmp == CMP_DEB);
     return true;
   };
   RowAux x{};
@@ -720,6 +722,7 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
     }
     has_filters = true;
   }
+  if (P.cmp != CMP_DEB) r.off = o;  // else Row::hi_pre2 holds key bytes 16..23
   rows.push_back(r);
   row_off.push_back(o);
   aux.push_back(x);

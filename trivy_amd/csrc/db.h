@@ -109,7 +109,7 @@ class DB {
   std::vector<uint32_t> slot_key;   // host only: slot -> Key index
   std::vector<uint8_t> name_arena;
   std::vector<Row> rows;
-  std::vector<RowOff> row_off;  // parallel to rows
+  std::vector<RowOff> row_off;  // parallel to rows (the dpkg grammar's rows keep their offsets here only)
   std::vector<RowAux> aux;          // parallel to rows (read only for ROW_FILTER rows)
   std::vector<uint32_t> aux_ids;
   std::vector<uint64_t> key_words;

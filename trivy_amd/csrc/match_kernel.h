@@ -99,7 +99,9 @@ using FusedFn = void (*)(uint32_t n_tiles, hipStream_t st, const FusedArgs& a);
 namespace {
 
 // KI_MVN: a Maven package (its rows may carry pairwise programs: the sweep defers those)
-enum : uint32_t { KI_VALID = 1u << 31, KI_SPILL = 1u << 30, KI_MVN = 1u << 29, KI_LEN = 0x3FFFu, KI_CLS_SHIFT = 26, KI_CLS_MASK = 7u };
+// KI_H24: a dpkg-grammar package (its rows carry 24-byte key heads, Row::hi_pre2)
+enum : uint32_t { KI_VALID = 1u << 31, KI_SPILL = 1u << 30, KI_MVN = 1u << 29, KI_H24 = 1u << 25, KI_LEN = 0x3FFFu,
+                  KI_CLS_SHIFT = 26, KI_CLS_MASK = 7u };
 
 // Block-wide exclusive scan of v over T lanes (wave shuffles + one LDS exchange); returns
 // the block total.  `wsum` holds T/64 words; two barriers.
@@ -215,7 +217,8 @@ __device__ __forceinline__ bool name_eq_slot(const uint8_t* s, uint32_t n, const
 template <class P>
 __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uint32_t plat, const PlatInfo& pi,
                                             uint32_t nlen, const uint8_t* name, bool valid, uint64_t h, uint4 q0,
-                                            uint4 q0n, uint32_t& rbeg, uint32_t& cnt, uint32_t* sflags = nullptr);
+                                            uint4 q0n, bool has_q0n, uint32_t& rbeg, uint32_t& cnt,
+                                            uint32_t* sflags = nullptr);
 
 template <class P>
 __device__ __forceinline__ uint4 home_slot(const ProbeArgs& a, uint64_t h, uint32_t step = 0) {
@@ -239,7 +242,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
     if (DIAG & 2) return;
     h = name_hash<P>(plat, name, nlen);
     q0 = home_slot<P>(a, h);
-    q0n = home_slot<P>(a, h, 1);
+    if constexpr (kPre) q0n = home_slot<P>(a, h, 1);
   };
   if constexpr (kPre) heads();
   if (!(DIAG & 1) && kb && ((GM >> CMP_DEB) & 1u) && pi.cmp == CMP_DEB) {
@@ -248,7 +251,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
     if (st != FAST_FALLBACK) {
       const bool valid = st == FAST_OK;
       const uint32_t* kw = reinterpret_cast<const uint32_t*>(kb);
-      uint32_t kinfo = (valid ? (kl & KI_LEN) | KI_VALID : 0u), koff = 0;
+      uint32_t kinfo = (valid ? (kl & KI_LEN) | KI_VALID : 0u) | KI_H24, koff = 0;
       r.k0 = r.k1 = r.k2 = 0;
       if (valid) {
         const uint64_t m0 = uint64_t(kw[0]) | (uint64_t(kw[1]) << 32), m1 = uint64_t(kw[2]) | (uint64_t(kw[3]) << 32);
@@ -260,7 +263,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
       }
       uint32_t cnt = 0, rbeg = 0;
       if constexpr (!kPre) heads();
-      if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, (kinfo & KI_VALID) != 0, h, q0, q0n, rbeg, cnt);
+      if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, (kinfo & KI_VALID) != 0, h, q0, q0n, kPre, rbeg, cnt);
       r.meta = make_uint4(rbeg, cnt, kinfo, koff);
       return;
     }
@@ -294,7 +297,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
   }
   uint32_t cnt = 0, rbeg = 0, sflags = 0;
   if constexpr (!kPre) heads();
-  if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, valid, h, q0, q0n, rbeg, cnt, &sflags);
+  if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, valid, h, q0, q0n, kPre, rbeg, cnt, &sflags);
   if (((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN) {
     // Maven rows compare parses, not keys (AUX_MVN): the installed version's parse, packed
     // into the batch scratch, and its text location take the tail slot - only when the key
@@ -321,6 +324,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
   }
   const uint32_t kl = hs.n;
   kinfo |= (kl & KI_LEN) | (valid ? KI_VALID : 0u) | ((cls & KI_CLS_MASK) << KI_CLS_SHIFT);
+  if (pi.cmp == CMP_DEB) kinfo |= KI_H24;
   if (((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN) kinfo |= KI_MVN;
   r.k0 = valid && kl ? be_word(hs.w0, kl < 8 ? kl : 8) : 0ull;
   r.k1 = valid && kl > 8 ? be_word(hs.w1, kl < 16 ? kl - 8 : 8) : 0ull;
@@ -331,15 +335,16 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
 template <class P>
 __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uint32_t plat, const PlatInfo& pi,
                                             uint32_t nlen, const uint8_t* name, bool valid, uint64_t h,
-                                            uint4 q0, uint4 q0n, uint32_t& rbeg, uint32_t& cnt, uint32_t* sflags) {
+                                            uint4 q0, uint4 q0n, bool has_q0n, uint32_t& rbeg, uint32_t& cnt,
+                                            uint32_t* sflags) {
   // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup;
   // lookup-first drivers (ubuntu.go:86-92) probe first, so a poisoned key still raises
   if (valid || (pi.flags & PLAT_LOOKUP_FIRST)) {
     uint32_t step = 0;
     for (uint64_t i = h & a.db.slot_mask;; i = (i + 1) & a.db.slot_mask, step++) {
       const uint4* sp = reinterpret_cast<const uint4*>(a.db.slots + i);
-      if (step == 1) q0 = q0n;
-      else if (step > 1) q0 = sp[0];
+      if (step == 1 && has_q0n) q0 = q0n;
+      else if (step > 0) q0 = sp[0];
       const uint4 q1 = sp[1], q2 = sp[2], q3 = sp[3];  // the rest of the 64-B slot
       const uint64_t sh = q0.x | (uint64_t(q0.y) << 32);
       if (sh == 0) break;
@@ -441,7 +446,7 @@ __global__ __launch_bounds__(kTile) void probe_kernel(ProbeArgs a) {
 
 template <int FILT>
 struct SweepShared {
-  uint64_t k0[kTile], k1[kTile], k2[kTile];  // key heads by tile package
+  uint64_t k0[kTile], k1[kTile], k2[FILT < 2 ? kTile : 1];  // key heads by tile package
   uint32_t kinfo[kTile];
   uint32_t koff[kTile];           // spill word offset of a long key (KI_SPILL)
   uint2 pattr[FILT ? kTile : 1];
@@ -519,13 +524,14 @@ __device__ __forceinline__ int cmp_be(uint64_t a0, uint64_t a1, const uint64_t* 
   return key_cmp(atail, na - 16, btail, nb - 16);
 }
 
-// sign(installed - bound) from the big-endian 24-byte heads alone, branch-free: valid
-// unless both heads tie and both keys are longer than 24 bytes (`tie`: the key tails).
+// sign(installed - bound) from the big-endian heads alone (hl = 16 or 24 bytes; a 16-byte head
+// passes a2 = b2 = 0), branch-free: valid unless both heads tie and both keys are longer than
+// the head (`tie`: the key tails).
 __device__ __forceinline__ int cmp_head(uint64_t a0, uint64_t a1, uint64_t a2, uint32_t na, uint64_t b0, uint64_t b1,
-                                        uint64_t b2, uint32_t nb, bool& tie) {
+                                        uint64_t b2, uint32_t nb, uint32_t hl, bool& tie) {
   const bool eq0 = a0 == b0, eq1 = eq0 && a1 == b1, eq = eq1 && a2 == b2;
   const bool lt = a0 < b0 || (eq0 && a1 < b1) || (eq1 && a2 < b2);
-  tie = eq && na > 24 && nb > 24;
+  tie = eq && na > hl && nb > hl;
   const int byl = (na > nb) - (na < nb);
   return eq ? byl : (lt ? -1 : 1);
 }
@@ -533,28 +539,34 @@ __device__ __forceinline__ int cmp_head(uint64_t a0, uint64_t a1, uint64_t a2, u
 // Interval test of tile package q's installed key against one row (global index ridx).
 // The common case (a bound decided by the inline 24-byte heads) runs without branches;
 // a 24-byte tie reads the key tails, a lower bound (library / rpm ranges) its key head.
-// ro: the row's bound offsets, loaded with the row where lower bounds are common (FILT >= 2:
-// library ranges), else read here on the rare path that needs them.
+// dpkg-grammar packages (FILT 0 kernels: all of them; else KI_H24) compare 24-byte heads and
+// find their rows' offsets in DB::row_off on the rare path that needs them; the other
+// grammars 16-byte heads with the offsets inline.
 template <int FILT, bool DEFER = false, class S>
 __device__ __forceinline__ uint32_t eval_row(const SweepArgs& a, const S& s, uint32_t q, uint32_t p, const Row& row,
-                                             uint32_t ridx, const RowOff& ro) {
+                                             uint32_t ridx) {
   const uint32_t ki = s.kinfo[q];
   const uint32_t kl = ki & KI_LEN;
-  const uint64_t k0 = s.k0[q], k1 = s.k1[q], k2 = s.k2[q];
-  const uint32_t nh = row.hi_len & KEY_LEN_MASK;
+  // h24: the row keeps its offsets in DB::row_off; c24: this kernel compares its 24-byte head
+  // (the all-grammar kernel, at its register cap, compares 16 bytes for every grammar)
+  const bool h24 = FILT == 0 || (ki & KI_H24), c24 = FILT < 2 && h24;
+  const uint64_t k0 = s.k0[q], k1 = s.k1[q], k2 = c24 ? s.k2[q] : 0ull;
+  const uint32_t nh = row.hi_len & KEY_LEN_MASK, hl = c24 ? 24u : 16u;
   bool tie = false;
-  int c = cmp_head(k0, k1, k2, kl, row.hi_pre0, row.hi_pre1, row.hi_pre2, nh, tie);
+  int c = cmp_head(k0, k1, k2, kl, row.hi_pre0, row.hi_pre1, c24 ? row.hi_pre2 : 0ull, nh, hl, tie);
   const bool hi_inf = (row.hi_len & KEY_INF) != 0;
-  if (tie && !hi_inf) {  // rare: same 24-byte head, both keys longer
+  if (tie && !hi_inf) {  // rare: same head, both keys longer
     const uint64_t* ktail =
         (ki & KI_SPILL) ? a.spill + s.koff[q] + 2 : reinterpret_cast<const uint64_t*>(a.tail + p);
-    c = key_cmp(ktail + 1, kl - 24, a.db.key_words + (FILT >= 2 ? ro.hi_off : a.db.row_off[ridx].hi_off) + 3, nh - 24);
+    const uint32_t w = hl / 8;
+    const uint32_t hi_off = h24 ? a.db.row_off[ridx].hi_off : row.off.hi_off;
+    c = key_cmp(ktail + (w - 2), kl - hl, a.db.key_words + hi_off + w, nh - hl);
   }
   bool m = hi_inf || ((row.hi_len & KEY_INCL) ? c <= 0 : c < 0);
   if (!(row.lo_len & KEY_INF) && m) {  // rare (library / rpm ranges): the bound's head from the arena
     const uint64_t* ktail =
         (ki & KI_SPILL) ? a.spill + s.koff[q] + 2 : reinterpret_cast<const uint64_t*>(a.tail + p);
-    const uint64_t* lw = a.db.key_words + (FILT >= 2 ? ro.lo_off : a.db.row_off[ridx].lo_off);
+    const uint64_t* lw = a.db.key_words + (h24 ? a.db.row_off[ridx].lo_off : row.off.lo_off);
     const uint32_t nl = row.lo_len & KEY_LEN_MASK;
     const uint64_t l0 = nl ? be_word(lw[0], nl < 8 ? nl : 8) : 0ull;
     const uint64_t l1 = nl > 8 ? be_word(lw[1], nl < 16 ? nl - 8 : 8) : 0ull;
@@ -663,7 +675,6 @@ __device__ __forceinline__ uint32_t sweep(const SweepArgs& a, SweepShared<FILT>&
     // re-read the tile's last pair), so the K loads are in flight together and the lane
     // waits once; a load under a branch would be waited for before the next one issues
     Row row[K];
-    RowOff ro[K] = {};
     uint32_t qq[K], rid[K];
 #pragma unroll
     for (int k = 0; k < K; k++) rid[k] = map_rank(s, map, shift, min(b0 + k * kTile + tid, total - 1));
@@ -674,14 +685,11 @@ __device__ __forceinline__ uint32_t sweep(const SweepArgs& a, SweepShared<FILT>&
       rid[k] = min(b0 + k * kTile + tid, total - 1) + s.nz_rd[r];
     }
 #pragma unroll
-    for (int k = 0; k < K; k++) {
-      row[k] = a.db.rows[rid[k]];
-      if constexpr (FILT >= 2) ro[k] = a.db.row_off[rid[k]];
-    }
+    for (int k = 0; k < K; k++) row[k] = a.db.rows[rid[k]];
     uint32_t mask = 0, pend = 0;
 #pragma unroll
     for (int k = 0; k < K; k++) {
-      const uint32_t e = eval_row<FILT, (FILT >= 2)>(a, s, qq[k], pbase + qq[k], row[k], rid[k], ro[k]);
+      const uint32_t e = eval_row<FILT, (FILT >= 2)>(a, s, qq[k], pbase + qq[k], row[k], rid[k]);
       const bool in = b0 + k * kTile + tid < total;
       mask |= (e == 1 && in) ? 1u << k : 0u;
       pend |= (e == 2 && in) ? 1u << k : 0u;
@@ -744,7 +752,6 @@ __device__ __forceinline__ uint32_t sweep_seg(const SweepArgs& a, const SweepSha
   uint32_t nm = 0;
   for (uint32_t b0 = s0; b0 < s1; b0 += 64 * K) {
     Row row[K];
-    RowOff ro[K] = {};
     uint32_t qq[K], rid[K];
 #pragma unroll
     for (int k = 0; k < K; k++) {
@@ -758,13 +765,10 @@ __device__ __forceinline__ uint32_t sweep_seg(const SweepArgs& a, const SweepSha
       rid[k] = min(b0 + k * 64 + lane, s1 - 1) + s.nz_rd[r];
     }
 #pragma unroll
-    for (int k = 0; k < K; k++) {
-      row[k] = a.db.rows[rid[k]];
-      if constexpr (FILT >= 2) ro[k] = a.db.row_off[rid[k]];
-    }
+    for (int k = 0; k < K; k++) row[k] = a.db.rows[rid[k]];
 #pragma unroll
     for (int k = 0; k < K; k++) {
-      const bool m = eval_row<FILT>(a, s, qq[k], pbase + qq[k], row[k], rid[k], ro[k]) != 0 && b0 + k * 64 + lane < s1;
+      const bool m = eval_row<FILT>(a, s, qq[k], pbase + qq[k], row[k], rid[k]) != 0 && b0 + k * 64 + lane < s1;
       const unsigned long long bal = __ballot(m);
       if (m) {
         const uint32_t pos = nm + uint32_t(__popcll(bal & lt));
@@ -795,7 +799,7 @@ __device__ __forceinline__ void sweep_tile(const SweepArgs& a, SweepShared<FILT>
   const uint32_t p = t * kTile + tid;
   s.k0[tid] = r.k0;
   s.k1[tid] = r.k1;
-  s.k2[tid] = r.k2;
+  if constexpr (FILT < 2) s.k2[tid] = r.k2;
   s.kinfo[tid] = r.meta.z;
   s.koff[tid] = r.meta.w;
   if constexpr (FILT) s.pattr[tid] = (a.attr && p < a.n) ? a.attr[p] : make_uint2(PA_ARCH_NONE, 0xFFFFFFFFu);
