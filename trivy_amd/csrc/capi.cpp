@@ -78,6 +78,10 @@ struct tvm_batch {
   bool st_valid = false;
   uint64_t st_n = 0;
   int64_t st_errp = -1;
+  // batch_has_redhat's answer for the first rh_seen_n packages against rh_seen_db
+  mutable uint64_t rh_seen_n = ~0ull;
+  mutable const void* rh_seen_db = nullptr;
+  mutable bool rh_seen = false;
   // tvm_batch_set_report: per package PkgName / InstalledVersion / PkgPath overrides
   // (rep[f][i] counts where rep_has[f][i] is set; shorter vectors = defaults beyond)
   std::vector<std::string> rep[3];
@@ -1408,6 +1412,10 @@ int tvm_match_filter_time(tvm_engine* e, tvm_batch* b, const tvm_filter_opts* o,
 
 // ---- end-to-end pipelined pass (pipeline.hip) -------------------------------------------
 
+namespace {
+bool batch_has_redhat(const tvm_batch* b, const DB& db);
+}  // namespace
+
 int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32_t chunk_packages, uint32_t flags,
                          char* err, size_t errlen) {
   if (!e || !b || chunk_packages == 0 ||
@@ -1429,6 +1437,7 @@ int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32
     return TVM_EDEVICE;
   }
   b->pinned = true;  // the pipeline was sized for exactly these packages: no more adds
+  (void)batch_has_redhat(b, e->eng->db());  // once per batch, here: tvm_pipeline_vulns reads the answer
   return TVM_OK;
 }
 
@@ -1803,6 +1812,8 @@ struct VulnSetStore {
 };
 
 bool batch_has_redhat(const tvm_batch* b, const DB& db) {
+  // packages are only ever appended: the answer holds until the batch grows or the DB changes
+  if (b->rh_seen_n == b->hb.pk.size() && b->rh_seen_db == &db) return b->rh_seen;
   const auto& pi = db.plat_info;
   std::atomic<bool> any{false};
   pool_range_for(b->hb.pk.size(), 1 << 16, [&](size_t a, size_t z) {
@@ -1814,7 +1825,10 @@ bool batch_has_redhat(const tvm_batch* b, const DB& db) {
       if (pl < pi.size() && pi[pl].drv == DRV_REDHAT) any.store(true, std::memory_order_relaxed);
     }
   });
-  return any.load();
+  b->rh_seen_n = b->hb.pk.size();
+  b->rh_seen_db = &db;
+  b->rh_seen = any.load();
+  return b->rh_seen;
 }
 
 void set_out(tvm_db* d, VulnSetStore* st, const uint32_t* row_end, size_t n_pkgs, uint32_t first_pkg,
