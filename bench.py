@@ -434,11 +434,18 @@ def main():
 
         # ---- timed region: match pass (+ gather to rank 0) -----------------------------------
         def step():
-            mb.launch(1, sync=True)
+            # passes queue back to back on the engine stream (each a full pass over the resident
+            # batch, its list overwriting the last one's); the timed region's closing sync waits
+            # for the last; the strong step's order kernel + gather are stream-ordered behind it
+            mb.launch(1, sync=False)
             if gather is not None:
                 do_gather()
 
-        wall = td.timed(step, steps=args.steps, warmup=args.warmup, sync=sync, device=cdev)
+        def step_sync():  # the engine stream (libtrivy_amd's HIP runtime), then torch's
+            mb.launch(0, sync=True)
+            sync()
+
+        wall = td.timed(step, steps=args.steps, warmup=args.warmup, sync=step_sync, device=cdev)
         if mb.status() != (total, -1, 0):
             raise RuntimeError("timed passes disagree with the first pass")
         n_job = wl.n * (1 if strong else world)  # packages all ranks match per step

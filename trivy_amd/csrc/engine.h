@@ -114,6 +114,11 @@ struct DevMatches {
   // control block (device): [0] total matches (reservation counter), [1] n - first
   // poisoned pkg (0 = none), [2] spill words used, [3] error bits
   unsigned long long* ctl = nullptr;
+  // device-resident launches alternate between two control blocks: a launch counts into
+  // ctl_next (zeroed by the launch before) and zeroes the block it leaves behind, so a pass
+  // is one kernel, no memset (Engine::launch); ctl_mem = the allocation
+  unsigned long long* ctl_next = nullptr;
+  unsigned long long* ctl_mem = nullptr;
 };
 // ERR_BOUNDS: a result move or an unpack found an index beyond the buffer it was sized for
 // (the store is dropped and the pass fails; never expected: a guard, not a code path)
@@ -355,13 +360,15 @@ class Engine {
   static void free_matches(int device, DevMatches& m, bool pooled = false);
 
   // Enqueues one match pass (probe + sweep over every tile) on `stream`; no host sync.
-  bool launch(const DevBatch& b, const DevMatches& m, hipStream_t stream, std::string& err);
+  // Moves m.ctl to the other control block (DevMatches::ctl_next).
+  bool launch(const DevBatch& b, DevMatches& m, hipStream_t stream, std::string& err);
   // The pass over tiles [t_begin, t_end) only: probe on `probe_st`, sweep on `sweep_st`
   // behind event `ev` (the caller zeroes m.ctl once before the first chunk).
   // co: a previous chunk's result move, run by extra workgroups of this launch (fused
   // variants) or by its own kernel ahead of it (split variants).
   bool launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_begin, uint32_t t_end, hipStream_t probe_st,
-                    hipStream_t sweep_st, hipEvent_t ev, std::string& err, const CopyOutArgs* co = nullptr);
+                    hipStream_t sweep_st, hipEvent_t ev, std::string& err, const CopyOutArgs* co = nullptr,
+                    unsigned long long* ctl_zero = nullptr);
 
   // After the pass: the match list as {package, advisory} pairs in (package, advisory) order.
   static bool fetch_ordered(const DevMatches& m, uint32_t n_pkgs, uint64_t total, std::vector<uint2>& out,

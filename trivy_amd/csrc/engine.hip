@@ -376,14 +376,20 @@ bool Engine::alloc_matches(uint64_t cap, uint32_t n_pkgs, DevMatches& m, std::st
   const int pd = pooled ? dev_ : -1;
   m.cap = std::max<uint64_t>(cap, 1);
   m.dir_cap = std::max<uint32_t>((n_pkgs + kTile - 1) / kTile, 1);
-  return dmalloc(&m.pkg, m.cap, "hipMalloc(matches)", err, pd) && dmalloc(&m.adv, m.cap, "hipMalloc(matches)", err, pd) &&
-         dmalloc(&m.dir, m.dir_cap, "hipMalloc(tile dir)", err, pd) && dmalloc(&m.ctl, 8, "hipMalloc(ctl)", err, pd);
+  if (!dmalloc(&m.pkg, m.cap, "hipMalloc(matches)", err, pd) || !dmalloc(&m.adv, m.cap, "hipMalloc(matches)", err, pd) ||
+      !dmalloc(&m.dir, m.dir_cap, "hipMalloc(tile dir)", err, pd) || !dmalloc(&m.ctl_mem, 16, "hipMalloc(ctl)", err, pd))
+    return false;
+  // both control blocks zero (Engine::launch alternates them)
+  if (!hip_ok(hipMemset(m.ctl_mem, 0, 16 * sizeof(unsigned long long)), "memset(ctl)", err)) return false;
+  m.ctl = m.ctl_mem;
+  m.ctl_next = m.ctl_mem + 8;
+  return true;
 }
 
 void Engine::free_matches(int device, DevMatches& m, bool pooled) {
   (void)hipSetDevice(device);
   for (void* p : {static_cast<void*>(m.pkg), static_cast<void*>(m.adv), static_cast<void*>(m.dir),
-                  static_cast<void*>(m.ctl)})
+                  static_cast<void*>(m.ctl_mem ? m.ctl_mem : m.ctl)})
     dfree(p, pooled, device);
   m = DevMatches{};
 }
@@ -411,7 +417,8 @@ bool Engine::fetch_ordered(const DevMatches& m, uint32_t n_pkgs, uint64_t total,
 }
 
 bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_begin, uint32_t t_end, hipStream_t pst,
-                          hipStream_t sst, hipEvent_t ev, std::string& err, const CopyOutArgs* co) {
+                          hipStream_t sst, hipEvent_t ev, std::string& err, const CopyOutArgs* co,
+                          unsigned long long* ctl_zero) {
   (void)hipSetDevice(dev_);
   if (t_end > b.n_tiles) t_end = b.n_tiles;
   if (t_begin >= t_end) return true;
@@ -442,6 +449,9 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
   pa.spill = b.spill;
   pa.spill_cap = b.spill_cap;
   const bool fused = kFusedVariant[vi - 1];
+  if (!fused && ctl_zero &&
+      !hip_ok(hipMemsetAsync(ctl_zero, 0, 8 * sizeof(unsigned long long), pst), "memset(ctl)", err))
+    return false;
   if (!fused) {
     if (co) launch_copy_out(pst, *co);
     probe_fn(b.gm)(nt, pst, pa);
@@ -487,6 +497,7 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
       fa.n_copy = n_copy;
     }
     if (!co && t_begin == 0 && t_end == b.n_tiles) fa.tile_map = b.tile_map;
+    fa.ctl_zero = co ? nullptr : ctl_zero;
     const FusedFn fn = fused_fn(b.gm, vi);
     if (!fn) {
       err = std::string("match-path variant ") + kVariantNames[vi - 1] + " is not built for this batch's grammar set";
@@ -500,13 +511,20 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
   return hip_ok(hipGetLastError(), "sweep kernel launch", err);
 }
 
-bool Engine::launch(const DevBatch& b, const DevMatches& m, hipStream_t st, std::string& err) {
+bool Engine::launch(const DevBatch& b, DevMatches& m, hipStream_t st, std::string& err) {
   (void)hipSetDevice(dev_);
-  if (!hip_ok(hipMemsetAsync(m.ctl, 0, 8 * sizeof(unsigned long long), st), "memset(ctl)", err)) return false;
-  if (b.n_tiles == 0) return true;
+  unsigned long long* zero = nullptr;  // the control block this pass leaves behind
+  if (m.ctl_next) {
+    std::swap(m.ctl, m.ctl_next);  // count into the block the last pass zeroed
+    zero = m.ctl_next;
+  } else if (!hip_ok(hipMemsetAsync(m.ctl, 0, 8 * sizeof(unsigned long long), st), "memset(ctl)", err)) {
+    return false;
+  }
+  if (b.n_tiles == 0)
+    return !zero || hip_ok(hipMemsetAsync(zero, 0, 8 * sizeof(unsigned long long), st), "memset(ctl)", err);
   // one launch over every tile (cutting the pass into chunks whose probe overlaps the
   // previous chunk's sweep on a second stream measured slower: DESIGN.md §4)
-  return launch_tiles(b, m, 0, b.n_tiles, st, st, nullptr, err);
+  return launch_tiles(b, m, 0, b.n_tiles, st, st, nullptr, err, nullptr, zero);
 }
 
 // ---- drop-in path: pooled buffers + coalescing of concurrent calls -------------------------

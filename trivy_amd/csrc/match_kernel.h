@@ -90,6 +90,7 @@ struct FusedArgs {
   CopyOutArgs co;       // end-to-end pipeline: the previous chunk's result move ...
   uint32_t n_copy = 0;  // ... by workgroups [0, n_copy) of this launch (0: none)
   const uint32_t* tile_map = nullptr;  // workgroup -> tile (DevBatch::tile_map; no result move)
+  unsigned long long* ctl_zero = nullptr;  // device-resident pass: the control block to zero for the next
 };
 
 using ProbeFn = void (*)(uint32_t n_tiles, hipStream_t st, const ProbeArgs& a);
@@ -966,6 +967,7 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
     }
   }
   const uint32_t tid = threadIdx.x;
+  if (!MOVE && fa.ctl_zero && blockIdx.x == 0 && tid < 8) fa.ctl_zero[tid] = 0ull;  // the next pass's counters
   const uint32_t t = MOVE ? blockIdx.x - fa.n_copy : (fa.tile_map ? fa.tile_map[blockIdx.x] : blockIdx.x);
   const uint32_t p = t * kTile + tid;
   uint2 d = make_uint2(0xFFFFFFFFu, 0);
