@@ -129,7 +129,8 @@ int variant_grammar_sets(int v) {
 // lower register count keeps 5 waves per SIMD where the filtered K=4 kernel drops to 4.
 int resolve_variant(int v, uint32_t gm) {
   if (v != 0) return v;
-  return 1 + (grammar_index(gm) == 0 ? kAutoVariant : kAutoVariantFiltered);
+  const int gi = grammar_index(gm);
+  return 1 + (gi == 0 ? kAutoVariant : gi == 1 ? kAutoVariantOS : kAutoVariantFiltered);
 }
 
 // ---- HostBatch ------------------------------------------------------------------------------

@@ -46,3 +46,6 @@ constexpr int kNumTuned = 0 TVM_MATCH_VARIANTS(TVM_VARIANT_COUNT_);
 // (C3 0.257 ms against 0.34-0.36 ms in segments).
 constexpr int kAutoVariant = 6;          // fused_k4_m2400_wseg
 constexpr int kAutoVariantFiltered = 1;  // fused_k2_m2048
+// OS grammar sets with row filters (rpm / apk: no library rows): per-wave staging + segments
+// at 6 waves, K = 2 (round 5 sweep, profiles/r05/sweep_c5.txt: C5 2.317 -> 2.283 ms)
+constexpr int kAutoVariantOS = 7;        // fused_k2_m2400_wseg6
