@@ -126,19 +126,16 @@ GENS = {"generic": gen_generic, "npm": gen_npm, "pep440": gen_pep, "maven": gen_
         "bitnami": gen_bitnami}
 
 
-def _mvn_intransitive(a, b):
-    """ComparableVersion is not a total order where a '.'-qualifier ordered above release
-    (sp / unknown, e.g. "99.jre") meets a '-' sub-list ordered below it ("99-rc1") at the
-    same position: str < list, list < null, null < str.  Such pairs have no consistent
-    sort key, so the KEY-order fuzz below skips them; Maven matching does
-    not use the key order (its rows are pairwise programs, AUX_MVN), and the IsVulnerable
-    fuzz and the GPU random parity test skip nothing."""
-    dot_hi = lambda v: re.search(r"\.(?!(?:alpha|beta|milestone|rc|cr|snapshot|ga|final|release)\b)[a-z]", v.lower())  # noqa
-    return bool((dot_hi(a) and "-" in b) or (dot_hi(b) and "-" in a))
+_MVN_NUMERIC = re.compile(r"^[0-9]{1,9}(\.[0-9]{1,9})*$")
 
 
 @pytest.mark.parametrize("g", list(GRAMMAR))
 def test_key_order_matches_oracle(g):
+    """Maven: ComparableVersion is not an order, and the product's Maven key
+    is the installed version's numeric projection (libver.h mvn_numeric_projection), which
+    only ever meets numeric bounds: pairs with a numeric side are checked (every installed
+    shape against numeric bounds, the non-transitive corners included); advisories with
+    other bounds are pairwise programs (the IsVulnerable fuzz below)."""
     r = random.Random(zlib.crc32(g.encode()))
     bad, n = [], 0
     for _ in range(20000):
@@ -149,7 +146,7 @@ def test_key_order_matches_oracle(g):
             continue
         ka, kb = key(g, a), key(g, b)
         assert ka is not None and kb is not None, (a, b)
-        if g == "maven" and _mvn_intransitive(a, b):
+        if g == "maven" and not (_MVN_NUMERIC.match(a) or _MVN_NUMERIC.match(b)):
             continue
         n += 1
         want = va.compare(vb)
@@ -158,6 +155,46 @@ def test_key_order_matches_oracle(g):
             bad.append((a, b, want, got))
     assert n > 5000
     assert not bad, bad[:10]
+
+
+def _mvn_any(r):
+    """Arbitrary ComparableVersion shapes: int / zero / qualifier items joined by '.', '-' or
+    nothing (digit <-> letter transitions open sub-lists), empty items included."""
+    items = ["0", "00", "1", "2", "10", "007", "alpha", "a", "b", "m", "rc", "cr", "snapshot", "ga", "final",
+             "release", "sp", "jre", "x", ""]
+    v = r.choice(["0", "1", "2", "10", "1.0", "alpha", "rc", "sp"])
+    for _ in range(r.randint(0, 5)):
+        v += r.choice([".", "-", "", "."]) + r.choice(items)
+    return v
+
+
+def _mvn_numeric_bound(r):
+    return ".".join(r.choice(["0", "0", "1", "2", "10", "007", "999999999"]) for _ in range(r.randint(1, 5)))
+
+
+def test_maven_projection_against_numeric_bounds():
+    """compare(V, B) for any installed V and numeric B is the key order of V's numeric
+    projection against B's key (libver.h mvn_numeric_projection): 60k pairs of arbitrary
+    shapes, the non-transitive ones of DESIGN.md §2.2 among them, against the oracle's
+    ComparableVersion."""
+    r = random.Random(355)
+    bad, n = [], 0
+    for _ in range(60000):
+        a, b = _mvn_any(r), _mvn_numeric_bound(r)
+        try:
+            va, vb = ol.MvnVer(a), ol.MvnVer(b)
+        except ol.VersionError:
+            assert key("maven", a) is None, a
+            continue
+        ka, kb = key("maven", a), key("maven", b)
+        assert ka is not None and kb is not None, (a, b)
+        n += 1
+        want = va.compare(vb)
+        if (ka > kb) - (ka < kb) != want:
+            bad.append((a, b, want))
+    assert n > 40000
+    assert not bad, bad[:10]
+    assert cls("maven", "1.0-rc1") == 0 and cls("maven", "1.2.3") == 0  # one class
 
 
 @pytest.mark.parametrize("g,v", [("generic", "1.2..4"), ("npm", "1.2"), ("npm", "1.2..4"), ("pep440", "1.2..4"),

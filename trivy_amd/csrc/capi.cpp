@@ -948,7 +948,10 @@ int tvm_lib_is_vulnerable_host(int grammar, const char* ver, size_t ver_len, con
   Advisory a;
   std::string e;
   if (!ver || !advisory_json || !decode_advisory(std::string_view(advisory_json, json_len), a, e)) return -1;
-  if (grammar == CMP_MAVEN) return mvn_is_vulnerable(a.vulnerable, a.patched, a.unaffected, std::string(ver, ver_len));
+  // Maven: the rows DB::compile_rows builds - intervals over the numeric projection for an
+  // advisory with numeric bounds, else the pairwise program
+  if (grammar == CMP_MAVEN && !mvn_hybrid(a.vulnerable, a.patched, a.unaffected))
+    return mvn_is_vulnerable(a.vulnerable, a.patched, a.unaffected, std::string(ver, ver_len));
   const LibRows r = lib_compile_advisory(uint8_t(grammar), a.vulnerable, a.patched, a.unaffected);
   return lib_rows_contain(uint8_t(grammar), r, std::string(ver, ver_len)) ? 1 : 0;
 }

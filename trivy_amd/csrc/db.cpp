@@ -547,39 +547,36 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
   // Maven: ComparableVersion is not an order, so in general no interval set
   // can stand for IsVulnerable: the row carries the advisory's program (AUX_MVN) and the
   // kernel evaluates it pairwise against the installed version.  Hybrid: when every bound
-  // text is numeric (libver.h mvn_numeric), numeric installed versions (class 1) are
-  // compared in the key order, which is exact on that domain - the advisory's intervals
-  // as class-1 rows below, and the program row only for class 0.
-  bool mvn_hybrid = false;
+  // text is numeric (libver.h mvn_numeric), every installed version compares with the
+  // bounds in the order of its numeric projection (libver.h mvn_numeric_projection), so the
+  // advisory is its key-order intervals below and no program.
   if (P.drv == DRV_LIBRARY && P.cmp == CMP_MAVEN) {
     std::vector<uint32_t> w;
     const MvnProgState st = mvn_program(a.vulnerable, a.patched, a.unaffected, w);
     if (st == MVN_NEVER) return false;
-    Row r{};
-    r.lo_len = r.hi_len = KEY_INF;
-    RowAux x{};
-    r.adv = ai | (st == MVN_ALWAYS ? ROW_ALWAYS : ROW_FILTER);
-    if (st == MVN_PROGRAM) {
-      mvn_hybrid = mvn_bounds_numeric(a.vulnerable, a.patched, a.unaffected) &&
-                   lib_compile_advisory(P.cmp, a.vulnerable, a.patched, a.unaffected).ok;
-      x.kind = AUX_MVN | (mvn_hybrid ? AUX_CLASS : 0u);
-      x.tag = mvn_hybrid ? 1u : 0u;  // class 0 only
-      x.list_off = uint32_t(aux_ids.size());
-      aux_ids.insert(aux_ids.end(), w.begin(), w.end());
-      has_filters = true;
+    if (st != MVN_PROGRAM || !mvn_hybrid(a.vulnerable, a.patched, a.unaffected)) {
+      Row r{};
+      r.lo_len = r.hi_len = KEY_INF;
+      RowAux x{};
+      r.adv = ai | (st == MVN_ALWAYS ? ROW_ALWAYS : ROW_FILTER);
+      if (st == MVN_PROGRAM) {
+        x.kind = AUX_MVN;
+        x.list_off = uint32_t(aux_ids.size());
+        aux_ids.insert(aux_ids.end(), w.begin(), w.end());
+        has_filters = true;
+      }
+      rows.push_back(r);
+      row_off.push_back(RowOff{});
+      aux.push_back(x);
+      return true;
     }
-    rows.push_back(r);
-    row_off.push_back(RowOff{});
-    aux.push_back(x);
-    if (!mvn_hybrid) return true;
   }
   if (P.drv == DRV_LIBRARY) {
     // compare.IsVulnerable as disjoint intervals per version class (libdb.h); classes
     // sharing an interval share its row; a row that holds for a subset of the classes
     // carries an AUX_CLASS filter.
     LibRows lr = lib_compile_advisory(P.cmp, a.vulnerable, a.patched, a.unaffected);
-    if (mvn_hybrid) lr.cls[0].clear();  // class 0 has the program row
-    if (lr.always && !mvn_hybrid) {
+    if (lr.always) {
       Row r{};
       r.adv = ai | ROW_ALWAYS;
       r.lo_len = r.hi_len = KEY_INF;
@@ -629,7 +626,7 @@ bool DB::compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::ve
       row_off.push_back(o);
       aux.push_back(x);
     }
-    return mvn_hybrid || !ivs.empty();
+    return !ivs.empty();
   }
   Row r{};
   RowOff o{};

@@ -945,7 +945,7 @@ int lib_classes(uint8_t cmp) {
   switch (cmp) {
     case CMP_NPM: return 2;
     case CMP_PEP440: return 8;
-    case CMP_MAVEN: return 2;  // 1 = numeric (libver.h mvn_numeric)
+    case CMP_MAVEN: return 1;  // one class: the numeric projection (libver.h mvn_numeric_projection)
     default: return 1;
   }
 }
@@ -1076,6 +1076,14 @@ bool mvn_bounds_numeric(const std::vector<std::string>& vulnerable, const std::v
           if (!mvn_numeric(U(txt), uint32_t(txt.size()))) return false;
     }
   return true;
+}
+
+bool mvn_hybrid(const std::vector<std::string>& vulnerable, const std::vector<std::string>& patched,
+                const std::vector<std::string>& unaffected) {
+  std::vector<uint32_t> w;
+  return mvn_program(vulnerable, patched, unaffected, w) == MVN_PROGRAM &&
+         mvn_bounds_numeric(vulnerable, patched, unaffected) &&
+         lib_compile_advisory(CMP_MAVEN, vulnerable, patched, unaffected).ok;
 }
 
 int mvn_is_vulnerable(const std::vector<std::string>& vulnerable, const std::vector<std::string>& patched,

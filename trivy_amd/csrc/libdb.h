@@ -37,12 +37,17 @@ struct LibRows {
 // Maven advisories as IsVulnerable programs (libver.h mvn_program_eval): ALWAYS (an empty
 // constraint string), NEVER (unparsable / nothing to match) or a program in `words`.
 enum MvnProgState { MVN_NEVER = 0, MVN_ALWAYS = 1, MVN_PROGRAM = 2 };
-// Every bound text of the advisory's constraints is numeric (libver.h mvn_numeric): the
-// advisory then also compiles to key-order intervals, exact for numeric installed versions.
+// Every bound text of the advisory's constraints is numeric (libver.h mvn_numeric).
 bool mvn_bounds_numeric(const std::vector<std::string>& vulnerable, const std::vector<std::string>& patched,
                         const std::vector<std::string>& unaffected);
 MvnProgState mvn_program(const std::vector<std::string>& vulnerable, const std::vector<std::string>& patched,
                          const std::vector<std::string>& unaffected, std::vector<uint32_t>& words);
+// The advisory is a program whose bounds are all numeric and compile: it is matched as
+// key-order intervals over the installed version's numeric projection (libver.h
+// mvn_numeric_projection), exact for every installed version; DB::compile_rows builds no
+// program row for it.
+bool mvn_hybrid(const std::vector<std::string>& vulnerable, const std::vector<std::string>& patched,
+                const std::vector<std::string>& unaffected);
 // compare.IsVulnerable for the Maven grammar, pairwise (host): 1 / 0.
 int mvn_is_vulnerable(const std::vector<std::string>& vulnerable, const std::vector<std::string>& patched,
                       const std::vector<std::string>& unaffected, const std::string& installed);

@@ -882,6 +882,60 @@ TVM_HD int mvn_cmp(const VA& A, const VB& B) {
   }
 }
 
+// ---- Maven, the installed version's key against numeric bounds -----------------------------
+// Against a numeric bound B (mvn_numeric: a flat list of ints) every installed version V
+// compares like a numeric version give or take an infinitesimal: let P be V's leading int
+// items at the top level (up to the first string or sub-list item) and T the rest.  Walking
+// V and B item by item, the first difference inside P is an int against an int (or against
+// null: B's zero padding), so it is P against B in zero-padded integer order; where B goes
+// on past P with a non-zero int, T's first item (a string or a sub-list) meets an int and
+// loses (int > string, int > list); where P and B are equal, B is exhausted and T against
+// null decides (its first item of non-zero relation).  So
+//   compare(V, B) = numeric(P) vs B, and on a tie sign(T against null),
+// which is the key order of  key(P) + [0x20 if T < null | 0x40 if T > null] + 0x30 :
+// 0x20 < end 0x30 < 0x40 < 0x68 / 0x70 (a zero / int item of any numeric extension of P).
+// The rows of an advisory whose every bound is numeric are therefore intervals over this key
+// for every installed version (db.cpp DB::compile_rows): no pairwise program runs for them.
+// Exact by the argument above; tests/test_libver_host.py checks it against the oracle's
+// ComparableVersion on the non-transitive shapes of DESIGN.md §2.2 as well.
+template <class Sink>
+TVM_HD bool mvn_numeric_projection(const uint8_t* s, uint32_t n, Sink& o) {
+  MvnParse P;
+  if (!mvn_parse(s, n, P)) return false;
+  const MvnParseView V{&P, s};
+  int pe = 0, last = -1;  // end of P; its last non-zero int
+  for (; pe < P.n; pe++) {
+    const MvnTok& t = P.t[pe];
+    if (t.removed) {
+      if (t.kind == MV_OPEN) break;  // an emptied sub-list ends the list
+      continue;                      // a dropped zero
+    }
+    if (t.kind != MV_INT) break;
+    if (!t.zero) last = pe;
+  }
+  for (int k = 0; k <= last; k++) {
+    const MvnTok& t = P.t[k];
+    if (t.removed) continue;
+    if (t.zero) {
+      o.put(0x68);  // a zero followed by a non-zero int
+    } else {
+      o.put(0x70);
+      put_digits(s, t.b, t.e, o);
+    }
+  }
+  int sg = 0;
+  for (int k = pe;;) {  // T against null: its items in turn until one is not equal to null
+    const int x = mvn_next(V, k);
+    if (x < 0) break;
+    sg = mvn_vs_null(V, x);
+    if (sg || P.t[x].kind == MV_OPEN) break;  // a sub-list is its parent's last item
+    k = x + 1;
+  }
+  if (sg) o.put(sg < 0 ? 0x20 : 0x40);
+  o.put(0x30);
+  return true;
+}
+
 // A Maven advisory program (u32 words, built by libdb.cpp mvn_program):
 //   w[0] = n_vulnerable_groups | n_secure_groups << 16, then the groups in that order;
 //   group = n_terms, then per term {op | n_tokens << 8 | text length << 16, word offset of
@@ -1058,10 +1112,7 @@ TVM_HD bool encode_version_cls_gm(uint8_t cmp, const uint8_t* s, uint32_t n, Sin
     if (cmp == CMP_PEP440) return pep_encode(s, n, o, cls);
   }
   if constexpr ((GM >> 7) & 1u) {  // CMP_MAVEN
-    if (cmp == CMP_MAVEN) {
-      cls = mvn_numeric(s, n) ? 1u : 0u;
-      return mvn_encode(s, n, o);
-    }
+    if (cmp == CMP_MAVEN) return mvn_numeric_projection(s, n, o);  // one class (see above)
   }
   if constexpr ((GM >> 8) & 1u) {  // CMP_GEM
     if (cmp == CMP_GEM) return gem_encode(s, n, o);
