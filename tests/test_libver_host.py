@@ -195,6 +195,9 @@ def test_maven_projection_against_numeric_bounds():
     assert n > 40000
     assert not bad, bad[:10]
     assert cls("maven", "1.0-rc1") == 0 and cls("maven", "1.2.3") == 0  # one class
+    for _ in range(5000):  # numeric texts: the streamed key == the parse's (a leading blank takes the parse)
+        b = _mvn_numeric_bound(r)
+        assert key("maven", b) == key("maven", " " + b), b
 
 
 @pytest.mark.parametrize("g,v", [("generic", "1.2..4"), ("npm", "1.2"), ("npm", "1.2..4"), ("pep440", "1.2..4"),

@@ -99,7 +99,7 @@ using FusedFn = void (*)(uint32_t n_tiles, hipStream_t st, const FusedArgs& a);
 
 namespace {
 
-// KI_MVN: a Maven package (its rows may carry pairwise programs: the sweep defers those)
+// KI_MVN: a Maven package whose key has program rows (the sweep defers those pairs)
 // KI_H24: a dpkg-grammar package (its rows carry 24-byte key heads, Row::hi_pre2)
 enum : uint32_t { KI_VALID = 1u << 31, KI_SPILL = 1u << 30, KI_MVN = 1u << 29, KI_H24 = 1u << 25, KI_LEN = 0x3FFFu,
                   KI_CLS_SHIFT = 26, KI_CLS_MASK = 7u };
@@ -328,7 +328,8 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
   const uint32_t kl = hs.n;
   kinfo |= (kl & KI_LEN) | (valid ? KI_VALID : 0u) | ((cls & KI_CLS_MASK) << KI_CLS_SHIFT);
   if (pi.cmp == CMP_DEB) kinfo |= KI_H24;
-  if (((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN) kinfo |= KI_MVN;
+  // only a key with program rows can defer a pair (numeric-bound advisories are intervals)
+  if (((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN && (sflags & (SLOT_MVN_C0 | SLOT_MVN_C1))) kinfo |= KI_MVN;
   r.k0 = valid && kl ? be_word(hs.w0, kl < 8 ? kl : 8) : 0ull;
   r.k1 = valid && kl > 8 ? be_word(hs.w1, kl < 16 ? kl - 8 : 8) : 0ull;
   r.k2 = valid && kl > 16 ? be_word(hs.w2, kl < 24 ? kl - 16 : 8) : 0ull;
