@@ -283,6 +283,8 @@ int tvm_match_time(tvm_engine* e, tvm_batch* b, int steps, double* ms, char* err
 uint64_t tvm_match_algorithmic_bytes(tvm_engine* e, tvm_batch* b);
 /* Host-side sort key of a version string (diagnostics/tests).  Grammars: 1 dpkg, 2 apk,
  * 3 rpm, 4 go-version, 5 npm, 6 PEP 440, 7 Maven, 8 RubyGems, 9 Bitnami.
+ * Maven: the key the product compares, the version's numeric projection (only ever compared
+ * with numeric bounds).
  * Returns the key length (<= cap bytes written) or -1 when the version does not parse. */
 int tvm_version_key(int grammar, const char* s, size_t n, uint8_t* out, size_t cap);
 /* Version class of a library grammar (npm: 1 pre-release; PEP 440: bits local/pre/post), -1 on error. */
@@ -293,7 +295,8 @@ int tvm_version_class(int grammar, const char* s, size_t n);
  * kernel hands the version to the generic encoder. */
 int tvm_deb_fast_key_host(const char* s, size_t n, uint32_t shift, uint8_t* out, size_t cap);
 /* Host-side compare.IsVulnerable through the load-time interval compiler (tests): 1/0, -1
- * when the advisory JSON does not decode. */
+ * when the advisory JSON does not decode.  Maven: the rows the product builds - intervals for
+ * an advisory whose bounds are all numeric, else the pairwise program. */
 int tvm_lib_is_vulnerable_host(int grammar, const char* ver, size_t ver_len, const char* advisory_json,
                                size_t json_len);
 /* Advisory fields for host-side inspection of batch results. */

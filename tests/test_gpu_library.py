@@ -1,6 +1,7 @@
 """GPU: library detection (pkg/detector/library) through the C-ABI against the reference's
 vectors (every compare_test.go KAT, driver_test.go, the lang-pkgs integration goldens) and
 against the oracle on random advisories for all six grammars."""
+import functools
 import glob
 import json
 import os
@@ -115,4 +116,38 @@ def test_random_parity_vs_oracle(g):
     got = detect(eng, LANG_OF[g], pkgs)
     want = ol.detect(od.Records(recs), LANG_OF[g], pkgs)
     assert len(want) > 100
+    assert canon(got) == canon(want)
+
+
+def test_maven_long_keys_vs_oracle():
+    """Maven versions whose keys pass 16 bytes and tie with the bounds' on their heads
+    (numeric-bound advisories are key-order intervals over the installed version's numeric
+    projection; such a key spills, since a Maven package's tail slot holds its program state):
+    the GPU result set equals the oracle's library.Detect."""
+    import oracle.drivers as od
+    import oracle.library as ol
+    from trivy_amd.detector.library import detect
+    r = random.Random(77)
+    base = ["1.2.3.4.5", "10.20.30.40.50", "1.0.0.0.7", "2023.10.15.1"]
+    tail = lambda: "".join(f".{r.choice([0, 1, 2, 9, 10, 99])}" for _ in range(r.randint(1, 3)))  # noqa: E731
+    recs = [{"path": ["data-source", "maven::src0"], "value": json.dumps({"ID": "s0", "Name": "S", "URL": "https://s"})}]
+    names = [f"long{i}" for i in range(60)]
+    for i, name in enumerate(names):
+        b = base[i % len(base)]
+        for j in range(r.randint(1, 3)):
+            lo, hi = sorted([b + tail(), b + tail()],
+                            key=functools.cmp_to_key(lambda x, y: ol.MvnVer(x).compare(ol.MvnVer(y))))
+            adv = r.choice([{"VulnerableVersions": [f"<{hi}"]}, {"VulnerableVersions": [f">={lo}, <{hi}"]},
+                            {"VulnerableVersions": [f"[{lo},{hi}]"]}, {"PatchedVersions": [f">={hi}"]},
+                            {"VulnerableVersions": [f"<={hi}"], "PatchedVersions": [f"{lo}"]}])
+            recs.append({"path": ["maven::src0", name, f"CVE-{j}"], "value": json.dumps(adv)})
+    pkgs = []
+    for i in range(4000):
+        k = r.randrange(len(names))
+        v = base[k % len(base)] + tail() + r.choice(["", "", "-rc1", ".jre", "-sp1", ".0.beta", "-1"])
+        pkgs.append({"Name": names[k], "Version": v, "ID": f"id{i}", "FilePath": ""})
+    eng = _engine_from_records("maven-long", recs)
+    got = detect(eng, "jar", pkgs)
+    want = ol.detect(od.Records(recs), "jar", pkgs)
+    assert len(want) > 500
     assert canon(got) == canon(want)

@@ -99,7 +99,7 @@ struct alignas(16) RowAux {
   uint16_t n_cpe;
 };
 //   AUX_CLASS     library rows: pass if bit <installed version class> of `tag` is set
-//                 (libver.h classes: npm pre-release, PEP 440 local/pre/post, Maven numeric).
+//                 (libver.h classes: npm pre-release, PEP 440 local/pre/post; Maven has one).
 //   AUX_MVN       Maven library rows: the advisory's IsVulnerable program at aux_ids[list_off]
 //                 evaluated pairwise against the installed version (libver.h mvn_program_eval).
 enum : uint32_t { AUX_ARCH_RH = 1, AUX_ARCH_IN = 2, AUX_CPE = 4, AUX_TAG = 8, AUX_CLASS = 16, AUX_MVN = 32 };
@@ -124,7 +124,9 @@ struct alignas(16) SlotVal {
   uint32_t row_count;
 };
 // SLOT_MVN_C0 / C1: the key has a Maven program row (AUX_MVN) that admits installed versions
-// of class 0 / 1 (libver.h mvn_numeric): the probe packs a Maven package's parse only then.
+// of class 0 / 1: the probe packs a Maven package's parse only then.  Maven has one class
+// since the numeric projection (libver.h mvn_numeric_projection), and program rows carry no
+// class filter, so both bits are set together.
 enum : uint32_t { SLOT_POISONED = 1u << 31, SLOT_MVN_C0 = 1u << 30, SLOT_MVN_C1 = 1u << 29, SLOT_LEN_MASK = 0x1FFFFFFFu };
 // Device hash slot: one 64-B cache line holding the hash, the row range and the first
 // kSlotNameWords*8 bytes of the name (memory order, zero padded), so a probe verifies the

@@ -273,9 +273,9 @@ uint64_t Engine::scratch_words(const HostBatch& hb) const {
       const uint2 d = hb.pk[i];
       const uint32_t vlen = d.y >> 16;
       const uint32_t need = (key_bound_any(vlen) + 7) / 8;
-      if (need > kKeyWords) w += need;
-      if (d.x < pi.size() && pi[d.x].cmp == CMP_MAVEN)
-        w += (uint64_t(kMvnPackedWords) * std::min<uint32_t>(2 * vlen + 3, kMvnMaxTok) + 1) / 2;
+      const bool mvn = d.x < pi.size() && pi[d.x].cmp == CMP_MAVEN;
+      if (need > (mvn ? 2u : kKeyWords)) w += need;  // Maven keys spill from 17 bytes (probe_one)
+      if (mvn) w += (uint64_t(kMvnPackedWords) * std::min<uint32_t>(2 * vlen + 3, kMvnMaxTok) + 1) / 2;
     }
     total.fetch_add(w, std::memory_order_relaxed);
   });

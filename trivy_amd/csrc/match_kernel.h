@@ -228,12 +228,10 @@ __device__ __forceinline__ uint4 home_slot(const ProbeArgs& a, uint64_t h, uint3
 
 // One package: encode, hash, probe.  P = uint32_t in the LDS or global address space of s.
 // kb / tab: the lane's LDS key buffer and the dpkg code table (nullptr: generic encoder only).
-// mvn_at: this package's spill words reserved by its tile (fused_kernel), ~0: reserve here.
 template <uint32_t GM, class P, int DIAG = 0>
 __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32_t plat, uint32_t nlen, uint32_t vlen,
                                           const uint8_t* name, const uint8_t* ver, uint64_t vglob, PkgRec& r,
-                                          uint8_t* kb = nullptr, const uint8_t* tab = nullptr,
-                                          unsigned long long mvn_at = ~0ull) {
+                                          uint8_t* kb = nullptr, const uint8_t* tab = nullptr) {
   const PlatInfo pi = a.db.plats[plat];
   // the dpkg-only kernels load the slot heads before the encoder; the other grammar sets
   // after it (their encoders' registers: held across them, the heads made the all-grammar
@@ -283,7 +281,10 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
   }
   hs.flush();
   uint32_t kinfo = 0, koff = 0;
-  if (valid && hs.n > kKeyWords * 8) {  // long key: the whole key again into the spill area
+  // long key: the whole key again into the spill area.  A Maven package's tail slot holds its
+  // program state (below), so its keys spill from 17 bytes on (Engine::scratch_words)
+  const bool mvn_pkg = ((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN;
+  if (valid && hs.n > (mvn_pkg ? 16u : kKeyWords * 8)) {
     const uint32_t need = (hs.n + 7) / 8;
     const unsigned long long o = atomicAdd(&a.ctl[2], (unsigned long long)need);
     if (o + need > a.spill_cap) {
@@ -311,7 +312,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
       MvnParse mp;
       if (mvn_parse(ver, vlen, mp)) {
         const uint32_t need = (kMvnPackedWords * mp.n + 1) / 2;
-        const unsigned long long o = mvn_at != ~0ull ? mvn_at : atomicAdd(&a.ctl[2], (unsigned long long)need);
+        const unsigned long long o = atomicAdd(&a.ctl[2], (unsigned long long)need);
         if (o + need > a.spill_cap) {  // the pass fails (ERR_SPILL); the package keeps no rows
           atomicOr(&a.ctl[3], (unsigned long long)ERR_SPILL);
           valid = false;
@@ -976,24 +977,6 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
   uint2 d = make_uint2(0xFFFFFFFFu, 0);
   if (p < a.n) d = a.pk[p];
   constexpr bool kWaveStage = (SEG & 2) != 0;
-  // Maven grammar: the tile reserves its packages' parse space (the host's per-package bound,
-  // Engine::scratch_words) with one atomic - a per-package atomic on the one spill counter
-  // queued behind every other Maven package of the grid
-  unsigned long long mvn_at = ~0ull;
-  if constexpr (((GM >> CMP_MAVEN) & 1u) != 0) {
-    const uint32_t vl = (p < a.n) ? (d.y >> 16) : 0u;
-    const uint32_t bound = (p < a.n && d.x < a.db.n_plats && a.db.plats[d.x].cmp == CMP_MAVEN)
-                               ? (uint32_t(kMvnPackedWords) * min(2 * vl + 3, uint32_t(kMvnMaxTok)) + 1) / 2
-                               : 0u;
-    if (__syncthreads_or(bound != 0)) {
-      uint32_t o = 0;
-      const uint32_t tot = block_exscan<kTile>(s.wsum[0], bound, tid, o);
-      if (tid == 0) s.base = atomicAdd(&a.ctl[2], (unsigned long long)tot);
-      __syncthreads();
-      mvn_at = s.base + o;  // read before the probe's key buffers overwrite s
-      __syncthreads();
-    }
-  }
   const uint32_t g = t * kGroupsPerTile + (kWaveStage ? (tid >> 6) : 0u);  // the window's first group
   const uint64_t w0 = a.tile_off[g], w1 = a.tile_off[kWaveStage ? g + 1 : (t + 1) * kGroupsPerTile];  // before the scan's barriers
   const uint32_t nlen = d.y & 0xFFFFu, vlen = d.y >> 16;
@@ -1022,11 +1005,10 @@ __global__ __launch_bounds__(kTile, WPE) void fused_kernel(FusedArgs fa) {
     if (staged) {
       const uint8_t* sb = reinterpret_cast<const uint8_t*>(sbuf) + uint32_t(w0 - base16) + off;
       probe_one<GM, uint32_t, DIAG & 3>(a, p, d.x, nlen, vlen, sb, sb + nlen, w0 + off + nlen, r,
-                                        reinterpret_cast<uint8_t*>(u.pr.kbuf) + tid * kFastKeyStride, u.pr.tab, mvn_at);
+                                        reinterpret_cast<uint8_t*>(u.pr.kbuf) + tid * kFastKeyStride, u.pr.tab);
     } else {
       const uint8_t* gb = a.arena + w0 + off;
-      probe_one<GM, uint32_t, DIAG & 3>(a, p, d.x, nlen, vlen, gb, gb + nlen, w0 + off + nlen, r, nullptr, nullptr,
-                                        mvn_at);
+      probe_one<GM, uint32_t, DIAG & 3>(a, p, d.x, nlen, vlen, gb, gb + nlen, w0 + off + nlen, r);
     }
   }
   if (DIAG & 4) r.meta.y = 0;  // no rows: the sweep does nothing
