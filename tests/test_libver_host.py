@@ -161,8 +161,8 @@ def _mvn_any(r):
     """Arbitrary ComparableVersion shapes: int / zero / qualifier items joined by '.', '-' or
     nothing (digit <-> letter transitions open sub-lists), empty items included."""
     items = ["0", "00", "1", "2", "10", "007", "alpha", "a", "b", "m", "rc", "cr", "snapshot", "ga", "final",
-             "release", "sp", "jre", "x", ""]
-    v = r.choice(["0", "1", "2", "10", "1.0", "alpha", "rc", "sp"])
+             "release", "sp", "jre", "x", "", "RC", "Final", "SNAPSHOT", "GA", "M", "x_y", "b+1"]
+    v = r.choice(["0", "1", "2", "10", "1.0", "alpha", "rc", "sp", "RELEASE"])
     for _ in range(r.randint(0, 5)):
         v += r.choice([".", "-", "", "."]) + r.choice(items)
     return v
@@ -195,7 +195,7 @@ def test_maven_projection_against_numeric_bounds():
     assert n > 40000
     assert not bad, bad[:10]
     assert cls("maven", "1.0-rc1") == 0 and cls("maven", "1.2.3") == 0  # one class
-    for _ in range(5000):  # numeric texts: the streamed key == the parse's (a leading blank takes the parse)
+    for _ in range(5000):  # numeric texts: surrounding blanks are trimmed before the parse
         b = _mvn_numeric_bound(r)
         assert key("maven", b) == key("maven", " " + b), b
 
