@@ -123,3 +123,35 @@ def test_sharded_match_gathers_to_single_rank_result(oracle_built):
     assert out[1][4] is None
     ca, cr = _csr(opk, oad, len(batch))
     assert csr[0] == ca.tolist() and csr[1] == cr.tolist()
+
+
+def _overflow_worker(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        g = td.CSRGather("cpu")
+        g.MAX_MATCHES = 5  # stand-in for 2^31: 3 + 3 matches overflow it
+        adv = torch.arange(3, dtype=torch.int32)
+        try:
+            g(adv, torch.tensor([1, 3], dtype=torch.int32), 3, 2)
+            q.put((rank, "returned"))
+        except ValueError:
+            q.put((rank, "raised"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_csr_gather_overflow_raises_on_every_rank():
+    """An oversized gather fails on every rank before any send (no rank left blocked)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_overflow_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = dict(q.get(timeout=100) for _ in ps)
+    for p in ps:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert out == {0: "raised", 1: "raised"}

@@ -97,6 +97,8 @@ class CSRGather:
     per match + 4 B per package over the wire, one device-side add, no reordering.  Buffers
     only grow, so a steady-state gather allocates nothing."""
 
+    MAX_MATCHES = 1 << 31  # row ends are int32
+
     def __init__(self, device, root=0):
         self.device = device
         self.root = root
@@ -118,6 +120,12 @@ class CSRGather:
         counts = [torch.zeros_like(cnt) for _ in range(ws)]
         dist.all_gather(counts, cnt)
         counts = [(int(c[0].item()), int(c[1].item())) for c in counts]
+        t_adv = sum(c[0] for c in counts)
+        t_pkg = sum(c[1] for c in counts)
+        # checked on every rank before any send: a root-only check would leave the senders
+        # blocked in isend
+        if t_adv >= self.MAX_MATCHES:
+            raise ValueError("row ends are 32-bit: gather below 2^31 matches at a time")
         if rank != self.root:
             ops = []
             if n_matches:
@@ -128,10 +136,6 @@ class CSRGather:
                 for r in dist.batch_isend_irecv(ops):
                     r.wait()
             return None
-        t_adv = sum(c[0] for c in counts)
-        t_pkg = sum(c[1] for c in counts)
-        if t_adv >= 1 << 31:
-            raise ValueError("row ends are 32-bit: gather below 2^31 matches at a time")
         self._grow(t_adv, t_pkg)
         ops, a0, p0, fix = [], 0, 0, []
         for r, (na, npk) in enumerate(counts):
