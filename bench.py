@@ -139,7 +139,8 @@ class Mix:
     bounded sample batch, at 1 and N threads."""
 
     per_target = 400
-    build_how = "tvm_batch_add_many_attrs per target (Python loop; attributes: arch, ksplice, CPE sets)"
+    build_how = ("tvm_batch_add_targets_attrs: one C-ABI call for every target of the batch (per target its bucket "
+                 "and attribute flags; arch / ksplice / CPE-set columns per package; CPE sets registered per batch)")
 
     def __init__(self, args, which):
         from tools import synth_mix as sm
@@ -204,14 +205,13 @@ class Mix:
         return out
 
     def fill(self, mb, b=0, e=None):
-        """Packages [b, e) (whole targets), one add call - one Result (result.Filter's scope:
-        its dedup and order) - per target of per_target packages, as the images / lockfiles
-        of a fleet arrive."""
-        e = self.n if e is None else e
-        for s, (p, g) in zip(self.starts, self.batch.groups):
-            lo, hi = max(b, s) - s, min(e, s + len(g["key"])) - s
-            for t0 in range(lo, hi, self.per_target):
-                self.sm.add_slice(mb, self.sdb, p, g, t0, min(hi, t0 + self.per_target))
+        """Packages [b, e) (whole targets) in one tvm_batch_add_targets_attrs call: one Result
+        (result.Filter's scope: its dedup and order) per target of per_target packages, as the
+        images / lockfiles of a fleet arrive.  The columns (one arena) are built once per
+        workload (tools/synth_mix.py BulkCols), as a caller's decoder would hand them over."""
+        if getattr(self, "_bulk", None) is None:
+            self._bulk = self.sm.BulkCols(self.sdb, self.batch, self.per_target)
+        self._bulk.add(mb, b, self.n if e is None else e)
 
     def cpu_baseline(self, budget_s, threads):
         """The native C port of the driver loops (oracle/mixmatch.c + oracle/libcmp.c, pinned by
@@ -279,9 +279,14 @@ def pmc_traffic(config, workload, variant, src_hash):
     for k, want in (("workload", workload), ("kernel_variant", variant), ("kernel_source", src_hash)):
         if d.get(k) != want:
             return None, f"profiles/pmc_summary_{config}.json is for {k}={d.get(k)!r}, this run is {want!r}"
-    return d["hbm_bytes_per_launch"], {"kernel": d["kernel"], "grid": d["grid"], "fetch_bytes_raw": d["fetch_bytes_raw"],
-                                       "write_bytes": d["write_bytes"], "avg_ns_full_grid": d["avg_ns_full_grid"],
-                                       "source": f"profiles/pmc_summary_{config}.json", "note": d["note"]}
+    sized = d.get("hbm_bytes_sized")
+    return (sized if sized else d["hbm_bytes_per_launch"]), {
+        "kernel": d["kernel"], "grid": d["grid"], "fetch_bytes_raw": d["fetch_bytes_raw"],
+        "fetch_bytes_sized": d.get("fetch_bytes_sized"), "write_bytes": d["write_bytes"],
+        "hbm_bytes_raw": d["hbm_bytes_per_launch"], "rdreq": d.get("rdreq"),
+        "traffic_is": ("corrected: read bytes by request size (128 R_128B + 64 R_64B + 32 R_32B) + WRITE_SIZE"
+                       if sized else "raw FETCH_SIZE + WRITE_SIZE (no request-size pass in the summary)"),
+        "avg_ns_full_grid": d["avg_ns_full_grid"], "source": f"profiles/pmc_summary_{config}.json", "note": d["note"]}
 
 
 def launch_ranks(n):
@@ -318,8 +323,8 @@ def main():
     ap.add_argument("--no-fill", action="store_true", help="c2: skip the FillInfo / Filter legs")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end pipelined pass")
     ap.add_argument("--chunk", type=int, default=1 << 20, help="end-to-end pass: packages per pipeline chunk")
-    ap.add_argument("--dropin", action="store_true",
-                    help="c2: also time 100-package requests through the per-target driver path")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="c2: skip the C1-shaped leg (100-package requests through the per-target driver path)")
     ap.add_argument("--variant", type=int, default=None, help="match-path variant (tvm_engine_set_variant)")
     ap.add_argument("--sweep", type=int, default=0,
                     help="time every match-path variant over N interleaved rounds (stderr table) first")
@@ -341,8 +346,14 @@ def main():
     if args.gpus is not None and world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     local = int(os.environ.get("LOCAL_RANK", 0))
+    # torch first: libtrivy_amd.so and torch's bundled HIP runtime share the SONAME
+    # libamdhip64.so.7, so the library then binds to torch's runtime (ROCm 7.0 in this image)
+    # rather than /opt/rocm's 7.2 it was built with; the line records which one ran
+    # (config.hip_runtime).  Loading the library first does not work: torch's HIP initialisation
+    # then fails on the box and no device is visible to either (measured)
     import torch
     import torch.distributed as dist
+    import trivy_amd
     # TVM_BENCH_BACKEND=gloo rehearses the N>1 path on a box with fewer GPUs than ranks
     # (ranks then share devices round-robin, the gather goes through host memory); the
     # scaling runs use RCCL, one rank per GPU
@@ -356,7 +367,6 @@ def main():
     gdev = f"cuda:{local}"
     cdev = gdev if backend == "nccl" else "cpu"  # where collectives run
 
-    import trivy_amd
     from trivy_amd import dist as td
     from trivy_amd._lib import lib
     from trivy_amd.batch import MatchBatch
@@ -515,33 +525,45 @@ def main():
         sr["mb"].close()
 
     # ---- end-to-end pipelined pass over PCIe (N = 1) -------------------------------------------
-    # the host batch in, the DetectedVulnerability set out: one pipelined pass (upload, match,
-    # per-package lists in pinned host memory) + tvm_pipeline_vulns over the result as it arrived
+    # the host batch in, the DetectedVulnerability set out and consumed: one pipelined pass
+    # (upload, match, per-package lists in pinned host memory) + tvm_pipeline_vulns over the
+    # result as it arrived (Red Hat batches: the per-CVE merge and the export over the pass's
+    # list, still in HBM) + tvm_vuln_set_walk, a native consumer that decodes every record
+    # index and reads its record and its package's InstalledVersion (INTEGRATION.md §3's loop)
     e2e = None
-    has_rh = "Red Hat" in wl.plats  # the per-CVE merge runs on the device-resident path (tvm_match_vulns)
+
+    def vulns_and_consume(m):
+        vs = m.vulns(pipeline=True)
+        t_c = time.perf_counter()
+        n_w, dig = vs.walk()
+        c_ms = (time.perf_counter() - t_c) * 1e3
+        if n_w != len(vs):
+            raise RuntimeError("the consumer walked another number of DetectedVulnerabilities than the set holds")
+        out = (vs.ms, c_ms, len(vs), vs.n_grp_recs)
+        vs.close()
+        return out
+
     if world == 1 and not args.no_e2e and rank == 0:
         mp = MatchBatch(eng)
         wl.fill(mp)
         mp.pipeline_prepare(match_cap=total, chunk_packages=args.chunk)
         for _ in range(max(1, args.warmup)):
             mp.pipeline_run()
+            vulns_and_consume(mp)
         npass = max(3, args.steps // 4)
         runs = []
         for _ in range(npass):
             got, ep, m = mp.pipeline_run()
             if got != total or ep != -1:
                 raise RuntimeError("end-to-end pass disagrees with the device-resident pass")
-            v_ms = None
-            if not has_rh:
-                vs = mp.vulns(pipeline=True)
-                v_ms = vs.ms
-                vs.close()
-            runs.append((m + (v_ms or 0.0), m, v_ms))
+            v_ms, c_ms, n_dv, n_grp = vulns_and_consume(mp)
+            runs.append((m + v_ms + c_ms, m, v_ms, c_ms))
         runs.sort(key=lambda r: r[0])
-        both, med, v_ms = runs[len(runs) // 2]
+        both, med, v_ms, c_ms = runs[len(runs) // 2]
         st = mp.pipeline_stats()
         e2e = {"packages_per_s": wl.n / (both / 1e3), "ms": both, "pass_ms": med, "vulns_ms": v_ms,
-               "pass_packages_per_s": wl.n / (med / 1e3), "passes": npass,
+               "consume_ms": c_ms, "pass_packages_per_s": wl.n / (med / 1e3), "passes": npass,
+               "detected_vulnerabilities": n_dv, "merged_group_records": n_grp,
                "result_form": "CSR, 3-byte advisory indices + row ends in pinned host memory",
                "h2d_bytes": st["h2d_bytes"], "d2h_bytes": st["d2h_bytes"], "chunks": st["chunks"],
                "pcie_GBs": (st["h2d_bytes"] + st["d2h_bytes"]) / (med / 1e3) / 1e9,
@@ -550,10 +572,11 @@ def main():
                          "version string once + per-package references, one DMA per chunk) + the kernel that "
                          "rebuilds each chunk in HBM + match kernels + the per-package advisory lists (CSR) "
                          "written into pinned host memory by the next launch's first workgroups (pass_ms) + "
-                         "tvm_pipeline_vulns: the DetectedVulnerability set (per-package record lists) over the "
-                         "result as it arrived (vulns_ms)" + ("" if not has_rh else
-                                                             "; Red Hat batches: pass only (the per-CVE merge "
-                                                             "runs on the device-resident path, see vulns)"),
+                         "tvm_pipeline_vulns, the DetectedVulnerability set (vulns_ms: the lists as they arrived; "
+                         "batches with Red Hat packages: the per-CVE merge + export over the pass's list in HBM and "
+                         "the merged groups' records) + tvm_vuln_set_walk on the host threads, every "
+                         "DetectedVulnerability's record index decoded, its record and its package's "
+                         "InstalledVersion read (consume_ms)",
                "prepare_ms": st["prepare_ms"],
                "outside": "prepare (once per batch: sizing, building the transport form on the host threads "
                           "(prepare_encode_ms); the batch is re-run, see fresh_batch for batches seen once)"}
@@ -574,24 +597,22 @@ def main():
             te = time.perf_counter()
             if got != total or ep != -1:
                 raise RuntimeError("fresh-batch pass disagrees with the device-resident pass")
-            v_ms = 0.0
-            if not has_rh:
-                vs = mf.vulns(pipeline=True)
-                v_ms = vs.ms
-                vs.close()
+            v_ms, c_ms, _, _ = vulns_and_consume(mf)
             st = mf.pipeline_stats()
             runs.append({"build_ms": (tp - tb) * 1e3, "prepare_ms": (tr - tp) * 1e3, "pass_ms": (te - tr) * 1e3,
-                         "vulns_ms": v_ms, "h2d_bytes": st["h2d_bytes"], "d2h_bytes": st["d2h_bytes"]})
+                         "vulns_ms": v_ms, "consume_ms": c_ms, "h2d_bytes": st["h2d_bytes"],
+                         "d2h_bytes": st["d2h_bytes"]})
             mf.close()
-        steady = sorted(runs[1:], key=lambda r: r["prepare_ms"] + r["pass_ms"] + r["vulns_ms"])
+        steady = sorted(runs[1:], key=lambda r: r["prepare_ms"] + r["pass_ms"] + r["vulns_ms"] + r["consume_ms"])
         med = steady[len(steady) // 2]
-        inner = med["prepare_ms"] + med["pass_ms"] + med["vulns_ms"]
+        inner = med["prepare_ms"] + med["pass_ms"] + med["vulns_ms"] + med["consume_ms"]
         fresh = dict(med, packages_per_s=wl.n / (inner / 1e3),
                      packages_per_s_with_build=wl.n / ((inner + med["build_ms"]) / 1e3), batches=len(runs),
                      form="raw (pinned staging copy on the host threads; no per-batch string dedup)",
                      inside="prepare (freeze, size, pinned staging copy, buffers from the block cache) + one "
                             "pipelined pass (upload, match, per-package advisory lists back in pinned host memory "
-                            "as the CSR: 3-byte indices + row ends) + tvm_pipeline_vulns (vulns_ms)",
+                            "as the CSR: 3-byte indices + row ends) + tvm_pipeline_vulns (vulns_ms) + "
+                            "tvm_vuln_set_walk (consume_ms)",
                      build=wl.build_how,
                      outside="build_ms (in packages_per_s_with_build only): the caller adding the batch's packages")
 
@@ -634,7 +655,7 @@ def main():
                                         "matches_per_s": total / (vex_ms / 1e3)}
 
     dropin = None
-    if args.dropin and args.config == "c2" and rank == 0:
+    if not args.no_dropin and args.config == "c2" and rank == 0 and world == 1:
         # C1-shaped request through the drop-in per-target path (debian Scanner.Detect,
         # debian.go:57-119): 100 packages of one Debian 12 image, through the C-ABI alone
         import ctypes
@@ -647,15 +668,17 @@ def main():
               for i in range(b0, b0 + 100)]
         arr, _keep = osp._pkg_array(pk)
         res, ebuf, now = L.Result(), L.errbuf(), osp._now(None)
-        n_calls, found = 200, 0
-        t_c = time.perf_counter()
+        n_calls, found, lat = 400, 0, []
         for _ in range(n_calls):
+            t_c = time.perf_counter()
             if lib().tvm_ospkg_driver_detect(eng.h, b"debian", b"12", None, arr, len(pk), now, ctypes.byref(res), ebuf,
                                              len(ebuf)):
                 raise RuntimeError(ebuf.value.decode())
             found = res.n
             lib().tvm_result_free(ctypes.byref(res))
-        c_ms = (time.perf_counter() - t_c) * 1e3 / n_calls
+            lat.append((time.perf_counter() - t_c) * 1e3)
+        lat = sorted(lat[20:])  # the first calls grow the drop-in buffers
+        c_ms = sum(lat) / len(lat)
         # the same call from 8 threads at once (a twirp server / k8s worker pool): the engine
         # coalesces the queued calls into shared launches (tvm_engine_dropin_stats)
         import threading
@@ -684,7 +707,9 @@ def main():
             raise RuntimeError(f"concurrent drop-in calls: {fails[:3]}")
         st1 = (ctypes.c_uint64 * 3)()
         lib().tvm_engine_dropin_stats(eng.h, st1)
-        dropin = {"workload": "c1-shaped: 100 debian-12 packages per call", "c_abi_ms_per_call": c_ms,
+        dropin = {"workload": "c1-shaped: 100 debian-12 packages per call (tvm_ospkg_driver_detect: debian "
+                              "Scanner.Detect, debian.go:57-119)", "c_abi_ms_per_call": c_ms,
+                  "p50_ms": lat[len(lat) // 2], "p99_ms": lat[int(len(lat) * 0.99)],
                   "vulnerabilities_per_call": found,
                   "concurrent": {"threads": n_thr, "calls": n_thr * per_thr,
                                  "calls_per_s": n_thr * per_thr / conc_s, "launches": st1[0] - st0[0],
@@ -724,7 +749,7 @@ def main():
             "config": {"workload": wl.name, "packages": wl.n, "packages_per_step": n_job, "packages_rank0": n_local,
                        "matches_rank0": total,
                        "kernel_variant": vname, "kernel_source": src_hash, "db_keys": wl.n_keys, "db_advisories": wl.n_adv,
-                       "platforms": wl.plats, "parallelism": par},
+                       "platforms": wl.plats, "parallelism": par, "hip_runtime": trivy_amd.runtime_info()},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_from": traffic_src,
                          "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": kernel_ms,

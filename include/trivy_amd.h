@@ -241,6 +241,16 @@ int64_t tvm_batch_add_many(tvm_batch* b, tvm_engine* e, const char* bucket, size
 int64_t tvm_batch_add_targets(tvm_batch* b, tvm_engine* e, size_t n_targets, const tvm_str* buckets,
                               const uint64_t* target_end, const char* arena, const uint64_t* name_off,
                               const uint32_t* name_len, const uint64_t* ver_off, const uint32_t* ver_len);
+/* tvm_batch_add_targets with the rpm drivers' attributes (what tvm_batch_add_many_attrs adds
+ * for one target): target_flags[t] = the TVM_ATTR_* bits of target t (NULL = none; KSPLICE
+ * and CPESET exclusive), and the attribute columns per package (arch strings in the arena,
+ * tvm_batch_cpe_set ids), read only for the packages of targets whose flags name them.  Both
+ * calls fill the batch on the host threads (the package scanners of pkg/scanner/local/scan.go:
+ * 170-194 hand packages over per target; here a fleet's targets arrive in one call). */
+int64_t tvm_batch_add_targets_attrs(tvm_batch* b, tvm_engine* e, size_t n_targets, const tvm_str* buckets,
+                                    const uint32_t* target_flags, const uint64_t* target_end, const char* arena,
+                                    const uint64_t* name_off, const uint32_t* name_len, const uint64_t* ver_off,
+                                    const uint32_t* ver_len, const tvm_attr_cols* attrs);
 int64_t tvm_batch_size(const tvm_batch* b);
 /* Copies the batch to the device and sizes the match buffer. */
 int tvm_batch_upload(tvm_engine* e, tvm_batch* b, uint64_t match_cap, char* err, size_t errlen);
@@ -251,7 +261,8 @@ int tvm_engine_sync(tvm_engine* e, char* err, size_t errlen);
  * own HIP runtime instance) and reports any pending asynchronous error.  Test and health-check
  * hook; no reference counterpart. */
 int tvm_device_sync(int device, char* err, size_t errlen);
-/* Process teardown: drains every device's queues, joins the library's host worker threads and
+/* Process teardown: drains the queues of every device an engine was opened on (a process that
+ * opened none starts no HIP work here), joins the library's host worker threads and
  * frees its cached device / pinned blocks, so that nothing of the library's is left for the
  * HIP runtime's own teardown at exit.  Call once before the process exits (the Python
  * binding registers it with atexit); the library stays usable (later calls run without the
@@ -366,6 +377,10 @@ int tvm_pipeline_times(tvm_batch* b, uint64_t* encode_us, uint64_t* prepare_us);
  * misses}; tvm_pool_trim frees every cached block. */
 void tvm_pool_stats(uint64_t out[4]);
 void tvm_pool_trim(void);
+/* The HIP runtime this library's calls bind to: hipRuntimeGetVersion / hipDriverGetVersion
+ * and the path of the libamdhip64 that provides them (a host process that loaded another
+ * libamdhip64.so.7 first - torch's bundled runtime - binds this library to that one). */
+int tvm_runtime_info(int* hip_runtime, int* hip_driver, char* path, size_t pathlen);
 
 /* ---- SBOM decode (the detector input of `trivy sbom`) ------------------------------------
  * Native CycloneDX JSON decode: pkg/sbom/cyclonedx/unmarshal.go:63-230 + pkg/sbom/io/decode.go:
@@ -460,10 +475,23 @@ typedef struct {
  * are merged on the device first (tvm_match_redhat_merge, if it has not run).  TVM_EINVAL when
  * the pass overflowed its match buffer, met an undecodable advisory or flagged an error. */
 int tvm_match_vulns(tvm_engine* e, tvm_batch* b, tvm_vuln_set* out, char* err, size_t errlen);
-/* The same from the last tvm_pipeline_run's result: the lists that pass left in pinned
- * memory, no copy (batches without Red Hat packages; valid until the next pass). */
+/* The same from the last completed tvm_pipeline_run (TVM_EINVAL before one).  Batches without
+ * Red Hat packages: the lists that pass left in pinned memory, no copy - the set is invalidated
+ * by the next tvm_pipeline_prepare / tvm_pipeline_run / tvm_batch_free of the batch.  Batches
+ * with Red Hat packages: the per-CVE merge (redhat.go:146-187) and the export run on the device
+ * over the pass's match list (still in HBM), and the set owns its lists (valid until
+ * tvm_vuln_set_free). */
 int tvm_pipeline_vulns(tvm_engine* e, tvm_batch* b, tvm_vuln_set* out, char* err, size_t errlen);
 void tvm_vuln_set_free(tvm_vuln_set* s);
+/* A consumer of a set, natively (INTEGRATION.md §3's loop on the host threads): every
+ * DetectedVulnerability's record index decoded, its record resolved (adv_recs / grp_recs) and
+ * read (VulnerabilityID, FixedVersion), its package's InstalledVersion located in the batch
+ * (tvm_batch_report_get).  n_out = DetectedVulnerabilities walked; digest = the wrapping sum
+ * over them of fmix64(p * 0x9E3779B97F4A7C15 + r * 0xC2B2AE3D27D4EB4F + (|InstalledVersion| << 40)
+ * + (VulnerabilityID[0] << 32) + |FixedVersion|), p = first_pkg + the package's batch index, r =
+ * the record index - what a caller's own loop over the set costs, and a check that it saw
+ * every entry (bench.py end_to_end consume_ms). */
+int tvm_vuln_set_walk(const tvm_vuln_set* s, const tvm_batch* b, uint64_t* n_out, uint64_t* digest);
 /* The package side of packages [first, first + n): names = the tvm_batch_set_report PkgName
  * (p = NULL: the caller's package Name), versions = InstalledVersion (the report's, else the
  * batch version, which is FormatVersion of the package for every driver comparing the binary

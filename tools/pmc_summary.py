@@ -80,6 +80,12 @@ def main(argv):
             d["write_bytes"] = c["WRITE_SIZE"] * 1024
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
             d["hbm_bytes_raw"] = d["fetch_bytes_raw"] + d["write_bytes"]
+        if "TCC_EA0_RDREQ_128B_sum" in c:  # read bytes by request size (profiles/r06/calib.txt)
+            r, r32 = c.get("TCC_EA0_RDREQ_sum", 0.0), c.get("TCC_EA0_RDREQ_32B_sum", 0.0)
+            r64, r128 = c.get("TCC_EA0_RDREQ_64B_sum", 0.0), c["TCC_EA0_RDREQ_128B_sum"]
+            d["fetch_bytes_sized"] = 128 * r128 + 64 * r64 + 32 * r32 + 64 * max(0.0, r - r128 - r64 - r32)
+            if "write_bytes" in d:
+                d["hbm_bytes_sized"] = d["fetch_bytes_sized"] + d["write_bytes"]
         rows.append(d)
         avg = f"avg {d['avg_ns'] / 1e3:.1f} us over {d['launches_traced']} traced launches" if d["avg_ns"] else "no trace"
         print(f"== {k}  grid {grid}  {avg}\n   {full}")
@@ -87,7 +93,7 @@ def main(argv):
         for n, v in sorted(c.items()):
             per = f"   ({v / waves:,.1f} per wave)" if waves and n.startswith("SQ_INSTS") else ""
             print(f"{n:>28}: {v:,.1f}{per}")
-        for n in ("fetch_bytes_raw", "write_bytes", "hbm_bytes_raw"):
+        for n in ("fetch_bytes_raw", "write_bytes", "hbm_bytes_raw", "fetch_bytes_sized", "hbm_bytes_sized"):
             if n in d:
                 print(f"{n:>28}: {d[n]:,.0f} per launch")
     if "--json" in opt:
@@ -106,10 +112,14 @@ def main(argv):
                 "grid": top["grid"], "avg_ns_full_grid": top["avg_ns"],
                 "fetch_bytes_raw": top["fetch_bytes_raw"], "write_bytes": top["write_bytes"],
                 "hbm_bytes_per_launch": top["hbm_bytes_raw"],
+                "fetch_bytes_sized": top.get("fetch_bytes_sized"), "hbm_bytes_sized": top.get("hbm_bytes_sized"),
+                "rdreq": {k: top["counters"].get(k) for k in ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum",
+                                                               "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")},
                 "note": "raw FETCH_SIZE + WRITE_SIZE of one full-grid launch (median over the profiled launches); "
-                        "MI355X_MICROARCH.md §HBM: gfx950 FETCH_SIZE counts half the bytes of 16-B/lane coalesced "
-                        "streaming reads (the staging and row loads have that shape), so the raw fetch is a lower "
-                        "bound on the bytes the kernel moved from beyond L2"}
+                        "FETCH_SIZE tallies every L2-to-fabric read request at 64 B, but streaming reads go out as "
+                        "128-B requests (calibrated on the match kernel's own load shapes, profiles/r06/calib.txt), "
+                        "so hbm_bytes_sized = 128 R_128B + 64 R_64B + 32 R_32B + WRITE_SIZE is the corrected figure "
+                        "(Infinity-Cache hits are still counted: bytes from beyond L2)"}
         with open(opt["--json"], "w") as f:
             json.dump(summ, f, indent=1)
         print(json.dumps(summ))

@@ -29,6 +29,9 @@ pmc() {  # name, counters...
 }
 pmc fetch FETCH_SIZE
 pmc write WRITE_SIZE
+# request sizes (tools/calib_fetch: FETCH_SIZE tallies every request at 64 B; the 128-B requests of
+# streaming reads are half-counted): bytes = 128 R_128B + 64 R_64B + 32 R_32B
+pmc rdreq TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum
 if [ "${PMC_EXTRA:-0}" == "1" ]; then
   pmc sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS
   pmc tcc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE GRBM_COUNT

@@ -404,3 +404,76 @@ def driver_packages(db, p, g, idx):
                 d["BuildInfo"] = {"ContentSets": list(cs), "Nvr": g["nvr"][i].decode(), "Arch": "x86_64"}
         pk.append(d)
     return pk
+
+
+class BulkCols:
+    """A MixBatch's columns in the form tvm_batch_add_targets_attrs takes them, built once per
+    batch: one arena (names, versions, arches), targets of `per_target` packages cut from each
+    group (images / lockfiles), per target its bucket and attribute flags (arch for Red Hat /
+    Oracle / Rocky, ksplice for Oracle, the CPE set for Red Hat), and per Red Hat package the
+    index of its (content sets, NVR) combination (registered per batch: cpe_set ids are
+    per-batch).  Package order = add_to's."""
+
+    def __init__(self, db, batch, per_target=400):
+        from trivy_amd.batch import ATTR_ARCH, ATTR_CPESET, ATTR_KSPLICE, arena_of
+        names, vers, arches = [], [], []
+        buckets, flags, ends = [], [], []
+        combo = []  # per package: (content sets, NVR) combination index, -1 = none
+        self.combos = {}
+        o = 0
+        for p, g in batch.groups:
+            bucket, kind = db.plats[p]
+            m = len(g["key"])
+            names.append(g["name"])
+            vers.append(g["ver"])
+            arches.append(g["arch"] if "arch" in g else np.full(m, b"", dtype="S1"))
+            f = (ATTR_ARCH if "arch" in g else 0) | (ATTR_KSPLICE if kind == "oracle" else 0) | \
+                (ATTR_CPESET if kind == "redhat" else 0)
+            cidx = np.full(m, -1, dtype=np.int64)
+            if kind == "redhat":
+                # (release, NVR when BuildInfo) -> combination index, vectorised over the group
+                _, first_i, inv = np.unique(np.char.add(np.char.add(g["rhrel"].astype("S"), b"|"),
+                                                        np.where(g["bi"], g["nvr"], b"")), return_index=True,
+                                            return_inverse=True)
+                for i in first_i.tolist():
+                    self.combos.setdefault(rh_cpe_key(g, i), len(self.combos))
+                cidx = np.array([self.combos[rh_cpe_key(g, i)] for i in first_i.tolist()], dtype=np.int64)[inv]
+            combo.append(cidx)
+            for t0 in range(0, m, per_target):
+                buckets.append(bucket)
+                flags.append(f)
+                ends.append(o + min(m, t0 + per_target))
+            o += m
+        self.n = o
+        self.buckets, self.flags = buckets, np.array(flags, dtype=np.uint32)
+        self.ends = np.array(ends, dtype=np.uint64)
+        self.combo = np.concatenate(combo) if combo else np.zeros(0, np.int64)
+        cat = lambda xs: np.concatenate(xs) if xs else np.zeros(0, dtype="S1")  # noqa: E731
+        self.arena, ((self.noff, self.nlen), (self.voff, self.vlen), (self.aoff, self.alen)) = \
+            arena_of(cat(names), cat(vers), cat(arches))
+
+    def add(self, mb, lo=0, hi=None):
+        """Adds the whole targets inside packages [lo, hi) to a MatchBatch in one call; returns
+        the first index."""
+        hi = self.n if hi is None else hi
+        starts = np.concatenate([[0], self.ends[:-1]]).astype(np.int64)
+        sel = np.nonzero((starts >= lo) & (self.ends.astype(np.int64) <= hi))[0]
+        if not len(sel):
+            return len(mb)
+        a, z = int(starts[sel[0]]), int(self.ends[sel[-1]])
+        ids = {}
+        cs = self.combo[a:z]
+        sets = np.zeros(z - a, dtype=np.uint32)
+        if (cs >= 0).any():
+            inv = {v: k for k, v in self.combos.items()}
+            for c in np.unique(cs[cs >= 0]).tolist():
+                k = inv[c]
+                ids[c] = mb.cpe_set(list(k[0]), k[1])
+            lut = np.zeros(len(self.combos), dtype=np.uint32)
+            for c, i in ids.items():
+                lut[c] = i
+            sets = np.where(cs >= 0, lut[np.maximum(cs, 0)], 0).astype(np.uint32)
+        return mb.add_targets([self.buckets[t] for t in sel.tolist()], self.ends[sel] - np.uint64(a), self.arena,
+                              self.noff[a:z], self.nlen[a:z], self.voff[a:z], self.vlen[a:z],
+                              flags=self.flags[sel], arch_off=self.aoff[a:z], arch_len=self.alen[a:z], cpe_sets=sets)
+

@@ -7,6 +7,6 @@ thin ctypes mirror of the reference's Go surfaces (pkg/detector/ospkg, ...) used
 by the tests and the benchmark.
 """
 from .db import DB, Engine, load_fixture_files  # noqa: F401
-from ._lib import lib, LIB_PATH  # noqa: F401
+from ._lib import lib, LIB_PATH, runtime_info  # noqa: F401
 
 __version__ = "0.1.0"

@@ -160,6 +160,9 @@ _SIG = [
     ("tvm_batch_add_targets", ctypes.c_int64, [_P, _P, ctypes.c_size_t, ctypes.POINTER(Str), ctypes.c_void_p,
                                                ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                ctypes.c_void_p]),
+    ("tvm_batch_add_targets_attrs", ctypes.c_int64, [_P, _P, ctypes.c_size_t, ctypes.POINTER(Str), ctypes.c_void_p,
+                                                     ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ("tvm_batch_cpe_set", ctypes.c_int64, [_P, _P, ctypes.c_void_p, ctypes.c_size_t, Str]),
     ("tvm_batch_add_many_attrs", ctypes.c_int64, [_P, _P, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -251,6 +254,8 @@ _SIG = [
     ("tvm_batch_set_report", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(Str),
                                             ctypes.POINTER(Str), ctypes.POINTER(Str)]),
     ("tvm_match_vulns", ctypes.c_int, [_P, _P, ctypes.POINTER(VulnSet), ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_runtime_info", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]),
+    ("tvm_vuln_set_walk", ctypes.c_int, [ctypes.POINTER(VulnSet), _P, ctypes.c_void_p, ctypes.c_void_p]),
     ("tvm_pipeline_vulns", ctypes.c_int, [_P, _P, ctypes.POINTER(VulnSet), ctypes.c_char_p, ctypes.c_size_t]),
     ("tvm_vuln_set_free", None, [ctypes.POINTER(VulnSet)]),
     ("tvm_batch_report_get", ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(RawStr),
@@ -294,3 +299,14 @@ def s(x):
 
 def errbuf():
     return ctypes.create_string_buffer(4096)
+
+
+def runtime_info():
+    """{"hip_runtime", "hip_driver", "libamdhip64"}: the HIP runtime libtrivy_amd's calls bind to
+    (tvm_runtime_info; after `import torch` that is torch's bundled libamdhip64.so if torch
+    loaded first - both carry the SONAME libamdhip64.so.7)."""
+    rt, drv, path = ctypes.c_int(), ctypes.c_int(), ctypes.create_string_buffer(1024)
+    lib().tvm_runtime_info(ctypes.byref(rt), ctypes.byref(drv), path, len(path))
+    fmt = lambda v: f"{v // 10_000_000}.{v // 100_000 % 100}.{v % 100_000}"  # noqa: E731  HIP_VERSION encoding
+    return {"hip_runtime": fmt(rt.value), "hip_driver": fmt(drv.value), "libamdhip64": path.value.decode()}
+

@@ -138,17 +138,31 @@ class MatchBatch:
             raise RuntimeError("tvm_batch_add_many rejected the packages")
         return first
 
-    def add_targets(self, buckets, target_end, arena, name_off, name_len, ver_off, ver_len):
+    def add_targets(self, buckets, target_end, arena, name_off, name_len, ver_off, ver_len, flags=None,
+                    arch_off=None, arch_len=None, cpe_sets=None):
         """Many targets in one call (tvm_batch_add_targets): target t = packages
-        [target_end[t-1], target_end[t]) of the arena columns under buckets[t]."""
-        from ._lib import Str
+        [target_end[t-1], target_end[t]) of the arena columns under buckets[t].  flags: per target
+        ATTR_* bits, with the per-package attribute columns (arch strings in the arena, cpe_set()
+        ids) - tvm_batch_add_targets_attrs."""
+        from ._lib import AttrCols, Str
         bl = [b.encode() if isinstance(b, str) else bytes(b) for b in buckets]
         arr = (Str * max(len(bl), 1))(*[Str(b, len(b)) for b in bl])
         te = np.ascontiguousarray(target_end, dtype=np.uint64)
         cols = [np.ascontiguousarray(c, dtype=t) for c, t in ((name_off, np.uint64), (name_len, np.uint32),
                                                               (ver_off, np.uint64), (ver_len, np.uint32))]
-        first = lib().tvm_batch_add_targets(self.h, self.engine.h, len(bl), arr, te.ctypes.data, arena,
-                                            *[c.ctypes.data for c in cols])
+        if flags is None:
+            first = lib().tvm_batch_add_targets(self.h, self.engine.h, len(bl), arr, te.ctypes.data, arena,
+                                                *[c.ctypes.data for c in cols])
+        else:
+            fl = np.ascontiguousarray(flags, dtype=np.uint32)
+            ao = None if arch_off is None else np.ascontiguousarray(arch_off, dtype=np.uint64)
+            al = None if arch_len is None else np.ascontiguousarray(arch_len, dtype=np.uint32)
+            cs = None if cpe_sets is None else np.ascontiguousarray(cpe_sets, dtype=np.uint32)
+            attrs = AttrCols(ao.ctypes.data if ao is not None else None, al.ctypes.data if al is not None else None,
+                             cs.ctypes.data if cs is not None else None)
+            first = lib().tvm_batch_add_targets_attrs(self.h, self.engine.h, len(bl), arr, fl.ctypes.data,
+                                                      te.ctypes.data, arena, *[c.ctypes.data for c in cols],
+                                                      ctypes.byref(attrs))
         if first < 0:
             raise RuntimeError("tvm_batch_add_targets rejected the targets")
         return first
@@ -537,16 +551,20 @@ class VulnSet:
         return d
 
     def dicts(self, pkgs=None, report=None):
-        """DetectedVulnerability dicts (small sets): pkgs maps a package index to the caller's
-        package dict (ID, Name, Identifier, Layer copied per the record's flags); report =
-        MatchBatch.report() columns (InstalledVersion, PkgPath, PkgName overrides)."""
+        """DetectedVulnerability dicts (small sets): pkgs maps a package index as the set
+        reports it (self.pkg: first_pkg + batch index, tvm_batch_set_package_base) to the
+        caller's package dict (ID, Name, Identifier, Layer copied per the record's flags);
+        report = MatchBatch.report() columns of the whole batch (batch indices from 0:
+        InstalledVersion, PkgPath, PkgName overrides)."""
         from ._lib import COPY_IDENTIFIER, COPY_LAYER, COPY_PKG_ID, COPY_PKG_NAME
         names, vers, paths = report if report is not None else self.batch.report()
+        base = int(self._c.first_pkg) if self._c is not None else 0
         out = []
         for p, r in zip(self.pkg.tolist(), self.rec.tolist()):
             d = dict(self.record(r))
             fl = d.pop("_copy")
             pk = (pkgs or {}).get(p, {})
+            p -= base  # the report columns are indexed from the batch's first package
             if fl & COPY_PKG_ID and pk.get("ID"):
                 d["PkgID"] = pk["ID"]
             name = names[p] if names[p] is not None else (pk.get("Name") if fl & COPY_PKG_NAME else None)
@@ -562,6 +580,38 @@ class VulnSet:
                 d["Layer"] = pk["Layer"]
             out.append(d)
         return out
+
+    def walk(self):
+        """tvm_vuln_set_walk: (DetectedVulnerabilities walked, digest) - a native consumer that
+        decodes every record index and reads its record and its package's InstalledVersion."""
+        n, d = ctypes.c_uint64(), ctypes.c_uint64()
+        if lib().tvm_vuln_set_walk(ctypes.byref(self._c), self.batch.h, ctypes.byref(n), ctypes.byref(d)):
+            raise RuntimeError("tvm_vuln_set_walk rejected the set")
+        return n.value, d.value
+
+    def digest(self, report=None):
+        """The walk's digest recomputed here (numpy) from the columns and the records."""
+        names, vers, _ = report if report is not None else self.batch.report()
+        M = np.uint64(0xFFFFFFFFFFFFFFFF)
+        base = int(self._c.first_pkg)
+        vlen = np.array([len(v.encode()) for v in vers], dtype=np.uint64)
+        uniq, inv = np.unique(self.rec, return_inverse=True)
+        id0 = np.zeros(len(uniq), np.uint64)
+        flen = np.zeros(len(uniq), np.uint64)
+        for k, r in enumerate(uniq.tolist()):
+            d = self.record(r)
+            id0[k] = d["VulnerabilityID"].encode()[0] if d["VulnerabilityID"] else 0
+            flen[k] = len(d.get("FixedVersion", "").encode())
+        with np.errstate(over="ignore"):
+            p = self.pkg.astype(np.uint64)
+            h = (p * np.uint64(0x9E3779B97F4A7C15) + self.rec.astype(np.uint64) * np.uint64(0xC2B2AE3D27D4EB4F)
+                 + (vlen[(p - np.uint64(base)).astype(np.int64)] << np.uint64(40)) + (id0[inv] << np.uint64(32))
+                 + flen[inv]) & M
+            for c in (0xff51afd7ed558ccd, 0xc4ceb9fe1a85ec53):
+                h ^= h >> np.uint64(33)
+                h *= np.uint64(c)
+            h ^= h >> np.uint64(33)
+            return int(h.sum(dtype=np.uint64))
 
     def close(self):
         if self._c is not None and self._c.priv:

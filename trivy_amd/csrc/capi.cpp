@@ -1,7 +1,10 @@
 // C-ABI implementation (include/trivy_amd.h).
 #include "../../include/trivy_amd.h"
 
+#include <dlfcn.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -91,6 +94,9 @@ struct tvm_batch {
   std::unique_ptr<Pipeline> pipe;      // tvm_pipeline_* state
   uint32_t pkg_base = 0;               // tvm_batch_set_package_base
   uint64_t pipe_total = 0;
+  bool pipe_ok = false;                // the pipeline's last pass completed (its result is valid)
+  int64_t pipe_errp = -1;              // that pass's first poisoned package (-1: none)
+  RedHatMerge pipe_rh;                 // the per-CVE merge over a pipelined pass's list (tvm_pipeline_vulns)
   uint64_t pipe_runs = 0, pipe_wide_for = ~0ull;  // passes run; the pass pipe_wide was widened for
   std::vector<uint32_t> pipe_wide;                // 3-byte result indices widened (tvm_pipeline_result)
   unsigned long long* order_scratch = nullptr;  // tvm_match_order_into: ticket + look-back word per tile
@@ -312,7 +318,12 @@ const char* tvm_db_advisory_vuln_id(const tvm_db* db, uint32_t adv) {
   return adv < db->db.advs.size() ? db->db.advs[adv].vuln_id.c_str() : nullptr;
 }
 
+// Devices an engine was opened on (bit d): tvm_shutdown drains those alone, and starts no
+// HIP runtime in a process that never opened one (SBOM decode, host-only work)
+static std::atomic<uint64_t> g_used_devices{0};
+
 tvm_engine* tvm_engine_open(tvm_db* db, int device, char* err, size_t errlen) {
+  if (device >= 0 && device < 64) g_used_devices.fetch_or(uint64_t(1) << device);
   if (!db || !db->finalized) {
     set_err(err, errlen, "tvm_engine_open: DB not finalized");
     return nullptr;
@@ -340,10 +351,10 @@ tvm_engine* tvm_engine_open(tvm_db* db, int device, char* err, size_t errlen) {
 void tvm_engine_close(tvm_engine* e) { delete e; }
 
 void tvm_shutdown(void) {
-  // every device the process sees: drain whatever the library queued
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) == hipSuccess)
-    for (int d = 0; d < ndev; d++)
+  // every device an engine of this library ran on: drain whatever the library queued
+  const uint64_t used = g_used_devices.load();
+  for (int d = 0; d < 64; d++)
+    if ((used >> d) & 1u)
       if (hipSetDevice(d) == hipSuccess) (void)hipDeviceSynchronize();
   WorkerPool::shutdown_all();
   release_encoders();
@@ -613,41 +624,142 @@ int64_t tvm_batch_add_many_attrs(tvm_batch* b, tvm_engine* e, const char* bucket
   return first;
 }
 
-int64_t tvm_batch_add_targets(tvm_batch* b, tvm_engine* e, size_t n_targets, const tvm_str* buckets,
-                              const uint64_t* target_end, const char* arena, const uint64_t* name_off,
-                              const uint32_t* name_len, const uint64_t* ver_off, const uint32_t* ver_len) {
-  if (!b || !e || b->uploaded || b->pinned || (n_targets && (!buckets || !target_end)))
-    return -1;
+// Many targets in one call, built on the host threads (pkg/scanner/local/scan.go:170-194 hands
+// packages over per target; a fleet batch holds thousands of targets): a pass over the
+// packages sums each piece's string bytes (and checks the CPE-set ids), one scan places the
+// pieces, then every piece writes its package words, string bytes, group offsets and
+// attributes straight into the batch arrays, sized once (BulkVec: no zero fill first).
+static int64_t add_targets_bulk(tvm_batch* b, tvm_engine* e, size_t n_targets, const tvm_str* buckets,
+                                const uint32_t* tflags, const uint64_t* target_end, const char* arena,
+                                const uint64_t* name_off, const uint32_t* name_len, const uint64_t* ver_off,
+                                const uint32_t* ver_len, const tvm_attr_cols* cols) {
+  const uint32_t known = TVM_ATTR_ARCH | TVM_ATTR_KSPLICE | TVM_ATTR_CPESET;
+  if (!b || !e || b->uploaded || b->pinned || (n_targets && (!buckets || !target_end))) return -1;
   const uint64_t n = n_targets ? target_end[n_targets - 1] : 0;
   if (n && (!arena || !name_off || !name_len || !ver_off || !ver_len)) return -1;
-  for (size_t t = 0; t < n_targets; t++)
+  uint32_t any_flags = 0;
+  for (size_t t = 0; t < n_targets; t++) {
     if (t && target_end[t] < target_end[t - 1]) return -1;
+    const uint32_t f = tflags ? tflags[t] : 0u;
+    if ((f & ~known) || ((f & TVM_ATTR_KSPLICE) && (f & TVM_ATTR_CPESET))) return -1;  // one attribute word
+    any_flags |= f;
+  }
+  if (((any_flags & TVM_ATTR_ARCH) && (!cols || !cols->arch_off || !cols->arch_len)) ||
+      ((any_flags & TVM_ATTR_CPESET) && (!cols || !cols->cpe_set)))
+    return -1;
   std::shared_lock<std::shared_mutex> lk(e->mu);
   if (!bind(b, e)) return -1;
   const DB& db = e->eng->db();
   HostBatch& hb = b->hb;
-  const int64_t first = int64_t(hb.pk.size());
-  uint64_t bytes = 0;
-  for (uint64_t i = 0; i < n; i++)
-    bytes += std::min<uint32_t>(name_len[i], 0xFFFF) + std::min<uint32_t>(ver_len[i], 0xFFFF);
-  reserve_more(hb, n);
-  hb.arena.reserve(hb.arena.size() + bytes);
-  hb.tile_off.reserve(hb.tile_off.size() + n / kGroup + 2);
+  const uint64_t s0 = hb.pk.size(), a0 = hb.arena.size();
+  if (s0 + n >= (uint64_t(1) << 32)) return -1;  // package indices are 32-bit
+  // per target: its platform (a fleet's targets repeat a few buckets)
+  std::vector<uint32_t> pid(n_targets);
   std::string_view last_bucket;
-  uint32_t pid = 0xFFFFFFFFu;
-  uint64_t i = 0;
+  uint32_t last_pid = 0xFFFFFFFFu;
   for (size_t t = 0; t < n_targets; t++) {
     const std::string_view bk = sv(buckets[t]);
-    if (t == 0 || bk != last_bucket) {  // a fleet's targets repeat a few platform buckets
+    if (t == 0 || bk != last_bucket) {
       const int32_t plat = db.find_plat(bk);
-      pid = plat < 0 ? 0xFFFFFFFFu : uint32_t(plat);
+      last_pid = plat < 0 ? 0xFFFFFFFFu : uint32_t(plat);
       last_bucket = bk;
     }
-    b->target_begin.push_back(uint32_t(hb.pk.size()));
-    for (; i < target_end[t]; i++)
-      hb.add(pid, std::string_view(arena + name_off[i], name_len[i]), std::string_view(arena + ver_off[i], ver_len[i]));
+    pid[t] = last_pid;
   }
-  return first;
+  const size_t n_sets = hb.cpe_words ? hb.cpe_bits.size() / hb.cpe_words : 0;
+  WorkerPool& wp = WorkerPool::get();
+  const size_t K = n ? std::min<size_t>(size_t(wp.size()) * 8, std::max<uint64_t>(1, n / 4096)) : 0;
+  auto piece = [&](size_t k) { return std::make_pair(n * k / K, n * (k + 1) / K); };
+  auto target_of = [&](uint64_t j) {  // the target holding new package j
+    return size_t(std::upper_bound(target_end, target_end + n_targets, j) - target_end);
+  };
+  std::vector<uint64_t> bytes(K + 1, 0);
+  std::atomic<bool> bad{false};
+  wp.parallel_for(K, [&](size_t k) {
+    const auto [j0, j1] = piece(k);
+    uint64_t s = 0;
+    size_t t = target_of(j0);
+    for (uint64_t j = j0; j < j1; j++) {
+      while (target_end[t] <= j) t++;
+      s += std::min<uint32_t>(name_len[j], 0xFFFF) + std::min<uint32_t>(ver_len[j], 0xFFFF);
+      if (tflags && (tflags[t] & TVM_ATTR_CPESET) && cols->cpe_set[j] >= n_sets) bad.store(true);
+    }
+    bytes[k + 1] = s;
+  });
+  if (bad.load()) return -1;
+  for (size_t k = 0; k < K; k++) bytes[k + 1] += bytes[k];
+  const bool with_attr = any_flags || !hb.attr.empty();
+  const uint2 no_attr = make_uint2(PA_ARCH_NONE, 0xFFFFFFFFu);
+  try {
+    hb.pk.resize(s0 + n);
+    hb.arena.resize(a0 + (K ? bytes[K] : 0));
+    hb.tile_off.resize((s0 + n + kGroup - 1) / kGroup);
+    if (with_attr) {
+      if (hb.attr.size() < s0) hb.attr.resize(s0, no_attr);
+      hb.attr.resize(s0 + n);
+    }
+  } catch (const std::bad_alloc&) {
+    hb.pk.resize(s0);
+    hb.arena.resize(a0);
+    hb.tile_off.resize((s0 + kGroup - 1) / kGroup);
+    if (with_attr) hb.attr.resize(std::min<size_t>(hb.attr.size(), s0));
+    return -1;
+  }
+  wp.parallel_for(K, [&](size_t k) {
+    const auto [j0, j1] = piece(k);
+    uint64_t o = a0 + bytes[k];
+    size_t t = target_of(j0);
+    std::string_view last_arch;
+    uint32_t last_arch_id = PA_ARCH_NONE;
+    bool have_arch = false;
+    uint8_t* ar = hb.arena.data();
+    for (uint64_t j = j0; j < j1; j++) {
+      while (target_end[t] <= j) t++;
+      const uint64_t i = s0 + j;
+      const uint32_t nl = std::min<uint32_t>(name_len[j], 0xFFFF), vl = std::min<uint32_t>(ver_len[j], 0xFFFF);
+      if (i % kGroup == 0) hb.tile_off[i / kGroup] = o;
+      hb.pk[i] = make_uint2(pid[t], nl | (vl << 16));
+      std::memcpy(ar + o, arena + name_off[j], nl);
+      std::memcpy(ar + o + nl, arena + ver_off[j], vl);
+      o += nl + vl;
+      if (!with_attr) continue;
+      const uint32_t f = tflags ? tflags[t] : 0u;
+      uint2 a = no_attr;
+      if (f & TVM_ATTR_ARCH) {
+        const std::string_view arch(arena + cols->arch_off[j], cols->arch_len[j]);
+        if (!have_arch || arch != last_arch) {  // packages of an image share a few arches
+          last_arch_id = db.arch_id(arch) | (arch == "noarch" ? PA_NOARCH : 0u);  // redhat.go:129
+          last_arch = arch;
+          have_arch = true;
+        }
+        a.x = last_arch_id;
+      }
+      if (f & TVM_ATTR_KSPLICE) {
+        const std::string_view ver(arena + ver_off[j], ver_len[j]);
+        const size_t dash = ver.find('-');  // release = text after the first '-' (rpm split, rpm.c)
+        a.y = db.ksplice_id(extract_ksplice(dash == std::string_view::npos ? std::string_view() : ver.substr(dash + 1)));
+      }
+      if (f & TVM_ATTR_CPESET) a.y = cols->cpe_set[j];
+      hb.attr[i] = a;
+    }
+  });
+  for (size_t t = 0; t < n_targets; t++) b->target_begin.push_back(uint32_t(s0 + (t ? target_end[t - 1] : 0)));
+  return int64_t(s0);
+}
+
+int64_t tvm_batch_add_targets(tvm_batch* b, tvm_engine* e, size_t n_targets, const tvm_str* buckets,
+                              const uint64_t* target_end, const char* arena, const uint64_t* name_off,
+                              const uint32_t* name_len, const uint64_t* ver_off, const uint32_t* ver_len) {
+  return add_targets_bulk(b, e, n_targets, buckets, nullptr, target_end, arena, name_off, name_len, ver_off, ver_len,
+                          nullptr);
+}
+
+int64_t tvm_batch_add_targets_attrs(tvm_batch* b, tvm_engine* e, size_t n_targets, const tvm_str* buckets,
+                                    const uint32_t* target_flags, const uint64_t* target_end, const char* arena,
+                                    const uint64_t* name_off, const uint32_t* name_len, const uint64_t* ver_off,
+                                    const uint32_t* ver_len, const tvm_attr_cols* attrs) {
+  return add_targets_bulk(b, e, n_targets, buckets, target_flags, target_end, arena, name_off, name_len, ver_off,
+                          ver_len, attrs);
 }
 
 int64_t tvm_batch_size(const tvm_batch* b) { return b ? int64_t(b->hb.pk.size()) : 0; }
@@ -1431,6 +1543,8 @@ int tvm_pipeline_prepare(tvm_engine* e, tvm_batch* b, uint64_t match_cap, uint32
   }
   b->pipe.reset(new Pipeline());
   b->pipe_total = 0;  // no valid pass of the new pipeline yet
+  b->pipe_ok = false;
+  b->pipe_rh.forget_tiles();
   b->pipe_wide_for = ~0ull;
   std::string msg;
   const bool packed = !(flags & TVM_PIPE_ADV32) && e->db->db.advs.size() < (1ull << 24);
@@ -1457,6 +1571,7 @@ int tvm_pipeline_run(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* 
   int64_t ep = -1;
   const auto t0 = std::chrono::steady_clock::now();
   b->pipe_total = 0;  // a failed pass leaves no result behind
+  b->pipe_ok = false;
   b->pipe_wide_for = ~0ull;
   const bool ok = b->pipe->run(*e->eng, b->hb, total, ep, bits, msg);
   const double dt = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1477,6 +1592,8 @@ int tvm_pipeline_run(tvm_engine* e, tvm_batch* b, uint64_t* n_matches, int64_t* 
     set_err(err, errlen, "tvm_pipeline_run: match buffer too small (prepare with match_cap >= n_matches)");
     return TVM_EINVAL;
   }
+  b->pipe_ok = true;
+  b->pipe_errp = ep;
   return TVM_OK;
 }
 
@@ -1527,7 +1644,7 @@ int tvm_wire_encode(size_t n, const uint32_t* plat, const char* arena, const uin
   for (uint32_t t = 0; t < n_tiles; t += chunk_tiles) bounds.push_back(t);
   bounds.push_back(n_tiles);
   if (n_tiles == 0) bounds = {0, 0};
-  std::vector<uint64_t> toff = hb.tile_off;
+  std::vector<uint64_t> toff(hb.tile_off.begin(), hb.tile_off.end());
   toff.resize(size_t(n_tiles) * kGroupsPerTile + 1, hb.arena.size());
   WireEncoder enc;
   std::string msg;
@@ -1567,6 +1684,22 @@ void tvm_pool_stats(uint64_t out[4]) {
 }
 
 void tvm_pool_trim(void) { pool_trim(); }
+
+int tvm_runtime_info(int* hip_runtime, int* hip_driver, char* path, size_t pathlen) {
+  int rt = 0, drv = 0;
+  // the HIP runtime THIS library's calls bind to: with a host process that loaded another
+  // libamdhip64.so.7 first (torch's bundled one), the dynamic linker hands that one to us too
+  const bool ok = hipRuntimeGetVersion(&rt) == hipSuccess;
+  (void)hipDriverGetVersion(&drv);
+  if (hip_runtime) *hip_runtime = rt;
+  if (hip_driver) *hip_driver = drv;
+  if (path && pathlen) {
+    Dl_info di{};
+    const char* where = dladdr(reinterpret_cast<void*>(&hipRuntimeGetVersion), &di) && di.dli_fname ? di.dli_fname : "";
+    std::snprintf(path, pathlen, "%s", where);
+  }
+  return ok ? TVM_OK : TVM_EDEVICE;
+}
 
 int tvm_pipeline_stats(tvm_batch* b, uint64_t out[5]) {
   if (!b || !b->pipe || !out) return TVM_EINVAL;
@@ -1629,6 +1762,21 @@ bool ensure_rh_rank(tvm_engine* e, std::string& err) {
   return true;
 }
 
+// Per tile of the batch: 1 = it holds Red Hat packages (the merge gives those a wave each).
+std::vector<uint8_t> rh_tile_flags(const HostBatch& hb, const DB& db, uint32_t n_tiles) {
+  const auto& pi = db.plat_info;
+  const size_t n = hb.pk.size();
+  std::vector<uint8_t> flags(n_tiles, 0);
+  range_for(flags.size(), 64, [&](size_t t0, size_t t1) {
+    for (size_t t = t0; t < t1; t++)
+      for (size_t p = t * kTile; p < std::min(n, (t + 1) * kTile) && !flags[t]; p++) {
+        const uint32_t plat = hb.pk[p].x;
+        flags[t] = plat < pi.size() && pi[plat].drv == DRV_REDHAT;
+      }
+  });
+  return flags;
+}
+
 RhInputs rh_inputs(tvm_engine* e, tvm_batch* b) {
   RhInputs in;
   in.pk = b->dev.pk;
@@ -1646,19 +1794,8 @@ RhInputs rh_inputs(tvm_engine* e, tvm_batch* b) {
 bool rh_launch(tvm_engine* e, tvm_batch* b, std::string& err) {
   (void)hipSetDevice(e->device);
   if (!ensure_rh_rank(e, err)) return false;
-  if (!b->rh.tiles_known()) {  // once per upload: which tiles hold Red Hat packages
-    const auto& pi = e->eng->db().plat_info;
-    const size_t n = b->hb.pk.size();
-    std::vector<uint8_t> flags(b->dev.n_tiles, 0);
-    range_for(flags.size(), 64, [&](size_t t0, size_t t1) {
-      for (size_t t = t0; t < t1; t++)
-        for (size_t p = t * kTile; p < std::min(n, (t + 1) * kTile) && !flags[t]; p++) {
-          const uint32_t plat = b->hb.pk[p].x;
-          flags[t] = plat < pi.size() && pi[plat].drv == DRV_REDHAT;
-        }
-    });
-    if (!b->rh.set_tiles(flags, err)) return false;
-  }
+  if (!b->rh.tiles_known() && !b->rh.set_tiles(rh_tile_flags(b->hb, e->eng->db(), b->dev.n_tiles), err))
+    return false;  // once per upload: which tiles hold Red Hat packages
   const RhInputs in = rh_inputs(e, b);
   if (!b->rh.launch(in, e->eng->stream(), err)) return false;
   b->merged = true;
@@ -1850,67 +1987,21 @@ void set_out(tvm_db* d, VulnSetStore* st, const uint32_t* row_end, size_t n_pkgs
   out->priv = st;
 }
 
-}  // namespace
 
-int tvm_match_vulns(tvm_engine* e, tvm_batch* b, tvm_vuln_set* out, char* err, size_t errlen) {
-  if (!e || !b || !out || !b->uploaded) return TVM_EINVAL;
-  memset(out, 0, sizeof(*out));
-  std::shared_lock<std::shared_mutex> lk(e->mu);
-  if (!bind(b, e)) {
-    set_err(err, errlen, kStale);
-    return TVM_EINVAL;
-  }
+// The DetectedVulnerability set of a device match list `in` (raw, or Red Hat-merged): the
+// export's per-package record lists in pinned memory, and the records of the merged Red Hat
+// groups built on the host threads from their members' own records - the first member's (ID,
+// Status, Severity), the representative's FixedVersion, and VendorIDs: the first member's own
+// when it is the one fixed member, else the sorted union of the fixed members'
+// (ustrings.Unique; redhat.go:146-187) - as pointers into those records.
+bool export_set(tvm_engine* e, const ExportList& in, size_t n_pkgs, uint32_t first_pkg, tvm_vuln_set* out,
+                std::string& msg) {
   const DB& db = e->eng->db();
-  std::string msg;
-  (void)hipSetDevice(e->device);
-  // Red Hat packages report merged groups (redhat.go:146-187): the merge runs first
-  if (!b->merged && batch_has_redhat(b, db) && !rh_launch(e, b, msg)) {
-    set_err(err, errlen, "tvm_match_vulns: " + msg);
-    return TVM_EDEVICE;
-  }
-  uint64_t total = 0, bits = 0;
-  int64_t ep = -1;
-  if (match_status_locked(e, b, &total, &ep, &bits) != TVM_OK) {
-    set_err(err, errlen, "tvm_match_vulns: reading the match status failed");
-    return TVM_EDEVICE;
-  }
-  if (bits || ep >= 0 || total > cur(b).cap || b->m.ctl == nullptr) {
-    set_err(err, errlen, bits ? "tvm_match_vulns: match kernel internal error bits " + std::to_string(bits)
-                         : ep >= 0 ? "tvm_match_vulns: the batch met an undecodable advisory (package " +
-                                         std::to_string(ep) + ")"
-                                   : "tvm_match_vulns: the match buffer overflowed (upload with a larger cap)");
-    return TVM_EINVAL;
-  }
-  templates(e->db);  // built by the first export of a DB (outside a caller's timed calls)
+  const VulnTemplates& tp = templates(e->db);  // built by the first export of a DB
   auto st = std::make_unique<VulnSetStore>();
-  ExportList in;
-  in.list = cur(b);
-  in.total = total;
-  in.n_tiles = b->dev.n_tiles;
-  in.pkg_base = b->dev.pkg_base;
-  if (b->merged) {
-    const RhMerged& mg = b->rh.merged();
-    in.rh = true;
-    in.base = mg.base;
-    in.grp = mg.grp;
-    in.raw_adv = b->m.adv;
-    in.raw_cap = b->m.cap;
-    in.pk = b->dev.pk;
-    in.plats = e->eng->device_plats();
-    in.n_plats = uint32_t(db.plat_info.size());
-  }
-  const uint32_t n_adv = uint32_t(db.advs.size());
-  if (!export_vulns(e->device, e->eng->stream(), in, n_adv, st->ex, msg)) {
-    set_err(err, errlen, "tvm_match_vulns: " + msg);
-    return TVM_EDEVICE;
-  }
-  // the merged Red Hat groups' records (redhat.go:146-187) on the host threads, from the
-  // members' own records: the first member's (ID, Status, Severity), the representative's
-  // FixedVersion, and VendorIDs - the first member's own when it is the one fixed member, else
-  // the sorted union of the fixed members' (ustrings.Unique) - as pointers into those records
+  if (!export_vulns(e->device, e->eng->stream(), in, uint32_t(db.advs.size()), st->ex, msg)) return false;
   const VulnExport& ex = st->ex;
   if (ex.n_groups) {
-    const VulnTemplates& tp = templates(e->db);
     st->gc.resize(ex.n_groups);
     st->gvp.resize(ex.n_groups);
     pool_range_for(ex.n_groups, 1 << 10, [&](size_t a, size_t z) {
@@ -1945,28 +2036,142 @@ int tvm_match_vulns(tvm_engine* e, tvm_batch* b, tvm_vuln_set* out, char* err, s
     });
   }
   const VulnSetStore* sp = st.get();
-  set_out(e->db, st.release(), sp->ex.row_end_h, b->hb.pk.size(), b->dev.pkg_base, sp->ex.rec_h, sp->ex.width,
-          sp->ex.n, out);
-  return TVM_OK;
+  set_out(e->db, st.release(), sp->ex.row_end_h, n_pkgs, first_pkg, sp->ex.rec_h, sp->ex.width, sp->ex.n, out);
+  return true;
 }
 
-int tvm_pipeline_vulns(tvm_engine* e, tvm_batch* b, tvm_vuln_set* out, char* err, size_t errlen) {
-  if (!e || !b || !out || !b->pipe || b->pipe_total > b->pipe->cap()) return TVM_EINVAL;
+}  // namespace
+
+int tvm_match_vulns(tvm_engine* e, tvm_batch* b, tvm_vuln_set* out, char* err, size_t errlen) {
+  if (!e || !b || !out || !b->uploaded) return TVM_EINVAL;
   memset(out, 0, sizeof(*out));
   std::shared_lock<std::shared_mutex> lk(e->mu);
   if (!bind(b, e)) {
     set_err(err, errlen, kStale);
     return TVM_EINVAL;
   }
-  if (batch_has_redhat(b, e->eng->db())) {
-    set_err(err, errlen, "tvm_pipeline_vulns: Red Hat packages are merged per CVE on the device-resident path "
-                         "(tvm_batch_upload + tvm_match_launch + tvm_match_vulns)");
+  const DB& db = e->eng->db();
+  std::string msg;
+  (void)hipSetDevice(e->device);
+  // Red Hat packages report merged groups (redhat.go:146-187): the merge runs first
+  if (!b->merged && batch_has_redhat(b, db) && !rh_launch(e, b, msg)) {
+    set_err(err, errlen, "tvm_match_vulns: " + msg);
+    return TVM_EDEVICE;
+  }
+  uint64_t total = 0, bits = 0;
+  int64_t ep = -1;
+  if (match_status_locked(e, b, &total, &ep, &bits) != TVM_OK) {
+    set_err(err, errlen, "tvm_match_vulns: reading the match status failed");
+    return TVM_EDEVICE;
+  }
+  if (bits || ep >= 0 || total > cur(b).cap || b->m.ctl == nullptr) {
+    set_err(err, errlen, bits ? "tvm_match_vulns: match kernel internal error bits " + std::to_string(bits)
+                         : ep >= 0 ? "tvm_match_vulns: the batch met an undecodable advisory (package " +
+                                         std::to_string(ep) + ")"
+                                   : "tvm_match_vulns: the match buffer overflowed (upload with a larger cap)");
     return TVM_EINVAL;
   }
-  templates(e->db);
-  auto st = std::make_unique<VulnSetStore>();
-  set_out(e->db, st.release(), b->pipe->row_end(), b->hb.pk.size(), b->pkg_base,
-          reinterpret_cast<const uint8_t*>(b->pipe->adv()), b->pipe->packed() ? 3u : 4u, b->pipe_total, out);
+  ExportList in;
+  in.list = cur(b);
+  in.total = total;
+  in.n_tiles = b->dev.n_tiles;
+  in.pkg_base = b->dev.pkg_base;
+  if (b->merged) {
+    const RhMerged& mg = b->rh.merged();
+    in.rh = true;
+    in.base = mg.base;
+    in.grp = mg.grp;
+    in.raw_adv = b->m.adv;
+    in.raw_cap = b->m.cap;
+    in.pk = b->dev.pk;
+    in.plats = e->eng->device_plats();
+    in.n_plats = uint32_t(db.plat_info.size());
+  }
+  if (!export_set(e, in, b->hb.pk.size(), b->dev.pkg_base, out, msg)) {
+    set_err(err, errlen, "tvm_match_vulns: " + msg);
+    return TVM_EDEVICE;
+  }
+  return TVM_OK;
+}
+
+int tvm_pipeline_vulns(tvm_engine* e, tvm_batch* b, tvm_vuln_set* out, char* err, size_t errlen) {
+  if (!e || !b || !out) return TVM_EINVAL;
+  memset(out, 0, sizeof(*out));
+  if (!b->pipe || !b->pipe_ok || b->pipe_total > b->pipe->cap()) {
+    set_err(err, errlen, "tvm_pipeline_vulns: no completed tvm_pipeline_run on this batch");
+    return TVM_EINVAL;
+  }
+  std::shared_lock<std::shared_mutex> lk(e->mu);
+  if (!bind(b, e)) {
+    set_err(err, errlen, kStale);
+    return TVM_EINVAL;
+  }
+  if (b->pipe_errp >= 0) {
+    set_err(err, errlen, "tvm_pipeline_vulns: the batch met an undecodable advisory (package " +
+                             std::to_string(b->pipe_errp) + ")");
+    return TVM_EINVAL;
+  }
+  const DB& db = e->eng->db();
+  if (!batch_has_redhat(b, db)) {  // the lists the pass left in pinned memory ARE the set (no copy)
+    templates(e->db);
+    auto st = std::make_unique<VulnSetStore>();
+    set_out(e->db, st.release(), b->pipe->row_end(), b->hb.pk.size(), b->pkg_base,
+            reinterpret_cast<const uint8_t*>(b->pipe->adv()), b->pipe->packed() ? 3u : 4u, b->pipe_total, out);
+    return TVM_OK;
+  }
+  // Red Hat packages report merged groups (redhat.go:146-187): the pass's whole match list is
+  // still in HBM (Pipeline::matches), so the device merge and the export run over it as over a
+  // device-resident pass's list, and the set is the export's own copy
+  std::string msg;
+  (void)hipSetDevice(e->device);
+  const Pipeline& P = *b->pipe;
+  const DevBatch& dv = P.dev_batch();
+  hipStream_t st = e->eng->stream();
+  if (!ensure_rh_rank(e, msg) ||
+      (!b->pipe_rh.tiles_known() && !b->pipe_rh.set_tiles(rh_tile_flags(b->hb, db, dv.n_tiles), msg))) {
+    set_err(err, errlen, "tvm_pipeline_vulns: " + msg);
+    return TVM_EDEVICE;
+  }
+  RhInputs ri;
+  ri.pk = dv.pk;
+  ri.plats = e->eng->device_plats();
+  ri.n_plats = uint32_t(db.plat_info.size());
+  ri.raw = &P.matches();
+  ri.n_tiles = dv.n_tiles;
+  ri.n = dv.n;
+  ri.pkg_base = dv.pkg_base;
+  ri.rk = e->rh_rank;
+  unsigned long long mctl[8] = {};
+  if (!b->pipe_rh.launch(ri, st, msg) ||
+      hipMemcpyAsync(mctl, b->pipe_rh.merged().m.ctl, sizeof(mctl), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    set_err(err, errlen, "tvm_pipeline_vulns: " + (msg.empty() ? std::string("redhat merge failed") : msg));
+    return TVM_EDEVICE;
+  }
+  if (mctl[3] || mctl[0] > b->pipe_rh.merged().cap) {
+    set_err(err, errlen, (mctl[3] & ERR_RH_ORDER)
+                             ? "tvm_pipeline_vulns: a Red Hat package's advisories are not grouped by VulnerabilityID"
+                             : "tvm_pipeline_vulns: redhat merge error bits " + std::to_string(mctl[3]));
+    return TVM_EDEVICE;
+  }
+  const RhMerged& mg = b->pipe_rh.merged();
+  ExportList in;
+  in.list = mg.m;
+  in.total = mctl[0];
+  in.n_tiles = dv.n_tiles;
+  in.pkg_base = dv.pkg_base;
+  in.rh = true;
+  in.base = mg.base;
+  in.grp = mg.grp;
+  in.raw_adv = P.matches().adv;
+  in.raw_cap = P.matches().cap;
+  in.pk = dv.pk;
+  in.plats = e->eng->device_plats();
+  in.n_plats = uint32_t(db.plat_info.size());
+  if (!export_set(e, in, b->hb.pk.size(), b->pkg_base, out, msg)) {
+    set_err(err, errlen, "tvm_pipeline_vulns: " + msg);
+    return TVM_EDEVICE;
+  }
   return TVM_OK;
 }
 
@@ -1974,6 +2179,61 @@ void tvm_vuln_set_free(tvm_vuln_set* s) {
   if (!s) return;
   delete static_cast<VulnSetStore*>(s->priv);
   memset(s, 0, sizeof(*s));
+}
+
+int tvm_vuln_set_walk(const tvm_vuln_set* s, const tvm_batch* b, uint64_t* n_out, uint64_t* digest) {
+  if (!s || !b || (s->n_pkgs && !s->row_end) || (s->n && !s->rec) || s->n_pkgs > b->hb.pk.size() ||
+      (s->rec_width != 3 && s->rec_width != 4))
+    return TVM_EINVAL;
+  const size_t np = s->n_pkgs;
+  if (np && s->row_end[np - 1] != s->n) return TVM_EINVAL;
+  const HostBatch& hb = b->hb;
+  std::atomic<uint64_t> dsum{0}, cnt{0}, bad{0};
+  // pieces of whole 64-package groups: a group's first package offset is tile_off[g]
+  const size_t groups = (np + kGroup - 1) / kGroup;
+  pool_range_for(groups, 64, [&](size_t g0, size_t g1) {
+    uint64_t d = 0, c = 0, nb = 0;
+    for (size_t g = g0; g < g1; g++) {
+      uint64_t off = hb.tile_off[g];
+      for (size_t p = g * kGroup; p < std::min(np, (g + 1) * kGroup); p++) {
+        const uint32_t nl = hb.pk[p].y & 0xFFFFu, vl = hb.pk[p].y >> 16;
+        uint64_t ilen = vl;  // InstalledVersion: the report's override, else the batch version
+        if (p < b->rep_has[1].size() && b->rep_has[1][p]) ilen = b->rep[1][p].size();
+        else if (vl) (void)*static_cast<const volatile uint8_t*>(hb.arena.data() + off + nl);  // touched
+        off += nl + vl;
+        const uint64_t i0 = p ? s->row_end[p - 1] : 0, i1 = s->row_end[p];
+        const uint64_t pg = uint64_t(s->first_pkg) + p;
+        for (uint64_t i = i0; i < i1; i++) {
+          const uint8_t* q = s->rec + i * s->rec_width;
+          uint64_t r = uint64_t(q[0]) | uint64_t(q[1]) << 8 | uint64_t(q[2]) << 16;
+          if (s->rec_width == 4) r |= uint64_t(q[3]) << 24;
+          const tvm_vuln* v = r < s->n_adv_recs ? s->adv_recs + r
+                              : r - s->n_adv_recs < s->n_grp_recs ? s->grp_recs + (r - s->n_adv_recs) : nullptr;
+          if (!v) {
+            nb++;
+            continue;
+          }
+          const uint64_t id0 = v->vulnerability_id ? uint8_t(v->vulnerability_id[0]) : 0;
+          const uint64_t fl = v->fixed_version ? std::strlen(v->fixed_version) : 0;
+          uint64_t h = pg * 0x9E3779B97F4A7C15ull + r * 0xC2B2AE3D27D4EB4Full + (ilen << 40) + (id0 << 32) + fl;
+          h ^= h >> 33;
+          h *= 0xff51afd7ed558ccdull;
+          h ^= h >> 33;
+          h *= 0xc4ceb9fe1a85ec53ull;
+          h ^= h >> 33;
+          d += h;
+          c++;
+        }
+      }
+    }
+    dsum.fetch_add(d, std::memory_order_relaxed);
+    cnt.fetch_add(c, std::memory_order_relaxed);
+    bad.fetch_add(nb, std::memory_order_relaxed);
+  });
+  if (bad.load()) return TVM_EINVAL;  // a record index beyond the set's records
+  if (n_out) *n_out = cnt.load();
+  if (digest) *digest = dsum.load();
+  return TVM_OK;
 }
 
 int tvm_batch_report_get(const tvm_batch* b, uint64_t first, uint64_t n, tvm_str* names, tvm_str* versions,

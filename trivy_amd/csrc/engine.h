@@ -8,6 +8,7 @@
 #include <mutex>
 #include <string>
 #include <string_view>
+#include <utility>
 #include <vector>
 
 #include "common.h"
@@ -34,6 +35,31 @@ struct DevDB {
   const uint32_t* aux_ids = nullptr;
 };
 
+// Vector storage whose growth leaves new elements default-initialised (plain data: untouched)
+// rather than zeroed: the bulk adds (tvm_batch_add_targets) size the batch arrays once and fill
+// them on the host threads, so no serial zero fill runs first and every page is first touched
+// by the thread that writes it.
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInitAlloc<U>;
+  };
+  NoInitAlloc() = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
+};
+template <class T>
+using BulkVec = std::vector<T, NoInitAlloc<T>>;
+
 // A package batch.  pk[i] = {plat, name_len | ver_len << 16}; the name and version bytes
 // of every package sit back to back in `arena`, package after package, so offsets are
 // implicit: tile_off[g] is the arena offset of package g * kGroup (the kernels scan the
@@ -43,10 +69,10 @@ struct DevDB {
 // PA_NOARCH, ksplice tag or CPE-set id}; CPE set s is the bitset cpe_bits[s * cpe_words ..
 // +cpe_words) over CPE indices.
 struct HostBatch {
-  std::vector<uint2> pk;
-  std::vector<uint8_t> arena;
-  std::vector<uint64_t> tile_off;
-  std::vector<uint2> attr;
+  BulkVec<uint2> pk;
+  BulkVec<uint8_t> arena;
+  BulkVec<uint64_t> tile_off;
+  BulkVec<uint2> attr;
   std::vector<uint32_t> cpe_bits;
   uint32_t cpe_words = 0;
   void add(uint32_t plat, std::string_view name, std::string_view ver);

@@ -297,8 +297,14 @@ bool Engine::alloc_batch(const HostBatch& hb, DevBatch& b, std::string& err, boo
   // every batch owns its scratch: launches of different batches (pipeline streams, the
   // engine stream, other threads) never write the same words
   b.spill_cap = std::max<uint64_t>(b.spill_words, 64);
+  // test hook (tests/test_gpu_spill.py): TVM_TEST_SPILL_CAP words of usable scratch, so the
+  // failure path of a long key (ERR_SPILL, no rows for the package) can be exercised; the
+  // allocation itself keeps its size
+  const uint64_t alloc_words = b.spill_cap;
+  if (const char* cap = std::getenv("TVM_TEST_SPILL_CAP"))
+    b.spill_cap = std::min<uint64_t>(b.spill_cap, std::strtoull(cap, nullptr, 10));
   // +32 B tail: the kernels stage whole 16-byte lines and read names as dword triples
-  return dmalloc(&b.spill, b.spill_cap, "hipMalloc(batch scratch)", err, pd) &&
+  return dmalloc(&b.spill, alloc_words, "hipMalloc(batch scratch)", err, pd) &&
          dmalloc(&b.pk, hb.pk.size(), "hipMalloc(batch)", err, pd) &&
          dmalloc(&b.tile_off, size_t(b.n_tiles) * kGroupsPerTile + 1, "hipMalloc(group offsets)", err, pd) &&
          dmalloc(&b.arena, (hb.arena.size() + 32 + 15) & ~size_t(15), "hipMalloc(batch arena)", err, pd) &&
@@ -309,7 +315,7 @@ bool Engine::alloc_batch(const HostBatch& hb, DevBatch& b, std::string& err, boo
 
 bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
   if (!alloc_batch(hb, b, err)) return false;
-  std::vector<uint64_t> toff(hb.tile_off);  // + the arena end, then padded to whole tiles
+  std::vector<uint64_t> toff(hb.tile_off.begin(), hb.tile_off.end());  // + the arena end, then padded to whole tiles
   toff.resize(size_t(hb.n_tiles()) * kGroupsPerTile + 1, hb.arena.size());
   if (!hb.pk.empty() && !hip_ok(hipMemcpy(b.pk, hb.pk.data(), hb.pk.size() * sizeof(uint2), hipMemcpyHostToDevice),
                                 "H2D batch", err))
@@ -443,7 +449,7 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
   pa.rec = b.rec + p0;
   pa.tail = b.tail + p0;
   pa.ctl = m.ctl;
-  if (!b.spill || b.spill_cap < b.spill_words) {
+  if (!b.spill || (b.spill_cap < b.spill_words && !std::getenv("TVM_TEST_SPILL_CAP"))) {
     err = "batch scratch missing or smaller than the batch needs";
     return false;
   }
@@ -691,7 +697,7 @@ bool Engine::dropin_run(Dropin& d, DropinReq* const* reqs, size_t n, std::string
     at += bytes;
     return r;
   };
-  std::vector<uint64_t> toff(hb.tile_off);
+  std::vector<uint64_t> toff(hb.tile_off.begin(), hb.tile_off.end());
   toff.resize(groups, hb.arena.size());
   b.cpe_words = hb.cpe_words;
   b.n_cpe_sets = hb.cpe_words ? uint32_t(hb.cpe_bits.size() / hb.cpe_words) : 0;

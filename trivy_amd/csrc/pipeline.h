@@ -60,6 +60,10 @@ class Pipeline {
   uint64_t d2h_bytes() const { return d2h_; }
   uint32_t chunks() const { return uint32_t(bounds_.size() - 1); }
   bool transport_form() const { return !wc_.empty(); }
+  // The batch and the whole pass's match list as the pass left them in HBM (every chunk's
+  // segments, tile directory over all tiles): the Red Hat merge of a pipelined pass reads them
+  const DevBatch& dev_batch() const { return db_; }
+  const DevMatches& matches() const { return m_; }
   uint64_t encode_us() const { return encode_us_; }    // building the transport form (host threads)
   uint64_t prepare_us() const { return prepare_us_; }  // the whole prepare(), encode included
 

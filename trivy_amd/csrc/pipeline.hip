@@ -270,7 +270,7 @@ bool Pipeline::prepare(Engine& eng, const HostBatch& hb, uint64_t match_cap, uin
   }
   if (n_tiles == 0) bounds_ = {0, 0};
   const uint32_t nc = uint32_t(bounds_.size() - 1);
-  toff_ = hb.tile_off;  // per 64-package group, + the arena end, padded to whole tiles
+  toff_.assign(hb.tile_off.begin(), hb.tile_off.end());  // per 64-package group, + the arena end, padded to whole tiles
   toff_.resize(size_t(n_tiles) * kGroupsPerTile + 1, hb.arena.size());
   cap_ = std::max<uint64_t>(match_cap, 1);
   packed_ = packed;
