@@ -8,7 +8,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtrivy_amd.so")
+# TVM_LIB_PATH: another build of the same library - the sanitizer build (libtrivy_amd_san.so,
+# `make -C trivy_amd/csrc san`) that tools/san/run.sh loads into the CPU tests
+LIB_PATH = os.environ.get("TVM_LIB_PATH") or os.path.join(_HERE, "libtrivy_amd.so")
 
 TVM_OK, TVM_EDETECT, TVM_EUNSUPPORTED_OS, TVM_EINVAL, TVM_EDEVICE, TVM_EUNSUPPORTED_TYPE = 0, 1, 2, 3, 4, 5
 COPY_PKG_ID, COPY_PKG_NAME, COPY_IDENTIFIER, COPY_LAYER = 1, 2, 4, 8

@@ -585,7 +585,7 @@ std::string_view Arena::keep(std::string_view a, std::string_view b, std::string
     left = sz;
   }
   char* d = at;
-  std::memcpy(d, a.data(), a.size());
+  if (!a.empty()) std::memcpy(d, a.data(), a.size());  // (an empty view may have a null data(): UBSan, tools/san)
   if (!b.empty()) std::memcpy(d + a.size(), b.data(), b.size());
   if (!c.empty()) std::memcpy(d + a.size() + b.size(), c.data(), c.size());
   at += n;
