@@ -485,12 +485,13 @@ int tvm_pipeline_vulns(tvm_engine* e, tvm_batch* b, tvm_vuln_set* out, char* err
 void tvm_vuln_set_free(tvm_vuln_set* s);
 /* A consumer of a set, natively (INTEGRATION.md §3's loop on the host threads): every
  * DetectedVulnerability's record index decoded, its record resolved (adv_recs / grp_recs) and
- * read (VulnerabilityID, FixedVersion), its package's InstalledVersion located in the batch
- * (tvm_batch_report_get).  n_out = DetectedVulnerabilities walked; digest = the wrapping sum
- * over them of fmix64(p * 0x9E3779B97F4A7C15 + r * 0xC2B2AE3D27D4EB4F + (|InstalledVersion| << 40)
- * + (VulnerabilityID[0] << 32) + |FixedVersion|), p = first_pkg + the package's batch index, r =
- * the record index - what a caller's own loop over the set costs, and a check that it saw
- * every entry (bench.py end_to_end consume_ms). */
+ * its value fields read (the string pointers are handed on, as the loop copies the record), its
+ * package's InstalledVersion located in the batch (tvm_batch_report_get).  n_out =
+ * DetectedVulnerabilities walked; digest = the wrapping sum over them of fmix64(p *
+ * 0x9E3779B97F4A7C15 + r * 0xC2B2AE3D27D4EB4F + (|InstalledVersion| << 40) + (status << 32) +
+ * (n_vendor_ids << 24) + (has_data_source << 8) + copy_flags), each field's low byte, p =
+ * first_pkg + the package's batch index, r = the record index - what a caller's own loop over
+ * the set costs, and a check that it saw every entry (bench.py end_to_end consume_ms). */
 int tvm_vuln_set_walk(const tvm_vuln_set* s, const tvm_batch* b, uint64_t* n_out, uint64_t* digest);
 /* The package side of packages [first, first + n): names = the tvm_batch_set_report PkgName
  * (p = NULL: the caller's package Name), versions = InstalledVersion (the report's, else the

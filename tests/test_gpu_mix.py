@@ -17,8 +17,10 @@ pytestmark = pytest.mark.gpu
 # C4 (BASELINE config 4): the mixed batch - dpkg (Debian / Ubuntu), the Red Hat family
 # (Red Hat CPE sets + merge, Oracle ksplice, alma, rocky arches), Alpine and four lockfile
 # ecosystems interleaved in one launch of the all-grammar kernel
+# c3lean: C3 without Maven (go / npm / PEP 440): the GM_LEAN kernel alone; c3 / c4 run their
+# tiles without Maven packages on it too (Engine::launch's split launch)
 CFGS = {"c5": (sm.C5_PLATS, sm.C5_WEIGHTS, 3000), "c3": (sm.C3_PLATS, sm.C3_WEIGHTS, 5000),
-        "c4": (sm.C4_PLATS, sm.C4_WEIGHTS, 2500)}
+        "c4": (sm.C4_PLATS, sm.C4_WEIGHTS, 2500), "c3lean": (sm.C3_PLATS, [15, 0, 40, 25], 5000)}
 
 
 @pytest.mark.parametrize("cfg", list(CFGS))
@@ -98,7 +100,7 @@ def test_mix_variants_agree(cfg):
     batch = sm.make_mix_batch(sdb, 60_000, weights, seed=23)
     ref = None
     try:
-        for v in variants(grammar_set=4 if cfg in ("c3", "c4") else 2):
+        for v in variants(grammar_set={"c3": 4, "c4": 4, "c3lean": 8}.get(cfg, 2)):
             lib().tvm_engine_set_variant(eng.h, v)
             mb = MatchBatch(eng)
             sm.add_to(mb, sdb, batch)

@@ -125,7 +125,7 @@ def test_empty_batch(world):
 
 def variants(grammar_set=1):
     """Indices of the non-ablation match-kernel variants (engine.hip kVariants) built for the
-    grammar set (bit 0 dpkg-only, 1 OS grammars, 2 any)."""
+    grammar set (bit 0 dpkg-only, 1 OS grammars, 2 any, 3 GM_LEAN: library grammars without Maven / RubyGems)."""
     from trivy_amd._lib import lib
     out, v = [], 0
     while lib().tvm_variant_name(v):

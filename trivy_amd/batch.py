@@ -596,17 +596,15 @@ class VulnSet:
         base = int(self._c.first_pkg)
         vlen = np.array([len(v.encode()) for v in vers], dtype=np.uint64)
         uniq, inv = np.unique(self.rec, return_inverse=True)
-        id0 = np.zeros(len(uniq), np.uint64)
-        flen = np.zeros(len(uniq), np.uint64)
+        fl = np.zeros(len(uniq), np.uint64)
         for k, r in enumerate(uniq.tolist()):
             d = self.record(r)
-            id0[k] = d["VulnerabilityID"].encode()[0] if d["VulnerabilityID"] else 0
-            flen[k] = len(d.get("FixedVersion", "").encode())
+            fl[k] = ((d.get("Status", 0) & 0xFF) << 32 | (len(d.get("VendorIDs", [])) & 0xFF) << 24
+                     | (1 << 8 if "DataSource" in d else 0) | (d["_copy"] & 0xFF))
         with np.errstate(over="ignore"):
             p = self.pkg.astype(np.uint64)
             h = (p * np.uint64(0x9E3779B97F4A7C15) + self.rec.astype(np.uint64) * np.uint64(0xC2B2AE3D27D4EB4F)
-                 + (vlen[(p - np.uint64(base)).astype(np.int64)] << np.uint64(40)) + (id0[inv] << np.uint64(32))
-                 + flen[inv]) & M
+                 + (vlen[(p - np.uint64(base)).astype(np.int64)] << np.uint64(40)) + fl[inv]) & M
             for c in (0xff51afd7ed558ccd, 0xc4ceb9fe1a85ec53):
                 h ^= h >> np.uint64(33)
                 h *= np.uint64(c)

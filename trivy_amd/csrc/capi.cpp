@@ -2188,11 +2188,23 @@ int tvm_vuln_set_walk(const tvm_vuln_set* s, const tvm_batch* b, uint64_t* n_out
   const size_t np = s->n_pkgs;
   if (np && s->row_end[np - 1] != s->n) return TVM_EINVAL;
   const HostBatch& hb = b->hb;
+  const uint32_t W = s->rec_width;
+  auto rec_at = [&](uint64_t i) {
+    const uint8_t* q = s->rec + i * W;
+    uint64_t r = uint64_t(q[0]) | uint64_t(q[1]) << 8 | uint64_t(q[2]) << 16;
+    return W == 4 ? r | uint64_t(q[3]) << 24 : r;
+  };
+  auto vuln_of = [&](uint64_t r) -> const tvm_vuln* {
+    return r < s->n_adv_recs ? s->adv_recs + r
+           : r - s->n_adv_recs < s->n_grp_recs ? s->grp_recs + (r - s->n_adv_recs) : nullptr;
+  };
   std::atomic<uint64_t> dsum{0}, cnt{0}, bad{0};
   // pieces of whole 64-package groups: a group's first package offset is tile_off[g]
   const size_t groups = (np + kGroup - 1) / kGroup;
   pool_range_for(groups, 64, [&](size_t g0, size_t g1) {
     uint64_t d = 0, c = 0, nb = 0;
+    const uint64_t i_end = std::min<size_t>(np, g1 * kGroup) ? s->row_end[std::min<size_t>(np, g1 * kGroup) - 1] : 0;
+    constexpr uint64_t kAhead = 16;  // records are scattered over the DB's: their loads overlap
     for (size_t g = g0; g < g1; g++) {
       uint64_t off = hb.tile_off[g];
       for (size_t p = g * kGroup; p < std::min(np, (g + 1) * kGroup); p++) {
@@ -2204,18 +2216,19 @@ int tvm_vuln_set_walk(const tvm_vuln_set* s, const tvm_batch* b, uint64_t* n_out
         const uint64_t i0 = p ? s->row_end[p - 1] : 0, i1 = s->row_end[p];
         const uint64_t pg = uint64_t(s->first_pkg) + p;
         for (uint64_t i = i0; i < i1; i++) {
-          const uint8_t* q = s->rec + i * s->rec_width;
-          uint64_t r = uint64_t(q[0]) | uint64_t(q[1]) << 8 | uint64_t(q[2]) << 16;
-          if (s->rec_width == 4) r |= uint64_t(q[3]) << 24;
-          const tvm_vuln* v = r < s->n_adv_recs ? s->adv_recs + r
-                              : r - s->n_adv_recs < s->n_grp_recs ? s->grp_recs + (r - s->n_adv_recs) : nullptr;
+          if (i + kAhead < i_end)
+            if (const tvm_vuln* ahead = vuln_of(rec_at(i + kAhead))) __builtin_prefetch(ahead);
+          const uint64_t r = rec_at(i);
+          const tvm_vuln* v = vuln_of(r);
           if (!v) {
             nb++;
             continue;
           }
-          const uint64_t id0 = v->vulnerability_id ? uint8_t(v->vulnerability_id[0]) : 0;
-          const uint64_t fl = v->fixed_version ? std::strlen(v->fixed_version) : 0;
-          uint64_t h = pg * 0x9E3779B97F4A7C15ull + r * 0xC2B2AE3D27D4EB4Full + (ilen << 40) + (id0 << 32) + fl;
+          // the record's value fields as a caller's copy reads them (its string pointers are
+          // handed on, not dereferenced, as INTEGRATION.md §3's loop does)
+          const uint64_t fl = uint64_t(uint32_t(v->status) & 0xFFu) << 32 | uint64_t(v->n_vendor_ids & 0xFFu) << 24 |
+                              uint64_t(v->has_data_source & 1) << 8 | (v->copy_flags & 0xFFu);
+          uint64_t h = pg * 0x9E3779B97F4A7C15ull + r * 0xC2B2AE3D27D4EB4Full + (ilen << 40) + fl;
           h ^= h >> 33;
           h *= 0xff51afd7ed558ccdull;
           h ^= h >> 33;

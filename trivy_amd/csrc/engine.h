@@ -116,6 +116,10 @@ struct DevBatch {
   // the heaviest tiles first, so the launch does not end on a tail of Maven-program tiles);
   // nullptr = tile order
   uint32_t* tile_map = nullptr;
+  // batches of the all-grammar set: the first n_lean_tiles entries of tile_map are the tiles
+  // without Maven / RubyGems packages, matched by the GM_LEAN kernel in a launch of their own
+  // (Engine::launch); the rest take the all-grammar kernel
+  uint32_t n_lean_tiles = 0;
   // probe -> sweep hand-off (device only)
   PkgRec* rec = nullptr;
   uint4* tail = nullptr;  // key bytes 16..31 per package
@@ -392,9 +396,12 @@ class Engine {
   // behind event `ev` (the caller zeroes m.ctl once before the first chunk).
   // co: a previous chunk's result move, run by extra workgroups of this launch (fused
   // variants) or by its own kernel ahead of it (split variants).
+  // tmap / tmap_n / gm: (fused variants, whole batch) the launch's grid is tmap_n workgroups
+  // over the tiles tmap lists, with the kernel of grammar set gm
   bool launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_begin, uint32_t t_end, hipStream_t probe_st,
                     hipStream_t sweep_st, hipEvent_t ev, std::string& err, const CopyOutArgs* co = nullptr,
-                    unsigned long long* ctl_zero = nullptr);
+                    unsigned long long* ctl_zero = nullptr, const uint32_t* tmap = nullptr, uint32_t tmap_n = 0,
+                    uint32_t gm = 0);
 
   // After the pass: the match list as {package, advisory} pairs in (package, advisory) order.
   static bool fetch_ordered(const DevMatches& m, uint32_t n_pkgs, uint64_t total, std::vector<uint2>& out,

@@ -31,6 +31,7 @@ const SweepFn* sweep_table(bool filt);
 const FusedFn* fused_table_DEB();
 const FusedFn* fused_table_OS();
 const FusedFn* fused_table_ALL();
+const FusedFn* fused_table_LEAN();
 
 namespace {
 
@@ -39,8 +40,13 @@ constexpr const char* kVariantNames[] = {
     TVM_MATCH_VARIANTS(TVM_NAME_)
 #undef TVM_NAME_
 };
-// Grammar-set index of a batch: 0 = dpkg only, 1 = OS grammars, 2 = any.
-int grammar_index(uint32_t gm) { return (gm & ~GM_DEB) == 0 ? 0 : (gm & ~GM_OS) == 0 ? 1 : 2; }
+// Grammar-set index of a batch: 0 = dpkg only, 1 = OS grammars, 2 = any, 3 = library grammars
+// without Maven / RubyGems (GM_LEAN; TVM_NO_LEAN=1: such batches take the all-grammar kernel,
+// for measurement).
+int grammar_index(uint32_t gm) {
+  static const bool no_lean = std::getenv("TVM_NO_LEAN") != nullptr;
+  return (gm & ~GM_DEB) == 0 ? 0 : (gm & ~GM_OS) == 0 ? 1 : ((gm & ~GM_LEAN) == 0 && !no_lean) ? 3 : 2;
+}
 constexpr int kNumVariants = 1 + kNumTuned;
 constexpr bool kFusedVariant[] = {
 #define TVM_F_(F, K, MB, NAME) F != 0,
@@ -52,6 +58,7 @@ FusedFn fused_fn(uint32_t gm, int vi) {
   switch (grammar_index(gm)) {
     case 0: return fused_table_DEB()[vi - 1];
     case 1: return fused_table_OS()[vi - 1];
+    case 3: return fused_table_LEAN()[vi - 1];
     default: return fused_table_ALL()[vi - 1];
   }
 }
@@ -116,12 +123,14 @@ const char* variant_name(int v) {
   if (v == 0) return "auto";
   return v > 0 && v < kNumVariants ? kVariantNames[v - 1] : nullptr;
 }
-// Grammar sets variant v is built for: bit 0 dpkg-only, bit 1 OS grammars, bit 2 all grammars.
+// Grammar sets variant v is built for: bit 0 dpkg-only, bit 1 OS grammars, bit 2 all grammars,
+// bit 3 GM_LEAN.
 int variant_grammar_sets(int v) {
-  if (v == 0) return 7;
+  if (v == 0) return 15;
   if (v < 0 || v >= kNumVariants) return 0;
-  if (!kFusedVariant[v - 1]) return 7;
-  return (fused_table_DEB()[v - 1] ? 1 : 0) | (fused_table_OS()[v - 1] ? 2 : 0) | (fused_table_ALL()[v - 1] ? 4 : 0);
+  if (!kFusedVariant[v - 1]) return 15;
+  return (fused_table_DEB()[v - 1] ? 1 : 0) | (fused_table_OS()[v - 1] ? 2 : 0) | (fused_table_ALL()[v - 1] ? 4 : 0) |
+         (fused_table_LEAN()[v - 1] ? 8 : 0);
 }
 
 // "auto": per grammar set, the fastest variant of bench.py --sweep on MI355X:
@@ -130,7 +139,7 @@ int variant_grammar_sets(int v) {
 int resolve_variant(int v, uint32_t gm) {
   if (v != 0) return v;
   const int gi = grammar_index(gm);
-  return 1 + (gi == 0 ? kAutoVariant : gi == 1 ? kAutoVariantOS : kAutoVariantFiltered);
+  return 1 + (gi == 0 ? kAutoVariant : gi == 1 ? kAutoVariantOS : gi == 3 ? kAutoVariantLean : kAutoVariantFiltered);
 }
 
 // ---- Engine -----------------------------------------------------------------------------------
@@ -298,9 +307,27 @@ bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
         w[t] = s;
       }
     });
+    // all-grammar batches: the tiles without Maven / RubyGems packages first (their own launch
+    // on the GM_LEAN kernel, Engine::launch), each part heaviest first
+    std::vector<uint8_t> full(b.n_tiles, 1);
+    static const bool no_lean = std::getenv("TVM_NO_LEAN") != nullptr;
+    if (grammar_index(b.gm) == 2 && !no_lean)
+      range_for(b.n_tiles, 64, [&](size_t t0, size_t t1) {
+        for (size_t t = t0; t < t1; t++) {
+          bool f = false;
+          for (size_t p = t * kTile; p < std::min(hb.pk.size(), (t + 1) * kTile) && !f; p++) {
+            const uint32_t plat = hb.pk[p].x;
+            f = plat < pi.size() && ((GM_LEAN >> pi[plat].cmp) & 1u) == 0;
+          }
+          full[t] = f;
+        }
+      });
     std::vector<uint32_t> order(b.n_tiles);
     for (uint32_t t = 0; t < b.n_tiles; t++) order[t] = t;
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return w[x] > w[y]; });
+    std::stable_sort(order.begin(), order.end(),
+                     [&](uint32_t x, uint32_t y) { return full[x] != full[y] ? full[x] < full[y] : w[x] > w[y]; });
+    b.n_lean_tiles = 0;
+    for (uint32_t t = 0; t < b.n_tiles; t++) b.n_lean_tiles += full[t] ? 0 : 1;
     if (!dmalloc(&b.tile_map, order.size(), "hipMalloc(tile order)", err) ||
         !hip_ok(hipMemcpy(b.tile_map, order.data(), order.size() * 4, hipMemcpyHostToDevice), "H2D tile order", err))
       return false;
@@ -373,7 +400,7 @@ bool Engine::fetch_ordered(const DevMatches& m, uint32_t n_pkgs, uint64_t total,
 
 bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_begin, uint32_t t_end, hipStream_t pst,
                           hipStream_t sst, hipEvent_t ev, std::string& err, const CopyOutArgs* co,
-                          unsigned long long* ctl_zero) {
+                          unsigned long long* ctl_zero, const uint32_t* tmap, uint32_t tmap_n, uint32_t gm) {
   (void)hipSetDevice(dev_);
   if (t_end > b.n_tiles) t_end = b.n_tiles;
   if (t_begin >= t_end) return true;
@@ -381,7 +408,12 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
     err = "tile directory smaller than the batch";
     return false;
   }
-  const int vi = resolve_variant(variant_, b.gm);
+  if (!gm) gm = b.gm;
+  const int vi = resolve_variant(variant_, gm);
+  if (tmap && (co || t_begin != 0 || t_end != b.n_tiles || !kFusedVariant[vi - 1] || tmap_n == 0)) {
+    err = "a tile-list launch is a fused pass over the whole batch";
+    return false;
+  }
   last_launched_ = vi;
   const uint32_t nt = t_end - t_begin;
   const uint32_t p0 = t_begin * kTile;
@@ -451,14 +483,14 @@ bool Engine::launch_tiles(const DevBatch& b, const DevMatches& m, uint32_t t_beg
       }();
       fa.n_copy = n_copy;
     }
-    if (!co && t_begin == 0 && t_end == b.n_tiles) fa.tile_map = b.tile_map;
+    if (!co && t_begin == 0 && t_end == b.n_tiles) fa.tile_map = tmap ? tmap : b.tile_map;
     fa.ctl_zero = co ? nullptr : ctl_zero;
-    const FusedFn fn = fused_fn(b.gm, vi);
+    const FusedFn fn = fused_fn(gm, vi);
     if (!fn) {
       err = std::string("match-path variant ") + kVariantNames[vi - 1] + " is not built for this batch's grammar set";
       return false;
     }
-    fn(nt, pst, fa);
+    fn(tmap ? tmap_n : nt, pst, fa);
     return hip_ok(hipGetLastError(), "match kernel launch", err);
   }
   const bool filt = (b.gm & ~GM_DEB) != 0;
@@ -478,7 +510,16 @@ bool Engine::launch(const DevBatch& b, DevMatches& m, hipStream_t st, std::strin
   if (b.n_tiles == 0)
     return !zero || hip_ok(hipMemsetAsync(zero, 0, 8 * sizeof(unsigned long long), st), "memset(ctl)", err);
   // one launch over every tile (cutting the pass into chunks whose probe overlaps the
-  // previous chunk's sweep on a second stream measured slower: DESIGN.md §4)
+  // previous chunk's sweep on a second stream measured slower: DESIGN.md §4) - or, for an
+  // all-grammar batch with tiles free of Maven / RubyGems packages, two: those tiles on the
+  // GM_LEAN kernel, then the rest on the all-grammar kernel (Engine::upload's tile_map order)
+  const uint32_t nl = b.n_lean_tiles;
+  if (nl && nl < b.n_tiles && b.tile_map && grammar_index(b.gm) == 2 && kFusedVariant[resolve_variant(variant_, b.gm) - 1] &&
+      kFusedVariant[resolve_variant(variant_, GM_LEAN) - 1]) {
+    return launch_tiles(b, m, 0, b.n_tiles, st, st, nullptr, err, nullptr, zero, b.tile_map, nl, GM_LEAN) &&
+           launch_tiles(b, m, 0, b.n_tiles, st, st, nullptr, err, nullptr, nullptr, b.tile_map + nl, b.n_tiles - nl,
+                        b.gm);
+  }
   return launch_tiles(b, m, 0, b.n_tiles, st, st, nullptr, err, nullptr, zero);
 }
 

@@ -1135,6 +1135,11 @@ enum : uint32_t {
   GM_DEB = 1u << CMP_DEB,
   GM_OS = GM_DEB | (1u << CMP_APK) | (1u << CMP_RPM),
   GM_ALL = 0x3FEu,
+  // every grammar but Maven and RubyGems: their parses (MvnParse, GemSeg arrays) and the Maven
+  // program evaluator are what put the all-grammar kernel at 96 VGPRs + ~800 B of scratch per
+  // lane; a kernel without them runs the lockfile ecosystems most tiles hold (go, npm, PEP 440,
+  // Bitnami) and the OS grammars
+  GM_LEAN = GM_ALL & ~((1u << CMP_MAVEN) | (1u << CMP_GEM)),
 };
 
 template <uint32_t GM, class Sink>

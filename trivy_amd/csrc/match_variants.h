@@ -49,3 +49,8 @@ constexpr int kAutoVariantFiltered = 1;  // fused_k2_m2048
 // OS grammar sets with row filters (rpm / apk: no library rows): per-wave staging + segments
 // at 6 waves, K = 2 (round 5 sweep, profiles/r05/sweep_c5.txt: C5 2.317 -> 2.283 ms)
 constexpr int kAutoVariantOS = 7;        // fused_k2_m2400_wseg6
+// library grammar sets without Maven / RubyGems (GM_LEAN): per-wave staging + segments at 6
+// waves, K = 2, as the OS set (round 6 sweep, go / npm / PEP 440 at 1M packages: fused K = 2
+// 0.1354 ms, wseg6 K = 2 0.1333, K = 3 0.1331; the all-grammar kernel 0.149;
+// profiles/r06/lean_ab/)
+constexpr int kAutoVariantLean = 7;  // fused_k2_m2400_wseg6
