@@ -307,7 +307,11 @@ int tvm_version_class(int grammar, const char* s, size_t n);
 int tvm_deb_fast_key_host(const char* s, size_t n, uint32_t shift, uint8_t* out, size_t cap);
 /* Host-side compare.IsVulnerable through the load-time interval compiler (tests): 1/0, -1
  * when the advisory JSON does not decode.  Maven: the rows the product builds - intervals for
- * an advisory whose bounds are all numeric, else the pairwise program. */
+ * an advisory whose bounds are all numeric, else the pairwise program - so it mirrors the
+ * device rows and is not ground truth for numeric-bound advisories; grammar |
+ * TVM_ISVULN_PAIRWISE evaluates every Maven advisory with the pairwise ComparableVersion
+ * program instead (tests check the two against each other and against the oracle). */
+enum { TVM_ISVULN_PAIRWISE = 0x100 };
 int tvm_lib_is_vulnerable_host(int grammar, const char* ver, size_t ver_len, const char* advisory_json,
                                size_t json_len);
 /* Advisory fields for host-side inspection of batch results. */

@@ -163,9 +163,11 @@ def test_match_fill_batch_vs_oracle():
     mb.close()
 
 
-def _filter_fixture(seed=9):
+def _filter_fixture(seed=9, copies=0):
     """A multi-result batch with repeated (name, version) packages inside results, FillInfo
-    run, plus the oracle's view of every result's DetectedVulnerability list."""
+    run, plus the oracle's view of every result's DetectedVulnerability list.  copies: every
+    result also ends with that many more copies of its first three packages (duplicated
+    lockfile rows: dedup groups of hundreds of packages)."""
     import trivy_amd
     from trivy_amd._lib import lib
     from trivy_amd.batch import MatchBatch
@@ -182,7 +184,7 @@ def _filter_fixture(seed=9):
     # duplicate a quarter of every result's packages (same name and version) at its end
     plat, names, vers, targets = [], [], [], []
     for p, s, e in b0.targets:
-        idx = list(range(s, e)) + list(range(s, e, 4))
+        idx = list(range(s, e)) + list(range(s, e, 4)) + [s + (k % 3) for k in range(copies)]
         start = len(names)
         for i in idx:
             plat.append(p)
@@ -254,6 +256,32 @@ def test_match_filter_batch_vs_oracle(opts):
     # exact pairs: the dedup winner is the reference's first-seen package
     assert got == [list(w["_pair"]) for w in want]
     assert mb.ignored_findings().tolist() == want_ign and (not findings or want_ign)
+    mb.close()
+
+
+def test_match_filter_many_duplicates_vs_oracle():
+    """Dedup groups of ~170 packages per result (500 extra copies of three packages): the
+    kept pairs equal oracle/filter.py, and a call stays fast - a repeating package's pair scans
+    the other packages of its dedup key until one beats it, and copies with the same list are
+    beaten by the first copy (filter.hip beaten_by; O(K M log M) for K copies of M pairs)."""
+    import time
+
+    import oracle.filter as of
+    mb, bucket, by_target, sdb = _filter_fixture(seed=4, copies=500)
+    opts = mb.filter_opts()
+    n = mb.filter(opts)
+    got = mb.filtered_pairs(n).tolist()
+    want = []
+    for vulns in by_target:
+        filled = vi.fill_info(bucket, [{k: x for k, x in v.items() if k != "_pair"} for v in vulns])
+        for f, v in zip(filled, vulns):
+            f["_pair"] = v["_pair"]
+        kept, _ = of.filter_vulnerabilities("", filled, ["UNKNOWN", "LOW", "MEDIUM", "HIGH", "CRITICAL"])
+        want += kept or []
+    assert got == [list(w["_pair"]) for w in want] and len(got) > 1000
+    t0 = time.perf_counter()
+    ms = mb.filter_time(opts, 5)
+    assert ms < 50 and time.perf_counter() - t0 < 5, ms
     mb.close()
 
 

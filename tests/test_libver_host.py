@@ -294,3 +294,28 @@ def test_maven_non_transitive_pairs_exact(ver, adv):
     """The shapes where ComparableVersion is not an order evaluate exactly
     as the oracle's pairwise IsVulnerable (host run of the kernel's program evaluator)."""
     assert host_vuln("maven", ver, adv) == int(ol.is_vulnerable("maven", ver, adv))
+
+
+def test_maven_rows_equal_pairwise_program():
+    """tvm_lib_is_vulnerable_host mirrors the device rows (numeric-bound advisories: key-order
+    intervals over the installed version's numeric projection); with TVM_ISVULN_PAIRWISE it runs
+    ComparableVersion's pairwise program for every advisory.  The two agree on random shapes
+    against numeric-bound advisories, and the pairwise form agrees with the oracle, so the
+    projection rows are checked against an independent evaluator, not against themselves."""
+    import random
+
+    import oracle.library as ol
+    r = random.Random(17)
+    n = 0
+    for _ in range(3000):
+        b1, b2 = sorted([".".join(str(r.randint(0, 12)) for _ in range(r.randint(1, 4))) for _ in range(2)])
+        adv = {"VulnerableVersions": [f">= {b1}, < {b2}"], "PatchedVersions": [b2]}
+        v = gen_maven(r)
+        rows = host_vuln("maven", v, adv)
+        b, j = v.encode(), json.dumps(adv).encode()
+        pair = lib().tvm_lib_is_vulnerable_host(GRAMMAR["maven"] | 0x100, b, len(b), j, len(j))
+        want = ol.is_vulnerable("maven", v, adv)
+        assert rows == pair == int(want), (v, adv, rows, pair, want)
+        n += 1
+    assert n > 2000
+

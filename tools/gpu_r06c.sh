@@ -12,5 +12,7 @@ TVM_NO_LEAN=1 timeout -k 10 200 python bench.py --config c3 --steps 20 --no-cpu 
 timeout -k 10 300 python bench.py --config c4 --packages 12500000 --steps 10 --no-cpu --no-e2e --no-fill > $O/c4.json 2> $O/c4.err || exit 1
 TVM_NO_LEAN=1 timeout -k 10 300 python bench.py --config c4 --packages 12500000 --steps 10 --no-cpu --no-e2e --no-fill > $O/c4_nolean.json 2> $O/c4_nolean.err || exit 1
 timeout -k 10 400 python bench.py --config c5 --steps 10 --cpu-seconds 4 > $O/c5.json 2> $O/c5.err || exit 1
+# measurement only: every row filter passing (libtrivy_amd_exp.so, TVM_EXP_NOAUX) - the filters' share of C5
+TVM_LIB_PATH=$R/trivy_amd/libtrivy_amd_exp.so timeout -k 10 300 python bench.py --config c5 --steps 10 --no-cpu --no-e2e --no-fill > $O/c5_noaux.json 2> $O/c5_noaux.err || exit 1
 for f in $O/*.json; do python -c "import json;d=json.loads(open('$f').read().strip().splitlines()[-1]);print('$f', d['roofline']['kernel_ms'], d['config']['kernel_variant'], round(d['roofline']['frac'],3))"; done
 echo done

@@ -999,8 +999,17 @@ uint64_t tvm_match_algorithmic_bytes(tvm_engine* e, tvm_batch* b) {
     for (uint64_t i = h & db.slot_mask; db.slot_hash[i]; i = (i + 1) & db.slot_mask) {
       if (db.slot_key[i] != uint32_t(k)) continue;
       const SlotVal& v = db.slot_val[i];
-      for (uint32_t r = 0; r < v.row_count; r++) {
-        const Row& row = db.rows[v.row_begin + r];
+      uint32_t cls = 0;  // a split key: the rows of the version's class (common.h SLOT_CLS_SPLIT)
+      if (v.name_len & SLOT_CLS_SPLIT) {
+        struct Sink {
+          void put(uint8_t) {}
+        } sk;
+        const char* ver = name.data() + nlen;
+        if (!encode_version_cls(db.plat_info[d.x].cmp, reinterpret_cast<const uint8_t*>(ver), vlen, sk, cls)) cls = 0;
+      }
+      const uint2 rr = slot_rows(v.name_len, v.row_begin, v.row_count, cls);
+      for (uint32_t r = 0; r < rr.y; r++) {
+        const Row& row = db.rows[rr.x + r];
         bytes += sizeof(Row);  // 16 B header + 16 B inline hi-key prefix
         if (!(row.hi_len & KEY_INF) && (row.hi_len & KEY_LEN_MASK) > 16) bytes += (row.hi_len & KEY_LEN_MASK) - 16;
         if (!(row.lo_len & KEY_INF)) bytes += row.lo_len & KEY_LEN_MASK;
@@ -1061,8 +1070,11 @@ int tvm_lib_is_vulnerable_host(int grammar, const char* ver, size_t ver_len, con
   std::string e;
   if (!ver || !advisory_json || !decode_advisory(std::string_view(advisory_json, json_len), a, e)) return -1;
   // Maven: the rows DB::compile_rows builds - intervals over the numeric projection for an
-  // advisory with numeric bounds, else the pairwise program
-  if (grammar == CMP_MAVEN && !mvn_hybrid(a.vulnerable, a.patched, a.unaffected))
+  // advisory with numeric bounds, else the pairwise program; TVM_ISVULN_PAIRWISE: always the
+  // pairwise program (ComparableVersion itself, the device's rows aside)
+  const bool pairwise = (grammar & TVM_ISVULN_PAIRWISE) != 0;
+  grammar &= ~TVM_ISVULN_PAIRWISE;
+  if (grammar == CMP_MAVEN && (pairwise || !mvn_hybrid(a.vulnerable, a.patched, a.unaffected)))
     return mvn_is_vulnerable(a.vulnerable, a.patched, a.unaffected, std::string(ver, ver_len));
   const LibRows r = lib_compile_advisory(uint8_t(grammar), a.vulnerable, a.patched, a.unaffected);
   return lib_rows_contain(uint8_t(grammar), r, std::string(ver, ver_len)) ? 1 : 0;

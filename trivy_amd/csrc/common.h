@@ -80,8 +80,17 @@ enum : uint16_t {
 enum : uint32_t {
   ROW_ALWAYS = 1u << 31, // in Row::adv: matches even when the installed version fails to parse
   ROW_FILTER = 1u << 30, // in Row::adv: also test the package against RowAux (arch / CPE / tag)
-  ROW_ADV_MASK = 0x3FFFFFFFu,
+  ROW_INLINE = 1u << 29, // in Row::adv (with ROW_FILTER): the predicates sit in the row itself (below)
+  ROW_ADV_MASK = 0x1FFFFFFFu,
 };
+// ROW_INLINE: an rpm-grammar row (only an upper bound: its lo_len is KEY_INF, its key offsets
+// live in DB::row_off) whose filter fits the row carries it in place of the offsets, so the
+// sweep tests it without the RowAux -> id-list chain of dependent loads:
+//   lo_len = KEY_INF | AUX kind bits (ARCH_RH / ARCH_IN / CPE / TAG, low 4 bits) | n_arch << 4 |
+//            n_cpe << 6 (2 bits each);
+//   off    = AUX_TAG: lo_off = the ksplice tag; else four 16-bit ids, the arch ids then the CPE
+//            indices (n_arch + n_cpe <= 4, every id < 0xFFFF).
+constexpr uint32_t kInlineIds = 4;
 
 // Per-(package, advisory) predicates beyond the version interval, read only for rows
 // flagged ROW_FILTER (rows[] and aux[] are parallel arrays):
@@ -127,7 +136,21 @@ struct alignas(16) SlotVal {
 // of class 0 / 1: the probe packs a Maven package's parse only then.  Maven has one class
 // since the numeric projection (libver.h mvn_numeric_projection), and program rows carry no
 // class filter, so both bits are set together.
-enum : uint32_t { SLOT_POISONED = 1u << 31, SLOT_MVN_C0 = 1u << 30, SLOT_MVN_C1 = 1u << 29, SLOT_LEN_MASK = 0x1FFFFFFFu };
+// SLOT_CLS_SPLIT: a library key whose rows differ by version class (PEP 440 local / pre / post,
+// npm pre-release: AUX_CLASS rows) keeps two lists back to back - A, the rows that admit class
+// 0 (the plain release versions most packages have), without their class filter, then B, every
+// row in advisory order as before - and row_count = |A| | |B| << 16: a class-0 package sweeps
+// [row_begin, row_begin + |A|), any other [row_begin + |A|, + |B|), each in advisory order.
+enum : uint32_t {
+  SLOT_POISONED = 1u << 31, SLOT_MVN_C0 = 1u << 30, SLOT_MVN_C1 = 1u << 29, SLOT_CLS_SPLIT = 1u << 28,
+  SLOT_LEN_MASK = 0x0FFFFFFFu
+};
+// The rows a package of version class cls sweeps: {begin, count} of a slot's row range.
+TVM_HD uint2 slot_rows(uint32_t name_len, uint32_t row_begin, uint32_t row_count, uint32_t cls) {
+  if (!(name_len & SLOT_CLS_SPLIT)) return make_uint2(row_begin, row_count);
+  const uint32_t na = row_count & 0xFFFFu;
+  return cls == 0 ? make_uint2(row_begin, na) : make_uint2(row_begin + na, row_count >> 16);
+}
 // Device hash slot: one 64-B cache line holding the hash, the row range and the first
 // kSlotNameWords*8 bytes of the name (memory order, zero padded), so a probe verifies the
 // name from the same line it read the hash from; longer names finish against the name

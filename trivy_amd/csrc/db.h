@@ -131,6 +131,9 @@ class DB {
   void flatten_os(uint32_t plat, const Bucket& b, int32_t ds);
   void flatten_library(uint32_t plat, const std::vector<std::pair<const Bucket*, int32_t>>& roots);
   bool compile_rows(const Platform& P, const Advisory& a, uint32_t ai, std::vector<uint8_t>& kb);
+  static constexpr uint32_t kRowSplit = 1u << 31;  // split_by_class's mark on a packed count
+  static constexpr uint32_t kRowsPerLine = 4;       // 32-B rows per 128-B line (a key's run starts on one)
+  void split_by_class(const Platform& P, uint32_t row_begin, uint32_t& row_count);
   void build_index();
 };
 

@@ -511,11 +511,17 @@ bool Engine::launch(const DevBatch& b, DevMatches& m, hipStream_t st, std::strin
     return !zero || hip_ok(hipMemsetAsync(zero, 0, 8 * sizeof(unsigned long long), st), "memset(ctl)", err);
   // one launch over every tile (cutting the pass into chunks whose probe overlaps the
   // previous chunk's sweep on a second stream measured slower: DESIGN.md §4) - or, for an
-  // all-grammar batch with tiles free of Maven / RubyGems packages, two: those tiles on the
-  // GM_LEAN kernel, then the rest on the all-grammar kernel (Engine::upload's tile_map order)
+  // all-grammar batch whose tiles are nearly all free of Maven / RubyGems packages (at most 1
+  // in kSplitFull needs the all-grammar kernel), two back to back: those tiles on the GM_LEAN
+  // kernel, then the rest (Engine::upload's tile_map order: lean tiles first, each part
+  // heaviest first).  The second launch starts when the first has drained (kernels on two
+  // streams did not overlap on this runtime either), so the split pays when the all-grammar
+  // part is small: C4's 12.5M share (8 % Maven tiles) 1.554 -> 1.508 ms; C3 (20 %) 0.156 ->
+  // 0.169 ms, which therefore stays one launch (profiles/r06/lean_ab/)
+  constexpr uint32_t kSplitFull = 10;
   const uint32_t nl = b.n_lean_tiles;
-  if (nl && nl < b.n_tiles && b.tile_map && grammar_index(b.gm) == 2 && kFusedVariant[resolve_variant(variant_, b.gm) - 1] &&
-      kFusedVariant[resolve_variant(variant_, GM_LEAN) - 1]) {
+  if (nl && nl < b.n_tiles && (b.n_tiles - nl) * kSplitFull <= b.n_tiles && b.tile_map && grammar_index(b.gm) == 2 &&
+      kFusedVariant[resolve_variant(variant_, b.gm) - 1] && kFusedVariant[resolve_variant(variant_, GM_LEAN) - 1]) {
     return launch_tiles(b, m, 0, b.n_tiles, st, st, nullptr, err, nullptr, zero, b.tile_map, nl, GM_LEAN) &&
            launch_tiles(b, m, 0, b.n_tiles, st, st, nullptr, err, nullptr, nullptr, b.tile_map + nl, b.n_tiles - nl,
                         b.gm);

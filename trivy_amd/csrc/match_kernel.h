@@ -219,7 +219,7 @@ template <class P>
 __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uint32_t plat, const PlatInfo& pi,
                                             uint32_t nlen, const uint8_t* name, bool valid, uint64_t h, uint4 q0,
                                             uint4 q0n, bool has_q0n, uint32_t& rbeg, uint32_t& cnt,
-                                            uint32_t* sflags = nullptr);
+                                            uint32_t* sflags = nullptr, uint32_t cls = 0);
 
 template <class P>
 __device__ __forceinline__ uint4 home_slot(const ProbeArgs& a, uint64_t h, uint32_t step = 0) {
@@ -260,7 +260,11 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
         r.k1 = kl > 8 ? be_word(m1, kl < 16 ? kl - 8 : 8) : 0ull;
         r.k2 = kl > 16 ? be_word(uint64_t(kw[4]) | (uint64_t(kw[5]) << 32), kl < 24 ? kl - 16 : 8) : 0ull;
         static_assert(kFastKeyCap <= kKeyWords * 8, "fast keys fit head + tail slot");
-        if (kl > 16) a.tail[p] = make_uint4(kw[4], kw[5], kw[6], kw[7]);
+        // dpkg-only kernels compare 24-byte heads (bytes 16..23 in r.k2), so their tail slot is
+        // read only past a 24-byte tie (bytes 24..31) or by a lower bound, which takes bytes
+        // 16..23 from k2 (eval_row): a key of 17..24 bytes writes nothing (C2: ~49 MB of tail
+        // stores per pass).  Other grammar sets keep it: their split-form sweeps compare 16.
+        if (kl > (GM == GM_DEB ? 24u : 16u)) a.tail[p] = make_uint4(kw[4], kw[5], kw[6], kw[7]);
       }
       uint32_t cnt = 0, rbeg = 0;
       if constexpr (!kPre) heads();
@@ -301,7 +305,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
   }
   uint32_t cnt = 0, rbeg = 0, sflags = 0;
   if constexpr (!kPre) heads();
-  if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, valid, h, q0, q0n, kPre, rbeg, cnt, &sflags);
+  if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, valid, h, q0, q0n, kPre, rbeg, cnt, &sflags, cls);
   if (((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN) {
     // Maven rows compare parses, not keys (AUX_MVN): the installed version's parse, packed
     // into the batch scratch, and its text location take the tail slot - only when the key
@@ -341,7 +345,7 @@ template <class P>
 __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uint32_t plat, const PlatInfo& pi,
                                             uint32_t nlen, const uint8_t* name, bool valid, uint64_t h,
                                             uint4 q0, uint4 q0n, bool has_q0n, uint32_t& rbeg, uint32_t& cnt,
-                                            uint32_t* sflags) {
+                                            uint32_t* sflags, uint32_t cls) {
   // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup;
   // lookup-first drivers (ubuntu.go:86-92) probe first, so a poisoned key still raises
   if (valid || (pi.flags & PLAT_LOOKUP_FIRST)) {
@@ -358,8 +362,9 @@ __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uin
       if (q1.x & SLOT_POISONED) {
         atomicMax(&a.ctl[1], (unsigned long long)(a.n_total - (a.p0 + p)));
       } else if (valid) {
-        cnt = q0.w;
-        rbeg = q0.z;
+        const uint2 rr = slot_rows(q1.x, q0.z, q0.w, cls);  // a split key: the list of the version's class
+        rbeg = rr.x;
+        cnt = rr.y;
         if (sflags) *sflags = q1.x & (SLOT_MVN_C0 | SLOT_MVN_C1);
       }
       break;
@@ -488,8 +493,37 @@ __device__ __forceinline__ bool mvn_pair(const SweepArgs& a, const uint32_t* ids
   return mvn_program_eval(ids, V);
 }
 
+// The predicates an rpm row carries inline (common.h ROW_INLINE): no load but the package's
+// CPE-set word.
+__device__ __forceinline__ uint32_t inline_pass(const SweepArgs& a, const Row& row, uint2 pa) {
+  const uint32_t kind = row.lo_len & 15u, na = (row.lo_len >> 4) & 3u, nc = (row.lo_len >> 6) & 3u;
+  if (kind & AUX_TAG) return row.off.lo_off == pa.y ? 1u : 0u;
+  const uint32_t w[2] = {row.off.lo_off, row.off.hi_off};
+  auto id = [&](uint32_t i) { return (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu; };
+  if (kind & (AUX_ARCH_RH | AUX_ARCH_IN)) {
+    bool ok = (kind & AUX_ARCH_RH) && (na == 0 || (pa.x & PA_NOARCH));
+    const uint32_t arch = pa.x & PA_ARCH_MASK;
+    for (uint32_t i = 0; i < na; i++) ok |= id(i) == arch;
+    if (!ok) return 0;
+  }
+  if (kind & AUX_CPE) {
+    if (pa.y >= a.n_cpe_sets) return 0;
+    const uint32_t* set = a.cpe_bits + size_t(pa.y) * a.cpe_words;
+    bool ok = false;
+    for (uint32_t i = 0; i < nc; i++) {
+      const uint32_t c = id(na + i);
+      ok |= (c >> 5) < a.cpe_words && ((set[c >> 5] >> (c & 31)) & 1u);
+    }
+    if (!ok) return 0;
+  }
+  return 1;
+}
+
 template <int FILT, bool DEFER = false>
 __device__ __forceinline__ uint32_t aux_pass(const SweepArgs& a, uint32_t ridx, uint2 pa, uint32_t ki, uint32_t p) {
+#ifdef TVM_EXP_NOAUX  // measurement only (make exp): every row filter passes - wrong lists by design
+  if (FILT < 2) return 1;
+#endif
   const RowAux x = a.db.aux[ridx];
   const uint32_t* ids = a.db.aux_ids + x.list_off;
   // the class first: a Maven hybrid program row is rejected for numeric versions before its
@@ -564,13 +598,17 @@ __device__ __forceinline__ uint32_t eval_row(const SweepArgs& a, const S& s, uin
     const uint64_t* ktail =
         (ki & KI_SPILL) ? a.spill + s.koff[q] + 2 : reinterpret_cast<const uint64_t*>(a.tail + p);
     const uint32_t w = hl / 8;
-    const uint32_t hi_off = h24 ? a.db.row_off[ridx].hi_off : row.off.hi_off;
+    const uint32_t hi_off = (h24 || (row.adv & ROW_INLINE)) ? a.db.row_off[ridx].hi_off : row.off.hi_off;
     c = key_cmp(ktail + (w - 2), kl - hl, a.db.key_words + hi_off + w, nh - hl);
   }
   bool m = hi_inf || ((row.hi_len & KEY_INCL) ? c <= 0 : c < 0);
   if (!(row.lo_len & KEY_INF) && m) {  // rare (library / rpm ranges): the bound's head from the arena
-    const uint64_t* ktail =
-        (ki & KI_SPILL) ? a.spill + s.koff[q] + 2 : reinterpret_cast<const uint64_t*>(a.tail + p);
+    // a 24-byte-head package of at most 24 key bytes wrote no tail slot (probe_one): its bytes
+    // 16..23 come from k2, back in memory order
+    const uint64_t t24[2] = {__builtin_bswap64(c24 ? k2 : 0ull), 0ull};
+    const uint64_t* ktail = (ki & KI_SPILL) ? a.spill + s.koff[q] + 2
+                            : (c24 && kl <= 24) ? t24
+                                                : reinterpret_cast<const uint64_t*>(a.tail + p);
     const uint64_t* lw = a.db.key_words + (h24 ? a.db.row_off[ridx].lo_off : row.off.lo_off);
     const uint32_t nl = row.lo_len & KEY_LEN_MASK;
     const uint64_t l0 = nl ? be_word(lw[0], nl < 8 ? nl : 8) : 0ull;
@@ -581,7 +619,8 @@ __device__ __forceinline__ uint32_t eval_row(const SweepArgs& a, const S& s, uin
   m = m && (ki & KI_VALID);
   m = m || (row.adv & ROW_ALWAYS);
   if constexpr (FILT) {
-    if (m && (row.adv & ROW_FILTER)) return aux_pass<FILT, DEFER>(a, ridx, s.pattr[q], ki, p);
+    if (m && (row.adv & ROW_FILTER))
+      return (row.adv & ROW_INLINE) ? inline_pass(a, row, s.pattr[q]) : aux_pass<FILT, DEFER>(a, ridx, s.pattr[q], ki, p);
   }
   return m ? 1u : 0u;
 }
