@@ -2216,7 +2216,9 @@ int tvm_vuln_set_walk(const tvm_vuln_set* s, const tvm_batch* b, uint64_t* n_out
   pool_range_for(groups, 64, [&](size_t g0, size_t g1) {
     uint64_t d = 0, c = 0, nb = 0;
     const uint64_t i_end = std::min<size_t>(np, g1 * kGroup) ? s->row_end[std::min<size_t>(np, g1 * kGroup) - 1] : 0;
-    constexpr uint64_t kAhead = 16;  // records are scattered over the DB's: their loads overlap
+    // records are scattered over the DB's (~1.7M x 136 B): their loads overlap, every line a
+    // record's fields span prefetched (a record straddles up to three 64-B lines)
+    constexpr uint64_t kAhead = 32;
     for (size_t g = g0; g < g1; g++) {
       uint64_t off = hb.tile_off[g];
       for (size_t p = g * kGroup; p < std::min(np, (g + 1) * kGroup); p++) {
@@ -2229,7 +2231,12 @@ int tvm_vuln_set_walk(const tvm_vuln_set* s, const tvm_batch* b, uint64_t* n_out
         const uint64_t pg = uint64_t(s->first_pkg) + p;
         for (uint64_t i = i0; i < i1; i++) {
           if (i + kAhead < i_end)
-            if (const tvm_vuln* ahead = vuln_of(rec_at(i + kAhead))) __builtin_prefetch(ahead);
+            if (const tvm_vuln* ahead = vuln_of(rec_at(i + kAhead))) {
+              const char* c = reinterpret_cast<const char*>(ahead);
+              __builtin_prefetch(c);
+              __builtin_prefetch(c + 64);
+              __builtin_prefetch(c + sizeof(tvm_vuln) - 1);
+            }
           const uint64_t r = rec_at(i);
           const tvm_vuln* v = vuln_of(r);
           if (!v) {
