@@ -2,6 +2,7 @@
 #include "db.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "json.h"
 #include "libdb.h"
@@ -826,9 +827,18 @@ void DB::build_index() {
       for (int64_t c : v)
         if (c >= 0 && c < int64_t(1) << 24) n_cpe = std::max<uint32_t>(n_cpe, uint32_t(c) + 1);
 
-  // hash index, load factor <= 0.5
+  // hash index, load factor <= 1/8 (TVM_SLOT_LOAD overrides it, for measurement).  Every extra
+  // slot a probe walks is a dependent round trip, and absent names (a quarter of the synthetic
+  // batches) walk to an empty slot: at most 1/2 (0.29 for C2's 150k keys) -> 1/8 took C2 0.410
+  // -> 0.394 ms, C3 0.154 -> 0.142, C5 2.08 -> 1.85 (profiles/r06/slotload/); 3/4 cost C2 26 %.
+  // The table is 64 B a slot: 134 MB for C2's keys, nothing next to 288 GB of HBM
+  static const double max_load = [] {
+    const char* v = std::getenv("TVM_SLOT_LOAD");
+    const double x = v ? std::atof(v) : 0.125;
+    return x > 0.01 && x < 0.95 ? x : 0.125;
+  }();
   uint64_t cap = 16;
-  while (cap < keys.size() * 2) cap <<= 1;
+  while (double(cap) * max_load < double(keys.size())) cap <<= 1;
   slot_mask = cap - 1;
   slot_hash.assign(cap, 0);
   slot_val.assign(cap, SlotVal{});
