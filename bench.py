@@ -252,14 +252,16 @@ def cpu_model():
 
 
 def kernel_source_hash():
-    """sha1 over the sources the match kernels are compiled from (their headers + kern_*.hip): ties a
-    committed PMC summary to the build it was measured on."""
+    """sha1 over the sources the match kernels are compiled from (their headers + kern_*.hip) and the
+    table builder whose layout they read (db.cpp / db.h: slot load, row packing): ties a committed PMC
+    summary to the build it was measured on."""
     import glob
     import hashlib
     h = hashlib.sha1()
     csrc = os.path.join(ROOT, "trivy_amd", "csrc")
     # the match kernels' translation units and the headers they include (Makefile HDRS_KERN)
-    kern_hdrs = ["common.h", "engine.h", "libver.h", "verkey.h", "unicode_tab.h", "match_kernel.h", "match_variants.h"]
+    kern_hdrs = ["common.h", "engine.h", "libver.h", "verkey.h", "unicode_tab.h", "match_kernel.h", "match_variants.h",
+                 "db.h", "db.cpp"]
     for f in sorted([os.path.join(csrc, h) for h in kern_hdrs] + glob.glob(os.path.join(csrc, "kern_*.hip"))):
         h.update(os.path.basename(f).encode())
         with open(f, "rb") as fh:
