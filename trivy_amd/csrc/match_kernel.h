@@ -212,9 +212,8 @@ __device__ __forceinline__ bool name_eq_slot(const uint8_t* s, uint32_t n, const
 }
 
 // Index probe of one package given its key state (shared by the fast and generic paths).
-// h / q0 / q0n: the name's hash and the first 16 bytes of its home slot and of the slot after
-// it, loaded before the version is encoded so the round trips overlap the encoder (the table
-// is at most half full, but a quarter of the lanes of a wave still probe a second slot).
+// h / q0 / q0n: the name's hash and the first 16 bytes of its home slot and (has_q0n) of the
+// slot after it, loaded before the version is encoded so the round trips overlap the encoder.
 template <class P>
 __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uint32_t plat, const PlatInfo& pi,
                                             uint32_t nlen, const uint8_t* name, bool valid, uint64_t h, uint4 q0,
@@ -239,11 +238,23 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
   constexpr bool kPre = GM == GM_DEB;
   uint64_t h = 0;
   uint4 q0 = make_uint4(0, 0, 0, 0), q0n = q0;
+  bool has_q0n = false;
   auto heads = [&]() {
     if (DIAG & 2) return;
     h = name_hash<P>(plat, name, nlen);
     q0 = home_slot<P>(a, h);
-    if constexpr (kPre) q0n = home_slot<P>(a, h, 1);
+    // the next slot's head too, but only from the home slot's own 128-B line (an even slot
+    // index: every L2 miss is a 128-B request, so it costs no request of its own); at slot
+    // load <= 1/8 a second slot is rarely probed, and fetching the next line for the odd home
+    // slots cost C2 a random request per second package
+#ifdef TVM_EXP_Q0N_ALWAYS  // measurement only (make exp): the round-5 form, next head always
+    if constexpr (kPre) { q0n = home_slot<P>(a, h, 1); has_q0n = true; }
+#else
+    if constexpr (kPre) {
+      has_q0n = !(h & a.db.slot_mask & 1);
+      if (has_q0n) q0n = home_slot<P>(a, h, 1);
+    }
+#endif
   };
   if constexpr (kPre) heads();
   if (!(DIAG & 1) && kb && ((GM >> CMP_DEB) & 1u) && pi.cmp == CMP_DEB) {
@@ -268,7 +279,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
       }
       uint32_t cnt = 0, rbeg = 0;
       if constexpr (!kPre) heads();
-      if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, (kinfo & KI_VALID) != 0, h, q0, q0n, kPre, rbeg, cnt);
+      if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, (kinfo & KI_VALID) != 0, h, q0, q0n, has_q0n, rbeg, cnt);
       r.meta = make_uint4(rbeg, cnt, kinfo, koff);
       return;
     }
@@ -305,7 +316,7 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
   }
   uint32_t cnt = 0, rbeg = 0, sflags = 0;
   if constexpr (!kPre) heads();
-  if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, valid, h, q0, q0n, kPre, rbeg, cnt, &sflags, cls);
+  if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, valid, h, q0, q0n, has_q0n, rbeg, cnt, &sflags, cls);
   if (((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN) {
     // Maven rows compare parses, not keys (AUX_MVN): the installed version's parse, packed
     // into the batch scratch, and its text location take the tail slot - only when the key
