@@ -165,6 +165,14 @@ struct alignas(64) Slot {
   uint64_t name[kSlotNameWords];
 };
 static_assert(sizeof(Slot) == 64, "one cache line per slot");
+// Slot fingerprints (DB::slot_fp): one byte a slot, 0 = empty, else the hash's top byte (1 for
+// 0).  The probe walks the chain in this array (1/64 of the slot bytes: 2 MB for 2^21 slots,
+// L2-resident) and reads a 64-B slot only where the fingerprint is the name's: an absent name
+// reads no slot at all.
+TVM_HD uint8_t slot_fp_of(uint64_t h) {
+  const uint8_t f = uint8_t(h >> 56);
+  return f ? f : uint8_t(1);
+}
 // Names in the DB name arena start 8-byte aligned, zero padded to a word boundary, and
 // the arena ends with kNameWords zero words: the probe verifies a name with kNameWords
 // independent word loads (one memory round trip) instead of a byte loop.

@@ -844,6 +844,7 @@ void DB::build_index() {
   slot_val.assign(cap, SlotVal{});
   slot_key.assign(cap, 0);
   slots.assign(cap, Slot{});
+  slot_fp.assign(cap, 0);
   name_arena.clear();
   for (size_t k = 0; k < keys.size(); k++) {
     const Key& key = keys[k];
@@ -851,6 +852,7 @@ void DB::build_index() {
     uint64_t i = h & slot_mask;
     while (slot_hash[i]) i = (i + 1) & slot_mask;
     slot_hash[i] = h;
+    slot_fp[i] = slot_fp_of(h);
     // which installed-version classes meet a Maven program row of the key (the probe packs a
     // Maven package's parse only for those)
     const bool split = (row_count[k] & kRowSplit) != 0;

@@ -106,6 +106,7 @@ class DB {
   std::vector<uint64_t> slot_hash;
   std::vector<SlotVal> slot_val;
   std::vector<Slot> slots;          // device probe table (common.h Slot), same positions
+  std::vector<uint8_t> slot_fp;     // device: per slot slot_fp_of(hash), 0 = empty (common.h)
   std::vector<uint32_t> slot_key;   // host only: slot -> Key index
   std::vector<uint8_t> name_arena;
   std::vector<Row> rows;

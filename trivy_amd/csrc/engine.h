@@ -24,6 +24,7 @@ constexpr int kGroupsPerTile = kTile / kGroup;
 // Device view of the flattened tables (db.h device images).
 struct DevDB {
   const Slot* slots = nullptr;
+  const uint8_t* slot_fp = nullptr;  // DB::slot_fp
   uint64_t slot_mask = 0;
   const uint8_t* name_arena = nullptr;
   const Row* rows = nullptr;

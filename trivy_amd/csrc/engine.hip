@@ -171,10 +171,11 @@ Engine* Engine::open(const DB& db, int device, std::string& err) {
     delete e;
     return nullptr;
   }
-  Slot* sl; uint8_t* na; Row* rows; RowOff* ro; uint64_t* kw; PlatInfo* pl; RowAux* ax; uint32_t* ai;
+  Slot* sl; uint8_t* fp; uint8_t* na; Row* rows; RowOff* ro; uint64_t* kw; PlatInfo* pl; RowAux* ax; uint32_t* ai;
   bool ok = upload_vec(db.aux, &ax, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.aux_ids, &ai, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.slots, &sl, e->allocs_, e->table_bytes_, err) &&
+            upload_vec(db.slot_fp, &fp, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.name_arena, &na, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.rows, &rows, e->allocs_, e->table_bytes_, err) &&
             upload_vec(db.row_off, &ro, e->allocs_, e->table_bytes_, err) &&
@@ -185,6 +186,7 @@ Engine* Engine::open(const DB& db, int device, std::string& err) {
     return nullptr;
   }
   e->d_.slots = sl;
+  e->d_.slot_fp = fp;
   e->d_.slot_mask = db.slot_mask;
   e->d_.name_arena = na;
   e->d_.rows = rows;
@@ -833,6 +835,7 @@ bool Engine::verify(std::string& err) {
   };
   const DB& db = *db_;
   return check(d_.slots, db.slots.data(), db.slots.size() * sizeof(Slot), "slots") &&
+         check(d_.slot_fp, db.slot_fp.data(), db.slot_fp.size(), "slot_fp") &&
          check(d_.name_arena, db.name_arena.data(), db.name_arena.size(), "name_arena") &&
          check(d_.rows, db.rows.data(), db.rows.size() * sizeof(Row), "rows") &&
          check(d_.row_off, db.row_off.data(), db.row_off.size() * sizeof(RowOff), "row_off") &&

@@ -212,17 +212,37 @@ __device__ __forceinline__ bool name_eq_slot(const uint8_t* s, uint32_t n, const
 }
 
 // Index probe of one package given its key state (shared by the fast and generic paths).
-// h / q0 / q0n: the name's hash and the first 16 bytes of its home slot and (has_q0n) of the
-// slot after it, loaded before the version is encoded so the round trips overlap the encoder.
+// h: the name's hash; start / found: the first slot of its chain whose fingerprint is the
+// name's (fp_chain), if any; q0 / q0n: the first 16 bytes of that slot and (has_q0n) of the
+// slot after it, loaded early so the round trips overlap the encoder.
 template <class P>
 __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uint32_t plat, const PlatInfo& pi,
-                                            uint32_t nlen, const uint8_t* name, bool valid, uint64_t h, uint4 q0,
-                                            uint4 q0n, bool has_q0n, uint32_t& rbeg, uint32_t& cnt,
-                                            uint32_t* sflags = nullptr, uint32_t cls = 0);
+                                            uint32_t nlen, const uint8_t* name, bool valid, uint64_t h,
+                                            uint64_t start, bool found, uint4 q0, uint4 q0n, bool has_q0n,
+                                            uint32_t& rbeg, uint32_t& cnt, uint32_t* sflags = nullptr,
+                                            uint32_t cls = 0);
 
-template <class P>
-__device__ __forceinline__ uint4 home_slot(const ProbeArgs& a, uint64_t h, uint32_t step = 0) {
-  return reinterpret_cast<const uint4*>(a.db.slots + ((h + step) & a.db.slot_mask))[0];
+__device__ __forceinline__ uint4 slot_head(const ProbeArgs& a, uint64_t i) {
+  return reinterpret_cast<const uint4*>(a.db.slots + (i & a.db.slot_mask))[0];
+}
+
+// The first slot of h's linear-probing chain whose fingerprint is h's (DB::slot_fp), or false
+// at the chain's end: slots with another fingerprint cannot hold the name, so they are passed
+// over without reading their 64 B, and an absent name (a quarter of the synthetic batches)
+// reads one byte from an L2-resident array instead of a 128-B line.
+__device__ __forceinline__ bool fp_chain(const ProbeArgs& a, uint64_t h, uint64_t& i) {
+  i = h & a.db.slot_mask;
+#ifdef TVM_EXP_NOFP  // measurement only (make exp): no fingerprint walk, every chain from its home slot
+  return true;
+#else
+  const uint8_t want = slot_fp_of(h);
+  for (;;) {
+    const uint8_t f = a.db.slot_fp[i];
+    if (f == 0) return false;
+    if (f == want) return true;
+    i = (i + 1) & a.db.slot_mask;
+  }
+#endif
 }
 
 // One package: encode, hash, probe.  P = uint32_t in the LDS or global address space of s.
@@ -232,29 +252,29 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
                                           const uint8_t* name, const uint8_t* ver, uint64_t vglob, PkgRec& r,
                                           uint8_t* kb = nullptr, const uint8_t* tab = nullptr) {
   const PlatInfo pi = a.db.plats[plat];
-  // the dpkg-only kernels load the slot heads before the encoder; the other grammar sets
-  // after it (their encoders' registers: held across them, the heads made the all-grammar
-  // kernel spill)
+  // the hash and the fingerprint walk come before the encoder; the dpkg-only kernels load the
+  // slot heads before it too, the other grammar sets after it (their encoders' registers: held
+  // across them, the heads made the all-grammar kernel spill)
   constexpr bool kPre = GM == GM_DEB;
-  uint64_t h = 0;
+  uint64_t h = 0, start = 0;
+  bool found = false;
   uint4 q0 = make_uint4(0, 0, 0, 0), q0n = q0;
   bool has_q0n = false;
-  auto heads = [&]() {
-    if (DIAG & 2) return;
+  if (!(DIAG & 2)) {
     h = name_hash<P>(plat, name, nlen);
-    q0 = home_slot<P>(a, h);
-    // the next slot's head too, but only from the home slot's own 128-B line (an even slot
-    // index: every L2 miss is a 128-B request, so it costs no request of its own); at slot
-    // load <= 1/8 a second slot is rarely probed, and fetching the next line for the odd home
-    // slots cost C2 a random request per second package
-#ifdef TVM_EXP_Q0N_ALWAYS  // measurement only (make exp): the round-5 form, next head always
-    if constexpr (kPre) { q0n = home_slot<P>(a, h, 1); has_q0n = true; }
-#else
+    found = fp_chain(a, h, start);
+  }
+  auto heads = [&]() {
+    if ((DIAG & 2) || !found) return;
+    q0 = slot_head(a, start);
+    // the next slot's head too, but only from the same 128-B line (an even slot index: every
+    // L2 miss is a 128-B request, so it costs no request of its own); at slot load <= 1/8 a
+    // second slot is rarely probed, and fetching the next line for the odd slots cost C2 a
+    // random request per second package (0.393 -> 0.386 ms, profiles/r06/q0n)
     if constexpr (kPre) {
-      has_q0n = !(h & a.db.slot_mask & 1);
-      if (has_q0n) q0n = home_slot<P>(a, h, 1);
+      has_q0n = !(start & 1);
+      if (has_q0n) q0n = slot_head(a, start + 1);
     }
-#endif
   };
   if constexpr (kPre) heads();
   if (!(DIAG & 1) && kb && ((GM >> CMP_DEB) & 1u) && pi.cmp == CMP_DEB) {
@@ -279,7 +299,8 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
       }
       uint32_t cnt = 0, rbeg = 0;
       if constexpr (!kPre) heads();
-      if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, (kinfo & KI_VALID) != 0, h, q0, q0n, has_q0n, rbeg, cnt);
+      if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, (kinfo & KI_VALID) != 0, h, start, found, q0, q0n, has_q0n,
+                                          rbeg, cnt);
       r.meta = make_uint4(rbeg, cnt, kinfo, koff);
       return;
     }
@@ -316,7 +337,8 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
   }
   uint32_t cnt = 0, rbeg = 0, sflags = 0;
   if constexpr (!kPre) heads();
-  if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, valid, h, q0, q0n, has_q0n, rbeg, cnt, &sflags, cls);
+  if (!(DIAG & 2)) probe_lookup<P>(a, p, plat, pi, nlen, name, valid, h, start, found, q0, q0n, has_q0n, rbeg, cnt,
+                                   &sflags, cls);
   if (((GM >> CMP_MAVEN) & 1u) && pi.cmp == CMP_MAVEN) {
     // Maven rows compare parses, not keys (AUX_MVN): the installed version's parse, packed
     // into the batch scratch, and its text location take the tail slot - only when the key
@@ -355,13 +377,13 @@ __device__ __forceinline__ void probe_one(const ProbeArgs& a, uint32_t p, uint32
 template <class P>
 __device__ __forceinline__ void probe_lookup(const ProbeArgs& a, uint32_t p, uint32_t plat, const PlatInfo& pi,
                                             uint32_t nlen, const uint8_t* name, bool valid, uint64_t h,
-                                            uint4 q0, uint4 q0n, bool has_q0n, uint32_t& rbeg, uint32_t& cnt,
-                                            uint32_t* sflags, uint32_t cls) {
+                                            uint64_t start, bool found, uint4 q0, uint4 q0n, bool has_q0n,
+                                            uint32_t& rbeg, uint32_t& cnt, uint32_t* sflags, uint32_t cls) {
   // parse-first drivers (debian.go:66-70) skip an unparsable package before the lookup;
   // lookup-first drivers (ubuntu.go:86-92) probe first, so a poisoned key still raises
-  if (valid || (pi.flags & PLAT_LOOKUP_FIRST)) {
+  if (found && (valid || (pi.flags & PLAT_LOOKUP_FIRST))) {
     uint32_t step = 0;
-    for (uint64_t i = h & a.db.slot_mask;; i = (i + 1) & a.db.slot_mask, step++) {
+    for (uint64_t i = start;; i = (i + 1) & a.db.slot_mask, step++) {
       const uint4* sp = reinterpret_cast<const uint4*>(a.db.slots + i);
       if (step == 1 && has_q0n) q0 = q0n;
       else if (step > 0) q0 = sp[0];
