@@ -81,11 +81,81 @@ def _driver_view(kind, p):
     raise ValueError(kind)
 
 
+def _fmt_cols(epoch, version, release):
+    """format_version (drivers.py) over columns: version, "-release" when set, "epoch:" when set."""
+    v = np.where(release != b"", np.char.add(np.char.add(version, b"-"), release), version)
+    return np.where(epoch != 0, np.char.add(np.char.add(epoch.astype("S"), b":"), v), v)
+
+
+def _per_unique(col, fn):
+    """fn over the distinct values of a bytes column, mapped back to every row."""
+    uniq, inv = np.unique(col, return_inverse=True)
+    return np.array([fn(u) for u in uniq.tolist()] or [b""], dtype=object)[inv]
+
+
+def _columnar_views(sm, sdb, p, g, idx, aid):
+    """The per-package fields Prepared's scalar loop takes from driver_packages + _driver_view,
+    over whole columns (numpy), for batches too large for a Python loop per package:
+    (lookup names, compared versions, installed versions, arch ids, skip, CPE-combination
+    representative rows).  Pinned to the scalar loop by tests/test_cport.py."""
+    bucket, kind = sdb.plats[p]
+    take = lambda c: g[c][idx]  # noqa: E731
+    n = len(idx)
+    if kind in sm.LANG_OF:
+        eco = ol.LANG[sm.LANG_OF[kind]][0]
+        ver = take("ver")
+        nm = _per_unique(take("name"), lambda b: ol.normalize_pkg_name(eco, b.decode()).encode())
+        return nm, ver, ver, np.full(n, -1, np.int32), np.zeros(n, np.uint8), None
+    name = take("pname") if kind == "redhat" else take("name")
+    ver = _fmt_cols(take("epoch"), take("version"), take("rel"))
+    label = take("label") if kind == "redhat" else np.full(n, b"", dtype="S1")
+    skip = np.zeros(n, np.uint8)
+    if kind in ("alma", "redhat"):
+        if kind == "redhat":
+            lab_u, lab_inv = np.unique(label, return_inverse=True)
+            ns = [b"" if not lb else od.add_modular_namespace("", lb.decode()).encode() for lb in lab_u.tolist()]
+            nm = np.char.add(np.array(ns, dtype="S")[lab_inv], name)
+            skip = np.char.endswith(take("rel"), b".remi").astype(np.uint8)
+        else:  # alma packages here carry no Modularitylabel
+            nm = name
+            skip = (np.char.find(take("rel"), b".module_el") >= 0).astype(np.uint8)
+    else:  # debian / ubuntu (SrcName = Name), alpine, rocky (no label), oracle
+        nm = name
+    arches = np.full(n, -1, np.int32)
+    if "arch" in g:
+        au, ainv = np.unique(take("arch"), return_inverse=True)
+        arches = np.array([aid(a.decode()) if a else -1 for a in au.tolist()], np.int32)[ainv]
+    combo = None
+    if kind == "redhat":  # one (content sets, NVR) per (release, BuildInfo NVR)
+        key = np.char.add(np.char.add(take("rhrel").astype("S"), b"|"), np.where(take("bi"), take("nvr"), b""))
+        _, combo_first, combo_inv = np.unique(key, return_index=True, return_inverse=True)
+        combo = (idx[combo_first], combo_inv)
+    return nm, ver, ver, arches, skip, combo
+
+
+class _Decoded:
+    """A bytes column read as str per element (Prepared.installed in the columnar form)."""
+
+    def __init__(self, col):
+        self.col = col
+
+    def __len__(self):
+        return len(self.col)
+
+    def __getitem__(self, i):
+        return self.col[i].decode()
+
+
 class Prepared:
     """Oracle-side digest of a sample: sample = [(platform index p, group g, row indices)] of a
-    tools/synth_mix.py MixBatch over MixDB sdb."""
+    tools/synth_mix.py MixBatch over MixDB sdb.  columnar: the per-package fields come from
+    _columnar_views (whole-batch checks at 10-20M packages); the default scalar form builds
+    every package's driver dict (oracle/drivers.py) and is the one the C port is pinned to."""
 
-    def __init__(self, sm, sdb, sample):
+    def __init__(self, sm, sdb, sample, columnar=False):
+        if columnar:
+            self._init_columnar(sm, sdb, sample)
+            return
         self.pkgs = []  # (plat, driver package dict) in sample order
         self.installed = []  # per package: the InstalledVersion its driver reports
         self.plat_family = []  # per platform: the OS driver family, or None for a language bucket
@@ -127,6 +197,66 @@ class Prepared:
                 skip.append(1 if sk else 0)
                 cpes.append([])
                 want[(p, nm)] = None
+        self.plat_of = np.array(plats, dtype=np.int64)
+        recs = self._records(sm, sdb, want)
+        cpe_of = {}  # (content sets, nvr) -> the CPE set (one per image, not per package)
+        for i, (p, pk) in enumerate(self.pkgs):
+            if sdb.plats[p][1] == "redhat":
+                cpes[i + 1] = self._cpe_set(recs, cpe_of, pk)
+        names = [x.encode() for x in names]
+        vers = [x.encode() for x in vers]
+        self._finish(sm, sdb, recs, want, aid, noarch, plat_drv, plat_gram, names, vers, plats, arches, skip, cpes)
+
+    def _init_columnar(self, sm, sdb, sample):
+        self.pkgs = None
+        plat_drv, plat_gram = [], []
+        self.plat_family = []
+        for bucket, kind in sdb.plats:
+            if kind in sm.LANG_OF:
+                plat_drv.append(MX_LIB)
+                plat_gram.append(GRAMMAR[ol.LANG[sm.LANG_OF[kind]][1]])
+                self.plat_family.append(None)
+            else:
+                plat_drv.append(MX[sm.DRIVER_OF[kind][0]])
+                plat_gram.append(0)
+                self.plat_family.append(sm.DRIVER_OF[kind][0])
+        arch_id = {}
+
+        def aid(a):
+            return arch_id.setdefault(a, len(arch_id))
+        noarch = aid("noarch")
+        cols = []
+        want = {}
+        for p, g, idx in sample:
+            nm, ver, inst, arches, skip, combo = _columnar_views(sm, sdb, p, g, np.asarray(idx), aid)
+            cols.append((p, g, nm, ver, inst, arches, skip, combo))
+            for u in np.unique(nm).tolist():
+                want[(p, u.decode())] = None
+        recs = self._records(sm, sdb, want)
+        cpe_of = {}
+        cpes = [[]]
+        for p, g, nm, ver, inst, arches, skip, combo in cols:
+            if combo is None:
+                cpes += [[]] * len(nm)
+                continue
+            first_rows, inv = combo
+            sets = []
+            for r in first_rows.tolist():  # the scalar form's own package dict, one per combination
+                pk = sm.driver_packages(sdb, p, g, [r])[0]
+                pk["_rel"] = int(g["rhrel"][r])
+                sets.append(self._cpe_set(recs, cpe_of, pk))
+            cpes += [sets[c] for c in inv.tolist()]
+        cat = lambda xs, dt: np.concatenate(xs) if xs else np.zeros(0, dt)  # noqa: E731
+        names = cat([c[2].astype("S") for c in cols], "S1")
+        vers = cat([c[3] for c in cols], "S1")
+        plats = cat([np.full(len(c[2]), c[0], np.int32) for c in cols], np.int32)
+        self.plat_of = plats.astype(np.int64)
+        self.installed = _Decoded(cat([c[4] for c in cols], "S1"))
+        self._finish(sm, sdb, recs, want, aid, noarch, plat_drv, plat_gram, names, vers, plats,
+                     cat([c[5] for c in cols], np.int32), cat([c[6] for c in cols], np.uint8), cpes)
+
+    @staticmethod
+    def _records(sm, sdb, want):
         # Red Hat CPE sets need the "Red Hat CPE" buckets: one Records over every record the
         # sample's keys touch (+ data sources)
         by_root = {}
@@ -136,17 +266,20 @@ class Prepared:
             for r in roots:
                 by_root.setdefault(r, set()).add(nm)
         by_root["Red Hat CPE"] = {"repository", "nvr", "cpe"}
-        recs = od.Records(sdb.records_for(by_root))
-        cpe_of = {}  # (content sets, nvr) -> the CPE set (one per image, not per package)
-        for i, (p, pk) in enumerate(self.pkgs):
-            if sdb.plats[p][1] == "redhat":
-                bi = pk.get("BuildInfo")
-                cs, nvr = ((od.REDHAT_DEFAULT_CONTENT_SETS.get(str(pk["_rel"]), []), "")
-                           if bi is None else (bi.get("ContentSets") or [], f"{bi.get('Nvr', '')}-{bi.get('Arch', '')}"))
-                k = (tuple(cs), nvr)
-                if k not in cpe_of:
-                    cpe_of[k] = recs.redhat_cpes(cs, [nvr])
-                cpes[i + 1] = cpe_of[k]
+        return od.Records(sdb.records_for(by_root))
+
+    @staticmethod
+    def _cpe_set(recs, cpe_of, pk):
+        """The CPE set of a Red Hat package (redhat.go:112-120), cached per (content sets, NVR)."""
+        bi = pk.get("BuildInfo")
+        cs, nvr = ((od.REDHAT_DEFAULT_CONTENT_SETS.get(str(pk["_rel"]), []), "")
+                   if bi is None else (bi.get("ContentSets") or [], f"{bi.get('Nvr', '')}-{bi.get('Arch', '')}"))
+        k = (tuple(cs), nvr)
+        if k not in cpe_of:
+            cpe_of[k] = recs.redhat_cpes(cs, [nvr])
+        return cpe_of[k]
+
+    def _finish(self, sm, sdb, recs, want, aid, noarch, plat_drv, plat_gram, names, vers, plats, arches, skip, cpes):
         # entries per wanted key
         ar = _Arena()
         vids = set()
@@ -227,8 +360,13 @@ class Prepared:
                            _p(c["aff_len"], _U32), _p(c["vul_off"], _U64), _p(c["vul_len"], _U32),
                            _p(c["sec_off"], _U64), _p(c["sec_len"], _U32), _p(c["flags"], _U32), _p(c["vid"], _I32),
                            _p(arr(ids_begin, np.int64), _I64), _p(c["n_arch"], _I32), _p(arr(ids or [0], np.int32), _I32))
-        def packed(strs):
-            bs = [x.encode() for x in strs]
+        def packed(bs):
+            if isinstance(bs, np.ndarray):  # a bytes column: lengths and the arena without a loop
+                ln = np.char.str_len(bs).astype(np.uint32) if len(bs) else np.zeros(0, np.uint32)
+                off = np.zeros(len(bs), dtype=np.uint64)
+                if len(bs):
+                    off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+                return b"".join(bs.tolist()), off, ln
             ln = np.fromiter((len(x) for x in bs), dtype=np.uint32, count=len(bs))
             off = np.zeros(len(bs), dtype=np.uint64)
             if len(bs):

@@ -5,6 +5,7 @@ comparers agree with oracle/library.py on the reference's compare_test.go tables
 is what bench.py's cpu_baseline times for those configs (1 thread and the box's threads)."""
 import collections
 
+import numpy as np
 import pytest
 
 from oracle import drivers as od
@@ -61,7 +62,7 @@ def _c_pairs(prep, pk, en, sdb):
     out = collections.Counter()
     for p, e in zip(pk.tolist(), en.tolist()):
         ent = prep.entries[e]
-        kind = sdb.plats[prep.pkgs[p][0]][1]
+        kind = sdb.plats[int(prep.plat_of[p])][1]
         fixed = od.rpm_string(ent["fixed"]) if kind == "redhat" and ent.get("fixed") else ""
         out[(p, ent["vid"], fixed)] += 1
     return out
@@ -77,6 +78,26 @@ def test_cport_equals_oracle_drivers(which, oracle_built):
         got = _c_pairs(prep, pk, en, sdb)
         assert sum(want.values()) > 500
         assert got == want, (which, threads, sorted((got - want).items())[:5], sorted((want - got).items())[:5])
+
+
+@pytest.mark.parametrize("which", ["c5", "c3", "c4"])
+def test_columnar_digest_equals_scalar(which, oracle_built):
+    """The columnar digest (Prepared(columnar=True): the whole-batch checks at 10-20M packages)
+    gives the scalar digest's packages, keys, entries and matches, Red Hat members included, on
+    the same sample - and on a shuffled row subset (the digest takes any row order)."""
+    sdb, sample = _sample(which, n=20000)
+    rng = np.random.default_rng(11)
+    for smp in (sample, [(p, g, sorted(rng.choice(len(idx), len(idx) // 2, replace=False).tolist()))
+                         for p, g, idx in sample]):
+        a = mix_c.Prepared(sm, sdb, smp)
+        b = mix_c.Prepared(sm, sdb, smp, columnar=True)
+        assert np.array_equal(a.plat_of, b.plat_of)
+        assert list(a.installed) == [b.installed[i] for i in range(len(b.installed))]
+        assert [(e["vid"], e.get("fixed"), e.get("vul")) for e in a.entries] == \
+            [(e["vid"], e.get("fixed"), e.get("vul")) for e in b.entries]
+        pa, ea = (x.copy() for x in mix_c.match(a, 4, members=True))
+        pb, eb = mix_c.match(b, 4, members=True)
+        assert len(pa) > 1000 and np.array_equal(pa, pb) and np.array_equal(ea, eb)
 
 
 def test_libcmp_is_vulnerable_on_reference_tables(oracle_built):

@@ -36,14 +36,16 @@ class Keys:
         return self.ids.setdefault(key, len(self.ids))
 
 
-def expected(sm, sdb, batch, keys, threads=8):
+def expected(sm, sdb, batch, keys, threads=8, columnar=False):
     """(pkg int64[], record id int64[], installed list per package) of the whole batch, in the
-    drivers' output order (by package; per package advisory / Get order, Red Hat by ID)."""
+    drivers' output order (by package; per package advisory / Get order, Red Hat by ID).
+    columnar: the oracle digests the packages column-wise (mix_c.Prepared columnar form, for
+    batches of 10-20M packages)."""
     sample = [(p, g, np.arange(len(g["key"]))) for p, g in batch.groups]
-    prep = mix_c.Prepared(sm, sdb, sample)
+    prep = mix_c.Prepared(sm, sdb, sample, columnar=columnar)
     pk, en = mix_c.match(prep, threads, members=True)
     pk, en = pk.copy(), en.copy()
-    plat_of = np.array([p for p, _ in prep.pkgs], dtype=np.int64)
+    plat_of = prep.plat_of
     fam = prep.plat_family
     rh_plat = np.array([f == "redhat" for f in fam], dtype=bool)
     rep = en >= 0
