@@ -35,6 +35,10 @@ const FusedFn* fused_table_LEAN();
 
 namespace {
 
+// Engine::launch splits an all-grammar batch in two launches when at most 1 tile in kSplitFull
+// needs the all-grammar kernel (the rest run on GM_LEAN); Engine::upload orders tiles for it.
+constexpr uint32_t kSplitFull = 10;
+
 constexpr const char* kVariantNames[] = {
 #define TVM_NAME_(F, K, MB, NAME) NAME,
     TVM_MATCH_VARIANTS(TVM_NAME_)
@@ -326,10 +330,20 @@ bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
       });
     std::vector<uint32_t> order(b.n_tiles);
     for (uint32_t t = 0; t < b.n_tiles; t++) order[t] = t;
-    std::stable_sort(order.begin(), order.end(),
-                     [&](uint32_t x, uint32_t y) { return full[x] != full[y] ? full[x] < full[y] : w[x] > w[y]; });
     b.n_lean_tiles = 0;
     for (uint32_t t = 0; t < b.n_tiles; t++) b.n_lean_tiles += full[t] ? 0 : 1;
+    // a batch Engine::launch splits keeps its parts apart (lean tiles first); one launch over
+    // every tile takes them heaviest first whatever their kernel part (TVM_TILE_ORDER=lean:
+    // the parts apart anyway, =full: the all-grammar tiles first - measurement only)
+    static const char* ord = std::getenv("TVM_TILE_ORDER");
+    const uint32_t n_full = b.n_tiles - b.n_lean_tiles;
+    const bool split = n_full && n_full < b.n_tiles && n_full * kSplitFull <= b.n_tiles;
+    const int mode = split || (ord && std::strcmp(ord, "lean") == 0) ? 0 : (ord && std::strcmp(ord, "full") == 0) ? 1 : 2;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+      if (mode == 0 && full[x] != full[y]) return full[x] < full[y];
+      if (mode == 1 && full[x] != full[y]) return full[x] > full[y];
+      return w[x] > w[y];
+    });
     if (!dmalloc(&b.tile_map, order.size(), "hipMalloc(tile order)", err) ||
         !hip_ok(hipMemcpy(b.tile_map, order.data(), order.size() * 4, hipMemcpyHostToDevice), "H2D tile order", err))
       return false;
@@ -520,7 +534,6 @@ bool Engine::launch(const DevBatch& b, DevMatches& m, hipStream_t st, std::strin
   // streams did not overlap on this runtime either), so the split pays when the all-grammar
   // part is small: C4's 12.5M share (8 % Maven tiles) 1.554 -> 1.508 ms; C3 (20 %) 0.156 ->
   // 0.169 ms, which therefore stays one launch (profiles/r06/lean_ab/)
-  constexpr uint32_t kSplitFull = 10;
   const uint32_t nl = b.n_lean_tiles;
   if (nl && nl < b.n_tiles && (b.n_tiles - nl) * kSplitFull <= b.n_tiles && b.tile_map && grammar_index(b.gm) == 2 &&
       kFusedVariant[resolve_variant(variant_, b.gm) - 1] && kFusedVariant[resolve_variant(variant_, GM_LEAN) - 1]) {
