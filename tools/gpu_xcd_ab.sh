@@ -1,0 +1,18 @@
+#!/bin/bash
+# A/B: XCD-affine tile order (product default: tiles cut by platform into 8 equal-weight runs,
+# run b % 8 at grid position b) vs heaviest first only (TVM_TILE_ORDER=w), alternated.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/xcd
+mkdir -p $O
+cd $R
+for i in 1 2; do
+  timeout -k 10 200 python bench.py --config c2 --steps 20 --no-cpu --no-e2e --no-fill --no-dropin > $O/c2_xcd_$i.json 2> $O/c2_xcd_$i.err || exit 1
+  TVM_TILE_ORDER=w timeout -k 10 200 python bench.py --config c2 --steps 20 --no-cpu --no-e2e --no-fill --no-dropin > $O/c2_w_$i.json 2> $O/c2_w_$i.err || exit 1
+done
+timeout -k 10 200 python bench.py --config c3 --steps 20 --no-cpu --no-e2e > $O/c3_xcd.json 2> $O/c3_xcd.err || exit 1
+TVM_TILE_ORDER=w timeout -k 10 200 python bench.py --config c3 --steps 20 --no-cpu --no-e2e > $O/c3_w.json 2> $O/c3_w.err || exit 1
+timeout -k 10 300 python bench.py --config c5 --steps 10 --no-cpu --no-e2e --no-fill > $O/c5_xcd.json 2> $O/c5_xcd.err || exit 1
+TVM_TILE_ORDER=w timeout -k 10 300 python bench.py --config c5 --steps 10 --no-cpu --no-e2e --no-fill > $O/c5_w.json 2> $O/c5_w.err || exit 1
+for f in $O/*.json; do python -c "import json;d=json.loads(open('$f').read().strip().splitlines()[-1]);print('$f'.split('/')[-1], d['roofline']['kernel_ms'], round(d['roofline']['frac'],3))"; done
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_golden.py tests/test_gpu_parity.py tests/test_gpu_bench_batch.py tests/test_gpu_mix.py > $O/tests.log 2>&1 || { tail -20 $O/tests.log; exit 1; }
+tail -1 $O/tests.log

@@ -38,6 +38,7 @@ namespace {
 // Engine::launch splits an all-grammar batch in two launches when at most 1 tile in kSplitFull
 // needs the all-grammar kernel (the rest run on GM_LEAN); Engine::upload orders tiles for it.
 constexpr uint32_t kSplitFull = 10;
+constexpr uint32_t kXcds = 8;  // MI355X: 8 XCDs, 32 CUs each
 
 constexpr const char* kVariantNames[] = {
 #define TVM_NAME_(F, K, MB, NAME) NAME,
@@ -276,6 +277,36 @@ bool Engine::alloc_batch(const HostBatch& hb, DevBatch& b, std::string& err, boo
          dmalloc(&b.tail, hb.pk.size(), "hipMalloc(key tails)", err, pd);
 }
 
+// Tile order for a grid's XCDs: workgroups are dealt round-robin over the 8 XCDs (blocks b and
+// b + 8 share one, MI355X_MICROARCH.md), and each XCD has its own L2.  The tiles, taken by
+// platform (the first package's), are cut into kXcds runs of equal predicted weight; position
+// b of the launch takes the next tile of run b % kXcds, heaviest first within the run, so one
+// XCD's L2 holds the hot rows of one or two platforms instead of every platform's.  Runs that
+// run out hand their positions to the others (the grid's tail).  `order`: in, heaviest first.
+static void xcd_order(const HostBatch& hb, const std::vector<uint64_t>& w, std::vector<uint32_t>& order) {
+  const uint32_t n = uint32_t(order.size());
+  std::vector<uint32_t> by_plat(n);
+  for (uint32_t t = 0; t < n; t++) by_plat[t] = t;
+  std::stable_sort(by_plat.begin(), by_plat.end(),
+                   [&](uint32_t x, uint32_t y) { return hb.pk[size_t(x) * kTile].x < hb.pk[size_t(y) * kTile].x; });
+  uint64_t total = 0;
+  for (uint64_t x : w) total += x;
+  std::vector<uint32_t> run_of(n);
+  uint64_t acc = 0;
+  for (uint32_t t : by_plat) {
+    run_of[t] = uint32_t(std::min<uint64_t>(kXcds - 1, total ? acc * kXcds / total : 0));
+    acc += w[t];
+  }
+  std::vector<std::vector<uint32_t>> runs(kXcds);
+  for (uint32_t t : order) runs[run_of[t]].push_back(t);  // heaviest first within each run
+  std::vector<size_t> next(kXcds, 0);
+  for (uint32_t b = 0; b < n; b++) {
+    uint32_t r = b % kXcds;
+    for (uint32_t k = 0; k < kXcds && next[r] == runs[r].size(); k++) r = (r + 1) % kXcds;
+    order[b] = runs[r][next[r]++];
+  }
+}
+
 bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
   if (!alloc_batch(hb, b, err)) return false;
   std::vector<uint64_t> toff(hb.tile_off.begin(), hb.tile_off.end());  // + the arena end, then padded to whole tiles
@@ -344,6 +375,12 @@ bool Engine::upload(const HostBatch& hb, DevBatch& b, std::string& err) {
       if (mode == 1 && full[x] != full[y]) return full[x] > full[y];
       return w[x] > w[y];
     });
+    // XCD-affine runs for the all-grammar kernel in one launch (C3 0.1375 -> 0.1319 ms: one or
+    // two grammars' code and rows per XCD); the dpkg and rpm / apk kernels keep the global
+    // heaviest-first order (C2 0.383 -> 0.393, C5 1.81 -> 2.40 ms with the runs: per-platform
+    // runs of equal predicted rows are not equal work there; profiles/r06/xcd/)
+    if (mode == 2 && grammar_index(b.gm) == 2 && !(ord && std::strcmp(ord, "w") == 0) && b.n_tiles >= 8 * kXcds)
+      xcd_order(hb, w, order);
     if (!dmalloc(&b.tile_map, order.size(), "hipMalloc(tile order)", err) ||
         !hip_ok(hipMemcpy(b.tile_map, order.data(), order.size() * 4, hipMemcpyHostToDevice), "H2D tile order", err))
       return false;
