@@ -281,8 +281,10 @@ bool Engine::alloc_batch(const HostBatch& hb, DevBatch& b, std::string& err, boo
 // b + 8 share one, MI355X_MICROARCH.md), and each XCD has its own L2.  The tiles, taken by
 // platform (the first package's), are cut into kXcds runs of equal predicted weight; position
 // b of the launch takes the next tile of run b % kXcds, heaviest first within the run, so one
-// XCD's L2 holds the hot rows of one or two platforms instead of every platform's.  Runs that
-// run out hand their positions to the others (the grid's tail).  `order`: in, heaviest first.
+// XCD's L2 holds the hot rows of one or two platforms instead of every platform's (and its CUs
+// run one or two grammars' paths of the all-grammar kernel).  Runs that run out hand their
+// positions to the others (the grid's tail).  `order`: in, heaviest first.  Used only where it
+// measured faster (Engine::upload).
 static void xcd_order(const HostBatch& hb, const std::vector<uint64_t>& w, std::vector<uint32_t>& order) {
   const uint32_t n = uint32_t(order.size());
   std::vector<uint32_t> by_plat(n);
